@@ -1,0 +1,148 @@
+/*
+ * ptzba.h — C-ABI of libptzba.so, the MI355X (gfx950) PTZ-SLAM bundle-adjustment + tracking library.
+ *
+ * Boundary style mirrors the reference's only native FFI, the rf_map ctypes shim
+ * (reference: slam_system/rf_map/python_package/rf_map.hpp:15-19, 47-64; rf_map_wrapper.py:13-82):
+ * extern "C" entry points, opaque handle from ptzba_new() / ptzba_delete(), caller-owned contiguous float64
+ * host buffers passed as plain pointers, in/out buffers carry the initial state in and the result out,
+ * the library never frees caller memory, one call at a time per handle.
+ * Improvement over the reference's void+assert: every call returns int status (0 = ok) and
+ * ptzba_last_error() returns a message; outputs are left unchanged on failure.
+ *
+ * Entry points and the reference interface each one replaces:
+ *   ptzba_set_problem   <- the data hand-off of bundle_adjustment.py:167-202 (points, src/dst/landmark
+ *                          index lists, u, v, ref pose) and the file-based stub
+ *                          backup/bundle_adjustment_python.hpp:21-24 (bundle_adjustment_opt, body empty)
+ *   ptzba_residual      <- bundle_adjustment._compute_residual (bundle_adjustment.py:25-106), same order
+ *   ptzba_linearize ... ptzba_accept
+ *                       <- scipy.optimize.least_squares(_compute_residual, x0, x_scale='jac',
+ *                          ftol=1e-4, method='trf') at bundle_adjustment.py:200-202 (one LM iteration
+ *                          = linearize + reduced camera system + solve + accept/reject)
+ *   ptz_ray_to_image    <- TransFunction.from_ray_to_image (transformation.py:99-135), batched
+ *   ptz_image_to_ray    <- TransFunction.from_image_to_ray (transformation.py:137-175), batched
+ *   ptz_project_rays    <- PTZCamera.project_ray(s) (ptz_camera.py:191-234), batched, signed q2
+ *   ptz_back_project_rays <- PTZCamera.back_project_to_ray(s) (ptz_camera.py:287-325), batched
+ *   ptz_h_jacobian      <- PtzSlam.compute_h_jacobian (ptz_slam.py:73-138) (central FD, same steps)
+ *   ptzba_build_landmarks <- build_matching_graph landmark-id bookkeeping (image_process.py:611-653)
+ *
+ * Angles are degrees, focal length / pixels as in the reference.  Poses are [pan, tilt, f] per
+ * frame; rays are [theta, phi] per landmark.  Frame 0 is the fixed gauge frame (bundle_adjustment.py:197).
+ */
+#ifndef PTZBA_H
+#define PTZBA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PTZBA_EXPORT __attribute__((visibility("default")))
+
+typedef struct ptzba_ctx* ptzba_handle;
+
+/* precision: arithmetic/record type of the per-observation kernels.  The reduced camera system,
+ * its factorisation and the parameter state are always fp64. */
+enum { PTZBA_FP64 = 0, PTZBA_FP32 = 1 };
+/* loss (scipy least_squares `loss=`): linear, or huber with f_scale */
+enum { PTZBA_LOSS_LINEAR = 0, PTZBA_LOSS_HUBER = 1 };
+
+typedef struct {
+    int32_t precision; /* PTZBA_FP64 | PTZBA_FP32 */
+    int32_t loss;      /* PTZBA_LOSS_LINEAR | PTZBA_LOSS_HUBER */
+    double f_scale;    /* huber scale (scipy f_scale); ignored for linear */
+    int32_t n_fixed;   /* number of leading fixed (gauge) frames; the reference fixes frame 0 -> 1 */
+    int32_t reserved;
+} ptzba_problem_opts;
+
+/* per-iteration scalars read back after ptzba_step (all fp64):
+ * [0] cost at the current state, [1] cost at the trial state, [2] predicted reduction,
+ * [3] |delta|^2, [4] |x|^2, [5] factorisation status (0 ok, >0 not positive definite),
+ * [6] max |gradient| (unscaled), [7] reserved */
+#define PTZBA_NSCALARS 8
+
+/* ---------------- lifecycle ---------------- */
+PTZBA_EXPORT ptzba_handle ptzba_new(int device);
+PTZBA_EXPORT void ptzba_delete(ptzba_handle h);
+PTZBA_EXPORT const char* ptzba_last_error(void);
+PTZBA_EXPORT const char* ptzba_version(void);
+/* Run all work of the handle on this hipStream_t (e.g. torch.cuda.current_stream().cuda_stream).
+ * NULL -> the handle's own stream. */
+PTZBA_EXPORT int ptzba_set_stream(ptzba_handle h, void* hip_stream);
+
+/* ---------------- problem ---------------- */
+/* Pair-form observation records in the reference residual order: record 2m is (frame i, landmark l,
+ * keypoint of i), record 2m+1 is (frame j, landmark l, keypoint of j) of match m
+ * (bundle_adjustment.py:67-99).  obs_xy is [n_obs][2]; obs_weight may be NULL (all 1) or hold
+ * integer multiplicities of de-duplicated records. */
+PTZBA_EXPORT int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_t n_obs,
+                                   const int32_t* obs_frame, const int32_t* obs_landmark,
+                                   const double* obs_xy, const double* obs_weight, double u, double v,
+                                   const ptzba_problem_opts* opts);
+/* structural counts: [0] n_pose [1] n_landmark [2] n_obs [3] n_segments (unique frame,landmark)
+ * [4] reduced-system size [5] landmarks with observations [6] max segments per landmark
+ * [7] bytes of device memory held */
+PTZBA_EXPORT int ptzba_problem_info(ptzba_handle h, int64_t* info8);
+
+/* residual r[2*n_obs] = projection - observation, record order (== _compute_residual) at
+ * x_full = [3*n_pose poses | 2*n_landmark rays] (fp64 host). Uses the handle's precision. */
+PTZBA_EXPORT int ptzba_residual(ptzba_handle h, const double* x_full, double* r_out);
+
+/* ---------------- state ---------------- */
+PTZBA_EXPORT int ptzba_set_state(ptzba_handle h, const double* ptz /*3*n_pose*/, const double* rays /*2*n_landmark*/);
+PTZBA_EXPORT int ptzba_get_state(ptzba_handle h, double* ptz, double* rays);
+
+/* ---------------- one Levenberg-Marquardt iteration, split at the exchange points -------------
+ * Single GPU:  ptzba_linearize; loop { ptzba_step(lambda); ptzba_read_scalars; ptzba_accept(ok) }.
+ * Multi-GPU (records sharded by landmark block, poses replicated): after ptzba_build_reduced the
+ * caller all-reduces (sum) the exchange buffer's reduced system, then ptzba_solve_reduced, then
+ * all-reduces the partial scalars, then ptzba_accept.  ptzba_step == build_reduced + solve_reduced. */
+PTZBA_EXPORT int ptzba_linearize(ptzba_handle h);
+PTZBA_EXPORT int ptzba_build_reduced(ptzba_handle h, double lambda);
+PTZBA_EXPORT int ptzba_solve_reduced(ptzba_handle h);
+PTZBA_EXPORT int ptzba_step(ptzba_handle h, double lambda);
+PTZBA_EXPORT int ptzba_read_scalars(ptzba_handle h, double* out /*PTZBA_NSCALARS*/);
+PTZBA_EXPORT int ptzba_accept(ptzba_handle h, int accept);
+/* Device pointers of the exchange regions (fp64): reduced system (n_sys*(n_sys+1) doubles: lower
+ * matrix n_sys x n_sys row-major then rhs n_sys) and the additive partial scalars (PTZBA_NSCALARS). */
+PTZBA_EXPORT int ptzba_exchange(ptzba_handle h, void** sys_ptr, int64_t* sys_count, void** scal_ptr);
+/* wait for all queued work of the handle */
+PTZBA_EXPORT int ptzba_sync(ptzba_handle h);
+/* average device time (ms) of the last n launches of the linearisation kernel (K1), measured with
+ * HIP events on the handle's stream; count of launches timed */
+PTZBA_EXPORT int ptzba_kernel_times(ptzba_handle h, double* ms_out /*4*/, int64_t* count_out /*4*/);
+PTZBA_EXPORT int ptzba_reset_kernel_times(ptzba_handle h, int enable);
+
+/* ---------------- camera model (batched, device-resident computation) ---------------- */
+PTZBA_EXPORT int ptz_ray_to_image(int device, int64_t n, double u, double v, const double* f,
+                                  const double* cam_pan, const double* cam_tilt, const double* theta,
+                                  const double* phi, double* x_out, double* y_out);
+PTZBA_EXPORT int ptz_image_to_ray(int device, int64_t n, double u, double v, const double* f,
+                                  const double* cam_pan, const double* cam_tilt, const double* x,
+                                  const double* y, double* theta_out, double* phi_out);
+/* PTZCamera matrix model with optional 6-parameter displacement (NULL = zeros); one camera, n rays */
+PTZBA_EXPORT int ptz_project_rays(int device, int64_t n, double u, double v, double f, double pan,
+                                  double tilt, const double* displacement6, const double* rays /*[n][2]*/,
+                                  double* xy_out /*[n][2]*/);
+PTZBA_EXPORT int ptz_back_project_rays(int device, int64_t n, double u, double v, double f, double pan,
+                                       double tilt, const double* displacement6, const double* xy,
+                                       double* rays_out);
+/* PtzSlam.compute_h_jacobian: H [2n][3+2n] row-major, dense, as the reference */
+PTZBA_EXPORT int ptz_h_jacobian(int device, int64_t n, double u, double v, double f, double pan,
+                                double tilt, const double* displacement6, const double* rays, double* H_out);
+
+/* ---------------- host bookkeeping (native) ---------------- */
+/* First-seen landmark ids over ordered pair match lists (image_process.py:611-639).
+ * pair_i/pair_j/pair_count: n_pairs; idx_a/idx_b: concatenated match keypoint indices.
+ * kp_count[n_frames]: keypoints per frame.  Output landmark id per match (of the src keypoint) and
+ * the landmark count; *n_inconsistent counts the reference's "in-consistent matching" warnings. */
+PTZBA_EXPORT int ptzba_build_landmarks(int32_t n_frames, const int64_t* kp_count, int64_t n_pairs,
+                                       const int32_t* pair_i, const int32_t* pair_j,
+                                       const int64_t* pair_count, const int64_t* idx_a,
+                                       const int64_t* idx_b, int64_t* landmark_out, int64_t* n_landmark,
+                                       int64_t* n_inconsistent);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PTZBA_H */

@@ -1,0 +1,489 @@
+"""
+CPU ORACLE for the PTZ-SLAM bundle-adjustment / tracking hot path.
+
+*** TEST INFRASTRUCTURE ONLY. ***  Only `tests/`, `__graft_entry__.smoke()` and the
+`cpu_baseline` leg of `bench.py` may import this module, and only as the checker / the
+CPU baseline.  The product (`pan-tilt-zoom-slam_amd/`) never imports it and never falls
+back to it.
+
+What it is: a clean-room, vectorised NumPy (fp64) restatement of the reference's Python
+hot path (all citations are into /root/reference/slam_system/):
+
+  * `from_ray_to_image`      transformation.py:99-135   (literal atan closed form)
+  * `from_image_to_ray`      transformation.py:137-175
+  * `project_ray(s)`         ptz_camera.py:191-234      (matrix form, signed q2, displacement)
+  * `back_project_to_ray(s)` ptz_camera.py:287-325
+  * `overlap_pan_angle`      util.py:49-72
+  * `get_overlap_index`      util.py:75-96
+  * `build_landmark_index`   image_process.py:611-653   (first-seen landmark id rule)
+  * `compute_residual`       bundle_adjustment.py:25-106 (pair order [dx_i,dy_i,dx_j,dy_j])
+  * `init_x0`                bundle_adjustment.py:174-197 (last-writer-wins ray init)
+  * `assemble_keyframes`     bundle_adjustment.py:216-248 (set() de-dup order)
+  * `solve_scipy`            bundle_adjustment.py:200-202 (scipy trf, x_scale='jac', ftol=1e-4)
+                             + `jac_sparsity` so it runs beyond toy sizes
+  * `compute_h_jacobian`     ptz_slam.py:73-138          (central FD, vectorised)
+  * `ekf_update`             ptz_slam.py:210-289          (incl. covariance write-back quirk)
+
+Parity pinning: this restatement is checked against golden vectors produced by running the
+reference itself in the build container (tests/golden/make_golden.py, fixtures
+tests/golden/*.npz) — see tests/test_oracle_golden.py.
+"""
+import math
+
+import numpy as np
+
+D2R = math.pi / 180.0
+
+
+# ----------------------------------------------------------------------------------------
+# L1 camera model
+# ----------------------------------------------------------------------------------------
+def from_ray_to_image(u, v, f, c_p, c_t, p, t):
+    """Vectorised restatement of TransFunction.from_ray_to_image (transformation.py:99-135).
+
+    Keeps the reference's closed form literally (atan of a ratio, sqrt(tan^2+1)), which is
+    what gives the `|q2|` semantics in y for rays behind the camera."""
+    pan = np.radians(p)
+    tilt = np.radians(t)
+    cp = np.radians(c_p)
+    ct = np.radians(c_t)
+    tp = np.tan(pan)
+    tt = np.tan(tilt)
+    sec = np.sqrt(tp * tp + 1.0)
+    num = tp * np.cos(cp) - np.sin(cp)
+    den = tp * np.sin(cp) * np.cos(ct) + tt * sec * np.sin(ct) + np.cos(ct) * np.cos(cp)
+    relative_pan = np.arctan(num / den)
+    relative_tilt = np.arctan(-(tp * np.sin(ct) * np.sin(cp) - tt * sec * np.cos(ct)
+                                + np.sin(ct) * np.cos(cp)) / np.sqrt(num * num + den * den))
+    dx = f * np.tan(relative_pan)
+    x = dx + u
+    y = -np.sqrt(f * f + dx * dx) * np.tan(relative_tilt) + v
+    return x, y
+
+
+def _rot_tilt_pan(c_p, c_t):
+    """R = R_tilt @ R_pan (ptz_camera.py:73-79) for arrays of angles in degrees -> [..., 3, 3]."""
+    a = np.radians(np.asarray(c_p, dtype=np.float64))
+    b = np.radians(np.asarray(c_t, dtype=np.float64))
+    ca, sa, cb, sb = np.cos(a), np.sin(a), np.cos(b), np.sin(b)
+    z = np.zeros_like(ca)
+    o = np.ones_like(ca)
+    rt = np.stack([np.stack([o, z, z], -1), np.stack([z, cb, sb], -1), np.stack([z, -sb, cb], -1)], -2)
+    rp = np.stack([np.stack([ca, z, -sa], -1), np.stack([z, o, z], -1), np.stack([sa, z, ca], -1)], -2)
+    return rt @ rp
+
+
+def from_image_to_ray(u, v, f, c_p, c_t, x, y):
+    """Vectorised restatement of TransFunction.from_image_to_ray (transformation.py:137-175)."""
+    x = np.asarray(x, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64)
+    theta_skim = np.arctan((x - u) / f)
+    phi_skim = np.arctan((y - v) / (-f * np.sqrt(1.0 + ((x - u) / f) ** 2)))
+    x3 = np.tan(theta_skim)
+    y3 = -np.tan(phi_skim) * np.sqrt(np.tan(theta_skim) ** 2 + 1.0)
+    r = _rot_tilt_pan(c_p, c_t)
+    rinv = np.linalg.inv(r)
+    vec = np.stack([x3, y3, np.ones_like(x3)], -1)
+    out = np.einsum('...ij,...j->...i', rinv, vec)
+    x3d, y3d, z3d = out[..., 0], out[..., 1], out[..., 2]
+    theta = np.arctan(x3d / z3d)
+    phi = np.arctan(-y3d / np.sqrt(x3d * x3d + z3d * z3d))
+    return np.degrees(theta), np.degrees(phi)
+
+
+def _displacement(f, disp):
+    """PTZCamera.compute_dispalcement (ptz_camera.py:106-115)."""
+    f = np.asarray(f, dtype=np.float64)
+    w = np.zeros(6) if disp is None else np.asarray(disp, dtype=np.float64)
+    return np.stack([w[0] + w[3] * f, w[1] + w[4] * f, w[2] + w[5] * f], -1)
+
+
+def project_rays(u, v, f, pan, tilt, rays, displacement=None):
+    """PTZCamera.project_ray over many rays (ptz_camera.py:191-210): matrix form, SIGNED q2.
+
+    Returns [n, 2] image points (no visibility filtering)."""
+    rays = np.asarray(rays, dtype=np.float64).reshape(-1, 2)
+    th = np.radians(rays[:, 0])
+    ph = np.radians(rays[:, 1])
+    tth = np.tan(th)
+    ray_p = np.stack([tth, -np.tan(ph) * np.sqrt(tth * tth + 1.0), np.ones_like(tth)], -1)
+    r = _rot_tilt_pan(pan, tilt)
+    d = _displacement(f, displacement)
+    cam = ray_p @ r.T + d
+    img = np.stack([f * cam[:, 0] + u * cam[:, 2], f * cam[:, 1] + v * cam[:, 2], cam[:, 2]], -1)
+    return np.stack([img[:, 0] / img[:, 2], img[:, 1] / img[:, 2]], -1)
+
+
+def project_rays_visible(u, v, f, pan, tilt, rays, height, width, displacement=None):
+    """PTZCamera.project_rays with (height, width) (ptz_camera.py:212-234): strict 0<x<w, 0<y<h.
+    Returns (points [k,2], index float [k])."""
+    pts = project_rays(u, v, f, pan, tilt, rays, displacement)
+    keep = (pts[:, 0] > 0) & (pts[:, 0] < width) & (pts[:, 1] > 0) & (pts[:, 1] < height)
+    idx = np.flatnonzero(keep).astype(np.float64)
+    return pts[keep], idx
+
+
+def back_project_to_rays(u, v, f, pan, tilt, points, displacement=None):
+    """PTZCamera.back_project_to_ray(s) (ptz_camera.py:287-325)."""
+    points = np.asarray(points, dtype=np.float64).reshape(-1, 2)
+    k = np.array([[f, 0, u], [0, f, v], [0, 0, 1.0]])
+    kinv = np.linalg.inv(k)
+    rinv = np.linalg.inv(_rot_tilt_pan(pan, tilt))
+    d = _displacement(f, displacement)
+    hom = np.concatenate([points, np.ones((len(points), 1))], 1)
+    p = (hom @ kinv.T - d) @ rinv.T
+    theta = np.arctan(p[:, 0] / p[:, 2])
+    phi = np.arctan(-p[:, 1] / np.sqrt(p[:, 0] ** 2 + p[:, 2] ** 2))
+    return np.stack([np.degrees(theta), np.degrees(phi)], -1)
+
+
+# ----------------------------------------------------------------------------------------
+# util
+# ----------------------------------------------------------------------------------------
+def overlap_pan_angle(fl_1, pan_1, fl_2, pan_2, im_width):
+    """util.py:49-72 (vectorised; pan only, no wrap-around)."""
+    w = im_width / 2.0
+    d1 = np.degrees(np.arctan(w / np.asarray(fl_1, dtype=np.float64)))
+    d2 = np.degrees(np.arctan(w / np.asarray(fl_2, dtype=np.float64)))
+    a1 = np.maximum(pan_1 - d1, pan_2 - d2)
+    a2 = np.minimum(pan_1 + d1, pan_2 + d2)
+    return np.maximum(0.0, a2 - a1)
+
+
+def get_overlap_index(index1, index2):
+    """util.py:75-96: two-pointer merge of two (assumed sorted) arrays."""
+    o1, o2 = [], []
+    p1 = p2 = 0
+    while p1 < len(index1) and p2 < len(index2):
+        if index1[p1] == index2[p2]:
+            o1.append(p1)
+            o2.append(p2)
+            p1 += 1
+            p2 += 1
+        elif index1[p1] < index2[p2]:
+            p1 += 1
+        else:
+            p2 += 1
+    return np.array(o1, dtype=np.int64), np.array(o2, dtype=np.int64)
+
+
+# ----------------------------------------------------------------------------------------
+# Matching-graph bookkeeping (image_process.py:611-653) — pure Python (bit-exact ids)
+# ----------------------------------------------------------------------------------------
+def build_landmark_index(n_frames, pair_list):
+    """pair_list: ordered list of (i, j, src_idx list, dst_idx list) for i<j (already capped).
+    Returns (src_pt_index, dst_pt_index, landmark_index) as N x N lists, n_landmark, n_warn."""
+    maps = [dict() for _ in range(n_frames)]
+    g = 0
+    warn = 0
+    for i, j, s, d in pair_list:
+        for a, b in zip(s, d):
+            ina = a in maps[i]
+            inb = b in maps[j]
+            if ina and inb:
+                if maps[i][a] != maps[j][b]:
+                    warn += 1
+            elif ina:
+                maps[j][b] = maps[i][a]
+            elif inb:
+                maps[i][a] = maps[j][b]
+            else:
+                maps[i][a] = g
+                maps[j][b] = g
+                g += 1
+    src = [[[] for _ in range(n_frames)] for _ in range(n_frames)]
+    dst = [[[] for _ in range(n_frames)] for _ in range(n_frames)]
+    lmk = [[[] for _ in range(n_frames)] for _ in range(n_frames)]
+    for i, j, s, d in pair_list:
+        src[i][j] = list(s)
+        dst[i][j] = list(d)
+        lmk[i][j] = [maps[i][a] for a in s]
+    return src, dst, lmk, g, warn
+
+
+def flatten_matches(src_pt_index, dst_pt_index, landmark_index):
+    """Flatten the N x N index lists in the reference's residual loop order
+    (bundle_adjustment.py:67-73: i outer, j inner, matches in list order).
+    Returns int64 arrays (i, j, kp1, kp2, landmark)."""
+    n = len(src_pt_index)
+    mi, mj, k1, k2, lm = [], [], [], [], []
+    for i in range(n):
+        for j in range(n):
+            s = src_pt_index[i][j]
+            if len(s) == 0:
+                continue
+            cnt = len(s)
+            mi.append(np.full(cnt, i, np.int64))
+            mj.append(np.full(cnt, j, np.int64))
+            k1.append(np.asarray(s, np.int64))
+            k2.append(np.asarray(dst_pt_index[i][j], np.int64))
+            lm.append(np.asarray(landmark_index[i][j], np.int64))
+    if not mi:
+        e = np.zeros(0, np.int64)
+        return e, e, e, e, e
+    return tuple(np.concatenate(a) for a in (mi, mj, k1, k2, lm))
+
+
+def pair_records(points, mi, mj, k1, k2, lm):
+    """Pair-form observation records in residual order: record 2m = (i, kp1), 2m+1 = (j, kp2).
+    Returns frame[int64 R], landmark[int64 R], xy[R, 2]."""
+    n = len(mi)
+    frame = np.empty(2 * n, np.int64)
+    frame[0::2] = mi
+    frame[1::2] = mj
+    landmark = np.repeat(lm, 2)
+    xy = np.empty((2 * n, 2))
+    for f in np.unique(frame) if n else []:
+        sel0 = np.flatnonzero(mi == f)
+        sel1 = np.flatnonzero(mj == f)
+        xy[2 * sel0] = points[f][k1[sel0]]
+        xy[2 * sel1 + 1] = points[f][k2[sel1]]
+    return frame, landmark, xy
+
+
+# ----------------------------------------------------------------------------------------
+# BA residual / init / assembly / solve
+# ----------------------------------------------------------------------------------------
+def compute_residual_records(x_full, n_pose, u, v, frame, landmark, xy):
+    """Residual of pair-form records: [proj(frame, landmark) - xy] flattened, fp64."""
+    ptz = x_full[:3 * n_pose].reshape(-1, 3)
+    rays = x_full[3 * n_pose:].reshape(-1, 2)
+    px, py = from_ray_to_image(u, v, ptz[frame, 2], ptz[frame, 0], ptz[frame, 1],
+                               rays[landmark, 0], rays[landmark, 1])
+    return np.stack([px - xy[:, 0], py - xy[:, 1]], -1).reshape(-1)
+
+
+def compute_residual(x, n_pose, n_landmark, n_residual, keypoints, src_pt_index, dst_pt_index,
+                     landmark_index, u, v, reference_pose):
+    """Same signature/semantics as bundle_adjustment._compute_residual (bundle_adjustment.py:25-106)."""
+    assert x.shape[0] == (n_pose - 1) * 3 + n_landmark * 2
+    x0 = np.concatenate([np.asarray(reference_pose, np.float64), x])
+    mi, mj, k1, k2, lm = flatten_matches(src_pt_index, dst_pt_index, landmark_index)
+    frame, landmark, xy = pair_records(keypoints, mi, mj, k1, k2, lm)
+    r = compute_residual_records(x0, n_pose, u, v, frame, landmark, xy)
+    assert r.shape[0] == n_residual
+    return r
+
+
+def init_x0(initial_ptzs, n_landmark, points, mi, mj, k1, lm, u, v):
+    """bundle_adjustment.py:174-194: poses from initial_ptzs, rays from from_image_to_ray of the
+    src observation in frame i; the LAST match (in loop order) referencing a landmark wins."""
+    n = len(initial_ptzs)
+    x0 = np.zeros(3 * n + 2 * n_landmark)
+    x0[:3 * n] = np.asarray(initial_ptzs, np.float64).reshape(-1)
+    if len(lm):
+        rev = len(lm) - 1 - np.unique(lm[::-1], return_index=True)[1]
+        last = np.sort(rev)
+        ii = mi[last]
+        pts = np.stack([points[i][k] for i, k in zip(ii, k1[last])]) if len(last) else np.zeros((0, 2))
+        ptz = np.asarray(initial_ptzs, np.float64)[ii]
+        th, ph = from_image_to_ray(u, v, ptz[:, 2], ptz[:, 0], ptz[:, 1], pts[:, 0], pts[:, 1])
+        lid = lm[last]
+        x0[3 * n + 2 * lid] = th
+        x0[3 * n + 2 * lid + 1] = ph
+    return x0
+
+
+def assemble_keyframe_pairs(n_frames, src_pt_index, dst_pt_index, landmark_index):
+    """bundle_adjustment.py:221-245: per keyframe, (local, global) pairs from src and dst roles,
+    de-duplicated through a Python set (its iteration order is the keyframe's feature order).
+    Returns list of (local_index list, global_index int32 array)."""
+    out = []
+    for i in range(n_frames):
+        pairs = []
+        for j in range(n_frames):
+            if len(src_pt_index[i][j]) == 0:
+                continue
+            for a, l in zip(src_pt_index[i][j], landmark_index[i][j]):
+                pairs.append((int(a), int(l)))
+        for j in range(n_frames):
+            if len(dst_pt_index[j][i]) == 0:
+                continue
+            for b, l in zip(dst_pt_index[j][i], landmark_index[j][i]):
+                pairs.append((int(b), int(l)))
+        pairs = set(pairs)
+        loc = [p[0] for p in pairs]
+        glb = [p[1] for p in pairs]
+        out.append((loc, np.array(glb, dtype=np.int32)))
+    return out
+
+
+def ba_jacobian_sparsity(n_pose, n_landmark, frame, landmark):
+    """Sparsity of d r / d x (frame 0 fixed) for pair-form records (2 rows each)."""
+    from scipy.sparse import coo_matrix
+    R = len(frame)
+    rows, cols = [], []
+    rr = np.arange(R)
+    for k in range(2):
+        row = 2 * rr + k
+        m = frame > 0
+        for c in range(3):
+            rows.append(row[m])
+            cols.append(3 * (frame[m] - 1) + c)
+        for c in range(2):
+            rows.append(row)
+            cols.append(3 * (n_pose - 1) + 2 * landmark + c)
+    rows = np.concatenate(rows)
+    cols = np.concatenate(cols)
+    return coo_matrix((np.ones(len(rows), np.int8), (rows, cols)),
+                      shape=(2 * R, 3 * (n_pose - 1) + 2 * n_landmark)).tocsr()
+
+
+def ba_jacobian(x, n_pose, n_landmark, u, v, ref_pose, frame, landmark):
+    """Analytic sparse Jacobian of the pair-form residual, fp64."""
+    from scipy.sparse import coo_matrix
+    x0 = np.concatenate([np.asarray(ref_pose, np.float64), x])
+    ptz = x0[:3 * n_pose].reshape(-1, 3)
+    rays = x0[3 * n_pose:].reshape(-1, 2)
+    J = record_jacobian(u, v, ptz[frame], rays[landmark])  # [R, 2, 5]
+    R = len(frame)
+    rows, cols, vals = [], [], []
+    rr = np.arange(R)
+    m = frame > 0
+    for k in range(2):
+        for c in range(3):
+            rows.append(2 * rr[m] + k)
+            cols.append(3 * (frame[m] - 1) + c)
+            vals.append(J[m, k, c])
+        for c in range(2):
+            rows.append(2 * rr + k)
+            cols.append(3 * (n_pose - 1) + 2 * landmark + c)
+            vals.append(J[:, k, 3 + c])
+    return coo_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))),
+                      shape=(2 * R, 3 * (n_pose - 1) + 2 * n_landmark)).tocsr()
+
+
+def record_jacobian(u, v, ptz, rays):
+    """d(x,y)/d(pan, tilt, f, theta, phi) per record (|q2| in y). [R,2,5]."""
+    a = np.radians(ptz[:, 0]); b = np.radians(ptz[:, 1]); f = ptz[:, 2]
+    th = np.radians(rays[:, 0]); ph = np.radians(rays[:, 1])
+    ca, sa, cb, sb = np.cos(a), np.sin(a), np.cos(b), np.sin(b)
+    tth, sth = np.tan(th), 1.0 / np.cos(th)
+    tph, sph = np.tan(ph), 1.0 / np.cos(ph)
+    p0 = tth
+    p1 = -tph * sth
+    w0 = ca * p0 - sa
+    w2 = sa * p0 + ca
+    q0 = w0
+    q1 = cb * p1 + sb * w2
+    q2 = -sb * p1 + cb * w2
+    aq2 = np.abs(q2)
+    sg = np.sign(q2)
+    # d(x,y)/dq
+    dx = np.stack([f / q2, np.zeros_like(f), -f * q0 / (q2 * q2)], -1)
+    dy = np.stack([np.zeros_like(f), f / aq2, -f * q1 * sg / (q2 * q2)], -1)
+    dq_pan = np.stack([-w2, sb * w0, cb * w0], -1) * D2R
+    dq_tilt = np.stack([np.zeros_like(f), q2, -q1], -1) * D2R
+    d0 = sth * sth
+    d1 = -tph * sth * tth
+    dq_th = np.stack([ca * d0, cb * d1 + sb * sa * d0, -sb * d1 + cb * sa * d0], -1) * D2R
+    e1 = -sph * sph * sth
+    dq_ph = np.stack([np.zeros_like(f), cb * e1, -sb * e1], -1) * D2R
+    J = np.zeros((len(f), 2, 5))
+    for c, dq in enumerate([dq_pan, dq_tilt]):
+        J[:, 0, c] = np.sum(dx * dq, -1)
+        J[:, 1, c] = np.sum(dy * dq, -1)
+    J[:, 0, 2] = q0 / q2
+    J[:, 1, 2] = q1 / aq2
+    for c, dq in enumerate([dq_th, dq_ph]):
+        J[:, 0, 3 + c] = np.sum(dx * dq, -1)
+        J[:, 1, 3 + c] = np.sum(dy * dq, -1)
+    return J
+
+
+def solve_scipy(x0_free, n_pose, n_landmark, u, v, ref_pose, frame, landmark, xy,
+                ftol=1e-4, xtol=1e-8, gtol=1e-8, analytic=False, loss='linear', f_scale=1.0,
+                max_nfev=None, verbose=0):
+    """bundle_adjustment.py:200-202 option set (method='trf', x_scale='jac', ftol=1e-4), with a
+    `jac_sparsity` (FD, as the reference) or an analytic sparse Jacobian (tight goldens)."""
+    from scipy.optimize import least_squares
+    ref_pose = np.asarray(ref_pose, np.float64)
+
+    def fun(x):
+        x_full = np.concatenate([ref_pose, x])
+        return compute_residual_records(x_full, n_pose, u, v, frame, landmark, xy)
+
+    kw = dict(x_scale='jac', ftol=ftol, xtol=xtol, gtol=gtol, method='trf', verbose=verbose,
+              loss=loss, f_scale=f_scale)
+    if max_nfev is not None:
+        kw['max_nfev'] = max_nfev
+    if analytic:
+        kw['jac'] = lambda x: ba_jacobian(x, n_pose, n_landmark, u, v, ref_pose, frame, landmark)
+        kw['tr_solver'] = 'exact' if len(x0_free) < 2000 else 'lsmr'
+    else:
+        kw['jac_sparsity'] = ba_jacobian_sparsity(n_pose, n_landmark, frame, landmark)
+    return least_squares(fun, x0_free, **kw)
+
+
+def ba_cost(x_full, n_pose, u, v, frame, landmark, xy, loss='linear', f_scale=1.0):
+    """scipy cost convention: 0.5 * sum rho(r_i^2) over scalar residuals."""
+    r = compute_residual_records(x_full, n_pose, u, v, frame, landmark, xy)
+    z = (r / f_scale) ** 2
+    if loss == 'huber':
+        rho = np.where(z <= 1.0, z, 2.0 * np.sqrt(z) - 1.0)
+        return 0.5 * f_scale ** 2 * float(np.sum(rho))
+    return 0.5 * float(np.sum(r * r))
+
+
+# ----------------------------------------------------------------------------------------
+# EKF tracking (ptz_slam.py:73-289)
+# ----------------------------------------------------------------------------------------
+def compute_h_jacobian(u, v, pan, tilt, f, rays, displacement=None):
+    """ptz_slam.py:73-138: central FD, d_angle = 0.001 deg, d_f = 0.1 px; H [2R, 3+2R]."""
+    rays = np.asarray(rays, np.float64).reshape(-1, 2)
+    n = len(rays)
+    da, dfl = 0.001, 0.1
+    H = np.zeros((2 * n, 3 + 2 * n))
+
+    def P(pp, tt, ff, rr):
+        return project_rays(u, v, ff, pp, tt, rr, displacement)
+
+    cols = [
+        (P(pan + da, tilt, f, rays) - P(pan - da, tilt, f, rays)) / (2 * da),
+        (P(pan, tilt + da, f, rays) - P(pan, tilt - da, f, rays)) / (2 * da),
+        (P(pan, tilt, f + dfl, rays) - P(pan, tilt, f - dfl, rays)) / (2 * dfl),
+    ]
+    for c in range(3):
+        H[0::2, c] = cols[c][:, 0]
+        H[1::2, c] = cols[c][:, 1]
+    dth = np.array([da, 0.0])
+    dph = np.array([0.0, da])
+    jt = (P(pan, tilt, f, rays + dth) - P(pan, tilt, f, rays - dth)) / (2 * da)
+    jp = (P(pan, tilt, f, rays + dph) - P(pan, tilt, f, rays - dph)) / (2 * da)
+    idx = np.arange(n)
+    H[2 * idx, 3 + 2 * idx] = jt[:, 0]
+    H[2 * idx, 4 + 2 * idx] = jp[:, 0]
+    H[2 * idx + 1, 3 + 2 * idx] = jt[:, 1]
+    H[2 * idx + 1, 4 + 2 * idx] = jp[:, 1]
+    return H
+
+
+def ekf_update(state, observed_keypoints, observed_keypoint_index, height, width, observe_var=0.1):
+    """ptz_slam.py:210-289 on a plain state dict: u, v, pan, tilt, f, displacement, rays [R,2],
+    state_cov [3+2R]^2. Returns a new state dict (and velocity)."""
+    s = {k: (np.array(v_, copy=True) if isinstance(v_, np.ndarray) else v_) for k, v_ in state.items()}
+    u, v = s['u'], s['v']
+    pred_pts, pred_idx = project_rays_visible(u, v, s['f'], s['pan'], s['tilt'], s['rays'], height, width,
+                                              s.get('displacement'))
+    o1, o2 = get_overlap_index(observed_keypoint_index, pred_idx)
+    y = (np.asarray(observed_keypoints)[o1] - pred_pts[o2]).reshape(-1)
+    matched = np.asarray(observed_keypoint_index)[o1].astype(np.int64)
+    nr = len(matched)
+    pr = np.concatenate([[0, 1, 2], np.stack([2 * matched + 3, 2 * matched + 4], -1).reshape(-1)]).astype(np.int64)
+    P = s['state_cov'][np.ix_(pr, pr)]
+    H = compute_h_jacobian(u, v, s['pan'], s['tilt'], s['f'], s['rays'][matched], s.get('displacement'))
+    Sk = H @ P @ H.T + observe_var * np.eye(2 * nr)
+    K = P @ H.T @ np.linalg.inv(Sk)
+    ky = K @ y
+    s['pan'] = s['pan'] + ky[0]
+    s['tilt'] = s['tilt'] + ky[1]
+    s['f'] = s['f'] + ky[2]
+    s['velocity'] = ky[0:3].copy()
+    s['rays'][matched] += ky[3:].reshape(-1, 2)
+    Pu = (np.eye(3 + 2 * nr) - K @ H) @ P
+    cov = s['state_cov']
+    cov[0:3, 0:3] = Pu[0:3, 0:3]
+    rows = 3 + 2 * matched
+    cov[np.ix_(rows, rows)] = Pu[3::2, 3::2]
+    cov[np.ix_(rows + 1, rows + 1)] = Pu[4::2, 4::2]
+    return s

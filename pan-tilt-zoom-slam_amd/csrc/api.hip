@@ -1,0 +1,760 @@
+// libptzba C-ABI (see include/ptzba.h): host-side problem preparation (native C++: stable counting
+// sorts into landmark-major records, segment / landmark / frame CSR, work ordering), device buffer
+// ownership, and the Levenberg-Marquardt step sequence over the gfx950 kernels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/ptzba.h"
+#include "ptzba_common.h"
+#include "ptzba_kernels.h"
+
+using namespace ptzba;
+
+static thread_local std::string g_err;
+
+static int fail(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return -1;
+}
+
+#define HIPCHK(expr)                                                                              \
+  do {                                                                                            \
+    hipError_t _e = (expr);                                                                       \
+    if (_e != hipSuccess) return fail("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, __LINE__); \
+  } while (0)
+
+// ------------------------------------------------------------------------------------------------
+struct DBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DBuf() = default;
+  DBuf(const DBuf&) = delete;
+  DBuf& operator=(const DBuf&) = delete;
+  ~DBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  int alloc(size_t n) {
+    release();
+    if (n == 0) n = 16;
+    hipError_t e = hipMalloc(&p, n);
+    if (e != hipSuccess) return fail("hipMalloc(%zu) failed: %s", n, hipGetErrorString(e));
+    bytes = n;
+    return 0;
+  }
+  template <typename T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+static size_t g_total_bytes(std::initializer_list<const DBuf*> l) {
+  size_t s = 0;
+  for (auto* b : l) s += b->bytes;
+  return s;
+}
+
+enum { TM_K1 = 0, TM_SCHUR = 1, TM_CHOL = 2, TM_BACK = 3, TM_N = 4 };
+constexpr int TM_POOL = 512;
+
+struct ptzba_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t st = nullptr;
+  // problem
+  bool have_problem = false;
+  int n_pose = 0, n_lm = 0, n_fixed = 1, precision = PTZBA_FP64, loss = PTZBA_LOSS_LINEAR;
+  double fs = 1.0;
+  int64_t n_rec = 0, n_seg = 0;
+  int n_work = 0, max_seg_per_lm = 0;
+  int n_sys = 0;
+  int64_t ld = 0;
+  double u = 0, v = 0;
+  bool weighted = false;
+  std::vector<int64_t> perm_host;  // sorted -> original record index
+  bool perm_uploaded = false;
+  // device: structure
+  DBuf rec_xy, rec_seg, rec_w, perm;
+  DBuf seg_frame, seg_lm, seg_rec_begin, lm_seg_begin, lm_order;
+  DBuf frame_seg_begin, frame_seg_list, frame_win_hi;
+  // device: state
+  DBuf ptz, rays, ptz_trial, rays_trial, D_pose, D_ray;
+  DBuf ft, rt;
+  DBuf seg_out[2], lm_out[2];
+  int cur = 0;
+  DBuf lm_aux, lm_red;
+  DBuf sys;  // [S ld*ld | b ld | g_pose ld | dU ld]
+  DBuf scal, loc, info, tile_nz;
+  double lambda = 0;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev[TM_N];
+  int ev_used[TM_N] = {0, 0, 0, 0};
+
+  int elem() const { return precision == PTZBA_FP32 ? 4 : 8; }
+  double* S() const { return sys.as<double>(); }
+  double* bvec() const { return sys.as<double>() + ld * ld; }
+  double* gpose() const { return sys.as<double>() + ld * ld + ld; }
+  double* dU() const { return sys.as<double>() + ld * ld + 2 * ld; }
+  int64_t sys_count() const { return ld * ld + 3 * ld; }
+};
+
+static void tm_begin(ptzba_ctx* h, int k) {
+  if (!h->timing || h->ev_used[k] + 2 > (int)h->ev[k].size()) return;
+  (void)hipEventRecord(h->ev[k][h->ev_used[k]], h->st);
+}
+static void tm_end(ptzba_ctx* h, int k) {
+  if (!h->timing || h->ev_used[k] + 2 > (int)h->ev[k].size()) return;
+  (void)hipEventRecord(h->ev[k][h->ev_used[k] + 1], h->st);
+  h->ev_used[k] += 2;
+}
+
+const char* ptzba_last_error(void) { return g_err.c_str(); }
+const char* ptzba_version(void) { return "ptzba 0.1 gfx950"; }
+
+ptzba_handle ptzba_new(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+    fail("no HIP device available");
+    return nullptr;
+  }
+  if (device < 0 || device >= n) {
+    fail("device %d out of range (%d devices)", device, n);
+    return nullptr;
+  }
+  if (hipSetDevice(device) != hipSuccess) {
+    fail("hipSetDevice(%d) failed", device);
+    return nullptr;
+  }
+  auto* h = new ptzba_ctx();
+  h->device = device;
+  if (hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    fail("hipStreamCreate failed");
+    return nullptr;
+  }
+  h->st = h->own;
+  return h;
+}
+
+void ptzba_delete(ptzba_handle h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->st) (void)hipStreamSynchronize(h->st);
+  for (int k = 0; k < TM_N; ++k)
+    for (auto e : h->ev[k]) (void)hipEventDestroy(e);
+  if (h->own) (void)hipStreamDestroy(h->own);
+  delete h;
+}
+
+int ptzba_set_stream(ptzba_handle h, void* stream) {
+  if (!h) return fail("null handle");
+  h->st = stream ? (hipStream_t)stream : h->own;
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+template <typename real>
+static int upload_records(ptzba_ctx* h, const std::vector<int64_t>& order, const double* obs_xy, const double* w) {
+  std::vector<real> xy(2 * h->n_rec);
+  for (int64_t r = 0; r < h->n_rec; ++r) {
+    xy[2 * r] = (real)obs_xy[2 * order[r]];
+    xy[2 * r + 1] = (real)obs_xy[2 * order[r] + 1];
+  }
+  if (h->rec_xy.alloc(xy.size() * sizeof(real))) return -1;
+  HIPCHK(hipMemcpy(h->rec_xy.p, xy.data(), xy.size() * sizeof(real), hipMemcpyHostToDevice));
+  if (w) {
+    std::vector<real> ww(h->n_rec);
+    for (int64_t r = 0; r < h->n_rec; ++r) ww[r] = (real)w[order[r]];
+    if (h->rec_w.alloc(ww.size() * sizeof(real))) return -1;
+    HIPCHK(hipMemcpy(h->rec_w.p, ww.data(), ww.size() * sizeof(real), hipMemcpyHostToDevice));
+  } else {
+    h->rec_w.release();
+  }
+  return 0;
+}
+
+template <typename T>
+static int upload(DBuf& b, const std::vector<T>& v) {
+  if (b.alloc(v.size() * sizeof(T))) return -1;
+  if (!v.empty()) HIPCHK(hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return 0;
+}
+
+int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_t n_obs, const int32_t* obs_frame,
+                      const int32_t* obs_landmark, const double* obs_xy, const double* obs_weight, double u, double v,
+                      const ptzba_problem_opts* opts) {
+  if (!h) return fail("null handle");
+  if (n_pose < 1 || n_landmark < 0 || n_obs < 0) return fail("bad sizes n_pose=%d n_landmark=%d n_obs=%lld", n_pose, n_landmark, (long long)n_obs);
+  if (n_obs > 0 && (!obs_frame || !obs_landmark || !obs_xy)) return fail("null observation pointer");
+  ptzba_problem_opts o{PTZBA_FP64, PTZBA_LOSS_LINEAR, 1.0, 1, 0};
+  if (opts) o = *opts;
+  if (o.precision != PTZBA_FP64 && o.precision != PTZBA_FP32) return fail("bad precision %d", o.precision);
+  if (o.loss != PTZBA_LOSS_LINEAR && o.loss != PTZBA_LOSS_HUBER) return fail("bad loss %d", o.loss);
+  if (o.n_fixed < 0 || o.n_fixed > n_pose) return fail("bad n_fixed %d", o.n_fixed);
+  if (o.loss == PTZBA_LOSS_HUBER && !(o.f_scale > 0)) return fail("huber needs f_scale > 0");
+  for (int64_t r = 0; r < n_obs; ++r) {
+    if (obs_frame[r] < 0 || obs_frame[r] >= n_pose) return fail("record %lld: frame %d out of range", (long long)r, obs_frame[r]);
+    if (obs_landmark[r] < 0 || obs_landmark[r] >= n_landmark)
+      return fail("record %lld: landmark %d out of range", (long long)r, obs_landmark[r]);
+    if (!std::isfinite(obs_xy[2 * r]) || !std::isfinite(obs_xy[2 * r + 1])) return fail("record %lld: non-finite observation", (long long)r);
+    if (obs_weight && !(obs_weight[r] >= 0)) return fail("record %lld: negative weight", (long long)r);
+  }
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->st));
+  h->have_problem = false;
+  h->n_pose = n_pose;
+  h->n_lm = n_landmark;
+  h->n_rec = n_obs;
+  h->precision = o.precision;
+  h->loss = o.loss;
+  h->fs = o.f_scale;
+  h->n_fixed = o.n_fixed;
+  h->u = u;
+  h->v = v;
+  h->weighted = obs_weight != nullptr;
+
+  // ---- stable counting sorts: by frame, then by landmark -> (landmark, frame, original index)
+  std::vector<int64_t> tmp(n_obs), order(n_obs);
+  {
+    std::vector<int64_t> c(n_pose + 1, 0);
+    for (int64_t r = 0; r < n_obs; ++r) c[obs_frame[r] + 1]++;
+    for (int f = 0; f < n_pose; ++f) c[f + 1] += c[f];
+    for (int64_t r = 0; r < n_obs; ++r) tmp[c[obs_frame[r]]++] = r;
+    std::vector<int64_t> d(n_landmark + 1, 0);
+    for (int64_t r = 0; r < n_obs; ++r) d[obs_landmark[r] + 1]++;
+    for (int l = 0; l < n_landmark; ++l) d[l + 1] += d[l];
+    for (int64_t k = 0; k < n_obs; ++k) {
+      int64_t r = tmp[k];
+      order[d[obs_landmark[r]]++] = r;
+    }
+  }
+  // ---- segments (unique landmark, frame)
+  std::vector<int32_t> seg_frame, seg_lm, rec_seg(n_obs);
+  std::vector<int64_t> seg_rec_begin;
+  std::vector<int32_t> lm_seg_begin(n_landmark + 1, 0);
+  seg_frame.reserve(n_obs / 4 + 16);
+  for (int64_t k = 0; k < n_obs; ++k) {
+    int64_t r = order[k];
+    if (k == 0 || obs_landmark[r] != obs_landmark[order[k - 1]] || obs_frame[r] != obs_frame[order[k - 1]]) {
+      if ((int64_t)seg_frame.size() >= INT32_MAX - 1) return fail("too many segments");
+      seg_frame.push_back(obs_frame[r]);
+      seg_lm.push_back(obs_landmark[r]);
+      seg_rec_begin.push_back(k);
+      lm_seg_begin[obs_landmark[r] + 1]++;
+    }
+    rec_seg[k] = (int32_t)seg_frame.size() - 1;
+  }
+  const int64_t n_seg = (int64_t)seg_frame.size();
+  seg_rec_begin.push_back(n_obs);
+  for (int l = 0; l < n_landmark; ++l) lm_seg_begin[l + 1] += lm_seg_begin[l];
+  h->n_seg = n_seg;
+  // ---- frame CSR over segments (stable: landmark ascending within a frame)
+  std::vector<int32_t> frame_seg_begin(n_pose + 1, 0), frame_seg_list(n_seg), frame_win_hi(n_pose);
+  for (int64_t s = 0; s < n_seg; ++s) frame_seg_begin[seg_frame[s] + 1]++;
+  for (int f = 0; f < n_pose; ++f) frame_seg_begin[f + 1] += frame_seg_begin[f];
+  {
+    std::vector<int32_t> c(frame_seg_begin.begin(), frame_seg_begin.end() - 1);
+    for (int64_t s = 0; s < n_seg; ++s) frame_seg_list[c[seg_frame[s]]++] = (int32_t)s;
+  }
+  for (int f = 0; f < n_pose; ++f) {
+    int hi = f;
+    for (int e = frame_seg_begin[f]; e < frame_seg_begin[f + 1]; ++e) {
+      int l = seg_lm[frame_seg_list[e]];
+      hi = std::max(hi, seg_frame[lm_seg_begin[l + 1] - 1]);
+    }
+    frame_win_hi[f] = hi;
+  }
+  // ---- landmark work order: heaviest (most records) first
+  std::vector<int32_t> lm_order;
+  int max_seg = 0;
+  for (int l = 0; l < n_landmark; ++l) {
+    int ns = lm_seg_begin[l + 1] - lm_seg_begin[l];
+    if (ns > 0) lm_order.push_back(l);
+    max_seg = std::max(max_seg, ns);
+  }
+  std::stable_sort(lm_order.begin(), lm_order.end(), [&](int a, int b) {
+    int64_t ra = seg_rec_begin[lm_seg_begin[a + 1]] - seg_rec_begin[lm_seg_begin[a]];
+    int64_t rb = seg_rec_begin[lm_seg_begin[b + 1]] - seg_rec_begin[lm_seg_begin[b]];
+    return ra > rb;
+  });
+  h->n_work = (int)lm_order.size();
+  h->max_seg_per_lm = max_seg;
+  h->n_sys = 3 * (n_pose - o.n_fixed);
+  h->ld = std::max<int64_t>(CHOL_NB, ((int64_t)h->n_sys + CHOL_NB - 1) / CHOL_NB * CHOL_NB);
+  if (h->ld > 20000) return fail("reduced system %d too large for the dense solver", h->n_sys);
+  h->perm_host = order;
+  h->perm_uploaded = false;
+
+  // ---- upload
+  int rc = h->precision == PTZBA_FP32 ? upload_records<float>(h, order, obs_xy, obs_weight)
+                                      : upload_records<double>(h, order, obs_xy, obs_weight);
+  if (rc) return rc;
+  if (upload(h->rec_seg, rec_seg) || upload(h->seg_frame, seg_frame) || upload(h->seg_lm, seg_lm) ||
+      upload(h->seg_rec_begin, seg_rec_begin) || upload(h->lm_seg_begin, lm_seg_begin) ||
+      upload(h->lm_order, lm_order) || upload(h->frame_seg_begin, frame_seg_begin) ||
+      upload(h->frame_seg_list, frame_seg_list) || upload(h->frame_win_hi, frame_win_hi))
+    return -1;
+  const size_t e = h->elem();
+  if (h->ptz.alloc(3 * n_pose * 8) || h->ptz_trial.alloc(3 * n_pose * 8) || h->rays.alloc(2 * (size_t)n_landmark * 8) ||
+      h->rays_trial.alloc(2 * (size_t)n_landmark * 8) || h->D_pose.alloc(3 * n_pose * 8) ||
+      h->D_ray.alloc(2 * (size_t)n_landmark * 8) || h->ft.alloc((size_t)n_pose * 8 * e) ||
+      h->rt.alloc((size_t)n_landmark * 8 * e) || h->seg_out[0].alloc((size_t)n_seg * 16 * e) ||
+      h->seg_out[1].alloc((size_t)n_seg * 16 * e) || h->lm_out[0].alloc((size_t)n_landmark * 8 * 8) ||
+      h->lm_out[1].alloc((size_t)n_landmark * 8 * 8) || h->lm_aux.alloc((size_t)n_landmark * 8 * 8) ||
+      h->lm_red.alloc((size_t)n_landmark * 4 * 8) || h->sys.alloc((size_t)h->sys_count() * 8) ||
+      h->scal.alloc(PTZBA_NSCALARS * 8) || h->loc.alloc(PTZBA_NSCALARS * 8) || h->info.alloc(16) ||
+      h->tile_nz.alloc((size_t)(h->ld / CHOL_NB + 1) * 4))
+    return -1;
+  HIPCHK(hipMemset(h->D_pose.p, 0, h->D_pose.bytes));
+  HIPCHK(hipMemset(h->D_ray.p, 0, h->D_ray.bytes));
+  HIPCHK(hipMemset(h->ptz.p, 0, h->ptz.bytes));
+  HIPCHK(hipMemset(h->rays.p, 0, h->rays.bytes));
+  HIPCHK(hipMemset(h->scal.p, 0, h->scal.bytes));
+  HIPCHK(hipMemset(h->loc.p, 0, h->loc.bytes));
+  h->cur = 0;
+  h->lambda = 0;
+  h->have_problem = true;
+  return 0;
+}
+
+int ptzba_problem_info(ptzba_handle h, int64_t* info) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  info[0] = h->n_pose;
+  info[1] = h->n_lm;
+  info[2] = h->n_rec;
+  info[3] = h->n_seg;
+  info[4] = h->n_sys;
+  info[5] = h->n_work;
+  info[6] = h->max_seg_per_lm;
+  info[7] = (int64_t)g_total_bytes({&h->rec_xy, &h->rec_seg, &h->rec_w, &h->perm, &h->seg_frame, &h->seg_lm,
+                                    &h->seg_rec_begin, &h->lm_seg_begin, &h->lm_order, &h->frame_seg_begin,
+                                    &h->frame_seg_list, &h->frame_win_hi, &h->ptz, &h->rays, &h->ptz_trial,
+                                    &h->rays_trial, &h->D_pose, &h->D_ray, &h->ft, &h->rt, &h->seg_out[0],
+                                    &h->seg_out[1], &h->lm_out[0], &h->lm_out[1], &h->lm_aux, &h->lm_red, &h->sys,
+                                    &h->scal, &h->loc});
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+static void tables(ptzba_ctx* h, const double* ptz, const double* rays) {
+  if (h->precision == PTZBA_FP32)
+    launch_tables<float>(ptz, rays, h->n_pose, h->n_lm, h->ft.p, h->rt.p, h->st);
+  else
+    launch_tables<double>(ptz, rays, h->n_pose, h->n_lm, h->ft.p, h->rt.p, h->st);
+}
+
+static void linearize_into(ptzba_ctx* h, int slot) {
+  LinArgs a;
+  a.lm_order = h->lm_order.as<int32_t>();
+  a.n_work = h->n_work;
+  a.lm_seg_begin = h->lm_seg_begin.as<int32_t>();
+  a.seg_frame = h->seg_frame.as<int32_t>();
+  a.seg_rec_begin = h->seg_rec_begin.as<int64_t>();
+  a.rec_seg = h->rec_seg.as<int32_t>();
+  a.rec_xy = h->rec_xy.p;
+  a.rec_w = h->weighted ? h->rec_w.p : nullptr;
+  a.ft = h->ft.p;
+  a.rt = h->rt.p;
+  a.u = h->u;
+  a.v = h->v;
+  a.fs2 = h->fs * h->fs;
+  a.inv_fs2 = 1.0 / (h->fs * h->fs);
+  a.seg_out = h->seg_out[slot].p;
+  a.lm_out = h->lm_out[slot].as<double>();
+  // landmarks without records keep zero rows
+  (void)hipMemsetAsync(h->lm_out[slot].p, 0, h->lm_out[slot].bytes, h->st);
+  tm_begin(h, TM_K1);
+  if (h->precision == PTZBA_FP32)
+    launch_linearize<float>(a, h->loss, h->st);
+  else
+    launch_linearize<double>(a, h->loss, h->st);
+  tm_end(h, TM_K1);
+}
+
+int ptzba_residual(ptzba_handle h, const double* x_full, double* r_out) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  HIPCHK(hipSetDevice(h->device));
+  if (!h->perm_uploaded) {
+    if (upload(h->perm, h->perm_host)) return -1;
+    h->perm_uploaded = true;
+  }
+  DBuf x, r;
+  if (x.alloc((3 * (size_t)h->n_pose + 2 * (size_t)h->n_lm) * 8) || r.alloc(2 * (size_t)h->n_rec * 8)) return -1;
+  HIPCHK(hipMemcpyAsync(x.p, x_full, x.bytes, hipMemcpyHostToDevice, h->st));
+  const double* px = x.as<double>();
+  tables(h, px, px + 3 * h->n_pose);
+  if (h->precision == PTZBA_FP32)
+    launch_residual<float>(h->rec_seg.as<int32_t>(), h->seg_frame.as<int32_t>(), h->seg_lm.as<int32_t>(), h->rec_xy.p,
+                           h->perm.as<int64_t>(), h->ft.p, h->rt.p, h->u, h->v, h->n_rec, r.as<double>(), h->st);
+  else
+    launch_residual<double>(h->rec_seg.as<int32_t>(), h->seg_frame.as<int32_t>(), h->seg_lm.as<int32_t>(), h->rec_xy.p,
+                            h->perm.as<int64_t>(), h->ft.p, h->rt.p, h->u, h->v, h->n_rec, r.as<double>(), h->st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(r_out, r.p, 2 * (size_t)h->n_rec * 8, hipMemcpyDeviceToHost, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  return 0;
+}
+
+int ptzba_set_state(ptzba_handle h, const double* ptz, const double* rays) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipMemcpyAsync(h->ptz.p, ptz, 3 * (size_t)h->n_pose * 8, hipMemcpyHostToDevice, h->st));
+  if (h->n_lm) HIPCHK(hipMemcpyAsync(h->rays.p, rays, 2 * (size_t)h->n_lm * 8, hipMemcpyHostToDevice, h->st));
+  HIPCHK(hipMemsetAsync(h->D_pose.p, 0, h->D_pose.bytes, h->st));
+  HIPCHK(hipMemsetAsync(h->D_ray.p, 0, h->D_ray.bytes, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  return 0;
+}
+
+int ptzba_get_state(ptzba_handle h, double* ptz, double* rays) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  HIPCHK(hipSetDevice(h->device));
+  if (ptz) HIPCHK(hipMemcpyAsync(ptz, h->ptz.p, 3 * (size_t)h->n_pose * 8, hipMemcpyDeviceToHost, h->st));
+  if (rays && h->n_lm) HIPCHK(hipMemcpyAsync(rays, h->rays.p, 2 * (size_t)h->n_lm * 8, hipMemcpyDeviceToHost, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  return 0;
+}
+
+int ptzba_linearize(ptzba_handle h) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  HIPCHK(hipSetDevice(h->device));
+  tables(h, h->ptz.as<double>(), h->rays.as<double>());
+  linearize_into(h, h->cur);
+  HIPCHK(hipMemsetAsync(h->scal.p, 0, h->scal.bytes, h->st));
+  launch_reduce_cols(h->lm_out[h->cur].as<double>() + 5, h->n_lm, 8, 1, 0, h->scal.as<double>(), h->st);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int ptzba_build_reduced(ptzba_handle h, double lambda) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  if (!(lambda >= 0) || !std::isfinite(lambda)) return fail("bad lambda");
+  HIPCHK(hipSetDevice(h->device));
+  h->lambda = lambda;
+  const int c = h->cur;
+  launch_landmark_damp(h->lm_out[c].as<double>(), h->lm_seg_begin.as<int32_t>(), h->D_ray.as<double>(),
+                       h->lm_aux.as<double>(), h->n_lm, lambda, h->st);
+  HIPCHK(hipMemsetAsync(h->sys.p, 0, h->sys.bytes, h->st));
+  SchurArgs a;
+  a.frame_seg_begin = h->frame_seg_begin.as<int32_t>();
+  a.frame_seg_list = h->frame_seg_list.as<int32_t>();
+  a.frame_win_hi = h->frame_win_hi.as<int32_t>();
+  a.seg_lm = h->seg_lm.as<int32_t>();
+  a.seg_frame = h->seg_frame.as<int32_t>();
+  a.lm_seg_begin = h->lm_seg_begin.as<int32_t>();
+  a.seg_out = h->seg_out[c].p;
+  a.lm_aux = h->lm_aux.as<double>();
+  a.S = h->S();
+  a.b = h->bvec();
+  a.g_pose = h->gpose();
+  a.dU = h->dU();
+  a.ld = h->ld;
+  a.n_fixed = h->n_fixed;
+  tm_begin(h, TM_SCHUR);
+  if (h->precision == PTZBA_FP32)
+    launch_schur<float>(a, h->n_pose - h->n_fixed, h->st);
+  else
+    launch_schur<double>(a, h->n_pose - h->n_fixed, h->st);
+  tm_end(h, TM_SCHUR);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int ptzba_solve_reduced(ptzba_handle h) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  HIPCHK(hipSetDevice(h->device));
+  const int c = h->cur, nx = 1 - c;
+  const int n_free = h->n_pose - h->n_fixed;
+  tm_begin(h, TM_CHOL);
+  launch_pose_damp(h->S(), h->ld, h->dU(), h->D_pose.as<double>(), h->n_pose, h->n_fixed, h->lambda, h->st);
+  launch_chol_prepare(h->S(), h->ld, h->n_sys, h->bvec(), h->info.as<int>(), h->st);
+  launch_cholesky(h->S(), h->ld, h->info.as<int>(), h->tile_nz.as<int>(), h->st);
+  launch_chol_solve(h->S(), h->ld, h->bvec(), h->st);
+  tm_end(h, TM_CHOL);
+  HIPCHK(hipGetLastError());
+  tm_begin(h, TM_BACK);
+  HIPCHK(hipMemsetAsync(h->loc.p, 0, h->loc.bytes, h->st));
+  launch_pose_trial(h->ptz.as<double>(), h->bvec(), h->gpose(), h->D_pose.as<double>(), h->ptz_trial.as<double>(),
+                    h->n_pose, h->n_fixed, h->lambda, h->loc.as<double>(), h->st);
+  BacksubArgs b;
+  b.lm_seg_begin = h->lm_seg_begin.as<int32_t>();
+  b.seg_frame = h->seg_frame.as<int32_t>();
+  b.seg_out = h->seg_out[c].p;
+  b.lm_out = h->lm_out[c].as<double>();
+  b.lm_aux = h->lm_aux.as<double>();
+  b.D_ray = h->D_ray.as<double>();
+  b.dpose = h->bvec();
+  b.rays = h->rays.as<double>();
+  b.rays_trial = h->rays_trial.as<double>();
+  b.lm_red = h->lm_red.as<double>();
+  b.n_lm = h->n_lm;
+  b.n_fixed = h->n_fixed;
+  b.lambda = h->lambda;
+  if (h->precision == PTZBA_FP32)
+    launch_backsub<float>(b, h->st);
+  else
+    launch_backsub<double>(b, h->st);
+  tm_end(h, TM_BACK);
+  (void)n_free;
+  // trial linearisation (its cost decides acceptance; kept as the next linearisation if accepted)
+  tables(h, h->ptz_trial.as<double>(), h->rays_trial.as<double>());
+  linearize_into(h, nx);
+  HIPCHK(hipMemsetAsync(h->scal.p, 0, h->scal.bytes, h->st));
+  launch_reduce_cols(h->lm_out[nx].as<double>() + 5, h->n_lm, 8, 1, 0, h->scal.as<double>() + 1, h->st);
+  launch_reduce_cols(h->lm_red.as<double>(), h->n_lm, 4, 3, 0, h->scal.as<double>() + 2, h->st);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int ptzba_step(ptzba_handle h, double lambda) {
+  int rc = ptzba_build_reduced(h, lambda);
+  if (rc) return rc;
+  return ptzba_solve_reduced(h);
+}
+
+int ptzba_read_scalars(ptzba_handle h, double* out) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  HIPCHK(hipSetDevice(h->device));
+  double s[PTZBA_NSCALARS], l[PTZBA_NSCALARS];
+  int inf[4] = {0, 0, 0, 0};
+  HIPCHK(hipMemcpyAsync(s, h->scal.p, sizeof(s), hipMemcpyDeviceToHost, h->st));
+  HIPCHK(hipMemcpyAsync(l, h->loc.p, sizeof(l), hipMemcpyDeviceToHost, h->st));
+  HIPCHK(hipMemcpyAsync(inf, h->info.p, sizeof(int), hipMemcpyDeviceToHost, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  out[0] = s[0];
+  out[1] = s[1];
+  out[2] = s[2] + l[0];
+  out[3] = s[3] + l[1];
+  out[4] = s[4] + l[2];
+  out[5] = (double)inf[0];
+  out[6] = l[3];
+  out[7] = 0;
+  return 0;
+}
+
+int ptzba_accept(ptzba_handle h, int accept) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  if (accept) {
+    h->cur = 1 - h->cur;
+    std::swap(h->ptz.p, h->ptz_trial.p);
+    std::swap(h->ptz.bytes, h->ptz_trial.bytes);
+    std::swap(h->rays.p, h->rays_trial.p);
+    std::swap(h->rays.bytes, h->rays_trial.bytes);
+  }
+  return 0;
+}
+
+int ptzba_exchange(ptzba_handle h, void** sys_ptr, int64_t* sys_count, void** scal_ptr) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  if (sys_ptr) *sys_ptr = h->sys.p;
+  if (sys_count) *sys_count = h->sys_count();
+  if (scal_ptr) *scal_ptr = h->scal.p;
+  return 0;
+}
+
+int ptzba_sync(ptzba_handle h) {
+  if (!h) return fail("null handle");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->st));
+  return 0;
+}
+
+int ptzba_reset_kernel_times(ptzba_handle h, int enable) {
+  if (!h) return fail("null handle");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->st));
+  for (int k = 0; k < TM_N; ++k) {
+    if (enable && h->ev[k].empty()) {
+      h->ev[k].resize(TM_POOL);
+      for (auto& e : h->ev[k]) HIPCHK(hipEventCreate(&e));
+    }
+    h->ev_used[k] = 0;
+  }
+  h->timing = enable != 0;
+  return 0;
+}
+
+int ptzba_kernel_times(ptzba_handle h, double* ms_out, int64_t* count_out) {
+  if (!h) return fail("null handle");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->st));
+  for (int k = 0; k < TM_N; ++k) {
+    double tot = 0;
+    int n = h->ev_used[k] / 2;
+    for (int i = 0; i < n; ++i) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, h->ev[k][2 * i], h->ev[k][2 * i + 1]));
+      tot += ms;
+    }
+    ms_out[k] = n ? tot / n : 0.0;
+    count_out[k] = n;
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// camera model batch API
+// ------------------------------------------------------------------------------------------------
+struct Tmp {
+  std::vector<DBuf*> bufs;
+  ~Tmp() {
+    for (auto* b : bufs) delete b;
+  }
+  double* in(const double* h, size_t n) {
+    auto* b = new DBuf();
+    bufs.push_back(b);
+    if (b->alloc(n * 8)) return nullptr;
+    if (hipMemcpy(b->p, h, n * 8, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    return b->as<double>();
+  }
+  double* out(size_t n) {
+    auto* b = new DBuf();
+    bufs.push_back(b);
+    if (b->alloc(n * 8)) return nullptr;
+    return b->as<double>();
+  }
+};
+
+#define NEED(p)                                   \
+  do {                                            \
+    if (!(p)) return fail("device allocation/copy failed"); \
+  } while (0)
+
+int ptz_ray_to_image(int device, int64_t n, double u, double v, const double* f, const double* cp, const double* ct,
+                     const double* th, const double* ph, double* x_out, double* y_out) {
+  if (n < 0) return fail("n < 0");
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(device));
+  Tmp t;
+  double *df = t.in(f, n), *dcp = t.in(cp, n), *dct = t.in(ct, n), *dth = t.in(th, n), *dph = t.in(ph, n);
+  double *dx = t.out(n), *dy = t.out(n);
+  NEED(df && dcp && dct && dth && dph && dx && dy);
+  launch_ray_to_image(n, u, v, df, dcp, dct, dth, dph, dx, dy, nullptr);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(x_out, dx, n * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(y_out, dy, n * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int ptz_image_to_ray(int device, int64_t n, double u, double v, const double* f, const double* cp, const double* ct,
+                     const double* x, const double* y, double* th_out, double* ph_out) {
+  if (n < 0) return fail("n < 0");
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(device));
+  Tmp t;
+  double *df = t.in(f, n), *dcp = t.in(cp, n), *dct = t.in(ct, n), *dx = t.in(x, n), *dy = t.in(y, n);
+  double *dth = t.out(n), *dph = t.out(n);
+  NEED(df && dcp && dct && dx && dy && dth && dph);
+  launch_image_to_ray(n, u, v, df, dcp, dct, dx, dy, dth, dph, nullptr);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(th_out, dth, n * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(ph_out, dph, n * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int ptz_project_rays(int device, int64_t n, double u, double v, double f, double pan, double tilt, const double* d6,
+                     const double* rays, double* xy_out) {
+  if (n < 0) return fail("n < 0");
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(device));
+  Tmp t;
+  double *dr = t.in(rays, 2 * n), *dxy = t.out(2 * n);
+  NEED(dr && dxy);
+  launch_project_rays(n, u, v, f, pan, tilt, d6, dr, dxy, nullptr);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(xy_out, dxy, 2 * n * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int ptz_back_project_rays(int device, int64_t n, double u, double v, double f, double pan, double tilt,
+                          const double* d6, const double* xy, double* rays_out) {
+  if (n < 0) return fail("n < 0");
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(device));
+  Tmp t;
+  double *dxy = t.in(xy, 2 * n), *dr = t.out(2 * n);
+  NEED(dxy && dr);
+  launch_back_project(n, u, v, f, pan, tilt, d6, dxy, dr, nullptr);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(rays_out, dr, 2 * n * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int ptz_h_jacobian(int device, int64_t n, double u, double v, double f, double pan, double tilt, const double* d6,
+                   const double* rays, double* H_out) {
+  if (n < 0) return fail("n < 0");
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(device));
+  Tmp t;
+  const size_t nh = (size_t)(2 * n) * (size_t)(3 + 2 * n);
+  double *dr = t.in(rays, 2 * n), *dH = t.out(nh);
+  NEED(dr && dH);
+  HIPCHK(hipMemset(dH, 0, nh * 8));
+  launch_h_jacobian(n, u, v, f, pan, tilt, d6, dr, dH, nullptr);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(H_out, dH, nh * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// matching-graph landmark ids: first-seen rule of image_process.py:611-639 (bit-exact)
+// ------------------------------------------------------------------------------------------------
+int ptzba_build_landmarks(int32_t n_frames, const int64_t* kp_count, int64_t n_pairs, const int32_t* pair_i,
+                          const int32_t* pair_j, const int64_t* pair_count, const int64_t* idx_a, const int64_t* idx_b,
+                          int64_t* landmark_out, int64_t* n_landmark, int64_t* n_inconsistent) {
+  if (n_frames < 0 || n_pairs < 0) return fail("bad sizes");
+  std::vector<std::vector<int64_t>> map(n_frames);
+  for (int f = 0; f < n_frames; ++f) {
+    if (kp_count[f] < 0) return fail("bad kp_count");
+    map[f].assign((size_t)kp_count[f], -1);
+  }
+  int64_t g = 0, warn = 0, off = 0;
+  for (int64_t p = 0; p < n_pairs; ++p) {
+    const int i = pair_i[p], j = pair_j[p];
+    if (i < 0 || i >= n_frames || j < 0 || j >= n_frames) return fail("pair %lld: frame out of range", (long long)p);
+    for (int64_t k = 0; k < pair_count[p]; ++k) {
+      const int64_t a = idx_a[off + k], b = idx_b[off + k];
+      if (a < 0 || a >= kp_count[i] || b < 0 || b >= kp_count[j]) return fail("pair %lld: keypoint index out of range", (long long)p);
+      int64_t& ma = map[i][a];
+      int64_t& mb = map[j][b];
+      if (ma >= 0 && mb >= 0) {
+        if (ma != mb) ++warn;
+      } else if (ma >= 0) {
+        mb = ma;
+      } else if (mb >= 0) {
+        ma = mb;
+      } else {
+        ma = g;
+        mb = g;
+        ++g;
+      }
+    }
+    off += pair_count[p];
+  }
+  // landmark of each match = landmark_index_map[i][idx1] after all pairs (image_process.py:652-653)
+  off = 0;
+  for (int64_t p = 0; p < n_pairs; ++p) {
+    for (int64_t k = 0; k < pair_count[p]; ++k) landmark_out[off + k] = map[pair_i[p]][idx_a[off + k]];
+    off += pair_count[p];
+  }
+  *n_landmark = g;
+  if (n_inconsistent) *n_inconsistent = warn;
+  return 0;
+}
+
+

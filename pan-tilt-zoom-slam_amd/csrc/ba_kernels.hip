@@ -1,0 +1,556 @@
+// Bundle-adjustment kernels for gfx950 (CDNA4, wave64).
+//
+// Hot path: one Levenberg-Marquardt iteration over the reference's
+// pair-form reprojection residual (bundle_adjustment.py:25-106), solved exactly through the
+// Schur complement on the keyframe poses instead of scipy's dense FD-Jacobian + SVD trf
+// (bundle_adjustment.py:200-202).
+//
+// Data layout in HBM (all built once by ptzba_set_problem, see api.hip):
+//   records   sorted by (landmark, frame, original index); SoA  rec_xy[2R] (real), rec_seg[R] (int32)
+//             and optional rec_w[R] (multiplicity of de-duplicated records)
+//   segments  one per unique (landmark, frame): seg_frame, seg_rec_begin (CSR into records);
+//             landmark CSR lm_seg_begin; frame CSR frame_seg_begin/frame_seg_list
+//   tables    FrameTab[n_pose] (cos/sin pan, cos/sin tilt, f), RayTab[n_lm] (ray direction + derivs)
+//   lin       seg_out[n_seg][16] = W(3x2) | U(3x3 sym, 6) | g_pose(3) | pad   (real)
+//             lm_out[n_lm][8]    = V(2x2 sym, 3) | g_ray(2) | cost | pad      (fp64)
+//
+// K1 `k_linearize` is the HBM-streaming kernel: one wave per landmark walks the landmark's records
+// (coalesced 8/16-B loads), forms residuals against per-segment projections staged in LDS, and
+// segment-reduces the sufficient statistics (sum w, sum w r per image axis) with a wave64 segmented
+// scan.  All observations of one (frame, landmark) segment share the projection and the 2x5
+// Jacobian (they depend on pose and ray only), so the Jacobian and the 3x3/3x2/2x2 normal-equation
+// blocks are formed once per segment.
+#include "ptzba_common.h"
+#include "ptzba_kernels.h"
+
+namespace ptzba {
+
+// ------------------------------------------------------------------------------------------------
+// tables
+// ------------------------------------------------------------------------------------------------
+template <typename real>
+__global__ void k_tables(const double* __restrict__ ptz, const double* __restrict__ rays, int n_pose,
+                         int n_lm, FrameTab<real>* __restrict__ ft, RayTab<real>* __restrict__ rt) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_pose) {
+    ft[i] = make_frame_tab<real>(ptz[3 * i], ptz[3 * i + 1], ptz[3 * i + 2]);
+  } else if (i < n_pose + n_lm) {
+    int l = i - n_pose;
+    rt[l] = make_ray_tab<real>(rays[2 * l], rays[2 * l + 1]);
+  }
+}
+
+template <typename real>
+void launch_tables(const double* ptz, const double* rays, int n_pose, int n_lm, void* ft, void* rt,
+                   hipStream_t st) {
+  int n = n_pose + n_lm;
+  hipLaunchKernelGGL(k_tables<real>, dim3((n + 255) / 256), dim3(256), 0, st, ptz, rays, n_pose, n_lm,
+                     (FrameTab<real>*)ft, (RayTab<real>*)rt);
+}
+
+// ------------------------------------------------------------------------------------------------
+// K1: linearize (residual + Jacobian + per-segment / per-landmark normal-equation blocks + cost)
+// ------------------------------------------------------------------------------------------------
+constexpr int SEGW = 128;  // segments per LDS window per wave
+
+template <typename real, int LOSS>
+__global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
+  __shared__ real s_x[4][SEGW], s_y[4][SEGW], s_acc[4][4][SEGW];
+  const int lane = lane_id();
+  const int wv = threadIdx.x >> 6;
+  const int task = blockIdx.x * 4 + wv;
+  if (task >= a.n_work) return;  // whole wave leaves; no block-level barriers in this kernel
+  const int l = a.lm_order[task];
+  const int s0 = a.lm_seg_begin[l], s1 = a.lm_seg_begin[l + 1];
+  const FrameTab<real>* __restrict__ ft = (const FrameTab<real>*)a.ft;
+  const RayTab<real> R = ((const RayTab<real>*)a.rt)[l];
+  const real* __restrict__ rec_xy = (const real*)a.rec_xy;
+  const real* __restrict__ rec_w = (const real*)a.rec_w;
+  real* __restrict__ seg_out = (real*)a.seg_out;
+  const real u = (real)a.u, v = (real)a.v;
+  const real fs2 = (real)a.fs2, ifs2 = (real)a.inv_fs2;
+  real* sx = s_x[wv];
+  real* sy = s_y[wv];
+  real* acc0 = s_acc[wv][0];
+  real* acc1 = s_acc[wv][1];
+  real* acc2 = s_acc[wv][2];
+  real* acc3 = s_acc[wv][3];
+
+  double V00 = 0, V01 = 0, V11 = 0, g0 = 0, g1 = 0, cost = 0;
+
+  for (int w0 = s0; w0 < s1; w0 += SEGW) {
+    const int w1 = min(s1, w0 + SEGW);
+    // phase A: projection of every segment of the window (lanes over segments)
+    for (int s = w0 + lane; s < w1; s += WAVE) {
+      const int sl = s - w0;
+      real x, y;
+      ptz_project<real>(ft[a.seg_frame[s]], R, u, v, x, y);
+      sx[sl] = x;
+      sy[sl] = y;
+      acc0[sl] = 0; acc1[sl] = 0; acc2[sl] = 0; acc3[sl] = 0;
+    }
+    wave_lds_fence();
+    // phase B: stream the window's records (coalesced), segmented reduction into LDS
+    const int64_t r0 = a.seg_rec_begin[w0], r1 = a.seg_rec_begin[w1];
+    for (int64_t rb = r0; rb < r1; rb += WAVE) {
+      const int64_t r = rb + lane;
+      const bool valid = r < r1;
+      int key = -1;
+      real ox = 0, oy = 0, wt = 0;
+      if (valid) {
+        key = a.rec_seg[r] - w0;
+        if constexpr (sizeof(real) == 4) {
+          float2 o = reinterpret_cast<const float2*>(rec_xy)[r];
+          ox = o.x; oy = o.y;
+        } else {
+          double2 o = reinterpret_cast<const double2*>(rec_xy)[r];
+          ox = o.x; oy = o.y;
+        }
+        wt = rec_w ? rec_w[r] : (real)1;
+      }
+      real rx = 0, ry = 0;
+      if (valid) {
+        rx = sx[key] - ox;
+        ry = sy[key] - oy;
+      }
+      real wx, wy, c;
+      if constexpr (LOSS == 0) {
+        wx = wt; wy = wt;
+        c = wt * (rx * rx + ry * ry);
+      } else {
+        // scipy 'huber': rho(z) = z (z<=1), 2 sqrt(z) - 1; weight rho'(z) = 1 or 1/sqrt(z)
+        real zx = rx * rx * ifs2, zy = ry * ry * ifs2;
+        real sqx = sqrt(zx), sqy = sqrt(zy);
+        bool ix = zx <= (real)1, iy = zy <= (real)1;
+        wx = ix ? wt : wt / sqx;
+        wy = iy ? wt : wt / sqy;
+        c = wt * fs2 * ((ix ? zx : (real)2 * sqx - (real)1) + (iy ? zy : (real)2 * sqy - (real)1));
+      }
+      cost += (double)c;
+      real v0 = wx, v1 = wy, v2 = wx * rx, v3 = wy * ry;
+      // segmented inclusive scan over the wave, segments = runs of equal key (records are sorted)
+#pragma unroll
+      for (int d = 1; d < WAVE; d <<= 1) {
+        int kk = __shfl_up(key, d, WAVE);
+        real t0 = __shfl_up(v0, d, WAVE);
+        real t1 = __shfl_up(v1, d, WAVE);
+        real t2 = __shfl_up(v2, d, WAVE);
+        real t3 = __shfl_up(v3, d, WAVE);
+        if (lane >= d && kk == key) {
+          v0 += t0; v1 += t1; v2 += t2; v3 += t3;
+        }
+      }
+      int knext = __shfl_down(key, 1, WAVE);
+      bool last = (lane == WAVE - 1) || (knext != key);
+      if (valid && last) {  // one writer per run per chunk; runs crossing chunks add in order
+        acc0[key] += v0; acc1[key] += v1; acc2[key] += v2; acc3[key] += v3;
+      }
+    }
+    wave_lds_fence();
+    // phase C: per-segment Jacobian and normal-equation blocks
+    for (int s = w0 + lane; s < w1; s += WAVE) {
+      const int sl = s - w0;
+      real x, y, J[2][5];
+      ptz_project_jac<real>(ft[a.seg_frame[s]], R, u, v, x, y, J);
+      const real Sx = acc0[sl], Sy = acc1[sl], Srx = acc2[sl], Sry = acc3[sl];
+      real* o = seg_out + (int64_t)s * 16;
+      // W = Jp^T diag(Sx,Sy) Jr  (3x2)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        o[2 * p + 0] = Sx * J[0][p] * J[0][3] + Sy * J[1][p] * J[1][3];
+        o[2 * p + 1] = Sx * J[0][p] * J[0][4] + Sy * J[1][p] * J[1][4];
+      }
+      // U = Jp^T diag Jp (upper: 00 01 02 11 12 22)
+      o[6] = Sx * J[0][0] * J[0][0] + Sy * J[1][0] * J[1][0];
+      o[7] = Sx * J[0][0] * J[0][1] + Sy * J[1][0] * J[1][1];
+      o[8] = Sx * J[0][0] * J[0][2] + Sy * J[1][0] * J[1][2];
+      o[9] = Sx * J[0][1] * J[0][1] + Sy * J[1][1] * J[1][1];
+      o[10] = Sx * J[0][1] * J[0][2] + Sy * J[1][1] * J[1][2];
+      o[11] = Sx * J[0][2] * J[0][2] + Sy * J[1][2] * J[1][2];
+      // g_pose = Jp^T (w r)
+      o[12] = J[0][0] * Srx + J[1][0] * Sry;
+      o[13] = J[0][1] * Srx + J[1][1] * Sry;
+      o[14] = J[0][2] * Srx + J[1][2] * Sry;
+      o[15] = 0;
+      V00 += (double)(Sx * J[0][3] * J[0][3] + Sy * J[1][3] * J[1][3]);
+      V01 += (double)(Sx * J[0][3] * J[0][4] + Sy * J[1][3] * J[1][4]);
+      V11 += (double)(Sx * J[0][4] * J[0][4] + Sy * J[1][4] * J[1][4]);
+      g0 += (double)(J[0][3] * Srx + J[1][3] * Sry);
+      g1 += (double)(J[0][4] * Srx + J[1][4] * Sry);
+    }
+    wave_lds_fence();
+  }
+  V00 = wave_sum(V00); V01 = wave_sum(V01); V11 = wave_sum(V11);
+  g0 = wave_sum(g0); g1 = wave_sum(g1); cost = wave_sum(cost);
+  if (lane == 0) {
+    double* o = a.lm_out + (int64_t)l * 8;
+    o[0] = V00; o[1] = V01; o[2] = V11; o[3] = g0; o[4] = g1; o[5] = 0.5 * cost; o[6] = 0; o[7] = 0;
+  }
+}
+
+template <typename real>
+void launch_linearize(const LinArgs& a, int loss, hipStream_t st) {
+  if (a.n_work <= 0) return;
+  dim3 grid((a.n_work + 3) / 4);
+  if (loss == 0)
+    hipLaunchKernelGGL((k_linearize<real, 0>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((k_linearize<real, 1>), grid, dim3(256), 0, st, a);
+}
+
+// ------------------------------------------------------------------------------------------------
+// landmark damping: V~ = V + lambda diag(D), D = max(D, diag V) (Marquardt scaling with the
+// monotone column-norm memory of scipy's x_scale='jac', common.py:598-612); Vinv and Vinv g.
+// lm_aux[l][8] = Vinv00 Vinv01 Vinv11 (Vinv g)0 (Vinv g)1 . . .
+// ------------------------------------------------------------------------------------------------
+__global__ void k_landmark_damp(const double* __restrict__ lm_out, const int32_t* __restrict__ lm_seg_begin,
+                                double* __restrict__ D_ray, double* __restrict__ lm_aux, int n_lm,
+                                double lambda) {
+  int l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= n_lm) return;
+  double* o = lm_aux + (int64_t)l * 8;
+  if (lm_seg_begin[l + 1] == lm_seg_begin[l]) {
+    for (int k = 0; k < 8; ++k) o[k] = 0;
+    return;
+  }
+  const double* in = lm_out + (int64_t)l * 8;
+  double d0 = fmax(D_ray[2 * l], fmax(in[0], 1e-12));
+  double d1 = fmax(D_ray[2 * l + 1], fmax(in[2], 1e-12));
+  D_ray[2 * l] = d0;
+  D_ray[2 * l + 1] = d1;
+  double a = in[0] + lambda * d0, b = in[1], c = in[2] + lambda * d1;
+  double det = a * c - b * b;
+  double i00 = 0, i01 = 0, i11 = 0;
+  if (det > 0 && isfinite(det)) {
+    double id = 1.0 / det;
+    i00 = c * id; i01 = -b * id; i11 = a * id;
+  }
+  o[0] = i00; o[1] = i01; o[2] = i11;
+  o[3] = i00 * in[3] + i01 * in[4];
+  o[4] = i01 * in[3] + i11 * in[4];
+  o[5] = 0; o[6] = 0; o[7] = det > 0 ? 0.0 : 1.0;
+}
+
+void launch_landmark_damp(const double* lm_out, const int32_t* lm_seg_begin, double* D_ray, double* lm_aux,
+                          int n_lm, double lambda, hipStream_t st) {
+  hipLaunchKernelGGL(k_landmark_damp, dim3((n_lm + 255) / 256), dim3(256), 0, st, lm_out, lm_seg_begin, D_ray,
+                     lm_aux, n_lm, lambda);
+}
+
+// ------------------------------------------------------------------------------------------------
+// K2: reduced camera system  S = U + lambda D - sum_l W_l V~_l^-1 W_l^T,
+//                            b = -g_pose + sum_l W_l V~_l^-1 g_l
+// One workgroup per free frame f1 builds block column f1 of the lower triangle (frames f2 >= f1);
+// the 3x3 blocks S[f1, f2] accumulate in LDS (fp64 atomics: each landmark's segments have distinct
+// frames, so lanes of one wave never collide; waves do).
+// ------------------------------------------------------------------------------------------------
+constexpr int SCHUR_WMAX = 448;  // frames per LDS window (448 * 9 * 8 B = 31.5 KiB)
+
+template <typename real>
+__global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
+  __shared__ double s_S[SCHUR_WMAX * 9];
+  __shared__ double s_red[4][16];
+  const int f1 = blockIdx.x + a.n_fixed;
+  const int lane = lane_id();
+  const int wv = threadIdx.x >> 6;
+  const real* __restrict__ seg_out = (const real*)a.seg_out;
+  const int e0 = a.frame_seg_begin[f1], e1 = a.frame_seg_begin[f1 + 1];
+  const int hi = a.frame_win_hi[f1];
+  const int col0 = 3 * (f1 - a.n_fixed);
+  const int64_t ld = a.ld;
+
+  // per-wave uniform accumulators: U (6), g_pose (3), sum W Vinv g (3)
+  double aU[6] = {0, 0, 0, 0, 0, 0}, ag[3] = {0, 0, 0}, ab[3] = {0, 0, 0};
+
+  for (int p0 = f1; p0 <= hi; p0 += SCHUR_WMAX) {
+    const int p1 = min(hi + 1, p0 + SCHUR_WMAX);  // window [p0, p1)
+    const int width = p1 - p0;
+    for (int k = threadIdx.x; k < width * 9; k += blockDim.x) s_S[k] = 0;
+    __syncthreads();
+    const bool first = (p0 == f1);
+    for (int e = e0 + wv; e < e1; e += 4) {
+      const int s1 = a.frame_seg_list[e];
+      const int l = a.seg_lm[s1];
+      const real* w1 = seg_out + (int64_t)s1 * 16;
+      const double* vi = a.lm_aux + (int64_t)l * 8;
+      const double i00 = vi[0], i01 = vi[1], i11 = vi[2];
+      double W[3][2];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) { W[q][0] = (double)w1[2 * q]; W[q][1] = (double)w1[2 * q + 1]; }
+      double Y[3][2];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        Y[q][0] = W[q][0] * i00 + W[q][1] * i01;
+        Y[q][1] = W[q][0] * i01 + W[q][1] * i11;
+      }
+      if (first) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) aU[k] += (double)w1[6 + k];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          ag[q] += (double)w1[12 + q];
+          ab[q] += W[q][0] * vi[3] + W[q][1] * vi[4];
+        }
+      }
+      const int send = a.lm_seg_begin[l + 1];
+      for (int s2 = s1 + lane; s2 < send; s2 += WAVE) {
+        const int f2 = a.seg_frame[s2];
+        if (f2 < p0) continue;
+        if (f2 >= p1) break;
+        const real* w2 = seg_out + (int64_t)s2 * 16;
+        double X[3][2];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) { X[q][0] = (double)w2[2 * q]; X[q][1] = (double)w2[2 * q + 1]; }
+        double* dst = s_S + (f2 - p0) * 9;
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+#pragma unroll
+          for (int r = 0; r < 3; ++r) atomicAdd(dst + 3 * q + r, -(Y[q][0] * X[r][0] + Y[q][1] * X[r][1]));
+      }
+    }
+    __syncthreads();
+    if (first) {
+      // combine the per-wave uniform accumulators
+      if (lane == 0) {
+        for (int k = 0; k < 6; ++k) s_red[wv][k] = aU[k];
+        for (int q = 0; q < 3; ++q) { s_red[wv][6 + q] = ag[q]; s_red[wv][9 + q] = ab[q]; }
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        double U[6], g[3], bb[3];
+        for (int k = 0; k < 6; ++k) U[k] = s_red[0][k] + s_red[1][k] + s_red[2][k] + s_red[3][k];
+        for (int q = 0; q < 3; ++q) {
+          g[q] = s_red[0][6 + q] + s_red[1][6 + q] + s_red[2][6 + q] + s_red[3][6 + q];
+          bb[q] = s_red[0][9 + q] + s_red[1][9 + q] + s_red[2][9 + q] + s_red[3][9 + q];
+        }
+        // diagonal block: U + Schur part already in s_S[0..8]; Marquardt damping is added after
+        // the (multi-GPU) exchange from the diag(U) written here (k_pose_damp)
+        const int ui[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
+        for (int q = 0; q < 3; ++q)
+          for (int r = 0; r < 3; ++r) s_S[3 * q + r] += U[ui[q][r]];
+        a.dU[col0 + 0] = U[0];
+        a.dU[col0 + 1] = U[3];
+        a.dU[col0 + 2] = U[5];
+        for (int q = 0; q < 3; ++q) {
+          a.b[col0 + q] = -g[q] + bb[q];
+          a.g_pose[col0 + q] = g[q];
+        }
+      }
+      __syncthreads();
+    }
+    // write block column f1, rows of frames in [p0, p1): S[row(f2)+r][col0+q] = S_{f1,f2}[q][r]
+    for (int k = threadIdx.x; k < width * 9; k += blockDim.x) {
+      const int t = k / 9, qr = k % 9, q = qr / 3, r = qr % 3;
+      const int f2 = p0 + t;
+      if (f2 < a.n_fixed) continue;
+      const int64_t row = 3 * (f2 - a.n_fixed) + r;
+      a.S[row * ld + col0 + q] = s_S[k];
+    }
+    __syncthreads();
+  }
+}
+
+template <typename real>
+void launch_schur(const SchurArgs& a, int n_free, hipStream_t st) {
+  if (n_free <= 0) return;
+  hipLaunchKernelGGL(k_schur<real>, dim3(n_free), dim3(256), 0, st, a);
+}
+
+// pose damping on the exchanged reduced system: D = max(D, diag U) (monotone), S_ii += lambda D_i
+__global__ void k_pose_damp(double* __restrict__ S, int64_t ld, const double* __restrict__ dU,
+                            double* __restrict__ D_pose, int n_pose, int n_fixed, double lambda) {
+  int k = blockIdx.x * blockDim.x + threadIdx.x;
+  int n = 3 * (n_pose - n_fixed);
+  if (k >= n) return;
+  double* D = D_pose + 3 * n_fixed + k;
+  double d = fmax(*D, fmax(dU[k], 1e-12));
+  *D = d;
+  S[(int64_t)k * ld + k] += lambda * d;
+}
+
+void launch_pose_damp(double* S, int64_t ld, const double* dU, double* D_pose, int n_pose, int n_fixed, double lambda,
+                      hipStream_t st) {
+  int n = 3 * (n_pose - n_fixed);
+  if (n > 0) hipLaunchKernelGGL(k_pose_damp, dim3((n + 255) / 256), dim3(256), 0, st, S, ld, dU, D_pose, n_pose, n_fixed, lambda);
+}
+
+// ------------------------------------------------------------------------------------------------
+// K5: back-substitution of the rays + trial state + predicted-reduction partials
+//   delta_l = -Vinv (g_l + sum_s W_s^T delta_p(f_s));  trial ray = ray + delta_l
+//   pred_l  = -1/2 g_l.delta_l + 1/2 lambda delta_l^T D delta_l
+// one wave per landmark (lanes over segments)
+// ------------------------------------------------------------------------------------------------
+template <typename real>
+__global__ __launch_bounds__(256) void k_backsub(BacksubArgs a) {
+  const int lane = lane_id();
+  const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (l >= a.n_lm) return;
+  const int s0 = a.lm_seg_begin[l], s1 = a.lm_seg_begin[l + 1];
+  const real* __restrict__ seg_out = (const real*)a.seg_out;
+  double t0 = 0, t1 = 0;
+  for (int s = s0 + lane; s < s1; s += WAVE) {
+    const int f = a.seg_frame[s];
+    if (f < a.n_fixed) continue;
+    const double* dp = a.dpose + 3 * (f - a.n_fixed);
+    const real* w = seg_out + (int64_t)s * 16;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      t0 += (double)w[2 * q] * dp[q];
+      t1 += (double)w[2 * q + 1] * dp[q];
+    }
+  }
+  t0 = wave_sum(t0);
+  t1 = wave_sum(t1);
+  if (lane == 0) {
+    double* red = a.lm_red + (int64_t)l * 4;
+    const double th = a.rays[2 * l], ph = a.rays[2 * l + 1];
+    if (s1 == s0) {
+      a.rays_trial[2 * l] = th;
+      a.rays_trial[2 * l + 1] = ph;
+      red[0] = 0; red[1] = 0; red[2] = 0; red[3] = 0;
+      return;
+    }
+    const double* lo = a.lm_out + (int64_t)l * 8;
+    const double* vi = a.lm_aux + (int64_t)l * 8;
+    const double r0 = lo[3] + t0, r1 = lo[4] + t1;
+    const double d0 = -(vi[0] * r0 + vi[1] * r1);
+    const double d1 = -(vi[1] * r0 + vi[2] * r1);
+    a.rays_trial[2 * l] = th + d0;
+    a.rays_trial[2 * l + 1] = ph + d1;
+    const double D0 = a.D_ray[2 * l], D1 = a.D_ray[2 * l + 1];
+    red[0] = -0.5 * (lo[3] * d0 + lo[4] * d1) + 0.5 * a.lambda * (D0 * d0 * d0 + D1 * d1 * d1);
+    red[1] = d0 * d0 + d1 * d1;
+    red[2] = th * th + ph * ph;
+    red[3] = fmax(fabs(lo[3]), fabs(lo[4]));
+  }
+}
+
+template <typename real>
+void launch_backsub(const BacksubArgs& a, hipStream_t st) {
+  if (a.n_lm <= 0) return;
+  hipLaunchKernelGGL(k_backsub<real>, dim3((a.n_lm + 3) / 4), dim3(256), 0, st, a);
+}
+
+// pose trial + pose partials (identical on every rank): one block
+__global__ void k_pose_trial(const double* __restrict__ ptz, const double* __restrict__ dpose,
+                             const double* __restrict__ g_pose, const double* __restrict__ D_pose,
+                             double* __restrict__ ptz_trial, int n_pose, int n_fixed, double lambda,
+                             double* __restrict__ out4) {
+  __shared__ double red[4][1024 / WAVE];
+  double pr = 0, dx = 0, xx = 0, gm = 0;
+  for (int i = threadIdx.x; i < 3 * n_pose; i += blockDim.x) {
+    const int f = i / 3;
+    const double x = ptz[i];
+    xx += x * x;
+    if (f < n_fixed) {
+      ptz_trial[i] = x;
+      continue;
+    }
+    const int k = i - 3 * n_fixed;
+    const double d = dpose[k];
+    ptz_trial[i] = x + d;
+    pr += -0.5 * g_pose[k] * d + 0.5 * lambda * D_pose[i] * d * d;
+    dx += d * d;
+    gm = fmax(gm, fabs(g_pose[k]));
+  }
+  pr = wave_sum(pr); dx = wave_sum(dx); xx = wave_sum(xx);
+  for (int o = 32; o > 0; o >>= 1) gm = fmax(gm, __shfl_xor(gm, o, WAVE));
+  const int w = threadIdx.x >> 6;
+  if (lane_id() == 0) { red[0][w] = pr; red[1][w] = dx; red[2][w] = xx; red[3][w] = gm; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    for (int k = 0; k < (int)(blockDim.x / WAVE); ++k) {
+      s0 += red[0][k]; s1 += red[1][k]; s2 += red[2][k]; s3 = fmax(s3, red[3][k]);
+    }
+    out4[0] = s0; out4[1] = s1; out4[2] = s2; out4[3] = s3;
+  }
+}
+
+void launch_pose_trial(const double* ptz, const double* dpose, const double* g_pose, const double* D_pose,
+                       double* ptz_trial, int n_pose, int n_fixed, double lambda, double* out4, hipStream_t st) {
+  hipLaunchKernelGGL(k_pose_trial, dim3(1), dim3(1024), 0, st, ptz, dpose, g_pose, D_pose, ptz_trial, n_pose,
+                     n_fixed, lambda, out4);
+}
+
+// deterministic strided reduction: out[k] = sum_i src[i*stride + off[k]] (fixed order), k < nk.
+// mode bit k set -> max(|.|) instead of sum for column k
+__global__ void k_reduce_cols(const double* __restrict__ src, int64_t n, int stride, int nk, int maxmask,
+                              double* __restrict__ out) {
+  __shared__ double red[8][1024 / WAVE];
+  double acc[8];
+  for (int k = 0; k < 8; ++k) acc[k] = 0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    for (int k = 0; k < nk; ++k) {
+      double x = src[i * stride + k];
+      if (maxmask & (1 << k)) acc[k] = fmax(acc[k], fabs(x));
+      else acc[k] += x;
+    }
+  }
+  for (int k = 0; k < nk; ++k) {
+    if (maxmask & (1 << k)) {
+      for (int o = 32; o > 0; o >>= 1) acc[k] = fmax(acc[k], __shfl_xor(acc[k], o, WAVE));
+    } else {
+      acc[k] = wave_sum(acc[k]);
+    }
+  }
+  const int w = threadIdx.x >> 6;
+  if (lane_id() == 0)
+    for (int k = 0; k < nk; ++k) red[k][w] = acc[k];
+  __syncthreads();
+  if (threadIdx.x < nk) {
+    const int k = threadIdx.x;
+    double s = 0;
+    for (int j = 0; j < (int)(blockDim.x / WAVE); ++j) s = (maxmask & (1 << k)) ? fmax(s, red[k][j]) : s + red[k][j];
+    out[k] = s;
+  }
+}
+
+void launch_reduce_cols(const double* src, int64_t n, int stride, int nk, int maxmask, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_reduce_cols, dim3(1), dim3(1024), 0, st, src, n, stride, nk, maxmask, out);
+}
+
+// ------------------------------------------------------------------------------------------------
+// record-order residual (parity API for bundle_adjustment._compute_residual)
+// ------------------------------------------------------------------------------------------------
+template <typename real>
+__global__ void k_residual(const int32_t* __restrict__ rec_seg, const int32_t* __restrict__ seg_frame,
+                           const int32_t* __restrict__ seg_lm, const real* __restrict__ rec_xy,
+                           const int64_t* __restrict__ perm, const FrameTab<real>* __restrict__ ft,
+                           const RayTab<real>* __restrict__ rt, double u, double v, int64_t n_rec,
+                           double* __restrict__ r_out) {
+  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rec) return;
+  const int s = rec_seg[r];
+  real x, y;
+  ptz_project<real>(ft[seg_frame[s]], rt[seg_lm[s]], (real)u, (real)v, x, y);
+  const int64_t o = perm[r];
+  r_out[2 * o] = (double)(x - rec_xy[2 * r]);
+  r_out[2 * o + 1] = (double)(y - rec_xy[2 * r + 1]);
+}
+
+template <typename real>
+void launch_residual(const int32_t* rec_seg, const int32_t* seg_frame, const int32_t* seg_lm, const void* rec_xy,
+                     const int64_t* perm, const void* ft, const void* rt, double u, double v, int64_t n_rec,
+                     double* r_out, hipStream_t st) {
+  if (n_rec <= 0) return;
+  hipLaunchKernelGGL(k_residual<real>, dim3((unsigned)((n_rec + 255) / 256)), dim3(256), 0, st, rec_seg, seg_frame,
+                     seg_lm, (const real*)rec_xy, perm, (const FrameTab<real>*)ft, (const RayTab<real>*)rt, u, v,
+                     n_rec, r_out);
+}
+
+// explicit instantiations
+template void launch_tables<float>(const double*, const double*, int, int, void*, void*, hipStream_t);
+template void launch_tables<double>(const double*, const double*, int, int, void*, void*, hipStream_t);
+template void launch_linearize<float>(const LinArgs&, int, hipStream_t);
+template void launch_linearize<double>(const LinArgs&, int, hipStream_t);
+template void launch_schur<float>(const SchurArgs&, int, hipStream_t);
+template void launch_schur<double>(const SchurArgs&, int, hipStream_t);
+template void launch_backsub<float>(const BacksubArgs&, hipStream_t);
+template void launch_backsub<double>(const BacksubArgs&, hipStream_t);
+template void launch_residual<float>(const int32_t*, const int32_t*, const int32_t*, const void*, const int64_t*,
+                                     const void*, const void*, double, double, int64_t, double*, hipStream_t);
+template void launch_residual<double>(const int32_t*, const int32_t*, const int32_t*, const void*, const int64_t*,
+                                      const void*, const void*, double, double, int64_t, double*, hipStream_t);
+
+}  // namespace ptzba

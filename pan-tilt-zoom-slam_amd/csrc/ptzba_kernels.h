@@ -1,0 +1,97 @@
+// Kernel argument blocks and host-side launchers of libptzba (internal header).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ptzba {
+
+struct LinArgs {
+  const int32_t* lm_order;       // [n_work] landmarks to process, heaviest first
+  int n_work;
+  const int32_t* lm_seg_begin;   // [n_lm+1]
+  const int32_t* seg_frame;      // [n_seg]
+  const int64_t* seg_rec_begin;  // [n_seg+1]
+  const int32_t* rec_seg;        // [n_rec]
+  const void* rec_xy;            // [2 n_rec] real
+  const void* rec_w;             // [n_rec] real or nullptr
+  const void* ft;                // FrameTab<real>[n_pose]
+  const void* rt;                // RayTab<real>[n_lm]
+  double u, v, fs2, inv_fs2;
+  void* seg_out;                 // [n_seg][16] real
+  double* lm_out;                // [n_lm][8]
+};
+
+struct SchurArgs {
+  const int32_t* frame_seg_begin;  // [n_pose+1]
+  const int32_t* frame_seg_list;   // [n_seg]
+  const int32_t* frame_win_hi;     // [n_pose]
+  const int32_t* seg_lm;           // [n_seg]
+  const int32_t* seg_frame;        // [n_seg]
+  const int32_t* lm_seg_begin;     // [n_lm+1]
+  const void* seg_out;             // [n_seg][16] real
+  const double* lm_aux;            // [n_lm][8]
+  double* S;                       // [ld][ld] lower, row-major
+  double* b;                       // [n_sys]
+  double* g_pose;                  // [n_sys]
+  double* dU;                      // [n_sys] diag of U (for Marquardt scaling)
+  int64_t ld;
+  int n_fixed;
+};
+
+struct BacksubArgs {
+  const int32_t* lm_seg_begin;
+  const int32_t* seg_frame;
+  const void* seg_out;
+  const double* lm_out;
+  const double* lm_aux;
+  const double* D_ray;
+  const double* dpose;   // [n_sys]
+  const double* rays;    // [2 n_lm]
+  double* rays_trial;    // [2 n_lm]
+  double* lm_red;        // [n_lm][4]: pred, |d|^2, |x|^2, |g|max
+  int n_lm;
+  int n_fixed;
+  double lambda;
+};
+
+template <typename real>
+void launch_tables(const double* ptz, const double* rays, int n_pose, int n_lm, void* ft, void* rt, hipStream_t st);
+template <typename real>
+void launch_linearize(const LinArgs& a, int loss, hipStream_t st);
+void launch_landmark_damp(const double* lm_out, const int32_t* lm_seg_begin, double* D_ray, double* lm_aux, int n_lm,
+                          double lambda, hipStream_t st);
+template <typename real>
+void launch_schur(const SchurArgs& a, int n_free, hipStream_t st);
+void launch_pose_damp(double* S, int64_t ld, const double* dU, double* D_pose, int n_pose, int n_fixed, double lambda,
+                      hipStream_t st);
+template <typename real>
+void launch_backsub(const BacksubArgs& a, hipStream_t st);
+void launch_pose_trial(const double* ptz, const double* dpose, const double* g_pose, const double* D_pose,
+                       double* ptz_trial, int n_pose, int n_fixed, double lambda, double* out4, hipStream_t st);
+void launch_reduce_cols(const double* src, int64_t n, int stride, int nk, int maxmask, double* out, hipStream_t st);
+template <typename real>
+void launch_residual(const int32_t* rec_seg, const int32_t* seg_frame, const int32_t* seg_lm, const void* rec_xy,
+                     const int64_t* perm, const void* ft, const void* rt, double u, double v, int64_t n_rec,
+                     double* r_out, hipStream_t st);
+
+// dense SPD solve of the reduced camera system (chol_kernels.hip)
+// A: [ld][ld] row-major fp64, lower triangle of an SPD matrix whose rows >= n are identity padding;
+// factor in place (L), then x = A^-1 b (b overwritten by x).  info[0] != 0 if not positive definite.
+constexpr int CHOL_NB = 32;
+void launch_chol_prepare(double* A, int64_t ld, int n, double* b, int* info, hipStream_t st);
+void launch_cholesky(double* A, int64_t ld, int* info, int* tile_nz, hipStream_t st);
+void launch_chol_solve(const double* L, int64_t ld, double* b, hipStream_t st);
+
+// camera batch kernels (camera_kernels.hip)
+void launch_ray_to_image(int64_t n, double u, double v, const double* f, const double* cp, const double* ct,
+                         const double* th, const double* ph, double* x, double* y, hipStream_t st);
+void launch_image_to_ray(int64_t n, double u, double v, const double* f, const double* cp, const double* ct,
+                         const double* x, const double* y, double* th, double* ph, hipStream_t st);
+void launch_project_rays(int64_t n, double u, double v, double f, double pan, double tilt, const double* disp6,
+                         const double* rays, double* xy, hipStream_t st);
+void launch_back_project(int64_t n, double u, double v, double f, double pan, double tilt, const double* disp6,
+                         const double* xy, double* rays, hipStream_t st);
+void launch_h_jacobian(int64_t n, double u, double v, double f, double pan, double tilt, const double* disp6,
+                       const double* rays, double* H, hipStream_t st);
+
+}  // namespace ptzba

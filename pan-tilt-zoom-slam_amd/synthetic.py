@@ -1,0 +1,267 @@
+"""
+Synthetic PTZ keyframe x ray-landmark problems (SURVEY §8d "Synthetic inputs").
+
+The reference feeds BA from SIFT detection + matching on real images (image_process.py:509-667);
+neither the images nor OpenCV exist here, so this module generates the reference's own data
+format directly: per-frame keypoint arrays, per-pair match index lists, and from them the
+pair-form observation records that `bundle_adjustment._compute_residual`
+(bundle_adjustment.py:25-106) iterates over.
+
+Spec:
+  camera u, v = 640, 360, image 1280 x 720; keyframe pans linspace(lo, hi, N);
+  tilt ~ U[-12, -4] deg; f ~ U[2500, 3500] px;
+  rays theta ~ U[lo-14, hi+14], phi ~ U[-19, 3];
+  visibility 0<x<1280, 0<y<720, q2>0;
+  pairs i<j with overlap_pan_angle > 5 and > 20 shared rays; cap 200 per pair (seeded permutation);
+  keypoint noise N(0, 0.5 px); initial poses: frame 0 exact, others + N(0, [0.5, 0.2, 40]);
+  initial rays from from_image_to_ray of the src observation, last writer wins.
+
+Everything here is host-side problem *construction* (numpy): it is the stand-in for the
+camera + feature front-end, not part of the solve.  The solve runs in libptzba.so.
+"""
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+U0, V0 = 640.0, 360.0
+WIDTH, HEIGHT = 1280, 720
+
+CONFIGS = {
+    # name: (n_kf, n_rays, pan_lo, pan_hi, tilt_rows)
+    "config1": (10, 200, 50.0, 68.0, None),
+    "config2": (50, 2000, 30.0, 70.0, None),
+    "config3": (500, 20000, -60.0, 60.0, None),
+    "config4": (5000, 200000, -60.0, 60.0, tuple(range(-65, 26, 10))),
+}
+
+
+def _project(u, v, f, pan, tilt, theta, phi):
+    """Closed-form BA projection (q form): x = u + f q0/q2, y = v + f q1/|q2|.
+    Broadcasting over arrays. Returns x, y, q2."""
+    a = np.radians(pan); b = np.radians(tilt)
+    th = np.radians(theta); ph = np.radians(phi)
+    p0 = np.tan(th)
+    p1 = -np.tan(ph) / np.cos(th)
+    ca, sa, cb, sb = np.cos(a), np.sin(a), np.cos(b), np.sin(b)
+    w0 = ca * p0 - sa
+    w2 = sa * p0 + ca
+    q1 = cb * p1 + sb * w2
+    q2 = -sb * p1 + cb * w2
+    return u + f * w0 / q2, v + f * q1 / np.abs(q2), q2
+
+
+def image_to_ray(u, v, f, pan, tilt, x, y):
+    """Back-projection (ray init rule of bundle_adjustment.py:193), vectorised closed form.
+    Equivalent to TransFunction.from_image_to_ray (transformation.py:137-175)."""
+    a = np.radians(pan); b = np.radians(tilt)
+    ca, sa, cb, sb = np.cos(a), np.sin(a), np.cos(b), np.sin(b)
+    c0 = (x - u) / f
+    c1 = (y - v) / f
+    # camera ray c = [c0, c1, 1]; world direction d = R^T c, R = R_x(b) R_y(a)
+    # R_x^T c:
+    e0 = c0
+    e1 = cb * c1 - sb
+    e2 = sb * c1 + cb
+    # R_y^T e:
+    d0 = ca * e0 + sa * e2
+    d1 = e1
+    d2 = -sa * e0 + ca * e2
+    theta = np.degrees(np.arctan(d0 / d2))
+    phi = np.degrees(np.arctan(-d1 / np.sqrt(d0 * d0 + d2 * d2)))
+    return theta, phi
+
+
+def overlap_pan_angle(fl_1, pan_1, fl_2, pan_2, im_width):
+    """util.py:49-72, vectorised."""
+    w = im_width / 2.0
+    d1 = np.degrees(np.arctan(w / np.asarray(fl_1, dtype=np.float64)))
+    d2 = np.degrees(np.arctan(w / np.asarray(fl_2, dtype=np.float64)))
+    a1 = np.maximum(pan_1 - d1, pan_2 - d2)
+    a2 = np.minimum(pan_1 + d1, pan_2 + d2)
+    return np.maximum(0.0, a2 - a1)
+
+
+@dataclass
+class Scene:
+    """Ground-truth scene + per-frame keypoints (the 'detector output')."""
+    gt_ptz: np.ndarray            # [N, 3] pan, tilt, f
+    init_ptz: np.ndarray          # [N, 3] noisy initial poses (frame 0 exact)
+    gt_rays: np.ndarray           # [M, 2] theta, phi (deg)
+    kp_xy: list                   # N arrays [K_i, 2] noisy keypoints (fp64)
+    kp_ray: list                  # N arrays [K_i] generator ray id per keypoint
+    u: float = U0
+    v: float = V0
+
+
+@dataclass
+class Problem:
+    """Pair-form BA problem in the reference's residual order (bundle_adjustment.py:67-99)."""
+    n_pose: int
+    n_landmark: int
+    frame: np.ndarray             # [R] int32 record frame      (record 2m = src, 2m+1 = dst of match m)
+    landmark: np.ndarray          # [R] int32 record landmark id (first-seen rule, image_process.py:611-639)
+    xy: np.ndarray                # [R, 2] fp64 observation
+    init_ptz: np.ndarray          # [N, 3]
+    init_rays: np.ndarray         # [M, 2] last-writer-wins init
+    gt_ptz: np.ndarray            # [N, 3]
+    gt_rays: np.ndarray           # [M, 2] ground truth for the relabelled landmarks
+    u: float = U0
+    v: float = V0
+    n_pairs: int = 0
+    meta: dict = field(default_factory=dict)
+
+    @property
+    def n_match(self):
+        return len(self.frame) // 2
+
+
+def make_scene(n_kf, n_rays, pan_lo, pan_hi, seed=0, tilt_rows=None, noise=0.5,
+               init_sigma=(0.5, 0.2, 40.0)):
+    rng = np.random.default_rng(seed)
+    if tilt_rows is None:
+        pans = np.linspace(pan_lo, pan_hi, n_kf)
+        tilts = rng.uniform(-12.0, -4.0, n_kf)
+        phi_lo, phi_hi = -19.0, 3.0
+    else:
+        rows = np.asarray(tilt_rows, np.float64)
+        per = n_kf // len(rows)
+        pans = np.tile(np.linspace(pan_lo, pan_hi, per), len(rows))
+        tilts = np.repeat(rows, per) + rng.uniform(-1.0, 1.0, per * len(rows))
+        phi_lo, phi_hi = -(rows.max() + 7.0), -(rows.min() - 7.0)
+        phi_lo, phi_hi = max(phi_lo, -80.0), min(phi_hi, 80.0)
+    fs = rng.uniform(2500.0, 3500.0, len(pans))
+    gt_ptz = np.stack([pans, tilts, fs], 1)
+    theta = rng.uniform(pan_lo - 14.0, pan_hi + 14.0, n_rays)
+    phi = rng.uniform(phi_lo, phi_hi, n_rays)
+    gt_rays = np.stack([theta, phi], 1)
+    kp_xy, kp_ray = [], []
+    for i in range(len(pans)):
+        x, y, q2 = _project(U0, V0, fs[i], pans[i], tilts[i], theta, phi)
+        vis = (q2 > 0) & (x > 0) & (x < WIDTH) & (y > 0) & (y < HEIGHT)
+        ids = np.flatnonzero(vis)
+        pts = np.stack([x[ids], y[ids]], 1) + rng.normal(0.0, noise, (len(ids), 2))
+        kp_xy.append(pts)
+        kp_ray.append(ids.astype(np.int64))
+    init = gt_ptz.copy()
+    init[1:] += rng.normal(0.0, 1.0, (len(pans) - 1, 3)) * np.asarray(init_sigma)
+    return Scene(gt_ptz=gt_ptz, init_ptz=init, gt_rays=gt_rays, kp_xy=kp_xy, kp_ray=kp_ray)
+
+
+def scene_pairs(scene, seed=0, min_match=20, max_match=200, overlap_deg=5.0, cap=True):
+    """Ordered list of (i, j, idx_i list, idx_j list) for i<j: overlap mask on the *initial*
+    poses (bundle_adjustment.py:135-144), shared keypoints = ground-truth matches, keep if
+    > min_match (image_process.py:590), cap to max_match with a seeded permutation."""
+    rng = np.random.default_rng(seed + 7919)
+    n = len(scene.kp_xy)
+    ip = scene.init_ptz
+    n_rays = len(scene.gt_rays)
+    # position of each ray in each frame's keypoint list (-1 if not visible)
+    pos = []
+    for i in range(n):
+        p = np.full(n_rays, -1, np.int64)
+        p[scene.kp_ray[i]] = np.arange(len(scene.kp_ray[i]))
+        pos.append(p)
+    out = []
+    for i in range(n):
+        ov = overlap_pan_angle(ip[i, 2], ip[i, 0], ip[:, 2], ip[:, 0], WIDTH)
+        for j in range(i + 1, n):
+            if ov[j] <= overlap_deg:
+                continue
+            shared = scene.kp_ray[i][pos[j][scene.kp_ray[i]] >= 0]
+            if len(shared) <= min_match:
+                continue
+            if cap and len(shared) > max_match:
+                shared = shared[rng.permutation(len(shared))[:max_match]]
+            out.append((i, j, pos[i][shared], pos[j][shared]))
+    return out
+
+
+def problem_from_pairs(scene, pairs):
+    """Build the pair-form problem from ordered pair lists, reproducing the reference's
+    first-seen landmark ids (image_process.py:611-639) and last-writer ray init
+    (bundle_adjustment.py:184-194).  Ground-truth matches are consistent, so a keypoint's
+    landmark is its generator ray and the first-seen rule reduces to first-occurrence order."""
+    n = len(scene.kp_xy)
+    if not pairs:
+        raise ValueError("no matched pairs")
+    mi = np.concatenate([np.full(len(a), i, np.int64) for i, j, a, b in pairs])
+    mj = np.concatenate([np.full(len(a), j, np.int64) for i, j, a, b in pairs])
+    k1 = np.concatenate([np.asarray(a, np.int64) for i, j, a, b in pairs])
+    k2 = np.concatenate([np.asarray(b, np.int64) for i, j, a, b in pairs])
+    # generator ray of every match (src keypoint's ray)
+    kp_ray_flat = np.concatenate(scene.kp_ray)
+    kp_off = np.concatenate([[0], np.cumsum([len(r) for r in scene.kp_ray])])
+    kp_xy_flat = np.concatenate(scene.kp_xy)
+    ray = kp_ray_flat[kp_off[mi] + k1]
+    # first-seen relabelling
+    uniq, first = np.unique(ray, return_index=True)
+    order = np.argsort(first, kind="stable")
+    relabel = np.full(len(scene.gt_rays), -1, np.int64)
+    relabel[uniq[order]] = np.arange(len(uniq))
+    lm = relabel[ray]
+    m = len(uniq)
+    R = 2 * len(mi)
+    frame = np.empty(R, np.int32)
+    frame[0::2] = mi
+    frame[1::2] = mj
+    landmark = np.repeat(lm, 2).astype(np.int32)
+    xy = np.empty((R, 2))
+    xy[0::2] = kp_xy_flat[kp_off[mi] + k1]
+    xy[1::2] = kp_xy_flat[kp_off[mj] + k2]
+    # last-writer-wins ray init from the src observation in frame i with the INITIAL pose
+    # landmark ids are exactly 0..m-1, so unique() of the reversed array lists them in order
+    src = len(lm) - 1 - np.unique(lm[::-1], return_index=True)[1]
+    ip = scene.init_ptz[mi[src]]
+    pts = kp_xy_flat[kp_off[mi[src]] + k1[src]]
+    th, ph = image_to_ray(scene.u, scene.v, ip[:, 2], ip[:, 0], ip[:, 1], pts[:, 0], pts[:, 1])
+    init_rays = np.stack([th, ph], 1)
+    gt_rays = scene.gt_rays[uniq[order]]
+    return Problem(n_pose=n, n_landmark=m, frame=frame, landmark=landmark, xy=xy,
+                   init_ptz=scene.init_ptz.copy(), init_rays=init_rays, gt_ptz=scene.gt_ptz.copy(),
+                   gt_rays=gt_rays, u=scene.u, v=scene.v, n_pairs=len(pairs),
+                   meta=dict(match_i=mi, match_j=mj, kp1=k1, kp2=k2))
+
+
+def make_problem(config="config3", seed=0):
+    """Synthetic BA problem for one of the BASELINE configs."""
+    n_kf, n_rays, lo, hi, rows = CONFIGS[config]
+    scene = make_scene(n_kf, n_rays, lo, hi, seed=seed, tilt_rows=rows)
+    pairs = scene_pairs(scene, seed=seed)
+    prob = problem_from_pairs(scene, pairs)
+    prob.meta["config"] = config
+    prob.meta["seed"] = seed
+    return prob
+
+
+def make_small_problem(n_kf, n_rays, lo, hi, seed=0, noise=0.5, init_sigma=(0.5, 0.2, 40.0)):
+    scene = make_scene(n_kf, n_rays, lo, hi, seed=seed, noise=noise, init_sigma=init_sigma)
+    return problem_from_pairs(scene, scene_pairs(scene, seed=seed))
+
+
+def dedup_records(frame, landmark, xy):
+    """Merge identical (frame, landmark, x, y) pair-form records into one weighted record.
+    The weighted cost sum_k w_k rho(r_k^2) equals the pair-form cost exactly."""
+    key = np.empty(len(frame), dtype=[("l", np.int64), ("f", np.int64), ("x", np.float64), ("y", np.float64)])
+    key["l"] = landmark
+    key["f"] = frame
+    key["x"] = xy[:, 0]
+    key["y"] = xy[:, 1]
+    uniq, inv, cnt = np.unique(key, return_inverse=True, return_counts=True)
+    return (uniq["f"].astype(np.int32), uniq["l"].astype(np.int32),
+            np.stack([uniq["x"], uniq["y"]], 1), cnt.astype(np.float64), inv)
+
+
+def pose_rmse(a, b):
+    """Per-component RMSE over keyframes 1..N-1."""
+    d = np.asarray(a)[1:] - np.asarray(b)[1:]
+    return np.sqrt(np.mean(d * d, axis=0))
+
+
+def _selftest():
+    p = make_problem("config1", seed=0)
+    print(p.n_pose, p.n_landmark, p.n_pairs, p.n_match, len(p.frame))
+
+
+if __name__ == "__main__":
+    _selftest()

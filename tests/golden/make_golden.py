@@ -1,0 +1,395 @@
+"""
+Generate golden fixtures by RUNNING THE REFERENCE (build container only; /root/reference does not
+exist on the GPU box).  Recipe = SURVEY §8c: the reference's Python hot path is imported in place
+with stub modules for its three import-time blockers (cv2, pyflann, the ctypes RF module), and its
+OpenCV front-end (`detect_compute_sift`, `match_sift_features`) is monkeypatched with synthetic
+ground-truth correspondences.  Everything downstream runs unmodified: matching-graph bookkeeping
+incl. the random.shuffle cap, landmark ids, x0 init, scipy trf, keyframe assembly, EKF update.
+
+Nothing from /root/reference is copied: only numeric inputs/outputs are written (tests/golden/*.npz).
+Bytecode writing is disabled so no reference .pyc lands anywhere.
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--quick]
+"""
+import argparse
+import os
+import random
+import sys
+import time
+import types
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference/slam_system"
+
+import numpy as np  # noqa: E402
+
+
+def install_stubs():
+    cv2 = types.ModuleType("cv2")
+    cv2.imwrite = lambda *a, **k: True
+    cv2.line = lambda *a, **k: None
+    sys.modules["cv2"] = cv2
+    sys.modules["pyflann"] = types.ModuleType("pyflann")
+    for name in ["rf_map", "rf_map.python_package", "rf_map.python_package.backup"]:
+        m = types.ModuleType(name)
+        m.__path__ = []
+        sys.modules[name] = m
+    rf = types.ModuleType("rf_map.python_package.backup.rf_map")
+    rf.RFMap = object
+    sys.modules["rf_map.python_package.backup.rf_map"] = rf
+    sys.path.insert(0, REF)
+
+
+install_stubs()
+sys.path.insert(0, os.path.join(REPO, "pan-tilt-zoom-slam_amd"))
+import synthetic  # noqa: E402  (the build's own generator: product module, numpy only)
+import bundle_adjustment as ref_ba  # noqa: E402  (REFERENCE module, via sys.path above)
+import image_process as ref_ip  # noqa: E402
+import transformation as ref_tf  # noqa: E402
+import ptz_camera as ref_cam  # noqa: E402
+import ptz_slam as ref_slam  # noqa: E402
+from scipy.optimize import least_squares  # noqa: E402
+
+assert ref_ba.__file__.startswith(REF), ref_ba.__file__
+assert synthetic.__file__.startswith(REPO)
+
+
+def out(name, **arrays):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **arrays)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+# --------------------------------------------------------------------------------------------
+# 1. projection KATs
+# --------------------------------------------------------------------------------------------
+def gen_projection(rng):
+    n = 2000
+    u, v = 640.0, 360.0
+    f = rng.uniform(1900, 4300, n)
+    cp = rng.uniform(40, 80, n)
+    ct = rng.uniform(-15, 0, n)
+    th = cp + rng.uniform(-20, 20, n)
+    ph = ct + rng.uniform(-10, 10, n)
+    # behind-camera subset (q2 < 0): ray > 90 deg away from the optical axis in pan
+    nb = 400
+    fb = rng.uniform(1900, 4300, nb)
+    cpb = rng.uniform(50, 80, nb)
+    ctb = rng.uniform(-15, 0, nb)
+    thb = rng.uniform(-85, -30, nb)
+    phb = rng.uniform(-25, 5, nb)
+    F = np.concatenate([f, fb]); CP = np.concatenate([cp, cpb]); CT = np.concatenate([ct, ctb])
+    TH = np.concatenate([th, thb]); PH = np.concatenate([ph, phb])
+    xy = np.array([ref_tf.TransFunction.from_ray_to_image(u, v, a, b, c, d, e)
+                   for a, b, c, d, e in zip(F, CP, CT, TH, PH)])
+    # back-projection of random image points
+    px = rng.uniform(0, 1280, n)
+    py = rng.uniform(0, 720, n)
+    ray = np.array([ref_tf.TransFunction.from_image_to_ray(u, v, a, b, c, d, e)
+                    for a, b, c, d, e in zip(f, cp, ct, px, py)])
+    # PTZCamera matrix form (signed q2), zero and non-zero displacement
+    nc = 300
+    disp = np.array([0.01, -0.02, 0.03, 1e-5, -2e-5, 3e-5])
+    cam_rows = []
+    for k in range(nc):
+        d = None if k % 2 == 0 else disp
+        cam = ref_cam.PTZCamera((u, v), np.zeros(3), np.eye(3), d)
+        cam.set_ptz([cp[k], ct[k], f[k]])
+        pr = cam.project_ray([th[k], ph[k]])
+        bp = cam.back_project_to_ray(px[k], py[k])
+        cam_rows.append([k % 2, cp[k], ct[k], f[k], th[k], ph[k], pr[0], pr[1], px[k], py[k], bp[0], bp[1]])
+    out("kat_projection.npz", u=u, v=v, f=F, cam_pan=CP, cam_tilt=CT, theta=TH, phi=PH, xy=xy,
+        n_front=n, bp_f=f, bp_pan=cp, bp_tilt=ct, bp_x=px, bp_y=py, bp_ray=ray,
+        cam_rows=np.array(cam_rows), displacement=disp)
+
+
+# --------------------------------------------------------------------------------------------
+# synthetic detect/match monkeypatch for the reference front-end
+# --------------------------------------------------------------------------------------------
+class KP:
+    __slots__ = ("pt",)
+
+    def __init__(self, x, y):
+        self.pt = (float(x), float(y))
+
+
+class FrontEnd:
+    """Stands in for cv2 SIFT + BF matching: 'images' are frame ids; matches are ground truth,
+    optionally with injected inconsistent matches."""
+
+    def __init__(self, scene, corrupt=0, seed=0):
+        self.scene = scene
+        self.corrupt = corrupt
+        self.rng = np.random.default_rng(seed)
+        self.raw = {}  # (i, j) -> (index1, index2) returned to the reference
+        self.kps = {}  # frame -> keypoint objects handed out (to recover local indices)
+
+    def detect(self, im, nfeatures, verbose=False):
+        i = int(im)
+        kps = [KP(x, y) for x, y in self.scene.kp_xy[i]]
+        des = np.full((len(kps), 128), i, dtype=np.float32)
+        des[:, 1] = np.arange(len(kps))
+        self.kps[i] = kps
+        return kps, des
+
+    def match(self, kp1, des1, kp2, des2, pts_array=False, verbose=False):
+        i = int(des1[0, 0]); j = int(des2[0, 0])
+        r1 = self.scene.kp_ray[i]; r2 = self.scene.kp_ray[j]
+        pos2 = {int(r): k for k, r in enumerate(r2)}
+        idx1, idx2 = [], []
+        for a, r in enumerate(r1):
+            b = pos2.get(int(r))
+            if b is not None:
+                idx1.append(a); idx2.append(b)
+        if self.corrupt and len(idx2) > 4:
+            for _ in range(self.corrupt):
+                p, q = self.rng.choice(len(idx2), 2, replace=False)
+                idx2[p], idx2[q] = idx2[q], idx2[p]
+        self.raw[(i, j)] = (list(idx1), list(idx2))
+        pts1 = np.array([kp1[a].pt for a in idx1]).reshape(-1, 2)
+        pts2 = np.array([kp2[b].pt for b in idx2]).reshape(-1, 2)
+        return pts1, idx1, pts2, idx2
+
+
+def pack_points(scene):
+    off = np.concatenate([[0], np.cumsum([len(p) for p in scene.kp_xy])]).astype(np.int64)
+    return np.concatenate(scene.kp_xy), off
+
+
+def pack_raw(raw):
+    keys = sorted(raw)
+    pi = np.array([k[0] for k in keys], np.int64)
+    pj = np.array([k[1] for k in keys], np.int64)
+    cnt = np.array([len(raw[k][0]) for k in keys], np.int64)
+    a = np.concatenate([np.asarray(raw[k][0], np.int64) for k in keys]) if keys else np.zeros(0, np.int64)
+    b = np.concatenate([np.asarray(raw[k][1], np.int64) for k in keys]) if keys else np.zeros(0, np.int64)
+    return pi, pj, cnt, a, b
+
+
+def pack_lists(src, dst, lmk):
+    n = len(src)
+    mi, mj, k1, k2, lm = [], [], [], [], []
+    for i in range(n):
+        for j in range(n):
+            for a, b, l in zip(src[i][j], dst[i][j], lmk[i][j]):
+                mi.append(i); mj.append(j); k1.append(a); k2.append(b); lm.append(l)
+    return [np.array(x, np.int64) for x in (mi, mj, k1, k2, lm)]
+
+
+# --------------------------------------------------------------------------------------------
+# 2-4. bundle_adjustment() end-to-end + residual vectors + tight optimum
+# --------------------------------------------------------------------------------------------
+def gen_ba(name, n_kf, n_rays, lo, hi, seed, tight=True):
+    scene = synthetic.make_scene(n_kf, n_rays, lo, hi, seed=seed)
+    fe = FrontEnd(scene)
+    ref_ip.detect_compute_sift = fe.detect
+    ref_ip.match_sift_features = fe.match
+    ref_ba.draw_matches = lambda *a, **k: None
+    captured = {}
+    real_ls = ref_ba.least_squares
+
+    def ls_capture(fun, x0, **kw):
+        captured["x0"] = np.array(x0, copy=True)
+        captured["args"] = kw["args"]
+        t0 = time.time()
+        res = real_ls(fun, x0, **kw)
+        captured["time"] = time.time() - t0
+        captured["res"] = res
+        return res
+
+    ref_ba.least_squares = ls_capture
+    random.seed(seed)
+    images = list(range(n_kf))
+    center = np.array([0.0, -10.0, 5.0])
+    rotation = np.eye(3)
+    t0 = time.time()
+    landmarks, keyframes = ref_ba.bundle_adjustment(images, list(range(100, 100 + n_kf)), "sift",
+                                                    scene.init_ptz.copy(), center, rotation,
+                                                    scene.u, scene.v, "/tmp", verbose=False)
+    wall = time.time() - t0
+    ref_ba.least_squares = real_ls
+    res = captured["res"]
+    (n_pose, n_landmark, n_residual, points, src, dst, lmk, u, v, ref_pose) = captured["args"]
+    mi, mj, k1, k2, lm = pack_lists(src, dst, lmk)
+    pts, off = pack_points(scene)
+    pi, pj, cnt, ra, rb = pack_raw(fe.raw)
+    # residual vectors at x0, x*, 3 perturbations
+    rng = np.random.default_rng(seed + 1)
+    xs = [captured["x0"], res.x]
+    for _ in range(3):
+        xs.append(res.x + rng.normal(0, 1, res.x.shape) * np.concatenate(
+            [np.tile([0.05, 0.05, 5.0], n_pose - 1), np.full(2 * n_landmark, 0.05)]))
+    rs = [ref_ba._compute_residual(x, *captured["args"]) for x in xs]
+    kf_local = []
+    for i, kf in enumerate(keyframes):
+        pos = {id(o): k for k, o in enumerate(fe.kps[i])}
+        kf_local.append(np.array([pos[id(o)] for o in kf.feature_pts], np.int64))
+    kf_lmk = [np.asarray(kf.landmark_index, np.int64) for kf in keyframes]
+    kf_pts = [np.array([p.pt for p in kf.feature_pts]).reshape(-1, 2) for kf in keyframes]
+    kf_off = np.concatenate([[0], np.cumsum([len(a) for a in kf_lmk])]).astype(np.int64)
+    data = dict(
+        n_kf=n_kf, n_rays=n_rays, lo=lo, hi=hi, seed=seed, u=u, v=v,
+        init_ptz=scene.init_ptz, gt_ptz=scene.gt_ptz, points=pts, points_off=off,
+        raw_pi=pi, raw_pj=pj, raw_cnt=cnt, raw_a=ra, raw_b=rb,
+        n_pose=n_pose, n_landmark=n_landmark, n_residual=n_residual,
+        m_i=mi, m_j=mj, m_k1=k1, m_k2=k2, m_lm=lm, ref_pose=np.asarray(ref_pose, np.float64),
+        x0=captured["x0"], x_ls=res.x, ls_cost=res.cost, ls_njev=res.njev, ls_nfev=res.nfev,
+        ls_status=res.status, ls_time=captured["time"], ba_wall=wall,
+        landmarks=landmarks, kf_ptz=np.array([[k.pan, k.tilt, k.f] for k in keyframes]),
+        kf_lmk=np.concatenate(kf_lmk) if kf_lmk else np.zeros(0), kf_off=kf_off,
+        kf_pts=np.concatenate(kf_pts) if kf_pts else np.zeros((0, 2)),
+        kf_local=np.concatenate(kf_local) if kf_local else np.zeros(0, np.int64),
+        xs=np.stack(xs), rs=np.stack(rs))
+    print(f"{name}: N={n_pose} M={n_landmark} residuals={n_residual} njev={res.njev} "
+          f"ls {captured['time']:.2f}s ({res.njev / captured['time']:.4f} it/s) status={res.status}")
+    if tight:
+        t0 = time.time()
+        rt = least_squares(ref_ba._compute_residual, captured["x0"], x_scale="jac", ftol=1e-15,
+                           xtol=1e-15, gtol=1e-15, method="trf", args=captured["args"])
+        data.update(x_tight=rt.x, tight_cost=rt.cost, tight_njev=rt.njev, tight_status=rt.status,
+                    tight_time=time.time() - t0)
+        print(f"  tight: cost {rt.cost:.6f} njev {rt.njev} status {rt.status} {time.time() - t0:.1f}s")
+    out(f"{name}.npz", **data)
+
+
+# --------------------------------------------------------------------------------------------
+# 6. matching-graph bookkeeping with caps (>200) and inconsistent matches
+# --------------------------------------------------------------------------------------------
+def gen_graph(seed):
+    scene = synthetic.make_scene(6, 900, 50, 60, seed=seed)
+    fe = FrontEnd(scene, corrupt=6, seed=seed)
+    ref_ip.detect_compute_sift = fe.detect
+    ref_ip.match_sift_features = fe.match
+    n = 6
+    mask = [[0] * n for _ in range(n)]
+    ip = scene.init_ptz
+    for i in range(n):
+        for j in range(n):
+            if synthetic.overlap_pan_angle(ip[i, 2], ip[i, 0], ip[j, 2], ip[j, 0], 1280) > 5:
+                mask[i][j] = 1
+    random.seed(seed)
+    kps, des, points, src, dst, lmk, n_landmark = ref_ip.build_matching_graph(list(range(n)), mask, "sift")
+    mi, mj, k1, k2, lm = pack_lists(src, dst, lmk)
+    pi, pj, cnt, ra, rb = pack_raw(fe.raw)
+    pts, off = pack_points(scene)
+    print(f"graph: landmarks={n_landmark} matches={len(mi)} raw={int(cnt.sum())} max_raw={int(cnt.max())}")
+    out("matching_graph.npz", seed=seed, mask=np.array(mask), raw_pi=pi, raw_pj=pj, raw_cnt=cnt, raw_a=ra,
+        raw_b=rb, n_landmark=n_landmark, m_i=mi, m_j=mj, m_k1=k1, m_k2=k2, m_lm=lm, points=pts, points_off=off)
+
+
+# --------------------------------------------------------------------------------------------
+# 7. EKF update (ptz_slam.py:210-289) and compute_h_jacobian (:73-138)
+# --------------------------------------------------------------------------------------------
+def gen_ekf(R, seed):
+    rng = np.random.default_rng(seed)
+    u, v = 640.0, 360.0
+    pan, tilt, f = 58.0, -8.0, 3000.0
+    cam = ref_cam.PTZCamera((u, v), np.array([0.0, -10.0, 5.0]), np.eye(3))
+    cam.set_ptz([pan, tilt, f])
+    pts = np.stack([rng.uniform(20, 1260, R), rng.uniform(20, 700, R)], 1)
+    rays = cam.back_project_to_rays(pts)
+    rays = rays + rng.normal(0, 0.02, rays.shape)
+    slam = ref_slam.PtzSlam()
+    slam.cameras = [cam]
+    slam.rays = rays.copy()
+    cov = slam.angle_var * np.eye(3 + 2 * R)
+    cov[2, 2] = slam.f_var
+    B = rng.normal(0, 3e-3, (3 + 2 * R, 4))  # low-rank correlation so cov0 = base + B B^T is storable
+    cov = cov + B @ B.T
+    slam.state_cov = cov.copy()
+    import copy
+    pred = copy.deepcopy(cam)
+    pred.set_ptz([pan + 0.05, tilt - 0.03, f + 5.0])
+    slam.current_camera = pred
+    # observations: true projections + noise, a sorted subset of rays (some dropped)
+    keep = np.sort(rng.choice(R, int(R * 0.8), replace=False))
+    true_cam = copy.deepcopy(cam)
+    true_cam.set_ptz([pan + 0.08, tilt - 0.05, f + 8.0])
+    obs = np.array([true_cam.project_ray(rays[k]) for k in keep]) + rng.normal(0, 0.3, (len(keep), 2))
+    before = dict(pan=pred.pan, tilt=pred.tilt, f=pred.focal_length, rays=slam.rays.copy(), cov=slam.state_cov.copy())
+    H = slam.compute_h_jacobian(pred.pan, pred.tilt, pred.focal_length, rays[keep[:20]])
+    t0 = time.time()
+    slam.ekf_update(obs, keep, 720, 1280)
+    dt = time.time() - t0
+    print(f"ekf R={R}: {dt:.3f}s")
+    cov1 = slam.state_cov
+    changed = np.argwhere(cov1 != before["cov"])
+    pick = changed[np.random.default_rng(seed + 9).choice(len(changed), min(3000, len(changed)), replace=False)]
+    out(f"ekf_R{R}.npz", u=u, v=v, pan0=before["pan"], tilt0=before["tilt"], f0=before["f"],
+        rays0=before["rays"], cov_base_diag=np.diag(slam.angle_var * np.eye(3 + 2 * R)).copy(), f_var=slam.f_var,
+        cov_B=B, obs=obs, obs_idx=keep, height=720, width=1280,
+        pan1=slam.current_camera.pan, tilt1=slam.current_camera.tilt, f1=slam.current_camera.focal_length,
+        velocity=slam.velocity, rays1=slam.rays, cov1_pose=cov1[:3, :3], cov1_diag=np.diag(cov1).copy(),
+        cov1_sum=float(cov1.sum()), cov1_sumsq=float((cov1 * cov1).sum()), n_changed=len(changed),
+        cov1_pick=pick, cov1_pick_val=cov1[pick[:, 0], pick[:, 1]], H=H, H_rays=rays[keep[:20]], time=dt)
+
+
+# --------------------------------------------------------------------------------------------
+# 5. config-2-scale optimum (oracle residual pinned by 2/4 above) + reference residual samples
+# --------------------------------------------------------------------------------------------
+def gen_config2():
+    sys.path.insert(0, REPO)
+    from oracle import ptz_oracle as orc
+    p = synthetic.make_problem("config2", seed=0)
+    n, m = p.n_pose, p.n_landmark
+    x0_full = np.concatenate([p.init_ptz.reshape(-1), p.init_rays.reshape(-1)])
+    # reference residual at x0 on a 1000-sample subset, via the reference's own loop
+    mi, mj, k1, k2 = (p.meta[k] for k in ("match_i", "match_j", "kp1", "kp2"))
+    lm = p.landmark[0::2].astype(np.int64)
+    # keypoints: per-frame arrays of the same scene (kp1/kp2 index into them)
+    scene = synthetic.make_scene(*synthetic.CONFIGS["config2"][:4], seed=0)
+    pts = scene.kp_xy
+    src = [[[] for _ in range(n)] for _ in range(n)]
+    dst = [[[] for _ in range(n)] for _ in range(n)]
+    lmk = [[[] for _ in range(n)] for _ in range(n)]
+    for a, b, c, d, l in zip(mi, mj, k1, k2, lm):
+        src[a][b].append(int(c)); dst[a][b].append(int(d)); lmk[a][b].append(int(l))
+    args = (n, m, 4 * len(mi), pts, src, dst, lmk, p.u, p.v, p.init_ptz[0])
+    t0 = time.time()
+    r_ref = ref_ba._compute_residual(x0_full[3:], *args)
+    t_ref = time.time() - t0
+    rng = np.random.default_rng(5)
+    sample = np.sort(rng.choice(len(r_ref), 1000, replace=False))
+    t0 = time.time()
+    res = orc.solve_scipy(x0_full[3:], n, m, p.u, p.v, p.init_ptz[0], p.frame.astype(np.int64),
+                          p.landmark.astype(np.int64), p.xy, ftol=1e-15, xtol=1e-15, gtol=1e-15, analytic=True)
+    print(f"config2 tight: cost {res.cost:.6f} njev {res.njev} status {res.status} {time.time() - t0:.1f}s; "
+          f"ref residual eval {t_ref:.2f}s")
+    res_h = orc.solve_scipy(x0_full[3:], n, m, p.u, p.v, p.init_ptz[0], p.frame.astype(np.int64),
+                            p.landmark.astype(np.int64), p.xy, ftol=1e-15, xtol=1e-15, gtol=1e-15,
+                            analytic=True, loss="huber", f_scale=1.0)
+    print(f"config2 tight huber: cost {res_h.cost:.6f} njev {res_h.njev} status {res_h.status}")
+    out("config2_optimum.npz", n_pose=n, n_landmark=m, n_records=len(p.frame),
+        frame_sum=int(p.frame.sum()), landmark_sum=int(p.landmark.astype(np.int64).sum()),
+        xy_sum=float(p.xy.sum()), x0=x0_full, r_ref_sample_idx=sample, r_ref_sample=r_ref[sample],
+        r_ref_sumsq=float(np.sum(r_ref * r_ref)), x_tight=res.x, tight_cost=res.cost,
+        x_tight_huber=res_h.x, tight_cost_huber=res_h.cost, ref_residual_time=t_ref)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    rng = np.random.default_rng(1)
+    todo = a.only.split(",") if a.only else ["proj", "ba", "graph", "ekf", "config2"]
+    if "proj" in todo:
+        gen_projection(rng)
+    if "ba" in todo:
+        gen_ba("ba_4x60", 4, 60, 55, 61, seed=1)
+        gen_ba("ba_6x120", 6, 120, 52, 62, seed=2)
+        if not a.quick:
+            gen_ba("ba_10x200", 10, 200, 50, 68, seed=1)
+    if "graph" in todo:
+        gen_graph(seed=3)
+    if "ekf" in todo:
+        gen_ekf(50, seed=4)
+        gen_ekf(300, seed=5)
+    if "config2" in todo:
+        gen_config2()
+
+
+if __name__ == "__main__":
+    main()
