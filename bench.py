@@ -1,0 +1,264 @@
+#!/usr/bin/env python3
+"""
+Headline benchmark (BASELINE.json): BA iterations/sec at 500 keyframes x 20k ray landmarks
+(config 3: fp32 LM + Huber on MI355X), plus pan/tilt/focal RMSE.
+
+One bench "step" = one Levenberg-Marquardt iteration = one linearisation (residual + Jacobian +
+normal-equation blocks over all pair-form records) + reduced-camera-system build + dense Cholesky
+solve + back-substitution + trial evaluation, rejected trial steps counted inside the iteration
+(scipy `njev` semantics).  The solver runs the reference's termination rule
+(ftol=1e-4, bundle_adjustment.py:200); when a solve converges the state is reset to x0 and solving
+continues until exactly K iterations were timed.  Inputs are resident in HBM before timing.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config config3] [--form pair|dedup]
+
+N > 1 (torchrun, one process per GPU): the records are sharded by landmark block across ranks
+(poses replicated); the reduced camera system and the partial scalars are summed with an RCCL
+all-reduce over xGMI each iteration (`scaling: strong`, same problem at every N).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "pan-tilt-zoom-slam_amd")
+sys.path.insert(0, PKG)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="config3")
+    ap.add_argument("--form", default="pair", choices=["pair", "dedup"])
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"])
+    ap.add_argument("--loss", default="huber", choices=["huber", "linear"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-accuracy", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "k1_traffic.json"))
+    ap.add_argument("--cpu-sample-kf", type=int, default=40)
+    return ap.parse_args()
+
+
+class _DevArray:
+    """__cuda_array_interface__ view of a device pointer owned by libptzba (for torch all-reduce)."""
+
+    def __init__(self, ptr, n):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<f8", "data": (ptr, False), "version": 3,
+                                         "strides": None}
+
+
+def shard_by_landmark(landmark, n_landmark, rank, world):
+    """Contiguous landmark blocks with ~equal record counts; returns record mask of this rank."""
+    cnt = np.bincount(landmark, minlength=n_landmark).astype(np.int64)
+    cum = np.cumsum(cnt)
+    tot = cum[-1]
+    bounds = [0] + [int(np.searchsorted(cum, tot * k / world)) for k in range(1, world)] + [n_landmark]
+    lo, hi = bounds[rank], bounds[rank + 1]
+    return (landmark >= lo) & (landmark < hi)
+
+
+def algorithmic_bytes_k1(info, precision, weighted):
+    """Minimum bytes one K1 launch moves with this data layout:
+    per record: obs x,y (2 reals) + segment id (int32) [+ weight]; per segment: frame id read twice,
+    record offset (int64), 16-real output block; per active landmark: order + CSR (8 B), ray table
+    (8 reals), 8-double output; frame table (8 reals per frame)."""
+    s = 4 if precision == "fp32" else 8
+    rec = 2 * s + 4 + (s if weighted else 0)
+    seg = 4 + 4 + 8 + 16 * s
+    lm = 8 + 8 * s + 64
+    return info["n_obs"] * rec + info["n_segments"] * seg + info["n_active_landmarks"] * lm + info["n_pose"] * 8 * s
+
+
+def survey_bytes_k1(info, precision):
+    """SURVEY §8d formula B = N_rec*S_rec + (3 N_kf + 2 N_lm) s + N_lm 5 s + N_kf 9 s (S_rec = 16/24)."""
+    s = 4 if precision == "fp32" else 8
+    srec = 16 if precision == "fp32" else 24
+    return info["n_obs"] * srec + (3 * info["n_pose"] + 2 * info["n_landmark"]) * s + info["n_landmark"] * 5 * s + \
+        info["n_pose"] * 9 * s
+
+
+def cpu_baseline(prob, n_kf_sample):
+    """Faithful CPU restatement (oracle): vectorised reference residual + scipy trf (x_scale='jac',
+    ftol=1e-4, FD Jacobian with jac_sparsity), 1 thread, on a keyframe-window sample of the headline
+    problem; it/s scaled to the full problem by the record ratio."""
+    from threadpoolctl import threadpool_limits
+    sys.path.insert(0, ROOT)
+    from oracle import ptz_oracle as orc
+    keep = (prob.frame < n_kf_sample)
+    # matches whose both records are inside the window
+    m_keep = keep[0::2] & keep[1::2]
+    rec_keep = np.repeat(m_keep, 2)
+    frame = prob.frame[rec_keep].astype(np.int64)
+    lm_old = prob.landmark[rec_keep].astype(np.int64)
+    uniq, lm = np.unique(lm_old, return_inverse=True)
+    xy = prob.xy[rec_keep]
+    n, m = n_kf_sample, len(uniq)
+    x0 = np.concatenate([prob.init_ptz[1:n].reshape(-1), prob.init_rays[uniq].reshape(-1)])
+    with threadpool_limits(limits=1):
+        t0 = time.perf_counter()
+        res = orc.solve_scipy(x0, n, m, prob.u, prob.v, prob.init_ptz[0], frame, lm, xy, ftol=1e-4)
+        dt = time.perf_counter() - t0
+    its = res.njev / dt
+    ratio = len(frame) / len(prob.frame)
+    return dict(value=its * ratio, unit="BA it/s", cores=1, kind="port",
+                sample=f"scipy trf (x_scale='jac', ftol=1e-4, FD jac_sparsity) on the first {n_kf_sample} keyframes "
+                       f"of {prob.meta.get('config')} ({len(frame)} of {len(prob.frame)} pair records, {m} landmarks): "
+                       f"{res.njev} iterations in {dt:.2f} s = {its:.4f} it/s, scaled by the record ratio {ratio:.4f}",
+                sample_its=its, sample_time_s=dt)
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    import ptzba
+    import synthetic
+
+    prob = synthetic.make_problem(a.config, seed=0)
+    frame, landmark, xy, w = prob.frame, prob.landmark, prob.xy, None
+    if a.form == "dedup":
+        frame, landmark, xy, w, _ = synthetic.dedup_records(frame, landmark, xy)
+    if world > 1:
+        sel = shard_by_landmark(landmark, prob.n_landmark, rank, world)
+        frame, landmark, xy = frame[sel], landmark[sel], xy[sel]
+        w = None if w is None else w[sel]
+    precision = ptzba.FP32 if a.precision == "fp32" else ptzba.FP64
+    loss = ptzba.LOSS_HUBER if a.loss == "huber" else ptzba.LOSS_LINEAR
+    h = ptzba.BAHandle(local if world > 1 else 0)
+    stream = torch.cuda.current_stream()
+    h.set_stream(stream.cuda_stream)
+    h.set_problem(prob.n_pose, prob.n_landmark, frame, landmark, xy, prob.u, prob.v, weight=w, precision=precision,
+                  loss=loss, f_scale=1.0)
+    info = h.info()
+
+    allreduce = None
+    if world > 1:
+        sys_ptr, sys_n, scal_ptr = h.exchange()
+        t_sys = torch.as_tensor(_DevArray(sys_ptr, sys_n), device=f"cuda:{local}")
+        t_scal = torch.as_tensor(_DevArray(scal_ptr, ptzba.NSCALARS), device=f"cuda:{local}")
+
+        def allreduce(kind):
+            dist.all_reduce(t_sys if kind == "sys" else t_scal)
+
+    def run_iters(k, timed=False):
+        done = 0
+        solves = 0
+        while done < k:
+            h.set_state(prob.init_ptz, prob.init_rays)
+            res = ptzba.LMSolver(h, ftol=1e-4, xtol=1e-8, max_iter=k - done, allreduce=allreduce).run()
+            done += max(res.njev, 1)
+            solves += 1
+            if res.njev == 0:
+                break
+        return done, solves
+
+    # warmup
+    run_iters(max(a.warmup, 1))
+    h.reset_kernel_times(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    iters, solves = run_iters(a.steps, timed=True)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    kt = h.kernel_times()
+    k1_ms, k1_n = kt["linearize"]
+
+    # accuracy: full fp32 LM solve vs a full fp64 solve of the same records, and vs ground truth
+    accuracy = None
+    if not a.no_accuracy and world == 1:
+        h.set_state(prob.init_ptz, prob.init_rays)
+        r32 = ptzba.LMSolver(h, ftol=1e-10, xtol=1e-12, max_iter=50).run()
+        ptz32, _ = h.get_state()
+        h64 = ptzba.BAHandle(0)
+        h64.set_problem(prob.n_pose, prob.n_landmark, frame, landmark, xy, prob.u, prob.v, weight=w,
+                        precision=ptzba.FP64, loss=loss, f_scale=1.0)
+        h64.set_state(prob.init_ptz, prob.init_rays)
+        r64 = ptzba.LMSolver(h64, ftol=1e-12, xtol=1e-12, max_iter=50).run()
+        ptz64, _ = h64.get_state()
+        h64.close()
+        accuracy = dict(rmse_fp32_vs_fp64=[float(x) for x in synthetic.pose_rmse(ptz32, ptz64)],
+                        rmse_fp64_vs_ground_truth=[float(x) for x in synthetic.pose_rmse(ptz64, prob.gt_ptz)],
+                        cost_fp32=r32.cost, cost_fp64=r64.cost, iters_fp32=r32.njev, iters_fp64=r64.njev,
+                        components=["pan_deg", "tilt_deg", "f_px"])
+
+    traffic = None
+    if os.path.exists(a.traffic_json):
+        try:
+            tj = json.load(open(a.traffic_json))
+            key = f"{a.config}/{a.form}/{a.precision}/{a.loss}"
+            if key in tj:
+                traffic = tj[key]["hbm_bytes_per_launch"]
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        alg = algorithmic_bytes_k1(info, a.precision, w is not None)
+        achieved = alg / (k1_ms * 1e-3) / 1e9 if k1_ms > 0 else 0.0
+        out = {
+            "metric": "BA iterations/sec at 500 KF x 20k rays; pan-tilt-focal RMSE vs reference",
+            "value": iters / elapsed,
+            "unit": "BA it/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": 1e3 * elapsed / iters,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32" if a.precision == "fp32" else "f64",
+            "data": "synthetic (SURVEY §8d generator, seed 0)",
+            "config": {"workload": f"{a.config}: {prob.n_pose} KF x {prob.n_landmark} ray landmarks, "
+                                   f"{info['n_obs']} {a.form}-form records/rank, {a.loss} loss, {a.precision} LM",
+                       "n_keyframes": prob.n_pose, "n_landmarks": prob.n_landmark, "n_records": int(len(prob.frame)),
+                       "n_matches": int(prob.n_match), "n_pairs": prob.n_pairs, "form": a.form,
+                       "parallelism": f"landmark-sharded x{world}" if world > 1 else "single GPU",
+                       "iterations_timed": iters, "solves_timed": solves},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_linearize (K1)",
+                         "k1_avg_ms": k1_ms, "k1_launches": k1_n, "algorithmic_bytes_per_launch": alg,
+                         "survey_formula_bytes_per_launch": survey_bytes_k1(info, a.precision)},
+            "kernel_ms": {k: v[0] for k, v in kt.items()},
+        }
+        if accuracy:
+            out["accuracy"] = accuracy
+        if not a.no_cpu_baseline and world == 1:
+            try:
+                cb = cpu_baseline(prob, a.cpu_sample_kf)
+                out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+                out["vs_cpu_baseline"] = out["value"] / cb["value"] if cb["value"] > 0 else None
+            except Exception as e:  # report, never hide
+                out["cpu_baseline"] = {"value": None, "error": repr(e)}
+        print(json.dumps(out))
+    h.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

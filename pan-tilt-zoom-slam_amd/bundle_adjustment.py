@@ -1,0 +1,174 @@
+"""
+Bundle adjustment — drop-in replacement for slam_system/bundle_adjustment.py.
+
+    bundle_adjustment(images, image_indices, feature_method, initial_ptzs, center, rotation, u, v,
+                      save_path, verbose=False)  ->  (landmarks float64 [M, 2], list[KeyFrame])
+
+Same signature, steps and outputs as the reference (bundle_adjustment.py:109-251):
+  1. pair mask: overlap_pan_angle(f_i, pan_i, f_j, pan_j, 1280) > 5 deg          (:135-144)
+  2. matching graph (image_process.build_matching_graph: front-end hooks + bit-exact bookkeeping)
+  3. n_residual = sum 4 |matches|; x0 = [poses | rays], each ray from from_image_to_ray of its
+     src observation in frame i with the LAST match in loop order winning          (:167-197)
+  4. optimisation — the reference's scipy `least_squares(_compute_residual, x0, x_scale='jac',
+     ftol=1e-4, method='trf')` (:200-202) is replaced by the GPU Levenberg-Marquardt of libptzba
+     (exact Schur-complement steps, same ftol termination rule), frame 0 fixed     (:197)
+  5. KeyFrame assembly with the reference's set() de-duplication order            (:214-248)
+
+Extra keyword arguments (all optional) select the numerics: precision ('fp64' default, 'fp32'),
+loss ('linear' as the reference, or 'huber'), f_scale, ftol/xtol/max_iter, device.
+`_compute_residual` keeps the reference signature and returns the identical residual vector
+(computed by libptzba, record order == the reference's loop order).
+"""
+import time
+
+import numpy as np
+
+import image_process
+import ptzba
+from key_frame import KeyFrame
+from util import overlap_pan_angle
+
+LAST_RESULT = {}
+
+
+def _records(n_pose, keypoints, src_pt_index, dst_pt_index, landmark_index):
+    """Pair-form records in the reference's residual order (bundle_adjustment.py:67-99):
+    for i, for j, for each match -> record (i, kp1) then (j, kp2)."""
+    fr, lm, xy = [], [], []
+    for i in range(n_pose):
+        for j in range(n_pose):
+            s = src_pt_index[i][j]
+            if len(s) == 0:
+                continue
+            a = np.asarray(s, np.int64)
+            b = np.asarray(dst_pt_index[i][j], np.int64)
+            l = np.asarray(landmark_index[i][j], np.int64)
+            m = len(a)
+            f = np.empty(2 * m, np.int32)
+            f[0::2] = i
+            f[1::2] = j
+            p = np.empty((2 * m, 2))
+            p[0::2] = np.asarray(keypoints[i], np.float64)[a]
+            p[1::2] = np.asarray(keypoints[j], np.float64)[b]
+            fr.append(f)
+            lm.append(np.repeat(l, 2).astype(np.int32))
+            xy.append(p)
+    if not fr:
+        return np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros((0, 2))
+    return np.concatenate(fr), np.concatenate(lm), np.concatenate(xy)
+
+
+def _compute_residual(x, n_pose, n_landmark, n_residual, keypoints, src_pt_index, dst_pt_index, landmark_index, u, v,
+                      reference_pose, verbose=False, precision=ptzba.FP64, device=0):
+    """bundle_adjustment.py:25-106 — same arguments, same residual vector (computed on the GPU)."""
+    assert x.shape[0] == (n_pose - 1) * 3 + n_landmark * 2
+    assert len(keypoints) == n_pose and len(src_pt_index) == n_pose
+    assert len(dst_pt_index) == n_pose and len(landmark_index) == n_pose
+    assert np.asarray(reference_pose).shape[0] == 3
+    frame, lm, xy = _records(n_pose, keypoints, src_pt_index, dst_pt_index, landmark_index)
+    assert 2 * len(frame) == n_residual
+    h = ptzba.BAHandle(device)
+    try:
+        h.set_problem(n_pose, n_landmark, frame, lm, xy, u, v, precision=precision)
+        r = h.residual(np.concatenate([np.asarray(reference_pose, np.float64), np.asarray(x, np.float64)]))
+    finally:
+        h.close()
+    if verbose:
+        e = np.sqrt(r[0::2] ** 2 + r[1::2] ** 2)
+        print("reprojection error is %f" % (e.sum() / (n_residual / 2)))
+    return r
+
+
+def bundle_adjustment(images, image_indices, feature_method, initial_ptzs, center, rotation, u, v, save_path,
+                      verbose=False, precision="fp64", loss="linear", f_scale=1.0, ftol=1e-4, xtol=1e-8,
+                      max_iter=100, device=0):
+    """bundle_adjustment.py:109-251 on the MI355X path.  Returns (landmarks [M,2], keyframes)."""
+    N = len(images)
+    assert N >= 1
+    assert len(image_indices) == N
+    initial_ptzs = np.asarray(initial_ptzs, np.float64)
+    assert initial_ptzs.shape[0] == N and initial_ptzs.shape[1] == 3
+    assert np.asarray(center).shape[0] == 3 and np.asarray(rotation).shape == (3, 3)
+    assert feature_method in ("sift", "orb", "latch")
+
+    # step 1: pair mask (bundle_adjustment.py:135-144)
+    image_match_mask = [[0 for _ in range(N)] for _ in range(N)]
+    for i in range(N):
+        for j in range(N):
+            if overlap_pan_angle(initial_ptzs[i][2], initial_ptzs[i][0], initial_ptzs[j][2], initial_ptzs[j][0],
+                                 1280) > 5:
+                image_match_mask[i][j] = 1
+    keypoints, descriptors, points, src_pt_index, dst_pt_index, landmark_index, n_landmark = \
+        image_process.build_matching_graph(images, image_match_mask, feature_method, verbose)
+    if image_process.draw_matches is not None and save_path:
+        for i in range(N):
+            for j in range(N):
+                if len(src_pt_index[i][j]):
+                    image_process.draw_matches(images[i], images[j], points[i].take(src_pt_index[i][j], axis=0),
+                                               points[j].take(dst_pt_index[i][j], axis=0),
+                                               save_path + "/" + str(i) + "_" + str(j) + ".jpg")
+
+    # step 2: data (bundle_adjustment.py:167-197)
+    n_residual = sum(len(src_pt_index[i][j]) * 4 for i in range(N) for j in range(N))
+    if verbose:
+        print("residual number is %d." % n_residual)
+    ref_pose = initial_ptzs[0]
+    frame, lm, xy = _records(N, points, src_pt_index, dst_pt_index, landmark_index)
+    rays0 = np.zeros((n_landmark, 2))
+    if n_landmark:
+        # last writer wins: the src record (even records) of the last match referencing each landmark
+        src_lm = lm[0::2]
+        last = len(src_lm) - 1 - np.unique(src_lm[::-1], return_index=True)[1]
+        lids = src_lm[last]
+        fi = frame[0::2][last]
+        pts = xy[0::2][last]
+        th, ph = ptzba.image_to_ray(u, v, initial_ptzs[fi, 2], initial_ptzs[fi, 0], initial_ptzs[fi, 1], pts[:, 0],
+                                    pts[:, 1], device=device)
+        rays0[lids, 0] = th
+        rays0[lids, 1] = ph
+
+    # step 3: optimisation on the GPU (replaces bundle_adjustment.py:200-202)
+    t0 = time.time()
+    all_poses = initial_ptzs.copy()
+    landmarks = rays0.copy()
+    if len(frame):
+        prec = ptzba.FP32 if precision == "fp32" else ptzba.FP64
+        ls = ptzba.LOSS_HUBER if loss == "huber" else ptzba.LOSS_LINEAR
+        all_poses, landmarks, res = ptzba.solve(N, n_landmark, frame, lm, xy, u, v, initial_ptzs, rays0, precision=prec,
+                                                loss=ls, f_scale=f_scale, device=device, ftol=ftol, xtol=xtol,
+                                                max_iter=max_iter)
+        all_poses[0] = ref_pose
+        LAST_RESULT.clear()
+        LAST_RESULT.update(result=res, n_residual=n_residual, n_landmark=n_landmark, time=time.time() - t0,
+                           x0=np.concatenate([initial_ptzs[1:].reshape(-1), rays0.reshape(-1)]))
+        if verbose:
+            print(f"GPU LM: {res}")
+
+    # step 5: keyframes (bundle_adjustment.py:214-248)
+    keyframes = []
+    for i in range(N):
+        pan, tilt, fl = all_poses[i]
+        key_frame = KeyFrame(images[i], image_indices[i], center, rotation, u, v, pan, tilt, fl)
+        pairs = []
+        for j in range(N):
+            if len(src_pt_index[i][j]) == 0:
+                continue
+            for idx1, idx3 in zip(src_pt_index[i][j], landmark_index[i][j]):
+                pairs.append((idx1, idx3))
+        for j in range(N):
+            if len(dst_pt_index[j][i]) == 0:
+                continue
+            for idx2, idx3 in zip(dst_pt_index[j][i], landmark_index[j][i]):
+                pairs.append((idx2, idx3))
+        pairs = set(pairs)
+        local_index, global_index = [], []
+        for pair in pairs:
+            local_index.append(pair[0])
+            global_index.append(pair[1])
+        key_frame.feature_pts = [keypoints[i][j] for j in local_index]
+        key_frame.feature_des = np.asarray(descriptors[i]).take(local_index, axis=0)
+        key_frame.landmark_index = np.array(global_index, dtype=np.int32)
+        keyframes.append(key_frame)
+        if verbose:
+            print("frame %d, landmark number %d" % (image_indices[i], len(key_frame.landmark_index)))
+    return landmarks, keyframes

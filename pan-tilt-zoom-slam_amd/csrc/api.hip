@@ -93,12 +93,14 @@ struct ptzba_ctx {
   DBuf frame_seg_begin, frame_seg_list, frame_win_hi;
   // device: state
   DBuf ptz, rays, ptz_trial, rays_trial, D_pose, D_ray;
-  DBuf ft, rt;
-  DBuf seg_out[2], lm_out[2];
+  DBuf ft, rt, ft64, rt64, seg_base;
+  DBuf seg_out[2], seg_w[2], lm_out[2];
   int cur = 0;
   DBuf lm_aux, lm_red;
   DBuf sys;  // [S ld*ld | b ld | g_pose ld | dU ld]
-  DBuf scal, loc, info, tile_nz;
+  DBuf scal, loc, info;
+  DBuf chol_tasks, chol_colfirst, chol_rowend, Ldiag, dpose;
+  std::vector<int> chol_task_off;  // host: per tile column, offsets into chol_tasks
   double lambda = 0;
   // timing
   bool timing = false;
@@ -168,12 +170,16 @@ int ptzba_set_stream(ptzba_handle h, void* stream) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// records hold obs - base(segment) in `real`; the per-segment base observation stays fp64, so the
+// per-record arithmetic of K1 works on O(residual) magnitudes even in fp32
 template <typename real>
-static int upload_records(ptzba_ctx* h, const std::vector<int64_t>& order, const double* obs_xy, const double* w) {
+static int upload_records(ptzba_ctx* h, const std::vector<int64_t>& order, const std::vector<int32_t>& rec_seg,
+                          const std::vector<double>& base, const double* obs_xy, const double* w) {
   std::vector<real> xy(2 * h->n_rec);
   for (int64_t r = 0; r < h->n_rec; ++r) {
-    xy[2 * r] = (real)obs_xy[2 * order[r]];
-    xy[2 * r + 1] = (real)obs_xy[2 * order[r] + 1];
+    const int32_t s = rec_seg[r];
+    xy[2 * r] = (real)(obs_xy[2 * order[r]] - base[2 * s]);
+    xy[2 * r + 1] = (real)(obs_xy[2 * order[r] + 1] - base[2 * s + 1]);
   }
   if (h->rec_xy.alloc(xy.size() * sizeof(real))) return -1;
   HIPCHK(hipMemcpy(h->rec_xy.p, xy.data(), xy.size() * sizeof(real), hipMemcpyHostToDevice));
@@ -192,6 +198,52 @@ template <typename T>
 static int upload(DBuf& b, const std::vector<T>& v) {
   if (b.alloc(v.size() * sizeof(T))) return -1;
   if (!v.empty()) HIPCHK(hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return 0;
+}
+
+// Envelope of the reduced camera system and the per-step task lists of the fused Cholesky.
+// Block column f1 holds rows of frames f2 in [f1, win_hi[f1]] (k_schur), so row-frame f2's first
+// non-zero column frame is lo(f2) = min{ f1 : win_hi[f1] >= f2 }.
+static int build_chol_plan(ptzba_ctx* h, const std::vector<int32_t>& win_hi) {
+  const int nf = h->n_fixed, n = h->n_sys;
+  const int T = (int)(h->ld / CHOL_NB);
+  std::vector<int> lo(h->n_pose, 0);
+  for (int f2 = nf; f2 < h->n_pose; ++f2) {
+    int f = f2;
+    for (int f1 = nf; f1 <= f2; ++f1)
+      if (win_hi[f1] >= f2) { f = f1; break; }
+    lo[f2] = f;
+  }
+  std::vector<int> colfirst(T, 0), rowend(T, 0);
+  for (int i = 0; i < T; ++i) {
+    int cf = i;
+    for (int r = i * CHOL_NB; r < (i + 1) * CHOL_NB; ++r) {
+      if (r < n) cf = std::min(cf, 3 * (lo[r / 3 + nf] - nf) / CHOL_NB);
+      else if (r == n) cf = 0;  // augmented right-hand-side row is dense
+    }
+    colfirst[i] = cf;
+  }
+  for (int kt = 0; kt < T; ++kt) {
+    int last = kt;
+    for (int i = kt; i < T; ++i)
+      if (colfirst[i] <= kt) last = i;
+    rowend[kt] = std::min(n, (last + 1) * CHOL_NB);
+  }
+  std::vector<int> tasks;
+  h->chol_task_off.assign(T + 1, 0);
+  for (int k = 0; k < T; ++k) {
+    h->chol_task_off[k] = (int)tasks.size();
+    for (int i = k; i < T; ++i)
+      if (colfirst[i] <= k) tasks.push_back((i << 15) | k);
+    if (k > 0)
+      for (int i = k + 1; i < T; ++i) {
+        if (colfirst[i] > k - 1) continue;
+        for (int j = k + 1; j <= i; ++j)
+          if (colfirst[j] <= k - 1) tasks.push_back((1 << 30) | (i << 15) | j);
+      }
+  }
+  h->chol_task_off[T] = (int)tasks.size();
+  if (upload(h->chol_tasks, tasks) || upload(h->chol_colfirst, colfirst) || upload(h->chol_rowend, rowend)) return -1;
   return 0;
 }
 
@@ -295,15 +347,22 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->n_work = (int)lm_order.size();
   h->max_seg_per_lm = max_seg;
   h->n_sys = 3 * (n_pose - o.n_fixed);
-  h->ld = std::max<int64_t>(CHOL_NB, ((int64_t)h->n_sys + CHOL_NB - 1) / CHOL_NB * CHOL_NB);
+  h->ld = ((int64_t)h->n_sys + 1 + CHOL_NB - 1) / CHOL_NB * CHOL_NB;  // + augmented rhs row
   if (h->ld > 20000) return fail("reduced system %d too large for the dense solver", h->n_sys);
   h->perm_host = order;
   h->perm_uploaded = false;
 
   // ---- upload
-  int rc = h->precision == PTZBA_FP32 ? upload_records<float>(h, order, obs_xy, obs_weight)
-                                      : upload_records<double>(h, order, obs_xy, obs_weight);
+  std::vector<double> seg_base(2 * n_seg);
+  for (int64_t s = 0; s < n_seg; ++s) {
+    const int64_t r = order[seg_rec_begin[s]];
+    seg_base[2 * s] = obs_xy[2 * r];
+    seg_base[2 * s + 1] = obs_xy[2 * r + 1];
+  }
+  int rc = h->precision == PTZBA_FP32 ? upload_records<float>(h, order, rec_seg, seg_base, obs_xy, obs_weight)
+                                      : upload_records<double>(h, order, rec_seg, seg_base, obs_xy, obs_weight);
   if (rc) return rc;
+  if (upload(h->seg_base, seg_base)) return -1;
   if (upload(h->rec_seg, rec_seg) || upload(h->seg_frame, seg_frame) || upload(h->seg_lm, seg_lm) ||
       upload(h->seg_rec_begin, seg_rec_begin) || upload(h->lm_seg_begin, lm_seg_begin) ||
       upload(h->lm_order, lm_order) || upload(h->frame_seg_begin, frame_seg_begin) ||
@@ -313,13 +372,16 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   if (h->ptz.alloc(3 * n_pose * 8) || h->ptz_trial.alloc(3 * n_pose * 8) || h->rays.alloc(2 * (size_t)n_landmark * 8) ||
       h->rays_trial.alloc(2 * (size_t)n_landmark * 8) || h->D_pose.alloc(3 * n_pose * 8) ||
       h->D_ray.alloc(2 * (size_t)n_landmark * 8) || h->ft.alloc((size_t)n_pose * 8 * e) ||
-      h->rt.alloc((size_t)n_landmark * 8 * e) || h->seg_out[0].alloc((size_t)n_seg * 16 * e) ||
-      h->seg_out[1].alloc((size_t)n_seg * 16 * e) || h->lm_out[0].alloc((size_t)n_landmark * 8 * 8) ||
+      h->rt.alloc((size_t)n_landmark * 8 * e) || h->ft64.alloc((size_t)n_pose * 64) ||
+      h->rt64.alloc((size_t)n_landmark * 64) || h->seg_out[0].alloc((size_t)n_seg * 16 * e) ||
+      h->seg_out[1].alloc((size_t)n_seg * 16 * e) || h->seg_w[0].alloc((size_t)n_seg * 8 * e) ||
+      h->seg_w[1].alloc((size_t)n_seg * 8 * e) || h->lm_out[0].alloc((size_t)n_landmark * 8 * 8) ||
       h->lm_out[1].alloc((size_t)n_landmark * 8 * 8) || h->lm_aux.alloc((size_t)n_landmark * 8 * 8) ||
       h->lm_red.alloc((size_t)n_landmark * 4 * 8) || h->sys.alloc((size_t)h->sys_count() * 8) ||
       h->scal.alloc(PTZBA_NSCALARS * 8) || h->loc.alloc(PTZBA_NSCALARS * 8) || h->info.alloc(16) ||
-      h->tile_nz.alloc((size_t)(h->ld / CHOL_NB + 1) * 4))
+      h->Ldiag.alloc((size_t)h->ld * CHOL_NB * 8) || h->dpose.alloc((size_t)h->ld * 8))
     return -1;
+  if (build_chol_plan(h, frame_win_hi)) return -1;
   HIPCHK(hipMemset(h->D_pose.p, 0, h->D_pose.bytes));
   HIPCHK(hipMemset(h->D_ray.p, 0, h->D_ray.bytes));
   HIPCHK(hipMemset(h->ptz.p, 0, h->ptz.bytes));
@@ -342,6 +404,7 @@ int ptzba_problem_info(ptzba_handle h, int64_t* info) {
   info[5] = h->n_work;
   info[6] = h->max_seg_per_lm;
   info[7] = (int64_t)g_total_bytes({&h->rec_xy, &h->rec_seg, &h->rec_w, &h->perm, &h->seg_frame, &h->seg_lm,
+                                    &h->seg_base, &h->ft64, &h->rt64,
                                     &h->seg_rec_begin, &h->lm_seg_begin, &h->lm_order, &h->frame_seg_begin,
                                     &h->frame_seg_list, &h->frame_win_hi, &h->ptz, &h->rays, &h->ptz_trial,
                                     &h->rays_trial, &h->D_pose, &h->D_ray, &h->ft, &h->rt, &h->seg_out[0],
@@ -351,11 +414,14 @@ int ptzba_problem_info(ptzba_handle h, int64_t* info) {
 }
 
 // ------------------------------------------------------------------------------------------------
+static void* ft_real(ptzba_ctx* h) { return h->precision == PTZBA_FP32 ? h->ft.p : h->ft64.p; }
+static void* rt_real(ptzba_ctx* h) { return h->precision == PTZBA_FP32 ? h->rt.p : h->rt64.p; }
+
 static void tables(ptzba_ctx* h, const double* ptz, const double* rays) {
   if (h->precision == PTZBA_FP32)
-    launch_tables<float>(ptz, rays, h->n_pose, h->n_lm, h->ft.p, h->rt.p, h->st);
+    launch_tables<float>(ptz, rays, h->n_pose, h->n_lm, h->ft64.p, h->rt64.p, h->ft.p, h->rt.p, h->st);
   else
-    launch_tables<double>(ptz, rays, h->n_pose, h->n_lm, h->ft.p, h->rt.p, h->st);
+    launch_tables<double>(ptz, rays, h->n_pose, h->n_lm, h->ft64.p, h->rt64.p, h->ft64.p, h->rt64.p, h->st);
 }
 
 static void linearize_into(ptzba_ctx* h, int slot) {
@@ -368,13 +434,17 @@ static void linearize_into(ptzba_ctx* h, int slot) {
   a.rec_seg = h->rec_seg.as<int32_t>();
   a.rec_xy = h->rec_xy.p;
   a.rec_w = h->weighted ? h->rec_w.p : nullptr;
-  a.ft = h->ft.p;
-  a.rt = h->rt.p;
+  a.ft = ft_real(h);
+  a.rt = rt_real(h);
+  a.ft64 = h->ft64.p;
+  a.rt64 = h->rt64.p;
+  a.seg_base = h->seg_base.as<double2>();
   a.u = h->u;
   a.v = h->v;
   a.fs2 = h->fs * h->fs;
   a.inv_fs2 = 1.0 / (h->fs * h->fs);
   a.seg_out = h->seg_out[slot].p;
+  a.seg_w = h->seg_w[slot].p;
   a.lm_out = h->lm_out[slot].as<double>();
   // landmarks without records keep zero rows
   (void)hipMemsetAsync(h->lm_out[slot].p, 0, h->lm_out[slot].bytes, h->st);
@@ -399,11 +469,13 @@ int ptzba_residual(ptzba_handle h, const double* x_full, double* r_out) {
   const double* px = x.as<double>();
   tables(h, px, px + 3 * h->n_pose);
   if (h->precision == PTZBA_FP32)
-    launch_residual<float>(h->rec_seg.as<int32_t>(), h->seg_frame.as<int32_t>(), h->seg_lm.as<int32_t>(), h->rec_xy.p,
-                           h->perm.as<int64_t>(), h->ft.p, h->rt.p, h->u, h->v, h->n_rec, r.as<double>(), h->st);
+    launch_residual<float>(h->rec_seg.as<int32_t>(), h->seg_frame.as<int32_t>(), h->seg_lm.as<int32_t>(),
+                           h->seg_base.as<double2>(), h->rec_xy.p, h->perm.as<int64_t>(), h->ft64.p, h->rt64.p, h->u,
+                           h->v, h->n_rec, r.as<double>(), h->st);
   else
-    launch_residual<double>(h->rec_seg.as<int32_t>(), h->seg_frame.as<int32_t>(), h->seg_lm.as<int32_t>(), h->rec_xy.p,
-                            h->perm.as<int64_t>(), h->ft.p, h->rt.p, h->u, h->v, h->n_rec, r.as<double>(), h->st);
+    launch_residual<double>(h->rec_seg.as<int32_t>(), h->seg_frame.as<int32_t>(), h->seg_lm.as<int32_t>(),
+                            h->seg_base.as<double2>(), h->rec_xy.p, h->perm.as<int64_t>(), h->ft64.p, h->rt64.p, h->u,
+                            h->v, h->n_rec, r.as<double>(), h->st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(r_out, r.p, 2 * (size_t)h->n_rec * 8, hipMemcpyDeviceToHost, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
@@ -458,6 +530,7 @@ int ptzba_build_reduced(ptzba_handle h, double lambda) {
   a.seg_frame = h->seg_frame.as<int32_t>();
   a.lm_seg_begin = h->lm_seg_begin.as<int32_t>();
   a.seg_out = h->seg_out[c].p;
+  a.seg_w = h->seg_w[c].p;
   a.lm_aux = h->lm_aux.as<double>();
   a.S = h->S();
   a.b = h->bvec();
@@ -483,13 +556,15 @@ int ptzba_solve_reduced(ptzba_handle h) {
   tm_begin(h, TM_CHOL);
   launch_pose_damp(h->S(), h->ld, h->dU(), h->D_pose.as<double>(), h->n_pose, h->n_fixed, h->lambda, h->st);
   launch_chol_prepare(h->S(), h->ld, h->n_sys, h->bvec(), h->info.as<int>(), h->st);
-  launch_cholesky(h->S(), h->ld, h->info.as<int>(), h->tile_nz.as<int>(), h->st);
-  launch_chol_solve(h->S(), h->ld, h->bvec(), h->st);
+  launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int>(), h->chol_task_off.data(), h->chol_colfirst.as<int>(),
+                  h->Ldiag.as<double>(), h->info.as<int>(), h->st);
+  launch_chol_backsolve(h->S(), h->ld, h->n_sys, h->chol_rowend.as<int>(), h->Ldiag.as<double>(), h->dpose.as<double>(),
+                        h->st);
   tm_end(h, TM_CHOL);
   HIPCHK(hipGetLastError());
   tm_begin(h, TM_BACK);
   HIPCHK(hipMemsetAsync(h->loc.p, 0, h->loc.bytes, h->st));
-  launch_pose_trial(h->ptz.as<double>(), h->bvec(), h->gpose(), h->D_pose.as<double>(), h->ptz_trial.as<double>(),
+  launch_pose_trial(h->ptz.as<double>(), h->dpose.as<double>(), h->gpose(), h->D_pose.as<double>(), h->ptz_trial.as<double>(),
                     h->n_pose, h->n_fixed, h->lambda, h->loc.as<double>(), h->st);
   BacksubArgs b;
   b.lm_seg_begin = h->lm_seg_begin.as<int32_t>();
@@ -498,7 +573,7 @@ int ptzba_solve_reduced(ptzba_handle h) {
   b.lm_out = h->lm_out[c].as<double>();
   b.lm_aux = h->lm_aux.as<double>();
   b.D_ray = h->D_ray.as<double>();
-  b.dpose = h->bvec();
+  b.dpose = h->dpose.as<double>();
   b.rays = h->rays.as<double>();
   b.rays_trial = h->rays_trial.as<double>();
   b.lm_red = h->lm_red.as<double>();

@@ -30,22 +30,37 @@ namespace ptzba {
 // ------------------------------------------------------------------------------------------------
 template <typename real>
 __global__ void k_tables(const double* __restrict__ ptz, const double* __restrict__ rays, int n_pose,
-                         int n_lm, FrameTab<real>* __restrict__ ft, RayTab<real>* __restrict__ rt) {
+                         int n_lm, FrameTab<double>* __restrict__ ft64, RayTab<double>* __restrict__ rt64,
+                         FrameTab<real>* __restrict__ ft, RayTab<real>* __restrict__ rt) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n_pose) {
-    ft[i] = make_frame_tab<real>(ptz[3 * i], ptz[3 * i + 1], ptz[3 * i + 2]);
+    FrameTab<double> t = make_frame_tab<double>(ptz[3 * i], ptz[3 * i + 1], ptz[3 * i + 2]);
+    ft64[i] = t;
+    if constexpr (sizeof(real) != sizeof(double)) {
+      FrameTab<real> r;
+      r.ca = (real)t.ca; r.sa = (real)t.sa; r.cb = (real)t.cb; r.sb = (real)t.sb; r.f = (real)t.f;
+      r.pad0 = r.pad1 = r.pad2 = (real)0;
+      ft[i] = r;
+    }
   } else if (i < n_pose + n_lm) {
     int l = i - n_pose;
-    rt[l] = make_ray_tab<real>(rays[2 * l], rays[2 * l + 1]);
+    RayTab<double> t = make_ray_tab<double>(rays[2 * l], rays[2 * l + 1]);
+    rt64[l] = t;
+    if constexpr (sizeof(real) != sizeof(double)) {
+      RayTab<real> r;
+      r.p0 = (real)t.p0; r.p1 = (real)t.p1; r.d0t = (real)t.d0t; r.d1t = (real)t.d1t; r.d1p = (real)t.d1p;
+      r.pad0 = r.pad1 = r.pad2 = (real)0;
+      rt[l] = r;
+    }
   }
 }
 
 template <typename real>
-void launch_tables(const double* ptz, const double* rays, int n_pose, int n_lm, void* ft, void* rt,
-                   hipStream_t st) {
+void launch_tables(const double* ptz, const double* rays, int n_pose, int n_lm, void* ft64, void* rt64, void* ft,
+                   void* rt, hipStream_t st) {
   int n = n_pose + n_lm;
   hipLaunchKernelGGL(k_tables<real>, dim3((n + 255) / 256), dim3(256), 0, st, ptz, rays, n_pose, n_lm,
-                     (FrameTab<real>*)ft, (RayTab<real>*)rt);
+                     (FrameTab<double>*)ft64, (RayTab<double>*)rt64, (FrameTab<real>*)ft, (RayTab<real>*)rt);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -64,9 +79,13 @@ __global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
   const int s0 = a.lm_seg_begin[l], s1 = a.lm_seg_begin[l + 1];
   const FrameTab<real>* __restrict__ ft = (const FrameTab<real>*)a.ft;
   const RayTab<real> R = ((const RayTab<real>*)a.rt)[l];
+  const FrameTab<double>* __restrict__ ft64 = (const FrameTab<double>*)a.ft64;
+  const RayTab<double> R64 = ((const RayTab<double>*)a.rt64)[l];
+  const double2* __restrict__ seg_base = a.seg_base;
   const real* __restrict__ rec_xy = (const real*)a.rec_xy;
   const real* __restrict__ rec_w = (const real*)a.rec_w;
   real* __restrict__ seg_out = (real*)a.seg_out;
+  real* __restrict__ seg_w = (real*)a.seg_w;
   const real u = (real)a.u, v = (real)a.v;
   const real fs2 = (real)a.fs2, ifs2 = (real)a.inv_fs2;
   real* sx = s_x[wv];
@@ -80,13 +99,15 @@ __global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
 
   for (int w0 = s0; w0 < s1; w0 += SEGW) {
     const int w1 = min(s1, w0 + SEGW);
-    // phase A: projection of every segment of the window (lanes over segments)
+    // phase A: fp64 projection of every segment of the window (lanes over segments), kept as the
+    // offset from the segment's base observation so phase B works on O(residual) magnitudes
     for (int s = w0 + lane; s < w1; s += WAVE) {
       const int sl = s - w0;
-      real x, y;
-      ptz_project<real>(ft[a.seg_frame[s]], R, u, v, x, y);
-      sx[sl] = x;
-      sy[sl] = y;
+      double x, y;
+      ptz_project<double>(ft64[a.seg_frame[s]], R64, a.u, a.v, x, y);
+      const double2 bs = seg_base[s];
+      sx[sl] = (real)(x - bs.x);
+      sy[sl] = (real)(y - bs.y);
       acc0[sl] = 0; acc1[sl] = 0; acc2[sl] = 0; acc3[sl] = 0;
     }
     wave_lds_fence();
@@ -151,7 +172,8 @@ __global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
     for (int s = w0 + lane; s < w1; s += WAVE) {
       const int sl = s - w0;
       real x, y, J[2][5];
-      ptz_project_jac<real>(ft[a.seg_frame[s]], R, u, v, x, y, J);
+      const int fs = a.seg_frame[s];
+      ptz_project_jac<real>(ft[fs], R, u, v, x, y, J);
       const real Sx = acc0[sl], Sy = acc1[sl], Srx = acc2[sl], Sry = acc3[sl];
       real* o = seg_out + (int64_t)s * 16;
       // W = Jp^T diag(Sx,Sy) Jr  (3x2)
@@ -172,6 +194,12 @@ __global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
       o[13] = J[0][1] * Srx + J[1][1] * Sry;
       o[14] = J[0][2] * Srx + J[1][2] * Sry;
       o[15] = 0;
+      // compact copy for the Schur kernel's inner loop: {W (6), frame id, 0} = 32 B (fp32) / 64 B (fp64)
+      real* cw = seg_w + (int64_t)s * 8;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) cw[k] = o[k];
+      cw[6] = __int_as_real<real>(fs);
+      cw[7] = 0;
       V00 += (double)(Sx * J[0][3] * J[0][3] + Sy * J[1][3] * J[1][3]);
       V01 += (double)(Sx * J[0][3] * J[0][4] + Sy * J[1][3] * J[1][4]);
       V11 += (double)(Sx * J[0][4] * J[0][4] + Sy * J[1][4] * J[1][4]);
@@ -238,112 +266,170 @@ void launch_landmark_damp(const double* lm_out, const int32_t* lm_seg_begin, dou
 }
 
 // ------------------------------------------------------------------------------------------------
-// K2: reduced camera system  S = U + lambda D - sum_l W_l V~_l^-1 W_l^T,
+// K2: reduced camera system  S = U - sum_l W_l V~_l^-1 W_l^T   (damping added after the exchange),
 //                            b = -g_pose + sum_l W_l V~_l^-1 g_l
-// One workgroup per free frame f1 builds block column f1 of the lower triangle (frames f2 >= f1);
-// the 3x3 blocks S[f1, f2] accumulate in LDS (fp64 atomics: each landmark's segments have distinct
-// frames, so lanes of one wave never collide; waves do).
+// One 1024-thread workgroup per free frame f1 builds block column f1 of the lower triangle
+// (frames f2 >= f1) in an LDS window of 3x3 blocks.  Each of the 16 waves takes a contiguous slice
+// of f1's segment list; per chunk of 64 segments the lanes fetch the segments' metadata in parallel
+// (segment -> landmark -> W, V~^-1: no per-segment dependent-load chain), then for each segment
+// (broadcast with readlane) the lanes walk landmark l's segments f2 >= f1 (distinct frames, so a
+// wave's lanes never collide) and add -Y W_f2^T (Y = W_f1 V~^-1) with LDS fp64 atomics
+// (ds_add_f64: waves may hit the same frame).
 // ------------------------------------------------------------------------------------------------
+#ifndef SCHUR_VARIANT
+#define SCHUR_VARIANT 0
+#endif
 constexpr int SCHUR_WMAX = 448;  // frames per LDS window (448 * 9 * 8 B = 31.5 KiB)
+constexpr int SCHUR_WAVES = 16;
+
+__device__ __forceinline__ double bcast(double v, int j) {
+  int lo = __builtin_amdgcn_readlane(__double2loint(v), j);
+  int hi = __builtin_amdgcn_readlane(__double2hiint(v), j);
+  return __hiloint2double(hi, lo);
+}
+
+// Bijection block -> item that gives each XCD group (b mod 8) a contiguous run of items.
+__device__ __forceinline__ int xcd_swizzle(int b, int nb) {
+  const int c = b & 7, idx = b >> 3;
+  int start = 0;
+  for (int q = 0; q < c; ++q) start += (nb - q + 7) >> 3;
+  return start + idx;
+}
 
 template <typename real>
-__global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
+__global__ __launch_bounds__(1024) void k_schur(SchurArgs a) {
   __shared__ double s_S[SCHUR_WMAX * 9];
-  __shared__ double s_red[4][16];
-  const int f1 = blockIdx.x + a.n_fixed;
+  __shared__ double s_red[SCHUR_WAVES][12];
+  // XCD-aware frame order: workgroups b and b+8 share an XCD (round-robin dispatch), so give each XCD
+  // a contiguous run of frames -> neighbouring frames (which share landmarks) hit the same L2.
+  const int f1 = xcd_swizzle(blockIdx.x, gridDim.x) + a.n_fixed;
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
+  const int half = lane >> 5, hl = lane & 31;
   const real* __restrict__ seg_out = (const real*)a.seg_out;
+  const real* __restrict__ seg_w = (const real*)a.seg_w;
   const int e0 = a.frame_seg_begin[f1], e1 = a.frame_seg_begin[f1 + 1];
+  const int ne = e1 - e0;
+  const int eb = e0 + (int)(((int64_t)ne * wv) / SCHUR_WAVES);
+  const int ee = e0 + (int)(((int64_t)ne * (wv + 1)) / SCHUR_WAVES);
   const int hi = a.frame_win_hi[f1];
   const int col0 = 3 * (f1 - a.n_fixed);
   const int64_t ld = a.ld;
 
-  // per-wave uniform accumulators: U (6), g_pose (3), sum W Vinv g (3)
   double aU[6] = {0, 0, 0, 0, 0, 0}, ag[3] = {0, 0, 0}, ab[3] = {0, 0, 0};
 
   for (int p0 = f1; p0 <= hi; p0 += SCHUR_WMAX) {
-    const int p1 = min(hi + 1, p0 + SCHUR_WMAX);  // window [p0, p1)
+    const int p1 = min(hi + 1, p0 + SCHUR_WMAX);
     const int width = p1 - p0;
+    const bool first = (p0 == f1);
     for (int k = threadIdx.x; k < width * 9; k += blockDim.x) s_S[k] = 0;
     __syncthreads();
-    const bool first = (p0 == f1);
-    for (int e = e0 + wv; e < e1; e += 4) {
-      const int s1 = a.frame_seg_list[e];
-      const int l = a.seg_lm[s1];
-      const real* w1 = seg_out + (int64_t)s1 * 16;
-      const double* vi = a.lm_aux + (int64_t)l * 8;
-      const double i00 = vi[0], i01 = vi[1], i11 = vi[2];
-      double W[3][2];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) { W[q][0] = (double)w1[2 * q]; W[q][1] = (double)w1[2 * q + 1]; }
-      double Y[3][2];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        Y[q][0] = W[q][0] * i00 + W[q][1] * i01;
-        Y[q][1] = W[q][0] * i01 + W[q][1] * i11;
-      }
-      if (first) {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) aU[k] += (double)w1[6 + k];
+    for (int cb = eb; cb < ee; cb += WAVE) {
+      // ---- lane-parallel metadata of up to 64 segments of f1
+      const int e = cb + lane;
+      const bool ok = e < ee;
+      int s1 = 0, send = 0;
+      double Y[3][2] = {{0, 0}, {0, 0}, {0, 0}};
+      if (ok) {
+        s1 = a.frame_seg_list[e];
+        const int l = a.seg_lm[s1];
+        send = a.lm_seg_begin[l + 1];
+        const real* w1 = seg_out + (int64_t)s1 * 16;
+        const double* vi = a.lm_aux + (int64_t)l * 8;
+        const double i00 = vi[0], i01 = vi[1], i11 = vi[2];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-          ag[q] += (double)w1[12 + q];
-          ab[q] += W[q][0] * vi[3] + W[q][1] * vi[4];
+          const double W0 = (double)w1[2 * q], W1 = (double)w1[2 * q + 1];
+          Y[q][0] = W0 * i00 + W1 * i01;
+          Y[q][1] = W0 * i01 + W1 * i11;
+          if (first) ab[q] += W0 * vi[3] + W1 * vi[4];
+        }
+        if (first) {
+#pragma unroll
+          for (int k = 0; k < 6; ++k) aU[k] += (double)w1[6 + k];
+#pragma unroll
+          for (int q = 0; q < 3; ++q) ag[q] += (double)w1[12 + q];
         }
       }
-      const int send = a.lm_seg_begin[l + 1];
-      for (int s2 = s1 + lane; s2 < send; s2 += WAVE) {
-        const int f2 = a.seg_frame[s2];
-        if (f2 < p0) continue;
-        if (f2 >= p1) break;
-        const real* w2 = seg_out + (int64_t)s2 * 16;
-        double X[3][2];
+      const int n = min(WAVE, ee - cb);
+      // two segments per step, one per half-wave (lanes of a half never collide; halves may -> atomics)
+      for (int j2 = 0; j2 < n; j2 += 2) {
+        const int j = min(j2 + half, n - 1);
+        const bool vj = (j2 + half) < n;
+        const int s1j = __shfl(s1, j, WAVE);
+        const int sendj = vj ? __shfl(send, j, WAVE) : 0;
+        double Yj[3][2];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) { X[q][0] = (double)w2[2 * q]; X[q][1] = (double)w2[2 * q + 1]; }
-        double* dst = s_S + (f2 - p0) * 9;
+        for (int q = 0; q < 3; ++q) {
+          Yj[q][0] = __shfl(Y[q][0], j, WAVE);
+          Yj[q][1] = __shfl(Y[q][1], j, WAVE);
+        }
+#if SCHUR_VARIANT == 3
+        if (sendj == -7)
+#endif
+        for (int s2 = s1j + hl; s2 < sendj; s2 += 32) {
+          const real* w2 = seg_w + (int64_t)s2 * 8;
+          const int f2 = __real_as_int(w2[6]);
+          double X[3][2];
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
+          for (int q = 0; q < 3; ++q) { X[q][0] = (double)w2[2 * q]; X[q][1] = (double)w2[2 * q + 1]; }
+          if (f2 >= p0 && f2 < p1) {
+            double* dst = s_S + (f2 - p0) * 9;
+#if SCHUR_VARIANT == 0
 #pragma unroll
-          for (int r = 0; r < 3; ++r) atomicAdd(dst + 3 * q + r, -(Y[q][0] * X[r][0] + Y[q][1] * X[r][1]));
+            for (int q = 0; q < 3; ++q)
+#pragma unroll
+              for (int r = 0; r < 3; ++r) atomicAdd(dst + 3 * q + r, -(Yj[q][0] * X[r][0] + Yj[q][1] * X[r][1]));
+#elif SCHUR_VARIANT == 1
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+#pragma unroll
+              for (int r = 0; r < 3; ++r) dst[3 * q + r] -= Yj[q][0] * X[r][0] + Yj[q][1] * X[r][1];
+#elif SCHUR_VARIANT == 2
+            double acc = 0;
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+#pragma unroll
+              for (int r = 0; r < 3; ++r) acc += Yj[q][0] * X[r][0] + Yj[q][1] * X[r][1];
+            if (acc == 12345.678) dst[0] = acc;
+#endif
+          }
+        }
       }
     }
-    __syncthreads();
     if (first) {
-      // combine the per-wave uniform accumulators
+#pragma unroll
+      for (int k = 0; k < 6; ++k) aU[k] = wave_sum(aU[k]);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) { ag[q] = wave_sum(ag[q]); ab[q] = wave_sum(ab[q]); }
       if (lane == 0) {
         for (int k = 0; k < 6; ++k) s_red[wv][k] = aU[k];
         for (int q = 0; q < 3; ++q) { s_red[wv][6 + q] = ag[q]; s_red[wv][9 + q] = ab[q]; }
       }
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        double U[6], g[3], bb[3];
-        for (int k = 0; k < 6; ++k) U[k] = s_red[0][k] + s_red[1][k] + s_red[2][k] + s_red[3][k];
-        for (int q = 0; q < 3; ++q) {
-          g[q] = s_red[0][6 + q] + s_red[1][6 + q] + s_red[2][6 + q] + s_red[3][6 + q];
-          bb[q] = s_red[0][9 + q] + s_red[1][9 + q] + s_red[2][9 + q] + s_red[3][9 + q];
-        }
-        // diagonal block: U + Schur part already in s_S[0..8]; Marquardt damping is added after
-        // the (multi-GPU) exchange from the diag(U) written here (k_pose_damp)
-        const int ui[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
-        for (int q = 0; q < 3; ++q)
-          for (int r = 0; r < 3; ++r) s_S[3 * q + r] += U[ui[q][r]];
-        a.dU[col0 + 0] = U[0];
-        a.dU[col0 + 1] = U[3];
-        a.dU[col0 + 2] = U[5];
-        for (int q = 0; q < 3; ++q) {
-          a.b[col0 + q] = -g[q] + bb[q];
-          a.g_pose[col0 + q] = g[q];
-        }
-      }
-      __syncthreads();
     }
+    __syncthreads();
+    if (first && threadIdx.x == 0) {
+      double U[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0}, bb[3] = {0, 0, 0};
+      for (int w = 0; w < SCHUR_WAVES; ++w) {
+        for (int k = 0; k < 6; ++k) U[k] += s_red[w][k];
+        for (int q = 0; q < 3; ++q) { g[q] += s_red[w][6 + q]; bb[q] += s_red[w][9 + q]; }
+      }
+      const int ui[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
+      for (int q = 0; q < 3; ++q)
+        for (int r = 0; r < 3; ++r) s_S[3 * q + r] += U[ui[q][r]];
+      for (int q = 0; q < 3; ++q) {
+        a.b[col0 + q] = -g[q] + bb[q];
+        a.g_pose[col0 + q] = g[q];
+      }
+      a.dU[col0 + 0] = U[0];
+      a.dU[col0 + 1] = U[3];
+      a.dU[col0 + 2] = U[5];
+    }
+    __syncthreads();
     // write block column f1, rows of frames in [p0, p1): S[row(f2)+r][col0+q] = S_{f1,f2}[q][r]
     for (int k = threadIdx.x; k < width * 9; k += blockDim.x) {
       const int t = k / 9, qr = k % 9, q = qr / 3, r = qr % 3;
-      const int f2 = p0 + t;
-      if (f2 < a.n_fixed) continue;
-      const int64_t row = 3 * (f2 - a.n_fixed) + r;
+      const int64_t row = 3 * (p0 + t - a.n_fixed) + r;
       a.S[row * ld + col0 + q] = s_S[k];
     }
     __syncthreads();
@@ -353,7 +439,7 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
 template <typename real>
 void launch_schur(const SchurArgs& a, int n_free, hipStream_t st) {
   if (n_free <= 0) return;
-  hipLaunchKernelGGL(k_schur<real>, dim3(n_free), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_schur<real>, dim3(n_free), dim3(64 * SCHUR_WAVES), 0, st, a);
 }
 
 // pose damping on the exchanged reduced system: D = max(D, diag U) (monotone), S_ii += lambda D_i
@@ -515,42 +601,46 @@ void launch_reduce_cols(const double* src, int64_t n, int stride, int nk, int ma
 // ------------------------------------------------------------------------------------------------
 template <typename real>
 __global__ void k_residual(const int32_t* __restrict__ rec_seg, const int32_t* __restrict__ seg_frame,
-                           const int32_t* __restrict__ seg_lm, const real* __restrict__ rec_xy,
-                           const int64_t* __restrict__ perm, const FrameTab<real>* __restrict__ ft,
-                           const RayTab<real>* __restrict__ rt, double u, double v, int64_t n_rec,
-                           double* __restrict__ r_out) {
+                           const int32_t* __restrict__ seg_lm, const double2* __restrict__ seg_base,
+                           const real* __restrict__ rec_xy, const int64_t* __restrict__ perm,
+                           const FrameTab<double>* __restrict__ ft64, const RayTab<double>* __restrict__ rt64,
+                           double u, double v, int64_t n_rec, double* __restrict__ r_out) {
   int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n_rec) return;
   const int s = rec_seg[r];
-  real x, y;
-  ptz_project<real>(ft[seg_frame[s]], rt[seg_lm[s]], (real)u, (real)v, x, y);
+  double x, y;
+  ptz_project<double>(ft64[seg_frame[s]], rt64[seg_lm[s]], u, v, x, y);
+  const double2 bs = seg_base[s];
+  const real ex = (real)(x - bs.x), ey = (real)(y - bs.y);
   const int64_t o = perm[r];
-  r_out[2 * o] = (double)(x - rec_xy[2 * r]);
-  r_out[2 * o + 1] = (double)(y - rec_xy[2 * r + 1]);
+  r_out[2 * o] = (double)(ex - rec_xy[2 * r]);
+  r_out[2 * o + 1] = (double)(ey - rec_xy[2 * r + 1]);
 }
 
 template <typename real>
-void launch_residual(const int32_t* rec_seg, const int32_t* seg_frame, const int32_t* seg_lm, const void* rec_xy,
-                     const int64_t* perm, const void* ft, const void* rt, double u, double v, int64_t n_rec,
-                     double* r_out, hipStream_t st) {
+void launch_residual(const int32_t* rec_seg, const int32_t* seg_frame, const int32_t* seg_lm, const double2* seg_base,
+                     const void* rec_xy, const int64_t* perm, const void* ft64, const void* rt64, double u, double v,
+                     int64_t n_rec, double* r_out, hipStream_t st) {
   if (n_rec <= 0) return;
   hipLaunchKernelGGL(k_residual<real>, dim3((unsigned)((n_rec + 255) / 256)), dim3(256), 0, st, rec_seg, seg_frame,
-                     seg_lm, (const real*)rec_xy, perm, (const FrameTab<real>*)ft, (const RayTab<real>*)rt, u, v,
-                     n_rec, r_out);
+                     seg_lm, seg_base, (const real*)rec_xy, perm, (const FrameTab<double>*)ft64,
+                     (const RayTab<double>*)rt64, u, v, n_rec, r_out);
 }
 
 // explicit instantiations
-template void launch_tables<float>(const double*, const double*, int, int, void*, void*, hipStream_t);
-template void launch_tables<double>(const double*, const double*, int, int, void*, void*, hipStream_t);
+template void launch_tables<float>(const double*, const double*, int, int, void*, void*, void*, void*, hipStream_t);
+template void launch_tables<double>(const double*, const double*, int, int, void*, void*, void*, void*, hipStream_t);
 template void launch_linearize<float>(const LinArgs&, int, hipStream_t);
 template void launch_linearize<double>(const LinArgs&, int, hipStream_t);
 template void launch_schur<float>(const SchurArgs&, int, hipStream_t);
 template void launch_schur<double>(const SchurArgs&, int, hipStream_t);
 template void launch_backsub<float>(const BacksubArgs&, hipStream_t);
 template void launch_backsub<double>(const BacksubArgs&, hipStream_t);
-template void launch_residual<float>(const int32_t*, const int32_t*, const int32_t*, const void*, const int64_t*,
-                                     const void*, const void*, double, double, int64_t, double*, hipStream_t);
-template void launch_residual<double>(const int32_t*, const int32_t*, const int32_t*, const void*, const int64_t*,
-                                      const void*, const void*, double, double, int64_t, double*, hipStream_t);
+template void launch_residual<float>(const int32_t*, const int32_t*, const int32_t*, const double2*, const void*,
+                                     const int64_t*, const void*, const void*, double, double, int64_t, double*,
+                                     hipStream_t);
+template void launch_residual<double>(const int32_t*, const int32_t*, const int32_t*, const double2*, const void*,
+                                      const int64_t*, const void*, const void*, double, double, int64_t, double*,
+                                      hipStream_t);
 
 }  // namespace ptzba

@@ -1,28 +1,42 @@
-// Dense fp64 Cholesky + triangular solves for the reduced camera system (gfx950).
+// Dense fp64 Cholesky solve of the reduced camera system (gfx950).
 //
-// The reduced camera system S (3(N-1) x 3(N-1), SPD) replaces scipy's dense SVD of the full
-// Jacobian (trf.py:467 via bundle_adjustment.py:200).  Right-looking blocked factorisation with
-// 32x32 tiles, in place, lower triangle, row-major:
-//   k_chol_diag   one wave factors the diagonal tile in LDS (no block barriers)
-//   k_chol_panel  one wave per 64 panel rows: row-wise forward substitution against L_kk
-//                 (L_kk broadcast from LDS), records which 32-row tiles are non-zero
-//   k_chol_update 32x32 tile SYRK/GEMM trailing update; tiles whose panel rows are zero are skipped
-//                 (S is block-banded: keyframes only couple to pan neighbours)
-// followed by one-workgroup forward and backward substitution.
+// The reduced camera system S (3(N-1) x 3(N-1), SPD, block-banded: keyframes couple only to pan
+// neighbours) replaces scipy's dense SVD of the full Jacobian (trf.py:467 via bundle_adjustment.py:200).
+//
+// Storage: row-major [ld][ld] lower triangle, ld = roundup(n + 1, 32).  Row n holds b^T (augmented
+// right-hand side) with a huge diagonal, so row n of the factor is y = L^-1 b: the forward
+// substitution comes out of the factorisation for free.  Rows > n are identity padding.
+//
+// Factorisation: 32x32 tiles, ONE launch per tile column k ("delayed update"):
+//   panel task (i, k):  T_ik <- A_ik - L_{i,k-1} L_{k,k-1}^T,  D <- A_kk - L_{k,k-1} L_{k,k-1}^T,
+//                       factor D in one wave (rows in registers, pivot column broadcast via LDS),
+//                       L_ik = T_ik L_kk^-T (lane per row, forward substitution)   [i == k: write L_kk]
+//   trailing task (i, j), i >= j > k:  A_ij <- A_ij - L_{i,k-1} L_{j,k-1}^T
+// Panel k-1's update reaches every tile exactly once (column k through the panel tasks, columns > k
+// through the trailing tasks of the same launch), so one launch per column suffices.  Only tiles
+// inside the profile (envelope) of S are visited; the envelope of L equals that of S.
+// Back substitution L^T x = y: one 1024-thread workgroup, 32-column steps, envelope-limited.
 #include "ptzba_common.h"
 #include "ptzba_kernels.h"
 
 namespace ptzba {
 
 constexpr int NB = CHOL_NB;
+constexpr double AUG_DIAG = 1e300;
 
-__global__ void k_chol_prepare(double* __restrict__ A, int64_t ld, int n, double* __restrict__ b, int* info) {
+__device__ __forceinline__ double bcast(double v, int j) {
+  int lo = __builtin_amdgcn_readlane(__double2loint(v), j);
+  int hi = __builtin_amdgcn_readlane(__double2hiint(v), j);
+  return __hiloint2double(hi, lo);
+}
+
+// augmented row / padding: A[n][j] = b[j], A[n][n] = huge, A[i][i] = 1 for i > n
+__global__ void k_chol_prepare(double* __restrict__ A, int64_t ld, int n, const double* __restrict__ b, int* info) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) info[0] = 0;
-  if (i >= n && i < ld) {
-    A[i * ld + i] = 1.0;
-    b[i] = 0.0;
-  }
+  if (i < n) A[(int64_t)n * ld + i] = b[i];
+  if (i == n) A[i * ld + i] = AUG_DIAG;
+  if (i > n && i < ld) A[i * ld + i] = 1.0;
 }
 
 void launch_chol_prepare(double* A, int64_t ld, int n, double* b, int* info, hipStream_t st) {
@@ -30,174 +44,199 @@ void launch_chol_prepare(double* A, int64_t ld, int n, double* b, int* info, hip
 }
 
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_chol_diag(double* __restrict__ A, int64_t ld, int k, int* info) {
-  __shared__ double T[NB][NB + 1];
-  const int lane = threadIdx.x;
-  double* base = A + (int64_t)k * NB * ld + (int64_t)k * NB;
-  for (int e = lane; e < NB * NB; e += WAVE) T[e / NB][e % NB] = base[(int64_t)(e / NB) * ld + (e % NB)];
-  wave_lds_fence();
-  const int i = lane & (NB - 1);
-  const int h = lane >> 5;
-  for (int j = 0; j < NB; ++j) {
-    double d = T[j][j];
-    if (!(d > 0.0)) {
-      if (lane == 0) atomicOr(info, 1);
-      d = 1e-300;
-    }
-    const double rs = 1.0 / sqrt(d);
-    wave_lds_fence();
-    if (h == 0 && i >= j) T[i][j] *= rs;
-    wave_lds_fence();
-    const double li = T[i][j];
-    if (i > j)
-      for (int m = j + 1 + h; m <= i; m += 2) T[i][m] -= li * T[m][j];
-    wave_lds_fence();
-  }
-  for (int e = lane; e < NB * NB; e += WAVE) {
-    const int r = e / NB, c = e % NB;
-    if (c <= r) base[(int64_t)r * ld + c] = T[r][c];
-  }
+__device__ __forceinline__ void load_tile(double (*dst)[NB + 1], const double* __restrict__ src, int64_t ld) {
+  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) dst[e >> 5][e & 31] = src[(int64_t)(e >> 5) * ld + (e & 31)];
 }
 
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_chol_panel(double* __restrict__ A, int64_t ld, int k, int* tile_nz) {
-  __shared__ double Lk[NB][NB + 1];
-  __shared__ double idg[NB];
-  const int lane = threadIdx.x;
-  const double* dbase = A + (int64_t)k * NB * ld + (int64_t)k * NB;
-  for (int e = lane; e < NB * NB; e += WAVE) {
-    const int r = e / NB, c = e % NB;
-    Lk[r][c] = c <= r ? dbase[(int64_t)r * ld + c] : 0.0;
-  }
-  wave_lds_fence();
-  if (lane < NB) idg[lane] = 1.0 / Lk[lane][lane];
-  wave_lds_fence();
-  const int64_t row = (int64_t)(k + 1) * NB + (int64_t)blockIdx.x * WAVE + lane;
-  const bool valid = row < ld;
-  double x[NB];
-  double* rp = A + row * ld + (int64_t)k * NB;
-#pragma unroll
-  for (int j = 0; j < NB; ++j) x[j] = valid ? rp[j] : 0.0;
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    x[j] *= idg[j];
-#pragma unroll
-    for (int m = j + 1; m < NB; ++m) x[m] -= x[j] * Lk[m][j];
-  }
-  bool nz = false;
-  if (valid) {
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      rp[j] = x[j];
-      nz |= (x[j] != 0.0);
-    }
-  }
-  const unsigned long long bal = __ballot(nz);
-  const int tile0 = (int)(((int64_t)(k + 1) * NB + (int64_t)blockIdx.x * WAVE) / NB);
-  const int ntiles = (int)(ld / NB);
-  if (lane == 0 && tile0 < ntiles) tile_nz[tile0] = (bal & 0xffffffffull) != 0;
-  if (lane == 32 && tile0 + 1 < ntiles) tile_nz[tile0 + 1] = (bal >> 32) != 0;
-}
-
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_chol_update(double* __restrict__ A, int64_t ld, int k,
-                                                     const int* __restrict__ tile_nz) {
-  const int i = k + 1 + blockIdx.x;
-  const int j = k + 1 + blockIdx.y;
-  if (j > i) return;
-  if (!tile_nz[i] || !tile_nz[j]) return;
-  __shared__ double Li[NB][NB + 1];
-  __shared__ double Lj[NB][NB + 1];
-  const double* pi = A + (int64_t)i * NB * ld + (int64_t)k * NB;
-  const double* pj = A + (int64_t)j * NB * ld + (int64_t)k * NB;
-  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-    const int r = e / NB, c = e % NB;
-    Li[r][c] = pi[(int64_t)r * ld + c];
-    Lj[r][c] = pj[(int64_t)r * ld + c];
-  }
-  __syncthreads();
+// C -= A B^T for 32x32 tiles in LDS (256 threads: 32 rows x 8 groups of 4 columns)
+__device__ __forceinline__ void tile_gemm_nt_sub(double (*C)[NB + 1], double (*A)[NB + 1], double (*B)[NB + 1]) {
   const int rr = threadIdx.x >> 3;
   const int cc = (threadIdx.x & 7) * 4;
   double acc[4] = {0, 0, 0, 0};
 #pragma unroll 8
   for (int m = 0; m < NB; ++m) {
-    const double a = Li[rr][m];
+    const double x = A[rr][m];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] += a * Lj[cc + q][m];
+    for (int q = 0; q < 4; ++q) acc[q] += x * B[cc + q][m];
   }
-  double* C = A + ((int64_t)i * NB + rr) * ld + (int64_t)j * NB + cc;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) C[q] -= acc[q];
+  for (int q = 0; q < 4; ++q) C[rr][cc + q] -= acc[q];
 }
 
-void launch_cholesky(double* A, int64_t ld, int* info, int* tile_nz, hipStream_t st) {
+// One wave factors the 32x32 SPD tile D (LDS) in place into its lower Cholesky factor; rdg[j] = 1/L_jj.
+// Lane i keeps row i in registers; the pivot column is broadcast with v_readlane (no LDS round trips,
+// no spills): right-looking on the unscaled pivot column, row_i[m] -= (A_ij / A_jj) A_mj, and at the
+// end L_ij = A_ij / sqrt(A_jj).
+__device__ __forceinline__ void wave_potrf32(double (*D)[NB + 1], double* rdg, int* info) {
+  const int lane = lane_id();
+  const int i = lane & (NB - 1);
+  double row[NB], dg[NB];
+#pragma unroll
+  for (int m = 0; m < NB; ++m) row[m] = D[i][m];
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    double d = bcast(row[j], j);
+    if (!(d > 0.0)) {
+      bad = true;
+      d = 1e-300;
+    }
+    const double li = row[j] * (1.0 / d);
+#pragma unroll
+    for (int m = j + 1; m < NB; ++m) row[m] -= li * bcast(row[j], m);
+    dg[j] = d;
+  }
+  if (bad && lane == 0) atomicOr(info, 1);
+  if (lane < NB) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const double r = 1.0 / sqrt(dg[j]);
+      D[i][j] = (j <= i) ? row[j] * r : 0.0;
+      if (lane == j) rdg[j] = r;
+    }
+  }
+  wave_lds_fence();
+}
+
+__global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64_t ld, int k,
+                                                   const int* __restrict__ tasks, const int* __restrict__ colfirst,
+                                                   double* __restrict__ Ldiag, int* info) {
+  __shared__ double sC[NB][NB + 1];  // target tile (panel T_ik / trailing A_ij)
+  __shared__ double sD[NB][NB + 1];  // diagonal tile -> L_kk
+  __shared__ double sA[NB][NB + 1];  // L_{i,k-1}
+  __shared__ double sB[NB][NB + 1];  // L_{k,k-1} or L_{j,k-1}
+  __shared__ double rdg[NB];
+  const int task = tasks[blockIdx.x];
+  const int type = task >> 30;
+  const int i = (task >> 15) & 0x7fff;
+  const int j = task & 0x7fff;
+  const int64_t NBl = NB;
+#ifndef CHOL_VARIANT
+#define CHOL_VARIANT 0
+#endif
+  if (type == 1) {
+#if CHOL_VARIANT == 3
+    return;
+#endif
+    // trailing: A_ij -= L_{i,k-1} L_{j,k-1}^T
+    double* C = A + i * NBl * ld + j * NBl;
+    load_tile(sC, C, ld);
+    load_tile(sA, A + i * NBl * ld + (k - 1) * NBl, ld);
+    load_tile(sB, A + j * NBl * ld + (k - 1) * NBl, ld);
+    __syncthreads();
+    tile_gemm_nt_sub(sC, sA, sB);
+    __syncthreads();
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) C[(int64_t)(e >> 5) * ld + (e & 31)] = sC[e >> 5][e & 31];
+    return;
+  }
+  // panel task (i, k)
+  const bool diag_only = (i == k);
+  const bool upd_k = (k > 0) && colfirst[k] <= k - 1;
+  const bool upd_i = (k > 0) && colfirst[i] <= k - 1;
+  load_tile(sD, A + (int64_t)k * NBl * ld + k * NBl, ld);
+  if (!diag_only) load_tile(sC, A + i * NBl * ld + k * NBl, ld);
+  if (upd_k) load_tile(sB, A + (int64_t)k * NBl * ld + (k - 1) * NBl, ld);
+  if (upd_i && !diag_only) load_tile(sA, A + i * NBl * ld + (k - 1) * NBl, ld);
+  __syncthreads();
+  if (upd_k) tile_gemm_nt_sub(sD, sB, sB);
+  if (upd_k && upd_i && !diag_only) tile_gemm_nt_sub(sC, sA, sB);
+  __syncthreads();
+#if CHOL_VARIANT != 1
+  if (threadIdx.x < WAVE) wave_potrf32(sD, rdg, info);
+#else
+  if (threadIdx.x < NB) rdg[threadIdx.x] = 1.0;
+#endif
+  __syncthreads();
+  if (diag_only) {
+    // A_kk itself stays untouched: other panel workgroups of this launch are still reading it
+    double* C = Ldiag + (int64_t)k * NB * NB;
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) C[e] = sD[e >> 5][e & 31];
+    return;
+  }
+  // L_ik = T_ik L_kk^-T : lane r solves row r
+  if (threadIdx.x < NB && CHOL_VARIANT != 2) {
+    const int r = threadIdx.x;
+    double x[NB];
+#pragma unroll
+    for (int m = 0; m < NB; ++m) x[m] = sC[r][m];
+#pragma unroll
+    for (int jj = 0; jj < NB; ++jj) {
+      x[jj] *= rdg[jj];
+#pragma unroll
+      for (int m = jj + 1; m < NB; ++m) x[m] -= x[jj] * sD[m][jj];
+      __builtin_amdgcn_sched_barrier(0);  // keep each step's LDS reads in the step (no hoisting -> no spills)
+    }
+#pragma unroll
+    for (int m = 0; m < NB; ++m) sC[r][m] = x[m];
+  }
+  __syncthreads();
+  double* C = A + i * NBl * ld + k * NBl;
+  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) C[(int64_t)(e >> 5) * ld + (e & 31)] = sC[e >> 5][e & 31];
+}
+
+void launch_cholesky(double* A, int64_t ld, const int* tasks, const int* task_off_host, const int* colfirst,
+                     double* Ldiag, int* info, hipStream_t st) {
   const int T = (int)(ld / NB);
   for (int k = 0; k < T; ++k) {
-    hipLaunchKernelGGL(k_chol_diag, dim3(1), dim3(64), 0, st, A, ld, k, info);
-    if (k + 1 < T) {
-      const int rows = (T - k - 1) * NB;
-      hipLaunchKernelGGL(k_chol_panel, dim3((rows + WAVE - 1) / WAVE), dim3(64), 0, st, A, ld, k, tile_nz);
-      hipLaunchKernelGGL(k_chol_update, dim3(T - k - 1, T - k - 1), dim3(256), 0, st, A, ld, k, tile_nz);
-    }
+    const int n = task_off_host[k + 1] - task_off_host[k];
+    if (n > 0)
+      hipLaunchKernelGGL(k_chol_step, dim3(n), dim3(256), 0, st, A, ld, k, tasks + task_off_host[k], colfirst, Ldiag,
+                         info);
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// one workgroup: forward L y = b, then backward L^T x = y (b overwritten); y lives in LDS
-__global__ __launch_bounds__(1024) void k_chol_solve(const double* __restrict__ L, int64_t ld, double* __restrict__ b) {
-  extern __shared__ __attribute__((aligned(16))) double yv[];
+// back substitution L^T x = y with y = row n of the factor; x written to xout[0..n)
+__global__ __launch_bounds__(1024) void k_chol_backsolve(const double* __restrict__ L, int64_t ld, int n,
+                                                         const int* __restrict__ rowend,
+                                                         const double* __restrict__ Ldiag, double* __restrict__ xout) {
+  extern __shared__ __attribute__((aligned(16))) double xv[];  // [ld]
+  __shared__ double part[32][NB + 1];
+  __shared__ double Lkk[NB][NB + 1];
   const int t = threadIdx.x;
-  const int T = (int)(ld / NB);
-  for (int i = t; i < ld; i += blockDim.x) yv[i] = b[i];
+  const int c = t & 31, sub = t >> 5;
+  const int Tn = (n + NB - 1) / NB;
+  // y = row n of the factor: off-diagonal tiles in place, the last partial tile in Ldiag
+  const int tn = n / NB, rn = n - tn * NB;
+  for (int i = t; i < ld; i += blockDim.x)
+    xv[i] = (i >= n) ? 0.0 : (i < tn * NB ? L[(int64_t)n * ld + i] : Ldiag[((int64_t)tn * NB + rn) * NB + (i - tn * NB)]);
   __syncthreads();
-  const int r = t >> 5, sub = t & 31;  // 32 rows x 32 partial lanes
-  // forward
-  for (int kt = 0; kt < T; ++kt) {
-    const int64_t row = (int64_t)kt * NB + r;
+  for (int kt = Tn - 1; kt >= 0; --kt) {
+    const int64_t c0 = (int64_t)kt * NB;
+    // stage L_kk and the envelope-limited column-block dot products
+    Lkk[t >> 5][t & 31] = Ldiag[(int64_t)kt * NB * NB + t];
     double s = 0;
-    const double* lp = L + row * ld;
-    for (int c = sub; c < kt * NB; c += 32) s += lp[c] * yv[c];
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 32);
-    if (sub == 0) yv[row] -= s;
+    const int r1 = min(rowend[kt], n);
+#pragma unroll 4
+    for (int i = (int)c0 + NB + sub; i < r1; i += 32) s += L[(int64_t)i * ld + c0 + c] * xv[i];
+    part[sub][c] = s;
     __syncthreads();
     if (t < WAVE) {
-      const int rl = t & (NB - 1);
-      const double* dl = L + (int64_t)kt * NB * ld + (int64_t)kt * NB;
-      for (int j = 0; j < NB; ++j) {
-        if (t == j) yv[kt * NB + j] /= dl[(int64_t)j * ld + j];
-        wave_lds_fence();
-        if (t < NB && rl > j) yv[kt * NB + rl] -= dl[(int64_t)rl * ld + j] * yv[kt * NB + j];
-        wave_lds_fence();
+      const int lane = t;
+      double tr = 0;
+      if (lane < NB) {
+        for (int q = 0; q < 32; ++q) tr += part[q][lane];
+        tr = xv[c0 + lane] - tr;
       }
+      // upper-triangular solve L_kk^T x = tr, lane r holds tr_r
+      const double rd = lane < NB ? 1.0 / Lkk[lane][lane] : 0.0;
+#pragma unroll
+      for (int jj = NB - 1; jj >= 0; --jj) {
+        const double tj = bcast(tr, jj) * bcast(rd, jj);
+        if (lane == jj) tr = tj;
+        if (lane < jj) tr -= Lkk[jj][lane] * tj;
+      }
+      if (lane < NB && c0 + lane < n) xv[c0 + lane] = tr;
     }
     __syncthreads();
   }
-  // backward: x_kt = L_kk^-T (y_kt - sum_{i>kt} L_{i,kt}^T x_i)
-  for (int kt = T - 1; kt >= 0; --kt) {
-    const int c = r;
-    double s = 0;
-    for (int64_t i = (int64_t)(kt + 1) * NB + sub; i < ld; i += 32) s += L[i * ld + (int64_t)kt * NB + c] * yv[i];
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 32);
-    if (sub == 0) yv[kt * NB + c] -= s;
-    __syncthreads();
-    if (t < WAVE) {
-      const double* dl = L + (int64_t)kt * NB * ld + (int64_t)kt * NB;
-      for (int j = NB - 1; j >= 0; --j) {
-        if (t == j) yv[kt * NB + j] /= dl[(int64_t)j * ld + j];
-        wave_lds_fence();
-        if (t < j) yv[kt * NB + t] -= dl[(int64_t)j * ld + t] * yv[kt * NB + j];
-        wave_lds_fence();
-      }
-    }
-    __syncthreads();
-  }
-  for (int i = t; i < ld; i += blockDim.x) b[i] = yv[i];
+  for (int i = t; i < n; i += blockDim.x) xout[i] = xv[i];
 }
 
-void launch_chol_solve(const double* L, int64_t ld, double* b, hipStream_t st) {
-  hipLaunchKernelGGL(k_chol_solve, dim3(1), dim3(1024), (size_t)ld * sizeof(double), st, L, ld, b);
+void launch_chol_backsolve(const double* L, int64_t ld, int n, const int* rowend, const double* Ldiag, double* xout,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(1024), (size_t)ld * sizeof(double), st, L, ld, n, rowend, Ldiag,
+                     xout);
 }
 
 }  // namespace ptzba

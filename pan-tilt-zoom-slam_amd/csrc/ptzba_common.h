@@ -128,3 +128,13 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+
+// an int carried in a real-typed slot (bit pattern; the low word for double)
+template <typename real>
+__device__ __forceinline__ real __int_as_real(int i);
+template <>
+__device__ __forceinline__ float __int_as_real<float>(int i) { return __int_as_float(i); }
+template <>
+__device__ __forceinline__ double __int_as_real<double>(int i) { return __longlong_as_double((long long)i); }
+__device__ __forceinline__ int __real_as_int(float x) { return __float_as_int(x); }
+__device__ __forceinline__ int __real_as_int(double x) { return (int)__double_as_longlong(x); }

@@ -16,8 +16,12 @@ struct LinArgs {
   const void* rec_w;             // [n_rec] real or nullptr
   const void* ft;                // FrameTab<real>[n_pose]
   const void* rt;                // RayTab<real>[n_lm]
+  const void* ft64;              // FrameTab<double>[n_pose]
+  const void* rt64;              // RayTab<double>[n_lm]
+  const double2* seg_base;       // [n_seg] base observation; records hold obs - base (real)
   double u, v, fs2, inv_fs2;
   void* seg_out;                 // [n_seg][16] real
+  void* seg_w;                   // [n_seg][8] real: W (6) | frame id bits | 0
   double* lm_out;                // [n_lm][8]
 };
 
@@ -29,6 +33,7 @@ struct SchurArgs {
   const int32_t* seg_frame;        // [n_seg]
   const int32_t* lm_seg_begin;     // [n_lm+1]
   const void* seg_out;             // [n_seg][16] real
+  const void* seg_w;               // [n_seg][8] real compact W + frame
   const double* lm_aux;            // [n_lm][8]
   double* S;                       // [ld][ld] lower, row-major
   double* b;                       // [n_sys]
@@ -55,7 +60,8 @@ struct BacksubArgs {
 };
 
 template <typename real>
-void launch_tables(const double* ptz, const double* rays, int n_pose, int n_lm, void* ft, void* rt, hipStream_t st);
+void launch_tables(const double* ptz, const double* rays, int n_pose, int n_lm, void* ft64, void* rt64, void* ft, void* rt,
+                   hipStream_t st);
 template <typename real>
 void launch_linearize(const LinArgs& a, int loss, hipStream_t st);
 void launch_landmark_damp(const double* lm_out, const int32_t* lm_seg_begin, double* D_ray, double* lm_aux, int n_lm,
@@ -70,17 +76,20 @@ void launch_pose_trial(const double* ptz, const double* dpose, const double* g_p
                        double* ptz_trial, int n_pose, int n_fixed, double lambda, double* out4, hipStream_t st);
 void launch_reduce_cols(const double* src, int64_t n, int stride, int nk, int maxmask, double* out, hipStream_t st);
 template <typename real>
-void launch_residual(const int32_t* rec_seg, const int32_t* seg_frame, const int32_t* seg_lm, const void* rec_xy,
-                     const int64_t* perm, const void* ft, const void* rt, double u, double v, int64_t n_rec,
-                     double* r_out, hipStream_t st);
+void launch_residual(const int32_t* rec_seg, const int32_t* seg_frame, const int32_t* seg_lm, const double2* seg_base,
+                     const void* rec_xy, const int64_t* perm, const void* ft64, const void* rt64, double u, double v,
+                     int64_t n_rec, double* r_out, hipStream_t st);
 
 // dense SPD solve of the reduced camera system (chol_kernels.hip)
-// A: [ld][ld] row-major fp64, lower triangle of an SPD matrix whose rows >= n are identity padding;
-// factor in place (L), then x = A^-1 b (b overwritten by x).  info[0] != 0 if not positive definite.
+// A: [ld][ld] row-major fp64, lower triangle of S (n x n), ld = roundup(n + 1, CHOL_NB).
+// prepare: row n <- b^T (augmented), A[n][n] huge, identity padding.  cholesky: one launch per tile
+// column over the host-built envelope task lists.  backsolve: x = S^-1 b into xout.
 constexpr int CHOL_NB = 32;
 void launch_chol_prepare(double* A, int64_t ld, int n, double* b, int* info, hipStream_t st);
-void launch_cholesky(double* A, int64_t ld, int* info, int* tile_nz, hipStream_t st);
-void launch_chol_solve(const double* L, int64_t ld, double* b, hipStream_t st);
+void launch_cholesky(double* A, int64_t ld, const int* tasks, const int* task_off_host, const int* colfirst,
+                     double* Ldiag, int* info, hipStream_t st);
+void launch_chol_backsolve(const double* L, int64_t ld, int n, const int* rowend, const double* Ldiag, double* xout,
+                           hipStream_t st);
 
 // camera batch kernels (camera_kernels.hip)
 void launch_ray_to_image(int64_t n, double u, double v, const double* f, const double* cp, const double* ct,

@@ -1,0 +1,74 @@
+"""
+KeyFrame record (reference: slam_system/key_frame.py:13-107) — same fields and .mat export.
+
+`feature_pts` holds keypoint objects with `.pt` (as cv2 returns) or an [N,2] array after
+convert_keypoint_to_array(); `landmark_index` is the int32 global ray id of each feature.
+"""
+import numpy as np
+import scipy.io as sio
+
+
+def rotation_matrix_to_vector(R):
+    """Rodrigues vector of a rotation matrix (stands in for cv.Rodrigues used at key_frame.py:97)."""
+    R = np.asarray(R, np.float64)
+    c = (np.trace(R) - 1.0) / 2.0
+    c = min(1.0, max(-1.0, c))
+    th = np.arccos(c)
+    if th < 1e-12:
+        return np.zeros(3)
+    if np.pi - th < 1e-6:
+        # axis from the symmetric part
+        M = (R + np.eye(3)) / 2.0
+        k = int(np.argmax(np.diag(M)))
+        ax = M[:, k] / np.sqrt(M[k, k])
+        return ax * th
+    ax = np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]]) / (2.0 * np.sin(th))
+    return ax * th
+
+
+class KeyFrame:
+    """A keyframe of the map (key_frame.py:16-51)."""
+
+    def __init__(self, img, img_index, center, rotation, u, v, pan, tilt, f):
+        self.img = img
+        self.img_index = img_index
+        self.feature_pts = np.ndarray(0)
+        self.feature_des = np.ndarray(0)
+        self.landmark_index = []
+        self.pan, self.tilt, self.f = pan, tilt, f
+        self.center = center
+        self.base_rotation = rotation
+        self.u = u
+        self.v = v
+
+    def get_feature_num(self):
+        return len(self.feature_pts)
+
+    def convert_keypoint_to_array(self, norm=True):
+        """key_frame.py:59-73."""
+        n = len(self.feature_pts)
+        pts = np.zeros((n, 2), dtype=np.float64)
+        for i in range(n):
+            p = self.feature_pts[i]
+            pts[i] = p.pt if hasattr(p, "pt") else p
+        des = np.asarray(self.feature_des, dtype=np.float64)
+        if norm and len(des):
+            des = des / np.linalg.norm(des, axis=1).reshape(-1, 1)
+        self.feature_pts = pts
+        self.feature_des = des
+
+    def save_to_mat(self, path):
+        """key_frame.py:75-107: keys im_name, keypoint, descriptor, camera (9x1), ptz (3x1)."""
+        if isinstance(self.feature_pts, list):
+            self.convert_keypoint_to_array()
+        br = np.asarray(self.base_rotation)
+        save_br = rotation_matrix_to_vector(br) if br.shape == (3, 3) else br.ravel()
+        data = {
+            "im_name": str(self.img_index) + ".jpg",
+            "keypoint": self.feature_pts,
+            "descriptor": self.feature_des,
+            "camera": np.array([self.u, self.v, self.f, save_br[0], save_br[1], save_br[2], self.center[0],
+                                self.center[1], self.center[2]]).reshape(-1, 1),
+            "ptz": np.array([self.pan, self.tilt, self.f]).reshape(-1, 1),
+        }
+        sio.savemat(path, mdict=data)

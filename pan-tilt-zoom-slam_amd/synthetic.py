@@ -265,3 +265,47 @@ def _selftest():
 
 if __name__ == "__main__":
     _selftest()
+
+
+class SyntheticFrontEnd:
+    """Correspondence source for the reference's front-end hooks (image_process.detect_compute_sift /
+    match_sift_features): 'images' are frame ids of a Scene, descriptors carry the frame id, matches are
+    the ground-truth shared rays (optionally with `corrupt` swapped matches per pair).  Stands in for
+    OpenCV SIFT + BF matching, the same way the golden-fixture generator drives the reference."""
+
+    def __init__(self, scene, corrupt=0, seed=0):
+        self.scene = scene
+        self.corrupt = corrupt
+        self.rng = np.random.default_rng(seed)
+
+    def detect(self, im, nfeatures=0, verbose=False):
+        import image_process
+        i = int(im)
+        kps = [image_process.KeyPoint(x, y) for x, y in self.scene.kp_xy[i]]
+        des = np.full((len(kps), 128), i, dtype=np.float32)
+        if len(kps):
+            des[:, 1] = np.arange(len(kps))
+        return kps, des
+
+    def match(self, kp1, des1, kp2, des2, pts_array=False, verbose=False):
+        i = int(des1[0, 0])
+        j = int(des2[0, 0])
+        r1, r2 = self.scene.kp_ray[i], self.scene.kp_ray[j]
+        pos2 = np.full(len(self.scene.gt_rays), -1, np.int64)
+        pos2[r2] = np.arange(len(r2))
+        p = pos2[r1]
+        idx1 = [int(a) for a in np.flatnonzero(p >= 0)]
+        idx2 = [int(b) for b in p[p >= 0]]
+        if self.corrupt and len(idx2) > 4:
+            for _ in range(self.corrupt):
+                a, b = self.rng.choice(len(idx2), 2, replace=False)
+                idx2[a], idx2[b] = idx2[b], idx2[a]
+        pts1 = np.array([kp1[a].pt for a in idx1]).reshape(-1, 2)
+        pts2 = np.array([kp2[b].pt for b in idx2]).reshape(-1, 2)
+        return pts1, idx1, pts2, idx2
+
+    def install(self):
+        import image_process
+        image_process.detect_compute_sift = self.detect
+        image_process.match_sift_features = self.match
+        return self
