@@ -356,8 +356,12 @@ __global__ __launch_bounds__(1024) void k_schur(SchurArgs a) {
       for (int j2 = 0; j2 < n; j2 += 2) {
         const int j = min(j2 + half, n - 1);
         const bool vj = (j2 + half) < n;
+        // every shuffle runs with the full wave active: a ds_bpermute issued under divergence reads 0
+        // from source lanes that are switched off (the upper half on an odd tail), which used to drop
+        // the chunk's last segment whenever it sat in lanes 32..63.
         const int s1j = __shfl(s1, j, WAVE);
-        const int sendj = vj ? __shfl(send, j, WAVE) : 0;
+        const int sendraw = __shfl(send, j, WAVE);
+        const int sendj = vj ? sendraw : 0;
         double Yj[3][2];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {

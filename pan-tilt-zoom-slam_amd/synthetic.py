@@ -42,7 +42,7 @@ def _project(u, v, f, pan, tilt, theta, phi):
     a = np.radians(pan); b = np.radians(tilt)
     th = np.radians(theta); ph = np.radians(phi)
     p0 = np.tan(th)
-    p1 = -np.tan(ph) / np.cos(th)
+    p1 = -np.tan(ph) * np.sqrt(p0 * p0 + 1.0)  # sqrt(tan^2+1), not sec: ptz_camera.py:205 semantics
     ca, sa, cb, sb = np.cos(a), np.sin(a), np.cos(b), np.sin(b)
     w0 = ca * p0 - sa
     w2 = sa * p0 + ca

@@ -158,3 +158,136 @@ def test_residual_matches_oracle_config2(gpu_available):
     np.testing.assert_allclose(r, r_o, rtol=0, atol=1e-8)
     np.testing.assert_allclose(r[d["r_ref_sample_idx"]], d["r_ref_sample"], rtol=0, atol=1e-8)
     assert abs(float(np.sum(r * r)) - float(d["r_ref_sumsq"])) <= 1e-9 * float(d["r_ref_sumsq"])
+
+
+def _install_fixture_frontend(d):
+    """Front-end hooks replaying the fixture's detector/matcher output (what the reference saw)."""
+    import image_process
+    off = d["points_off"]
+    n = len(off) - 1
+    pts = [d["points"][off[i]:off[i + 1]] for i in range(n)]
+    raw = {}
+    o = 0
+    for i, j, c in zip(d["raw_pi"], d["raw_pj"], d["raw_cnt"]):
+        raw[(int(i), int(j))] = (list(d["raw_a"][o:o + c]), list(d["raw_b"][o:o + c]))
+        o += c
+    kp_store = {}
+
+    def detect(im, nfeatures, verbose=False):
+        i = int(im)
+        kps = [image_process.KeyPoint(x, y) for x, y in pts[i]]
+        kp_store[i] = kps
+        des = np.full((len(kps), 128), i, np.float32)
+        des[:, 1] = np.arange(len(kps))
+        return kps, des
+
+    def match(kp1, des1, kp2, des2, pts_array=False, verbose=False):
+        a, b = raw[(int(des1[0, 0]), int(des2[0, 0]))]
+        return None, list(a), None, list(b)
+
+    saved = (image_process.detect_compute_sift, image_process.match_sift_features)
+    image_process.detect_compute_sift, image_process.match_sift_features = detect, match
+    return saved, kp_store
+
+
+@pytest.mark.parametrize("name", ["ba_6x120", "ba_10x200"])
+def test_dropin_bundle_adjustment_matches_reference(gpu_available, name):
+    """bundle_adjustment() drop-in on the reference's own inputs: landmark ids, keyframe feature order
+    (set() order) bit-exact; poses/rays at the reference's tight optimum (1e-6 deg, 1e-4 px)."""
+    import random
+    import image_process
+    import bundle_adjustment as ba
+    d = golden(name + ".npz")
+    n = int(d["n_pose"])
+    saved, kp_store = _install_fixture_frontend(d)
+    try:
+        random.seed(int(d["seed"]))
+        landmarks, keyframes = ba.bundle_adjustment(list(range(n)), list(range(100, 100 + n)), "sift",
+                                                    d["init_ptz"].copy(), np.array([0.0, -10.0, 5.0]), np.eye(3),
+                                                    float(d["u"]), float(d["v"]), "", ftol=1e-14, xtol=1e-14,
+                                                    max_iter=200)
+    finally:
+        image_process.detect_compute_sift, image_process.match_sift_features = saved
+    assert landmarks.shape == (int(d["n_landmark"]), 2)
+    off = d["kf_off"]
+    for i, kf in enumerate(keyframes):
+        np.testing.assert_array_equal(kf.landmark_index.astype(np.int64), d["kf_lmk"][off[i]:off[i + 1]])
+        pos = {id(o): k for k, o in enumerate(kp_store[i])}
+        np.testing.assert_array_equal([pos[id(o)] for o in kf.feature_pts], d["kf_local"][off[i]:off[i + 1]])
+        assert kf.img_index == 100 + i
+    assert int(ba.LAST_RESULT["n_residual"]) == int(d["n_residual"])
+    np.testing.assert_allclose(ba.LAST_RESULT["x0"], d["x0"], rtol=0, atol=1e-9)
+    xt = d["x_tight"]
+    ptz = np.array([[k.pan, k.tilt, k.f] for k in keyframes])
+    ptz_t = np.concatenate([d["ref_pose"], xt[:3 * (n - 1)]]).reshape(-1, 3)
+    np.testing.assert_allclose(ptz[:, :2], ptz_t[:, :2], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(ptz[:, 2], ptz_t[:, 2], rtol=0, atol=1e-4)
+    np.testing.assert_allclose(landmarks.reshape(-1), xt[3 * (n - 1):], rtol=0, atol=1e-6)
+
+
+def test_compute_residual_dropin_signature(gpu_available):
+    """bundle_adjustment._compute_residual keeps the reference signature and output."""
+    import bundle_adjustment as ba
+    from test_oracle_golden import _lists_from_flat
+    d = golden("ba_10x200.npz")
+    n, m = int(d["n_pose"]), int(d["n_landmark"])
+    src, dst, lmk = _lists_from_flat(n, d["m_i"], d["m_j"], d["m_k1"], d["m_k2"], d["m_lm"])
+    off = d["points_off"]
+    pts = [d["points"][off[i]:off[i + 1]] for i in range(n)]
+    for x, r_ref in zip(d["xs"][:2], d["rs"][:2]):
+        r = ba._compute_residual(x, n, m, int(d["n_residual"]), pts, src, dst, lmk, float(d["u"]), float(d["v"]),
+                                 d["ref_pose"])
+        np.testing.assert_allclose(r, r_ref, rtol=0, atol=1e-8)
+
+
+@pytest.mark.parametrize("cfg", ["config1", "config2"])
+@pytest.mark.parametrize("precision", [0, 1])
+def test_single_gauss_newton_step_is_exact(gpu_available, precision, cfg):
+    """One undamped step (lambda = 0) == the exact solution of J^T J dx = -J^T r with the oracle's
+    analytic Jacobian (sparse normal equations), i.e. linearisation + Schur + Cholesky +
+    back-substitution are exact.  config2 spans five 32x32 Cholesky tiles and >32 segments per
+    Schur wave chunk (the multi-tile / odd-tail paths config1 never reaches).
+    Tolerance: fp64 1e-7 relative to |dx|; fp32 2e-3 relative (fp32 normal-equation blocks)."""
+    import scipy.sparse.linalg as spla
+    import ptzba
+    import synthetic
+    from oracle import ptz_oracle as orc
+    p = synthetic.make_problem(cfg, seed=0)
+    h = ptzba.BAHandle(0)
+    h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=precision)
+    h.set_state(p.init_ptz, p.init_rays)
+    h.linearize()
+    h.build_reduced(0.0)
+    h.solve_reduced()
+    s = h.read_scalars()
+    assert s[5] == 0
+    h.accept(True)
+    ptz1, rays1 = h.get_state()
+    h.close()
+    dx_gpu = np.concatenate([(ptz1 - p.init_ptz)[1:].reshape(-1), (rays1 - p.init_rays).reshape(-1)])
+    x0 = np.concatenate([p.init_ptz[1:].reshape(-1), p.init_rays.reshape(-1)])
+    fr, lm = p.frame.astype(np.int64), p.landmark.astype(np.int64)
+    J = orc.ba_jacobian(x0, p.n_pose, p.n_landmark, p.u, p.v, p.init_ptz[0], fr, lm).tocsc()
+    r = orc.compute_residual_records(np.concatenate([p.init_ptz[0], x0]), p.n_pose, p.u, p.v, fr, lm, p.xy)
+    dx = spla.spsolve((J.T @ J).tocsc(), -(J.T @ r))
+    tol = 1e-7 if precision == 0 else 2e-3
+    err = np.abs(dx_gpu - dx).max() / np.abs(dx).max()
+    assert err < tol, err
+
+
+@pytest.mark.gpu
+def test_analytic_jacobian_matches_fd_cpu():
+    """CPU check of the Appendix-A Jacobian used by K1 (oracle mirror) against central FD."""
+    import synthetic
+    from oracle import ptz_oracle as orc
+    p = synthetic.make_problem("config1", seed=0)
+    x0 = np.concatenate([p.init_ptz[1:].reshape(-1), p.init_rays.reshape(-1)])
+    fr, lm = p.frame.astype(np.int64), p.landmark.astype(np.int64)
+    J = orc.ba_jacobian(x0, p.n_pose, p.n_landmark, p.u, p.v, p.init_ptz[0], fr, lm).toarray()
+    f = lambda x: orc.compute_residual_records(np.concatenate([p.init_ptz[0], x]), p.n_pose, p.u, p.v, fr, lm, p.xy)
+    rng = np.random.default_rng(0)
+    for c in rng.choice(len(x0), 40, replace=False):
+        e = np.zeros_like(x0)
+        e[c] = 1e-5 if c < 3 * (p.n_pose - 1) and c % 3 != 2 else (1e-3 if c < 3 * (p.n_pose - 1) else 1e-5)
+        fd = (f(x0 + e) - f(x0 - e)) / (2 * e[c])
+        np.testing.assert_allclose(J[:, c], fd, rtol=1e-5, atol=1e-5 * max(1.0, np.abs(fd).max()))

@@ -1,0 +1,136 @@
+"""CPU-side checks of the product: the C-ABI library loads and exports every entry point declared in
+include/ptzba.h, the native bookkeeping (no GPU needed) is bit-exact against the reference's
+fixture, and the host mirror of build_matching_graph reproduces the reference's lists."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, golden
+
+HEADER = os.path.join(ROOT, "include", "ptzba.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    return re.findall(r"PTZBA_EXPORT\s+[\w\s\*]+?\b(\w+)\s*\(", txt)
+
+
+def test_library_exports_every_declared_symbol():
+    import ctypes
+    import ptzba
+    assert os.path.exists(ptzba.LIB_PATH), "build libptzba.so first (make -C pan-tilt-zoom-slam_amd/csrc)"
+    L = ctypes.CDLL(ptzba.LIB_PATH)
+    syms = declared_symbols()
+    assert len(syms) >= 25
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    assert set(syms) == set(ptzba.EXPORTED_SYMBOLS)
+
+
+def test_no_gpu_fails_loudly():
+    """Without a device the handle constructor fails with a message (there is no CPU fallback)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import ptzba
+    with pytest.raises(ptzba.PtzbaError, match="no HIP device"):
+        ptzba.BAHandle(0)
+
+
+def test_native_landmark_ids_bit_exact():
+    """ptzba_build_landmarks (C++) == reference first-seen rule on the matching-graph fixture."""
+    import ptzba
+    from test_oracle_golden import _graph_pairs_reference_order
+    d = golden("matching_graph.npz")
+    n, pairs = _graph_pairs_reference_order(d)
+    off = d["points_off"]
+    kp_count = [int(off[i + 1] - off[i]) for i in range(n)]
+    lms, n_landmark, n_inconsistent = ptzba.build_landmarks(kp_count, pairs)
+    assert n_landmark == int(d["n_landmark"])
+    assert n_inconsistent > 0
+    got = np.concatenate(lms)
+    # the fixture's flat lists are in (i, j) loop order == pair order
+    np.testing.assert_array_equal(got, d["m_lm"])
+
+
+def test_build_matching_graph_host_mirror():
+    """image_process.build_matching_graph with the recorded front-end output == the reference's lists,
+    including the random.shuffle cap (global `random`, seeded) and inconsistent-match handling."""
+    import random
+    import image_process
+    d = golden("matching_graph.npz")
+    off = d["points_off"]
+    n = len(off) - 1
+    pts = [d["points"][off[i]:off[i + 1]] for i in range(n)]
+    raw = {}
+    o = 0
+    for i, j, c in zip(d["raw_pi"], d["raw_pj"], d["raw_cnt"]):
+        raw[(int(i), int(j))] = (list(d["raw_a"][o:o + c]), list(d["raw_b"][o:o + c]))
+        o += c
+
+    def detect(im, nfeatures, verbose=False):
+        i = int(im)
+        kps = [image_process.KeyPoint(x, y) for x, y in pts[i]]
+        des = np.full((len(kps), 128), i, np.float32)
+        return kps, des
+
+    def match(kp1, des1, kp2, des2, pts_array=False, verbose=False):
+        a, b = raw[(int(des1[0, 0]), int(des2[0, 0]))]
+        return None, list(a), None, list(b)
+
+    saved = image_process.detect_compute_sift, image_process.match_sift_features
+    image_process.detect_compute_sift, image_process.match_sift_features = detect, match
+    try:
+        random.seed(int(d["seed"]))
+        kps, des, points, src, dst, lmk, n_landmark = image_process.build_matching_graph(
+            list(range(n)), [list(r) for r in d["mask"]], "sift")
+    finally:
+        image_process.detect_compute_sift, image_process.match_sift_features = saved
+    assert n_landmark == int(d["n_landmark"])
+    from test_oracle_golden import _lists_from_flat
+    s2, d2, l2 = _lists_from_flat(n, d["m_i"], d["m_j"], d["m_k1"], d["m_k2"], d["m_lm"])
+    assert src == s2 and dst == d2 and lmk == l2
+    for i in range(n):
+        np.testing.assert_allclose(points[i], pts[i])
+
+
+def test_keypoints_masking_semantics():
+    import image_process
+    mask = np.zeros((10, 20), np.uint8)
+    mask[2:5, 3:8] = 1
+    pts = np.array([[3.9, 2.1], [8.0, 2.0], [7.99, 4.99], [0.0, 0.0]])
+    np.testing.assert_array_equal(image_process.keypoints_masking(pts, mask), [0, 2])
+    kps = [image_process.KeyPoint(x, y) for x, y in pts]
+    np.testing.assert_array_equal(image_process.keypoints_masking(kps, mask), [0, 2])
+
+
+def test_overlap_and_merge_helpers():
+    import util
+    from oracle import ptz_oracle as orc
+    rng = np.random.default_rng(0)
+    for _ in range(50):
+        a = rng.uniform(1500, 4000, 2)
+        p = rng.uniform(30, 70, 2)
+        assert abs(util.overlap_pan_angle(a[0], p[0], a[1], p[1], 1280) -
+                   float(orc.overlap_pan_angle(a[0], p[0], a[1], p[1], 1280))) < 1e-12
+    i1 = np.sort(rng.choice(100, 40, replace=False))
+    i2 = np.sort(rng.choice(100, 60, replace=False)).astype(np.float64)
+    for x, y in zip(util.get_overlap_index(i1, i2), orc.get_overlap_index(i1, i2)):
+        np.testing.assert_array_equal(x, y)
+
+
+def test_dedup_records_cost_identity():
+    """Weighted de-duplicated records reproduce the pair-form cost exactly."""
+    import synthetic
+    from oracle import ptz_oracle as orc
+    p = synthetic.make_problem("config1", seed=0)
+    f, l, xy, w, inv = synthetic.dedup_records(p.frame, p.landmark, p.xy)
+    x = np.concatenate([p.init_ptz.reshape(-1), p.init_rays.reshape(-1)])
+    r_pair = orc.compute_residual_records(x, p.n_pose, p.u, p.v, p.frame.astype(np.int64), p.landmark.astype(np.int64),
+                                          p.xy)
+    r_d = orc.compute_residual_records(x, p.n_pose, p.u, p.v, f.astype(np.int64), l.astype(np.int64), xy)
+    c_pair = 0.5 * np.sum(r_pair ** 2)
+    c_d = 0.5 * np.sum(np.repeat(w, 2) * r_d ** 2)
+    assert abs(c_pair - c_d) <= 1e-12 * c_pair

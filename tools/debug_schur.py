@@ -1,0 +1,38 @@
+import sys, numpy as np, torch
+sys.path.insert(0, "pan-tilt-zoom-slam_amd"); sys.path.insert(0, ".")
+import ptzba, synthetic
+from oracle import ptz_oracle as orc
+from bench import _DevArray
+p = synthetic.make_problem(sys.argv[1] if len(sys.argv) > 1 else "config2", seed=0)
+fr, lm = p.frame.astype(np.int64), p.landmark.astype(np.int64)
+h = ptzba.BAHandle(0)
+h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=0)
+h.set_state(p.init_ptz, p.init_rays)
+h.linearize(); h.build_reduced(0.0); h.sync()
+sp, n, scp = h.exchange()
+t = torch.as_tensor(_DevArray(sp, n), device="cuda:0").cpu().numpy().copy()
+ns = 3 * (p.n_pose - 1); ld = int(round((-3 + np.sqrt(9 + 4 * n)) / 2))
+assert ld * ld + 3 * ld == n, (ld, n)
+S_gpu = np.tril(t[:ld * ld].reshape(ld, ld))[:ns, :ns]; b_gpu = t[ld * ld: ld * ld + ns]
+x0 = np.concatenate([p.init_ptz[1:].reshape(-1), p.init_rays.reshape(-1)])
+J = orc.ba_jacobian(x0, p.n_pose, p.n_landmark, p.u, p.v, p.init_ptz[0], fr, lm).tocsc()
+r = orc.compute_residual_records(np.concatenate([p.init_ptz[0], x0]), p.n_pose, p.u, p.v, fr, lm, p.xy)
+H = (J.T @ J).toarray(); g = J.T @ r
+Hpp = H[:ns, :ns]; Hpl = H[:ns, ns:]; Hll = H[ns:, ns:]
+Hll_inv = np.zeros_like(Hll)
+for l in range(p.n_landmark):
+    blk = Hll[2*l:2*l+2, 2*l:2*l+2]
+    Hll_inv[2*l:2*l+2, 2*l:2*l+2] = np.linalg.inv(blk)
+S = Hpp - Hpl @ Hll_inv @ Hpl.T
+b = -g[:ns] + Hpl @ Hll_inv @ g[ns:]
+Sl = np.tril(S)
+err = np.abs(S_gpu - Sl)
+print("S rel err max", err.max() / np.abs(Sl).max(), "at", np.unravel_index(err.argmax(), err.shape), "b rel err", np.abs(b_gpu - b).max() / np.abs(b).max())
+bad = np.argwhere(err > 1e-6 * np.abs(Sl).max())
+print("n bad entries", len(bad), bad[:10])
+# solve check
+h.solve_reduced(); h.accept(True); ptz1, _ = h.get_state()
+dp = (ptz1 - p.init_ptz)[1:].reshape(-1)
+dp_exact = np.linalg.solve(S, b)
+dp_from_gpuS = np.linalg.solve(S_gpu + np.tril(S_gpu, -1).T, b_gpu)
+print("dp err vs exact", np.abs(dp - dp_exact).max(), "dp err vs solve(S_gpu)", np.abs(dp - dp_from_gpuS).max(), "|dp|", np.abs(dp_exact).max())
