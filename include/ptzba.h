@@ -142,6 +142,42 @@ PTZBA_EXPORT int ptzba_build_landmarks(int32_t n_frames, const int64_t* kp_count
                                        const int64_t* idx_b, int64_t* landmark_out, int64_t* n_landmark,
                                        int64_t* n_inconsistent);
 
+/* ---------------- EKF tracking state (ptz_slam.py:21-71, 210-315, 376-384, 424-426) ----------------
+ * A handle owns the ray landmarks [R][2] and the dense state covariance [(3+2R)][(3+2R)] (row-major,
+ * order pan, tilt, f, theta_0, phi_0, ...) in device memory; the reference keeps them as the numpy
+ * attributes PtzSlam.rays / PtzSlam.state_cov.  Same ownership rules as ptzba_*: caller-owned host
+ * buffers are copied, device buffers belong to the handle, one HIP stream per handle. */
+typedef struct ptzekf_ctx* ptzekf_handle;
+PTZBA_EXPORT ptzekf_handle ptzekf_new(int device);
+PTZBA_EXPORT void ptzekf_delete(ptzekf_handle h);
+PTZBA_EXPORT int ptzekf_num_rays(ptzekf_handle h);
+/* replaces assignments to PtzSlam.rays / .state_cov (init_system, ptz_slam.py:190-200) */
+PTZBA_EXPORT int ptzekf_set_state(ptzekf_handle h, int32_t n_ray, const double* rays, const double* cov);
+/* reads PtzSlam.rays / .state_cov back; either pointer may be NULL */
+PTZBA_EXPORT int ptzekf_get_state(ptzekf_handle h, double* rays_out, double* cov_out);
+/* predict step of tracking(): state_cov[0:3,0:3] += q (ptz_slam.py:425-426); q row-major 3x3 */
+PTZBA_EXPORT int ptzekf_add_pose_cov(ptzekf_handle h, const double* q9);
+/* PtzSlam.remove_rays (ptz_slam.py:291-315): np.delete semantics (negative indices wrap, duplicates ok) */
+PTZBA_EXPORT int ptzekf_remove_rays(ptzekf_handle h, int64_t n, const int64_t* index);
+/* PtzSlam.add_rays state growth (ptz_slam.py:376-384): append rays, zero rows/cols, var on the diagonal */
+PTZBA_EXPORT int ptzekf_add_rays(ptzekf_handle h, int64_t n, const double* rays, double var);
+/* PTZCamera.project_rays(self.rays, height, width) over the handle's rays (ptz_camera.py:212-234):
+ * points strictly inside the image, in ray order; index_out as float like the reference.
+ * ptz = (pan, tilt, f); xy_out [R][2] and index_out [R] sized for all rays; *count_out = visible. */
+PTZBA_EXPORT int ptzekf_project_visible(ptzekf_handle h, double u, double v, const double* displacement6,
+                                        const double* ptz, int32_t height, int32_t width, double* xy_out,
+                                        double* index_out, int32_t* count_out);
+/* PtzSlam.ekf_update (ptz_slam.py:210-289): predicted camera ptz_inout (pan, tilt, f) is replaced by
+ * the updated one; observed keypoints obs_xy [n_obs][2] with global ray indices obs_index [n_obs]
+ * (matched against the visible predicted rays with the reference's get_overlap_index walk,
+ * util.py:75-97); observe_var = the reference's R = observe_var * I (0.1).  Rays and covariance are
+ * updated in place on the device with the reference's write-back (:281-289).  velocity_out (3) =
+ * K y [0:3] (:273); *n_matched_out = matched rays.  Fails (state untouched) if H P H^T + R is not SPD. */
+PTZBA_EXPORT int ptzekf_update(ptzekf_handle h, double u, double v, const double* displacement6,
+                               double* ptz_inout, int64_t n_obs, const double* obs_xy, const int64_t* obs_index,
+                               int32_t height, int32_t width, double observe_var, double* velocity_out,
+                               int32_t* n_matched_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -16,51 +16,9 @@
 #include "../../include/ptzba.h"
 #include "ptzba_common.h"
 #include "ptzba_kernels.h"
+#include "host_util.h"
 
 using namespace ptzba;
-
-static thread_local std::string g_err;
-
-static int fail(const char* fmt, ...) {
-  char buf[1024];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof(buf), fmt, ap);
-  va_end(ap);
-  g_err = buf;
-  return -1;
-}
-
-#define HIPCHK(expr)                                                                              \
-  do {                                                                                            \
-    hipError_t _e = (expr);                                                                       \
-    if (_e != hipSuccess) return fail("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, __LINE__); \
-  } while (0)
-
-// ------------------------------------------------------------------------------------------------
-struct DBuf {
-  void* p = nullptr;
-  size_t bytes = 0;
-  DBuf() = default;
-  DBuf(const DBuf&) = delete;
-  DBuf& operator=(const DBuf&) = delete;
-  ~DBuf() { release(); }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    bytes = 0;
-  }
-  int alloc(size_t n) {
-    release();
-    if (n == 0) n = 16;
-    hipError_t e = hipMalloc(&p, n);
-    if (e != hipSuccess) return fail("hipMalloc(%zu) failed: %s", n, hipGetErrorString(e));
-    bytes = n;
-    return 0;
-  }
-  template <typename T>
-  T* as() const { return reinterpret_cast<T*>(p); }
-};
 
 static size_t g_total_bytes(std::initializer_list<const DBuf*> l) {
   size_t s = 0;
@@ -129,19 +87,7 @@ const char* ptzba_last_error(void) { return g_err.c_str(); }
 const char* ptzba_version(void) { return "ptzba 0.1 gfx950"; }
 
 ptzba_handle ptzba_new(int device) {
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
-    fail("no HIP device available");
-    return nullptr;
-  }
-  if (device < 0 || device >= n) {
-    fail("device %d out of range (%d devices)", device, n);
-    return nullptr;
-  }
-  if (hipSetDevice(device) != hipSuccess) {
-    fail("hipSetDevice(%d) failed", device);
-    return nullptr;
-  }
+  if (select_device(device)) return nullptr;
   auto* h = new ptzba_ctx();
   h->device = device;
   if (hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess) {

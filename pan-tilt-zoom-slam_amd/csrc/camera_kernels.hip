@@ -8,18 +8,9 @@
 //                    (0.001 deg, 0.1 px) of project_ray, written into the dense [2n, 3+2n] H
 #include "ptzba_common.h"
 #include "ptzba_kernels.h"
+#include "camera_model.h"
 
 namespace ptzba {
-
-__device__ __forceinline__ void rot_tp(double pan, double tilt, double R[3][3]) {
-  double sa, ca, sb, cb;
-  sincos(pan * PTZ_D2R, &sa, &ca);
-  sincos(tilt * PTZ_D2R, &sb, &cb);
-  // R_tilt @ R_pan, ptz_camera.py:73-79
-  R[0][0] = ca;       R[0][1] = 0;   R[0][2] = -sa;
-  R[1][0] = sb * sa;  R[1][1] = cb;  R[1][2] = sb * ca;
-  R[2][0] = cb * sa;  R[2][1] = -sb; R[2][2] = cb * ca;
-}
 
 __global__ void k_ray_to_image(int64_t n, double u, double v, const double* __restrict__ f,
                                const double* __restrict__ cp, const double* __restrict__ ct,
@@ -35,24 +26,6 @@ __global__ void k_ray_to_image(int64_t n, double u, double v, const double* __re
   y[i] = yy;
 }
 
-__device__ __forceinline__ void back_project(double u, double v, double f, double pan, double tilt,
-                                             const double* d6, double x, double y, double& th, double& ph) {
-  double R[3][3];
-  rot_tp(pan, tilt, R);
-  double c[3] = {(x - u) / f, (y - v) / f, 1.0};
-  if (d6) {
-    c[0] -= d6[0] + d6[3] * f;
-    c[1] -= d6[1] + d6[4] * f;
-    c[2] -= d6[2] + d6[5] * f;
-  }
-  // R^-1 = R^T
-  double p0 = R[0][0] * c[0] + R[1][0] * c[1] + R[2][0] * c[2];
-  double p1 = R[0][1] * c[0] + R[1][1] * c[1] + R[2][1] * c[2];
-  double p2 = R[0][2] * c[0] + R[1][2] * c[1] + R[2][2] * c[2];
-  th = atan(p0 / p2) / PTZ_D2R;
-  ph = atan(-p1 / sqrt(p0 * p0 + p2 * p2)) / PTZ_D2R;
-}
-
 __global__ void k_image_to_ray(int64_t n, double u, double v, const double* __restrict__ f,
                                const double* __restrict__ cp, const double* __restrict__ ct,
                                const double* __restrict__ x, const double* __restrict__ y,
@@ -63,26 +36,6 @@ __global__ void k_image_to_ray(int64_t n, double u, double v, const double* __re
   back_project(u, v, f[i], cp[i], ct[i], nullptr, x[i], y[i], a, b);
   th[i] = a;
   ph[i] = b;
-}
-
-struct Disp {
-  double d[6];
-};
-
-__device__ __forceinline__ void project_ray_mat(double u, double v, double f, const double R[3][3], const Disp& D,
-                                                bool has_d, double th, double ph, double& x, double& y) {
-  double t = tan(th * PTZ_D2R);
-  double p[3] = {t, -tan(ph * PTZ_D2R) * sqrt(t * t + 1.0), 1.0};
-  double c[3];
-  for (int r = 0; r < 3; ++r) c[r] = R[r][0] * p[0] + R[r][1] * p[1] + R[r][2] * p[2];
-  if (has_d) {
-    c[0] += D.d[0] + D.d[3] * f;
-    c[1] += D.d[1] + D.d[4] * f;
-    c[2] += D.d[2] + D.d[5] * f;
-  }
-  double w = c[2];
-  x = (f * c[0] + u * w) / w;
-  y = (f * c[1] + v * w) / w;
 }
 
 __global__ void k_project_rays(int64_t n, double u, double v, double f, double pan, double tilt, Disp D, int has_d,
@@ -111,37 +64,14 @@ __global__ void k_h_jacobian(int64_t n, double u, double v, double f, double pan
                              const double* __restrict__ rays, double* __restrict__ H) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const double da = 0.001, dfl = 0.1;
-  const double th = rays[2 * i], ph = rays[2 * i + 1];
+  double h[10];
+  h_fd_block(u, v, f, pan, tilt, D, has_d, rays[2 * i], rays[2 * i + 1], h);
   const int64_t ncol = 3 + 2 * n;
-  double R[3][3], x1, y1, x2, y2;
   double* h0 = H + (2 * i) * ncol;
   double* h1 = H + (2 * i + 1) * ncol;
-  rot_tp(pan - da, tilt, R);
-  project_ray_mat(u, v, f, R, D, has_d, th, ph, x1, y1);
-  rot_tp(pan + da, tilt, R);
-  project_ray_mat(u, v, f, R, D, has_d, th, ph, x2, y2);
-  h0[0] = (x2 - x1) / (2 * da);
-  h1[0] = (y2 - y1) / (2 * da);
-  rot_tp(pan, tilt - da, R);
-  project_ray_mat(u, v, f, R, D, has_d, th, ph, x1, y1);
-  rot_tp(pan, tilt + da, R);
-  project_ray_mat(u, v, f, R, D, has_d, th, ph, x2, y2);
-  h0[1] = (x2 - x1) / (2 * da);
-  h1[1] = (y2 - y1) / (2 * da);
-  rot_tp(pan, tilt, R);
-  project_ray_mat(u, v, f - dfl, R, D, has_d, th, ph, x1, y1);
-  project_ray_mat(u, v, f + dfl, R, D, has_d, th, ph, x2, y2);
-  h0[2] = (x2 - x1) / (2 * dfl);
-  h1[2] = (y2 - y1) / (2 * dfl);
-  project_ray_mat(u, v, f, R, D, has_d, th - da, ph, x1, y1);
-  project_ray_mat(u, v, f, R, D, has_d, th + da, ph, x2, y2);
-  h0[3 + 2 * i] = (x2 - x1) / (2 * da);
-  h1[3 + 2 * i] = (y2 - y1) / (2 * da);
-  project_ray_mat(u, v, f, R, D, has_d, th, ph - da, x1, y1);
-  project_ray_mat(u, v, f, R, D, has_d, th, ph + da, x2, y2);
-  h0[4 + 2 * i] = (x2 - x1) / (2 * da);
-  h1[4 + 2 * i] = (y2 - y1) / (2 * da);
+  for (int q = 0; q < 3; ++q) { h0[q] = h[q]; h1[q] = h[3 + q]; }
+  h0[3 + 2 * i] = h[6]; h0[4 + 2 * i] = h[7];
+  h1[3 + 2 * i] = h[8]; h1[4 + 2 * i] = h[9];
 }
 
 static inline dim3 g1(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }

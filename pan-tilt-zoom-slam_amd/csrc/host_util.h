@@ -1,0 +1,65 @@
+// Host-side helpers shared by the C-ABI translation units: thread-local last-error string, HIP
+// status checks, and an owning device buffer.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+namespace ptzba {
+
+inline thread_local std::string g_err;
+
+inline int fail(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return -1;
+}
+
+#define HIPCHK(expr)                                                                              \
+  do {                                                                                            \
+    hipError_t _e = (expr);                                                                       \
+    if (_e != hipSuccess) return fail("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, __LINE__); \
+  } while (0)
+
+struct DBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DBuf() = default;
+  DBuf(const DBuf&) = delete;
+  DBuf& operator=(const DBuf&) = delete;
+  ~DBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  int alloc(size_t n) {
+    release();
+    if (n == 0) n = 16;
+    hipError_t e = hipMalloc(&p, n);
+    if (e != hipSuccess) return fail("hipMalloc(%zu) failed: %s", n, hipGetErrorString(e));
+    bytes = n;
+    return 0;
+  }
+  // keep the allocation when it is already large enough (contents are not preserved otherwise)
+  int reserve(size_t n) { return n <= bytes && p ? 0 : alloc(n + n / 4); }
+  template <typename T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// Device (hipSetDevice) check shared by the handle constructors.
+inline int select_device(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail("no HIP device available");
+  if (device < 0 || device >= n) return fail("device %d out of range (%d devices)", device, n);
+  if (hipSetDevice(device) != hipSuccess) return fail("hipSetDevice(%d) failed", device);
+  return 0;
+}
+
+}  // namespace ptzba

@@ -78,6 +78,16 @@ def lib():
         "ptz_back_project_rays": ([I, I64, D, D, D, D, D, V, V, V], I),
         "ptz_h_jacobian": ([I, I64, D, D, D, D, D, V, V, V], I),
         "ptzba_build_landmarks": ([I32, V, I64, V, V, V, V, V, V, V, V], I),
+        "ptzekf_new": ([I], V),
+        "ptzekf_delete": ([V], None),
+        "ptzekf_num_rays": ([V], I),
+        "ptzekf_set_state": ([V, I32, V, V], I),
+        "ptzekf_get_state": ([V, V, V], I),
+        "ptzekf_add_pose_cov": ([V, V], I),
+        "ptzekf_remove_rays": ([V, I64, V], I),
+        "ptzekf_add_rays": ([V, I64, V, D], I),
+        "ptzekf_project_visible": ([V, D, D, V, V, I32, I32, V, V, POINTER(c_int32)], I),
+        "ptzekf_update": ([V, D, D, V, V, I64, V, V, I32, I32, D, V, POINTER(c_int32)], I),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(L, name)
@@ -93,6 +103,8 @@ EXPORTED_SYMBOLS = [
     "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_read_scalars", "ptzba_accept",
     "ptzba_exchange", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptz_ray_to_image",
     "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks",
+    "ptzekf_new", "ptzekf_delete", "ptzekf_num_rays", "ptzekf_set_state", "ptzekf_get_state", "ptzekf_add_pose_cov",
+    "ptzekf_remove_rays", "ptzekf_add_rays", "ptzekf_project_visible", "ptzekf_update",
 ]
 
 
@@ -309,6 +321,87 @@ class BAHandle:
 # ---------------------------------------------------------------------------------------------
 # Levenberg-Marquardt driver
 # ---------------------------------------------------------------------------------------------
+class EKFHandle:
+    """Device-resident EKF tracking state (rays [R,2] + covariance [(3+2R)^2]) and its update
+    (include/ptzba.h, ptzekf_*).  Mirrors the state half of PtzSlam (ptz_slam.py:21-71, 210-315)."""
+
+    def __init__(self, device=0):
+        L = lib()
+        self._h = L.ptzekf_new(int(device))
+        if not self._h:
+            raise PtzbaError(f"ptzekf_new: {L.ptzba_last_error().decode()}")
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().ptzekf_delete(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def n_ray(self):
+        return int(lib().ptzekf_num_rays(self._h))
+
+    def set_state(self, rays, cov):
+        rays = _f64(rays).reshape(-1, 2)
+        n = len(rays)
+        cov = _f64(cov)
+        if cov.shape != (3 + 2 * n, 3 + 2 * n):
+            raise ValueError(f"state_cov must be [{3 + 2 * n}, {3 + 2 * n}], got {cov.shape}")
+        _check(lib().ptzekf_set_state(self._h, n, _ptr(rays), _ptr(cov)), "ptzekf_set_state")
+
+    def get_state(self, rays=True, cov=True):
+        n = self.n_ray
+        r = np.empty((n, 2)) if rays else None
+        c = np.empty((3 + 2 * n, 3 + 2 * n)) if cov else None
+        _check(lib().ptzekf_get_state(self._h, _ptr(r), _ptr(c)), "ptzekf_get_state")
+        return r, c
+
+    def add_pose_cov(self, q):
+        q = _f64(q).reshape(3, 3)
+        _check(lib().ptzekf_add_pose_cov(self._h, _ptr(q)), "ptzekf_add_pose_cov")
+
+    def remove_rays(self, index):
+        idx = np.ascontiguousarray(np.asarray(index).reshape(-1), dtype=np.int64)
+        _check(lib().ptzekf_remove_rays(self._h, len(idx), _ptr(idx)), "ptzekf_remove_rays")
+
+    def add_rays(self, rays, var):
+        rays = _f64(rays).reshape(-1, 2)
+        _check(lib().ptzekf_add_rays(self._h, len(rays), _ptr(rays), float(var)), "ptzekf_add_rays")
+
+    def project_visible(self, u, v, ptz, height, width, displacement=None):
+        n = self.n_ray
+        xy = np.empty((max(n, 1), 2))
+        idx = np.empty(max(n, 1))
+        cnt = c_int32(0)
+        d6 = None if displacement is None else _f64(displacement, (6,))
+        _check(lib().ptzekf_project_visible(self._h, float(u), float(v), _ptr(d6), _ptr(_f64(ptz, (3,))),
+                                            int(height), int(width), _ptr(xy), _ptr(idx), ctypes.byref(cnt)),
+               "ptzekf_project_visible")
+        c = cnt.value
+        return xy[:c].copy(), idx[:c].copy()
+
+    def update(self, u, v, ptz, obs_xy, obs_index, height, width, observe_var=0.1, displacement=None):
+        """Returns (updated ptz [3], velocity [3], n_matched)."""
+        ptz = _f64(ptz, (3,)).copy()
+        obs_xy = _f64(obs_xy).reshape(-1, 2)
+        obs_index = np.ascontiguousarray(np.asarray(obs_index).reshape(-1), dtype=np.int64)
+        if len(obs_index) != len(obs_xy):
+            raise ValueError("observed keypoints and indices differ in length")
+        vel = np.zeros(3)
+        nm = c_int32(0)
+        d6 = None if displacement is None else _f64(displacement, (6,))
+        _check(lib().ptzekf_update(self._h, float(u), float(v), _ptr(d6), _ptr(ptz), len(obs_index), _ptr(obs_xy),
+                                   _ptr(obs_index), int(height), int(width), float(observe_var), _ptr(vel),
+                                   ctypes.byref(nm)), "ptzekf_update")
+        return ptz, vel, nm.value
+
+
 class LMResult:
     def __init__(self, **kw):
         self.__dict__.update(kw)
