@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-accuracy", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "k1_traffic.json"))
-    ap.add_argument("--cpu-sample-kf", type=int, default=40)
+    ap.add_argument("--cpu-sample-kf", type=int, default=80)
     return ap.parse_args()
 
 

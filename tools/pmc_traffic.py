@@ -1,0 +1,45 @@
+"""Per-launch HBM traffic of a kernel from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
+
+FETCH_SIZE / WRITE_SIZE are in KiB (rocprofv3 derived counters).  On gfx950 FETCH_SIZE reports half of
+the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md, HBM section), so the read bytes are
+2 x FETCH_SIZE; WRITE_SIZE is taken as is.  Writes a JSON entry keyed like bench.py's --traffic-json.
+  python tools/pmc_traffic.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR KEY OUT_JSON
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_dispatch(d, counter, kernel):
+    vals = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if row["Counter_Name"] == counter and kernel in row["Kernel_Name"]:
+                k = (row["Process_Id"], row["Dispatch_Id"])
+                vals[k] = vals.get(k, 0.0) + float(row["Counter_Value"])
+    return list(vals.values())
+
+
+def main():
+    fdir, wdir, kernel, key, out = sys.argv[1:6]
+    fe = per_dispatch(fdir, "FETCH_SIZE", kernel)
+    wr = per_dispatch(wdir, "WRITE_SIZE", kernel)
+    if not fe or not wr:
+        raise SystemExit(f"no dispatches of {kernel}: fetch {len(fe)} write {len(wr)}")
+    fkib = sum(fe) / len(fe)
+    wkib = sum(wr) / len(wr)
+    entry = {"kernel": kernel, "launches_fetch_pass": len(fe), "launches_write_pass": len(wr),
+             "fetch_size_kib_avg": fkib, "write_size_kib_avg": wkib,
+             "read_bytes_corrected": 2 * fkib * 1024, "write_bytes": wkib * 1024,
+             "hbm_bytes_per_launch": 2 * fkib * 1024 + wkib * 1024,
+             "correction": "read = 2 x FETCH_SIZE (gfx950 half-count of wide coalesced reads), write = WRITE_SIZE"}
+    db = json.load(open(out)) if os.path.exists(out) else {}
+    db[key] = entry
+    json.dump(db, open(out, "w"), indent=1)
+    print(json.dumps(entry, indent=1))
+
+
+if __name__ == "__main__":
+    main()
