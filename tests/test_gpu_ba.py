@@ -291,3 +291,51 @@ def test_analytic_jacobian_matches_fd_cpu():
         e[c] = 1e-5 if c < 3 * (p.n_pose - 1) and c % 3 != 2 else (1e-3 if c < 3 * (p.n_pose - 1) else 1e-5)
         fd = (f(x0 + e) - f(x0 - e)) / (2 * e[c])
         np.testing.assert_allclose(J[:, c], fd, rtol=1e-5, atol=1e-5 * max(1.0, np.abs(fd).max()))
+
+
+def test_exchange_region_sums_over_landmark_shards(gpu_available):
+    """The N>1 protocol on one device: two landmark-shard handles' exchange regions sum to the
+    whole-problem handle's reduced system; after writing the sum back, each shard takes the same pose
+    step and its own landmarks' step (bench.py all-reduces exactly these buffers over RCCL)."""
+    import torch
+    import bench
+    import ptzba
+    import synthetic
+    p = synthetic.make_problem("config2", seed=0)
+    hs = []
+    for sel in [np.ones(len(p.frame), bool)] + [bench.shard_by_landmark(p.landmark, p.n_landmark, r, 2)
+                                                 for r in range(2)]:
+        h = ptzba.BAHandle(0)
+        h.set_problem(p.n_pose, p.n_landmark, p.frame[sel], p.landmark[sel], p.xy[sel], p.u, p.v)
+        h.set_state(p.init_ptz, p.init_rays)
+        h.linearize()
+        h.build_reduced(1e-3)
+        h.sync()
+        hs.append((h, sel))
+    views = []
+    for h, _ in hs:
+        sp, n, scp = h.exchange()
+        views.append((torch.as_tensor(bench._DevArray(sp, n), device="cuda:0"),
+                      torch.as_tensor(bench._DevArray(scp, ptzba.NSCALARS), device="cuda:0")))
+    full = views[0][0].cpu().numpy()
+    summed = (views[1][0] + views[2][0])
+    err = np.abs(summed.cpu().numpy() - full).max() / np.abs(full).max()
+    assert err < 1e-12, err
+    views[1][0].copy_(summed)
+    views[2][0].copy_(summed)
+    torch.cuda.synchronize()
+    for h, _ in hs:
+        h.solve_reduced()
+    s = [h.read_scalars() for h, _ in hs]
+    # trial cost is rank-local: the shards' values add up to the whole problem's
+    assert abs(s[1][1] + s[2][1] - s[0][1]) <= 1e-10 * s[0][1]
+    for h, _ in hs:
+        h.accept(True)
+    ptz0, rays0 = hs[0][0].get_state()
+    for h, sel in hs[1:]:
+        ptz, rays = h.get_state()
+        np.testing.assert_allclose(ptz, ptz0, rtol=0, atol=1e-9)
+        own = np.unique(p.landmark[sel])
+        np.testing.assert_allclose(rays[own], rays0[own], rtol=0, atol=1e-9)
+    for h, _ in hs:
+        h.close()
