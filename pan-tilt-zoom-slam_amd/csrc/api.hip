@@ -54,9 +54,11 @@ struct ptzba_ctx {
   DBuf ft, rt, ft64, rt64, seg_base;
   DBuf seg_out[2], seg_w[2], lm_out[2];
   int cur = 0;
-  DBuf lm_aux, lm_red;
+  DBuf lm_aux, lm_red, red_scratch;
   DBuf sys;  // [S ld*ld | b ld | g_pose ld | dU ld]
   DBuf scal, loc, info;
+  DBuf scal_pack;               // device block [scal 8 | loc 8 | info]
+  double* scal_host = nullptr;   // pinned host copy of scal_pack
   DBuf chol_tasks, chol_colfirst, chol_rowend, Ldiag, dpose;
   std::vector<int> chol_task_off;  // host: per tile column, offsets into chol_tasks
   double lambda = 0;
@@ -106,6 +108,7 @@ void ptzba_delete(ptzba_handle h) {
   for (int k = 0; k < TM_N; ++k)
     for (auto e : h->ev[k]) (void)hipEventDestroy(e);
   if (h->own) (void)hipStreamDestroy(h->own);
+  if (h->scal_host) (void)hipHostFree(h->scal_host);
   delete h;
 }
 
@@ -324,7 +327,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       h->seg_w[1].alloc((size_t)n_seg * 8 * e) || h->lm_out[0].alloc((size_t)n_landmark * 8 * 8) ||
       h->lm_out[1].alloc((size_t)n_landmark * 8 * 8) || h->lm_aux.alloc((size_t)n_landmark * 8 * 8) ||
       h->lm_red.alloc((size_t)n_landmark * 4 * 8) || h->sys.alloc((size_t)h->sys_count() * 8) ||
-      h->scal.alloc(PTZBA_NSCALARS * 8) || h->loc.alloc(PTZBA_NSCALARS * 8) || h->info.alloc(16) ||
+      h->scal.alloc(PTZBA_NSCALARS * 8) || h->red_scratch.alloc(RED_SCRATCH * 8) || h->loc.alloc(PTZBA_NSCALARS * 8) || h->info.alloc(16) ||
       h->Ldiag.alloc((size_t)h->ld * CHOL_NB * 8) || h->dpose.alloc((size_t)h->ld * 8))
     return -1;
   if (build_chol_plan(h, frame_win_hi)) return -1;
@@ -333,6 +336,9 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   HIPCHK(hipMemset(h->ptz.p, 0, h->ptz.bytes));
   HIPCHK(hipMemset(h->rays.p, 0, h->rays.bytes));
   HIPCHK(hipMemset(h->scal.p, 0, h->scal.bytes));
+  HIPCHK(hipMemset(h->red_scratch.p, 0, h->red_scratch.bytes));
+  if (!h->scal_host) HIPCHK(hipHostMalloc((void**)&h->scal_host, 24 * sizeof(double), hipHostMallocDefault));
+  if (!h->scal_pack.p && h->scal_pack.alloc(24 * sizeof(double))) return -1;
   HIPCHK(hipMemset(h->loc.p, 0, h->loc.bytes));
   h->cur = 0;
   h->lambda = 0;
@@ -454,7 +460,8 @@ int ptzba_linearize(ptzba_handle h) {
   tables(h, h->ptz.as<double>(), h->rays.as<double>());
   linearize_into(h, h->cur);
   HIPCHK(hipMemsetAsync(h->scal.p, 0, h->scal.bytes, h->st));
-  launch_reduce_cols(h->lm_out[h->cur].as<double>() + 5, h->n_lm, 8, 1, 0, h->scal.as<double>(), h->st);
+  launch_reduce_cols(h->lm_out[h->cur].as<double>() + 5, h->n_lm, 8, 1, 0, h->scal.as<double>(),
+                     h->red_scratch.as<double>(), h->st);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -536,8 +543,10 @@ int ptzba_solve_reduced(ptzba_handle h) {
   tables(h, h->ptz_trial.as<double>(), h->rays_trial.as<double>());
   linearize_into(h, nx);
   HIPCHK(hipMemsetAsync(h->scal.p, 0, h->scal.bytes, h->st));
-  launch_reduce_cols(h->lm_out[nx].as<double>() + 5, h->n_lm, 8, 1, 0, h->scal.as<double>() + 1, h->st);
-  launch_reduce_cols(h->lm_red.as<double>(), h->n_lm, 4, 3, 0, h->scal.as<double>() + 2, h->st);
+  launch_reduce_cols(h->lm_out[nx].as<double>() + 5, h->n_lm, 8, 1, 0, h->scal.as<double>() + 1,
+                     h->red_scratch.as<double>(), h->st);
+  launch_reduce_cols(h->lm_red.as<double>(), h->n_lm, 4, 3, 0, h->scal.as<double>() + 2, h->red_scratch.as<double>(),
+                     h->st);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -551,18 +560,19 @@ int ptzba_step(ptzba_handle h, double lambda) {
 int ptzba_read_scalars(ptzba_handle h, double* out) {
   if (!h || !h->have_problem) return fail("no problem set");
   HIPCHK(hipSetDevice(h->device));
-  double s[PTZBA_NSCALARS], l[PTZBA_NSCALARS];
-  int inf[4] = {0, 0, 0, 0};
-  HIPCHK(hipMemcpyAsync(s, h->scal.p, sizeof(s), hipMemcpyDeviceToHost, h->st));
-  HIPCHK(hipMemcpyAsync(l, h->loc.p, sizeof(l), hipMemcpyDeviceToHost, h->st));
-  HIPCHK(hipMemcpyAsync(inf, h->info.p, sizeof(int), hipMemcpyDeviceToHost, h->st));
+  // one kernel packs scal | loc | info, one copy brings the block to pinned host memory
+  launch_pack_scalars(h->scal.as<double>(), h->loc.as<double>(), h->info.as<int>(), h->scal_pack.as<double>(), h->st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(h->scal_host, h->scal_pack.p, 17 * sizeof(double), hipMemcpyDeviceToHost, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
+  const double* s = h->scal_host;
+  const double* l = h->scal_host + 8;
   out[0] = s[0];
   out[1] = s[1];
   out[2] = s[2] + l[0];
   out[3] = s[3] + l[1];
   out[4] = s[4] + l[2];
-  out[5] = (double)inf[0];
+  out[5] = h->scal_host[16];
   out[6] = l[3];
   out[7] = 0;
   return 0;

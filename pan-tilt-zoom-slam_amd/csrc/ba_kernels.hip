@@ -563,21 +563,32 @@ void launch_pose_trial(const double* ptz, const double* dpose, const double* g_p
                      n_fixed, lambda, out4);
 }
 
-// deterministic strided reduction: out[k] = sum_i src[i*stride + off[k]] (fixed order), k < nk.
-// mode bit k set -> max(|.|) instead of sum for column k
-__global__ void k_reduce_cols(const double* __restrict__ src, int64_t n, int stride, int nk, int maxmask,
-                              double* __restrict__ out) {
-  __shared__ double red[8][1024 / WAVE];
+// deterministic strided reduction: out[k] = sum_i src[i*stride + k] (fixed order), k < nk;
+// mode bit k set -> max(|.|) instead of sum for column k.  RED_BLOCKS workgroups reduce contiguous row
+// ranges into scratch partials; the last workgroup to finish (agent-scope counter) combines them in
+// block order and re-arms the counter, so the result is bitwise reproducible in one launch.
+constexpr int RED_BLOCKS = 64;
+__global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ src, int64_t n, int stride, int nk,
+                                                     int maxmask, double* __restrict__ out,
+                                                     double* __restrict__ partial, unsigned* __restrict__ counter) {
+  __shared__ double red[8][256 / WAVE];
+  __shared__ bool last;
+  const int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t i0 = blockIdx.x * chunk, i1 = min(n, i0 + chunk);
   double acc[8];
+#pragma unroll
   for (int k = 0; k < 8; ++k) acc[k] = 0;
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-    for (int k = 0; k < nk; ++k) {
-      double x = src[i * stride + k];
-      if (maxmask & (1 << k)) acc[k] = fmax(acc[k], fabs(x));
-      else acc[k] += x;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k >= nk) break;
+      const double x = src[i * stride + k];
+      acc[k] = (maxmask & (1 << k)) ? fmax(acc[k], fabs(x)) : acc[k] + x;
     }
   }
-  for (int k = 0; k < nk; ++k) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (k >= nk) break;
     if (maxmask & (1 << k)) {
       for (int o = 32; o > 0; o >>= 1) acc[k] = fmax(acc[k], __shfl_xor(acc[k], o, WAVE));
     } else {
@@ -592,12 +603,44 @@ __global__ void k_reduce_cols(const double* __restrict__ src, int64_t n, int str
     const int k = threadIdx.x;
     double s = 0;
     for (int j = 0; j < (int)(blockDim.x / WAVE); ++j) s = (maxmask & (1 << k)) ? fmax(s, red[k][j]) : s + red[k][j];
+    partial[blockIdx.x * 8 + k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned done = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = (done == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x < nk) {
+    const int k = threadIdx.x;
+    double s = 0;
+    for (int b = 0; b < (int)gridDim.x; ++b) {
+      const double x = __hip_atomic_load(partial + b * 8 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s = (maxmask & (1 << k)) ? fmax(s, x) : s + x;
+    }
     out[k] = s;
   }
+  if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-void launch_reduce_cols(const double* src, int64_t n, int stride, int nk, int maxmask, double* out, hipStream_t st) {
-  hipLaunchKernelGGL(k_reduce_cols, dim3(1), dim3(1024), 0, st, src, n, stride, nk, maxmask, out);
+__global__ void k_pack_scalars(const double* __restrict__ scal, const double* __restrict__ loc,
+                               const int* __restrict__ info, double* __restrict__ host) {
+  const int t = threadIdx.x;
+  if (t < 8) host[t] = scal[t];
+  else if (t < 16) host[t] = loc[t - 8];
+  else if (t == 16) host[16] = (double)info[0];
+}
+
+void launch_pack_scalars(const double* scal, const double* loc, const int* info, double* host_dev, hipStream_t st) {
+  hipLaunchKernelGGL(k_pack_scalars, dim3(1), dim3(64), 0, st, scal, loc, info, host_dev);
+}
+
+void launch_reduce_cols(const double* src, int64_t n, int stride, int nk, int maxmask, double* out, double* scratch,
+                        hipStream_t st) {
+  unsigned* counter = reinterpret_cast<unsigned*>(scratch + RED_BLOCKS * 8);
+  hipLaunchKernelGGL(k_reduce_cols, dim3(RED_BLOCKS), dim3(256), 0, st, src, n, stride, nk, maxmask, out, scratch,
+                     counter);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -48,31 +48,54 @@ __device__ __forceinline__ void load_tile(double (*dst)[NB + 1], const double* _
   for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) dst[e >> 5][e & 31] = src[(int64_t)(e >> 5) * ld + (e & 31)];
 }
 
-// C -= A B^T for 32x32 tiles in LDS (256 threads: 32 rows x 8 groups of 4 columns)
+// C -= A B^T for 32x32 tiles in LDS on the fp64 matrix cores: 256 threads = 4 waves, wave w owns the
+// 16x16 block (16 (w>>1), 16 (w&1)) and runs 8 v_mfma_f64_16x16x4_f64 (k = 4 per step).  Operand lane
+// maps (gfx950): A[i = l&15][k = l>>4], B[k = l>>4][j = l&15]; D[row = (l>>4) + 4 r][col = l&15].
+typedef double v4f64 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void tile_gemm_nt_sub(double (*C)[NB + 1], double (*A)[NB + 1], double (*B)[NB + 1]) {
-  const int rr = threadIdx.x >> 3;
-  const int cc = (threadIdx.x & 7) * 4;
-  double acc[4] = {0, 0, 0, 0};
-#pragma unroll 8
-  for (int m = 0; m < NB; ++m) {
-    const double x = A[rr][m];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int bi = (w >> 1) * 16, bj = (w & 1) * 16;
+  const int li = l & 15, lk = l >> 4;
+  v4f64 acc;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] += x * B[cc + q][m];
+  for (int r = 0; r < 4; ++r) acc[r] = C[bi + lk + 4 * r][bj + li];
+#pragma unroll
+  for (int s = 0; s < NB / 4; ++s) {
+    const double a = -A[bi + li][4 * s + lk];
+    const double b = B[bj + li][4 * s + lk];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) C[rr][cc + q] -= acc[q];
+  for (int r = 0; r < 4; ++r) C[bi + lk + 4 * r][bj + li] = acc[r];
 }
 
-// One wave factors the 32x32 SPD tile D (LDS) in place into its lower Cholesky factor; rdg[j] = 1/L_jj.
-// Lane i keeps row i in registers; the pivot column is broadcast with v_readlane (no LDS round trips,
-// no spills): right-looking on the unscaled pivot column, row_i[m] -= (A_ij / A_jj) A_mj, and at the
-// end L_ij = A_ij / sqrt(A_jj).
-__device__ __forceinline__ void wave_potrf32(double (*D)[NB + 1], double* rdg, int* info) {
+// fp64 reciprocal and reciprocal square root: hardware estimate + two Newton steps (full double
+// precision, a much shorter dependent chain than IEEE division / sqrt on the pivot critical path)
+__device__ __forceinline__ double rcp_nr(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(r, fma(-d, r, 1.0), r);
+  return fma(r, fma(-d, r, 1.0), r);
+}
+__device__ __forceinline__ double rsq_nr(double d) {
+  double y = __builtin_amdgcn_rsq(d);
+  y = y * fma(-0.5 * d * y, y, 1.5);
+  return y * fma(-0.5 * d * y, y, 1.5);
+}
+
+// One wave factors the 32x32 SPD tile D and, in the same sweep, solves X = T L^-T for a 32x32 tile T.
+// Lanes 0..31 hold the rows of D, lanes 32..63 the rows of T, in registers.  Right-looking step j
+// broadcasts the (unscaled) pivot column A_mj with v_readlane; every lane applies
+//     v[m] -= (v[j] / A_jj) A_mj,  m > j,
+// which is the Cholesky update for a row of D and the forward substitution for a row of T.  At the end
+// L_ij = v_i[j] / sqrt(A_jj) (j <= i; L_ii = sqrt(A_jj)) and X_rj = x_r[j] / sqrt(A_jj).  Writes the
+// lower factor into D (zero above), X into T (when given), rdg[j] = 1/L_jj.
+__device__ __forceinline__ void wave_potrf_trsm32(double (*D)[NB + 1], double (*T)[NB + 1], double* rdg, int* info) {
   const int lane = lane_id();
-  const int i = lane & (NB - 1);
-  double row[NB], dg[NB];
+  const bool isT = lane >= NB;
+  const int r = lane & (NB - 1);
+  double row[NB], rs[NB];
 #pragma unroll
-  for (int m = 0; m < NB; ++m) row[m] = D[i][m];
+  for (int m = 0; m < NB; ++m) row[m] = (isT && T) ? T[r][m] : D[r][m];
   bool bad = false;
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
@@ -81,19 +104,22 @@ __device__ __forceinline__ void wave_potrf32(double (*D)[NB + 1], double* rdg, i
       bad = true;
       d = 1e-300;
     }
-    const double li = row[j] * (1.0 / d);
+    rs[j] = rsq_nr(d);
+    const double li = row[j] * rcp_nr(d);
 #pragma unroll
     for (int m = j + 1; m < NB; ++m) row[m] -= li * bcast(row[j], m);
-    dg[j] = d;
   }
   if (bad && lane == 0) atomicOr(info, 1);
-  if (lane < NB) {
+  if (!isT) {
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const double r = 1.0 / sqrt(dg[j]);
-      D[i][j] = (j <= i) ? row[j] * r : 0.0;
-      if (lane == j) rdg[j] = r;
+    for (int j = 0; j < NB; ++j) D[r][j] = (j <= r) ? row[j] * rs[j] : 0.0;
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) rdg[j] = rs[j];
     }
+  } else if (T) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j) T[r][j] = row[j] * rs[j];
   }
   wave_lds_fence();
 }
@@ -138,13 +164,13 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   if (upd_k) load_tile(sB, A + (int64_t)k * NBl * ld + (k - 1) * NBl, ld);
   if (upd_i && !diag_only) load_tile(sA, A + i * NBl * ld + (k - 1) * NBl, ld);
   __syncthreads();
+#if CHOL_VARIANT != 4
   if (upd_k) tile_gemm_nt_sub(sD, sB, sB);
   if (upd_k && upd_i && !diag_only) tile_gemm_nt_sub(sC, sA, sB);
+#endif
   __syncthreads();
 #if CHOL_VARIANT != 1
-  if (threadIdx.x < WAVE) wave_potrf32(sD, rdg, info);
-#else
-  if (threadIdx.x < NB) rdg[threadIdx.x] = 1.0;
+  if (threadIdx.x < WAVE) wave_potrf_trsm32(sD, diag_only ? nullptr : sC, rdg, info);
 #endif
   __syncthreads();
   if (diag_only) {
@@ -152,22 +178,6 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
     double* C = Ldiag + (int64_t)k * NB * NB;
     for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) C[e] = sD[e >> 5][e & 31];
     return;
-  }
-  // L_ik = T_ik L_kk^-T : lane r solves row r
-  if (threadIdx.x < NB && CHOL_VARIANT != 2) {
-    const int r = threadIdx.x;
-    double x[NB];
-#pragma unroll
-    for (int m = 0; m < NB; ++m) x[m] = sC[r][m];
-#pragma unroll
-    for (int jj = 0; jj < NB; ++jj) {
-      x[jj] *= rdg[jj];
-#pragma unroll
-      for (int m = jj + 1; m < NB; ++m) x[m] -= x[jj] * sD[m][jj];
-      __builtin_amdgcn_sched_barrier(0);  // keep each step's LDS reads in the step (no hoisting -> no spills)
-    }
-#pragma unroll
-    for (int m = 0; m < NB; ++m) sC[r][m] = x[m];
   }
   __syncthreads();
   double* C = A + i * NBl * ld + k * NBl;
@@ -203,7 +213,8 @@ __global__ __launch_bounds__(1024) void k_chol_backsolve(const double* __restric
   __syncthreads();
   for (int kt = Tn - 1; kt >= 0; --kt) {
     const int64_t c0 = (int64_t)kt * NB;
-    // stage L_kk and the envelope-limited column-block dot products
+    // stage L_kk and the envelope-limited column-block dot products (a register prefetch of the next
+    // tile column during the solve measured slower: 333 vs 258 us at config3)
     Lkk[t >> 5][t & 31] = Ldiag[(int64_t)kt * NB * NB + t];
     double s = 0;
     const int r1 = min(rowend[kt], n);
@@ -219,7 +230,7 @@ __global__ __launch_bounds__(1024) void k_chol_backsolve(const double* __restric
         tr = xv[c0 + lane] - tr;
       }
       // upper-triangular solve L_kk^T x = tr, lane r holds tr_r
-      const double rd = lane < NB ? 1.0 / Lkk[lane][lane] : 0.0;
+      const double rd = lane < NB ? rcp_nr(Lkk[lane][lane]) : 0.0;
 #pragma unroll
       for (int jj = NB - 1; jj >= 0; --jj) {
         const double tj = bcast(tr, jj) * bcast(rd, jj);

@@ -74,7 +74,12 @@ template <typename real>
 void launch_backsub(const BacksubArgs& a, hipStream_t st);
 void launch_pose_trial(const double* ptz, const double* dpose, const double* g_pose, const double* D_pose,
                        double* ptz_trial, int n_pose, int n_fixed, double lambda, double* out4, hipStream_t st);
-void launch_reduce_cols(const double* src, int64_t n, int stride, int nk, int maxmask, double* out, hipStream_t st);
+// scratch: RED_SCRATCH doubles (partials + counter), zero-initialised once, reused across calls
+constexpr int RED_SCRATCH = 64 * 8 + 2;
+// scal[8] | loc[8] | info -> one packed device block (read back with a single copy)
+void launch_pack_scalars(const double* scal, const double* loc, const int* info, double* host_dev, hipStream_t st);
+void launch_reduce_cols(const double* src, int64_t n, int stride, int nk, int maxmask, double* out, double* scratch,
+                        hipStream_t st);
 template <typename real>
 void launch_residual(const int32_t* rec_seg, const int32_t* seg_frame, const int32_t* seg_lm, const double2* seg_base,
                      const void* rec_xy, const int64_t* perm, const void* ft64, const void* rt64, double u, double v,

@@ -1,0 +1,353 @@
+// Microbenchmark: 32x32 fp64 tile Cholesky (potrf) and triangular solve (TRSM, X = T L^-T) variants
+// for the fused k_chol_step.  Each workgroup (256 threads) repeats potrf+trsm REPS times on its own
+// SPD tile; grid = many workgroups; reports us per (potrf, trsm) and checks results vs variant 0.
+//   hipcc -O3 --offload-arch=gfx950 tools/potrf_bench.hip -o tools/potrf_bench && tools/potrf_bench
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+constexpr int NB = 32, WAVE = 64, REPS = 16;
+
+__device__ __forceinline__ double bcast(double v, int j) {
+  int lo = __builtin_amdgcn_readlane(__double2loint(v), j);
+  int hi = __builtin_amdgcn_readlane(__double2hiint(v), j);
+  return __hiloint2double(hi, lo);
+}
+
+// ---- V0: rows in registers, pivot column by readlane (current library code)
+__device__ void potrf_v0(double (*D)[NB + 1], double* rdg) {
+  const int lane = threadIdx.x & 63;
+  double row[NB];
+#pragma unroll
+  for (int m = 0; m < NB; ++m) row[m] = D[lane & 31][m];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const double d = bcast(row[j], j);
+    const double r = 1.0 / sqrt(d);
+    if (lane == j) rdg[j] = r;
+    const double li = row[j] / d;
+#pragma unroll
+    for (int m = j + 1; m < NB; ++m) row[m] -= li * bcast(row[j], m);
+  }
+  if (lane < NB) {
+#pragma unroll
+    for (int m = 0; m < NB; ++m) D[lane][m] = row[m];
+  }
+}
+
+// ---- V1: readlanes of the whole pivot column first (distinct SGPRs), then the FMAs
+__device__ void potrf_v1(double (*D)[NB + 1], double* rdg) {
+  const int lane = threadIdx.x & 63;
+  double row[NB];
+#pragma unroll
+  for (int m = 0; m < NB; ++m) row[m] = D[lane & 31][m];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    double c[NB];
+#pragma unroll
+    for (int m = j; m < NB; ++m) c[m] = bcast(row[j], m);
+    const double d = c[j];
+    const double r = 1.0 / sqrt(d);
+    if (lane == j) rdg[j] = r;
+    const double li = row[j] / d;
+#pragma unroll
+    for (int m = j + 1; m < NB; ++m) row[m] -= li * c[m];
+  }
+  if (lane < NB) {
+#pragma unroll
+    for (int m = 0; m < NB; ++m) D[lane][m] = row[m];
+  }
+}
+
+// ---- V2: rows in registers, pivot column broadcast through LDS (uniform-address reads)
+__device__ void potrf_v2(double (*D)[NB + 1], double* rdg, double* col) {
+  const int lane = threadIdx.x & 63;
+  double row[NB];
+#pragma unroll
+  for (int m = 0; m < NB; ++m) row[m] = D[lane & 31][m];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    if (lane < NB) col[lane] = row[j];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const double d = col[j];
+    const double li = row[j] / d;
+    if (lane == j) rdg[j] = 1.0 / sqrt(d);
+#pragma unroll
+    for (int m = j + 1; m < NB; ++m) row[m] -= li * col[m];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  }
+  if (lane < NB) {
+#pragma unroll
+    for (int m = 0; m < NB; ++m) D[lane][m] = row[m];
+  }
+}
+
+// ---- V3: two lanes per row (lane 2r: columns 0..15, lane 2r+1: columns 16..31), LDS broadcast
+__device__ void potrf_v3(double (*D)[NB + 1], double* rdg, double* col) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane >> 1, h = lane & 1;
+  double row[16];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) row[m] = D[r][16 * h + m];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    // owner of column j publishes A_rj for its row
+    if (h == (j >> 4)) col[r] = row[j & 15];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const double d = col[j];
+    const double li = col[r] / d;
+    if (lane == 2 * j) rdg[j] = 1.0 / sqrt(d);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int gm = 16 * h + m;
+      if (gm > j) row[m] -= li * col[gm];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  }
+#pragma unroll
+  for (int m = 0; m < 16; ++m) D[r][16 * h + m] = row[m];
+}
+
+
+__device__ __forceinline__ double rcp_nr(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(r, fma(-d, r, 1.0), r);
+  r = fma(r, fma(-d, r, 1.0), r);
+  return r;
+}
+__device__ __forceinline__ double rsq_nr(double d) {
+  double y = __builtin_amdgcn_rsq(d);
+  y = y * fma(-0.5 * d * y, y, 1.5);
+  y = y * fma(-0.5 * d * y, y, 1.5);
+  return y;
+}
+
+// ---- V8: fused potrf + TRSM on one wave: lanes 0..31 hold the rows of D, lanes 32..63 the rows of T.
+// Right-looking step j: v[m] -= (v[j] / d_j) * A_mj (m > j) is the Cholesky update for D rows and the
+// forward substitution for T rows alike.  Pivot column by readlane, fast rcp/rsq + Newton.
+template <bool FAST>
+__device__ void potrf_trsm_v8(double (*D)[NB + 1], double (*C)[NB + 1], double* rdg) {
+  const int lane = threadIdx.x & 63;
+  const bool isT = lane >= NB;
+  double row[NB];
+#pragma unroll
+  for (int m = 0; m < NB; ++m) row[m] = isT ? C[lane - NB][m] : D[lane][m];
+  double rs[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const double d = bcast(row[j], j);
+    const double inv = FAST ? rcp_nr(d) : 1.0 / d;
+    rs[j] = FAST ? rsq_nr(d) : 1.0 / sqrt(d);
+    const double li = row[j] * inv;
+#pragma unroll
+    for (int m = j + 1; m < NB; ++m) row[m] -= li * bcast(row[j], m);
+  }
+  // scale: L_ij = row_i[j] rs_j (j < i), rdg_j = rs_j; X_rj = x_j rs_j
+#pragma unroll
+  for (int m = 0; m < NB; ++m) row[m] *= rs[m];
+  if (lane < NB) rdg[lane] = 0;  // placeholder, rdg below
+  if (lane == 0) {
+#pragma unroll
+    for (int m = 0; m < NB; ++m) rdg[m] = rs[m];
+  }
+  if (isT) {
+#pragma unroll
+    for (int m = 0; m < NB; ++m) C[lane - NB][m] = row[m];
+  } else {
+#pragma unroll
+    for (int m = 0; m < NB; ++m) D[lane][m] = row[m];
+  }
+}
+
+// ---- TRSM variants: X = T L^-T with L = D (scaled on the fly: L_mj = D[m][j] * rdg[j] for m > j, L_jj = 1/rdg)
+// T0: lane per row, sched_barrier per step (library)
+__device__ void trsm_t0(double (*C)[NB + 1], double (*D)[NB + 1], const double* rdg) {
+  const int r = threadIdx.x;
+  if (r >= NB) return;
+  double x[NB];
+#pragma unroll
+  for (int m = 0; m < NB; ++m) x[m] = C[r][m];
+#pragma unroll
+  for (int jj = 0; jj < NB; ++jj) {
+    x[jj] *= rdg[jj];
+#pragma unroll
+    for (int m = jj + 1; m < NB; ++m) x[m] -= x[jj] * D[m][jj];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int m = 0; m < NB; ++m) C[r][m] = x[m];
+}
+
+// T1: lane per row, no scheduling barrier (compiler free to pipeline LDS reads)
+__device__ void trsm_t1(double (*C)[NB + 1], double (*D)[NB + 1], const double* rdg) {
+  const int r = threadIdx.x;
+  if (r >= NB) return;
+  double x[NB];
+#pragma unroll
+  for (int m = 0; m < NB; ++m) x[m] = C[r][m];
+#pragma unroll
+  for (int jj = 0; jj < NB; ++jj) {
+    x[jj] *= rdg[jj];
+#pragma unroll
+    for (int m = jj + 1; m < NB; ++m) x[m] -= x[jj] * D[m][jj];
+    if ((jj & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int m = 0; m < NB; ++m) C[r][m] = x[m];
+}
+
+// T2: 4 waves, 8 lanes per row?  -> instead: 2 waves x 32 lanes, each wave half the rows, D transposed
+// in LDS (Dt[jj][m]) so the per-step column is a contiguous, vectorisable read
+__device__ void trsm_t2(double (*C)[NB + 1], double (*Dt)[NB + 1], const double* rdg) {
+  const int r = threadIdx.x;
+  if (r >= NB) return;
+  double x[NB];
+#pragma unroll
+  for (int m = 0; m < NB; ++m) x[m] = C[r][m];
+#pragma unroll
+  for (int jj = 0; jj < NB; ++jj) {
+    x[jj] *= rdg[jj];
+#pragma unroll
+    for (int m = jj + 1; m < NB; ++m) x[m] -= x[jj] * Dt[jj][m];
+    if ((jj & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int m = 0; m < NB; ++m) C[r][m] = x[m];
+}
+
+template <int PV, int TV>
+__global__ __launch_bounds__(256) void k_bench(const double* __restrict__ A, const double* __restrict__ T,
+                                               double* __restrict__ L, double* __restrict__ X) {
+  __shared__ double sD[NB][NB + 1];
+  __shared__ double sDt[NB][NB + 1];
+  __shared__ double sC[NB][NB + 1];
+  __shared__ double rdg[NB];
+  __shared__ double col[NB];
+  const double* a = A + (size_t)blockIdx.x * NB * NB;
+  const double* t = T + (size_t)blockIdx.x * NB * NB;
+  for (int rep = 0; rep < REPS; ++rep) {
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+      sD[e >> 5][e & 31] = a[e];
+      sC[e >> 5][e & 31] = t[e];
+    }
+    __syncthreads();
+    if (threadIdx.x < WAVE) {
+      if (PV == 0) potrf_v0(sD, rdg);
+      if (PV == 1) potrf_v1(sD, rdg);
+      if (PV == 2) potrf_v2(sD, rdg, col);
+      if (PV == 3) potrf_v3(sD, rdg, col);
+      if (PV == 7) potrf_v0(sD, rdg);
+      if (PV == 8) potrf_trsm_v8<true>(sD, sC, rdg);
+      if (PV == 9) potrf_trsm_v8<false>(sD, sC, rdg);
+    }
+    __syncthreads();
+    if (TV == 2) {
+      for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) sDt[e & 31][e >> 5] = sD[e >> 5][e & 31];
+      __syncthreads();
+    }
+    if (TV == 0) trsm_t0(sC, sD, rdg);
+    if (TV == 1) trsm_t1(sC, sD, rdg);
+    if (TV == 2) trsm_t2(sC, sDt, rdg);
+    __syncthreads();
+  }
+  double* l = L + (size_t)blockIdx.x * NB * NB;
+  double* x = X + (size_t)blockIdx.x * NB * NB;
+  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+    const int i = e >> 5, j = e & 31;
+    if (PV >= 8) l[e] = (j < i) ? sD[i][j] : (j == i ? 1.0 / rdg[i] : 0.0);
+    else l[e] = (j < i) ? sD[i][j] * rdg[j] : (j == i ? 1.0 / rdg[i] : 0.0);
+    x[e] = sC[i][j];
+  }
+}
+
+#define CK(x)                                                              \
+  do {                                                                     \
+    hipError_t e_ = (x);                                                   \
+    if (e_ != hipSuccess) {                                                \
+      printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      exit(1);                                                             \
+    }                                                                      \
+  } while (0)
+
+template <int PV, int TV>
+double run(int nb, double* dA, double* dT, double* dL, double* dX, std::vector<double>& L, std::vector<double>& X) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  hipLaunchKernelGGL((k_bench<PV, TV>), dim3(nb), dim3(256), 0, 0, dA, dT, dL, dX);
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(e0));
+  for (int it = 0; it < 5; ++it) hipLaunchKernelGGL((k_bench<PV, TV>), dim3(nb), dim3(256), 0, 0, dA, dT, dL, dX);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  L.resize((size_t)nb * NB * NB);
+  X.resize((size_t)nb * NB * NB);
+  CK(hipMemcpy(L.data(), dL, L.size() * 8, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(X.data(), dX, X.size() * 8, hipMemcpyDeviceToHost));
+  return ms * 1e3 / 5 / REPS;  // us per (load + potrf + trsm), all workgroups concurrent
+}
+
+int main() {
+  const int nb = 64;  // workgroups (one tile each) -> runs concurrently, time = per-tile latency
+  std::vector<double> A((size_t)nb * NB * NB), T((size_t)nb * NB * NB);
+  srand(1);
+  for (int b = 0; b < nb; ++b) {
+    std::vector<double> B(NB * NB);
+    for (auto& x : B) x = (double)rand() / RAND_MAX - 0.5;
+    for (int i = 0; i < NB; ++i)
+      for (int j = 0; j < NB; ++j) {
+        double s = (i == j) ? NB : 0.0;
+        for (int k = 0; k < NB; ++k) s += B[i * NB + k] * B[j * NB + k];
+        A[(size_t)b * NB * NB + i * NB + j] = s;
+        T[(size_t)b * NB * NB + i * NB + j] = (double)rand() / RAND_MAX - 0.5;
+      }
+  }
+  double *dA, *dT, *dL, *dX;
+  CK(hipMalloc(&dA, A.size() * 8));
+  CK(hipMalloc(&dT, T.size() * 8));
+  CK(hipMalloc(&dL, A.size() * 8));
+  CK(hipMalloc(&dX, A.size() * 8));
+  CK(hipMemcpy(dA, A.data(), A.size() * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dT, T.data(), T.size() * 8, hipMemcpyHostToDevice));
+  std::vector<double> L0, X0, L, X;
+  auto cmp = [&](const char* name, double us) {
+    double el = 0, ex = 0;
+    for (size_t i = 0; i < L.size(); ++i) el = fmax(el, fabs(L[i] - L0[i]));
+    // X vs a CPU forward substitution X L^T = T with the reference L0
+    for (int b = 0; b < nb; ++b)
+      for (int r = 0; r < NB; ++r) {
+        double x[NB];
+        for (int c = 0; c < NB; ++c) {
+          double s = T[(size_t)b * NB * NB + r * NB + c];
+          for (int m = 0; m < c; ++m) s -= x[m] * L0[(size_t)b * NB * NB + c * NB + m];
+          x[c] = s / L0[(size_t)b * NB * NB + c * NB + c];
+          ex = fmax(ex, fabs(x[c] - X[(size_t)b * NB * NB + r * NB + c]));
+        }
+      }
+    printf("%-22s %8.3f us   max|dL| %.2e  max|dX| %.2e\n", name, us, el, ex);
+  };
+  double us = run<0, 0>(nb, dA, dT, dL, dX, L0, X0);
+  L = L0; X = X0;
+  cmp("potrf v0 + trsm t0", us);
+  cmp("potrf v1 + trsm t0", run<1, 0>(nb, dA, dT, dL, dX, L, X));
+  cmp("potrf v2 + trsm t0", run<2, 0>(nb, dA, dT, dL, dX, L, X));
+  cmp("potrf v3 + trsm t0", run<3, 0>(nb, dA, dT, dL, dX, L, X));
+  cmp("potrf v0 + trsm t1", run<0, 1>(nb, dA, dT, dL, dX, L, X));
+  cmp("potrf v0 + trsm t2", run<0, 2>(nb, dA, dT, dL, dX, L, X));
+  cmp("potrf v2 + trsm t1", run<2, 1>(nb, dA, dT, dL, dX, L, X));
+  cmp("potrf v3 + trsm t2", run<3, 2>(nb, dA, dT, dL, dX, L, X));
+  cmp("potrf v0 only (no trsm)", run<7, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("load only", run<6, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("fused v8 fast rcp", run<8, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("fused v9 ieee div", run<9, 9>(nb, dA, dT, dL, dX, L, X));
+  return 0;
+}
