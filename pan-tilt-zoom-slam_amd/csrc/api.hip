@@ -52,7 +52,7 @@ struct ptzba_ctx {
   // device: state
   DBuf ptz, rays, ptz_trial, rays_trial, D_pose, D_ray;
   DBuf ft, rt, ft64, rt64, seg_base;
-  DBuf seg_out[2], seg_w[2], lm_out[2];
+  DBuf seg_ug[2], seg_w[2], lm_out[2];
   int cur = 0;
   DBuf lm_aux, lm_red, red_scratch;
   DBuf sys;  // [S ld*ld | b ld | g_pose ld | dU ld]
@@ -295,6 +295,15 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   });
   h->n_work = (int)lm_order.size();
   h->max_seg_per_lm = max_seg;
+  if (n_obs >= ((int64_t)1 << 31)) return fail("n_obs %lld exceeds the 2^31 record limit of a handle (shard it)", (long long)n_obs);
+  std::vector<int32_t> lm_work(4 * (size_t)h->n_work);
+  for (int k = 0; k < h->n_work; ++k) {
+    const int l = lm_order[k];
+    lm_work[4 * k + 0] = l;
+    lm_work[4 * k + 1] = lm_seg_begin[l];
+    lm_work[4 * k + 2] = lm_seg_begin[l + 1];
+    lm_work[4 * k + 3] = (int32_t)seg_rec_begin[lm_seg_begin[l]];
+  }
   h->n_sys = 3 * (n_pose - o.n_fixed);
   h->ld = ((int64_t)h->n_sys + 1 + CHOL_NB - 1) / CHOL_NB * CHOL_NB;  // + augmented rhs row
   if (h->ld > 20000) return fail("reduced system %d too large for the dense solver", h->n_sys);
@@ -314,7 +323,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   if (upload(h->seg_base, seg_base)) return -1;
   if (upload(h->rec_seg, rec_seg) || upload(h->seg_frame, seg_frame) || upload(h->seg_lm, seg_lm) ||
       upload(h->seg_rec_begin, seg_rec_begin) || upload(h->lm_seg_begin, lm_seg_begin) ||
-      upload(h->lm_order, lm_order) || upload(h->frame_seg_begin, frame_seg_begin) ||
+      upload(h->lm_order, lm_work) || upload(h->frame_seg_begin, frame_seg_begin) ||
       upload(h->frame_seg_list, frame_seg_list) || upload(h->frame_win_hi, frame_win_hi))
     return -1;
   const size_t e = h->elem();
@@ -322,8 +331,8 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       h->rays_trial.alloc(2 * (size_t)n_landmark * 8) || h->D_pose.alloc(3 * n_pose * 8) ||
       h->D_ray.alloc(2 * (size_t)n_landmark * 8) || h->ft.alloc((size_t)n_pose * 8 * e) ||
       h->rt.alloc((size_t)n_landmark * 8 * e) || h->ft64.alloc((size_t)n_pose * 64) ||
-      h->rt64.alloc((size_t)n_landmark * 64) || h->seg_out[0].alloc((size_t)n_seg * 16 * e) ||
-      h->seg_out[1].alloc((size_t)n_seg * 16 * e) || h->seg_w[0].alloc((size_t)n_seg * 8 * e) ||
+      h->rt64.alloc((size_t)n_landmark * 64) || h->seg_ug[0].alloc((size_t)n_seg * 12 * e) ||
+      h->seg_ug[1].alloc((size_t)n_seg * 12 * e) || h->seg_w[0].alloc((size_t)n_seg * 8 * e) ||
       h->seg_w[1].alloc((size_t)n_seg * 8 * e) || h->lm_out[0].alloc((size_t)n_landmark * 8 * 8) ||
       h->lm_out[1].alloc((size_t)n_landmark * 8 * 8) || h->lm_aux.alloc((size_t)n_landmark * 8 * 8) ||
       h->lm_red.alloc((size_t)n_landmark * 4 * 8) || h->sys.alloc((size_t)h->sys_count() * 8) ||
@@ -359,8 +368,8 @@ int ptzba_problem_info(ptzba_handle h, int64_t* info) {
                                     &h->seg_base, &h->ft64, &h->rt64,
                                     &h->seg_rec_begin, &h->lm_seg_begin, &h->lm_order, &h->frame_seg_begin,
                                     &h->frame_seg_list, &h->frame_win_hi, &h->ptz, &h->rays, &h->ptz_trial,
-                                    &h->rays_trial, &h->D_pose, &h->D_ray, &h->ft, &h->rt, &h->seg_out[0],
-                                    &h->seg_out[1], &h->lm_out[0], &h->lm_out[1], &h->lm_aux, &h->lm_red, &h->sys,
+                                    &h->rays_trial, &h->D_pose, &h->D_ray, &h->ft, &h->rt, &h->seg_ug[0],
+                                    &h->seg_ug[1], &h->lm_out[0], &h->lm_out[1], &h->lm_aux, &h->lm_red, &h->sys,
                                     &h->scal, &h->loc});
   return 0;
 }
@@ -378,7 +387,7 @@ static void tables(ptzba_ctx* h, const double* ptz, const double* rays) {
 
 static void linearize_into(ptzba_ctx* h, int slot) {
   LinArgs a;
-  a.lm_order = h->lm_order.as<int32_t>();
+  a.lm_work = h->lm_order.as<int4>();
   a.n_work = h->n_work;
   a.lm_seg_begin = h->lm_seg_begin.as<int32_t>();
   a.seg_frame = h->seg_frame.as<int32_t>();
@@ -395,7 +404,7 @@ static void linearize_into(ptzba_ctx* h, int slot) {
   a.v = h->v;
   a.fs2 = h->fs * h->fs;
   a.inv_fs2 = 1.0 / (h->fs * h->fs);
-  a.seg_out = h->seg_out[slot].p;
+  a.seg_ug = h->seg_ug[slot].p;
   a.seg_w = h->seg_w[slot].p;
   a.lm_out = h->lm_out[slot].as<double>();
   // landmarks without records keep zero rows
@@ -482,7 +491,7 @@ int ptzba_build_reduced(ptzba_handle h, double lambda) {
   a.seg_lm = h->seg_lm.as<int32_t>();
   a.seg_frame = h->seg_frame.as<int32_t>();
   a.lm_seg_begin = h->lm_seg_begin.as<int32_t>();
-  a.seg_out = h->seg_out[c].p;
+  a.seg_ug = h->seg_ug[c].p;
   a.seg_w = h->seg_w[c].p;
   a.lm_aux = h->lm_aux.as<double>();
   a.S = h->S();
@@ -522,7 +531,7 @@ int ptzba_solve_reduced(ptzba_handle h) {
   BacksubArgs b;
   b.lm_seg_begin = h->lm_seg_begin.as<int32_t>();
   b.seg_frame = h->seg_frame.as<int32_t>();
-  b.seg_out = h->seg_out[c].p;
+  b.seg_w = h->seg_w[c].p;
   b.lm_out = h->lm_out[c].as<double>();
   b.lm_aux = h->lm_aux.as<double>();
   b.D_ray = h->D_ray.as<double>();

@@ -11,7 +11,8 @@
 //   segments  one per unique (landmark, frame): seg_frame, seg_rec_begin (CSR into records);
 //             landmark CSR lm_seg_begin; frame CSR frame_seg_begin/frame_seg_list
 //   tables    FrameTab[n_pose] (cos/sin pan, cos/sin tilt, f), RayTab[n_lm] (ray direction + derivs)
-//   lin       seg_out[n_seg][16] = W(3x2) | U(3x3 sym, 6) | g_pose(3) | pad   (real)
+//   lin       seg_w[n_seg][8]   = W(3x2) | frame id | 0           (real, Schur inner loop + back-subst.)
+//             seg_ug[n_seg][12] = U(3x3 sym, 6) | g_pose(3) | pad   (real, reduced per frame by Schur)
 //             lm_out[n_lm][8]    = V(2x2 sym, 3) | g_ray(2) | cost | pad      (fp64)
 //
 // K1 `k_linearize` is the HBM-streaming kernel: one wave per landmark walks the landmark's records
@@ -66,17 +67,60 @@ void launch_tables(const double* ptz, const double* rays, int n_pose, int n_lm, 
 // ------------------------------------------------------------------------------------------------
 // K1: linearize (residual + Jacobian + per-segment / per-landmark normal-equation blocks + cost)
 // ------------------------------------------------------------------------------------------------
-constexpr int SEGW = 128;  // segments per LDS window per wave
+constexpr int SEGW = 128;    // segments per LDS window per wave
+constexpr int K1_UNROLL = 4;  // record batches in flight per wave
+#ifndef K1_MIN_WAVES
+#define K1_MIN_WAVES 5  // waves per SIMD the register budget must allow (occupancy)
+#endif
+
+// ---- DPP lane shuffles (VALU, no LDS round trip).  Lanes whose source is out of range or whose row
+// is masked off read 0 (bound_ctrl), which the segmented scan treats as "different segment".
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int dpp_i(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, ROWMASK, 0xf, true);
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_r(float x) {
+  return __int_as_float(dpp_i<CTRL, ROWMASK>(__float_as_int(x)));
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_r(double x) {
+  const int lo = dpp_i<CTRL, ROWMASK>(__double2loint(x)), hi = dpp_i<CTRL, ROWMASK>(__double2hiint(x));
+  return __hiloint2double(hi, lo);
+}
+constexpr int DPP_ROW_SHR1 = 0x111, DPP_ROW_SHR2 = 0x112, DPP_ROW_SHR4 = 0x114, DPP_ROW_SHR8 = 0x118;
+constexpr int DPP_ROW_BCAST15 = 0x142, DPP_ROW_BCAST31 = 0x143, DPP_WAVE_SHL1 = 0x130;
+
+// one Kogge-Stone step of the segmented inclusive scan (keys sorted within the wave; kenc >= 1)
+template <int CTRL, int ROWMASK, typename real>
+__device__ __forceinline__ void seg_scan_step(int kenc, real& v0, real& v1, real& v2, real& v3) {
+  const int kk = dpp_i<CTRL, ROWMASK>(kenc);
+  const real t0 = dpp_r<CTRL, ROWMASK>(v0), t1 = dpp_r<CTRL, ROWMASK>(v1);
+  const real t2 = dpp_r<CTRL, ROWMASK>(v2), t3 = dpp_r<CTRL, ROWMASK>(v3);
+  if (kk == kenc) {
+    v0 += t0; v1 += t1; v2 += t2; v3 += t3;
+  }
+}
+
+__device__ __forceinline__ void store4(float* p, float a, float b, float c, float d) {
+  *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+}
+__device__ __forceinline__ void store4(double* p, double a, double b, double c, double d) {
+  reinterpret_cast<double2*>(p)[0] = make_double2(a, b);
+  reinterpret_cast<double2*>(p)[1] = make_double2(c, d);
+}
 
 template <typename real, int LOSS>
-__global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
+__global__ __launch_bounds__(256, K1_MIN_WAVES) void k_linearize(LinArgs a) {
   __shared__ real s_x[4][SEGW], s_y[4][SEGW], s_acc[4][4][SEGW];
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
   const int task = blockIdx.x * 4 + wv;
   if (task >= a.n_work) return;  // whole wave leaves; no block-level barriers in this kernel
-  const int l = a.lm_order[task];
-  const int s0 = a.lm_seg_begin[l], s1 = a.lm_seg_begin[l + 1];
+  // one 16-B work descriptor {landmark, first segment, end segment, first record}: no dependent
+  // lm_order -> lm_seg_begin -> seg_rec_begin chain before the records can be requested
+  const int4 wd = a.lm_work[task];
+  const int l = wd.x, s0 = wd.y, s1 = wd.z;
   const FrameTab<real>* __restrict__ ft = (const FrameTab<real>*)a.ft;
   const RayTab<real> R = ((const RayTab<real>*)a.rt)[l];
   const FrameTab<double>* __restrict__ ft64 = (const FrameTab<double>*)a.ft64;
@@ -84,7 +128,7 @@ __global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
   const double2* __restrict__ seg_base = a.seg_base;
   const real* __restrict__ rec_xy = (const real*)a.rec_xy;
   const real* __restrict__ rec_w = (const real*)a.rec_w;
-  real* __restrict__ seg_out = (real*)a.seg_out;
+  real* __restrict__ seg_ug = (real*)a.seg_ug;
   real* __restrict__ seg_w = (real*)a.seg_w;
   const real u = (real)a.u, v = (real)a.v;
   const real fs2 = (real)a.fs2, ifs2 = (real)a.inv_fs2;
@@ -99,107 +143,130 @@ __global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
 
   for (int w0 = s0; w0 < s1; w0 += SEGW) {
     const int w1 = min(s1, w0 + SEGW);
+    const int64_t r0 = (w0 == s0) ? (int64_t)(uint32_t)wd.w : a.seg_rec_begin[w0];
+    const int64_t r1 = a.seg_rec_begin[w1];
     // phase A: fp64 projection of every segment of the window (lanes over segments), kept as the
-    // offset from the segment's base observation so phase B works on O(residual) magnitudes
-    for (int s = w0 + lane; s < w1; s += WAVE) {
-      const int sl = s - w0;
-      double x, y;
-      ptz_project<double>(ft64[a.seg_frame[s]], R64, a.u, a.v, x, y);
-      const double2 bs = seg_base[s];
-      sx[sl] = (real)(x - bs.x);
-      sy[sl] = (real)(y - bs.y);
-      acc0[sl] = 0; acc1[sl] = 0; acc2[sl] = 0; acc3[sl] = 0;
+    // offset from the segment's base observation so phase B works on O(residual) magnitudes.  The
+    // frame ids stay in registers for phase C.
+    int fsv[SEGW / WAVE];
+#pragma unroll
+    for (int i = 0; i < SEGW / WAVE; ++i) {
+      const int s = w0 + lane + i * WAVE;
+      fsv[i] = 0;
+      if (s < w1) {
+        const int sl = s - w0;
+        const int fs = a.seg_frame[s];
+        fsv[i] = fs;
+        double x, y;
+        ptz_project<double>(ft64[fs], R64, a.u, a.v, x, y);
+        const double2 bs = seg_base[s];
+        sx[sl] = (real)(x - bs.x);
+        sy[sl] = (real)(y - bs.y);
+        acc0[sl] = 0; acc1[sl] = 0; acc2[sl] = 0; acc3[sl] = 0;
+      }
     }
     wave_lds_fence();
-    // phase B: stream the window's records (coalesced), segmented reduction into LDS
-    const int64_t r0 = a.seg_rec_begin[w0], r1 = a.seg_rec_begin[w1];
-    for (int64_t rb = r0; rb < r1; rb += WAVE) {
-      const int64_t r = rb + lane;
-      const bool valid = r < r1;
-      int key = -1;
-      real ox = 0, oy = 0, wt = 0;
-      if (valid) {
-        key = a.rec_seg[r] - w0;
-        if constexpr (sizeof(real) == 4) {
-          float2 o = reinterpret_cast<const float2*>(rec_xy)[r];
-          ox = o.x; oy = o.y;
-        } else {
-          double2 o = reinterpret_cast<const double2*>(rec_xy)[r];
-          ox = o.x; oy = o.y;
-        }
-        wt = rec_w ? rec_w[r] : (real)1;
-      }
-      real rx = 0, ry = 0;
-      if (valid) {
-        rx = sx[key] - ox;
-        ry = sy[key] - oy;
-      }
-      real wx, wy, c;
-      if constexpr (LOSS == 0) {
-        wx = wt; wy = wt;
-        c = wt * (rx * rx + ry * ry);
-      } else {
-        // scipy 'huber': rho(z) = z (z<=1), 2 sqrt(z) - 1; weight rho'(z) = 1 or 1/sqrt(z)
-        real zx = rx * rx * ifs2, zy = ry * ry * ifs2;
-        real sqx = sqrt(zx), sqy = sqrt(zy);
-        bool ix = zx <= (real)1, iy = zy <= (real)1;
-        wx = ix ? wt : wt / sqx;
-        wy = iy ? wt : wt / sqy;
-        c = wt * fs2 * ((ix ? zx : (real)2 * sqx - (real)1) + (iy ? zy : (real)2 * sqy - (real)1));
-      }
-      cost += (double)c;
-      real v0 = wx, v1 = wy, v2 = wx * rx, v3 = wy * ry;
-      // segmented inclusive scan over the wave, segments = runs of equal key (records are sorted)
+    // phase B: stream the window's records (coalesced), segmented reduction into LDS.  Four 64-record
+    // batches are loaded before any is consumed, so each wave keeps 4x the bytes in flight.
+    for (int64_t rb = r0; rb < r1; rb += K1_UNROLL * WAVE) {
+      int keyu[K1_UNROLL];
+      real oxu[K1_UNROLL], oyu[K1_UNROLL], wtu[K1_UNROLL];
 #pragma unroll
-      for (int d = 1; d < WAVE; d <<= 1) {
-        int kk = __shfl_up(key, d, WAVE);
-        real t0 = __shfl_up(v0, d, WAVE);
-        real t1 = __shfl_up(v1, d, WAVE);
-        real t2 = __shfl_up(v2, d, WAVE);
-        real t3 = __shfl_up(v3, d, WAVE);
-        if (lane >= d && kk == key) {
-          v0 += t0; v1 += t1; v2 += t2; v3 += t3;
+      for (int u = 0; u < K1_UNROLL; ++u) {
+        const int64_t r = rb + u * WAVE + lane;
+        keyu[u] = -1;
+        oxu[u] = 0; oyu[u] = 0; wtu[u] = 0;
+        if (r < r1) {
+          keyu[u] = a.rec_seg[r] - w0;
+          if constexpr (sizeof(real) == 4) {
+            const float2 o = reinterpret_cast<const float2*>(rec_xy)[r];
+            oxu[u] = o.x; oyu[u] = o.y;
+          } else {
+            const double2 o = reinterpret_cast<const double2*>(rec_xy)[r];
+            oxu[u] = o.x; oyu[u] = o.y;
+          }
+          wtu[u] = rec_w ? rec_w[r] : (real)1;
         }
       }
-      int knext = __shfl_down(key, 1, WAVE);
-      bool last = (lane == WAVE - 1) || (knext != key);
-      if (valid && last) {  // one writer per run per chunk; runs crossing chunks add in order
-        acc0[key] += v0; acc1[key] += v1; acc2[key] += v2; acc3[key] += v3;
+#pragma unroll
+      for (int u = 0; u < K1_UNROLL; ++u) {
+        if (rb + u * WAVE >= r1) break;  // wave-uniform
+        const int key = keyu[u];
+        const bool valid = key >= 0;
+        real rx = 0, ry = 0;
+        if (valid) {
+          rx = sx[key] - oxu[u];
+          ry = sy[key] - oyu[u];
+        }
+        const real wt = wtu[u];
+        real wx, wy, c;
+        if constexpr (LOSS == 0) {
+          wx = wt; wy = wt;
+          c = wt * (rx * rx + ry * ry);
+        } else {
+          // scipy 'huber': rho(z) = z (z<=1), 2 sqrt(z) - 1; weight rho'(z) = 1 or 1/sqrt(z)
+          real zx = rx * rx * ifs2, zy = ry * ry * ifs2;
+          bool ix = zx <= (real)1, iy = zy <= (real)1;
+          real sqx, sqy;
+          if constexpr (sizeof(real) == 4) {  // v_rsq_f32: 1 ulp, no IEEE divide in the record loop
+            const real rsx = __builtin_amdgcn_rsqf(ix ? (real)1 : zx), rsy = __builtin_amdgcn_rsqf(iy ? (real)1 : zy);
+            sqx = zx * rsx; sqy = zy * rsy;
+            wx = ix ? wt : wt * rsx;
+            wy = iy ? wt : wt * rsy;
+          } else {
+            sqx = sqrt(zx); sqy = sqrt(zy);
+            wx = ix ? wt : wt / sqx;
+            wy = iy ? wt : wt / sqy;
+          }
+          c = wt * fs2 * ((ix ? zx : (real)2 * sqx - (real)1) + (iy ? zy : (real)2 * sqy - (real)1));
+        }
+        cost += (double)c;
+        real v0 = wx, v1 = wy, v2 = wx * rx, v3 = wy * ry;
+        // segmented inclusive scan over the wave, segments = runs of equal key (records are sorted):
+        // shifts 1, 2, 4, 8 inside each 16-lane row, then row 15 -> rows 1, 3 and lane 31 -> rows 2, 3
+        const int kenc = key + 2;  // >= 1; 0 is what a masked / out-of-row DPP source reads
+        seg_scan_step<DPP_ROW_SHR1, 0xf>(kenc, v0, v1, v2, v3);
+        seg_scan_step<DPP_ROW_SHR2, 0xf>(kenc, v0, v1, v2, v3);
+        seg_scan_step<DPP_ROW_SHR4, 0xf>(kenc, v0, v1, v2, v3);
+        seg_scan_step<DPP_ROW_SHR8, 0xf>(kenc, v0, v1, v2, v3);
+        seg_scan_step<DPP_ROW_BCAST15, 0xa>(kenc, v0, v1, v2, v3);
+        seg_scan_step<DPP_ROW_BCAST31, 0xc>(kenc, v0, v1, v2, v3);
+        const int knext = dpp_i<DPP_WAVE_SHL1, 0xf>(kenc);  // lane 63 reads 0
+        const bool last = knext != kenc;
+        if (valid && last) {  // one writer per run per batch; runs crossing batches add in order
+          acc0[key] += v0; acc1[key] += v1; acc2[key] += v2; acc3[key] += v3;
+        }
       }
     }
     wave_lds_fence();
     // phase C: per-segment Jacobian and normal-equation blocks
-    for (int s = w0 + lane; s < w1; s += WAVE) {
+#pragma unroll
+    for (int i = 0; i < SEGW / WAVE; ++i) {
+      const int s = w0 + lane + i * WAVE;
+      if (s >= w1) break;
       const int sl = s - w0;
       real x, y, J[2][5];
-      const int fs = a.seg_frame[s];
+      const int fs = fsv[i];
       ptz_project_jac<real>(ft[fs], R, u, v, x, y, J);
       const real Sx = acc0[sl], Sy = acc1[sl], Srx = acc2[sl], Sry = acc3[sl];
-      real* o = seg_out + (int64_t)s * 16;
-      // W = Jp^T diag(Sx,Sy) Jr  (3x2)
+      // W = Jp^T diag(Sx,Sy) Jr (3x2), U = Jp^T diag Jp (upper: 00 01 02 11 12 22), g_pose = Jp^T (w r)
+      real W[6];
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
-        o[2 * p + 0] = Sx * J[0][p] * J[0][3] + Sy * J[1][p] * J[1][3];
-        o[2 * p + 1] = Sx * J[0][p] * J[0][4] + Sy * J[1][p] * J[1][4];
+        W[2 * p + 0] = Sx * J[0][p] * J[0][3] + Sy * J[1][p] * J[1][3];
+        W[2 * p + 1] = Sx * J[0][p] * J[0][4] + Sy * J[1][p] * J[1][4];
       }
-      // U = Jp^T diag Jp (upper: 00 01 02 11 12 22)
-      o[6] = Sx * J[0][0] * J[0][0] + Sy * J[1][0] * J[1][0];
-      o[7] = Sx * J[0][0] * J[0][1] + Sy * J[1][0] * J[1][1];
-      o[8] = Sx * J[0][0] * J[0][2] + Sy * J[1][0] * J[1][2];
-      o[9] = Sx * J[0][1] * J[0][1] + Sy * J[1][1] * J[1][1];
-      o[10] = Sx * J[0][1] * J[0][2] + Sy * J[1][1] * J[1][2];
-      o[11] = Sx * J[0][2] * J[0][2] + Sy * J[1][2] * J[1][2];
-      // g_pose = Jp^T (w r)
-      o[12] = J[0][0] * Srx + J[1][0] * Sry;
-      o[13] = J[0][1] * Srx + J[1][1] * Sry;
-      o[14] = J[0][2] * Srx + J[1][2] * Sry;
-      o[15] = 0;
-      // compact copy for the Schur kernel's inner loop: {W (6), frame id, 0} = 32 B (fp32) / 64 B (fp64)
+      // seg_w[8] = {W (6), frame id, 0}: the Schur kernel's inner-loop record and the back-substitution's W
       real* cw = seg_w + (int64_t)s * 8;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) cw[k] = o[k];
-      cw[6] = __int_as_real<real>(fs);
-      cw[7] = 0;
+      store4(cw, W[0], W[1], W[2], W[3]);
+      store4(cw + 4, W[4], W[5], __int_as_real<real>(fs), (real)0);
+      // seg_ug[12] = {U (6), g_pose (3), 0, 0, 0}: reduced per frame by the Schur kernel
+      real* o = seg_ug + (int64_t)s * 12;
+      store4(o, Sx * J[0][0] * J[0][0] + Sy * J[1][0] * J[1][0], Sx * J[0][0] * J[0][1] + Sy * J[1][0] * J[1][1],
+             Sx * J[0][0] * J[0][2] + Sy * J[1][0] * J[1][2], Sx * J[0][1] * J[0][1] + Sy * J[1][1] * J[1][1]);
+      store4(o + 4, Sx * J[0][1] * J[0][2] + Sy * J[1][1] * J[1][2], Sx * J[0][2] * J[0][2] + Sy * J[1][2] * J[1][2],
+             J[0][0] * Srx + J[1][0] * Sry, J[0][1] * Srx + J[1][1] * Sry);
+      store4(o + 8, J[0][2] * Srx + J[1][2] * Sry, (real)0, (real)0, (real)0);
       V00 += (double)(Sx * J[0][3] * J[0][3] + Sy * J[1][3] * J[1][3]);
       V01 += (double)(Sx * J[0][3] * J[0][4] + Sy * J[1][3] * J[1][4]);
       V11 += (double)(Sx * J[0][4] * J[0][4] + Sy * J[1][4] * J[1][4]);
@@ -306,7 +373,7 @@ __global__ __launch_bounds__(1024) void k_schur(SchurArgs a) {
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
   const int half = lane >> 5, hl = lane & 31;
-  const real* __restrict__ seg_out = (const real*)a.seg_out;
+  const real* __restrict__ seg_ug = (const real*)a.seg_ug;
   const real* __restrict__ seg_w = (const real*)a.seg_w;
   const int e0 = a.frame_seg_begin[f1], e1 = a.frame_seg_begin[f1 + 1];
   const int ne = e1 - e0;
@@ -334,7 +401,7 @@ __global__ __launch_bounds__(1024) void k_schur(SchurArgs a) {
         s1 = a.frame_seg_list[e];
         const int l = a.seg_lm[s1];
         send = a.lm_seg_begin[l + 1];
-        const real* w1 = seg_out + (int64_t)s1 * 16;
+        const real* w1 = seg_w + (int64_t)s1 * 8;
         const double* vi = a.lm_aux + (int64_t)l * 8;
         const double i00 = vi[0], i01 = vi[1], i11 = vi[2];
 #pragma unroll
@@ -345,10 +412,11 @@ __global__ __launch_bounds__(1024) void k_schur(SchurArgs a) {
           if (first) ab[q] += W0 * vi[3] + W1 * vi[4];
         }
         if (first) {
+          const real* u1 = seg_ug + (int64_t)s1 * 12;
 #pragma unroll
-          for (int k = 0; k < 6; ++k) aU[k] += (double)w1[6 + k];
+          for (int k = 0; k < 6; ++k) aU[k] += (double)u1[k];
 #pragma unroll
-          for (int q = 0; q < 3; ++q) ag[q] += (double)w1[12 + q];
+          for (int q = 0; q < 3; ++q) ag[q] += (double)u1[6 + q];
         }
       }
       const int n = min(WAVE, ee - cb);
@@ -476,13 +544,13 @@ __global__ __launch_bounds__(256) void k_backsub(BacksubArgs a) {
   const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (l >= a.n_lm) return;
   const int s0 = a.lm_seg_begin[l], s1 = a.lm_seg_begin[l + 1];
-  const real* __restrict__ seg_out = (const real*)a.seg_out;
+  const real* __restrict__ seg_w = (const real*)a.seg_w;
   double t0 = 0, t1 = 0;
   for (int s = s0 + lane; s < s1; s += WAVE) {
     const int f = a.seg_frame[s];
     if (f < a.n_fixed) continue;
     const double* dp = a.dpose + 3 * (f - a.n_fixed);
-    const real* w = seg_out + (int64_t)s * 16;
+    const real* w = seg_w + (int64_t)s * 8;
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       t0 += (double)w[2 * q] * dp[q];

@@ -6,7 +6,7 @@
 namespace ptzba {
 
 struct LinArgs {
-  const int32_t* lm_order;       // [n_work] landmarks to process, heaviest first
+  const int4* lm_work;           // [n_work] {landmark, s0, s1, first record}, heaviest first
   int n_work;
   const int32_t* lm_seg_begin;   // [n_lm+1]
   const int32_t* seg_frame;      // [n_seg]
@@ -20,7 +20,7 @@ struct LinArgs {
   const void* rt64;              // RayTab<double>[n_lm]
   const double2* seg_base;       // [n_seg] base observation; records hold obs - base (real)
   double u, v, fs2, inv_fs2;
-  void* seg_out;                 // [n_seg][16] real
+  void* seg_ug;                  // [n_seg][12] real: U (6) | g_pose (3) | 0 0 0
   void* seg_w;                   // [n_seg][8] real: W (6) | frame id bits | 0
   double* lm_out;                // [n_lm][8]
 };
@@ -32,7 +32,7 @@ struct SchurArgs {
   const int32_t* seg_lm;           // [n_seg]
   const int32_t* seg_frame;        // [n_seg]
   const int32_t* lm_seg_begin;     // [n_lm+1]
-  const void* seg_out;             // [n_seg][16] real
+  const void* seg_ug;              // [n_seg][12] real: U | g_pose
   const void* seg_w;               // [n_seg][8] real compact W + frame
   const double* lm_aux;            // [n_lm][8]
   double* S;                       // [ld][ld] lower, row-major
@@ -46,7 +46,7 @@ struct SchurArgs {
 struct BacksubArgs {
   const int32_t* lm_seg_begin;
   const int32_t* seg_frame;
-  const void* seg_out;
+  const void* seg_w;     // [n_seg][8] real: W | frame
   const double* lm_out;
   const double* lm_aux;
   const double* D_ray;
