@@ -139,6 +139,9 @@ def main():
     frame, landmark, xy, w = prob.frame, prob.landmark, prob.xy, None
     if a.form == "dedup":
         frame, landmark, xy, w, _ = synthetic.dedup_records(frame, landmark, xy)
+    # the coupling window of the WHOLE problem: every rank passes the same one, so all ranks choose the
+    # same system order and take bit-identical pose steps
+    win_hi = ptzba.frame_coupling_window(prob.n_pose, frame, landmark)
     if world > 1:
         sel = shard_by_landmark(landmark, prob.n_landmark, rank, world)
         frame, landmark, xy = frame[sel], landmark[sel], xy[sel]
@@ -149,8 +152,9 @@ def main():
     stream = torch.cuda.current_stream()
     h.set_stream(stream.cuda_stream)
     h.set_problem(prob.n_pose, prob.n_landmark, frame, landmark, xy, prob.u, prob.v, weight=w, precision=precision,
-                  loss=loss, f_scale=1.0)
+                  loss=loss, f_scale=1.0, frame_win_hi=win_hi)
     info = h.info()
+    sinfo = h.solver_info()
 
     allreduce = None
     if world > 1:
@@ -242,6 +246,7 @@ def main():
                        "n_keyframes": prob.n_pose, "n_landmarks": prob.n_landmark, "n_records": int(len(prob.frame)),
                        "n_matches": int(prob.n_match), "n_pairs": prob.n_pairs, "form": a.form,
                        "parallelism": f"landmark-sharded x{world}" if world > 1 else "single GPU",
+                       "reduced_system": sinfo,
                        "iterations_timed": iters, "solves_timed": solves},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_linearize (K1)",

@@ -47,12 +47,19 @@ enum { PTZBA_FP64 = 0, PTZBA_FP32 = 1 };
 /* loss (scipy least_squares `loss=`): linear, or huber with f_scale */
 enum { PTZBA_LOSS_LINEAR = 0, PTZBA_LOSS_HUBER = 1 };
 
+/* ordering of the reduced camera system: natural frame order, or one level of nested dissection
+ * (left block | right block reversed | separator) when it shortens the factorisation's critical path */
+enum { PTZBA_ORDER_NATURAL = 0, PTZBA_ORDER_NESTED = 1, PTZBA_ORDER_NESTED_FORCE = 2 /* tests */ };
+
 typedef struct {
-    int32_t precision; /* PTZBA_FP64 | PTZBA_FP32 */
-    int32_t loss;      /* PTZBA_LOSS_LINEAR | PTZBA_LOSS_HUBER */
-    double f_scale;    /* huber scale (scipy f_scale); ignored for linear */
-    int32_t n_fixed;   /* number of leading fixed (gauge) frames; the reference fixes frame 0 -> 1 */
-    int32_t reserved;
+    int32_t precision;             /* PTZBA_FP64 | PTZBA_FP32 */
+    int32_t loss;                  /* PTZBA_LOSS_LINEAR | PTZBA_LOSS_HUBER */
+    double f_scale;                /* huber scale (scipy f_scale); ignored for linear */
+    int32_t n_fixed;               /* number of leading fixed (gauge) frames; the reference fixes frame 0 -> 1 */
+    int32_t ordering;              /* PTZBA_ORDER_NATURAL | PTZBA_ORDER_NESTED */
+    const int32_t* frame_win_hi;   /* optional [n_pose]: highest frame sharing a landmark with each frame,
+                                      over ALL records of a sharded problem; every rank must pass the same
+                                      array so all ranks pick the same system order.  NULL: local records */
 } ptzba_problem_opts;
 
 /* per-iteration scalars read back after ptzba_step (all fp64):
@@ -83,6 +90,9 @@ PTZBA_EXPORT int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_lan
  * [4] reduced-system size [5] landmarks with observations [6] max segments per landmark
  * [7] bytes of device memory held */
 PTZBA_EXPORT int ptzba_problem_info(ptzba_handle h, int64_t* info8);
+/* solver layout: [0] n_aug (system rows incl. padding), [1] ld, [2] factorisation launches (levels),
+ * [3] ordering actually used (PTZBA_ORDER_*) */
+PTZBA_EXPORT int ptzba_solver_info(ptzba_handle h, int64_t* info4);
 
 /* residual r[2*n_obs] = projection - observation, record order (== _compute_residual) at
  * x_full = [3*n_pose poses | 2*n_landmark rays] (fp64 host). Uses the handle's precision. */

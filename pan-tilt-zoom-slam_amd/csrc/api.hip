@@ -59,8 +59,11 @@ struct ptzba_ctx {
   DBuf scal, loc, info;
   DBuf scal_pack;               // device block [scal 8 | loc 8 | info]
   double* scal_host = nullptr;   // pinned host copy of scal_pack
-  DBuf chol_tasks, chol_colfirst, chol_rowend, Ldiag, dpose;
-  std::vector<int> chol_task_off;  // host: per tile column, offsets into chol_tasks
+  DBuf chol_tasks, Ldiag, dpose;
+  std::vector<int> chol_task_off;  // host: per elimination level, offsets into chol_tasks
+  int chol_levels = 0, n_aug = 0, n_chain = 1;
+  bool nested = false;
+  DBuf frame_pos, row_pad, bs_chain_off, bs_chain_cols, bs_col_off, bs_col_tiles;
   double lambda = 0;
   // timing
   bool timing = false;
@@ -150,50 +153,194 @@ static int upload(DBuf& b, const std::vector<T>& v) {
   return 0;
 }
 
-// Envelope of the reduced camera system and the per-step task lists of the fused Cholesky.
-// Block column f1 holds rows of frames f2 in [f1, win_hi[f1]] (k_schur), so row-frame f2's first
-// non-zero column frame is lo(f2) = min{ f1 : win_hi[f1] >= f2 }.
-static int build_chol_plan(ptzba_ctx* h, const std::vector<int32_t>& win_hi) {
-  const int nf = h->n_fixed, n = h->n_sys;
-  const int T = (int)(h->ld / CHOL_NB);
-  std::vector<int> lo(h->n_pose, 0);
-  for (int f2 = nf; f2 < h->n_pose; ++f2) {
-    int f = f2;
-    for (int f1 = nf; f1 <= f2; ++f1)
-      if (win_hi[f1] >= f2) { f = f1; break; }
-    lo[f2] = f;
-  }
-  std::vector<int> colfirst(T, 0), rowend(T, 0);
-  for (int i = 0; i < T; ++i) {
-    int cf = i;
-    for (int r = i * CHOL_NB; r < (i + 1) * CHOL_NB; ++r) {
-      if (r < n) cf = std::min(cf, 3 * (lo[r / 3 + nf] - nf) / CHOL_NB);
-      else if (r == n) cf = 0;  // augmented right-hand-side row is dense
+// ------------------------------------------------------------------------------------------------
+// system order of the reduced camera system and the tile-level factorisation plan
+// ------------------------------------------------------------------------------------------------
+static int pad_tile(int x) { return (x + CHOL_NB - 1) / CHOL_NB * CHOL_NB; }
+
+struct SysOrder {
+  std::vector<int32_t> pos;  // [n_pose] system row of the frame's pan (-1: fixed)
+  std::vector<uint8_t> pad;  // [n_aug] identity padding rows
+  int n_aug = 0;
+  bool nested = false;
+  int tiles_a = 0, tiles_b = 0;  // nested: tile columns of parts A and B (C follows)
+};
+
+static SysOrder natural_order(int n_pose, int nf) {
+  SysOrder o;
+  o.pos.assign(n_pose, -1);
+  for (int f = nf; f < n_pose; ++f) o.pos[f] = 3 * (f - nf);
+  o.n_aug = 3 * (n_pose - nf);
+  o.pad.assign(o.n_aug, 0);
+  return o;
+}
+
+// One level of nested dissection of the frame chain: A = [nf, m), separator C = [m, c_end) with
+// c_end past every frame A couples to, B = [c_end, n_pose) (decoupled from A).  System order
+// [A | B reversed | C], each part padded to whole tiles: A and B factor side by side, their couplings
+// to C are eliminated last, and the back-substitution splits into two chains after C.  Chosen only when
+// it shortens the critical path of tile columns.
+static bool nested_order(int n_pose, int nf, const std::vector<int32_t>& win, SysOrder& o, bool force) {
+  const int nfree = n_pose - nf;
+  if (nfree < (force ? 3 : 16)) return false;
+  std::vector<int> pmax(n_pose + 1, -1);
+  for (int f = nf; f < n_pose; ++f) pmax[f + 1] = std::max(pmax[f], (int)win[f]);
+  const int nat = pad_tile(3 * nfree + 1) / CHOL_NB;
+  int best_m = -1, best = nat;
+  (void)force;
+  for (int m = nf + 1; m < n_pose; ++m) {
+    const int cend = std::max(m, pmax[m] + 1);
+    if (cend >= n_pose) break;
+    const int ta = pad_tile(3 * (m - nf)) / CHOL_NB, tb = pad_tile(3 * (n_pose - cend)) / CHOL_NB;
+    const int tc = pad_tile(3 * (cend - m)) / CHOL_NB;
+    const int chain = std::max(ta, tb) + tc + 1;
+    if (chain < best) {
+      best = chain;
+      best_m = m;
     }
-    colfirst[i] = cf;
   }
-  for (int kt = 0; kt < T; ++kt) {
-    int last = kt;
-    for (int i = kt; i < T; ++i)
-      if (colfirst[i] <= kt) last = i;
-    rowend[kt] = std::min(n, (last + 1) * CHOL_NB);
+  if (force) {  // testing: the most balanced split with a non-empty B, whatever the gain
+    best_m = -1;
+    int bal = INT32_MAX;
+    for (int m = nf + 1; m < n_pose; ++m) {
+      const int cend = std::max(m, pmax[m] + 1);
+      if (cend >= n_pose) break;
+      const int d = std::abs((m - nf) - (n_pose - cend));
+      if (d < bal) { bal = d; best_m = m; }
+    }
   }
-  std::vector<int> tasks;
-  h->chol_task_off.assign(T + 1, 0);
+  if (best_m < 0 || (!force && best + 2 > nat)) return false;
+  const int m = best_m, cend = std::max(m, pmax[m] + 1);
+  const int ar = 3 * (m - nf), br = 3 * (n_pose - cend), cr = 3 * (cend - m);
+  const int ap = pad_tile(ar), bp = pad_tile(br), cp = pad_tile(cr);
+  o.pos.assign(n_pose, -1);
+  for (int f = nf; f < m; ++f) o.pos[f] = 3 * (f - nf);
+  for (int f = n_pose - 1; f >= cend; --f) o.pos[f] = ap + 3 * (n_pose - 1 - f);
+  for (int f = m; f < cend; ++f) o.pos[f] = ap + bp + 3 * (f - m);
+  o.n_aug = ap + bp + cp;
+  o.pad.assign(o.n_aug, 0);
+  for (int r = ar; r < ap; ++r) o.pad[r] = 1;
+  for (int r = ap + br; r < ap + bp; ++r) o.pad[r] = 1;
+  for (int r = ap + bp + cr; r < o.n_aug; ++r) o.pad[r] = 1;
+  o.nested = true;
+  o.tiles_a = ap / CHOL_NB;
+  o.tiles_b = bp / CHOL_NB;
+  return true;
+}
+
+struct CholPlan {
+  std::vector<int32_t> tasks;  // int4 records
+  std::vector<int> level_off;
+  std::vector<int> chain_off, chain_cols, col_off, col_tiles;
+  int n_levels = 0;
+};
+
+// Tile structure (coupled frame pairs + the dense augmented row + symbolic fill), elimination levels
+// (at most two tile columns per level), tasks per level and back-substitution chains.
+static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<int32_t>& win, int64_t ld, CholPlan& P) {
+  const int T = (int)(ld / CHOL_NB);
+  std::vector<std::vector<uint8_t>> nz(T, std::vector<uint8_t>(T, 0));
+  auto mark = [&](int r, int c) {
+    int ti = r / CHOL_NB, tj = c / CHOL_NB;
+    if (ti < tj) std::swap(ti, tj);
+    nz[ti][tj] = 1;
+  };
+  for (int f1 = nf; f1 < n_pose; ++f1)
+    for (int f2 = f1; f2 <= std::min(n_pose - 1, (int)win[f1]); ++f2) {
+      const int p1 = o.pos[f1], p2 = o.pos[f2];
+      mark(p2, p1); mark(p2 + 2, p1); mark(p2, p1 + 2); mark(p2 + 2, p1 + 2);
+    }
+  const int ta = o.n_aug / CHOL_NB;  // tile holding the augmented row
+  for (int j = 0; j <= ta; ++j) nz[ta][j] = 1;
+  for (int i = 0; i < T; ++i) nz[i][i] = 1;
+  for (int k = 0; k < T; ++k) {  // symbolic fill
+    std::vector<int> R;
+    for (int i = k + 1; i < T; ++i)
+      if (nz[i][k]) R.push_back(i);
+    for (size_t x = 0; x < R.size(); ++x)
+      for (size_t y = 0; y <= x; ++y) nz[R[x]][R[y]] = 1;
+  }
+  std::vector<int> level(T, 0), count;
   for (int k = 0; k < T; ++k) {
-    h->chol_task_off[k] = (int)tasks.size();
-    for (int i = k; i < T; ++i)
-      if (colfirst[i] <= k) tasks.push_back((i << 15) | k);
-    if (k > 0)
-      for (int i = k + 1; i < T; ++i) {
-        if (colfirst[i] > k - 1) continue;
-        for (int j = k + 1; j <= i; ++j)
-          if (colfirst[j] <= k - 1) tasks.push_back((1 << 30) | (i << 15) | j);
-      }
+    int L = 0;
+    for (int p = 0; p < k; ++p)
+      if (nz[k][p]) L = std::max(L, level[p] + 1);
+    while (L < (int)count.size() && count[L] >= 2) ++L;  // at most two columns per launch
+    if (L >= (int)count.size()) count.resize(L + 1, 0);
+    count[L]++;
+    level[k] = L;
   }
-  h->chol_task_off[T] = (int)tasks.size();
-  if (upload(h->chol_tasks, tasks) || upload(h->chol_colfirst, colfirst) || upload(h->chol_rowend, rowend)) return -1;
-  return 0;
+  const int nL = (int)count.size();
+  std::vector<std::vector<int>> K(nL);
+  for (int k = 0; k < T; ++k) K[level[k]].push_back(k);
+  P.tasks.clear();
+  P.level_off.assign(nL + 1, 0);
+  auto push = [&](int type, int i, int j, int w) {
+    P.tasks.push_back(type); P.tasks.push_back(i); P.tasks.push_back(j); P.tasks.push_back(w);
+  };
+  for (int L = 0; L < nL; ++L) {
+    P.level_off[L] = (int)(P.tasks.size() / 4);
+    const std::vector<int> none;
+    const std::vector<int>& prev = L > 0 ? K[L - 1] : none;
+    for (int k : K[L]) {
+      std::vector<int> pd;
+      for (int pp : prev)
+        if (pp < k && nz[k][pp]) pd.push_back(pp);
+      for (int i = k; i < T; ++i) {
+        if (!nz[i][k]) continue;
+        int tm = 0;
+        for (size_t u = 0; u < pd.size(); ++u)
+          if (i == k || nz[i][pd[u]]) tm |= 1 << u;
+        push(0, i, k, chol_pack_updates(pd.size() > 0 ? pd[0] : -1, pd.size() > 1 ? pd[1] : -1, tm));
+      }
+    }
+    // trailing updates from the previous level's panels into tiles of columns factored later
+    std::vector<std::pair<int64_t, int>> upd;  // (tile key, panel)
+    for (int pp : prev) {
+      std::vector<int> R;
+      for (int i = pp + 1; i < T; ++i)
+        if (nz[i][pp]) R.push_back(i);
+      for (size_t x = 0; x < R.size(); ++x)
+        for (size_t y = 0; y <= x; ++y)
+          if (level[R[y]] > L) upd.push_back({(int64_t)R[x] * T + R[y], pp});
+    }
+    std::sort(upd.begin(), upd.end());
+    for (size_t x = 0; x < upd.size();) {
+      size_t y = x + 1;
+      while (y < upd.size() && upd[y].first == upd[x].first) ++y;
+      const int i = (int)(upd[x].first / T), j = (int)(upd[x].first % T);
+      push(1, i, j, chol_pack_updates(upd[x].second, y - x > 1 ? upd[x + 1].second : -1, 3));
+      x = y;
+    }
+  }
+  P.level_off[nL] = (int)(P.tasks.size() / 4);
+  P.n_levels = nL;
+  // back-substitution: tile columns holding unknowns, their nonzero row tiles, chains
+  const int Tx = (o.n_aug + CHOL_NB - 1) / CHOL_NB;
+  P.col_off.assign(T + 1, 0);
+  P.col_tiles.clear();
+  for (int kt = 0; kt < T; ++kt) {
+    P.col_off[kt] = (int)P.col_tiles.size();
+    if (kt < Tx)
+      for (int i = kt + 1; i < Tx; ++i)
+        if (nz[i][kt]) P.col_tiles.push_back(i);
+  }
+  P.col_off[T] = (int)P.col_tiles.size();
+  P.chain_off.assign(1, 0);
+  P.chain_cols.clear();
+  if (o.nested) {
+    const int c0 = o.tiles_a + o.tiles_b;
+    for (int part = 0; part < 2; ++part) {
+      for (int kt = Tx - 1; kt >= c0; --kt) P.chain_cols.push_back(kt);
+      const int lo = part == 0 ? 0 : o.tiles_a, hi = part == 0 ? o.tiles_a : c0;
+      for (int kt = hi - 1; kt >= lo; --kt) P.chain_cols.push_back(kt);
+      P.chain_off.push_back((int)P.chain_cols.size());
+    }
+  } else {
+    for (int kt = Tx - 1; kt >= 0; --kt) P.chain_cols.push_back(kt);
+    P.chain_off.push_back((int)P.chain_cols.size());
+  }
+  return true;
 }
 
 int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_t n_obs, const int32_t* obs_frame,
@@ -202,12 +349,16 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   if (!h) return fail("null handle");
   if (n_pose < 1 || n_landmark < 0 || n_obs < 0) return fail("bad sizes n_pose=%d n_landmark=%d n_obs=%lld", n_pose, n_landmark, (long long)n_obs);
   if (n_obs > 0 && (!obs_frame || !obs_landmark || !obs_xy)) return fail("null observation pointer");
-  ptzba_problem_opts o{PTZBA_FP64, PTZBA_LOSS_LINEAR, 1.0, 1, 0};
+  ptzba_problem_opts o{PTZBA_FP64, PTZBA_LOSS_LINEAR, 1.0, 1, PTZBA_ORDER_NESTED, nullptr};
   if (opts) o = *opts;
   if (o.precision != PTZBA_FP64 && o.precision != PTZBA_FP32) return fail("bad precision %d", o.precision);
   if (o.loss != PTZBA_LOSS_LINEAR && o.loss != PTZBA_LOSS_HUBER) return fail("bad loss %d", o.loss);
   if (o.n_fixed < 0 || o.n_fixed > n_pose) return fail("bad n_fixed %d", o.n_fixed);
   if (o.loss == PTZBA_LOSS_HUBER && !(o.f_scale > 0)) return fail("huber needs f_scale > 0");
+  if (o.ordering < PTZBA_ORDER_NATURAL || o.ordering > PTZBA_ORDER_NESTED_FORCE) return fail("bad ordering %d", o.ordering);
+  if (o.frame_win_hi)
+    for (int f = 0; f < n_pose; ++f)
+      if (o.frame_win_hi[f] < f || o.frame_win_hi[f] >= n_pose) return fail("frame_win_hi[%d] = %d out of range", f, o.frame_win_hi[f]);
   for (int64_t r = 0; r < n_obs; ++r) {
     if (obs_frame[r] < 0 || obs_frame[r] >= n_pose) return fail("record %lld: frame %d out of range", (long long)r, obs_frame[r]);
     if (obs_landmark[r] < 0 || obs_landmark[r] >= n_landmark)
@@ -305,8 +456,25 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     lm_work[4 * k + 3] = (int32_t)seg_rec_begin[lm_seg_begin[l]];
   }
   h->n_sys = 3 * (n_pose - o.n_fixed);
-  h->ld = ((int64_t)h->n_sys + 1 + CHOL_NB - 1) / CHOL_NB * CHOL_NB;  // + augmented rhs row
-  if (h->ld > 20000) return fail("reduced system %d too large for the dense solver", h->n_sys);
+  // system order and factorisation plan (from the coupling window; a sharded problem passes the global one)
+  std::vector<int32_t> win(frame_win_hi);
+  if (o.frame_win_hi)
+    for (int f = 0; f < n_pose; ++f) win[f] = std::max(win[f], o.frame_win_hi[f]);
+  SysOrder sorder;
+  if (!(o.ordering != PTZBA_ORDER_NATURAL &&
+        nested_order(n_pose, o.n_fixed, win, sorder, o.ordering == PTZBA_ORDER_NESTED_FORCE)))
+    sorder = natural_order(n_pose, o.n_fixed);
+  h->n_aug = sorder.n_aug;
+  h->nested = sorder.nested;
+  h->ld = pad_tile(h->n_aug + 1);  // + augmented rhs row
+  // the back-substitution keeps x ([ld] doubles) in LDS next to 17 KiB of staging
+  if (h->ld > 17408) return fail("reduced system %d too large for the dense solver", h->n_sys);
+  CholPlan plan;
+  make_plan(sorder, n_pose, o.n_fixed, win, h->ld, plan);
+  h->chol_task_off = plan.level_off;
+  h->chol_levels = plan.n_levels;
+  h->n_chain = (int)plan.chain_off.size() - 1;
+  frame_win_hi = win;  // K2 windows follow the same (possibly global) coupling
   h->perm_host = order;
   h->perm_uploaded = false;
 
@@ -339,7 +507,10 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       h->scal.alloc(PTZBA_NSCALARS * 8) || h->red_scratch.alloc(RED_SCRATCH * 8) || h->loc.alloc(PTZBA_NSCALARS * 8) || h->info.alloc(16) ||
       h->Ldiag.alloc((size_t)h->ld * CHOL_NB * 8) || h->dpose.alloc((size_t)h->ld * 8))
     return -1;
-  if (build_chol_plan(h, frame_win_hi)) return -1;
+  if (upload(h->chol_tasks, plan.tasks) || upload(h->frame_pos, sorder.pos) || upload(h->row_pad, sorder.pad) ||
+      upload(h->bs_chain_off, plan.chain_off) || upload(h->bs_chain_cols, plan.chain_cols) ||
+      upload(h->bs_col_off, plan.col_off) || upload(h->bs_col_tiles, plan.col_tiles))
+    return -1;
   HIPCHK(hipMemset(h->D_pose.p, 0, h->D_pose.bytes));
   HIPCHK(hipMemset(h->D_ray.p, 0, h->D_ray.bytes));
   HIPCHK(hipMemset(h->ptz.p, 0, h->ptz.bytes));
@@ -415,6 +586,15 @@ static void linearize_into(ptzba_ctx* h, int slot) {
   else
     launch_linearize<double>(a, h->loss, h->st);
   tm_end(h, TM_K1);
+}
+
+int ptzba_solver_info(ptzba_handle h, int64_t* info4) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  info4[0] = h->n_aug;
+  info4[1] = h->ld;
+  info4[2] = h->chol_levels;
+  info4[3] = h->nested ? PTZBA_ORDER_NESTED : PTZBA_ORDER_NATURAL;
+  return 0;
 }
 
 int ptzba_residual(ptzba_handle h, const double* x_full, double* r_out) {
@@ -494,6 +674,7 @@ int ptzba_build_reduced(ptzba_handle h, double lambda) {
   a.seg_ug = h->seg_ug[c].p;
   a.seg_w = h->seg_w[c].p;
   a.lm_aux = h->lm_aux.as<double>();
+  a.frame_pos = h->frame_pos.as<int32_t>();
   a.S = h->S();
   a.b = h->bvec();
   a.g_pose = h->gpose();
@@ -516,17 +697,20 @@ int ptzba_solve_reduced(ptzba_handle h) {
   const int c = h->cur, nx = 1 - c;
   const int n_free = h->n_pose - h->n_fixed;
   tm_begin(h, TM_CHOL);
-  launch_pose_damp(h->S(), h->ld, h->dU(), h->D_pose.as<double>(), h->n_pose, h->n_fixed, h->lambda, h->st);
-  launch_chol_prepare(h->S(), h->ld, h->n_sys, h->bvec(), h->info.as<int>(), h->st);
-  launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int>(), h->chol_task_off.data(), h->chol_colfirst.as<int>(),
+  launch_pose_damp(h->S(), h->ld, h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
+                   h->lambda, h->st);
+  launch_chol_prepare(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(), h->st);
+  launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
                   h->Ldiag.as<double>(), h->info.as<int>(), h->st);
-  launch_chol_backsolve(h->S(), h->ld, h->n_sys, h->chol_rowend.as<int>(), h->Ldiag.as<double>(), h->dpose.as<double>(),
+  launch_chol_backsolve(h->S(), h->ld, h->n_aug, h->n_chain, h->bs_chain_off.as<int>(), h->bs_chain_cols.as<int>(),
+                        h->bs_col_off.as<int>(), h->bs_col_tiles.as<int>(), h->Ldiag.as<double>(), h->dpose.as<double>(),
                         h->st);
   tm_end(h, TM_CHOL);
   HIPCHK(hipGetLastError());
   tm_begin(h, TM_BACK);
   HIPCHK(hipMemsetAsync(h->loc.p, 0, h->loc.bytes, h->st));
-  launch_pose_trial(h->ptz.as<double>(), h->dpose.as<double>(), h->gpose(), h->D_pose.as<double>(), h->ptz_trial.as<double>(),
+  launch_pose_trial(h->ptz.as<double>(), h->dpose.as<double>(), h->gpose(), h->D_pose.as<double>(),
+                    h->frame_pos.as<int32_t>(), h->ptz_trial.as<double>(),
                     h->n_pose, h->n_fixed, h->lambda, h->loc.as<double>(), h->st);
   BacksubArgs b;
   b.lm_seg_begin = h->lm_seg_begin.as<int32_t>();
@@ -536,6 +720,7 @@ int ptzba_solve_reduced(ptzba_handle h) {
   b.lm_aux = h->lm_aux.as<double>();
   b.D_ray = h->D_ray.as<double>();
   b.dpose = h->dpose.as<double>();
+  b.frame_pos = h->frame_pos.as<int32_t>();
   b.rays = h->rays.as<double>();
   b.rays_trial = h->rays_trial.as<double>();
   b.lm_red = h->lm_red.as<double>();

@@ -380,7 +380,7 @@ __global__ __launch_bounds__(1024) void k_schur(SchurArgs a) {
   const int eb = e0 + (int)(((int64_t)ne * wv) / SCHUR_WAVES);
   const int ee = e0 + (int)(((int64_t)ne * (wv + 1)) / SCHUR_WAVES);
   const int hi = a.frame_win_hi[f1];
-  const int col0 = 3 * (f1 - a.n_fixed);
+  const int col0 = a.frame_pos[f1];  // system row/column of f1's pan
   const int64_t ld = a.ld;
 
   double aU[6] = {0, 0, 0, 0, 0, 0}, ag[3] = {0, 0, 0}, ab[3] = {0, 0, 0};
@@ -498,11 +498,13 @@ __global__ __launch_bounds__(1024) void k_schur(SchurArgs a) {
       a.dU[col0 + 2] = U[5];
     }
     __syncthreads();
-    // write block column f1, rows of frames in [p0, p1): S[row(f2)+r][col0+q] = S_{f1,f2}[q][r]
+    // write block (f2, f1) for frames f2 in [p0, p1) into the lower triangle of the system order:
+    // S[pos(f2)+r][pos(f1)+q] = S_{f1,f2}[q][r], or its mirror when f2 precedes f1 in that order
     for (int k = threadIdx.x; k < width * 9; k += blockDim.x) {
       const int t = k / 9, qr = k % 9, q = qr / 3, r = qr % 3;
-      const int64_t row = 3 * (p0 + t - a.n_fixed) + r;
-      a.S[row * ld + col0 + q] = s_S[k];
+      const int64_t pf2 = a.frame_pos[p0 + t];
+      if (pf2 >= col0) a.S[(pf2 + r) * ld + col0 + q] = s_S[k];
+      else a.S[(int64_t)(col0 + q) * ld + pf2 + r] = s_S[k];
     }
     __syncthreads();
   }
@@ -516,20 +518,25 @@ void launch_schur(const SchurArgs& a, int n_free, hipStream_t st) {
 
 // pose damping on the exchanged reduced system: D = max(D, diag U) (monotone), S_ii += lambda D_i
 __global__ void k_pose_damp(double* __restrict__ S, int64_t ld, const double* __restrict__ dU,
-                            double* __restrict__ D_pose, int n_pose, int n_fixed, double lambda) {
+                            double* __restrict__ D_pose, const int32_t* __restrict__ frame_pos, int n_pose,
+                            int n_fixed, double lambda) {
   int k = blockIdx.x * blockDim.x + threadIdx.x;
   int n = 3 * (n_pose - n_fixed);
   if (k >= n) return;
+  const int f = n_fixed + k / 3;
+  const int64_t row = frame_pos[f] + k % 3;
   double* D = D_pose + 3 * n_fixed + k;
-  double d = fmax(*D, fmax(dU[k], 1e-12));
+  double d = fmax(*D, fmax(dU[row], 1e-12));
   *D = d;
-  S[(int64_t)k * ld + k] += lambda * d;
+  S[row * ld + row] += lambda * d;
 }
 
-void launch_pose_damp(double* S, int64_t ld, const double* dU, double* D_pose, int n_pose, int n_fixed, double lambda,
-                      hipStream_t st) {
+void launch_pose_damp(double* S, int64_t ld, const double* dU, double* D_pose, const int32_t* frame_pos, int n_pose,
+                      int n_fixed, double lambda, hipStream_t st) {
   int n = 3 * (n_pose - n_fixed);
-  if (n > 0) hipLaunchKernelGGL(k_pose_damp, dim3((n + 255) / 256), dim3(256), 0, st, S, ld, dU, D_pose, n_pose, n_fixed, lambda);
+  if (n > 0)
+    hipLaunchKernelGGL(k_pose_damp, dim3((n + 255) / 256), dim3(256), 0, st, S, ld, dU, D_pose, frame_pos, n_pose,
+                       n_fixed, lambda);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -549,7 +556,7 @@ __global__ __launch_bounds__(256) void k_backsub(BacksubArgs a) {
   for (int s = s0 + lane; s < s1; s += WAVE) {
     const int f = a.seg_frame[s];
     if (f < a.n_fixed) continue;
-    const double* dp = a.dpose + 3 * (f - a.n_fixed);
+    const double* dp = a.dpose + a.frame_pos[f];
     const real* w = seg_w + (int64_t)s * 8;
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -592,7 +599,7 @@ void launch_backsub(const BacksubArgs& a, hipStream_t st) {
 // pose trial + pose partials (identical on every rank): one block
 __global__ void k_pose_trial(const double* __restrict__ ptz, const double* __restrict__ dpose,
                              const double* __restrict__ g_pose, const double* __restrict__ D_pose,
-                             double* __restrict__ ptz_trial, int n_pose, int n_fixed, double lambda,
+                             const int32_t* __restrict__ frame_pos, double* __restrict__ ptz_trial, int n_pose, int n_fixed, double lambda,
                              double* __restrict__ out4) {
   __shared__ double red[4][1024 / WAVE];
   double pr = 0, dx = 0, xx = 0, gm = 0;
@@ -604,7 +611,7 @@ __global__ void k_pose_trial(const double* __restrict__ ptz, const double* __res
       ptz_trial[i] = x;
       continue;
     }
-    const int k = i - 3 * n_fixed;
+    const int k = frame_pos[f] + (i - 3 * f);  // system row
     const double d = dpose[k];
     ptz_trial[i] = x + d;
     pr += -0.5 * g_pose[k] * d + 0.5 * lambda * D_pose[i] * d * d;
@@ -626,9 +633,10 @@ __global__ void k_pose_trial(const double* __restrict__ ptz, const double* __res
 }
 
 void launch_pose_trial(const double* ptz, const double* dpose, const double* g_pose, const double* D_pose,
-                       double* ptz_trial, int n_pose, int n_fixed, double lambda, double* out4, hipStream_t st) {
-  hipLaunchKernelGGL(k_pose_trial, dim3(1), dim3(1024), 0, st, ptz, dpose, g_pose, D_pose, ptz_trial, n_pose,
-                     n_fixed, lambda, out4);
+                       const int32_t* frame_pos, double* ptz_trial, int n_pose, int n_fixed, double lambda, double* out4,
+                       hipStream_t st) {
+  hipLaunchKernelGGL(k_pose_trial, dim3(1), dim3(1024), 0, st, ptz, dpose, g_pose, D_pose, frame_pos, ptz_trial,
+                     n_pose, n_fixed, lambda, out4);
 }
 
 // deterministic strided reduction: out[k] = sum_i src[i*stride + k] (fixed order), k < nk;

@@ -1,21 +1,25 @@
-// Dense fp64 Cholesky solve of the reduced camera system (gfx950).
+// Dense-tile fp64 Cholesky solve of the reduced camera system (gfx950).
 //
-// The reduced camera system S (3(N-1) x 3(N-1), SPD, block-banded: keyframes couple only to pan
-// neighbours) replaces scipy's dense SVD of the full Jacobian (trf.py:467 via bundle_adjustment.py:200).
+// The reduced camera system S (SPD, block-banded: keyframes couple only to pan neighbours) replaces
+// scipy's dense SVD of the full Jacobian (trf.py:467 via bundle_adjustment.py:200).
 //
-// Storage: row-major [ld][ld] lower triangle, ld = roundup(n + 1, 32).  Row n holds b^T (augmented
-// right-hand side) with a huge diagonal, so row n of the factor is y = L^-1 b: the forward
-// substitution comes out of the factorisation for free.  Rows > n are identity padding.
+// Storage: row-major [ld][ld] lower triangle in the solver's system order (api.hip: natural frame
+// order, or nested dissection [A | B reversed | C] with each part padded to whole 32-row tiles;
+// padding rows are identity).  Row n_aug holds b^T (augmented right-hand side) with a huge diagonal,
+// so row n_aug of the factor is y = L^-1 b: the forward substitution comes out of the factorisation.
 //
-// Factorisation: 32x32 tiles, ONE launch per tile column k ("delayed update"):
-//   panel task (i, k):  T_ik <- A_ik - L_{i,k-1} L_{k,k-1}^T,  D <- A_kk - L_{k,k-1} L_{k,k-1}^T,
-//                       factor D in one wave (rows in registers, pivot column broadcast via LDS),
-//                       L_ik = T_ik L_kk^-T (lane per row, forward substitution)   [i == k: write L_kk]
-//   trailing task (i, j), i >= j > k:  A_ij <- A_ij - L_{i,k-1} L_{j,k-1}^T
-// Panel k-1's update reaches every tile exactly once (column k through the panel tasks, columns > k
-// through the trailing tasks of the same launch), so one launch per column suffices.  Only tiles
-// inside the profile (envelope) of S are visited; the envelope of L equals that of S.
-// Back substitution L^T x = y: one 1024-thread workgroup, 32-column steps, envelope-limited.
+// Factorisation: 32x32 tiles, one launch per LEVEL of the tile-column elimination tree ("delayed
+// update"; natural order = one column per level, nested dissection = the A and B chains side by side).
+// A task carries its tile (i, j) and up to two update panels p from the previous level:
+//   panel task (i, k):   D <- A_kk - sum_p L_kp L_kp^T,  T <- A_ik - sum_p L_ip L_kp^T,
+//                        then one wave factors D and solves L_ik = T L_kk^-T in the same sweep
+//                        (wave_potrf_trsm32)   [i == k: L_kk -> Ldiag]
+//   trailing task (i,j): A_ij <- A_ij - sum_p L_ip L_jp^T   (column j is factored at a later level)
+// Every update (i, j, p) is applied exactly once, at the level after p's: by the trailing tasks, or by
+// column j's panel tasks when j is factored at that very level.  Only structurally nonzero tiles
+// (symbolic fill on the tile graph) are visited.
+// Back substitution L^T x = y: one 1024-thread workgroup per chain of tile columns (nested
+// dissection: C then A, C then B), dot products over each column's nonzero row tiles.
 #include "ptzba_common.h"
 #include "ptzba_kernels.h"
 
@@ -30,17 +34,22 @@ __device__ __forceinline__ double bcast(double v, int j) {
   return __hiloint2double(hi, lo);
 }
 
-// augmented row / padding: A[n][j] = b[j], A[n][n] = huge, A[i][i] = 1 for i > n
-__global__ void k_chol_prepare(double* __restrict__ A, int64_t ld, int n, const double* __restrict__ b, int* info) {
+// augmented row / padding: A[n][j] = b[j], A[n][n] = huge, A[i][i] = 1 for padding rows (pad[i], i < n)
+// and for every row after n
+__global__ void k_chol_prepare(double* __restrict__ A, int64_t ld, int n, const double* __restrict__ b,
+                               const uint8_t* __restrict__ pad, int* info) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) info[0] = 0;
-  if (i < n) A[(int64_t)n * ld + i] = b[i];
+  if (i < n) {
+    A[(int64_t)n * ld + i] = b[i];
+    if (pad && pad[i]) A[i * ld + i] = 1.0;
+  }
   if (i == n) A[i * ld + i] = AUG_DIAG;
   if (i > n && i < ld) A[i * ld + i] = 1.0;
 }
 
-void launch_chol_prepare(double* A, int64_t ld, int n, double* b, int* info, hipStream_t st) {
-  hipLaunchKernelGGL(k_chol_prepare, dim3((unsigned)((ld + 255) / 256)), dim3(256), 0, st, A, ld, n, b, info);
+void launch_chol_prepare(double* A, int64_t ld, int n, double* b, const uint8_t* pad, int* info, hipStream_t st) {
+  hipLaunchKernelGGL(k_chol_prepare, dim3((unsigned)((ld + 255) / 256)), dim3(256), 0, st, A, ld, n, b, pad, info);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -124,18 +133,20 @@ __device__ __forceinline__ void wave_potrf_trsm32(double (*D)[NB + 1], double (*
   wave_lds_fence();
 }
 
-__global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64_t ld, int k,
-                                                   const int* __restrict__ tasks, const int* __restrict__ colfirst,
-                                                   double* __restrict__ Ldiag, int* info) {
+__global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64_t ld,
+                                                   const int4* __restrict__ tasks, double* __restrict__ Ldiag,
+                                                   int* info) {
   __shared__ double sC[NB][NB + 1];  // target tile (panel T_ik / trailing A_ij)
   __shared__ double sD[NB][NB + 1];  // diagonal tile -> L_kk
-  __shared__ double sA[NB][NB + 1];  // L_{i,k-1}
-  __shared__ double sB[NB][NB + 1];  // L_{k,k-1} or L_{j,k-1}
+  __shared__ double sA[NB][NB + 1];  // L_ip
+  __shared__ double sB[NB][NB + 1];  // L_kp or L_jp
   __shared__ double rdg[NB];
-  const int task = tasks[blockIdx.x];
-  const int type = task >> 30;
-  const int i = (task >> 15) & 0x7fff;
-  const int j = task & 0x7fff;
+  const int4 tk = tasks[blockIdx.x];
+  const int type = tk.x, i = tk.y, j = tk.z;
+  int up[2];
+  up[0] = (tk.w & 0x3fff) - 1;
+  up[1] = ((tk.w >> 14) & 0x3fff) - 1;
+  const int tmask = (tk.w >> 28) & 3;  // panel: which updates also apply to T
   const int64_t NBl = NB;
 #ifndef CHOL_VARIANT
 #define CHOL_VARIANT 0
@@ -144,30 +155,41 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
 #if CHOL_VARIANT == 3
     return;
 #endif
-    // trailing: A_ij -= L_{i,k-1} L_{j,k-1}^T
+    // trailing: A_ij -= sum_p L_ip L_jp^T
     double* C = A + i * NBl * ld + j * NBl;
     load_tile(sC, C, ld);
-    load_tile(sA, A + i * NBl * ld + (k - 1) * NBl, ld);
-    load_tile(sB, A + j * NBl * ld + (k - 1) * NBl, ld);
-    __syncthreads();
-    tile_gemm_nt_sub(sC, sA, sB);
-    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int pp = up[u];
+      if (pp < 0) continue;
+      load_tile(sA, A + i * NBl * ld + pp * NBl, ld);
+      load_tile(sB, A + j * NBl * ld + pp * NBl, ld);
+      __syncthreads();
+      tile_gemm_nt_sub(sC, sA, sB);
+      __syncthreads();
+    }
     for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) C[(int64_t)(e >> 5) * ld + (e & 31)] = sC[e >> 5][e & 31];
     return;
   }
-  // panel task (i, k)
+  // panel task (i, k = j)
+  const int k = j;
   const bool diag_only = (i == k);
-  const bool upd_k = (k > 0) && colfirst[k] <= k - 1;
-  const bool upd_i = (k > 0) && colfirst[i] <= k - 1;
   load_tile(sD, A + (int64_t)k * NBl * ld + k * NBl, ld);
   if (!diag_only) load_tile(sC, A + i * NBl * ld + k * NBl, ld);
-  if (upd_k) load_tile(sB, A + (int64_t)k * NBl * ld + (k - 1) * NBl, ld);
-  if (upd_i && !diag_only) load_tile(sA, A + i * NBl * ld + (k - 1) * NBl, ld);
-  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int pp = up[u];
+    if (pp < 0) continue;
+    const bool updT = !diag_only && ((tmask >> u) & 1);
+    load_tile(sB, A + (int64_t)k * NBl * ld + pp * NBl, ld);
+    if (updT) load_tile(sA, A + i * NBl * ld + pp * NBl, ld);
+    __syncthreads();
 #if CHOL_VARIANT != 4
-  if (upd_k) tile_gemm_nt_sub(sD, sB, sB);
-  if (upd_k && upd_i && !diag_only) tile_gemm_nt_sub(sC, sA, sB);
+    tile_gemm_nt_sub(sD, sB, sB);
+    if (updT) tile_gemm_nt_sub(sC, sA, sB);
 #endif
+    __syncthreads();
+  }
   __syncthreads();
 #if CHOL_VARIANT != 1
   if (threadIdx.x < WAVE) wave_potrf_trsm32(sD, diag_only ? nullptr : sC, rdg, info);
@@ -179,54 +201,59 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
     for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) C[e] = sD[e >> 5][e & 31];
     return;
   }
-  __syncthreads();
   double* C = A + i * NBl * ld + k * NBl;
   for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) C[(int64_t)(e >> 5) * ld + (e & 31)] = sC[e >> 5][e & 31];
 }
 
-void launch_cholesky(double* A, int64_t ld, const int* tasks, const int* task_off_host, const int* colfirst,
-                     double* Ldiag, int* info, hipStream_t st) {
-  const int T = (int)(ld / NB);
-  for (int k = 0; k < T; ++k) {
-    const int n = task_off_host[k + 1] - task_off_host[k];
+void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_off_host, int n_launch, double* Ldiag,
+                     int* info, hipStream_t st) {
+  for (int L = 0; L < n_launch; ++L) {
+    const int n = task_off_host[L + 1] - task_off_host[L];
     if (n > 0)
-      hipLaunchKernelGGL(k_chol_step, dim3(n), dim3(256), 0, st, A, ld, k, tasks + task_off_host[k], colfirst, Ldiag,
-                         info);
+      hipLaunchKernelGGL(k_chol_step, dim3(n), dim3(256), 0, st, A, ld, tasks + task_off_host[L], Ldiag, info);
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// back substitution L^T x = y with y = row n of the factor; x written to xout[0..n)
+// back substitution L^T x = y with y = row n of the factor; x written to xout[0..n).  Workgroup c
+// walks chain c (tile columns in processing order); column kt's dot products run over its nonzero row
+// tiles col_tiles[col_off[kt] .. col_off[kt+1]) (all below kt).  Chains that share tile columns
+// (the nested-dissection separator) compute them identically.
 __global__ __launch_bounds__(1024) void k_chol_backsolve(const double* __restrict__ L, int64_t ld, int n,
-                                                         const int* __restrict__ rowend,
+                                                         const int* __restrict__ chain_off,
+                                                         const int* __restrict__ chain_cols,
+                                                         const int* __restrict__ col_off,
+                                                         const int* __restrict__ col_tiles,
                                                          const double* __restrict__ Ldiag, double* __restrict__ xout) {
   extern __shared__ __attribute__((aligned(16))) double xv[];  // [ld]
   __shared__ double part[32][NB + 1];
   __shared__ double Lkk[NB][NB + 1];
   const int t = threadIdx.x;
   const int c = t & 31, sub = t >> 5;
-  const int Tn = (n + NB - 1) / NB;
-  // y = row n of the factor: off-diagonal tiles in place, the last partial tile in Ldiag
+  // y = row n of the factor: off-diagonal tiles in place, the tile holding row n in Ldiag
   const int tn = n / NB, rn = n - tn * NB;
   for (int i = t; i < ld; i += blockDim.x)
     xv[i] = (i >= n) ? 0.0 : (i < tn * NB ? L[(int64_t)n * ld + i] : Ldiag[((int64_t)tn * NB + rn) * NB + (i - tn * NB)]);
   __syncthreads();
-  for (int kt = Tn - 1; kt >= 0; --kt) {
+  const int q0 = chain_off[blockIdx.x], q1 = chain_off[blockIdx.x + 1];
+  for (int q = q0; q < q1; ++q) {
+    const int kt = chain_cols[q];
     const int64_t c0 = (int64_t)kt * NB;
-    // stage L_kk and the envelope-limited column-block dot products (a register prefetch of the next
-    // tile column during the solve measured slower: 333 vs 258 us at config3)
     Lkk[t >> 5][t & 31] = Ldiag[(int64_t)kt * NB * NB + t];
     double s = 0;
-    const int r1 = min(rowend[kt], n);
+    const int e0 = col_off[kt], nrow = (col_off[kt + 1] - e0) * NB;
 #pragma unroll 4
-    for (int i = (int)c0 + NB + sub; i < r1; i += 32) s += L[(int64_t)i * ld + c0 + c] * xv[i];
+    for (int rr = sub; rr < nrow; rr += 32) {
+      const int64_t i = (int64_t)col_tiles[e0 + (rr >> 5)] * NB + (rr & 31);
+      s += L[i * ld + c0 + c] * xv[i];
+    }
     part[sub][c] = s;
     __syncthreads();
     if (t < WAVE) {
       const int lane = t;
       double tr = 0;
       if (lane < NB) {
-        for (int q = 0; q < 32; ++q) tr += part[q][lane];
+        for (int qq = 0; qq < 32; ++qq) tr += part[qq][lane];
         tr = xv[c0 + lane] - tr;
       }
       // upper-triangular solve L_kk^T x = tr, lane r holds tr_r
@@ -237,17 +264,19 @@ __global__ __launch_bounds__(1024) void k_chol_backsolve(const double* __restric
         if (lane == jj) tr = tj;
         if (lane < jj) tr -= Lkk[jj][lane] * tj;
       }
-      if (lane < NB && c0 + lane < n) xv[c0 + lane] = tr;
+      if (lane < NB && c0 + lane < n) {
+        xv[c0 + lane] = tr;
+        xout[c0 + lane] = tr;
+      }
     }
     __syncthreads();
   }
-  for (int i = t; i < n; i += blockDim.x) xout[i] = xv[i];
 }
 
-void launch_chol_backsolve(const double* L, int64_t ld, int n, const int* rowend, const double* Ldiag, double* xout,
-                           hipStream_t st) {
-  hipLaunchKernelGGL(k_chol_backsolve, dim3(1), dim3(1024), (size_t)ld * sizeof(double), st, L, ld, n, rowend, Ldiag,
-                     xout);
+void launch_chol_backsolve(const double* L, int64_t ld, int n, int n_chain, const int* chain_off, const int* chain_cols,
+                           const int* col_off, const int* col_tiles, const double* Ldiag, double* xout, hipStream_t st) {
+  hipLaunchKernelGGL(k_chol_backsolve, dim3(n_chain), dim3(1024), (size_t)ld * sizeof(double), st, L, ld, n, chain_off,
+                     chain_cols, col_off, col_tiles, Ldiag, xout);
 }
 
 }  // namespace ptzba

@@ -210,11 +210,11 @@ struct ptzekf_ctx {
   int n_ray = 0;
   DBuf rays[2], cov[2];
   int cur = 0;
-  DBuf pred_xy, vis, obs_xy, idx, Hc, yv, M, tasks, colfirst, Ldiag, info, ky3;
+  DBuf pred_xy, vis, obs_xy, idx, Hc, yv, M, tasks, Ldiag, info, ky3;
   std::vector<uint8_t> vis_h;
   std::vector<int> task_off;
   int64_t plan_ld = -1;
-  int plan_mp = -1;
+  int plan_mp = -1, n_launch = 0;
   int64_t ns() const { return 3 + 2 * (int64_t)n_ray; }
 };
 
@@ -226,29 +226,26 @@ static Disp make_disp(const double* d6, int& has) {
   return D;
 }
 
-// task list of the partial factorisation: tile columns 0..Tm-1 (panel + trailing), then one
-// flush launch applying panel Tm-1 to the trailing block (tiles i >= j >= Tm)
+// task list of the partial factorisation: tile columns 0..Tm-1 (panel + trailing, each updated by
+// the previous column), then one flush launch applying panel Tm-1 to the trailing block (i >= j >= Tm)
 static int build_partial_plan(ptzekf_ctx* h, int64_t ld, int mp) {
   if (h->plan_ld == ld && h->plan_mp == mp) return 0;
   const int T = (int)(ld / CHOL_NB), Tm = mp / CHOL_NB;
-  std::vector<int> tasks;
-  h->task_off.assign(T + 1, 0);
-  for (int k = 0; k < T; ++k) {
+  std::vector<int4> tasks;
+  h->task_off.assign(Tm + 2, 0);
+  for (int k = 0; k <= Tm; ++k) {
     h->task_off[k] = (int)tasks.size();
-    if (k < Tm) {
-      for (int i = k; i < T; ++i) tasks.push_back((0 << 30) | (i << 15) | k);
-      if (k >= 1)
-        for (int j = k + 1; j < T; ++j)
-          for (int i = j; i < T; ++i) tasks.push_back((1 << 30) | (i << 15) | j);
-    } else if (k == Tm) {
-      for (int j = Tm; j < T; ++j)
-        for (int i = j; i < T; ++i) tasks.push_back((1 << 30) | (i << 15) | j);
-    }
+    const int w = chol_pack_updates(k - 1, -1, 1);  // k == 0: no update panel
+    if (k < Tm)
+      for (int i = k; i < T; ++i) tasks.push_back(make_int4(0, i, k, w));
+    if (k >= 1)
+      for (int j = (k < Tm ? k + 1 : Tm); j < T; ++j)
+        for (int i = j; i < T; ++i) tasks.push_back(make_int4(1, i, j, w));
   }
-  h->task_off[T] = (int)tasks.size();
-  if (h->tasks.reserve(tasks.size() * 4 + 4) || h->colfirst.reserve((size_t)T * 4)) return -1;
-  HIPCHK(hipMemcpy(h->tasks.p, tasks.data(), tasks.size() * 4, hipMemcpyHostToDevice));
-  HIPCHK(hipMemset(h->colfirst.p, 0, (size_t)T * 4));
+  h->task_off[Tm + 1] = (int)tasks.size();
+  h->n_launch = Tm + 1;
+  if (h->tasks.reserve(tasks.size() * sizeof(int4) + 16)) return -1;
+  HIPCHK(hipMemcpy(h->tasks.p, tasks.data(), tasks.size() * sizeof(int4), hipMemcpyHostToDevice));
   h->plan_ld = ld;
   h->plan_mp = mp;
   return 0;
@@ -489,7 +486,7 @@ int ptzekf_update(ptzekf_handle h, double u, double v, const double* disp6, doub
                      h->Hc.as<double>(), h->yv.as<double>(), observe_var, M);
   HIPCHK(hipGetLastError());
   // 4. partial factorisation through the S columns (+ flush of the trailing update)
-  launch_cholesky(M, d.ld, h->tasks.as<int>(), h->task_off.data(), h->colfirst.as<int>(), h->Ldiag.as<double>(),
+  launch_cholesky(M, d.ld, h->tasks.as<int4>(), h->task_off.data(), h->n_launch, h->Ldiag.as<double>(),
                   h->info.as<int>(), h->st);
   HIPCHK(hipGetLastError());
   // 5. state update and covariance write-back (skipped on the device when S was not SPD)

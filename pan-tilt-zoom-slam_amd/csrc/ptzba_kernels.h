@@ -35,6 +35,7 @@ struct SchurArgs {
   const void* seg_ug;              // [n_seg][12] real: U | g_pose
   const void* seg_w;               // [n_seg][8] real compact W + frame
   const double* lm_aux;            // [n_lm][8]
+  const int32_t* frame_pos;        // [n_pose] system row of the frame's pan (-1: fixed)
   double* S;                       // [ld][ld] lower, row-major
   double* b;                       // [n_sys]
   double* g_pose;                  // [n_sys]
@@ -50,7 +51,8 @@ struct BacksubArgs {
   const double* lm_out;
   const double* lm_aux;
   const double* D_ray;
-  const double* dpose;   // [n_sys]
+  const double* dpose;   // [n_aug] system order
+  const int32_t* frame_pos;
   const double* rays;    // [2 n_lm]
   double* rays_trial;    // [2 n_lm]
   double* lm_red;        // [n_lm][4]: pred, |d|^2, |x|^2, |g|max
@@ -68,11 +70,13 @@ void launch_landmark_damp(const double* lm_out, const int32_t* lm_seg_begin, dou
                           double lambda, hipStream_t st);
 template <typename real>
 void launch_schur(const SchurArgs& a, int n_free, hipStream_t st);
-void launch_pose_damp(double* S, int64_t ld, const double* dU, double* D_pose, int n_pose, int n_fixed, double lambda,
+void launch_pose_damp(double* S, int64_t ld, const double* dU, double* D_pose, const int32_t* frame_pos, int n_pose,
+                      int n_fixed, double lambda,
                       hipStream_t st);
 template <typename real>
 void launch_backsub(const BacksubArgs& a, hipStream_t st);
 void launch_pose_trial(const double* ptz, const double* dpose, const double* g_pose, const double* D_pose,
+                       const int32_t* frame_pos,
                        double* ptz_trial, int n_pose, int n_fixed, double lambda, double* out4, hipStream_t st);
 // scratch: RED_SCRATCH doubles (partials + counter), zero-initialised once, reused across calls
 constexpr int RED_SCRATCH = 64 * 8 + 2;
@@ -85,16 +89,19 @@ void launch_residual(const int32_t* rec_seg, const int32_t* seg_frame, const int
                      const void* rec_xy, const int64_t* perm, const void* ft64, const void* rt64, double u, double v,
                      int64_t n_rec, double* r_out, hipStream_t st);
 
-// dense SPD solve of the reduced camera system (chol_kernels.hip)
-// A: [ld][ld] row-major fp64, lower triangle of S (n x n), ld = roundup(n + 1, CHOL_NB).
-// prepare: row n <- b^T (augmented), A[n][n] huge, identity padding.  cholesky: one launch per tile
-// column over the host-built envelope task lists.  backsolve: x = S^-1 b into xout.
+// dense-tile SPD solve of the reduced camera system (chol_kernels.hip)
+// A: [ld][ld] row-major fp64, lower triangle of S in system order (n = n_aug rows incl. padding),
+// ld = roundup(n + 1, CHOL_NB).  prepare: row n <- b^T (augmented), A[n][n] huge, identity on padding
+// rows.  cholesky: one launch per elimination level over host-built int4 tasks
+// {type, i, j, packed update panels}.  backsolve: x = S^-1 b into xout, one workgroup per chain.
 constexpr int CHOL_NB = 32;
-void launch_chol_prepare(double* A, int64_t ld, int n, double* b, int* info, hipStream_t st);
-void launch_cholesky(double* A, int64_t ld, const int* tasks, const int* task_off_host, const int* colfirst,
-                     double* Ldiag, int* info, hipStream_t st);
-void launch_chol_backsolve(const double* L, int64_t ld, int n, const int* rowend, const double* Ldiag, double* xout,
-                           hipStream_t st);
+void launch_chol_prepare(double* A, int64_t ld, int n, double* b, const uint8_t* pad, int* info, hipStream_t st);
+void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_off_host, int n_launch, double* Ldiag,
+                     int* info, hipStream_t st);
+void launch_chol_backsolve(const double* L, int64_t ld, int n, int n_chain, const int* chain_off, const int* chain_cols,
+                           const int* col_off, const int* col_tiles, const double* Ldiag, double* xout, hipStream_t st);
+// task word w: bits 0-13 update panel p1 + 1, bits 14-27 p2 + 1 (0 = none), bits 28/29: p1/p2 also update T
+inline int chol_pack_updates(int p1, int p2, int tmask) { return (p1 + 1) | ((p2 + 1) << 14) | (tmask << 28); }
 
 // camera batch kernels (camera_kernels.hip)
 void launch_ray_to_image(int64_t n, double u, double v, const double* f, const double* cp, const double* ct,

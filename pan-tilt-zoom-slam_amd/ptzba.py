@@ -32,9 +32,12 @@ NSCALARS = 8
 _lib = None
 
 
+ORDER_NATURAL, ORDER_NESTED, ORDER_NESTED_FORCE = 0, 1, 2
+
+
 class ptzba_problem_opts(Structure):
     _fields_ = [("precision", c_int32), ("loss", c_int32), ("f_scale", c_double), ("n_fixed", c_int32),
-                ("reserved", c_int32)]
+                ("ordering", c_int32), ("frame_win_hi", c_void_p)]
 
 
 def _ptr(a):
@@ -59,6 +62,7 @@ def lib():
         "ptzba_set_stream": ([V, V], I),
         "ptzba_set_problem": ([V, I32, I32, I64, V, V, V, V, D, D, POINTER(ptzba_problem_opts)], I),
         "ptzba_problem_info": ([V, V], I),
+        "ptzba_solver_info": ([V, V], I),
         "ptzba_residual": ([V, V, V], I),
         "ptzba_set_state": ([V, V, V], I),
         "ptzba_get_state": ([V, V, V], I),
@@ -99,7 +103,7 @@ def lib():
 
 EXPORTED_SYMBOLS = [
     "ptzba_new", "ptzba_delete", "ptzba_last_error", "ptzba_version", "ptzba_set_stream", "ptzba_set_problem",
-    "ptzba_problem_info", "ptzba_residual", "ptzba_set_state", "ptzba_get_state", "ptzba_linearize",
+    "ptzba_problem_info", "ptzba_solver_info", "ptzba_residual", "ptzba_set_state", "ptzba_get_state", "ptzba_linearize",
     "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_read_scalars", "ptzba_accept",
     "ptzba_exchange", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptz_ray_to_image",
     "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks",
@@ -211,6 +215,20 @@ def build_landmarks(kp_count, pairs):
 # ---------------------------------------------------------------------------------------------
 # BA handle
 # ---------------------------------------------------------------------------------------------
+def frame_coupling_window(n_pose, frame, landmark):
+    """Highest frame sharing a landmark with each frame (>= the frame itself): the coupling window
+    ptzba_set_problem derives from its own records.  Computed on the full record set it is the
+    `frame_win_hi` every rank of a sharded solve passes, so all ranks choose the same system order."""
+    frame = np.asarray(frame, np.int64)
+    landmark = np.asarray(landmark, np.int64)
+    n_lm = int(landmark.max()) + 1 if len(landmark) else 0
+    lm_hi = np.full(n_lm, -1, np.int64)
+    np.maximum.at(lm_hi, landmark, frame)
+    win = np.arange(n_pose, dtype=np.int64)
+    np.maximum.at(win, frame, lm_hi[landmark])
+    return win.astype(np.int32)
+
+
 class BAHandle:
     """One device-resident BA problem (opaque C handle, rf_map_wrapper.RFMap style)."""
 
@@ -237,7 +255,9 @@ class BAHandle:
         _check(lib().ptzba_set_stream(self.h, c_void_p(stream_ptr or 0)), "ptzba_set_stream")
 
     def set_problem(self, n_pose, n_landmark, frame, landmark, xy, u, v, weight=None, precision=FP64,
-                    loss=LOSS_LINEAR, f_scale=1.0, n_fixed=1):
+                    loss=LOSS_LINEAR, f_scale=1.0, n_fixed=1, ordering=ORDER_NESTED, frame_win_hi=None):
+        """frame_win_hi: optional global coupling window (see include/ptzba.h); pass the same array on
+        every rank of a sharded solve (frame_coupling_window() of the full record set)."""
         frame = np.ascontiguousarray(frame, dtype=np.int32)
         landmark = np.ascontiguousarray(landmark, dtype=np.int32)
         xy = _f64(xy, (-1, 2))
@@ -245,11 +265,21 @@ class BAHandle:
         if len(landmark) != n or len(xy) != n:
             raise ValueError("frame/landmark/xy length mismatch")
         w = None if weight is None else _f64(weight, (n,))
-        opts = ptzba_problem_opts(int(precision), int(loss), float(f_scale), int(n_fixed), 0)
+        self._win = None if frame_win_hi is None else np.ascontiguousarray(frame_win_hi, dtype=np.int32)
+        if self._win is not None and len(self._win) != int(n_pose):
+            raise ValueError("frame_win_hi must have n_pose entries")
+        opts = ptzba_problem_opts(int(precision), int(loss), float(f_scale), int(n_fixed), int(ordering),
+                                  _ptr(self._win).value if self._win is not None else None)
         _check(lib().ptzba_set_problem(self.h, int(n_pose), int(n_landmark), n, _ptr(frame), _ptr(landmark), _ptr(xy),
                                        _ptr(w), float(u), float(v), ctypes.byref(opts)), "ptzba_set_problem")
         self.n_pose, self.n_landmark, self.n_obs = int(n_pose), int(n_landmark), n
         self.precision = precision
+
+    def solver_info(self):
+        out = np.zeros(4, np.int64)
+        _check(lib().ptzba_solver_info(self.h, _ptr(out)), "ptzba_solver_info")
+        return dict(n_aug=int(out[0]), ld=int(out[1]), levels=int(out[2]),
+                    ordering="nested" if out[3] != ORDER_NATURAL else "natural")
 
     def info(self):
         out = np.zeros(8, np.int64)

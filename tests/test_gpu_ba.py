@@ -240,13 +240,15 @@ def test_compute_residual_dropin_signature(gpu_available):
         np.testing.assert_allclose(r, r_ref, rtol=0, atol=1e-8)
 
 
-@pytest.mark.parametrize("cfg", ["config1", "config2"])
+@pytest.mark.parametrize("cfg,ordering", [("config1", 0), ("config2", 0), ("config2", 2), ("config2", 1)])
 @pytest.mark.parametrize("precision", [0, 1])
-def test_single_gauss_newton_step_is_exact(gpu_available, precision, cfg):
+def test_single_gauss_newton_step_is_exact(gpu_available, precision, cfg, ordering):
     """One undamped step (lambda = 0) == the exact solution of J^T J dx = -J^T r with the oracle's
     analytic Jacobian (sparse normal equations), i.e. linearisation + Schur + Cholesky +
     back-substitution are exact.  config2 spans five 32x32 Cholesky tiles and >32 segments per
     Schur wave chunk (the multi-tile / odd-tail paths config1 never reaches).
+    ordering 2 forces the nested-dissection system order ([A | B reversed | C], padded tiles, two
+    back-substitution chains) that config3 selects on its own.
     Tolerance: fp64 1e-7 relative to |dx|; fp32 2e-3 relative (fp32 normal-equation blocks)."""
     import scipy.sparse.linalg as spla
     import ptzba
@@ -254,7 +256,9 @@ def test_single_gauss_newton_step_is_exact(gpu_available, precision, cfg):
     from oracle import ptz_oracle as orc
     p = synthetic.make_problem(cfg, seed=0)
     h = ptzba.BAHandle(0)
-    h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=precision)
+    h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=precision, ordering=ordering)
+    if ordering == 2:
+        assert h.solver_info()["ordering"] == "nested"
     h.set_state(p.init_ptz, p.init_rays)
     h.linearize()
     h.build_reduced(0.0)
