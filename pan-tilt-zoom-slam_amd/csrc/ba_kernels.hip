@@ -343,11 +343,9 @@ void launch_landmark_damp(const double* lm_out, const int32_t* lm_seg_begin, dou
 // wave's lanes never collide) and add -Y W_f2^T (Y = W_f1 V~^-1) with LDS fp64 atomics
 // (ds_add_f64: waves may hit the same frame).
 // ------------------------------------------------------------------------------------------------
-#ifndef SCHUR_VARIANT
-#define SCHUR_VARIANT 0
-#endif
 constexpr int SCHUR_WMAX = 448;  // frames per LDS window (448 * 9 * 8 B = 31.5 KiB)
-constexpr int SCHUR_WAVES = 16;
+constexpr int SCHUR_WAVES = 8;   // 512-thread workgroups: two or three frames per CU
+constexpr int SCHUR_PF = 3;      // partner-batch prefetch ring depth per half-wave
 
 __device__ __forceinline__ double bcast(double v, int j) {
   int lo = __builtin_amdgcn_readlane(__double2loint(v), j);
@@ -364,9 +362,11 @@ __device__ __forceinline__ int xcd_swizzle(int b, int nb) {
 }
 
 template <typename real>
-__global__ __launch_bounds__(1024) void k_schur(SchurArgs a) {
+__global__ __launch_bounds__(64 * SCHUR_WAVES) void k_schur(SchurArgs a) {
   __shared__ double s_S[SCHUR_WMAX * 9];
   __shared__ double s_red[SCHUR_WAVES][12];
+  __shared__ double2 s_Y[SCHUR_WAVES][WAVE][3];  // per chunk: Y = W V^-1 of each segment (3x2)
+  __shared__ int2 s_seg[SCHUR_WAVES][WAVE];       // per chunk: (first partner s1, end of landmark)
   // XCD-aware frame order: workgroups b and b+8 share an XCD (round-robin dispatch), so give each XCD
   // a contiguous run of frames -> neighbouring frames (which share landmarks) hit the same L2.
   const int f1 = xcd_swizzle(blockIdx.x, gridDim.x) + a.n_fixed;
@@ -420,54 +420,94 @@ __global__ __launch_bounds__(1024) void k_schur(SchurArgs a) {
         }
       }
       const int n = min(WAVE, ee - cb);
-      // two segments per step, one per half-wave (lanes of a half never collide; halves may -> atomics)
-      for (int j2 = 0; j2 < n; j2 += 2) {
-        const int j = min(j2 + half, n - 1);
-        const bool vj = (j2 + half) < n;
-        // every shuffle runs with the full wave active: a ds_bpermute issued under divergence reads 0
-        // from source lanes that are switched off (the upper half on an odd tail), which used to drop
-        // the chunk's last segment whenever it sat in lanes 32..63.
-        const int s1j = __shfl(s1, j, WAVE);
-        const int sendraw = __shfl(send, j, WAVE);
-        const int sendj = vj ? sendraw : 0;
-        double Yj[3][2];
+      // stage the chunk's segment metadata for broadcast reads by the half-waves
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          Yj[q][0] = __shfl(Y[q][0], j, WAVE);
-          Yj[q][1] = __shfl(Y[q][1], j, WAVE);
+      for (int q = 0; q < 3; ++q) s_Y[wv][lane][q] = make_double2(Y[q][0], Y[q][1]);
+      s_seg[wv][lane] = make_int2(s1, send);
+      wave_lds_fence();
+      // Work items = (segment, batch of 32 partners); half-wave h walks the items of segments j = h,
+      // h+2, ...  A ring of SCHUR_PF items per half is in flight: every ring load is unconditional (an
+      // exhausted half reloads a valid segment and drops the result), so the compiler can wait for one
+      // slot at a time (a conditional or synchronous load in the loop would drain the whole ring).
+      const int nb_lane = ok ? (send - s1 + 31) >> 5 : 0;
+      int items_even = (lane & 1) ? 0 : nb_lane, items_odd = (lane & 1) ? nb_lane : 0;
+      items_even = wave_sum_i(items_even);
+      items_odd = wave_sum_i(items_odd);
+      const int my_items = half ? items_odd : items_even;
+      const int nsteps = max(items_even, items_odd);
+      // fetch-side cursor of this half: segment fj, batch fb (segments without items are skipped)
+      int fj = half, fb = 0, fs1 = 0, fsend = 0;
+      auto seek = [&]() {
+        for (; fj < n; fj += 2) {
+          const int2 g = s_seg[wv][fj];
+          if (g.y > g.x) {
+            fs1 = g.x;
+            fsend = g.y;
+            return;
+          }
         }
-#if SCHUR_VARIANT == 3
-        if (sendj == -7)
-#endif
-        for (int s2 = s1j + hl; s2 < sendj; s2 += 32) {
-          const real* w2 = seg_w + (int64_t)s2 * 8;
-          const int f2 = __real_as_int(w2[6]);
-          double X[3][2];
+        fs1 = 0;
+        fsend = 0;
+      };
+      seek();
+      real xr[SCHUR_PF][8];
+      int jr[SCHUR_PF], s2r[SCHUR_PF], endr[SCHUR_PF];
+      auto fetch = [&](real(&x)[8], int& jo, int& s2o, int& endo) {
+        const int s2 = fs1 + 32 * fb + hl;
+        jo = min(fj, n - 1);
+        s2o = s2;
+        endo = fsend;
+        const int sl = (s2 < fsend) ? s2 : 0;  // an exhausted half loads segment 0 and drops it
+        if constexpr (sizeof(real) == 4) {
+          const float4* w2 = reinterpret_cast<const float4*>(seg_w + (int64_t)sl * 8);
+          const float4 lo = w2[0], hi4 = w2[1];
+          x[0] = lo.x; x[1] = lo.y; x[2] = lo.z; x[3] = lo.w; x[4] = hi4.x; x[5] = hi4.y; x[6] = hi4.z; x[7] = hi4.w;
+        } else {
+          const double2* w2 = reinterpret_cast<const double2*>(seg_w + (int64_t)sl * 8);
 #pragma unroll
-          for (int q = 0; q < 3; ++q) { X[q][0] = (double)w2[2 * q]; X[q][1] = (double)w2[2 * q + 1]; }
-          if (f2 >= p0 && f2 < p1) {
-            double* dst = s_S + (f2 - p0) * 9;
-#if SCHUR_VARIANT == 0
+          for (int k = 0; k < 4; ++k) {
+            const double2 d = w2[k];
+            x[2 * k] = d.x; x[2 * k + 1] = d.y;
+          }
+        }
+        // advance the cursor
+        ++fb;
+        if (32 * fb >= fsend - fs1) {
+          fj += 2;
+          fb = 0;
+          seek();
+        }
+      };
 #pragma unroll
-            for (int q = 0; q < 3; ++q)
+      for (int u = 0; u < SCHUR_PF; ++u) fetch(xr[u], jr[u], s2r[u], endr[u]);
+      for (int t0 = 0; t0 < nsteps; t0 += SCHUR_PF) {
 #pragma unroll
-              for (int r = 0; r < 3; ++r) atomicAdd(dst + 3 * q + r, -(Yj[q][0] * X[r][0] + Yj[q][1] * X[r][1]));
-#elif SCHUR_VARIANT == 1
+        for (int u = 0; u < SCHUR_PF; ++u) {
+          if (t0 + u < nsteps) {  // wave-uniform
+            if (t0 + u < my_items && s2r[u] < endr[u]) {
+              double Yj[3][2];
 #pragma unroll
-            for (int q = 0; q < 3; ++q)
+              for (int q = 0; q < 3; ++q) {
+                const double2 yq = s_Y[wv][jr[u]][q];
+                Yj[q][0] = yq.x;
+                Yj[q][1] = yq.y;
+              }
+              const real* w2v = xr[u];
+              const int f2 = __real_as_int(w2v[6]);
+              if (f2 >= p0 && f2 < p1) {
+                double* dst = s_S + (f2 - p0) * 9;
 #pragma unroll
-              for (int r = 0; r < 3; ++r) dst[3 * q + r] -= Yj[q][0] * X[r][0] + Yj[q][1] * X[r][1];
-#elif SCHUR_VARIANT == 2
-            double acc = 0;
+                for (int q = 0; q < 3; ++q)
 #pragma unroll
-            for (int q = 0; q < 3; ++q)
-#pragma unroll
-              for (int r = 0; r < 3; ++r) acc += Yj[q][0] * X[r][0] + Yj[q][1] * X[r][1];
-            if (acc == 12345.678) dst[0] = acc;
-#endif
+                  for (int r = 0; r < 3; ++r)
+                    atomicAdd(dst + 3 * q + r, -(Yj[q][0] * (double)w2v[2 * r] + Yj[q][1] * (double)w2v[2 * r + 1]));
+              }
+            }
+            fetch(xr[u], jr[u], s2r[u], endr[u]);
           }
         }
       }
+      wave_lds_fence();  // the next chunk restages s_Y / s_seg
     }
     if (first) {
 #pragma unroll

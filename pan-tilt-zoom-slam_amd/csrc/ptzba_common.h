@@ -119,6 +119,11 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
+__device__ __forceinline__ int wave_sum_i(int v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
 
 // Make this wave's LDS writes visible to its own later LDS reads by other lanes, and stop the

@@ -9,7 +9,7 @@ h = ptzba.BAHandle(0)
 h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=0)
 h.set_state(p.init_ptz, p.init_rays)
 h.linearize(); h.build_reduced(0.0); h.sync()
-sp, n, scp = h.exchange()
+sp, n, scp = h.exchange(); print("solver", h.solver_info())
 t = torch.as_tensor(_DevArray(sp, n), device="cuda:0").cpu().numpy().copy()
 ns = 3 * (p.n_pose - 1); ld = int(round((-3 + np.sqrt(9 + 4 * n)) / 2))
 assert ld * ld + 3 * ld == n, (ld, n)

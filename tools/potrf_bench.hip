@@ -166,6 +166,73 @@ __device__ void potrf_trsm_v8(double (*D)[NB + 1], double (*C)[NB + 1], double* 
   }
 }
 
+
+// ---- V10: fused potrf + TRSM with the pivot column broadcast through LDS, software-pipelined:
+// in step j every lane first updates its element j+1, publishes it to colbuf[(j+1)&1], then does the
+// rest of the step; step j+1 reads the column with wide uniform-address loads.  One scheduling
+// barrier per step keeps the compiler from hoisting later steps' reads (register spills).
+__device__ void potrf_trsm_v10(double (*D)[NB + 1], double (*C)[NB + 1], double* rdg, double (*colbuf)[NB]) {
+  const int lane = threadIdx.x & 63;
+  const bool isT = lane >= NB;
+  double row[NB];
+#pragma unroll
+  for (int m = 0; m < NB; ++m) row[m] = isT ? C[lane - NB][m] : D[lane][m];
+  if (!isT) colbuf[0][lane] = row[0];
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const double* col = colbuf[j & 1];
+    const double d = col[j];
+    if (lane == 0) rdg[j] = rsq_nr(d);
+    const double li = row[j] * rcp_nr(d);
+    if (j + 1 < NB) {
+      row[j + 1] -= li * col[j + 1];
+      if (!isT) colbuf[(j + 1) & 1][lane] = row[j + 1];
+    }
+#pragma unroll
+    for (int m = j + 2; m < NB; ++m) row[m] -= li * col[m];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+  for (int m = 0; m < NB; ++m) row[m] *= rdg[m];
+  if (isT) {
+#pragma unroll
+    for (int m = 0; m < NB; ++m) C[lane - NB][m] = row[m];
+  } else {
+#pragma unroll
+    for (int m = 0; m < NB; ++m) D[lane][m] = row[m];
+  }
+}
+
+// ---- V11: V8 (readlane broadcast) with rs kept in LDS
+__device__ void potrf_trsm_v11(double (*D)[NB + 1], double (*C)[NB + 1], double* rdg) {
+  const int lane = threadIdx.x & 63;
+  const bool isT = lane >= NB;
+  double row[NB];
+#pragma unroll
+  for (int m = 0; m < NB; ++m) row[m] = isT ? C[lane - NB][m] : D[lane][m];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const double d = bcast(row[j], j);
+    if (lane == 0) rdg[j] = rsq_nr(d);
+    const double li = row[j] * rcp_nr(d);
+#pragma unroll
+    for (int m = j + 1; m < NB; ++m) row[m] -= li * bcast(row[j], m);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+  for (int m = 0; m < NB; ++m) row[m] *= rdg[m];
+  if (isT) {
+#pragma unroll
+    for (int m = 0; m < NB; ++m) C[lane - NB][m] = row[m];
+  } else {
+#pragma unroll
+    for (int m = 0; m < NB; ++m) D[lane][m] = row[m];
+  }
+}
+
 // ---- TRSM variants: X = T L^-T with L = D (scaled on the fly: L_mj = D[m][j] * rdg[j] for m > j, L_jj = 1/rdg)
 // T0: lane per row, sched_barrier per step (library)
 __device__ void trsm_t0(double (*C)[NB + 1], double (*D)[NB + 1], const double* rdg) {
@@ -230,6 +297,7 @@ __global__ __launch_bounds__(256) void k_bench(const double* __restrict__ A, con
   __shared__ double sC[NB][NB + 1];
   __shared__ double rdg[NB];
   __shared__ double col[NB];
+  __shared__ double colbuf[2][NB];
   const double* a = A + (size_t)blockIdx.x * NB * NB;
   const double* t = T + (size_t)blockIdx.x * NB * NB;
   for (int rep = 0; rep < REPS; ++rep) {
@@ -246,6 +314,8 @@ __global__ __launch_bounds__(256) void k_bench(const double* __restrict__ A, con
       if (PV == 7) potrf_v0(sD, rdg);
       if (PV == 8) potrf_trsm_v8<true>(sD, sC, rdg);
       if (PV == 9) potrf_trsm_v8<false>(sD, sC, rdg);
+      if (PV == 10) potrf_trsm_v10(sD, sC, rdg, colbuf);
+      if (PV == 11) potrf_trsm_v11(sD, sC, rdg);
     }
     __syncthreads();
     if (TV == 2) {
@@ -349,5 +419,7 @@ int main() {
   cmp("load only", run<6, 9>(nb, dA, dT, dL, dX, L, X));
   cmp("fused v8 fast rcp", run<8, 9>(nb, dA, dT, dL, dX, L, X));
   cmp("fused v9 ieee div", run<9, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("fused v10 lds pipelined", run<10, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("fused v11 readlane, rs in lds", run<11, 9>(nb, dA, dT, dL, dX, L, X));
   return 0;
 }
