@@ -128,8 +128,11 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        # one process per GPU over RCCL ("nccl").  PTZBA_DIST_BACKEND=gloo rehearses the same protocol
+        # with several ranks on one device (the ranks then share GPU local % device_count)
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(os.environ.get("PTZBA_DIST_BACKEND", "nccl"))
     else:
         torch.cuda.set_device(0)
     import ptzba
@@ -157,13 +160,22 @@ def main():
     sinfo = h.solver_info()
 
     allreduce = None
+    exchange_doubles = 0
     if world > 1:
-        sys_ptr, sys_n, scal_ptr = h.exchange()
-        t_sys = torch.as_tensor(_DevArray(sys_ptr, sys_n), device=f"cuda:{local}")
+        # packed exchange: only the tiles of the reduced system the Schur kernel writes, plus b|g|dU
+        xb_ptr, xb_n = h.exchange_packed()
+        _, _, scal_ptr = h.exchange()
+        t_sys = torch.as_tensor(_DevArray(xb_ptr, xb_n), device=f"cuda:{local}")
         t_scal = torch.as_tensor(_DevArray(scal_ptr, ptzba.NSCALARS), device=f"cuda:{local}")
+        exchange_doubles = xb_n
 
         def allreduce(kind):
-            dist.all_reduce(t_sys if kind == "sys" else t_scal)
+            if kind == "sys":
+                h.pack()
+                dist.all_reduce(t_sys)
+                h.unpack()
+            else:
+                dist.all_reduce(t_scal)
 
     def run_iters(k, timed=False):
         done = 0
@@ -247,6 +259,7 @@ def main():
                        "n_matches": int(prob.n_match), "n_pairs": prob.n_pairs, "form": a.form,
                        "parallelism": f"landmark-sharded x{world}" if world > 1 else "single GPU",
                        "reduced_system": sinfo,
+                       "allreduce_bytes_per_iteration": 8 * (exchange_doubles + ptzba.NSCALARS) if world > 1 else 0,
                        "iterations_timed": iters, "solves_timed": solves},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_linearize (K1)",

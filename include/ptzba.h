@@ -73,9 +73,12 @@ PTZBA_EXPORT ptzba_handle ptzba_new(int device);
 PTZBA_EXPORT void ptzba_delete(ptzba_handle h);
 PTZBA_EXPORT const char* ptzba_last_error(void);
 PTZBA_EXPORT const char* ptzba_version(void);
-/* Run all work of the handle on this hipStream_t (e.g. torch.cuda.current_stream().cuda_stream).
- * NULL -> the handle's own stream. */
+/* Run all work of the handle on this hipStream_t, e.g. torch.cuda.current_stream().cuda_stream, so
+ * collectives issued on that stream are ordered with the handle's kernels.  NULL is the default
+ * (null) stream, which is what torch's current stream usually is.  A new handle uses a private
+ * non-blocking stream; ptzba_use_own_stream returns to it. */
 PTZBA_EXPORT int ptzba_set_stream(ptzba_handle h, void* hip_stream);
+PTZBA_EXPORT int ptzba_use_own_stream(ptzba_handle h);
 
 /* ---------------- problem ---------------- */
 /* Pair-form observation records in the reference residual order: record 2m is (frame i, landmark l,
@@ -116,6 +119,13 @@ PTZBA_EXPORT int ptzba_accept(ptzba_handle h, int accept);
 /* Device pointers of the exchange regions (fp64): reduced system (n_sys*(n_sys+1) doubles: lower
  * matrix n_sys x n_sys row-major then rhs n_sys) and the additive partial scalars (PTZBA_NSCALARS). */
 PTZBA_EXPORT int ptzba_exchange(ptzba_handle h, void** sys_ptr, int64_t* sys_count, void** scal_ptr);
+/* Packed exchange for sharded solves: a contiguous device buffer (fp64, *count doubles) holding only
+ * the tiles of the reduced system the Schur kernel can write, then b | g_pose | dU.  Sequence per
+ * iteration: ptzba_build_reduced -> ptzba_pack -> all-reduce(sum) of the buffer -> ptzba_unpack ->
+ * ptzba_solve_reduced.  Pack/unpack are queued on the handle's stream. */
+PTZBA_EXPORT int ptzba_exchange_packed(ptzba_handle h, void** buf, int64_t* count);
+PTZBA_EXPORT int ptzba_pack(ptzba_handle h);
+PTZBA_EXPORT int ptzba_unpack(ptzba_handle h);
 /* wait for all queued work of the handle */
 PTZBA_EXPORT int ptzba_sync(ptzba_handle h);
 /* average device time (ms) of the last n launches of the linearisation kernel (K1), measured with

@@ -64,6 +64,8 @@ struct ptzba_ctx {
   int chol_levels = 0, n_aug = 0, n_chain = 1;
   bool nested = false;
   DBuf frame_pos, row_pad, bs_chain_off, bs_chain_cols, bs_col_off, bs_col_tiles;
+  DBuf xtiles, xbuf;  // packed exchange: tile list, buffer
+  int n_xtiles = 0;
   double lambda = 0;
   // timing
   bool timing = false;
@@ -117,9 +119,13 @@ void ptzba_delete(ptzba_handle h) {
 
 int ptzba_set_stream(ptzba_handle h, void* stream) {
   if (!h) return fail("null handle");
-  h->st = stream ? (hipStream_t)stream : h->own;
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->st));  // work already queued on the previous stream completes first
+  h->st = (hipStream_t)stream;          // NULL = the default stream (torch's current_stream() is often it)
   return 0;
 }
+
+int ptzba_use_own_stream(ptzba_handle h) { return h ? ptzba_set_stream(h, h->own) : fail("null handle"); }
 
 // ------------------------------------------------------------------------------------------------
 // records hold obs - base(segment) in `real`; the per-segment base observation stays fp64, so the
@@ -232,6 +238,7 @@ struct CholPlan {
   std::vector<int32_t> tasks;  // int4 records
   std::vector<int> level_off;
   std::vector<int> chain_off, chain_cols, col_off, col_tiles;
+  std::vector<int32_t> xtiles;  // (ti, tj) pairs the Schur kernel can write (before fill), for the exchange
   int n_levels = 0;
 };
 
@@ -250,6 +257,10 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
       const int p1 = o.pos[f1], p2 = o.pos[f2];
       mark(p2, p1); mark(p2 + 2, p1); mark(p2, p1 + 2); mark(p2 + 2, p1 + 2);
     }
+  P.xtiles.clear();
+  for (int i = 0; i < T; ++i)
+    for (int j = 0; j <= i; ++j)
+      if (nz[i][j] || i == j) { P.xtiles.push_back(i); P.xtiles.push_back(j); }
   const int ta = o.n_aug / CHOL_NB;  // tile holding the augmented row
   for (int j = 0; j <= ta; ++j) nz[ta][j] = 1;
   for (int i = 0; i < T; ++i) nz[i][i] = 1;
@@ -509,8 +520,10 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     return -1;
   if (upload(h->chol_tasks, plan.tasks) || upload(h->frame_pos, sorder.pos) || upload(h->row_pad, sorder.pad) ||
       upload(h->bs_chain_off, plan.chain_off) || upload(h->bs_chain_cols, plan.chain_cols) ||
-      upload(h->bs_col_off, plan.col_off) || upload(h->bs_col_tiles, plan.col_tiles))
+      upload(h->bs_col_off, plan.col_off) || upload(h->bs_col_tiles, plan.col_tiles) || upload(h->xtiles, plan.xtiles))
     return -1;
+  h->n_xtiles = (int)(plan.xtiles.size() / 2);
+  h->xbuf.release();  // allocated on first ptzba_exchange_packed
   HIPCHK(hipMemset(h->D_pose.p, 0, h->D_pose.bytes));
   HIPCHK(hipMemset(h->D_ray.p, 0, h->D_ray.bytes));
   HIPCHK(hipMemset(h->ptz.p, 0, h->ptz.bytes));
@@ -791,6 +804,26 @@ int ptzba_exchange(ptzba_handle h, void** sys_ptr, int64_t* sys_count, void** sc
   if (scal_ptr) *scal_ptr = h->scal.p;
   return 0;
 }
+
+int ptzba_exchange_packed(ptzba_handle h, void** buf, int64_t* count) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  const int64_t n = (int64_t)h->n_xtiles * CHOL_NB * CHOL_NB + 3 * h->ld;
+  if (!h->xbuf.p && h->xbuf.alloc((size_t)n * 8)) return -1;
+  if (buf) *buf = h->xbuf.p;
+  if (count) *count = n;
+  return 0;
+}
+
+static int pack_impl(ptzba_handle h, int unpack) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  if (!h->xbuf.p) return fail("call ptzba_exchange_packed first");
+  HIPCHK(hipSetDevice(h->device));
+  launch_pack_exchange(h->S(), h->ld, h->xtiles.as<int2>(), h->n_xtiles, h->bvec(), h->xbuf.as<double>(), unpack, h->st);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+int ptzba_pack(ptzba_handle h) { return pack_impl(h, 0); }
+int ptzba_unpack(ptzba_handle h) { return pack_impl(h, 1); }
 
 int ptzba_sync(ptzba_handle h) {
   if (!h) return fail("null handle");

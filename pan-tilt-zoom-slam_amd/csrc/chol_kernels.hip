@@ -279,4 +279,33 @@ void launch_chol_backsolve(const double* L, int64_t ld, int n, int n_chain, cons
                      chain_cols, col_off, col_tiles, Ldiag, xout);
 }
 
+// packed exchange: the lower tiles the Schur kernel can write (xt[k] = (ti, tj)) and the three
+// length-ld vectors b | g_pose | dU, copied between the system matrix and a contiguous buffer
+// (unpack != 0: buffer -> matrix).  Block k < n_tiles moves tile k; the last block moves the vectors.
+__global__ void k_pack_exchange(double* __restrict__ S, int64_t ld, const int2* __restrict__ xt, int n_tiles,
+                                double* __restrict__ vec, double* __restrict__ buf, int unpack) {
+  const int k = blockIdx.x;
+  if (k < n_tiles) {
+    const int2 t = xt[k];
+    double* tile = S + (int64_t)t.x * NB * ld + (int64_t)t.y * NB;
+    double* b = buf + (int64_t)k * NB * NB;
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+      double* m = tile + (int64_t)(e >> 5) * ld + (e & 31);
+      if (unpack) *m = b[e];
+      else b[e] = *m;
+    }
+    return;
+  }
+  double* b = buf + (int64_t)n_tiles * NB * NB;
+  for (int64_t e = threadIdx.x; e < 3 * ld; e += blockDim.x) {
+    if (unpack) vec[e] = b[e];
+    else b[e] = vec[e];
+  }
+}
+
+void launch_pack_exchange(double* S, int64_t ld, const int2* xt, int n_tiles, double* vec, double* buf, int unpack,
+                          hipStream_t st) {
+  hipLaunchKernelGGL(k_pack_exchange, dim3(n_tiles + 1), dim3(256), 0, st, S, ld, xt, n_tiles, vec, buf, unpack);
+}
+
 }  // namespace ptzba

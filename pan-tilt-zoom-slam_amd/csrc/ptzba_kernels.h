@@ -100,6 +100,9 @@ void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_o
                      int* info, hipStream_t st);
 void launch_chol_backsolve(const double* L, int64_t ld, int n, int n_chain, const int* chain_off, const int* chain_cols,
                            const int* col_off, const int* col_tiles, const double* Ldiag, double* xout, hipStream_t st);
+// packed exchange of the Schur-written tiles + b | g_pose | dU (vec = b, contiguous 3 ld doubles)
+void launch_pack_exchange(double* S, int64_t ld, const int2* xt, int n_tiles, double* vec, double* buf, int unpack,
+                          hipStream_t st);
 // task word w: bits 0-13 update panel p1 + 1, bits 14-27 p2 + 1 (0 = none), bits 28/29: p1/p2 also update T
 inline int chol_pack_updates(int p1, int p2, int tmask) { return (p1 + 1) | ((p2 + 1) << 14) | (tmask << 28); }
 

@@ -60,6 +60,7 @@ def lib():
         "ptzba_last_error": ([], c_char_p),
         "ptzba_version": ([], c_char_p),
         "ptzba_set_stream": ([V, V], I),
+        "ptzba_use_own_stream": ([V], I),
         "ptzba_set_problem": ([V, I32, I32, I64, V, V, V, V, D, D, POINTER(ptzba_problem_opts)], I),
         "ptzba_problem_info": ([V, V], I),
         "ptzba_solver_info": ([V, V], I),
@@ -73,6 +74,9 @@ def lib():
         "ptzba_read_scalars": ([V, V], I),
         "ptzba_accept": ([V, I], I),
         "ptzba_exchange": ([V, POINTER(c_void_p), POINTER(c_int64), POINTER(c_void_p)], I),
+        "ptzba_exchange_packed": ([V, POINTER(c_void_p), POINTER(c_int64)], I),
+        "ptzba_pack": ([V], I),
+        "ptzba_unpack": ([V], I),
         "ptzba_sync": ([V], I),
         "ptzba_kernel_times": ([V, V, V], I),
         "ptzba_reset_kernel_times": ([V, I], I),
@@ -102,10 +106,10 @@ def lib():
 
 
 EXPORTED_SYMBOLS = [
-    "ptzba_new", "ptzba_delete", "ptzba_last_error", "ptzba_version", "ptzba_set_stream", "ptzba_set_problem",
+    "ptzba_new", "ptzba_delete", "ptzba_last_error", "ptzba_version", "ptzba_set_stream", "ptzba_use_own_stream", "ptzba_set_problem",
     "ptzba_problem_info", "ptzba_solver_info", "ptzba_residual", "ptzba_set_state", "ptzba_get_state", "ptzba_linearize",
     "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_read_scalars", "ptzba_accept",
-    "ptzba_exchange", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptz_ray_to_image",
+    "ptzba_exchange", "ptzba_exchange_packed", "ptzba_pack", "ptzba_unpack", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptz_ray_to_image",
     "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks",
     "ptzekf_new", "ptzekf_delete", "ptzekf_num_rays", "ptzekf_set_state", "ptzekf_get_state", "ptzekf_add_pose_cov",
     "ptzekf_remove_rays", "ptzekf_add_rays", "ptzekf_project_visible", "ptzekf_update",
@@ -252,7 +256,11 @@ class BAHandle:
             pass
 
     def set_stream(self, stream_ptr):
+        """Queue the handle's work on this hipStream_t (0 / None = the default stream)."""
         _check(lib().ptzba_set_stream(self.h, c_void_p(stream_ptr or 0)), "ptzba_set_stream")
+
+    def use_own_stream(self):
+        _check(lib().ptzba_use_own_stream(self.h), "ptzba_use_own_stream")
 
     def set_problem(self, n_pose, n_landmark, frame, landmark, xy, u, v, weight=None, precision=FP64,
                     loss=LOSS_LINEAR, f_scale=1.0, n_fixed=1, ordering=ORDER_NESTED, frame_win_hi=None):
@@ -333,6 +341,18 @@ class BAHandle:
         sc = c_void_p(0)
         _check(lib().ptzba_exchange(self.h, ctypes.byref(sp), ctypes.byref(cnt), ctypes.byref(sc)), "ptzba_exchange")
         return sp.value, int(cnt.value), sc.value
+
+    def exchange_packed(self):
+        """(device pointer, count) of the packed exchange buffer (see include/ptzba.h)."""
+        p, n = c_void_p(), c_int64()
+        _check(lib().ptzba_exchange_packed(self.h, ctypes.byref(p), ctypes.byref(n)), "ptzba_exchange_packed")
+        return p.value, n.value
+
+    def pack(self):
+        _check(lib().ptzba_pack(self.h), "ptzba_pack")
+
+    def unpack(self):
+        _check(lib().ptzba_unpack(self.h), "ptzba_unpack")
 
     def sync(self):
         _check(lib().ptzba_sync(self.h), "ptzba_sync")

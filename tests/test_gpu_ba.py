@@ -297,7 +297,8 @@ def test_analytic_jacobian_matches_fd_cpu():
         np.testing.assert_allclose(J[:, c], fd, rtol=1e-5, atol=1e-5 * max(1.0, np.abs(fd).max()))
 
 
-def test_exchange_region_sums_over_landmark_shards(gpu_available):
+@pytest.mark.parametrize("packed", [False, True])
+def test_exchange_region_sums_over_landmark_shards(gpu_available, packed):
     """The N>1 protocol on one device: two landmark-shard handles' exchange regions sum to the
     whole-problem handle's reduced system; after writing the sum back, each shard takes the same pose
     step and its own landmarks' step (bench.py all-reduces exactly these buffers over RCCL)."""
@@ -306,11 +307,13 @@ def test_exchange_region_sums_over_landmark_shards(gpu_available):
     import ptzba
     import synthetic
     p = synthetic.make_problem("config2", seed=0)
+    win = ptzba.frame_coupling_window(p.n_pose, p.frame, p.landmark)  # global window, as bench.py passes
     hs = []
     for sel in [np.ones(len(p.frame), bool)] + [bench.shard_by_landmark(p.landmark, p.n_landmark, r, 2)
                                                  for r in range(2)]:
         h = ptzba.BAHandle(0)
-        h.set_problem(p.n_pose, p.n_landmark, p.frame[sel], p.landmark[sel], p.xy[sel], p.u, p.v)
+        h.set_problem(p.n_pose, p.n_landmark, p.frame[sel], p.landmark[sel], p.xy[sel], p.u, p.v, frame_win_hi=win,
+                      ordering=ptzba.ORDER_NESTED_FORCE)
         h.set_state(p.init_ptz, p.init_rays)
         h.linearize()
         h.build_reduced(1e-3)
@@ -318,16 +321,24 @@ def test_exchange_region_sums_over_landmark_shards(gpu_available):
         hs.append((h, sel))
     views = []
     for h, _ in hs:
-        sp, n, scp = h.exchange()
-        views.append((torch.as_tensor(bench._DevArray(sp, n), device="cuda:0"),
-                      torch.as_tensor(bench._DevArray(scp, ptzba.NSCALARS), device="cuda:0")))
-    full = views[0][0].cpu().numpy()
-    summed = (views[1][0] + views[2][0])
+        if packed:
+            sp, n = h.exchange_packed()
+            h.pack()
+            h.sync()
+        else:
+            sp, n, _ = h.exchange()
+        views.append(torch.as_tensor(bench._DevArray(sp, n), device="cuda:0"))
+    assert len({int(v.numel()) for v in views}) == 1  # same layout on every "rank"
+    full = views[0].cpu().numpy()
+    summed = (views[1] + views[2])
     err = np.abs(summed.cpu().numpy() - full).max() / np.abs(full).max()
     assert err < 1e-12, err
-    views[1][0].copy_(summed)
-    views[2][0].copy_(summed)
+    views[1].copy_(summed)
+    views[2].copy_(summed)
     torch.cuda.synchronize()
+    if packed:
+        for h, _ in hs[1:]:
+            h.unpack()
     for h, _ in hs:
         h.solve_reduced()
     s = [h.read_scalars() for h, _ in hs]
