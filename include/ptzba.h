@@ -151,6 +151,26 @@ PTZBA_EXPORT int ptz_back_project_rays(int device, int64_t n, double u, double v
 PTZBA_EXPORT int ptz_h_jacobian(int device, int64_t n, double u, double v, double f, double pan,
                                 double tilt, const double* displacement6, const double* rays, double* H_out);
 
+/* ---------------- pose-only refinement (relocalization.py:22-40, 186) ----------------
+ * Levenberg-Marquardt over (pan, tilt, f) with the rays fixed, residual = from_ray_to_image(ray) -
+ * point (transformation.py:99-135), one workgroup per hypothesis on the device.  Hypotheses share the
+ * n_corr correspondences, or hypothesis h uses subset_index[subset_offsets[h] .. subset_offsets[h+1])
+ * (both NULL: all).  ptz_inout [n_hyp][3] holds the initial poses and receives the refined ones;
+ * cost_out = 0.5 sum rho(r^2), iters_out = accepted iterations, status_out as ptzba.LMSolver
+ * (2 ftol, 3 xtol, 0 max_iter, -1 no decrease).  Any output pointer may be NULL. */
+typedef struct {
+    int32_t max_iter;  /* default 100 */
+    int32_t loss;      /* PTZBA_LOSS_LINEAR | PTZBA_LOSS_HUBER */
+    double ftol;       /* the reference's 1e-4 */
+    double xtol;       /* scipy default 1e-8 */
+    double f_scale;
+} ptz_refine_opts;
+PTZBA_EXPORT int ptz_refine_poses(int device, int32_t n_hyp, double* ptz_inout, int64_t n_corr,
+                                  const double* rays, const double* points, double u, double v,
+                                  const int64_t* subset_offsets, const int32_t* subset_index,
+                                  const ptz_refine_opts* opts, double* cost_out, int32_t* iters_out,
+                                  int32_t* status_out);
+
 /* ---------------- host bookkeeping (native) ---------------- */
 /* First-seen landmark ids over ordered pair match lists (image_process.py:611-639).
  * pair_i/pair_j/pair_count: n_pairs; idx_a/idx_b: concatenated match keypoint indices.

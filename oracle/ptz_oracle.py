@@ -487,3 +487,24 @@ def ekf_update(state, observed_keypoints, observed_keypoint_index, height, width
     cov[np.ix_(rows, rows)] = Pu[3::2, 3::2]
     cov[np.ix_(rows + 1, rows + 1)] = Pu[4::2, 4::2]
     return s
+
+
+# --------------------------------------------------------------------------------------------
+# relocalisation (relocalization.py)
+# --------------------------------------------------------------------------------------------
+def reloc_residual(pose, rays, points, u, v):
+    """relocalization.py:22-40: [x_i - px_i, y_i - py_i] interleaved, from_ray_to_image projection."""
+    rays = np.asarray(rays, np.float64).reshape(-1, 2)
+    points = np.asarray(points, np.float64).reshape(-1, 2)
+    n = len(rays)
+    x, y = from_ray_to_image(u, v, np.full(n, pose[2]), np.full(n, pose[0]), np.full(n, pose[1]), rays[:, 0],
+                             rays[:, 1])
+    return np.stack([x - points[:, 0], y - points[:, 1]], 1).reshape(-1)
+
+
+def refine_pose(pose0, rays, points, u, v, ftol=1e-4, xtol=1e-8, gtol=1e-8):
+    """relocalization.py:186: least_squares(_compute_residual, pose, x_scale='jac', ftol=1e-4, 'trf')."""
+    from scipy.optimize import least_squares
+    res = least_squares(reloc_residual, np.asarray(pose0, np.float64), x_scale='jac', ftol=ftol, xtol=xtol,
+                        gtol=gtol, method='trf', args=(rays, points, u, v))
+    return res.x, res.cost

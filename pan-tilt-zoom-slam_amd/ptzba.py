@@ -35,6 +35,11 @@ _lib = None
 ORDER_NATURAL, ORDER_NESTED, ORDER_NESTED_FORCE = 0, 1, 2
 
 
+class ptz_refine_opts(Structure):
+    _fields_ = [("max_iter", c_int32), ("loss", c_int32), ("ftol", c_double), ("xtol", c_double),
+                ("f_scale", c_double)]
+
+
 class ptzba_problem_opts(Structure):
     _fields_ = [("precision", c_int32), ("loss", c_int32), ("f_scale", c_double), ("n_fixed", c_int32),
                 ("ordering", c_int32), ("frame_win_hi", c_void_p)]
@@ -86,6 +91,7 @@ def lib():
         "ptz_back_project_rays": ([I, I64, D, D, D, D, D, V, V, V], I),
         "ptz_h_jacobian": ([I, I64, D, D, D, D, D, V, V, V], I),
         "ptzba_build_landmarks": ([I32, V, I64, V, V, V, V, V, V, V, V], I),
+        "ptz_refine_poses": ([I, I32, V, I64, V, V, D, D, V, V, POINTER(ptz_refine_opts), V, V, V], I),
         "ptzekf_new": ([I], V),
         "ptzekf_delete": ([V], None),
         "ptzekf_num_rays": ([V], I),
@@ -111,7 +117,7 @@ EXPORTED_SYMBOLS = [
     "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_read_scalars", "ptzba_accept",
     "ptzba_exchange", "ptzba_exchange_packed", "ptzba_pack", "ptzba_unpack", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptz_ray_to_image",
     "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks",
-    "ptzekf_new", "ptzekf_delete", "ptzekf_num_rays", "ptzekf_set_state", "ptzekf_get_state", "ptzekf_add_pose_cov",
+    "ptz_refine_poses", "ptzekf_new", "ptzekf_delete", "ptzekf_num_rays", "ptzekf_set_state", "ptzekf_get_state", "ptzekf_add_pose_cov",
     "ptzekf_remove_rays", "ptzekf_add_rays", "ptzekf_project_visible", "ptzekf_update",
 ]
 
@@ -195,6 +201,35 @@ def h_jacobian(u, v, f, pan, tilt, rays, displacement=None, device=0):
     _check(lib().ptz_h_jacobian(device, n, u, v, float(f), float(pan), float(tilt), _ptr(d), _ptr(rays), _ptr(H)),
            "ptz_h_jacobian")
     return H
+
+
+def refine_poses(u, v, init_ptz, rays, points, subsets=None, ftol=1e-4, xtol=1e-8, max_iter=100, loss=LOSS_LINEAR,
+                 f_scale=1.0, device=0):
+    """Pose-only LM with the rays fixed (relocalization.py:22-40, 186), batched over hypotheses.
+    init_ptz [n_hyp, 3]; rays / points [n, 2]; subsets: optional list of index arrays (one per
+    hypothesis).  Returns (ptz [n_hyp, 3], cost [n_hyp], iterations [n_hyp], status [n_hyp])."""
+    ptz = _f64(init_ptz).reshape(-1, 3).copy()
+    rays = _f64(rays).reshape(-1, 2)
+    points = _f64(points).reshape(-1, 2)
+    if len(rays) != len(points):
+        raise ValueError("rays and points differ in length")
+    n_hyp = len(ptz)
+    off = idx = None
+    if subsets is not None:
+        if len(subsets) != n_hyp:
+            raise ValueError("one subset per hypothesis")
+        off = np.zeros(n_hyp + 1, np.int64)
+        off[1:] = np.cumsum([len(s) for s in subsets])
+        idx = np.ascontiguousarray(np.concatenate([np.asarray(s, np.int64) for s in subsets]) if n_hyp else
+                                   np.zeros(0), dtype=np.int32)
+    cost = np.zeros(n_hyp)
+    its = np.zeros(n_hyp, np.int32)
+    st = np.zeros(n_hyp, np.int32)
+    opts = ptz_refine_opts(int(max_iter), int(loss), float(ftol), float(xtol), float(f_scale))
+    _check(lib().ptz_refine_poses(int(device), n_hyp, _ptr(ptz), len(rays), _ptr(rays), _ptr(points), float(u),
+                                  float(v), _ptr(off), _ptr(idx), ctypes.byref(opts), _ptr(cost), _ptr(its), _ptr(st)),
+           "ptz_refine_poses")
+    return ptz, cost, its, st
 
 
 def build_landmarks(kp_count, pairs):

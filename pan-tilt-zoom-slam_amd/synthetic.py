@@ -309,3 +309,72 @@ class SyntheticFrontEnd:
         image_process.detect_compute_sift = self.detect
         image_process.match_sift_features = self.match
         return self
+
+
+class _KP:
+    """cv2.KeyPoint stand-in (.pt only), usable where the product's image_process is not importable."""
+    __slots__ = ("pt",)
+
+    def __init__(self, x, y):
+        self.pt = (float(x), float(y))
+
+
+class RayFrontEnd:
+    """Deterministic detector / matcher over a known ray set for relocalisation (relocalization.py):
+    an 'image' is an integer id into `cams` ([n_img, 3] pan, tilt, f); its keypoints are the projections
+    (from_ray_to_image, the BA camera model) of the rays strictly inside the image, in ray order, capped at
+    `nfeatures`, with per-(image, ray) Gaussian pixel noise; descriptors carry (image id, ray id).
+    `match` pairs keypoints by ray id and, like the reference's match_sift_features, returns
+    (None, [], None, []) when 8 or fewer matches survive."""
+
+    def __init__(self, rays, cams, u=640.0, v=360.0, width=1280, height=720, noise=0.3, seed=0):
+        self.rays = np.asarray(rays, np.float64)
+        self.cams = np.asarray(cams, np.float64)
+        self.u, self.v, self.width, self.height = float(u), float(v), width, height
+        self.noise, self.seed = noise, seed
+
+    def keypoints(self, im, nfeatures=0):
+        pan, tilt, f = self.cams[int(im)]
+        n = len(self.rays)
+        x, y, q2 = _project(self.u, self.v, np.full(n, f), np.full(n, pan), np.full(n, tilt), self.rays[:, 0],
+                            self.rays[:, 1])
+        vis = np.flatnonzero((q2 > 0) & (x > 0) & (x < self.width) & (y > 0) & (y < self.height))
+        if nfeatures:
+            vis = vis[:nfeatures]
+        pts = np.stack([x[vis], y[vis]], 1)
+        for k, r in enumerate(vis):
+            g = np.random.default_rng(self.seed * 1000003 + int(im) * 100003 + int(r))
+            pts[k] += g.normal(0, self.noise, 2)
+        return pts, vis
+
+    def detect(self, im, nfeatures=0, verbose=False):
+        pts, vis = self.keypoints(im, nfeatures)
+        des = np.zeros((len(vis), 128), np.float32)
+        des[:, 0] = int(im)
+        des[:, 1] = vis
+        des[:, 2] = 1.0
+        return [_KP(a, b) for a, b in pts], des
+
+    def match(self, kp1, des1, kp2, des2, pts_array=False, verbose=False):
+        r1 = np.asarray(des1)[:, 1].astype(np.int64) if len(des1) else np.zeros(0, np.int64)
+        r2 = np.asarray(des2)[:, 1].astype(np.int64) if len(des2) else np.zeros(0, np.int64)
+        pos2 = {int(r): j for j, r in enumerate(r2)}
+        idx1 = [i for i, r in enumerate(r1) if int(r) in pos2]
+        idx2 = [pos2[int(r1[i])] for i in idx1]
+        if len(idx1) <= 8:
+            return None, [], None, []
+        p1 = np.array([kp1[i] if pts_array else kp1[i].pt for i in idx1], np.float64).reshape(-1, 2)
+        p2 = np.array([kp2[j] if pts_array else kp2[j].pt for j in idx2], np.float64).reshape(-1, 2)
+        return p1, idx1, p2, idx2
+
+
+def reloc_scene(seed=3):
+    """Rays + keyframe cameras + a lost camera for the relocalisation fixtures (reloc.npz)."""
+    rng = np.random.default_rng(seed)
+    n = 900
+    rays = np.stack([rng.uniform(10, 95, n), rng.uniform(-20, 4, n)], 1)
+    kf = np.array([[30.0, -8.0, 3000.0], [45.0, -8.5, 2900.0], [60.0, -7.5, 3100.0], [75.0, -8.0, 3000.0]])
+    lost_true = np.array([52.0, -7.0, 3200.0])
+    lost_init = lost_true + np.array([1.5, -0.6, 120.0])
+    cams = np.vstack([kf, lost_true[None]])  # image ids 0..3 keyframes, 4 the lost frame
+    return rays, cams, lost_init

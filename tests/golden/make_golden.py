@@ -401,13 +401,48 @@ def gen_config2():
         x_tight_huber=res_h.x, tight_cost_huber=res_h.cost, ref_residual_time=t_ref)
 
 
+
+# --------------------------------------------------------------------------------------------
+# 8. relocalisation (relocalization.py): pose-only least_squares and relocalization_camera
+# --------------------------------------------------------------------------------------------
+def gen_reloc(seed):
+    import relocalization as ref_rl  # REFERENCE module
+    import scene_map as ref_sm
+    import key_frame as ref_kf
+    assert ref_rl.__file__.startswith(REF)
+    u, v = 640.0, 360.0
+    # (1) the refinement call of relocalization.py:186 on its own, reference residual (:22-40)
+    rng = np.random.default_rng(seed)
+    true = np.array([47.0, -9.0, 3100.0])
+    px = np.stack([rng.uniform(40, 1240, 300), rng.uniform(40, 680, 300)], 1)
+    rays = np.array([ref_tf.TransFunction.from_image_to_ray(u, v, true[2], true[0], true[1], x, y) for x, y in px])
+    points = px + rng.normal(0, 0.5, px.shape)
+    pose0 = true + np.array([0.8, -0.4, 60.0])
+    r1 = least_squares(ref_rl._compute_residual, pose0, verbose=0, x_scale='jac', ftol=1e-4, method='trf',
+                       args=(rays, points, u, v))
+    rt = least_squares(ref_rl._compute_residual, pose0, x_scale='jac', ftol=1e-15, xtol=1e-15, gtol=1e-15,
+                       method='trf', args=(rays, points, u, v))
+    # (2) relocalization_camera end to end with the ray front-end monkeypatched in
+    srays, cams, lost_init = synthetic.reloc_scene(seed)
+    fe = synthetic.RayFrontEnd(srays, cams)
+    ref_ip.detect_compute_sift = fe.detect
+    ref_rl.match_sift_features = fe.match
+    m = ref_sm.Map('sift')
+    for k in range(4):
+        pan, tilt, f = cams[k]
+        m.keyframe_list.append(ref_kf.KeyFrame(k, k, np.zeros(3), np.eye(3), u, v, pan, tilt, f))
+    reloc = ref_rl.relocalization_camera(m, 4, lost_init.copy())
+    out("reloc.npz", u=u, v=v, rays=rays, points=points, pose0=pose0, x_ftol=r1.x, cost_ftol=r1.cost,
+        njev_ftol=r1.njev, x_tight=rt.x, cost_tight=rt.cost, scene_seed=seed, scene_rays=srays, scene_cams=cams,
+        lost_init=lost_init, reloc_pose=np.asarray(reloc, np.float64))
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--only", default="")
     a = ap.parse_args()
     rng = np.random.default_rng(1)
-    todo = a.only.split(",") if a.only else ["proj", "ba", "graph", "ekf", "config2"]
+    todo = a.only.split(",") if a.only else ["proj", "ba", "graph", "ekf", "config2", "reloc"]
     if "proj" in todo:
         gen_projection(rng)
     if "ba" in todo:
@@ -420,6 +455,8 @@ def main():
     if "ekf" in todo:
         gen_ekf(50, seed=4)
         gen_ekf(300, seed=5)
+    if "reloc" in todo:
+        gen_reloc(3)
     if "config2" in todo:
         gen_config2()
 

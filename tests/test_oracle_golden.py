@@ -196,3 +196,13 @@ def test_synthetic_generator_matches_reference_rules():
     frame, landmark, xy = orc.pair_records(scene.kp_xy, mi, mj, k1, k2, lm)
     np.testing.assert_array_equal(frame, prob.frame)
     np.testing.assert_allclose(xy, prob.xy)
+
+
+def test_reloc_oracle_pinned_to_reference():
+    """relocalization.py:22-40 restated: the reference's own least_squares optimum and cost."""
+    d = golden("reloc.npz")
+    u, v = float(d["u"]), float(d["v"])
+    r = orc.reloc_residual(d["x_tight"], d["rays"], d["points"], u, v)
+    assert abs(0.5 * float(r @ r) - float(d["cost_tight"])) <= 1e-9 * float(d["cost_tight"])
+    x, c = orc.refine_pose(d["pose0"], d["rays"], d["points"], u, v, ftol=1e-15, xtol=1e-15, gtol=1e-15)
+    assert np.all(np.abs(x - d["x_tight"]) <= [1e-9, 1e-9, 1e-7])
