@@ -24,6 +24,7 @@
  *   ptz_back_project_rays <- PTZCamera.back_project_to_ray(s) (ptz_camera.py:287-325), batched
  *   ptz_h_jacobian      <- PtzSlam.compute_h_jacobian (ptz_slam.py:73-138) (central FD, same steps)
  *   ptzba_build_landmarks <- build_matching_graph landmark-id bookkeeping (image_process.py:611-653)
+ *   ptz_py_shuffle_prefix / ptz_keyframe_features / ptz_pack_records <- BA data prep
  *
  * Angles are degrees, focal length / pixels as in the reference.  Poses are [pan, tilt, f] per
  * frame; rays are [theta, phi] per landmark.  Frame 0 is the fixed gauge frame (bundle_adjustment.py:197).
@@ -181,6 +182,37 @@ PTZBA_EXPORT int ptzba_build_landmarks(int32_t n_frames, const int64_t* kp_count
                                        const int64_t* pair_count, const int64_t* idx_a,
                                        const int64_t* idx_b, int64_t* landmark_out, int64_t* n_landmark,
                                        int64_t* n_inconsistent);
+
+/* ---------------- correspondence -> packed-observation builder (builder.cpp) ----------------
+ * Interpreter-defined orderings the reference's BA results depend on, reproduced bit for bit.
+ *
+ * ptz_py_shuffle_prefix <- random.shuffle(rand_list)[0:200] (image_process.py:592-597) on the GLOBAL
+ *   Mersenne Twister: mt_state[625] = random.getstate()[1] (624 words + index), updated in place for
+ *   random.setstate().  Shuffles range(lens[l]) for each list in order and writes the first
+ *   min(lens[l], keep) entries of each to out (concatenated). */
+PTZBA_EXPORT int ptz_py_shuffle_prefix(uint32_t* mt_state, int64_t n_lists, const int64_t* lens, int64_t keep,
+                                       int64_t* out);
+/* Iteration order of CPython set() built from the tuple sequence (a[k], b[k]) (non-negative ints). */
+PTZBA_EXPORT int ptz_set_order_pairs(int64_t n, const int64_t* a, const int64_t* b, int64_t* out_a,
+                                     int64_t* out_b, int64_t* n_out);
+/* Keyframe (local keypoint, landmark) lists <- bundle_adjustment.py:218-239: for frame f the tuples
+ * (src_pt_index[f][j], landmark_index[f][j]) for j ascending, then (dst_pt_index[j][f],
+ * landmark_index[j][f]) for j ascending, de-duplicated in set() iteration order.  Matches are given
+ * flat in pair order ((i, j) lexicographic, i < j): frames m_i/m_j, keypoints k1/k2, landmark lm.
+ * Output: out_off[n_frames+1] CSR over out_local/out_global (each sized >= 2 n_matches). */
+PTZBA_EXPORT int ptz_keyframe_features(int32_t n_frames, int64_t n_matches, const int32_t* m_i,
+                                       const int32_t* m_j, const int64_t* k1, const int64_t* k2,
+                                       const int64_t* lm, int64_t* out_off, int64_t* out_local,
+                                       int64_t* out_global);
+/* Pair-form records in _compute_residual order (bundle_adjustment.py:67-99): record 2k = (m_i, k1),
+ * 2k+1 = (m_j, k2), both on landmark lm[k]; xy from the keypoint table kp_xy[kp_off[f] + k][2].
+ * landmark_src_rec[l] = record of the src observation of the LAST match of landmark l, the one the
+ * reference initialises the ray from (bundle_adjustment.py:186-195), -1 if none. */
+PTZBA_EXPORT int ptz_pack_records(int32_t n_frames, int64_t n_matches, const int32_t* m_i, const int32_t* m_j,
+                                  const int64_t* k1, const int64_t* k2, const int64_t* lm,
+                                  const int64_t* kp_off, const double* kp_xy, int64_t n_landmark,
+                                  int32_t* rec_frame, int32_t* rec_landmark, double* rec_xy,
+                                  int64_t* landmark_src_rec);
 
 /* ---------------- EKF tracking state (ptz_slam.py:21-71, 210-315, 376-384, 424-426) ----------------
  * A handle owns the ray landmarks [R][2] and the dense state covariance [(3+2R)][(3+2R)] (row-major,

@@ -13,6 +13,8 @@ Same signature, steps and outputs as the reference (bundle_adjustment.py:109-251
      ftol=1e-4, method='trf')` (:200-202) is replaced by the GPU Levenberg-Marquardt of libptzba
      (exact Schur-complement steps, same ftol termination rule), frame 0 fixed     (:197)
   5. KeyFrame assembly with the reference's set() de-duplication order            (:214-248)
+Steps 2, 3 and 5 run on correspondence.MatchGraph (native builder); pass a
+correspondence.CorrespondenceCache as `correspondences=` to skip re-detection/re-matching.
 
 Extra keyword arguments (all optional) select the numerics: precision ('fp64' default, 'fp32'),
 loss ('linear' as the reference, or 'huber'), f_scale, ftol/xtol/max_iter, device.
@@ -31,31 +33,34 @@ from util import overlap_pan_angle
 LAST_RESULT = {}
 
 
-def _records(n_pose, keypoints, src_pt_index, dst_pt_index, landmark_index):
-    """Pair-form records in the reference's residual order (bundle_adjustment.py:67-99):
-    for i, for j, for each match -> record (i, kp1) then (j, kp2)."""
-    fr, lm, xy = [], [], []
+def _flatten(n_pose, src_pt_index, dst_pt_index, landmark_index):
+    """Flat match arrays (m_i, m_j, k1, k2, lm) in the reference's residual loop order
+    (bundle_adjustment.py:67-99: for i, for j, for each match)."""
+    mi, mj, a, b, l = [], [], [], [], []
     for i in range(n_pose):
         for j in range(n_pose):
             s = src_pt_index[i][j]
             if len(s) == 0:
                 continue
-            a = np.asarray(s, np.int64)
-            b = np.asarray(dst_pt_index[i][j], np.int64)
-            l = np.asarray(landmark_index[i][j], np.int64)
-            m = len(a)
-            f = np.empty(2 * m, np.int32)
-            f[0::2] = i
-            f[1::2] = j
-            p = np.empty((2 * m, 2))
-            p[0::2] = np.asarray(keypoints[i], np.float64)[a]
-            p[1::2] = np.asarray(keypoints[j], np.float64)[b]
-            fr.append(f)
-            lm.append(np.repeat(l, 2).astype(np.int32))
-            xy.append(p)
-    if not fr:
-        return np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros((0, 2))
-    return np.concatenate(fr), np.concatenate(lm), np.concatenate(xy)
+            a.append(np.asarray(s, np.int64))
+            b.append(np.asarray(dst_pt_index[i][j], np.int64))
+            l.append(np.asarray(landmark_index[i][j], np.int64))
+            mi.append(np.full(len(s), i, np.int32))
+            mj.append(np.full(len(s), j, np.int32))
+    cat = lambda x, t: np.concatenate(x) if x else np.zeros(0, t)
+    return cat(mi, np.int32), cat(mj, np.int32), cat(a, np.int64), cat(b, np.int64), cat(l, np.int64)
+
+
+def _records(n_pose, keypoints, src_pt_index, dst_pt_index, landmark_index):
+    """Pair-form records in the reference's residual order: for i, for j, for each match ->
+    record (i, kp1) then (j, kp2)."""
+    mi, mj, a, b, l = _flatten(n_pose, src_pt_index, dst_pt_index, landmark_index)
+    pts = [np.asarray(k, np.float64).reshape(-1, 2) for k in keypoints]
+    kp_off = np.concatenate([[0], np.cumsum([len(p) for p in pts])]).astype(np.int64)
+    kp_xy = np.concatenate(pts) if pts else np.zeros((0, 2))
+    n_lm = int(l.max()) + 1 if len(l) else 0
+    fr, lm, xy, _ = ptzba.pack_records(n_pose, mi, mj, a, b, l, kp_off, kp_xy, n_lm)
+    return fr, lm, xy
 
 
 def _compute_residual(x, n_pose, n_landmark, n_residual, keypoints, src_pt_index, dst_pt_index, landmark_index, u, v,
@@ -81,8 +86,11 @@ def _compute_residual(x, n_pose, n_landmark, n_residual, keypoints, src_pt_index
 
 def bundle_adjustment(images, image_indices, feature_method, initial_ptzs, center, rotation, u, v, save_path,
                       verbose=False, precision="fp64", loss="linear", f_scale=1.0, ftol=1e-4, xtol=1e-8,
-                      max_iter=100, device=0):
-    """bundle_adjustment.py:109-251 on the MI355X path.  Returns (landmarks [M,2], keyframes)."""
+                      max_iter=100, device=0, correspondences=None):
+    """bundle_adjustment.py:109-251 on the MI355X path.  Returns (landmarks [M,2], keyframes).
+    `correspondences`: optional correspondence.CorrespondenceCache keyed by image_indices, so repeated
+    calls over growing / sliding keyframe sets only detect new images and match new pairs."""
+    import correspondence
     N = len(images)
     assert N >= 1
     assert len(image_indices) == N
@@ -90,6 +98,8 @@ def bundle_adjustment(images, image_indices, feature_method, initial_ptzs, cente
     assert initial_ptzs.shape[0] == N and initial_ptzs.shape[1] == 3
     assert np.asarray(center).shape[0] == 3 and np.asarray(rotation).shape == (3, 3)
     assert feature_method in ("sift", "orb", "latch")
+    timing = {}
+    t_start = time.time()
 
     # step 1: pair mask (bundle_adjustment.py:135-144)
     image_match_mask = [[0 for _ in range(N)] for _ in range(N)]
@@ -98,39 +108,43 @@ def bundle_adjustment(images, image_indices, feature_method, initial_ptzs, cente
             if overlap_pan_angle(initial_ptzs[i][2], initial_ptzs[i][0], initial_ptzs[j][2], initial_ptzs[j][0],
                                  1280) > 5:
                 image_match_mask[i][j] = 1
-    keypoints, descriptors, points, src_pt_index, dst_pt_index, landmark_index, n_landmark = \
-        image_process.build_matching_graph(images, image_match_mask, feature_method, verbose)
+    g = correspondence.build_graph(images, image_match_mask, feature_method, verbose, cache=correspondences,
+                                   keys=list(image_indices))
+    keypoints, descriptors, n_landmark = g.keypoints, g.descriptors, g.n_landmark
     if image_process.draw_matches is not None and save_path:
-        for i in range(N):
-            for j in range(N):
-                if len(src_pt_index[i][j]):
-                    image_process.draw_matches(images[i], images[j], points[i].take(src_pt_index[i][j], axis=0),
-                                               points[j].take(dst_pt_index[i][j], axis=0),
-                                               save_path + "/" + str(i) + "_" + str(j) + ".jpg")
+        pts = g.points()
+        for p in range(len(g.pair_i)):
+            i, j = int(g.pair_i[p]), int(g.pair_j[p])
+            a, b = g.pair_off[p], g.pair_off[p + 1]
+            image_process.draw_matches(images[i], images[j], pts[i][g.k1[a:b]], pts[j][g.k2[a:b]],
+                                       save_path + "/" + str(i) + "_" + str(j) + ".jpg")
+    timing["graph"] = time.time() - t_start
 
     # step 2: data (bundle_adjustment.py:167-197)
-    n_residual = sum(len(src_pt_index[i][j]) * 4 for i in range(N) for j in range(N))
+    t1 = time.time()
+    n_residual = 4 * g.n_matches
     if verbose:
         print("residual number is %d." % n_residual)
     ref_pose = initial_ptzs[0]
-    frame, lm, xy = _records(N, points, src_pt_index, dst_pt_index, landmark_index)
+    frame, lm, xy, src_rec = g.records()
     rays0 = np.zeros((n_landmark, 2))
     if n_landmark:
-        # last writer wins: the src record (even records) of the last match referencing each landmark
-        src_lm = lm[0::2]
-        last = len(src_lm) - 1 - np.unique(src_lm[::-1], return_index=True)[1]
-        lids = src_lm[last]
-        fi = frame[0::2][last]
-        pts = xy[0::2][last]
-        th, ph = ptzba.image_to_ray(u, v, initial_ptzs[fi, 2], initial_ptzs[fi, 0], initial_ptzs[fi, 1], pts[:, 0],
-                                    pts[:, 1], device=device)
+        # each ray from the src observation of the last match referencing it (last writer wins)
+        has = src_rec >= 0
+        lids = np.flatnonzero(has)
+        rec = src_rec[has]
+        fi = frame[rec]
+        th, ph = ptzba.image_to_ray(u, v, initial_ptzs[fi, 2], initial_ptzs[fi, 0], initial_ptzs[fi, 1], xy[rec, 0],
+                                    xy[rec, 1], device=device)
         rays0[lids, 0] = th
         rays0[lids, 1] = ph
+    timing["records"] = time.time() - t1
 
     # step 3: optimisation on the GPU (replaces bundle_adjustment.py:200-202)
     t0 = time.time()
     all_poses = initial_ptzs.copy()
     landmarks = rays0.copy()
+    res = None
     if len(frame):
         prec = ptzba.FP32 if precision == "fp32" else ptzba.FP64
         ls = ptzba.LOSS_HUBER if loss == "huber" else ptzba.LOSS_LINEAR
@@ -138,37 +152,27 @@ def bundle_adjustment(images, image_indices, feature_method, initial_ptzs, cente
                                                 loss=ls, f_scale=f_scale, device=device, ftol=ftol, xtol=xtol,
                                                 max_iter=max_iter)
         all_poses[0] = ref_pose
-        LAST_RESULT.clear()
-        LAST_RESULT.update(result=res, n_residual=n_residual, n_landmark=n_landmark, time=time.time() - t0,
-                           x0=np.concatenate([initial_ptzs[1:].reshape(-1), rays0.reshape(-1)]))
         if verbose:
             print(f"GPU LM: {res}")
+    timing["solve"] = time.time() - t0
 
-    # step 5: keyframes (bundle_adjustment.py:214-248)
+    # step 5: keyframes (bundle_adjustment.py:214-248), features in the reference's set() order
+    t2 = time.time()
+    off, loc, glo = g.keyframe_features()
     keyframes = []
     for i in range(N):
         pan, tilt, fl = all_poses[i]
         key_frame = KeyFrame(images[i], image_indices[i], center, rotation, u, v, pan, tilt, fl)
-        pairs = []
-        for j in range(N):
-            if len(src_pt_index[i][j]) == 0:
-                continue
-            for idx1, idx3 in zip(src_pt_index[i][j], landmark_index[i][j]):
-                pairs.append((idx1, idx3))
-        for j in range(N):
-            if len(dst_pt_index[j][i]) == 0:
-                continue
-            for idx2, idx3 in zip(dst_pt_index[j][i], landmark_index[j][i]):
-                pairs.append((idx2, idx3))
-        pairs = set(pairs)
-        local_index, global_index = [], []
-        for pair in pairs:
-            local_index.append(pair[0])
-            global_index.append(pair[1])
-        key_frame.feature_pts = [keypoints[i][j] for j in local_index]
+        local_index = loc[off[i]:off[i + 1]]
+        kps = keypoints[i]
+        key_frame.feature_pts = list(map(kps.__getitem__, local_index.tolist()))
         key_frame.feature_des = np.asarray(descriptors[i]).take(local_index, axis=0)
-        key_frame.landmark_index = np.array(global_index, dtype=np.int32)
+        key_frame.landmark_index = glo[off[i]:off[i + 1]].astype(np.int32)
         keyframes.append(key_frame)
         if verbose:
             print("frame %d, landmark number %d" % (image_indices[i], len(key_frame.landmark_index)))
+    timing["keyframes"] = time.time() - t2
+    LAST_RESULT.clear()
+    LAST_RESULT.update(result=res, n_residual=n_residual, n_landmark=n_landmark, time=timing["solve"],
+                       timing=timing, x0=np.concatenate([initial_ptzs[1:].reshape(-1), rays0.reshape(-1)]))
     return landmarks, keyframes

@@ -1,0 +1,297 @@
+// Correspondence -> packed-observation builder (host, native).  SURVEY §8f-2.
+//
+// The reference assembles the BA problem in Python loops (image_process.py:568-667,
+// bundle_adjustment.py:167-197, 214-248).  Three of its steps carry interpreter-defined ordering that the
+// results depend on bit for bit; they are reproduced here exactly, so a native build is a drop-in:
+//
+//   * the 200-match cap draws `random.shuffle` from the GLOBAL Mersenne Twister (image_process.py:592-597):
+//     ptz_py_shuffle_prefix replays CPython's shuffle / _randbelow / getrandbits on that generator's
+//     state (random.getstate() in, random.setstate() out);
+//   * keyframe features are the iteration order of `set(pairs)` over (local, global) tuples
+//     (bundle_adjustment.py:222-239): ptz_keyframe_features inserts the same tuple sequence into an
+//     open-addressing table with CPython's tuple hash (xxHash lanes, 3.8+) and set probing (linear
+//     probes + perturbation, resize policy), then reads the table in slot order;
+//   * x0 rays come from the src observation of the LAST match of each landmark (bundle_adjustment.py:
+//     186-195): ptz_pack_records reports that record per landmark while packing.
+//
+// Python verifies the two interpreter-defined emulations against the live interpreter once per process
+// (correspondence.py:_self_check) and uses the interpreter itself if they ever disagree.
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../../include/ptzba.h"
+#include "host_util.h"
+
+using ptzba::fail;
+
+namespace {
+
+// ---- MT19937 exactly as CPython's _randommodule.c (genrand_uint32) ----
+constexpr int MT_N = 624, MT_M = 397;
+
+struct MT {
+  uint32_t s[MT_N];
+  int idx;
+  uint32_t next() {
+    if (idx >= MT_N) {
+      static const uint32_t mag01[2] = {0u, 0x9908b0dfu};
+      int kk = 0;
+      uint32_t y;
+      for (; kk < MT_N - MT_M; kk++) {
+        y = (s[kk] & 0x80000000u) | (s[kk + 1] & 0x7fffffffu);
+        s[kk] = s[kk + MT_M] ^ (y >> 1) ^ mag01[y & 1u];
+      }
+      for (; kk < MT_N - 1; kk++) {
+        y = (s[kk] & 0x80000000u) | (s[kk + 1] & 0x7fffffffu);
+        s[kk] = s[kk + (MT_M - MT_N)] ^ (y >> 1) ^ mag01[y & 1u];
+      }
+      y = (s[MT_N - 1] & 0x80000000u) | (s[0] & 0x7fffffffu);
+      s[MT_N - 1] = s[MT_M - 1] ^ (y >> 1) ^ mag01[y & 1u];
+      idx = 0;
+    }
+    uint32_t y = s[idx++];
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+  }
+  // Random._randbelow_with_getrandbits(n), n < 2^31: k = n.bit_length(); r = getrandbits(k) until r < n
+  uint32_t below(uint32_t n) {
+    const int k = 32 - __builtin_clz(n);
+    uint32_t r;
+    do {
+      r = next() >> (32 - k);
+    } while (r >= n);
+    return r;
+  }
+};
+
+// ---- CPython 3.8+ tuple hash of a 2-tuple of non-negative ints (< 2^61 - 1, so hash(int) == int) ----
+inline uint64_t tuple2_hash(uint64_t a, uint64_t b) {
+  const uint64_t P1 = 11400714785074694791ull, P2 = 14029467366897019727ull, P5 = 2870177450012600261ull;
+  uint64_t acc = P5;
+  acc += a * P2;
+  acc = (acc << 31) | (acc >> 33);
+  acc *= P1;
+  acc += b * P2;
+  acc = (acc << 31) | (acc >> 33);
+  acc *= P1;
+  acc += 2ull ^ (P5 ^ 3527539ull);
+  if (acc == ~0ull) return 1546275796ull;
+  return acc;
+}
+
+// ---- CPython set (Objects/setobject.c): insertion-only table, iteration = slot order ----
+struct PySetEmu {
+  static constexpr size_t LINEAR_PROBES = 9, PERTURB_SHIFT = 5, MINSIZE = 8;
+  struct Slot {
+    int64_t a, b;
+    uint64_t h;
+    bool used;
+  };
+  std::vector<Slot> t;
+  size_t mask = MINSIZE - 1, fill = 0;
+
+  void reset() {
+    t.assign(MINSIZE, Slot{0, 0, 0, false});
+    mask = MINSIZE - 1;
+    fill = 0;
+  }
+  static void insert_clean(std::vector<Slot>& tab, size_t m, const Slot& e) {
+    size_t perturb = e.h, i = e.h & m;
+    for (;;) {
+      if (!tab[i].used) {
+        tab[i] = e;
+        return;
+      }
+      if (i + LINEAR_PROBES <= m) {
+        for (size_t j = 1; j <= LINEAR_PROBES; ++j)
+          if (!tab[i + j].used) {
+            tab[i + j] = e;
+            return;
+          }
+      }
+      perturb >>= PERTURB_SHIFT;
+      i = (i * 5 + 1 + perturb) & m;
+    }
+  }
+  void resize(size_t minused) {
+    size_t ns = MINSIZE;
+    while (ns <= minused) ns <<= 1;
+    std::vector<Slot> nt(ns, Slot{0, 0, 0, false});
+    for (size_t k = 0; k <= mask; ++k)
+      if (t[k].used) insert_clean(nt, ns - 1, t[k]);
+    t.swap(nt);
+    mask = ns - 1;
+  }
+  void add(int64_t a, int64_t b) {
+    const uint64_t h = tuple2_hash((uint64_t)a, (uint64_t)b);
+    size_t i = h & mask, perturb = h;
+    size_t slot;
+    if (!t[i].used) {
+      slot = i;
+    } else {
+      for (;;) {
+        if (t[i].h == h && t[i].a == a && t[i].b == b) return;  // already present
+        bool found = false;
+        if (i + LINEAR_PROBES <= mask) {
+          for (size_t j = 1; j <= LINEAR_PROBES; ++j) {
+            const Slot& e = t[i + j];
+            if (!e.used) {
+              slot = i + j;
+              found = true;
+              break;
+            }
+            if (e.h == h && e.a == a && e.b == b) return;
+          }
+        }
+        if (found) break;
+        perturb >>= PERTURB_SHIFT;
+        i = (i * 5 + 1 + perturb) & mask;
+        if (!t[i].used) {
+          slot = i;
+          break;
+        }
+      }
+    }
+    t[slot] = Slot{a, b, h, true};
+    ++fill;  // no deletions: fill == used
+    if (fill * 5 < mask * 3) return;
+    resize(fill > 50000 ? fill * 2 : fill * 4);
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int ptz_py_shuffle_prefix(uint32_t* mt_state, int64_t n_lists, const int64_t* lens, int64_t keep,
+                          int64_t* out) {
+  if (!mt_state || n_lists < 0 || keep < 0) return fail("ptz_py_shuffle_prefix: bad arguments");
+  if (mt_state[MT_N] > (uint32_t)MT_N) return fail("ptz_py_shuffle_prefix: bad generator index");
+  MT g;
+  memcpy(g.s, mt_state, sizeof(g.s));
+  g.idx = (int)mt_state[MT_N];
+  std::vector<int64_t> perm;
+  int64_t o = 0;
+  for (int64_t l = 0; l < n_lists; ++l) {
+    const int64_t n = lens[l];
+    if (n < 0 || n >= (int64_t)1 << 31) return fail("ptz_py_shuffle_prefix: list %lld length %lld", (long long)l,
+                                                    (long long)n);
+    perm.resize((size_t)n);
+    for (int64_t k = 0; k < n; ++k) perm[k] = k;
+    // random.shuffle: for i in reversed(range(1, len(x))): j = _randbelow(i + 1); swap
+    for (int64_t i = n - 1; i >= 1; --i) {
+      const int64_t j = g.below((uint32_t)(i + 1));
+      const int64_t t = perm[i];
+      perm[i] = perm[j];
+      perm[j] = t;
+    }
+    const int64_t m = n < keep ? n : keep;
+    for (int64_t k = 0; k < m; ++k) out[o + k] = perm[k];
+    o += m;
+  }
+  memcpy(mt_state, g.s, sizeof(g.s));
+  mt_state[MT_N] = (uint32_t)g.idx;
+  return 0;
+}
+
+int ptz_set_order_pairs(int64_t n, const int64_t* a, const int64_t* b, int64_t* out_a, int64_t* out_b,
+                        int64_t* n_out) {
+  PySetEmu s;
+  s.reset();
+  for (int64_t k = 0; k < n; ++k) {
+    if (a[k] < 0 || b[k] < 0) return fail("ptz_set_order_pairs: negative value");
+    s.add(a[k], b[k]);
+  }
+  int64_t o = 0;
+  for (size_t k = 0; k <= s.mask; ++k)
+    if (s.t[k].used) {
+      out_a[o] = s.t[k].a;
+      out_b[o] = s.t[k].b;
+      ++o;
+    }
+  *n_out = o;
+  return 0;
+}
+
+int ptz_keyframe_features(int32_t n_frames, int64_t n_matches, const int32_t* m_i, const int32_t* m_j,
+                          const int64_t* k1, const int64_t* k2, const int64_t* lm, int64_t* out_off,
+                          int64_t* out_local, int64_t* out_global) {
+  if (n_frames < 0 || n_matches < 0) return fail("ptz_keyframe_features: bad sizes");
+  // matches must be in the reference's pair order: (i, j) lexicographic, i < j
+  for (int64_t k = 0; k < n_matches; ++k) {
+    if (m_i[k] < 0 || m_j[k] >= n_frames || m_i[k] >= m_j[k])
+      return fail("ptz_keyframe_features: match %lld has bad frames (%d, %d)", (long long)k, m_i[k], m_j[k]);
+    if (k && (m_i[k] < m_i[k - 1] || (m_i[k] == m_i[k - 1] && m_j[k] < m_j[k - 1])))
+      return fail("ptz_keyframe_features: matches not in (i, j) order at %lld", (long long)k);
+    if (k1[k] < 0 || k2[k] < 0 || lm[k] < 0) return fail("ptz_keyframe_features: negative index at %lld",
+                                                          (long long)k);
+  }
+  // src role of frame f: matches with m_i == f (contiguous, j ascending); dst role: matches with
+  // m_j == f in global order (= m_i ascending) -> stable counting sort by m_j
+  std::vector<int64_t> src_off(n_frames + 1, 0), dst_off(n_frames + 1, 0), dst_list(n_matches);
+  for (int64_t k = 0; k < n_matches; ++k) {
+    src_off[m_i[k] + 1]++;
+    dst_off[m_j[k] + 1]++;
+  }
+  for (int f = 0; f < n_frames; ++f) {
+    src_off[f + 1] += src_off[f];
+    dst_off[f + 1] += dst_off[f];
+  }
+  {
+    std::vector<int64_t> cur(dst_off.begin(), dst_off.end() - 1);
+    for (int64_t k = 0; k < n_matches; ++k) dst_list[cur[m_j[k]]++] = k;
+  }
+  PySetEmu s;
+  int64_t o = 0;
+  out_off[0] = 0;
+  for (int f = 0; f < n_frames; ++f) {
+    s.reset();
+    for (int64_t k = src_off[f]; k < src_off[f + 1]; ++k) s.add(k1[k], lm[k]);
+    for (int64_t q = dst_off[f]; q < dst_off[f + 1]; ++q) {
+      const int64_t k = dst_list[q];
+      s.add(k2[k], lm[k]);
+    }
+    for (size_t k = 0; k <= s.mask; ++k)
+      if (s.t[k].used) {
+        out_local[o] = s.t[k].a;
+        out_global[o] = s.t[k].b;
+        ++o;
+      }
+    out_off[f + 1] = o;
+  }
+  return 0;
+}
+
+int ptz_pack_records(int32_t n_frames, int64_t n_matches, const int32_t* m_i, const int32_t* m_j,
+                     const int64_t* k1, const int64_t* k2, const int64_t* lm, const int64_t* kp_off,
+                     const double* kp_xy, int64_t n_landmark, int32_t* rec_frame, int32_t* rec_landmark,
+                     double* rec_xy, int64_t* landmark_src_rec) {
+  if (n_frames < 0 || n_matches < 0 || n_landmark < 0) return fail("ptz_pack_records: bad sizes");
+  for (int64_t l = 0; l < n_landmark; ++l) landmark_src_rec[l] = -1;
+  for (int64_t k = 0; k < n_matches; ++k) {
+    const int i = m_i[k], j = m_j[k];
+    if (i < 0 || i >= n_frames || j < 0 || j >= n_frames) return fail("ptz_pack_records: match %lld frame", (long long)k);
+    const int64_t a = k1[k], b = k2[k], l = lm[k];
+    if (a < 0 || a >= kp_off[i + 1] - kp_off[i] || b < 0 || b >= kp_off[j + 1] - kp_off[j])
+      return fail("ptz_pack_records: match %lld keypoint out of range", (long long)k);
+    if (l < 0 || l >= n_landmark) return fail("ptz_pack_records: match %lld landmark out of range", (long long)k);
+    const double* p = kp_xy + 2 * (kp_off[i] + a);
+    const double* q = kp_xy + 2 * (kp_off[j] + b);
+    rec_frame[2 * k] = i;
+    rec_frame[2 * k + 1] = j;
+    rec_landmark[2 * k] = rec_landmark[2 * k + 1] = (int32_t)l;
+    rec_xy[4 * k + 0] = p[0];
+    rec_xy[4 * k + 1] = p[1];
+    rec_xy[4 * k + 2] = q[0];
+    rec_xy[4 * k + 3] = q[1];
+    landmark_src_rec[l] = 2 * k;  // last writer wins
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -15,12 +15,9 @@ What this module does implement is the bookkeeping of `build_matching_graph`
     module (:592-597), so a seeded `random` reproduces the reference bit for bit;
   * landmark ids by the first-seen rule (:611-639) — computed natively in libptzba
     (ptzba_build_landmarks), including the count of the reference's "in-consistent matching" warnings.
+The graph itself is built by correspondence.build_graph (flat arrays, native cap-shuffle replay).
 """
-import random
-
 import numpy as np
-
-import ptzba
 
 
 class KeyPoint:
@@ -108,52 +105,9 @@ def _match(kp1, des1, kp2, des2, feature_method):
 
 def build_matching_graph(images, image_match_mask=[], feature_method="sift", verbose=False):
     """image_process.py:509-667.  Returns (keypoints, descriptors, points, src_pt_index, dst_pt_index,
-    landmark_index, landmark_num) with identical contents and list ordering."""
-    assert feature_method in ("sift", "orb", "latch")
-    n = len(images)
-    if len(image_match_mask) != 0:
-        assert len(image_match_mask) == n
-        for m in image_match_mask:
-            assert len(m) == n
-    elif verbose:
-        print("Warning: image match mask is NOT used, may have false positive matches!")
-    keypoints, descriptors = [], []
-    for im in images:
-        kp, des = _detect(im, feature_method)
-        keypoints.append(kp)
-        descriptors.append(des)
-    min_match_num, max_match_num = 20, 200
-    pairs = []
-    for i in range(n):
-        for j in range(i + 1, n):
-            if len(image_match_mask) != 0 and image_match_mask[i][j] == 0:
-                continue
-            _, index1, _, index2 = _match(keypoints[i], descriptors[i], keypoints[j], descriptors[j], feature_method)
-            assert len(index1) == len(index2)
-            if len(index1) > min_match_num:
-                if len(index1) > max_match_num:
-                    rand_list = list(range(len(index1)))
-                    random.shuffle(rand_list)
-                    rand_list = rand_list[0:max_match_num]
-                    index1 = [index1[k] for k in rand_list]
-                    index2 = [index2[k] for k in rand_list]
-                pairs.append((i, j, [int(a) for a in index1], [int(b) for b in index2]))
-                if verbose:
-                    print("%d matches between image: %d and %d" % (len(index1), i, j))
-            elif verbose:
-                print("no enough matches between image: %d and %d" % (i, j))
-    kp_count = [len(k) for k in keypoints]
-    lm_lists, n_landmark, n_inconsistent = ptzba.build_landmarks(kp_count, pairs) if pairs else ([], 0, 0)
-    if n_inconsistent and verbose:
-        print("Warning: %d in-consistent matching results" % n_inconsistent)
-    src = [[[] for _ in range(n)] for _ in range(n)]
-    dst = [[[] for _ in range(n)] for _ in range(n)]
-    lmk = [[[] for _ in range(n)] for _ in range(n)]
-    for (i, j, a, b), lm in zip(pairs, lm_lists):
-        src[i][j] = a
-        dst[i][j] = b
-        lmk[i][j] = [int(x) for x in lm]
-    points = [np.array([k.pt for k in kps], dtype=np.float64).reshape(-1, 2) for kps in keypoints]
-    if verbose:
-        print("number of landmark is %d" % n_landmark)
-    return keypoints, descriptors, points, src, dst, lmk, n_landmark
+    landmark_index, landmark_num) with identical contents and list ordering (built natively by
+    correspondence.build_graph; see there for the cap-shuffle replay)."""
+    import correspondence
+    g = correspondence.build_graph(images, image_match_mask, feature_method, verbose)
+    src, dst, lmk = g.lists()
+    return g.keypoints, g.descriptors, g.points(), src, dst, lmk, g.n_landmark

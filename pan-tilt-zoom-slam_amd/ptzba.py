@@ -91,6 +91,10 @@ def lib():
         "ptz_back_project_rays": ([I, I64, D, D, D, D, D, V, V, V], I),
         "ptz_h_jacobian": ([I, I64, D, D, D, D, D, V, V, V], I),
         "ptzba_build_landmarks": ([I32, V, I64, V, V, V, V, V, V, V, V], I),
+        "ptz_py_shuffle_prefix": ([V, I64, V, I64, V], I),
+        "ptz_set_order_pairs": ([I64, V, V, V, V, V], I),
+        "ptz_keyframe_features": ([I32, I64, V, V, V, V, V, V, V, V], I),
+        "ptz_pack_records": ([I32, I64, V, V, V, V, V, V, V, I64, V, V, V, V], I),
         "ptz_refine_poses": ([I, I32, V, I64, V, V, D, D, V, V, POINTER(ptz_refine_opts), V, V, V], I),
         "ptzekf_new": ([I], V),
         "ptzekf_delete": ([V], None),
@@ -117,6 +121,7 @@ EXPORTED_SYMBOLS = [
     "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_read_scalars", "ptzba_accept",
     "ptzba_exchange", "ptzba_exchange_packed", "ptzba_pack", "ptzba_unpack", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptz_ray_to_image",
     "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks",
+    "ptz_py_shuffle_prefix", "ptz_set_order_pairs", "ptz_keyframe_features", "ptz_pack_records",
     "ptz_refine_poses", "ptzekf_new", "ptzekf_delete", "ptzekf_num_rays", "ptzekf_set_state", "ptzekf_get_state", "ptzekf_add_pose_cov",
     "ptzekf_remove_rays", "ptzekf_add_rays", "ptzekf_project_visible", "ptzekf_update",
 ]
@@ -232,23 +237,96 @@ def refine_poses(u, v, init_ptz, rays, points, subsets=None, ftol=1e-4, xtol=1e-
     return ptz, cost, its, st
 
 
-def build_landmarks(kp_count, pairs):
-    """First-seen landmark ids (image_process.py:611-653) in native code.
-    pairs: ordered list of (i, j, idx_a, idx_b).  Returns (list of per-pair landmark arrays, n_landmark,
-    n_inconsistent)."""
+def build_landmarks_flat(kp_count, pair_i, pair_j, pair_count, idx_a, idx_b):
+    """First-seen landmark ids (image_process.py:611-653) in native code, over flat pair arrays.
+    Returns (landmark id per match int64, n_landmark, n_inconsistent)."""
     kp = np.ascontiguousarray(kp_count, dtype=np.int64)
-    pi = np.array([p[0] for p in pairs], np.int32)
-    pj = np.array([p[1] for p in pairs], np.int32)
-    cnt = np.array([len(p[2]) for p in pairs], np.int64)
-    a = np.ascontiguousarray(np.concatenate([np.asarray(p[2], np.int64) for p in pairs]) if pairs else np.zeros(0, np.int64))
-    b = np.ascontiguousarray(np.concatenate([np.asarray(p[3], np.int64) for p in pairs]) if pairs else np.zeros(0, np.int64))
+    pi = np.ascontiguousarray(pair_i, dtype=np.int32)
+    pj = np.ascontiguousarray(pair_j, dtype=np.int32)
+    cnt = np.ascontiguousarray(pair_count, dtype=np.int64)
+    a = np.ascontiguousarray(idx_a, dtype=np.int64)
+    b = np.ascontiguousarray(idx_b, dtype=np.int64)
+    assert len(pi) == len(pj) == len(cnt) and len(a) == len(b) == int(cnt.sum())
     out = np.empty(len(a), np.int64)
     nl = c_int64(0)
     ninc = c_int64(0)
-    _check(lib().ptzba_build_landmarks(len(kp), _ptr(kp), len(pairs), _ptr(pi), _ptr(pj), _ptr(cnt), _ptr(a), _ptr(b),
+    _check(lib().ptzba_build_landmarks(len(kp), _ptr(kp), len(pi), _ptr(pi), _ptr(pj), _ptr(cnt), _ptr(a), _ptr(b),
                                        _ptr(out), ctypes.addressof(nl), ctypes.addressof(ninc)), "ptzba_build_landmarks")
+    return out, int(nl.value), int(ninc.value)
+
+
+def build_landmarks(kp_count, pairs):
+    """build_landmarks_flat over an ordered list of (i, j, idx_a, idx_b).  Returns (list of per-pair
+    landmark arrays, n_landmark, n_inconsistent)."""
+    cnt = np.array([len(p[2]) for p in pairs], np.int64)
+    cat = lambda k: np.concatenate([np.asarray(p[k], np.int64) for p in pairs]) if pairs else np.zeros(0, np.int64)
+    out, nl, ninc = build_landmarks_flat(kp_count, [p[0] for p in pairs], [p[1] for p in pairs], cnt, cat(2), cat(3))
     offs = np.concatenate([[0], np.cumsum(cnt)])
-    return [out[offs[k]:offs[k + 1]] for k in range(len(pairs))], int(nl.value), int(ninc.value)
+    return [out[offs[k]:offs[k + 1]] for k in range(len(pairs))], nl, ninc
+
+
+def py_shuffle_prefix(lens, keep, rand=None):
+    """random.shuffle(list(range(n)))[:keep] for each n in `lens`, in order, drawn from the Mersenne Twister
+    of `rand` (default: the global `random` module, as image_process.py:592-597), whose state advances
+    exactly as the interpreter's own shuffles would.  Returns the concatenated prefixes (int64)."""
+    import random as _random
+    rand = _random if rand is None else rand
+    version, internal, gauss = rand.getstate()
+    mt = np.array(internal, dtype=np.uint32)
+    lens = np.ascontiguousarray(lens, dtype=np.int64)
+    out = np.empty(int(np.minimum(lens, keep).sum()), np.int64)
+    _check(lib().ptz_py_shuffle_prefix(_ptr(mt), len(lens), _ptr(lens), int(keep), _ptr(out)), "ptz_py_shuffle_prefix")
+    rand.setstate((version, tuple(int(x) for x in mt), gauss))
+    return out
+
+
+def set_order_pairs(a, b):
+    """Iteration order of set(zip(a, b)) (CPython 3.8+ tuple hash and set probing), in native code."""
+    a = np.ascontiguousarray(a, dtype=np.int64)
+    b = np.ascontiguousarray(b, dtype=np.int64)
+    oa = np.empty(len(a), np.int64)
+    ob = np.empty(len(a), np.int64)
+    n = c_int64(0)
+    _check(lib().ptz_set_order_pairs(len(a), _ptr(a), _ptr(b), _ptr(oa), _ptr(ob), ctypes.addressof(n)),
+           "ptz_set_order_pairs")
+    return oa[:n.value], ob[:n.value]
+
+
+def keyframe_features(n_frames, m_i, m_j, k1, k2, lm):
+    """Per-keyframe (local keypoint, landmark) lists in the reference's set() order
+    (bundle_adjustment.py:218-239).  Returns (off [n_frames+1], local, global) CSR arrays."""
+    m_i = np.ascontiguousarray(m_i, dtype=np.int32)
+    m_j = np.ascontiguousarray(m_j, dtype=np.int32)
+    k1 = np.ascontiguousarray(k1, dtype=np.int64)
+    k2 = np.ascontiguousarray(k2, dtype=np.int64)
+    lm = np.ascontiguousarray(lm, dtype=np.int64)
+    off = np.empty(n_frames + 1, np.int64)
+    loc = np.empty(2 * len(m_i), np.int64)
+    glo = np.empty(2 * len(m_i), np.int64)
+    _check(lib().ptz_keyframe_features(int(n_frames), len(m_i), _ptr(m_i), _ptr(m_j), _ptr(k1), _ptr(k2), _ptr(lm),
+                                       _ptr(off), _ptr(loc), _ptr(glo)), "ptz_keyframe_features")
+    return off, loc[:off[-1]], glo[:off[-1]]
+
+
+def pack_records(n_frames, m_i, m_j, k1, k2, lm, kp_off, kp_xy, n_landmark):
+    """Pair-form records (frame int32 [2m], landmark int32 [2m], xy [2m, 2]) in _compute_residual order and
+    the x0 source record of each landmark (bundle_adjustment.py:67-99, 186-195)."""
+    m_i = np.ascontiguousarray(m_i, dtype=np.int32)
+    m_j = np.ascontiguousarray(m_j, dtype=np.int32)
+    k1 = np.ascontiguousarray(k1, dtype=np.int64)
+    k2 = np.ascontiguousarray(k2, dtype=np.int64)
+    lm = np.ascontiguousarray(lm, dtype=np.int64)
+    kp_off = np.ascontiguousarray(kp_off, dtype=np.int64)
+    kp_xy = np.ascontiguousarray(kp_xy, dtype=np.float64).reshape(-1, 2)
+    m = len(m_i)
+    fr = np.empty(2 * m, np.int32)
+    ll = np.empty(2 * m, np.int32)
+    xy = np.empty((2 * m, 2), np.float64)
+    src = np.empty(int(n_landmark), np.int64)
+    _check(lib().ptz_pack_records(int(n_frames), m, _ptr(m_i), _ptr(m_j), _ptr(k1), _ptr(k2), _ptr(lm), _ptr(kp_off),
+                                  _ptr(kp_xy), int(n_landmark), _ptr(fr), _ptr(ll), _ptr(xy), _ptr(src)),
+           "ptz_pack_records")
+    return fr, ll, xy, src
 
 
 # ---------------------------------------------------------------------------------------------

@@ -3,8 +3,12 @@ Map of keyframes and global ray landmarks (reference: slam_system/scene_map.py:1
 
 `Map.add_keyframe_with_ba` re-runs bundle adjustment over all keyframes, as the reference does
 (scene_map.py:53-117), on the GPU.  `RandomForestMap` keeps the reference's sliding-window BA
-(`bundle_adjustment_processing`, window `max_ba_frame`, scene_map.py:198-234); its random-forest
+(`bundle_adjustment_processing`, last `max_ba_frame` keyframes, scene_map.py:198-244); its random-forest
 relocaliser (C++ rf_map via ctypes) is out of scope and raises if used.
+
+Both keep a correspondence.CorrespondenceCache keyed by KeyFrame.img_index: the reference re-detects
+every keyframe and re-matches every pair on each BA call; here only the new keyframe is detected and
+only its pairs are matched, with identical results.
 """
 import time
 
@@ -12,18 +16,20 @@ import numpy as np
 import scipy.io as sio
 
 from bundle_adjustment import bundle_adjustment
+from correspondence import CorrespondenceCache
 from key_frame import KeyFrame
 from util import overlap_pan_angle
 
 
 class Map:
-    def __init__(self, feature_method):
+    def __init__(self, feature_method, cache_correspondences=True):
         assert feature_method in ("sift", "orb", "latch")
         self.global_ray = np.ndarray([0, 2])
         self.keyframe_list = []
         self.feature_method = feature_method
         self.ba_options = {}
         self.last_ba_time = None
+        self.correspondences = CorrespondenceCache() if cache_correspondences else None
 
     def add_first_keyframe(self, keyframe, verbose=False):
         assert isinstance(keyframe, KeyFrame)
@@ -47,7 +53,8 @@ class Map:
         initial_ptzs = np.array([[k.pan, k.tilt, k.f] for k in self.keyframe_list], dtype=np.float64).reshape(n, 3)
         start = time.time()
         landmarks, keyframes = bundle_adjustment(images, image_indices, self.feature_method, initial_ptzs, ref.center,
-                                                 ref.base_rotation, ref.u, ref.v, save_path, verbose, **self.ba_options)
+                                                 ref.base_rotation, ref.u, ref.v, save_path, verbose,
+                                                 correspondences=self.correspondences, **self.ba_options)
         end = time.time()
         self.keyframe_list.pop()
         self.global_ray = landmarks
@@ -84,36 +91,44 @@ class Map:
 
 
 class RandomForestMap:
-    """Sliding-window BA of scene_map.py:171-234 (last `max_ba_frame` keyframes, first kept as the gauge).
-    The random-forest relocaliser itself is not part of this build."""
+    """Sliding-window BA of scene_map.py:171-244: the last `max_ba_frame` keyframes are adjusted (the first
+    of them is the gauge, bundle_adjustment fixes frame 0), older keyframes are kept as they are.  The
+    random-forest map files / relocaliser (rf_map, C++) are not part of this build."""
 
-    def __init__(self, max_ba_frame=10, feature_method="sift"):
+    def __init__(self, max_ba_frame=10, feature_method="sift", cache_correspondences=True):
         self.keyframe_list = []
         self.feature_method = feature_method
         self.max_ba_frame = max_ba_frame
         self.global_ray = np.ndarray([0, 2])
+        self.ba_options = {}
+        self.correspondences = CorrespondenceCache() if cache_correspondences else None
 
     def add_keyframe(self, keyframe):
         self.keyframe_list.append(keyframe)
         if len(self.keyframe_list) > 1:
             self.bundle_adjustment_processing()
 
-    def bundle_adjustment_processing(self, save_path="", verbose=False):
+    def bundle_adjustment_processing(self, save_path="./bundle_result", verbose=False):
         ref = self.keyframe_list[0]
         n = len(self.keyframe_list)
-        if n > self.max_ba_frame:
-            window = [ref] + self.keyframe_list[n - self.max_ba_frame + 1:]
-        else:
-            window = list(self.keyframe_list)
+        window = [k for i, k in enumerate(self.keyframe_list) if i >= n - self.max_ba_frame]
+        kept = [k for i, k in enumerate(self.keyframe_list) if i < n - self.max_ba_frame]
         images = [k.img for k in window]
         idx = [k.img_index for k in window]
         ptzs = np.array([[k.pan, k.tilt, k.f] for k in window], dtype=np.float64)
+        if self.correspondences is not None:
+            self.correspondences.retain(idx)
         landmarks, kfs = bundle_adjustment(images, idx, self.feature_method, ptzs, ref.center, ref.base_rotation, ref.u,
-                                           ref.v, save_path, verbose)
-        self.global_ray = landmarks
-        for old, new in zip(window, kfs):
-            old.pan, old.tilt, old.f = new.pan, new.tilt, new.f
-            old.feature_pts, old.feature_des, old.landmark_index = new.feature_pts, new.feature_des, new.landmark_index
+                                           ref.v, save_path, verbose, correspondences=self.correspondences,
+                                           **self.ba_options)
+        self.global_ray = landmarks  # window-local ray ids (the reference discards them)
+        self.keyframe_list = kept
+        for i, kf in enumerate(kfs):
+            if kf.get_feature_num() > 0:
+                kf.convert_keypoint_to_array()
+                self.keyframe_list.append(kf)
+            else:
+                print("warning: key frame, %d, image index %d is not included in the map" % (i, idx[i]))
         return landmarks, kfs
 
     def relocalize(self, keyframe, ptz):

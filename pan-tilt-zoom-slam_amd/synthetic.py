@@ -276,7 +276,7 @@ class SyntheticFrontEnd:
     def __init__(self, scene, corrupt=0, seed=0):
         self.scene = scene
         self.corrupt = corrupt
-        self.rng = np.random.default_rng(seed)
+        self.seed = seed
 
     def detect(self, im, nfeatures=0, verbose=False):
         import image_process
@@ -291,18 +291,28 @@ class SyntheticFrontEnd:
         i = int(des1[0, 0])
         j = int(des2[0, 0])
         r1, r2 = self.scene.kp_ray[i], self.scene.kp_ray[j]
-        pos2 = np.full(len(self.scene.gt_rays), -1, np.int64)
-        pos2[r2] = np.arange(len(r2))
+        pos2 = self._pos(j)
         p = pos2[r1]
-        idx1 = [int(a) for a in np.flatnonzero(p >= 0)]
-        idx2 = [int(b) for b in p[p >= 0]]
+        idx1 = np.flatnonzero(p >= 0)
+        idx2 = p[idx1]
         if self.corrupt and len(idx2) > 4:
+            rng = np.random.default_rng([self.seed, i, j])  # deterministic per pair, like a real matcher
             for _ in range(self.corrupt):
-                a, b = self.rng.choice(len(idx2), 2, replace=False)
+                a, b = rng.choice(len(idx2), 2, replace=False)
                 idx2[a], idx2[b] = idx2[b], idx2[a]
-        pts1 = np.array([kp1[a].pt for a in idx1]).reshape(-1, 2)
-        pts2 = np.array([kp2[b].pt for b in idx2]).reshape(-1, 2)
+        pts1 = np.asarray(self.scene.kp_xy[i], np.float64).reshape(-1, 2)[idx1]
+        pts2 = np.asarray(self.scene.kp_xy[j], np.float64).reshape(-1, 2)[idx2]
         return pts1, idx1, pts2, idx2
+
+    def _pos(self, j):
+        """ray id -> keypoint position in frame j (-1: not seen), cached per frame."""
+        cache = self.__dict__.setdefault("_pos_cache", {})
+        if j not in cache:
+            r2 = self.scene.kp_ray[j]
+            pos = np.full(len(self.scene.gt_rays), -1, np.int64)
+            pos[r2] = np.arange(len(r2))
+            cache[j] = pos
+        return cache[j]
 
     def install(self):
         import image_process

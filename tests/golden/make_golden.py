@@ -436,13 +436,88 @@ def gen_reloc(seed):
         njev_ftol=r1.njev, x_tight=rt.x, cost_tight=rt.cost, scene_seed=seed, scene_rays=srays, scene_cams=cams,
         lost_init=lost_init, reloc_pose=np.asarray(reloc, np.float64))
 
+# --------------------------------------------------------------------------------------------
+# 8f-2. incremental maps: Map.add_keyframe_with_ba (scene_map.py:53-117) and the sliding window of
+# RandomForestMap.bundle_adjustment_processing (scene_map.py:198-244), whole sequences
+# --------------------------------------------------------------------------------------------
+def _map_state(step, kfs, rays, acc):
+    for kf in kfs:
+        pts = kf.feature_pts
+        xy = np.array([p.pt for p in pts]).reshape(-1, 2) if isinstance(pts, list) else np.asarray(pts).reshape(-1, 2)
+        acc["kf_step"].append(step)
+        acc["kf_img"].append(int(kf.img))
+        acc["kf_index"].append(int(kf.img_index))
+        acc["kf_ptz"].append([kf.pan, kf.tilt, kf.f])
+        acc["kf_nfeat"].append(len(xy))
+        acc["feat_xy"].append(xy)
+        acc["feat_lmk"].append(np.asarray(kf.landmark_index, np.int64).reshape(-1))
+    acc["ray_n"].append(len(rays))
+    acc["rays"].append(np.asarray(rays, np.float64).reshape(-1, 2))
+
+
+def _pack_state(acc):
+    return dict(kf_step=np.array(acc["kf_step"]), kf_img=np.array(acc["kf_img"]), kf_index=np.array(acc["kf_index"]),
+                kf_ptz=np.array(acc["kf_ptz"]), kf_nfeat=np.array(acc["kf_nfeat"]),
+                feat_xy=np.concatenate(acc["feat_xy"]), feat_lmk=np.concatenate(acc["feat_lmk"]),
+                ray_n=np.array(acc["ray_n"]), rays=np.concatenate(acc["rays"]))
+
+
+def gen_maps(seed):
+    import scene_map as ref_sm
+    import key_frame as ref_kf
+    center, rot = np.array([0.0, -10.0, 5.0]), np.eye(3)
+    ref_ba.draw_matches = lambda *a, **k: None
+    # (1) growing map, every keyframe added with BA
+    scene = synthetic.make_scene(6, 150, 54, 63, seed=seed)
+    fe = FrontEnd(scene)
+    calls = {"detect": 0, "match": 0}
+
+    def det(*a, **k):
+        calls["detect"] += 1
+        return fe.detect(*a, **k)
+
+    def mat(*a, **k):
+        calls["match"] += 1
+        return fe.match(*a, **k)
+    ref_ip.detect_compute_sift, ref_ip.match_sift_features = det, mat
+    random.seed(seed)
+    ip = scene.init_ptz
+    m = ref_sm.Map('sift')
+    m.add_first_keyframe(ref_kf.KeyFrame(0, 100, center, rot, scene.u, scene.v, *ip[0]))
+    acc = {k: [] for k in ("kf_step", "kf_img", "kf_index", "kf_ptz", "kf_nfeat", "feat_xy", "feat_lmk", "ray_n",
+                           "rays")}
+    t0 = time.time()
+    for k in range(1, 6):
+        m.add_keyframe_with_ba(ref_kf.KeyFrame(k, 100 + k, center, rot, scene.u, scene.v, *ip[k]), "/tmp")
+        _map_state(k, m.keyframe_list, m.global_ray, acc)
+    print(f"map: {time.time() - t0:.1f}s detect calls {calls['detect']} match calls {calls['match']}")
+    out("map_incremental.npz", seed=seed, u=scene.u, v=scene.v, init_ptz=ip, ref_detect_calls=calls["detect"],
+        ref_match_calls=calls["match"], **_pack_state(acc))
+    # (2) sliding window of 10 over 12 keyframes
+    scene = synthetic.make_scene(12, 160, 50, 66, seed=seed + 1)
+    fe = FrontEnd(scene)
+    ref_ip.detect_compute_sift, ref_ip.match_sift_features = fe.detect, fe.match
+    random.seed(seed + 1)
+    ip = scene.init_ptz
+    rf = ref_sm.RandomForestMap()
+    acc = {k: [] for k in acc}
+    t0 = time.time()
+    for k in range(12):
+        rf.keyframe_list.append(ref_kf.KeyFrame(k, 200 + k, center, rot, scene.u, scene.v, *ip[k]))
+        if len(rf.keyframe_list) > 1:
+            rf.bundle_adjustment_processing()
+        _map_state(k, rf.keyframe_list, np.zeros((0, 2)), acc)
+    print(f"window: {time.time() - t0:.1f}s")
+    out("map_window.npz", seed=seed + 1, u=scene.u, v=scene.v, init_ptz=ip, **_pack_state(acc))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--only", default="")
     a = ap.parse_args()
     rng = np.random.default_rng(1)
-    todo = a.only.split(",") if a.only else ["proj", "ba", "graph", "ekf", "config2", "reloc"]
+    todo = a.only.split(",") if a.only else ["proj", "ba", "graph", "ekf", "config2", "reloc", "maps"]
     if "proj" in todo:
         gen_projection(rng)
     if "ba" in todo:
@@ -457,6 +532,8 @@ def main():
         gen_ekf(300, seed=5)
     if "reloc" in todo:
         gen_reloc(3)
+    if "maps" in todo:
+        gen_maps(21)
     if "config2" in todo:
         gen_config2()
 

@@ -1,0 +1,157 @@
+"""Correspondence -> packed-observation builder (libptzba builder.cpp + correspondence.py),
+CPU only.  Bit-exact against the reference's fixtures (tests/golden/ba_*.npz, matching_graph.npz, made by
+running bundle_adjustment / build_matching_graph of the reference) and against the running interpreter
+for the two interpreter-defined orderings the reference depends on (random.shuffle, set iteration)."""
+import random
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+
+@pytest.mark.parametrize("name", ["ba_4x60", "ba_6x120", "ba_10x200"])
+def test_keyframe_features_set_order_bit_exact(name):
+    """bundle_adjustment.py:214-248: per-keyframe (local, landmark) lists in set() order."""
+    import ptzba
+    d = golden(name + ".npz")
+    off, loc, glo = ptzba.keyframe_features(int(d["n_pose"]), d["m_i"], d["m_j"], d["m_k1"], d["m_k2"], d["m_lm"])
+    np.testing.assert_array_equal(off, d["kf_off"])
+    np.testing.assert_array_equal(loc, d["kf_local"])
+    np.testing.assert_array_equal(glo, d["kf_lmk"])
+
+
+@pytest.mark.parametrize("name", ["ba_4x60", "ba_10x200"])
+def test_pack_records_and_x0_source(name):
+    """Records in _compute_residual order and the x0 ray of every landmark from the last match's src
+    observation (bundle_adjustment.py:186-195) == the reference's x0."""
+    import ptzba
+    from oracle import ptz_oracle as orc
+    d = golden(name + ".npz")
+    n, m = int(d["n_pose"]), int(d["n_landmark"])
+    fr, lm, xy, src = ptzba.pack_records(n, d["m_i"], d["m_j"], d["m_k1"], d["m_k2"], d["m_lm"], d["points_off"],
+                                         d["points"], m)
+    np.testing.assert_array_equal(fr[0::2], d["m_i"])
+    np.testing.assert_array_equal(fr[1::2], d["m_j"])
+    np.testing.assert_array_equal(lm[0::2], d["m_lm"])
+    pts, off = d["points"], d["points_off"]
+    np.testing.assert_array_equal(xy[0::2], pts[off[d["m_i"]] + d["m_k1"]])
+    np.testing.assert_array_equal(xy[1::2], pts[off[d["m_j"]] + d["m_k2"]])
+    assert np.all(src >= 0) and np.all(src % 2 == 0)
+    ip = d["init_ptz"]
+    f = fr[src]
+    th, ph = orc.from_image_to_ray(float(d["u"]), float(d["v"]), ip[f, 2], ip[f, 0], ip[f, 1], xy[src, 0], xy[src, 1])
+    x0_rays = d["x0"][3 * (n - 1):].reshape(-1, 2)
+    np.testing.assert_allclose(np.stack([th, ph], 1), x0_rays, rtol=0, atol=1e-10)
+
+
+def test_shuffle_replay_matches_interpreter():
+    """random.shuffle prefix + generator state afterwards, incl. lengths around powers of two."""
+    import ptzba
+    rng = np.random.default_rng(3)
+    lens = [2, 3, 4, 5, 201, 255, 256, 257, 1023, 1024, 1025, 4096] + rng.integers(2, 3000, 40).tolist()
+    for seed in (0, 1, 99):
+        random.seed(seed)
+        want = []
+        for n in lens:
+            lst = list(range(n))
+            random.shuffle(lst)
+            want += lst[:200]
+        nxt = random.getrandbits(32)
+        random.seed(seed)
+        got = ptzba.py_shuffle_prefix(lens, 200)
+        np.testing.assert_array_equal(got, want)
+        assert random.getrandbits(32) == nxt
+
+
+def test_set_order_matches_interpreter():
+    import ptzba
+    rng = np.random.default_rng(5)
+    for n, hi in ((0, 1), (1, 1), (7, 3), (5000, 200), (120000, 60000)):
+        a = rng.integers(0, hi, n)
+        b = rng.integers(0, 4 * hi, n)
+        oa, ob = ptzba.set_order_pairs(a, b)
+        assert list(zip(oa.tolist(), ob.tolist())) == list(set(zip(a.tolist(), b.tolist())))
+
+
+def _scene_frontend(n_kf=7, n_rays=700, seed=11):
+    import synthetic
+    sc = synthetic.make_scene(n_kf, n_rays, 50, 62, seed=seed)
+    fe = synthetic.SyntheticFrontEnd(sc, corrupt=3, seed=seed)
+    calls = {"detect": 0, "match": 0}
+
+    def det(im, nf=0, verbose=False):
+        calls["detect"] += 1
+        return fe.detect(im, nf, verbose)
+
+    def mat(*a, **k):
+        calls["match"] += 1
+        return fe.match(*a, **k)
+    return sc, det, mat, calls
+
+
+def _mask(ptz):
+    from util import overlap_pan_angle
+    n = len(ptz)
+    return [[1 if overlap_pan_angle(ptz[i][2], ptz[i][0], ptz[j][2], ptz[j][0], 1280) > 5 else 0 for j in range(n)]
+            for i in range(n)]
+
+
+def test_cached_graph_equals_full_rebuild():
+    """Incremental keyframe sets through a CorrespondenceCache == the reference's full rebuild on every
+    call (same ids, same capped matches, same global `random` stream), with each image detected once and
+    each pair matched once."""
+    import correspondence
+    import image_process
+    sc, det, mat, calls = _scene_frontend()
+    saved = image_process.detect_compute_sift, image_process.match_sift_features
+    image_process.detect_compute_sift, image_process.match_sift_features = det, mat
+    try:
+        cache = correspondence.CorrespondenceCache()
+        n_all = len(sc.init_ptz)
+        full_matches = 0
+        for n in range(2, n_all + 1):
+            ims = list(range(n))
+            mask = _mask(sc.init_ptz[:n])
+            random.seed(1000 + n)
+            g_full = correspondence.build_graph(ims, mask, "sift")
+            full_state = random.getstate()
+            full_matches += sum(mask[i][j] for i in range(n) for j in range(i + 1, n))
+            random.seed(1000 + n)
+            g = correspondence.build_graph(ims, mask, "sift", cache=cache, keys=[100 + k for k in ims])
+            assert random.getstate() == full_state
+            for f in ("pair_i", "pair_j", "pair_off", "k1", "k2", "lm", "kp_xy"):
+                np.testing.assert_array_equal(getattr(g, f), getattr(g_full, f))
+            assert g.n_landmark == g_full.n_landmark and g.n_inconsistent == g_full.n_inconsistent
+        assert cache.n_detect == n_all
+        assert cache.n_match == sum(_mask(sc.init_ptz)[i][j] for i in range(n_all) for j in range(i + 1, n_all))
+        assert calls["match"] == full_matches + cache.n_match
+        # sliding window: drop the oldest images, nothing new to detect or match
+        cache.retain([100 + k for k in range(3, n_all)])
+        before = cache.n_match
+        g = correspondence.build_graph(list(range(3, n_all)), _mask(sc.init_ptz[3:]), "sift", cache=cache,
+                                       keys=[100 + k for k in range(3, n_all)])
+        assert cache.n_match == before and g.n_matches > 0
+    finally:
+        image_process.detect_compute_sift, image_process.match_sift_features = saved
+
+
+def test_cache_redetects_changed_image():
+    import correspondence
+    import image_process
+    sc, det, mat, calls = _scene_frontend(4, 400)
+    saved = image_process.detect_compute_sift, image_process.match_sift_features
+    image_process.detect_compute_sift, image_process.match_sift_features = det, mat
+    try:
+        cache = correspondence.CorrespondenceCache()
+        mask = _mask(sc.init_ptz)
+        correspondence.build_graph([0, 1, 2, 3], mask, "sift", cache=cache, keys=[0, 1, 2, 3])
+        n0 = cache.n_detect
+        # key 3 now shows a different image (frame 2's): re-detected, its pairs re-matched
+        correspondence.build_graph([0, 1, 2, 2], mask, "sift", cache=cache, keys=[0, 1, 2, 3])
+        assert cache.n_detect == n0 + 1
+        # duplicate keys disable the cache for the call rather than mixing images up
+        g = correspondence.build_graph([0, 1], [r[:2] for r in mask[:2]], "sift", cache=cache, keys=[5, 5])
+        assert cache.n_detect == n0 + 1 and g.n_frames == 2
+    finally:
+        image_process.detect_compute_sift, image_process.match_sift_features = saved
