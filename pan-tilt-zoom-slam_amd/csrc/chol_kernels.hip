@@ -52,9 +52,22 @@ void launch_chol_prepare(double* A, int64_t ld, int n, double* b, const uint8_t*
   hipLaunchKernelGGL(k_chol_prepare, dim3((unsigned)((ld + 255) / 256)), dim3(256), 0, st, A, ld, n, b, pad, info);
 }
 
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void load_tile(double (*dst)[NB + 1], const double* __restrict__ src, int64_t ld) {
-  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) dst[e >> 5][e & 31] = src[(int64_t)(e >> 5) * ld + (e & 31)];
+// Batched tile staging: every thread fetches its 4 elements of each tile into registers first (all global
+// loads of a task in flight together: one memory round trip per task instead of one per update panel),
+// then writes them to LDS.  256 threads per workgroup.
+__device__ __forceinline__ void fetch_tile(double (&v)[4], const double* __restrict__ src, int64_t ld) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = threadIdx.x + 256 * q;
+    v[q] = src[(int64_t)(e >> 5) * ld + (e & 31)];
+  }
+}
+__device__ __forceinline__ void put_tile(double (*dst)[NB + 1], const double (&v)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = threadIdx.x + 256 * q;
+    dst[e >> 5][e & 31] = v[q];
+  }
 }
 
 // C -= A B^T for 32x32 tiles in LDS on the fp64 matrix cores: 256 threads = 4 waves, wave w owns the
@@ -92,43 +105,97 @@ __device__ __forceinline__ double rsq_nr(double d) {
 }
 
 // One wave factors the 32x32 SPD tile D and, in the same sweep, solves X = T L^-T for a 32x32 tile T.
-// Lanes 0..31 hold the rows of D, lanes 32..63 the rows of T, in registers.  Right-looking step j
-// broadcasts the (unscaled) pivot column A_mj with v_readlane; every lane applies
-//     v[m] -= (v[j] / A_jj) A_mj,  m > j,
-// which is the Cholesky update for a row of D and the forward substitution for a row of T.  At the end
-// L_ij = v_i[j] / sqrt(A_jj) (j <= i; L_ii = sqrt(A_jj)) and X_rj = x_r[j] / sqrt(A_jj).  Writes the
-// lower factor into D (zero above), X into T (when given), rdg[j] = 1/L_jj.
-__device__ __forceinline__ void wave_potrf_trsm32(double (*D)[NB + 1], double (*T)[NB + 1], double* rdg, int* info) {
+// Lanes 0..31 hold the rows of D, lanes 32..63 the rows of T, in registers.  Right-looking elimination
+// with the pivots in blocks of PB: step j applies  v[m] -= (v[j] / A_jj) A_mj  (m > j) to every lane's
+// row -- the Cholesky update for a row of D, the forward substitution for a row of T.
+//   * inside a block the pivot column moves by v_readlane (PB(PB-1)/2 elements per block);
+//   * after the block the D lanes publish their PB block values to LDS (cb) once, and the trailing
+//     rank-PB update reads them with uniform-address 16-byte loads (broadcast), MC rows per chunk with
+//     the next chunk's loads in flight.  A v_readlane broadcast costs ~8 cycles per 32-bit half on
+//     gfx950, an LDS-fed fp64 FMA ~6.7 cycles per element (tools/isa_probe.hip, tools/potrf_bench.hip).
+//   * every updated row value is pinned by an empty asm: otherwise the FMAs float past the chunk
+//     boundaries in the DAG and all LDS operands stay live (spills);
+//   * the 32 rsqrt run once at the end, vectorised (lane j keeps its pivot d_j).
+// At the end L_ij = v_i[j] / sqrt(A_jj) (j <= i; L_ii = sqrt(A_jj)) and X_rj = x_r[j] / sqrt(A_jj).
+// Writes the lower factor into D (zero above), X into T (when given), rdg[j] = 1/L_jj.
+constexpr int PB = 4, PMC = 4;
+__device__ __forceinline__ void wave_potrf_trsm32(double (*D)[NB + 1], double (*T)[NB + 1], double* rdg,
+                                                  double (*cb)[PB], int* info) {
   const int lane = lane_id();
   const bool isT = lane >= NB;
   const int r = lane & (NB - 1);
-  double row[NB], rs[NB];
+  double row[NB];
 #pragma unroll
   for (int m = 0; m < NB; ++m) row[m] = (isT && T) ? T[r][m] : D[r][m];
   bool bad = false;
+  double dm = 1.0;
 #pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    double d = bcast(row[j], j);
-    if (!(d > 0.0)) {
-      bad = true;
-      d = 1e-300;
+  for (int kb = 0; kb < NB; kb += PB) {
+    double w[PB];
+#pragma unroll
+    for (int j = kb; j < kb + PB; ++j) {
+      double d = bcast(row[j], j);
+      if (!(d > 0.0)) {
+        bad = true;
+        d = 1e-300;
+      }
+      dm = (lane == j) ? d : dm;
+      const double li = row[j] * rcp_nr(d);
+      w[j - kb] = li;
+#pragma unroll
+      for (int m = j + 1; m < kb + PB; ++m) row[m] -= li * bcast(row[j], m);
     }
-    rs[j] = rsq_nr(d);
-    const double li = row[j] * rcp_nr(d);
+    if (kb + PB < NB) {
+      if (!isT) {
 #pragma unroll
-    for (int m = j + 1; m < NB; ++m) row[m] -= li * bcast(row[j], m);
+        for (int k = 0; k < PB; ++k) cb[r][k] = row[kb + k];
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are visible
+      __builtin_amdgcn_wave_barrier();
+      const int m0 = kb + PB;
+      double nxt[PMC][PB];
+#pragma unroll
+      for (int q = 0; q < PMC; ++q)
+#pragma unroll
+        for (int k = 0; k < PB; ++k) nxt[q][k] = (m0 + q < NB) ? cb[m0 + q][k] : 0.0;
+#pragma unroll
+      for (int mc = m0; mc < NB; mc += PMC) {
+        double cur[PMC][PB];
+#pragma unroll
+        for (int q = 0; q < PMC; ++q)
+#pragma unroll
+          for (int k = 0; k < PB; ++k) cur[q][k] = nxt[q][k];
+        if (mc + PMC < NB) {
+#pragma unroll
+          for (int q = 0; q < PMC; ++q)
+#pragma unroll
+            for (int k = 0; k < PB; ++k) nxt[q][k] = (mc + PMC + q < NB) ? cb[mc + PMC + q][k] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < PMC; ++q) {
+          if (mc + q < NB) {
+            double sacc = row[mc + q];
+#pragma unroll
+            for (int k = 0; k < PB; ++k) sacc -= w[k] * cur[q][k];
+            row[mc + q] = sacc;
+            asm volatile("" : "+v"(row[mc + q]));
+          }
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // all reads of cb done before the next block rewrites it
+      __builtin_amdgcn_wave_barrier();
+    }
   }
   if (bad && lane == 0) atomicOr(info, 1);
+  if (lane < NB) rdg[lane] = rsq_nr(dm);
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
   if (!isT) {
 #pragma unroll
-    for (int j = 0; j < NB; ++j) D[r][j] = (j <= r) ? row[j] * rs[j] : 0.0;
-    if (lane == 0) {
-#pragma unroll
-      for (int j = 0; j < NB; ++j) rdg[j] = rs[j];
-    }
+    for (int j = 0; j < NB; ++j) D[r][j] = (j <= r) ? row[j] * rdg[j] : 0.0;
   } else if (T) {
 #pragma unroll
-    for (int j = 0; j < NB; ++j) T[r][j] = row[j] * rs[j];
+    for (int j = 0; j < NB; ++j) T[r][j] = row[j] * rdg[j];
   }
   wave_lds_fence();
 }
@@ -136,63 +203,87 @@ __device__ __forceinline__ void wave_potrf_trsm32(double (*D)[NB + 1], double (*
 __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64_t ld,
                                                    const int4* __restrict__ tasks, double* __restrict__ Ldiag,
                                                    int* info) {
-  __shared__ double sC[NB][NB + 1];  // target tile (panel T_ik / trailing A_ij)
-  __shared__ double sD[NB][NB + 1];  // diagonal tile -> L_kk
-  __shared__ double sA[NB][NB + 1];  // L_ip
-  __shared__ double sB[NB][NB + 1];  // L_kp or L_jp
+  __shared__ double sC[NB][NB + 1];     // target tile (panel T_ik / trailing A_ij)
+  __shared__ double sD[NB][NB + 1];     // diagonal tile -> L_kk
+  __shared__ double sA[2][NB][NB + 1];  // L_ip of the two update panels
+  __shared__ double sB[2][NB][NB + 1];  // L_kp or L_jp of the two update panels
   __shared__ double rdg[NB];
+  __shared__ __attribute__((aligned(16))) double cb[NB][PB];  // potrf block columns (broadcast reads)
   const int4 tk = tasks[blockIdx.x];
   const int type = tk.x, i = tk.y, j = tk.z;
-  int up[2];
-  up[0] = (tk.w & 0x3fff) - 1;
-  up[1] = ((tk.w >> 14) & 0x3fff) - 1;
+  const int up0 = (tk.w & 0x3fff) - 1;
+  const int up1 = ((tk.w >> 14) & 0x3fff) - 1;
   const int tmask = (tk.w >> 28) & 3;  // panel: which updates also apply to T
   const int64_t NBl = NB;
 #ifndef CHOL_VARIANT
 #define CHOL_VARIANT 0
 #endif
+#if CHOL_VARIANT == 5
+  return;
+#endif
+  double v0[4], v1[4], v2[4], v3[4], v4[4], v5[4];
   if (type == 1) {
 #if CHOL_VARIANT == 3
     return;
 #endif
     // trailing: A_ij -= sum_p L_ip L_jp^T
     double* C = A + i * NBl * ld + j * NBl;
-    load_tile(sC, C, ld);
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int pp = up[u];
-      if (pp < 0) continue;
-      load_tile(sA, A + i * NBl * ld + pp * NBl, ld);
-      load_tile(sB, A + j * NBl * ld + pp * NBl, ld);
-      __syncthreads();
-      tile_gemm_nt_sub(sC, sA, sB);
-      __syncthreads();
+    fetch_tile(v0, C, ld);
+    if (up0 >= 0) {
+      fetch_tile(v1, A + i * NBl * ld + up0 * NBl, ld);
+      fetch_tile(v2, A + j * NBl * ld + up0 * NBl, ld);
     }
+    if (up1 >= 0) {
+      fetch_tile(v3, A + i * NBl * ld + up1 * NBl, ld);
+      fetch_tile(v4, A + j * NBl * ld + up1 * NBl, ld);
+    }
+    put_tile(sC, v0);
+    if (up0 >= 0) {
+      put_tile(sA[0], v1);
+      put_tile(sB[0], v2);
+    }
+    if (up1 >= 0) {
+      put_tile(sA[1], v3);
+      put_tile(sB[1], v4);
+    }
+    __syncthreads();
+    // each wave owns one 16x16 block of C: consecutive updates need no barrier in between
+    if (up0 >= 0) tile_gemm_nt_sub(sC, sA[0], sB[0]);
+    if (up1 >= 0) tile_gemm_nt_sub(sC, sA[1], sB[1]);
+    __syncthreads();
     for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) C[(int64_t)(e >> 5) * ld + (e & 31)] = sC[e >> 5][e & 31];
     return;
   }
   // panel task (i, k = j)
   const int k = j;
   const bool diag_only = (i == k);
-  load_tile(sD, A + (int64_t)k * NBl * ld + k * NBl, ld);
-  if (!diag_only) load_tile(sC, A + i * NBl * ld + k * NBl, ld);
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int pp = up[u];
-    if (pp < 0) continue;
-    const bool updT = !diag_only && ((tmask >> u) & 1);
-    load_tile(sB, A + (int64_t)k * NBl * ld + pp * NBl, ld);
-    if (updT) load_tile(sA, A + i * NBl * ld + pp * NBl, ld);
-    __syncthreads();
+  const bool updT0 = !diag_only && (tmask & 1), updT1 = !diag_only && (tmask & 2);
+  fetch_tile(v0, A + (int64_t)k * NBl * ld + k * NBl, ld);
+  if (!diag_only) fetch_tile(v1, A + i * NBl * ld + k * NBl, ld);
+  if (up0 >= 0) fetch_tile(v2, A + (int64_t)k * NBl * ld + up0 * NBl, ld);
+  if (updT0 && up0 >= 0) fetch_tile(v3, A + i * NBl * ld + up0 * NBl, ld);
+  if (up1 >= 0) fetch_tile(v4, A + (int64_t)k * NBl * ld + up1 * NBl, ld);
+  if (updT1 && up1 >= 0) fetch_tile(v5, A + i * NBl * ld + up1 * NBl, ld);
+  put_tile(sD, v0);
+  if (!diag_only) put_tile(sC, v1);
+  if (up0 >= 0) put_tile(sB[0], v2);
+  if (updT0 && up0 >= 0) put_tile(sA[0], v3);
+  if (up1 >= 0) put_tile(sB[1], v4);
+  if (updT1 && up1 >= 0) put_tile(sA[1], v5);
+  __syncthreads();
 #if CHOL_VARIANT != 4
-    tile_gemm_nt_sub(sD, sB, sB);
-    if (updT) tile_gemm_nt_sub(sC, sA, sB);
-#endif
-    __syncthreads();
+  if (up0 >= 0) {
+    tile_gemm_nt_sub(sD, sB[0], sB[0]);
+    if (updT0) tile_gemm_nt_sub(sC, sA[0], sB[0]);
   }
+  if (up1 >= 0) {
+    tile_gemm_nt_sub(sD, sB[1], sB[1]);
+    if (updT1) tile_gemm_nt_sub(sC, sA[1], sB[1]);
+  }
+#endif
   __syncthreads();
 #if CHOL_VARIANT != 1
-  if (threadIdx.x < WAVE) wave_potrf_trsm32(sD, diag_only ? nullptr : sC, rdg, info);
+  if (threadIdx.x < WAVE) wave_potrf_trsm32(sD, diag_only ? nullptr : sC, rdg, cb, info);
 #endif
   __syncthreads();
   if (diag_only) {

@@ -233,6 +233,287 @@ __device__ void potrf_trsm_v11(double (*D)[NB + 1], double (*C)[NB + 1], double*
   }
 }
 
+// ---- V12<B>: fused potrf + TRSM, pivots in blocks of B.  Inside a block the pivot column moves by readlane
+// (B(B-1)/2 elements); after the block the D lanes publish their B block values to LDS once, and the
+// trailing rank-B update of every row reads them with uniform-address (broadcast) 16-byte loads.
+template <int B>
+__device__ void potrf_trsm_v12(double (*D)[NB + 1], double (*C)[NB + 1], double* rdg, double (*cb)[B]) {
+  const int lane = threadIdx.x & 63;
+  const bool isT = lane >= NB;
+  double row[NB];
+#pragma unroll
+  for (int m = 0; m < NB; ++m) row[m] = isT ? C[lane - NB][m] : D[lane][m];
+#pragma unroll
+  for (int kb = 0; kb < NB; kb += B) {
+    double w[B];
+#pragma unroll
+    for (int j = kb; j < kb + B; ++j) {
+      const double d = bcast(row[j], j);
+      if (lane == 0) rdg[j] = rsq_nr(d);
+      const double li = row[j] * rcp_nr(d);
+      w[j - kb] = li;
+#pragma unroll
+      for (int m = j + 1; m < kb + B; ++m) row[m] -= li * bcast(row[j], m);
+    }
+    if (kb + B < NB) {
+      if (!isT) {
+#pragma unroll
+        for (int k = 0; k < B; ++k) cb[lane][k] = row[kb + k];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int m = kb + B; m < NB; ++m) {
+        double s = row[m];
+#pragma unroll
+        for (int k = 0; k < B; ++k) s -= w[k] * cb[m][k];
+        row[m] = s;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+  for (int m = 0; m < NB; ++m) row[m] *= rdg[m];
+  if (isT) {
+#pragma unroll
+    for (int m = 0; m < NB; ++m) C[lane - NB][m] = row[m];
+  } else {
+#pragma unroll
+    for (int m = 0; m < NB; ++m) D[lane][m] = row[m];
+  }
+}
+
+// ---- V15<B, MC>: V12 with the trailing update software-pipelined in chunks of MC rows (the reads of chunk
+// c+1 issue before the FMAs of chunk c) and a scheduling barrier per chunk (no hoisting, no spills).
+template <int B, int MC>
+__device__ void potrf_trsm_v15(double (*D)[NB + 1], double (*C)[NB + 1], double* rdg, double (*cb)[B]) {
+  const int lane = threadIdx.x & 63;
+  const bool isT = lane >= NB;
+  double row[NB];
+#pragma unroll
+  for (int m = 0; m < NB; ++m) row[m] = isT ? C[lane - NB][m] : D[lane][m];
+#pragma unroll
+  for (int kb = 0; kb < NB; kb += B) {
+    double w[B];
+#pragma unroll
+    for (int j = kb; j < kb + B; ++j) {
+      const double d = bcast(row[j], j);
+      if (lane == 0) rdg[j] = rsq_nr(d);
+      const double li = row[j] * rcp_nr(d);
+      w[j - kb] = li;
+#pragma unroll
+      for (int m = j + 1; m < kb + B; ++m) row[m] -= li * bcast(row[j], m);
+    }
+    if (kb + B < NB) {
+      if (!isT) {
+#pragma unroll
+        for (int k = 0; k < B; ++k) cb[lane][k] = row[kb + k];
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      constexpr int M0 = 0;
+      const int m0 = kb + B;
+      double nxt[MC][B];
+#pragma unroll
+      for (int q = 0; q < MC; ++q)
+#pragma unroll
+        for (int k = 0; k < B; ++k) nxt[q][k] = (m0 + q < NB) ? cb[m0 + q][k] : 0.0;
+#pragma unroll
+      for (int mc = m0; mc < NB; mc += MC) {
+        double cur[MC][B];
+#pragma unroll
+        for (int q = 0; q < MC; ++q)
+#pragma unroll
+          for (int k = 0; k < B; ++k) cur[q][k] = nxt[q][k];
+        if (mc + MC < NB) {
+#pragma unroll
+          for (int q = 0; q < MC; ++q)
+#pragma unroll
+            for (int k = 0; k < B; ++k) nxt[q][k] = (mc + MC + q < NB) ? cb[mc + MC + q][k] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < MC; ++q) {
+          if (mc + q < NB) {
+            double s = row[mc + q];
+#pragma unroll
+            for (int k = 0; k < B; ++k) s -= w[k] * cur[q][k];
+            row[mc + q] = s;
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      (void)M0;
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+  for (int m = 0; m < NB; ++m) row[m] *= rdg[m];
+  if (isT) {
+#pragma unroll
+    for (int m = 0; m < NB; ++m) C[lane - NB][m] = row[m];
+  } else {
+#pragma unroll
+    for (int m = 0; m < NB; ++m) D[lane][m] = row[m];
+  }
+}
+
+// ---- V19<B, MC>: V15 with every updated row value pinned by an empty asm (the FMAs otherwise float past
+// the scheduling barriers in the DAG and keep every LDS operand live: spills).
+template <int B, int MC>
+__device__ void potrf_trsm_v19(double (*D)[NB + 1], double (*C)[NB + 1], double* rdg, double (*cb)[B]) {
+  const int lane = threadIdx.x & 63;
+  const bool isT = lane >= NB;
+  double row[NB];
+#pragma unroll
+  for (int m = 0; m < NB; ++m) row[m] = isT ? C[lane - NB][m] : D[lane][m];
+#pragma unroll
+  for (int kb = 0; kb < NB; kb += B) {
+    double w[B];
+#pragma unroll
+    for (int j = kb; j < kb + B; ++j) {
+      const double d = bcast(row[j], j);
+      if (lane == 0) rdg[j] = rsq_nr(d);
+      const double li = row[j] * rcp_nr(d);
+      w[j - kb] = li;
+#pragma unroll
+      for (int m = j + 1; m < kb + B; ++m) row[m] -= li * bcast(row[j], m);
+    }
+    if (kb + B < NB) {
+      if (!isT) {
+#pragma unroll
+        for (int k = 0; k < B; ++k) cb[lane][k] = row[kb + k];
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      const int m0 = kb + B;
+      double nxt[MC][B];
+#pragma unroll
+      for (int q = 0; q < MC; ++q)
+#pragma unroll
+        for (int k = 0; k < B; ++k) nxt[q][k] = (m0 + q < NB) ? cb[m0 + q][k] : 0.0;
+#pragma unroll
+      for (int mc = m0; mc < NB; mc += MC) {
+        double cur[MC][B];
+#pragma unroll
+        for (int q = 0; q < MC; ++q)
+#pragma unroll
+          for (int k = 0; k < B; ++k) cur[q][k] = nxt[q][k];
+        if (mc + MC < NB) {
+#pragma unroll
+          for (int q = 0; q < MC; ++q)
+#pragma unroll
+            for (int k = 0; k < B; ++k) nxt[q][k] = (mc + MC + q < NB) ? cb[mc + MC + q][k] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < MC; ++q) {
+          if (mc + q < NB) {
+            double s = row[mc + q];
+#pragma unroll
+            for (int k = 0; k < B; ++k) s -= w[k] * cur[q][k];
+            row[mc + q] = s;
+            asm volatile("" : "+v"(row[mc + q]));
+          }
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+  for (int m = 0; m < NB; ++m) row[m] *= rdg[m];
+  if (isT) {
+#pragma unroll
+    for (int m = 0; m < NB; ++m) C[lane - NB][m] = row[m];
+  } else {
+#pragma unroll
+    for (int m = 0; m < NB; ++m) D[lane][m] = row[m];
+  }
+}
+
+template <int B, int MC>
+__device__ void potrf_trsm_v24(double (*D)[NB + 1], double (*C)[NB + 1], double* rdg, double (*cb)[B]) {
+  const int lane = threadIdx.x & 63;
+  const bool isT = lane >= NB;
+  double row[NB];
+#pragma unroll
+  for (int m = 0; m < NB; ++m) row[m] = isT ? C[lane - NB][m] : D[lane][m];
+  double dm = 1.0;  // lane j keeps pivot d_j; the 32 rsq run once, vectorised, at the end
+#pragma unroll
+  for (int kb = 0; kb < NB; kb += B) {
+    double w[B];
+#pragma unroll
+    for (int j = kb; j < kb + B; ++j) {
+      const double d = bcast(row[j], j);
+      dm = (lane == j) ? d : dm;
+      const double li = row[j] * rcp_nr(d);
+      w[j - kb] = li;
+#pragma unroll
+      for (int m = j + 1; m < kb + B; ++m) row[m] -= li * bcast(row[j], m);
+    }
+    if (kb + B < NB) {
+      if (!isT) {
+#pragma unroll
+        for (int k = 0; k < B; ++k) cb[lane][k] = row[kb + k];
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      const int m0 = kb + B;
+      double nxt[MC][B];
+#pragma unroll
+      for (int q = 0; q < MC; ++q)
+#pragma unroll
+        for (int k = 0; k < B; ++k) nxt[q][k] = (m0 + q < NB) ? cb[m0 + q][k] : 0.0;
+#pragma unroll
+      for (int mc = m0; mc < NB; mc += MC) {
+        double cur[MC][B];
+#pragma unroll
+        for (int q = 0; q < MC; ++q)
+#pragma unroll
+          for (int k = 0; k < B; ++k) cur[q][k] = nxt[q][k];
+        if (mc + MC < NB) {
+#pragma unroll
+          for (int q = 0; q < MC; ++q)
+#pragma unroll
+            for (int k = 0; k < B; ++k) nxt[q][k] = (mc + MC + q < NB) ? cb[mc + MC + q][k] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < MC; ++q) {
+          if (mc + q < NB) {
+            double s = row[mc + q];
+#pragma unroll
+            for (int k = 0; k < B; ++k) s -= w[k] * cur[q][k];
+            row[mc + q] = s;
+            asm volatile("" : "+v"(row[mc + q]));
+          }
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  if (lane < NB) rdg[lane] = rsq_nr(dm);
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int m = 0; m < NB; ++m) row[m] *= rdg[m];
+  if (isT) {
+#pragma unroll
+    for (int m = 0; m < NB; ++m) C[lane - NB][m] = row[m];
+  } else {
+#pragma unroll
+    for (int m = 0; m < NB; ++m) D[lane][m] = row[m];
+  }
+}
+
 // ---- TRSM variants: X = T L^-T with L = D (scaled on the fly: L_mj = D[m][j] * rdg[j] for m > j, L_jj = 1/rdg)
 // T0: lane per row, sched_barrier per step (library)
 __device__ void trsm_t0(double (*C)[NB + 1], double (*D)[NB + 1], const double* rdg) {
@@ -298,6 +579,8 @@ __global__ __launch_bounds__(256) void k_bench(const double* __restrict__ A, con
   __shared__ double rdg[NB];
   __shared__ double col[NB];
   __shared__ double colbuf[2][NB];
+  __shared__ __attribute__((aligned(16))) double cb4[NB][4];
+  __shared__ __attribute__((aligned(16))) double cb8[NB][8];
   const double* a = A + (size_t)blockIdx.x * NB * NB;
   const double* t = T + (size_t)blockIdx.x * NB * NB;
   for (int rep = 0; rep < REPS; ++rep) {
@@ -316,6 +599,21 @@ __global__ __launch_bounds__(256) void k_bench(const double* __restrict__ A, con
       if (PV == 9) potrf_trsm_v8<false>(sD, sC, rdg);
       if (PV == 10) potrf_trsm_v10(sD, sC, rdg, colbuf);
       if (PV == 11) potrf_trsm_v11(sD, sC, rdg);
+      if (PV == 12) potrf_trsm_v12<4>(sD, sC, rdg, cb4);
+      if (PV == 13) potrf_trsm_v12<8>(sD, sC, rdg, cb8);
+      if (PV == 14) potrf_trsm_v12<2>(sD, sC, rdg, (double(*)[2])cb4);
+      if (PV == 15) potrf_trsm_v15<4, 4>(sD, sC, rdg, cb4);
+      if (PV == 16) potrf_trsm_v15<8, 2>(sD, sC, rdg, cb8);
+      if (PV == 17) potrf_trsm_v15<4, 2>(sD, sC, rdg, cb4);
+      if (PV == 18) potrf_trsm_v15<2, 4>(sD, sC, rdg, (double(*)[2])cb4);
+      if (PV == 19) potrf_trsm_v19<4, 4>(sD, sC, rdg, cb4);
+      if (PV == 20) potrf_trsm_v19<8, 2>(sD, sC, rdg, cb8);
+      if (PV == 21) potrf_trsm_v19<4, 2>(sD, sC, rdg, cb4);
+      if (PV == 22) potrf_trsm_v19<8, 4>(sD, sC, rdg, cb8);
+      if (PV == 23) potrf_trsm_v19<2, 4>(sD, sC, rdg, (double(*)[2])cb4);
+      if (PV == 24) potrf_trsm_v24<4, 4>(sD, sC, rdg, cb4);
+      if (PV == 25) potrf_trsm_v24<8, 2>(sD, sC, rdg, cb8);
+      if (PV == 26) potrf_trsm_v24<8, 4>(sD, sC, rdg, cb8);
     }
     __syncthreads();
     if (TV == 2) {
@@ -421,5 +719,20 @@ int main() {
   cmp("fused v9 ieee div", run<9, 9>(nb, dA, dT, dL, dX, L, X));
   cmp("fused v10 lds pipelined", run<10, 9>(nb, dA, dT, dL, dX, L, X));
   cmp("fused v11 readlane, rs in lds", run<11, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("fused v12 blocked B=4", run<12, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("fused v13 blocked B=8", run<13, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("fused v14 blocked B=2", run<14, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("fused v15 pipelined B=4 MC=4", run<15, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("fused v16 pipelined B=8 MC=2", run<16, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("fused v17 pipelined B=4 MC=2", run<17, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("fused v18 pipelined B=2 MC=4", run<18, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("fused v19 pinned B=4 MC=4", run<19, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("fused v20 pinned B=8 MC=2", run<20, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("fused v21 pinned B=4 MC=2", run<21, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("fused v22 pinned B=8 MC=4", run<22, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("fused v23 pinned B=2 MC=4", run<23, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("fused v24 pinned+rsq end B=4 MC=4", run<24, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("fused v25 pinned+rsq end B=8 MC=2", run<25, 9>(nb, dA, dT, dL, dX, L, X));
+  cmp("fused v26 pinned+rsq end B=8 MC=4", run<26, 9>(nb, dA, dT, dL, dX, L, X));
   return 0;
 }
