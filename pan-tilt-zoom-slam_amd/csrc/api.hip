@@ -49,10 +49,14 @@ struct ptzba_ctx {
   DBuf rec_xy, rec_seg, rec_w, perm;
   DBuf seg_frame, seg_lm, seg_rec_begin, lm_seg_begin, lm_order;
   DBuf frame_seg_begin, frame_seg_list, frame_win_hi;
+  DBuf s2_items, s2_groups, s2_lm, lm_meta, frame_seg_info;  // K2 work items / tiles / lists, slot ranges
+  DBuf s2_part, fdiag;                                        // K2 split partials, per-frame U | g | b
+  int n_s2_items = 0, n_s2_groups = 0;
+  int64_t n_slot = 0;  // dense landmark x frame slots (W table rows)
   // device: state
   DBuf ptz, rays, ptz_trial, rays_trial, D_pose, D_ray;
   DBuf ft, rt, ft64, rt64, seg_base;
-  DBuf seg_ug[2], seg_w[2], lm_out[2];
+  DBuf seg_ug[2], w_slot[2], lm_out[2];
   int cur = 0;
   DBuf lm_aux, lm_red, red_scratch;
   DBuf sys;  // [S ld*ld | b ld | g_pose ld | dU ld]
@@ -442,6 +446,74 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     }
     frame_win_hi[f] = hi;
   }
+  // ---- register-blocked K2 structure: per landmark its frame range [first, last] and a dense W slot
+  // per frame in it; K2 tiles (SCHUR_F1 frames x 64 partner frames) with the landmarks that reach them,
+  std::vector<int32_t> lm_meta(4 * (size_t)std::max(n_landmark, 1), 0), frame_seg_info(4 * (size_t)n_seg), s2_items, s2_groups,
+      s2_lm;
+  {
+    int64_t toff = 0;
+    for (int l = 0; l < n_landmark; ++l) {
+      const int s0 = lm_seg_begin[l], s1 = lm_seg_begin[l + 1];
+      if (s1 == s0) continue;
+      const int lo = seg_frame[s0], hi = seg_frame[s1 - 1];  // segments are frame-ordered per landmark
+      lm_meta[4 * l] = lo;
+      lm_meta[4 * l + 1] = hi;
+      lm_meta[4 * l + 2] = (int32_t)toff;
+      toff += hi - lo + 1;
+      if (toff >= INT32_MAX) return fail("landmark x frame slot table exceeds 2^31 rows");
+    }
+    h->n_slot = toff;
+    for (int64_t e = 0; e < n_seg; ++e) {
+      const int s = frame_seg_list[e], l = seg_lm[s];
+      frame_seg_info[4 * e] = s;
+      frame_seg_info[4 * e + 1] = l;
+      frame_seg_info[4 * e + 2] = lm_meta[4 * l + 2] + seg_frame[s] - lm_meta[4 * l];
+      frame_seg_info[4 * e + 3] = 0;
+    }
+    // split size: about two work items per CU over the whole list volume, at least 64 landmarks
+    std::vector<std::vector<int32_t>> tiles;
+    std::vector<int32_t> tile_key;
+    std::vector<int32_t> un;
+    int64_t total = 0;
+    for (int f1b = o.n_fixed; f1b < n_pose; f1b += SCHUR_F1) {
+      un.clear();
+      for (int f = f1b; f < std::min(n_pose, f1b + SCHUR_F1); ++f)
+        for (int e = frame_seg_begin[f]; e < frame_seg_begin[f + 1]; ++e) un.push_back(seg_lm[frame_seg_list[e]]);
+      std::sort(un.begin(), un.end());
+      un.erase(std::unique(un.begin(), un.end()), un.end());
+      int hi = f1b;
+      for (int l : un) hi = std::max(hi, lm_meta[4 * l + 1]);
+      const int nc = (hi - f1b) / WAVE + 1;
+      for (int c = 0; c < nc; ++c) {
+        std::vector<int32_t> lst;
+        for (int l : un)
+          if (c == 0 || lm_meta[4 * l + 1] >= f1b + WAVE * c) lst.push_back(l);
+        total += (int64_t)lst.size();
+        tiles.push_back(std::move(lst));
+        tile_key.push_back(f1b);
+        tile_key.push_back(c);
+      }
+    }
+    const int64_t split = std::min<int64_t>(SCHUR_LMAX, std::max<int64_t>(64, (total + 511) / 512));
+    for (size_t k = 0; k < tiles.size(); ++k) {
+      const auto& lst = tiles[k];
+      const int n = (int)lst.size();
+      const int nparts = (int)((n + split - 1) / split);
+      const int i0 = (int)(s2_items.size() / 4);
+      for (int pp = 0; pp < nparts; ++pp) {
+        const int a0 = (int)((int64_t)n * pp / nparts), a1 = (int)((int64_t)n * (pp + 1) / nparts);
+        const int b0 = (int)(s2_lm.size() / 4);
+        for (int q = a0; q < a1; ++q) {
+          const int l = lst[q];
+          s2_lm.insert(s2_lm.end(), {l, lm_meta[4 * l], lm_meta[4 * l + 1], lm_meta[4 * l + 2]});
+        }
+        s2_items.insert(s2_items.end(), {tile_key[2 * k], tile_key[2 * k + 1], b0, (int32_t)(s2_lm.size() / 4)});
+      }
+      s2_groups.insert(s2_groups.end(), {tile_key[2 * k], tile_key[2 * k + 1], i0, (int32_t)(s2_items.size() / 4)});
+    }
+    h->n_s2_groups = (int)(s2_groups.size() / 4);
+    h->n_s2_items = (int)(s2_items.size() / 4);
+  }
   // ---- landmark work order: heaviest (most records) first
   std::vector<int32_t> lm_order;
   int max_seg = 0;
@@ -503,7 +575,10 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   if (upload(h->rec_seg, rec_seg) || upload(h->seg_frame, seg_frame) || upload(h->seg_lm, seg_lm) ||
       upload(h->seg_rec_begin, seg_rec_begin) || upload(h->lm_seg_begin, lm_seg_begin) ||
       upload(h->lm_order, lm_work) || upload(h->frame_seg_begin, frame_seg_begin) ||
-      upload(h->frame_seg_list, frame_seg_list) || upload(h->frame_win_hi, frame_win_hi))
+      upload(h->frame_seg_list, frame_seg_list) || upload(h->frame_win_hi, frame_win_hi) ||
+      upload(h->s2_items, s2_items) || upload(h->s2_groups, s2_groups) || upload(h->s2_lm, s2_lm) ||
+      upload(h->lm_meta, lm_meta) ||
+      upload(h->frame_seg_info, frame_seg_info))
     return -1;
   const size_t e = h->elem();
   if (h->ptz.alloc(3 * n_pose * 8) || h->ptz_trial.alloc(3 * n_pose * 8) || h->rays.alloc(2 * (size_t)n_landmark * 8) ||
@@ -511,12 +586,14 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       h->D_ray.alloc(2 * (size_t)n_landmark * 8) || h->ft.alloc((size_t)n_pose * 8 * e) ||
       h->rt.alloc((size_t)n_landmark * 8 * e) || h->ft64.alloc((size_t)n_pose * 64) ||
       h->rt64.alloc((size_t)n_landmark * 64) || h->seg_ug[0].alloc((size_t)n_seg * 12 * e) ||
-      h->seg_ug[1].alloc((size_t)n_seg * 12 * e) || h->seg_w[0].alloc((size_t)n_seg * 8 * e) ||
-      h->seg_w[1].alloc((size_t)n_seg * 8 * e) || h->lm_out[0].alloc((size_t)n_landmark * 8 * 8) ||
+      h->seg_ug[1].alloc((size_t)n_seg * 12 * e) || h->w_slot[0].alloc((size_t)std::max<int64_t>(h->n_slot, 1) * 8 * e) ||
+      h->w_slot[1].alloc((size_t)std::max<int64_t>(h->n_slot, 1) * 8 * e) || h->lm_out[0].alloc((size_t)n_landmark * 8 * 8) ||
       h->lm_out[1].alloc((size_t)n_landmark * 8 * 8) || h->lm_aux.alloc((size_t)n_landmark * 8 * 8) ||
       h->lm_red.alloc((size_t)n_landmark * 4 * 8) || h->sys.alloc((size_t)h->sys_count() * 8) ||
       h->scal.alloc(PTZBA_NSCALARS * 8) || h->red_scratch.alloc(RED_SCRATCH * 8) || h->loc.alloc(PTZBA_NSCALARS * 8) || h->info.alloc(16) ||
-      h->Ldiag.alloc((size_t)h->ld * CHOL_NB * 8) || h->dpose.alloc((size_t)h->ld * 8))
+      h->Ldiag.alloc((size_t)h->ld * CHOL_NB * 8) || h->dpose.alloc((size_t)h->ld * 8) ||
+      h->s2_part.alloc((size_t)std::max(h->n_s2_items, 1) * SCHUR_F1 * 9 * WAVE * 8) ||
+      h->fdiag.alloc((size_t)n_pose * 12 * 8))
     return -1;
   if (upload(h->chol_tasks, plan.tasks) || upload(h->frame_pos, sorder.pos) || upload(h->row_pad, sorder.pad) ||
       upload(h->bs_chain_off, plan.chain_off) || upload(h->bs_chain_cols, plan.chain_cols) ||
@@ -526,6 +603,8 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->xbuf.release();  // allocated on first ptzba_exchange_packed
   HIPCHK(hipMemset(h->D_pose.p, 0, h->D_pose.bytes));
   HIPCHK(hipMemset(h->D_ray.p, 0, h->D_ray.bytes));
+  HIPCHK(hipMemset(h->w_slot[0].p, 0, h->w_slot[0].bytes));  // slots of unobserved frames stay zero
+  HIPCHK(hipMemset(h->w_slot[1].p, 0, h->w_slot[1].bytes));
   HIPCHK(hipMemset(h->ptz.p, 0, h->ptz.bytes));
   HIPCHK(hipMemset(h->rays.p, 0, h->rays.bytes));
   HIPCHK(hipMemset(h->scal.p, 0, h->scal.bytes));
@@ -553,7 +632,7 @@ int ptzba_problem_info(ptzba_handle h, int64_t* info) {
                                     &h->seg_rec_begin, &h->lm_seg_begin, &h->lm_order, &h->frame_seg_begin,
                                     &h->frame_seg_list, &h->frame_win_hi, &h->ptz, &h->rays, &h->ptz_trial,
                                     &h->rays_trial, &h->D_pose, &h->D_ray, &h->ft, &h->rt, &h->seg_ug[0],
-                                    &h->seg_ug[1], &h->lm_out[0], &h->lm_out[1], &h->lm_aux, &h->lm_red, &h->sys,
+                                    &h->seg_ug[1], &h->w_slot[0], &h->w_slot[1], &h->lm_out[0], &h->lm_out[1], &h->lm_aux, &h->lm_red, &h->sys,
                                     &h->scal, &h->loc});
   return 0;
 }
@@ -589,7 +668,8 @@ static void linearize_into(ptzba_ctx* h, int slot) {
   a.fs2 = h->fs * h->fs;
   a.inv_fs2 = 1.0 / (h->fs * h->fs);
   a.seg_ug = h->seg_ug[slot].p;
-  a.seg_w = h->seg_w[slot].p;
+  a.w_slot = h->w_slot[slot].p;
+  a.lm_meta = h->lm_meta.as<int4>();
   a.lm_out = h->lm_out[slot].as<double>();
   // landmarks without records keep zero rows
   (void)hipMemsetAsync(h->lm_out[slot].p, 0, h->lm_out[slot].bytes, h->st);
@@ -678,14 +758,16 @@ int ptzba_build_reduced(ptzba_handle h, double lambda) {
                        h->lm_aux.as<double>(), h->n_lm, lambda, h->st);
   HIPCHK(hipMemsetAsync(h->sys.p, 0, h->sys.bytes, h->st));
   SchurArgs a;
+  a.items = h->s2_items.as<int4>();
+  a.groups = h->s2_groups.as<int4>();
+  a.part = h->s2_part.as<double>();
+  a.fdiag = h->fdiag.as<double>();
+  a.item_lm = h->s2_lm.as<int4>();
   a.frame_seg_begin = h->frame_seg_begin.as<int32_t>();
-  a.frame_seg_list = h->frame_seg_list.as<int32_t>();
+  a.frame_seg_info = h->frame_seg_info.as<int4>();
   a.frame_win_hi = h->frame_win_hi.as<int32_t>();
-  a.seg_lm = h->seg_lm.as<int32_t>();
-  a.seg_frame = h->seg_frame.as<int32_t>();
-  a.lm_seg_begin = h->lm_seg_begin.as<int32_t>();
   a.seg_ug = h->seg_ug[c].p;
-  a.seg_w = h->seg_w[c].p;
+  a.w_slot = h->w_slot[c].p;
   a.lm_aux = h->lm_aux.as<double>();
   a.frame_pos = h->frame_pos.as<int32_t>();
   a.S = h->S();
@@ -693,12 +775,12 @@ int ptzba_build_reduced(ptzba_handle h, double lambda) {
   a.g_pose = h->gpose();
   a.dU = h->dU();
   a.ld = h->ld;
-  a.n_fixed = h->n_fixed;
+  a.n_pose = h->n_pose;
   tm_begin(h, TM_SCHUR);
   if (h->precision == PTZBA_FP32)
-    launch_schur<float>(a, h->n_pose - h->n_fixed, h->st);
+    launch_schur<float>(a, h->n_s2_items, h->n_s2_groups, h->n_fixed, h->st);
   else
-    launch_schur<double>(a, h->n_pose - h->n_fixed, h->st);
+    launch_schur<double>(a, h->n_s2_items, h->n_s2_groups, h->n_fixed, h->st);
   tm_end(h, TM_SCHUR);
   HIPCHK(hipGetLastError());
   return 0;
@@ -728,7 +810,8 @@ int ptzba_solve_reduced(ptzba_handle h) {
   BacksubArgs b;
   b.lm_seg_begin = h->lm_seg_begin.as<int32_t>();
   b.seg_frame = h->seg_frame.as<int32_t>();
-  b.seg_w = h->seg_w[c].p;
+  b.w_slot = h->w_slot[c].p;
+  b.lm_meta = h->lm_meta.as<int4>();
   b.lm_out = h->lm_out[c].as<double>();
   b.lm_aux = h->lm_aux.as<double>();
   b.D_ray = h->D_ray.as<double>();

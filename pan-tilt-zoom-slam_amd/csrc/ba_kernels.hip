@@ -11,7 +11,8 @@
 //   segments  one per unique (landmark, frame): seg_frame, seg_rec_begin (CSR into records);
 //             landmark CSR lm_seg_begin; frame CSR frame_seg_begin/frame_seg_list
 //   tables    FrameTab[n_pose] (cos/sin pan, cos/sin tilt, f), RayTab[n_lm] (ray direction + derivs)
-//   lin       seg_w[n_seg][8]   = W(3x2) | frame id | 0           (real, Schur inner loop + back-subst.)
+//   lin       w_slot[n_slot][8] = W(3x2) | 0 0  (real) in the dense landmark x frame slot table:
+//                                 slot = toff_l + frame - first_l; slots of unobserved frames stay 0
 //             seg_ug[n_seg][12] = U(3x3 sym, 6) | g_pose(3) | pad   (real, reduced per frame by Schur)
 //             lm_out[n_lm][8]    = V(2x2 sym, 3) | g_ray(2) | cost | pad      (fp64)
 //
@@ -129,7 +130,9 @@ __global__ __launch_bounds__(256, K1_MIN_WAVES) void k_linearize(LinArgs a) {
   const real* __restrict__ rec_xy = (const real*)a.rec_xy;
   const real* __restrict__ rec_w = (const real*)a.rec_w;
   real* __restrict__ seg_ug = (real*)a.seg_ug;
-  real* __restrict__ seg_w = (real*)a.seg_w;
+  real* __restrict__ w_slot = (real*)a.w_slot;
+  const int4 lmeta = a.lm_meta[l];  // {first frame, last frame, slot offset, 0}
+  const int64_t slot0 = (int64_t)lmeta.z - lmeta.x;
   const real u = (real)a.u, v = (real)a.v;
   const real fs2 = (real)a.fs2, ifs2 = (real)a.inv_fs2;
   real* sx = s_x[wv];
@@ -256,10 +259,11 @@ __global__ __launch_bounds__(256, K1_MIN_WAVES) void k_linearize(LinArgs a) {
         W[2 * p + 0] = Sx * J[0][p] * J[0][3] + Sy * J[1][p] * J[1][3];
         W[2 * p + 1] = Sx * J[0][p] * J[0][4] + Sy * J[1][p] * J[1][4];
       }
-      // seg_w[8] = {W (6), frame id, 0}: the Schur kernel's inner-loop record and the back-substitution's W
-      real* cw = seg_w + (int64_t)s * 8;
+      // W into the landmark's dense frame slot: the Schur kernel's inner-loop operand and the
+      // back-substitution's W
+      real* cw = w_slot + (slot0 + fs) * 8;
       store4(cw, W[0], W[1], W[2], W[3]);
-      store4(cw + 4, W[4], W[5], __int_as_real<real>(fs), (real)0);
+      store4(cw + 4, W[4], W[5], (real)0, (real)0);
       // seg_ug[12] = {U (6), g_pose (3), 0, 0, 0}: reduced per frame by the Schur kernel
       real* o = seg_ug + (int64_t)s * 12;
       store4(o, Sx * J[0][0] * J[0][0] + Sy * J[1][0] * J[1][0], Sx * J[0][0] * J[0][1] + Sy * J[1][0] * J[1][1],
@@ -332,229 +336,6 @@ void launch_landmark_damp(const double* lm_out, const int32_t* lm_seg_begin, dou
                      lm_aux, n_lm, lambda);
 }
 
-// ------------------------------------------------------------------------------------------------
-// K2: reduced camera system  S = U - sum_l W_l V~_l^-1 W_l^T   (damping added after the exchange),
-//                            b = -g_pose + sum_l W_l V~_l^-1 g_l
-// One 1024-thread workgroup per free frame f1 builds block column f1 of the lower triangle
-// (frames f2 >= f1) in an LDS window of 3x3 blocks.  Each of the 16 waves takes a contiguous slice
-// of f1's segment list; per chunk of 64 segments the lanes fetch the segments' metadata in parallel
-// (segment -> landmark -> W, V~^-1: no per-segment dependent-load chain), then for each segment
-// (broadcast with readlane) the lanes walk landmark l's segments f2 >= f1 (distinct frames, so a
-// wave's lanes never collide) and add -Y W_f2^T (Y = W_f1 V~^-1) with LDS fp64 atomics
-// (ds_add_f64: waves may hit the same frame).
-// ------------------------------------------------------------------------------------------------
-constexpr int SCHUR_WMAX = 448;  // frames per LDS window (448 * 9 * 8 B = 31.5 KiB)
-constexpr int SCHUR_WAVES = 8;   // 512-thread workgroups: two or three frames per CU
-constexpr int SCHUR_PF = 3;      // partner-batch prefetch ring depth per half-wave
-
-__device__ __forceinline__ double bcast(double v, int j) {
-  int lo = __builtin_amdgcn_readlane(__double2loint(v), j);
-  int hi = __builtin_amdgcn_readlane(__double2hiint(v), j);
-  return __hiloint2double(hi, lo);
-}
-
-// Bijection block -> item that gives each XCD group (b mod 8) a contiguous run of items.
-__device__ __forceinline__ int xcd_swizzle(int b, int nb) {
-  const int c = b & 7, idx = b >> 3;
-  int start = 0;
-  for (int q = 0; q < c; ++q) start += (nb - q + 7) >> 3;
-  return start + idx;
-}
-
-template <typename real>
-__global__ __launch_bounds__(64 * SCHUR_WAVES) void k_schur(SchurArgs a) {
-  __shared__ double s_S[SCHUR_WMAX * 9];
-  __shared__ double s_red[SCHUR_WAVES][12];
-  __shared__ double2 s_Y[SCHUR_WAVES][WAVE][3];  // per chunk: Y = W V^-1 of each segment (3x2)
-  __shared__ int2 s_seg[SCHUR_WAVES][WAVE];       // per chunk: (first partner s1, end of landmark)
-  // XCD-aware frame order: workgroups b and b+8 share an XCD (round-robin dispatch), so give each XCD
-  // a contiguous run of frames -> neighbouring frames (which share landmarks) hit the same L2.
-  const int f1 = xcd_swizzle(blockIdx.x, gridDim.x) + a.n_fixed;
-  const int lane = lane_id();
-  const int wv = threadIdx.x >> 6;
-  const int half = lane >> 5, hl = lane & 31;
-  const real* __restrict__ seg_ug = (const real*)a.seg_ug;
-  const real* __restrict__ seg_w = (const real*)a.seg_w;
-  const int e0 = a.frame_seg_begin[f1], e1 = a.frame_seg_begin[f1 + 1];
-  const int ne = e1 - e0;
-  const int eb = e0 + (int)(((int64_t)ne * wv) / SCHUR_WAVES);
-  const int ee = e0 + (int)(((int64_t)ne * (wv + 1)) / SCHUR_WAVES);
-  const int hi = a.frame_win_hi[f1];
-  const int col0 = a.frame_pos[f1];  // system row/column of f1's pan
-  const int64_t ld = a.ld;
-
-  double aU[6] = {0, 0, 0, 0, 0, 0}, ag[3] = {0, 0, 0}, ab[3] = {0, 0, 0};
-
-  for (int p0 = f1; p0 <= hi; p0 += SCHUR_WMAX) {
-    const int p1 = min(hi + 1, p0 + SCHUR_WMAX);
-    const int width = p1 - p0;
-    const bool first = (p0 == f1);
-    for (int k = threadIdx.x; k < width * 9; k += blockDim.x) s_S[k] = 0;
-    __syncthreads();
-    for (int cb = eb; cb < ee; cb += WAVE) {
-      // ---- lane-parallel metadata of up to 64 segments of f1
-      const int e = cb + lane;
-      const bool ok = e < ee;
-      int s1 = 0, send = 0;
-      double Y[3][2] = {{0, 0}, {0, 0}, {0, 0}};
-      if (ok) {
-        s1 = a.frame_seg_list[e];
-        const int l = a.seg_lm[s1];
-        send = a.lm_seg_begin[l + 1];
-        const real* w1 = seg_w + (int64_t)s1 * 8;
-        const double* vi = a.lm_aux + (int64_t)l * 8;
-        const double i00 = vi[0], i01 = vi[1], i11 = vi[2];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          const double W0 = (double)w1[2 * q], W1 = (double)w1[2 * q + 1];
-          Y[q][0] = W0 * i00 + W1 * i01;
-          Y[q][1] = W0 * i01 + W1 * i11;
-          if (first) ab[q] += W0 * vi[3] + W1 * vi[4];
-        }
-        if (first) {
-          const real* u1 = seg_ug + (int64_t)s1 * 12;
-#pragma unroll
-          for (int k = 0; k < 6; ++k) aU[k] += (double)u1[k];
-#pragma unroll
-          for (int q = 0; q < 3; ++q) ag[q] += (double)u1[6 + q];
-        }
-      }
-      const int n = min(WAVE, ee - cb);
-      // stage the chunk's segment metadata for broadcast reads by the half-waves
-#pragma unroll
-      for (int q = 0; q < 3; ++q) s_Y[wv][lane][q] = make_double2(Y[q][0], Y[q][1]);
-      s_seg[wv][lane] = make_int2(s1, send);
-      wave_lds_fence();
-      // Work items = (segment, batch of 32 partners); half-wave h walks the items of segments j = h,
-      // h+2, ...  A ring of SCHUR_PF items per half is in flight: every ring load is unconditional (an
-      // exhausted half reloads a valid segment and drops the result), so the compiler can wait for one
-      // slot at a time (a conditional or synchronous load in the loop would drain the whole ring).
-      const int nb_lane = ok ? (send - s1 + 31) >> 5 : 0;
-      int items_even = (lane & 1) ? 0 : nb_lane, items_odd = (lane & 1) ? nb_lane : 0;
-      items_even = wave_sum_i(items_even);
-      items_odd = wave_sum_i(items_odd);
-      const int my_items = half ? items_odd : items_even;
-      const int nsteps = max(items_even, items_odd);
-      // fetch-side cursor of this half: segment fj, batch fb (segments without items are skipped)
-      int fj = half, fb = 0, fs1 = 0, fsend = 0;
-      auto seek = [&]() {
-        for (; fj < n; fj += 2) {
-          const int2 g = s_seg[wv][fj];
-          if (g.y > g.x) {
-            fs1 = g.x;
-            fsend = g.y;
-            return;
-          }
-        }
-        fs1 = 0;
-        fsend = 0;
-      };
-      seek();
-      real xr[SCHUR_PF][8];
-      int jr[SCHUR_PF], s2r[SCHUR_PF], endr[SCHUR_PF];
-      auto fetch = [&](real(&x)[8], int& jo, int& s2o, int& endo) {
-        const int s2 = fs1 + 32 * fb + hl;
-        jo = min(fj, n - 1);
-        s2o = s2;
-        endo = fsend;
-        const int sl = (s2 < fsend) ? s2 : 0;  // an exhausted half loads segment 0 and drops it
-        if constexpr (sizeof(real) == 4) {
-          const float4* w2 = reinterpret_cast<const float4*>(seg_w + (int64_t)sl * 8);
-          const float4 lo = w2[0], hi4 = w2[1];
-          x[0] = lo.x; x[1] = lo.y; x[2] = lo.z; x[3] = lo.w; x[4] = hi4.x; x[5] = hi4.y; x[6] = hi4.z; x[7] = hi4.w;
-        } else {
-          const double2* w2 = reinterpret_cast<const double2*>(seg_w + (int64_t)sl * 8);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const double2 d = w2[k];
-            x[2 * k] = d.x; x[2 * k + 1] = d.y;
-          }
-        }
-        // advance the cursor
-        ++fb;
-        if (32 * fb >= fsend - fs1) {
-          fj += 2;
-          fb = 0;
-          seek();
-        }
-      };
-#pragma unroll
-      for (int u = 0; u < SCHUR_PF; ++u) fetch(xr[u], jr[u], s2r[u], endr[u]);
-      for (int t0 = 0; t0 < nsteps; t0 += SCHUR_PF) {
-#pragma unroll
-        for (int u = 0; u < SCHUR_PF; ++u) {
-          if (t0 + u < nsteps) {  // wave-uniform
-            if (t0 + u < my_items && s2r[u] < endr[u]) {
-              double Yj[3][2];
-#pragma unroll
-              for (int q = 0; q < 3; ++q) {
-                const double2 yq = s_Y[wv][jr[u]][q];
-                Yj[q][0] = yq.x;
-                Yj[q][1] = yq.y;
-              }
-              const real* w2v = xr[u];
-              const int f2 = __real_as_int(w2v[6]);
-              if (f2 >= p0 && f2 < p1) {
-                double* dst = s_S + (f2 - p0) * 9;
-#pragma unroll
-                for (int q = 0; q < 3; ++q)
-#pragma unroll
-                  for (int r = 0; r < 3; ++r)
-                    atomicAdd(dst + 3 * q + r, -(Yj[q][0] * (double)w2v[2 * r] + Yj[q][1] * (double)w2v[2 * r + 1]));
-              }
-            }
-            fetch(xr[u], jr[u], s2r[u], endr[u]);
-          }
-        }
-      }
-      wave_lds_fence();  // the next chunk restages s_Y / s_seg
-    }
-    if (first) {
-#pragma unroll
-      for (int k = 0; k < 6; ++k) aU[k] = wave_sum(aU[k]);
-#pragma unroll
-      for (int q = 0; q < 3; ++q) { ag[q] = wave_sum(ag[q]); ab[q] = wave_sum(ab[q]); }
-      if (lane == 0) {
-        for (int k = 0; k < 6; ++k) s_red[wv][k] = aU[k];
-        for (int q = 0; q < 3; ++q) { s_red[wv][6 + q] = ag[q]; s_red[wv][9 + q] = ab[q]; }
-      }
-    }
-    __syncthreads();
-    if (first && threadIdx.x == 0) {
-      double U[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0}, bb[3] = {0, 0, 0};
-      for (int w = 0; w < SCHUR_WAVES; ++w) {
-        for (int k = 0; k < 6; ++k) U[k] += s_red[w][k];
-        for (int q = 0; q < 3; ++q) { g[q] += s_red[w][6 + q]; bb[q] += s_red[w][9 + q]; }
-      }
-      const int ui[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
-      for (int q = 0; q < 3; ++q)
-        for (int r = 0; r < 3; ++r) s_S[3 * q + r] += U[ui[q][r]];
-      for (int q = 0; q < 3; ++q) {
-        a.b[col0 + q] = -g[q] + bb[q];
-        a.g_pose[col0 + q] = g[q];
-      }
-      a.dU[col0 + 0] = U[0];
-      a.dU[col0 + 1] = U[3];
-      a.dU[col0 + 2] = U[5];
-    }
-    __syncthreads();
-    // write block (f2, f1) for frames f2 in [p0, p1) into the lower triangle of the system order:
-    // S[pos(f2)+r][pos(f1)+q] = S_{f1,f2}[q][r], or its mirror when f2 precedes f1 in that order
-    for (int k = threadIdx.x; k < width * 9; k += blockDim.x) {
-      const int t = k / 9, qr = k % 9, q = qr / 3, r = qr % 3;
-      const int64_t pf2 = a.frame_pos[p0 + t];
-      if (pf2 >= col0) a.S[(pf2 + r) * ld + col0 + q] = s_S[k];
-      else a.S[(int64_t)(col0 + q) * ld + pf2 + r] = s_S[k];
-    }
-    __syncthreads();
-  }
-}
-
-template <typename real>
-void launch_schur(const SchurArgs& a, int n_free, hipStream_t st) {
-  if (n_free <= 0) return;
-  hipLaunchKernelGGL(k_schur<real>, dim3(n_free), dim3(64 * SCHUR_WAVES), 0, st, a);
-}
 
 // pose damping on the exchanged reduced system: D = max(D, diag U) (monotone), S_ii += lambda D_i
 __global__ void k_pose_damp(double* __restrict__ S, int64_t ld, const double* __restrict__ dU,
@@ -591,13 +372,14 @@ __global__ __launch_bounds__(256) void k_backsub(BacksubArgs a) {
   const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (l >= a.n_lm) return;
   const int s0 = a.lm_seg_begin[l], s1 = a.lm_seg_begin[l + 1];
-  const real* __restrict__ seg_w = (const real*)a.seg_w;
+  const real* __restrict__ w_slot = (const real*)a.w_slot;
+  const int4 lmeta = a.lm_meta[l];
   double t0 = 0, t1 = 0;
   for (int s = s0 + lane; s < s1; s += WAVE) {
     const int f = a.seg_frame[s];
     if (f < a.n_fixed) continue;
     const double* dp = a.dpose + a.frame_pos[f];
-    const real* w = seg_w + (int64_t)s * 8;
+    const real* w = w_slot + ((int64_t)lmeta.z + f - lmeta.x) * 8;
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       t0 += (double)w[2 * q] * dp[q];
@@ -795,8 +577,6 @@ template void launch_tables<float>(const double*, const double*, int, int, void*
 template void launch_tables<double>(const double*, const double*, int, int, void*, void*, void*, void*, hipStream_t);
 template void launch_linearize<float>(const LinArgs&, int, hipStream_t);
 template void launch_linearize<double>(const LinArgs&, int, hipStream_t);
-template void launch_schur<float>(const SchurArgs&, int, hipStream_t);
-template void launch_schur<double>(const SchurArgs&, int, hipStream_t);
 template void launch_backsub<float>(const BacksubArgs&, hipStream_t);
 template void launch_backsub<double>(const BacksubArgs&, hipStream_t);
 template void launch_residual<float>(const int32_t*, const int32_t*, const int32_t*, const double2*, const void*,

@@ -21,33 +21,41 @@ struct LinArgs {
   const double2* seg_base;       // [n_seg] base observation; records hold obs - base (real)
   double u, v, fs2, inv_fs2;
   void* seg_ug;                  // [n_seg][12] real: U (6) | g_pose (3) | 0 0 0
-  void* seg_w;                   // [n_seg][8] real: W (6) | frame id bits | 0
+  void* w_slot;                  // [n_slot][8] real: W (6) | 0 0 at slot toff_l + frame - first_l
+  const int4* lm_meta;           // [n_lm] {first frame, last frame, slot offset, 0}
   double* lm_out;                // [n_lm][8]
 };
 
+// K2 tiles: block of SCHUR_F1 consecutive free frames x chunk of 64 partner frames; work items are
+// splits of a tile's landmark list.  Static structure built once by ptzba_set_problem.
+constexpr int SCHUR_F1 = 32;
+constexpr int SCHUR_LMAX = 512;  // landmarks per work item (split size cap)
 struct SchurArgs {
-  const int32_t* frame_seg_begin;  // [n_pose+1]
-  const int32_t* frame_seg_list;   // [n_seg]
-  const int32_t* frame_win_hi;     // [n_pose]
-  const int32_t* seg_lm;           // [n_seg]
-  const int32_t* seg_frame;        // [n_seg]
-  const int32_t* lm_seg_begin;     // [n_lm+1]
-  const void* seg_ug;              // [n_seg][12] real: U | g_pose
-  const void* seg_w;               // [n_seg][8] real compact W + frame
-  const double* lm_aux;            // [n_lm][8]
-  const int32_t* frame_pos;        // [n_pose] system row of the frame's pan (-1: fixed)
-  double* S;                       // [ld][ld] lower, row-major
-  double* b;                       // [n_sys]
-  double* g_pose;                  // [n_sys]
-  double* dU;                      // [n_sys] diag of U (for Marquardt scaling)
+  const int4* items;              // [n_items] {f1b, chunk, list begin, list end}
+  const int4* groups;             // [n_groups] per tile {f1b, chunk, first item, end item}
+  const int4* item_lm;            // item landmark lists: {landmark, first frame, last frame, slot offset}
+  const int32_t* frame_seg_begin; // [n_pose+1]
+  const int4* frame_seg_info;     // [n_seg] frame CSR entries {segment, landmark, W slot, 0}
+  const int32_t* frame_win_hi;    // [n_pose]
+  const void* seg_ug;             // [n_seg][12] real: U | g_pose
+  const void* w_slot;             // [n_slot][8] real: W | 0 0 (dense landmark x frame slots)
+  const double* lm_aux;           // [n_lm][8]
+  const int32_t* frame_pos;       // [n_pose] system row of the frame's pan (-1: fixed)
+  double* part;                   // [n_items][SCHUR_F1][9][64] split partials
+  double* fdiag;                  // [n_pose][12] U (6) | g_pose (3) | sum W V~^-1 g (3)
+  double* S;                      // [ld][ld] lower, row-major
+  double* b;                      // [n_sys]
+  double* g_pose;                 // [n_sys]
+  double* dU;                     // [n_sys] diag of U (for Marquardt scaling)
   int64_t ld;
-  int n_fixed;
+  int n_pose;
 };
 
 struct BacksubArgs {
   const int32_t* lm_seg_begin;
   const int32_t* seg_frame;
-  const void* seg_w;     // [n_seg][8] real: W | frame
+  const void* w_slot;    // [n_slot][8] real: W | 0 0
+  const int4* lm_meta;   // [n_lm] {first frame, last frame, slot offset, 0}
   const double* lm_out;
   const double* lm_aux;
   const double* D_ray;
@@ -68,11 +76,11 @@ template <typename real>
 void launch_linearize(const LinArgs& a, int loss, hipStream_t st);
 void launch_landmark_damp(const double* lm_out, const int32_t* lm_seg_begin, double* D_ray, double* lm_aux, int n_lm,
                           double lambda, hipStream_t st);
-template <typename real>
-void launch_schur(const SchurArgs& a, int n_free, hipStream_t st);
 void launch_pose_damp(double* S, int64_t ld, const double* dU, double* D_pose, const int32_t* frame_pos, int n_pose,
                       int n_fixed, double lambda,
                       hipStream_t st);
+template <typename real>
+void launch_schur(const SchurArgs& a, int n_items, int n_groups, int n_fixed, hipStream_t st);
 template <typename real>
 void launch_backsub(const BacksubArgs& a, hipStream_t st);
 void launch_pose_trial(const double* ptz, const double* dpose, const double* g_pose, const double* D_pose,

@@ -1,0 +1,273 @@
+// K2 of libptzba for gfx950: the reduced camera system of the Schur complement (SURVEY §8a row a4,
+// the exact replacement of scipy's dense trf solve at bundle_adjustment.py:200-202).
+// Compiled without SLP vectorisation: packing the per-lane FMA chains into v_pk_* operations with
+// register shuffles serialises them (dependent pk_mul -> pk_fma -> pk_add chains with s_nop hazards).
+#include "ptzba_common.h"
+#include "ptzba_kernels.h"
+
+namespace ptzba {
+
+// ------------------------------------------------------------------------------------------------
+// K2: reduced camera system  S = U - sum_l W_l V~_l^-1 W_l^T   (damping added after the exchange),
+//                            b = -g_pose + sum_l W_l V~_l^-1 g_l
+// Three launches:
+//   k_frame_diag   one workgroup per free frame: U, g_pose and sum_l W V~^-1 g_l over the frame's
+//                  segments (frame CSR) -> fdiag[f][12];
+//   k_schur        the coupling blocks, register-blocked with LDS-staged operands (below);
+//   k_schur_reduce sums the split partials of each tile, adds U on the diagonal, writes S (lower
+//                  triangle, system order) and b | g_pose | diag U.
+// k_schur work item = (tile: block F1 of 32 consecutive free frames x chunk of 64 partner frames,
+// split of the tile's landmark list).  Lane = partner frame f2; wave w owns the 4 frames f1 = f1b+4w..
+// of F1, so a lane accumulates the four 3x3 blocks S_{f1,f2} in registers (no atomics, no scatter).
+// W lives in the dense landmark x frame slot table (slot = toff_l + f - first_l, written by K1; slots
+// of frames that do not see the landmark stay zero).  Per batch of SNB landmarks the workgroup stages
+// in LDS, double-buffered with the next batch's loads in flight during the current batch's FMAs:
+//   * the landmarks' W rows over the chunk's 64 frames (coalesced: consecutive slots) -- loaded once
+//     and read by all 8 waves (32 frames of reuse per load);
+//   * Y = W_{f1,l} V~_l^-1 for every (landmark, f1 in F1) pair (zero where f1 does not see l), so the
+//     batch's FMAs run straight-line without branches.
+// Products are accumulated in the record precision per batch and flushed to fp64 registers; each
+// split writes its fp64 blocks to a partial buffer [item][32 f1][9][64 f2] (coalesced), reduced by
+// k_schur_reduce in a fixed order (deterministic).
+// ------------------------------------------------------------------------------------------------
+#ifndef S2_ABL
+#define S2_ABL 0  // ablation switch for measurements: 1 = no FMAs, 2 = no operand loads
+#endif
+constexpr int SF = SCHUR_F1;   // frames per F1 block
+constexpr int SFW = SF / 8;    // f1 frames per wave (8 waves)
+
+// Bijection block -> item that gives each XCD group (b mod 8) a contiguous run of items.
+__device__ __forceinline__ int xcd_swizzle(int b, int nb) {
+  const int c = b & 7, idx = b >> 3;
+  int start = 0;
+  for (int q = 0; q < c; ++q) start += (nb - q + 7) >> 3;
+  return start + idx;
+}
+
+// the 6 W values of a slot row (8 reals, 16-B aligned)
+template <typename real>
+__device__ __forceinline__ void load_w6(real (&x)[6], const real* __restrict__ p) {
+  if constexpr (sizeof(real) == 4) {
+    const float4 lo = reinterpret_cast<const float4*>(p)[0];
+    const float2 hi = reinterpret_cast<const float2*>(p)[2];
+    x[0] = lo.x; x[1] = lo.y; x[2] = lo.z; x[3] = lo.w; x[4] = hi.x; x[5] = hi.y;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const double2 d = reinterpret_cast<const double2*>(p)[k];
+      x[2 * k] = d.x; x[2 * k + 1] = d.y;
+    }
+  }
+}
+
+// one 256-thread workgroup per free frame; frame_seg_info[e] = {segment, landmark, W slot, 0}
+template <typename real>
+__global__ __launch_bounds__(256) void k_frame_diag(SchurArgs a, int n_fixed) {
+  __shared__ double red[4][12];
+  const int f = n_fixed + blockIdx.x;
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  const real* __restrict__ seg_ug = (const real*)a.seg_ug;
+  const real* __restrict__ w_slot = (const real*)a.w_slot;
+  double acc[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) acc[k] = 0;
+  const int e1 = a.frame_seg_begin[f + 1];
+#pragma unroll 2
+  for (int e = a.frame_seg_begin[f] + threadIdx.x; e < e1; e += 256) {
+    const int4 m = a.frame_seg_info[e];
+    const real* u = seg_ug + (int64_t)m.x * 12;
+    const double* vi = a.lm_aux + (int64_t)m.y * 8;
+    real w[6];
+    load_w6(w, w_slot + (int64_t)m.z * 8);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) acc[k] += (double)u[k];
+    const double vg0 = vi[3], vg1 = vi[4];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) acc[9 + q] += (double)w[2 * q] * vg0 + (double)w[2 * q + 1] * vg1;
+  }
+#pragma unroll
+  for (int k = 0; k < 12; ++k) {
+    const double v = wave_sum(acc[k]);
+    if (lane == 0) red[wv][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 12) {
+    const int k = threadIdx.x;
+    a.fdiag[(int64_t)f * 12 + k] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
+  }
+}
+
+template <typename real>
+__global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
+  // fp64 (parity path) stages half as many landmarks per batch to stay inside 160 KiB of LDS
+  constexpr int SNB = sizeof(real) == 4 ? 16 : 8;
+  constexpr int WP = sizeof(real) == 4 ? 8 : 6;  // 16-B aligned row pitch for 6 values
+  __shared__ real sW[2][SNB][6][WAVE];                             // W rows of the chunk's frames (SoA)
+  __shared__ __attribute__((aligned(16))) real sY[2][SNB][SF][WP];  // Y of (landmark, f1); 0 if unobserved
+  __shared__ int4 sL[SCHUR_LMAX];                                    // the item's landmark list
+  const int item = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int4 it = a.items[item];
+  const int f1b = it.x, chunk = it.y, lb = it.z, nl = it.w - it.z;
+  const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+  const int f2base = f1b + WAVE * chunk;
+  const real* __restrict__ w_slot = (const real*)a.w_slot;
+  for (int k = t; k < nl; k += 512) sL[k] = a.item_lm[lb + k];
+  __syncthreads();
+
+  // ---- staging registers: W slots (e = t, t + 512 over [SNB][64]) and one Y pair (j = t / SF, i = t % SF;
+  // fp64: threads >= SNB*SF repeat a pair and do not stage it).  Branch-free, so the loads stay in flight
+  // until stage() consumes them after the current batch's FMAs.
+  constexpr int NSL = SNB * WAVE / 512;  // W slots per thread per batch (2 fp32, 1 fp64)
+  real rw[NSL][6];
+  bool rwin[NSL];
+  real ryw[6];
+  double rvi[3];
+  bool ryin;
+  const int yj = (t / SF) & (SNB - 1), yi = t & (SF - 1);
+  auto fetch = [&](int p) {  // landmarks [p, p + SNB) of the list
+#pragma unroll
+    for (int q = 0; q < NSL; ++q) {
+      const int e = t + 512 * q, j = e >> 6, ln = e & 63;
+      const int4 m = sL[min(p + j, nl - 1)];  // {landmark, first frame, last frame, slot offset}
+      const int idx = f2base + ln - m.y;
+      rwin[q] = (p + j < nl) && idx >= 0 && f2base + ln <= m.z;
+      load_w6(rw[q], w_slot + (int64_t)(m.w + min(max(idx, 0), m.z - m.y)) * 8);
+    }
+    const int f = f1b + yi;
+    const int4 m = sL[min(p + yj, nl - 1)];
+    ryin = (p + yj < nl) && f >= m.y && f <= m.z;
+    load_w6(ryw, w_slot + (int64_t)(m.w + min(max(f - m.y, 0), m.z - m.y)) * 8);
+    const double* vi = a.lm_aux + (int64_t)m.x * 8;
+    rvi[0] = vi[0]; rvi[1] = vi[1]; rvi[2] = vi[2];
+  };
+  auto stage = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < NSL; ++q) {
+      const int e = t + 512 * q, j = e >> 6, ln = e & 63;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) sW[buf][j][k][ln] = rwin[q] ? rw[q][k] : (real)0;
+    }
+    if (t < SNB * SF) {
+      real* y = sY[buf][yj][yi];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const double W0 = ryin ? (double)ryw[2 * q] : 0.0, W1 = ryin ? (double)ryw[2 * q + 1] : 0.0;
+        y[2 * q] = (real)-(W0 * rvi[0] + W1 * rvi[1]);  // staged negated: the FMAs accumulate -Y W^T
+        y[2 * q + 1] = (real)-(W0 * rvi[1] + W1 * rvi[2]);
+      }
+    }
+  };
+
+  double acc[SFW][9];
+#pragma unroll
+  for (int i = 0; i < SFW; ++i)
+#pragma unroll
+    for (int k = 0; k < 9; ++k) acc[i][k] = 0;
+
+  if (nl > 0) {
+    fetch(0);
+    stage(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int p = 0; p < nl; p += SNB) {
+    const bool more = p + SNB < nl;  // block-uniform
+    if (S2_ABL != 2) fetch(p + SNB);  // next batch's loads in flight during this batch's FMAs (unconditional: no phi
+                     // at a join forces an early wait; past the list the lanes load clamped slots)
+    real accr[SFW][9];
+#pragma unroll
+    for (int i = 0; i < SFW; ++i)
+#pragma unroll
+      for (int k = 0; k < 9; ++k) accr[i][k] = 0;
+    if (S2_ABL != 1)
+    // straight-line over the whole batch: slots past the list and unobserved (landmark, f1) pairs were
+    // staged as zeros, so no branch (and no wait at a branch) interrupts the LDS reads and the FMAs
+#pragma unroll 2
+    for (int j = 0; j < SNB; ++j) {
+      real w2[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) w2[k] = sW[buf][j][k][lane];
+#pragma unroll
+      for (int i = 0; i < SFW; ++i) {
+        const real* ys = sY[buf][j][SFW * wv + i];
+        real y[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) y[k] = ys[k];
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+#pragma unroll
+          for (int r = 0; r < 3; ++r) {
+            accr[i][3 * q + r] = fma(y[2 * q], w2[2 * r], accr[i][3 * q + r]);
+            accr[i][3 * q + r] = fma(y[2 * q + 1], w2[2 * r + 1], accr[i][3 * q + r]);
+          }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < SFW; ++i)
+#pragma unroll
+      for (int k = 0; k < 9; ++k) acc[i][k] += (double)accr[i][k];
+    if (more) stage(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // partial blocks of this split: part[item][f1 local][k][f2 lane]
+  double* out = a.part + (int64_t)item * (SF * 9 * WAVE);
+#pragma unroll
+  for (int i = 0; i < SFW; ++i)
+#pragma unroll
+    for (int k = 0; k < 9; ++k) out[((SFW * wv + i) * 9 + k) * WAVE + lane] = acc[i][k];
+}
+
+// tile reduction: thread = one element of a tile (grid: tile x 72 blocks of 256); fixed-order sum of the
+// splits, U on the diagonal blocks, write the lower triangle in the system order (mirror when f2
+// precedes f1); chunk-0 tiles also write b | g_pose | diag U of their frames.
+__global__ __launch_bounds__(256) void k_schur_reduce(SchurArgs a) {
+  constexpr int NE = SF * 9 * WAVE;
+  const int4 g = a.groups[blockIdx.y];  // {f1b, chunk, first item, end item}
+  const int f1b = g.x, chunk = g.y;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int ln = e & 63, ik = e >> 6, i = ik / 9, k = ik - 9 * i, q = k / 3, r = k - 3 * q;
+  const int f1 = f1b + i, f2 = f1b + WAVE * chunk + ln;
+  if (f1 < a.n_pose && f2 >= f1 && f2 <= a.frame_win_hi[f1]) {
+    const double* p = a.part + e;
+    double v = 0;
+    int it = g.z;
+    for (; it + 4 <= g.w; it += 4) {
+      const double p0 = p[(int64_t)it * NE], p1 = p[(int64_t)(it + 1) * NE];
+      const double p2 = p[(int64_t)(it + 2) * NE], p3 = p[(int64_t)(it + 3) * NE];
+      v += p0; v += p1; v += p2; v += p3;
+    }
+    for (; it < g.w; ++it) v += p[(int64_t)it * NE];
+    if (f2 == f1) {
+      const int ui = q <= r ? (q == 0 ? r : (q == 1 ? 2 + r : 5)) : (r == 0 ? q : (r == 1 ? 2 + q : 5));
+      v += a.fdiag[(int64_t)f1 * 12 + ui];
+    }
+    const int64_t ld = a.ld, col0 = a.frame_pos[f1], pf2 = a.frame_pos[f2];
+    if (pf2 >= col0) a.S[(pf2 + r) * ld + col0 + q] = v;
+    else a.S[(col0 + q) * ld + pf2 + r] = v;
+  }
+  if (chunk == 0 && blockIdx.x == 0 && threadIdx.x < SF * 3) {
+    const int i2 = threadIdx.x / 3, q2 = threadIdx.x - 3 * i2, f = f1b + i2;
+    if (f < a.n_pose) {
+      const double* d = a.fdiag + (int64_t)f * 12;
+      const int c0 = a.frame_pos[f];
+      a.b[c0 + q2] = -d[6 + q2] + d[9 + q2];
+      a.g_pose[c0 + q2] = d[6 + q2];
+      a.dU[c0 + q2] = d[q2 == 0 ? 0 : (q2 == 1 ? 3 : 5)];
+    }
+  }
+}
+
+template <typename real>
+void launch_schur(const SchurArgs& a, int n_items, int n_groups, int n_fixed, hipStream_t st) {
+  const int n_free = a.n_pose - n_fixed;
+  if (n_free <= 0) return;
+  hipLaunchKernelGGL(k_frame_diag<real>, dim3(n_free), dim3(256), 0, st, a, n_fixed);
+  if (n_items > 0) hipLaunchKernelGGL(k_schur<real>, dim3(n_items), dim3(512), 0, st, a);
+  if (n_groups > 0) hipLaunchKernelGGL(k_schur_reduce, dim3(SF * 9 * WAVE / 256, n_groups), dim3(256), 0, st, a);
+}
+
+template void launch_schur<float>(const SchurArgs&, int, int, int, hipStream_t);
+template void launch_schur<double>(const SchurArgs&, int, int, int, hipStream_t);
+
+}  // namespace ptzba
