@@ -49,14 +49,14 @@ struct ptzba_ctx {
   DBuf rec_xy, rec_seg, rec_w, perm;
   DBuf seg_frame, seg_lm, seg_rec_begin, lm_seg_begin, lm_order;
   DBuf frame_seg_begin, frame_seg_list, frame_win_hi;
-  DBuf s2_items, s2_groups, s2_lm, lm_meta, frame_seg_info;  // K2 work items / tiles / lists, slot ranges
-  DBuf s2_part, fdiag;                                        // K2 split partials, per-frame U | g | b
+  DBuf s2_items, s2_groups, s2_lm, lm_meta;  // K2 work items / tiles / lists, slot ranges
+  DBuf s2_part, part_diag;                                    // K2 split partials (blocks, diagonal terms)
   int n_s2_items = 0, n_s2_groups = 0;
   int64_t n_slot = 0;  // dense landmark x frame slots (W table rows)
   // device: state
   DBuf ptz, rays, ptz_trial, rays_trial, D_pose, D_ray;
   DBuf ft, rt, ft64, rt64, seg_base;
-  DBuf seg_ug[2], w_slot[2], lm_out[2];
+  DBuf ug_slot[2], w_slot[2], lm_out[2];
   int cur = 0;
   DBuf lm_aux, lm_red, red_scratch;
   DBuf sys;  // [S ld*ld | b ld | g_pose ld | dU ld]
@@ -448,7 +448,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   }
   // ---- register-blocked K2 structure: per landmark its frame range [first, last] and a dense W slot
   // per frame in it; K2 tiles (SCHUR_F1 frames x 64 partner frames) with the landmarks that reach them,
-  std::vector<int32_t> lm_meta(4 * (size_t)std::max(n_landmark, 1), 0), frame_seg_info(4 * (size_t)n_seg), s2_items, s2_groups,
+  std::vector<int32_t> lm_meta(4 * (size_t)std::max(n_landmark, 1), 0), s2_items, s2_groups,
       s2_lm;
   {
     int64_t toff = 0;
@@ -463,13 +463,6 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       if (toff >= INT32_MAX) return fail("landmark x frame slot table exceeds 2^31 rows");
     }
     h->n_slot = toff;
-    for (int64_t e = 0; e < n_seg; ++e) {
-      const int s = frame_seg_list[e], l = seg_lm[s];
-      frame_seg_info[4 * e] = s;
-      frame_seg_info[4 * e + 1] = l;
-      frame_seg_info[4 * e + 2] = lm_meta[4 * l + 2] + seg_frame[s] - lm_meta[4 * l];
-      frame_seg_info[4 * e + 3] = 0;
-    }
     // split size: about two work items per CU over the whole list volume, at least 64 landmarks
     std::vector<std::vector<int32_t>> tiles;
     std::vector<int32_t> tile_key;
@@ -494,7 +487,11 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
         tile_key.push_back(c);
       }
     }
-    const int64_t split = std::min<int64_t>(SCHUR_LMAX, std::max<int64_t>(64, (total + 511) / 512));
+    // split size: at most ~512 work items (two rounds of one workgroup per CU) counting the per-tile
+    // rounding, at least 64 landmarks, at most SCHUR_LMAX (the LDS list)
+    const int64_t n_tiles = (int64_t)tiles.size();
+    const int64_t split = std::min<int64_t>(SCHUR_LMAX, std::max<int64_t>(64, (total + std::max<int64_t>(512 - n_tiles, 64) - 1) /
+                                                                                 std::max<int64_t>(512 - n_tiles, 64)));
     for (size_t k = 0; k < tiles.size(); ++k) {
       const auto& lst = tiles[k];
       const int n = (int)lst.size();
@@ -577,23 +574,22 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       upload(h->lm_order, lm_work) || upload(h->frame_seg_begin, frame_seg_begin) ||
       upload(h->frame_seg_list, frame_seg_list) || upload(h->frame_win_hi, frame_win_hi) ||
       upload(h->s2_items, s2_items) || upload(h->s2_groups, s2_groups) || upload(h->s2_lm, s2_lm) ||
-      upload(h->lm_meta, lm_meta) ||
-      upload(h->frame_seg_info, frame_seg_info))
+      upload(h->lm_meta, lm_meta))
     return -1;
   const size_t e = h->elem();
   if (h->ptz.alloc(3 * n_pose * 8) || h->ptz_trial.alloc(3 * n_pose * 8) || h->rays.alloc(2 * (size_t)n_landmark * 8) ||
       h->rays_trial.alloc(2 * (size_t)n_landmark * 8) || h->D_pose.alloc(3 * n_pose * 8) ||
       h->D_ray.alloc(2 * (size_t)n_landmark * 8) || h->ft.alloc((size_t)n_pose * 8 * e) ||
       h->rt.alloc((size_t)n_landmark * 8 * e) || h->ft64.alloc((size_t)n_pose * 64) ||
-      h->rt64.alloc((size_t)n_landmark * 64) || h->seg_ug[0].alloc((size_t)n_seg * 12 * e) ||
-      h->seg_ug[1].alloc((size_t)n_seg * 12 * e) || h->w_slot[0].alloc((size_t)std::max<int64_t>(h->n_slot, 1) * 8 * e) ||
+      h->rt64.alloc((size_t)n_landmark * 64) || h->ug_slot[0].alloc((size_t)std::max<int64_t>(h->n_slot, 1) * 12 * e) ||
+      h->ug_slot[1].alloc((size_t)std::max<int64_t>(h->n_slot, 1) * 12 * e) || h->w_slot[0].alloc((size_t)std::max<int64_t>(h->n_slot, 1) * 8 * e) ||
       h->w_slot[1].alloc((size_t)std::max<int64_t>(h->n_slot, 1) * 8 * e) || h->lm_out[0].alloc((size_t)n_landmark * 8 * 8) ||
       h->lm_out[1].alloc((size_t)n_landmark * 8 * 8) || h->lm_aux.alloc((size_t)n_landmark * 8 * 8) ||
       h->lm_red.alloc((size_t)n_landmark * 4 * 8) || h->sys.alloc((size_t)h->sys_count() * 8) ||
       h->scal.alloc(PTZBA_NSCALARS * 8) || h->red_scratch.alloc(RED_SCRATCH * 8) || h->loc.alloc(PTZBA_NSCALARS * 8) || h->info.alloc(16) ||
       h->Ldiag.alloc((size_t)h->ld * CHOL_NB * 8) || h->dpose.alloc((size_t)h->ld * 8) ||
       h->s2_part.alloc((size_t)std::max(h->n_s2_items, 1) * SCHUR_F1 * 9 * WAVE * 8) ||
-      h->fdiag.alloc((size_t)n_pose * 12 * 8))
+      h->part_diag.alloc((size_t)std::max(h->n_s2_items, 1) * SCHUR_F1 * 12 * 8))
     return -1;
   if (upload(h->chol_tasks, plan.tasks) || upload(h->frame_pos, sorder.pos) || upload(h->row_pad, sorder.pad) ||
       upload(h->bs_chain_off, plan.chain_off) || upload(h->bs_chain_cols, plan.chain_cols) ||
@@ -605,6 +601,8 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   HIPCHK(hipMemset(h->D_ray.p, 0, h->D_ray.bytes));
   HIPCHK(hipMemset(h->w_slot[0].p, 0, h->w_slot[0].bytes));  // slots of unobserved frames stay zero
   HIPCHK(hipMemset(h->w_slot[1].p, 0, h->w_slot[1].bytes));
+  HIPCHK(hipMemset(h->ug_slot[0].p, 0, h->ug_slot[0].bytes));
+  HIPCHK(hipMemset(h->ug_slot[1].p, 0, h->ug_slot[1].bytes));
   HIPCHK(hipMemset(h->ptz.p, 0, h->ptz.bytes));
   HIPCHK(hipMemset(h->rays.p, 0, h->rays.bytes));
   HIPCHK(hipMemset(h->scal.p, 0, h->scal.bytes));
@@ -631,8 +629,8 @@ int ptzba_problem_info(ptzba_handle h, int64_t* info) {
                                     &h->seg_base, &h->ft64, &h->rt64,
                                     &h->seg_rec_begin, &h->lm_seg_begin, &h->lm_order, &h->frame_seg_begin,
                                     &h->frame_seg_list, &h->frame_win_hi, &h->ptz, &h->rays, &h->ptz_trial,
-                                    &h->rays_trial, &h->D_pose, &h->D_ray, &h->ft, &h->rt, &h->seg_ug[0],
-                                    &h->seg_ug[1], &h->w_slot[0], &h->w_slot[1], &h->lm_out[0], &h->lm_out[1], &h->lm_aux, &h->lm_red, &h->sys,
+                                    &h->rays_trial, &h->D_pose, &h->D_ray, &h->ft, &h->rt, &h->ug_slot[0],
+                                    &h->ug_slot[1], &h->w_slot[0], &h->w_slot[1], &h->lm_out[0], &h->lm_out[1], &h->lm_aux, &h->lm_red, &h->sys,
                                     &h->scal, &h->loc});
   return 0;
 }
@@ -667,7 +665,7 @@ static void linearize_into(ptzba_ctx* h, int slot) {
   a.v = h->v;
   a.fs2 = h->fs * h->fs;
   a.inv_fs2 = 1.0 / (h->fs * h->fs);
-  a.seg_ug = h->seg_ug[slot].p;
+  a.ug_slot = h->ug_slot[slot].p;
   a.w_slot = h->w_slot[slot].p;
   a.lm_meta = h->lm_meta.as<int4>();
   a.lm_out = h->lm_out[slot].as<double>();
@@ -761,12 +759,10 @@ int ptzba_build_reduced(ptzba_handle h, double lambda) {
   a.items = h->s2_items.as<int4>();
   a.groups = h->s2_groups.as<int4>();
   a.part = h->s2_part.as<double>();
-  a.fdiag = h->fdiag.as<double>();
+  a.part_diag = h->part_diag.as<double>();
   a.item_lm = h->s2_lm.as<int4>();
-  a.frame_seg_begin = h->frame_seg_begin.as<int32_t>();
-  a.frame_seg_info = h->frame_seg_info.as<int4>();
   a.frame_win_hi = h->frame_win_hi.as<int32_t>();
-  a.seg_ug = h->seg_ug[c].p;
+  a.ug_slot = h->ug_slot[c].p;
   a.w_slot = h->w_slot[c].p;
   a.lm_aux = h->lm_aux.as<double>();
   a.frame_pos = h->frame_pos.as<int32_t>();

@@ -13,7 +13,7 @@
 //   tables    FrameTab[n_pose] (cos/sin pan, cos/sin tilt, f), RayTab[n_lm] (ray direction + derivs)
 //   lin       w_slot[n_slot][8] = W(3x2) | 0 0  (real) in the dense landmark x frame slot table:
 //                                 slot = toff_l + frame - first_l; slots of unobserved frames stay 0
-//             seg_ug[n_seg][12] = U(3x3 sym, 6) | g_pose(3) | pad   (real, reduced per frame by Schur)
+//             ug_slot[n_slot][12] = U(3x3 sym, 6) | g_pose(3) | pad (real, same slots; summed per frame by K2)
 //             lm_out[n_lm][8]    = V(2x2 sym, 3) | g_ray(2) | cost | pad      (fp64)
 //
 // K1 `k_linearize` is the HBM-streaming kernel: one wave per landmark walks the landmark's records
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256, K1_MIN_WAVES) void k_linearize(LinArgs a) {
   const double2* __restrict__ seg_base = a.seg_base;
   const real* __restrict__ rec_xy = (const real*)a.rec_xy;
   const real* __restrict__ rec_w = (const real*)a.rec_w;
-  real* __restrict__ seg_ug = (real*)a.seg_ug;
+  real* __restrict__ ug_slot = (real*)a.ug_slot;
   real* __restrict__ w_slot = (real*)a.w_slot;
   const int4 lmeta = a.lm_meta[l];  // {first frame, last frame, slot offset, 0}
   const int64_t slot0 = (int64_t)lmeta.z - lmeta.x;
@@ -264,8 +264,8 @@ __global__ __launch_bounds__(256, K1_MIN_WAVES) void k_linearize(LinArgs a) {
       real* cw = w_slot + (slot0 + fs) * 8;
       store4(cw, W[0], W[1], W[2], W[3]);
       store4(cw + 4, W[4], W[5], (real)0, (real)0);
-      // seg_ug[12] = {U (6), g_pose (3), 0, 0, 0}: reduced per frame by the Schur kernel
-      real* o = seg_ug + (int64_t)s * 12;
+      // U (6) | g_pose (3) | 0 0 0 into the same dense slot: summed per frame by the Schur kernel
+      real* o = ug_slot + (slot0 + fs) * 12;
       store4(o, Sx * J[0][0] * J[0][0] + Sy * J[1][0] * J[1][0], Sx * J[0][0] * J[0][1] + Sy * J[1][0] * J[1][1],
              Sx * J[0][0] * J[0][2] + Sy * J[1][0] * J[1][2], Sx * J[0][1] * J[0][1] + Sy * J[1][1] * J[1][1]);
       store4(o + 4, Sx * J[0][1] * J[0][2] + Sy * J[1][1] * J[1][2], Sx * J[0][2] * J[0][2] + Sy * J[1][2] * J[1][2],

@@ -20,7 +20,7 @@ struct LinArgs {
   const void* rt64;              // RayTab<double>[n_lm]
   const double2* seg_base;       // [n_seg] base observation; records hold obs - base (real)
   double u, v, fs2, inv_fs2;
-  void* seg_ug;                  // [n_seg][12] real: U (6) | g_pose (3) | 0 0 0
+  void* ug_slot;                 // [n_slot][12] real: U (6) | g_pose (3) | 0 0 0 (dense slots)
   void* w_slot;                  // [n_slot][8] real: W (6) | 0 0 at slot toff_l + frame - first_l
   const int4* lm_meta;           // [n_lm] {first frame, last frame, slot offset, 0}
   double* lm_out;                // [n_lm][8]
@@ -34,15 +34,13 @@ struct SchurArgs {
   const int4* items;              // [n_items] {f1b, chunk, list begin, list end}
   const int4* groups;             // [n_groups] per tile {f1b, chunk, first item, end item}
   const int4* item_lm;            // item landmark lists: {landmark, first frame, last frame, slot offset}
-  const int32_t* frame_seg_begin; // [n_pose+1]
-  const int4* frame_seg_info;     // [n_seg] frame CSR entries {segment, landmark, W slot, 0}
   const int32_t* frame_win_hi;    // [n_pose]
-  const void* seg_ug;             // [n_seg][12] real: U | g_pose
+  const void* ug_slot;            // [n_slot][12] real: U (6) | g_pose (3) | 0 (dense slots)
   const void* w_slot;             // [n_slot][8] real: W | 0 0 (dense landmark x frame slots)
   const double* lm_aux;           // [n_lm][8]
   const int32_t* frame_pos;       // [n_pose] system row of the frame's pan (-1: fixed)
   double* part;                   // [n_items][SCHUR_F1][9][64] split partials
-  double* fdiag;                  // [n_pose][12] U (6) | g_pose (3) | sum W V~^-1 g (3)
+  double* part_diag;              // [n_items][SCHUR_F1][12] chunk-0 splits: U | g_pose | sum W V~^-1 g
   double* S;                      // [ld][ld] lower, row-major
   double* b;                      // [n_sys]
   double* g_pose;                 // [n_sys]

@@ -10,10 +10,9 @@ namespace ptzba {
 // ------------------------------------------------------------------------------------------------
 // K2: reduced camera system  S = U - sum_l W_l V~_l^-1 W_l^T   (damping added after the exchange),
 //                            b = -g_pose + sum_l W_l V~_l^-1 g_l
-// Three launches:
-//   k_frame_diag   one workgroup per free frame: U, g_pose and sum_l W V~^-1 g_l over the frame's
-//                  segments (frame CSR) -> fdiag[f][12];
-//   k_schur        the coupling blocks, register-blocked with LDS-staged operands (below);
+// Two launches:
+//   k_schur        the coupling blocks, register-blocked with LDS-staged operands (below); chunk-0
+//                  items also sum the diagonal terms (U, g_pose, W V~^-1 g) of their frames;
 //   k_schur_reduce sums the split partials of each tile, adds U on the diagonal, writes S (lower
 //                  triangle, system order) and b | g_pose | diag U.
 // k_schur work item = (tile: block F1 of 32 consecutive free frames x chunk of 64 partner frames,
@@ -60,43 +59,6 @@ __device__ __forceinline__ void load_w6(real (&x)[6], const real* __restrict__ p
   }
 }
 
-// one 256-thread workgroup per free frame; frame_seg_info[e] = {segment, landmark, W slot, 0}
-template <typename real>
-__global__ __launch_bounds__(256) void k_frame_diag(SchurArgs a, int n_fixed) {
-  __shared__ double red[4][12];
-  const int f = n_fixed + blockIdx.x;
-  const int lane = lane_id(), wv = threadIdx.x >> 6;
-  const real* __restrict__ seg_ug = (const real*)a.seg_ug;
-  const real* __restrict__ w_slot = (const real*)a.w_slot;
-  double acc[12];
-#pragma unroll
-  for (int k = 0; k < 12; ++k) acc[k] = 0;
-  const int e1 = a.frame_seg_begin[f + 1];
-#pragma unroll 2
-  for (int e = a.frame_seg_begin[f] + threadIdx.x; e < e1; e += 256) {
-    const int4 m = a.frame_seg_info[e];
-    const real* u = seg_ug + (int64_t)m.x * 12;
-    const double* vi = a.lm_aux + (int64_t)m.y * 8;
-    real w[6];
-    load_w6(w, w_slot + (int64_t)m.z * 8);
-#pragma unroll
-    for (int k = 0; k < 9; ++k) acc[k] += (double)u[k];
-    const double vg0 = vi[3], vg1 = vi[4];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) acc[9 + q] += (double)w[2 * q] * vg0 + (double)w[2 * q + 1] * vg1;
-  }
-#pragma unroll
-  for (int k = 0; k < 12; ++k) {
-    const double v = wave_sum(acc[k]);
-    if (lane == 0) red[wv][k] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x < 12) {
-    const int k = threadIdx.x;
-    a.fdiag[(int64_t)f * 12 + k] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
-  }
-}
-
 template <typename real>
 __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
   // fp64 (parity path) stages half as many landmarks per batch to stay inside 160 KiB of LDS
@@ -113,6 +75,48 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
   const real* __restrict__ w_slot = (const real*)a.w_slot;
   for (int k = t; k < nl; k += 512) sL[k] = a.item_lm[lb + k];
   __syncthreads();
+
+  if (chunk == 0) {
+    // diagonal terms of the F1 frames over this split's landmarks: U, g_pose and W V~^-1 g, read from
+    // the dense slots (thread = (landmark j0 + 16 k, frame i): consecutive threads, consecutive slots)
+    const real* __restrict__ ug_slot = (const real*)a.ug_slot;
+    const int i = t & (SF - 1), f = f1b + i;
+    double acc[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) acc[k] = 0;
+#pragma unroll 2
+    for (int j = t >> 5; j < nl; j += 512 / SF) {
+      const int4 m = sL[j];
+      const bool in = f >= m.y && f <= m.z;
+      const int64_t slot = m.w + min(max(f - m.y, 0), m.z - m.y);
+      real u[12], w[6];
+      load_w6(w, w_slot + slot * 8);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const auto v4 = reinterpret_cast<const typename std::conditional<sizeof(real) == 4, float4, double4>::type*>(
+            ug_slot + slot * 12)[k];
+        u[4 * k] = v4.x; u[4 * k + 1] = v4.y; u[4 * k + 2] = v4.z; u[4 * k + 3] = v4.w;
+      }
+      const double* vi = a.lm_aux + (int64_t)m.x * 8;
+      const double vg0 = vi[3], vg1 = vi[4];
+      if (in) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) acc[k] += (double)u[k];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) acc[9 + q] += (double)w[2 * q] * vg0 + (double)w[2 * q + 1] * vg1;
+      }
+    }
+    double* red = reinterpret_cast<double*>(&sW[0][0][0][0]);  // [16][SF][12], free until staging
+#pragma unroll
+    for (int k = 0; k < 12; ++k) red[t * 12 + k] = acc[k];
+    __syncthreads();
+    if (t < SF * 12) {
+      double v = 0;
+      for (int j0 = 0; j0 < 512 / SF; ++j0) v += red[j0 * SF * 12 + t];
+      a.part_diag[(int64_t)item * SF * 12 + t] = v;
+    }
+    __syncthreads();
+  }
 
   // ---- staging registers: W slots (e = t, t + 512 over [SNB][64]) and one Y pair (j = t / SF, i = t % SF;
   // fp64: threads >= SNB*SF repeat a pair and do not stage it).  Branch-free, so the loads stay in flight
@@ -238,9 +242,9 @@ __global__ __launch_bounds__(256) void k_schur_reduce(SchurArgs a) {
       v += p0; v += p1; v += p2; v += p3;
     }
     for (; it < g.w; ++it) v += p[(int64_t)it * NE];
-    if (f2 == f1) {
+    if (f2 == f1) {  // chunk 0: U of the frame, summed over the tile's splits
       const int ui = q <= r ? (q == 0 ? r : (q == 1 ? 2 + r : 5)) : (r == 0 ? q : (r == 1 ? 2 + q : 5));
-      v += a.fdiag[(int64_t)f1 * 12 + ui];
+      for (int it2 = g.z; it2 < g.w; ++it2) v += a.part_diag[((int64_t)it2 * SF + i) * 12 + ui];
     }
     const int64_t ld = a.ld, col0 = a.frame_pos[f1], pf2 = a.frame_pos[f2];
     if (pf2 >= col0) a.S[(pf2 + r) * ld + col0 + q] = v;
@@ -249,7 +253,10 @@ __global__ __launch_bounds__(256) void k_schur_reduce(SchurArgs a) {
   if (chunk == 0 && blockIdx.x == 0 && threadIdx.x < SF * 3) {
     const int i2 = threadIdx.x / 3, q2 = threadIdx.x - 3 * i2, f = f1b + i2;
     if (f < a.n_pose) {
-      const double* d = a.fdiag + (int64_t)f * 12;
+      double d[12];
+      for (int k = 0; k < 12; ++k) d[k] = 0;
+      for (int it2 = g.z; it2 < g.w; ++it2)
+        for (int k = 0; k < 12; ++k) d[k] += a.part_diag[((int64_t)it2 * SF + i2) * 12 + k];
       const int c0 = a.frame_pos[f];
       a.b[c0 + q2] = -d[6 + q2] + d[9 + q2];
       a.g_pose[c0 + q2] = d[6 + q2];
@@ -262,7 +269,6 @@ template <typename real>
 void launch_schur(const SchurArgs& a, int n_items, int n_groups, int n_fixed, hipStream_t st) {
   const int n_free = a.n_pose - n_fixed;
   if (n_free <= 0) return;
-  hipLaunchKernelGGL(k_frame_diag<real>, dim3(n_free), dim3(256), 0, st, a, n_fixed);
   if (n_items > 0) hipLaunchKernelGGL(k_schur<real>, dim3(n_items), dim3(512), 0, st, a);
   if (n_groups > 0) hipLaunchKernelGGL(k_schur_reduce, dim3(SF * 9 * WAVE / 256, n_groups), dim3(256), 0, st, a);
 }
