@@ -63,11 +63,12 @@ struct ptzba_ctx {
   DBuf scal, loc, info;
   DBuf scal_pack;               // device block [scal 8 | loc 8 | info]
   double* scal_host = nullptr;   // pinned host copy of scal_pack
-  DBuf chol_tasks, Ldiag, dpose;
+  DBuf chol_tasks, Ldiag, Minv, dpose;  // Minv: inverses of the diagonal factor tiles (back-substitution)
   std::vector<int> chol_task_off;  // host: per elimination level, offsets into chol_tasks
   int chol_levels = 0, n_aug = 0, n_chain = 1;
   bool nested = false;
-  DBuf frame_pos, row_pad, bs_chain_off, bs_chain_cols, bs_col_off, bs_col_tiles;
+  DBuf frame_pos, row_pad, bs_chain_off, bs_chain_cols, bs_upd_off, bs_upd_tiles;
+  int bs_nupd = 0, bs_npos = 0;
   DBuf xtiles, xbuf;  // packed exchange: tile list, buffer
   int n_xtiles = 0;
   double lambda = 0;
@@ -241,7 +242,7 @@ static bool nested_order(int n_pose, int nf, const std::vector<int32_t>& win, Sy
 struct CholPlan {
   std::vector<int32_t> tasks;  // int4 records
   std::vector<int> level_off;
-  std::vector<int> chain_off, chain_cols, col_off, col_tiles;
+  std::vector<int> chain_off, chain_cols, upd_off, upd_tiles;
   std::vector<int32_t> xtiles;  // (ti, tj) pairs the Schur kernel can write (before fill), for the exchange
   int n_levels = 0;
 };
@@ -330,17 +331,9 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
   }
   P.level_off[nL] = (int)(P.tasks.size() / 4);
   P.n_levels = nL;
-  // back-substitution: tile columns holding unknowns, their nonzero row tiles, chains
+  // back-substitution: chains of tile columns holding unknowns and, per chain position, the chain's
+  // later columns coupled to that row tile (right-looking updates)
   const int Tx = (o.n_aug + CHOL_NB - 1) / CHOL_NB;
-  P.col_off.assign(T + 1, 0);
-  P.col_tiles.clear();
-  for (int kt = 0; kt < T; ++kt) {
-    P.col_off[kt] = (int)P.col_tiles.size();
-    if (kt < Tx)
-      for (int i = kt + 1; i < Tx; ++i)
-        if (nz[i][kt]) P.col_tiles.push_back(i);
-  }
-  P.col_off[T] = (int)P.col_tiles.size();
   P.chain_off.assign(1, 0);
   P.chain_cols.clear();
   if (o.nested) {
@@ -354,6 +347,18 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
   } else {
     for (int kt = Tx - 1; kt >= 0; --kt) P.chain_cols.push_back(kt);
     P.chain_off.push_back((int)P.chain_cols.size());
+  }
+  P.upd_off.assign(1, 0);
+  P.upd_tiles.clear();
+  for (size_t ch = 0; ch + 1 < P.chain_off.size(); ++ch) {
+    std::vector<uint8_t> in_chain(T, 0);
+    for (int q = P.chain_off[ch]; q < P.chain_off[ch + 1]; ++q) in_chain[P.chain_cols[q]] = 1;
+    for (int q = P.chain_off[ch]; q < P.chain_off[ch + 1]; ++q) {
+      const int kt = P.chain_cols[q];
+      for (int j = 0; j < kt; ++j)
+        if (in_chain[j] && nz[kt][j]) P.upd_tiles.push_back(j);
+      P.upd_off.push_back((int)P.upd_tiles.size());
+    }
   }
   return true;
 }
@@ -587,15 +592,21 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       h->lm_out[1].alloc((size_t)n_landmark * 8 * 8) || h->lm_aux.alloc((size_t)n_landmark * 8 * 8) ||
       h->lm_red.alloc((size_t)n_landmark * 4 * 8) || h->sys.alloc((size_t)h->sys_count() * 8) ||
       h->scal.alloc(PTZBA_NSCALARS * 8) || h->red_scratch.alloc(RED_SCRATCH * 8) || h->loc.alloc(PTZBA_NSCALARS * 8) || h->info.alloc(16) ||
-      h->Ldiag.alloc((size_t)h->ld * CHOL_NB * 8) || h->dpose.alloc((size_t)h->ld * 8) ||
+      h->Ldiag.alloc((size_t)h->ld * CHOL_NB * 8) || h->Minv.alloc((size_t)h->ld * CHOL_NB * 8) ||
+      h->dpose.alloc((size_t)h->ld * 8) ||
       h->s2_part.alloc((size_t)std::max(h->n_s2_items, 1) * SCHUR_F1 * 9 * WAVE * 8) ||
       h->part_diag.alloc((size_t)std::max(h->n_s2_items, 1) * SCHUR_F1 * 12 * 8))
     return -1;
   if (upload(h->chol_tasks, plan.tasks) || upload(h->frame_pos, sorder.pos) || upload(h->row_pad, sorder.pad) ||
       upload(h->bs_chain_off, plan.chain_off) || upload(h->bs_chain_cols, plan.chain_cols) ||
-      upload(h->bs_col_off, plan.col_off) || upload(h->bs_col_tiles, plan.col_tiles) || upload(h->xtiles, plan.xtiles))
+      upload(h->bs_upd_off, plan.upd_off) || upload(h->bs_upd_tiles, plan.upd_tiles) || upload(h->xtiles, plan.xtiles))
     return -1;
   h->n_xtiles = (int)(plan.xtiles.size() / 2);
+  h->bs_nupd = (int)plan.upd_tiles.size();
+  h->bs_npos = (int)plan.chain_cols.size();
+  // the back-substitution keeps r and its update lists in LDS (plus ~9 KiB of static staging)
+  if (h->ld * 8 + (h->bs_npos + 1 + h->bs_nupd) * 4 > 150 * 1024)
+    return fail("reduced system %d too large for the dense solver's back-substitution", h->n_sys);
   h->xbuf.release();  // allocated on first ptzba_exchange_packed
   HIPCHK(hipMemset(h->D_pose.p, 0, h->D_pose.bytes));
   HIPCHK(hipMemset(h->D_ray.p, 0, h->D_ray.bytes));
@@ -793,9 +804,9 @@ int ptzba_solve_reduced(ptzba_handle h) {
   launch_chol_prepare(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(), h->st);
   launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
                   h->Ldiag.as<double>(), h->info.as<int>(), h->st);
-  launch_chol_backsolve(h->S(), h->ld, h->n_aug, h->n_chain, h->bs_chain_off.as<int>(), h->bs_chain_cols.as<int>(),
-                        h->bs_col_off.as<int>(), h->bs_col_tiles.as<int>(), h->Ldiag.as<double>(), h->dpose.as<double>(),
-                        h->st);
+  launch_chol_backsolve(h->S(), h->ld, h->n_aug, h->n_chain, h->bs_npos, h->bs_chain_off.as<int>(),
+                        h->bs_chain_cols.as<int>(), h->bs_upd_off.as<int>(), h->bs_upd_tiles.as<int>(), h->bs_nupd,
+                        h->Ldiag.as<double>(), h->Minv.as<double>(), h->dpose.as<double>(), h->st);
   tm_end(h, TM_CHOL);
   HIPCHK(hipGetLastError());
   tm_begin(h, TM_BACK);

@@ -19,7 +19,7 @@
 // column j's panel tasks when j is factored at that very level.  Only structurally nonzero tiles
 // (symbolic fill on the tile graph) are visited.
 // Back substitution L^T x = y: one 1024-thread workgroup per chain of tile columns (nested
-// dissection: C then A, C then B), dot products over each column's nonzero row tiles.
+// dissection: C then A, C then B), right-looking updates of an LDS-resident right-hand side.
 #include "ptzba_common.h"
 #include "ptzba_kernels.h"
 
@@ -306,68 +306,155 @@ void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_o
 }
 
 // ---------------------------------------------------------------------------------------------
+// inverses of the diagonal factor tiles: M_kt = L_kt,kt^-1 (lower), row-major [kt][32][32].  One wave
+// per tile: lane j computes column j by forward substitution against e_j (row i of L broadcast from LDS).
+__global__ __launch_bounds__(64) void k_tile_inv(const double* __restrict__ Ldiag, double* __restrict__ Minv) {
+  __shared__ double Lt[NB][NB + 1];
+  const int kt = blockIdx.x, lane = threadIdx.x, j = lane & (NB - 1);
+  const double* src = Ldiag + (int64_t)kt * NB * NB;
+  for (int e = lane; e < NB * NB; e += WAVE) Lt[e >> 5][e & 31] = src[e];
+  __syncthreads();
+  double m[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    double sacc = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < i; ++k) sacc = fma(-Lt[i][k], m[k], sacc);  // m[k] = 0 for k < j
+    m[i] = (i >= j) ? sacc * rcp_nr(Lt[i][i]) : 0.0;
+  }
+  if (lane < NB) {
+    double* dst = Minv + (int64_t)kt * NB * NB + lane;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) dst[i * NB] = m[i];
+  }
+}
+
 // back substitution L^T x = y with y = row n of the factor; x written to xout[0..n).  Workgroup c
-// walks chain c (tile columns in processing order); column kt's dot products run over its nonzero row
-// tiles col_tiles[col_off[kt] .. col_off[kt+1]) (all below kt).  Chains that share tile columns
-// (the nested-dissection separator) compute them identically.
+// walks chain c (tile columns in processing order, descending; nested dissection: C then A, C then B;
+// chains compute shared columns identically), right-looking: the running right-hand side r (init y)
+// lives in LDS; per column kt one wave forms x_kt = M_kt^T r_kt (32-term dot products, no serial
+// chain), then the waves apply x_kt to the chain's later columns coupled to row tile kt
+// (r_j -= L_kt,j^T x_kt; wave = update tile, lane = (column, row half)).  The next column's L values, update tiles
+// only, and M column do not depend on x: they are loaded into registers right after this column's
+// update, in flight during the next column's barrier and solve.  upd_off / upd_tiles (per chain
+// position) list the update tiles; more than 32 load directly.
+#ifdef BS_TIMING
+__device__ long long g_bs_stamps[2][128][6];
+__device__ long long g_bs_edges[2][4];
+#define BS_STAMP(k) do { if (threadIdx.x == 0 && q - q0 < 128) g_bs_stamps[blockIdx.x & 1][q - q0][k] = clock64(); } while (0)
+#else
+#define BS_STAMP(k) do { } while (0)
+#endif
 __global__ __launch_bounds__(1024) void k_chol_backsolve(const double* __restrict__ L, int64_t ld, int n,
                                                          const int* __restrict__ chain_off,
                                                          const int* __restrict__ chain_cols,
-                                                         const int* __restrict__ col_off,
-                                                         const int* __restrict__ col_tiles,
-                                                         const double* __restrict__ Ldiag, double* __restrict__ xout) {
-  extern __shared__ __attribute__((aligned(16))) double xv[];  // [ld]
-  __shared__ double part[32][NB + 1];
-  __shared__ double Lkk[NB][NB + 1];
+                                                         const int* __restrict__ upd_off,
+                                                         const int* __restrict__ upd_tiles, int n_upd,
+                                                         const double* __restrict__ Ldiag,
+                                                         const double* __restrict__ Minv, double* __restrict__ xout) {
+  extern __shared__ __attribute__((aligned(16))) double xv[];  // [ld] | upd_off [nq+1] | upd_tiles [n_upd] (int)
+  __shared__ double sM[NB][NB + 1];
+#ifdef BS_TIMING
+  if (threadIdx.x == 0) g_bs_edges[blockIdx.x & 1][0] = clock64();
+#endif
+  const int nq = chain_off[gridDim.x];
+  int* s_uoff = reinterpret_cast<int*>(xv + ld);
+  int* s_ut = s_uoff + nq + 1;
   const int t = threadIdx.x;
-  const int c = t & 31, sub = t >> 5;
+  const int c = t & 31, u = t >> 5, wv = t >> 6;
   // y = row n of the factor: off-diagonal tiles in place, the tile holding row n in Ldiag
   const int tn = n / NB, rn = n - tn * NB;
   for (int i = t; i < ld; i += blockDim.x)
     xv[i] = (i >= n) ? 0.0 : (i < tn * NB ? L[(int64_t)n * ld + i] : Ldiag[((int64_t)tn * NB + rn) * NB + (i - tn * NB)]);
+  for (int i = t; i <= nq; i += blockDim.x) s_uoff[i] = upd_off[i];
+  for (int i = t; i < n_upd; i += blockDim.x) s_ut[i] = upd_tiles[i];
   __syncthreads();
   const int q0 = chain_off[blockIdx.x], q1 = chain_off[blockIdx.x + 1];
+  // wave w updates tiles w and w + 16 of the row's list; lane = (column c, row half h)
+  const int h = (t >> 5) & 1;
+  double pv[2][NB / 2];  // rows h*16 .. h*16+15 of the two update tiles, column c
+  double md;             // element t of M_kt (row-major), staged to LDS for the solve
+  auto prefetch = [&](int q) {
+    const int qq = min(q, q1 - 1), kt = chain_cols[qq];
+    const int e0 = s_uoff[qq], nu = s_uoff[qq + 1] - e0;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      // waves whose tile is past the list skip the loads (wave-uniform branch); kept values are never read
+      if (__builtin_amdgcn_readfirstlane(wv + 16 * p) < nu) {
+        const int jt = s_ut[e0 + wv + 16 * p];
+        const double* src = L + ((int64_t)kt * NB + h * (NB / 2)) * ld + (int64_t)jt * NB + c;
+#pragma unroll
+        for (int i = 0; i < NB / 2; ++i) pv[p][i] = src[(int64_t)i * ld];
+      }
+    }
+    md = Minv[(int64_t)kt * NB * NB + t];
+  };
+#ifdef BS_TIMING
+  if (threadIdx.x == 0) g_bs_edges[blockIdx.x & 1][1] = clock64();
+#endif
+  prefetch(q0);
   for (int q = q0; q < q1; ++q) {
     const int kt = chain_cols[q];
     const int64_t c0 = (int64_t)kt * NB;
-    Lkk[t >> 5][t & 31] = Ldiag[(int64_t)kt * NB * NB + t];
-    double s = 0;
-    const int e0 = col_off[kt], nrow = (col_off[kt + 1] - e0) * NB;
-#pragma unroll 4
-    for (int rr = sub; rr < nrow; rr += 32) {
-      const int64_t i = (int64_t)col_tiles[e0 + (rr >> 5)] * NB + (rr & 31);
-      s += L[i * ld + c0 + c] * xv[i];
-    }
-    part[sub][c] = s;
-    __syncthreads();
-    if (t < WAVE) {
-      const int lane = t;
-      double tr = 0;
-      if (lane < NB) {
-        for (int qq = 0; qq < 32; ++qq) tr += part[qq][lane];
-        tr = xv[c0 + lane] - tr;
-      }
-      // upper-triangular solve L_kk^T x = tr, lane r holds tr_r
-      const double rd = lane < NB ? rcp_nr(Lkk[lane][lane]) : 0.0;
+    BS_STAMP(0);
+    sM[t >> 5][t & 31] = md;
+    __syncthreads();  // M_kt staged; the previous column's updates of r visible
+    BS_STAMP(1);
+    if (t < WAVE) {  // x_kt = M^T r_kt: lane c sums column c of M against r (broadcast reads)
+      double s4[4] = {0, 0, 0, 0};
 #pragma unroll
-      for (int jj = NB - 1; jj >= 0; --jj) {
-        const double tj = bcast(tr, jj) * bcast(rd, jj);
-        if (lane == jj) tr = tj;
-        if (lane < jj) tr -= Lkk[jj][lane] * tj;
-      }
-      if (lane < NB && c0 + lane < n) {
-        xv[c0 + lane] = tr;
-        xout[c0 + lane] = tr;
+      for (int k = 0; k < NB; ++k) s4[k & 3] = fma(sM[k][c], xv[c0 + k], s4[k & 3]);
+      const double x = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+      if (t < NB) {
+        xv[c0 + t] = x;
+        if (c0 + t < n) xout[c0 + t] = x;
       }
     }
-    __syncthreads();
+    BS_STAMP(2);
+    __syncthreads();  // x_kt visible
+    BS_STAMP(3);
+    const int e0 = s_uoff[q], nu = s_uoff[q + 1] - e0;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      if (wv + 16 * p < nu) {  // wave-uniform
+        double s4[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < NB / 2; ++i) s4[i & 3] = fma(pv[p][i], xv[c0 + h * (NB / 2) + i], s4[i & 3]);
+        double sacc = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+        sacc += __shfl_xor(sacc, 32, WAVE);
+        if (h == 0) xv[(int64_t)s_ut[e0 + wv + 16 * p] * NB + c] -= sacc;
+      }
+    }
+    for (int uu = u + 32; uu < nu; uu += 32) {  // rare: rows with more than 32 update tiles
+      const int64_t jc = (int64_t)s_ut[e0 + uu] * NB + c;
+      double sacc = 0;
+#pragma unroll 8
+      for (int i = 0; i < NB; ++i) sacc += L[(c0 + i) * ld + jc] * xv[c0 + i];
+      xv[jc] -= sacc;
+    }
+    BS_STAMP(4);
+    prefetch(q + 1);  // next column's values in flight during its barrier and solve
+    BS_STAMP(5);
   }
+#ifdef BS_TIMING
+  if (threadIdx.x == 0) g_bs_edges[blockIdx.x & 1][2] = clock64();
+#endif
 }
+#ifdef BS_TIMING
+extern "C" int ptzba_debug_bs_stamps(long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bs_stamps), sizeof(g_bs_stamps)) != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(out + 2 * 128 * 6, HIP_SYMBOL(g_bs_edges), sizeof(g_bs_edges)) == hipSuccess ? 0 : -1;
+}
+#endif
 
-void launch_chol_backsolve(const double* L, int64_t ld, int n, int n_chain, const int* chain_off, const int* chain_cols,
-                           const int* col_off, const int* col_tiles, const double* Ldiag, double* xout, hipStream_t st) {
-  hipLaunchKernelGGL(k_chol_backsolve, dim3(n_chain), dim3(1024), (size_t)ld * sizeof(double), st, L, ld, n, chain_off,
-                     chain_cols, col_off, col_tiles, Ldiag, xout);
+void launch_chol_backsolve(const double* L, int64_t ld, int n, int n_chain, int n_pos, const int* chain_off,
+                           const int* chain_cols, const int* upd_off, const int* upd_tiles, int n_upd,
+                           const double* Ldiag, double* Minv, double* xout, hipStream_t st) {
+  const int tx = (n + NB - 1) / NB;
+  hipLaunchKernelGGL(k_tile_inv, dim3(tx), dim3(64), 0, st, Ldiag, Minv);
+  const size_t lds = (size_t)ld * sizeof(double) + (size_t)(n_pos + 1 + n_upd) * sizeof(int);
+  hipLaunchKernelGGL(k_chol_backsolve, dim3(n_chain), dim3(1024), lds, st, L, ld, n, chain_off, chain_cols, upd_off,
+                     upd_tiles, n_upd, Ldiag, Minv, xout);
 }
 
 // packed exchange: the lower tiles the Schur kernel can write (xt[k] = (ti, tj)) and the three
