@@ -612,6 +612,8 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   HIPCHK(hipMemset(h->D_ray.p, 0, h->D_ray.bytes));
   HIPCHK(hipMemset(h->w_slot[0].p, 0, h->w_slot[0].bytes));  // slots of unobserved frames stay zero
   HIPCHK(hipMemset(h->w_slot[1].p, 0, h->w_slot[1].bytes));
+  HIPCHK(hipMemset(h->lm_out[0].p, 0, h->lm_out[0].bytes));  // landmarks without records keep zero rows
+  HIPCHK(hipMemset(h->lm_out[1].p, 0, h->lm_out[1].bytes));
   HIPCHK(hipMemset(h->ug_slot[0].p, 0, h->ug_slot[0].bytes));
   HIPCHK(hipMemset(h->ug_slot[1].p, 0, h->ug_slot[1].bytes));
   HIPCHK(hipMemset(h->ptz.p, 0, h->ptz.bytes));
@@ -680,8 +682,6 @@ static void linearize_into(ptzba_ctx* h, int slot) {
   a.w_slot = h->w_slot[slot].p;
   a.lm_meta = h->lm_meta.as<int4>();
   a.lm_out = h->lm_out[slot].as<double>();
-  // landmarks without records keep zero rows
-  (void)hipMemsetAsync(h->lm_out[slot].p, 0, h->lm_out[slot].bytes, h->st);
   tm_begin(h, TM_K1);
   if (h->precision == PTZBA_FP32)
     launch_linearize<float>(a, h->loss, h->st);

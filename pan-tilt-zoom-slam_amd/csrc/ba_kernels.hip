@@ -510,13 +510,15 @@ __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ 
   }
   __syncthreads();
   if (!last) return;
+  // all partials in parallel (agent-scope loads: other workgroups wrote them), then a fixed-order sum
+  __shared__ double fin[RED_BLOCKS][8];
+  for (int e = threadIdx.x; e < (int)gridDim.x * 8; e += blockDim.x)
+    fin[e >> 3][e & 7] = __hip_atomic_load(partial + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
   if (threadIdx.x < nk) {
     const int k = threadIdx.x;
     double s = 0;
-    for (int b = 0; b < (int)gridDim.x; ++b) {
-      const double x = __hip_atomic_load(partial + b * 8 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s = (maxmask & (1 << k)) ? fmax(s, x) : s + x;
-    }
+    for (int b = 0; b < (int)gridDim.x; ++b) s = (maxmask & (1 << k)) ? fmax(s, fin[b][k]) : s + fin[b][k];
     out[k] = s;
   }
   if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

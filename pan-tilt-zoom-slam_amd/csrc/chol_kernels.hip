@@ -200,6 +200,13 @@ __device__ __forceinline__ void wave_potrf_trsm32(double (*D)[NB + 1], double (*
   wave_lds_fence();
 }
 
+#ifdef CS_TIMING
+__device__ long long g_cs_stamps[64][6];
+__device__ int g_cs_level;
+#define CS_STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x == 0 && cs_lvl < 64) g_cs_stamps[cs_lvl][k] = clock64(); } while (0)
+#else
+#define CS_STAMP(k) do { } while (0)
+#endif
 __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64_t ld,
                                                    const int4* __restrict__ tasks, double* __restrict__ Ldiag,
                                                    int* info) {
@@ -215,6 +222,11 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   const int up1 = ((tk.w >> 14) & 0x3fff) - 1;
   const int tmask = (tk.w >> 28) & 3;  // panel: which updates also apply to T
   const int64_t NBl = NB;
+#ifdef CS_TIMING
+  const int cs_lvl = g_cs_level;
+  if (threadIdx.x == 0 && blockIdx.x == 0 && cs_lvl < 64) g_cs_stamps[cs_lvl][5] = type;
+#endif
+  CS_STAMP(0);
 #ifndef CHOL_VARIANT
 #define CHOL_VARIANT 0
 #endif
@@ -271,6 +283,7 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   if (up1 >= 0) put_tile(sB[1], v4);
   if (updT1 && up1 >= 0) put_tile(sA[1], v5);
   __syncthreads();
+  CS_STAMP(1);
 #if CHOL_VARIANT != 4
   if (up0 >= 0) {
     tile_gemm_nt_sub(sD, sB[0], sB[0]);
@@ -282,10 +295,18 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   }
 #endif
   __syncthreads();
+  CS_STAMP(2);
 #if CHOL_VARIANT != 1
   if (threadIdx.x < WAVE) wave_potrf_trsm32(sD, diag_only ? nullptr : sC, rdg, cb, info);
 #endif
   __syncthreads();
+  CS_STAMP(3);
+#ifdef CS_TIMING
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    CS_STAMP(4);
+    g_cs_level = cs_lvl + 1;
+  }
+#endif
   if (diag_only) {
     // A_kk itself stays untouched: other panel workgroups of this launch are still reading it
     double* C = Ldiag + (int64_t)k * NB * NB;
@@ -440,6 +461,13 @@ __global__ __launch_bounds__(1024) void k_chol_backsolve(const double* __restric
   if (threadIdx.x == 0) g_bs_edges[blockIdx.x & 1][2] = clock64();
 #endif
 }
+#ifdef CS_TIMING
+extern "C" int ptzba_debug_cs_stamps(long long* out) {
+  const int zero = 0;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cs_stamps), sizeof(g_cs_stamps)) != hipSuccess) return -1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_cs_level), &zero, sizeof(int)) == hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef BS_TIMING
 extern "C" int ptzba_debug_bs_stamps(long long* out) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bs_stamps), sizeof(g_bs_stamps)) != hipSuccess) return -1;
