@@ -200,6 +200,86 @@ __device__ __forceinline__ void wave_potrf_trsm32(double (*D)[NB + 1], double (*
   wave_lds_fence();
 }
 
+// Workgroup form of the same factorisation (256 threads = 4 waves): rows in lanes as above (lanes 0..31
+// rows of D, 32..63 rows of T), the 32 columns split over the 4 waves (wave w keeps columns w + 4 i in
+// registers).  Pivot blocks of 8: the waves publish the block's 8 columns to LDS, wave 0 eliminates
+// inside the block (pivot values by v_readlane) and publishes the multipliers, then every wave applies
+// the rank-8 update to its own columns (the pivot-column values broadcast from LDS).  The trailing
+// update -- most of the FMAs -- runs on four SIMDs instead of one.
+constexpr int WB = 8;
+#ifndef CHOL_WG
+#define CHOL_WG 1  // 1: workgroup potrf+trsm (4 waves), 0: single-wave sweep
+#endif
+__device__ __forceinline__ void wg_potrf_trsm32(double (*D)[NB + 1], double (*T)[NB + 1], double* rdg,
+                                                double (*pan)[WB + 1], double (*mul)[WB + 1], double* dg, int* info) {
+  const int w = threadIdx.x >> 6, lane = lane_id();
+  const bool isT = lane >= NB;
+  const int r = lane & (NB - 1);
+  const bool have = !isT || T != nullptr;
+  double col[NB / 4];
+#pragma unroll
+  for (int i = 0; i < NB / 4; ++i) col[i] = have ? (isT ? T[r][w + 4 * i] : D[r][w + 4 * i]) : 0.0;
+  bool bad = false;
+#pragma unroll
+  for (int kb = 0; kb < NB; kb += WB) {
+    pan[lane][w] = col[kb / 4];
+    pan[lane][4 + w] = col[kb / 4 + 1];
+    __syncthreads();
+    if (w == 0) {
+      double v[WB], mu[WB];
+#pragma unroll
+      for (int k = 0; k < WB; ++k) v[k] = pan[lane][k];
+#pragma unroll
+      for (int j = 0; j < WB; ++j) {
+        double d = bcast(v[j], kb + j);
+        if (!(d > 0.0)) {
+          bad = true;
+          d = 1e-300;
+        }
+        if (lane == 0) dg[kb + j] = d;
+        mu[j] = v[j] * rcp_nr(d);
+#pragma unroll
+        for (int m = j + 1; m < WB; ++m) v[m] -= mu[j] * bcast(v[j], kb + m);
+      }
+#pragma unroll
+      for (int k = 0; k < WB; ++k) {
+        pan[lane][k] = v[k];
+        mul[lane][k] = mu[k];
+      }
+    }
+    __syncthreads();
+    col[kb / 4] = pan[lane][w];
+    col[kb / 4 + 1] = pan[lane][4 + w];
+    if (kb + WB < NB) {
+      double mu[WB];
+#pragma unroll
+      for (int k = 0; k < WB; ++k) mu[k] = mul[lane][k];
+#pragma unroll
+      for (int i = kb / 4 + 2; i < NB / 4; ++i) {
+        const int m = w + 4 * i;
+        double sacc = col[i];
+#pragma unroll
+        for (int k = 0; k < WB; ++k) sacc = fma(-mu[k], pan[m][k], sacc);
+        col[i] = sacc;
+      }
+      __syncthreads();  // pan / mul are rewritten by the next block
+    }
+  }
+  if (bad && lane == 0) atomicOr(info, 1);
+  if (threadIdx.x < NB) rdg[threadIdx.x] = rsq_nr(dg[threadIdx.x]);
+  __syncthreads();
+  if (have) {
+#pragma unroll
+    for (int i = 0; i < NB / 4; ++i) {
+      const int m = w + 4 * i;
+      const double val = col[i] * rdg[m];
+      if (isT) T[r][m] = val;
+      else D[r][m] = (m <= r) ? val : 0.0;
+    }
+  }
+  __syncthreads();
+}
+
 #ifdef CS_TIMING
 __device__ long long g_cs_stamps[64][6];
 __device__ int g_cs_level;
@@ -215,7 +295,12 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   __shared__ double sA[2][NB][NB + 1];  // L_ip of the two update panels
   __shared__ double sB[2][NB][NB + 1];  // L_kp or L_jp of the two update panels
   __shared__ double rdg[NB];
+#if !CHOL_WG
   __shared__ __attribute__((aligned(16))) double cb[NB][PB];  // potrf block columns (broadcast reads)
+#endif
+#if CHOL_WG
+  __shared__ double s_pan[2 * NB][WB + 1], s_mul[2 * NB][WB + 1], s_dg[NB];
+#endif
   const int4 tk = tasks[blockIdx.x];
   const int type = tk.x, i = tk.y, j = tk.z;
   const int up0 = (tk.w & 0x3fff) - 1;
@@ -297,7 +382,11 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   __syncthreads();
   CS_STAMP(2);
 #if CHOL_VARIANT != 1
+#if CHOL_WG
+  wg_potrf_trsm32(sD, diag_only ? nullptr : sC, rdg, s_pan, s_mul, s_dg, info);
+#else
   if (threadIdx.x < WAVE) wave_potrf_trsm32(sD, diag_only ? nullptr : sC, rdg, cb, info);
+#endif
 #endif
   __syncthreads();
   CS_STAMP(3);
