@@ -114,6 +114,28 @@ PTZBA_EXPORT int ptzba_get_state(ptzba_handle h, double* ptz, double* rays);
 PTZBA_EXPORT int ptzba_linearize(ptzba_handle h);
 PTZBA_EXPORT int ptzba_build_reduced(ptzba_handle h, double lambda);
 PTZBA_EXPORT int ptzba_solve_reduced(ptzba_handle h);
+/* Device-driven Levenberg-Marquardt: the accept/reject decisions, damping update and termination
+ * tests of the host loop (ptzba.LMSolver; scipy common.py:705-718 rules) run on the device, so trials
+ * queue back to back.  Sequence: lm_start (linearise at the current state) [all-reduce scalars];
+ * lm_init; then per trial k: lm_build [all-reduce system]; lm_solve [all-reduce scalars];
+ * lm_decide(k).  lm_wait(k) blocks until trial k's decision is on the host (a ring of 4 records: wait
+ * for trial k before deciding trial k + 4).  Enqueueing trial k + 1's build before waiting for trial k
+ * hides the host round trip; a build after the final decision is harmless. */
+typedef struct {
+  double ftol, xtol, gtol;                    /* scipy's ftol/xtol/gtol tests (gtol <= 0: off) */
+  double lambda0, min_lambda, max_lambda;     /* Marquardt damping: start, floor, give-up bound */
+  int32_t max_iter, max_retries, gauss_newton; /* accepted iterations; rejections in a row; lambda0 = 0 GN */
+} ptzba_lm_opts;
+typedef struct {
+  double cost, initial_cost, lambda;
+  int32_t iterations, nfev, trials, retries, status, done, accepted;  /* status: 0 max_iter, 1 gtol, 2 ftol, 3 xtol, -1 failed */
+} ptzba_lm_record;
+PTZBA_EXPORT int ptzba_lm_start(ptzba_handle h);
+PTZBA_EXPORT int ptzba_lm_init(ptzba_handle h, const ptzba_lm_opts* opts);
+PTZBA_EXPORT int ptzba_lm_build(ptzba_handle h);
+PTZBA_EXPORT int ptzba_lm_solve(ptzba_handle h);
+PTZBA_EXPORT int ptzba_lm_decide(ptzba_handle h, int trial);
+PTZBA_EXPORT int ptzba_lm_wait(ptzba_handle h, int trial, ptzba_lm_record* out);
 PTZBA_EXPORT int ptzba_step(ptzba_handle h, double lambda);
 PTZBA_EXPORT int ptzba_read_scalars(ptzba_handle h, double* out /*PTZBA_NSCALARS*/);
 PTZBA_EXPORT int ptzba_accept(ptzba_handle h, int accept);
@@ -129,8 +151,10 @@ PTZBA_EXPORT int ptzba_pack(ptzba_handle h);
 PTZBA_EXPORT int ptzba_unpack(ptzba_handle h);
 /* wait for all queued work of the handle */
 PTZBA_EXPORT int ptzba_sync(ptzba_handle h);
-/* average device time (ms) of the last n launches of the linearisation kernel (K1), measured with
- * HIP events on the handle's stream; count of launches timed */
+/* average device time (ms) per launch of the kernel groups [K1 linearisation, Schur build, Cholesky
+ * solve, back-substitution], measured with HIP events on the handle's stream; launches timed.
+ * reset: `enable` is a bitmask of the groups to time (1 K1, 2 Schur, 4 Cholesky, 8 back-subst.;
+ * 0 off).  Each timed group adds two event records (a few microseconds) per launch. */
 PTZBA_EXPORT int ptzba_kernel_times(ptzba_handle h, double* ms_out /*4*/, int64_t* count_out /*4*/);
 PTZBA_EXPORT int ptzba_reset_kernel_times(ptzba_handle h, int enable);
 

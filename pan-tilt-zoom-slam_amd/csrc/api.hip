@@ -27,6 +27,7 @@ static size_t g_total_bytes(std::initializer_list<const DBuf*> l) {
 }
 
 enum { TM_K1 = 0, TM_SCHUR = 1, TM_CHOL = 2, TM_BACK = 3, TM_N = 4 };
+constexpr int LM_RING = 4;
 constexpr int TM_POOL = 512;
 
 struct ptzba_ctx {
@@ -72,8 +73,12 @@ struct ptzba_ctx {
   DBuf xtiles, xbuf;  // packed exchange: tile list, buffer
   int n_xtiles = 0;
   double lambda = 0;
+  // device-driven LM: state, pinned record ring, events
+  DBuf lmdev;
+  LMDev* lm_host = nullptr;
+  hipEvent_t lm_ev[4] = {nullptr, nullptr, nullptr, nullptr};
   // timing
-  bool timing = false;
+  int timing = 0;  // bitmask of timed kernel groups (1 K1, 2 Schur, 4 Cholesky solve, 8 back-substitution)
   std::vector<hipEvent_t> ev[TM_N];
   int ev_used[TM_N] = {0, 0, 0, 0};
 
@@ -86,11 +91,11 @@ struct ptzba_ctx {
 };
 
 static void tm_begin(ptzba_ctx* h, int k) {
-  if (!h->timing || h->ev_used[k] + 2 > (int)h->ev[k].size()) return;
+  if (!((h->timing >> k) & 1) || h->ev_used[k] + 2 > (int)h->ev[k].size()) return;
   (void)hipEventRecord(h->ev[k][h->ev_used[k]], h->st);
 }
 static void tm_end(ptzba_ctx* h, int k) {
-  if (!h->timing || h->ev_used[k] + 2 > (int)h->ev[k].size()) return;
+  if (!((h->timing >> k) & 1) || h->ev_used[k] + 2 > (int)h->ev[k].size()) return;
   (void)hipEventRecord(h->ev[k][h->ev_used[k] + 1], h->st);
   h->ev_used[k] += 2;
 }
@@ -119,6 +124,9 @@ void ptzba_delete(ptzba_handle h) {
     for (auto e : h->ev[k]) (void)hipEventDestroy(e);
   if (h->own) (void)hipStreamDestroy(h->own);
   if (h->scal_host) (void)hipHostFree(h->scal_host);
+  if (h->lm_host) (void)hipHostFree(h->lm_host);
+  for (auto e : h->lm_ev)
+    if (e) (void)hipEventDestroy(e);
   delete h;
 }
 
@@ -652,14 +660,14 @@ int ptzba_problem_info(ptzba_handle h, int64_t* info) {
 static void* ft_real(ptzba_ctx* h) { return h->precision == PTZBA_FP32 ? h->ft.p : h->ft64.p; }
 static void* rt_real(ptzba_ctx* h) { return h->precision == PTZBA_FP32 ? h->rt.p : h->rt64.p; }
 
-static void tables(ptzba_ctx* h, const double* ptz, const double* rays) {
+static void tables(ptzba_ctx* h, const double* ptz, const double* rays, const int* run_if = nullptr) {
   if (h->precision == PTZBA_FP32)
-    launch_tables<float>(ptz, rays, h->n_pose, h->n_lm, h->ft64.p, h->rt64.p, h->ft.p, h->rt.p, h->st);
+    launch_tables<float>(ptz, rays, h->n_pose, h->n_lm, h->ft64.p, h->rt64.p, h->ft.p, h->rt.p, run_if, h->st);
   else
-    launch_tables<double>(ptz, rays, h->n_pose, h->n_lm, h->ft64.p, h->rt64.p, h->ft64.p, h->rt64.p, h->st);
+    launch_tables<double>(ptz, rays, h->n_pose, h->n_lm, h->ft64.p, h->rt64.p, h->ft64.p, h->rt64.p, run_if, h->st);
 }
 
-static void linearize_into(ptzba_ctx* h, int slot) {
+static void linearize_into(ptzba_ctx* h, int slot, const int* run_if = nullptr) {
   LinArgs a;
   a.lm_work = h->lm_order.as<int4>();
   a.n_work = h->n_work;
@@ -682,12 +690,13 @@ static void linearize_into(ptzba_ctx* h, int slot) {
   a.w_slot = h->w_slot[slot].p;
   a.lm_meta = h->lm_meta.as<int4>();
   a.lm_out = h->lm_out[slot].as<double>();
-  tm_begin(h, TM_K1);
+  a.run_if = run_if;
+  if (!run_if) tm_begin(h, TM_K1);  // conditional re-linearisations are not timed (often no-ops)
   if (h->precision == PTZBA_FP32)
     launch_linearize<float>(a, h->loss, h->st);
   else
     launch_linearize<double>(a, h->loss, h->st);
-  tm_end(h, TM_K1);
+  if (!run_if) tm_end(h, TM_K1);
 }
 
 int ptzba_solver_info(ptzba_handle h, int64_t* info4) {
@@ -757,14 +766,12 @@ int ptzba_linearize(ptzba_handle h) {
   return 0;
 }
 
-int ptzba_build_reduced(ptzba_handle h, double lambda) {
-  if (!h || !h->have_problem) return fail("no problem set");
-  if (!(lambda >= 0) || !std::isfinite(lambda)) return fail("bad lambda");
-  HIPCHK(hipSetDevice(h->device));
-  h->lambda = lambda;
+// reduced camera system at the current linearisation (slot h->cur); lambda from the argument or, in
+// the device-driven LM (lam_dev != nullptr), from device memory
+static int build_impl(ptzba_ctx* h, double lambda, const double* lam_dev, const int* skip_if = nullptr) {
   const int c = h->cur;
   launch_landmark_damp(h->lm_out[c].as<double>(), h->lm_seg_begin.as<int32_t>(), h->D_ray.as<double>(),
-                       h->lm_aux.as<double>(), h->n_lm, lambda, h->st);
+                       h->lm_aux.as<double>(), h->n_lm, lambda, lam_dev, skip_if, h->st);
   HIPCHK(hipMemsetAsync(h->sys.p, 0, h->sys.bytes, h->st));
   SchurArgs a;
   a.items = h->s2_items.as<int4>();
@@ -783,6 +790,7 @@ int ptzba_build_reduced(ptzba_handle h, double lambda) {
   a.dU = h->dU();
   a.ld = h->ld;
   a.n_pose = h->n_pose;
+  a.skip_if = skip_if;
   tm_begin(h, TM_SCHUR);
   if (h->precision == PTZBA_FP32)
     launch_schur<float>(a, h->n_s2_items, h->n_s2_groups, h->n_fixed, h->st);
@@ -793,14 +801,20 @@ int ptzba_build_reduced(ptzba_handle h, double lambda) {
   return 0;
 }
 
-int ptzba_solve_reduced(ptzba_handle h) {
+int ptzba_build_reduced(ptzba_handle h, double lambda) {
   if (!h || !h->have_problem) return fail("no problem set");
+  if (!(lambda >= 0) || !std::isfinite(lambda)) return fail("bad lambda");
   HIPCHK(hipSetDevice(h->device));
-  const int c = h->cur, nx = 1 - c;
-  const int n_free = h->n_pose - h->n_fixed;
+  h->lambda = lambda;
+  return build_impl(h, lambda, nullptr);
+}
+
+// damped solve, trial state, trial linearisation into slot `nx` and the trial scalars
+static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx) {
+  const int c = h->cur;
   tm_begin(h, TM_CHOL);
   launch_pose_damp(h->S(), h->ld, h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
-                   h->lambda, h->st);
+                   h->lambda, lam_dev, h->st);
   launch_chol_prepare(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(), h->st);
   launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
                   h->Ldiag.as<double>(), h->info.as<int>(), h->st);
@@ -810,10 +824,9 @@ int ptzba_solve_reduced(ptzba_handle h) {
   tm_end(h, TM_CHOL);
   HIPCHK(hipGetLastError());
   tm_begin(h, TM_BACK);
-  HIPCHK(hipMemsetAsync(h->loc.p, 0, h->loc.bytes, h->st));
   launch_pose_trial(h->ptz.as<double>(), h->dpose.as<double>(), h->gpose(), h->D_pose.as<double>(),
                     h->frame_pos.as<int32_t>(), h->ptz_trial.as<double>(),
-                    h->n_pose, h->n_fixed, h->lambda, h->loc.as<double>(), h->st);
+                    h->n_pose, h->n_fixed, h->lambda, lam_dev, h->loc.as<double>(), h->st);
   BacksubArgs b;
   b.lm_seg_begin = h->lm_seg_begin.as<int32_t>();
   b.seg_frame = h->seg_frame.as<int32_t>();
@@ -830,21 +843,114 @@ int ptzba_solve_reduced(ptzba_handle h) {
   b.n_lm = h->n_lm;
   b.n_fixed = h->n_fixed;
   b.lambda = h->lambda;
+  b.lam_dev = lam_dev;
   if (h->precision == PTZBA_FP32)
     launch_backsub<float>(b, h->st);
   else
     launch_backsub<double>(b, h->st);
   tm_end(h, TM_BACK);
-  (void)n_free;
   // trial linearisation (its cost decides acceptance; kept as the next linearisation if accepted)
   tables(h, h->ptz_trial.as<double>(), h->rays_trial.as<double>());
   linearize_into(h, nx);
-  HIPCHK(hipMemsetAsync(h->scal.p, 0, h->scal.bytes, h->st));
+  // scal[1] (trial cost) and scal[2..4] are overwritten below, loc[0..3] by k_pose_trial: no memsets
   launch_reduce_cols(h->lm_out[nx].as<double>() + 5, h->n_lm, 8, 1, 0, h->scal.as<double>() + 1,
                      h->red_scratch.as<double>(), h->st);
   launch_reduce_cols(h->lm_red.as<double>(), h->n_lm, 4, 3, 0, h->scal.as<double>() + 2, h->red_scratch.as<double>(),
                      h->st);
   HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int ptzba_solve_reduced(ptzba_handle h) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  HIPCHK(hipSetDevice(h->device));
+  return solve_impl(h, nullptr, 1 - h->cur);
+}
+
+// ------------------------------------------------------------------------------------------------
+// device-driven Levenberg-Marquardt (the decisions of ptzba.LMSolver on the device): the host only
+// enqueues trials and polls a pinned record ring, so no trial waits for a host round trip.  A single
+// linearisation slot: the trial linearises into it, a rejected trial re-linearises the current point.
+// ------------------------------------------------------------------------------------------------
+static int lm_check(ptzba_ctx* h) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  if (!h->lmdev.p) return fail("call ptzba_lm_start first");
+  return 0;
+}
+
+int ptzba_lm_start(ptzba_handle h) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  HIPCHK(hipSetDevice(h->device));
+  if (!h->lmdev.p && h->lmdev.alloc(sizeof(LMDev))) return -1;
+  if (!h->lm_host) {
+    HIPCHK(hipHostMalloc((void**)&h->lm_host, LM_RING * sizeof(LMDev), hipHostMallocDefault));
+    for (int k = 0; k < LM_RING; ++k) HIPCHK(hipEventCreateWithFlags(&h->lm_ev[k], hipEventDisableTiming));
+  }
+  h->cur = 0;
+  return ptzba_linearize(h);
+}
+
+int ptzba_lm_init(ptzba_handle h, const ptzba_lm_opts* o) {
+  if (lm_check(h)) return -1;
+  if (!o) return fail("null options");
+  if (!(o->lambda0 >= 0) || !(o->min_lambda > 0) || !(o->max_lambda > 0) || o->max_iter < 0 || o->max_retries < 1)
+    return fail("bad LM options");
+  HIPCHK(hipSetDevice(h->device));
+  LMParams p{o->ftol, o->xtol, o->gtol, o->lambda0, o->min_lambda, o->max_lambda, o->max_iter, o->max_retries,
+             o->gauss_newton ? 1 : 0, 0};
+  launch_lm_init(h->lmdev.as<LMDev>(), h->scal.as<double>(), p, h->st);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int ptzba_lm_build(ptzba_handle h) {
+  if (lm_check(h)) return -1;
+  HIPCHK(hipSetDevice(h->device));
+  // a build queued after the final decision (the host pipelines one trial ahead) exits at once
+  return build_impl(h, 0.0, &h->lmdev.as<LMDev>()->lam, &h->lmdev.as<LMDev>()->done);
+}
+
+int ptzba_lm_solve(ptzba_handle h) {
+  if (lm_check(h)) return -1;
+  HIPCHK(hipSetDevice(h->device));
+  return solve_impl(h, &h->lmdev.as<LMDev>()->lam, h->cur);
+}
+
+int ptzba_lm_decide(ptzba_handle h, int trial) {
+  if (lm_check(h)) return -1;
+  if (trial < 0) return fail("bad trial index");
+  HIPCHK(hipSetDevice(h->device));
+  LMDev* st = h->lmdev.as<LMDev>();
+  const int k = trial % LM_RING;
+  // the record is written by the decision kernel straight into pinned host memory
+  launch_lm_decide(st, h->scal.as<double>(), h->loc.as<double>(), h->info.as<int>(), h->lm_host + k, h->st);
+  launch_lm_commit(st, h->ptz.as<double>(), h->ptz_trial.as<double>(), 3 * h->n_pose, h->rays.as<double>(),
+                   h->rays_trial.as<double>(), 2 * (int64_t)h->n_lm, h->st);
+  // rejected: the trial overwrote the linearisation slot -> rebuild it at the current point
+  tables(h, h->ptz.as<double>(), h->rays.as<double>(), &st->relin);
+  linearize_into(h, h->cur, &st->relin);
+  HIPCHK(hipEventRecord(h->lm_ev[k], h->st));
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int ptzba_lm_wait(ptzba_handle h, int trial, ptzba_lm_record* out) {
+  if (lm_check(h)) return -1;
+  if (trial < 0 || !out) return fail("bad arguments");
+  HIPCHK(hipSetDevice(h->device));
+  const int k = trial % LM_RING;
+  HIPCHK(hipEventSynchronize(h->lm_ev[k]));
+  const LMDev& r = h->lm_host[k];
+  out->cost = r.cost;
+  out->initial_cost = r.initial_cost;
+  out->lambda = r.lam;
+  out->iterations = r.it;
+  out->nfev = r.nfev;
+  out->trials = r.trials;
+  out->retries = r.retries;
+  out->status = r.status;
+  out->done = r.done;
+  out->accepted = r.accepted;
   return 0;
 }
 
@@ -927,13 +1033,13 @@ int ptzba_reset_kernel_times(ptzba_handle h, int enable) {
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipStreamSynchronize(h->st));
   for (int k = 0; k < TM_N; ++k) {
-    if (enable && h->ev[k].empty()) {
+    if (((enable >> k) & 1) && h->ev[k].empty()) {
       h->ev[k].resize(TM_POOL);
       for (auto& e : h->ev[k]) HIPCHK(hipEventCreate(&e));
     }
     h->ev_used[k] = 0;
   }
-  h->timing = enable != 0;
+  h->timing = enable & ((1 << TM_N) - 1);
   return 0;
 }
 

@@ -33,7 +33,9 @@ namespace ptzba {
 template <typename real>
 __global__ void k_tables(const double* __restrict__ ptz, const double* __restrict__ rays, int n_pose,
                          int n_lm, FrameTab<double>* __restrict__ ft64, RayTab<double>* __restrict__ rt64,
-                         FrameTab<real>* __restrict__ ft, RayTab<real>* __restrict__ rt) {
+                         FrameTab<real>* __restrict__ ft, RayTab<real>* __restrict__ rt,
+                         const int* __restrict__ run_if) {
+  if (run_if && !*run_if) return;
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n_pose) {
     FrameTab<double> t = make_frame_tab<double>(ptz[3 * i], ptz[3 * i + 1], ptz[3 * i + 2]);
@@ -59,10 +61,10 @@ __global__ void k_tables(const double* __restrict__ ptz, const double* __restric
 
 template <typename real>
 void launch_tables(const double* ptz, const double* rays, int n_pose, int n_lm, void* ft64, void* rt64, void* ft,
-                   void* rt, hipStream_t st) {
+                   void* rt, const int* run_if, hipStream_t st) {
   int n = n_pose + n_lm;
   hipLaunchKernelGGL(k_tables<real>, dim3((n + 255) / 256), dim3(256), 0, st, ptz, rays, n_pose, n_lm,
-                     (FrameTab<double>*)ft64, (RayTab<double>*)rt64, (FrameTab<real>*)ft, (RayTab<real>*)rt);
+                     (FrameTab<double>*)ft64, (RayTab<double>*)rt64, (FrameTab<real>*)ft, (RayTab<real>*)rt, run_if);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -111,13 +113,16 @@ __device__ __forceinline__ void store4(double* p, double a, double b, double c, 
   reinterpret_cast<double2*>(p)[1] = make_double2(c, d);
 }
 
-template <typename real, int LOSS>
+// RELIN: the conditional re-linearisation after a rejected trial of the device-driven LM (a separate
+// instantiation, so profiles and K1 timings see only the unconditional launches)
+template <typename real, int LOSS, bool RELIN>
 __global__ __launch_bounds__(256, K1_MIN_WAVES) void k_linearize(LinArgs a) {
   __shared__ real s_x[4][SEGW], s_y[4][SEGW], s_acc[4][4][SEGW];
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
   const int task = blockIdx.x * 4 + wv;
   if (task >= a.n_work) return;  // whole wave leaves; no block-level barriers in this kernel
+  if (RELIN && !*a.run_if) return;  // device-driven LM: re-linearisation only after a rejected trial
   // one 16-B work descriptor {landmark, first segment, end segment, first record}: no dependent
   // lm_order -> lm_seg_begin -> seg_rec_begin chain before the records can be requested
   const int4 wd = a.lm_work[task];
@@ -291,10 +296,14 @@ template <typename real>
 void launch_linearize(const LinArgs& a, int loss, hipStream_t st) {
   if (a.n_work <= 0) return;
   dim3 grid((a.n_work + 3) / 4);
-  if (loss == 0)
-    hipLaunchKernelGGL((k_linearize<real, 0>), grid, dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((k_linearize<real, 1>), grid, dim3(256), 0, st, a);
+  const bool relin = a.run_if != nullptr;
+  if (loss == 0) {
+    if (relin) hipLaunchKernelGGL((k_linearize<real, 0, true>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_linearize<real, 0, false>), grid, dim3(256), 0, st, a);
+  } else {
+    if (relin) hipLaunchKernelGGL((k_linearize<real, 1, true>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_linearize<real, 1, false>), grid, dim3(256), 0, st, a);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -304,7 +313,10 @@ void launch_linearize(const LinArgs& a, int loss, hipStream_t st) {
 // ------------------------------------------------------------------------------------------------
 __global__ void k_landmark_damp(const double* __restrict__ lm_out, const int32_t* __restrict__ lm_seg_begin,
                                 double* __restrict__ D_ray, double* __restrict__ lm_aux, int n_lm,
-                                double lambda) {
+                                double lambda_arg, const double* __restrict__ lam_dev,
+                                const int* __restrict__ skip_if) {
+  if (skip_if && *skip_if) return;
+  const double lambda = lam_dev ? *lam_dev : lambda_arg;
   int l = blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= n_lm) return;
   double* o = lm_aux + (int64_t)l * 8;
@@ -331,16 +343,17 @@ __global__ void k_landmark_damp(const double* __restrict__ lm_out, const int32_t
 }
 
 void launch_landmark_damp(const double* lm_out, const int32_t* lm_seg_begin, double* D_ray, double* lm_aux,
-                          int n_lm, double lambda, hipStream_t st) {
+                          int n_lm, double lambda, const double* lam_dev, const int* skip_if, hipStream_t st) {
   hipLaunchKernelGGL(k_landmark_damp, dim3((n_lm + 255) / 256), dim3(256), 0, st, lm_out, lm_seg_begin, D_ray,
-                     lm_aux, n_lm, lambda);
+                     lm_aux, n_lm, lambda, lam_dev, skip_if);
 }
 
 
 // pose damping on the exchanged reduced system: D = max(D, diag U) (monotone), S_ii += lambda D_i
 __global__ void k_pose_damp(double* __restrict__ S, int64_t ld, const double* __restrict__ dU,
                             double* __restrict__ D_pose, const int32_t* __restrict__ frame_pos, int n_pose,
-                            int n_fixed, double lambda) {
+                            int n_fixed, double lambda_arg, const double* __restrict__ lam_dev) {
+  const double lambda = lam_dev ? *lam_dev : lambda_arg;
   int k = blockIdx.x * blockDim.x + threadIdx.x;
   int n = 3 * (n_pose - n_fixed);
   if (k >= n) return;
@@ -353,11 +366,11 @@ __global__ void k_pose_damp(double* __restrict__ S, int64_t ld, const double* __
 }
 
 void launch_pose_damp(double* S, int64_t ld, const double* dU, double* D_pose, const int32_t* frame_pos, int n_pose,
-                      int n_fixed, double lambda, hipStream_t st) {
+                      int n_fixed, double lambda, const double* lam_dev, hipStream_t st) {
   int n = 3 * (n_pose - n_fixed);
   if (n > 0)
     hipLaunchKernelGGL(k_pose_damp, dim3((n + 255) / 256), dim3(256), 0, st, S, ld, dU, D_pose, frame_pos, n_pose,
-                       n_fixed, lambda);
+                       n_fixed, lambda, lam_dev);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -405,7 +418,8 @@ __global__ __launch_bounds__(256) void k_backsub(BacksubArgs a) {
     a.rays_trial[2 * l] = th + d0;
     a.rays_trial[2 * l + 1] = ph + d1;
     const double D0 = a.D_ray[2 * l], D1 = a.D_ray[2 * l + 1];
-    red[0] = -0.5 * (lo[3] * d0 + lo[4] * d1) + 0.5 * a.lambda * (D0 * d0 * d0 + D1 * d1 * d1);
+    const double lam = a.lam_dev ? *a.lam_dev : a.lambda;
+    red[0] = -0.5 * (lo[3] * d0 + lo[4] * d1) + 0.5 * lam * (D0 * d0 * d0 + D1 * d1 * d1);
     red[1] = d0 * d0 + d1 * d1;
     red[2] = th * th + ph * ph;
     red[3] = fmax(fabs(lo[3]), fabs(lo[4]));
@@ -421,8 +435,9 @@ void launch_backsub(const BacksubArgs& a, hipStream_t st) {
 // pose trial + pose partials (identical on every rank): one block
 __global__ void k_pose_trial(const double* __restrict__ ptz, const double* __restrict__ dpose,
                              const double* __restrict__ g_pose, const double* __restrict__ D_pose,
-                             const int32_t* __restrict__ frame_pos, double* __restrict__ ptz_trial, int n_pose, int n_fixed, double lambda,
-                             double* __restrict__ out4) {
+                             const int32_t* __restrict__ frame_pos, double* __restrict__ ptz_trial, int n_pose, int n_fixed,
+                             double lambda_arg, const double* __restrict__ lam_dev, double* __restrict__ out4) {
+  const double lambda = lam_dev ? *lam_dev : lambda_arg;
   __shared__ double red[4][1024 / WAVE];
   double pr = 0, dx = 0, xx = 0, gm = 0;
   for (int i = threadIdx.x; i < 3 * n_pose; i += blockDim.x) {
@@ -455,10 +470,10 @@ __global__ void k_pose_trial(const double* __restrict__ ptz, const double* __res
 }
 
 void launch_pose_trial(const double* ptz, const double* dpose, const double* g_pose, const double* D_pose,
-                       const int32_t* frame_pos, double* ptz_trial, int n_pose, int n_fixed, double lambda, double* out4,
-                       hipStream_t st) {
+                       const int32_t* frame_pos, double* ptz_trial, int n_pose, int n_fixed, double lambda,
+                       const double* lam_dev, double* out4, hipStream_t st) {
   hipLaunchKernelGGL(k_pose_trial, dim3(1), dim3(1024), 0, st, ptz, dpose, g_pose, D_pose, frame_pos, ptz_trial,
-                     n_pose, n_fixed, lambda, out4);
+                     n_pose, n_fixed, lambda, lam_dev, out4);
 }
 
 // deterministic strided reduction: out[k] = sum_i src[i*stride + k] (fixed order), k < nk;
@@ -574,9 +589,112 @@ void launch_residual(const int32_t* rec_seg, const int32_t* seg_frame, const int
                      (const RayTab<double>*)rt64, u, v, n_rec, r_out);
 }
 
+// ------------------------------------------------------------------------------------------------
+// device-resident Levenberg-Marquardt control (the decision logic of ptzba.LMSolver, which follows
+// scipy's trf acceptance / termination rules, common.py:705-718): one thread per call.
+// ------------------------------------------------------------------------------------------------
+__global__ void k_lm_init(LMDev* st, const double* __restrict__ scal, LMParams p) {
+  st->p = p;
+  st->cost = scal[0];
+  st->initial_cost = scal[0];
+  st->lam = p.lambda0;
+  st->nu = 2.0;
+  st->it = 0;
+  st->nfev = 1;
+  st->trials = 0;
+  st->retries = 0;
+  st->status = 0;
+  st->done = 0;
+  st->accepted = 0;
+  st->relin = 0;
+}
+
+__global__ void k_lm_decide(LMDev* st, const double* __restrict__ scal, const double* __restrict__ loc,
+                            const int* __restrict__ info, LMDev* __restrict__ rec) {
+  LMDev s = *st;
+  s.accepted = 0;
+  s.relin = 0;
+  if (!s.done) {
+    const LMParams& p = s.p;
+    const double new_cost = scal[1], pred = scal[2] + loc[0], dx2 = scal[3] + loc[1], x2 = scal[4] + loc[2];
+    const double gmax = loc[3];
+    s.nfev += 1;
+    s.trials += 1;
+    const bool ok = info[0] == 0 && isfinite(new_cost) && isfinite(pred);
+    const double actual = s.cost - new_cost;
+    const double rho = (ok && pred > 0) ? actual / pred : -1.0;
+    const bool gn0 = p.gauss_newton && s.lam == 0.0;
+    if (ok && (rho > 0 || (gn0 && actual >= 0))) {
+      s.accepted = 1;
+      if (!gn0) {
+        const double t = 2.0 * rho - 1.0;
+        s.lam = fmax(p.min_lambda, s.lam * fmax(1.0 / 3.0, 1.0 - t * t * t));
+      }
+      s.nu = 2.0;
+      s.retries = 0;
+      s.it += 1;
+      const double old = s.cost;
+      s.cost = new_cost;
+      s.last_actual = actual;
+      s.last_rho = rho;
+      if (actual < p.ftol * old && rho > 0.25) {
+        s.status = 2;
+        s.done = 1;
+      } else if (sqrt(dx2) < p.xtol * (p.xtol + sqrt(x2))) {
+        s.status = 3;
+        s.done = 1;
+      } else if (p.gtol > 0 && gmax < p.gtol) {
+        s.status = 1;
+        s.done = 1;
+      } else if (s.it >= p.max_iter) {
+        s.status = 0;
+        s.done = 1;
+      }
+    } else {
+      s.lam = s.lam > 0 ? fmax(s.lam * s.nu, 1e-9) : 1e-9;
+      s.nu *= 2.0;
+      s.retries += 1;
+      if (s.lam > p.max_lambda) {
+        s.status = 0;
+        s.done = 1;
+      } else if (s.retries >= p.max_retries) {
+        s.status = -1;
+        s.done = 1;
+      } else {
+        s.relin = 1;  // the trial overwrote the linearisation: rebuild it at the current point
+      }
+    }
+  }
+  *st = s;
+  *rec = s;
+}
+
+// accepted trial -> current state (the trial's linearisation is already in place)
+__global__ void k_lm_commit(const LMDev* __restrict__ st, double* __restrict__ ptz, const double* __restrict__ ptz_trial,
+                            int n3, double* __restrict__ rays, const double* __restrict__ rays_trial, int64_t n2) {
+  if (!st->accepted) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n3 + n2; i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < n3) ptz[i] = ptz_trial[i];
+    else rays[i - n3] = rays_trial[i - n3];
+  }
+}
+
+void launch_lm_init(LMDev* st, const double* scal, const LMParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(1), 0, s, st, scal, p);
+}
+void launch_lm_decide(LMDev* st, const double* scal, const double* loc, const int* info, LMDev* rec, hipStream_t s) {
+  hipLaunchKernelGGL(k_lm_decide, dim3(1), dim3(1), 0, s, st, scal, loc, info, rec);
+}
+void launch_lm_commit(const LMDev* st, double* ptz, const double* ptz_trial, int n3, double* rays,
+                      const double* rays_trial, int64_t n2, hipStream_t s) {
+  hipLaunchKernelGGL(k_lm_commit, dim3(64), dim3(256), 0, s, st, ptz, ptz_trial, n3, rays, rays_trial, n2);
+}
+
 // explicit instantiations
-template void launch_tables<float>(const double*, const double*, int, int, void*, void*, void*, void*, hipStream_t);
-template void launch_tables<double>(const double*, const double*, int, int, void*, void*, void*, void*, hipStream_t);
+template void launch_tables<float>(const double*, const double*, int, int, void*, void*, void*, void*, const int*,
+                                   hipStream_t);
+template void launch_tables<double>(const double*, const double*, int, int, void*, void*, void*, void*, const int*,
+                                    hipStream_t);
 template void launch_linearize<float>(const LinArgs&, int, hipStream_t);
 template void launch_linearize<double>(const LinArgs&, int, hipStream_t);
 template void launch_backsub<float>(const BacksubArgs&, hipStream_t);

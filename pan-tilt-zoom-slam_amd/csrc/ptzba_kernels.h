@@ -21,6 +21,7 @@ struct LinArgs {
   const double2* seg_base;       // [n_seg] base observation; records hold obs - base (real)
   double u, v, fs2, inv_fs2;
   void* ug_slot;                 // [n_slot][12] real: U (6) | g_pose (3) | 0 0 0 (dense slots)
+  const int* run_if;             // nullptr, or: skip the launch when *run_if == 0 (device-driven LM)
   void* w_slot;                  // [n_slot][8] real: W (6) | 0 0 at slot toff_l + frame - first_l
   const int4* lm_meta;           // [n_lm] {first frame, last frame, slot offset, 0}
   double* lm_out;                // [n_lm][8]
@@ -47,6 +48,7 @@ struct SchurArgs {
   double* dU;                     // [n_sys] diag of U (for Marquardt scaling)
   int64_t ld;
   int n_pose;
+  const int* skip_if;             // nullptr, or: exit at once when *skip_if != 0 (device-driven LM)
 };
 
 struct BacksubArgs {
@@ -65,25 +67,41 @@ struct BacksubArgs {
   int n_lm;
   int n_fixed;
   double lambda;
+  const double* lam_dev;  // nullptr, or lambda read from device memory (device-driven LM)
 };
+
+// device-driven Levenberg-Marquardt state (ptzba_lm_*): parameters, running state, last decision
+struct LMParams {
+  double ftol, xtol, gtol, lambda0, min_lambda, max_lambda;
+  int max_iter, max_retries, gauss_newton, pad;
+};
+struct LMDev {
+  LMParams p;
+  double cost, initial_cost, lam, nu, last_actual, last_rho;
+  int it, nfev, trials, retries, status, done, accepted, relin;
+};
+void launch_lm_init(LMDev* st, const double* scal, const LMParams& p, hipStream_t s);
+void launch_lm_decide(LMDev* st, const double* scal, const double* loc, const int* info, LMDev* rec, hipStream_t s);
+void launch_lm_commit(const LMDev* st, double* ptz, const double* ptz_trial, int n3, double* rays,
+                      const double* rays_trial, int64_t n2, hipStream_t s);
 
 template <typename real>
 void launch_tables(const double* ptz, const double* rays, int n_pose, int n_lm, void* ft64, void* rt64, void* ft, void* rt,
-                   hipStream_t st);
+                   const int* run_if, hipStream_t st);
 template <typename real>
 void launch_linearize(const LinArgs& a, int loss, hipStream_t st);
 void launch_landmark_damp(const double* lm_out, const int32_t* lm_seg_begin, double* D_ray, double* lm_aux, int n_lm,
-                          double lambda, hipStream_t st);
+                          double lambda, const double* lam_dev, const int* skip_if, hipStream_t st);
 void launch_pose_damp(double* S, int64_t ld, const double* dU, double* D_pose, const int32_t* frame_pos, int n_pose,
-                      int n_fixed, double lambda,
-                      hipStream_t st);
+                      int n_fixed, double lambda, const double* lam_dev, hipStream_t st);
 template <typename real>
 void launch_schur(const SchurArgs& a, int n_items, int n_groups, int n_fixed, hipStream_t st);
 template <typename real>
 void launch_backsub(const BacksubArgs& a, hipStream_t st);
 void launch_pose_trial(const double* ptz, const double* dpose, const double* g_pose, const double* D_pose,
                        const int32_t* frame_pos,
-                       double* ptz_trial, int n_pose, int n_fixed, double lambda, double* out4, hipStream_t st);
+                       double* ptz_trial, int n_pose, int n_fixed, double lambda, const double* lam_dev, double* out4,
+                       hipStream_t st);
 // scratch: RED_SCRATCH doubles (partials + counter), zero-initialised once, reused across calls
 constexpr int RED_SCRATCH = 64 * 8 + 2;
 // scal[8] | loc[8] | info -> one packed device block (read back with a single copy)

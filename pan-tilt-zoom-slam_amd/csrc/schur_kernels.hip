@@ -67,6 +67,7 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
   __shared__ real sW[2][SNB][6][WAVE];                             // W rows of the chunk's frames (SoA)
   __shared__ __attribute__((aligned(16))) real sY[2][SNB][SF][WP];  // Y of (landmark, f1); 0 if unobserved
   __shared__ int4 sL[SCHUR_LMAX];                                    // the item's landmark list
+  if (a.skip_if && *a.skip_if) return;
   const int item = xcd_swizzle(blockIdx.x, gridDim.x);
   const int4 it = a.items[item];
   const int f1b = it.x, chunk = it.y, lb = it.z, nl = it.w - it.z;
@@ -227,6 +228,7 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
 // precedes f1); chunk-0 tiles also write b | g_pose | diag U of their frames.
 __global__ __launch_bounds__(256) void k_schur_reduce(SchurArgs a) {
   constexpr int NE = SF * 9 * WAVE;
+  if (a.skip_if && *a.skip_if) return;
   const int4 g = a.groups[blockIdx.y];  // {f1b, chunk, first item, end item}
   const int f1b = g.x, chunk = g.y;
   const int e = blockIdx.x * 256 + threadIdx.x;

@@ -40,6 +40,18 @@ class ptz_refine_opts(Structure):
                 ("f_scale", c_double)]
 
 
+class ptzba_lm_opts(Structure):
+    _fields_ = [("ftol", c_double), ("xtol", c_double), ("gtol", c_double), ("lambda0", c_double),
+                ("min_lambda", c_double), ("max_lambda", c_double), ("max_iter", c_int32), ("max_retries", c_int32),
+                ("gauss_newton", c_int32)]
+
+
+class ptzba_lm_record(Structure):
+    _fields_ = [("cost", c_double), ("initial_cost", c_double), ("lam", c_double), ("iterations", c_int32),
+                ("nfev", c_int32), ("trials", c_int32), ("retries", c_int32), ("status", c_int32), ("done", c_int32),
+                ("accepted", c_int32)]
+
+
 class ptzba_problem_opts(Structure):
     _fields_ = [("precision", c_int32), ("loss", c_int32), ("f_scale", c_double), ("n_fixed", c_int32),
                 ("ordering", c_int32), ("frame_win_hi", c_void_p)]
@@ -76,6 +88,12 @@ def lib():
         "ptzba_build_reduced": ([V, D], I),
         "ptzba_solve_reduced": ([V], I),
         "ptzba_step": ([V, D], I),
+        "ptzba_lm_start": ([V], I),
+        "ptzba_lm_init": ([V, POINTER(ptzba_lm_opts)], I),
+        "ptzba_lm_build": ([V], I),
+        "ptzba_lm_solve": ([V], I),
+        "ptzba_lm_decide": ([V, I], I),
+        "ptzba_lm_wait": ([V, I, POINTER(ptzba_lm_record)], I),
         "ptzba_read_scalars": ([V, V], I),
         "ptzba_accept": ([V, I], I),
         "ptzba_exchange": ([V, POINTER(c_void_p), POINTER(c_int64), POINTER(c_void_p)], I),
@@ -119,6 +137,7 @@ EXPORTED_SYMBOLS = [
     "ptzba_new", "ptzba_delete", "ptzba_last_error", "ptzba_version", "ptzba_set_stream", "ptzba_use_own_stream", "ptzba_set_problem",
     "ptzba_problem_info", "ptzba_solver_info", "ptzba_residual", "ptzba_set_state", "ptzba_get_state", "ptzba_linearize",
     "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_read_scalars", "ptzba_accept",
+    "ptzba_lm_start", "ptzba_lm_init", "ptzba_lm_build", "ptzba_lm_solve", "ptzba_lm_decide", "ptzba_lm_wait",
     "ptzba_exchange", "ptzba_exchange_packed", "ptzba_pack", "ptzba_unpack", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptz_ray_to_image",
     "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks",
     "ptz_py_shuffle_prefix", "ptz_set_order_pairs", "ptz_keyframe_features", "ptz_pack_records",
@@ -448,6 +467,27 @@ class BAHandle:
     def accept(self, ok):
         _check(lib().ptzba_accept(self.h, 1 if ok else 0), "ptzba_accept")
 
+    # device-driven LM (include/ptzba.h ptzba_lm_*)
+    def lm_start(self):
+        _check(lib().ptzba_lm_start(self.h), "ptzba_lm_start")
+
+    def lm_init(self, opts):
+        _check(lib().ptzba_lm_init(self.h, ctypes.byref(opts)), "ptzba_lm_init")
+
+    def lm_build(self):
+        _check(lib().ptzba_lm_build(self.h), "ptzba_lm_build")
+
+    def lm_solve(self):
+        _check(lib().ptzba_lm_solve(self.h), "ptzba_lm_solve")
+
+    def lm_decide(self, k):
+        _check(lib().ptzba_lm_decide(self.h, int(k)), "ptzba_lm_decide")
+
+    def lm_wait(self, k):
+        r = ptzba_lm_record()
+        _check(lib().ptzba_lm_wait(self.h, int(k), ctypes.byref(r)), "ptzba_lm_wait")
+        return r
+
     def exchange(self):
         sp = c_void_p(0)
         cnt = c_int64(0)
@@ -470,8 +510,9 @@ class BAHandle:
     def sync(self):
         _check(lib().ptzba_sync(self.h), "ptzba_sync")
 
-    def reset_kernel_times(self, enable=True):
-        _check(lib().ptzba_reset_kernel_times(self.h, 1 if enable else 0), "ptzba_reset_kernel_times")
+    def reset_kernel_times(self, enable=True, groups=0xF):
+        """Restart kernel timing; `groups` bitmask: 1 K1, 2 Schur, 4 Cholesky solve, 8 back-substitution."""
+        _check(lib().ptzba_reset_kernel_times(self.h, int(groups) if enable else 0), "ptzba_reset_kernel_times")
 
     def kernel_times(self):
         ms = np.zeros(4)
@@ -582,10 +623,15 @@ class LMSolver:
 
     `allreduce(kind)` (optional) is called at the two exchange points of a multi-GPU solve:
     kind == 'sys' after build_reduced (sum of the reduced camera system), kind == 'scal' after
-    linearize / solve_reduced (sum of the partial scalars).  Single GPU: None."""
+    linearize / solve_reduced (sum of the partial scalars).  Single GPU: None.
+
+    device_loop=True (default): the accept/reject decisions run on the device (ptzba_lm_*) and the host
+    enqueues trial k+1's reduced-system build before it waits for trial k's decision, so the GPU never
+    idles on a host round trip.  device_loop=False (or verbose): the same decisions on the host after
+    reading each trial's scalars (also used for handles without ptzba_lm_*, e.g. test doubles)."""
 
     def __init__(self, handle, ftol=1e-4, xtol=1e-8, gtol=0.0, max_iter=100, lambda0=1e-4, min_lambda=1e-12,
-                 max_lambda=1e16, gauss_newton=False, allreduce=None, verbose=0, max_retries=30):
+                 max_lambda=1e16, gauss_newton=False, allreduce=None, verbose=0, max_retries=30, device_loop=True):
         self.h = handle
         self.ftol, self.xtol, self.gtol = ftol, xtol, gtol
         self.max_iter = max_iter
@@ -595,6 +641,7 @@ class LMSolver:
         self.allreduce = allreduce
         self.verbose = verbose
         self.max_retries = max_retries
+        self.device_loop = device_loop and hasattr(handle, "lm_start")
 
     def _scalars(self):
         if self.allreduce is not None:
@@ -602,6 +649,51 @@ class LMSolver:
         return self.h.read_scalars()
 
     def run(self, iterations=None, check_termination=True):
+        if self.device_loop and check_termination and not self.verbose:
+            return self._run_device(iterations)
+        return self._run_host(iterations, check_termination)
+
+    def _run_device(self, iterations=None):
+        h = self.h
+        t0 = time.perf_counter()
+        max_iter = self.max_iter if iterations is None else iterations
+        h.lm_start()
+        if self.allreduce is not None:
+            self.allreduce("scal")
+        h.lm_init(ptzba_lm_opts(self.ftol, self.xtol, self.gtol, self.lambda0, self.min_lambda, self.max_lambda,
+                                int(max_iter), int(self.max_retries), 1 if self.gauss_newton else 0))
+
+        def build():
+            h.lm_build()
+            if self.allreduce is not None:
+                self.allreduce("sys")
+
+        if max_iter <= 0:
+            h.sync()
+            cost = float(h.read_scalars()[0])
+            return LMResult(status=0, message=STATUS_MSG[0], cost=cost, initial_cost=cost, njev=0, nfev=1,
+                            iterations=0, lam=self.lambda0, time=time.perf_counter() - t0, history=[], trials=0)
+        build()
+        limit = max_iter * (self.max_retries + 1)
+        k = 0
+        while True:
+            h.lm_solve()
+            if self.allreduce is not None:
+                self.allreduce("scal")
+            h.lm_decide(k)
+            if k + 1 < limit:
+                build()  # next trial's build queued behind this decision (harmless after the last one)
+            rec = h.lm_wait(k)
+            k += 1
+            if rec.done or k >= limit:
+                break
+        h.sync()
+        t1 = time.perf_counter()
+        return LMResult(status=rec.status, message=STATUS_MSG.get(rec.status, "?"), cost=rec.cost,
+                        initial_cost=rec.initial_cost, njev=rec.iterations, nfev=rec.nfev, iterations=rec.iterations,
+                        lam=rec.lam, time=t1 - t0, history=[], trials=rec.trials)
+
+    def _run_host(self, iterations=None, check_termination=True):
         h = self.h
         t0 = time.perf_counter()
         h.linearize()

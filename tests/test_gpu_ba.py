@@ -354,3 +354,46 @@ def test_exchange_region_sums_over_landmark_shards(gpu_available, packed):
         np.testing.assert_allclose(rays[own], rays0[own], rtol=0, atol=1e-9)
     for h, _ in hs:
         h.close()
+
+
+@pytest.mark.parametrize("config,precision,loss", [("config1", 0, 0), ("config1", 1, 1), ("config2", 1, 1)])
+def test_device_loop_equals_host_loop(gpu_available, config, precision, loss):
+    """The device-driven LM (ptzba_lm_*: decisions on the GPU, pipelined trials, single linearisation
+    slot with re-linearisation after a rejected trial) takes exactly the host loop's decisions: same
+    accepted-iteration count, status and (bitwise-deterministic kernels) the same state."""
+    import ptzba
+    import synthetic
+    p = synthetic.make_problem(config, seed=1)
+    out = []
+    for device_loop in (False, True):
+        h = ptzba.BAHandle(0)
+        h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=precision, loss=loss,
+                      f_scale=1.0)
+        h.set_state(p.init_ptz, p.init_rays)
+        res = ptzba.LMSolver(h, ftol=1e-8, xtol=1e-12, max_iter=40, device_loop=device_loop).run()
+        ptz, rays = h.get_state()
+        out.append((res, ptz, rays))
+        h.close()
+    (rh, ph, yh), (rd, pd, yd) = out
+    assert rd.njev == rh.njev and rd.status == rh.status and rd.nfev == rh.nfev, (rh, rd)
+    assert abs(rd.cost - rh.cost) <= 1e-12 * rh.cost
+    np.testing.assert_allclose(pd, ph, rtol=0, atol=1e-10)
+    np.testing.assert_allclose(yd, yh, rtol=0, atol=1e-10)
+
+
+def test_device_loop_rejections_and_limits(gpu_available):
+    """A huge initial damping forces rejected trials (re-linearisation path) and max_iter stops early."""
+    import ptzba
+    import synthetic
+    p = synthetic.make_problem("config1", seed=2)
+    for kw in (dict(lambda0=1e-9, max_iter=3), dict(lambda0=1e6, max_iter=25)):
+        res = []
+        for device_loop in (False, True):
+            h = ptzba.BAHandle(0)
+            h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=0)
+            h.set_state(p.init_ptz, p.init_rays)
+            res.append((ptzba.LMSolver(h, ftol=1e-10, xtol=1e-14, device_loop=device_loop, **kw).run(), h.get_state()))
+            h.close()
+        (a, sa), (b, sb) = res
+        assert (a.njev, a.nfev, a.status) == (b.njev, b.nfev, b.status), (a, b)
+        np.testing.assert_allclose(sb[0], sa[0], rtol=0, atol=1e-10)
