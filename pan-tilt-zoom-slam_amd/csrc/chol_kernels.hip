@@ -200,6 +200,11 @@ __device__ __forceinline__ void wave_potrf_trsm32(double (*D)[NB + 1], double (*
   wave_lds_fence();
 }
 
+#ifdef CS_TIMING
+__device__ long long g_cs_stamps[64][6];
+__device__ long long g_cs_wg[64][10];
+__device__ int g_cs_level;
+#endif
 // Workgroup form of the same factorisation (256 threads = 4 waves): rows in lanes as above (lanes 0..31
 // rows of D, 32..63 rows of T), the 32 columns split over the 4 waves (wave w keeps columns w + 4 i in
 // registers).  Pivot blocks of 8: the waves publish the block's 8 columns to LDS, wave 0 eliminates
@@ -220,6 +225,11 @@ __device__ __forceinline__ void wg_potrf_trsm32(double (*D)[NB + 1], double (*T)
 #pragma unroll
   for (int i = 0; i < NB / 4; ++i) col[i] = have ? (isT ? T[r][w + 4 * i] : D[r][w + 4 * i]) : 0.0;
   bool bad = false;
+#ifdef CS_TIMING
+  long long* wst = g_cs_wg[g_cs_level < 64 ? g_cs_level : 63];
+  const bool wrec = threadIdx.x == 0 && blockIdx.x == 0;
+  if (wrec) wst[0] = clock64();
+#endif
 #pragma unroll
   for (int kb = 0; kb < NB; kb += WB) {
     pan[lane][w] = col[kb / 4];
@@ -248,6 +258,9 @@ __device__ __forceinline__ void wg_potrf_trsm32(double (*D)[NB + 1], double (*T)
       }
     }
     __syncthreads();
+#ifdef CS_TIMING
+    if (wrec) wst[1 + 2 * (kb / WB)] = clock64();
+#endif
     col[kb / 4] = pan[lane][w];
     col[kb / 4 + 1] = pan[lane][4 + w];
     if (kb + WB < NB) {
@@ -264,6 +277,9 @@ __device__ __forceinline__ void wg_potrf_trsm32(double (*D)[NB + 1], double (*T)
       }
       __syncthreads();  // pan / mul are rewritten by the next block
     }
+#ifdef CS_TIMING
+    if (wrec) wst[2 + 2 * (kb / WB)] = clock64();
+#endif
   }
   if (bad && lane == 0) atomicOr(info, 1);
   if (threadIdx.x < NB) rdg[threadIdx.x] = rsq_nr(dg[threadIdx.x]);
@@ -281,8 +297,6 @@ __device__ __forceinline__ void wg_potrf_trsm32(double (*D)[NB + 1], double (*T)
 }
 
 #ifdef CS_TIMING
-__device__ long long g_cs_stamps[64][6];
-__device__ int g_cs_level;
 #define CS_STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x == 0 && cs_lvl < 64) g_cs_stamps[cs_lvl][k] = clock64(); } while (0)
 #else
 #define CS_STAMP(k) do { } while (0)
@@ -554,6 +568,7 @@ __global__ __launch_bounds__(1024) void k_chol_backsolve(const double* __restric
 extern "C" int ptzba_debug_cs_stamps(long long* out) {
   const int zero = 0;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cs_stamps), sizeof(g_cs_stamps)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out + 64 * 6, HIP_SYMBOL(g_cs_wg), sizeof(g_cs_wg)) != hipSuccess) return -1;
   return hipMemcpyToSymbol(HIP_SYMBOL(g_cs_level), &zero, sizeof(int)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -59,15 +59,36 @@ __device__ __forceinline__ void load_w6(real (&x)[6], const real* __restrict__ p
   }
 }
 
+#ifdef SK_TIMING
+__device__ long long g_sk[16][16];
+#define SK_T(k) do { if (skrec) sk[k] = clock64(); } while (0)
+#define SK_ACC(k, t0) do { if (skrec) sk[k] += clock64() - (t0); } while (0)
+#define SK_NOW(t0) do { if (skrec) t0 = clock64(); } while (0)
+#else
+#define SK_T(k) do { } while (0)
+#define SK_ACC(k, t0) do { } while (0)
+#define SK_NOW(t0) do { } while (0)
+#endif
 template <typename real>
 __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
   // fp64 (parity path) stages half as many landmarks per batch to stay inside 160 KiB of LDS
   constexpr int SNB = sizeof(real) == 4 ? 16 : 8;
   constexpr int WP = sizeof(real) == 4 ? 8 : 6;  // 16-B aligned row pitch for 6 values
   __shared__ real sW[2][SNB][6][WAVE];                             // W rows of the chunk's frames (SoA)
-  __shared__ __attribute__((aligned(16))) real sY[2][SNB][SF][WP];  // Y of (landmark, f1); 0 if unobserved
+  // Y of (landmark, f1), 0 if unobserved.  fp32: frames (2p, 2p+1) interleaved per component, so one
+  // 8-byte read gives the pair's value for the packed FMAs; fp64: one row of 6 per frame.
+  __shared__ __attribute__((aligned(16))) real sY[2][SNB][SF][WP];
   __shared__ int4 sL[SCHUR_LMAX];                                    // the item's landmark list
   if (a.skip_if && *a.skip_if) return;
+#ifdef SK_TIMING
+  const bool skrec = threadIdx.x == 0 && blockIdx.x < 16;
+  long long* sk = g_sk[blockIdx.x & 15];
+  if (skrec)
+    for (int k = 0; k < 16; ++k) sk[k] = 0;
+#endif
+  long long skt = 0;
+  (void)skt;
+  SK_T(0);
   const int item = xcd_swizzle(blockIdx.x, gridDim.x);
   const int4 it = a.items[item];
   const int f1b = it.x, chunk = it.y, lb = it.z, nl = it.w - it.z;
@@ -76,6 +97,7 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
   const real* __restrict__ w_slot = (const real*)a.w_slot;
   for (int k = t; k < nl; k += 512) sL[k] = a.item_lm[lb + k];
   __syncthreads();
+  SK_T(1);
 
   if (chunk == 0) {
     // diagonal terms of the F1 frames over this split's landmarks: U, g_pose and W V~^-1 g, read from
@@ -85,26 +107,37 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
     double acc[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) acc[k] = 0;
-#pragma unroll 2
-    for (int j = t >> 5; j < nl; j += 512 / SF) {
-      const int4 m = sL[j];
-      const bool in = f >= m.y && f <= m.z;
-      const int64_t slot = m.w + min(max(f - m.y, 0), m.z - m.y);
-      real u[12], w[6];
-      load_w6(w, w_slot + slot * 8);
+    // DU landmarks per thread and step, all loads issued before any is consumed (clamped, branch-free)
+    constexpr int DU = 4, JS = 512 / SF;
+    for (int j0 = t >> 5; j0 < nl; j0 += DU * JS) {
+      real u[DU][12], w[DU][6];
+      double vg[DU][2];
+      bool in[DU];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const auto v4 = reinterpret_cast<const typename std::conditional<sizeof(real) == 4, float4, double4>::type*>(
-            ug_slot + slot * 12)[k];
-        u[4 * k] = v4.x; u[4 * k + 1] = v4.y; u[4 * k + 2] = v4.z; u[4 * k + 3] = v4.w;
+      for (int d = 0; d < DU; ++d) {
+        const int j = j0 + d * JS;
+        const int4 m = sL[min(j, nl - 1)];
+        in[d] = j < nl && f >= m.y && f <= m.z;
+        const int64_t slot = m.w + min(max(f - m.y, 0), m.z - m.y);
+        load_w6(w[d], w_slot + slot * 8);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const auto v4 = reinterpret_cast<const typename std::conditional<sizeof(real) == 4, float4, double4>::type*>(
+              ug_slot + slot * 12)[k];
+          u[d][4 * k] = v4.x; u[d][4 * k + 1] = v4.y; u[d][4 * k + 2] = v4.z; u[d][4 * k + 3] = v4.w;
+        }
+        const double* vi = a.lm_aux + (int64_t)m.x * 8;
+        vg[d][0] = vi[3];
+        vg[d][1] = vi[4];
       }
-      const double* vi = a.lm_aux + (int64_t)m.x * 8;
-      const double vg0 = vi[3], vg1 = vi[4];
-      if (in) {
 #pragma unroll
-        for (int k = 0; k < 9; ++k) acc[k] += (double)u[k];
+      for (int d = 0; d < DU; ++d) {
+        if (in[d]) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) acc[9 + q] += (double)w[2 * q] * vg0 + (double)w[2 * q + 1] * vg1;
+          for (int k = 0; k < 9; ++k) acc[k] += (double)u[d][k];
+#pragma unroll
+          for (int q = 0; q < 3; ++q) acc[9 + q] += (double)w[d][2 * q] * vg[d][0] + (double)w[d][2 * q + 1] * vg[d][1];
+        }
       }
     }
     double* red = reinterpret_cast<double*>(&sW[0][0][0][0]);  // [16][SF][12], free until staging
@@ -118,6 +151,7 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
     }
     __syncthreads();
   }
+  SK_T(2);
 
   // ---- staging registers: W slots (e = t, t + 512 over [SNB][64]) and one Y pair (j = t / SF, i = t % SF;
   // fp64: threads >= SNB*SF repeat a pair and do not stage it).  Branch-free, so the loads stay in flight
@@ -153,12 +187,14 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
       for (int k = 0; k < 6; ++k) sW[buf][j][k][ln] = rwin[q] ? rw[q][k] : (real)0;
     }
     if (t < SNB * SF) {
-      real* y = sY[buf][yj][yi];
+      // pair layout (fp32): element (frame 2p + h, component k) at [2p][0] + 2 k + h of the pair's 16 reals
+      real* y = sizeof(real) == 4 ? &sY[buf][yj][yi & ~1][0] + (yi & 1) : sY[buf][yj][yi];
+      const int ks = sizeof(real) == 4 ? 2 : 1;
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         const double W0 = ryin ? (double)ryw[2 * q] : 0.0, W1 = ryin ? (double)ryw[2 * q + 1] : 0.0;
-        y[2 * q] = (real)-(W0 * rvi[0] + W1 * rvi[1]);  // staged negated: the FMAs accumulate -Y W^T
-        y[2 * q + 1] = (real)-(W0 * rvi[1] + W1 * rvi[2]);
+        y[ks * (2 * q)] = (real)-(W0 * rvi[0] + W1 * rvi[1]);  // staged negated: the FMAs accumulate -Y W^T
+        y[ks * (2 * q + 1)] = (real)-(W0 * rvi[1] + W1 * rvi[2]);
       }
     }
   };
@@ -174,6 +210,13 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
     stage(0);
   }
   __syncthreads();
+  SK_T(3);
+#ifdef SK_TIMING
+  if (skrec) {
+    sk[8] = nl;
+    sk[9] = chunk;
+  }
+#endif
   int buf = 0;
   for (int p = 0; p < nl; p += SNB) {
     const bool more = p + SNB < nl;  // block-uniform
@@ -184,44 +227,94 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
     for (int i = 0; i < SFW; ++i)
 #pragma unroll
       for (int k = 0; k < 9; ++k) accr[i][k] = 0;
-    if (S2_ABL != 1)
+    SK_NOW(skt);
     // straight-line over the whole batch: slots past the list and unobserved (landmark, f1) pairs were
     // staged as zeros, so no branch (and no wait at a branch) interrupts the LDS reads and the FMAs
+    if constexpr (sizeof(real) == 4) {
+      // packed: one v_pk_fma_f32 updates the same block entry of two frames (2p, 2p+1)
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      f2 accp[SFW / 2][9];
+#pragma unroll
+      for (int pp = 0; pp < SFW / 2; ++pp)
+#pragma unroll
+        for (int k = 0; k < 9; ++k) accp[pp][k] = f2{0.f, 0.f};
 #pragma unroll 2
-    for (int j = 0; j < SNB; ++j) {
-      real w2[6];
+      for (int j = 0; j < SNB; ++j) {
+        float w2[6];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) w2[k] = sW[buf][j][k][lane];
+        for (int k = 0; k < 6; ++k) w2[k] = sW[buf][j][k][lane];
 #pragma unroll
-      for (int i = 0; i < SFW; ++i) {
-        const real* ys = sY[buf][j][SFW * wv + i];
-        real y[6];
+        for (int pp = 0; pp < SFW / 2; ++pp) {
+          const f2* ys = reinterpret_cast<const f2*>(&sY[buf][j][SFW * wv + 2 * pp][0]);
+          f2 y[6];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) y[k] = ys[k];
+          for (int k = 0; k < 6; ++k) y[k] = ys[k];
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
+          for (int q = 0; q < 3; ++q)
 #pragma unroll
-          for (int r = 0; r < 3; ++r) {
-            accr[i][3 * q + r] = fma(y[2 * q], w2[2 * r], accr[i][3 * q + r]);
-            accr[i][3 * q + r] = fma(y[2 * q + 1], w2[2 * r + 1], accr[i][3 * q + r]);
-          }
+            for (int r = 0; r < 3; ++r) {
+              accp[pp][3 * q + r] = __builtin_elementwise_fma(y[2 * q], f2{w2[2 * r], w2[2 * r]}, accp[pp][3 * q + r]);
+              accp[pp][3 * q + r] =
+                  __builtin_elementwise_fma(y[2 * q + 1], f2{w2[2 * r + 1], w2[2 * r + 1]}, accp[pp][3 * q + r]);
+            }
+        }
       }
+#pragma unroll
+      for (int pp = 0; pp < SFW / 2; ++pp)
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          acc[2 * pp][k] += (double)accp[pp][k].x;
+          acc[2 * pp + 1][k] += (double)accp[pp][k].y;
+        }
+    } else {
+#pragma unroll 2
+      for (int j = 0; j < SNB; ++j) {
+        real w2[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) w2[k] = sW[buf][j][k][lane];
+#pragma unroll
+        for (int i = 0; i < SFW; ++i) {
+          const real* ys = sY[buf][j][SFW * wv + i];
+          real y[6];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) y[k] = ys[k];
+#pragma unroll
+          for (int q = 0; q < 3; ++q)
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+              accr[i][3 * q + r] = fma(y[2 * q], w2[2 * r], accr[i][3 * q + r]);
+              accr[i][3 * q + r] = fma(y[2 * q + 1], w2[2 * r + 1], accr[i][3 * q + r]);
+            }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < SFW; ++i)
+#pragma unroll
+        for (int k = 0; k < 9; ++k) acc[i][k] += (double)accr[i][k];
     }
-#pragma unroll
-    for (int i = 0; i < SFW; ++i)
-#pragma unroll
-      for (int k = 0; k < 9; ++k) acc[i][k] += (double)accr[i][k];
+    SK_ACC(4, skt);  // compute
+    SK_NOW(skt);
     if (more) stage(buf ^ 1);
+    SK_ACC(5, skt);  // stage (waits for the prefetched loads)
+    SK_NOW(skt);
     __syncthreads();
+    SK_ACC(6, skt);  // barrier
     buf ^= 1;
   }
+  SK_T(7);
   // partial blocks of this split: part[item][f1 local][k][f2 lane]
   double* out = a.part + (int64_t)item * (SF * 9 * WAVE);
 #pragma unroll
   for (int i = 0; i < SFW; ++i)
 #pragma unroll
     for (int k = 0; k < 9; ++k) out[((SFW * wv + i) * 9 + k) * WAVE + lane] = acc[i][k];
+  SK_T(10);
 }
+#ifdef SK_TIMING
+extern "C" int ptzba_debug_sk(long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sk), sizeof(g_sk)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // tile reduction: thread = one element of a tile (grid: tile x 72 blocks of 256); fixed-order sum of the
 // splits, U on the diagonal blocks, write the lower triangle in the system order (mirror when f2

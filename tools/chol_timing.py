@@ -20,7 +20,7 @@ h.set_state(p.init_ptz, p.init_rays)
 ptzba.LMSolver(h, ftol=1e-4, xtol=1e-8, max_iter=2).run()
 L = ptzba.lib()
 L.ptzba_debug_cs_stamps.argtypes = [ctypes.c_void_p]
-buf = np.zeros((64, 6), dtype=np.int64)
+buf = np.zeros(64 * 6 + 64 * 10, dtype=np.int64)
 h.linearize()
 h.build_reduced(1e-3)
 h.sync()
@@ -28,7 +28,10 @@ assert L.ptzba_debug_cs_stamps(buf.ctypes.data) == 0  # reset the level counter
 h.solve_reduced()
 h.sync()
 assert L.ptzba_debug_cs_stamps(buf.ctypes.data) == 0
+wg = buf[64 * 6:].reshape(64, 10)
+buf = buf[:64 * 6].reshape(64, 6)
 nz = np.nonzero(buf[:, 0])[0]
+print("potrf blocks [panel, update] x4 (mean over levels 0..29):", np.diff(wg[:30, :9], axis=1).mean(0).round(0))
 print(f"{len(nz)} levels, first->last start {buf[nz[-1], 0] - buf[nz[0], 0]} ticks")
 ph = np.diff(buf[nz, :4], axis=1)
 gap = buf[nz[1:], 0] - buf[nz[:-1], 3]
