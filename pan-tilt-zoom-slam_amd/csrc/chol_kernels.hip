@@ -212,8 +212,11 @@ __device__ int g_cs_level;
 // the rank-8 update to its own columns (the pivot-column values broadcast from LDS).  The trailing
 // update -- most of the FMAs -- runs on four SIMDs instead of one.
 constexpr int WB = 8;
+#ifndef LA_BW
+#define LA_BW 4  // pivot block of the lookahead form
+#endif
 #ifndef CHOL_WG
-#define CHOL_WG 1  // 1: workgroup potrf+trsm (4 waves), 0: single-wave sweep
+#define CHOL_WG 3  // 3: flag-synchronised lookahead, 2: lookahead workgroup potrf+trsm, 1: workgroup (4 waves), 0: single-wave sweep
 #endif
 __device__ __forceinline__ void wg_potrf_trsm32(double (*D)[NB + 1], double (*T)[NB + 1], double* rdg,
                                                 double (*pan)[WB + 1], double (*mul)[WB + 1], double* dg, int* info) {
@@ -296,6 +299,261 @@ __device__ __forceinline__ void wg_potrf_trsm32(double (*D)[NB + 1], double (*T)
   __syncthreads();
 }
 
+// reciprocal square root by a series step on the hardware estimate: e = 1 - d y0^2 (|e| ~ 5e-8),
+// y = y0 (1 + e/2 + 3e^2/8) -- full double precision in 4 dependent operations (rsq_nr: 6)
+__device__ __forceinline__ double rsq_fast(double d) {
+  const double y0 = __builtin_amdgcn_rsq(d);
+  const double e = fma(-d * y0, y0, 1.0);
+  return fma(y0 * e, fma(e, 0.375, 0.5), y0);
+}
+
+// Lookahead workgroup form (CHOL_WG 2).  Rows in lanes as above; the tile stays in LDS.  Wave 0 runs
+// the critical chain, one stage per pivot block s of BW columns:
+//   * apply block s-1's update to block s (its own lanes' rows; the block-(s-1) factor rows of the D
+//     lanes come from LDS as uniform broadcast reads),
+//   * publish block s's BWxBW diagonal part P, and every lane factors P = L_P L_P^T itself (no
+//     cross-lane traffic on the pivot chain, no v_readlane),
+//   * solve its own row against L_P: l = a L_P^-T -- for a D row that is its L_ij, for a T row its
+//     X_rj -- and store l to LDS (Lb[s]).
+// Meanwhile waves 1-3 apply block s-1's update to blocks s+1.. (off the chain).  One barrier per stage.
+// fp64 VALU issue (~8 cycles per instruction for one wave) bounds the chain wave, so the block is small:
+// the redundant factorisation of P costs O(BW^3) instructions per stage.  D's upper triangle may hold
+// anything: those lanes' results are never read by another lane and are zeroed on output.
+template <int BW>
+__device__ __forceinline__ void wg_potrf_trsm32_la(double (*D)[NB + 1], double (*T)[NB + 1],
+                                                   double (*Lb)[2 * NB][BW], double (*Pb)[BW], int* info) {
+  constexpr int NS = NB / BW;
+  const int w = threadIdx.x >> 6, lane = lane_id();
+  const bool isT = lane >= NB;
+  const int r = lane & (NB - 1);
+  const bool have = !isT || T != nullptr;
+  double* row = (isT && T) ? T[r] : D[r];
+  bool bad = false;
+  double lp[BW];
+#pragma unroll
+  for (int k = 0; k < BW; ++k) lp[k] = 0.0;
+#ifdef CS_TIMING
+  long long* wst = g_cs_wg[g_cs_level < 64 ? g_cs_level : 63];
+  const bool wrec = threadIdx.x == 0 && blockIdx.x == 0;
+  if (wrec) wst[0] = clock64();
+#endif
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int kb = s * BW;
+    if (w == 0) {
+      double a[BW];
+#pragma unroll
+      for (int j = 0; j < BW; ++j) a[j] = row[kb + j];
+      if (s > 0) {
+#pragma unroll
+        for (int j = 0; j < BW; ++j) {
+          double acc = a[j];
+#pragma unroll
+          for (int k = 0; k < BW; ++k) acc = fma(-lp[k], Lb[s - 1][kb + j][k], acc);
+          a[j] = acc;
+        }
+      }
+      if (lane >= kb && lane < kb + BW) {
+#pragma unroll
+        for (int j = 0; j < BW; ++j) Pb[lane - kb][j] = a[j];
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      __builtin_amdgcn_wave_barrier();
+      double P[BW][BW], y[BW];
+#pragma unroll
+      for (int i = 0; i < BW; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) P[i][j] = Pb[i][j];
+#pragma unroll
+      for (int j = 0; j < BW; ++j) {
+        double d = P[j][j];
+        if (!(d > 0.0)) {
+          bad = true;
+          d = 1e-300;
+        }
+        y[j] = rsq_fast(d);
+#pragma unroll
+        for (int i = j + 1; i < BW; ++i) P[i][j] *= y[j];
+#pragma unroll
+        for (int i = j + 1; i < BW; ++i)
+#pragma unroll
+          for (int m = j + 1; m <= i; ++m) P[i][m] = fma(-P[i][j], P[m][j], P[i][m]);
+      }
+#pragma unroll
+      for (int j = 0; j < BW; ++j) {
+        const double x = a[j] * y[j];
+        lp[j] = x;
+#pragma unroll
+        for (int i = j + 1; i < BW; ++i) a[i] = fma(-P[i][j], x, a[i]);
+      }
+#pragma unroll
+      for (int j = 0; j < BW; ++j) Lb[s][lane][j] = lp[j];
+    } else if (s > 0 && s + 1 < NS) {
+      double l[BW];
+#pragma unroll
+      for (int k = 0; k < BW; ++k) l[k] = Lb[s - 1][lane][k];
+      for (int m = kb + BW + w - 1; m < NB; m += 3) {
+        double acc = row[m];
+#pragma unroll
+        for (int k = 0; k < BW; ++k) acc = fma(-l[k], Lb[s - 1][m][k], acc);
+        if (have) row[m] = acc;
+      }
+    }
+    __syncthreads();
+#ifdef CS_TIMING
+    if (wrec && s < 9) wst[1 + s] = clock64();
+#endif
+  }
+  if (bad && lane == 0 && w == 0) atomicOr(info, 1);
+  // wave w writes columns 8w .. 8w+7 of the factor
+  if (have) {
+#pragma unroll
+    for (int j = 0; j < NB / 4; ++j) {
+      const int m = w * (NB / 4) + j;
+      const double val = Lb[m / BW][lane][m % BW];
+      if (isT) T[r][m] = val;
+      else D[r][m] = (m <= r) ? val : 0.0;
+    }
+  }
+  __syncthreads();
+}
+
+// Flag-synchronised form of the lookahead sweep (CHOL_WG 3): the same stages, but no workgroup barrier
+// per stage.  LDS counters carry the two dependencies instead:
+//   nl = number of factor blocks wave 0 has published (waves 1-3 wait for block t-1 before stage t),
+//   nu[t] = helper waves that have brought block t+1 up to date (wave 0 waits for all 3 before it
+//           starts block t+1).
+__device__ __forceinline__ int lds_poll(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <int BW>
+__device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (*T)[NB + 1],
+                                                   double (*Lb)[2 * NB][BW], double (*Pb)[BW], int* flags,
+                                                   int* info) {
+  constexpr int NS = NB / BW;
+  const int w = threadIdx.x >> 6, lane = lane_id();
+  const bool isT = lane >= NB;
+  const int r = lane & (NB - 1);
+  const bool have = !isT || T != nullptr;
+  double* row = (isT && T) ? T[r] : D[r];
+  int* nl = flags;
+  int* nu = flags + 1;  // [NS]
+  if (threadIdx.x <= NS) flags[threadIdx.x] = 0;
+  __syncthreads();
+#ifdef CS_TIMING
+  long long* wst = g_cs_wg[g_cs_level < 64 ? g_cs_level : 63];
+  const bool wrec = threadIdx.x == 0 && blockIdx.x == 0;
+  if (wrec) wst[0] = clock64();
+#endif
+  if (w == 0) {
+    bool bad = false;
+    double lp[BW];
+#pragma unroll
+    for (int k = 0; k < BW; ++k) lp[k] = 0.0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int kb = s * BW;
+      if (s >= 2) {
+        while (lds_poll(&nu[s - 1]) < 3) __builtin_amdgcn_s_sleep(0);
+      }
+      double a[BW];
+#pragma unroll
+      for (int j = 0; j < BW; ++j) a[j] = row[kb + j];
+      if (s > 0) {
+#pragma unroll
+        for (int j = 0; j < BW; ++j) {
+          double acc = a[j];
+#pragma unroll
+          for (int k = 0; k < BW; ++k) acc = fma(-lp[k], Lb[s - 1][kb + j][k], acc);
+          a[j] = acc;
+        }
+      }
+      if (lane >= kb && lane < kb + BW) {
+#pragma unroll
+        for (int j = 0; j < BW; ++j) Pb[lane - kb][j] = a[j];
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      __builtin_amdgcn_wave_barrier();
+      double P[BW][BW], y[BW];
+#pragma unroll
+      for (int i = 0; i < BW; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) P[i][j] = Pb[i][j];
+#pragma unroll
+      for (int j = 0; j < BW; ++j) {
+        double d = P[j][j];
+        if (!(d > 0.0)) {
+          bad = true;
+          d = 1e-300;
+        }
+        y[j] = rsq_fast(d);
+#pragma unroll
+        for (int i = j + 1; i < BW; ++i) P[i][j] *= y[j];
+#pragma unroll
+        for (int i = j + 1; i < BW; ++i)
+#pragma unroll
+          for (int m = j + 1; m <= i; ++m) P[i][m] = fma(-P[i][j], P[m][j], P[i][m]);
+      }
+#pragma unroll
+      for (int j = 0; j < BW; ++j) {
+        const double x = a[j] * y[j];
+        lp[j] = x;
+#pragma unroll
+        for (int i = j + 1; i < BW; ++i) a[i] = fma(-P[i][j], x, a[i]);
+      }
+#pragma unroll
+      for (int j = 0; j < BW; ++j) Lb[s][lane][j] = lp[j];
+      if (s + 2 < NS) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) __hip_atomic_store(nl, s + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+#ifdef CS_TIMING
+      if (wrec && s < 9) wst[1 + s] = clock64();
+#endif
+    }
+    if (bad && lane == 0) atomicOr(info, 1);
+  } else {
+    // helpers, left-looking: during wave 0's stage t they bring block t+1 up to date with the factor
+    // blocks 0..t-1 (wave 0 adds block t itself), so each block is written once and wave 0 never waits
+    // for bulk updates.  Column m belongs to wave 1 + m % 3.
+    const int u = w - 1;  // 0..2
+    double lr[NS][BW];    // this lane's row of the published factor blocks
+#pragma unroll
+    for (int t = 1; t + 1 < NS; ++t) {
+      const int kb = t * BW;
+      while (lds_poll(nl) < t) __builtin_amdgcn_s_sleep(0);
+#pragma unroll
+      for (int k = 0; k < BW; ++k) lr[t - 1][k] = Lb[t - 1][lane][k];
+#pragma unroll
+      for (int m = kb + BW; m < kb + 2 * BW; ++m) {
+        if (m % 3 != u) continue;
+        double acc = row[m];
+#pragma unroll
+        for (int b = 0; b < t; ++b)
+#pragma unroll
+          for (int k = 0; k < BW; ++k) acc = fma(-lr[b][k], Lb[b][m][k], acc);
+        if (have) row[m] = acc;
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) __hip_atomic_fetch_add(&nu[t], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  __syncthreads();
+  // wave w writes columns 8w .. 8w+7 of the factor
+  if (have) {
+#pragma unroll
+    for (int j = 0; j < NB / 4; ++j) {
+      const int m = w * (NB / 4) + j;
+      const double val = Lb[m / BW][lane][m % BW];
+      if (isT) T[r][m] = val;
+      else D[r][m] = (m <= r) ? val : 0.0;
+    }
+  }
+  __syncthreads();
+}
+
 #ifdef CS_TIMING
 #define CS_STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x == 0 && cs_lvl < 64) g_cs_stamps[cs_lvl][k] = clock64(); } while (0)
 #else
@@ -308,12 +566,18 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   __shared__ double sD[NB][NB + 1];     // diagonal tile -> L_kk
   __shared__ double sA[2][NB][NB + 1];  // L_ip of the two update panels
   __shared__ double sB[2][NB][NB + 1];  // L_kp or L_jp of the two update panels
+#if CHOL_WG < 2
   __shared__ double rdg[NB];
+#endif
 #if !CHOL_WG
   __shared__ __attribute__((aligned(16))) double cb[NB][PB];  // potrf block columns (broadcast reads)
 #endif
-#if CHOL_WG
+#if CHOL_WG == 1
   __shared__ double s_pan[2 * NB][WB + 1], s_mul[2 * NB][WB + 1], s_dg[NB];
+#elif CHOL_WG >= 2
+  __shared__ __attribute__((aligned(16))) double s_lb[NB / LA_BW][2 * NB][LA_BW];
+  __shared__ __attribute__((aligned(16))) double s_pb[LA_BW][LA_BW];
+  __shared__ int s_flags[NB / LA_BW + 1];
 #endif
   const int4 tk = tasks[blockIdx.x];
   const int type = tk.x, i = tk.y, j = tk.z;
@@ -396,7 +660,11 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   __syncthreads();
   CS_STAMP(2);
 #if CHOL_VARIANT != 1
-#if CHOL_WG
+#if CHOL_WG == 3
+  wg_potrf_trsm32_df<LA_BW>(sD, diag_only ? nullptr : sC, s_lb, s_pb, s_flags, info);
+#elif CHOL_WG == 2
+  wg_potrf_trsm32_la<LA_BW>(sD, diag_only ? nullptr : sC, s_lb, s_pb, info);
+#elif CHOL_WG == 1
   wg_potrf_trsm32(sD, diag_only ? nullptr : sC, rdg, s_pan, s_mul, s_dg, info);
 #else
   if (threadIdx.x < WAVE) wave_potrf_trsm32(sD, diag_only ? nullptr : sC, rdg, cb, info);

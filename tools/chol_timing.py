@@ -31,7 +31,7 @@ assert L.ptzba_debug_cs_stamps(buf.ctypes.data) == 0
 wg = buf[64 * 6:].reshape(64, 10)
 buf = buf[:64 * 6].reshape(64, 6)
 nz = np.nonzero(buf[:, 0])[0]
-print("potrf blocks [panel, update] x4 (mean over levels 0..29):", np.diff(wg[:30, :9], axis=1).mean(0).round(0))
+print("potrf stamps, successive differences (mean over levels 0..29):", np.diff(wg[:30, :9], axis=1).mean(0).round(0))
 print(f"{len(nz)} levels, first->last start {buf[nz[-1], 0] - buf[nz[0], 0]} ticks")
 ph = np.diff(buf[nz, :4], axis=1)
 gap = buf[nz[1:], 0] - buf[nz[:-1], 3]
