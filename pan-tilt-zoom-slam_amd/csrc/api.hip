@@ -68,8 +68,8 @@ struct ptzba_ctx {
   std::vector<int> chol_task_off;  // host: per elimination level, offsets into chol_tasks
   int chol_levels = 0, n_aug = 0, n_chain = 1;
   bool nested = false;
-  DBuf frame_pos, row_pad, bs_chain_off, bs_chain_cols, bs_upd_off, bs_upd_tiles;
-  int bs_nupd = 0, bs_npos = 0;
+  DBuf frame_pos, row_pad, bs_chain_off, bs_chain_cols, bs_upd_off, bs_upd_tiles, bs_la_tasks;
+  int bs_nupd = 0, bs_npos = 0, bs_ntasks = 0;
   DBuf xtiles, xbuf;  // packed exchange: tile list, buffer
   int n_xtiles = 0;
   double lambda = 0;
@@ -251,6 +251,8 @@ struct CholPlan {
   std::vector<int32_t> tasks;  // int4 records
   std::vector<int> level_off;
   std::vector<int> chain_off, chain_cols, upd_off, upd_tiles;
+  std::vector<int> la_tasks;  // lookahead back substitution: la [npos] | task_off [n_chain * BS_HELPERS + 1] | tasks
+  int n_tasks = 0;
   std::vector<int32_t> xtiles;  // (ti, tj) pairs the Schur kernel can write (before fill), for the exchange
   int n_levels = 0;
 };
@@ -368,6 +370,27 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
       P.upd_off.push_back((int)P.upd_tiles.size());
     }
   }
+  // lookahead back substitution: the next position's tile when the current row couples to it, and per
+  // (chain, helper wave) the other updates (position, tile j with j % BS_HELPERS == helper) in order
+  const int npos = (int)P.chain_cols.size(), nch = (int)P.chain_off.size() - 1;
+  std::vector<int> la(npos, -1), toff(1, 0), tasks;
+  for (int ch = 0; ch < nch; ++ch)
+    for (int q = P.chain_off[ch]; q + 1 < P.chain_off[ch + 1]; ++q)
+      for (int e = P.upd_off[q]; e < P.upd_off[q + 1]; ++e)
+        if (P.upd_tiles[e] == P.chain_cols[q + 1]) la[q] = P.chain_cols[q + 1];
+  for (int ch = 0; ch < nch; ++ch)
+    for (int hw = 0; hw < BS_HELPERS; ++hw) {
+      for (int q = P.chain_off[ch]; q < P.chain_off[ch + 1]; ++q)
+        for (int e = P.upd_off[q]; e < P.upd_off[q + 1]; ++e) {
+          const int j = P.upd_tiles[e];
+          if (j % BS_HELPERS == hw && j != la[q]) tasks.push_back((q << 16) | j);
+        }
+      toff.push_back((int)tasks.size());
+    }
+  P.n_tasks = (int)tasks.size();
+  P.la_tasks = la;
+  P.la_tasks.insert(P.la_tasks.end(), toff.begin(), toff.end());
+  P.la_tasks.insert(P.la_tasks.end(), tasks.begin(), tasks.end());
   return true;
 }
 
@@ -607,13 +630,16 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     return -1;
   if (upload(h->chol_tasks, plan.tasks) || upload(h->frame_pos, sorder.pos) || upload(h->row_pad, sorder.pad) ||
       upload(h->bs_chain_off, plan.chain_off) || upload(h->bs_chain_cols, plan.chain_cols) ||
-      upload(h->bs_upd_off, plan.upd_off) || upload(h->bs_upd_tiles, plan.upd_tiles) || upload(h->xtiles, plan.xtiles))
+      upload(h->bs_upd_off, plan.upd_off) || upload(h->bs_upd_tiles, plan.upd_tiles) || upload(h->xtiles, plan.xtiles) ||
+      upload(h->bs_la_tasks, plan.la_tasks))
     return -1;
   h->n_xtiles = (int)(plan.xtiles.size() / 2);
   h->bs_nupd = (int)plan.upd_tiles.size();
   h->bs_npos = (int)plan.chain_cols.size();
+  h->bs_ntasks = plan.n_tasks;
   // the back-substitution keeps r and its update lists in LDS (plus ~9 KiB of static staging)
-  if (h->ld * 8 + (h->bs_npos + 1 + h->bs_nupd) * 4 > 150 * 1024)
+  // (lookahead form: + 48 KiB ring of M / L blocks)
+  if (h->ld * 8 + (std::max(h->bs_npos + 1 + h->bs_nupd, 2 * h->bs_npos + h->bs_ntasks)) * 4 > 100 * 1024)
     return fail("reduced system %d too large for the dense solver's back-substitution", h->n_sys);
   h->xbuf.release();  // allocated on first ptzba_exchange_packed
   HIPCHK(hipMemset(h->D_pose.p, 0, h->D_pose.bytes));
@@ -820,6 +846,7 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx) {
                   h->Ldiag.as<double>(), h->info.as<int>(), h->st);
   launch_chol_backsolve(h->S(), h->ld, h->n_aug, h->n_chain, h->bs_npos, h->bs_chain_off.as<int>(),
                         h->bs_chain_cols.as<int>(), h->bs_upd_off.as<int>(), h->bs_upd_tiles.as<int>(), h->bs_nupd,
+                        h->bs_la_tasks.as<int>(), h->bs_ntasks,
                         h->Ldiag.as<double>(), h->Minv.as<double>(), h->dpose.as<double>(), h->st);
   tm_end(h, TM_CHOL);
   HIPCHK(hipGetLastError());

@@ -26,6 +26,9 @@
 namespace ptzba {
 
 constexpr int NB = CHOL_NB;
+#ifndef BS_LA
+#define BS_LA 1  // 1: lookahead back substitution (k_chol_backsolve_la), 0: barrier per column
+#endif
 constexpr double AUG_DIAG = 1e300;
 
 __device__ __forceinline__ double bcast(double v, int j) {
@@ -425,6 +428,21 @@ __device__ __forceinline__ void wg_potrf_trsm32_la(double (*D)[NB + 1], double (
 //           starts block t+1).
 __device__ __forceinline__ int lds_poll(const int* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// LDS-only hand-off between waves of one workgroup without release/acquire semantics (those also wait
+// for the wave's outstanding global loads, i.e. for its prefetches): the producer waits for its own LDS
+// writes (lgkmcnt) and stores the counter; the consumer polls it and its later LDS reads stay behind
+// the poll (LDS operations of a wave execute in order; compiler barrier against reordering).
+__device__ __forceinline__ void lds_signal(int* p, int v) {
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  if (lane_id() == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait_ge(const int* p, int v, int sleep) {
+  while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < v) {
+    if (sleep) __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");
 }
 template <int BW>
 __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (*T)[NB + 1],
@@ -832,6 +850,176 @@ __global__ __launch_bounds__(1024) void k_chol_backsolve(const double* __restric
   if (threadIdx.x == 0) g_bs_edges[blockIdx.x & 1][2] = clock64();
 #endif
 }
+// Back substitution with a lookahead chain wave (BS_LA, default).  Same data and result as
+// k_chol_backsolve, no workgroup barrier in the column loop:
+//   * wave 0 walks the chain: x_kt = M_kt^T r_kt, publishes x (LDS counter xcnt), then at once forms the
+//     contribution of x_kt to the NEXT column's right-hand side (L_kt,next^T x_kt, in registers), so
+//     the next solve waits only for the older contributions;
+//   * the BS_HELPERS other waves own the right-hand-side tiles (tile j -> helper j % BS_HELPERS) and
+//     apply every other update r_j -= L_kt,j^T x_kt, walking a host-built task list (position, tile) in
+//     column order with the L tiles of the next two tasks in flight, and publish their progress
+//     (prog[w] = first column not yet done);
+//   * before solving position q the chain wave waits until the owner of its tile has finished the
+//     columns up to q-2 (column q-1's part is the lookahead).
+// Each r_j is summed in a fixed order (owner's columns in order, then the lookahead): deterministic.
+// A loader wave streams each position's M and lookahead L blocks into an LDS ring up to 3 positions
+// ahead, so the chain wave issues no global loads.
+// la_tasks = [lookahead tile per position (-1: none) | task offsets per (chain, helper) | tasks q<<16|j].
+__global__ __launch_bounds__(64 * (BS_HELPERS + 2)) void k_chol_backsolve_la(
+    const double* __restrict__ L, int64_t ld, int n, const int* __restrict__ chain_off,
+    const int* __restrict__ chain_cols, const int* __restrict__ la_tasks, const double* __restrict__ Ldiag,
+    const double* __restrict__ Minv, double* __restrict__ xout) {
+  constexpr int NH = BS_HELPERS, RING = 3;
+  extern __shared__ __attribute__((aligned(16))) double xv[];  // [ld] r / x | cols [nq] | la [nq] | tasks (int)
+  __shared__ int s_xcnt, s_prog[NH], s_toff[NH + 1], s_ready, s_cdone;
+  __shared__ double s_ring[RING][2][NB * NB];  // M_kt | L_kt,next of the chain's coming positions
+  const int nq = chain_off[gridDim.x];
+  const int* toff_g = la_tasks + nq;
+  const int* task_g = toff_g + gridDim.x * NH + 1;
+  int* s_cc = reinterpret_cast<int*>(xv + ld);
+  int* s_la = s_cc + nq;
+  int* s_task = s_la + nq;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int c = lane & 31, h = lane >> 5;  // column of the tile, row half
+#ifdef BS_TIMING
+  if (t == 0) g_bs_edges[blockIdx.x & 1][0] = clock64();
+#define BSL_STAMP(q, k) do { if (t == 0 && (q) - q0 < 128) g_bs_stamps[blockIdx.x & 1][(q) - q0][k] = clock64(); } while (0)
+#else
+#define BSL_STAMP(q, k) do { } while (0)
+#endif
+  const int tn = n / NB, rn = n - tn * NB;
+  const int q0 = chain_off[blockIdx.x], q1 = chain_off[blockIdx.x + 1];
+  const int tb = toff_g[blockIdx.x * NH], te = toff_g[blockIdx.x * NH + NH];
+  for (int i = t; i < ld; i += blockDim.x)
+    xv[i] = (i >= n) ? 0.0 : (i < tn * NB ? L[(int64_t)n * ld + i] : Ldiag[((int64_t)tn * NB + rn) * NB + (i - tn * NB)]);
+  for (int i = t; i < nq; i += blockDim.x) {
+    s_cc[i] = chain_cols[i];
+    s_la[i] = la_tasks[i];
+  }
+  for (int i = t; i < te - tb; i += blockDim.x) s_task[i] = task_g[tb + i];
+  if (t <= NH) s_toff[t] = toff_g[blockIdx.x * NH + t] - tb;
+  if (t == 0) {
+    s_xcnt = q0;
+    s_ready = q0;
+    s_cdone = q0;
+  }
+  if (t < NH) {  // columns before a helper's first task are trivially done
+    const int k0 = toff_g[blockIdx.x * NH + t], k1 = toff_g[blockIdx.x * NH + t + 1];
+    s_prog[t] = k0 < k1 ? (task_g[k0] >> 16) : q1;
+  }
+  __syncthreads();
+#ifdef BS_TIMING
+  if (t == 0) g_bs_edges[blockIdx.x & 1][1] = clock64();
+#endif
+  if (wv == 0) {
+    double la_c = 0.0;  // lookahead contribution to the current tile's r (column c)
+    for (int q = q0; q < q1; ++q) {
+      const int kt = s_cc[q];
+      const int64_t c0 = (int64_t)kt * NB;
+      const double* sm = s_ring[(q - q0) % RING][0];
+      const double* sl = s_ring[(q - q0) % RING][1];
+      BSL_STAMP(q, 0);
+      // this position's M and L blocks from the ring into registers first: the reads overlap the wait
+      // for the owner of the tile
+      lds_wait_ge(&s_ready, q + 1, 0);
+      BSL_STAMP(q, 1);
+      double mv[NB / 2], lv[NB / 2];
+#pragma unroll
+      for (int i = 0; i < NB / 2; ++i) {
+        mv[i] = sm[(h * (NB / 2) + i) * NB + c];
+        lv[i] = sl[(h * (NB / 2) + i) * NB + c];
+      }
+      lds_wait_ge(&s_prog[kt % NH], q - 1, 0);
+      BSL_STAMP(q, 2);
+      const double r = xv[c0 + c] - la_c;
+      if (h == 0) xv[c0 + c] = r;
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      double s4[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int i = 0; i < NB / 2; ++i)
+        s4[i & 3] = fma(mv[i], xv[c0 + h * (NB / 2) + i], s4[i & 3]);
+      double xs = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+      xs += __shfl_xor(xs, 32, WAVE);
+      if (h == 0) {
+        xv[c0 + c] = xs;
+        if (c0 + c < n) xout[c0 + c] = xs;
+      }
+      lds_signal(&s_xcnt, q + 1);
+      BSL_STAMP(q, 3);
+      la_c = 0.0;
+      if (s_la[q] >= 0) {
+        double u4[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < NB / 2; ++i)
+          u4[i & 3] = fma(lv[i], xv[c0 + h * (NB / 2) + i], u4[i & 3]);
+        la_c = (u4[0] + u4[1]) + (u4[2] + u4[3]);
+        la_c += __shfl_xor(la_c, 32, WAVE);
+      }
+      lds_signal(&s_cdone, q + 1);  // ring slot free
+      BSL_STAMP(q, 4);
+    }
+#ifdef BS_TIMING
+    if (t == 0) g_bs_edges[blockIdx.x & 1][2] = clock64();
+#endif
+  } else if (wv == NH + 1) {
+    // loader: M_kt and L_kt,next of position q into ring slot (q - q0) % RING, up to RING positions ahead
+    for (int q = q0; q < q1; ++q) {
+      lds_wait_ge(&s_cdone, q - RING + 1, 1);
+      const int kt = s_cc[q], la = max(s_la[q], 0);
+      double vm[NB * NB / WAVE], vl[NB * NB / WAVE];
+#pragma unroll
+      for (int i = 0; i < NB * NB / WAVE; ++i) {
+        const int e = lane + WAVE * i;
+        vm[i] = Minv[(int64_t)kt * NB * NB + e];
+        vl[i] = L[((int64_t)kt * NB + (e >> 5)) * ld + (int64_t)la * NB + (e & 31)];
+      }
+      double* sm = s_ring[(q - q0) % RING][0];
+      double* sl = s_ring[(q - q0) % RING][1];
+#pragma unroll
+      for (int i = 0; i < NB * NB / WAVE; ++i) {
+        sm[lane + WAVE * i] = vm[i];
+        sl[lane + WAVE * i] = vl[i];
+      }
+      lds_signal(&s_ready, q + 1);
+    }
+  } else {
+    const int me = wv - 1, k0 = s_toff[me], k1 = s_toff[me + 1];
+    if (k0 < k1) {
+      double tA[NB / 2], tB[NB / 2];
+      auto fetch = [&](int k, double (&lt)[NB / 2]) {  // L_kt,j of task k (clamped)
+        const int tk = s_task[min(k, k1 - 1)], kt = s_cc[tk >> 16], j = tk & 0xffff;
+        const double* lp = L + ((int64_t)kt * NB + h * (NB / 2)) * ld + (int64_t)j * NB + c;
+#pragma unroll
+        for (int i = 0; i < NB / 2; ++i) lt[i] = lp[(int64_t)i * ld];
+      };
+      auto run = [&](int k, const double (&lt)[NB / 2]) {
+        const int tk = s_task[k], q = tk >> 16, j = tk & 0xffff;
+        const int64_t c0 = (int64_t)s_cc[q] * NB;
+        lds_wait_ge(&s_xcnt, q + 1, 1);
+        double s4[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < NB / 2; ++i) s4[i & 3] = fma(lt[i], xv[c0 + h * (NB / 2) + i], s4[i & 3]);
+        double sacc = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+        sacc += __shfl_xor(sacc, 32, WAVE);
+        if (h == 0) xv[(int64_t)j * NB + c] -= sacc;
+        const int qn = k + 1 < k1 ? (s_task[k + 1] >> 16) : q1;
+        if (qn > q) {
+          lds_signal(&s_prog[me], qn);
+        }
+      };
+      fetch(k0, tA);
+      for (int k = k0; k < k1; k += 2) {
+        fetch(k + 1, tB);
+        run(k, tA);
+        if (k + 1 >= k1) break;
+        fetch(k + 2, tA);
+        run(k + 1, tB);
+      }
+    }
+  }
+}
+
 #ifdef CS_TIMING
 extern "C" int ptzba_debug_cs_stamps(long long* out) {
   const int zero = 0;
@@ -849,12 +1037,19 @@ extern "C" int ptzba_debug_bs_stamps(long long* out) {
 
 void launch_chol_backsolve(const double* L, int64_t ld, int n, int n_chain, int n_pos, const int* chain_off,
                            const int* chain_cols, const int* upd_off, const int* upd_tiles, int n_upd,
-                           const double* Ldiag, double* Minv, double* xout, hipStream_t st) {
+                           const int* la_tasks, int n_tasks, const double* Ldiag, double* Minv, double* xout,
+                           hipStream_t st) {
   const int tx = (n + NB - 1) / NB;
   hipLaunchKernelGGL(k_tile_inv, dim3(tx), dim3(64), 0, st, Ldiag, Minv);
+#if BS_LA
+  const size_t lds = (size_t)ld * sizeof(double) + (size_t)(2 * n_pos + n_tasks) * sizeof(int);
+  hipLaunchKernelGGL(k_chol_backsolve_la, dim3(n_chain), dim3(64 * (BS_HELPERS + 2)), lds, st, L, ld, n, chain_off,
+                     chain_cols, la_tasks, Ldiag, Minv, xout);
+#else
   const size_t lds = (size_t)ld * sizeof(double) + (size_t)(n_pos + 1 + n_upd) * sizeof(int);
   hipLaunchKernelGGL(k_chol_backsolve, dim3(n_chain), dim3(1024), lds, st, L, ld, n, chain_off, chain_cols, upd_off,
                      upd_tiles, n_upd, Ldiag, Minv, xout);
+#endif
 }
 
 // packed exchange: the lower tiles the Schur kernel can write (xt[k] = (ti, tj)) and the three

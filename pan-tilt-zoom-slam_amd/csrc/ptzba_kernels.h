@@ -122,9 +122,13 @@ constexpr int CHOL_NB = 32;
 void launch_chol_prepare(double* A, int64_t ld, int n, double* b, const uint8_t* pad, int* info, hipStream_t st);
 void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_off_host, int n_launch, double* Ldiag,
                      int* info, hipStream_t st);
+// la_tasks: lookahead back substitution's [lookahead tile per position | task offsets per (chain, helper) |
+// tasks q << 16 | tile], built by the host plan (api.hip make_plan)
+constexpr int BS_HELPERS = 7;
 void launch_chol_backsolve(const double* L, int64_t ld, int n, int n_chain, int n_pos, const int* chain_off,
                            const int* chain_cols, const int* upd_off, const int* upd_tiles, int n_upd,
-                           const double* Ldiag, double* Minv, double* xout, hipStream_t st);
+                           const int* la_tasks, int n_tasks, const double* Ldiag, double* Minv, double* xout,
+                           hipStream_t st);
 // packed exchange of the Schur-written tiles + b | g_pose | dU (vec = b, contiguous 3 ld doubles)
 void launch_pack_exchange(double* S, int64_t ld, const int2* xt, int n_tiles, double* vec, double* buf, int unpack,
                           hipStream_t st);

@@ -33,6 +33,10 @@ for ch in range(2):
         continue
     tot = buf[ch, nz[-1], 5] - buf[ch, nz[0], 0]
     print(f"chain {ch}: {len(nz)} columns, {tot} cycles total")
-    print("   mean per column [barrier1, solve, barrier2, update, prefetch]:", d[nz].mean(0).round(0))
+    print("   mean per column, successive stamp differences:", d[nz].mean(0).round(0),
+          "(k_chol_backsolve: barrier1, solve, barrier2, update, prefetch; k_chol_backsolve_la: ring wait,"
+          " M/L reads + owner wait, solve + publish, lookahead)")
+    st = buf[ch, nz, 0]
+    print("   mean start-to-start per column:", np.diff(st).mean().round(0))
     for q in nz[:6]:
         print("   ", q, d[q])
