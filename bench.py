@@ -67,14 +67,14 @@ def shard_by_landmark(landmark, n_landmark, rank, world):
 
 def algorithmic_bytes_k1(info, precision, weighted):
     """Bytes one K1 (k_linearize) launch must move with this data layout (DESIGN.md §4 Roofline):
-      per record : obs delta x,y (2 reals) + segment id (int32) [+ weight real]
+      per record : obs delta x,y (2 reals) + 1-byte segment key [+ weight real]
       per segment: frame id read in phase A and C (2 x 4 B), record offset (int64), base obs (2 fp64),
                    U|g_pose block out (12 reals), W+frame out (8 reals)
       per landmark (active): work-order id + CSR bounds (12 B), ray tables (8 reals + 8 fp64),
                    8-double output
       per frame  : frame tables (8 reals + 8 fp64)"""
     s = 4 if precision == "fp32" else 8
-    rec = 2 * s + 4 + (s if weighted else 0)
+    rec = 2 * s + 1 + (s if weighted else 0)
     seg = 4 + 4 + 8 + 16 + 12 * s + 8 * s
     lm = 12 + 8 * s + 64 + 64
     return (info["n_obs"] * rec + info["n_segments"] * seg + info["n_active_landmarks"] * lm +

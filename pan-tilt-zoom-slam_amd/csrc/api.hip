@@ -47,7 +47,7 @@ struct ptzba_ctx {
   std::vector<int64_t> perm_host;  // sorted -> original record index
   bool perm_uploaded = false;
   // device: structure
-  DBuf rec_xy, rec_seg, rec_w, perm;
+  DBuf rec_xy, rec_seg, rec_w, perm, rec_key;
   DBuf seg_frame, seg_lm, seg_rec_begin, lm_seg_begin, lm_order;
   DBuf frame_seg_begin, frame_seg_list, frame_win_hi;
   DBuf s2_items, s2_groups, s2_lm, lm_meta;  // K2 work items / tiles / lists, slot ranges
@@ -605,6 +605,14 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
                                       : upload_records<double>(h, order, rec_seg, seg_base, obs_xy, obs_weight);
   if (rc) return rc;
   if (upload(h->seg_base, seg_base)) return -1;
+  {  // K1's 1-byte segment key: the record's segment within its landmark's window of K1_SEGW segments
+    std::vector<uint8_t> key(n_obs);
+    for (int64_t k = 0; k < n_obs; ++k) {
+      const int32_t sg = rec_seg[k];
+      key[k] = (uint8_t)((sg - lm_seg_begin[seg_lm[sg]]) % K1_SEGW);
+    }
+    if (upload(h->rec_key, key)) return -1;
+  }
   if (upload(h->rec_seg, rec_seg) || upload(h->seg_frame, seg_frame) || upload(h->seg_lm, seg_lm) ||
       upload(h->seg_rec_begin, seg_rec_begin) || upload(h->lm_seg_begin, lm_seg_begin) ||
       upload(h->lm_order, lm_work) || upload(h->frame_seg_begin, frame_seg_begin) ||
@@ -701,6 +709,7 @@ static void linearize_into(ptzba_ctx* h, int slot, const int* run_if = nullptr) 
   a.seg_frame = h->seg_frame.as<int32_t>();
   a.seg_rec_begin = h->seg_rec_begin.as<int64_t>();
   a.rec_seg = h->rec_seg.as<int32_t>();
+  a.rec_key = h->rec_key.as<uint8_t>();
   a.rec_xy = h->rec_xy.p;
   a.rec_w = h->weighted ? h->rec_w.p : nullptr;
   a.ft = ft_real(h);

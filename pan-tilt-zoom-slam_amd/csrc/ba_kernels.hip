@@ -70,10 +70,15 @@ void launch_tables(const double* ptz, const double* rays, int n_pose, int n_lm, 
 // ------------------------------------------------------------------------------------------------
 // K1: linearize (residual + Jacobian + per-segment / per-landmark normal-equation blocks + cost)
 // ------------------------------------------------------------------------------------------------
-constexpr int SEGW = 128;    // segments per LDS window per wave
-constexpr int K1_UNROLL = 4;  // record batches in flight per wave
+constexpr int SEGW = K1_SEGW;  // segments per LDS window per wave
+#ifndef K1_UNROLL
+#define K1_UNROLL 3  // record batches per group (two groups in flight per wave)
+#endif
+#ifndef K1_FTV
+#define K1_FTV 1  // phase-C frame tables loaded during phase A
+#endif
 #ifndef K1_MIN_WAVES
-#define K1_MIN_WAVES 5  // waves per SIMD the register budget must allow (occupancy)
+#define K1_MIN_WAVES 4  // waves per SIMD the register budget must allow (occupancy)
 #endif
 
 // ---- DPP lane shuffles (VALU, no LDS round trip).  Lanes whose source is out of range or whose row
@@ -149,14 +154,97 @@ __global__ __launch_bounds__(256, K1_MIN_WAVES) void k_linearize(LinArgs a) {
 
   double V00 = 0, V01 = 0, V11 = 0, g0 = 0, g1 = 0, cost = 0;
 
+  // phase B record group: K1_UNROLL batches of 64 records (1-byte segment key, obs delta x, y, weight).
+  // Loads are unconditional (index clamped to the window), validity is recomputed where the group is
+  // consumed: a conditional load would merge at a join and force its wait early.
+  struct Grp {
+    int key[K1_UNROLL];
+    real ox[K1_UNROLL], oy[K1_UNROLL], wt[K1_UNROLL];
+  };
+  auto load_grp = [&](Grp& g, int64_t rb, int64_t r1) {
+#pragma unroll
+    for (int u = 0; u < K1_UNROLL; ++u) {
+      const int64_t r = min(rb + u * WAVE + lane, r1 - 1);
+      g.key[u] = a.rec_key[r];
+      if constexpr (sizeof(real) == 4) {
+        const float2 o = reinterpret_cast<const float2*>(rec_xy)[r];
+        g.ox[u] = o.x; g.oy[u] = o.y;
+      } else {
+        const double2 o = reinterpret_cast<const double2*>(rec_xy)[r];
+        g.ox[u] = o.x; g.oy[u] = o.y;
+      }
+      g.wt[u] = rec_w ? rec_w[r] : (real)1;
+    }
+  };
+  auto consume = [&](const Grp& g, int64_t rb, int64_t r1) {
+#pragma unroll
+    for (int u = 0; u < K1_UNROLL; ++u) {
+      if (rb + u * WAVE >= r1) break;  // wave-uniform
+      const bool valid = rb + u * WAVE + lane < r1;
+      const int key = valid ? g.key[u] : -1;
+      real rx = 0, ry = 0;
+      if (valid) {
+        rx = sx[key] - g.ox[u];
+        ry = sy[key] - g.oy[u];
+      }
+      const real wt = valid ? g.wt[u] : (real)0;
+      real wx, wy, c;
+      if constexpr (LOSS == 0) {
+        wx = wt; wy = wt;
+        c = wt * (rx * rx + ry * ry);
+      } else {
+        // scipy 'huber': rho(z) = z (z<=1), 2 sqrt(z) - 1; weight rho'(z) = 1 or 1/sqrt(z)
+        real zx = rx * rx * ifs2, zy = ry * ry * ifs2;
+        bool ix = zx <= (real)1, iy = zy <= (real)1;
+        real sqx, sqy;
+        if constexpr (sizeof(real) == 4) {  // v_rsq_f32: 1 ulp, no IEEE divide in the record loop
+          const real rsx = __builtin_amdgcn_rsqf(ix ? (real)1 : zx), rsy = __builtin_amdgcn_rsqf(iy ? (real)1 : zy);
+          sqx = zx * rsx; sqy = zy * rsy;
+          wx = ix ? wt : wt * rsx;
+          wy = iy ? wt : wt * rsy;
+        } else {
+          sqx = sqrt(zx); sqy = sqrt(zy);
+          wx = ix ? wt : wt / sqx;
+          wy = iy ? wt : wt / sqy;
+        }
+        c = wt * fs2 * ((ix ? zx : (real)2 * sqx - (real)1) + (iy ? zy : (real)2 * sqy - (real)1));
+      }
+      cost += (double)c;
+      real v0 = wx, v1 = wy, v2 = wx * rx, v3 = wy * ry;
+      // segmented inclusive scan over the wave, segments = runs of equal key (records are sorted):
+      // shifts 1, 2, 4, 8 inside each 16-lane row, then row 15 -> rows 1, 3 and lane 31 -> rows 2, 3
+      const int kenc = key + 2;  // >= 1; 0 is what a masked / out-of-row DPP source reads
+      seg_scan_step<DPP_ROW_SHR1, 0xf>(kenc, v0, v1, v2, v3);
+      seg_scan_step<DPP_ROW_SHR2, 0xf>(kenc, v0, v1, v2, v3);
+      seg_scan_step<DPP_ROW_SHR4, 0xf>(kenc, v0, v1, v2, v3);
+      seg_scan_step<DPP_ROW_SHR8, 0xf>(kenc, v0, v1, v2, v3);
+      seg_scan_step<DPP_ROW_BCAST15, 0xa>(kenc, v0, v1, v2, v3);
+      seg_scan_step<DPP_ROW_BCAST31, 0xc>(kenc, v0, v1, v2, v3);
+      const int knext = dpp_i<DPP_WAVE_SHL1, 0xf>(kenc);  // lane 63 reads 0
+      const bool last = knext != kenc;
+      if (valid && last) {  // one writer per run per batch; runs crossing batches add in order
+        acc0[key] += v0; acc1[key] += v1; acc2[key] += v2; acc3[key] += v3;
+      }
+    }
+  };
+
   for (int w0 = s0; w0 < s1; w0 += SEGW) {
     const int w1 = min(s1, w0 + SEGW);
     const int64_t r0 = (w0 == s0) ? (int64_t)(uint32_t)wd.w : a.seg_rec_begin[w0];
     const int64_t r1 = a.seg_rec_begin[w1];
+    // the window's first record group is requested before phase A: its latency overlaps the projections
+    Grp ga, gb;
+    load_grp(ga, r0, r1);
     // phase A: fp64 projection of every segment of the window (lanes over segments), kept as the
     // offset from the segment's base observation so phase B works on O(residual) magnitudes.  The
-    // frame ids stay in registers for phase C.
+    // frame ids and the phase-C frame tables stay in registers.
     int fsv[SEGW / WAVE];
+    FrameTab<real> ftv[SEGW / WAVE];
+#if K1_FTV
+#define K1_FTV_PREFETCH(i) ftv[i] = ft[fsv[i]]
+#else
+#define K1_FTV_PREFETCH(i) (void)0
+#endif
 #pragma unroll
     for (int i = 0; i < SEGW / WAVE; ++i) {
       const int s = w0 + lane + i * WAVE;
@@ -172,79 +260,17 @@ __global__ __launch_bounds__(256, K1_MIN_WAVES) void k_linearize(LinArgs a) {
         sy[sl] = (real)(y - bs.y);
         acc0[sl] = 0; acc1[sl] = 0; acc2[sl] = 0; acc3[sl] = 0;
       }
+      K1_FTV_PREFETCH(i);
     }
     wave_lds_fence();
-    // phase B: stream the window's records (coalesced), segmented reduction into LDS.  Four 64-record
-    // batches are loaded before any is consumed, so each wave keeps 4x the bytes in flight.
-    for (int64_t rb = r0; rb < r1; rb += K1_UNROLL * WAVE) {
-      int keyu[K1_UNROLL];
-      real oxu[K1_UNROLL], oyu[K1_UNROLL], wtu[K1_UNROLL];
-#pragma unroll
-      for (int u = 0; u < K1_UNROLL; ++u) {
-        const int64_t r = rb + u * WAVE + lane;
-        keyu[u] = -1;
-        oxu[u] = 0; oyu[u] = 0; wtu[u] = 0;
-        if (r < r1) {
-          keyu[u] = a.rec_seg[r] - w0;
-          if constexpr (sizeof(real) == 4) {
-            const float2 o = reinterpret_cast<const float2*>(rec_xy)[r];
-            oxu[u] = o.x; oyu[u] = o.y;
-          } else {
-            const double2 o = reinterpret_cast<const double2*>(rec_xy)[r];
-            oxu[u] = o.x; oyu[u] = o.y;
-          }
-          wtu[u] = rec_w ? rec_w[r] : (real)1;
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < K1_UNROLL; ++u) {
-        if (rb + u * WAVE >= r1) break;  // wave-uniform
-        const int key = keyu[u];
-        const bool valid = key >= 0;
-        real rx = 0, ry = 0;
-        if (valid) {
-          rx = sx[key] - oxu[u];
-          ry = sy[key] - oyu[u];
-        }
-        const real wt = wtu[u];
-        real wx, wy, c;
-        if constexpr (LOSS == 0) {
-          wx = wt; wy = wt;
-          c = wt * (rx * rx + ry * ry);
-        } else {
-          // scipy 'huber': rho(z) = z (z<=1), 2 sqrt(z) - 1; weight rho'(z) = 1 or 1/sqrt(z)
-          real zx = rx * rx * ifs2, zy = ry * ry * ifs2;
-          bool ix = zx <= (real)1, iy = zy <= (real)1;
-          real sqx, sqy;
-          if constexpr (sizeof(real) == 4) {  // v_rsq_f32: 1 ulp, no IEEE divide in the record loop
-            const real rsx = __builtin_amdgcn_rsqf(ix ? (real)1 : zx), rsy = __builtin_amdgcn_rsqf(iy ? (real)1 : zy);
-            sqx = zx * rsx; sqy = zy * rsy;
-            wx = ix ? wt : wt * rsx;
-            wy = iy ? wt : wt * rsy;
-          } else {
-            sqx = sqrt(zx); sqy = sqrt(zy);
-            wx = ix ? wt : wt / sqx;
-            wy = iy ? wt : wt / sqy;
-          }
-          c = wt * fs2 * ((ix ? zx : (real)2 * sqx - (real)1) + (iy ? zy : (real)2 * sqy - (real)1));
-        }
-        cost += (double)c;
-        real v0 = wx, v1 = wy, v2 = wx * rx, v3 = wy * ry;
-        // segmented inclusive scan over the wave, segments = runs of equal key (records are sorted):
-        // shifts 1, 2, 4, 8 inside each 16-lane row, then row 15 -> rows 1, 3 and lane 31 -> rows 2, 3
-        const int kenc = key + 2;  // >= 1; 0 is what a masked / out-of-row DPP source reads
-        seg_scan_step<DPP_ROW_SHR1, 0xf>(kenc, v0, v1, v2, v3);
-        seg_scan_step<DPP_ROW_SHR2, 0xf>(kenc, v0, v1, v2, v3);
-        seg_scan_step<DPP_ROW_SHR4, 0xf>(kenc, v0, v1, v2, v3);
-        seg_scan_step<DPP_ROW_SHR8, 0xf>(kenc, v0, v1, v2, v3);
-        seg_scan_step<DPP_ROW_BCAST15, 0xa>(kenc, v0, v1, v2, v3);
-        seg_scan_step<DPP_ROW_BCAST31, 0xc>(kenc, v0, v1, v2, v3);
-        const int knext = dpp_i<DPP_WAVE_SHL1, 0xf>(kenc);  // lane 63 reads 0
-        const bool last = knext != kenc;
-        if (valid && last) {  // one writer per run per batch; runs crossing batches add in order
-          acc0[key] += v0; acc1[key] += v1; acc2[key] += v2; acc3[key] += v3;
-        }
-      }
+    // phase B: stream the window's records (coalesced), segmented reduction into LDS.  Two register
+    // groups alternate: the next group's loads are in flight while the current one is consumed.
+    for (int64_t rb = r0; rb < r1; rb += 2 * K1_UNROLL * WAVE) {
+      load_grp(gb, rb + K1_UNROLL * WAVE, r1);
+      consume(ga, rb, r1);
+      if (rb + K1_UNROLL * WAVE >= r1) break;
+      load_grp(ga, rb + 2 * K1_UNROLL * WAVE, r1);
+      consume(gb, rb + K1_UNROLL * WAVE, r1);
     }
     wave_lds_fence();
     // phase C: per-segment Jacobian and normal-equation blocks
@@ -255,7 +281,11 @@ __global__ __launch_bounds__(256, K1_MIN_WAVES) void k_linearize(LinArgs a) {
       const int sl = s - w0;
       real x, y, J[2][5];
       const int fs = fsv[i];
+#if K1_FTV
+      ptz_project_jac<real>(ftv[i], R, u, v, x, y, J);
+#else
       ptz_project_jac<real>(ft[fs], R, u, v, x, y, J);
+#endif
       const real Sx = acc0[sl], Sy = acc1[sl], Srx = acc2[sl], Sry = acc3[sl];
       // W = Jp^T diag(Sx,Sy) Jr (3x2), U = Jp^T diag Jp (upper: 00 01 02 11 12 22), g_pose = Jp^T (w r)
       real W[6];

@@ -5,6 +5,7 @@
 
 namespace ptzba {
 
+constexpr int K1_SEGW = 128;  // K1 segments per LDS window per wave
 struct LinArgs {
   const int4* lm_work;           // [n_work] {landmark, s0, s1, first record}, heaviest first
   int n_work;
@@ -12,6 +13,7 @@ struct LinArgs {
   const int32_t* seg_frame;      // [n_seg]
   const int64_t* seg_rec_begin;  // [n_seg+1]
   const int32_t* rec_seg;        // [n_rec]
+  const uint8_t* rec_key;        // [n_rec] segment - first segment of the landmark, mod K1_SEGW
   const void* rec_xy;            // [2 n_rec] real
   const void* rec_w;             // [n_rec] real or nullptr
   const void* ft;                // FrameTab<real>[n_pose]
