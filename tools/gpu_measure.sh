@@ -7,11 +7,12 @@ TAG=${TAG:-r01}
 mkdir -p gpurun_out
 timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/${TAG}_gpu_tests.log 2>&1 || { echo TESTFAIL; tail -30 gpurun_out/${TAG}_gpu_tests.log; exit 1; }
 tail -2 gpurun_out/${TAG}_gpu_tests.log
-timeout -k 10 400 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { echo BENCHFAIL; tail gpurun_out/${TAG}_bench.err; exit 1; }
-cat gpurun_out/${TAG}_bench.json
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 BARGS="--steps 20 --warmup 3 --no-cpu-baseline --no-accuracy"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof_stats -o run --output-format csv -- python bench.py $BARGS > gpurun_out/${TAG}_prof_stats.log 2>&1 || { echo PROFFAIL; tail gpurun_out/${TAG}_prof_stats.log; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/${TAG}_pmc_fetch -o run --output-format csv -- python bench.py $BARGS > gpurun_out/${TAG}_pmc_fetch.log 2>&1 || { echo PMCFAIL; tail gpurun_out/${TAG}_pmc_fetch.log; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/${TAG}_pmc_write -o run --output-format csv -- python bench.py $BARGS > gpurun_out/${TAG}_pmc_write.log 2>&1 || { echo PMCFAIL; tail gpurun_out/${TAG}_pmc_write.log; exit 1; }
-find gpurun_out/${TAG}_prof_stats gpurun_out/${TAG}_pmc_fetch gpurun_out/${TAG}_pmc_write -name "*.csv" | head -20
+# the bench line's traffic field comes from this run's PMC passes
+python tools/pmc_traffic.py gpurun_out/${TAG}_pmc_fetch gpurun_out/${TAG}_pmc_write k_linearize config3/pair/fp32/huber gpurun_out/${TAG}_k1_traffic.json > /dev/null || { echo TRAFFICFAIL; exit 1; }
+timeout -k 10 400 python bench.py --traffic-json gpurun_out/${TAG}_k1_traffic.json > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { echo BENCHFAIL; tail gpurun_out/${TAG}_bench.err; exit 1; }
+cat gpurun_out/${TAG}_bench.json
