@@ -232,8 +232,8 @@ def main():
                         cost_fp32=r32.cost, cost_fp64=r64.cost, iters_fp32=r32.njev, iters_fp64=r64.njev,
                         components=["pan_deg", "tilt_deg", "f_px"])
 
-    traffic = None
-    if os.path.exists(a.traffic_json):
+    traffic = None  # PMC passes are taken on the whole problem (N = 1); a shard's launch moves less
+    if world == 1 and os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
             key = f"{a.config}/{a.form}/{a.precision}/{a.loss}"
