@@ -503,7 +503,6 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     std::vector<std::vector<int32_t>> tiles;
     std::vector<int32_t> tile_key;
     std::vector<int32_t> un;
-    int64_t total = 0;
     for (int f1b = o.n_fixed; f1b < n_pose; f1b += SCHUR_F1) {
       un.clear();
       for (int f = f1b; f < std::min(n_pose, f1b + SCHUR_F1); ++f)
@@ -517,21 +516,27 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
         std::vector<int32_t> lst;
         for (int l : un)
           if (c == 0 || lm_meta[4 * l + 1] >= f1b + WAVE * c) lst.push_back(l);
-        total += (int64_t)lst.size();
         tiles.push_back(std::move(lst));
         tile_key.push_back(f1b);
         tile_key.push_back(c);
       }
     }
     // split size: at most ~512 work items (two rounds of one workgroup per CU) counting the per-tile
-    // rounding, at least 64 landmarks, at most SCHUR_LMAX (the LDS list)
+    // rounding, at least 64 landmarks, at most SCHUR_LMAX (the LDS list).  Chunk-0 items also sum the
+    // diagonal terms (~25 % more time per landmark, measured with tools/schur_timing.py): their lists
+    // are weighted so that every item takes about the same time and the two rounds pack evenly.
+    constexpr int64_t W0 = 5, WD = 4;  // chunk-0 weight W0 / WD
+    int64_t total_w = 0;
+    for (size_t k = 0; k < tiles.size(); ++k)
+      total_w += (int64_t)tiles[k].size() * (tile_key[2 * k + 1] == 0 ? W0 : WD);
     const int64_t n_tiles = (int64_t)tiles.size();
-    const int64_t split = std::min<int64_t>(SCHUR_LMAX, std::max<int64_t>(64, (total + std::max<int64_t>(512 - n_tiles, 64) - 1) /
-                                                                                 std::max<int64_t>(512 - n_tiles, 64)));
+    const int64_t slots = std::max<int64_t>(512 - n_tiles, 64);
+    const int64_t split_w = std::max<int64_t>(64 * WD, (total_w + slots - 1) / slots);
     for (size_t k = 0; k < tiles.size(); ++k) {
       const auto& lst = tiles[k];
       const int n = (int)lst.size();
-      const int nparts = (int)((n + split - 1) / split);
+      const int64_t nw = (int64_t)n * (tile_key[2 * k + 1] == 0 ? W0 : WD);
+      const int nparts = (int)std::max<int64_t>((nw + split_w - 1) / split_w, (n + SCHUR_LMAX - 1) / SCHUR_LMAX);
       const int i0 = (int)(s2_items.size() / 4);
       for (int pp = 0; pp < nparts; ++pp) {
         const int a0 = (int)((int64_t)n * pp / nparts), a1 = (int)((int64_t)n * (pp + 1) / nparts);

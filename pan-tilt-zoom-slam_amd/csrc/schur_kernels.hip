@@ -29,6 +29,9 @@ namespace ptzba {
 // split writes its fp64 blocks to a partial buffer [item][32 f1][9][64 f2] (coalesced), reduced by
 // k_schur_reduce in a fixed order (deterministic).
 // ------------------------------------------------------------------------------------------------
+#ifndef S2_DU
+#define S2_DU 4  // diagonal-term loads in flight per thread (chunk-0 items)
+#endif
 #ifndef S2_ABL
 #define S2_ABL 0  // ablation switch for measurements: 1 = no FMAs, 2 = no operand loads
 #endif
@@ -61,6 +64,7 @@ __device__ __forceinline__ void load_w6(real (&x)[6], const real* __restrict__ p
 
 #ifdef SK_TIMING
 __device__ long long g_sk[16][16];
+__device__ long long g_sk_items[4096][4];  // per item: start, end (s_memrealtime, 100 MHz), chunk, nl
 #define SK_T(k) do { if (skrec) sk[k] = clock64(); } while (0)
 #define SK_ACC(k, t0) do { if (skrec) sk[k] += clock64() - (t0); } while (0)
 #define SK_NOW(t0) do { if (skrec) t0 = clock64(); } while (0)
@@ -91,6 +95,13 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
   SK_T(0);
   const int item = xcd_swizzle(blockIdx.x, gridDim.x);
   const int4 it = a.items[item];
+#ifdef SK_TIMING
+  if (threadIdx.x == 0 && item < 4096) {
+    g_sk_items[item][0] = __builtin_amdgcn_s_memrealtime();
+    g_sk_items[item][2] = it.y;
+    g_sk_items[item][3] = it.w - it.z;
+  }
+#endif
   const int f1b = it.x, chunk = it.y, lb = it.z, nl = it.w - it.z;
   const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
   const int f2base = f1b + WAVE * chunk;
@@ -108,7 +119,7 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
 #pragma unroll
     for (int k = 0; k < 12; ++k) acc[k] = 0;
     // DU landmarks per thread and step, all loads issued before any is consumed (clamped, branch-free)
-    constexpr int DU = 4, JS = 512 / SF;
+    constexpr int DU = S2_DU, JS = 512 / SF;
     for (int j0 = t >> 5; j0 < nl; j0 += DU * JS) {
       real u[DU][12], w[DU][6];
       double vg[DU][2];
@@ -309,10 +320,17 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
 #pragma unroll
     for (int k = 0; k < 9; ++k) out[((SFW * wv + i) * 9 + k) * WAVE + lane] = acc[i][k];
   SK_T(10);
+#ifdef SK_TIMING
+  __syncthreads();
+  if (threadIdx.x == 0 && item < 4096) g_sk_items[item][1] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 #ifdef SK_TIMING
 extern "C" int ptzba_debug_sk(long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sk), sizeof(g_sk)) == hipSuccess ? 0 : -1;
+}
+extern "C" int ptzba_debug_sk_items(long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sk_items), sizeof(g_sk_items)) == hipSuccess ? 0 : -1;
 }
 #endif
 
