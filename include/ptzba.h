@@ -153,8 +153,9 @@ PTZBA_EXPORT int ptzba_unpack(ptzba_handle h);
 PTZBA_EXPORT int ptzba_sync(ptzba_handle h);
 /* average device time (ms) per launch of the kernel groups [K1 linearisation, Schur build, Cholesky
  * solve, back-substitution], measured with HIP events on the handle's stream; launches timed.
- * reset: `enable` is a bitmask of the groups to time (1 K1, 2 Schur, 4 Cholesky, 8 back-subst.;
- * 0 off).  Each timed group adds two event records (a few microseconds) per launch. */
+ * reset: `enable` bits 0-3 select the groups to time (1 K1, 2 Schur, 4 Cholesky, 8 back-subst.;
+ * 0 off); bits 8-15 = sampling stride s (0/1: every launch): a group records its event pair around
+ * every s-th launch only.  Each recorded event adds a few-microsecond gap to the stream. */
 PTZBA_EXPORT int ptzba_kernel_times(ptzba_handle h, double* ms_out /*4*/, int64_t* count_out /*4*/);
 PTZBA_EXPORT int ptzba_reset_kernel_times(ptzba_handle h, int enable);
 

@@ -72,15 +72,19 @@ struct ptzba_ctx {
   int bs_nupd = 0, bs_npos = 0, bs_ntasks = 0;
   DBuf xtiles, xbuf;  // packed exchange: tile list, buffer
   int n_xtiles = 0;
+  DBuf ztiles;  // tiles zeroed before each build (the rest of the system region stays zero)
+  int n_ztiles = 0;
   double lambda = 0;
   // device-driven LM: state, pinned record ring, events
   DBuf lmdev;
   LMDev* lm_host = nullptr;
-  hipEvent_t lm_ev[4] = {nullptr, nullptr, nullptr, nullptr};
   // timing
   int timing = 0;  // bitmask of timed kernel groups (1 K1, 2 Schur, 4 Cholesky solve, 8 back-substitution)
   std::vector<hipEvent_t> ev[TM_N];
   int ev_used[TM_N] = {0, 0, 0, 0};
+  int64_t tm_seen[TM_N] = {0, 0, 0, 0};
+  bool tm_sampled[TM_N] = {false, false, false, false};
+  int tm_stride = 1;
 
   int elem() const { return precision == PTZBA_FP32 ? 4 : 8; }
   double* S() const { return sys.as<double>(); }
@@ -90,14 +94,20 @@ struct ptzba_ctx {
   int64_t sys_count() const { return ld * ld + 3 * ld; }
 };
 
+// a timed group records an event pair around every tm_stride-th launch (each record adds a gap to the
+// stream; sampling keeps that overhead out of most launches)
 static void tm_begin(ptzba_ctx* h, int k) {
+  h->tm_sampled[k] = false;
   if (!((h->timing >> k) & 1) || h->ev_used[k] + 2 > (int)h->ev[k].size()) return;
+  if (h->tm_seen[k]++ % h->tm_stride != 0) return;
+  h->tm_sampled[k] = true;
   (void)hipEventRecord(h->ev[k][h->ev_used[k]], h->st);
 }
 static void tm_end(ptzba_ctx* h, int k) {
-  if (!((h->timing >> k) & 1) || h->ev_used[k] + 2 > (int)h->ev[k].size()) return;
+  if (!h->tm_sampled[k]) return;
   (void)hipEventRecord(h->ev[k][h->ev_used[k] + 1], h->st);
   h->ev_used[k] += 2;
+  h->tm_sampled[k] = false;
 }
 
 const char* ptzba_last_error(void) { return g_err.c_str(); }
@@ -125,8 +135,6 @@ void ptzba_delete(ptzba_handle h) {
   if (h->own) (void)hipStreamDestroy(h->own);
   if (h->scal_host) (void)hipHostFree(h->scal_host);
   if (h->lm_host) (void)hipHostFree(h->lm_host);
-  for (auto e : h->lm_ev)
-    if (e) (void)hipEventDestroy(e);
   delete h;
 }
 
@@ -254,6 +262,7 @@ struct CholPlan {
   std::vector<int> la_tasks;  // lookahead back substitution: la [npos] | task_off [n_chain * BS_HELPERS + 1] | tasks
   int n_tasks = 0;
   std::vector<int32_t> xtiles;  // (ti, tj) pairs the Schur kernel can write (before fill), for the exchange
+  std::vector<int32_t> ztiles;  // (ti, tj) lower tiles of the factor's pattern (incl. fill): zeroed per build
   int n_levels = 0;
 };
 
@@ -296,6 +305,10 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
     count[L]++;
     level[k] = L;
   }
+  P.ztiles.clear();
+  for (int i = 0; i < T; ++i)
+    for (int j = 0; j <= i; ++j)
+      if (nz[i][j]) { P.ztiles.push_back(i); P.ztiles.push_back(j); }
   const int nL = (int)count.size();
   std::vector<std::vector<int>> K(nL);
   for (int k = 0; k < T; ++k) K[level[k]].push_back(k);
@@ -643,10 +656,12 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     return -1;
   if (upload(h->chol_tasks, plan.tasks) || upload(h->frame_pos, sorder.pos) || upload(h->row_pad, sorder.pad) ||
       upload(h->bs_chain_off, plan.chain_off) || upload(h->bs_chain_cols, plan.chain_cols) ||
-      upload(h->bs_upd_off, plan.upd_off) || upload(h->bs_upd_tiles, plan.upd_tiles) || upload(h->xtiles, plan.xtiles) ||
+      upload(h->bs_upd_off, plan.upd_off) || upload(h->bs_upd_tiles, plan.upd_tiles) || upload(h->xtiles, plan.xtiles) || upload(h->ztiles, plan.ztiles) ||
       upload(h->bs_la_tasks, plan.la_tasks))
     return -1;
   h->n_xtiles = (int)(plan.xtiles.size() / 2);
+  h->n_ztiles = (int)(plan.ztiles.size() / 2);
+  HIPCHK(hipMemset(h->sys.p, 0, h->sys.bytes));  // outside the factor's tiles it is never written
   h->bs_nupd = (int)plan.upd_tiles.size();
   h->bs_npos = (int)plan.chain_cols.size();
   h->bs_ntasks = plan.n_tasks;
@@ -812,7 +827,7 @@ static int build_impl(ptzba_ctx* h, double lambda, const double* lam_dev, const 
   const int c = h->cur;
   launch_landmark_damp(h->lm_out[c].as<double>(), h->lm_seg_begin.as<int32_t>(), h->D_ray.as<double>(),
                        h->lm_aux.as<double>(), h->n_lm, lambda, lam_dev, skip_if, h->st);
-  HIPCHK(hipMemsetAsync(h->sys.p, 0, h->sys.bytes, h->st));
+  launch_zero_tiles(h->S(), h->ld, h->ztiles.as<int2>(), h->n_ztiles, h->bvec(), 3 * h->ld, h->st);
   SchurArgs a;
   a.items = h->s2_items.as<int4>();
   a.groups = h->s2_groups.as<int4>();
@@ -853,9 +868,9 @@ int ptzba_build_reduced(ptzba_handle h, double lambda) {
 static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx) {
   const int c = h->cur;
   tm_begin(h, TM_CHOL);
-  launch_pose_damp(h->S(), h->ld, h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
-                   h->lambda, lam_dev, h->st);
-  launch_chol_prepare(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(), h->st);
+  launch_chol_prepare_damped(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(),
+                             h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
+                             h->lambda, lam_dev, h->st);
   launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
                   h->Ldiag.as<double>(), h->info.as<int>(), h->st);
   launch_chol_backsolve(h->S(), h->ld, h->n_aug, h->n_chain, h->bs_npos, h->bs_chain_off.as<int>(),
@@ -924,8 +939,7 @@ int ptzba_lm_start(ptzba_handle h) {
   HIPCHK(hipSetDevice(h->device));
   if (!h->lmdev.p && h->lmdev.alloc(sizeof(LMDev))) return -1;
   if (!h->lm_host) {
-    HIPCHK(hipHostMalloc((void**)&h->lm_host, LM_RING * sizeof(LMDev), hipHostMallocDefault));
-    for (int k = 0; k < LM_RING; ++k) HIPCHK(hipEventCreateWithFlags(&h->lm_ev[k], hipEventDisableTiming));
+    HIPCHK(hipHostMalloc((void**)&h->lm_host, LM_RING * sizeof(LMDev), hipHostMallocCoherent));
   }
   h->cur = 0;
   return ptzba_linearize(h);
@@ -939,6 +953,8 @@ int ptzba_lm_init(ptzba_handle h, const ptzba_lm_opts* o) {
   HIPCHK(hipSetDevice(h->device));
   LMParams p{o->ftol, o->xtol, o->gtol, o->lambda0, o->min_lambda, o->max_lambda, o->max_iter, o->max_retries,
              o->gauss_newton ? 1 : 0, 0};
+  // no decision of an earlier run is in flight (its lm_wait returned): clear the ring's sequence tags
+  for (int k = 0; k < LM_RING; ++k) __atomic_store_n(&h->lm_host[k].seq, 0, __ATOMIC_RELAXED);
   launch_lm_init(h->lmdev.as<LMDev>(), h->scal.as<double>(), p, h->st);
   HIPCHK(hipGetLastError());
   return 0;
@@ -964,13 +980,13 @@ int ptzba_lm_decide(ptzba_handle h, int trial) {
   LMDev* st = h->lmdev.as<LMDev>();
   const int k = trial % LM_RING;
   // the record is written by the decision kernel straight into pinned host memory
-  launch_lm_decide(st, h->scal.as<double>(), h->loc.as<double>(), h->info.as<int>(), h->lm_host + k, h->st);
+  launch_lm_decide(st, h->scal.as<double>(), h->loc.as<double>(), h->info.as<int>(), h->lm_host + k, trial + 1,
+                   h->st);
   launch_lm_commit(st, h->ptz.as<double>(), h->ptz_trial.as<double>(), 3 * h->n_pose, h->rays.as<double>(),
                    h->rays_trial.as<double>(), 2 * (int64_t)h->n_lm, h->st);
   // rejected: the trial overwrote the linearisation slot -> rebuild it at the current point
   tables(h, h->ptz.as<double>(), h->rays.as<double>(), &st->relin);
   linearize_into(h, h->cur, &st->relin);
-  HIPCHK(hipEventRecord(h->lm_ev[k], h->st));
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -980,7 +996,17 @@ int ptzba_lm_wait(ptzba_handle h, int trial, ptzba_lm_record* out) {
   if (trial < 0 || !out) return fail("bad arguments");
   HIPCHK(hipSetDevice(h->device));
   const int k = trial % LM_RING;
-  HIPCHK(hipEventSynchronize(h->lm_ev[k]));
+  // the decision kernel tags its record last; poll the tag (an event record per trial would add a
+  // ~6 us gap to the stream).  Every 4096 polls check that the stream is still alive.
+  for (int64_t n = 0; __atomic_load_n(&h->lm_host[k].seq, __ATOMIC_ACQUIRE) != trial + 1; ++n) {
+    if ((n & 4095) == 4095) {
+      const hipError_t q = hipStreamQuery(h->st);
+      if (q != hipSuccess && q != hipErrorNotReady) return fail("lm_wait: stream error %s", hipGetErrorString(q));
+      if (q == hipSuccess && __atomic_load_n(&h->lm_host[k].seq, __ATOMIC_ACQUIRE) != trial + 1)
+        return fail("lm_wait: no decision record for trial %d (was ptzba_lm_decide called?)", trial);
+    }
+    __builtin_ia32_pause();
+  }
   const LMDev& r = h->lm_host[k];
   out->cost = r.cost;
   out->initial_cost = r.initial_cost;
@@ -1079,8 +1105,11 @@ int ptzba_reset_kernel_times(ptzba_handle h, int enable) {
       for (auto& e : h->ev[k]) HIPCHK(hipEventCreate(&e));
     }
     h->ev_used[k] = 0;
+    h->tm_seen[k] = 0;
+    h->tm_sampled[k] = false;
   }
   h->timing = enable & ((1 << TM_N) - 1);
+  h->tm_stride = std::max(1, (enable >> 8) & 0xff);
   return 0;
 }
 

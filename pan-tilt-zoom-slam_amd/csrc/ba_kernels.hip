@@ -378,31 +378,7 @@ void launch_landmark_damp(const double* lm_out, const int32_t* lm_seg_begin, dou
                      lm_aux, n_lm, lambda, lam_dev, skip_if);
 }
 
-
-// pose damping on the exchanged reduced system: D = max(D, diag U) (monotone), S_ii += lambda D_i
-__global__ void k_pose_damp(double* __restrict__ S, int64_t ld, const double* __restrict__ dU,
-                            double* __restrict__ D_pose, const int32_t* __restrict__ frame_pos, int n_pose,
-                            int n_fixed, double lambda_arg, const double* __restrict__ lam_dev) {
-  const double lambda = lam_dev ? *lam_dev : lambda_arg;
-  int k = blockIdx.x * blockDim.x + threadIdx.x;
-  int n = 3 * (n_pose - n_fixed);
-  if (k >= n) return;
-  const int f = n_fixed + k / 3;
-  const int64_t row = frame_pos[f] + k % 3;
-  double* D = D_pose + 3 * n_fixed + k;
-  double d = fmax(*D, fmax(dU[row], 1e-12));
-  *D = d;
-  S[row * ld + row] += lambda * d;
-}
-
-void launch_pose_damp(double* S, int64_t ld, const double* dU, double* D_pose, const int32_t* frame_pos, int n_pose,
-                      int n_fixed, double lambda, const double* lam_dev, hipStream_t st) {
-  int n = 3 * (n_pose - n_fixed);
-  if (n > 0)
-    hipLaunchKernelGGL(k_pose_damp, dim3((n + 255) / 256), dim3(256), 0, st, S, ld, dU, D_pose, frame_pos, n_pose,
-                       n_fixed, lambda, lam_dev);
-}
-
+// (pose damping of the exchanged reduced system: k_chol_prepare, chol_kernels.hip)
 // ------------------------------------------------------------------------------------------------
 // K5: back-substitution of the rays + trial state + predicted-reduction partials
 //   delta_l = -Vinv (g_l + sum_s W_s^T delta_p(f_s));  trial ray = ray + delta_l
@@ -640,7 +616,7 @@ __global__ void k_lm_init(LMDev* st, const double* __restrict__ scal, LMParams p
 }
 
 __global__ void k_lm_decide(LMDev* st, const double* __restrict__ scal, const double* __restrict__ loc,
-                            const int* __restrict__ info, LMDev* __restrict__ rec) {
+                            const int* __restrict__ info, LMDev* __restrict__ rec, int seq) {
   LMDev s = *st;
   s.accepted = 0;
   s.relin = 0;
@@ -696,7 +672,11 @@ __global__ void k_lm_decide(LMDev* st, const double* __restrict__ scal, const do
     }
   }
   *st = s;
+  s.seq = 0;
   *rec = s;
+  // the host polls rec->seq (pinned memory): the record's fields must be visible before it
+  __threadfence_system();
+  __hip_atomic_store(&rec->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // accepted trial -> current state (the trial's linearisation is already in place)
@@ -712,8 +692,9 @@ __global__ void k_lm_commit(const LMDev* __restrict__ st, double* __restrict__ p
 void launch_lm_init(LMDev* st, const double* scal, const LMParams& p, hipStream_t s) {
   hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(1), 0, s, st, scal, p);
 }
-void launch_lm_decide(LMDev* st, const double* scal, const double* loc, const int* info, LMDev* rec, hipStream_t s) {
-  hipLaunchKernelGGL(k_lm_decide, dim3(1), dim3(1), 0, s, st, scal, loc, info, rec);
+void launch_lm_decide(LMDev* st, const double* scal, const double* loc, const int* info, LMDev* rec, int seq,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(k_lm_decide, dim3(1), dim3(1), 0, s, st, scal, loc, info, rec, seq);
 }
 void launch_lm_commit(const LMDev* st, double* ptz, const double* ptz_trial, int n3, double* rays,
                       const double* rays_trial, int64_t n2, hipStream_t s) {

@@ -20,6 +20,8 @@
 // (symbolic fill on the tile graph) are visited.
 // Back substitution L^T x = y: one 1024-thread workgroup per chain of tile columns (nested
 // dissection: C then A, C then B), right-looking updates of an LDS-resident right-hand side.
+#include <algorithm>
+
 #include "ptzba_common.h"
 #include "ptzba_kernels.h"
 
@@ -38,9 +40,19 @@ __device__ __forceinline__ double bcast(double v, int j) {
 }
 
 // augmented row / padding: A[n][j] = b[j], A[n][n] = huge, A[i][i] = 1 for padding rows (pad[i], i < n)
-// and for every row after n
+// and for every row after n.  With PoseDamp (BA solve): also the Marquardt damping of the pose rows,
+// D_f = max(D_f, diag U_f), S_ff += lambda D_f (scipy x_scale='jac', common.py:598-612) -- disjoint
+// rows from the padding, so one launch does both.
+struct PoseDamp {
+  const double* dU;
+  double* D_pose;
+  const int32_t* frame_pos;
+  int n_pose, n_fixed;
+  double lambda;
+  const double* lam_dev;
+};
 __global__ void k_chol_prepare(double* __restrict__ A, int64_t ld, int n, const double* __restrict__ b,
-                               const uint8_t* __restrict__ pad, int* info) {
+                               const uint8_t* __restrict__ pad, int* info, PoseDamp pd) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) info[0] = 0;
   if (i < n) {
@@ -49,10 +61,27 @@ __global__ void k_chol_prepare(double* __restrict__ A, int64_t ld, int n, const 
   }
   if (i == n) A[i * ld + i] = AUG_DIAG;
   if (i > n && i < ld) A[i * ld + i] = 1.0;
+  if (pd.dU && i < 3 * (int64_t)(pd.n_pose - pd.n_fixed)) {
+    const double lambda = pd.lam_dev ? *pd.lam_dev : pd.lambda;
+    const int f = pd.n_fixed + (int)(i / 3);
+    const int64_t row = pd.frame_pos[f] + i % 3;
+    double* D = pd.D_pose + 3 * pd.n_fixed + i;
+    const double d = fmax(*D, fmax(pd.dU[row], 1e-12));
+    *D = d;
+    A[row * ld + row] += lambda * d;
+  }
 }
 
 void launch_chol_prepare(double* A, int64_t ld, int n, double* b, const uint8_t* pad, int* info, hipStream_t st) {
-  hipLaunchKernelGGL(k_chol_prepare, dim3((unsigned)((ld + 255) / 256)), dim3(256), 0, st, A, ld, n, b, pad, info);
+  hipLaunchKernelGGL(k_chol_prepare, dim3((unsigned)((ld + 255) / 256)), dim3(256), 0, st, A, ld, n, b, pad, info,
+                     PoseDamp{nullptr, nullptr, nullptr, 0, 0, 0.0, nullptr});
+}
+void launch_chol_prepare_damped(double* A, int64_t ld, int n, double* b, const uint8_t* pad, int* info,
+                                const double* dU, double* D_pose, const int32_t* frame_pos, int n_pose, int n_fixed,
+                                double lambda, const double* lam_dev, hipStream_t st) {
+  const int64_t m = std::max<int64_t>(ld, 3 * (int64_t)(n_pose - n_fixed));
+  hipLaunchKernelGGL(k_chol_prepare, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, A, ld, n, b, pad, info,
+                     PoseDamp{dU, D_pose, frame_pos, n_pose, n_fixed, lambda, lam_dev});
 }
 
 // Batched tile staging: every thread fetches its 4 elements of each tile into registers first (all global
@@ -717,25 +746,32 @@ void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_o
 
 // ---------------------------------------------------------------------------------------------
 // inverses of the diagonal factor tiles: M_kt = L_kt,kt^-1 (lower), row-major [kt][32][32].  One wave
-// per tile: lane j computes column j by forward substitution against e_j (row i of L broadcast from LDS).
+// per tile: lane j computes column j by forward substitution against e_j, right-looking (after m_k is
+// known, every later row's running sum takes its term at once), so the dependent chain is one
+// multiply and one FMA per row; the diagonal reciprocals are formed up front, off the chain.
 __global__ __launch_bounds__(64) void k_tile_inv(const double* __restrict__ Ldiag, double* __restrict__ Minv) {
-  __shared__ double Lt[NB][NB + 1];
+  __shared__ __attribute__((aligned(16))) double Lt[NB][NB];
+  __shared__ double rinv[NB];
   const int kt = blockIdx.x, lane = threadIdx.x, j = lane & (NB - 1);
   const double* src = Ldiag + (int64_t)kt * NB * NB;
   for (int e = lane; e < NB * NB; e += WAVE) Lt[e >> 5][e & 31] = src[e];
   __syncthreads();
-  double m[NB];
+  if (lane < NB) rinv[lane] = rcp_nr(Lt[lane][lane]);
+  __syncthreads();
+  double acc[NB];
 #pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    double sacc = (i == j) ? 1.0 : 0.0;
+  for (int i = 0; i < NB; ++i) acc[i] = (i == j) ? 1.0 : 0.0;
 #pragma unroll
-    for (int k = 0; k < i; ++k) sacc = fma(-Lt[i][k], m[k], sacc);  // m[k] = 0 for k < j
-    m[i] = (i >= j) ? sacc * rcp_nr(Lt[i][i]) : 0.0;
+  for (int k = 0; k < NB; ++k) {
+    const double mk = (k >= j) ? acc[k] * rinv[k] : 0.0;  // m_k (0 above the diagonal)
+    acc[k] = mk;
+#pragma unroll
+    for (int i = k + 1; i < NB; ++i) acc[i] = fma(-Lt[i][k], mk, acc[i]);
   }
   if (lane < NB) {
     double* dst = Minv + (int64_t)kt * NB * NB + lane;
 #pragma unroll
-    for (int i = 0; i < NB; ++i) dst[i * NB] = m[i];
+    for (int i = 0; i < NB; ++i) dst[i * NB] = acc[i];
   }
 }
 
@@ -1074,6 +1110,22 @@ __global__ void k_pack_exchange(double* __restrict__ S, int64_t ld, const int2* 
     if (unpack) vec[e] = b[e];
     else b[e] = vec[e];
   }
+}
+
+// zero the listed 32x32 tiles of S (block k < n_tiles) and n_vec doubles at vec (last block)
+__global__ __launch_bounds__(256) void k_zero_tiles(double* __restrict__ S, int64_t ld, const int2* __restrict__ zt,
+                                                    int n_tiles, double* __restrict__ vec, int64_t n_vec) {
+  if ((int)blockIdx.x < n_tiles) {
+    const int2 tij = zt[blockIdx.x];
+    double* T = S + (int64_t)tij.x * NB * ld + (int64_t)tij.y * NB;
+    for (int e = threadIdx.x; e < NB * NB / 2; e += blockDim.x)
+      *reinterpret_cast<double2*>(T + (int64_t)(e >> 4) * ld + 2 * (e & 15)) = make_double2(0.0, 0.0);
+  } else {
+    for (int64_t e = threadIdx.x; e < n_vec; e += blockDim.x) vec[e] = 0.0;
+  }
+}
+void launch_zero_tiles(double* S, int64_t ld, const int2* zt, int n_tiles, double* vec, int64_t n_vec, hipStream_t st) {
+  hipLaunchKernelGGL(k_zero_tiles, dim3(n_tiles + 1), dim3(256), 0, st, S, ld, zt, n_tiles, vec, n_vec);
 }
 
 void launch_pack_exchange(double* S, int64_t ld, const int2* xt, int n_tiles, double* vec, double* buf, int unpack,

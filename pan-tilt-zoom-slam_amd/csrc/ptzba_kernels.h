@@ -81,9 +81,11 @@ struct LMDev {
   LMParams p;
   double cost, initial_cost, lam, nu, last_actual, last_rho;
   int it, nfev, trials, retries, status, done, accepted, relin;
+  int seq, pad2;  // host ring record: written last (after a system-scope fence) = trial index + 1
 };
 void launch_lm_init(LMDev* st, const double* scal, const LMParams& p, hipStream_t s);
-void launch_lm_decide(LMDev* st, const double* scal, const double* loc, const int* info, LMDev* rec, hipStream_t s);
+void launch_lm_decide(LMDev* st, const double* scal, const double* loc, const int* info, LMDev* rec, int seq,
+                      hipStream_t s);
 void launch_lm_commit(const LMDev* st, double* ptz, const double* ptz_trial, int n3, double* rays,
                       const double* rays_trial, int64_t n2, hipStream_t s);
 
@@ -94,8 +96,6 @@ template <typename real>
 void launch_linearize(const LinArgs& a, int loss, hipStream_t st);
 void launch_landmark_damp(const double* lm_out, const int32_t* lm_seg_begin, double* D_ray, double* lm_aux, int n_lm,
                           double lambda, const double* lam_dev, const int* skip_if, hipStream_t st);
-void launch_pose_damp(double* S, int64_t ld, const double* dU, double* D_pose, const int32_t* frame_pos, int n_pose,
-                      int n_fixed, double lambda, const double* lam_dev, hipStream_t st);
 template <typename real>
 void launch_schur(const SchurArgs& a, int n_items, int n_groups, int n_fixed, hipStream_t st);
 template <typename real>
@@ -122,6 +122,10 @@ void launch_residual(const int32_t* rec_seg, const int32_t* seg_frame, const int
 // {type, i, j, packed update panels}.  backsolve: x = S^-1 b into xout, one workgroup per chain.
 constexpr int CHOL_NB = 32;
 void launch_chol_prepare(double* A, int64_t ld, int n, double* b, const uint8_t* pad, int* info, hipStream_t st);
+// the same plus the Marquardt damping of the pose rows (k_pose_damp's work) in one launch
+void launch_chol_prepare_damped(double* A, int64_t ld, int n, double* b, const uint8_t* pad, int* info,
+                                const double* dU, double* D_pose, const int32_t* frame_pos, int n_pose, int n_fixed,
+                                double lambda, const double* lam_dev, hipStream_t st);
 void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_off_host, int n_launch, double* Ldiag,
                      int* info, hipStream_t st);
 // la_tasks: lookahead back substitution's [lookahead tile per position | task offsets per (chain, helper) |
@@ -131,6 +135,9 @@ void launch_chol_backsolve(const double* L, int64_t ld, int n, int n_chain, int 
                            const int* chain_cols, const int* upd_off, const int* upd_tiles, int n_upd,
                            const int* la_tasks, int n_tasks, const double* Ldiag, double* Minv, double* xout,
                            hipStream_t st);
+// zero the factor pattern's tiles and the b | g_pose | dU vectors before a build (replaces a memset of
+// the whole ld x ld region: entries outside the pattern are never written)
+void launch_zero_tiles(double* S, int64_t ld, const int2* zt, int n_tiles, double* vec, int64_t n_vec, hipStream_t st);
 // packed exchange of the Schur-written tiles + b | g_pose | dU (vec = b, contiguous 3 ld doubles)
 void launch_pack_exchange(double* S, int64_t ld, const int2* xt, int n_tiles, double* vec, double* buf, int unpack,
                           hipStream_t st);

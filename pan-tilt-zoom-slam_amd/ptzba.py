@@ -510,9 +510,11 @@ class BAHandle:
     def sync(self):
         _check(lib().ptzba_sync(self.h), "ptzba_sync")
 
-    def reset_kernel_times(self, enable=True, groups=0xF):
-        """Restart kernel timing; `groups` bitmask: 1 K1, 2 Schur, 4 Cholesky solve, 8 back-substitution."""
-        _check(lib().ptzba_reset_kernel_times(self.h, int(groups) if enable else 0), "ptzba_reset_kernel_times")
+    def reset_kernel_times(self, enable=True, groups=0xF, stride=1):
+        """Restart kernel timing; `groups` bitmask: 1 K1, 2 Schur, 4 Cholesky solve, 8 back-substitution;
+        events around every `stride`-th launch of a group (each event record adds a gap to the stream)."""
+        flags = (int(groups) | (max(1, min(255, int(stride))) << 8)) if enable else 0
+        _check(lib().ptzba_reset_kernel_times(self.h, flags), "ptzba_reset_kernel_times")
 
     def kernel_times(self):
         ms = np.zeros(4)
