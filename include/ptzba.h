@@ -105,6 +105,11 @@ PTZBA_EXPORT int ptzba_residual(ptzba_handle h, const double* x_full, double* r_
 /* ---------------- state ---------------- */
 PTZBA_EXPORT int ptzba_set_state(ptzba_handle h, const double* ptz /*3*n_pose*/, const double* rays /*2*n_landmark*/);
 PTZBA_EXPORT int ptzba_get_state(ptzba_handle h, double* ptz, double* rays);
+/* Device-resident restart point: save_state snapshots the current state on the device, restore_state
+ * copies it back and resets the Marquardt scaling (as set_state does) -- both stream-ordered, no host
+ * transfer or synchronisation (restarting a solve from x0 without a PCIe upload). */
+PTZBA_EXPORT int ptzba_save_state(ptzba_handle h);
+PTZBA_EXPORT int ptzba_restore_state(ptzba_handle h);
 
 /* ---------------- one Levenberg-Marquardt iteration, split at the exchange points -------------
  * Single GPU:  ptzba_linearize; loop { ptzba_step(lambda); ptzba_read_scalars; ptzba_accept(ok) }.

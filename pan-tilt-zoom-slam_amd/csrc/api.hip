@@ -56,6 +56,7 @@ struct ptzba_ctx {
   int64_t n_slot = 0;  // dense landmark x frame slots (W table rows)
   // device: state
   DBuf ptz, rays, ptz_trial, rays_trial, D_pose, D_ray;
+  DBuf ptz_saved, rays_saved;  // ptzba_save_state / ptzba_restore_state (device-resident restart point)
   DBuf ft, rt, ft64, rt64, seg_base;
   DBuf ug_slot[2], w_slot[2], lm_out[2];
   int cur = 0;
@@ -433,6 +434,8 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipStreamSynchronize(h->st));
   h->have_problem = false;
+  h->ptz_saved.release();
+  h->rays_saved.release();
   h->n_pose = n_pose;
   h->n_lm = n_landmark;
   h->n_rec = n_obs;
@@ -797,6 +800,29 @@ int ptzba_set_state(ptzba_handle h, const double* ptz, const double* rays) {
   HIPCHK(hipMemsetAsync(h->D_pose.p, 0, h->D_pose.bytes, h->st));
   HIPCHK(hipMemsetAsync(h->D_ray.p, 0, h->D_ray.bytes, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
+  return 0;
+}
+
+// device-resident restart point: snapshot the current state / restore it (stream-ordered, no host sync)
+int ptzba_save_state(ptzba_handle h) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  HIPCHK(hipSetDevice(h->device));
+  if (h->ptz_saved.alloc(h->ptz.bytes) || h->rays_saved.alloc(std::max<size_t>(h->rays.bytes, 8))) return -1;
+  HIPCHK(hipMemcpyAsync(h->ptz_saved.p, h->ptz.p, 3 * (size_t)h->n_pose * 8, hipMemcpyDeviceToDevice, h->st));
+  if (h->n_lm)
+    HIPCHK(hipMemcpyAsync(h->rays_saved.p, h->rays.p, 2 * (size_t)h->n_lm * 8, hipMemcpyDeviceToDevice, h->st));
+  return 0;
+}
+
+int ptzba_restore_state(ptzba_handle h) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  if (!h->ptz_saved.p) return fail("no saved state (ptzba_save_state)");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipMemcpyAsync(h->ptz.p, h->ptz_saved.p, 3 * (size_t)h->n_pose * 8, hipMemcpyDeviceToDevice, h->st));
+  if (h->n_lm)
+    HIPCHK(hipMemcpyAsync(h->rays.p, h->rays_saved.p, 2 * (size_t)h->n_lm * 8, hipMemcpyDeviceToDevice, h->st));
+  HIPCHK(hipMemsetAsync(h->D_pose.p, 0, h->D_pose.bytes, h->st));
+  HIPCHK(hipMemsetAsync(h->D_ray.p, 0, h->D_ray.bytes, h->st));
   return 0;
 }
 

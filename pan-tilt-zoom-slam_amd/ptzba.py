@@ -103,6 +103,8 @@ def lib():
         "ptzba_sync": ([V], I),
         "ptzba_kernel_times": ([V, V, V], I),
         "ptzba_reset_kernel_times": ([V, I], I),
+        "ptzba_save_state": ([V], I),
+        "ptzba_restore_state": ([V], I),
         "ptz_ray_to_image": ([I, I64, D, D, V, V, V, V, V, V, V], I),
         "ptz_image_to_ray": ([I, I64, D, D, V, V, V, V, V, V, V], I),
         "ptz_project_rays": ([I, I64, D, D, D, D, D, V, V, V], I),
@@ -138,7 +140,7 @@ EXPORTED_SYMBOLS = [
     "ptzba_problem_info", "ptzba_solver_info", "ptzba_residual", "ptzba_set_state", "ptzba_get_state", "ptzba_linearize",
     "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_read_scalars", "ptzba_accept",
     "ptzba_lm_start", "ptzba_lm_init", "ptzba_lm_build", "ptzba_lm_solve", "ptzba_lm_decide", "ptzba_lm_wait",
-    "ptzba_exchange", "ptzba_exchange_packed", "ptzba_pack", "ptzba_unpack", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptz_ray_to_image",
+    "ptzba_exchange", "ptzba_exchange_packed", "ptzba_pack", "ptzba_unpack", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptzba_save_state", "ptzba_restore_state", "ptz_ray_to_image",
     "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks",
     "ptz_py_shuffle_prefix", "ptz_set_order_pairs", "ptz_keyframe_features", "ptz_pack_records",
     "ptz_refine_poses", "ptzekf_new", "ptzekf_delete", "ptzekf_num_rays", "ptzekf_set_state", "ptzekf_get_state", "ptzekf_add_pose_cov",
@@ -441,6 +443,14 @@ class BAHandle:
         rays = _f64(rays, (self.n_landmark, 2))
         _check(lib().ptzba_set_state(self.h, _ptr(ptz), _ptr(rays)), "ptzba_set_state")
 
+    def save_state(self):
+        """Snapshot the current state on the device (restart point for restore_state)."""
+        _check(lib().ptzba_save_state(self.h), "ptzba_save_state")
+
+    def restore_state(self):
+        """Restore the saved state on the device (stream-ordered; no host transfer)."""
+        _check(lib().ptzba_restore_state(self.h), "ptzba_restore_state")
+
     def get_state(self):
         ptz = np.empty((self.n_pose, 3))
         rays = np.empty((self.n_landmark, 2))
@@ -689,7 +699,8 @@ class LMSolver:
             k += 1
             if rec.done or k >= limit:
                 break
-        h.sync()
+        # no stream sync here: what is still queued (the speculative build after the final decision) is
+        # skipped on the device, and every reader of the state (get_state, ...) orders itself on the stream
         t1 = time.perf_counter()
         return LMResult(status=rec.status, message=STATUS_MSG.get(rec.status, "?"), cost=rec.cost,
                         initial_cost=rec.initial_cost, njev=rec.iterations, nfev=rec.nfev, iterations=rec.iterations,
