@@ -42,7 +42,7 @@ struct SchurArgs {
   const void* w_slot;             // [n_slot][8] real: W | 0 0 (dense landmark x frame slots)
   const double* lm_aux;           // [n_lm][8]
   const int32_t* frame_pos;       // [n_pose] system row of the frame's pan (-1: fixed)
-  double* part;                   // [n_items][SCHUR_F1][9][64] split partials
+  void* part;                     // [n_items][SCHUR_F1][9][64] split partials (record precision)
   double* part_diag;              // [n_items][SCHUR_F1][12] chunk-0 splits: U | g_pose | sum W V~^-1 g
   double* S;                      // [ld][ld] lower, row-major
   double* b;                      // [n_sys]

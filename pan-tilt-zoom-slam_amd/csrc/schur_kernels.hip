@@ -314,11 +314,13 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
   }
   SK_T(7);
   // partial blocks of this split: part[item][f1 local][k][f2 lane]
-  double* out = a.part + (int64_t)item * (SF * 9 * WAVE);
+  // split partials in the record precision: half the bytes of fp64 for the fp32 path (each is a sum of
+  // fp64-flushed batches, rounded once; the reduce sums them in fp64)
+  real* out = (real*)a.part + (int64_t)item * (SF * 9 * WAVE);
 #pragma unroll
   for (int i = 0; i < SFW; ++i)
 #pragma unroll
-    for (int k = 0; k < 9; ++k) out[((SFW * wv + i) * 9 + k) * WAVE + lane] = acc[i][k];
+    for (int k = 0; k < 9; ++k) out[((SFW * wv + i) * 9 + k) * WAVE + lane] = (real)acc[i][k];
   SK_T(10);
 #ifdef SK_TIMING
   __syncthreads();
@@ -337,6 +339,7 @@ extern "C" int ptzba_debug_sk_items(long long* out) {
 // tile reduction: thread = one element of a tile (grid: tile x 72 blocks of 256); fixed-order sum of the
 // splits, U on the diagonal blocks, write the lower triangle in the system order (mirror when f2
 // precedes f1); chunk-0 tiles also write b | g_pose | diag U of their frames.
+template <typename real>
 __global__ __launch_bounds__(256) void k_schur_reduce(SchurArgs a) {
   constexpr int NE = SF * 9 * WAVE;
   if (a.skip_if && *a.skip_if) return;
@@ -346,7 +349,7 @@ __global__ __launch_bounds__(256) void k_schur_reduce(SchurArgs a) {
   const int ln = e & 63, ik = e >> 6, i = ik / 9, k = ik - 9 * i, q = k / 3, r = k - 3 * q;
   const int f1 = f1b + i, f2 = f1b + WAVE * chunk + ln;
   if (f1 < a.n_pose && f2 >= f1 && f2 <= a.frame_win_hi[f1]) {
-    const double* p = a.part + e;
+    const real* p = (const real*)a.part + e;
     double v = 0;
     int it = g.z;
     for (; it + 4 <= g.w; it += 4) {
@@ -354,7 +357,7 @@ __global__ __launch_bounds__(256) void k_schur_reduce(SchurArgs a) {
       const double p2 = p[(int64_t)(it + 2) * NE], p3 = p[(int64_t)(it + 3) * NE];
       v += p0; v += p1; v += p2; v += p3;
     }
-    for (; it < g.w; ++it) v += p[(int64_t)it * NE];
+    for (; it < g.w; ++it) v += (double)p[(int64_t)it * NE];
     if (f2 == f1) {  // chunk 0: U of the frame, summed over the tile's splits
       const int ui = q <= r ? (q == 0 ? r : (q == 1 ? 2 + r : 5)) : (r == 0 ? q : (r == 1 ? 2 + q : 5));
       for (int it2 = g.z; it2 < g.w; ++it2) v += a.part_diag[((int64_t)it2 * SF + i) * 12 + ui];
@@ -383,7 +386,7 @@ void launch_schur(const SchurArgs& a, int n_items, int n_groups, int n_fixed, hi
   const int n_free = a.n_pose - n_fixed;
   if (n_free <= 0) return;
   if (n_items > 0) hipLaunchKernelGGL(k_schur<real>, dim3(n_items), dim3(512), 0, st, a);
-  if (n_groups > 0) hipLaunchKernelGGL(k_schur_reduce, dim3(SF * 9 * WAVE / 256, n_groups), dim3(256), 0, st, a);
+  if (n_groups > 0) hipLaunchKernelGGL(k_schur_reduce<real>, dim3(SF * 9 * WAVE / 256, n_groups), dim3(256), 0, st, a);
 }
 
 template void launch_schur<float>(const SchurArgs&, int, int, int, hipStream_t);
