@@ -16,3 +16,7 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/${TAG}
 python tools/pmc_traffic.py gpurun_out/${TAG}_pmc_fetch gpurun_out/${TAG}_pmc_write k_linearize config3/pair/fp32/huber gpurun_out/${TAG}_k1_traffic.json > /dev/null || { echo TRAFFICFAIL; exit 1; }
 timeout -k 10 400 python bench.py --traffic-json gpurun_out/${TAG}_k1_traffic.json > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { echo BENCHFAIL; tail gpurun_out/${TAG}_bench.err; exit 1; }
 cat gpurun_out/${TAG}_bench.json
+# PMC byte-count calibration of the access widths K1 uses (1 GiB streams and a cache-resident table)
+timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/${TAG}_cal_fetch -o run --output-format csv -- ./tools/pmc_calib.bin > gpurun_out/${TAG}_cal_fetch.log 2>&1 || { echo CALFAIL; exit 1; }
+timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/${TAG}_cal_write -o run --output-format csv -- ./tools/pmc_calib.bin > gpurun_out/${TAG}_cal_write.log 2>&1 || { echo CALFAIL; exit 1; }
+python tools/pmc_calib_summary.py gpurun_out/${TAG}_cal_fetch gpurun_out/${TAG}_cal_write gpurun_out/${TAG}_pmc_calib.json

@@ -13,10 +13,16 @@ import sys
 
 
 def per_dispatch(d, counter, kernel):
+    """Summed counter per dispatch of the kernel.  `kernel` is a substring of the kernel name; K1's
+    conditional re-linearisation instantiation (`k_linearize<..., true>`, a no-op launch on most trials)
+    is excluded so that the average is over the real K1 launches."""
     vals = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            if row["Counter_Name"] == counter and kernel in row["Kernel_Name"]:
+            name = row["Kernel_Name"]
+            if kernel == "k_linearize" and "true>" in name:
+                continue
+            if row["Counter_Name"] == counter and kernel in name:
                 k = (row["Process_Id"], row["Dispatch_Id"])
                 vals[k] = vals.get(k, 0.0) + float(row["Counter_Value"])
     return list(vals.values())
@@ -34,7 +40,9 @@ def main():
              "fetch_size_kib_avg": fkib, "write_size_kib_avg": wkib,
              "read_bytes_corrected": 2 * fkib * 1024, "write_bytes": wkib * 1024,
              "hbm_bytes_per_launch": 2 * fkib * 1024 + wkib * 1024,
-             "correction": "read = 2 x FETCH_SIZE (gfx950 half-count of wide coalesced reads), write = WRITE_SIZE"}
+             "correction": "read = 2 x FETCH_SIZE, write = WRITE_SIZE (calibrated with tools/pmc_calib.hip: "
+                           "FETCH_SIZE = 0.5 x bytes for 1/4/8/16-B coalesced loads, cache-resident or not; "
+                           "WRITE_SIZE = bytes for 16-B stores)"}
     db = json.load(open(out)) if os.path.exists(out) else {}
     db[key] = entry
     json.dump(db, open(out, "w"), indent=1)

@@ -28,4 +28,5 @@ with open(f"profiles/{tag}_pmc_summary_{name}.csv", "w") as out:
         for k, v in sorted(acc.items(), key=lambda kv: -sum(kv[1])):
             out.write(f"{ctr},\"{k}\",{len(v)},{sum(v) / len(v):.1f}\n")
 shutil.copy(f"{src}/{tag}_k1_traffic.json", "profiles/k1_traffic.json")  # the file the bench line read
+shutil.copy(f"{src}/{tag}_pmc_calib.json", f"profiles/{tag}_pmc_calib.json")
 print("saved", tag)
