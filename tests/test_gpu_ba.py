@@ -397,3 +397,28 @@ def test_device_loop_rejections_and_limits(gpu_available):
         (a, sa), (b, sb) = res
         assert (a.njev, a.nfev, a.status) == (b.njev, b.nfev, b.status), (a, b)
         np.testing.assert_allclose(sb[0], sa[0], rtol=0, atol=1e-10)
+
+
+def test_save_restore_state_restarts_identically(gpu_available):
+    """ptzba_save_state / ptzba_restore_state (device-resident restart point, no host upload): the
+    restored state is x0 bit for bit, and a second solve from it repeats the first one exactly
+    (deterministic kernels; the Marquardt scaling is reset as by set_state)."""
+    import ptzba
+    import synthetic
+    p = synthetic.make_problem("config1", seed=3)
+    h = ptzba.BAHandle(0)
+    h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=1, loss=1, f_scale=1.0)
+    h.set_state(p.init_ptz, p.init_rays)
+    h.save_state()
+    runs = []
+    for _ in range(2):
+        h.restore_state()
+        ptz0, rays0 = h.get_state()
+        assert np.array_equal(ptz0, np.asarray(p.init_ptz, np.float64).reshape(ptz0.shape))
+        assert np.array_equal(rays0, np.asarray(p.init_rays, np.float64).reshape(rays0.shape))
+        res = ptzba.LMSolver(h, ftol=1e-6, xtol=1e-10, max_iter=30).run()
+        runs.append((res, h.get_state()))
+    (a, sa), (b, sb) = runs
+    assert (a.njev, a.nfev, a.status) == (b.njev, b.nfev, b.status) and a.cost == b.cost
+    assert np.array_equal(sa[0], sb[0]) and np.array_equal(sa[1], sb[1])
+    h.close()
