@@ -194,8 +194,17 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
 #pragma unroll
     for (int q = 0; q < NSL; ++q) {
       const int e = t + 512 * q, j = e >> 6, ln = e & 63;
+      if constexpr (sizeof(real) == 4) {
+        // fp32: W as component pairs (w_2r, w_2r+1) per lane, so the packed FMAs take one half of a
+        // loaded pair for both result halves (op_sel) instead of building splat pairs with moves
+        float2* w2p = reinterpret_cast<float2*>(&sW[0][0][0][0]) + ((buf * SNB + j) * 3) * WAVE + ln;
 #pragma unroll
-      for (int k = 0; k < 6; ++k) sW[buf][j][k][ln] = rwin[q] ? rw[q][k] : (real)0;
+        for (int r = 0; r < 3; ++r)
+          w2p[r * WAVE] = rwin[q] ? make_float2(rw[q][2 * r], rw[q][2 * r + 1]) : make_float2(0.f, 0.f);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) sW[buf][j][k][ln] = rwin[q] ? rw[q][k] : (real)0;
+      }
     }
     if (t < SNB * SF) {
       // pair layout (fp32): element (frame 2p + h, component k) at [2p][0] + 2 k + h of the pair's 16 reals
@@ -251,9 +260,10 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
         for (int k = 0; k < 9; ++k) accp[pp][k] = f2{0.f, 0.f};
 #pragma unroll 2
       for (int j = 0; j < SNB; ++j) {
-        float w2[6];
+        const f2* wsrc = reinterpret_cast<const f2*>(&sW[0][0][0][0]) + ((buf * SNB + j) * 3) * WAVE + lane;
+        f2 wp[3];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) w2[k] = sW[buf][j][k][lane];
+        for (int r = 0; r < 3; ++r) wp[r] = wsrc[r * WAVE];
 #pragma unroll
         for (int pp = 0; pp < SFW / 2; ++pp) {
           const f2* ys = reinterpret_cast<const f2*>(&sY[buf][j][SFW * wv + 2 * pp][0]);
@@ -264,9 +274,10 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
           for (int q = 0; q < 3; ++q)
 #pragma unroll
             for (int r = 0; r < 3; ++r) {
-              accp[pp][3 * q + r] = __builtin_elementwise_fma(y[2 * q], f2{w2[2 * r], w2[2 * r]}, accp[pp][3 * q + r]);
-              accp[pp][3 * q + r] =
-                  __builtin_elementwise_fma(y[2 * q + 1], f2{w2[2 * r + 1], w2[2 * r + 1]}, accp[pp][3 * q + r]);
+              accp[pp][3 * q + r] = __builtin_elementwise_fma(y[2 * q], __builtin_shufflevector(wp[r], wp[r], 0, 0),
+                                                              accp[pp][3 * q + r]);
+              accp[pp][3 * q + r] = __builtin_elementwise_fma(y[2 * q + 1], __builtin_shufflevector(wp[r], wp[r], 1, 1),
+                                                              accp[pp][3 * q + r]);
             }
         }
       }
