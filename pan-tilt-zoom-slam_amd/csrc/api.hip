@@ -728,7 +728,6 @@ static void linearize_into(ptzba_ctx* h, int slot, const int* run_if = nullptr) 
   LinArgs a;
   a.lm_work = h->lm_order.as<int4>();
   a.n_work = h->n_work;
-  a.n_rec = h->n_rec;
   a.lm_seg_begin = h->lm_seg_begin.as<int32_t>();
   a.seg_frame = h->seg_frame.as<int32_t>();
   a.seg_rec_begin = h->seg_rec_begin.as<int64_t>();

@@ -155,8 +155,8 @@ __global__ __launch_bounds__(256, K1_MIN_WAVES) void k_linearize(LinArgs a) {
   double V00 = 0, V01 = 0, V11 = 0, g0 = 0, g1 = 0, cost = 0;
 
   // phase B record group: K1_UNROLL batches of 64 records (1-byte segment key, obs delta x, y, weight).
-  // Loads are unconditional (index clamped to the record array, not to the window: the first group can
-  // then be requested before the window's end is known), validity is recomputed where the group is
+  // Loads are unconditional (index clamped to the window's last record: lanes past the end re-read a
+  // line already fetched, not the next landmark's records), validity is recomputed where the group is
   // consumed: a conditional load would merge at a join and force its wait early.
   struct Grp {
     int key[K1_UNROLL];
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(256, K1_MIN_WAVES) void k_linearize(LinArgs a) {
   auto load_grp = [&](Grp& g, int64_t rb, int64_t r1) {
 #pragma unroll
     for (int u = 0; u < K1_UNROLL; ++u) {
-      const int64_t r = min(rb + u * WAVE + lane, a.n_rec - 1);
+      const int64_t r = min(rb + u * WAVE + lane, r1 - 1);
       g.key[u] = a.rec_key[r];
       if constexpr (sizeof(real) == 4) {
         const float2 o = reinterpret_cast<const float2*>(rec_xy)[r];

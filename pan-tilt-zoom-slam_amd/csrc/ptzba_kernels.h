@@ -9,7 +9,6 @@ constexpr int K1_SEGW = 128;  // K1 segments per LDS window per wave
 struct LinArgs {
   const int4* lm_work;           // [n_work] {landmark, s0, s1, first record}, heaviest first
   int n_work;
-  int64_t n_rec;                 // records in total (K1 clamps its unconditional loads to the array)
   const int32_t* lm_seg_begin;   // [n_lm+1]
   const int32_t* seg_frame;      // [n_seg]
   const int64_t* seg_rec_begin;  // [n_seg+1]
