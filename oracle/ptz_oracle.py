@@ -408,8 +408,12 @@ def solve_scipy(x0_free, n_pose, n_landmark, u, v, ref_pose, frame, landmark, xy
     if max_nfev is not None:
         kw['max_nfev'] = max_nfev
     if analytic:
-        kw['jac'] = lambda x: ba_jacobian(x, n_pose, n_landmark, u, v, ref_pose, frame, landmark)
-        kw['tr_solver'] = 'exact' if len(x0_free) < 2000 else 'lsmr'
+        if len(x0_free) < 2000:  # scipy's 'exact' trust-region solver needs a dense Jacobian
+            kw['jac'] = lambda x: ba_jacobian(x, n_pose, n_landmark, u, v, ref_pose, frame, landmark).toarray()
+            kw['tr_solver'] = 'exact'
+        else:
+            kw['jac'] = lambda x: ba_jacobian(x, n_pose, n_landmark, u, v, ref_pose, frame, landmark)
+            kw['tr_solver'] = 'lsmr'
     else:
         kw['jac_sparsity'] = ba_jacobian_sparsity(n_pose, n_landmark, frame, landmark)
     return least_squares(fun, x0_free, **kw)
