@@ -161,7 +161,8 @@ static int upload_records(ptzba_ctx* h, const std::vector<int64_t>& order, const
     xy[2 * r] = (real)(obs_xy[2 * order[r]] - base[2 * s]);
     xy[2 * r + 1] = (real)(obs_xy[2 * order[r] + 1] - base[2 * s + 1]);
   }
-  if (h->rec_xy.alloc(xy.size() * sizeof(real))) return -1;
+  // padded by 4 records: K1's coarsened loads read whole 4-record groups
+  if (h->rec_xy.alloc((xy.size() + 8) * sizeof(real))) return -1;
   HIPCHK(hipMemcpy(h->rec_xy.p, xy.data(), xy.size() * sizeof(real), hipMemcpyHostToDevice));
   if (w) {
     std::vector<real> ww(h->n_rec);
@@ -627,7 +628,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   if (rc) return rc;
   if (upload(h->seg_base, seg_base)) return -1;
   {  // K1's 1-byte segment key: the record's segment within its landmark's window of K1_SEGW segments
-    std::vector<uint8_t> key(n_obs);
+    std::vector<uint8_t> key(n_obs + 4);  // + 4: K1 reads whole 4-record key groups
     for (int64_t k = 0; k < n_obs; ++k) {
       const int32_t sg = rec_seg[k];
       key[k] = (uint8_t)((sg - lm_seg_begin[seg_lm[sg]]) % K1_SEGW);

@@ -77,6 +77,9 @@ constexpr int SEGW = K1_SEGW;  // segments per LDS window per wave
 #ifndef K1_FTV
 #define K1_FTV 1  // phase-C frame tables loaded during phase A
 #endif
+#ifndef K1_COARSE
+#define K1_COARSE 1  // 0: 1 record per lane per batch; 1: 4 records per lane per batch, one scan per 256 records
+#endif
 #ifndef K1_MIN_WAVES
 #define K1_MIN_WAVES 4  // waves per SIMD the register budget must allow (occupancy)
 #endif
@@ -229,13 +232,109 @@ __global__ __launch_bounds__(256, K1_MIN_WAVES) void k_linearize(LinArgs a) {
     }
   };
 
+#if K1_COARSE
+  // thread-coarsened variant: a lane owns 4 consecutive records of a 256-record batch (4-aligned:
+  // one 4-B key load and two 16-B delta loads per lane), reduces its own runs, and only its tail run
+  // enters the wave's segmented scan (one scan per 256 records); records before r0 / after r1 of the
+  // aligned batch are masked (the record arrays are padded to a multiple of 4)
+  struct CGrp {
+    uint32_t key4;
+    real ox[4], oy[4], wt[4];
+  };
+  auto load_cgrp = [&](CGrp& g, int64_t rb, int64_t r1) {
+    const int64_t q = min(rb + 4 * lane, (r1 - 1) & ~(int64_t)3);
+    g.key4 = *reinterpret_cast<const uint32_t*>(a.rec_key + q);
+    if constexpr (sizeof(real) == 4) {
+      const float4 p0 = reinterpret_cast<const float4*>(rec_xy)[q / 2];
+      const float4 p1 = reinterpret_cast<const float4*>(rec_xy)[q / 2 + 1];
+      g.ox[0] = p0.x; g.oy[0] = p0.y; g.ox[1] = p0.z; g.oy[1] = p0.w;
+      g.ox[2] = p1.x; g.oy[2] = p1.y; g.ox[3] = p1.z; g.oy[3] = p1.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double2 o = reinterpret_cast<const double2*>(rec_xy)[q + j];
+        g.ox[j] = o.x; g.oy[j] = o.y;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) g.wt[j] = rec_w ? rec_w[min(q + j, r1 - 1)] : (real)1;
+  };
+  auto consume_c = [&](const CGrp& g, int64_t rb, int64_t r0, int64_t r1) {
+    int key[4];
+    real v[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t idx = rb + 4 * lane + j;
+      const bool valid = idx >= r0 && idx < r1;
+      key[j] = valid ? (int)((g.key4 >> (8 * j)) & 0xffu) : (idx < r0 ? -1 : 255);
+      real rx = 0, ry = 0;
+      if (valid) {
+        rx = sx[key[j]] - g.ox[j];
+        ry = sy[key[j]] - g.oy[j];
+      }
+      const real wt = valid ? g.wt[j] : (real)0;
+      real wx, wy, c;
+      if constexpr (LOSS == 0) {
+        wx = wt; wy = wt;
+        c = wt * (rx * rx + ry * ry);
+      } else {
+        real zx = rx * rx * ifs2, zy = ry * ry * ifs2;
+        bool ix = zx <= (real)1, iy = zy <= (real)1;
+        real sqx, sqy;
+        if constexpr (sizeof(real) == 4) {
+          const real rsx = __builtin_amdgcn_rsqf(ix ? (real)1 : zx), rsy = __builtin_amdgcn_rsqf(iy ? (real)1 : zy);
+          sqx = zx * rsx; sqy = zy * rsy;
+          wx = ix ? wt : wt * rsx;
+          wy = iy ? wt : wt * rsy;
+        } else {
+          sqx = sqrt(zx); sqy = sqrt(zy);
+          wx = ix ? wt : wt / sqx;
+          wy = iy ? wt : wt / sqy;
+        }
+        c = wt * fs2 * ((ix ? zx : (real)2 * sqx - (real)1) + (iy ? zy : (real)2 * sqy - (real)1));
+      }
+      cost += (double)c;
+      v[j][0] = wx; v[j][1] = wy; v[j][2] = wx * rx; v[j][3] = wy * ry;
+    }
+    // the lane's tail run (key of its last record) joins the scan; earlier runs are the lane's alone
+    // unless they continue a previous lane's tail: LDS atomic adds for those
+    const int kt = key[3];
+    real t0 = v[3][0], t1 = v[3][1], t2 = v[3][2], t3 = v[3][3];
+#pragma unroll
+    for (int j = 2; j >= 0; --j) {
+      if (key[j] == kt) {
+        t0 += v[j][0]; t1 += v[j][1]; t2 += v[j][2]; t3 += v[j][3];
+      } else if (key[j] >= 0) {
+        atomicAdd(acc0 + key[j], v[j][0]); atomicAdd(acc1 + key[j], v[j][1]);
+        atomicAdd(acc2 + key[j], v[j][2]); atomicAdd(acc3 + key[j], v[j][3]);
+      }
+    }
+    const int kenc = kt + 2;
+    seg_scan_step<DPP_ROW_SHR1, 0xf>(kenc, t0, t1, t2, t3);
+    seg_scan_step<DPP_ROW_SHR2, 0xf>(kenc, t0, t1, t2, t3);
+    seg_scan_step<DPP_ROW_SHR4, 0xf>(kenc, t0, t1, t2, t3);
+    seg_scan_step<DPP_ROW_SHR8, 0xf>(kenc, t0, t1, t2, t3);
+    seg_scan_step<DPP_ROW_BCAST15, 0xa>(kenc, t0, t1, t2, t3);
+    seg_scan_step<DPP_ROW_BCAST31, 0xc>(kenc, t0, t1, t2, t3);
+    const int knext = dpp_i<DPP_WAVE_SHL1, 0xf>(kenc);
+    if (knext != kenc && kt >= 0 && kt < SEGW) {
+      acc0[kt] += t0; acc1[kt] += t1; acc2[kt] += t2; acc3[kt] += t3;
+    }
+  };
+#endif
+
   for (int w0 = s0; w0 < s1; w0 += SEGW) {
     const int w1 = min(s1, w0 + SEGW);
     const int64_t r0 = (w0 == s0) ? (int64_t)(uint32_t)wd.w : a.seg_rec_begin[w0];
     const int64_t r1 = a.seg_rec_begin[w1];
     // the window's first record group is requested before phase A: its latency overlaps the projections
+#if K1_COARSE
+    CGrp ca, cb;
+    load_cgrp(ca, r0 & ~(int64_t)3, r1);
+#else
     Grp ga, gb;
     load_grp(ga, r0, r1);
+#endif
     // phase A: fp64 projection of every segment of the window (lanes over segments), kept as the
     // offset from the segment's base observation so phase B works on O(residual) magnitudes.  The
     // frame ids and the phase-C frame tables stay in registers.
@@ -266,6 +365,15 @@ __global__ __launch_bounds__(256, K1_MIN_WAVES) void k_linearize(LinArgs a) {
     wave_lds_fence();
     // phase B: stream the window's records (coalesced), segmented reduction into LDS.  Two register
     // groups alternate: the next group's loads are in flight while the current one is consumed.
+#if K1_COARSE
+    for (int64_t rb = r0 & ~(int64_t)3; rb < r1; rb += 2 * 4 * WAVE) {
+      load_cgrp(cb, rb + 4 * WAVE, r1);
+      consume_c(ca, rb, r0, r1);
+      if (rb + 4 * WAVE >= r1) break;
+      load_cgrp(ca, rb + 2 * 4 * WAVE, r1);
+      consume_c(cb, rb + 4 * WAVE, r0, r1);
+    }
+#else
     for (int64_t rb = r0; rb < r1; rb += 2 * K1_UNROLL * WAVE) {
       load_grp(gb, rb + K1_UNROLL * WAVE, r1);
       consume(ga, rb, r1);
@@ -273,6 +381,7 @@ __global__ __launch_bounds__(256, K1_MIN_WAVES) void k_linearize(LinArgs a) {
       load_grp(ga, rb + 2 * K1_UNROLL * WAVE, r1);
       consume(gb, rb + K1_UNROLL * WAVE, r1);
     }
+#endif
     wave_lds_fence();
     // phase C: per-segment Jacobian and normal-equation blocks
 #pragma unroll
