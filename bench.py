@@ -12,13 +12,18 @@ continues until exactly K iterations were timed.  Inputs are resident in HBM bef
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config config3] [--form pair|dedup]
 
-N > 1 (torchrun, one process per GPU): the records are sharded by landmark block across ranks
-(poses replicated); the reduced camera system and the partial scalars are summed with an RCCL
-all-reduce over xGMI each iteration (`scaling: strong`, same problem at every N).
+N > 1 (one process per GPU): `--gpus N` without a torch.distributed environment re-launches this script
+under `python -m torch.distributed.run --nproc-per-node N` (a child process, started before anything
+touches the GPU); under the launcher the records are sharded by landmark block across ranks (poses
+replicated) and the reduced camera system and the partial scalars are summed with an RCCL all-reduce
+over xGMI each iteration (`scaling: strong`, same problem at every N).  A world size that differs from
+--gpus is an error.  `--dry-run` stops after the rendezvous (launcher plumbing test, no GPU).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -43,8 +48,31 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-accuracy", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "k1_traffic.json"))
-    ap.add_argument("--cpu-sample-kf", type=int, default=80)
+    ap.add_argument("--cpu-sample-kf", default="40,60,80",
+                    help="keyframe windows of the CPU baseline fit (comma separated)")
+    ap.add_argument("--cpu-full", action="store_true",
+                    help="time the CPU restatement on the full problem (bounded to --cpu-full-nfev evaluations)")
+    ap.add_argument("--cpu-full-nfev", type=int, default=3)
+    ap.add_argument("--no-secondary", action="store_true", help="skip the fp64 / linear-loss leg")
+    ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache K1 pass")
+    ap.add_argument("--dry-run", action="store_true", help="launcher / rendezvous plumbing only (no GPU work)")
     return ap.parse_args()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(a):
+    """--gpus N > 1 outside a torch.distributed launch: run N ranks of this script under
+    torch.distributed.run (a child process; this parent never touches the GPU) and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 class _DevArray:
@@ -89,51 +117,112 @@ def survey_bytes_k1(info, precision):
         info["n_pose"] * 9 * s
 
 
-def cpu_baseline(prob, n_kf_sample):
-    """Faithful CPU restatement (oracle): vectorised reference residual + scipy trf (x_scale='jac',
-    ftol=1e-4, FD Jacobian with jac_sparsity), 1 thread, on a keyframe-window sample of the headline
-    problem; it/s scaled to the full problem by the record ratio."""
-    from threadpoolctl import threadpool_limits
-    sys.path.insert(0, ROOT)
-    from oracle import ptz_oracle as orc
-    keep = (prob.frame < n_kf_sample)
-    # matches whose both records are inside the window
+def _cpu_window(prob, n_kf):
+    """Sub-problem of the first n_kf keyframes: matches whose both records lie inside the window."""
+    keep = (prob.frame < n_kf)
     m_keep = keep[0::2] & keep[1::2]
     rec_keep = np.repeat(m_keep, 2)
     frame = prob.frame[rec_keep].astype(np.int64)
     lm_old = prob.landmark[rec_keep].astype(np.int64)
     uniq, lm = np.unique(lm_old, return_inverse=True)
     xy = prob.xy[rec_keep]
-    n, m = n_kf_sample, len(uniq)
-    x0 = np.concatenate([prob.init_ptz[1:n].reshape(-1), prob.init_rays[uniq].reshape(-1)])
+    x0 = np.concatenate([prob.init_ptz[1:n_kf].reshape(-1), prob.init_rays[uniq].reshape(-1)])
+    return frame, lm, xy, len(uniq), x0
+
+
+def cpu_baseline(prob, windows, full=False, full_nfev=3):
+    """Faithful CPU restatement (oracle): vectorised reference residual + scipy trf (x_scale='jac',
+    ftol=1e-4, FD Jacobian with jac_sparsity), 1 thread.  Default: timed on keyframe windows of the headline
+    problem and extrapolated to the full record count with a least-squares power law t = c R^alpha fitted
+    over the windows (SURVEY's full-size run is super-linear in R).  full=True: the full problem itself,
+    bounded to `full_nfev` residual evaluations (one Jacobian), i.e. a measurement, not a fit."""
+    import scipy
+    from threadpoolctl import threadpool_limits, threadpool_info
+    sys.path.insert(0, ROOT)
+    from oracle import ptz_oracle as orc
+    R_full = len(prob.frame)
+    env = dict(os_cpu_count=os.cpu_count(), scipy=scipy.__version__, numpy=np.__version__, threads_used=1,
+               blas=[{k: d.get(k) for k in ("internal_api", "num_threads")} for d in threadpool_info()])
     with threadpool_limits(limits=1):
-        t0 = time.perf_counter()
-        res = orc.solve_scipy(x0, n, m, prob.u, prob.v, prob.init_ptz[0], frame, lm, xy, ftol=1e-4)
-        dt = time.perf_counter() - t0
-    its = res.njev / dt
-    ratio = len(frame) / len(prob.frame)
-    return dict(value=its * ratio, unit="BA it/s", cores=1, kind="port",
-                sample=f"scipy trf (x_scale='jac', ftol=1e-4, FD jac_sparsity) on the first {n_kf_sample} keyframes "
-                       f"of {prob.meta.get('config')} ({len(frame)} of {len(prob.frame)} pair records, {m} landmarks): "
-                       f"{res.njev} iterations in {dt:.2f} s = {its:.4f} it/s, scaled by the record ratio {ratio:.4f}",
-                sample_its=its, sample_time_s=dt)
+        if full:
+            frame = prob.frame.astype(np.int64)
+            lm = prob.landmark.astype(np.int64)
+            x0 = np.concatenate([prob.init_ptz[1:].reshape(-1), prob.init_rays.reshape(-1)])
+            t0 = time.perf_counter()
+            res = orc.solve_scipy(x0, prob.n_pose, prob.n_landmark, prob.u, prob.v, prob.init_ptz[0], frame, lm,
+                                  prob.xy, ftol=1e-4, max_nfev=full_nfev)
+            dt = time.perf_counter() - t0
+            its = max(res.njev, 1) / dt
+            return dict(value=its, unit="BA it/s", cores=1, kind="port", env=env,
+                        sample=f"scipy trf (x_scale='jac', ftol=1e-4, FD jac_sparsity) on the FULL {prob.meta.get('config')} "
+                               f"({R_full} pair records), stopped after max_nfev={full_nfev}: {res.njev} Jacobian(s), "
+                               f"{res.nfev} evaluations in {dt:.1f} s")
+        pts = []
+        for n_kf in windows:
+            frame, lm, xy, m, x0 = _cpu_window(prob, n_kf)
+            t0 = time.perf_counter()
+            res = orc.solve_scipy(x0, n_kf, m, prob.u, prob.v, prob.init_ptz[0], frame, lm, xy, ftol=1e-4)
+            dt = time.perf_counter() - t0
+            pts.append((n_kf, len(frame), m, res.njev, dt, dt / max(res.njev, 1)))
+    lr = np.log([p[1] for p in pts])
+    lt = np.log([p[5] for p in pts])
+    alpha, logc = np.polyfit(lr, lt, 1) if len(pts) > 1 else (1.0, lt[0] - lr[0])
+    alpha = max(float(alpha), 1.0)  # never extrapolate sub-linearly in the record count
+    t_full = float(np.exp(logc + alpha * np.log(R_full))) if len(pts) > 1 else pts[0][5] * R_full / pts[0][1]
+    desc = "; ".join(f"{p[0]} KF: {p[1]} records, {p[2]} landmarks, {p[3]} its in {p[4]:.2f} s" for p in pts)
+    return dict(value=1.0 / t_full, unit="BA it/s", cores=1, kind="port", env=env, fit_alpha=alpha,
+                sample=f"scipy trf (x_scale='jac', ftol=1e-4, FD jac_sparsity), 1 thread, on keyframe windows of "
+                       f"{prob.meta.get('config')} [{desc}]; seconds/iteration fitted as c*R^{alpha:.3f} and evaluated at "
+                       f"the full R = {R_full} records")
+
+
+def _git_blob(path):
+    """Provenance of a committed measurement file: its git blob id (None outside a checkout)."""
+    try:
+        return subprocess.run(["git", "-C", ROOT, "hash-object", path], capture_output=True, text=True,
+                              timeout=10).stdout.strip() or None
+    except Exception:
+        return None
 
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if a.gpus > 1 and env_world is None:
+        sys.exit(launch_ranks(a))
+    world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but the launcher started {world} rank(s)", file=sys.stderr)
+        sys.exit(3)
     import torch
     dist = None
+    backend = "none"
     if world > 1:
         import torch.distributed as dist
         # one process per GPU over RCCL ("nccl").  PTZBA_DIST_BACKEND=gloo rehearses the same protocol
         # with several ranks on one device (the ranks then share GPU local % device_count)
-        local = local % max(1, torch.cuda.device_count())
-        torch.cuda.set_device(local)
-        dist.init_process_group(os.environ.get("PTZBA_DIST_BACKEND", "nccl"))
-    else:
+        backend = os.environ.get("PTZBA_DIST_BACKEND", "gloo" if a.dry_run else "nccl")
+        if not a.dry_run:
+            local = local % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend)
+        if dist.get_world_size() != a.gpus:
+            print(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {a.gpus}", file=sys.stderr)
+            sys.exit(3)
+        backend = dist.get_backend()
+    if a.dry_run:
+        if dist:
+            dist.barrier()
+        if rank == 0:
+            print(json.dumps({"metric": "BA iterations/sec at 500 KF x 20k rays; pan-tilt-focal RMSE vs reference",
+                              "value": None, "unit": "BA it/s", "n_gpus": world, "world_size": world,
+                              "backend": backend, "dry_run": True}))
+        if dist:
+            dist.destroy_process_group()
+        return
+    if world == 1:
         torch.cuda.set_device(0)
     import ptzba
     import synthetic
@@ -181,46 +270,57 @@ def main():
     h.set_state(prob.init_ptz, prob.init_rays)
     h.save_state()
 
-    def run_iters(k, timed=False):
+    def run_iters(hh, k, ar=None):
         done = 0
         solves = 0
         while done < k:
-            h.restore_state()
-            res = ptzba.LMSolver(h, ftol=1e-4, xtol=1e-8, max_iter=k - done, allreduce=allreduce).run()
+            hh.restore_state()
+            res = ptzba.LMSolver(hh, ftol=1e-4, xtol=1e-8, max_iter=k - done, allreduce=ar).run()
             done += max(res.njev, 1)
             solves += 1
             if res.njev == 0:
                 break
         return done, solves
 
+    def timed(hh, steps, ar=None):
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        its, nsolve = run_iters(hh, steps, ar)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if dist:
+            tt = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        return its, nsolve, el
+
     # warmup
-    run_iters(max(a.warmup, 1))
+    run_iters(h, max(a.warmup, 1), allreduce)
     # K1's HIP events stay on during the timed region (roofline), around every 4th K1 launch (each event
     # record adds a gap to the stream; the launches are identical work); the other groups' events are
     # timed in a separate pass afterwards
     h.reset_kernel_times(True, groups=1, stride=4)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    iters, solves = run_iters(a.steps, timed=True)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    iters, solves, elapsed = timed(h, a.steps, allreduce)
     k1_ms, k1_n = h.kernel_times()["linearize"]
     h.reset_kernel_times(True, groups=0xF)
-    run_iters(min(5, a.steps))
+    run_iters(h, min(5, a.steps), allreduce)
     kt = h.kernel_times()
+    # cold-cache K1: a 1 GiB scratch write before each timed K1 launch (outside its events) evicts L2 and
+    # the 256 MB Infinity Cache, so the launch streams its records from HBM (SURVEY §8d caveat)
+    k1_cold_ms = k1_cold_n = None
+    if not a.no_cold:
+        h.reset_kernel_times(True, groups=1, flush=True)
+        run_iters(h, min(5, a.steps), allreduce)
+        k1_cold_ms, k1_cold_n = h.kernel_times()["linearize"]
     h.reset_kernel_times(False)
 
     # accuracy: full fp32 LM solve vs a full fp64 solve of the same records, and vs ground truth
     accuracy = None
+    secondary = None
     if not a.no_accuracy and world == 1:
         h.set_state(prob.init_ptz, prob.init_rays)
         r32 = ptzba.LMSolver(h, ftol=1e-10, xtol=1e-12, max_iter=50).run()
@@ -236,14 +336,43 @@ def main():
                         rmse_fp64_vs_ground_truth=[float(x) for x in synthetic.pose_rmse(ptz64, prob.gt_ptz)],
                         cost_fp32=r32.cost, cost_fp64=r64.cost, iters_fp32=r32.njev, iters_fp64=r64.njev,
                         components=["pan_deg", "tilt_deg", "f_px"])
+    if not a.no_secondary and world == 1 and not (a.precision == "fp64" and a.loss == "linear"):
+        # the reference's own arithmetic and loss (fp64, linear: bundle_adjustment.py:200), same records
+        hs = ptzba.BAHandle(0)
+        hs.set_stream(stream.cuda_stream)
+        hs.set_problem(prob.n_pose, prob.n_landmark, frame, landmark, xy, prob.u, prob.v, weight=w,
+                       precision=ptzba.FP64, loss=ptzba.LOSS_LINEAR, f_scale=1.0)
+        hs.set_state(prob.init_ptz, prob.init_rays)
+        hs.save_state()
+        run_iters(hs, max(a.warmup, 1))
+        hs.reset_kernel_times(True, groups=1, stride=4)
+        s_it, s_solves, s_el = timed(hs, a.steps)
+        s_k1, _ = hs.kernel_times()["linearize"]
+        hs.reset_kernel_times(True, groups=0xF)
+        run_iters(hs, min(5, a.steps))
+        s_kt = hs.kernel_times()
+        hs.reset_kernel_times(False)
+        s_alg = algorithmic_bytes_k1(hs.info(), "fp64", w is not None)
+        s_ach = s_alg / (s_k1 * 1e-3) / 1e9 if s_k1 > 0 else 0.0
+        secondary = {"precision": "fp64", "loss": "linear", "value": s_it / s_el, "unit": "BA it/s",
+                     "ms_per_step": 1e3 * s_el / s_it, "iterations_timed": s_it, "solves_timed": s_solves,
+                     "roofline": {"bound": "hbm", "achieved": s_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": s_ach / HBM_PEAK_GBS, "k1_avg_ms": s_k1, "algorithmic_bytes_per_launch": s_alg,
+                                  "note": "fp64 K1 moves > 256 MB per launch (larger than the Infinity Cache)"},
+                     "kernel_ms": {k: v[0] for k, v in s_kt.items()}}
+        hs.close()
 
-    traffic = None  # PMC passes are taken on the whole problem (N = 1); a shard's launch moves less
+    traffic = traffic_src = None  # PMC passes are taken on the whole problem (N = 1); a shard's launch moves less
     if world == 1 and os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
             key = f"{a.config}/{a.form}/{a.precision}/{a.loss}"
             if key in tj:
                 traffic = tj[key]["hbm_bytes_per_launch"]
+                rel = os.path.relpath(a.traffic_json, ROOT)
+                traffic_src = {"file": rel, "git_blob": _git_blob(a.traffic_json), "key": key,
+                               "measured_by": tj[key].get("measured_by", "tools/gpu_measure.sh (rocprofv3 --pmc "
+                                                          "FETCH_SIZE / WRITE_SIZE, separate passes)")}
         except Exception:
             traffic = None
 
@@ -263,8 +392,11 @@ def main():
             "vs_baseline": None,
             "dtype": "f32" if a.precision == "fp32" else "f64",
             "data": "synthetic (SURVEY §8d generator, seed 0)",
-            "config": {"workload": f"{a.config}: {prob.n_pose} KF x {prob.n_landmark} ray landmarks, "
-                                   f"{info['n_obs']} {a.form}-form records/rank, {a.loss} loss, {a.precision} LM",
+            "world_size": world,
+            "backend": backend,
+            "config": {"workload": f"{a.config}: {prob.n_pose} KF x {synthetic.CONFIGS[a.config][1]} generated rays "
+                                   f"({prob.n_landmark} matched), {info['n_obs']} {a.form}-form records/rank, "
+                                   f"{a.loss} loss, {a.precision} LM",
                        "n_keyframes": prob.n_pose, "n_landmarks": prob.n_landmark, "n_records": int(len(prob.frame)),
                        "n_matches": int(prob.n_match), "n_pairs": prob.n_pairs, "form": a.form,
                        "parallelism": f"landmark-sharded x{world}" if world > 1 else "single GPU",
@@ -272,17 +404,26 @@ def main():
                        "allreduce_bytes_per_iteration": 8 * (exchange_doubles + ptzba.NSCALARS) if world > 1 else 0,
                        "iterations_timed": iters, "solves_timed": solves},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_linearize (K1)",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": "k_linearize (K1)",
                          "k1_avg_ms": k1_ms, "k1_launches_timed": k1_n, "k1_event_stride": 4, "algorithmic_bytes_per_launch": alg,
                          "survey_formula_bytes_per_launch": survey_bytes_k1(info, a.precision)},
             "kernel_ms": {k: v[0] for k, v in kt.items()},
         }
+        if k1_cold_ms:
+            ach_c = alg / (k1_cold_ms * 1e-3) / 1e9
+            out["roofline"]["cold_cache"] = {"k1_avg_ms": k1_cold_ms, "launches": k1_cold_n, "achieved": ach_c,
+                                             "frac": ach_c / HBM_PEAK_GBS,
+                                             "method": "1 GiB scratch write before each timed K1 launch"}
         if accuracy:
             out["accuracy"] = accuracy
+        if secondary:
+            out["fp64_linear"] = secondary
         if not a.no_cpu_baseline and world == 1:
             try:
-                cb = cpu_baseline(prob, a.cpu_sample_kf)
-                out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+                cb = cpu_baseline(prob, [int(x) for x in str(a.cpu_sample_kf).split(",") if x], full=a.cpu_full,
+                                  full_nfev=a.cpu_full_nfev)
+                out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample", "env")}
                 out["vs_cpu_baseline"] = out["value"] / cb["value"] if cb["value"] > 0 else None
             except Exception as e:  # report, never hide
                 out["cpu_baseline"] = {"value": None, "error": repr(e)}

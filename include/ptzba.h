@@ -141,6 +141,17 @@ PTZBA_EXPORT int ptzba_lm_build(ptzba_handle h);
 PTZBA_EXPORT int ptzba_lm_solve(ptzba_handle h);
 PTZBA_EXPORT int ptzba_lm_decide(ptzba_handle h, int trial);
 PTZBA_EXPORT int ptzba_lm_wait(ptzba_handle h, int trial, ptzba_lm_record* out);
+/* One-shot solve (single process): ptz_inout [3*n_pose] / rays_inout [2*n_landmark] carry x0 in and the
+ * optimum out (left unchanged on failure); opts NULL = the reference's option set (ftol 1e-4, xtol 1e-8,
+ * gtol off, 100 iterations).  Runs the device-driven LM above to termination.  Replaces the optimizer
+ * call of bundle_adjustment.py:200-202 and the empty file-based C stub bundle_adjustment_opt
+ * (rf_map/python_package/backup/bundle_adjustment_python.hpp:21-24). */
+typedef struct {
+  double cost, initial_cost, time_s;
+  int32_t iterations, nfev, trials, status;  /* status as ptzba_lm_record */
+} ptzba_report;
+PTZBA_EXPORT int ptzba_solve(ptzba_handle h, double* ptz_inout, double* rays_inout, const ptzba_lm_opts* opts,
+                             ptzba_report* report);
 PTZBA_EXPORT int ptzba_step(ptzba_handle h, double lambda);
 PTZBA_EXPORT int ptzba_read_scalars(ptzba_handle h, double* out /*PTZBA_NSCALARS*/);
 PTZBA_EXPORT int ptzba_accept(ptzba_handle h, int accept);
@@ -160,7 +171,10 @@ PTZBA_EXPORT int ptzba_sync(ptzba_handle h);
  * solve, back-substitution], measured with HIP events on the handle's stream; launches timed.
  * reset: `enable` bits 0-3 select the groups to time (1 K1, 2 Schur, 4 Cholesky, 8 back-subst.;
  * 0 off); bits 8-15 = sampling stride s (0/1: every launch): a group records its event pair around
- * every s-th launch only.  Each recorded event adds a few-microsecond gap to the stream. */
+ * every s-th launch only.  Each recorded event adds a few-microsecond gap to the stream.
+ * PTZBA_TIME_FLUSH (bit 16): cold-cache K1 timing -- before each timed K1 launch a kernel writes a
+ * 1 GiB scratch buffer (larger than L2 + the 256 MB Infinity Cache), outside the timed event pair. */
+#define PTZBA_TIME_FLUSH 0x10000
 PTZBA_EXPORT int ptzba_kernel_times(ptzba_handle h, double* ms_out /*4*/, int64_t* count_out /*4*/);
 PTZBA_EXPORT int ptzba_reset_kernel_times(ptzba_handle h, int enable);
 

@@ -80,8 +80,14 @@ constexpr int SEGW = K1_SEGW;  // segments per LDS window per wave
 #ifndef K1_COARSE
 #define K1_COARSE 1  // 0: 1 record per lane per batch; 1: 4 records per lane per batch, one scan per 256 records
 #endif
+#ifndef K1_COARSE64
+#define K1_COARSE64 K1_COARSE  // the same choice for the fp64 instantiation
+#endif
 #ifndef K1_MIN_WAVES
 #define K1_MIN_WAVES 4  // waves per SIMD the register budget must allow (occupancy)
+#endif
+#ifndef K1_MIN_WAVES64
+#define K1_MIN_WAVES64 K1_MIN_WAVES
 #endif
 
 // ---- DPP lane shuffles (VALU, no LDS round trip).  Lanes whose source is out of range or whose row
@@ -124,7 +130,8 @@ __device__ __forceinline__ void store4(double* p, double a, double b, double c, 
 // RELIN: the conditional re-linearisation after a rejected trial of the device-driven LM (a separate
 // instantiation, so profiles and K1 timings see only the unconditional launches)
 template <typename real, int LOSS, bool RELIN>
-__global__ __launch_bounds__(256, K1_MIN_WAVES) void k_linearize(LinArgs a) {
+__global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVES64) void k_linearize(LinArgs a) {
+  constexpr bool COARSE = sizeof(real) == 4 ? K1_COARSE : K1_COARSE64;
   __shared__ real s_x[4][SEGW], s_y[4][SEGW], s_acc[4][4][SEGW];
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
@@ -232,7 +239,6 @@ __global__ __launch_bounds__(256, K1_MIN_WAVES) void k_linearize(LinArgs a) {
     }
   };
 
-#if K1_COARSE
   // thread-coarsened variant: a lane owns 4 consecutive records of a 256-record batch (4-aligned:
   // one 4-B key load and two 16-B delta loads per lane), reduces its own runs, and only its tail run
   // enters the wave's segmented scan (one scan per 256 records); records before r0 / after r1 of the
@@ -317,24 +323,21 @@ __global__ __launch_bounds__(256, K1_MIN_WAVES) void k_linearize(LinArgs a) {
     seg_scan_step<DPP_ROW_BCAST15, 0xa>(kenc, t0, t1, t2, t3);
     seg_scan_step<DPP_ROW_BCAST31, 0xc>(kenc, t0, t1, t2, t3);
     const int knext = dpp_i<DPP_WAVE_SHL1, 0xf>(kenc);
+    // LDS atomic (no-return ds_add): the next lane's head run may add into the same slot in this batch
     if (knext != kenc && kt >= 0 && kt < SEGW) {
-      acc0[kt] += t0; acc1[kt] += t1; acc2[kt] += t2; acc3[kt] += t3;
+      atomicAdd(acc0 + kt, t0); atomicAdd(acc1 + kt, t1); atomicAdd(acc2 + kt, t2); atomicAdd(acc3 + kt, t3);
     }
   };
-#endif
 
   for (int w0 = s0; w0 < s1; w0 += SEGW) {
     const int w1 = min(s1, w0 + SEGW);
     const int64_t r0 = (w0 == s0) ? (int64_t)(uint32_t)wd.w : a.seg_rec_begin[w0];
     const int64_t r1 = a.seg_rec_begin[w1];
     // the window's first record group is requested before phase A: its latency overlaps the projections
-#if K1_COARSE
     CGrp ca, cb;
-    load_cgrp(ca, r0 & ~(int64_t)3, r1);
-#else
     Grp ga, gb;
-    load_grp(ga, r0, r1);
-#endif
+    if constexpr (COARSE) load_cgrp(ca, r0 & ~(int64_t)3, r1);
+    else load_grp(ga, r0, r1);
     // phase A: fp64 projection of every segment of the window (lanes over segments), kept as the
     // offset from the segment's base observation so phase B works on O(residual) magnitudes.  The
     // frame ids and the phase-C frame tables stay in registers.
@@ -365,23 +368,23 @@ __global__ __launch_bounds__(256, K1_MIN_WAVES) void k_linearize(LinArgs a) {
     wave_lds_fence();
     // phase B: stream the window's records (coalesced), segmented reduction into LDS.  Two register
     // groups alternate: the next group's loads are in flight while the current one is consumed.
-#if K1_COARSE
-    for (int64_t rb = r0 & ~(int64_t)3; rb < r1; rb += 2 * 4 * WAVE) {
-      load_cgrp(cb, rb + 4 * WAVE, r1);
-      consume_c(ca, rb, r0, r1);
-      if (rb + 4 * WAVE >= r1) break;
-      load_cgrp(ca, rb + 2 * 4 * WAVE, r1);
-      consume_c(cb, rb + 4 * WAVE, r0, r1);
+    if constexpr (COARSE) {
+      for (int64_t rb = r0 & ~(int64_t)3; rb < r1; rb += 2 * 4 * WAVE) {
+        load_cgrp(cb, rb + 4 * WAVE, r1);
+        consume_c(ca, rb, r0, r1);
+        if (rb + 4 * WAVE >= r1) break;
+        load_cgrp(ca, rb + 2 * 4 * WAVE, r1);
+        consume_c(cb, rb + 4 * WAVE, r0, r1);
+      }
+    } else {
+      for (int64_t rb = r0; rb < r1; rb += 2 * K1_UNROLL * WAVE) {
+        load_grp(gb, rb + K1_UNROLL * WAVE, r1);
+        consume(ga, rb, r1);
+        if (rb + K1_UNROLL * WAVE >= r1) break;
+        load_grp(ga, rb + 2 * K1_UNROLL * WAVE, r1);
+        consume(gb, rb + K1_UNROLL * WAVE, r1);
+      }
     }
-#else
-    for (int64_t rb = r0; rb < r1; rb += 2 * K1_UNROLL * WAVE) {
-      load_grp(gb, rb + K1_UNROLL * WAVE, r1);
-      consume(ga, rb, r1);
-      if (rb + K1_UNROLL * WAVE >= r1) break;
-      load_grp(ga, rb + 2 * K1_UNROLL * WAVE, r1);
-      consume(gb, rb + K1_UNROLL * WAVE, r1);
-    }
-#endif
     wave_lds_fence();
     // phase C: per-segment Jacobian and normal-equation blocks
 #pragma unroll

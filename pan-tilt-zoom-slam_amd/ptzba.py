@@ -52,6 +52,14 @@ class ptzba_lm_record(Structure):
                 ("accepted", c_int32)]
 
 
+class ptzba_report(Structure):
+    _fields_ = [("cost", c_double), ("initial_cost", c_double), ("time_s", c_double), ("iterations", c_int32),
+                ("nfev", c_int32), ("trials", c_int32), ("status", c_int32)]
+
+
+TIME_FLUSH = 0x10000  # include/ptzba.h PTZBA_TIME_FLUSH: cold-cache K1 timing
+
+
 class ptzba_problem_opts(Structure):
     _fields_ = [("precision", c_int32), ("loss", c_int32), ("f_scale", c_double), ("n_fixed", c_int32),
                 ("ordering", c_int32), ("frame_win_hi", c_void_p)]
@@ -88,6 +96,7 @@ def lib():
         "ptzba_build_reduced": ([V, D], I),
         "ptzba_solve_reduced": ([V], I),
         "ptzba_step": ([V, D], I),
+        "ptzba_solve": ([V, V, V, POINTER(ptzba_lm_opts), POINTER(ptzba_report)], I),
         "ptzba_lm_start": ([V], I),
         "ptzba_lm_init": ([V, POINTER(ptzba_lm_opts)], I),
         "ptzba_lm_build": ([V], I),
@@ -138,7 +147,7 @@ def lib():
 EXPORTED_SYMBOLS = [
     "ptzba_new", "ptzba_delete", "ptzba_last_error", "ptzba_version", "ptzba_set_stream", "ptzba_use_own_stream", "ptzba_set_problem",
     "ptzba_problem_info", "ptzba_solver_info", "ptzba_residual", "ptzba_set_state", "ptzba_get_state", "ptzba_linearize",
-    "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_read_scalars", "ptzba_accept",
+    "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_solve", "ptzba_read_scalars", "ptzba_accept",
     "ptzba_lm_start", "ptzba_lm_init", "ptzba_lm_build", "ptzba_lm_solve", "ptzba_lm_decide", "ptzba_lm_wait",
     "ptzba_exchange", "ptzba_exchange_packed", "ptzba_pack", "ptzba_unpack", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptzba_save_state", "ptzba_restore_state", "ptz_ray_to_image",
     "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks",
@@ -493,6 +502,20 @@ class BAHandle:
     def lm_decide(self, k):
         _check(lib().ptzba_lm_decide(self.h, int(k)), "ptzba_lm_decide")
 
+    def solve(self, ptz, rays, ftol=1e-4, xtol=1e-8, gtol=0.0, max_iter=100, lambda0=1e-4, min_lambda=1e-12,
+              max_lambda=1e16, max_retries=30, gauss_newton=False):
+        """One-shot ptzba_solve (C-driven LM to termination).  Returns (ptz [N,3], rays [M,2], LMResult)."""
+        ptz = _f64(ptz, (self.n_pose, 3)).copy()
+        rays = _f64(rays, (self.n_landmark, 2)).copy()
+        opts = ptzba_lm_opts(ftol, xtol, gtol, 0.0 if gauss_newton else lambda0, min_lambda, max_lambda, int(max_iter),
+                             int(max_retries), 1 if gauss_newton else 0)
+        rep = ptzba_report()
+        _check(lib().ptzba_solve(self.h, _ptr(ptz), _ptr(rays), ctypes.byref(opts), ctypes.byref(rep)), "ptzba_solve")
+        res = LMResult(status=rep.status, message=STATUS_MSG.get(rep.status, "?"), cost=rep.cost,
+                       initial_cost=rep.initial_cost, njev=rep.iterations, nfev=rep.nfev, iterations=rep.iterations,
+                       lam=float("nan"), time=rep.time_s, history=[], trials=rep.trials)
+        return ptz, rays, res
+
     def lm_wait(self, k):
         r = ptzba_lm_record()
         _check(lib().ptzba_lm_wait(self.h, int(k), ctypes.byref(r)), "ptzba_lm_wait")
@@ -520,10 +543,11 @@ class BAHandle:
     def sync(self):
         _check(lib().ptzba_sync(self.h), "ptzba_sync")
 
-    def reset_kernel_times(self, enable=True, groups=0xF, stride=1):
+    def reset_kernel_times(self, enable=True, groups=0xF, stride=1, flush=False):
         """Restart kernel timing; `groups` bitmask: 1 K1, 2 Schur, 4 Cholesky solve, 8 back-substitution;
-        events around every `stride`-th launch of a group (each event record adds a gap to the stream)."""
-        flags = (int(groups) | (max(1, min(255, int(stride))) << 8)) if enable else 0
+        events around every `stride`-th launch of a group (each event record adds a gap to the stream).
+        flush: cold-cache K1 timing (a 1 GiB scratch write before each timed K1 launch, outside the events)."""
+        flags = (int(groups) | (max(1, min(255, int(stride))) << 8) | (TIME_FLUSH if flush else 0)) if enable else 0
         _check(lib().ptzba_reset_kernel_times(self.h, flags), "ptzba_reset_kernel_times")
 
     def kernel_times(self):

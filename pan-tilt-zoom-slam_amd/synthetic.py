@@ -116,6 +116,21 @@ class Problem:
         return len(self.frame) // 2
 
 
+def _theta_window(f, pan, tilt, width=WIDTH, height=HEIGHT, u=U0, v=V0):
+    """Conservative [lo, hi] (deg) of the ray azimuths theta a camera can see: a pixel ray
+    c = [c0, c1, 1] has theta - pan = atan(c0 / (cos(tilt) + sin(tilt) c1)) while that denominator is
+    positive, so |theta - pan| <= atan(max|c0| / min(cos + sin c1)).  None when the image reaches the
+    horizon of the tilted frame (no bound: test every ray)."""
+    b = math.radians(tilt)
+    c0 = max(u, width - u) / f
+    c1 = max(v, height - v) / f
+    den = math.cos(b) - abs(math.sin(b)) * c1
+    if den <= 1e-3:
+        return None
+    half = math.degrees(math.atan(c0 / den)) + 0.5
+    return pan - half, pan + half
+
+
 def make_scene(n_kf, n_rays, pan_lo, pan_hi, seed=0, tilt_rows=None, noise=0.5,
                init_sigma=(0.5, 0.2, 40.0)):
     rng = np.random.default_rng(seed)
@@ -124,23 +139,34 @@ def make_scene(n_kf, n_rays, pan_lo, pan_hi, seed=0, tilt_rows=None, noise=0.5,
         tilts = rng.uniform(-12.0, -4.0, n_kf)
         phi_lo, phi_hi = -19.0, 3.0
     else:
+        # config 4: rows of keyframes at several tilts; a camera at tilt t sees elevations phi ~ t +- 7
+        # (config 3: tilt U[-12, -4], phi U[-19, 3]), so phi spans [min row - 7, max row + 7]
         rows = np.asarray(tilt_rows, np.float64)
         per = n_kf // len(rows)
         pans = np.tile(np.linspace(pan_lo, pan_hi, per), len(rows))
         tilts = np.repeat(rows, per) + rng.uniform(-1.0, 1.0, per * len(rows))
-        phi_lo, phi_hi = -(rows.max() + 7.0), -(rows.min() - 7.0)
-        phi_lo, phi_hi = max(phi_lo, -80.0), min(phi_hi, 80.0)
+        phi_lo, phi_hi = max(rows.min() - 7.0, -80.0), min(rows.max() + 7.0, 80.0)
     fs = rng.uniform(2500.0, 3500.0, len(pans))
     gt_ptz = np.stack([pans, tilts, fs], 1)
     theta = rng.uniform(pan_lo - 14.0, pan_hi + 14.0, n_rays)
     phi = rng.uniform(phi_lo, phi_hi, n_rays)
     gt_rays = np.stack([theta, phi], 1)
+    # rays sorted by azimuth: a frame projects only the rays inside its theta window (same visible ids,
+    # in the same ascending order, as projecting every ray)
+    by_theta = np.argsort(theta, kind="stable")
+    theta_sorted = theta[by_theta]
     kp_xy, kp_ray = [], []
     for i in range(len(pans)):
-        x, y, q2 = _project(U0, V0, fs[i], pans[i], tilts[i], theta, phi)
+        win = _theta_window(fs[i], pans[i], tilts[i])
+        if win is None:
+            cand = np.arange(n_rays)
+        else:
+            lo, hi = np.searchsorted(theta_sorted, win[0]), np.searchsorted(theta_sorted, win[1], side="right")
+            cand = np.sort(by_theta[lo:hi])
+        x, y, q2 = _project(U0, V0, fs[i], pans[i], tilts[i], theta[cand], phi[cand])
         vis = (q2 > 0) & (x > 0) & (x < WIDTH) & (y > 0) & (y < HEIGHT)
-        ids = np.flatnonzero(vis)
-        pts = np.stack([x[ids], y[ids]], 1) + rng.normal(0.0, noise, (len(ids), 2))
+        ids = cand[vis]
+        pts = np.stack([x[vis], y[vis]], 1) + rng.normal(0.0, noise, (len(ids), 2))
         kp_xy.append(pts)
         kp_ray.append(ids.astype(np.int64))
     init = gt_ptz.copy()
@@ -151,29 +177,37 @@ def make_scene(n_kf, n_rays, pan_lo, pan_hi, seed=0, tilt_rows=None, noise=0.5,
 def scene_pairs(scene, seed=0, min_match=20, max_match=200, overlap_deg=5.0, cap=True):
     """Ordered list of (i, j, idx_i list, idx_j list) for i<j: overlap mask on the *initial*
     poses (bundle_adjustment.py:135-144), shared keypoints = ground-truth matches, keep if
-    > min_match (image_process.py:590), cap to max_match with a seeded permutation."""
+    > min_match (image_process.py:590), cap to max_match with a seeded permutation.
+
+    Candidate pairs come from the shared-ray counts of the frame x ray incidence matrix (one sparse
+    product); the permutations are drawn for the kept pairs in (i, j) order, as a double loop would."""
+    import scipy.sparse as sp
     rng = np.random.default_rng(seed + 7919)
     n = len(scene.kp_xy)
     ip = scene.init_ptz
     n_rays = len(scene.gt_rays)
-    # position of each ray in each frame's keypoint list (-1 if not visible)
-    pos = []
-    for i in range(n):
-        p = np.full(n_rays, -1, np.int64)
-        p[scene.kp_ray[i]] = np.arange(len(scene.kp_ray[i]))
-        pos.append(p)
+    lens = np.array([len(r) for r in scene.kp_ray], np.int64)
+    inc = sp.csr_matrix((np.ones(int(lens.sum()), np.int32),
+                         (np.repeat(np.arange(n), lens), np.concatenate(scene.kp_ray) if n else [])),
+                        shape=(n, n_rays))
+    shared_cnt = sp.triu(inc @ inc.T, k=1).tocoo()
+    keep = shared_cnt.data > min_match
+    ci, cj = shared_cnt.row[keep].astype(np.int64), shared_cnt.col[keep].astype(np.int64)
+    ov = overlap_pan_angle(ip[ci, 2], ip[ci, 0], ip[cj, 2], ip[cj, 0], WIDTH)
+    sel = ov > overlap_deg
+    ci, cj = ci[sel], cj[sel]
+    order = np.lexsort((cj, ci))
     out = []
-    for i in range(n):
-        ov = overlap_pan_angle(ip[i, 2], ip[i, 0], ip[:, 2], ip[:, 0], WIDTH)
-        for j in range(i + 1, n):
-            if ov[j] <= overlap_deg:
-                continue
-            shared = scene.kp_ray[i][pos[j][scene.kp_ray[i]] >= 0]
-            if len(shared) <= min_match:
-                continue
-            if cap and len(shared) > max_match:
-                shared = shared[rng.permutation(len(shared))[:max_match]]
-            out.append((i, j, pos[i][shared], pos[j][shared]))
+    for i, j in zip(ci[order].tolist(), cj[order].tolist()):
+        ri, rj = scene.kp_ray[i], scene.kp_ray[j]          # ascending ray ids
+        pos = np.searchsorted(rj, ri)
+        hit = rj[np.minimum(pos, len(rj) - 1)] == ri
+        a = np.flatnonzero(hit)                           # positions in frame i (ascending ray id)
+        b = pos[hit]                                      # positions of the same rays in frame j
+        if cap and len(a) > max_match:
+            perm = rng.permutation(len(a))[:max_match]
+            a, b = a[perm], b[perm]
+        out.append((i, j, a, b))
     return out
 
 

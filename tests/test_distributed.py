@@ -108,3 +108,32 @@ def test_two_rank_solve_matches_single_rank(tmp_path):
                                      prob.landmark.astype(np.int64), prob.xy)
     g = J.T @ r
     assert res1.status == 2 and np.abs(g).max() < 1e-4 * np.abs(J).max()
+
+
+def _bench_line(out):
+    import json
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert lines, out
+    return json.loads(lines[-1])
+
+
+def test_bench_gpus_launches_ranks():
+    """`bench.py --gpus 2` outside a launcher starts 2 ranks (torch.distributed.run child process) that
+    rendezvous over gloo; --dry-run stops after the rendezvous (no GPU in this container)."""
+    import subprocess
+    env = dict(os.environ, PTZBA_DIST_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _bench_line(r.stdout)
+    assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["backend"] == "gloo"
+
+
+def test_bench_rejects_world_size_mismatch():
+    """A launcher world size that differs from --gpus is an error (exit 3), never a silent N=1 run."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
