@@ -87,7 +87,7 @@ constexpr int SEGW = K1_SEGW;  // segments per LDS window per wave
 #define K1_MIN_WAVES 4  // waves per SIMD the register budget must allow (occupancy)
 #endif
 #ifndef K1_MIN_WAVES64
-#define K1_MIN_WAVES64 K1_MIN_WAVES
+#define K1_MIN_WAVES64 3  // fp64: 4 waves/SIMD spill 128-196 B/lane; 3 fit (fp64 K1 193 -> 138 us, r02 A/B)
 #endif
 
 // ---- DPP lane shuffles (VALU, no LDS round trip).  Lanes whose source is out of range or whose row
