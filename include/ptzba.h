@@ -95,8 +95,10 @@ PTZBA_EXPORT int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_lan
  * [7] bytes of device memory held */
 PTZBA_EXPORT int ptzba_problem_info(ptzba_handle h, int64_t* info8);
 /* solver layout: [0] n_aug (system rows incl. padding), [1] ld, [2] factorisation launches (levels),
- * [3] ordering actually used (PTZBA_ORDER_*) */
-PTZBA_EXPORT int ptzba_solver_info(ptzba_handle h, int64_t* info4);
+ * [3] ordering actually used (PTZBA_ORDER_*), [4] back-substitution form (0 lookahead, 1 left-looking:
+ * systems whose lists exceed LDS), [5] dense landmark x frame slots, [6] Schur work items,
+ * [7] factor pattern tiles */
+PTZBA_EXPORT int ptzba_solver_info(ptzba_handle h, int64_t* info8);
 
 /* residual r[2*n_obs] = projection - observation, record order (== _compute_residual) at
  * x_full = [3*n_pose poses | 2*n_landmark rays] (fp64 host). Uses the handle's precision. */
@@ -221,6 +223,11 @@ PTZBA_EXPORT int ptz_refine_poses(int device, int32_t n_hyp, double* ptz_inout, 
  * pair_i/pair_j/pair_count: n_pairs; idx_a/idx_b: concatenated match keypoint indices.
  * kp_count[n_frames]: keypoints per frame.  Output landmark id per match (of the src keypoint) and
  * the landmark count; *n_inconsistent counts the reference's "in-consistent matching" warnings. */
+/* Coupling window of a record set (host only, O(n_obs)): win_out[f] = the highest frame that shares a
+ * landmark with frame f (>= f).  Computed over ALL records it is the frame_win_hi every rank of a
+ * landmark-sharded solve passes in ptzba_problem_opts. */
+PTZBA_EXPORT int ptzba_coupling_window(int32_t n_pose, int32_t n_landmark, int64_t n_obs, const int32_t* obs_frame,
+                                       const int32_t* obs_landmark, int32_t* win_out);
 PTZBA_EXPORT int ptzba_build_landmarks(int32_t n_frames, const int64_t* kp_count, int64_t n_pairs,
                                        const int32_t* pair_i, const int32_t* pair_j,
                                        const int64_t* pair_count, const int64_t* idx_a,

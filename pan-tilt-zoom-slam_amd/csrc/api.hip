@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -72,6 +73,8 @@ struct ptzba_ctx {
   bool nested = false;
   DBuf frame_pos, row_pad, bs_chain_off, bs_chain_cols, bs_upd_off, bs_upd_tiles, bs_la_tasks;
   int bs_nupd = 0, bs_npos = 0, bs_ntasks = 0;
+  DBuf bs_lo_off, bs_lo_tiles;  // left-looking back substitution lists (large systems)
+  bool bs_ll = false;
   DBuf xtiles, xbuf;  // packed exchange: tile list, buffer
   int n_xtiles = 0;
   DBuf ztiles;  // tiles zeroed before each build (the rest of the system region stays zero)
@@ -277,6 +280,7 @@ struct CholPlan {
   std::vector<int> chain_off, chain_cols, upd_off, upd_tiles;
   std::vector<int> la_tasks;  // lookahead back substitution: la [npos] | task_off [n_chain * BS_HELPERS + 1] | tasks
   int n_tasks = 0;
+  std::vector<int> lo_off, lo_tiles;  // left-looking back substitution: per position the solved row tiles coupled to it
   std::vector<int32_t> xtiles;  // (ti, tj) pairs the Schur kernel can write (before fill), for the exchange
   std::vector<int32_t> ztiles;  // (ti, tj) lower tiles of the factor's pattern (incl. fill): zeroed per build
   int n_levels = 0;
@@ -397,6 +401,18 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
       for (int j = 0; j < kt; ++j)
         if (in_chain[j] && nz[kt][j]) P.upd_tiles.push_back(j);
       P.upd_off.push_back((int)P.upd_tiles.size());
+    }
+  }
+  P.lo_off.assign(1, 0);
+  P.lo_tiles.clear();
+  for (size_t ch = 0; ch + 1 < P.chain_off.size(); ++ch) {
+    std::vector<uint8_t> in_chain(T, 0);
+    for (int q = P.chain_off[ch]; q < P.chain_off[ch + 1]; ++q) in_chain[P.chain_cols[q]] = 1;
+    for (int q = P.chain_off[ch]; q < P.chain_off[ch + 1]; ++q) {
+      const int kt = P.chain_cols[q];
+      for (int i = kt + 1; i < Tx; ++i)
+        if (in_chain[i] && nz[i][kt]) P.lo_tiles.push_back(i);
+      P.lo_off.push_back((int)P.lo_tiles.size());
     }
   }
   // lookahead back substitution: the next position's tile when the current row couples to it, and per
@@ -544,9 +560,21 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       for (int l : un) hi = std::max(hi, lm_meta[4 * l + 1]);
       const int nc = (hi - f1b) / WAVE + 1;
       for (int c = 0; c < nc; ++c) {
+        // a landmark enters chunk c only when it sees a frame of the chunk (its frame set can have gaps:
+        // on a multi-row keyframe grid a landmark seen by two tilt rows spans a whole row of frames)
         std::vector<int32_t> lst;
-        for (int l : un)
-          if (c == 0 || lm_meta[4 * l + 1] >= f1b + WAVE * c) lst.push_back(l);
+        const int c_lo = f1b + WAVE * c, c_hi = c_lo + WAVE - 1;
+        for (int l : un) {
+          if (c > 0) {
+            if (lm_meta[4 * l + 1] < c_lo) continue;
+            const int32_t* fb = seg_frame.data() + lm_seg_begin[l];
+            const int32_t* fe = seg_frame.data() + lm_seg_begin[l + 1];
+            const int32_t* it = std::lower_bound(fb, fe, c_lo);
+            if (it == fe || *it > c_hi) continue;
+          }
+          lst.push_back(l);
+        }
+        if (lst.empty()) continue;
         tiles.push_back(std::move(lst));
         tile_key.push_back(f1b);
         tile_key.push_back(c);
@@ -619,8 +647,8 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->n_aug = sorder.n_aug;
   h->nested = sorder.nested;
   h->ld = pad_tile(h->n_aug + 1);  // + augmented rhs row
-  // the back-substitution keeps x ([ld] doubles) in LDS next to 17 KiB of staging
-  if (h->ld > 17408) return fail("reduced system %d too large for the dense solver", h->n_sys);
+  // the back-substitution keeps x ([ld] doubles) in LDS
+  if (h->ld > CHOL_MAX_LD) return fail("reduced system %d too large for the dense solver", h->n_sys);
   CholPlan plan;
   make_plan(sorder, n_pose, o.n_fixed, win, h->ld, plan);
   h->chol_task_off = plan.level_off;
@@ -675,7 +703,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   if (upload(h->chol_tasks, plan.tasks) || upload(h->frame_pos, sorder.pos) || upload(h->row_pad, sorder.pad) ||
       upload(h->bs_chain_off, plan.chain_off) || upload(h->bs_chain_cols, plan.chain_cols) ||
       upload(h->bs_upd_off, plan.upd_off) || upload(h->bs_upd_tiles, plan.upd_tiles) || upload(h->xtiles, plan.xtiles) || upload(h->ztiles, plan.ztiles) ||
-      upload(h->bs_la_tasks, plan.la_tasks))
+      upload(h->bs_la_tasks, plan.la_tasks) || upload(h->bs_lo_off, plan.lo_off) || upload(h->bs_lo_tiles, plan.lo_tiles))
     return -1;
   h->n_xtiles = (int)(plan.xtiles.size() / 2);
   h->n_ztiles = (int)(plan.ztiles.size() / 2);
@@ -685,8 +713,10 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->bs_ntasks = plan.n_tasks;
   // the back-substitution keeps r and its update lists in LDS (plus ~9 KiB of static staging)
   // (lookahead form: + 48 KiB ring of M / L blocks)
-  if (h->ld * 8 + (std::max(h->bs_npos + 1 + h->bs_nupd, 2 * h->bs_npos + h->bs_ntasks)) * 4 > 100 * 1024)
-    return fail("reduced system %d too large for the dense solver's back-substitution", h->n_sys);
+  // (lookahead form: + 48 KiB ring of M / L blocks); larger systems take the left-looking form, whose lists
+  // stay in global memory
+  h->bs_ll = h->ld * 8 + (std::max(h->bs_npos + 1 + h->bs_nupd, 2 * h->bs_npos + h->bs_ntasks)) * 4 > 100 * 1024;
+  if (const char* e = getenv("PTZBA_BACKSOLVE")) h->bs_ll = h->bs_ll || std::string(e) == "ll";  // testing knob
   h->xbuf.release();  // allocated on first ptzba_exchange_packed
   HIPCHK(hipMemset(h->D_pose.p, 0, h->D_pose.bytes));
   HIPCHK(hipMemset(h->D_ray.p, 0, h->D_ray.bytes));
@@ -772,12 +802,16 @@ static void linearize_into(ptzba_ctx* h, int slot, const int* run_if = nullptr) 
   if (!run_if) tm_end(h, TM_K1);
 }
 
-int ptzba_solver_info(ptzba_handle h, int64_t* info4) {
+int ptzba_solver_info(ptzba_handle h, int64_t* info8) {
   if (!h || !h->have_problem) return fail("no problem set");
-  info4[0] = h->n_aug;
-  info4[1] = h->ld;
-  info4[2] = h->chol_levels;
-  info4[3] = h->nested ? PTZBA_ORDER_NESTED : PTZBA_ORDER_NATURAL;
+  info8[0] = h->n_aug;
+  info8[1] = h->ld;
+  info8[2] = h->chol_levels;
+  info8[3] = h->nested ? PTZBA_ORDER_NESTED : PTZBA_ORDER_NATURAL;
+  info8[4] = h->bs_ll ? 1 : 0;
+  info8[5] = h->n_slot;
+  info8[6] = h->n_s2_items;
+  info8[7] = h->n_ztiles;
   return 0;
 }
 
@@ -917,7 +951,8 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx) {
   launch_chol_backsolve(h->S(), h->ld, h->n_aug, h->n_chain, h->bs_npos, h->bs_chain_off.as<int>(),
                         h->bs_chain_cols.as<int>(), h->bs_upd_off.as<int>(), h->bs_upd_tiles.as<int>(), h->bs_nupd,
                         h->bs_la_tasks.as<int>(), h->bs_ntasks,
-                        h->Ldiag.as<double>(), h->Minv.as<double>(), h->dpose.as<double>(), h->st);
+                        h->Ldiag.as<double>(), h->Minv.as<double>(), h->dpose.as<double>(),
+                        h->bs_ll ? h->bs_lo_off.as<int>() : nullptr, h->bs_lo_tiles.as<int>(), h->st);
   tm_end(h, TM_CHOL);
   HIPCHK(hipGetLastError());
   tm_begin(h, TM_BACK);
@@ -1322,6 +1357,21 @@ int ptz_h_jacobian(int device, int64_t n, double u, double v, double f, double p
   launch_h_jacobian(n, u, v, f, pan, tilt, d6, dr, dH, nullptr);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(H_out, dH, nh * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int ptzba_coupling_window(int32_t n_pose, int32_t n_landmark, int64_t n_obs, const int32_t* obs_frame,
+                          const int32_t* obs_landmark, int32_t* win_out) {
+  if (n_pose < 1 || n_landmark < 0 || n_obs < 0 || !win_out || (n_obs > 0 && (!obs_frame || !obs_landmark)))
+    return fail("bad arguments");
+  std::vector<int32_t> hi(std::max(n_landmark, 1), -1);
+  for (int64_t r = 0; r < n_obs; ++r) {
+    const int32_t f = obs_frame[r], l = obs_landmark[r];
+    if (f < 0 || f >= n_pose || l < 0 || l >= n_landmark) return fail("record %lld out of range", (long long)r);
+    hi[l] = std::max(hi[l], f);
+  }
+  for (int f = 0; f < n_pose; ++f) win_out[f] = f;
+  for (int64_t r = 0; r < n_obs; ++r) win_out[obs_frame[r]] = std::max(win_out[obs_frame[r]], hi[obs_landmark[r]]);
   return 0;
 }
 

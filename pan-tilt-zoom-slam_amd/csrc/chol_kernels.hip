@@ -1056,6 +1056,80 @@ __global__ __launch_bounds__(64 * (BS_HELPERS + 2)) void k_chol_backsolve_la(
   }
 }
 
+// Left-looking back substitution for systems whose update lists do not fit the lookahead kernel's LDS
+// (multi-row keyframe grids: thousands of frames, a coupling band of ~60 tiles).  One 1024-thread
+// workgroup per chain; x (init y) stays in LDS, the lists come from global memory.  Per chain position
+// (column kt, descending): r_kt = y_kt - sum_i L_i,kt^T x_i over the already-solved row tiles i coupled
+// to kt (lo_off / lo_tiles: host-built, ascending i) -- wave w takes tiles w, w + 16, ..., lane =
+// (column c, row half h), 16 independent loads per tile; the per-wave partials are summed in a fixed
+// order (deterministic) and wave 0 solves x_kt = M_kt^T r_kt.
+constexpr int BSL_WAVES = 16;
+__global__ __launch_bounds__(64 * BSL_WAVES) void k_chol_backsolve_ll(
+    const double* __restrict__ L, int64_t ld, int n, const int* __restrict__ chain_off,
+    const int* __restrict__ chain_cols, const int* __restrict__ lo_off, const int* __restrict__ lo_tiles,
+    const double* __restrict__ Ldiag, const double* __restrict__ Minv, double* __restrict__ xout) {
+  extern __shared__ __attribute__((aligned(16))) double xv[];  // [ld]
+  __shared__ double red[BSL_WAVES][NB];
+  __shared__ double rk[NB];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int c = lane & 31, h = lane >> 5;
+  const int tn = n / NB, rn = n - tn * NB;
+  for (int i = t; i < ld; i += blockDim.x)
+    xv[i] = (i >= n) ? 0.0 : (i < tn * NB ? L[(int64_t)n * ld + i] : Ldiag[((int64_t)tn * NB + rn) * NB + (i - tn * NB)]);
+  __syncthreads();
+  const int q0 = chain_off[blockIdx.x], q1 = chain_off[blockIdx.x + 1];
+  for (int q = q0; q < q1; ++q) {
+    const int kt = chain_cols[q];
+    const int64_t c0 = (int64_t)kt * NB;
+    const int e0 = lo_off[q], e1 = lo_off[q + 1];
+    double acc = 0.0;
+    for (int e = e0 + wv; e < e1; e += 2 * BSL_WAVES) {
+      const bool two = e + BSL_WAVES < e1;  // wave-uniform
+      const int i0 = lo_tiles[e], i1 = lo_tiles[two ? e + BSL_WAVES : e];
+      const double* p0 = L + ((int64_t)i0 * NB + h * (NB / 2)) * ld + c0 + c;
+      const double* p1 = L + ((int64_t)i1 * NB + h * (NB / 2)) * ld + c0 + c;
+      double a0[NB / 2], a1[NB / 2];
+#pragma unroll
+      for (int r = 0; r < NB / 2; ++r) a0[r] = p0[(int64_t)r * ld];
+#pragma unroll
+      for (int r = 0; r < NB / 2; ++r) a1[r] = p1[(int64_t)r * ld];
+      const double* x0 = xv + (int64_t)i0 * NB + h * (NB / 2);
+      const double* x1 = xv + (int64_t)i1 * NB + h * (NB / 2);
+#pragma unroll
+      for (int r = 0; r < NB / 2; ++r) acc = fma(a0[r], x0[r], acc);
+      if (two) {
+#pragma unroll
+        for (int r = 0; r < NB / 2; ++r) acc = fma(a1[r], x1[r], acc);
+      }
+    }
+    acc += __shfl_xor(acc, 32, WAVE);
+    if (h == 0) red[wv][c] = acc;
+    __syncthreads();
+    if (wv == 0) {
+      double s = 0.0;
+#pragma unroll
+      for (int w = 0; w < BSL_WAVES; ++w) s += red[w][c];
+      if (h == 0) rk[c] = xv[c0 + c] - s;
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      const double* m = Minv + (int64_t)kt * NB * NB + c;  // x_c = sum_k M[k][c] r_k
+      double s4[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < NB / 2; ++k) {
+        const int kk = h * (NB / 2) + k;
+        s4[k & 3] = fma(m[kk * NB], rk[kk], s4[k & 3]);
+      }
+      double x = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+      x += __shfl_xor(x, 32, WAVE);
+      if (h == 0) {
+        xv[c0 + c] = x;
+        if (c0 + c < n) xout[c0 + c] = x;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 #ifdef CS_TIMING
 extern "C" int ptzba_debug_cs_stamps(long long* out) {
   const int zero = 0;
@@ -1074,9 +1148,14 @@ extern "C" int ptzba_debug_bs_stamps(long long* out) {
 void launch_chol_backsolve(const double* L, int64_t ld, int n, int n_chain, int n_pos, const int* chain_off,
                            const int* chain_cols, const int* upd_off, const int* upd_tiles, int n_upd,
                            const int* la_tasks, int n_tasks, const double* Ldiag, double* Minv, double* xout,
-                           hipStream_t st) {
+                           const int* lo_off, const int* lo_tiles, hipStream_t st) {
   const int tx = (n + NB - 1) / NB;
   hipLaunchKernelGGL(k_tile_inv, dim3(tx), dim3(64), 0, st, Ldiag, Minv);
+  if (lo_off) {  // large systems: left-looking form (api.hip chooses it when the lookahead lists exceed LDS)
+    hipLaunchKernelGGL(k_chol_backsolve_ll, dim3(n_chain), dim3(64 * BSL_WAVES), (size_t)ld * sizeof(double), st, L,
+                       ld, n, chain_off, chain_cols, lo_off, lo_tiles, Ldiag, Minv, xout);
+    return;
+  }
 #if BS_LA
   const size_t lds = (size_t)ld * sizeof(double) + (size_t)(2 * n_pos + n_tasks) * sizeof(int);
   hipLaunchKernelGGL(k_chol_backsolve_la, dim3(n_chain), dim3(64 * (BS_HELPERS + 2)), lds, st, L, ld, n, chain_off,

@@ -134,7 +134,9 @@ constexpr int BS_HELPERS = 7;
 void launch_chol_backsolve(const double* L, int64_t ld, int n, int n_chain, int n_pos, const int* chain_off,
                            const int* chain_cols, const int* upd_off, const int* upd_tiles, int n_upd,
                            const int* la_tasks, int n_tasks, const double* Ldiag, double* Minv, double* xout,
-                           hipStream_t st);
+                           const int* lo_off, const int* lo_tiles, hipStream_t st);
+// largest ld the back substitution keeps in LDS (left-looking form: x [ld] doubles + 4.4 KiB)
+constexpr int64_t CHOL_MAX_LD = 18944;
 // zero the factor pattern's tiles and the b | g_pose | dU vectors before a build (replaces a memset of
 // the whole ld x ld region: entries outside the pattern are never written)
 void launch_zero_tiles(double* S, int64_t ld, const int2* zt, int n_tiles, double* vec, int64_t n_vec, hipStream_t st);

@@ -120,6 +120,7 @@ def lib():
         "ptz_back_project_rays": ([I, I64, D, D, D, D, D, V, V, V], I),
         "ptz_h_jacobian": ([I, I64, D, D, D, D, D, V, V, V], I),
         "ptzba_build_landmarks": ([I32, V, I64, V, V, V, V, V, V, V, V], I),
+        "ptzba_coupling_window": ([I32, I32, I64, V, V, V], I),
         "ptz_py_shuffle_prefix": ([V, I64, V, I64, V], I),
         "ptz_set_order_pairs": ([I64, V, V, V, V, V], I),
         "ptz_keyframe_features": ([I32, I64, V, V, V, V, V, V, V, V], I),
@@ -150,7 +151,7 @@ EXPORTED_SYMBOLS = [
     "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_solve", "ptzba_read_scalars", "ptzba_accept",
     "ptzba_lm_start", "ptzba_lm_init", "ptzba_lm_build", "ptzba_lm_solve", "ptzba_lm_decide", "ptzba_lm_wait",
     "ptzba_exchange", "ptzba_exchange_packed", "ptzba_pack", "ptzba_unpack", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptzba_save_state", "ptzba_restore_state", "ptz_ray_to_image",
-    "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks",
+    "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks", "ptzba_coupling_window",
     "ptz_py_shuffle_prefix", "ptz_set_order_pairs", "ptz_keyframe_features", "ptz_pack_records",
     "ptz_refine_poses", "ptzekf_new", "ptzekf_delete", "ptzekf_num_rays", "ptzekf_set_state", "ptzekf_get_state", "ptzekf_add_pose_cov",
     "ptzekf_remove_rays", "ptzekf_add_rays", "ptzekf_project_visible", "ptzekf_update",
@@ -366,14 +367,13 @@ def frame_coupling_window(n_pose, frame, landmark):
     """Highest frame sharing a landmark with each frame (>= the frame itself): the coupling window
     ptzba_set_problem derives from its own records.  Computed on the full record set it is the
     `frame_win_hi` every rank of a sharded solve passes, so all ranks choose the same system order."""
-    frame = np.asarray(frame, np.int64)
-    landmark = np.asarray(landmark, np.int64)
+    frame = np.ascontiguousarray(frame, np.int32)
+    landmark = np.ascontiguousarray(landmark, np.int32)
     n_lm = int(landmark.max()) + 1 if len(landmark) else 0
-    lm_hi = np.full(n_lm, -1, np.int64)
-    np.maximum.at(lm_hi, landmark, frame)
-    win = np.arange(n_pose, dtype=np.int64)
-    np.maximum.at(win, frame, lm_hi[landmark])
-    return win.astype(np.int32)
+    win = np.empty(int(n_pose), np.int32)
+    _check(lib().ptzba_coupling_window(int(n_pose), n_lm, len(frame), _ptr(frame), _ptr(landmark), _ptr(win)),
+           "ptzba_coupling_window")
+    return win
 
 
 class BAHandle:
@@ -427,10 +427,12 @@ class BAHandle:
         self.precision = precision
 
     def solver_info(self):
-        out = np.zeros(4, np.int64)
+        out = np.zeros(8, np.int64)
         _check(lib().ptzba_solver_info(self.h, _ptr(out)), "ptzba_solver_info")
         return dict(n_aug=int(out[0]), ld=int(out[1]), levels=int(out[2]),
-                    ordering="nested" if out[3] != ORDER_NATURAL else "natural")
+                    ordering="nested" if out[3] != ORDER_NATURAL else "natural",
+                    backsolve="left-looking" if out[4] else "lookahead", n_slot=int(out[5]), schur_items=int(out[6]),
+                    pattern_tiles=int(out[7]))
 
     def info(self):
         out = np.zeros(8, np.int64)

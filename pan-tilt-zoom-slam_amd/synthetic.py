@@ -257,9 +257,73 @@ def problem_from_pairs(scene, pairs):
                    meta=dict(match_i=mi, match_j=mj, kp1=k1, kp2=k2))
 
 
+def _synth_lib():
+    import ctypes
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libptzsynth.so")
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} missing: build it with `make -C pan-tilt-zoom-slam_amd/csrc`")
+    L = ctypes.CDLL(path)
+    L.ptzsynth_grid_new.restype = ctypes.c_void_p
+    L.ptzsynth_grid_new.argtypes = [ctypes.c_void_p]
+    L.ptzsynth_counts.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    L.ptzsynth_fetch.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 7
+    L.ptzsynth_free.argtypes = [ctypes.c_void_p]
+    return L
+
+
+def make_grid_problem(n_kf, n_rays, lo, hi, rows, seed=0, threads=None, noise=0.5, init_sigma=(0.5, 0.2, 40.0),
+                      min_match=20, max_match=200, overlap_deg=5.0):
+    """Multi-row keyframe grid (config 4) from the threaded native generator (csrc/synth.cpp): same spec
+    as make_scene/scene_pairs/problem_from_pairs with row-major frames, counter-based random streams."""
+    import ctypes
+    import os
+
+    class Params(ctypes.Structure):
+        _fields_ = [("n_kf", ctypes.c_int32), ("n_rays", ctypes.c_int32), ("n_rows", ctypes.c_int32),
+                    ("threads", ctypes.c_int32), ("pan_lo", ctypes.c_double), ("pan_hi", ctypes.c_double),
+                    ("rows", ctypes.c_void_p), ("seed", ctypes.c_uint64), ("noise", ctypes.c_double),
+                    ("sig_pan", ctypes.c_double), ("sig_tilt", ctypes.c_double), ("sig_f", ctypes.c_double),
+                    ("min_match", ctypes.c_int32), ("max_match", ctypes.c_int32), ("overlap_deg", ctypes.c_double)]
+
+    L = _synth_lib()
+    rows_a = np.ascontiguousarray(rows, np.float64)
+    if threads is None:
+        threads = min(16, len(os.sched_getaffinity(0)))
+    p = Params(int(n_kf), int(n_rays), len(rows_a), int(threads), float(lo), float(hi), rows_a.ctypes.data,
+               int(seed), float(noise), *[float(s) for s in init_sigma], int(min_match), int(max_match),
+               float(overlap_deg))
+    h = L.ptzsynth_grid_new(ctypes.byref(p))
+    if not h:
+        raise ValueError("bad grid parameters")
+    try:
+        c = np.zeros(4, np.int64)
+        L.ptzsynth_counts(h, c.ctypes.data)
+        n, m, r, npairs = (int(x) for x in c)
+        frame = np.empty(r, np.int32)
+        landmark = np.empty(r, np.int32)
+        xy = np.empty((r, 2))
+        init_ptz, gt_ptz = np.empty((n, 3)), np.empty((n, 3))
+        init_rays, gt_rays = np.empty((m, 2)), np.empty((m, 2))
+        L.ptzsynth_fetch(h, frame.ctypes.data, landmark.ctypes.data, xy.ctypes.data, init_ptz.ctypes.data,
+                         gt_ptz.ctypes.data, init_rays.ctypes.data, gt_rays.ctypes.data)
+    finally:
+        L.ptzsynth_free(h)
+    return Problem(n_pose=n, n_landmark=m, frame=frame, landmark=landmark, xy=xy, init_ptz=init_ptz,
+                   init_rays=init_rays, gt_ptz=gt_ptz, gt_rays=gt_rays, n_pairs=npairs,
+                   meta=dict(generator="csrc/synth.cpp", rows=list(rows_a)))
+
+
 def make_problem(config="config3", seed=0):
-    """Synthetic BA problem for one of the BASELINE configs."""
+    """Synthetic BA problem for one of the BASELINE configs.  Config 4 (tilt rows) comes from
+    the native grid generator; configs 1-3 from the numpy path (the fixtures and the bench are pinned to
+    its random streams)."""
     n_kf, n_rays, lo, hi, rows = CONFIGS[config]
+    if rows is not None:
+        prob = make_grid_problem(n_kf, n_rays, lo, hi, rows, seed=seed)
+        prob.meta["config"] = config
+        prob.meta["seed"] = seed
+        return prob
     scene = make_scene(n_kf, n_rays, lo, hi, seed=seed, tilt_rows=rows)
     pairs = scene_pairs(scene, seed=seed)
     prob = problem_from_pairs(scene, pairs)

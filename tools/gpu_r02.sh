@@ -7,6 +7,14 @@ STAGES=${STAGES:-tests,bench,dist,ab64,prof}
 mkdir -p gpurun_out
 P=$PWD/pan-tilt-zoom-slam_amd
 has() { case ",$STAGES," in *",$1,"*) return 0;; esac; return 1; }
+if has grid; then
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_config4.py -k grid -x -v --timeout 200 --timeout-method thread > gpurun_out/${TAG}_grid.log 2>&1 || { echo GRIDFAIL; tail -40 gpurun_out/${TAG}_grid.log; exit 1; }
+  tail -3 gpurun_out/${TAG}_grid.log
+fi
+if has c4; then
+  timeout -k 10 900 python -u -m pytest tests/test_gpu_config4.py -k config4 -x -v -s --timeout 800 --timeout-method thread > gpurun_out/${TAG}_c4.log 2>&1 || { echo C4FAIL; tail -40 gpurun_out/${TAG}_c4.log; exit 1; }
+  grep -E "config4|set_problem|passed|failed" gpurun_out/${TAG}_c4.log | cut -c1-1500
+fi
 if has tests; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${TAG}_gpu_tests.log 2>&1 || { echo TESTFAIL; tail -40 gpurun_out/${TAG}_gpu_tests.log; exit 1; }
   tail -3 gpurun_out/${TAG}_gpu_tests.log
@@ -14,6 +22,10 @@ fi
 if has bench; then
   timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { echo BENCHFAIL; tail -20 gpurun_out/${TAG}_bench.err; exit 1; }
   tail -c 3000 gpurun_out/${TAG}_bench.json
+fi
+if has c4bench; then
+  timeout -k 10 900 python -u bench.py --config config4 --steps 3 --warmup 1 --no-cpu-baseline --no-accuracy --no-secondary --no-cold > gpurun_out/${TAG}_c4bench.json 2> gpurun_out/${TAG}_c4bench.err || { echo C4BENCHFAIL; tail -20 gpurun_out/${TAG}_c4bench.err; exit 1; }
+  tail -c 3000 gpurun_out/${TAG}_c4bench.json
 fi
 if has dist; then
   PTZBA_DIST_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/${TAG}_dist2.json 2> gpurun_out/${TAG}_dist2.err || { echo DISTFAIL; tail -20 gpurun_out/${TAG}_dist2.err; exit 1; }
