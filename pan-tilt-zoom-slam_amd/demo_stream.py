@@ -1,0 +1,116 @@
+"""
+Streaming PTZ SLAM driver (BASELINE configs[4]): the demo_soccer.py loop (demo_soccer.py:17-55) on a
+synthetic 1080p court stream -- per frame `PtzSlam.tracking` (LK flow + homography RANSAC stand-in, EKF
+update on the GPU, ray removal / addition), `relocalize` + `init_system` when tracking is lost, and
+`add_keyframe` (keyframe bundle adjustment on the GPU) when the map asks for a new keyframe.
+
+The keyframe map is the reference's `Map` (every keyframe adjusted, scene_map.py:53-117) or, with
+--window N, a sliding window over the last N keyframes (the rule of RandomForestMap.bundle_adjustment_
+processing, scene_map.py:198-244, with the window the config asks for: 30).  --keyframe-every K adds a
+keyframe every K frames on top of the reference's overlap rule (ptz_slam.py:458), so long windows fill up.
+
+  python demo_stream.py [--frames 300] [--window 30] [--keyframe-every 10] [--json]
+
+Prints one JSON line: end-to-end frames/s, per-frame tracking latency, keyframe BA latency, pose error
+against the ground truth, and the time spent inside the front-end stand-in (synthetic.StreamFrontEnd:
+not part of the SLAM path; the fps without it is reported too).
+"""
+import argparse
+import contextlib
+import io
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+if HERE not in sys.path:
+    sys.path.insert(0, HERE)
+
+
+def run_stream(slam, scene, n_frames, camera0, keyframe_every=None, on_frame=None):
+    """The demo_soccer.py:17-55 loop over frames 0..n_frames-1 of `scene` with an initialised `slam`
+    object (this build's PtzSlam or the reference's).  Returns per-frame records and timings."""
+    img = scene.image(0)
+    slam.init_system(img, camera0)
+    slam.add_keyframe(img, camera0, 0, enable_rf=False)
+    rec = dict(ptz=[list(camera0.get_ptz())], velocity=[[0.0, 0.0, 0.0]], n_rays=[len(slam.rays)],
+               n_kp=[len(slam.previous_keypoints)], keyframe=[1], lost=[0], t_track=[0.0], t_kf=[0.0])
+    for i in range(1, n_frames):
+        img = scene.image(i)
+        t0 = time.perf_counter()
+        slam.tracking(next_img=img, bad_tracking_percentage=80)
+        t1 = time.perf_counter()
+        added = lost = 0
+        if slam.tracking_lost:
+            cam = slam.relocalize(img, slam.current_camera, enable_rf=False)
+            slam.init_system(img, cam)
+            lost = 1
+        elif slam.new_keyframe or (keyframe_every and i % keyframe_every == 0):
+            slam.add_keyframe(img, slam.current_camera, i, enable_rf=False)
+            slam.new_keyframe = False
+            added = 1
+        t2 = time.perf_counter()
+        cam = slam.cameras[i] if i < len(slam.cameras) else slam.current_camera
+        rec["ptz"].append([cam.pan, cam.tilt, cam.focal_length])
+        rec["velocity"].append([float(x) for x in np.asarray(slam.velocity).reshape(-1)[:3]])
+        rec["n_rays"].append(len(slam.rays))
+        rec["n_kp"].append(len(slam.previous_keypoints))
+        rec["keyframe"].append(added)
+        rec["lost"].append(lost)
+        rec["t_track"].append(t1 - t0)
+        rec["t_kf"].append(t2 - t1)
+        if on_frame:
+            on_frame(i, slam)
+    return rec
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=300)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--window", type=int, default=30, help="keyframes per sliding-window BA (0: all, as Map)")
+    ap.add_argument("--keyframe-every", type=int, default=10)
+    ap.add_argument("--pan-range", type=float, default=40.0)
+    ap.add_argument("--verbose", action="store_true")
+    a = ap.parse_args()
+    import ptzba
+    import synthetic
+    from ptz_slam import PtzSlam
+    from scene_map import Map
+    scene = synthetic.StreamScene(a.frames, seed=a.seed, pan_lo=-a.pan_range / 2, pan_hi=a.pan_range / 2)
+    fe = synthetic.StreamFrontEnd(scene).install()
+    slam = PtzSlam()
+    slam.keyframe_map = Map("sift", max_ba_frame=a.window or None)
+    quiet = contextlib.nullcontext() if a.verbose else contextlib.redirect_stdout(io.StringIO())
+    t0 = time.perf_counter()
+    with quiet:
+        rec = run_stream(slam, scene, a.frames, scene.camera(0), keyframe_every=a.keyframe_every)
+    wall = time.perf_counter() - t0
+    est = np.asarray(rec["ptz"])
+    err = est - scene.cams[:len(est)]
+    tt = np.asarray(rec["t_track"][1:])
+    tk = np.asarray([t for t, k in zip(rec["t_kf"], rec["keyframe"]) if k][1:] or [0.0])
+    out = {
+        "workload": f"config5: streaming PTZ tracking, {a.frames} frames 1920x1080, keyframe BA window "
+                    f"{a.window or 'all'}, keyframe every {a.keyframe_every} frames + overlap rule",
+        "frames": a.frames, "fps_end_to_end": a.frames / wall, "wall_s": wall,
+        "frontend_standin_s": fe.time, "fps_excluding_frontend_standin": a.frames / max(wall - fe.time, 1e-9),
+        "tracking_ms": {"mean": 1e3 * float(tt.mean()), "p50": 1e3 * float(np.median(tt)),
+                        "p99": 1e3 * float(np.percentile(tt, 99))},
+        "keyframes": int(sum(rec["keyframe"])), "keyframe_ba_ms": {"mean": 1e3 * float(tk.mean()),
+                                                                  "max": 1e3 * float(tk.max())},
+        "final_keyframes_in_map": len(slam.keyframe_map.keyframe_list), "rays_final": rec["n_rays"][-1],
+        "lost_frames": int(sum(rec["lost"])),
+        "pose_rmse_vs_truth": {"pan_deg": float(np.sqrt(np.mean(err[:, 0] ** 2))),
+                               "tilt_deg": float(np.sqrt(np.mean(err[:, 1] ** 2))),
+                               "f_px": float(np.sqrt(np.mean(err[:, 2] ** 2)))},
+        "device": ptzba.lib().ptzba_version().decode(),
+    }
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

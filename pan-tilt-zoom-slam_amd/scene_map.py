@@ -22,13 +22,18 @@ from util import overlap_pan_angle
 
 
 class Map:
-    def __init__(self, feature_method, cache_correspondences=True):
+    """max_ba_frame: None (the reference: every keyframe is adjusted) or N: only the last N keyframes are
+    adjusted, older ones stay as they are (RandomForestMap's window rule, scene_map.py:198-244; the
+    streaming config's 30-keyframe window)."""
+
+    def __init__(self, feature_method, cache_correspondences=True, max_ba_frame=None):
         assert feature_method in ("sift", "orb", "latch")
         self.global_ray = np.ndarray([0, 2])
         self.keyframe_list = []
         self.feature_method = feature_method
         self.ba_options = {}
         self.last_ba_time = None
+        self.max_ba_frame = max_ba_frame
         self.correspondences = CorrespondenceCache() if cache_correspondences else None
 
     def add_first_keyframe(self, keyframe, verbose=False):
@@ -47,6 +52,12 @@ class Map:
         assert len(self.keyframe_list) >= 1
         ref = self.keyframe_list[0]
         self.add_keyframe_without_ba(keyframe, False)
+        kept = []
+        if self.max_ba_frame and len(self.keyframe_list) > self.max_ba_frame:
+            kept = self.keyframe_list[:-self.max_ba_frame]
+            self.keyframe_list = self.keyframe_list[-self.max_ba_frame:]
+            if self.correspondences is not None:
+                self.correspondences.retain([k.img_index for k in self.keyframe_list])
         n = len(self.keyframe_list)
         images = [k.img for k in self.keyframe_list]
         image_indices = [k.img_index for k in self.keyframe_list]
@@ -58,7 +69,7 @@ class Map:
         end = time.time()
         self.keyframe_list.pop()
         self.global_ray = landmarks
-        self.keyframe_list = []
+        self.keyframe_list = list(kept)
         for i, kf in enumerate(keyframes):
             if kf.get_feature_num() > 0:
                 self.keyframe_list.append(kf)

@@ -486,3 +486,185 @@ def reloc_scene(seed=3):
     lost_init = lost_true + np.array([1.5, -0.6, 120.0])
     cams = np.vstack([kf, lost_true[None]])  # image ids 0..3 keyframes, 4 the lost frame
     return rays, cams, lost_init
+
+
+# ------------------------------------------------------------------------------------------------
+# Streaming sequence (BASELINE configs[4]: per-frame PTZ tracking on a 1080p synthetic court)
+# ------------------------------------------------------------------------------------------------
+def _hash_u64(*keys):
+    """splitmix64 of a key tuple (vectorised over numpy uint64 arrays): counter-based random numbers that
+    depend only on the keys, so every consumer (the reference run that made the fixture, this build)
+    draws the same values for the same (frame, point) regardless of call order or float round-off."""
+    with np.errstate(over="ignore"):
+        z = np.uint64(0x9E3779B97F4A7C15)
+        for k in keys:
+            z = (z ^ np.asarray(k, dtype=np.uint64)) * np.uint64(0xBF58476D1CE4E5B9)
+            z = z ^ (z >> np.uint64(31))
+            z = z * np.uint64(0x94D049BB133111EB)
+            z = z ^ (z >> np.uint64(29))
+    return z
+
+
+def _unit(*keys):
+    return (_hash_u64(*keys) >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+
+
+def _normal(*keys):
+    u1 = np.maximum(_unit(*keys, 1), 1e-300)
+    u2 = _unit(*keys, 2)
+    return np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2)
+
+
+class SynthImage:
+    """One frame of a synthetic stream: the reference reads only `img.shape[0:2]` (ptz_slam.py:333, 434)
+    and hands the object to the front-end, which recognises the frame by int(img)."""
+    __slots__ = ("index", "shape")
+
+    def __init__(self, index, height, width):
+        self.index = int(index)
+        self.shape = (int(height), int(width))
+
+    def __int__(self):
+        return self.index
+
+    __index__ = __int__
+
+    def __repr__(self):
+        return f"SynthImage({self.index})"
+
+
+class StreamScene:
+    """A PTZ broadcast camera sweeping a court: ground-truth pan/tilt/focal per frame (smooth sweep with a
+    zoom oscillation, 1920x1080, principal point at the centre) and a field of world rays the detector
+    sees (theta U[-50, 50], phi U[-24, 4] deg)."""
+
+    def __init__(self, n_frames, seed=0, n_rays=40000, width=1920, height=1080, pan_lo=-18.0, pan_hi=18.0):
+        self.n, self.seed = int(n_frames), int(seed)
+        self.width, self.height = int(width), int(height)
+        self.u, self.v = width / 2.0, height / 2.0
+        t = np.arange(self.n, dtype=np.float64)
+        T = max(self.n - 1, 1)
+        pan = pan_lo + (pan_hi - pan_lo) * 0.5 * (1.0 - np.cos(np.pi * t / T))
+        tilt = -9.0 + 1.2 * np.sin(2.0 * np.pi * t / 97.0)
+        f = 2600.0 + 300.0 * np.sin(2.0 * np.pi * t / 151.0)
+        self.cams = np.stack([pan, tilt, f], 1)
+        rng = np.random.default_rng(seed + 17)
+        self.rays = np.stack([rng.uniform(-50.0, 50.0, n_rays), rng.uniform(-24.0, 4.0, n_rays)], 1)
+        self.response = rng.permutation(n_rays)  # detector strength rank per ray (lower = stronger)
+
+    def image(self, i):
+        return SynthImage(i, self.height, self.width)
+
+    def camera(self, i):
+        """ptz_camera.PTZCamera of frame i (the ground truth; the sequence's first camera seeds the tracker)."""
+        from ptz_camera import PTZCamera
+        cam = PTZCamera((self.u, self.v), np.array([0.0, -16.0, 5.0]), np.eye(3))
+        cam.set_ptz(self.cams[i].copy())
+        return cam
+
+
+class StreamFrontEnd:
+    """Stand-in for the reference's OpenCV front-end on a StreamScene (the way make_golden.py's FrontEnd
+    stands in for SIFT + BF matching):
+      * detect_compute_sift(img, n): the visible world rays of frame img, strongest first, capped at n;
+        keypoint = true projection + N(0, 0.3 px); descriptor carries the ray id;
+      * match_sift_features: ground-truth correspondences by ray id (as match_sift_features' ratio test
+        would give on distinctive features); (None, [], None, []) below 9 matches, like the reference;
+      * optical_flow_matching(img, next_img, points): a pure-rotation camera moves image content by the
+        homography of the two TRUE poses: back-project with frame img's camera, project with next_img's,
+        + N(0, 0.2 px); points leaving the image fail (image_process.py:393-415); 3 % of the points
+        (keyed by (frame, index)) are displaced 6-20 px (players, flicker);
+      * homography_ransac: the undisplaced points are the inliers (a 0.5 px RANSAC separates them).
+    Every random number is keyed by (seed, frame, point), so the reference run and this build see the same
+    data."""
+
+    def __init__(self, scene, noise=0.3, flow_noise=0.2, outlier_rate=0.03):
+        self.s = scene
+        self.noise, self.flow_noise, self.outlier_rate = noise, flow_noise, outlier_rate
+        self._last = None
+        self.time = 0.0  # seconds spent inside the stand-in (reported separately by the stream driver)
+
+    # ---- detection / matching (keyframes, init_system, add_rays)
+    def _visible(self, i):
+        pan, tilt, f = self.s.cams[i]
+        r = self.s.rays
+        x, y, q2 = _project(self.s.u, self.s.v, f, pan, tilt, r[:, 0], r[:, 1])
+        vis = np.flatnonzero((q2 > 0) & (x > 0) & (x < self.s.width) & (y > 0) & (y < self.s.height))
+        vis = vis[np.argsort(self.s.response[vis], kind="stable")]
+        return vis, x[vis], y[vis]
+
+    def detect(self, im, nfeatures=0, verbose=False):
+        import time
+        t0 = time.perf_counter()
+        i = int(im)
+        vis, x, y = self._visible(i)
+        if nfeatures and nfeatures > 0:
+            vis, x, y = vis[:nfeatures], x[:nfeatures], y[:nfeatures]
+        x = x + self.noise * _normal(self.s.seed, 1, i, vis)
+        y = y + self.noise * _normal(self.s.seed, 2, i, vis)
+        ok = (x > 0) & (x < self.s.width) & (y > 0) & (y < self.s.height)
+        vis, x, y = vis[ok], x[ok], y[ok]
+        kps = [_KP(a, b) for a, b in zip(x, y)]
+        des = np.zeros((len(vis), 128), np.float32)
+        des[:, 0] = vis + 1
+        des[:, 1] = i
+        des[:, 2] = 1.0
+        self.time += time.perf_counter() - t0
+        return kps, des
+
+    def match(self, kp1, des1, kp2, des2, pts_array=False, verbose=False):
+        r1 = np.rint(np.asarray(des1)[:, 0]).astype(np.int64) if len(des1) else np.zeros(0, np.int64)
+        r2 = np.rint(np.asarray(des2)[:, 0]).astype(np.int64) if len(des2) else np.zeros(0, np.int64)
+        pos2 = {int(r): j for j, r in enumerate(r2)}
+        idx1 = [i for i, r in enumerate(r1) if int(r) in pos2]
+        idx2 = [pos2[int(r1[i])] for i in idx1]
+        if len(idx1) <= 8:
+            return None, [], None, []
+        p1 = np.array([kp1[i] if pts_array else kp1[i].pt for i in idx1], np.float64).reshape(-1, 2)
+        p2 = np.array([kp2[j] if pts_array else kp2[j].pt for j in idx2], np.float64).reshape(-1, 2)
+        return p1, idx1, p2, idx2
+
+    # ---- frame-to-frame tracking (ptz_slam.py:397 -> image_process.py:464-506)
+    def optical_flow(self, img, next_img, points, ssd_threshold=20):
+        import time
+        t0 = time.perf_counter()
+        i, j = int(img), int(next_img)
+        p = np.asarray(points, np.float64).reshape(-1, 2)
+        k = np.arange(len(p))
+        a = self.s.cams[i]
+        b = self.s.cams[j]
+        th, ph = image_to_ray(self.s.u, self.s.v, a[2], a[0], a[1], p[:, 0], p[:, 1])
+        x, y, q2 = _project(self.s.u, self.s.v, b[2], b[0], b[1], th, ph)
+        x = x + self.flow_noise * _normal(self.s.seed, 3, j, k)
+        y = y + self.flow_noise * _normal(self.s.seed, 4, j, k)
+        bad = _unit(self.s.seed, 5, j, k) < self.outlier_rate
+        mag = 6.0 + 14.0 * _unit(self.s.seed, 6, j, k)
+        ang = 2.0 * np.pi * _unit(self.s.seed, 7, j, k)
+        x = np.where(bad, x + mag * np.cos(ang), x)
+        y = np.where(bad, y + mag * np.sin(ang), y)
+        h, w = self.s.height, self.s.width
+        ok = (q2 > 0) & (x > 0) & (x < w) & (y > 0) & (y < h)
+        matched = [int(t) for t in np.flatnonzero(ok)]
+        self._last = bad[ok]
+        self.time += time.perf_counter() - t0
+        return matched, np.stack([x[ok], y[ok]], 1).reshape(-1, 2)
+
+    def ransac(self, points1, points2, reprojection_threshold=0.5, return_matrix=False):
+        assert self._last is not None and len(self._last) == len(points1) == len(points2)
+        index = [int(t) for t in np.flatnonzero(~self._last)]
+        if return_matrix:
+            return index, None
+        return index
+
+    def install(self, *modules):
+        """Assign the hooks in image_process (this build) or in the given modules (e.g. the reference's
+        image_process when generating fixtures)."""
+        if not modules:
+            import image_process
+            modules = (image_process,)
+        for m in modules:
+            m.detect_compute_sift = self.detect
+            m.match_sift_features = self.match
+            m.optical_flow_matching = self.optical_flow
+            m.homography_ransac = self.ransac
+        return self

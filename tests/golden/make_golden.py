@@ -511,13 +511,70 @@ def gen_maps(seed):
     out("map_window.npz", seed=seed + 1, u=scene.u, v=scene.v, init_ptz=ip, **_pack_state(acc))
 
 
+# --------------------------------------------------------------------------------------------
+# config 5: the streaming loop of demo_soccer.py:17-55 (PtzSlam.tracking / add_keyframe) on a synthetic
+# 1080p stream, the front-end stand-in (synthetic.StreamFrontEnd) assigned to the reference's hooks
+# --------------------------------------------------------------------------------------------
+class _NumpyIndexCompat:
+    """numpy as seen by the reference's ptz_slam module, with the one numpy-1.x behaviour it relies on:
+    PtzSlam.remove_rays builds its covariance index list with np.append on a float array
+    (ptz_slam.py:309-315) and passes it to np.delete, which numpy 1.11 (the README's pin) accepted and
+    numpy 2 rejects.  Float index arrays are cast to int; everything else is numpy itself."""
+
+    def __getattr__(self, name):
+        return getattr(np, name)
+
+    @staticmethod
+    def delete(arr, obj, axis=None):
+        o = np.asarray(obj)
+        if o.dtype.kind == "f":
+            o = o.astype(np.int64)
+        return np.delete(arr, o, axis=axis)
+
+
+def gen_stream(seed, n_frames):
+    _sp = importlib.util.spec_from_file_location("demo_stream", os.path.join(REPO, "pan-tilt-zoom-slam_amd",
+                                                                             "demo_stream.py"))
+    demo_stream = importlib.util.module_from_spec(_sp)
+    _sp.loader.exec_module(demo_stream)
+    sc = synthetic.StreamScene(n_frames, seed=seed)
+    fe = synthetic.StreamFrontEnd(sc).install(ref_ip)
+    # ptz_slam binds the front-end names at import (`from image_process import *`, ptz_slam.py:17): rebind
+    # them to image_process's own functions, which call the assigned hooks
+    ref_slam.detect_compute_sift_array = ref_ip.detect_compute_sift_array
+    ref_slam.matching_and_ransac = ref_ip.matching_and_ransac
+    ref_ba.draw_matches = lambda *a, **k: None
+    ref_slam.np = _NumpyIndexCompat()
+    random.seed(seed)
+    slam = ref_slam.PtzSlam()
+    cam0 = ref_cam.PTZCamera((sc.u, sc.v), np.array([0.0, -16.0, 5.0]), np.eye(3))
+    cam0.set_ptz(sc.cams[0].copy())
+    cov_diag, cov_pose = [], []
+
+    def on_frame(i, s):
+        cov_diag.append(np.diag(s.state_cov).copy())
+        cov_pose.append(s.state_cov[0:3, :].copy())
+
+    t0 = time.time()
+    rec = demo_stream.run_stream(slam, sc, n_frames, cam0, on_frame=on_frame)
+    print(f"stream: {n_frames} frames in {time.time() - t0:.1f}s, keyframes {sum(rec['keyframe'])}, "
+          f"rays {rec['n_rays'][-1]}")
+    kfs = slam.keyframe_map.keyframe_list
+    out("stream.npz", seed=seed, n_frames=n_frames, ptz=np.array(rec["ptz"]), velocity=np.array(rec["velocity"]),
+        n_rays=np.array(rec["n_rays"]), n_kp=np.array(rec["n_kp"]), keyframe=np.array(rec["keyframe"]),
+        lost=np.array(rec["lost"]), rays=np.asarray(slam.rays), cov_diag=np.concatenate(cov_diag),
+        cov_diag_n=np.array([len(c) for c in cov_diag]), cov_pose=np.concatenate(cov_pose, axis=1),
+        kf_index=np.array([k.img_index for k in kfs]), kf_ptz=np.array([[k.pan, k.tilt, k.f] for k in kfs]),
+        global_ray=np.asarray(slam.keyframe_map.global_ray))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--only", default="")
     a = ap.parse_args()
     rng = np.random.default_rng(1)
-    todo = a.only.split(",") if a.only else ["proj", "ba", "graph", "ekf", "config2", "reloc", "maps"]
+    todo = a.only.split(",") if a.only else ["proj", "ba", "graph", "ekf", "config2", "reloc", "maps", "stream"]
     if "proj" in todo:
         gen_projection(rng)
     if "ba" in todo:
@@ -536,6 +593,8 @@ def main():
         gen_maps(21)
     if "config2" in todo:
         gen_config2()
+    if "stream" in todo:
+        gen_stream(7, 30)
 
 
 if __name__ == "__main__":
