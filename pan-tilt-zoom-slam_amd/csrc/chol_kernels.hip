@@ -106,7 +106,10 @@ __device__ __forceinline__ void put_tile(double (*dst)[NB + 1], const double (&v
 // 16x16 block (16 (w>>1), 16 (w&1)) and runs 8 v_mfma_f64_16x16x4_f64 (k = 4 per step).  Operand lane
 // maps (gfx950): A[i = l&15][k = l>>4], B[k = l>>4][j = l&15]; D[row = (l>>4) + 4 r][col = l&15].
 typedef double v4f64 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void tile_gemm_nt_sub(double (*C)[NB + 1], double (*A)[NB + 1], double (*B)[NB + 1]) {
+// SG: C -= A Sigma B^T with Sigma = diag(sg) (the signed factor of an indefinite system, see k_chol_step)
+template <bool SG = false>
+__device__ __forceinline__ void tile_gemm_nt_sub(double (*C)[NB + 1], double (*A)[NB + 1], double (*B)[NB + 1],
+                                                 const double* sg = nullptr) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int bi = (w >> 1) * 16, bj = (w & 1) * 16;
   const int li = l & 15, lk = l >> 4;
@@ -116,7 +119,8 @@ __device__ __forceinline__ void tile_gemm_nt_sub(double (*C)[NB + 1], double (*A
 #pragma unroll
   for (int s = 0; s < NB / 4; ++s) {
     const double a = -A[bi + li][4 * s + lk];
-    const double b = B[bj + li][4 * s + lk];
+    double b = B[bj + li][4 * s + lk];
+    if constexpr (SG) b *= sg[4 * s + lk];
     acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
   }
 #pragma unroll
@@ -473,10 +477,14 @@ __device__ __forceinline__ void lds_wait_ge(const int* p, int v, int sleep) {
   }
   asm volatile("" ::: "memory");
 }
-template <int BW>
+// SG (signed, for the indefinite EKF innovation matrix): factor A = L Sigma L^T, Sigma = diag(+-1) --
+// a pivot d < 0 gives L_jj = sqrt(|d|), sigma_j = -1 (Sylvester: as many negative pivots as negative
+// eigenvalues; no pivoting, as np.linalg.inv of the reference would not need); every update carries the
+// sign of its pivot.  The signs go to sig[NB] (LDS) for the caller.  SG = false is the SPD factor.
+template <int BW, bool SG = false>
 __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (*T)[NB + 1],
                                                    double (*Lb)[2 * NB][BW], double (*Pb)[BW], int* flags,
-                                                   int* info) {
+                                                   int* info, double* sig = nullptr) {
   constexpr int NS = NB / BW;
   const int w = threadIdx.x >> 6, lane = lane_id();
   const bool isT = lane >= NB;
@@ -494,7 +502,7 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
 #endif
   if (w == 0) {
     bool bad = false;
-    double lp[BW];
+    double lp[BW];  // this lane's factor values of the last block (SG: sigma_k L_rk, the update operand)
 #pragma unroll
     for (int k = 0; k < BW; ++k) lp[k] = 0.0;
 #pragma unroll
@@ -521,7 +529,7 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
       __builtin_amdgcn_wave_barrier();
-      double P[BW][BW], y[BW];
+      double P[BW][BW], y[BW], sg[BW];
 #pragma unroll
       for (int i = 0; i < BW; ++i)
 #pragma unroll
@@ -529,27 +537,46 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
 #pragma unroll
       for (int j = 0; j < BW; ++j) {
         double d = P[j][j];
+        sg[j] = 1.0;
+        if constexpr (SG) {
+          if (d < 0.0) {
+            sg[j] = -1.0;
+            d = -d;
+          }
+        }
         if (!(d > 0.0)) {
           bad = true;
           d = 1e-300;
         }
         y[j] = rsq_fast(d);
 #pragma unroll
-        for (int i = j + 1; i < BW; ++i) P[i][j] *= y[j];
+        for (int i = j + 1; i < BW; ++i) P[i][j] *= y[j];  // = sigma_j L_ij
 #pragma unroll
         for (int i = j + 1; i < BW; ++i)
 #pragma unroll
-          for (int m = j + 1; m <= i; ++m) P[i][m] = fma(-P[i][j], P[m][j], P[i][m]);
+          for (int m = j + 1; m <= i; ++m) {
+            if constexpr (SG) P[i][m] = fma(-sg[j] * P[i][j], P[m][j], P[i][m]);
+            else P[i][m] = fma(-P[i][j], P[m][j], P[i][m]);
+          }
       }
 #pragma unroll
       for (int j = 0; j < BW; ++j) {
-        const double x = a[j] * y[j];
+        const double x = a[j] * y[j];  // sigma_j L_rj
         lp[j] = x;
 #pragma unroll
-        for (int i = j + 1; i < BW; ++i) a[i] = fma(-P[i][j], x, a[i]);
+        for (int i = j + 1; i < BW; ++i) {
+          if constexpr (SG) a[i] = fma(-sg[j] * P[i][j], x, a[i]);
+          else a[i] = fma(-P[i][j], x, a[i]);
+        }
       }
 #pragma unroll
-      for (int j = 0; j < BW; ++j) Lb[s][lane][j] = lp[j];
+      for (int j = 0; j < BW; ++j) Lb[s][lane][j] = SG ? sg[j] * lp[j] : lp[j];  // L_rj
+      if constexpr (SG) {
+        if (lane == 0) {
+#pragma unroll
+          for (int j = 0; j < BW; ++j) sig[kb + j] = sg[j];
+        }
+      }
       if (s + 2 < NS) {
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
@@ -571,7 +598,10 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
       const int kb = t * BW;
       while (lds_poll(nl) < t) __builtin_amdgcn_s_sleep(0);
 #pragma unroll
-      for (int k = 0; k < BW; ++k) lr[t - 1][k] = Lb[t - 1][lane][k];
+      for (int k = 0; k < BW; ++k) {
+        lr[t - 1][k] = Lb[t - 1][lane][k];
+        if constexpr (SG) lr[t - 1][k] *= sig[(t - 1) * BW + k];  // published before nl (same LDS order)
+      }
 #pragma unroll
       for (int m = kb + BW; m < kb + 2 * BW; ++m) {
         if (m % 3 != u) continue;
@@ -606,9 +636,12 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
 #else
 #define CS_STAMP(k) do { } while (0)
 #endif
+// SG: signed factor A = L Sigma L^T (indefinite systems: the EKF innovation block, ekf.hip); sgn[ld] holds
+// sigma per factored row, written by each column's diagonal task and applied to the update panels
+template <bool SG>
 __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64_t ld,
                                                    const int4* __restrict__ tasks, double* __restrict__ Ldiag,
-                                                   int* info) {
+                                                   int* info, double* __restrict__ sgn) {
   __shared__ double sC[NB][NB + 1];     // target tile (panel T_ik / trailing A_ij)
   __shared__ double sD[NB][NB + 1];     // diagonal tile -> L_kk
   __shared__ double sA[2][NB][NB + 1];  // L_ip of the two update panels
@@ -626,6 +659,8 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   __shared__ __attribute__((aligned(16))) double s_pb[LA_BW][LA_BW];
   __shared__ int s_flags[NB / LA_BW + 1];
 #endif
+  __shared__ double s_sgp[2][NB];  // SG: signs of the two update panels' columns
+  __shared__ double s_sig[NB];     // SG: signs of this column's pivots
   const int4 tk = tasks[blockIdx.x];
   const int type = tk.x, i = tk.y, j = tk.z;
   const int up0 = (tk.w & 0x3fff) - 1;
@@ -668,10 +703,16 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
       put_tile(sA[1], v3);
       put_tile(sB[1], v4);
     }
+    if constexpr (SG) {
+      if (threadIdx.x < 2 * NB) {
+        const int q = threadIdx.x >> 5, up = q ? up1 : up0;
+        s_sgp[q][threadIdx.x & 31] = up >= 0 ? sgn[(int64_t)up * NB + (threadIdx.x & 31)] : 1.0;
+      }
+    }
     __syncthreads();
     // each wave owns one 16x16 block of C: consecutive updates need no barrier in between
-    if (up0 >= 0) tile_gemm_nt_sub(sC, sA[0], sB[0]);
-    if (up1 >= 0) tile_gemm_nt_sub(sC, sA[1], sB[1]);
+    if (up0 >= 0) tile_gemm_nt_sub<SG>(sC, sA[0], sB[0], s_sgp[0]);
+    if (up1 >= 0) tile_gemm_nt_sub<SG>(sC, sA[1], sB[1], s_sgp[1]);
     __syncthreads();
     for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) C[(int64_t)(e >> 5) * ld + (e & 31)] = sC[e >> 5][e & 31];
     return;
@@ -692,23 +733,29 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   if (updT0 && up0 >= 0) put_tile(sA[0], v3);
   if (up1 >= 0) put_tile(sB[1], v4);
   if (updT1 && up1 >= 0) put_tile(sA[1], v5);
+  if constexpr (SG) {
+    if (threadIdx.x < 2 * NB) {
+      const int q = threadIdx.x >> 5, up = q ? up1 : up0;
+      s_sgp[q][threadIdx.x & 31] = up >= 0 ? sgn[(int64_t)up * NB + (threadIdx.x & 31)] : 1.0;
+    }
+  }
   __syncthreads();
   CS_STAMP(1);
 #if CHOL_VARIANT != 4
   if (up0 >= 0) {
-    tile_gemm_nt_sub(sD, sB[0], sB[0]);
-    if (updT0) tile_gemm_nt_sub(sC, sA[0], sB[0]);
+    tile_gemm_nt_sub<SG>(sD, sB[0], sB[0], s_sgp[0]);
+    if (updT0) tile_gemm_nt_sub<SG>(sC, sA[0], sB[0], s_sgp[0]);
   }
   if (up1 >= 0) {
-    tile_gemm_nt_sub(sD, sB[1], sB[1]);
-    if (updT1) tile_gemm_nt_sub(sC, sA[1], sB[1]);
+    tile_gemm_nt_sub<SG>(sD, sB[1], sB[1], s_sgp[1]);
+    if (updT1) tile_gemm_nt_sub<SG>(sC, sA[1], sB[1], s_sgp[1]);
   }
 #endif
   __syncthreads();
   CS_STAMP(2);
 #if CHOL_VARIANT != 1
 #if CHOL_WG == 3
-  wg_potrf_trsm32_df<LA_BW>(sD, diag_only ? nullptr : sC, s_lb, s_pb, s_flags, info);
+  wg_potrf_trsm32_df<LA_BW, SG>(sD, diag_only ? nullptr : sC, s_lb, s_pb, s_flags, info, s_sig);
 #elif CHOL_WG == 2
   wg_potrf_trsm32_la<LA_BW>(sD, diag_only ? nullptr : sC, s_lb, s_pb, info);
 #elif CHOL_WG == 1
@@ -729,6 +776,9 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
     // A_kk itself stays untouched: other panel workgroups of this launch are still reading it
     double* C = Ldiag + (int64_t)k * NB * NB;
     for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) C[e] = sD[e >> 5][e & 31];
+    if constexpr (SG) {
+      if (threadIdx.x < NB) sgn[(int64_t)k * NB + threadIdx.x] = s_sig[threadIdx.x];
+    }
     return;
   }
   double* C = A + i * NBl * ld + k * NBl;
@@ -736,11 +786,16 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
 }
 
 void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_off_host, int n_launch, double* Ldiag,
-                     int* info, hipStream_t st) {
+                     int* info, hipStream_t st, double* sgn) {
   for (int L = 0; L < n_launch; ++L) {
     const int n = task_off_host[L + 1] - task_off_host[L];
-    if (n > 0)
-      hipLaunchKernelGGL(k_chol_step, dim3(n), dim3(256), 0, st, A, ld, tasks + task_off_host[L], Ldiag, info);
+    if (n <= 0) continue;
+    if (sgn)
+      hipLaunchKernelGGL(k_chol_step<true>, dim3(n), dim3(256), 0, st, A, ld, tasks + task_off_host[L], Ldiag, info,
+                         sgn);
+    else
+      hipLaunchKernelGGL(k_chol_step<false>, dim3(n), dim3(256), 0, st, A, ld, tasks + task_off_host[L], Ldiag, info,
+                         sgn);
   }
 }
 

@@ -15,7 +15,7 @@
 //   M =  [ (H P)^T                  P     ]
 //        [ y^T                      0     ]
 //
-// is factored by the tiled Cholesky of chol_kernels.hip only through the S columns (plus one
+// is factored by the tiled (signed) Cholesky of chol_kernels.hip only through the S columns (plus one
 // flush launch of the trailing update).  The trailing block is then the Schur complement
 //   P - (HP)^T S^-1 HP = (I - K H) P          and in the y row   -y^T S^-1 H P = -(K y)^T,
 // i.e. the reference's Kalman gain K = P H^T S^-1 (ptz_slam.py:256-262) and updated covariance
@@ -210,7 +210,7 @@ struct ptzekf_ctx {
   int n_ray = 0;
   DBuf rays[2], cov[2];
   int cur = 0;
-  DBuf pred_xy, vis, obs_xy, idx, Hc, yv, M, tasks, Ldiag, info, ky3;
+  DBuf pred_xy, vis, obs_xy, idx, Hc, yv, M, tasks, Ldiag, info, ky3, sgn;
   std::vector<uint8_t> vis_h;
   std::vector<int> task_off;
   int64_t plan_ld = -1;
@@ -465,7 +465,7 @@ int ptzekf_update(ptzekf_handle h, double u, double v, const double* disp6, doub
   if (build_partial_plan(h, d.ld, d.mp)) return -1;
   if (h->idx.reserve((size_t)nr * 8) || h->obs_xy.reserve((size_t)n_obs * 16) || h->Hc.reserve((size_t)nr * 80) ||
       h->yv.reserve((size_t)nr * 16) || h->M.reserve((size_t)(d.ld * d.ld) * 8) ||
-      h->Ldiag.reserve((size_t)Tm * CHOL_NB * CHOL_NB * 8))
+      h->Ldiag.reserve((size_t)Tm * CHOL_NB * CHOL_NB * 8) || h->sgn.reserve((size_t)d.ld * 8))
     return -1;
   int32_t* d_matched = h->idx.as<int32_t>();
   int32_t* d_o1 = d_matched + nr;
@@ -485,9 +485,12 @@ int ptzekf_update(ptzekf_handle h, double u, double v, const double* disp6, doub
   hipLaunchKernelGGL(k_ekf_assemble_s, dim3(nblk(d.m), (unsigned)(d.m + 1)), dim3(256), 0, h->st, d,
                      h->Hc.as<double>(), h->yv.as<double>(), observe_var, M);
   HIPCHK(hipGetLastError());
-  // 4. partial factorisation through the S columns (+ flush of the trailing update)
+  // 4. partial factorisation through the S columns (+ flush of the trailing update).  Signed form
+  //    S = L Sigma L^T: the reference inverts S with np.linalg.inv (ptz_slam.py:258), and its covariance
+  //    write-back (ptz_slam.py:282-289) leaves P indefinite after some frames, so S can have negative
+  //    eigenvalues; for an SPD S the signed factor is the Cholesky factor, bit for bit.
   launch_cholesky(M, d.ld, h->tasks.as<int4>(), h->task_off.data(), h->n_launch, h->Ldiag.as<double>(),
-                  h->info.as<int>(), h->st);
+                  h->info.as<int>(), h->st, h->sgn.as<double>());
   HIPCHK(hipGetLastError());
   // 5. state update and covariance write-back (skipped on the device when S was not SPD)
   hipLaunchKernelGGL(k_ekf_apply_vec, dim3(nblk(std::max(nr, 9))), dim3(256), 0, h->st, d, d_matched, M,
@@ -500,7 +503,7 @@ int ptzekf_update(ptzekf_handle h, double u, double v, const double* disp6, doub
   HIPCHK(hipMemcpyAsync(ky, h->ky3.p, 24, hipMemcpyDeviceToHost, h->st));
   HIPCHK(hipMemcpyAsync(&info, h->info.p, 4, hipMemcpyDeviceToHost, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
-  if (info != 0) return fail("innovation covariance H P H^T + R is not positive definite (pivot %d)", info);
+  if (info != 0) return fail("innovation covariance H P H^T + R is singular (zero pivot, flag %d)", info);
   ptz_inout[0] = pan + ky[0];
   ptz_inout[1] = tilt + ky[1];
   ptz_inout[2] = f + ky[2];

@@ -72,7 +72,7 @@ def main():
     ap.add_argument("--frames", type=int, default=300)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--window", type=int, default=30, help="keyframes per sliding-window BA (0: all, as Map)")
-    ap.add_argument("--keyframe-every", type=int, default=10)
+    ap.add_argument("--keyframe-every", type=int, default=5)
     ap.add_argument("--pan-range", type=float, default=40.0)
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args()

@@ -117,6 +117,36 @@ def test_ekf_update_matches_oracle(gpu_available, R, seed, shuffle, dup):
     assert np.array_equal(cov1 != s["state_cov"], ref["state_cov"] != s["state_cov"])
 
 
+@pytest.mark.parametrize("R,seed", [(300, 21), (40, 22)])
+def test_ekf_update_indefinite_innovation(gpu_available, R, seed):
+    """The reference's covariance write-back (ptz_slam.py:282-289) leaves the state covariance indefinite
+    after a few dozen frames (measured on the reference's own PtzSlam run: make_golden.py gen_stream
+    stream), so S = H P H^T + R gets negative eigenvalues; the reference inverts it with np.linalg.inv
+    (ptz_slam.py:258).  The GPU update factors S = L Sigma L^T (signed) and must equal the oracle."""
+    import ptzba
+    from oracle import ptz_oracle as orc
+    s, obs, keep = _random_state(R, seed)
+    s["state_cov"][0:3, 0:3] -= 0.02 * np.eye(3)  # pose block pushed negative: S loses definiteness
+    # the innovation covariance really is indefinite (oracle's own S)
+    pred, pidx = orc.project_rays_visible(s["u"], s["v"], s["f"], s["pan"], s["tilt"], s["rays"], 1080, 1920)
+    o1, _ = orc.get_overlap_index(keep, pidx)
+    m = np.asarray(keep)[o1]
+    pr = np.concatenate([[0, 1, 2], np.stack([2 * m + 3, 2 * m + 4], -1).reshape(-1)])
+    H = orc.compute_h_jacobian(s["u"], s["v"], s["pan"], s["tilt"], s["f"], s["rays"][m])
+    S = H @ s["state_cov"][np.ix_(pr, pr)] @ H.T + 0.1 * np.eye(2 * len(m))
+    assert np.linalg.eigvalsh(S).min() < 0
+    ref = orc.ekf_update(s, obs, keep, 1080, 1920)
+    h = ptzba.EKFHandle(0)
+    h.set_state(s["rays"], s["state_cov"])
+    ptz, vel, nm = h.update(s["u"], s["v"], [s["pan"], s["tilt"], s["f"]], obs, keep, 1080, 1920, 0.1)
+    rays1, cov1 = h.get_state()
+    h.close()
+    scale = np.abs(ref["velocity"]).max()
+    np.testing.assert_allclose(vel, ref["velocity"], rtol=0, atol=1e-7 * scale + 1e-9)
+    np.testing.assert_allclose(rays1, ref["rays"], rtol=0, atol=1e-8)
+    np.testing.assert_allclose(cov1, ref["state_cov"], rtol=1e-6, atol=1e-10)
+
+
 def test_ekf_update_no_match_leaves_state(gpu_available):
     import ptzba
     s, obs, keep = _random_state(50, 3)

@@ -45,8 +45,11 @@ def test_stream_matches_reference(gpu_available):
             setattr(image_process, k, v)
     for key in ("keyframe", "lost", "n_rays", "n_kp"):
         np.testing.assert_array_equal(np.array(rec[key]), d[key], err_msg=key)
-    np.testing.assert_allclose(np.array(rec["ptz"]), d["ptz"], rtol=0, atol=1e-6 * np.array([1.0, 1.0, 100.0]))
-    np.testing.assert_allclose(np.array(rec["velocity"]), d["velocity"], rtol=0, atol=1e-6 * np.array([1, 1, 100.0]))
+    tol = 1e-6 * np.array([1.0, 1.0, 100.0])
+    dp = np.abs(np.array(rec["ptz"]) - d["ptz"]).max(axis=0)
+    dv = np.abs(np.array(rec["velocity"]) - d["velocity"]).max(axis=0)
+    print("max |ptz - ref|", dp, "max |velocity - ref|", dv)
+    assert np.all(dp <= tol) and np.all(dv <= tol), (dp, dv)
     np.testing.assert_allclose(np.asarray(slam.rays), d["rays"], rtol=0, atol=1e-6)
     np.testing.assert_array_equal(np.array([len(c) for c in cov_diag]), d["cov_diag_n"])
     np.testing.assert_allclose(np.concatenate(cov_diag), d["cov_diag"], rtol=1e-6, atol=1e-12)

@@ -15,6 +15,14 @@ if has c4; then
   timeout -k 10 900 python -u -m pytest tests/test_gpu_config4.py -k config4 -x -v -s --timeout 800 --timeout-method thread > gpurun_out/${TAG}_c4.log 2>&1 || { echo C4FAIL; tail -40 gpurun_out/${TAG}_c4.log; exit 1; }
   grep -E "config4|set_problem|passed|failed" gpurun_out/${TAG}_c4.log | cut -c1-1500
 fi
+if has stream; then
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_ekf.py tests/test_gpu_stream.py -x -v -s --timeout 500 --timeout-method thread > gpurun_out/${TAG}_stream.log 2>&1 || { echo STREAMFAIL; grep -v "^tracking\|^overlap" gpurun_out/${TAG}_stream.log | tail -60; exit 1; }
+  grep -E "passed|failed|rmse" gpurun_out/${TAG}_stream.log
+fi
+if has demo; then
+  timeout -k 10 600 python -u pan-tilt-zoom-slam_amd/demo_stream.py --frames 300 --window 30 --keyframe-every 5 > gpurun_out/${TAG}_demo_stream.json 2> gpurun_out/${TAG}_demo_stream.err || { echo DEMOFAIL; tail -30 gpurun_out/${TAG}_demo_stream.err; exit 1; }
+  cat gpurun_out/${TAG}_demo_stream.json
+fi
 if has tests; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${TAG}_gpu_tests.log 2>&1 || { echo TESTFAIL; tail -40 gpurun_out/${TAG}_gpu_tests.log; exit 1; }
   tail -3 gpurun_out/${TAG}_gpu_tests.log
