@@ -46,6 +46,11 @@ if has ab64; then
     python -c "import json; d=json.loads(open('gpurun_out/${TAG}_ab64_$v.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$v it/s', round(d['value'],1), 'k1 ms', round(r['k1_avg_ms'],4), 'frac', round(r['frac'],3), 'cold', r.get('cold_cache',{}).get('k1_avg_ms'))"
   done
 fi
+if has c4prof; then
+  cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_c4prof -o run --output-format csv -- python bench.py --config config4 --steps 3 --warmup 1 --no-cpu-baseline --no-accuracy --no-secondary --no-cold > gpurun_out/${TAG}_c4prof.log 2>&1 || { echo C4PROFFAIL; tail gpurun_out/${TAG}_c4prof.log; exit 1; }
+  head -14 gpurun_out/${TAG}_c4prof/run_kernel_stats.csv | cut -d, -f1-4 | cut -c1-120
+fi
 if has prof; then
   cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof_stats -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-accuracy --no-secondary --no-cold > gpurun_out/${TAG}_prof_stats.log 2>&1 || { echo PROFFAIL; tail gpurun_out/${TAG}_prof_stats.log; exit 1; }
