@@ -223,6 +223,22 @@ PTZBA_EXPORT int ptz_refine_poses(int device, int32_t n_hyp, double* ptz_inout, 
  * pair_i/pair_j/pair_count: n_pairs; idx_a/idx_b: concatenated match keypoint indices.
  * kp_count[n_frames]: keypoints per frame.  Output landmark id per match (of the src keypoint) and
  * the landmark count; *n_inconsistent counts the reference's "in-consistent matching" warnings. */
+/* ---------------- feature front-end (image_process.py:178-234, 418-441) ---------------- */
+/* Brute-force 2-nearest-neighbour matching in L2 (cv.BFMatcher().knnMatch(des1, des2, k=2)): for each of the
+ * n1 query descriptors the two nearest of the n2 train descriptors, idx_out[2*i+0/1] (ties: lower index
+ * first; -1 when n2 < 2) and their L2 distances dist_out[2*i+0/1].  Descriptors are fp32 rows of `dim`.
+ * The ratio test of match_sift_features (m < 0.7 n) runs on the host. */
+PTZBA_EXPORT int ptz_match_knn2(int device, int64_t n1, int64_t n2, int32_t dim, const float* des1, const float* des2,
+                                int32_t* idx_out, float* dist_out);
+/* Homography RANSAC (cv.findHomography(..., RANSAC, threshold) as called by homography_ransac): n_hyp
+ * hypotheses from 4-point samples keyed by (seed, hypothesis, draw), DLT in Hartley-normalised coordinates,
+ * the hypothesis with most inliers (reprojection error < threshold px; ties: lowest index), a linear
+ * least-squares refit on its inliers, and the final inlier mask (mask_out[n], 1 = inlier), H_out[9]
+ * (row-major, H[8] = 1) and the inlier count.  n >= 4. */
+PTZBA_EXPORT int ptz_homography_ransac(int device, int64_t n, const double* pts1, const double* pts2, double threshold,
+                                       int32_t n_hyp, uint64_t seed, uint8_t* mask_out, double* H_out,
+                                       int32_t* n_inliers_out);
+
 /* Coupling window of a record set (host only, O(n_obs)): win_out[f] = the highest frame that shares a
  * landmark with frame f (>= f).  Computed over ALL records it is the frame_win_hi every rank of a
  * landmark-sharded solve passes in ptzba_problem_opts. */

@@ -512,3 +512,114 @@ def refine_pose(pose0, rays, points, u, v, ftol=1e-4, xtol=1e-8, gtol=1e-8):
     res = least_squares(reloc_residual, np.asarray(pose0, np.float64), x_scale='jac', ftol=ftol, xtol=xtol,
                         gtol=gtol, method='trf', args=(rays, points, u, v))
     return res.x, res.cost
+
+
+# --------------------------------------------------------------------------------------------
+# feature front-end (image_process.py:178-234, 418-441): the GPU matcher / RANSAC's restatement
+# --------------------------------------------------------------------------------------------
+def knn2(des1, des2):
+    """cv.BFMatcher().knnMatch(des1, des2, k=2) (image_process.py:191), L2: for each query the two nearest
+    train rows, ties to the lower index.  Distances summed in fp64 (exact for SIFT's integer descriptors)."""
+    a = np.asarray(des1, np.float64)
+    b = np.asarray(des2, np.float64)
+    d2 = ((a[:, None, :] - b[None, :, :]) ** 2).sum(-1)
+    order = np.lexsort((np.broadcast_to(np.arange(len(b)), d2.shape), d2), axis=1)[:, :2]
+    return order.astype(np.int32), np.sqrt(np.take_along_axis(d2, order, 1))
+
+
+_M64 = (1 << 64) - 1
+
+
+def _mix64(z):
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def _ransac_draw(seed, h, k, attempt, n):
+    z = _mix64((seed * 0x9E3779B97F4A7C15 + (h << 20) + (attempt << 4) + k + 1) & _M64)
+    return z % n
+
+
+def _ransac_sample(seed, h, n):
+    s = []
+    for k in range(4):
+        att = 0
+        while True:
+            v = _ransac_draw(seed, h, k, att, n)
+            att += 1
+            if v not in s or att >= 64:
+                break
+        s.append(v)
+    return s
+
+
+def _solve8(M):
+    """Gaussian elimination with partial pivoting on the 8x9 augmented system (the GPU's solve8)."""
+    M = np.array(M, dtype=np.float64)
+    for c in range(8):
+        p = c + int(np.argmax(np.abs(M[c:, c])))
+        if not np.abs(M[p, c]) > 1e-12:
+            return None
+        if p != c:
+            M[[c, p]] = M[[p, c]]
+        inv = 1.0 / M[c, c]
+        for r in range(c + 1, 8):
+            f = M[r, c] * inv
+            M[r, c:] -= f * M[c, c:]
+    x = np.zeros(8)
+    for c in range(7, -1, -1):
+        x[c] = (M[c, 8] - M[c, c + 1:8] @ x[c + 1:]) / M[c, c]
+    return x
+
+
+def _dlt_rows(x, y, u, v):
+    return ([x, y, 1, 0, 0, 0, -u * x, -u * y, u], [0, 0, 0, x, y, 1, -v * x, -v * y, v])
+
+
+def homography_ransac(p1, p2, threshold, n_hyp=2000, seed=0):
+    """Restatement of ptz_homography_ransac (the cv.findHomography RANSAC call of image_process.py:433):
+    counter-keyed 4-point samples, Hartley-normalised DLT, most inliers (then lowest index), linear
+    least-squares refit on the inliers, final mask.  Returns (mask, H, count)."""
+    p1 = np.asarray(p1, np.float64).reshape(-1, 2)
+    p2 = np.asarray(p2, np.float64).reshape(-1, 2)
+    n = len(p1)
+    c1, c2 = p1.mean(0), p2.mean(0)
+    s1 = np.sqrt(2.0) * n / np.sqrt(((p1 - c1) ** 2).sum(1)).sum()
+    s2 = np.sqrt(2.0) * n / np.sqrt(((p2 - c2) ** 2).sum(1)).sum()
+    q1, q2 = s1 * (p1 - c1), s2 * (p2 - c2)
+    T1 = np.array([[s1, 0, -s1 * c1[0]], [0, s1, -s1 * c1[1]], [0, 0, 1]])
+    T2i = np.array([[1 / s2, 0, c2[0]], [0, 1 / s2, c2[1]], [0, 0, 1]])
+
+    def denorm(h):
+        return T2i @ np.append(h, 1.0).reshape(3, 3) @ T1
+
+    def err2(H):
+        w = H[2, 0] * p1[:, 0] + H[2, 1] * p1[:, 1] + H[2, 2]
+        px = (H[0, 0] * p1[:, 0] + H[0, 1] * p1[:, 1] + H[0, 2]) / w
+        py = (H[1, 0] * p1[:, 0] + H[1, 1] * p1[:, 1] + H[1, 2]) / w
+        return (px - p2[:, 0]) ** 2 + (py - p2[:, 1]) ** 2
+
+    thr2 = threshold * threshold
+    best, best_h, best_H = -1, -1, None
+    for h in range(n_hyp):
+        s = _ransac_sample(seed, h, n)
+        rows = []
+        for k in s:
+            rows.extend(_dlt_rows(q1[k, 0], q1[k, 1], q2[k, 0], q2[k, 1]))
+        x = _solve8(rows)
+        if x is None:
+            continue
+        H = denorm(x)
+        c = int((err2(H) < thr2).sum())
+        if c > best:
+            best, best_h, best_H = c, h, H
+    if best_H is None:
+        return np.zeros(n, bool), np.zeros((3, 3)), 0
+    inl = err2(best_H) < thr2
+    A = np.array([r for i in np.flatnonzero(inl) for r in _dlt_rows(q1[i, 0], q1[i, 1], q2[i, 0], q2[i, 1])])
+    G = A.T @ A
+    x = _solve8(np.concatenate([G[:8, :8], G[:8, 8:9]], 1))
+    H = denorm(x) if x is not None else best_H
+    mask = err2(H) < thr2
+    return mask, H / H[2, 2], int(mask.sum())

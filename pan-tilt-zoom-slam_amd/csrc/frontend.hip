@@ -1,0 +1,415 @@
+// Feature front-end on the GPU: the matching half of image_process.match_sift_features
+// (image_process.py:178-234) -- brute-force 2-nearest-neighbour search in L2 (cv.BFMatcher().knnMatch(k=2))
+// and the homography RANSAC behind it (homography_ransac, image_process.py:418-441, cv.findHomography with
+// RANSAC).  Detection (SIFT/ORB on pixels) and LK flow stay front-end hooks.
+//
+//   ptz_match_knn2         one 64x64 tile of squared L2 distances per workgroup (fp32, 4x4 outputs per
+//                          thread, descriptors staged through LDS in k-chunks of 16), then one wave per query
+//                          keeps the two nearest (distance, index), ties to the lower index.  For SIFT's
+//                          integer-valued descriptors (0..255, 128-d) every partial sum is an exact fp32
+//                          integer, so the distances equal any other summation order bit for bit.
+//   ptz_homography_ransac  hypotheses from counter-keyed 4-point samples (the sampling stream is a function of
+//                          (seed, hypothesis, draw) only), one lane per hypothesis solves the 8x8 DLT system
+//                          (normalised coordinates, partial pivoting), a workgroup of 256 scores 64 hypotheses
+//                          against every point, the best (most inliers, then lowest index) is kept with a 64-bit
+//                          atomic max; one workgroup refits H by linear least squares on its inliers and writes
+//                          the final mask.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "../../include/ptzba.h"
+#include "host_util.h"
+#include "ptzba_common.h"
+
+namespace ptzba {
+
+constexpr int KT = 64, KC = 16;  // distance tile, k-chunk
+
+__global__ __launch_bounds__(256) void k_sqdist(int n1, int n2, int dim, const float* __restrict__ a,
+                                                const float* __restrict__ b, float* __restrict__ d) {
+  __shared__ float sa[KC][KT + 4], sb[KC][KT + 4];
+  const int t = threadIdx.x, tx = t & 15, ty = t >> 4;
+  const int q0 = blockIdx.y * KT, j0 = blockIdx.x * KT;
+  float acc[4][4] = {};
+  for (int k0 = 0; k0 < dim; k0 += KC) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {  // 64 rows x 16 dims each for a and b: 1024 values, 4 per thread
+      const int e = t + 256 * p, r = e >> 4, k = e & 15;
+      const int qa = q0 + r, jb = j0 + r, kk = k0 + k;
+      sa[k][r] = (qa < n1 && kk < dim) ? a[(int64_t)qa * dim + kk] : 0.f;
+      sb[k][r] = (jb < n2 && kk < dim) ? b[(int64_t)jb * dim + kk] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      float av[4], bv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        av[i] = sa[k][ty * 4 + i];
+        bv[i] = sb[k][tx * 4 + i];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float df = av[i] - bv[j];
+          acc[i][j] = fmaf(df, df, acc[i][j]);
+        }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = q0 + ty * 4 + i;
+    if (q >= n1) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int jj = j0 + tx * 4 + j;
+      if (jj < n2) d[(int64_t)q * n2 + jj] = acc[i][j];
+    }
+  }
+}
+
+// (d, idx) lexicographic: smaller distance first, then smaller index
+__device__ __forceinline__ bool lt(float d1, int i1, float d2, int i2) { return d1 < d2 || (d1 == d2 && i1 < i2); }
+
+__global__ __launch_bounds__(256) void k_top2(int n1, int n2, const float* __restrict__ d, int* __restrict__ idx,
+                                              float* __restrict__ dist) {
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (q >= n1) return;
+  float b1 = INFINITY, b2 = INFINITY;
+  int i1 = 0x7fffffff, i2 = 0x7fffffff;
+  for (int j = lane; j < n2; j += 64) {
+    const float v = d[(int64_t)q * n2 + j];
+    if (lt(v, j, b1, i1)) {
+      b2 = b1; i2 = i1; b1 = v; i1 = j;
+    } else if (lt(v, j, b2, i2)) {
+      b2 = v; i2 = j;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float ob1 = __shfl_xor(b1, off), ob2 = __shfl_xor(b2, off);
+    const int oi1 = __shfl_xor(i1, off), oi2 = __shfl_xor(i2, off);
+    // merge two sorted pairs {b1 <= b2}, {ob1 <= ob2}
+    float n1v, n2v;
+    int n1i, n2i;
+    if (lt(b1, i1, ob1, oi1)) {
+      n1v = b1; n1i = i1;
+      if (lt(b2, i2, ob1, oi1)) { n2v = b2; n2i = i2; } else { n2v = ob1; n2i = oi1; }
+    } else {
+      n1v = ob1; n1i = oi1;
+      if (lt(b1, i1, ob2, oi2)) { n2v = b1; n2i = i1; } else { n2v = ob2; n2i = oi2; }
+    }
+    b1 = n1v; i1 = n1i; b2 = n2v; i2 = n2i;
+  }
+  if (lane == 0) {
+    idx[2 * q] = i1;
+    idx[2 * q + 1] = n2 > 1 ? i2 : -1;
+    dist[2 * q] = sqrtf(b1);
+    dist[2 * q + 1] = n2 > 1 ? sqrtf(b2) : INFINITY;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// homography RANSAC
+// ---------------------------------------------------------------------------------------------
+__device__ __host__ inline uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+// draw k of hypothesis h: a function of (seed, h, k, attempt) only
+__device__ __host__ inline uint32_t ransac_draw(uint64_t seed, uint32_t h, uint32_t k, uint32_t attempt, uint32_t n) {
+  const uint64_t z = mix64(seed * 0x9E3779B97F4A7C15ull + ((uint64_t)h << 20) + ((uint64_t)attempt << 4) + k + 1);
+  return (uint32_t)(z % n);
+}
+
+struct Norm {
+  double c1x, c1y, s1, c2x, c2y, s2;  // p' = s (p - c)
+};
+
+// solve the 8x8 system M x = r (row-major M[8][9] augmented) by Gaussian elimination with partial
+// pivoting; false if singular
+__device__ __host__ inline bool solve8(double (&M)[8][9], double (&x)[8]) {
+  for (int c = 0; c < 8; ++c) {
+    int p = c;
+    double best = fabs(M[c][c]);
+    for (int r = c + 1; r < 8; ++r)
+      if (fabs(M[r][c]) > best) { best = fabs(M[r][c]); p = r; }
+    if (!(best > 1e-12)) return false;
+    if (p != c)
+      for (int k = 0; k < 9; ++k) { const double tmp = M[c][k]; M[c][k] = M[p][k]; M[p][k] = tmp; }
+    const double inv = 1.0 / M[c][c];
+    for (int r = c + 1; r < 8; ++r) {
+      const double f = M[r][c] * inv;
+      for (int k = c; k < 9; ++k) M[r][k] -= f * M[c][k];
+    }
+  }
+  for (int c = 7; c >= 0; --c) {
+    double s = M[c][8];
+    for (int k = c + 1; k < 8; ++k) s -= M[c][k] * x[k];
+    x[c] = s / M[c][c];
+  }
+  return true;
+}
+
+// the two DLT rows of one correspondence (h33 = 1) in normalised coordinates
+__device__ __host__ inline void dlt_rows(double x, double y, double u, double v, double (&r0)[9], double (&r1)[9]) {
+  r0[0] = x; r0[1] = y; r0[2] = 1; r0[3] = 0; r0[4] = 0; r0[5] = 0; r0[6] = -u * x; r0[7] = -u * y; r0[8] = u;
+  r1[0] = 0; r1[1] = 0; r1[2] = 0; r1[3] = x; r1[4] = y; r1[5] = 1; r1[6] = -v * x; r1[7] = -v * y; r1[8] = v;
+}
+
+// H (pixel coordinates) from the normalised solution h: H = T2^-1 Hn T1
+__device__ __host__ inline void denormalise(const double (&h)[8], const Norm& N, double (&H)[9]) {
+  const double Hn[9] = {h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], 1.0};
+  // Hn T1: T1 = [[s1, 0, -s1 c1x], [0, s1, -s1 c1y], [0, 0, 1]]
+  double A[9];
+  for (int r = 0; r < 3; ++r) {
+    A[3 * r + 0] = Hn[3 * r + 0] * N.s1;
+    A[3 * r + 1] = Hn[3 * r + 1] * N.s1;
+    A[3 * r + 2] = Hn[3 * r + 2] - Hn[3 * r + 0] * N.s1 * N.c1x - Hn[3 * r + 1] * N.s1 * N.c1y;
+  }
+  // T2^-1 = [[1/s2, 0, c2x], [0, 1/s2, c2y], [0, 0, 1]]
+  for (int c = 0; c < 3; ++c) {
+    H[0 + c] = A[0 + c] / N.s2 + N.c2x * A[6 + c];
+    H[3 + c] = A[3 + c] / N.s2 + N.c2y * A[6 + c];
+    H[6 + c] = A[6 + c];
+  }
+}
+
+__device__ __host__ inline double reproj_err2(const double (&H)[9], double x, double y, double u, double v) {
+  const double w = H[6] * x + H[7] * y + H[8];
+  const double px = (H[0] * x + H[1] * y + H[2]) / w, py = (H[3] * x + H[4] * y + H[5]) / w;
+  return (px - u) * (px - u) + (py - v) * (py - v);
+}
+
+constexpr int RH = 64;  // hypotheses per workgroup
+
+__global__ __launch_bounds__(256) void k_ransac_score(int n, const double* __restrict__ p1, const double* __restrict__ p2,
+                                                      Norm N, double thr2, int n_hyp, uint64_t seed,
+                                                      unsigned long long* __restrict__ best) {
+  __shared__ double sH[RH][9];
+  __shared__ int sOk[RH];
+  __shared__ int sCnt[4][RH];
+  const int t = threadIdx.x, h0 = blockIdx.x * RH;
+  if (t < RH) {
+    const int h = h0 + t;
+    bool ok = h < n_hyp;
+    double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 1};
+    if (ok) {
+      uint32_t s[4];
+      for (int k = 0; k < 4; ++k) {
+        uint32_t att = 0, v;
+        bool dup;
+        do {
+          v = ransac_draw(seed, (uint32_t)h, (uint32_t)k, att++, (uint32_t)n);
+          dup = false;
+          for (int m = 0; m < k; ++m) dup |= (s[m] == v);
+        } while (dup && att < 64);
+        s[k] = v;
+      }
+      double M[8][9];
+      for (int k = 0; k < 4; ++k) {
+        const double x = N.s1 * (p1[2 * s[k]] - N.c1x), y = N.s1 * (p1[2 * s[k] + 1] - N.c1y);
+        const double u = N.s2 * (p2[2 * s[k]] - N.c2x), v = N.s2 * (p2[2 * s[k] + 1] - N.c2y);
+        dlt_rows(x, y, u, v, M[2 * k], M[2 * k + 1]);
+      }
+      double hv[8];
+      ok = solve8(M, hv);
+      if (ok) denormalise(hv, N, H);
+    }
+    for (int k = 0; k < 9; ++k) sH[t][k] = H[k];
+    sOk[t] = ok ? 1 : 0;
+  }
+  __syncthreads();
+  const int hl = t & (RH - 1), part = t >> 6;
+  double H[9];
+  for (int k = 0; k < 9; ++k) H[k] = sH[hl][k];
+  int cnt = 0;
+  if (sOk[hl])
+    for (int i = part; i < n; i += 4)
+      cnt += reproj_err2(H, p1[2 * i], p1[2 * i + 1], p2[2 * i], p2[2 * i + 1]) < thr2 ? 1 : 0;
+  sCnt[part][hl] = cnt;
+  __syncthreads();
+  if (t < RH && sOk[t] && h0 + t < n_hyp) {
+    const int c = sCnt[0][t] + sCnt[1][t] + sCnt[2][t] + sCnt[3][t];
+    const unsigned long long key = ((unsigned long long)c << 32) | (0xffffffffu - (unsigned)(h0 + t));
+    atomicMax(best, key);
+  }
+}
+
+// one workgroup: the best hypothesis' H, its inliers, a linear least-squares refit on them (normal
+// equations of the DLT rows in normalised coordinates, fixed-order reduction), the final mask
+__global__ __launch_bounds__(256) void k_ransac_refine(int n, const double* __restrict__ p1, const double* __restrict__ p2,
+                                                       Norm N, double thr2, uint64_t seed,
+                                                       const unsigned long long* __restrict__ best,
+                                                       uint8_t* __restrict__ mask, double* __restrict__ Hout,
+                                                       int* __restrict__ nin) {
+  __shared__ double sH[9];
+  __shared__ double red[256][45];  // 8x9 augmented normal equations (upper part of the 9x9 Gram matrix)
+  __shared__ int sOk;
+  const int t = threadIdx.x;
+  const unsigned long long key = *best;
+  if (t == 0) {
+    const uint32_t h = 0xffffffffu - (uint32_t)(key & 0xffffffffu);
+    uint32_t s[4];
+    for (int k = 0; k < 4; ++k) {
+      uint32_t att = 0, v;
+      bool dup;
+      do {
+        v = ransac_draw(seed, h, (uint32_t)k, att++, (uint32_t)n);
+        dup = false;
+        for (int m = 0; m < k; ++m) dup |= (s[m] == v);
+      } while (dup && att < 64);
+      s[k] = v;
+    }
+    double M[8][9], hv[8], H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 1};
+    for (int k = 0; k < 4; ++k) {
+      const double x = N.s1 * (p1[2 * s[k]] - N.c1x), y = N.s1 * (p1[2 * s[k] + 1] - N.c1y);
+      const double u = N.s2 * (p2[2 * s[k]] - N.c2x), v = N.s2 * (p2[2 * s[k] + 1] - N.c2y);
+      dlt_rows(x, y, u, v, M[2 * k], M[2 * k + 1]);
+    }
+    sOk = key != 0 && solve8(M, hv);
+    if (sOk) denormalise(hv, N, H);
+    for (int k = 0; k < 9; ++k) sH[k] = H[k];
+  }
+  __syncthreads();
+  if (!sOk) {
+    for (int i = t; i < n; i += 256) mask[i] = 0;
+    if (t < 9) Hout[t] = 0.0;
+    if (t == 0) *nin = 0;
+    return;
+  }
+  double H[9];
+  for (int k = 0; k < 9; ++k) H[k] = sH[k];
+  double g[45];
+  for (int k = 0; k < 45; ++k) g[k] = 0.0;
+  for (int i = t; i < n; i += 256) {
+    if (!(reproj_err2(H, p1[2 * i], p1[2 * i + 1], p2[2 * i], p2[2 * i + 1]) < thr2)) continue;
+    double r0[9], r1[9];
+    const double x = N.s1 * (p1[2 * i] - N.c1x), y = N.s1 * (p1[2 * i + 1] - N.c1y);
+    const double u = N.s2 * (p2[2 * i] - N.c2x), v = N.s2 * (p2[2 * i + 1] - N.c2y);
+    dlt_rows(x, y, u, v, r0, r1);
+    int e = 0;
+    for (int a = 0; a < 8; ++a)
+      for (int b = a; b < 9; ++b) g[e++] += r0[a] * r0[b] + r1[a] * r1[b];
+  }
+  for (int k = 0; k < 44; ++k) red[t][k] = g[k];
+  __syncthreads();
+  if (t < 44) {
+    double s = 0.0;
+    for (int q = 0; q < 256; ++q) s += red[q][t];
+    red[0][t] = s;
+  }
+  __syncthreads();
+  if (t == 0) {
+    double M[8][9], hv[8];
+    int e = 0;
+    for (int a = 0; a < 8; ++a)
+      for (int b = a; b < 9; ++b) {
+        M[a][b] = red[0][e++];
+        if (b < 8) M[b][a] = M[a][b];
+      }
+    if (solve8(M, hv)) {
+      double Hr[9];
+      denormalise(hv, N, Hr);
+      for (int k = 0; k < 9; ++k) sH[k] = Hr[k];
+    }
+  }
+  __syncthreads();
+  for (int k = 0; k < 9; ++k) H[k] = sH[k];
+  int cnt = 0;
+  for (int i = t; i < n; i += 256) {
+    const uint8_t m = reproj_err2(H, p1[2 * i], p1[2 * i + 1], p2[2 * i], p2[2 * i + 1]) < thr2 ? 1 : 0;
+    mask[i] = m;
+    cnt += m;
+  }
+  __shared__ int sc[256];
+  sc[t] = cnt;
+  __syncthreads();
+  if (t == 0) {
+    int c = 0;
+    for (int q = 0; q < 256; ++q) c += sc[q];
+    *nin = c;
+  }
+  if (t < 9) Hout[t] = H[t] / H[8];
+}
+
+}  // namespace ptzba
+
+using namespace ptzba;
+
+int ptz_match_knn2(int device, int64_t n1, int64_t n2, int32_t dim, const float* des1, const float* des2,
+                   int32_t* idx_out, float* dist_out) {
+  if (n1 < 0 || n2 < 0 || dim <= 0) return fail("bad sizes n1=%lld n2=%lld dim=%d", (long long)n1, (long long)n2, dim);
+  if (n1 == 0) return 0;
+  if (!des1 || !idx_out || !dist_out || (n2 > 0 && !des2)) return fail("null argument");
+  if (n1 * n2 > ((int64_t)1 << 31)) return fail("distance matrix %lld x %lld too large", (long long)n1, (long long)n2);
+  if (n2 == 0) {
+    for (int64_t i = 0; i < n1; ++i) {
+      idx_out[2 * i] = idx_out[2 * i + 1] = -1;
+      dist_out[2 * i] = dist_out[2 * i + 1] = INFINITY;
+    }
+    return 0;
+  }
+  if (select_device(device)) return -1;
+  DBuf a, b, d, idx, dist;
+  if (a.alloc((size_t)n1 * dim * 4) || b.alloc((size_t)n2 * dim * 4) || d.alloc((size_t)n1 * n2 * 4) ||
+      idx.alloc((size_t)n1 * 8) || dist.alloc((size_t)n1 * 8))
+    return -1;
+  HIPCHK(hipMemcpy(a.p, des1, (size_t)n1 * dim * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(b.p, des2, (size_t)n2 * dim * 4, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_sqdist, dim3((unsigned)((n2 + KT - 1) / KT), (unsigned)((n1 + KT - 1) / KT)), dim3(256), 0, nullptr,
+                     (int)n1, (int)n2, dim, a.as<float>(), b.as<float>(), d.as<float>());
+  hipLaunchKernelGGL(k_top2, dim3((unsigned)((n1 + 3) / 4)), dim3(256), 0, nullptr, (int)n1, (int)n2, d.as<float>(),
+                     idx.as<int>(), dist.as<float>());
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(idx_out, idx.p, (size_t)n1 * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(dist_out, dist.p, (size_t)n1 * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int ptz_homography_ransac(int device, int64_t n, const double* pts1, const double* pts2, double threshold,
+                          int32_t n_hyp, uint64_t seed, uint8_t* mask_out, double* H_out, int32_t* n_inliers_out) {
+  if (n < 4) return fail("homography RANSAC needs at least 4 correspondences (got %lld)", (long long)n);
+  if (!pts1 || !pts2 || !mask_out || !H_out || !n_inliers_out) return fail("null argument");
+  if (!(threshold > 0) || n_hyp < 1) return fail("bad threshold / hypothesis count");
+  if (n >= ((int64_t)1 << 31)) return fail("too many correspondences");
+  // Hartley normalisation of each point set (centroid, mean distance sqrt(2)); host, O(n)
+  Norm N{};
+  {
+    double sx1 = 0, sy1 = 0, sx2 = 0, sy2 = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      sx1 += pts1[2 * i]; sy1 += pts1[2 * i + 1]; sx2 += pts2[2 * i]; sy2 += pts2[2 * i + 1];
+    }
+    N.c1x = sx1 / n; N.c1y = sy1 / n; N.c2x = sx2 / n; N.c2y = sy2 / n;
+    double d1 = 0, d2 = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      d1 += std::sqrt((pts1[2 * i] - N.c1x) * (pts1[2 * i] - N.c1x) + (pts1[2 * i + 1] - N.c1y) * (pts1[2 * i + 1] - N.c1y));
+      d2 += std::sqrt((pts2[2 * i] - N.c2x) * (pts2[2 * i] - N.c2x) + (pts2[2 * i + 1] - N.c2y) * (pts2[2 * i + 1] - N.c2y));
+    }
+    N.s1 = d1 > 0 ? std::sqrt(2.0) * n / d1 : 1.0;
+    N.s2 = d2 > 0 ? std::sqrt(2.0) * n / d2 : 1.0;
+  }
+  if (select_device(device)) return -1;
+  DBuf p1, p2, best, mask, H, nin;
+  if (p1.alloc((size_t)n * 16) || p2.alloc((size_t)n * 16) || best.alloc(8) || mask.alloc((size_t)n) ||
+      H.alloc(72) || nin.alloc(4))
+    return -1;
+  HIPCHK(hipMemcpy(p1.p, pts1, (size_t)n * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(p2.p, pts2, (size_t)n * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(best.p, 0, 8));
+  const double thr2 = threshold * threshold;
+  hipLaunchKernelGGL(k_ransac_score, dim3((unsigned)((n_hyp + RH - 1) / RH)), dim3(256), 0, nullptr, (int)n,
+                     p1.as<double>(), p2.as<double>(), N, thr2, n_hyp, seed, best.as<unsigned long long>());
+  hipLaunchKernelGGL(k_ransac_refine, dim3(1), dim3(256), 0, nullptr, (int)n, p1.as<double>(), p2.as<double>(), N, thr2,
+                     seed, best.as<unsigned long long>(), mask.as<uint8_t>(), H.as<double>(), nin.as<int>());
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(mask_out, mask.p, (size_t)n, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(H_out, H.p, 72, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(n_inliers_out, nin.p, 4, hipMemcpyDeviceToHost));
+  return 0;
+}

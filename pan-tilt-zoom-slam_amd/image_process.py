@@ -41,11 +41,11 @@ def _hook(name):
 detect_compute_sift = _hook("detect_compute_sift")              # (im, nfeatures, verbose) -> (kps, des)
 detect_compute_orb = _hook("detect_compute_orb")
 detect_compute_latch = _hook("detect_compute_latch")
-match_sift_features = _hook("match_sift_features")              # (kp1, des1, kp2, des2, pts_array, verbose)
+# match_sift_features / homography_ransac: GPU implementations below (kNN-2 + ratio test + RANSAC);
+# a correspondence source may still assign its own
 match_orb_features = _hook("match_orb_features")
 match_latch_features = _hook("match_latch_features")
 optical_flow_matching = _hook("optical_flow_matching")
-homography_ransac = _hook("homography_ransac")
 draw_matches = None  # optional visualisation hook (bundle_adjustment.py:153-163)
 
 
@@ -57,6 +57,50 @@ def detect_compute_sift_array(im, nfeatures, norm=True):
     if norm and len(des):
         des = (des / np.linalg.norm(des, axis=1).reshape(-1, 1)).astype(np.float64)
     return pts, des
+
+
+def match_sift_features(keypoint1, descriptor1, keypoint2, descriptor2, pts_array=False, verbose=False):
+    """image_process.py:178-234 on the GPU: 2-nearest-neighbour L2 matching (cv.BFMatcher().knnMatch, k=2:
+    libptzba ptz_match_knn2), Lowe's ratio test m < 0.7 n, then the homography RANSAC inliers (1 px).
+    Returns (pts1, index1, pts2, index2) like the reference; (None, [], None, []) below 9 ratio-test
+    survivors."""
+    import ptzba
+    d1 = np.asarray(descriptor1, dtype=np.float32)
+    d2 = np.asarray(descriptor2, dtype=np.float32)
+    idx, dist = ptzba.match_knn2(d1, d2)
+    good = np.flatnonzero(dist[:, 0] < 0.7 * dist[:, 1]) if len(d2) >= 2 else np.zeros(0, np.int64)
+    if verbose:
+        print('%d matches passed the ratio test' % len(good))
+    if len(good) <= 8:
+        print('warning: match sift features failed, not enough matching')
+        return None, [], None, []
+    index1 = good.astype(np.int32)
+    index2 = idx[good, 0].astype(np.int32)
+    if pts_array:
+        pts1 = np.asarray(keypoint1, np.float64).reshape(-1, 2)[index1]
+        pts2 = np.asarray(keypoint2, np.float64).reshape(-1, 2)[index2]
+    else:
+        pts1 = np.array([keypoint1[i].pt for i in index1], np.float64).reshape(-1, 2)
+        pts2 = np.array([keypoint2[j].pt for j in index2], np.float64).reshape(-1, 2)
+    inlier_index = homography_ransac(pts1, pts2, 1.0)
+    if verbose:
+        print('%d matches passed the homography ransac' % len(inlier_index))
+    return pts1[inlier_index, :], index1[inlier_index].tolist(), pts2[inlier_index, :], index2[inlier_index].tolist()
+
+
+def homography_ransac(points1, points2, reprojection_threshold=0.5, return_matrix=False):
+    """image_process.py:418-441 on the GPU (libptzba ptz_homography_ransac: 2000 counter-keyed 4-point
+    hypotheses, DLT, most inliers, least-squares refit): RANSAC inlier indices [, homography]."""
+    import ptzba
+    p1 = np.asarray(points1, np.float64).reshape(-1, 2)
+    p2 = np.asarray(points2, np.float64).reshape(-1, 2)
+    assert p1.shape[0] == p2.shape[0]
+    assert p1.shape[0] >= 4
+    mask, H, _ = ptzba.homography_ransac(p1, p2, reprojection_threshold)
+    index = [int(i) for i in np.flatnonzero(mask)]
+    if return_matrix:
+        return index, H
+    return index
 
 
 def keypoints_masking(kp, mask):

@@ -121,6 +121,8 @@ def lib():
         "ptz_h_jacobian": ([I, I64, D, D, D, D, D, V, V, V], I),
         "ptzba_build_landmarks": ([I32, V, I64, V, V, V, V, V, V, V, V], I),
         "ptzba_coupling_window": ([I32, I32, I64, V, V, V], I),
+        "ptz_match_knn2": ([I, I64, I64, I32, V, V, V, V], I),
+        "ptz_homography_ransac": ([I, I64, V, V, D, I32, ctypes.c_uint64, V, V, POINTER(c_int32)], I),
         "ptz_py_shuffle_prefix": ([V, I64, V, I64, V], I),
         "ptz_set_order_pairs": ([I64, V, V, V, V, V], I),
         "ptz_keyframe_features": ([I32, I64, V, V, V, V, V, V, V, V], I),
@@ -151,7 +153,7 @@ EXPORTED_SYMBOLS = [
     "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_solve", "ptzba_read_scalars", "ptzba_accept",
     "ptzba_lm_start", "ptzba_lm_init", "ptzba_lm_build", "ptzba_lm_solve", "ptzba_lm_decide", "ptzba_lm_wait",
     "ptzba_exchange", "ptzba_exchange_packed", "ptzba_pack", "ptzba_unpack", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptzba_save_state", "ptzba_restore_state", "ptz_ray_to_image",
-    "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks", "ptzba_coupling_window",
+    "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks", "ptzba_coupling_window", "ptz_match_knn2", "ptz_homography_ransac",
     "ptz_py_shuffle_prefix", "ptz_set_order_pairs", "ptz_keyframe_features", "ptz_pack_records",
     "ptz_refine_poses", "ptzekf_new", "ptzekf_delete", "ptzekf_num_rays", "ptzekf_set_state", "ptzekf_get_state", "ptzekf_add_pose_cov",
     "ptzekf_remove_rays", "ptzekf_add_rays", "ptzekf_project_visible", "ptzekf_update",
@@ -237,6 +239,38 @@ def h_jacobian(u, v, f, pan, tilt, rays, displacement=None, device=0):
     _check(lib().ptz_h_jacobian(device, n, u, v, float(f), float(pan), float(tilt), _ptr(d), _ptr(rays), _ptr(H)),
            "ptz_h_jacobian")
     return H
+
+
+def match_knn2(des1, des2, device=None):
+    """cv.BFMatcher().knnMatch(des1, des2, k=2) on the GPU (image_process.py:191): the two nearest train
+    descriptors of every query, as (idx [n1, 2] int32, dist [n1, 2] float32 L2); ties to the lower index."""
+    d1 = np.ascontiguousarray(des1, dtype=np.float32)
+    d2 = np.ascontiguousarray(des2, dtype=np.float32)
+    if d1.ndim != 2 or d2.ndim != 2 or (len(d2) and d1.shape[1] != d2.shape[1]):
+        raise ValueError("descriptor arrays must be [n, dim] with the same dim")
+    n1 = len(d1)
+    idx = np.empty((n1, 2), np.int32)
+    dist = np.empty((n1, 2), np.float32)
+    if n1:
+        _check(lib().ptz_match_knn2(default_device() if device is None else device, n1, len(d2), d1.shape[1], _ptr(d1),
+                                    _ptr(d2), _ptr(idx), _ptr(dist)), "ptz_match_knn2")
+    return idx, dist
+
+
+def homography_ransac(points1, points2, threshold, n_hyp=2000, seed=0, device=None):
+    """Homography RANSAC on the GPU (the cv.findHomography call of image_process.py:433): returns
+    (inlier mask [n] bool, H [3, 3], inlier count)."""
+    p1 = _f64(points1, (-1, 2))
+    p2 = _f64(points2, (-1, 2))
+    if len(p1) != len(p2):
+        raise ValueError("point arrays differ in length")
+    mask = np.zeros(len(p1), np.uint8)
+    H = np.zeros(9)
+    nin = c_int32(0)
+    _check(lib().ptz_homography_ransac(default_device() if device is None else device, len(p1), _ptr(p1), _ptr(p2),
+                                       float(threshold), int(n_hyp), int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(mask), _ptr(H),
+                                       ctypes.byref(nin)), "ptz_homography_ransac")
+    return mask.astype(bool), H.reshape(3, 3), int(nin.value)
 
 
 def refine_poses(u, v, init_ptz, rays, points, subsets=None, ftol=1e-4, xtol=1e-8, max_iter=100, loss=LOSS_LINEAR,
