@@ -900,9 +900,9 @@ int ptzba_linearize(ptzba_handle h) {
 // the device-driven LM (lam_dev != nullptr), from device memory
 static int build_impl(ptzba_ctx* h, double lambda, const double* lam_dev, const int* skip_if = nullptr) {
   const int c = h->cur;
-  launch_landmark_damp(h->lm_out[c].as<double>(), h->lm_seg_begin.as<int32_t>(), h->D_ray.as<double>(),
-                       h->lm_aux.as<double>(), h->n_lm, lambda, lam_dev, skip_if, h->st);
-  launch_zero_tiles(h->S(), h->ld, h->ztiles.as<int2>(), h->n_ztiles, h->bvec(), 3 * h->ld, h->st);
+  launch_build_prologue(h->S(), h->ld, h->ztiles.as<int2>(), h->n_ztiles, h->bvec(), 3 * h->ld,
+                        h->lm_out[c].as<double>(), h->lm_seg_begin.as<int32_t>(), h->D_ray.as<double>(),
+                        h->lm_aux.as<double>(), h->n_lm, lambda, lam_dev, skip_if, h->st);
   SchurArgs a;
   a.items = h->s2_items.as<int4>();
   a.groups = h->s2_groups.as<int4>();
@@ -956,9 +956,6 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx) {
   tm_end(h, TM_CHOL);
   HIPCHK(hipGetLastError());
   tm_begin(h, TM_BACK);
-  launch_pose_trial(h->ptz.as<double>(), h->dpose.as<double>(), h->gpose(), h->D_pose.as<double>(),
-                    h->frame_pos.as<int32_t>(), h->ptz_trial.as<double>(),
-                    h->n_pose, h->n_fixed, h->lambda, lam_dev, h->loc.as<double>(), h->st);
   BacksubArgs b;
   b.lm_seg_begin = h->lm_seg_begin.as<int32_t>();
   b.seg_frame = h->seg_frame.as<int32_t>();
@@ -976,19 +973,19 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx) {
   b.n_fixed = h->n_fixed;
   b.lambda = h->lambda;
   b.lam_dev = lam_dev;
+  // ray back-substitution, trial poses and the trial's frame / ray tables: one launch
   if (h->precision == PTZBA_FP32)
-    launch_backsub<float>(b, h->st);
+    launch_trial<float>(b, h->ptz.as<double>(), h->gpose(), h->D_pose.as<double>(), h->ptz_trial.as<double>(),
+                        h->loc.as<double>(), h->n_pose, h->ft64.p, h->rt64.p, h->ft.p, h->rt.p, h->st);
   else
-    launch_backsub<double>(b, h->st);
+    launch_trial<double>(b, h->ptz.as<double>(), h->gpose(), h->D_pose.as<double>(), h->ptz_trial.as<double>(),
+                         h->loc.as<double>(), h->n_pose, h->ft64.p, h->rt64.p, h->ft64.p, h->rt64.p, h->st);
   tm_end(h, TM_BACK);
   // trial linearisation (its cost decides acceptance; kept as the next linearisation if accepted)
-  tables(h, h->ptz_trial.as<double>(), h->rays_trial.as<double>());
   linearize_into(h, nx);
-  // scal[1] (trial cost) and scal[2..4] are overwritten below, loc[0..3] by k_pose_trial: no memsets
+  // scal[1] (trial cost) and scal[2..4] are overwritten below, loc[0..3] by the trial kernel: no memsets
   launch_reduce_cols(h->lm_out[nx].as<double>() + 5, h->n_lm, 8, 1, 0, h->scal.as<double>() + 1,
-                     h->red_scratch.as<double>(), h->st);
-  launch_reduce_cols(h->lm_red.as<double>(), h->n_lm, 4, 3, 0, h->scal.as<double>() + 2, h->red_scratch.as<double>(),
-                     h->st);
+                     h->red_scratch.as<double>(), h->st, h->lm_red.as<double>(), 4, 3, h->scal.as<double>() + 2);
   HIPCHK(hipGetLastError());
   return 0;
 }

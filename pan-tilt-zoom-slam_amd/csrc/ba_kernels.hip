@@ -454,13 +454,30 @@ void launch_linearize(const LinArgs& a, int loss, hipStream_t st) {
 // monotone column-norm memory of scipy's x_scale='jac', common.py:598-612); Vinv and Vinv g.
 // lm_aux[l][8] = Vinv00 Vinv01 Vinv11 (Vinv g)0 (Vinv g)1 . . .
 // ------------------------------------------------------------------------------------------------
-__global__ void k_landmark_damp(const double* __restrict__ lm_out, const int32_t* __restrict__ lm_seg_begin,
-                                double* __restrict__ D_ray, double* __restrict__ lm_aux, int n_lm,
-                                double lambda_arg, const double* __restrict__ lam_dev,
-                                const int* __restrict__ skip_if) {
+// Build prologue in one launch: blocks [0, n_tiles) zero the factor pattern's tiles of S, block n_tiles the
+// b | g_pose | dU vectors, the rest damp the landmark blocks as above.
+__global__ __launch_bounds__(256) void k_build_prologue(double* __restrict__ S, int64_t ld, const int2* __restrict__ zt,
+                                                        int n_tiles, double* __restrict__ vec, int64_t n_vec,
+                                                        const double* __restrict__ lm_out,
+                                                        const int32_t* __restrict__ lm_seg_begin,
+                                                        double* __restrict__ D_ray, double* __restrict__ lm_aux, int n_lm,
+                                                        double lambda_arg, const double* __restrict__ lam_dev,
+                                                        const int* __restrict__ skip_if) {
+  const int b = blockIdx.x;
+  if (b < n_tiles) {
+    const int2 tij = zt[b];
+    double* T = S + (int64_t)tij.x * CHOL_NB * ld + (int64_t)tij.y * CHOL_NB;
+    for (int e = threadIdx.x; e < CHOL_NB * CHOL_NB / 2; e += blockDim.x)
+      *reinterpret_cast<double2*>(T + (int64_t)(e >> 4) * ld + 2 * (e & 15)) = make_double2(0.0, 0.0);
+    return;
+  }
+  if (b == n_tiles) {
+    for (int64_t e = threadIdx.x; e < n_vec; e += blockDim.x) vec[e] = 0.0;
+    return;
+  }
   if (skip_if && *skip_if) return;
   const double lambda = lam_dev ? *lam_dev : lambda_arg;
-  int l = blockIdx.x * blockDim.x + threadIdx.x;
+  const int l = (b - n_tiles - 1) * blockDim.x + threadIdx.x;
   if (l >= n_lm) return;
   double* o = lm_aux + (int64_t)l * 8;
   if (lm_seg_begin[l + 1] == lm_seg_begin[l]) {
@@ -472,12 +489,12 @@ __global__ void k_landmark_damp(const double* __restrict__ lm_out, const int32_t
   double d1 = fmax(D_ray[2 * l + 1], fmax(in[2], 1e-12));
   D_ray[2 * l] = d0;
   D_ray[2 * l + 1] = d1;
-  double a = in[0] + lambda * d0, b = in[1], c = in[2] + lambda * d1;
-  double det = a * c - b * b;
+  double a = in[0] + lambda * d0, bb = in[1], c = in[2] + lambda * d1;
+  double det = a * c - bb * bb;
   double i00 = 0, i01 = 0, i11 = 0;
   if (det > 0 && isfinite(det)) {
     double id = 1.0 / det;
-    i00 = c * id; i01 = -b * id; i11 = a * id;
+    i00 = c * id; i01 = -bb * id; i11 = a * id;
   }
   o[0] = i00; o[1] = i01; o[2] = i11;
   o[3] = i00 * in[3] + i01 * in[4];
@@ -485,10 +502,12 @@ __global__ void k_landmark_damp(const double* __restrict__ lm_out, const int32_t
   o[5] = 0; o[6] = 0; o[7] = det > 0 ? 0.0 : 1.0;
 }
 
-void launch_landmark_damp(const double* lm_out, const int32_t* lm_seg_begin, double* D_ray, double* lm_aux,
-                          int n_lm, double lambda, const double* lam_dev, const int* skip_if, hipStream_t st) {
-  hipLaunchKernelGGL(k_landmark_damp, dim3((n_lm + 255) / 256), dim3(256), 0, st, lm_out, lm_seg_begin, D_ray,
-                     lm_aux, n_lm, lambda, lam_dev, skip_if);
+void launch_build_prologue(double* S, int64_t ld, const int2* zt, int n_tiles, double* vec, int64_t n_vec,
+                           const double* lm_out, const int32_t* lm_seg_begin, double* D_ray, double* lm_aux, int n_lm,
+                           double lambda, const double* lam_dev, const int* skip_if, hipStream_t st) {
+  const unsigned nb = (unsigned)(n_tiles + 1 + (n_lm + 255) / 256);
+  hipLaunchKernelGGL(k_build_prologue, dim3(nb), dim3(256), 0, st, S, ld, zt, n_tiles, vec, n_vec, lm_out, lm_seg_begin,
+                     D_ray, lm_aux, n_lm, lambda, lam_dev, skip_if);
 }
 
 // (pose damping of the exchanged reduced system: k_chol_prepare, chol_kernels.hip)
@@ -498,8 +517,67 @@ void launch_landmark_damp(const double* lm_out, const int32_t* lm_seg_begin, dou
 //   pred_l  = -1/2 g_l.delta_l + 1/2 lambda delta_l^T D delta_l
 // one wave per landmark (lanes over segments)
 // ------------------------------------------------------------------------------------------------
+// Trial state in one launch (with the trial's frame / ray tables, which the trial linearisation reads):
+// blocks [0, nb) back-substitute 4 landmarks each as above, the last block forms the trial poses, their
+// tables and the pose partials (one thread per frame, fixed-order reduction: identical on every rank).
+struct PoseTrialArgs {
+  const double* ptz;
+  const double* g_pose;
+  const double* D_pose;
+  double* ptz_trial;
+  double* out4;
+  int n_pose;
+};
 template <typename real>
-__global__ __launch_bounds__(256) void k_backsub(BacksubArgs a) {
+__global__ __launch_bounds__(256) void k_trial(BacksubArgs a, PoseTrialArgs pa, FrameTab<double>* __restrict__ ft64,
+                                               RayTab<double>* __restrict__ rt64, FrameTab<real>* __restrict__ ft,
+                                               RayTab<real>* __restrict__ rt) {
+  const int nb = (a.n_lm + 3) / 4;
+  if ((int)blockIdx.x == nb) {
+    const double lambda = a.lam_dev ? *a.lam_dev : a.lambda;
+    __shared__ double red[4][256 / WAVE];
+    double pr = 0, dx = 0, xx = 0, gm = 0;
+    for (int f = threadIdx.x; f < pa.n_pose; f += blockDim.x) {
+      double x3[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const double x = pa.ptz[3 * f + q];
+        xx += x * x;
+        double y = x;
+        if (f >= a.n_fixed) {
+          const int k = a.frame_pos[f] + q;  // system row
+          const double d = a.dpose[k];
+          y = x + d;
+          pr += -0.5 * pa.g_pose[k] * d + 0.5 * lambda * pa.D_pose[3 * f + q] * d * d;
+          dx += d * d;
+          gm = fmax(gm, fabs(pa.g_pose[k]));
+        }
+        pa.ptz_trial[3 * f + q] = y;
+        x3[q] = y;
+      }
+      const FrameTab<double> t = make_frame_tab<double>(x3[0], x3[1], x3[2]);
+      ft64[f] = t;
+      if constexpr (sizeof(real) != sizeof(double)) {
+        FrameTab<real> r;
+        r.ca = (real)t.ca; r.sa = (real)t.sa; r.cb = (real)t.cb; r.sb = (real)t.sb; r.f = (real)t.f;
+        r.pad0 = r.pad1 = r.pad2 = (real)0;
+        ft[f] = r;
+      }
+    }
+    pr = wave_sum(pr); dx = wave_sum(dx); xx = wave_sum(xx);
+    for (int o = 32; o > 0; o >>= 1) gm = fmax(gm, __shfl_xor(gm, o, WAVE));
+    const int w = threadIdx.x >> 6;
+    if (lane_id() == 0) { red[0][w] = pr; red[1][w] = dx; red[2][w] = xx; red[3][w] = gm; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+      for (int k = 0; k < (int)(blockDim.x / WAVE); ++k) {
+        s0 += red[0][k]; s1 += red[1][k]; s2 += red[2][k]; s3 = fmax(s3, red[3][k]);
+      }
+      pa.out4[0] = s0; pa.out4[1] = s1; pa.out4[2] = s2; pa.out4[3] = s3;
+    }
+    return;
+  }
   const int lane = lane_id();
   const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (l >= a.n_lm) return;
@@ -523,76 +601,43 @@ __global__ __launch_bounds__(256) void k_backsub(BacksubArgs a) {
   if (lane == 0) {
     double* red = a.lm_red + (int64_t)l * 4;
     const double th = a.rays[2 * l], ph = a.rays[2 * l + 1];
+    double nth = th, nph = ph;
     if (s1 == s0) {
-      a.rays_trial[2 * l] = th;
-      a.rays_trial[2 * l + 1] = ph;
       red[0] = 0; red[1] = 0; red[2] = 0; red[3] = 0;
-      return;
+    } else {
+      const double* lo = a.lm_out + (int64_t)l * 8;
+      const double* vi = a.lm_aux + (int64_t)l * 8;
+      const double r0 = lo[3] + t0, r1 = lo[4] + t1;
+      const double d0 = -(vi[0] * r0 + vi[1] * r1);
+      const double d1 = -(vi[1] * r0 + vi[2] * r1);
+      nth = th + d0;
+      nph = ph + d1;
+      const double D0 = a.D_ray[2 * l], D1 = a.D_ray[2 * l + 1];
+      const double lam = a.lam_dev ? *a.lam_dev : a.lambda;
+      red[0] = -0.5 * (lo[3] * d0 + lo[4] * d1) + 0.5 * lam * (D0 * d0 * d0 + D1 * d1 * d1);
+      red[1] = d0 * d0 + d1 * d1;
+      red[2] = th * th + ph * ph;
+      red[3] = fmax(fabs(lo[3]), fabs(lo[4]));
     }
-    const double* lo = a.lm_out + (int64_t)l * 8;
-    const double* vi = a.lm_aux + (int64_t)l * 8;
-    const double r0 = lo[3] + t0, r1 = lo[4] + t1;
-    const double d0 = -(vi[0] * r0 + vi[1] * r1);
-    const double d1 = -(vi[1] * r0 + vi[2] * r1);
-    a.rays_trial[2 * l] = th + d0;
-    a.rays_trial[2 * l + 1] = ph + d1;
-    const double D0 = a.D_ray[2 * l], D1 = a.D_ray[2 * l + 1];
-    const double lam = a.lam_dev ? *a.lam_dev : a.lambda;
-    red[0] = -0.5 * (lo[3] * d0 + lo[4] * d1) + 0.5 * lam * (D0 * d0 * d0 + D1 * d1 * d1);
-    red[1] = d0 * d0 + d1 * d1;
-    red[2] = th * th + ph * ph;
-    red[3] = fmax(fabs(lo[3]), fabs(lo[4]));
+    a.rays_trial[2 * l] = nth;
+    a.rays_trial[2 * l + 1] = nph;
+    const RayTab<double> t = make_ray_tab<double>(nth, nph);
+    rt64[l] = t;
+    if constexpr (sizeof(real) != sizeof(double)) {
+      RayTab<real> r;
+      r.p0 = (real)t.p0; r.p1 = (real)t.p1; r.d0t = (real)t.d0t; r.d1t = (real)t.d1t; r.d1p = (real)t.d1p;
+      r.pad0 = r.pad1 = r.pad2 = (real)0;
+      rt[l] = r;
+    }
   }
 }
 
 template <typename real>
-void launch_backsub(const BacksubArgs& a, hipStream_t st) {
-  if (a.n_lm <= 0) return;
-  hipLaunchKernelGGL(k_backsub<real>, dim3((a.n_lm + 3) / 4), dim3(256), 0, st, a);
-}
-
-// pose trial + pose partials (identical on every rank): one block
-__global__ void k_pose_trial(const double* __restrict__ ptz, const double* __restrict__ dpose,
-                             const double* __restrict__ g_pose, const double* __restrict__ D_pose,
-                             const int32_t* __restrict__ frame_pos, double* __restrict__ ptz_trial, int n_pose, int n_fixed,
-                             double lambda_arg, const double* __restrict__ lam_dev, double* __restrict__ out4) {
-  const double lambda = lam_dev ? *lam_dev : lambda_arg;
-  __shared__ double red[4][1024 / WAVE];
-  double pr = 0, dx = 0, xx = 0, gm = 0;
-  for (int i = threadIdx.x; i < 3 * n_pose; i += blockDim.x) {
-    const int f = i / 3;
-    const double x = ptz[i];
-    xx += x * x;
-    if (f < n_fixed) {
-      ptz_trial[i] = x;
-      continue;
-    }
-    const int k = frame_pos[f] + (i - 3 * f);  // system row
-    const double d = dpose[k];
-    ptz_trial[i] = x + d;
-    pr += -0.5 * g_pose[k] * d + 0.5 * lambda * D_pose[i] * d * d;
-    dx += d * d;
-    gm = fmax(gm, fabs(g_pose[k]));
-  }
-  pr = wave_sum(pr); dx = wave_sum(dx); xx = wave_sum(xx);
-  for (int o = 32; o > 0; o >>= 1) gm = fmax(gm, __shfl_xor(gm, o, WAVE));
-  const int w = threadIdx.x >> 6;
-  if (lane_id() == 0) { red[0][w] = pr; red[1][w] = dx; red[2][w] = xx; red[3][w] = gm; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-    for (int k = 0; k < (int)(blockDim.x / WAVE); ++k) {
-      s0 += red[0][k]; s1 += red[1][k]; s2 += red[2][k]; s3 = fmax(s3, red[3][k]);
-    }
-    out4[0] = s0; out4[1] = s1; out4[2] = s2; out4[3] = s3;
-  }
-}
-
-void launch_pose_trial(const double* ptz, const double* dpose, const double* g_pose, const double* D_pose,
-                       const int32_t* frame_pos, double* ptz_trial, int n_pose, int n_fixed, double lambda,
-                       const double* lam_dev, double* out4, hipStream_t st) {
-  hipLaunchKernelGGL(k_pose_trial, dim3(1), dim3(1024), 0, st, ptz, dpose, g_pose, D_pose, frame_pos, ptz_trial,
-                     n_pose, n_fixed, lambda, lam_dev, out4);
+void launch_trial(const BacksubArgs& a, const double* ptz, const double* g_pose, const double* D_pose, double* ptz_trial,
+                  double* out4, int n_pose, void* ft64, void* rt64, void* ft, void* rt, hipStream_t st) {
+  PoseTrialArgs pa{ptz, g_pose, D_pose, ptz_trial, out4, n_pose};
+  hipLaunchKernelGGL(k_trial<real>, dim3((unsigned)((a.n_lm + 3) / 4 + 1)), dim3(256), 0, st, a, pa,
+                     (FrameTab<double>*)ft64, (RayTab<double>*)rt64, (FrameTab<real>*)ft, (RayTab<real>*)rt);
 }
 
 // deterministic strided reduction: out[k] = sum_i src[i*stride + k] (fixed order), k < nk;
@@ -600,9 +645,13 @@ void launch_pose_trial(const double* ptz, const double* dpose, const double* g_p
 // ranges into scratch partials; the last workgroup to finish (agent-scope counter) combines them in
 // block order and re-arms the counter, so the result is bitwise reproducible in one launch.
 constexpr int RED_BLOCKS = 64;
+// (src2, stride2, nk2, out2): an optional second set of columns over the same n rows, reduced in the same
+// launch into out2 (columns nk .. nk + nk2 - 1 of the internal accumulators; nk + nk2 <= 8)
 __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ src, int64_t n, int stride, int nk,
                                                      int maxmask, double* __restrict__ out,
-                                                     double* __restrict__ partial, unsigned* __restrict__ counter) {
+                                                     double* __restrict__ partial, unsigned* __restrict__ counter,
+                                                     const double* __restrict__ src2, int stride2, int nk2,
+                                                     double* __restrict__ out2) {
   __shared__ double red[8][256 / WAVE];
   __shared__ bool last;
   const int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
@@ -613,11 +662,12 @@ __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ 
   for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      if (k >= nk) break;
-      const double x = src[i * stride + k];
+      if (k >= nk + nk2) break;
+      const double x = k < nk ? src[i * stride + k] : src2[i * stride2 + (k - nk)];
       acc[k] = (maxmask & (1 << k)) ? fmax(acc[k], fabs(x)) : acc[k] + x;
     }
   }
+  nk += nk2;  // from here on: all accumulated columns
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     if (k >= nk) break;
@@ -653,7 +703,8 @@ __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ 
     const int k = threadIdx.x;
     double s = 0;
     for (int b = 0; b < (int)gridDim.x; ++b) s = (maxmask & (1 << k)) ? fmax(s, fin[b][k]) : s + fin[b][k];
-    out[k] = s;
+    if (k < nk - nk2) out[k] = s;
+    else out2[k - (nk - nk2)] = s;
   }
   if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -671,10 +722,10 @@ void launch_pack_scalars(const double* scal, const double* loc, const int* info,
 }
 
 void launch_reduce_cols(const double* src, int64_t n, int stride, int nk, int maxmask, double* out, double* scratch,
-                        hipStream_t st) {
+                        hipStream_t st, const double* src2, int stride2, int nk2, double* out2) {
   unsigned* counter = reinterpret_cast<unsigned*>(scratch + RED_BLOCKS * 8);
   hipLaunchKernelGGL(k_reduce_cols, dim3(RED_BLOCKS), dim3(256), 0, st, src, n, stride, nk, maxmask, out, scratch,
-                     counter);
+                     counter, src2, stride2, src2 ? nk2 : 0, out2);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -821,8 +872,10 @@ template void launch_tables<double>(const double*, const double*, int, int, void
                                     hipStream_t);
 template void launch_linearize<float>(const LinArgs&, int, hipStream_t);
 template void launch_linearize<double>(const LinArgs&, int, hipStream_t);
-template void launch_backsub<float>(const BacksubArgs&, hipStream_t);
-template void launch_backsub<double>(const BacksubArgs&, hipStream_t);
+template void launch_trial<float>(const BacksubArgs&, const double*, const double*, const double*, double*, double*, int,
+                                  void*, void*, void*, void*, hipStream_t);
+template void launch_trial<double>(const BacksubArgs&, const double*, const double*, const double*, double*, double*,
+                                   int, void*, void*, void*, void*, hipStream_t);
 template void launch_residual<float>(const int32_t*, const int32_t*, const int32_t*, const double2*, const void*,
                                      const int64_t*, const void*, const void*, double, double, int64_t, double*,
                                      hipStream_t);

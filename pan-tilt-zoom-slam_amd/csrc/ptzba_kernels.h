@@ -94,22 +94,23 @@ void launch_tables(const double* ptz, const double* rays, int n_pose, int n_lm, 
                    const int* run_if, hipStream_t st);
 template <typename real>
 void launch_linearize(const LinArgs& a, int loss, hipStream_t st);
-void launch_landmark_damp(const double* lm_out, const int32_t* lm_seg_begin, double* D_ray, double* lm_aux, int n_lm,
-                          double lambda, const double* lam_dev, const int* skip_if, hipStream_t st);
 template <typename real>
 void launch_schur(const SchurArgs& a, int n_items, int n_groups, int n_fixed, hipStream_t st);
-template <typename real>
-void launch_backsub(const BacksubArgs& a, hipStream_t st);
-void launch_pose_trial(const double* ptz, const double* dpose, const double* g_pose, const double* D_pose,
-                       const int32_t* frame_pos,
-                       double* ptz_trial, int n_pose, int n_fixed, double lambda, const double* lam_dev, double* out4,
-                       hipStream_t st);
 // scratch: RED_SCRATCH doubles (partials + counter), zero-initialised once, reused across calls
 constexpr int RED_SCRATCH = 64 * 8 + 2;
 // scal[8] | loc[8] | info -> one packed device block (read back with a single copy)
 void launch_pack_scalars(const double* scal, const double* loc, const int* info, double* host_dev, hipStream_t st);
 void launch_reduce_cols(const double* src, int64_t n, int stride, int nk, int maxmask, double* out, double* scratch,
-                        hipStream_t st);
+                        hipStream_t st, const double* src2 = nullptr, int stride2 = 0, int nk2 = 0,
+                        double* out2 = nullptr);
+// build prologue (zero pattern tiles + b|g|dU, landmark damping) in one launch
+void launch_build_prologue(double* S, int64_t ld, const int2* zt, int n_tiles, double* vec, int64_t n_vec,
+                           const double* lm_out, const int32_t* lm_seg_begin, double* D_ray, double* lm_aux, int n_lm,
+                           double lambda, const double* lam_dev, const int* skip_if, hipStream_t st);
+// trial state (ray back-substitution + pose trial + the trial's frame / ray tables) in one launch
+template <typename real>
+void launch_trial(const BacksubArgs& a, const double* ptz, const double* g_pose, const double* D_pose, double* ptz_trial,
+                  double* out4, int n_pose, void* ft64, void* rt64, void* ft, void* rt, hipStream_t st);
 template <typename real>
 void launch_residual(const int32_t* rec_seg, const int32_t* seg_frame, const int32_t* seg_lm, const double2* seg_base,
                      const void* rec_xy, const int64_t* perm, const void* ft64, const void* rt64, double u, double v,
