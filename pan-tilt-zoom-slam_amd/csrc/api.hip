@@ -172,6 +172,8 @@ int ptzba_use_own_stream(ptzba_handle h) { return h ? ptzba_set_stream(h, h->own
 template <typename real>
 static int upload_records(ptzba_ctx* h, const std::vector<int64_t>& order, const std::vector<int32_t>& rec_seg,
                           const std::vector<double>& base, const double* obs_xy, const double* w) {
+  // synchronous uploads: the host vectors die at return (the handle's stream does not order itself
+  // behind the legacy null stream, so every upload / memset of set_problem goes on h->st)
   std::vector<real> xy(2 * h->n_rec);
   for (int64_t r = 0; r < h->n_rec; ++r) {
     const int32_t s = rec_seg[r];
@@ -180,22 +182,29 @@ static int upload_records(ptzba_ctx* h, const std::vector<int64_t>& order, const
   }
   // padded by 4 records: K1's coarsened loads read whole 4-record groups
   if (h->rec_xy.alloc((xy.size() + 8) * sizeof(real))) return -1;
-  HIPCHK(hipMemcpy(h->rec_xy.p, xy.data(), xy.size() * sizeof(real), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpyAsync(h->rec_xy.p, xy.data(), xy.size() * sizeof(real), hipMemcpyHostToDevice, h->st));
+  HIPCHK(hipMemsetAsync(reinterpret_cast<real*>(h->rec_xy.p) + xy.size(), 0, 8 * sizeof(real), h->st));
   if (w) {
     std::vector<real> ww(h->n_rec);
     for (int64_t r = 0; r < h->n_rec; ++r) ww[r] = (real)w[order[r]];
     if (h->rec_w.alloc(ww.size() * sizeof(real))) return -1;
-    HIPCHK(hipMemcpy(h->rec_w.p, ww.data(), ww.size() * sizeof(real), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpyAsync(h->rec_w.p, ww.data(), ww.size() * sizeof(real), hipMemcpyHostToDevice, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
   } else {
     h->rec_w.release();
   }
+  HIPCHK(hipStreamSynchronize(h->st));
   return 0;
 }
 
+// blocking upload on stream st (nullptr: the null stream); returns after the copy has landed
 template <typename T>
-static int upload(DBuf& b, const std::vector<T>& v) {
+static int upload(DBuf& b, const std::vector<T>& v, hipStream_t st = nullptr) {
   if (b.alloc(v.size() * sizeof(T))) return -1;
-  if (!v.empty()) HIPCHK(hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  if (!v.empty()) {
+    HIPCHK(hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
   return 0;
 }
 
@@ -668,21 +677,21 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   int rc = h->precision == PTZBA_FP32 ? upload_records<float>(h, order, rec_seg, seg_base, obs_xy, obs_weight)
                                       : upload_records<double>(h, order, rec_seg, seg_base, obs_xy, obs_weight);
   if (rc) return rc;
-  if (upload(h->seg_base, seg_base)) return -1;
+  if (upload(h->seg_base, seg_base, h->st)) return -1;
   {  // K1's 1-byte segment key: the record's segment within its landmark's window of K1_SEGW segments
     std::vector<uint8_t> key(n_obs + 4);  // + 4: K1 reads whole 4-record key groups
     for (int64_t k = 0; k < n_obs; ++k) {
       const int32_t sg = rec_seg[k];
       key[k] = (uint8_t)((sg - lm_seg_begin[seg_lm[sg]]) % K1_SEGW);
     }
-    if (upload(h->rec_key, key)) return -1;
+    if (upload(h->rec_key, key, h->st)) return -1;
   }
-  if (upload(h->rec_seg, rec_seg) || upload(h->seg_frame, seg_frame) || upload(h->seg_lm, seg_lm) ||
-      upload(h->seg_rec_begin, seg_rec_begin) || upload(h->lm_seg_begin, lm_seg_begin) ||
-      upload(h->lm_order, lm_work) || upload(h->frame_seg_begin, frame_seg_begin) ||
-      upload(h->frame_seg_list, frame_seg_list) || upload(h->frame_win_hi, frame_win_hi) ||
-      upload(h->s2_items, s2_items) || upload(h->s2_groups, s2_groups) || upload(h->s2_lm, s2_lm) ||
-      upload(h->lm_meta, lm_meta))
+  if (upload(h->rec_seg, rec_seg, h->st) || upload(h->seg_frame, seg_frame, h->st) || upload(h->seg_lm, seg_lm, h->st) ||
+      upload(h->seg_rec_begin, seg_rec_begin, h->st) || upload(h->lm_seg_begin, lm_seg_begin, h->st) ||
+      upload(h->lm_order, lm_work, h->st) || upload(h->frame_seg_begin, frame_seg_begin, h->st) ||
+      upload(h->frame_seg_list, frame_seg_list, h->st) || upload(h->frame_win_hi, frame_win_hi, h->st) ||
+      upload(h->s2_items, s2_items, h->st) || upload(h->s2_groups, s2_groups, h->st) || upload(h->s2_lm, s2_lm, h->st) ||
+      upload(h->lm_meta, lm_meta, h->st))
     return -1;
   const size_t e = h->elem();
   if (h->ptz.alloc(3 * n_pose * 8) || h->ptz_trial.alloc(3 * n_pose * 8) || h->rays.alloc(2 * (size_t)n_landmark * 8) ||
@@ -700,14 +709,14 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       h->s2_part.alloc((size_t)std::max(h->n_s2_items, 1) * SCHUR_F1 * 9 * WAVE * 8) ||
       h->part_diag.alloc((size_t)std::max(h->n_s2_items, 1) * SCHUR_F1 * 12 * 8))
     return -1;
-  if (upload(h->chol_tasks, plan.tasks) || upload(h->frame_pos, sorder.pos) || upload(h->row_pad, sorder.pad) ||
-      upload(h->bs_chain_off, plan.chain_off) || upload(h->bs_chain_cols, plan.chain_cols) ||
-      upload(h->bs_upd_off, plan.upd_off) || upload(h->bs_upd_tiles, plan.upd_tiles) || upload(h->xtiles, plan.xtiles) || upload(h->ztiles, plan.ztiles) ||
-      upload(h->bs_la_tasks, plan.la_tasks) || upload(h->bs_lo_off, plan.lo_off) || upload(h->bs_lo_tiles, plan.lo_tiles))
+  if (upload(h->chol_tasks, plan.tasks, h->st) || upload(h->frame_pos, sorder.pos, h->st) || upload(h->row_pad, sorder.pad, h->st) ||
+      upload(h->bs_chain_off, plan.chain_off, h->st) || upload(h->bs_chain_cols, plan.chain_cols, h->st) ||
+      upload(h->bs_upd_off, plan.upd_off, h->st) || upload(h->bs_upd_tiles, plan.upd_tiles, h->st) || upload(h->xtiles, plan.xtiles, h->st) || upload(h->ztiles, plan.ztiles, h->st) ||
+      upload(h->bs_la_tasks, plan.la_tasks, h->st) || upload(h->bs_lo_off, plan.lo_off, h->st) || upload(h->bs_lo_tiles, plan.lo_tiles, h->st))
     return -1;
   h->n_xtiles = (int)(plan.xtiles.size() / 2);
   h->n_ztiles = (int)(plan.ztiles.size() / 2);
-  HIPCHK(hipMemset(h->sys.p, 0, h->sys.bytes));  // outside the factor's tiles it is never written
+  HIPCHK(hipMemsetAsync(h->sys.p, 0, h->sys.bytes, h->st));  // outside the factor's tiles it is never written
   h->bs_nupd = (int)plan.upd_tiles.size();
   h->bs_npos = (int)plan.chain_cols.size();
   h->bs_ntasks = plan.n_tasks;
@@ -718,23 +727,24 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->bs_ll = h->ld * 8 + (std::max(h->bs_npos + 1 + h->bs_nupd, 2 * h->bs_npos + h->bs_ntasks)) * 4 > 100 * 1024;
   if (const char* e = getenv("PTZBA_BACKSOLVE")) h->bs_ll = h->bs_ll || std::string(e) == "ll";  // testing knob
   h->xbuf.release();  // allocated on first ptzba_exchange_packed
-  HIPCHK(hipMemset(h->D_pose.p, 0, h->D_pose.bytes));
-  HIPCHK(hipMemset(h->D_ray.p, 0, h->D_ray.bytes));
-  HIPCHK(hipMemset(h->w_slot[0].p, 0, h->w_slot[0].bytes));  // slots of unobserved frames stay zero
-  HIPCHK(hipMemset(h->w_slot[1].p, 0, h->w_slot[1].bytes));
-  HIPCHK(hipMemset(h->lm_out[0].p, 0, h->lm_out[0].bytes));  // landmarks without records keep zero rows
-  HIPCHK(hipMemset(h->lm_out[1].p, 0, h->lm_out[1].bytes));
-  HIPCHK(hipMemset(h->ug_slot[0].p, 0, h->ug_slot[0].bytes));
-  HIPCHK(hipMemset(h->ug_slot[1].p, 0, h->ug_slot[1].bytes));
-  HIPCHK(hipMemset(h->ptz.p, 0, h->ptz.bytes));
-  HIPCHK(hipMemset(h->rays.p, 0, h->rays.bytes));
-  HIPCHK(hipMemset(h->scal.p, 0, h->scal.bytes));
-  HIPCHK(hipMemset(h->red_scratch.p, 0, h->red_scratch.bytes));
+  HIPCHK(hipMemsetAsync(h->D_pose.p, 0, h->D_pose.bytes, h->st));
+  HIPCHK(hipMemsetAsync(h->D_ray.p, 0, h->D_ray.bytes, h->st));
+  HIPCHK(hipMemsetAsync(h->w_slot[0].p, 0, h->w_slot[0].bytes, h->st));  // slots of unobserved frames stay zero
+  HIPCHK(hipMemsetAsync(h->w_slot[1].p, 0, h->w_slot[1].bytes, h->st));
+  HIPCHK(hipMemsetAsync(h->lm_out[0].p, 0, h->lm_out[0].bytes, h->st));  // landmarks without records keep zero rows
+  HIPCHK(hipMemsetAsync(h->lm_out[1].p, 0, h->lm_out[1].bytes, h->st));
+  HIPCHK(hipMemsetAsync(h->ug_slot[0].p, 0, h->ug_slot[0].bytes, h->st));
+  HIPCHK(hipMemsetAsync(h->ug_slot[1].p, 0, h->ug_slot[1].bytes, h->st));
+  HIPCHK(hipMemsetAsync(h->ptz.p, 0, h->ptz.bytes, h->st));
+  HIPCHK(hipMemsetAsync(h->rays.p, 0, h->rays.bytes, h->st));
+  HIPCHK(hipMemsetAsync(h->scal.p, 0, h->scal.bytes, h->st));
+  HIPCHK(hipMemsetAsync(h->red_scratch.p, 0, h->red_scratch.bytes, h->st));
   if (!h->scal_host) HIPCHK(hipHostMalloc((void**)&h->scal_host, 24 * sizeof(double), hipHostMallocDefault));
   if (!h->scal_pack.p && h->scal_pack.alloc(24 * sizeof(double))) return -1;
-  HIPCHK(hipMemset(h->loc.p, 0, h->loc.bytes));
+  HIPCHK(hipMemsetAsync(h->loc.p, 0, h->loc.bytes, h->st));
   h->cur = 0;
   h->lambda = 0;
+  HIPCHK(hipStreamSynchronize(h->st));  // every initialisation above has landed before the handle is used
   h->have_problem = true;
   return 0;
 }
@@ -769,7 +779,9 @@ static void tables(ptzba_ctx* h, const double* ptz, const double* rays, const in
     launch_tables<double>(ptz, rays, h->n_pose, h->n_lm, h->ft64.p, h->rt64.p, h->ft64.p, h->rt64.p, run_if, h->st);
 }
 
-static void linearize_into(ptzba_ctx* h, int slot, const int* run_if = nullptr) {
+// sel != nullptr (device-driven LM): the kernel writes slot (*sel ^ sel_xor), chosen on the device
+static void linearize_into(ptzba_ctx* h, int slot, const int* run_if = nullptr, const int* sel = nullptr,
+                           int sel_xor = 0) {
   LinArgs a;
   a.lm_work = h->lm_order.as<int4>();
   a.n_work = h->n_work;
@@ -794,6 +806,16 @@ static void linearize_into(ptzba_ctx* h, int slot, const int* run_if = nullptr) 
   a.lm_meta = h->lm_meta.as<int4>();
   a.lm_out = h->lm_out[slot].as<double>();
   a.run_if = run_if;
+  a.sel = sel;
+  a.sel_xor = sel_xor;
+  if (sel) {
+    a.ug_slot = h->ug_slot[0].p;
+    a.w_slot = h->w_slot[0].p;
+    a.lm_out = h->lm_out[0].as<double>();
+  }
+  a.ug_slot1 = h->ug_slot[1].p;
+  a.w_slot1 = h->w_slot[1].p;
+  a.lm_out1 = h->lm_out[1].as<double>();
   if (!run_if) tm_begin(h, TM_K1);  // conditional re-linearisations are not timed (often no-ops)
   if (h->precision == PTZBA_FP32)
     launch_linearize<float>(a, h->loss, h->st);
@@ -819,7 +841,7 @@ int ptzba_residual(ptzba_handle h, const double* x_full, double* r_out) {
   if (!h || !h->have_problem) return fail("no problem set");
   HIPCHK(hipSetDevice(h->device));
   if (!h->perm_uploaded) {
-    if (upload(h->perm, h->perm_host)) return -1;
+    if (upload(h->perm, h->perm_host, h->st)) return -1;
     h->perm_uploaded = true;
   }
   DBuf x, r;
@@ -896,13 +918,15 @@ int ptzba_linearize(ptzba_handle h) {
   return 0;
 }
 
-// reduced camera system at the current linearisation (slot h->cur); lambda from the argument or, in
-// the device-driven LM (lam_dev != nullptr), from device memory
-static int build_impl(ptzba_ctx* h, double lambda, const double* lam_dev, const int* skip_if = nullptr) {
-  const int c = h->cur;
+// reduced camera system at the current linearisation (slot h->cur, or in the device-driven LM slot *sel);
+// lambda from the argument or, in the device-driven LM (lam_dev != nullptr), from device memory
+static int build_impl(ptzba_ctx* h, double lambda, const double* lam_dev, const int* skip_if = nullptr,
+                      const int* sel = nullptr) {
+  const int c = sel ? 0 : h->cur;
   launch_build_prologue(h->S(), h->ld, h->ztiles.as<int2>(), h->n_ztiles, h->bvec(), 3 * h->ld,
                         h->lm_out[c].as<double>(), h->lm_seg_begin.as<int32_t>(), h->D_ray.as<double>(),
-                        h->lm_aux.as<double>(), h->n_lm, lambda, lam_dev, skip_if, h->st);
+                        h->lm_aux.as<double>(), h->n_lm, lambda, lam_dev, skip_if, h->st, h->lm_out[1].as<double>(),
+                        sel);
   SchurArgs a;
   a.items = h->s2_items.as<int4>();
   a.groups = h->s2_groups.as<int4>();
@@ -921,6 +945,9 @@ static int build_impl(ptzba_ctx* h, double lambda, const double* lam_dev, const 
   a.ld = h->ld;
   a.n_pose = h->n_pose;
   a.skip_if = skip_if;
+  a.ug_slot1 = h->ug_slot[1].p;
+  a.w_slot1 = h->w_slot[1].p;
+  a.sel = sel;
   tm_begin(h, TM_SCHUR);
   if (h->precision == PTZBA_FP32)
     launch_schur<float>(a, h->n_s2_items, h->n_s2_groups, h->n_fixed, h->st);
@@ -939,9 +966,11 @@ int ptzba_build_reduced(ptzba_handle h, double lambda) {
   return build_impl(h, lambda, nullptr);
 }
 
-// damped solve, trial state, trial linearisation into slot `nx` and the trial scalars
-static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx) {
-  const int c = h->cur;
+// damped solve, trial state, trial linearisation into slot `nx` and the trial scalars (device-driven LM:
+// current slot *sel, trial slot *sel ^ 1, chosen on the device)
+static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* sel = nullptr) {
+  const int c = sel ? 0 : h->cur;
+  if (sel) nx = 1;  // the trial's slot, with the other slot as the selector's alternative
   tm_begin(h, TM_CHOL);
   launch_chol_prepare_damped(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(),
                              h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
@@ -973,6 +1002,9 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx) {
   b.n_fixed = h->n_fixed;
   b.lambda = h->lambda;
   b.lam_dev = lam_dev;
+  b.w_slot1 = h->w_slot[1].p;
+  b.lm_out1 = h->lm_out[1].as<double>();
+  b.sel = sel;
   // ray back-substitution, trial poses and the trial's frame / ray tables: one launch
   if (h->precision == PTZBA_FP32)
     launch_trial<float>(b, h->ptz.as<double>(), h->gpose(), h->D_pose.as<double>(), h->ptz_trial.as<double>(),
@@ -982,10 +1014,11 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx) {
                          h->loc.as<double>(), h->n_pose, h->ft64.p, h->rt64.p, h->ft64.p, h->rt64.p, h->st);
   tm_end(h, TM_BACK);
   // trial linearisation (its cost decides acceptance; kept as the next linearisation if accepted)
-  linearize_into(h, nx);
+  linearize_into(h, nx, nullptr, sel, 1);
   // scal[1] (trial cost) and scal[2..4] are overwritten below, loc[0..3] by the trial kernel: no memsets
-  launch_reduce_cols(h->lm_out[nx].as<double>() + 5, h->n_lm, 8, 1, 0, h->scal.as<double>() + 1,
-                     h->red_scratch.as<double>(), h->st, h->lm_red.as<double>(), 4, 3, h->scal.as<double>() + 2);
+  launch_reduce_cols(h->lm_out[sel ? 0 : nx].as<double>() + 5, h->n_lm, 8, 1, 0, h->scal.as<double>() + 1,
+                     h->red_scratch.as<double>(), h->st, h->lm_red.as<double>(), 4, 3, h->scal.as<double>() + 2,
+                     h->lm_out[1].as<double>() + 5, sel, 1);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -998,8 +1031,9 @@ int ptzba_solve_reduced(ptzba_handle h) {
 
 // ------------------------------------------------------------------------------------------------
 // device-driven Levenberg-Marquardt (the decisions of ptzba.LMSolver on the device): the host only
-// enqueues trials and polls a pinned record ring, so no trial waits for a host round trip.  A single
-// linearisation slot: the trial linearises into it, a rejected trial re-linearises the current point.
+// enqueues trials and polls a pinned record ring, so no trial waits for a host round trip.  The two
+// linearisation slots are selected on the device (LMDev::cur): a trial linearises into the other slot, an
+// accepted trial flips cur, a rejected one leaves the current linearisation in place (no re-linearisation).
 // ------------------------------------------------------------------------------------------------
 static int lm_check(ptzba_ctx* h) {
   if (!h || !h->have_problem) return fail("no problem set");
@@ -1028,7 +1062,7 @@ int ptzba_lm_init(ptzba_handle h, const ptzba_lm_opts* o) {
              o->gauss_newton ? 1 : 0, 0};
   // no decision of an earlier run is in flight (its lm_wait returned): clear the ring's sequence tags
   for (int k = 0; k < LM_RING; ++k) __atomic_store_n(&h->lm_host[k].seq, 0, __ATOMIC_RELAXED);
-  launch_lm_init(h->lmdev.as<LMDev>(), h->scal.as<double>(), p, h->st);
+  launch_lm_init(h->lmdev.as<LMDev>(), h->scal.as<double>(), p, h->cur, h->st);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1037,13 +1071,13 @@ int ptzba_lm_build(ptzba_handle h) {
   if (lm_check(h)) return -1;
   HIPCHK(hipSetDevice(h->device));
   // a build queued after the final decision (the host pipelines one trial ahead) exits at once
-  return build_impl(h, 0.0, &h->lmdev.as<LMDev>()->lam, &h->lmdev.as<LMDev>()->done);
+  return build_impl(h, 0.0, &h->lmdev.as<LMDev>()->lam, &h->lmdev.as<LMDev>()->done, &h->lmdev.as<LMDev>()->cur);
 }
 
 int ptzba_lm_solve(ptzba_handle h) {
   if (lm_check(h)) return -1;
   HIPCHK(hipSetDevice(h->device));
-  return solve_impl(h, &h->lmdev.as<LMDev>()->lam, h->cur);
+  return solve_impl(h, &h->lmdev.as<LMDev>()->lam, 1 - h->cur, &h->lmdev.as<LMDev>()->cur);
 }
 
 int ptzba_lm_decide(ptzba_handle h, int trial) {
@@ -1057,9 +1091,6 @@ int ptzba_lm_decide(ptzba_handle h, int trial) {
                    h->st);
   launch_lm_commit(st, h->ptz.as<double>(), h->ptz_trial.as<double>(), 3 * h->n_pose, h->rays.as<double>(),
                    h->rays_trial.as<double>(), 2 * (int64_t)h->n_lm, h->st);
-  // rejected: the trial overwrote the linearisation slot -> rebuild it at the current point
-  tables(h, h->ptz.as<double>(), h->rays.as<double>(), &st->relin);
-  linearize_into(h, h->cur, &st->relin);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1091,6 +1122,7 @@ int ptzba_lm_wait(ptzba_handle h, int trial, ptzba_lm_record* out) {
   out->status = r.status;
   out->done = r.done;
   out->accepted = r.accepted;
+  h->cur = r.cur;  // the host's view of the current slot follows the device (ptzba_accept / linearize)
   return 0;
 }
 

@@ -149,8 +149,9 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
   const double2* __restrict__ seg_base = a.seg_base;
   const real* __restrict__ rec_xy = (const real*)a.rec_xy;
   const real* __restrict__ rec_w = (const real*)a.rec_w;
-  real* __restrict__ ug_slot = (real*)a.ug_slot;
-  real* __restrict__ w_slot = (real*)a.w_slot;
+  const bool alt = a.sel && ((*a.sel ^ a.sel_xor) & 1);  // device-chosen linearisation slot
+  real* __restrict__ ug_slot = (real*)(alt ? a.ug_slot1 : a.ug_slot);
+  real* __restrict__ w_slot = (real*)(alt ? a.w_slot1 : a.w_slot);
   const int4 lmeta = a.lm_meta[l];  // {first frame, last frame, slot offset, 0}
   const int64_t slot0 = (int64_t)lmeta.z - lmeta.x;
   const real u = (real)a.u, v = (real)a.v;
@@ -430,7 +431,7 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
   V00 = wave_sum(V00); V01 = wave_sum(V01); V11 = wave_sum(V11);
   g0 = wave_sum(g0); g1 = wave_sum(g1); cost = wave_sum(cost);
   if (lane == 0) {
-    double* o = a.lm_out + (int64_t)l * 8;
+    double* o = (alt ? a.lm_out1 : a.lm_out) + (int64_t)l * 8;
     o[0] = V00; o[1] = V01; o[2] = V11; o[3] = g0; o[4] = g1; o[5] = 0.5 * cost; o[6] = 0; o[7] = 0;
   }
 }
@@ -462,7 +463,8 @@ __global__ __launch_bounds__(256) void k_build_prologue(double* __restrict__ S, 
                                                         const int32_t* __restrict__ lm_seg_begin,
                                                         double* __restrict__ D_ray, double* __restrict__ lm_aux, int n_lm,
                                                         double lambda_arg, const double* __restrict__ lam_dev,
-                                                        const int* __restrict__ skip_if) {
+                                                        const int* __restrict__ skip_if,
+                                                        const double* __restrict__ lm_out1, const int* __restrict__ sel) {
   const int b = blockIdx.x;
   if (b < n_tiles) {
     const int2 tij = zt[b];
@@ -484,7 +486,7 @@ __global__ __launch_bounds__(256) void k_build_prologue(double* __restrict__ S, 
     for (int k = 0; k < 8; ++k) o[k] = 0;
     return;
   }
-  const double* in = lm_out + (int64_t)l * 8;
+  const double* in = ((sel && *sel) ? lm_out1 : lm_out) + (int64_t)l * 8;
   double d0 = fmax(D_ray[2 * l], fmax(in[0], 1e-12));
   double d1 = fmax(D_ray[2 * l + 1], fmax(in[2], 1e-12));
   D_ray[2 * l] = d0;
@@ -504,10 +506,11 @@ __global__ __launch_bounds__(256) void k_build_prologue(double* __restrict__ S, 
 
 void launch_build_prologue(double* S, int64_t ld, const int2* zt, int n_tiles, double* vec, int64_t n_vec,
                            const double* lm_out, const int32_t* lm_seg_begin, double* D_ray, double* lm_aux, int n_lm,
-                           double lambda, const double* lam_dev, const int* skip_if, hipStream_t st) {
+                           double lambda, const double* lam_dev, const int* skip_if, hipStream_t st,
+                           const double* lm_out1, const int* sel) {
   const unsigned nb = (unsigned)(n_tiles + 1 + (n_lm + 255) / 256);
   hipLaunchKernelGGL(k_build_prologue, dim3(nb), dim3(256), 0, st, S, ld, zt, n_tiles, vec, n_vec, lm_out, lm_seg_begin,
-                     D_ray, lm_aux, n_lm, lambda, lam_dev, skip_if);
+                     D_ray, lm_aux, n_lm, lambda, lam_dev, skip_if, lm_out1, sel);
 }
 
 // (pose damping of the exchanged reduced system: k_chol_prepare, chol_kernels.hip)
@@ -582,7 +585,8 @@ __global__ __launch_bounds__(256) void k_trial(BacksubArgs a, PoseTrialArgs pa, 
   const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (l >= a.n_lm) return;
   const int s0 = a.lm_seg_begin[l], s1 = a.lm_seg_begin[l + 1];
-  const real* __restrict__ w_slot = (const real*)a.w_slot;
+  const bool alt = a.sel && *a.sel;  // device-chosen linearisation slot
+  const real* __restrict__ w_slot = (const real*)(alt ? a.w_slot1 : a.w_slot);
   const int4 lmeta = a.lm_meta[l];
   double t0 = 0, t1 = 0;
   for (int s = s0 + lane; s < s1; s += WAVE) {
@@ -605,7 +609,7 @@ __global__ __launch_bounds__(256) void k_trial(BacksubArgs a, PoseTrialArgs pa, 
     if (s1 == s0) {
       red[0] = 0; red[1] = 0; red[2] = 0; red[3] = 0;
     } else {
-      const double* lo = a.lm_out + (int64_t)l * 8;
+      const double* lo = (alt ? a.lm_out1 : a.lm_out) + (int64_t)l * 8;
       const double* vi = a.lm_aux + (int64_t)l * 8;
       const double r0 = lo[3] + t0, r1 = lo[4] + t1;
       const double d0 = -(vi[0] * r0 + vi[1] * r1);
@@ -651,7 +655,9 @@ __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ 
                                                      int maxmask, double* __restrict__ out,
                                                      double* __restrict__ partial, unsigned* __restrict__ counter,
                                                      const double* __restrict__ src2, int stride2, int nk2,
-                                                     double* __restrict__ out2) {
+                                                     double* __restrict__ out2, const double* __restrict__ src1,
+                                                     const int* __restrict__ sel, int sel_xor) {
+  if (sel && ((*sel ^ sel_xor) & 1)) src = src1;
   __shared__ double red[8][256 / WAVE];
   __shared__ bool last;
   const int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
@@ -722,10 +728,11 @@ void launch_pack_scalars(const double* scal, const double* loc, const int* info,
 }
 
 void launch_reduce_cols(const double* src, int64_t n, int stride, int nk, int maxmask, double* out, double* scratch,
-                        hipStream_t st, const double* src2, int stride2, int nk2, double* out2) {
+                        hipStream_t st, const double* src2, int stride2, int nk2, double* out2, const double* src1,
+                        const int* sel, int sel_xor) {
   unsigned* counter = reinterpret_cast<unsigned*>(scratch + RED_BLOCKS * 8);
   hipLaunchKernelGGL(k_reduce_cols, dim3(RED_BLOCKS), dim3(256), 0, st, src, n, stride, nk, maxmask, out, scratch,
-                     counter, src2, stride2, src2 ? nk2 : 0, out2);
+                     counter, src2, stride2, src2 ? nk2 : 0, out2, src1, sel, sel_xor);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -763,8 +770,9 @@ void launch_residual(const int32_t* rec_seg, const int32_t* seg_frame, const int
 // device-resident Levenberg-Marquardt control (the decision logic of ptzba.LMSolver, which follows
 // scipy's trf acceptance / termination rules, common.py:705-718): one thread per call.
 // ------------------------------------------------------------------------------------------------
-__global__ void k_lm_init(LMDev* st, const double* __restrict__ scal, LMParams p) {
+__global__ void k_lm_init(LMDev* st, const double* __restrict__ scal, LMParams p, int cur0) {
   st->p = p;
+  st->cur = cur0;
   st->cost = scal[0];
   st->initial_cost = scal[0];
   st->lam = p.lambda0;
@@ -796,6 +804,7 @@ __global__ void k_lm_decide(LMDev* st, const double* __restrict__ scal, const do
     const bool gn0 = p.gauss_newton && s.lam == 0.0;
     if (ok && (rho > 0 || (gn0 && actual >= 0))) {
       s.accepted = 1;
+      s.cur ^= 1;  // the trial's linearisation (other slot) becomes current
       if (!gn0) {
         const double t = 2.0 * rho - 1.0;
         s.lam = fmax(p.min_lambda, s.lam * fmax(1.0 / 3.0, 1.0 - t * t * t));
@@ -830,9 +839,7 @@ __global__ void k_lm_decide(LMDev* st, const double* __restrict__ scal, const do
       } else if (s.retries >= p.max_retries) {
         s.status = -1;
         s.done = 1;
-      } else {
-        s.relin = 1;  // the trial overwrote the linearisation: rebuild it at the current point
-      }
+      }  // rejected: the current linearisation is intact in its slot (the trial wrote the other one)
     }
   }
   *st = s;
@@ -853,8 +860,8 @@ __global__ void k_lm_commit(const LMDev* __restrict__ st, double* __restrict__ p
   }
 }
 
-void launch_lm_init(LMDev* st, const double* scal, const LMParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(1), 0, s, st, scal, p);
+void launch_lm_init(LMDev* st, const double* scal, const LMParams& p, int cur0, hipStream_t s) {
+  hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(1), 0, s, st, scal, p, cur0);
 }
 void launch_lm_decide(LMDev* st, const double* scal, const double* loc, const int* info, LMDev* rec, int seq,
                       hipStream_t s) {

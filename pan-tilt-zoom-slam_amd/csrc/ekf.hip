@@ -245,7 +245,8 @@ static int build_partial_plan(ptzekf_ctx* h, int64_t ld, int mp) {
   h->task_off[Tm + 1] = (int)tasks.size();
   h->n_launch = Tm + 1;
   if (h->tasks.reserve(tasks.size() * sizeof(int4) + 16)) return -1;
-  HIPCHK(hipMemcpy(h->tasks.p, tasks.data(), tasks.size() * sizeof(int4), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpyAsync(h->tasks.p, tasks.data(), tasks.size() * sizeof(int4), hipMemcpyHostToDevice, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));  // ordered before the factorisation launches on h->st
   h->plan_ld = ld;
   h->plan_mp = mp;
   return 0;
@@ -287,8 +288,9 @@ int ptzekf_set_state(ptzekf_handle h, int32_t n_ray, const double* rays, const d
   const int64_t ns = 3 + 2 * (int64_t)n_ray;
   h->cur = 0;
   if (h->rays[0].reserve((size_t)n_ray * 16 + 16) || h->cov[0].reserve((size_t)(ns * ns) * 8)) return -1;
-  if (n_ray) HIPCHK(hipMemcpy(h->rays[0].p, rays, (size_t)n_ray * 16, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->cov[0].p, cov, (size_t)(ns * ns) * 8, hipMemcpyHostToDevice));
+  if (n_ray) HIPCHK(hipMemcpyAsync(h->rays[0].p, rays, (size_t)n_ray * 16, hipMemcpyHostToDevice, h->st));
+  HIPCHK(hipMemcpyAsync(h->cov[0].p, cov, (size_t)(ns * ns) * 8, hipMemcpyHostToDevice, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
   h->n_ray = n_ray;
   return 0;
 }

@@ -27,6 +27,13 @@ struct LinArgs {
   void* w_slot;                  // [n_slot][8] real: W (6) | 0 0 at slot toff_l + frame - first_l
   const int4* lm_meta;           // [n_lm] {first frame, last frame, slot offset, 0}
   double* lm_out;                // [n_lm][8]
+  // device-driven LM: the linearisation slot is chosen on the device -- with sel != nullptr the kernel writes
+  // slot ((*sel) ^ sel_xor): 0 = ug_slot / w_slot / lm_out above, 1 = the *1 buffers
+  void* ug_slot1;
+  void* w_slot1;
+  double* lm_out1;
+  const int* sel;
+  int sel_xor;
 };
 
 // K2 tiles: block of SCHUR_F1 consecutive free frames x chunk of 64 partner frames; work items are
@@ -51,6 +58,9 @@ struct SchurArgs {
   int64_t ld;
   int n_pose;
   const int* skip_if;             // nullptr, or: exit at once when *skip_if != 0 (device-driven LM)
+  const void* ug_slot1;           // sel != nullptr: read slot *sel (1 = these buffers), see LinArgs
+  const void* w_slot1;
+  const int* sel;
 };
 
 struct BacksubArgs {
@@ -70,6 +80,9 @@ struct BacksubArgs {
   int n_fixed;
   double lambda;
   const double* lam_dev;  // nullptr, or lambda read from device memory (device-driven LM)
+  const void* w_slot1;    // sel != nullptr: read slot *sel (1 = these buffers), see LinArgs
+  const double* lm_out1;
+  const int* sel;
 };
 
 // device-driven Levenberg-Marquardt state (ptzba_lm_*): parameters, running state, last decision
@@ -81,9 +94,10 @@ struct LMDev {
   LMParams p;
   double cost, initial_cost, lam, nu, last_actual, last_rho;
   int it, nfev, trials, retries, status, done, accepted, relin;
-  int seq, pad2;  // host ring record: written last (after a system-scope fence) = trial index + 1
+  int seq;  // host ring record: written last (after a system-scope fence) = trial index + 1
+  int cur;  // current linearisation slot (flips on an accepted trial: the trial linearised into the other)
 };
-void launch_lm_init(LMDev* st, const double* scal, const LMParams& p, hipStream_t s);
+void launch_lm_init(LMDev* st, const double* scal, const LMParams& p, int cur0, hipStream_t s);
 void launch_lm_decide(LMDev* st, const double* scal, const double* loc, const int* info, LMDev* rec, int seq,
                       hipStream_t s);
 void launch_lm_commit(const LMDev* st, double* ptz, const double* ptz_trial, int n3, double* rays,
@@ -100,13 +114,16 @@ void launch_schur(const SchurArgs& a, int n_items, int n_groups, int n_fixed, hi
 constexpr int RED_SCRATCH = 64 * 8 + 2;
 // scal[8] | loc[8] | info -> one packed device block (read back with a single copy)
 void launch_pack_scalars(const double* scal, const double* loc, const int* info, double* host_dev, hipStream_t st);
+// src1 / sel / sel_xor: with sel != nullptr the first source is src when ((*sel) ^ sel_xor) == 0, else src1
 void launch_reduce_cols(const double* src, int64_t n, int stride, int nk, int maxmask, double* out, double* scratch,
                         hipStream_t st, const double* src2 = nullptr, int stride2 = 0, int nk2 = 0,
-                        double* out2 = nullptr);
+                        double* out2 = nullptr, const double* src1 = nullptr, const int* sel = nullptr,
+                        int sel_xor = 0);
 // build prologue (zero pattern tiles + b|g|dU, landmark damping) in one launch
 void launch_build_prologue(double* S, int64_t ld, const int2* zt, int n_tiles, double* vec, int64_t n_vec,
                            const double* lm_out, const int32_t* lm_seg_begin, double* D_ray, double* lm_aux, int n_lm,
-                           double lambda, const double* lam_dev, const int* skip_if, hipStream_t st);
+                           double lambda, const double* lam_dev, const int* skip_if, hipStream_t st,
+                           const double* lm_out1 = nullptr, const int* sel = nullptr);
 // trial state (ray back-substitution + pose trial + the trial's frame / ray tables) in one launch
 template <typename real>
 void launch_trial(const BacksubArgs& a, const double* ptz, const double* g_pose, const double* D_pose, double* ptz_trial,

@@ -105,7 +105,8 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
   const int f1b = it.x, chunk = it.y, lb = it.z, nl = it.w - it.z;
   const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
   const int f2base = f1b + WAVE * chunk;
-  const real* __restrict__ w_slot = (const real*)a.w_slot;
+  const bool alt = a.sel && *a.sel;  // device-chosen linearisation slot
+  const real* __restrict__ w_slot = (const real*)(alt ? a.w_slot1 : a.w_slot);
   for (int k = t; k < nl; k += 512) sL[k] = a.item_lm[lb + k];
   __syncthreads();
   SK_T(1);
@@ -113,7 +114,7 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
   if (chunk == 0) {
     // diagonal terms of the F1 frames over this split's landmarks: U, g_pose and W V~^-1 g, read from
     // the dense slots (thread = (landmark j0 + 16 k, frame i): consecutive threads, consecutive slots)
-    const real* __restrict__ ug_slot = (const real*)a.ug_slot;
+    const real* __restrict__ ug_slot = (const real*)(alt ? a.ug_slot1 : a.ug_slot);
     const int i = t & (SF - 1), f = f1b + i;
     double acc[12];
 #pragma unroll
