@@ -219,10 +219,6 @@ PTZBA_EXPORT int ptz_refine_poses(int device, int32_t n_hyp, double* ptz_inout, 
                                   int32_t* status_out);
 
 /* ---------------- host bookkeeping (native) ---------------- */
-/* First-seen landmark ids over ordered pair match lists (image_process.py:611-639).
- * pair_i/pair_j/pair_count: n_pairs; idx_a/idx_b: concatenated match keypoint indices.
- * kp_count[n_frames]: keypoints per frame.  Output landmark id per match (of the src keypoint) and
- * the landmark count; *n_inconsistent counts the reference's "in-consistent matching" warnings. */
 /* ---------------- feature front-end (image_process.py:178-234, 418-441) ---------------- */
 /* Brute-force 2-nearest-neighbour matching in L2 (cv.BFMatcher().knnMatch(des1, des2, k=2)): for each of the
  * n1 query descriptors the two nearest of the n2 train descriptors, idx_out[2*i+0/1] (ties: lower index
@@ -238,12 +234,26 @@ PTZBA_EXPORT int ptz_match_knn2(int device, int64_t n1, int64_t n2, int32_t dim,
 PTZBA_EXPORT int ptz_homography_ransac(int device, int64_t n, const double* pts1, const double* pts2, double threshold,
                                        int32_t n_hyp, uint64_t seed, uint8_t* mask_out, double* H_out,
                                        int32_t* n_inliers_out);
+/* Pyramidal Lucas-Kanade point tracking (cv.calcOpticalFlowPyrLK(img, next_img, points, None, winSize=(31, 31))
+ * as called by optical_flow_matching, image_process.py:393-415).  img0/img1: 8-bit grey, width x height,
+ * row-major.  Pyramid of `levels` (cv.pyrDown: 5x5 binomial, reflect-101), Scharr gradients, window `win`
+ * (odd, <= 31), at most max_iter Newton steps per level, stop when the step is below eps px; bilinear
+ * samples clamp to the image.  Per point: pts1_out [n][2]; status_out 1 = tracked (the window's smaller
+ * structure-tensor eigenvalue / win^2 >= min_eig at every level and the result inside the image);
+ * err_out = mean |I - J| over the window at the final position (the reference keeps err < 20). */
+PTZBA_EXPORT int ptz_lk_track(int device, int32_t width, int32_t height, const uint8_t* img0, const uint8_t* img1,
+                              int64_t n, const float* pts0, int32_t levels, int32_t win, int32_t max_iter, double eps,
+                              double min_eig, float* pts1_out, uint8_t* status_out, float* err_out);
 
 /* Coupling window of a record set (host only, O(n_obs)): win_out[f] = the highest frame that shares a
  * landmark with frame f (>= f).  Computed over ALL records it is the frame_win_hi every rank of a
  * landmark-sharded solve passes in ptzba_problem_opts. */
 PTZBA_EXPORT int ptzba_coupling_window(int32_t n_pose, int32_t n_landmark, int64_t n_obs, const int32_t* obs_frame,
                                        const int32_t* obs_landmark, int32_t* win_out);
+/* First-seen landmark ids over ordered pair match lists (image_process.py:611-639).
+ * pair_i/pair_j/pair_count: n_pairs; idx_a/idx_b: concatenated match keypoint indices.
+ * kp_count[n_frames]: keypoints per frame.  Output landmark id per match (of the src keypoint) and
+ * the landmark count; *n_inconsistent counts the reference's "in-consistent matching" warnings. */
 PTZBA_EXPORT int ptzba_build_landmarks(int32_t n_frames, const int64_t* kp_count, int64_t n_pairs,
                                        const int32_t* pair_i, const int32_t* pair_j,
                                        const int64_t* pair_count, const int64_t* idx_a,
@@ -311,7 +321,9 @@ PTZBA_EXPORT int ptzekf_project_visible(ptzekf_handle h, double u, double v, con
  * (matched against the visible predicted rays with the reference's get_overlap_index walk,
  * util.py:75-97); observe_var = the reference's R = observe_var * I (0.1).  Rays and covariance are
  * updated in place on the device with the reference's write-back (:281-289).  velocity_out (3) =
- * K y [0:3] (:273); *n_matched_out = matched rays.  Fails (state untouched) if H P H^T + R is not SPD. */
+ * K y [0:3] (:273); *n_matched_out = matched rays.  H P H^T + R is factored as L S L^T with a signed
+ * diagonal S (it can be indefinite: the reference inverts it regardless); fails (state untouched) only
+ * when it is singular. */
 PTZBA_EXPORT int ptzekf_update(ptzekf_handle h, double u, double v, const double* displacement6,
                                double* ptz_inout, int64_t n_obs, const double* obs_xy, const int64_t* obs_index,
                                int32_t height, int32_t width, double observe_var, double* velocity_out,

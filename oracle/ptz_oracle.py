@@ -623,3 +623,91 @@ def homography_ransac(p1, p2, threshold, n_hyp=2000, seed=0):
     H = denorm(x) if x is not None else best_H
     mask = err2(H) < thr2
     return mask, H / H[2, 2], int(mask.sum())
+
+
+# ---------------------------------------------------------------------------------------------
+# pyramidal Lucas-Kanade (cv.calcOpticalFlowPyrLK(img, next_img, points, None, winSize=(31, 31)),
+# optical_flow_matching, image_process.py:393-415).  OpenCV is not installed here, so this restates the
+# algorithm ptz_lk_track implements (include/ptzba.h): parity of the GPU path is pinned to THIS restatement
+# and to the known motion of synthetic images; agreement with cv2's own numbers is unpinned.
+# ---------------------------------------------------------------------------------------------
+def pyr_down(img):
+    """cv.pyrDown: 5x5 binomial [1 4 6 4 1]^2 / 256 over a reflect-101 border, every second pixel."""
+    h, w = img.shape
+    P = np.pad(np.asarray(img, np.float64), 2, mode="reflect")
+    k = np.array([1.0, 4.0, 6.0, 4.0, 1.0])
+    dh, dw = (h + 1) // 2, (w + 1) // 2
+    rows = sum(k[i] * P[i:i + 2 * dh:2, :] for i in range(5))
+    return sum(k[j] * rows[:, j:j + 2 * dw:2] for j in range(5)) / 256.0
+
+
+def scharr(img):
+    """Scharr derivatives / 32 over a reflect-101 border: (gx, gy)."""
+    P = np.pad(np.asarray(img, np.float64), 1, mode="reflect")
+    h, w = img.shape
+    S = lambda dy, dx: P[1 + dy:1 + dy + h, 1 + dx:1 + dx + w]
+    gx = (3 * (S(-1, 1) - S(-1, -1)) + 10 * (S(0, 1) - S(0, -1)) + 3 * (S(1, 1) - S(1, -1))) / 32.0
+    gy = (3 * (S(1, -1) - S(-1, -1)) + 10 * (S(1, 0) - S(-1, 0)) + 3 * (S(1, 1) - S(-1, 1))) / 32.0
+    return gx, gy
+
+
+def bilinear(img, x, y):
+    """Bilinear sample with the coordinates clamped to the image (ptz_lk_track's sampler)."""
+    h, w = img.shape
+    x = np.clip(x, 0.0, w - 1.0)
+    y = np.clip(y, 0.0, h - 1.0)
+    x0 = np.minimum(x.astype(np.int64), max(w - 2, 0))
+    y0 = np.minimum(y.astype(np.int64), max(h - 2, 0))
+    x1 = np.minimum(x0 + 1, w - 1)
+    y1 = np.minimum(y0 + 1, h - 1)
+    ax, ay = x - x0, y - y0
+    return (1 - ay) * ((1 - ax) * img[y0, x0] + ax * img[y0, x1]) + ay * ((1 - ax) * img[y1, x0] + ax * img[y1, x1])
+
+
+def lk_track(img0, img1, pts, win=31, levels=4, max_iter=30, eps=0.01, min_eig=1e-4):
+    """Restatement of ptz_lk_track: returns (next points [n, 2], status [n] uint8, err [n])."""
+    pts = np.asarray(pts, np.float64).reshape(-1, 2)
+    n = len(pts)
+    I = [np.asarray(img0, np.float64)]
+    J = [np.asarray(img1, np.float64)]
+    for _ in range(1, levels):
+        I.append(pyr_down(I[-1]))
+        J.append(pyr_down(J[-1]))
+    half = win // 2
+    oy, ox = np.divmod(np.arange(win * win), win)
+    ox = (ox - half).astype(np.float64)[None, :]
+    oy = (oy - half).astype(np.float64)[None, :]
+    g = np.zeros((n, 2))
+    d = np.zeros((n, 2))
+    ok = np.ones(n, bool)
+    area = win * win
+    for L in range(levels - 1, -1, -1):
+        c = pts / (1 << L)
+        X, Y = c[:, :1] + ox, c[:, 1:] + oy
+        gxL, gyL = scharr(I[L])
+        Iv, Ix, Iy = bilinear(I[L], X, Y), bilinear(gxL, X, Y), bilinear(gyL, X, Y)
+        a, b, cc = (Ix * Ix).sum(1), (Ix * Iy).sum(1), (Iy * Iy).sum(1)
+        det = a * cc - b * b
+        mineig = 0.5 * (a + cc - np.sqrt(np.maximum((a - cc) ** 2 + 4 * b * b, 0.0))) / area
+        ok &= (mineig >= min_eig) & (det > 0)
+        d[:] = 0.0
+        act = ok.copy()
+        for _ in range(max_iter):
+            if not act.any():
+                break
+            e = Iv - bilinear(J[L], X + (g[:, :1] + d[:, :1]), Y + (g[:, 1:] + d[:, 1:]))
+            b0, b1 = (e * Ix).sum(1), (e * Iy).sum(1)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                ddx = (cc * b0 - b * b1) / det
+                ddy = (a * b1 - b * b0) / det
+            d[act, 0] += ddx[act]
+            d[act, 1] += ddy[act]
+            act &= ~(ddx * ddx + ddy * ddy < eps * eps)
+        if L > 0:
+            g = np.where(ok[:, None], 2.0 * (g + d), g)
+    nxt = pts + g + d
+    h, w = I[0].shape
+    err = np.abs(bilinear(I[0], pts[:, :1] + ox, pts[:, 1:] + oy) -
+                 bilinear(J[0], nxt[:, :1] + ox, nxt[:, 1:] + oy)).sum(1) / area
+    inside = (nxt[:, 0] >= 0) & (nxt[:, 1] >= 0) & (nxt[:, 0] <= w - 1) & (nxt[:, 1] <= h - 1)
+    return nxt, (ok & inside).astype(np.uint8), np.where(ok, err, np.inf)

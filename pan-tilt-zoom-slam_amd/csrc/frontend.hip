@@ -413,3 +413,231 @@ int ptz_homography_ransac(int device, int64_t n, const double* pts1, const doubl
   HIPCHK(hipMemcpy(n_inliers_out, nin.p, 4, hipMemcpyDeviceToHost));
   return 0;
 }
+
+namespace ptzba {
+// ---------------------------------------------------------------------------------------------
+// pyramidal Lucas-Kanade point tracking (cv.calcOpticalFlowPyrLK(img, next_img, points, None,
+// winSize=(31, 31)) as called by optical_flow_matching, image_process.py:393-415)
+//   pyramid: level l+1 = 5x5 binomial [1 4 6 4 1]/16 blur of level l (reflect-101 border), every
+//            second pixel (cv.pyrDown); gradients: Scharr 3x3 / 32 (reflect-101)
+//   per point, one 256-thread workgroup: from the coarsest level down, the window's samples of the
+//   first image and its gradients (bilinear, clamped to the image) give G = sum [Ix Iy]^T [Ix Iy];
+//   Newton steps d += G^-1 sum (I - J(x + g + d)) [Ix Iy] until |delta| < eps or max_iter; the
+//   guess doubles to the next level.  status 0 when G's smaller eigenvalue / window area < min_eig at
+//   any level or the point leaves the image; err = mean |I - J| over the window at the final position.
+// Sums are fp64 with a fixed-order LDS reduction (deterministic).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int refl101(int i, int n) {
+  if (n == 1) return 0;
+  while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
+  return i;
+}
+
+__global__ void k_u8_to_f32(int n, const uint8_t* __restrict__ src, float* __restrict__ dst) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = (float)src[i];
+}
+
+__global__ void k_pyr_down(int sw, int sh, const float* __restrict__ src, int dw, int dh, float* __restrict__ dst) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= dw || y >= dh) return;
+  const float k[5] = {1.f, 4.f, 6.f, 4.f, 1.f};
+  float s = 0.f;
+  for (int i = 0; i < 5; ++i) {
+    const int yy = refl101(2 * y + i - 2, sh);
+    float r = 0.f;
+    for (int j = 0; j < 5; ++j) r += k[j] * src[(int64_t)yy * sw + refl101(2 * x + j - 2, sw)];
+    s += k[i] * r;
+  }
+  dst[(int64_t)y * dw + x] = s * (1.f / 256.f);
+}
+
+__global__ void k_scharr(int w, int h, const float* __restrict__ src, float* __restrict__ gx, float* __restrict__ gy) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= w) return;
+  const int xm = refl101(x - 1, w), xp = refl101(x + 1, w), ym = refl101(y - 1, h), yp = refl101(y + 1, h);
+  auto P = [&](int yy, int xx) { return src[(int64_t)yy * w + xx]; };
+  gx[(int64_t)y * w + x] = (3.f * (P(ym, xp) - P(ym, xm)) + 10.f * (P(y, xp) - P(y, xm)) + 3.f * (P(yp, xp) - P(yp, xm))) *
+                           (1.f / 32.f);
+  gy[(int64_t)y * w + x] = (3.f * (P(yp, xm) - P(ym, xm)) + 10.f * (P(yp, x) - P(ym, x)) + 3.f * (P(yp, xp) - P(ym, xp))) *
+                           (1.f / 32.f);
+}
+
+__device__ __forceinline__ double bil(const float* __restrict__ im, int w, int h, double x, double y) {
+  x = fmin(fmax(x, 0.0), (double)(w - 1));
+  y = fmin(fmax(y, 0.0), (double)(h - 1));
+  const int x0 = min((int)x, w - 2 < 0 ? 0 : w - 2), y0 = min((int)y, h - 2 < 0 ? 0 : h - 2);
+  const int x1 = min(x0 + 1, w - 1), y1 = min(y0 + 1, h - 1);
+  const double ax = x - x0, ay = y - y0;
+  const double a = im[(int64_t)y0 * w + x0], b = im[(int64_t)y0 * w + x1], c = im[(int64_t)y1 * w + x0],
+               d = im[(int64_t)y1 * w + x1];
+  return (1 - ay) * ((1 - ax) * a + ax * b) + ay * ((1 - ax) * c + ax * d);
+}
+
+constexpr int LK_MAXLV = 6;
+struct LkPyr {
+  const float* I[LK_MAXLV];
+  const float* J[LK_MAXLV];
+  const float* gx[LK_MAXLV];
+  const float* gy[LK_MAXLV];
+  int w[LK_MAXLV], h[LK_MAXLV];
+  int levels;
+};
+
+// block-wide fixed-order sum of NV doubles (256 threads)
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double (*red)[NV]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) red[t][k] = v[k];
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (t < s)
+#pragma unroll
+      for (int k = 0; k < NV; ++k) red[t][k] += red[t + s][k];
+    __syncthreads();
+  }
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = red[0][k];
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void k_lk_track(LkPyr P, int n, const float* __restrict__ pts, int half, int max_iter,
+                                                  double eps, double min_eig, float* __restrict__ out_pts,
+                                                  uint8_t* __restrict__ status, float* __restrict__ err) {
+  __shared__ double red[256][3];
+  const int q = blockIdx.x, t = threadIdx.x;
+  if (q >= n) return;
+  const int win = 2 * half + 1, area = win * win;
+  constexpr int SPT = 4;  // window samples per thread (31 x 31 = 961 <= 1024)
+  const double px = pts[2 * q], py = pts[2 * q + 1];
+  double gxv = 0.0, gyv = 0.0;  // guess at the current level
+  bool ok = true;
+  double dx = 0.0, dy = 0.0;
+  for (int L = P.levels - 1; L >= 0 && ok; --L) {
+    const double sc = 1.0 / (double)(1 << L);
+    const double cx = px * sc, cy = py * sc;
+    const int w = P.w[L], h = P.h[L];
+    double Iv[SPT], Ixv[SPT], Iyv[SPT];
+    double g[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < SPT; ++s) {
+      const int e = t + 256 * s;
+      Iv[s] = Ixv[s] = Iyv[s] = 0.0;
+      if (e < area) {
+        const double x = cx + (e % win - half), y = cy + (e / win - half);
+        Iv[s] = bil(P.I[L], w, h, x, y);
+        Ixv[s] = bil(P.gx[L], w, h, x, y);
+        Iyv[s] = bil(P.gy[L], w, h, x, y);
+        g[0] += Ixv[s] * Ixv[s];
+        g[1] += Ixv[s] * Iyv[s];
+        g[2] += Iyv[s] * Iyv[s];
+      }
+    }
+    block_sum<3>(g, red);
+    const double tr = g[0] + g[2], det = g[0] * g[2] - g[1] * g[1];
+    const double mineig = 0.5 * (tr - sqrt(fmax((g[0] - g[2]) * (g[0] - g[2]) + 4.0 * g[1] * g[1], 0.0))) / area;
+    if (!(mineig >= min_eig) || !(det > 0)) {
+      ok = false;
+      break;
+    }
+    dx = dy = 0.0;
+    for (int it = 0; it < max_iter; ++it) {
+      double b[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < SPT; ++s) {
+        const int e = t + 256 * s;
+        if (e < area) {
+          const double x = cx + (e % win - half) + gxv + dx, y = cy + (e / win - half) + gyv + dy;
+          const double ediff = Iv[s] - bil(P.J[L], w, h, x, y);
+          b[0] += ediff * Ixv[s];
+          b[1] += ediff * Iyv[s];
+        }
+      }
+      block_sum<3>(b, red);
+      const double ddx = (g[2] * b[0] - g[1] * b[1]) / det, ddy = (g[0] * b[1] - g[1] * b[0]) / det;
+      dx += ddx;
+      dy += ddy;
+      if (ddx * ddx + ddy * ddy < eps * eps) break;
+    }
+    if (L > 0) {
+      gxv = 2.0 * (gxv + dx);
+      gyv = 2.0 * (gyv + dy);
+    }
+  }
+  const double nx = px + gxv + dx, ny = py + gyv + dy;
+  double e1[3] = {0.0, 0.0, 0.0};
+  if (ok) {
+    const int w = P.w[0], h = P.h[0];
+    for (int e = t; e < area; e += 256) {
+      const double ox = (e % win - half), oy = (e / win - half);
+      e1[0] += fabs(bil(P.I[0], w, h, px + ox, py + oy) - bil(P.J[0], w, h, nx + ox, ny + oy));
+    }
+  }
+  block_sum<3>(e1, red);
+  if (t == 0) {
+    const bool inside = nx >= 0 && ny >= 0 && nx <= P.w[0] - 1 && ny <= P.h[0] - 1;
+    out_pts[2 * q] = (float)nx;
+    out_pts[2 * q + 1] = (float)ny;
+    status[q] = (ok && inside) ? 1 : 0;
+    err[q] = ok ? (float)(e1[0] / area) : INFINITY;
+  }
+}
+
+}  // namespace ptzba
+
+int ptz_lk_track(int device, int32_t width, int32_t height, const uint8_t* img0, const uint8_t* img1, int64_t n,
+                 const float* pts0, int32_t levels, int32_t win, int32_t max_iter, double eps, double min_eig,
+                 float* pts1_out, uint8_t* status_out, float* err_out) {
+  using namespace ptzba;
+  if (width < 2 || height < 2 || !img0 || !img1) return fail("bad image");
+  if (n < 0 || (n > 0 && (!pts0 || !pts1_out || !status_out || !err_out))) return fail("bad point list");
+  if (levels < 1 || levels > LK_MAXLV || win < 3 || (win & 1) == 0 || win > 31 || max_iter < 1)
+    return fail("bad LK parameters (levels 1..%d, odd win 3..31)", LK_MAXLV);
+  if (n == 0) return 0;
+  if (select_device(device)) return -1;
+  const int64_t np = (int64_t)width * height;
+  std::vector<int> W(levels), H(levels);
+  W[0] = width; H[0] = height;
+  int64_t tot = 0;
+  for (int l = 0; l < levels; ++l) {
+    if (l > 0) { W[l] = (W[l - 1] + 1) / 2; H[l] = (H[l - 1] + 1) / 2; }
+    tot += (int64_t)W[l] * H[l];
+  }
+  DBuf u8, bufI, bufJ, bufX, bufY, dp, dout, dst, derr;
+  if (u8.alloc((size_t)np * 2) || bufI.alloc((size_t)tot * 4) || bufJ.alloc((size_t)tot * 4) ||
+      bufX.alloc((size_t)tot * 4) || bufY.alloc((size_t)tot * 4) || dp.alloc((size_t)n * 8) || dout.alloc((size_t)n * 8) ||
+      dst.alloc((size_t)n) || derr.alloc((size_t)n * 4))
+    return -1;
+  HIPCHK(hipMemcpy(u8.p, img0, (size_t)np, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(u8.as<uint8_t>() + np, img1, (size_t)np, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dp.p, pts0, (size_t)n * 8, hipMemcpyHostToDevice));
+  LkPyr P{};
+  P.levels = levels;
+  int64_t off = 0;
+  for (int l = 0; l < levels; ++l) {
+    P.I[l] = bufI.as<float>() + off; P.J[l] = bufJ.as<float>() + off;
+    P.gx[l] = bufX.as<float>() + off; P.gy[l] = bufY.as<float>() + off;
+    P.w[l] = W[l]; P.h[l] = H[l];
+    off += (int64_t)W[l] * H[l];
+  }
+  hipLaunchKernelGGL(k_u8_to_f32, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, nullptr, (int)np, u8.as<uint8_t>(),
+                     (float*)P.I[0]);
+  hipLaunchKernelGGL(k_u8_to_f32, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, nullptr, (int)np,
+                     u8.as<uint8_t>() + np, (float*)P.J[0]);
+  for (int l = 1; l < levels; ++l) {
+    const dim3 g((unsigned)((W[l] + 127) / 128), (unsigned)H[l]);
+    hipLaunchKernelGGL(k_pyr_down, g, dim3(128), 0, nullptr, W[l - 1], H[l - 1], P.I[l - 1], W[l], H[l], (float*)P.I[l]);
+    hipLaunchKernelGGL(k_pyr_down, g, dim3(128), 0, nullptr, W[l - 1], H[l - 1], P.J[l - 1], W[l], H[l], (float*)P.J[l]);
+  }
+  for (int l = 0; l < levels; ++l)
+    hipLaunchKernelGGL(k_scharr, dim3((unsigned)((W[l] + 127) / 128), (unsigned)H[l]), dim3(128), 0, nullptr, W[l], H[l],
+                       P.I[l], (float*)P.gx[l], (float*)P.gy[l]);
+  hipLaunchKernelGGL(k_lk_track, dim3((unsigned)n), dim3(256), 0, nullptr, P, (int)n, dp.as<float>(), win / 2, max_iter,
+                     eps, min_eig, dout.as<float>(), dst.as<uint8_t>(), derr.as<float>());
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(pts1_out, dout.p, (size_t)n * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(status_out, dst.p, (size_t)n, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(err_out, derr.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  return 0;
+}

@@ -41,11 +41,10 @@ def _hook(name):
 detect_compute_sift = _hook("detect_compute_sift")              # (im, nfeatures, verbose) -> (kps, des)
 detect_compute_orb = _hook("detect_compute_orb")
 detect_compute_latch = _hook("detect_compute_latch")
-# match_sift_features / homography_ransac: GPU implementations below (kNN-2 + ratio test + RANSAC);
-# a correspondence source may still assign its own
+# match_sift_features / homography_ransac / optical_flow_matching: GPU implementations below (kNN-2 +
+# ratio test + RANSAC, pyramidal LK); a correspondence source may still assign its own
 match_orb_features = _hook("match_orb_features")
 match_latch_features = _hook("match_latch_features")
-optical_flow_matching = _hook("optical_flow_matching")
 draw_matches = None  # optional visualisation hook (bundle_adjustment.py:153-163)
 
 
@@ -101,6 +100,28 @@ def homography_ransac(points1, points2, reprojection_threshold=0.5, return_matri
     if return_matrix:
         return index, H
     return index
+
+
+def _grey_u8(img):
+    a = np.asarray(img)
+    if a.ndim == 3:  # BGR -> grey, ITU-R BT.601 weights (cv.COLOR_BGR2GRAY)
+        a = a[..., 2] * 0.299 + a[..., 1] * 0.587 + a[..., 0] * 0.114
+    return np.clip(np.rint(a), 0, 255).astype(np.uint8) if a.dtype != np.uint8 else a
+
+
+def optical_flow_matching(img, next_img, points, ssd_threshold=20):
+    """image_process.py:393-415 on the GPU (libptzba ptz_lk_track: pyramidal LK, 31 x 31 window, 4 levels,
+    30 iterations, eps 0.01): indices of the points tracked with err < ssd_threshold and strictly inside
+    the image, and their positions in next_img ([m, 2])."""
+    import ptzba
+    a, b = _grey_u8(img), _grey_u8(next_img)
+    pts = np.asarray(points, np.float32).reshape(-1, 2)
+    nxt, status, err = ptzba.lk_track(a, b, pts, win=31)
+    h, w = a.shape[0], a.shape[1]
+    x, y = nxt[:, 0], nxt[:, 1]
+    keep = (status == 1) & (err < ssd_threshold) & (x > 0) & (x < w) & (y > 0) & (y < h)
+    matched_index = [int(i) for i in np.flatnonzero(keep)]
+    return matched_index, np.array([nxt[i] for i in matched_index])
 
 
 def keypoints_masking(kp, mask):

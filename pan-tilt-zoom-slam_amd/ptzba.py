@@ -123,6 +123,7 @@ def lib():
         "ptzba_coupling_window": ([I32, I32, I64, V, V, V], I),
         "ptz_match_knn2": ([I, I64, I64, I32, V, V, V, V], I),
         "ptz_homography_ransac": ([I, I64, V, V, D, I32, ctypes.c_uint64, V, V, POINTER(c_int32)], I),
+        "ptz_lk_track": ([I, I32, I32, V, V, I64, V, I32, I32, I32, D, D, V, V, V], I),
         "ptz_py_shuffle_prefix": ([V, I64, V, I64, V], I),
         "ptz_set_order_pairs": ([I64, V, V, V, V, V], I),
         "ptz_keyframe_features": ([I32, I64, V, V, V, V, V, V, V, V], I),
@@ -153,7 +154,7 @@ EXPORTED_SYMBOLS = [
     "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_solve", "ptzba_read_scalars", "ptzba_accept",
     "ptzba_lm_start", "ptzba_lm_init", "ptzba_lm_build", "ptzba_lm_solve", "ptzba_lm_decide", "ptzba_lm_wait",
     "ptzba_exchange", "ptzba_exchange_packed", "ptzba_pack", "ptzba_unpack", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptzba_save_state", "ptzba_restore_state", "ptz_ray_to_image",
-    "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks", "ptzba_coupling_window", "ptz_match_knn2", "ptz_homography_ransac",
+    "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks", "ptzba_coupling_window", "ptz_match_knn2", "ptz_homography_ransac", "ptz_lk_track",
     "ptz_py_shuffle_prefix", "ptz_set_order_pairs", "ptz_keyframe_features", "ptz_pack_records",
     "ptz_refine_poses", "ptzekf_new", "ptzekf_delete", "ptzekf_num_rays", "ptzekf_set_state", "ptzekf_get_state", "ptzekf_add_pose_cov",
     "ptzekf_remove_rays", "ptzekf_add_rays", "ptzekf_project_visible", "ptzekf_update",
@@ -271,6 +272,26 @@ def homography_ransac(points1, points2, threshold, n_hyp=2000, seed=0, device=No
                                        float(threshold), int(n_hyp), int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(mask), _ptr(H),
                                        ctypes.byref(nin)), "ptz_homography_ransac")
     return mask.astype(bool), H.reshape(3, 3), int(nin.value)
+
+
+def lk_track(img0, img1, points, win=31, levels=4, max_iter=30, eps=0.01, min_eig=1e-4, device=None):
+    """Pyramidal Lucas-Kanade on the GPU (the cv.calcOpticalFlowPyrLK call of image_process.py:402, winSize
+    31 x 31, OpenCV's default maxLevel 3 / 30 iterations / eps 0.01): 8-bit grey images [h, w], points [n, 2]
+    (x, y).  Returns (next points [n, 2] float32, status [n] uint8, err [n] float32 = mean |I - J|)."""
+    a = np.ascontiguousarray(img0, dtype=np.uint8)
+    b = np.ascontiguousarray(img1, dtype=np.uint8)
+    if a.ndim != 2 or a.shape != b.shape:
+        raise ValueError("images must be 2-D 8-bit grey of the same shape")
+    pts = np.ascontiguousarray(np.asarray(points, dtype=np.float32).reshape(-1, 2))
+    n = len(pts)
+    out = np.empty((n, 2), np.float32)
+    st = np.zeros(n, np.uint8)
+    err = np.zeros(n, np.float32)
+    if n:
+        _check(lib().ptz_lk_track(default_device() if device is None else device, a.shape[1], a.shape[0], _ptr(a),
+                                  _ptr(b), n, _ptr(pts), int(levels), int(win), int(max_iter), float(eps),
+                                  float(min_eig), _ptr(out), _ptr(st), _ptr(err)), "ptz_lk_track")
+    return out, st, err
 
 
 def refine_poses(u, v, init_ptz, rays, points, subsets=None, ftol=1e-4, xtol=1e-8, max_iter=100, loss=LOSS_LINEAR,

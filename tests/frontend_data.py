@@ -53,3 +53,57 @@ def homography_points(seed=0, n=600, outlier_frac=0.25, noise=0.3):
     out = rng.random(n) < outlier_frac
     p2[out] += rng.uniform(5, 60, (out.sum(), 2)) * rng.choice([-1, 1], (out.sum(), 2))
     return p1, p2, H, ~out
+
+
+def _mix64(z):
+    z = np.asarray(z, np.uint64)
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def value_noise(x, y, seed=0, cells=(40.0, 17.0, 7.0, 3.0), amps=(55.0, 40.0, 28.0, 14.0)):
+    """Smooth procedural texture T(x, y) (continuous in x, y, defined everywhere): octaves of lattice value
+    noise with smoothstep interpolation; lattice values are a hash of (seed, octave, i, j)."""
+    x = np.asarray(x, np.float64)
+    y = np.asarray(y, np.float64)
+    out = np.full(np.broadcast(x, y).shape, 128.0)
+    for o, (c, a) in enumerate(zip(cells, amps)):
+        gx, gy = x / c, y / c
+        i0, j0 = np.floor(gx), np.floor(gy)
+        fx, fy = gx - i0, gy - j0
+        sx, sy = fx * fx * (3 - 2 * fx), fy * fy * (3 - 2 * fy)
+        base = np.uint64((seed * 1315423911 + o * 2654435761) & 0xFFFFFFFFFFFF)
+
+        def lat(di, dj):
+            ii = (i0 + di).astype(np.int64).astype(np.uint64)
+            jj = (j0 + dj).astype(np.int64).astype(np.uint64)
+            with np.errstate(over="ignore"):
+                h = _mix64(base * np.uint64(0x9E3779B97F4A7C15) + ii * np.uint64(0x632BE59BD9B4E019) +
+                           jj * np.uint64(0x85EBCA77C2B2AE63))
+            return (h >> np.uint64(11)).astype(np.float64) / float(1 << 53) * 2.0 - 1.0
+        top = lat(0, 0) * (1 - sx) + lat(1, 0) * sx
+        bot = lat(0, 1) * (1 - sx) + lat(1, 1) * sx
+        out += a * (top * (1 - sy) + bot * sy)
+    return out
+
+
+def textured_pair(seed=0, width=320, height=240, d_pan=0.6, d_tilt=-0.3, f=600.0, df=8.0, flat_box=None):
+    """Two 8-bit grey views of a textured scene under a PTZ motion: I(p) = T(p), J(p) = T(H^-1 p) with H the
+    pure-rotation homography between the views.  flat_box = (x0, y0, x1, y1) paints a constant region in both
+    (untrackable).  Returns (I, J, H)."""
+    u, v = width / 2.0, height / 2.0
+    H = ptz_homography(u, v, np.array([10.0, -5.0, f]), np.array([10.0 + d_pan, -5.0 + d_tilt, f + df]))
+    yy, xx = np.mgrid[0:height, 0:width].astype(np.float64)
+    Hi = np.linalg.inv(H)
+    q = np.stack([xx.ravel(), yy.ravel(), np.ones(xx.size)], 1) @ Hi.T
+    I = value_noise(xx, yy, seed)
+    J = value_noise((q[:, 0] / q[:, 2]).reshape(xx.shape), (q[:, 1] / q[:, 2]).reshape(xx.shape), seed)
+    I8 = np.clip(np.rint(I), 0, 255).astype(np.uint8)
+    J8 = np.clip(np.rint(J), 0, 255).astype(np.uint8)
+    if flat_box is not None:
+        x0, y0, x1, y1 = flat_box
+        I8[y0:y1, x0:x1] = 100
+        J8[y0:y1, x0:x1] = 100
+    return I8, J8, H

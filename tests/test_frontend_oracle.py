@@ -1,6 +1,8 @@
-"""CPU checks of the front-end oracle (oracle/ptz_oracle.py knn2 / homography_ransac, test infrastructure):
-the kNN restatement against an explicit per-query sort, and the RANSAC restatement against the ground
-truth of synthetic correspondences (the GPU kernels are compared with these in test_gpu_frontend.py)."""
+"""CPU checks of the front-end oracle (oracle/ptz_oracle.py knn2 / homography_ransac / lk_track, test
+infrastructure): the kNN restatement against an explicit per-query sort, the RANSAC restatement against the
+ground truth of synthetic correspondences, the LK restatement's pyramid / gradient kernels against known
+answers and its tracks against the known motion of synthetic textured views (the GPU kernels are compared
+with these in test_gpu_frontend.py)."""
 import numpy as np
 
 import frontend_data
@@ -25,3 +27,32 @@ def test_ransac_oracle_recovers_truth():
     mask, Hh, cnt = orc.homography_ransac(p1, p2, 1.0, n_hyp=300, seed=5)
     assert cnt == mask.sum() and np.array_equal(mask, inl)
     np.testing.assert_allclose(Hh, H, rtol=0, atol=1e-3 * np.abs(H).max())
+
+
+def test_pyr_down_and_scharr_known_answers():
+    from oracle import ptz_oracle as orc
+    # a constant image stays constant; a linear ramp keeps its slope (x2 per level) away from the border
+    assert np.allclose(orc.pyr_down(np.full((9, 13), 7.0)), 7.0)
+    assert orc.pyr_down(np.zeros((9, 13))).shape == (5, 7)
+    yy, xx = np.mgrid[0:20, 0:30].astype(np.float64)
+    ramp = 3.0 * xx - 2.0 * yy
+    d = orc.pyr_down(ramp)
+    assert np.allclose(d[2:-2, 2:-2], 3.0 * 2 * np.mgrid[0:10, 0:15][1][2:-2, 2:-2] - 2.0 * 2 * np.mgrid[0:10, 0:15][0][2:-2, 2:-2])
+    gx, gy = orc.scharr(ramp)
+    assert np.allclose(gx[1:-1, 1:-1], 3.0) and np.allclose(gy[1:-1, 1:-1], -2.0)  # Scharr / 32 = the slope
+    # bilinear sampling reproduces a plane exactly and clamps outside
+    assert np.allclose(orc.bilinear(ramp, np.array([3.25, -5.0]), np.array([4.5, 2.0])), [3 * 3.25 - 9.0, -4.0])
+
+
+def test_lk_oracle_tracks_known_motion():
+    """lk_track on two textured views a PTZ homography apart (9 px / 5 px motion): every interior point is
+    tracked, median error vs the true motion < 0.05 px, all < 0.5 px; a flat (textureless) patch fails."""
+    from oracle import ptz_oracle as orc
+    I, J, H = frontend_data.textured_pair(seed=1, flat_box=(240, 150, 320, 240))
+    rng = np.random.default_rng(0)
+    p = np.stack([rng.uniform(20, 230, 200), rng.uniform(20, 140, 200)], 1)
+    flat = np.array([[285.0, 200.0], [290.0, 205.0]])
+    nxt, st, err = orc.lk_track(I, J, np.r_[p, flat])
+    e = np.linalg.norm(nxt[:200] - frontend_data.apply_h(H, p), axis=1)
+    assert st[:200].all() and np.median(e) < 0.05 and e.max() < 0.5 and err[:200].max() < 5
+    assert not st[200:].any() and np.isinf(err[200:]).all()

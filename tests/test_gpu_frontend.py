@@ -1,7 +1,11 @@
 """GPU front-end through the C-ABI: ptz_match_knn2 (cv.BFMatcher().knnMatch(k=2),
 image_process.py:191) and ptz_homography_ransac (cv.findHomography RANSAC, image_process.py:433), and
 image_process.match_sift_features (:178-234) composed from them, against the oracle restatements
-(oracle/ptz_oracle.py knn2 / homography_ransac) on synthetic SIFT-like data.
+(oracle/ptz_oracle.py knn2 / homography_ransac) on synthetic SIFT-like data; ptz_lk_track
+(cv.calcOpticalFlowPyrLK, image_process.py:402) and image_process.optical_flow_matching (:393-415) against
+oracle lk_track and the known motion of synthetic textured views (positions within 0.02 px of the oracle:
+the GPU pyramid is fp32 and the sums run in another order, so a Newton stop decision near eps = 0.01 px
+can differ; err within 1e-3).
 Exact: kNN indices and distances (integer-valued descriptors: every fp32 partial sum is exact), the RANSAC
 inlier mask and count (same counter-keyed samples; H to 1e-9 relative).  OpenCV itself is not in the image,
 so the oracle restates the published algorithms -- parity with cv2 is unpinned; the tests pin the GPU to
@@ -66,3 +70,77 @@ def test_homography_ransac_hook_signature(gpu_available):
     idx, Hm = image_process.homography_ransac(p1, p2, 1.0, return_matrix=True)
     assert idx == np.flatnonzero(inl).tolist() or len(set(idx) ^ set(np.flatnonzero(inl).tolist())) <= 1
     np.testing.assert_allclose(Hm, H, rtol=0, atol=2e-3 * np.abs(H).max())
+
+
+def _lk_points(seed, n, w, h, margin=20):
+    rng = np.random.default_rng(seed)
+    return np.stack([rng.uniform(margin, w - margin, n), rng.uniform(margin, h - margin, n)], 1).astype(np.float32)
+
+
+def _lk_compare(I, J, p, **kw):
+    import ptzba
+    from oracle import ptz_oracle as orc
+    nxt, st, err = ptzba.lk_track(I, J, p, **kw)
+    rn, rst, rerr = orc.lk_track(I, J, p.astype(np.float64), **kw)
+    both = (st == 1) & (rst == 1)
+    assert (st != rst).sum() <= max(1, len(p) // 100)
+    assert np.abs(nxt[both] - rn[both]).max() < 0.02
+    assert np.abs(err[both] - rerr[both]).max() < 1e-3
+    same = st == rst  # err is inf exactly where the eigenvalue test failed (a point that left the image keeps it)
+    assert np.array_equal(np.isinf(err[same]), np.isinf(rerr[same]))
+    return nxt, st, err
+
+
+@pytest.mark.parametrize("seed,w,h,kw", [(1, 320, 240, {}), (2, 257, 199, {"win": 21, "levels": 3}),
+                                         (3, 640, 360, {"levels": 5})])
+def test_lk_track_matches_oracle(gpu_available, seed, w, h, kw):
+    I, J, H = frontend_data.textured_pair(seed=seed, width=w, height=h, flat_box=(0, 0, 40, 40))
+    p = _lk_points(seed, 300, w, h)
+    p[:3] = [[15.0, 15.0], [20.0, 22.0], [w - 1.0, h - 1.0]]  # flat patch (fails) and the image corner
+    nxt, st, err = _lk_compare(I, J, p, **kw)
+    assert st[:2].sum() == 0
+    good = st == 1
+    e = np.linalg.norm(nxt[good] - frontend_data.apply_h(H, p[good].astype(np.float64)), axis=1)
+    assert good.mean() > 0.9 and np.median(e) < 0.06
+
+
+def test_lk_track_1080p_known_motion(gpu_available):
+    """Full-size frame (1920 x 1080, the stream's size), 2000 points: tracked against the true motion."""
+    import ptzba
+    I, J, H = frontend_data.textured_pair(seed=4, width=1920, height=1080, f=2500.0, d_pan=0.25, d_tilt=0.1)
+    p = _lk_points(4, 2000, 1920, 1080, margin=30)
+    nxt, st, err = ptzba.lk_track(I, J, p)
+    e = np.linalg.norm(nxt - frontend_data.apply_h(H, p.astype(np.float64)), axis=1)
+    assert st.all() and np.median(e) < 0.05 and np.percentile(e, 99) < 0.3 and err.max() < 8
+    # the oracle on a subset
+    _lk_compare(I, J, p[:100])
+
+
+def test_lk_track_edge_cases(gpu_available):
+    import ptzba
+    I, J, _ = frontend_data.textured_pair(seed=5)
+    nxt, st, err = ptzba.lk_track(I, J, np.zeros((0, 2), np.float32))
+    assert nxt.shape == (0, 2) and st.shape == (0,)
+    flat = np.full((64, 64), 90, np.uint8)
+    nxt, st, err = ptzba.lk_track(flat, flat, np.array([[30.0, 30.0]], np.float32))
+    assert st[0] == 0 and np.isinf(err[0])
+    with pytest.raises(ptzba.PtzbaError):
+        ptzba.lk_track(I, J, np.array([[5.0, 5.0]], np.float32), win=32)
+    with pytest.raises(ValueError):
+        ptzba.lk_track(I, J[:10], np.array([[5.0, 5.0]], np.float32))
+
+
+def test_optical_flow_matching_gpu(gpu_available):
+    """image_process.optical_flow_matching (GPU default) as image_process.py:393-415 calls it: points with
+    err < 20 strictly inside the image, in order, and their next positions; colour input converts to grey."""
+    import image_process
+    from oracle import ptz_oracle as orc
+    I, J, H = frontend_data.textured_pair(seed=6, width=480, height=270, d_pan=1.2)
+    p = _lk_points(6, 400, 480, 270, margin=2).astype(np.float64)
+    idx, nxt = image_process.optical_flow_matching(I, J, p)
+    rn, rst, rerr = orc.lk_track(I, J, p)
+    keep = (rst == 1) & (rerr < 20) & (rn[:, 0] > 0) & (rn[:, 0] < 480) & (rn[:, 1] > 0) & (rn[:, 1] < 270)
+    assert len(set(idx) ^ set(np.flatnonzero(keep).tolist())) <= 2
+    assert nxt.shape == (len(idx), 2) and idx == sorted(idx)
+    idx3, nxt3 = image_process.optical_flow_matching(np.dstack([I] * 3), np.dstack([J] * 3), p)
+    assert idx3 == idx and np.array_equal(nxt3, nxt)
