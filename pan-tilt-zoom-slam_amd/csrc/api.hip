@@ -780,8 +780,7 @@ static void tables(ptzba_ctx* h, const double* ptz, const double* rays, const in
 }
 
 // sel != nullptr (device-driven LM): the kernel writes slot (*sel ^ sel_xor), chosen on the device
-static void linearize_into(ptzba_ctx* h, int slot, const int* run_if = nullptr, const int* sel = nullptr,
-                           int sel_xor = 0) {
+static void linearize_into(ptzba_ctx* h, int slot, const int* sel = nullptr, int sel_xor = 0) {
   LinArgs a;
   a.lm_work = h->lm_order.as<int4>();
   a.n_work = h->n_work;
@@ -805,7 +804,6 @@ static void linearize_into(ptzba_ctx* h, int slot, const int* run_if = nullptr, 
   a.w_slot = h->w_slot[slot].p;
   a.lm_meta = h->lm_meta.as<int4>();
   a.lm_out = h->lm_out[slot].as<double>();
-  a.run_if = run_if;
   a.sel = sel;
   a.sel_xor = sel_xor;
   if (sel) {
@@ -816,12 +814,12 @@ static void linearize_into(ptzba_ctx* h, int slot, const int* run_if = nullptr, 
   a.ug_slot1 = h->ug_slot[1].p;
   a.w_slot1 = h->w_slot[1].p;
   a.lm_out1 = h->lm_out[1].as<double>();
-  if (!run_if) tm_begin(h, TM_K1);  // conditional re-linearisations are not timed (often no-ops)
+  tm_begin(h, TM_K1);
   if (h->precision == PTZBA_FP32)
     launch_linearize<float>(a, h->loss, h->st);
   else
     launch_linearize<double>(a, h->loss, h->st);
-  if (!run_if) tm_end(h, TM_K1);
+  tm_end(h, TM_K1);
 }
 
 int ptzba_solver_info(ptzba_handle h, int64_t* info8) {
@@ -1014,7 +1012,7 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
                          h->loc.as<double>(), h->n_pose, h->ft64.p, h->rt64.p, h->ft64.p, h->rt64.p, h->st);
   tm_end(h, TM_BACK);
   // trial linearisation (its cost decides acceptance; kept as the next linearisation if accepted)
-  linearize_into(h, nx, nullptr, sel, 1);
+  linearize_into(h, nx, sel, 1);
   // scal[1] (trial cost) and scal[2..4] are overwritten below, loc[0..3] by the trial kernel: no memsets
   launch_reduce_cols(h->lm_out[sel ? 0 : nx].as<double>() + 5, h->n_lm, 8, 1, 0, h->scal.as<double>() + 1,
                      h->red_scratch.as<double>(), h->st, h->lm_red.as<double>(), 4, 3, h->scal.as<double>() + 2,

@@ -83,6 +83,9 @@ constexpr int SEGW = K1_SEGW;  // segments per LDS window per wave
 #ifndef K1_COARSE64
 #define K1_COARSE64 K1_COARSE  // the same choice for the fp64 instantiation
 #endif
+#ifndef K1_TAIL_ATOMIC
+#define K1_TAIL_ATOMIC 0  // 1: tail-run adds of the coarsened reduction as LDS atomics (7 us slower at config 3)
+#endif
 #ifndef K1_MIN_WAVES
 #define K1_MIN_WAVES 4  // waves per SIMD the register budget must allow (occupancy)
 #endif
@@ -127,9 +130,7 @@ __device__ __forceinline__ void store4(double* p, double a, double b, double c, 
   reinterpret_cast<double2*>(p)[1] = make_double2(c, d);
 }
 
-// RELIN: the conditional re-linearisation after a rejected trial of the device-driven LM (a separate
-// instantiation, so profiles and K1 timings see only the unconditional launches)
-template <typename real, int LOSS, bool RELIN>
+template <typename real, int LOSS>
 __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVES64) void k_linearize(LinArgs a) {
   constexpr bool COARSE = sizeof(real) == 4 ? K1_COARSE : K1_COARSE64;
   __shared__ real s_x[4][SEGW], s_y[4][SEGW], s_acc[4][4][SEGW];
@@ -137,7 +138,6 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
   const int wv = threadIdx.x >> 6;
   const int task = blockIdx.x * 4 + wv;
   if (task >= a.n_work) return;  // whole wave leaves; no block-level barriers in this kernel
-  if (RELIN && !*a.run_if) return;  // device-driven LM: re-linearisation only after a rejected trial
   // one 16-B work descriptor {landmark, first segment, end segment, first record}: no dependent
   // lm_order -> lm_seg_begin -> seg_rec_begin chain before the records can be requested
   const int4 wd = a.lm_work[task];
@@ -324,9 +324,17 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
     seg_scan_step<DPP_ROW_BCAST15, 0xa>(kenc, t0, t1, t2, t3);
     seg_scan_step<DPP_ROW_BCAST31, 0xc>(kenc, t0, t1, t2, t3);
     const int knext = dpp_i<DPP_WAVE_SHL1, 0xf>(kenc);
-    // LDS atomic (no-return ds_add): the next lane's head run may add into the same slot in this batch
+    // The next lane's head run may have added into the same slot above (ds_add).  A wave's LDS operations
+    // execute in issue order, so a plain read-modify-write issued after those adds sees them; the compiler
+    // must not hoist the read above them (per lane it can prove key[j] != kt, but the adds of OTHER lanes
+    // alias), hence the compiler barrier.  K1_TAIL_ATOMIC=1 keeps the atomic form.
     if (knext != kenc && kt >= 0 && kt < SEGW) {
+#if K1_TAIL_ATOMIC
       atomicAdd(acc0 + kt, t0); atomicAdd(acc1 + kt, t1); atomicAdd(acc2 + kt, t2); atomicAdd(acc3 + kt, t3);
+#else
+      asm volatile("" ::: "memory");
+      acc0[kt] += t0; acc1[kt] += t1; acc2[kt] += t2; acc3[kt] += t3;
+#endif
     }
   };
 
@@ -440,14 +448,8 @@ template <typename real>
 void launch_linearize(const LinArgs& a, int loss, hipStream_t st) {
   if (a.n_work <= 0) return;
   dim3 grid((a.n_work + 3) / 4);
-  const bool relin = a.run_if != nullptr;
-  if (loss == 0) {
-    if (relin) hipLaunchKernelGGL((k_linearize<real, 0, true>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((k_linearize<real, 0, false>), grid, dim3(256), 0, st, a);
-  } else {
-    if (relin) hipLaunchKernelGGL((k_linearize<real, 1, true>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((k_linearize<real, 1, false>), grid, dim3(256), 0, st, a);
-  }
+  if (loss == 0) hipLaunchKernelGGL((k_linearize<real, 0>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((k_linearize<real, 1>), grid, dim3(256), 0, st, a);
 }
 
 // ------------------------------------------------------------------------------------------------

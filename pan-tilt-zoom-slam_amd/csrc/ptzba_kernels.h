@@ -23,7 +23,6 @@ struct LinArgs {
   const double2* seg_base;       // [n_seg] base observation; records hold obs - base (real)
   double u, v, fs2, inv_fs2;
   void* ug_slot;                 // [n_slot][12] real: U (6) | g_pose (3) | 0 0 0 (dense slots)
-  const int* run_if;             // nullptr, or: skip the launch when *run_if == 0 (device-driven LM)
   void* w_slot;                  // [n_slot][8] real: W (6) | 0 0 at slot toff_l + frame - first_l
   const int4* lm_meta;           // [n_lm] {first frame, last frame, slot offset, 0}
   double* lm_out;                // [n_lm][8]
