@@ -74,9 +74,6 @@ constexpr int SEGW = K1_SEGW;  // segments per LDS window per wave
 #ifndef K1_UNROLL
 #define K1_UNROLL 3  // record batches per group (two groups in flight per wave)
 #endif
-#ifndef K1_FTV
-#define K1_FTV 1  // phase-C frame tables loaded during phase A
-#endif
 #ifndef K1_COARSE
 #define K1_COARSE 1  // 0: 1 record per lane per batch; 1: 4 records per lane per batch, one scan per 256 records
 #endif
@@ -111,6 +108,20 @@ __device__ __forceinline__ double dpp_r(double x) {
 constexpr int DPP_ROW_SHR1 = 0x111, DPP_ROW_SHR2 = 0x112, DPP_ROW_SHR4 = 0x114, DPP_ROW_SHR8 = 0x118;
 constexpr int DPP_ROW_BCAST15 = 0x142, DPP_ROW_BCAST31 = 0x143, DPP_WAVE_SHL1 = 0x130;
 
+// Wave total by a DPP inclusive scan (VALU only): the sum is valid in lane 63.  Needs every lane active.
+// The butterfly of wave_sum costs one LDS round trip (ds_bpermute) per step and value: at the end of K1
+// six fp64 butterflies took ~5K cycles per wave, 15 % of the wave's time (K1_TIMING build).
+template <typename T>
+__device__ __forceinline__ T wave_total(T v) {
+  v += dpp_r<DPP_ROW_SHR1, 0xf>(v);
+  v += dpp_r<DPP_ROW_SHR2, 0xf>(v);
+  v += dpp_r<DPP_ROW_SHR4, 0xf>(v);
+  v += dpp_r<DPP_ROW_SHR8, 0xf>(v);
+  v += dpp_r<DPP_ROW_BCAST15, 0xa>(v);
+  v += dpp_r<DPP_ROW_BCAST31, 0xc>(v);
+  return v;
+}
+
 // one Kogge-Stone step of the segmented inclusive scan (keys sorted within the wave; kenc >= 1)
 template <int CTRL, int ROWMASK, typename real>
 __device__ __forceinline__ void seg_scan_step(int kenc, real& v0, real& v1, real& v2, real& v3) {
@@ -130,6 +141,16 @@ __device__ __forceinline__ void store4(double* p, double a, double b, double c, 
   reinterpret_cast<double2*>(p)[1] = make_double2(c, d);
 }
 
+#ifdef K1_TIMING
+// phase timing build (tools/k1_timing.py): per task (plain stores, no shared counters: same-address atomics
+// from every wave would serialise the launch) start / end stamps (s_memrealtime) and clock64 phase sums
+__device__ long long g_k1_items[32768][8];  // start, end, A, B, C, final, segments, -
+#define K1_NOW(t) do { t = clock64(); } while (0)
+#define K1_ACC(k, t0, t1) do { k1acc[k] += (t1) - (t0); } while (0)
+#else
+#define K1_NOW(t) do { } while (0)
+#define K1_ACC(k, t0, t1) do { } while (0)
+#endif
 template <typename real, int LOSS>
 __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVES64) void k_linearize(LinArgs a) {
   constexpr bool COARSE = sizeof(real) == 4 ? K1_COARSE : K1_COARSE64;
@@ -138,22 +159,30 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
   const int wv = threadIdx.x >> 6;
   const int task = blockIdx.x * 4 + wv;
   if (task >= a.n_work) return;  // whole wave leaves; no block-level barriers in this kernel
-  // one 16-B work descriptor {landmark, first segment, end segment, first record}: no dependent
-  // lm_order -> lm_seg_begin -> seg_rec_begin chain before the records can be requested
-  const int4 wd = a.lm_work[task];
+  long long kt0 = 0, kt1 = 0, kt2 = 0, kt3 = 0, kt4 = 0, k1acc[4] = {0, 0, 0, 0};
+  (void)kt0; (void)kt1; (void)kt2; (void)kt3; (void)kt4; (void)k1acc;
+  K1_NOW(kt0);
+#ifdef K1_TIMING
+  if (lane == 0 && task < 32768) g_k1_items[task][0] = __builtin_amdgcn_s_memrealtime();
+#endif
+  // one 32-B work descriptor {landmark, first segment, end segment, first record | first frame, last
+  // frame, slot offset, 0}: no dependent lm_order -> lm_seg_begin -> seg_rec_begin -> lm_meta chain before
+  // the records and the frame tables can be requested
+  const int4 wd = a.lm_work[2 * task];
+  const int4 wm = a.lm_work[2 * task + 1];
   const int l = wd.x, s0 = wd.y, s1 = wd.z;
-  const FrameTab<real>* __restrict__ ft = (const FrameTab<real>*)a.ft;
-  const RayTab<real> R = ((const RayTab<real>*)a.rt)[l];
   const FrameTab<double>* __restrict__ ft64 = (const FrameTab<double>*)a.ft64;
   const RayTab<double> R64 = ((const RayTab<double>*)a.rt64)[l];
+  RayTab<real> R;  // the record-precision table is the rounded fp64 one (k_tables)
+  R.p0 = (real)R64.p0; R.p1 = (real)R64.p1; R.d0t = (real)R64.d0t; R.d1t = (real)R64.d1t; R.d1p = (real)R64.d1p;
+  const FrameTab<real>* __restrict__ ft = (const FrameTab<real>*)a.ft;
   const double2* __restrict__ seg_base = a.seg_base;
   const real* __restrict__ rec_xy = (const real*)a.rec_xy;
   const real* __restrict__ rec_w = (const real*)a.rec_w;
   const bool alt = a.sel && ((*a.sel ^ a.sel_xor) & 1);  // device-chosen linearisation slot
   real* __restrict__ ug_slot = (real*)(alt ? a.ug_slot1 : a.ug_slot);
   real* __restrict__ w_slot = (real*)(alt ? a.w_slot1 : a.w_slot);
-  const int4 lmeta = a.lm_meta[l];  // {first frame, last frame, slot offset, 0}
-  const int64_t slot0 = (int64_t)lmeta.z - lmeta.x;
+  const int64_t slot0 = (int64_t)wm.z - wm.x;
   const real u = (real)a.u, v = (real)a.v;
   const real fs2 = (real)a.fs2, ifs2 = (real)a.inv_fs2;
   real* sx = s_x[wv];
@@ -351,12 +380,7 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
     // offset from the segment's base observation so phase B works on O(residual) magnitudes.  The
     // frame ids and the phase-C frame tables stay in registers.
     int fsv[SEGW / WAVE];
-    FrameTab<real> ftv[SEGW / WAVE];
-#if K1_FTV
-#define K1_FTV_PREFETCH(i) ftv[i] = ft[fsv[i]]
-#else
-#define K1_FTV_PREFETCH(i) (void)0
-#endif
+    FrameTab<real> ftv[SEGW / WAVE];  // phase C's frame tables, loaded here (off phase C's path)
 #pragma unroll
     for (int i = 0; i < SEGW / WAVE; ++i) {
       const int s = w0 + lane + i * WAVE;
@@ -372,9 +396,11 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
         sy[sl] = (real)(y - bs.y);
         acc0[sl] = 0; acc1[sl] = 0; acc2[sl] = 0; acc3[sl] = 0;
       }
-      K1_FTV_PREFETCH(i);
+      ftv[i] = ft[fsv[i]];
     }
     wave_lds_fence();
+    K1_NOW(kt1);
+    K1_ACC(0, kt0, kt1);
     // phase B: stream the window's records (coalesced), segmented reduction into LDS.  Two register
     // groups alternate: the next group's loads are in flight while the current one is consumed.
     if constexpr (COARSE) {
@@ -395,6 +421,8 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
       }
     }
     wave_lds_fence();
+    K1_NOW(kt2);
+    K1_ACC(1, kt1, kt2);
     // phase C: per-segment Jacobian and normal-equation blocks
 #pragma unroll
     for (int i = 0; i < SEGW / WAVE; ++i) {
@@ -403,11 +431,7 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
       const int sl = s - w0;
       real x, y, J[2][5];
       const int fs = fsv[i];
-#if K1_FTV
       ptz_project_jac<real>(ftv[i], R, u, v, x, y, J);
-#else
-      ptz_project_jac<real>(ft[fs], R, u, v, x, y, J);
-#endif
       const real Sx = acc0[sl], Sy = acc1[sl], Srx = acc2[sl], Sry = acc3[sl];
       // W = Jp^T diag(Sx,Sy) Jr (3x2), U = Jp^T diag Jp (upper: 00 01 02 11 12 22), g_pose = Jp^T (w r)
       real W[6];
@@ -435,13 +459,25 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
       g1 += (double)(J[0][4] * Srx + J[1][4] * Sry);
     }
     wave_lds_fence();
+    K1_NOW(kt3);
+    K1_ACC(2, kt2, kt3);
+    kt0 = kt3;
   }
-  V00 = wave_sum(V00); V01 = wave_sum(V01); V11 = wave_sum(V11);
-  g0 = wave_sum(g0); g1 = wave_sum(g1); cost = wave_sum(cost);
-  if (lane == 0) {
+  V00 = wave_total(V00); V01 = wave_total(V01); V11 = wave_total(V11);
+  g0 = wave_total(g0); g1 = wave_total(g1); cost = wave_total(cost);
+  if (lane == WAVE - 1) {
     double* o = (alt ? a.lm_out1 : a.lm_out) + (int64_t)l * 8;
     o[0] = V00; o[1] = V01; o[2] = V11; o[3] = g0; o[4] = g1; o[5] = 0.5 * cost; o[6] = 0; o[7] = 0;
   }
+#ifdef K1_TIMING
+  K1_NOW(kt4);
+  K1_ACC(3, kt3, kt4);
+  if (lane == 0 && task < 32768) {
+    g_k1_items[task][1] = __builtin_amdgcn_s_memrealtime();
+    for (int k = 0; k < 4; ++k) g_k1_items[task][2 + k] = k1acc[k];
+    g_k1_items[task][6] = s1 - s0;
+  }
+#endif
 }
 
 template <typename real>
@@ -602,9 +638,9 @@ __global__ __launch_bounds__(256) void k_trial(BacksubArgs a, PoseTrialArgs pa, 
       t1 += (double)w[2 * q + 1] * dp[q];
     }
   }
-  t0 = wave_sum(t0);
-  t1 = wave_sum(t1);
-  if (lane == 0) {
+  t0 = wave_total(t0);
+  t1 = wave_total(t1);
+  if (lane == WAVE - 1) {
     double* red = a.lm_red + (int64_t)l * 4;
     const double th = a.rays[2 * l], ph = a.rays[2 * l + 1];
     double nth = th, nph = ph;
@@ -893,3 +929,13 @@ template void launch_residual<double>(const int32_t*, const int32_t*, const int3
                                       hipStream_t);
 
 }  // namespace ptzba
+
+#ifdef K1_TIMING
+// the first n tasks' records of the last launch: [start, end (s_memrealtime, 100 MHz), cycles in phase A
+// (incl. the descriptor), B, C, final, segments, -]
+extern "C" int ptzba_debug_k1(long long* items, int n) {
+  if (hipMemcpyFromSymbol(items, HIP_SYMBOL(ptzba::g_k1_items), (size_t)(n < 32768 ? n : 32768) * 64) != hipSuccess)
+    return -1;
+  return 0;
+}
+#endif

@@ -7,7 +7,7 @@ namespace ptzba {
 
 constexpr int K1_SEGW = 128;  // K1 segments per LDS window per wave
 struct LinArgs {
-  const int4* lm_work;           // [n_work] {landmark, s0, s1, first record}, heaviest first
+  const int4* lm_work;           // [2 n_work] {landmark, s0, s1, first record}, {lm_meta}, heaviest first
   int n_work;
   const int32_t* lm_seg_begin;   // [n_lm+1]
   const int32_t* seg_frame;      // [n_seg]
