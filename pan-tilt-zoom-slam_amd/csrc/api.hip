@@ -636,7 +636,8 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->n_work = (int)lm_order.size();
   h->max_seg_per_lm = max_seg;
   if (n_obs >= ((int64_t)1 << 31)) return fail("n_obs %lld exceeds the 2^31 record limit of a handle (shard it)", (long long)n_obs);
-  // K1 work descriptors, 32 B: {landmark, first segment, end segment, first record | lm_meta}
+  // K1 work descriptors, 32 B: {landmark, first segment, end segment, first record | first frame, last
+  // frame, slot offset (lm_meta), end record of the first K1_SEGW-segment window}
   std::vector<int32_t> lm_work(8 * (size_t)h->n_work);
   for (int k = 0; k < h->n_work; ++k) {
     const int l = lm_order[k];
@@ -644,7 +645,8 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     lm_work[8 * k + 1] = lm_seg_begin[l];
     lm_work[8 * k + 2] = lm_seg_begin[l + 1];
     lm_work[8 * k + 3] = (int32_t)seg_rec_begin[lm_seg_begin[l]];
-    for (int q = 0; q < 4; ++q) lm_work[8 * k + 4 + q] = lm_meta[4 * l + q];
+    for (int q = 0; q < 3; ++q) lm_work[8 * k + 4 + q] = lm_meta[4 * l + q];
+    lm_work[8 * k + 7] = (int32_t)seg_rec_begin[std::min(lm_seg_begin[l + 1], lm_seg_begin[l] + K1_SEGW)];
   }
   h->n_sys = 3 * (n_pose - o.n_fixed);
   // system order and factorisation plan (from the coupling window; a sharded problem passes the global one)

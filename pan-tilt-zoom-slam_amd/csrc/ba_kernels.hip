@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
   if (lane == 0 && task < 32768) g_k1_items[task][0] = __builtin_amdgcn_s_memrealtime();
 #endif
   // one 32-B work descriptor {landmark, first segment, end segment, first record | first frame, last
-  // frame, slot offset, 0}: no dependent lm_order -> lm_seg_begin -> seg_rec_begin -> lm_meta chain before
+  // frame, slot offset, end record of the first window}: no dependent lm_order -> lm_seg_begin -> seg_rec_begin -> lm_meta chain before
   // the records and the frame tables can be requested
   const int4 wd = a.lm_work[2 * task];
   const int4 wm = a.lm_work[2 * task + 1];
@@ -369,13 +369,18 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
 
   for (int w0 = s0; w0 < s1; w0 += SEGW) {
     const int w1 = min(s1, w0 + SEGW);
+    // the first window's record range comes with the descriptor (no dependent load before the records)
     const int64_t r0 = (w0 == s0) ? (int64_t)(uint32_t)wd.w : a.seg_rec_begin[w0];
-    const int64_t r1 = a.seg_rec_begin[w1];
+    const int64_t r1 = (w0 == s0) ? (int64_t)(uint32_t)wm.w : a.seg_rec_begin[w1];
     // the window's first record group is requested before phase A: its latency overlaps the projections
     CGrp ca, cb;
     Grp ga, gb;
-    if constexpr (COARSE) load_cgrp(ca, r0 & ~(int64_t)3, r1);
-    else load_grp(ga, r0, r1);
+    const int64_t rb0 = r0 & ~(int64_t)3;
+    if constexpr (COARSE) {
+      load_cgrp(ca, rb0, r1);
+    } else {
+      load_grp(ga, r0, r1);
+    }
     // phase A: fp64 projection of every segment of the window (lanes over segments), kept as the
     // offset from the segment's base observation so phase B works on O(residual) magnitudes.  The
     // frame ids and the phase-C frame tables stay in registers.
@@ -403,6 +408,8 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
     K1_ACC(0, kt0, kt1);
     // phase B: stream the window's records (coalesced), segmented reduction into LDS.  Two register
     // groups alternate: the next group's loads are in flight while the current one is consumed.
+    // (An LDS-DMA ring of 3 batches per wave, global_load_lds, was measured slower: hipcc puts a
+    // vmcnt(0) -- every pending DMA -- in front of each LDS write of the reduction)
     if constexpr (COARSE) {
       for (int64_t rb = r0 & ~(int64_t)3; rb < r1; rb += 2 * 4 * WAVE) {
         load_cgrp(cb, rb + 4 * WAVE, r1);
