@@ -83,6 +83,12 @@ constexpr int SEGW = K1_SEGW;  // segments per LDS window per wave
 #ifndef K1_TAIL_ATOMIC
 #define K1_TAIL_ATOMIC 0  // 1: tail-run adds of the coarsened reduction as LDS atomics (7 us slower at config 3)
 #endif
+#ifndef K1_FTV_LATE
+#define K1_FTV_LATE 0  // 1: phase C loads its frame tables itself (frees registers; measured slower)
+#endif
+#ifndef K1_DEPTH
+#define K1_DEPTH 2  // fp32 coarsened path: record groups in flight per wave (3: same phase B time, more registers)
+#endif
 #ifndef K1_MIN_WAVES
 #define K1_MIN_WAVES 4  // waves per SIMD the register budget must allow (occupancy)
 #endif
@@ -298,6 +304,7 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
   auto consume_c = [&](const CGrp& g, int64_t rb, int64_t r0, int64_t r1) {
     int key[4];
     real v[4][4];
+    real cb = 0;  // the batch's cost terms, summed in the record precision, then added in fp64
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t idx = rb + 4 * lane + j;
@@ -329,9 +336,10 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
         }
         c = wt * fs2 * ((ix ? zx : (real)2 * sqx - (real)1) + (iy ? zy : (real)2 * sqy - (real)1));
       }
-      cost += (double)c;
+      cb += c;
       v[j][0] = wx; v[j][1] = wy; v[j][2] = wx * rx; v[j][3] = wy * ry;
     }
+    cost += (double)cb;
     // the lane's tail run (key of its last record) joins the scan; earlier runs are the lane's alone
     // unless they continue a previous lane's tail: LDS atomic adds for those
     const int kt = key[3];
@@ -373,10 +381,14 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
     const int64_t r0 = (w0 == s0) ? (int64_t)(uint32_t)wd.w : a.seg_rec_begin[w0];
     const int64_t r1 = (w0 == s0) ? (int64_t)(uint32_t)wm.w : a.seg_rec_begin[w1];
     // the window's first record group is requested before phase A: its latency overlaps the projections
-    CGrp ca, cb;
+    CGrp ca, cb, cc;
     Grp ga, gb;
     const int64_t rb0 = r0 & ~(int64_t)3;
-    if constexpr (COARSE) {
+    constexpr bool D3 = COARSE && K1_DEPTH == 3 && sizeof(real) == 4;
+    if constexpr (D3) {
+      load_cgrp(ca, rb0, r1);
+      load_cgrp(cb, rb0 + 4 * WAVE, r1);
+    } else if constexpr (COARSE) {
       load_cgrp(ca, rb0, r1);
     } else {
       load_grp(ga, r0, r1);
@@ -385,7 +397,9 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
     // offset from the segment's base observation so phase B works on O(residual) magnitudes.  The
     // frame ids and the phase-C frame tables stay in registers.
     int fsv[SEGW / WAVE];
+#if !K1_FTV_LATE
     FrameTab<real> ftv[SEGW / WAVE];  // phase C's frame tables, loaded here (off phase C's path)
+#endif
 #pragma unroll
     for (int i = 0; i < SEGW / WAVE; ++i) {
       const int s = w0 + lane + i * WAVE;
@@ -401,7 +415,11 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
         sy[sl] = (real)(y - bs.y);
         acc0[sl] = 0; acc1[sl] = 0; acc2[sl] = 0; acc3[sl] = 0;
       }
-      ftv[i] = ft[fsv[i]];
+#if !K1_FTV_LATE
+      // the five used fields only (not the 32-B struct)
+      const FrameTab<real>* fp = ft + fsv[i];
+      ftv[i].ca = fp->ca; ftv[i].sa = fp->sa; ftv[i].cb = fp->cb; ftv[i].sb = fp->sb; ftv[i].f = fp->f;
+#endif
     }
     wave_lds_fence();
     K1_NOW(kt1);
@@ -410,7 +428,20 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
     // groups alternate: the next group's loads are in flight while the current one is consumed.
     // (An LDS-DMA ring of 3 batches per wave, global_load_lds, was measured slower: hipcc puts a
     // vmcnt(0) -- every pending DMA -- in front of each LDS write of the reduction)
-    if constexpr (COARSE) {
+    if constexpr (D3) {
+      // three groups rotate: two requested before phase A, the third here; a group is refilled right
+      // after it is consumed, two batches ahead
+      for (int64_t rb = rb0; rb < r1; rb += 3 * 4 * WAVE) {
+        load_cgrp(cc, rb + 2 * 4 * WAVE, r1);
+        consume_c(ca, rb, r0, r1);
+        if (rb + 4 * WAVE >= r1) break;
+        load_cgrp(ca, rb + 3 * 4 * WAVE, r1);
+        consume_c(cb, rb + 4 * WAVE, r0, r1);
+        if (rb + 2 * 4 * WAVE >= r1) break;
+        load_cgrp(cb, rb + 4 * 4 * WAVE, r1);
+        consume_c(cc, rb + 2 * 4 * WAVE, r0, r1);
+      }
+    } else if constexpr (COARSE) {
       for (int64_t rb = r0 & ~(int64_t)3; rb < r1; rb += 2 * 4 * WAVE) {
         load_cgrp(cb, rb + 4 * WAVE, r1);
         consume_c(ca, rb, r0, r1);
@@ -438,7 +469,11 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
       const int sl = s - w0;
       real x, y, J[2][5];
       const int fs = fsv[i];
+#if K1_FTV_LATE
+      ptz_project_jac<real>(ft[fs], R, u, v, x, y, J);
+#else
       ptz_project_jac<real>(ftv[i], R, u, v, x, y, J);
+#endif
       const real Sx = acc0[sl], Sy = acc1[sl], Srx = acc2[sl], Sry = acc3[sl];
       // W = Jp^T diag(Sx,Sy) Jr (3x2), U = Jp^T diag Jp (upper: 00 01 02 11 12 22), g_pose = Jp^T (w r)
       real W[6];
