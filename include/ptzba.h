@@ -245,6 +245,14 @@ PTZBA_EXPORT int ptz_lk_track(int device, int32_t width, int32_t height, const u
                               int64_t n, const float* pts0, int32_t levels, int32_t win, int32_t max_iter, double eps,
                               double min_eig, float* pts1_out, uint8_t* status_out, float* err_out);
 
+/* SIFT keypoints and descriptors (cv.xfeatures2d.SIFT_create(nfeatures).detectAndCompute as detect_compute_sift calls
+ * it, image_process.py:56-79): img 8-bit grey width x height; OpenCV's defaults (image doubled, 3 layers per octave,
+ * sigma 1.6, contrast 0.04, edge 10).  Keypoints ordered by (-response, y, x, angle) and cut to nfeatures (> 0;
+ * 0 keeps all); *n_out = their number, of which the first min(n, max_kp) are written: kp_out [.][4] = (x, y, size,
+ * angle in degrees), response_out [.] (may be NULL), des_out [.][128] (integer values 0..255 as float). */
+PTZBA_EXPORT int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int32_t nfeatures, int32_t max_kp,
+                          float* kp_out, float* response_out, float* des_out, int32_t* n_out);
+
 /* Coupling window of a record set (host only, O(n_obs)): win_out[f] = the highest frame that shares a
  * landmark with frame f (>= f).  Computed over ALL records it is the frame_win_hi every rank of a
  * landmark-sharded solve passes in ptzba_problem_opts. */

@@ -711,3 +711,307 @@ def lk_track(img0, img1, pts, win=31, levels=4, max_iter=30, eps=0.01, min_eig=1
                  bilinear(J[0], nxt[:, :1] + ox, nxt[:, 1:] + oy)).sum(1) / area
     inside = (nxt[:, 0] >= 0) & (nxt[:, 1] >= 0) & (nxt[:, 0] <= w - 1) & (nxt[:, 1] <= h - 1)
     return nxt, (ok & inside).astype(np.uint8), np.where(ok, err, np.inf)
+
+
+# ---------------------------------------------------------------------------------------------
+# SIFT detection + description (cv.xfeatures2d.SIFT_create(nfeatures).detectAndCompute, detect_compute_sift,
+# image_process.py:56-79).  OpenCV is not installed here: this restates Lowe's algorithm with OpenCV's
+# defaults (3 layers per octave, contrast 0.04, edge 10, sigma 1.6, input blur 0.5, image doubled first) as
+# ptz_sift implements it (include/ptzba.h); parity of the GPU path is pinned to THIS restatement and to
+# repeatability under known homographies -- agreement with cv2's keypoints is unpinned.  Deliberate
+# differences from OpenCV: exact atan2 instead of fastAtan2, keypoints ordered by (-response, y, x, angle)
+# before the nfeatures cut.  The Gaussian pyramid is float32 with the GPU's operation order (bit-exact).
+# ---------------------------------------------------------------------------------------------
+SIFT_LAYERS, SIFT_CONTRAST, SIFT_EDGE, SIFT_SIGMA, SIFT_INIT_SIGMA = 3, 0.04, 10.0, 1.6, 0.5
+SIFT_BORDER, SIFT_MAX_INTERP, SIFT_ORI_BINS, SIFT_ORI_PEAK = 5, 5, 36, 0.8
+SIFT_D, SIFT_N = 4, 8
+
+
+def sift_gauss_kernel(sigma):
+    """Separable Gaussian weights (float32) as the host passes them to the GPU: size round(8 sigma + 1) | 1."""
+    k = int(round(sigma * 8 + 1)) | 1
+    r = k // 2
+    w = [math.exp(-float(i - r) * float(i - r) / (2.0 * sigma * sigma)) for i in range(k)]  # libm exp, as the host
+    s = 0.0
+    for v in w:
+        s += v
+    return np.array([v / s for v in w], np.float64).astype(np.float32)
+
+
+def _refl101(i, n):
+    if n == 1:
+        return np.zeros_like(i)
+    p = 2 * n - 2
+    i = np.abs(i) % p
+    return np.where(i >= n, p - i, i)
+
+
+def sift_blur(img, sigma):
+    """Row then column pass, reflect-101 border, float32 accumulation k = 0..K-1 (mul, then add)."""
+    w = sift_gauss_kernel(sigma)
+    r = len(w) // 2
+    h, wd = img.shape
+    img = img.astype(np.float32)
+    xs = np.arange(wd)
+    acc = np.zeros_like(img)
+    for k in range(len(w)):
+        acc = acc + w[k] * img[:, _refl101(xs + k - r, wd)]
+    ys = np.arange(h)
+    out = np.zeros_like(acc)
+    for k in range(len(w)):
+        out = out + w[k] * acc[_refl101(ys + k - r, h), :]
+    return out
+
+
+def sift_upscale(img):
+    """2x bilinear (OpenCV INTER_LINEAR centres: src = dst / 2 - 0.25), float32, clamped at the border."""
+    h, w = img.shape
+    img = img.astype(np.float32)
+
+    def coords(n_src, n_dst):
+        s = np.arange(n_dst, dtype=np.float32) * np.float32(0.5) - np.float32(0.25)
+        i0 = np.floor(s).astype(np.int64)
+        a = (s - i0).astype(np.float32)
+        lo = i0 < 0
+        a[lo] = 0
+        i0[lo] = 0
+        hi = i0 >= n_src - 1
+        a[hi] = 0
+        i0[hi] = n_src - 1
+        return i0, np.minimum(i0 + 1, n_src - 1), a
+    x0, x1, ax = coords(w, 2 * w)
+    y0, y1, ay = coords(h, 2 * h)
+    one = np.float32(1)
+    top = (one - ax)[None, :] * img[y0][:, x0] + ax[None, :] * img[y0][:, x1]
+    bot = (one - ax)[None, :] * img[y1][:, x0] + ax[None, :] * img[y1][:, x1]
+    return (one - ay)[:, None] * top + ay[:, None] * bot
+
+
+def sift_pyramid(img_u8):
+    """Gaussian pyramid [octave][S + 3] and DoG pyramid [octave][S + 2] (float32)."""
+    S = SIFT_LAYERS
+    base = sift_upscale(np.asarray(img_u8, np.float32))
+    base = sift_blur(base, np.sqrt(max(SIFT_SIGMA ** 2 - (2 * SIFT_INIT_SIGMA) ** 2, 0.01)))
+    n_oct = int(round(np.log2(min(base.shape)) - 2))
+    k = 2.0 ** (1.0 / S)
+    sig = [SIFT_SIGMA]
+    for i in range(1, S + 3):
+        prev = (k ** (i - 1)) * SIFT_SIGMA
+        sig.append(np.sqrt((prev * k) ** 2 - prev ** 2))
+    gp, dp = [], []
+    for o in range(n_oct):
+        lv = [base if o == 0 else gp[o - 1][S][::2, ::2][:gp[o - 1][S].shape[0] // 2, :gp[o - 1][S].shape[1] // 2]]
+        for i in range(1, S + 3):
+            lv.append(sift_blur(lv[-1], sig[i]))
+        gp.append(lv)
+        dp.append([lv[i + 1] - lv[i] for i in range(S + 2)])
+    return gp, dp
+
+
+def _sift_refine(D, o, l, r, c):
+    """adjustLocalExtrema in fp64; returns (l, r, c, xi, xr, xc, contr) or None."""
+    S = SIFT_LAYERS
+    sc = 1.0 / 255.0
+    ds, s2, cs = sc * 0.5, sc, sc * 0.25
+    rows, cols = D[0].shape
+    for it in range(SIFT_MAX_INTERP):
+        P, C, N = D[l - 1].astype(np.float64), D[l].astype(np.float64), D[l + 1].astype(np.float64)
+        dD = np.array([(C[r, c + 1] - C[r, c - 1]) * ds, (C[r + 1, c] - C[r - 1, c]) * ds, (N[r, c] - P[r, c]) * ds])
+        v2 = C[r, c] * 2
+        dxx = (C[r, c + 1] + C[r, c - 1] - v2) * s2
+        dyy = (C[r + 1, c] + C[r - 1, c] - v2) * s2
+        dss = (N[r, c] + P[r, c] - v2) * s2
+        dxy = (C[r + 1, c + 1] - C[r + 1, c - 1] - C[r - 1, c + 1] + C[r - 1, c - 1]) * cs
+        dxs = (N[r, c + 1] - N[r, c - 1] - P[r, c + 1] + P[r, c - 1]) * cs
+        dys = (N[r + 1, c] - N[r - 1, c] - P[r + 1, c] + P[r - 1, c]) * cs
+        X = _solve3_sym(dxx, dxy, dxs, dyy, dys, dss, dD)
+        if X is None:
+            return None
+        xc, xr, xi = -X[0], -X[1], -X[2]
+        if abs(xi) < 0.5 and abs(xr) < 0.5 and abs(xc) < 0.5:
+            break
+        if abs(xi) > 1e6 or abs(xr) > 1e6 or abs(xc) > 1e6:
+            return None
+        c += int(round(xc))
+        r += int(round(xr))
+        l += int(round(xi))
+        if l < 1 or l > S or c < SIFT_BORDER or c >= cols - SIFT_BORDER or r < SIFT_BORDER or r >= rows - SIFT_BORDER:
+            return None
+    else:
+        return None
+    P, C, N = D[l - 1].astype(np.float64), D[l].astype(np.float64), D[l + 1].astype(np.float64)
+    dD = np.array([(C[r, c + 1] - C[r, c - 1]) * ds, (C[r + 1, c] - C[r - 1, c]) * ds, (N[r, c] - P[r, c]) * ds])
+    t = dD[0] * xc + dD[1] * xr + dD[2] * xi
+    contr = C[r, c] * sc + t * 0.5
+    if abs(contr) * S < SIFT_CONTRAST:
+        return None
+    v2 = C[r, c] * 2
+    dxx = (C[r, c + 1] + C[r, c - 1] - v2) * s2
+    dyy = (C[r + 1, c] + C[r - 1, c] - v2) * s2
+    dxy = (C[r + 1, c + 1] - C[r + 1, c - 1] - C[r - 1, c + 1] + C[r - 1, c - 1]) * cs
+    tr, det = dxx + dyy, dxx * dyy - dxy * dxy
+    if det <= 0 or tr * tr * SIFT_EDGE >= (SIFT_EDGE + 1) ** 2 * det:
+        return None
+    return l, r, c, xi, xr, xc, contr
+
+
+def _solve3_sym(a, b, c, d, e, f, y):
+    """[[a b c] [b d e] [c e f]] x = y by the explicit adjugate (the GPU's formula, fp64)."""
+    A0, A1, A2 = d * f - e * e, c * e - b * f, b * e - c * d
+    det = a * A0 + b * A1 + c * A2
+    if det == 0:
+        return None
+    B1, B2, C2 = a * f - c * c, b * c - a * e, a * d - b * b
+    inv = 1.0 / det
+    return np.array([(A0 * y[0] + A1 * y[1] + A2 * y[2]) * inv, (A1 * y[0] + B1 * y[1] + B2 * y[2]) * inv,
+                     (A2 * y[0] + B2 * y[1] + C2 * y[2]) * inv])
+
+
+def _grad(img, r, c):
+    return img[r, c + 1] - img[r, c - 1], img[r - 1, c] - img[r + 1, c]
+
+
+def sift_detect(img_u8):
+    """All keypoints: list of dicts (x, y, size, angle, response, octave o, layer l, r, c) in image coords."""
+    S = SIFT_LAYERS
+    gp, dp = sift_pyramid(img_u8)
+    thr = np.floor(0.5 * SIFT_CONTRAST / S * 255)
+    kps = []
+    for o, D in enumerate(dp):
+        rows, cols = D[0].shape
+        if rows <= 2 * SIFT_BORDER or cols <= 2 * SIFT_BORDER:
+            continue
+        for l in range(1, S + 1):
+            C = D[l]
+            b = SIFT_BORDER
+            v = C[b:rows - b, b:cols - b]
+            nb = []
+            for dl in (-1, 0, 1):
+                for dy in (-1, 0, 1):
+                    for dx in (-1, 0, 1):
+                        if dl == 0 and dy == 0 and dx == 0:
+                            continue
+                        nb.append(D[l + dl][b + dy:rows - b + dy, b + dx:cols - b + dx])
+            nb = np.stack(nb)
+            ismax = (v > 0) & np.all(v[None] >= nb, axis=0)
+            ismin = (v < 0) & np.all(v[None] <= nb, axis=0)
+            cand = (np.abs(v) > thr) & (ismax | ismin)
+            for r, c in zip(*np.nonzero(cand)):
+                res = _sift_refine(D, o, l, int(r) + b, int(c) + b)
+                if res is None:
+                    continue
+                L, R, Cc, xi, xr, xc, contr = res
+                scale = 2.0 ** (o - 1)  # octave 0 is the doubled image
+                size = SIFT_SIGMA * 2.0 ** ((L + xi) / S) * 2.0 ** o * 2 * 0.5
+                x, y = (Cc + xc) * scale, (R + xr) * scale
+                scl_oct = SIFT_SIGMA * 2.0 ** ((L + xi) / S)
+                for ang in _sift_orientations(gp[o][L], R, Cc, scl_oct):
+                    kps.append(dict(x=np.float32(x), y=np.float32(y), size=np.float32(size), angle=np.float32(ang),
+                                    response=np.float32(abs(contr)), o=o, l=L, r=R, c=Cc,
+                                    scl=float(np.float32(scl_oct))))
+    return kps, gp
+
+
+def _sift_orientations(img, r, c, scl):
+    n = SIFT_ORI_BINS
+    rad = int(round(3 * 1.5 * scl))
+    sig = 1.5 * scl
+    rows, cols = img.shape
+    hist = np.zeros(n, np.float32)
+    es = np.float32(-1.0 / (2.0 * sig * sig))
+    for i in range(-rad, rad + 1):
+        y = r + i
+        if y <= 0 or y >= rows - 1:
+            continue
+        for j in range(-rad, rad + 1):
+            x = c + j
+            if x <= 0 or x >= cols - 1:
+                continue
+            dx, dy = _grad(img, y, x)
+            w = np.float32(np.exp(np.float32(i * i + j * j) * es))
+            ori = np.float32(np.degrees(np.arctan2(np.float64(dy), np.float64(dx))))
+            if ori < 0:
+                ori = np.float32(ori + 360)
+            mag = np.float32(np.sqrt(np.float32(dx * dx + dy * dy)))
+            bn = int(np.rint(np.float32(n / 360.0) * ori))
+            bn = bn - n if bn >= n else (bn + n if bn < 0 else bn)
+            hist[bn] = np.float32(hist[bn] + np.float32(w * mag))
+    sm = np.zeros(n, np.float32)
+    for i in range(n):
+        sm[i] = (np.float32(hist[(i - 2) % n] + hist[(i + 2) % n]) * np.float32(1 / 16.) +
+                 np.float32(hist[(i - 1) % n] + hist[(i + 1) % n]) * np.float32(4 / 16.) + hist[i] * np.float32(6 / 16.))
+    omax = sm.max()
+    out = []
+    for j in range(n):
+        lft, rgt = sm[(j - 1) % n], sm[(j + 1) % n]
+        if sm[j] > lft and sm[j] > rgt and sm[j] >= omax * np.float32(SIFT_ORI_PEAK):
+            bn = j + 0.5 * (lft - rgt) / (lft - 2 * sm[j] + rgt)
+            bn = bn + n if bn < 0 else (bn - n if bn >= n else bn)
+            ang = 360.0 - (360.0 / n) * bn
+            out.append(0.0 if abs(ang - 360.0) < 1.2e-7 else ang)
+    return out
+
+
+def sift_descriptor(img, x, y, angle, scl):
+    """calcSIFTDescriptor at octave coordinates (x, y), orientation `angle` (deg), scale scl: 128 values
+    (integers 0..255 as float32)."""
+    d, n = SIFT_D, SIFT_N
+    ori = 360.0 - angle
+    if abs(ori - 360.0) < 1.2e-7:
+        ori = 0.0
+    cos_t, sin_t = np.cos(np.radians(ori)), np.sin(np.radians(ori))
+    hist_w = 3.0 * scl
+    rad = int(round(hist_w * np.sqrt(2.0) * (d + 1) * 0.5))
+    rows, cols = img.shape
+    rad = min(rad, int(np.sqrt(float(rows) ** 2 + float(cols) ** 2)))
+    cos_t /= hist_w
+    sin_t /= hist_w
+    px, py = int(round(x)), int(round(y))
+    hist = np.zeros((d + 2, d + 2, n + 2), np.float64)
+    es = -1.0 / (d * d * 0.5)
+    bpr = n / 360.0
+    for i in range(-rad, rad + 1):
+        for j in range(-rad, rad + 1):
+            c_rot = j * cos_t - i * sin_t
+            r_rot = j * sin_t + i * cos_t
+            rbin = r_rot + d / 2 - 0.5
+            cbin = c_rot + d / 2 - 0.5
+            r, c = py + i, px + j
+            if not (-1 < rbin < d and -1 < cbin < d and 0 < r < rows - 1 and 0 < c < cols - 1):
+                continue
+            dx, dy = float(img[r, c + 1] - img[r, c - 1]), float(img[r - 1, c] - img[r + 1, c])
+            w = np.exp((c_rot * c_rot + r_rot * r_rot) * es)
+            o = np.degrees(np.arctan2(dy, dx))
+            o = o + 360 if o < 0 else o
+            mag = np.sqrt(dx * dx + dy * dy) * w
+            obin = (o - ori) * bpr
+            r0, c0, o0 = int(np.floor(rbin)), int(np.floor(cbin)), int(np.floor(obin))
+            rb, cb, ob = rbin - r0, cbin - c0, obin - o0
+            o0 = o0 + n if o0 < 0 else (o0 - n if o0 >= n else o0)
+            for dr, wr in ((0, 1 - rb), (1, rb)):
+                for dc, wc in ((0, 1 - cb), (1, cb)):
+                    for do, wo in ((0, 1 - ob), (1, ob)):
+                        hist[r0 + 1 + dr, c0 + 1 + dc, o0 + do] += mag * wr * wc * wo
+    hist[:, :, 0] += hist[:, :, n]
+    hist[:, :, 1] += hist[:, :, n + 1]
+    v = hist[1:d + 1, 1:d + 1, :n].reshape(-1)
+    thr = np.sqrt((v * v).sum()) * 0.2
+    v = np.minimum(v, thr)
+    nrm = 512.0 / max(np.sqrt((v * v).sum()), 1.2e-7)
+    return np.clip(np.rint(v * nrm), 0, 255).astype(np.float32)
+
+
+def sift_detect_compute(img_u8, nfeatures=0):
+    """detectAndCompute: (keypoints [n, 4] = x, y, size, angle (image coords), response [n], descriptors [n, 128])
+    ordered by (-response, y, x, angle), cut to nfeatures (> 0)."""
+    kps, gp = sift_detect(img_u8)
+    kps.sort(key=lambda k: (-float(k["response"]), float(k["y"]), float(k["x"]), float(k["angle"])))
+    if nfeatures > 0:
+        kps = kps[:nfeatures]
+    kp = np.array([[k["x"], k["y"], k["size"], k["angle"]] for k in kps], np.float32).reshape(-1, 4)
+    resp = np.array([k["response"] for k in kps], np.float32)
+    des = np.zeros((len(kps), 128), np.float32)
+    for i, k in enumerate(kps):
+        s = 2.0 ** (k["o"] - 1)
+        des[i] = sift_descriptor(gp[k["o"]][k["l"]], k["x"] / s, k["y"] / s, k["angle"], k["scl"])
+    return kp, resp, des

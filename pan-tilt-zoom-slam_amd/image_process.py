@@ -21,11 +21,14 @@ import numpy as np
 
 
 class KeyPoint:
-    """Minimal stand-in for cv2.KeyPoint: the reference only reads `.pt`."""
-    __slots__ = ("pt",)
+    """Stand-in for cv2.KeyPoint (the reference only reads `.pt`; size / angle / response as SIFT sets them)."""
+    __slots__ = ("pt", "size", "angle", "response")
 
-    def __init__(self, x, y):
+    def __init__(self, x, y, size=0.0, angle=-1.0, response=0.0):
         self.pt = (float(x), float(y))
+        self.size = float(size)
+        self.angle = float(angle)
+        self.response = float(response)
 
 
 def _hook(name):
@@ -38,14 +41,32 @@ def _hook(name):
 
 
 # ---- front-end hooks (assigned by a correspondence source) ----
-detect_compute_sift = _hook("detect_compute_sift")              # (im, nfeatures, verbose) -> (kps, des)
 detect_compute_orb = _hook("detect_compute_orb")
 detect_compute_latch = _hook("detect_compute_latch")
-# match_sift_features / homography_ransac / optical_flow_matching: GPU implementations below (kNN-2 +
-# ratio test + RANSAC, pyramidal LK); a correspondence source may still assign its own
+# detect_compute_sift / detect_sift / match_sift_features / homography_ransac / optical_flow_matching: GPU
+# implementations below (SIFT, kNN-2 + ratio test + RANSAC, pyramidal LK); a correspondence source may
+# still assign its own
 match_orb_features = _hook("match_orb_features")
 match_latch_features = _hook("match_latch_features")
 draw_matches = None  # optional visualisation hook (bundle_adjustment.py:153-163)
+
+
+def detect_compute_sift(im, nfeatures, verbose=False):
+    """image_process.py:56-79 on the GPU (libptzba ptz_sift: OpenCV's SIFT defaults): keypoints (KeyPoint with
+    .pt, .size, .angle, .response) strongest first, at most nfeatures (> 0), and descriptors [n, 128] float32."""
+    import ptzba
+    kp, resp, des = ptzba.sift(_grey_u8(im), int(nfeatures))
+    key_point = [KeyPoint(k[0], k[1], k[2], k[3], r) for k, r in zip(kp, resp)]
+    if verbose:
+        print('detect: %d SIFT keypoints.' % len(key_point))
+    return key_point, des
+
+
+def detect_sift(im, nfeatures=50):
+    """image_process.py:14-33 on the GPU: SIFT keypoint locations [n, 2] float32."""
+    import ptzba
+    kp, _, _ = ptzba.sift(_grey_u8(im), int(nfeatures))
+    return np.ascontiguousarray(kp[:, :2])
 
 
 def detect_compute_sift_array(im, nfeatures, norm=True):

@@ -124,6 +124,7 @@ def lib():
         "ptz_match_knn2": ([I, I64, I64, I32, V, V, V, V], I),
         "ptz_homography_ransac": ([I, I64, V, V, D, I32, ctypes.c_uint64, V, V, POINTER(c_int32)], I),
         "ptz_lk_track": ([I, I32, I32, V, V, I64, V, I32, I32, I32, D, D, V, V, V], I),
+        "ptz_sift": ([I, I32, I32, V, I32, I32, V, V, V, POINTER(c_int32)], I),
         "ptz_py_shuffle_prefix": ([V, I64, V, I64, V], I),
         "ptz_set_order_pairs": ([I64, V, V, V, V, V], I),
         "ptz_keyframe_features": ([I32, I64, V, V, V, V, V, V, V, V], I),
@@ -154,7 +155,7 @@ EXPORTED_SYMBOLS = [
     "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_solve", "ptzba_read_scalars", "ptzba_accept",
     "ptzba_lm_start", "ptzba_lm_init", "ptzba_lm_build", "ptzba_lm_solve", "ptzba_lm_decide", "ptzba_lm_wait",
     "ptzba_exchange", "ptzba_exchange_packed", "ptzba_pack", "ptzba_unpack", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptzba_save_state", "ptzba_restore_state", "ptz_ray_to_image",
-    "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks", "ptzba_coupling_window", "ptz_match_knn2", "ptz_homography_ransac", "ptz_lk_track",
+    "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks", "ptzba_coupling_window", "ptz_match_knn2", "ptz_homography_ransac", "ptz_lk_track", "ptz_sift",
     "ptz_py_shuffle_prefix", "ptz_set_order_pairs", "ptz_keyframe_features", "ptz_pack_records",
     "ptz_refine_poses", "ptzekf_new", "ptzekf_delete", "ptzekf_num_rays", "ptzekf_set_state", "ptzekf_get_state", "ptzekf_add_pose_cov",
     "ptzekf_remove_rays", "ptzekf_add_rays", "ptzekf_project_visible", "ptzekf_update",
@@ -292,6 +293,29 @@ def lk_track(img0, img1, points, win=31, levels=4, max_iter=30, eps=0.01, min_ei
                                   _ptr(b), n, _ptr(pts), int(levels), int(win), int(max_iter), float(eps),
                                   float(min_eig), _ptr(out), _ptr(st), _ptr(err)), "ptz_lk_track")
     return out, st, err
+
+
+def sift(img, nfeatures=0, device=None):
+    """SIFT detectAndCompute on the GPU (image_process.py:67-68, OpenCV's defaults): 8-bit grey image [h, w].
+    Returns (keypoints [n, 4] float32 = x, y, size, angle; response [n]; descriptors [n, 128] float32 with
+    integer values), ordered by decreasing response, at most nfeatures (> 0)."""
+    a = np.ascontiguousarray(img, dtype=np.uint8)
+    if a.ndim != 2:
+        raise ValueError("sift expects a 2-D 8-bit grey image")
+    dev = default_device() if device is None else device
+    n = c_int32(0)
+    cap = nfeatures if nfeatures > 0 else 4096
+    while True:
+        kp = np.zeros((cap, 4), np.float32)
+        resp = np.zeros(cap, np.float32)
+        des = np.zeros((cap, 128), np.float32)
+        _check(lib().ptz_sift(dev, a.shape[1], a.shape[0], _ptr(a), int(nfeatures), cap, _ptr(kp), _ptr(resp),
+                              _ptr(des), ctypes.byref(n)), "ptz_sift")
+        if n.value <= cap:
+            break
+        cap = n.value
+    k = n.value
+    return kp[:k], resp[:k], des[:k]
 
 
 def refine_poses(u, v, init_ptz, rays, points, subsets=None, ftol=1e-4, xtol=1e-8, max_iter=100, loss=LOSS_LINEAR,

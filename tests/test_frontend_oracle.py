@@ -56,3 +56,25 @@ def test_lk_oracle_tracks_known_motion():
     e = np.linalg.norm(nxt[:200] - frontend_data.apply_h(H, p), axis=1)
     assert st[:200].all() and np.median(e) < 0.05 and e.max() < 0.5 and err[:200].max() < 5
     assert not st[200:].any() and np.isinf(err[200:]).all()
+
+
+def test_sift_oracle_matches_under_known_motion():
+    """sift_detect_compute on two textured views a PTZ homography apart: the ratio-test matches of its
+    descriptors land within 1 px of the true motion; keypoints are ordered by response and cut to nfeatures."""
+    from oracle import ptz_oracle as orc
+    I, J, H = frontend_data.textured_pair(seed=2, width=192, height=144, d_pan=0.5, f=400.0)
+    kp1, r1, d1 = orc.sift_detect_compute(I, 80)
+    kp2, r2, d2 = orc.sift_detect_compute(J, 80)
+    assert len(kp1) == 80 and np.all(np.diff(r1) <= 0)
+    assert np.all((d1 >= 0) & (d1 <= 255)) and np.array_equal(d1, np.rint(d1))
+    idx, dist = orc.knn2(d1, d2)
+    good = np.flatnonzero(dist[:, 0] < 0.7 * dist[:, 1])
+    err = np.linalg.norm(frontend_data.apply_h(H, kp1[good, :2].astype(np.float64)) - kp2[idx[good, 0], :2], axis=1)
+    assert len(good) >= 30 and np.mean(err < 1.0) > 0.9
+
+
+def test_sift_gaussian_weights_and_border():
+    from oracle import ptz_oracle as orc
+    w = orc.sift_gauss_kernel(1.6)
+    assert len(w) == 15 and abs(float(w.sum()) - 1) < 1e-6 and np.allclose(w, w[::-1])
+    assert orc._refl101(np.array([-3, -1, 0, 4, 5, 7, 9]), 5).tolist() == [3, 1, 0, 4, 3, 1, 1]

@@ -144,3 +144,67 @@ def test_optical_flow_matching_gpu(gpu_available):
     assert nxt.shape == (len(idx), 2) and idx == sorted(idx)
     idx3, nxt3 = image_process.optical_flow_matching(np.dstack([I] * 3), np.dstack([J] * 3), p)
     assert idx3 == idx and np.array_equal(nxt3, nxt)
+
+
+def _sift_match(kg, ko):
+    """index pairs (gpu, oracle) of keypoints at the same place and orientation"""
+    pairs = []
+    for i, k in enumerate(ko):
+        d = np.abs(kg[:, :2] - k[:2]).max(1) + np.minimum(np.abs(kg[:, 3] - k[3]), 360 - np.abs(kg[:, 3] - k[3])) / 360
+        j = int(np.argmin(d)) if len(kg) else -1
+        if j >= 0 and d[j] < 2e-3:
+            pairs.append((j, i))
+    return np.array(pairs, np.int64).reshape(-1, 2)
+
+
+@pytest.mark.parametrize("seed,w,h", [(2, 192, 144), (3, 257, 181)])
+def test_sift_matches_oracle(gpu_available, seed, w, h):
+    """ptz_sift against the oracle restatement: the float32 pyramid is bit-identical (no contraction, same
+    operation order) and the fp64 refinement follows the same evaluation order, so the keypoint set, positions,
+    sizes and responses agree exactly; angles to 1e-3 deg (atan2 / exp of different libraries); descriptors
+    (rounded integers of a renormalised histogram summed in another order) within 1, identical for >= 99 %
+    of keypoints (measured: 100 %, profiles/r02_sift_check.txt)."""
+    import ptzba
+    from oracle import ptz_oracle as orc
+    I, _, _ = frontend_data.textured_pair(seed=seed, width=w, height=h, d_pan=0.5, f=400.0)
+    kg, rg, dg = ptzba.sift(I, 0)
+    ko, ro, do = orc.sift_detect_compute(I, 0)
+    assert len(kg) == len(ko) > 50
+    pr = _sift_match(kg, ko)
+    assert len(pr) == len(ko)
+    assert np.array_equal(kg[pr[:, 0], :3], ko[pr[:, 1], :3]) and np.array_equal(rg[pr[:, 0]], ro[pr[:, 1]])
+    da = np.abs(kg[pr[:, 0], 3] - ko[pr[:, 1], 3])
+    assert np.minimum(da, 360 - da).max() < 1e-3
+    dd = np.abs(dg[pr[:, 0]] - do[pr[:, 1]])
+    assert dd.max() <= 1 and np.mean(dd.max(1) == 0) >= 0.99
+    assert np.all(np.diff(rg) <= 0)
+
+
+def test_sift_front_end_recovers_homography(gpu_available):
+    """The whole GPU front-end on two 640 x 360 textured views: SIFT (ptz_sift) -> kNN-2 + ratio test ->
+    homography RANSAC (image_process.match_sift_features) recovers the true PTZ homography."""
+    import image_process
+    I, J, H = frontend_data.textured_pair(seed=7, width=640, height=360, d_pan=1.5, d_tilt=-0.5, f=900.0, df=12.0)
+    k1, d1 = image_process.detect_compute_sift(I, 1500)
+    k2, d2 = image_process.detect_compute_sift(J, 1500)
+    assert 200 < len(k1) <= 1500 and d1.shape == (len(k1), 128) and d1.dtype == np.float32
+    pts1, i1, pts2, i2 = image_process.match_sift_features(k1, d1, k2, d2)
+    assert len(i1) >= 100
+    err = np.linalg.norm(frontend_data.apply_h(H, pts1) - pts2, axis=1)
+    assert np.median(err) < 0.2 and err.max() < 1.5
+    _, Hm = image_process.homography_ransac(pts1, pts2, 1.0, return_matrix=True)
+    probe = np.array([[100.0, 80.0], [540.0, 300.0], [320.0, 180.0]])
+    assert np.abs(frontend_data.apply_h(Hm, probe) - frontend_data.apply_h(H, probe)).max() < 0.5
+
+
+def test_sift_hooks_signature(gpu_available):
+    """detect_compute_sift(im, nfeatures, verbose) / detect_sift(im, nfeatures) / detect_compute_sift_array as
+    image_process.py:14-102 define them; colour input is converted to grey; nfeatures caps the count."""
+    import image_process
+    I, _, _ = frontend_data.textured_pair(seed=8, width=320, height=200, f=500.0)
+    kps, des = image_process.detect_compute_sift(I, 50)
+    assert len(kps) == 50 and des.shape == (50, 128) and all(hasattr(k, "pt") for k in kps)
+    pts = image_process.detect_sift(np.dstack([I] * 3), 50)
+    assert pts.shape == (50, 2) and np.allclose(pts, [k.pt for k in kps])
+    arr, ades = image_process.detect_compute_sift_array(I, 50)
+    assert arr.shape == (50, 2) and np.allclose(np.linalg.norm(ades, axis=1), 1.0)
