@@ -245,6 +245,12 @@ PTZBA_EXPORT int ptz_lk_track(int device, int32_t width, int32_t height, const u
                               int64_t n, const float* pts0, int32_t levels, int32_t win, int32_t max_iter, double eps,
                               double min_eig, float* pts1_out, uint8_t* status_out, float* err_out);
 
+/* Hamming nearest neighbours both ways (cv.BFMatcher(cv.NORM_HAMMING, crossCheck=True).match of match_orb_features /
+ * match_latch_features, image_process.py:237-310): binary descriptors of nbytes (multiple of 4, <= 64);
+ * idx12[i] / dist12[i] = the nearest des2 row of des1 row i and its bit distance, idx21[j] the nearest des1 row of
+ * des2 row j (ties: lower index; -1 when the other set is empty).  Cross-checked matches: i with idx21[idx12[i]] == i. */
+PTZBA_EXPORT int ptz_match_hamming(int device, int64_t n1, int64_t n2, int32_t nbytes, const uint8_t* des1,
+                                   const uint8_t* des2, int32_t* idx12, int32_t* dist12, int32_t* idx21);
 /* SIFT keypoints and descriptors (cv.xfeatures2d.SIFT_create(nfeatures).detectAndCompute as detect_compute_sift calls
  * it, image_process.py:56-79): img 8-bit grey width x height; OpenCV's defaults (image doubled, 3 layers per octave,
  * sigma 1.6, contrast 0.04, edge 10).  Keypoints ordered by (-response, y, x, angle) and cut to nfeatures (> 0;

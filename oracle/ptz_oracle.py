@@ -1015,3 +1015,15 @@ def sift_detect_compute(img_u8, nfeatures=0):
         s = 2.0 ** (k["o"] - 1)
         des[i] = sift_descriptor(gp[k["o"]][k["l"]], k["x"] / s, k["y"] / s, k["angle"], k["scl"])
     return kp, resp, des
+
+
+def hamming_cross(des1, des2):
+    """cv.BFMatcher(cv.NORM_HAMMING, crossCheck=True).match restated (image_process.py:249-250): mutual
+    nearest neighbours by bit distance, ties to the lower index, in query order -> (query, train, distance)."""
+    a = np.unpackbits(np.asarray(des1, np.uint8), axis=1).astype(np.int32)
+    b = np.unpackbits(np.asarray(des2, np.uint8), axis=1).astype(np.int32)
+    D = a @ (1 - b).T + (1 - a) @ b.T
+    i12 = np.argmin(D, axis=1)
+    i21 = np.argmin(D, axis=0)
+    q = np.flatnonzero(i21[i12] == np.arange(len(a)))
+    return q, i12[q], D[q, i12[q]]

@@ -641,3 +641,70 @@ int ptz_lk_track(int device, int32_t width, int32_t height, const uint8_t* img0,
   HIPCHK(hipMemcpy(err_out, derr.p, (size_t)n * 4, hipMemcpyDeviceToHost));
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Hamming nearest neighbours both ways (cv.BFMatcher(cv.NORM_HAMMING, crossCheck=True).match, the matching
+// step of match_orb_features / match_latch_features, image_process.py:237-310): one wave per query keeps the
+// nearest train descriptor (ties to the lower index); the host keeps the mutual pairs.
+// ---------------------------------------------------------------------------------------------
+namespace ptzba {
+constexpr int HAM_MAXW = 16;  // descriptor words (<= 64 bytes)
+
+__global__ __launch_bounds__(256) void k_hamming_nn(int nq, int nt, int words, const uint32_t* __restrict__ q,
+                                                    const uint32_t* __restrict__ t, int* __restrict__ idx,
+                                                    int* __restrict__ dist) {
+  const int qi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (qi >= nq) return;
+  uint32_t qv[HAM_MAXW];
+#pragma unroll
+  for (int k = 0; k < HAM_MAXW; ++k) qv[k] = k < words ? q[(int64_t)qi * words + k] : 0u;
+  int bd = 0x7fffffff, bi = 0x7fffffff;
+  for (int j = lane; j < nt; j += 64) {
+    int d = 0;
+#pragma unroll
+    for (int k = 0; k < HAM_MAXW; ++k)
+      if (k < words) d += __popc(qv[k] ^ t[(int64_t)j * words + k]);
+    if (d < bd) { bd = d; bi = j; }  // j ascends per lane: the first minimum
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const int od = __shfl_xor(bd, off), oi = __shfl_xor(bi, off);
+    if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
+  }
+  if (lane == 0) {
+    idx[qi] = nt > 0 ? bi : -1;
+    dist[qi] = nt > 0 ? bd : -1;
+  }
+}
+}  // namespace ptzba
+
+int ptz_match_hamming(int device, int64_t n1, int64_t n2, int32_t nbytes, const uint8_t* des1, const uint8_t* des2,
+                      int32_t* idx12, int32_t* dist12, int32_t* idx21) {
+  using namespace ptzba;
+  if (n1 < 0 || n2 < 0 || nbytes <= 0 || nbytes % 4 || nbytes > 4 * HAM_MAXW)
+    return fail("bad descriptor shape (bytes per descriptor: a multiple of 4, at most %d)", 4 * HAM_MAXW);
+  if ((n1 && (!des1 || !idx12 || !dist12)) || (n2 && (!des2 || !idx21))) return fail("null buffer");
+  if (n1 == 0 && n2 == 0) return 0;
+  if (select_device(device)) return -1;
+  const int words = nbytes / 4;
+  DBuf a, b, i12, d12, i21, d21;
+  if (a.alloc((size_t)std::max<int64_t>(n1, 1) * nbytes) || b.alloc((size_t)std::max<int64_t>(n2, 1) * nbytes) ||
+      i12.alloc((size_t)std::max<int64_t>(n1, 1) * 4) || d12.alloc((size_t)std::max<int64_t>(n1, 1) * 4) ||
+      i21.alloc((size_t)std::max<int64_t>(n2, 1) * 4) || d21.alloc((size_t)std::max<int64_t>(n2, 1) * 4))
+    return -1;
+  if (n1) HIPCHK(hipMemcpy(a.p, des1, (size_t)n1 * nbytes, hipMemcpyHostToDevice));
+  if (n2) HIPCHK(hipMemcpy(b.p, des2, (size_t)n2 * nbytes, hipMemcpyHostToDevice));
+  if (n1)
+    hipLaunchKernelGGL(k_hamming_nn, dim3((unsigned)((n1 + 3) / 4)), dim3(256), 0, nullptr, (int)n1, (int)n2, words,
+                       a.as<uint32_t>(), b.as<uint32_t>(), i12.as<int>(), d12.as<int>());
+  if (n2)
+    hipLaunchKernelGGL(k_hamming_nn, dim3((unsigned)((n2 + 3) / 4)), dim3(256), 0, nullptr, (int)n2, (int)n1, words,
+                       b.as<uint32_t>(), a.as<uint32_t>(), i21.as<int>(), d21.as<int>());
+  HIPCHK(hipGetLastError());
+  if (n1) {
+    HIPCHK(hipMemcpy(idx12, i12.p, (size_t)n1 * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(dist12, d12.p, (size_t)n1 * 4, hipMemcpyDeviceToHost));
+  }
+  if (n2) HIPCHK(hipMemcpy(idx21, i21.p, (size_t)n2 * 4, hipMemcpyDeviceToHost));
+  return 0;
+}

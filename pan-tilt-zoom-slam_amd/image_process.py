@@ -46,8 +46,6 @@ detect_compute_latch = _hook("detect_compute_latch")
 # detect_compute_sift / detect_sift / match_sift_features / homography_ransac / optical_flow_matching: GPU
 # implementations below (SIFT, kNN-2 + ratio test + RANSAC, pyramidal LK); a correspondence source may
 # still assign its own
-match_orb_features = _hook("match_orb_features")
-match_latch_features = _hook("match_latch_features")
 draw_matches = None  # optional visualisation hook (bundle_adjustment.py:153-163)
 
 
@@ -106,6 +104,26 @@ def match_sift_features(keypoint1, descriptor1, keypoint2, descriptor2, pts_arra
     if verbose:
         print('%d matches passed the homography ransac' % len(inlier_index))
     return pts1[inlier_index, :], index1[inlier_index].tolist(), pts2[inlier_index, :], index2[inlier_index].tolist()
+
+
+def match_orb_features(keypiont1, descriptor1, keypoint2, descriptor2, verbose=False):
+    """image_process.py:237-272 on the GPU: cross-checked Hamming matching (libptzba ptz_match_hamming), then
+    the homography RANSAC inliers (1 px).  Returns (pts1, index1, pts2, index2)."""
+    import ptzba
+    assert len(keypiont1) >= 4  # assume homography matching
+    q, t, _ = ptzba.match_hamming_cross(descriptor1, descriptor2)
+    pts1 = np.array([keypiont1[i].pt for i in q], np.float64).reshape(-1, 2)
+    pts2 = np.array([keypoint2[j].pt for j in t], np.float64).reshape(-1, 2)
+    index1, index2 = q.astype(np.int32), t.astype(np.int32)
+    inlier_index = homography_ransac(pts1, pts2, 1.0)
+    if verbose:
+        print('%d matches passed the homography ransac' % len(inlier_index))
+    return pts1[inlier_index, :], index1[inlier_index].tolist(), pts2[inlier_index, :], index2[inlier_index].tolist()
+
+
+def match_latch_features(keypiont1, descriptor1, keypoint2, descriptor2, verbose=False):
+    """image_process.py:275-310: the same cross-checked Hamming matching + RANSAC for LATCH descriptors."""
+    return match_orb_features(keypiont1, descriptor1, keypoint2, descriptor2, verbose)
 
 
 def homography_ransac(points1, points2, reprojection_threshold=0.5, return_matrix=False):

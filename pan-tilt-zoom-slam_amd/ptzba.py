@@ -125,6 +125,7 @@ def lib():
         "ptz_homography_ransac": ([I, I64, V, V, D, I32, ctypes.c_uint64, V, V, POINTER(c_int32)], I),
         "ptz_lk_track": ([I, I32, I32, V, V, I64, V, I32, I32, I32, D, D, V, V, V], I),
         "ptz_sift": ([I, I32, I32, V, I32, I32, V, V, V, POINTER(c_int32)], I),
+        "ptz_match_hamming": ([I, I64, I64, I32, V, V, V, V, V], I),
         "ptz_py_shuffle_prefix": ([V, I64, V, I64, V], I),
         "ptz_set_order_pairs": ([I64, V, V, V, V, V], I),
         "ptz_keyframe_features": ([I32, I64, V, V, V, V, V, V, V, V], I),
@@ -155,7 +156,7 @@ EXPORTED_SYMBOLS = [
     "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_solve", "ptzba_read_scalars", "ptzba_accept",
     "ptzba_lm_start", "ptzba_lm_init", "ptzba_lm_build", "ptzba_lm_solve", "ptzba_lm_decide", "ptzba_lm_wait",
     "ptzba_exchange", "ptzba_exchange_packed", "ptzba_pack", "ptzba_unpack", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptzba_save_state", "ptzba_restore_state", "ptz_ray_to_image",
-    "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks", "ptzba_coupling_window", "ptz_match_knn2", "ptz_homography_ransac", "ptz_lk_track", "ptz_sift",
+    "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks", "ptzba_coupling_window", "ptz_match_knn2", "ptz_homography_ransac", "ptz_lk_track", "ptz_sift", "ptz_match_hamming",
     "ptz_py_shuffle_prefix", "ptz_set_order_pairs", "ptz_keyframe_features", "ptz_pack_records",
     "ptz_refine_poses", "ptzekf_new", "ptzekf_delete", "ptzekf_num_rays", "ptzekf_set_state", "ptzekf_get_state", "ptzekf_add_pose_cov",
     "ptzekf_remove_rays", "ptzekf_add_rays", "ptzekf_project_visible", "ptzekf_update",
@@ -293,6 +294,31 @@ def lk_track(img0, img1, points, win=31, levels=4, max_iter=30, eps=0.01, min_ei
                                   _ptr(b), n, _ptr(pts), int(levels), int(win), int(max_iter), float(eps),
                                   float(min_eig), _ptr(out), _ptr(st), _ptr(err)), "ptz_lk_track")
     return out, st, err
+
+
+def match_hamming_cross(des1, des2, device=None):
+    """cv.BFMatcher(cv.NORM_HAMMING, crossCheck=True).match(des1, des2) on the GPU (image_process.py:249-250):
+    binary descriptors [n, nbytes] uint8.  Returns (query index, train index, bit distance) arrays of the
+    mutual nearest neighbours, in query order."""
+    a = np.ascontiguousarray(des1, dtype=np.uint8)
+    b = np.ascontiguousarray(des2, dtype=np.uint8)
+    if a.ndim != 2 or b.ndim != 2 or (len(a) and len(b) and a.shape[1] != b.shape[1]):
+        raise ValueError("descriptor arrays must be [n, nbytes] with the same nbytes")
+    nb = a.shape[1] if len(a) else b.shape[1]
+    pad = (-nb) % 4
+    if pad:  # zero bytes add no distance
+        a = np.ascontiguousarray(np.pad(a, ((0, 0), (0, pad))))
+        b = np.ascontiguousarray(np.pad(b, ((0, 0), (0, pad))))
+    i12 = np.empty(len(a), np.int32)
+    d12 = np.empty(len(a), np.int32)
+    i21 = np.empty(len(b), np.int32)
+    if len(a) and len(b):
+        _check(lib().ptz_match_hamming(default_device() if device is None else device, len(a), len(b), nb + pad,
+                                       _ptr(a), _ptr(b), _ptr(i12), _ptr(d12), _ptr(i21)), "ptz_match_hamming")
+    else:
+        return np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.int32)
+    q = np.flatnonzero(i21[i12] == np.arange(len(a)))
+    return q, i12[q].astype(np.int64), d12[q]
 
 
 def sift(img, nfeatures=0, device=None):

@@ -107,3 +107,25 @@ def textured_pair(seed=0, width=320, height=240, d_pan=0.6, d_tilt=-0.3, f=600.0
         I8[y0:y1, x0:x1] = 100
         J8[y0:y1, x0:x1] = 100
     return I8, J8, H
+
+
+def binary_views(seed=0, n_common=300, n_only=100, nbytes=32, flips=6):
+    """ORB/LATCH-like binary descriptors of world features in two PTZ views: a few flipped bits between
+    views, distractors on both sides, keypoints under the true homography (+ noise)."""
+    rng = np.random.default_rng(seed)
+    H = ptz_homography(640.0, 360.0, np.array([12.0, -6.0, 2200.0]), np.array([14.5, -5.2, 2300.0]))
+    p1 = np.stack([rng.uniform(50, 1200, n_common), rng.uniform(40, 680, n_common)], 1)
+    p2 = apply_h(H, p1) + rng.normal(0, 0.2, p1.shape)
+    F = rng.integers(0, 256, (n_common, nbytes), dtype=np.uint8)
+    G = F.copy()
+    for i in range(n_common):
+        for b in rng.choice(nbytes * 8, flips, replace=False):
+            G[i, b // 8] ^= np.uint8(1 << (b % 8))
+    D1 = np.r_[F, rng.integers(0, 256, (n_only, nbytes), dtype=np.uint8)]
+    D2 = np.r_[G, rng.integers(0, 256, (n_only, nbytes), dtype=np.uint8)]
+    x1 = np.r_[p1, rng.uniform(0, 1280, (n_only, 2))]
+    x2 = np.r_[p2, rng.uniform(0, 1280, (n_only, 2))]
+    perm = rng.permutation(len(x2))
+    inv = np.argsort(perm)
+    truth = {k: int(inv[k]) for k in range(n_common)}
+    return x1, D1, x2[perm], D2[perm], H, truth

@@ -78,3 +78,17 @@ def test_sift_gaussian_weights_and_border():
     w = orc.sift_gauss_kernel(1.6)
     assert len(w) == 15 and abs(float(w.sum()) - 1) < 1e-6 and np.allclose(w, w[::-1])
     assert orc._refl101(np.array([-3, -1, 0, 4, 5, 7, 9]), 5).tolist() == [3, 1, 0, 4, 3, 1, 1]
+
+
+def test_hamming_cross_oracle_matches_bruteforce():
+    from oracle import ptz_oracle as orc
+    rng = np.random.default_rng(3)
+    a = rng.integers(0, 4, (40, 4), dtype=np.uint8)  # many ties
+    b = rng.integers(0, 4, (55, 4), dtype=np.uint8)
+    q, t, d = orc.hamming_cross(a, b)
+    pc = lambda x, y: sum(bin(int(u) ^ int(v)).count("1") for u, v in zip(x, y))
+    D = np.array([[pc(x, y) for y in b] for x in a])
+    nn12 = [min(range(len(b)), key=lambda j: (D[i, j], j)) for i in range(len(a))]
+    nn21 = [min(range(len(a)), key=lambda i: (D[i, j], i)) for j in range(len(b))]
+    exp = [i for i in range(len(a)) if nn21[nn12[i]] == i]
+    assert q.tolist() == exp and t.tolist() == [nn12[i] for i in exp] and d.tolist() == [D[i, nn12[i]] for i in exp]

@@ -208,3 +208,29 @@ def test_sift_hooks_signature(gpu_available):
     assert pts.shape == (50, 2) and np.allclose(pts, [k.pt for k in kps])
     arr, ades = image_process.detect_compute_sift_array(I, 50)
     assert arr.shape == (50, 2) and np.allclose(np.linalg.norm(ades, axis=1), 1.0)
+
+
+@pytest.mark.parametrize("nbytes", [32, 64, 30])
+def test_hamming_cross_matches_oracle(gpu_available, nbytes):
+    """ptz_match_hamming (cv.BFMatcher(NORM_HAMMING, crossCheck=True)) == the oracle, ties included."""
+    import ptzba
+    from oracle import ptz_oracle as orc
+    x1, d1, x2, d2, H, truth = frontend_data.binary_views(seed=nbytes, nbytes=nbytes)
+    d2[7] = d2[3]  # an exact tie on the train side
+    q, t, d = ptzba.match_hamming_cross(d1, d2)
+    rq, rt, rd = orc.hamming_cross(d1, d2)
+    assert np.array_equal(q, rq) and np.array_equal(t, rt) and np.array_equal(d, rd)
+    assert sum(truth.get(int(a)) == int(b) for a, b in zip(q, t)) >= 290
+
+
+def test_match_orb_features_gpu(gpu_available):
+    """image_process.match_orb_features / match_latch_features (GPU default): cross-checked Hamming matching +
+    RANSAC keep the true correspondences of two PTZ views and drop the distractors."""
+    import image_process
+    x1, d1, x2, d2, H, truth = frontend_data.binary_views(seed=11)
+    k1 = [image_process.KeyPoint(*p) for p in x1]
+    k2 = [image_process.KeyPoint(*p) for p in x2]
+    for fn in (image_process.match_orb_features, image_process.match_latch_features):
+        pts1, i1, pts2, i2 = fn(k1, d1, k2, d2)
+        assert len(i1) >= 280 and all(truth.get(a) == b for a, b in zip(i1, i2))
+        np.testing.assert_allclose(pts1, x1[i1])
