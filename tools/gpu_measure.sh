@@ -13,7 +13,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof_sta
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/${TAG}_pmc_fetch -o run --output-format csv -- python bench.py $BARGS > gpurun_out/${TAG}_pmc_fetch.log 2>&1 || { echo PMCFAIL; tail gpurun_out/${TAG}_pmc_fetch.log; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/${TAG}_pmc_write -o run --output-format csv -- python bench.py $BARGS > gpurun_out/${TAG}_pmc_write.log 2>&1 || { echo PMCFAIL; tail gpurun_out/${TAG}_pmc_write.log; exit 1; }
 # the bench line's traffic field comes from this run's PMC passes
-python tools/pmc_traffic.py gpurun_out/${TAG}_pmc_fetch gpurun_out/${TAG}_pmc_write k_linearize config3/pair/fp32/huber gpurun_out/${TAG}_k1_traffic.json > /dev/null || { echo TRAFFICFAIL; exit 1; }
+python tools/pmc_traffic.py gpurun_out/${TAG}_pmc_fetch gpurun_out/${TAG}_pmc_write "k_linearize<float, 1>" config3/pair/fp32/huber gpurun_out/${TAG}_k1_traffic.json > /dev/null || { echo TRAFFICFAIL; exit 1; }
 timeout -k 10 400 python bench.py --traffic-json gpurun_out/${TAG}_k1_traffic.json > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { echo BENCHFAIL; tail gpurun_out/${TAG}_bench.err; exit 1; }
 cat gpurun_out/${TAG}_bench.json
 # PMC byte-count calibration of the access widths K1 uses (1 GiB streams and a cache-resident table)
