@@ -563,6 +563,73 @@ class StreamScene:
         return cam
 
 
+def _back_project(u, v, f, pan, tilt, x, y):
+    """Inverse of _project for points in front of the camera (q2 > 0): pixel -> ray (theta, phi) in degrees."""
+    a = np.radians(pan); b = np.radians(tilt)
+    ca, sa, cb, sb = np.cos(a), np.sin(a), np.cos(b), np.sin(b)
+    q0, q1, q2 = (x - u) / f, (y - v) / f, 1.0
+    v0, v1, v2 = q0, cb * q1 - sb * q2, sb * q1 + cb * q2
+    d0, d1, d2 = ca * v0 + sa * v2, v1, -sa * v0 + ca * v2
+    p0, p1 = d0 / d2, d1 / d2
+    return np.degrees(np.arctan(p0)), np.degrees(np.arctan(-p1 / np.sqrt(p0 * p0 + 1.0)))
+
+
+class RenderedStream:
+    """8-bit grey 1080p frames of a StreamScene rendered from a textured panorama of the ray sphere (octaves of
+    smoothed lattice noise over (theta, phi), cells 2.0 / 0.8 / 0.3 / 0.12 deg): every pixel is back-projected
+    with the frame's TRUE camera (_back_project, the q-form model) and samples the panorama bilinearly.  Feeds the
+    real front-end (GPU SIFT, pyramidal LK, homography RANSAC) instead of StreamFrontEnd's stand-in.
+    Frames are rendered on first use and cached."""
+
+    def __init__(self, scene, seed=0, res=0.02, octaves=((2.0, 55.0), (0.8, 40.0), (0.3, 28.0), (0.12, 14.0))):
+        self.s = scene
+        self.cams = scene.cams
+        self.u, self.v, self.width, self.height = scene.u, scene.v, scene.width, scene.height
+        W, H = scene.width, scene.height
+        bx = np.array([0, W / 2, W - 1, 0, W - 1, 0, W / 2, W - 1], np.float64)
+        by = np.array([0, 0, 0, H / 2, H / 2, H - 1, H - 1, H - 1], np.float64)
+        th, ph = _back_project(scene.u, scene.v, self.cams[:, 2:3], self.cams[:, 0:1], self.cams[:, 1:2], bx, by)
+        m = 1.0
+        self.th0, self.ph0 = th.min() - m, ph.min() - m
+        nx = int(np.ceil((th.max() + m - self.th0) / res)) + 2
+        ny = int(np.ceil((ph.max() + m - self.ph0) / res)) + 2
+        self.res = res
+        rng = np.random.default_rng(seed + 101)
+        gx = self.th0 + res * np.arange(nx)
+        gy = self.ph0 + res * np.arange(ny)
+        pano = np.full((ny, nx), 128.0, np.float32)
+        for cell, amp in octaves:
+            lx, ly = int(np.ceil(nx * res / cell)) + 3, int(np.ceil(ny * res / cell)) + 3
+            lat = rng.uniform(-1.0, 1.0, (ly, lx)).astype(np.float32)
+            fx, fy = (gx - self.th0) / cell, (gy - self.ph0) / cell
+            ix, iy = np.floor(fx).astype(np.int64), np.floor(fy).astype(np.int64)
+            sx, sy = fx - ix, fy - iy
+            sx, sy = (sx * sx * (3 - 2 * sx)).astype(np.float32), (sy * sy * (3 - 2 * sy)).astype(np.float32)
+            top = lat[iy][:, ix] * (1 - sx) + lat[iy][:, ix + 1] * sx
+            bot = lat[iy + 1][:, ix] * (1 - sx) + lat[iy + 1][:, ix + 1] * sx
+            pano += amp * (top * (1 - sy)[:, None] + bot * sy[:, None])
+        self.pano = pano
+        yy, xx = np.mgrid[0:H, 0:W]
+        self._xy = (xx.astype(np.float64).ravel(), yy.astype(np.float64).ravel())
+        self._cache = {}
+
+    def image(self, i):
+        if i not in self._cache:
+            pan, tilt, f = self.cams[i]
+            th, ph = _back_project(self.u, self.v, f, pan, tilt, *self._xy)
+            fx, fy = (th - self.th0) / self.res, (ph - self.ph0) / self.res
+            ix = np.clip(np.floor(fx).astype(np.int64), 0, self.pano.shape[1] - 2)
+            iy = np.clip(np.floor(fy).astype(np.int64), 0, self.pano.shape[0] - 2)
+            ax, ay = (fx - ix).astype(np.float32), (fy - iy).astype(np.float32)
+            P = self.pano
+            val = (P[iy, ix] * (1 - ax) + P[iy, ix + 1] * ax) * (1 - ay) + (P[iy + 1, ix] * (1 - ax) + P[iy + 1, ix + 1] * ax) * ay
+            self._cache[i] = np.clip(np.rint(val), 0, 255).astype(np.uint8).reshape(self.height, self.width)
+        return self._cache[i]
+
+    def camera(self, i):
+        return self.s.camera(i)
+
+
 class StreamFrontEnd:
     """Stand-in for the reference's OpenCV front-end on a StreamScene (the way make_golden.py's FrontEnd
     stands in for SIFT + BF matching):

@@ -92,3 +92,33 @@ def test_stream_sliding_window_runs(gpu_available):
     rmse = np.sqrt(np.mean(err ** 2, axis=0))
     print("pose rmse vs truth", rmse)
     assert rmse[0] < 0.5 and rmse[1] < 0.5 and rmse[2] < 50.0, rmse
+
+
+def test_stream_with_gpu_front_end(gpu_available):
+    """Config 5 end to end with the REAL front-end: 1080p frames rendered from a textured panorama
+    (synthetic.RenderedStream), GPU SIFT at init / keyframes / ray addition, pyramidal LK + homography RANSAC
+    per frame, EKF and keyframe BA on the GPU (demo_stream.py --frontend gpu).  Nothing is lost and the
+    poses follow the truth to a few hundredths of a degree."""
+    import contextlib
+    import io
+    import image_process
+    import synthetic
+    from demo_stream import run_stream
+    for k in ("detect_compute_sift", "optical_flow_matching", "homography_ransac", "match_sift_features"):
+        fn = getattr(image_process, k)
+        assert fn.__module__ == "image_process" and fn.__name__ == k, f"{k} is not the GPU default"
+    from ptz_slam import PtzSlam
+    from scene_map import Map
+    n = 40
+    scene = synthetic.StreamScene(n, seed=3, pan_lo=-4.0, pan_hi=4.0)
+    source = synthetic.RenderedStream(scene, seed=3)
+    slam = PtzSlam()
+    slam.keyframe_map = Map("sift", max_ba_frame=30)
+    with contextlib.redirect_stdout(io.StringIO()):
+        rec = run_stream(slam, source, n, scene.camera(0), keyframe_every=5)
+    est = np.asarray(rec["ptz"])
+    err = est - scene.cams[:n]
+    assert sum(rec["lost"]) == 0 and sum(rec["keyframe"]) >= 8
+    assert np.sqrt(np.mean(err[:, 0] ** 2)) < 0.05 and np.sqrt(np.mean(err[:, 1] ** 2)) < 0.05
+    assert np.sqrt(np.mean(err[:, 2] ** 2)) < 8.0
+    assert min(rec["n_rays"]) > 100
