@@ -604,10 +604,19 @@ int ptz_lk_track(int device, int32_t width, int32_t height, const uint8_t* img0,
     if (l > 0) { W[l] = (W[l - 1] + 1) / 2; H[l] = (H[l - 1] + 1) / 2; }
     tot += (int64_t)W[l] * H[l];
   }
-  DBuf u8, bufI, bufJ, bufX, bufY, dp, dout, dst, derr;
-  if (u8.alloc((size_t)np * 2) || bufI.alloc((size_t)tot * 4) || bufJ.alloc((size_t)tot * 4) ||
-      bufX.alloc((size_t)tot * 4) || bufY.alloc((size_t)tot * 4) || dp.alloc((size_t)n * 8) || dout.alloc((size_t)n * 8) ||
-      dst.alloc((size_t)n) || derr.alloc((size_t)n * 4))
+  // work buffers kept across calls (a stream tracks every frame): one set per device, grown, never shrunk
+  struct LkWork {
+    DBuf u8, bufI, bufJ, bufX, bufY, dp, dout, dst, derr;
+  };
+  static std::vector<LkWork*> works;
+  if ((int)works.size() <= device) works.resize(device + 1, nullptr);
+  if (!works[device]) works[device] = new LkWork;
+  LkWork& Wk = *works[device];
+  DBuf &u8 = Wk.u8, &bufI = Wk.bufI, &bufJ = Wk.bufJ, &bufX = Wk.bufX, &bufY = Wk.bufY, &dp = Wk.dp, &dout = Wk.dout;
+  DBuf &dst = Wk.dst, &derr = Wk.derr;
+  if (u8.reserve((size_t)np * 2) || bufI.reserve((size_t)tot * 4) || bufJ.reserve((size_t)tot * 4) ||
+      bufX.reserve((size_t)tot * 4) || bufY.reserve((size_t)tot * 4) || dp.reserve((size_t)n * 8) ||
+      dout.reserve((size_t)n * 8) || dst.reserve((size_t)n) || derr.reserve((size_t)n * 4))
     return -1;
   HIPCHK(hipMemcpy(u8.p, img0, (size_t)np, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(u8.as<uint8_t>() + np, img1, (size_t)np, hipMemcpyHostToDevice));

@@ -332,6 +332,19 @@ __global__ __launch_bounds__(256) void k_sift_descr(const SiftKp* __restrict__ k
 }  // namespace ptzba
 
 namespace {
+// Device work buffers kept across calls (one set per device; grown, never shrunk; deliberately not freed at
+// exit): a stream calls SIFT on every frame, and allocating ~0.5 GB of pyramid per call cost more than
+// the kernels.
+struct SiftWork {
+  ptzba::DBuf dimg, dg, dd, dtmp, dk, dcand, dcnt, dkp, dptr, dow, doh, dsel, ddes;
+};
+SiftWork& sift_work(int device) {
+  static std::vector<SiftWork*> w;
+  if ((int)w.size() <= device) w.resize(device + 1, nullptr);
+  if (!w[device]) w[device] = new SiftWork;
+  return *w[device];
+}
+
 std::vector<float> sift_kernel(double sigma) {
   int k = (int)std::nearbyint(sigma * 8 + 1) | 1;
   const int r = k / 2;
@@ -379,11 +392,13 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
     kmax = std::max(kmax, kern[i].size());
   }
   const int CAP = 1 << 17;
-  DBuf dimg, dg, dd, dtmp, dk, dcand, dcnt, dkp, dptr, dow, doh, dsel, ddes;
-  if (dimg.alloc((size_t)width * height) || dg.alloc((size_t)gtot * 4) || dd.alloc((size_t)dtot * 4) ||
-      dtmp.alloc((size_t)W0 * H0 * 4) || dk.alloc((SIFT_S + 3) * kmax * 4) || dcand.alloc(CAP * sizeof(SiftCand)) ||
-      dcnt.alloc(16) || dkp.alloc(CAP * sizeof(SiftKp)) || dptr.alloc(n_oct * (SIFT_S + 3) * sizeof(float*)) ||
-      dow.alloc(n_oct * 4) || doh.alloc(n_oct * 4))
+  SiftWork& Wk = sift_work(device);
+  DBuf &dimg = Wk.dimg, &dg = Wk.dg, &dd = Wk.dd, &dtmp = Wk.dtmp, &dk = Wk.dk, &dcand = Wk.dcand, &dcnt = Wk.dcnt;
+  DBuf &dkp = Wk.dkp, &dptr = Wk.dptr, &dow = Wk.dow, &doh = Wk.doh, &dsel = Wk.dsel, &ddes = Wk.ddes;
+  if (dimg.reserve((size_t)width * height) || dg.reserve((size_t)gtot * 4) || dd.reserve((size_t)dtot * 4) ||
+      dtmp.reserve((size_t)W0 * H0 * 4) || dk.reserve((SIFT_S + 3) * kmax * 4) || dcand.reserve(CAP * sizeof(SiftCand)) ||
+      dcnt.reserve(16) || dkp.reserve(CAP * sizeof(SiftKp)) || dptr.reserve(n_oct * (SIFT_S + 3) * sizeof(float*)) ||
+      dow.reserve(n_oct * 4) || doh.reserve(n_oct * 4))
     return -1;
   HIPCHK(hipMemcpy(dimg.p, img, (size_t)width * height, hipMemcpyHostToDevice));
   std::vector<float> kflat((SIFT_S + 3) * kmax, 0.f);
@@ -448,7 +463,7 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
   *n_out = n;
   n = std::min(n, (int)max_kp);
   if (n <= 0) return 0;
-  if (dsel.alloc((size_t)n * sizeof(SiftKp)) || ddes.alloc((size_t)n * 128 * 4)) return -1;
+  if (dsel.reserve((size_t)n * sizeof(SiftKp)) || ddes.reserve((size_t)n * 128 * 4)) return -1;
   HIPCHK(hipMemcpy(dsel.p, kps.data(), (size_t)n * sizeof(SiftKp), hipMemcpyHostToDevice));
   hipLaunchKernelGGL(k_sift_descr, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, nullptr, dsel.as<SiftKp>(), n,
                      (const float* const*)dptr.p, dow.as<int>(), doh.as<int>(), ddes.as<float>());

@@ -907,10 +907,17 @@ class LMSolver:
                         njev=it, nfev=nfev, iterations=it, lam=lam, time=t1 - t0, history=history)
 
 
+_solve_handles = {}
+
+
 def solve(n_pose, n_landmark, frame, landmark, xy, u, v, init_ptz, init_rays, weight=None, precision=FP64,
           loss=LOSS_LINEAR, f_scale=1.0, device=0, **lm_kw):
-    """Convenience one-shot solve.  Returns (ptz [N,3], rays [M,2], LMResult)."""
-    h = BAHandle(device)
+    """Convenience one-shot solve.  Returns (ptz [N,3], rays [M,2], LMResult).  One handle per device is kept
+    between calls (a keyframe map solves on every new keyframe: creating and destroying a handle -- stream,
+    pinned records, device buffers -- cost ~6 ms per call); set_problem replaces its problem."""
+    h = _solve_handles.get(device)
+    if h is None or h.h is None:
+        h = _solve_handles[device] = BAHandle(device)
     try:
         h.set_problem(n_pose, n_landmark, frame, landmark, xy, u, v, weight=weight, precision=precision, loss=loss,
                       f_scale=f_scale)
@@ -918,5 +925,7 @@ def solve(n_pose, n_landmark, frame, landmark, xy, u, v, init_ptz, init_rays, we
         res = LMSolver(h, **lm_kw).run()
         ptz, rays = h.get_state()
         return ptz, rays, res
-    finally:
+    except Exception:
+        _solve_handles.pop(device, None)
         h.close()
+        raise
