@@ -74,25 +74,53 @@ __global__ void k_sift_up(int w, int h, const uint8_t* __restrict__ src, float* 
   dst[(int64_t)y * W + x] = ((by * top) + (ay * bot));
 }
 
-__global__ void k_sift_blur_rows(int w, int h, const float* __restrict__ src, float* __restrict__ dst,
-                                 const float* __restrict__ wt, int K) {
-  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
-  if (x >= w) return;
-  const int r = K / 2;
+// separable blur through LDS: a row segment (+ halo) / a column tile (+ halo rows) is read once; the
+// accumulation order over k is unchanged (bit-identical to the per-pixel form and to the oracle)
+constexpr int BLUR_RMAX = 32, BLUR_TX = 256, BLUR_CT = 64, BLUR_CR = 64;
+__global__ __launch_bounds__(BLUR_TX) void k_sift_blur_rows(int w, int h, const float* __restrict__ src,
+                                                             float* __restrict__ dst, const float* __restrict__ wt, int K) {
+  __shared__ float tile[BLUR_TX + 2 * BLUR_RMAX];
+  __shared__ float sw[2 * BLUR_RMAX + 1];
+  const int x0 = blockIdx.x * BLUR_TX, y = blockIdx.y, r = K / 2, t = threadIdx.x;
   const float* row = src + (int64_t)y * w;
+  for (int i = t; i < BLUR_TX + 2 * r; i += BLUR_TX) tile[i] = row[refl101(x0 + i - r, w)];
+  if (t < K) sw[t] = wt[t];
+  __syncthreads();
+  const int x = x0 + t;
+  if (x >= w) return;
   float acc = 0.f;
-  for (int k = 0; k < K; ++k) acc = (acc + (wt[k] * row[refl101(x + k - r, w)]));
+  for (int k = 0; k < K; ++k) acc = acc + sw[k] * tile[t + k];
   dst[(int64_t)y * w + x] = acc;
 }
 
-__global__ void k_sift_blur_cols(int w, int h, const float* __restrict__ src, float* __restrict__ dst,
-                                 const float* __restrict__ wt, int K) {
-  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+__global__ __launch_bounds__(256) void k_sift_blur_cols(int w, int h, const float* __restrict__ src,
+                                                         float* __restrict__ dst, const float* __restrict__ wt, int K) {
+  __shared__ float tile[BLUR_CR + 2 * BLUR_RMAX][BLUR_CT + 1];
+  __shared__ float sw[2 * BLUR_RMAX + 1];
+  const int tx = threadIdx.x & (BLUR_CT - 1), ty = threadIdx.x / BLUR_CT;  // 64 x 4
+  const int x0 = blockIdx.x * BLUR_CT, y0 = blockIdx.y * BLUR_CR, r = K / 2;
+  const int x = x0 + tx;
+  const int nrow = BLUR_CR + 2 * r;
+  for (int i = ty; i < nrow; i += 256 / BLUR_CT)
+    tile[i][tx] = x < w ? src[(int64_t)refl101(y0 + i - r, h) * w + x] : 0.f;
+  if (threadIdx.x < K) sw[threadIdx.x] = wt[threadIdx.x];
+  __syncthreads();
   if (x >= w) return;
-  const int r = K / 2;
-  float acc = 0.f;
-  for (int k = 0; k < K; ++k) acc = (acc + (wt[k] * src[(int64_t)refl101(y + k - r, h) * w + x]));
-  dst[(int64_t)y * w + x] = acc;
+  // four independent accumulation chains per thread (rows yb, yb + 4, yb + 8, yb + 12)
+  for (int yb = ty; yb < BLUR_CR; yb += 16) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float wk = sw[k];
+      a0 = a0 + wk * tile[yb + k][tx];
+      a1 = a1 + wk * tile[yb + 4 + k][tx];
+      a2 = a2 + wk * tile[yb + 8 + k][tx];
+      a3 = a3 + wk * tile[yb + 12 + k][tx];
+    }
+    const float a[4] = {a0, a1, a2, a3};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (y0 + yb + 4 * q < h) dst[(int64_t)(y0 + yb + 4 * q) * w + x] = a[q];
+  }
 }
 
 __global__ void k_sift_down(int sw, const float* __restrict__ src, int dw, int dh, float* __restrict__ dst) {
@@ -391,6 +419,7 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
     kern[i] = sift_kernel(std::sqrt((prev * kf) * (prev * kf) - prev * prev));
     kmax = std::max(kmax, kern[i].size());
   }
+  if ((int)kmax / 2 > BLUR_RMAX) return fail("blur radius %d exceeds %d", (int)kmax / 2, BLUR_RMAX);
   const int CAP = 1 << 17;
   SiftWork& Wk = sift_work(device);
   DBuf &dimg = Wk.dimg, &dg = Wk.dg, &dd = Wk.dd, &dtmp = Wk.dtmp, &dk = Wk.dk, &dcand = Wk.dcand, &dcnt = Wk.dcnt;
@@ -415,11 +444,10 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
     for (int i = 0; i < SIFT_S + 3; ++i) gptr[o * (SIFT_S + 3) + i] = G + goff[o] + (int64_t)i * ow[o] * oh[o];
   HIPCHK(hipMemcpy(dptr.p, gptr.data(), gptr.size() * sizeof(float*), hipMemcpyHostToDevice));
   auto blur = [&](int w, int h, const float* src, float* dst, int ki) {
-    const dim3 g((unsigned)((w + 127) / 128), (unsigned)h);
-    hipLaunchKernelGGL(k_sift_blur_rows, g, dim3(128), 0, nullptr, w, h, src, T, dk.as<float>() + ki * kmax,
-                       (int)kern[ki].size());
-    hipLaunchKernelGGL(k_sift_blur_cols, g, dim3(128), 0, nullptr, w, h, T, dst, dk.as<float>() + ki * kmax,
-                       (int)kern[ki].size());
+    hipLaunchKernelGGL(k_sift_blur_rows, dim3((unsigned)((w + BLUR_TX - 1) / BLUR_TX), (unsigned)h), dim3(BLUR_TX), 0,
+                       nullptr, w, h, src, T, dk.as<float>() + ki * kmax, (int)kern[ki].size());
+    hipLaunchKernelGGL(k_sift_blur_cols, dim3((unsigned)((w + BLUR_CT - 1) / BLUR_CT), (unsigned)((h + BLUR_CR - 1) / BLUR_CR)),
+                       dim3(256), 0, nullptr, w, h, T, dst, dk.as<float>() + ki * kmax, (int)kern[ki].size());
   };
   // base: doubled image, then the blur from the assumed input blur to sigma
   hipLaunchKernelGGL(k_sift_up, dim3((unsigned)((W0 + 127) / 128), (unsigned)H0), dim3(128), 0, nullptr, width, height,
