@@ -60,6 +60,9 @@ def detect_compute_sift(im, nfeatures, verbose=False):
     return key_point, des
 
 
+_gpu_detect_compute_sift = detect_compute_sift
+
+
 def detect_sift(im, nfeatures=50):
     """image_process.py:14-33 on the GPU: SIFT keypoint locations [n, 2] float32."""
     import ptzba
@@ -69,8 +72,13 @@ def detect_sift(im, nfeatures=50):
 
 def detect_compute_sift_array(im, nfeatures, norm=True):
     """image_process.py:82-102: keypoints as an [N,2] array, descriptors (L2-normalised) [N,128]."""
-    kps, des = detect_compute_sift(im, nfeatures)
-    pts = np.array([k.pt for k in kps], dtype=np.float64).reshape(-1, 2)
+    if detect_compute_sift is _gpu_detect_compute_sift:  # the GPU default: straight from the arrays
+        import ptzba
+        kp, _, des = ptzba.sift(_grey_u8(im), int(nfeatures))
+        pts = kp[:, :2].astype(np.float64)
+    else:  # a correspondence source assigned its own detector
+        kps, des = detect_compute_sift(im, nfeatures)
+        pts = np.array([k.pt for k in kps], dtype=np.float64).reshape(-1, 2)
     des = np.asarray(des)
     if norm and len(des):
         des = (des / np.linalg.norm(des, axis=1).reshape(-1, 1)).astype(np.float64)

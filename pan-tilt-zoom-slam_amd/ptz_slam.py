@@ -153,12 +153,24 @@ class PtzSlam:
             new_keypoints = new_keypoints[bounding_box_mask_index]
             new_des = new_des[bounding_box_mask_index]
 
-        # remove keypoints within 50 px of the projected existing rays (ptz_slam.py:357-370)
-        mask = np.ones(img.shape[0:2], np.uint8)
-        for j in range(len(keypoints)):
-            x, y = keypoints[j]
-            mask[int(max(0, y - 50)):int(min(height, y + 50)), int(max(0, x - 50)):int(min(width, x + 50))] = 0
-        existing_keypoints_mask_index = keypoints_masking(new_keypoints, mask)
+        # remove keypoints within 50 px of the projected existing rays (ptz_slam.py:357-370): the reference zeroes
+        # a 100 x 100 box of a mask per existing point, then keeps the keypoints whose integer pixel is still 1;
+        # the same boxes (same integer bounds) tested against all keypoints at once
+        kp_old = np.asarray(keypoints, np.float64).reshape(-1, 2)
+        nk = np.asarray(new_keypoints, np.float64).reshape(-1, 2)
+        if len(kp_old) and len(nk):
+            ylo = np.maximum(0.0, kp_old[:, 1] - 50).astype(np.int64)
+            yhi = np.minimum(float(height), kp_old[:, 1] + 50).astype(np.int64)
+            xlo = np.maximum(0.0, kp_old[:, 0] - 50).astype(np.int64)
+            xhi = np.minimum(float(width), kp_old[:, 0] + 50).astype(np.int64)
+            xi, yi = nk[:, 0].astype(np.int64), nk[:, 1].astype(np.int64)
+            covered = np.zeros(len(nk), bool)
+            for a in range(0, len(kp_old), 256):  # bounded temporaries
+                b = slice(a, a + 256)
+                covered |= ((ylo[b, None] <= yi) & (yi < yhi[b, None]) & (xlo[b, None] <= xi) & (xi < xhi[b, None])).any(0)
+            existing_keypoints_mask_index = np.flatnonzero(~covered).astype(np.int32)
+        else:
+            existing_keypoints_mask_index = np.arange(len(nk), dtype=np.int32)
         new_keypoints = new_keypoints[existing_keypoints_mask_index]
         new_des = new_des[existing_keypoints_mask_index]
 
