@@ -25,6 +25,16 @@
 
 namespace ptzba {
 
+// Per-device work buffers of one entry point, kept across calls (grown by DBuf::reserve, never shrunk,
+// deliberately not freed at exit): the stream and the keyframe maps call these per frame / per pair.
+template <typename Work>
+Work& work_for(int device) {
+  static std::vector<Work*> w;
+  if ((int)w.size() <= device) w.resize(device + 1, nullptr);
+  if (!w[device]) w[device] = new Work;
+  return *w[device];
+}
+
 constexpr int KT = 64, KC = 16;  // distance tile, k-chunk
 
 __global__ __launch_bounds__(256) void k_sqdist(int n1, int n2, int dim, const float* __restrict__ a,
@@ -356,9 +366,13 @@ int ptz_match_knn2(int device, int64_t n1, int64_t n2, int32_t dim, const float*
     return 0;
   }
   if (select_device(device)) return -1;
-  DBuf a, b, d, idx, dist;
-  if (a.alloc((size_t)n1 * dim * 4) || b.alloc((size_t)n2 * dim * 4) || d.alloc((size_t)n1 * n2 * 4) ||
-      idx.alloc((size_t)n1 * 8) || dist.alloc((size_t)n1 * 8))
+  struct KnnWork {
+    DBuf a, b, d, idx, dist;
+  };
+  KnnWork& Wk = work_for<KnnWork>(device);  // kept across calls: a keyframe matches ~15 pairs
+  DBuf &a = Wk.a, &b = Wk.b, &d = Wk.d, &idx = Wk.idx, &dist = Wk.dist;
+  if (a.reserve((size_t)n1 * dim * 4) || b.reserve((size_t)n2 * dim * 4) || d.reserve((size_t)n1 * n2 * 4) ||
+      idx.reserve((size_t)n1 * 8) || dist.reserve((size_t)n1 * 8))
     return -1;
   HIPCHK(hipMemcpy(a.p, des1, (size_t)n1 * dim * 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(b.p, des2, (size_t)n2 * dim * 4, hipMemcpyHostToDevice));
@@ -395,9 +409,13 @@ int ptz_homography_ransac(int device, int64_t n, const double* pts1, const doubl
     N.s2 = d2 > 0 ? std::sqrt(2.0) * n / d2 : 1.0;
   }
   if (select_device(device)) return -1;
-  DBuf p1, p2, best, mask, H, nin;
-  if (p1.alloc((size_t)n * 16) || p2.alloc((size_t)n * 16) || best.alloc(8) || mask.alloc((size_t)n) ||
-      H.alloc(72) || nin.alloc(4))
+  struct RansacWork {
+    DBuf p1, p2, best, mask, H, nin;
+  };
+  RansacWork& Wk = work_for<RansacWork>(device);
+  DBuf &p1 = Wk.p1, &p2 = Wk.p2, &best = Wk.best, &mask = Wk.mask, &H = Wk.H, &nin = Wk.nin;
+  if (p1.reserve((size_t)n * 16) || p2.reserve((size_t)n * 16) || best.reserve(8) || mask.reserve((size_t)n) ||
+      H.reserve(72) || nin.reserve(4))
     return -1;
   HIPCHK(hipMemcpy(p1.p, pts1, (size_t)n * 16, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(p2.p, pts2, (size_t)n * 16, hipMemcpyHostToDevice));

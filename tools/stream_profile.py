@@ -28,3 +28,4 @@ with contextlib.redirect_stdout(io.StringIO()):
     pr.disable()
 st = pstats.Stats(pr)
 st.sort_stats("tottime").print_stats(25)
+st.sort_stats("cumtime").print_stats(45)
