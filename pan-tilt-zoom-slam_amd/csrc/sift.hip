@@ -470,14 +470,16 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
   HIPCHK(hipGetLastError());
   int cnt[2];
   HIPCHK(hipMemcpy(cnt, dcnt.p, 8, hipMemcpyDeviceToHost));
-  const int nc = std::min(cnt[0], CAP);
+  if (cnt[0] > CAP) return fail("%d SIFT extrema exceed the candidate list (%d)", cnt[0], CAP);
+  const int nc = cnt[0];
   if (nc > 0)
     hipLaunchKernelGGL(k_sift_orient, dim3((unsigned)((nc + 3) / 4)), dim3(256), 0, nullptr, dcand.as<SiftCand>(),
                        dcnt.as<int>(), (const float* const*)dptr.p, dow.as<int>(), doh.as<int>(), dkp.as<SiftKp>(),
                        dcnt.as<int>() + 1, CAP);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(cnt, dcnt.p, 8, hipMemcpyDeviceToHost));
-  const int nk = std::min(cnt[1], CAP);
+  if (cnt[1] > CAP) return fail("%d SIFT keypoints exceed the keypoint list (%d)", cnt[1], CAP);
+  const int nk = cnt[1];
   std::vector<SiftKp> kps(nk);
   if (nk) HIPCHK(hipMemcpy(kps.data(), dkp.p, (size_t)nk * sizeof(SiftKp), hipMemcpyDeviceToHost));
   std::stable_sort(kps.begin(), kps.end(), [](const SiftKp& a, const SiftKp& b) {
