@@ -2,6 +2,9 @@
 // the exact replacement of scipy's dense trf solve at bundle_adjustment.py:200-202).
 // Compiled without SLP vectorisation: packing the per-lane FMA chains into v_pk_* operations with
 // register shuffles serialises them (dependent pk_mul -> pk_fma -> pk_add chains with s_nop hazards).
+#include <cstdlib>
+#include <string>
+
 #include "ptzba_common.h"
 #include "ptzba_kernels.h"
 
@@ -62,6 +65,63 @@ __device__ __forceinline__ void load_w6(real (&x)[6], const real* __restrict__ p
   }
 }
 
+// chunk-0 items: diagonal terms of the F1 frames over this split's landmarks: U, g_pose and W V~^-1 g,
+// read from the dense slots (thread = (landmark j0 + 16 k, frame i): consecutive threads, consecutive
+// slots), reduced through `red` ([512][12] doubles of LDS that is free until staging) into part_diag.
+template <typename real>
+__device__ __forceinline__ void schur_diag_terms(const SchurArgs& a, const int4* sL, int nl, int f1b, int item,
+                                                 bool alt, double* red) {
+  const int t = threadIdx.x;
+  const real* __restrict__ w_slot = (const real*)(alt ? a.w_slot1 : a.w_slot);
+  const real* __restrict__ ug_slot = (const real*)(alt ? a.ug_slot1 : a.ug_slot);
+  const int i = t & (SF - 1), f = f1b + i;
+  double acc[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) acc[k] = 0;
+  // DU landmarks per thread and step, all loads issued before any is consumed (clamped, branch-free)
+  constexpr int DU = S2_DU, JS = 512 / SF;
+  for (int j0 = t >> 5; j0 < nl; j0 += DU * JS) {
+    real u[DU][12], w[DU][6];
+    double vg[DU][2];
+    bool in[DU];
+#pragma unroll
+    for (int d = 0; d < DU; ++d) {
+      const int j = j0 + d * JS;
+      const int4 m = sL[min(j, nl - 1)];
+      in[d] = j < nl && f >= m.y && f <= m.z;
+      const int64_t slot = m.w + min(max(f - m.y, 0), m.z - m.y);
+      load_w6(w[d], w_slot + slot * 8);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const auto v4 = reinterpret_cast<const typename std::conditional<sizeof(real) == 4, float4, double4>::type*>(
+            ug_slot + slot * 12)[k];
+        u[d][4 * k] = v4.x; u[d][4 * k + 1] = v4.y; u[d][4 * k + 2] = v4.z; u[d][4 * k + 3] = v4.w;
+      }
+      const double* vi = a.lm_aux + (int64_t)m.x * 8;
+      vg[d][0] = vi[3];
+      vg[d][1] = vi[4];
+    }
+#pragma unroll
+    for (int d = 0; d < DU; ++d) {
+      if (in[d]) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) acc[k] += (double)u[d][k];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) acc[9 + q] += (double)w[d][2 * q] * vg[d][0] + (double)w[d][2 * q + 1] * vg[d][1];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 12; ++k) red[t * 12 + k] = acc[k];
+  __syncthreads();
+  if (t < SF * 12) {
+    double v = 0;
+    for (int j0 = 0; j0 < 512 / SF; ++j0) v += red[j0 * SF * 12 + t];
+    a.part_diag[(int64_t)item * SF * 12 + t] = v;
+  }
+  __syncthreads();
+}
+
 #ifdef SK_TIMING
 __device__ long long g_sk[16][16];
 __device__ long long g_sk_items[4096][4];  // per item: start, end (s_memrealtime, 100 MHz), chunk, nl
@@ -111,58 +171,7 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
   __syncthreads();
   SK_T(1);
 
-  if (chunk == 0) {
-    // diagonal terms of the F1 frames over this split's landmarks: U, g_pose and W V~^-1 g, read from
-    // the dense slots (thread = (landmark j0 + 16 k, frame i): consecutive threads, consecutive slots)
-    const real* __restrict__ ug_slot = (const real*)(alt ? a.ug_slot1 : a.ug_slot);
-    const int i = t & (SF - 1), f = f1b + i;
-    double acc[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) acc[k] = 0;
-    // DU landmarks per thread and step, all loads issued before any is consumed (clamped, branch-free)
-    constexpr int DU = S2_DU, JS = 512 / SF;
-    for (int j0 = t >> 5; j0 < nl; j0 += DU * JS) {
-      real u[DU][12], w[DU][6];
-      double vg[DU][2];
-      bool in[DU];
-#pragma unroll
-      for (int d = 0; d < DU; ++d) {
-        const int j = j0 + d * JS;
-        const int4 m = sL[min(j, nl - 1)];
-        in[d] = j < nl && f >= m.y && f <= m.z;
-        const int64_t slot = m.w + min(max(f - m.y, 0), m.z - m.y);
-        load_w6(w[d], w_slot + slot * 8);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const auto v4 = reinterpret_cast<const typename std::conditional<sizeof(real) == 4, float4, double4>::type*>(
-              ug_slot + slot * 12)[k];
-          u[d][4 * k] = v4.x; u[d][4 * k + 1] = v4.y; u[d][4 * k + 2] = v4.z; u[d][4 * k + 3] = v4.w;
-        }
-        const double* vi = a.lm_aux + (int64_t)m.x * 8;
-        vg[d][0] = vi[3];
-        vg[d][1] = vi[4];
-      }
-#pragma unroll
-      for (int d = 0; d < DU; ++d) {
-        if (in[d]) {
-#pragma unroll
-          for (int k = 0; k < 9; ++k) acc[k] += (double)u[d][k];
-#pragma unroll
-          for (int q = 0; q < 3; ++q) acc[9 + q] += (double)w[d][2 * q] * vg[d][0] + (double)w[d][2 * q + 1] * vg[d][1];
-        }
-      }
-    }
-    double* red = reinterpret_cast<double*>(&sW[0][0][0][0]);  // [16][SF][12], free until staging
-#pragma unroll
-    for (int k = 0; k < 12; ++k) red[t * 12 + k] = acc[k];
-    __syncthreads();
-    if (t < SF * 12) {
-      double v = 0;
-      for (int j0 = 0; j0 < 512 / SF; ++j0) v += red[j0 * SF * 12 + t];
-      a.part_diag[(int64_t)item * SF * 12 + t] = v;
-    }
-    __syncthreads();
-  }
+  if (chunk == 0) schur_diag_terms<real>(a, sL, nl, f1b, item, alt, reinterpret_cast<double*>(&sW[0][0][0][0]));
   SK_T(2);
 
   // ---- staging registers: W slots (e = t, t + 512 over [SNB][64]) and one Y pair (j = t / SF, i = t % SF;
@@ -339,6 +348,170 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
   if (threadIdx.x == 0 && item < 4096) g_sk_items[item][1] = __builtin_amdgcn_s_memrealtime();
 #endif
 }
+// ------------------------------------------------------------------------------------------------
+// K2 on the matrix cores (fp32 path, the default): the same work items, split partials and diagonal
+// terms as k_schur; each batch of 16 landmarks is one k-step (K = 16 landmarks x 2 ray dimensions) of
+// v_mfma_f32_16x16x32_f16 over the item's 96 x 192 block S(F1 dofs, chunk dofs) -- 72 output blocks of
+// 16 x 16, nine per wave (3 row blocks x 3 column blocks).  Zero products (a landmark covers ~19 % of a
+// tile) cost matrix-core cycles instead of VALU issue.
+// Precision: every operand is split x = hi + lo into two fp16 (22 significant bits) and a product is
+// hi*hi + hi*lo + lo*hi (the dropped lo*lo is ~2^-22 of it), accumulated in fp32 per batch and flushed
+// to fp64 as in k_schur.  Range: W (~1e4 px^2) and Y = -W V~^-1 (~1) would not both fit fp16, so row
+// k = (landmark, d) of W is scaled by g_l = 2^round(log2 sqrt(tr V~_l^-1)) and the same row of Y by
+// 1 / g_l: the product Y^T W is unchanged (powers of two: exact), both factors ~ sqrt(|W| |Y|).
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+constexpr int MKP = 40;  // k pitch of an operand row in halves: 80-B rows keep the 16-B fragment reads aligned
+
+__device__ __forceinline__ void split_f16(float x, _Float16& h, _Float16& l) {
+  h = (_Float16)x;
+  l = (_Float16)(x - (float)h);  // x - h is exact in fp32
+}
+
+__global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
+  constexpr int SNB = 16;                // landmarks per batch
+  constexpr int NSL = SNB * WAVE / 512;  // W slots staged per thread per batch
+  __shared__ __attribute__((aligned(16))) _Float16 sY[2][2][3 * SF][MKP];     // [buf][hi|lo][q*32 + f1][2j + d]
+  __shared__ __attribute__((aligned(16))) _Float16 sWt[2][2][3 * WAVE][MKP];  // [buf][hi|lo][r*64 + f2][2j + d]
+  __shared__ int4 sL[SCHUR_LMAX];
+  __shared__ float sG[SCHUR_LMAX];  // g_l per landmark of the list
+  if (a.skip_if && *a.skip_if) return;
+  const int item = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int4 it = a.items[item];
+  const int f1b = it.x, chunk = it.y, lb = it.z, nl = it.w - it.z;
+  const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+  const int f2base = f1b + WAVE * chunk;
+  const bool alt = a.sel && *a.sel;  // device-chosen linearisation slot
+  const float* __restrict__ w_slot = (const float*)(alt ? a.w_slot1 : a.w_slot);
+  for (int k = t; k < nl; k += 512) {
+    const int4 m = a.item_lm[lb + k];
+    sL[k] = m;
+    const double* vi = a.lm_aux + (int64_t)m.x * 8;
+    int e = 0;
+    (void)frexp(vi[0] + vi[2], &e);
+    sG[k] = ldexpf(1.f, e / 2);
+  }
+  __syncthreads();
+  if (chunk == 0) schur_diag_terms<float>(a, sL, nl, f1b, item, alt, reinterpret_cast<double*>(&sWt[0][0][0][0]));
+
+  float rw[NSL][6], rgw[NSL], ryw[6], ryg;
+  bool rwin[NSL], ryin;
+  double rvi[3];
+  const int yj = t / SF, yi = t & (SF - 1);
+  auto fetch = [&](int p) {  // landmarks [p, p + SNB) of the list (clamped, branch-free)
+#pragma unroll
+    for (int q = 0; q < NSL; ++q) {
+      const int e = t + 512 * q, j = e >> 6, ln = e & 63;
+      const int jj = min(p + j, nl - 1);
+      const int4 m = sL[jj];
+      const int idx = f2base + ln - m.y;
+      rwin[q] = (p + j < nl) && idx >= 0 && f2base + ln <= m.z;
+      rgw[q] = sG[jj];
+      load_w6(rw[q], w_slot + (int64_t)(m.w + min(max(idx, 0), m.z - m.y)) * 8);
+    }
+    const int f = f1b + yi, jj = min(p + yj, nl - 1);
+    const int4 m = sL[jj];
+    ryin = (p + yj < nl) && f >= m.y && f <= m.z;
+    ryg = sG[jj];
+    load_w6(ryw, w_slot + (int64_t)(m.w + min(max(f - m.y, 0), m.z - m.y)) * 8);
+    const double* vi = a.lm_aux + (int64_t)m.x * 8;
+    rvi[0] = vi[0]; rvi[1] = vi[1]; rvi[2] = vi[2];
+  };
+  auto stage = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < NSL; ++q) {
+      const int e = t + 512 * q, j = e >> 6, ln = e & 63;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const float x0 = rwin[q] ? rw[q][2 * r] * rgw[q] : 0.f, x1 = rwin[q] ? rw[q][2 * r + 1] * rgw[q] : 0.f;
+        _Float16 h0, l0, h1, l1;
+        split_f16(x0, h0, l0);
+        split_f16(x1, h1, l1);
+        *reinterpret_cast<h2v*>(&sWt[buf][0][r * WAVE + ln][2 * j]) = h2v{h0, h1};
+        *reinterpret_cast<h2v*>(&sWt[buf][1][r * WAVE + ln][2 * j]) = h2v{l0, l1};
+      }
+    }
+    const double gi = 1.0 / (double)ryg;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const double W0 = ryin ? (double)ryw[2 * q] : 0.0, W1 = ryin ? (double)ryw[2 * q + 1] : 0.0;
+      // staged negated: the products accumulate -Y W^T
+      const float y0 = (float)(-(W0 * rvi[0] + W1 * rvi[1]) * gi), y1 = (float)(-(W0 * rvi[1] + W1 * rvi[2]) * gi);
+      _Float16 h0, l0, h1, l1;
+      split_f16(y0, h0, l0);
+      split_f16(y1, h1, l1);
+      *reinterpret_cast<h2v*>(&sY[buf][0][q * SF + yi][2 * yj]) = h2v{h0, h1};
+      *reinterpret_cast<h2v*>(&sY[buf][1][q * SF + yi][2 * yj]) = h2v{l0, l1};
+    }
+  };
+
+  const int rg = wv >> 2, cg = wv & 3;             // row blocks 3rg.., column blocks 3cg..
+  const int fr = lane & 15, fk = (lane >> 4) * 8;  // fragment row / column and k offset of this lane
+  double acc[3][3][4];
+#pragma unroll
+  for (int x = 0; x < 3; ++x)
+#pragma unroll
+    for (int y = 0; y < 3; ++y)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) acc[x][y][v] = 0;
+  if (nl > 0) {
+    fetch(0);
+    stage(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int p = 0; p < nl; p += SNB) {
+    const bool more = p + SNB < nl;  // block-uniform
+    fetch(p + SNB);                  // next batch's loads in flight during this batch's MFMAs
+    h8v ah[3], al[3], bh[3], bl[3];
+#pragma unroll
+    for (int x = 0; x < 3; ++x) {
+      const int row = 16 * (3 * rg + x) + fr, col = 16 * (3 * cg + x) + fr;
+      ah[x] = *reinterpret_cast<const h8v*>(&sY[buf][0][row][fk]);
+      al[x] = *reinterpret_cast<const h8v*>(&sY[buf][1][row][fk]);
+      bh[x] = *reinterpret_cast<const h8v*>(&sWt[buf][0][col][fk]);
+      bl[x] = *reinterpret_cast<const h8v*>(&sWt[buf][1][col][fk]);
+    }
+#pragma unroll
+    for (int x = 0; x < 3; ++x)
+#pragma unroll
+      for (int y = 0; y < 3; ++y) {
+        f4v c = {0.f, 0.f, 0.f, 0.f};
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[x], bh[y], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[x], bl[y], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[x], bh[y], c, 0, 0, 0);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[x][y][v] += (double)c[v];
+      }
+    if (more) stage(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // partial blocks of this split: part[item][f1 local][3q + r][f2], as k_schur writes them
+  float* out = (float*)a.part + (int64_t)item * (SF * 9 * WAVE);
+#pragma unroll
+  for (int x = 0; x < 3; ++x)
+#pragma unroll
+    for (int y = 0; y < 3; ++y)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int row = 16 * (3 * rg + x) + (lane >> 4) * 4 + v, col = 16 * (3 * cg + y) + fr;
+        const int q = row / SF, i = row % SF, r = col / WAVE, f2 = col % WAVE;
+        out[(i * 9 + 3 * q + r) * WAVE + f2] = (float)acc[x][y][v];
+      }
+}
+
+// PTZBA_SCHUR=valu selects the VALU kernel for the fp32 path (A/B measurements)
+static bool schur_use_mfma() {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("PTZBA_SCHUR");
+    mode = (e && std::string(e) == "valu") ? 0 : 1;
+  }
+  return mode == 1;
+}
+
 #ifdef SK_TIMING
 extern "C" int ptzba_debug_sk(long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sk), sizeof(g_sk)) == hipSuccess ? 0 : -1;
@@ -397,7 +570,12 @@ template <typename real>
 void launch_schur(const SchurArgs& a, int n_items, int n_groups, int n_fixed, hipStream_t st) {
   const int n_free = a.n_pose - n_fixed;
   if (n_free <= 0) return;
-  if (n_items > 0) hipLaunchKernelGGL(k_schur<real>, dim3(n_items), dim3(512), 0, st, a);
+  if (n_items > 0) {
+    if (sizeof(real) == 4 && schur_use_mfma())
+      hipLaunchKernelGGL(k_schur_mf, dim3(n_items), dim3(512), 0, st, a);
+    else
+      hipLaunchKernelGGL(k_schur<real>, dim3(n_items), dim3(512), 0, st, a);
+  }
   if (n_groups > 0) hipLaunchKernelGGL(k_schur_reduce<real>, dim3(SF * 9 * WAVE / 256, n_groups), dim3(256), 0, st, a);
 }
 
