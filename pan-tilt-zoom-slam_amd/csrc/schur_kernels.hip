@@ -362,7 +362,13 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
 typedef float f4v __attribute__((ext_vector_type(4)));
-constexpr int MKP = 40;  // k pitch of an operand row in halves: 80-B rows keep the 16-B fragment reads aligned
+constexpr int MKP = 40;
+#ifndef MF_STAGE_ALWAYS
+#define MF_STAGE_ALWAYS 0
+#endif
+#ifndef MF_FLUSH
+#define MF_FLUSH 4  // batches (of 16 landmarks) accumulated in fp32 between fp64 flushes
+#endif  // k pitch of an operand row in halves: 80-B rows keep the 16-B fragment reads aligned
 
 __device__ __forceinline__ void split_f16(float x, _Float16& h, _Float16& l) {
   h = (_Float16)x;
@@ -397,7 +403,7 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
 
   float rw[NSL][6], rgw[NSL], ryw[6], ryg;
   bool rwin[NSL], ryin;
-  double rvi[3];
+  float rvi[3];
   const int yj = t / SF, yi = t & (SF - 1);
   auto fetch = [&](int p) {  // landmarks [p, p + SNB) of the list (clamped, branch-free)
 #pragma unroll
@@ -416,7 +422,7 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
     ryg = sG[jj];
     load_w6(ryw, w_slot + (int64_t)(m.w + min(max(f - m.y, 0), m.z - m.y)) * 8);
     const double* vi = a.lm_aux + (int64_t)m.x * 8;
-    rvi[0] = vi[0]; rvi[1] = vi[1]; rvi[2] = vi[2];
+    rvi[0] = (float)vi[0]; rvi[1] = (float)vi[1]; rvi[2] = (float)vi[2];
   };
   auto stage = [&](int buf) {
 #pragma unroll
@@ -432,12 +438,12 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
         *reinterpret_cast<h2v*>(&sWt[buf][1][r * WAVE + ln][2 * j]) = h2v{l0, l1};
       }
     }
-    const double gi = 1.0 / (double)ryg;
+    const float gi = 1.f / ryg;  // a power of two: exact
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      const double W0 = ryin ? (double)ryw[2 * q] : 0.0, W1 = ryin ? (double)ryw[2 * q + 1] : 0.0;
-      // staged negated: the products accumulate -Y W^T
-      const float y0 = (float)(-(W0 * rvi[0] + W1 * rvi[1]) * gi), y1 = (float)(-(W0 * rvi[1] + W1 * rvi[2]) * gi);
+      const float W0 = ryin ? ryw[2 * q] * gi : 0.f, W1 = ryin ? ryw[2 * q + 1] * gi : 0.f;
+      // staged negated: the products accumulate -Y W^T (fp32 is exact enough: the operand keeps 22 bits)
+      const float y0 = -fmaf(W0, rvi[0], W1 * rvi[1]), y1 = -fmaf(W0, rvi[1], W1 * rvi[2]);
       _Float16 h0, l0, h1, l1;
       split_f16(y0, h0, l0);
       split_f16(y1, h1, l1);
@@ -460,7 +466,12 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
     stage(0);
   }
   __syncthreads();
-  int buf = 0;
+  int buf = 0, nb = 0;
+  f4v c[3][3];
+#pragma unroll
+  for (int x = 0; x < 3; ++x)
+#pragma unroll
+    for (int y = 0; y < 3; ++y) c[x][y] = f4v{0.f, 0.f, 0.f, 0.f};
   for (int p = 0; p < nl; p += SNB) {
     const bool more = p + SNB < nl;  // block-uniform
     fetch(p + SNB);                  // next batch's loads in flight during this batch's MFMAs
@@ -477,14 +488,28 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
     for (int x = 0; x < 3; ++x)
 #pragma unroll
       for (int y = 0; y < 3; ++y) {
-        f4v c = {0.f, 0.f, 0.f, 0.f};
-        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[x], bh[y], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[x], bl[y], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[x], bh[y], c, 0, 0, 0);
-#pragma unroll
-        for (int v = 0; v < 4; ++v) acc[x][y][v] += (double)c[v];
+        c[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[x], bh[y], c[x][y], 0, 0, 0);
+        c[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[x], bl[y], c[x][y], 0, 0, 0);
+        c[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[x], bh[y], c[x][y], 0, 0, 0);
       }
+    // fp32 partial sums over MF_FLUSH batches, then into fp64 (block-uniform condition)
+    if (++nb == MF_FLUSH || !more) {
+      nb = 0;
+#pragma unroll
+      for (int x = 0; x < 3; ++x)
+#pragma unroll
+        for (int y = 0; y < 3; ++y) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) acc[x][y][v] += (double)c[x][y][v];
+          c[x][y] = f4v{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+#if MF_STAGE_ALWAYS
+    stage(buf ^ 1);  // unconditional (past the list it stages zeros nobody reads): no branch between the
+                     // MFMAs and the staging VALU work, so the scheduler can interleave them
+#else
     if (more) stage(buf ^ 1);
+#endif
     __syncthreads();
     buf ^= 1;
   }
