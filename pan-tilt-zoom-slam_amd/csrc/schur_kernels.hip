@@ -360,19 +360,18 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
 // k = (landmark, d) of W is scaled by g_l = 2^round(log2 sqrt(tr V~_l^-1)) and the same row of Y by
 // 1 / g_l: the product Y^T W is unchanged (powers of two: exact), both factors ~ sqrt(|W| |Y|).
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
-typedef _Float16 h2v __attribute__((ext_vector_type(2)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 constexpr int MKP = 40;
-#ifndef MF_STAGE_ALWAYS
-#define MF_STAGE_ALWAYS 0
-#endif
 #ifndef MF_FLUSH
 #define MF_FLUSH 4  // batches (of 16 landmarks) accumulated in fp32 between fp64 flushes
 #endif  // k pitch of an operand row in halves: 80-B rows keep the 16-B fragment reads aligned
 
-__device__ __forceinline__ void split_f16(float x, _Float16& h, _Float16& l) {
-  h = (_Float16)x;
-  l = (_Float16)(x - (float)h);  // x - h is exact in fp32
+// (x0, x1) -> hi + lo, each a packed pair of fp16 (v_cvt_pkrtz: toward zero; x - hi is exact in fp32 and
+// has at most 13 significant bits, of which lo keeps 11)
+typedef __fp16 hp2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split_pk(float x0, float x1, hp2v& h, hp2v& l) {
+  h = __builtin_amdgcn_cvt_pkrtz(x0, x1);
+  l = __builtin_amdgcn_cvt_pkrtz(x0 - (float)h[0], x1 - (float)h[1]);
 }
 
 __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
@@ -401,80 +400,73 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
   __syncthreads();
   if (chunk == 0) schur_diag_terms<float>(a, sL, nl, f1b, item, alt, reinterpret_cast<double*>(&sWt[0][0][0][0]));
 
-  float rw[NSL][6], rgw[NSL], ryw[6], ryg;
-  bool rwin[NSL], ryin;
-  float rvi[3];
+  // staging registers of one batch (two sets: the loads of batch p + 2 are issued while batch p is
+  // multiplied and batch p + 1 staged, so each load has two batches of MFMA time to arrive)
+  struct Pre {
+    float rw[NSL][6], rgw[NSL], ryw[6], ryg, rvi[3];
+    bool rwin[NSL], ryin;
+  };
   const int yj = t / SF, yi = t & (SF - 1);
-  auto fetch = [&](int p) {  // landmarks [p, p + SNB) of the list (clamped, branch-free)
+  auto fetch = [&](Pre& P, int p) {  // landmarks [p, p + SNB) of the list (clamped, branch-free)
 #pragma unroll
     for (int q = 0; q < NSL; ++q) {
       const int e = t + 512 * q, j = e >> 6, ln = e & 63;
       const int jj = min(p + j, nl - 1);
       const int4 m = sL[jj];
       const int idx = f2base + ln - m.y;
-      rwin[q] = (p + j < nl) && idx >= 0 && f2base + ln <= m.z;
-      rgw[q] = sG[jj];
-      load_w6(rw[q], w_slot + (int64_t)(m.w + min(max(idx, 0), m.z - m.y)) * 8);
+      P.rwin[q] = (p + j < nl) && idx >= 0 && f2base + ln <= m.z;
+      P.rgw[q] = sG[jj];
+      load_w6(P.rw[q], w_slot + (int64_t)(m.w + min(max(idx, 0), m.z - m.y)) * 8);
     }
     const int f = f1b + yi, jj = min(p + yj, nl - 1);
     const int4 m = sL[jj];
-    ryin = (p + yj < nl) && f >= m.y && f <= m.z;
-    ryg = sG[jj];
-    load_w6(ryw, w_slot + (int64_t)(m.w + min(max(f - m.y, 0), m.z - m.y)) * 8);
+    P.ryin = (p + yj < nl) && f >= m.y && f <= m.z;
+    P.ryg = sG[jj];
+    load_w6(P.ryw, w_slot + (int64_t)(m.w + min(max(f - m.y, 0), m.z - m.y)) * 8);
     const double* vi = a.lm_aux + (int64_t)m.x * 8;
-    rvi[0] = (float)vi[0]; rvi[1] = (float)vi[1]; rvi[2] = (float)vi[2];
+    P.rvi[0] = (float)vi[0]; P.rvi[1] = (float)vi[1]; P.rvi[2] = (float)vi[2];
   };
-  auto stage = [&](int buf) {
+  auto stage = [&](const Pre& P, int buf) {
 #pragma unroll
     for (int q = 0; q < NSL; ++q) {
       const int e = t + 512 * q, j = e >> 6, ln = e & 63;
+      const float gq = P.rwin[q] ? P.rgw[q] : 0.f;
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
-        const float x0 = rwin[q] ? rw[q][2 * r] * rgw[q] : 0.f, x1 = rwin[q] ? rw[q][2 * r + 1] * rgw[q] : 0.f;
-        _Float16 h0, l0, h1, l1;
-        split_f16(x0, h0, l0);
-        split_f16(x1, h1, l1);
-        *reinterpret_cast<h2v*>(&sWt[buf][0][r * WAVE + ln][2 * j]) = h2v{h0, h1};
-        *reinterpret_cast<h2v*>(&sWt[buf][1][r * WAVE + ln][2 * j]) = h2v{l0, l1};
+        hp2v h, l;
+        split_pk(P.rw[q][2 * r] * gq, P.rw[q][2 * r + 1] * gq, h, l);
+        *reinterpret_cast<hp2v*>(&sWt[buf][0][r * WAVE + ln][2 * j]) = h;
+        *reinterpret_cast<hp2v*>(&sWt[buf][1][r * WAVE + ln][2 * j]) = l;
       }
     }
-    const float gi = 1.f / ryg;  // a power of two: exact
+    // Y / g = -(W / g) V~^-1, staged negated: the products accumulate -Y W^T (fp32 is exact enough: the
+    // operand keeps 22 bits).  1 / g is a power of two: exact.
+    const float gi = P.ryin ? 1.f / P.ryg : 0.f;
+    const float v0 = P.rvi[0] * gi, v1 = P.rvi[1] * gi, v2 = P.rvi[2] * gi;
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      const float W0 = ryin ? ryw[2 * q] * gi : 0.f, W1 = ryin ? ryw[2 * q + 1] * gi : 0.f;
-      // staged negated: the products accumulate -Y W^T (fp32 is exact enough: the operand keeps 22 bits)
-      const float y0 = -fmaf(W0, rvi[0], W1 * rvi[1]), y1 = -fmaf(W0, rvi[1], W1 * rvi[2]);
-      _Float16 h0, l0, h1, l1;
-      split_f16(y0, h0, l0);
-      split_f16(y1, h1, l1);
-      *reinterpret_cast<h2v*>(&sY[buf][0][q * SF + yi][2 * yj]) = h2v{h0, h1};
-      *reinterpret_cast<h2v*>(&sY[buf][1][q * SF + yi][2 * yj]) = h2v{l0, l1};
+      const float W0 = P.ryw[2 * q], W1 = P.ryw[2 * q + 1];
+      hp2v h, l;
+      split_pk(-fmaf(W0, v0, W1 * v1), -fmaf(W0, v1, W1 * v2), h, l);
+      *reinterpret_cast<hp2v*>(&sY[buf][0][q * SF + yi][2 * yj]) = h;
+      *reinterpret_cast<hp2v*>(&sY[buf][1][q * SF + yi][2 * yj]) = l;
     }
   };
 
   const int rg = wv >> 2, cg = wv & 3;             // row blocks 3rg.., column blocks 3cg..
   const int fr = lane & 15, fk = (lane >> 4) * 8;  // fragment row / column and k offset of this lane
   double acc[3][3][4];
-#pragma unroll
-  for (int x = 0; x < 3; ++x)
-#pragma unroll
-    for (int y = 0; y < 3; ++y)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) acc[x][y][v] = 0;
-  if (nl > 0) {
-    fetch(0);
-    stage(0);
-  }
-  __syncthreads();
-  int buf = 0, nb = 0;
   f4v c[3][3];
 #pragma unroll
   for (int x = 0; x < 3; ++x)
 #pragma unroll
-    for (int y = 0; y < 3; ++y) c[x][y] = f4v{0.f, 0.f, 0.f, 0.f};
-  for (int p = 0; p < nl; p += SNB) {
-    const bool more = p + SNB < nl;  // block-uniform
-    fetch(p + SNB);                  // next batch's loads in flight during this batch's MFMAs
+    for (int y = 0; y < 3; ++y) {
+      c[x][y] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int v = 0; v < 4; ++v) acc[x][y][v] = 0;
+    }
+  int nb = 0;
+  auto compute = [&](int buf, bool last) {
     h8v ah[3], al[3], bh[3], bl[3];
 #pragma unroll
     for (int x = 0; x < 3; ++x) {
@@ -493,7 +485,7 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
         c[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[x], bh[y], c[x][y], 0, 0, 0);
       }
     // fp32 partial sums over MF_FLUSH batches, then into fp64 (block-uniform condition)
-    if (++nb == MF_FLUSH || !more) {
+    if (++nb == MF_FLUSH || last) {
       nb = 0;
 #pragma unroll
       for (int x = 0; x < 3; ++x)
@@ -504,14 +496,25 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
           c[x][y] = f4v{0.f, 0.f, 0.f, 0.f};
         }
     }
-#if MF_STAGE_ALWAYS
-    stage(buf ^ 1);  // unconditional (past the list it stages zeros nobody reads): no branch between the
-                     // MFMAs and the staging VALU work, so the scheduler can interleave them
-#else
-    if (more) stage(buf ^ 1);
-#endif
+  };
+  Pre A, B;
+  if (nl > 0) {
+    fetch(A, 0);
+    fetch(B, SNB);
+    stage(A, 0);
+  }
+  __syncthreads();
+  // batch p in buffer 0 from set A, batch p + SNB in buffer 1 from set B (block-uniform control flow)
+  for (int p = 0; p < nl; p += 2 * SNB) {
+    fetch(A, p + 2 * SNB);
+    compute(0, p + SNB >= nl);
+    if (p + SNB < nl) stage(B, 1);
     __syncthreads();
-    buf ^= 1;
+    if (p + SNB >= nl) break;
+    fetch(B, p + 3 * SNB);
+    compute(1, p + 2 * SNB >= nl);
+    if (p + 2 * SNB < nl) stage(A, 0);
+    __syncthreads();
   }
   // partial blocks of this split: part[item][f1 local][3q + r][f2], as k_schur writes them
   float* out = (float*)a.part + (int64_t)item * (SF * 9 * WAVE);
