@@ -69,6 +69,7 @@ struct ptzba_ctx {
   double* scal_host = nullptr;   // pinned host copy of scal_pack
   DBuf chol_tasks, Ldiag, Minv, dpose;  // Minv: inverses of the diagonal factor tiles (back-substitution)
   std::vector<int> chol_task_off;  // host: per elimination level, offsets into chol_tasks
+  std::vector<int32_t> chol_tasks_host;  // host copy of chol_tasks (int4 records)
   int chol_levels = 0, n_aug = 0, n_chain = 1;
   bool nested = false;
   DBuf frame_pos, row_pad, bs_chain_off, bs_chain_cols, bs_upd_off, bs_upd_tiles, bs_la_tasks;
@@ -665,6 +666,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   CholPlan plan;
   make_plan(sorder, n_pose, o.n_fixed, win, h->ld, plan);
   h->chol_task_off = plan.level_off;
+  h->chol_tasks_host = plan.tasks;
   h->chol_levels = plan.n_levels;
   h->n_chain = (int)plan.chain_off.size() - 1;
   frame_win_hi = win;  // K2 windows follow the same (possibly global) coupling
@@ -978,7 +980,8 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
                              h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
                              h->lambda, lam_dev, h->st);
   launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
-                  h->Ldiag.as<double>(), h->info.as<int>(), h->st);
+                  h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr,
+                  reinterpret_cast<const int4*>(h->chol_tasks_host.data()));
   launch_chol_backsolve(h->S(), h->ld, h->n_aug, h->n_chain, h->bs_npos, h->bs_chain_off.as<int>(),
                         h->bs_chain_cols.as<int>(), h->bs_upd_off.as<int>(), h->bs_upd_tiles.as<int>(), h->bs_nupd,
                         h->bs_la_tasks.as<int>(), h->bs_ntasks,

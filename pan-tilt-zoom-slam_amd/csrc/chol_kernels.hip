@@ -22,6 +22,9 @@
 // dissection: C then A, C then B), right-looking updates of an LDS-resident right-hand side.
 #include <algorithm>
 
+#include <cstdlib>
+#include <cstring>
+
 #include "ptzba_common.h"
 #include "ptzba_kernels.h"
 
@@ -638,10 +641,20 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
 #endif
 // SG: signed factor A = L Sigma L^T (indefinite systems: the EKF innovation block, ekf.hip); sgn[ld] holds
 // sigma per factored row, written by each column's diagonal task and applied to the update panels
-template <bool SG>
-__global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64_t ld,
-                                                   const int4* __restrict__ tasks, double* __restrict__ Ldiag,
-                                                   int* info, double* __restrict__ sgn) {
+// A level's tasks: by value in the kernel arguments when they fit (the workgroup's first dependent global
+// load -- tasks[blockIdx.x] before any tile address is known -- disappears from the level's critical path),
+// else a device array.
+struct CholTaskPtr {
+  const int4* p;
+  __device__ int4 get(int b) const { return p[b]; }
+};
+struct CholTaskVal {
+  int4 t[CHOL_KT];
+  __device__ int4 get(int b) const { return t[b]; }
+};
+template <bool SG, typename TaskArg>
+__global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64_t ld, const TaskArg tasks,
+                                                   double* __restrict__ Ldiag, int* info, double* __restrict__ sgn) {
   __shared__ double sC[NB][NB + 1];     // target tile (panel T_ik / trailing A_ij)
   __shared__ double sD[NB][NB + 1];     // diagonal tile -> L_kk
   __shared__ double sA[2][NB][NB + 1];  // L_ip of the two update panels
@@ -661,7 +674,7 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
 #endif
   __shared__ double s_sgp[2][NB];  // SG: signs of the two update panels' columns
   __shared__ double s_sig[NB];     // SG: signs of this column's pivots
-  const int4 tk = tasks[blockIdx.x];
+  const int4 tk = tasks.get(blockIdx.x);
   const int type = tk.x, i = tk.y, j = tk.z;
   const int up0 = (tk.w & 0x3fff) - 1;
   const int up1 = ((tk.w >> 14) & 0x3fff) - 1;
@@ -786,16 +799,25 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
 }
 
 void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_off_host, int n_launch, double* Ldiag,
-                     int* info, hipStream_t st, double* sgn) {
+                     int* info, hipStream_t st, double* sgn, const int4* tasks_host) {
+  static const bool by_value = !getenv("PTZBA_CHOL_TASKS_PTR");  // A/B knob
   for (int L = 0; L < n_launch; ++L) {
     const int n = task_off_host[L + 1] - task_off_host[L];
     if (n <= 0) continue;
+    if (tasks_host && by_value && n <= CHOL_KT) {
+      CholTaskVal tv;
+      std::memcpy(tv.t, tasks_host + task_off_host[L], n * sizeof(int4));
+      if (sgn)
+        hipLaunchKernelGGL((k_chol_step<true, CholTaskVal>), dim3(n), dim3(256), 0, st, A, ld, tv, Ldiag, info, sgn);
+      else
+        hipLaunchKernelGGL((k_chol_step<false, CholTaskVal>), dim3(n), dim3(256), 0, st, A, ld, tv, Ldiag, info, sgn);
+      continue;
+    }
+    const CholTaskPtr tp{tasks + task_off_host[L]};
     if (sgn)
-      hipLaunchKernelGGL(k_chol_step<true>, dim3(n), dim3(256), 0, st, A, ld, tasks + task_off_host[L], Ldiag, info,
-                         sgn);
+      hipLaunchKernelGGL((k_chol_step<true, CholTaskPtr>), dim3(n), dim3(256), 0, st, A, ld, tp, Ldiag, info, sgn);
     else
-      hipLaunchKernelGGL(k_chol_step<false>, dim3(n), dim3(256), 0, st, A, ld, tasks + task_off_host[L], Ldiag, info,
-                         sgn);
+      hipLaunchKernelGGL((k_chol_step<false, CholTaskPtr>), dim3(n), dim3(256), 0, st, A, ld, tp, Ldiag, info, sgn);
   }
 }
 

@@ -213,6 +213,7 @@ struct ptzekf_ctx {
   DBuf pred_xy, vis, obs_xy, idx, Hc, yv, M, tasks, Ldiag, info, ky3, sgn;
   std::vector<uint8_t> vis_h;
   std::vector<int> task_off;
+  std::vector<int4> tasks_host;
   int64_t plan_ld = -1;
   int plan_mp = -1, n_launch = 0;
   int64_t ns() const { return 3 + 2 * (int64_t)n_ray; }
@@ -247,6 +248,7 @@ static int build_partial_plan(ptzekf_ctx* h, int64_t ld, int mp) {
   if (h->tasks.reserve(tasks.size() * sizeof(int4) + 16)) return -1;
   HIPCHK(hipMemcpyAsync(h->tasks.p, tasks.data(), tasks.size() * sizeof(int4), hipMemcpyHostToDevice, h->st));
   HIPCHK(hipStreamSynchronize(h->st));  // ordered before the factorisation launches on h->st
+  h->tasks_host = tasks;
   h->plan_ld = ld;
   h->plan_mp = mp;
   return 0;
@@ -492,7 +494,7 @@ int ptzekf_update(ptzekf_handle h, double u, double v, const double* disp6, doub
   //    write-back (ptz_slam.py:282-289) leaves P indefinite after some frames, so S can have negative
   //    eigenvalues; for an SPD S the signed factor is the Cholesky factor, bit for bit.
   launch_cholesky(M, d.ld, h->tasks.as<int4>(), h->task_off.data(), h->n_launch, h->Ldiag.as<double>(),
-                  h->info.as<int>(), h->st, h->sgn.as<double>());
+                  h->info.as<int>(), h->st, h->sgn.as<double>(), h->tasks_host.data());
   HIPCHK(hipGetLastError());
   // 5. state update and covariance write-back (skipped on the device when S was not SPD)
   hipLaunchKernelGGL(k_ekf_apply_vec, dim3(nblk(std::max(nr, 9))), dim3(256), 0, h->st, d, d_matched, M,

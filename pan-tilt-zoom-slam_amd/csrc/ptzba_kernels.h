@@ -144,8 +144,10 @@ void launch_chol_prepare_damped(double* A, int64_t ld, int n, double* b, const u
                                 const double* dU, double* D_pose, const int32_t* frame_pos, int n_pose, int n_fixed,
                                 double lambda, const double* lam_dev, hipStream_t st);
 // sgn != nullptr: signed factor L Sigma L^T of an indefinite matrix (sigma per row into sgn[ld])
+// tasks_host (optional, the host copy of `tasks`): levels of <= CHOL_KT tasks pass them by value
+constexpr int CHOL_KT = 240;  // 3.75 KB of kernel arguments
 void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_off_host, int n_launch, double* Ldiag,
-                     int* info, hipStream_t st, double* sgn = nullptr);
+                     int* info, hipStream_t st, double* sgn = nullptr, const int4* tasks_host = nullptr);
 // la_tasks: lookahead back substitution's [lookahead tile per position | task offsets per (chain, helper) |
 // tasks q << 16 | tile], built by the host plan (api.hip make_plan)
 constexpr int BS_HELPERS = 7;
