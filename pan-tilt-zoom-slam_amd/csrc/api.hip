@@ -594,7 +594,9 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     // rounding, at least 64 landmarks, at most SCHUR_LMAX (the LDS list).  Chunk-0 items also sum the
     // diagonal terms (~25 % more time per landmark, measured with tools/schur_timing.py): their lists
     // are weighted so that every item takes about the same time and the two rounds pack evenly.
-    constexpr int64_t W0 = 5, WD = 4;  // chunk-0 weight W0 / WD
+    int64_t W0 = 5;
+    constexpr int64_t WD = 4;  // chunk-0 weight W0 / WD
+    if (const char* e = getenv("PTZBA_S2_W0")) W0 = std::max(1, atoi(e));  // A/B knob
     int64_t total_w = 0;
     for (size_t k = 0; k < tiles.size(); ++k)
       total_w += (int64_t)tiles[k].size() * (tile_key[2 * k + 1] == 0 ? W0 : WD);

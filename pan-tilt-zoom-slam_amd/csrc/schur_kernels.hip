@@ -362,6 +362,12 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 constexpr int MKP = 40;
+#ifndef MF_DIAG_FUSED
+#define MF_DIAG_FUSED 1  // chunk-0 diagonal terms inside the batch pipeline (0: a phase before it)
+#endif
+#ifndef MF_ABL
+#define MF_ABL 0  // ablations for measurements: 1 = no MFMAs, 2 = no operand loads, 3 = no staging
+#endif
 #ifndef MF_FLUSH
 #define MF_FLUSH 4  // batches (of 16 landmarks) accumulated in fp32 between fp64 flushes
 #endif  // k pitch of an operand row in halves: 80-B rows keep the 16-B fragment reads aligned
@@ -382,8 +388,24 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
   __shared__ int4 sL[SCHUR_LMAX];
   __shared__ float sG[SCHUR_LMAX];  // g_l per landmark of the list
   if (a.skip_if && *a.skip_if) return;
+#ifdef SK_TIMING
+  const bool skrec = threadIdx.x == 0 && blockIdx.x < 16;
+  long long* sk = g_sk[blockIdx.x & 15];
+  if (skrec)
+    for (int k = 0; k < 16; ++k) sk[k] = 0;
+#endif
+  long long skt = 0;
+  (void)skt;
+  SK_T(0);
   const int item = xcd_swizzle(blockIdx.x, gridDim.x);
   const int4 it = a.items[item];
+#ifdef SK_TIMING
+  if (threadIdx.x == 0 && item < 4096) {
+    g_sk_items[item][0] = __builtin_amdgcn_s_memrealtime();
+    g_sk_items[item][2] = it.y;
+    g_sk_items[item][3] = it.w - it.z;
+  }
+#endif
   const int f1b = it.x, chunk = it.y, lb = it.z, nl = it.w - it.z;
   const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
   const int f2base = f1b + WAVE * chunk;
@@ -398,7 +420,10 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
     sG[k] = ldexpf(1.f, e / 2);
   }
   __syncthreads();
+  SK_T(1);
+#if !MF_DIAG_FUSED
   if (chunk == 0) schur_diag_terms<float>(a, sL, nl, f1b, item, alt, reinterpret_cast<double*>(&sWt[0][0][0][0]));
+#endif
 
   // staging registers of one batch (two sets: the loads of batch p + 2 are issued while batch p is
   // multiplied and batch p + 1 staged, so each load has two batches of MFMA time to arrive)
@@ -416,17 +441,24 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
       const int idx = f2base + ln - m.y;
       P.rwin[q] = (p + j < nl) && idx >= 0 && f2base + ln <= m.z;
       P.rgw[q] = sG[jj];
+      if (MF_ABL == 2) { for (int k = 0; k < 6; ++k) P.rw[q][k] = (float)(m.w & 7); } else
       load_w6(P.rw[q], w_slot + (int64_t)(m.w + min(max(idx, 0), m.z - m.y)) * 8);
     }
     const int f = f1b + yi, jj = min(p + yj, nl - 1);
     const int4 m = sL[jj];
     P.ryin = (p + yj < nl) && f >= m.y && f <= m.z;
     P.ryg = sG[jj];
+    if (MF_ABL == 2) {
+      for (int k = 0; k < 6; ++k) P.ryw[k] = (float)(m.w & 3);
+      P.rvi[0] = P.rvi[1] = P.rvi[2] = (float)(m.x & 1);
+      return;
+    }
     load_w6(P.ryw, w_slot + (int64_t)(m.w + min(max(f - m.y, 0), m.z - m.y)) * 8);
     const double* vi = a.lm_aux + (int64_t)m.x * 8;
     P.rvi[0] = (float)vi[0]; P.rvi[1] = (float)vi[1]; P.rvi[2] = (float)vi[2];
   };
   auto stage = [&](const Pre& P, int buf) {
+    if (MF_ABL == 3) return;
 #pragma unroll
     for (int q = 0; q < NSL; ++q) {
       const int e = t + 512 * q, j = e >> 6, ln = e & 63;
@@ -467,23 +499,26 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
     }
   int nb = 0;
   auto compute = [&](int buf, bool last) {
-    h8v ah[3], al[3], bh[3], bl[3];
+    h8v bh[3], bl[3];
 #pragma unroll
-    for (int x = 0; x < 3; ++x) {
-      const int row = 16 * (3 * rg + x) + fr, col = 16 * (3 * cg + x) + fr;
-      ah[x] = *reinterpret_cast<const h8v*>(&sY[buf][0][row][fk]);
-      al[x] = *reinterpret_cast<const h8v*>(&sY[buf][1][row][fk]);
-      bh[x] = *reinterpret_cast<const h8v*>(&sWt[buf][0][col][fk]);
-      bl[x] = *reinterpret_cast<const h8v*>(&sWt[buf][1][col][fk]);
+    for (int y = 0; y < 3; ++y) {
+      const int col = 16 * (3 * cg + y) + fr;
+      bh[y] = *reinterpret_cast<const h8v*>(&sWt[buf][0][col][fk]);
+      bl[y] = *reinterpret_cast<const h8v*>(&sWt[buf][1][col][fk]);
     }
 #pragma unroll
-    for (int x = 0; x < 3; ++x)
+    for (int x = 0; x < 3; ++x) {
+      const int row = 16 * (3 * rg + x) + fr;
+      const h8v ah = *reinterpret_cast<const h8v*>(&sY[buf][0][row][fk]);
+      const h8v al = *reinterpret_cast<const h8v*>(&sY[buf][1][row][fk]);
 #pragma unroll
       for (int y = 0; y < 3; ++y) {
-        c[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[x], bh[y], c[x][y], 0, 0, 0);
-        c[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[x], bl[y], c[x][y], 0, 0, 0);
-        c[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[x], bh[y], c[x][y], 0, 0, 0);
+        if (MF_ABL == 1) { c[x][y][0] += (float)ah[0] + (float)bl[y][1]; continue; }
+        c[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[y], c[x][y], 0, 0, 0);
+        c[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[y], c[x][y], 0, 0, 0);
+        c[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[y], c[x][y], 0, 0, 0);
       }
+    }
     // fp32 partial sums over MF_FLUSH batches, then into fp64 (block-uniform condition)
     if (++nb == MF_FLUSH || last) {
       nb = 0;
@@ -497,25 +532,104 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
         }
     }
   };
+  SK_T(2);
+#if MF_DIAG_FUSED
+  // chunk-0 items: the diagonal terms (U, g_pose, W V~^-1 g of the F1 frames; HBM-bound, ~100 MB per
+  // build) ride in the batch pipeline instead of a phase of their own: the thread that stages Y of
+  // (landmark, f1) also sums that pair's terms, its U|g loads issued one batch ahead, under the MFMAs.
+  const bool diag = chunk == 0;
+  const float* __restrict__ ug_slot = (const float*)(alt ? a.ug_slot1 : a.ug_slot);
+  float du[9], dvg[2];
+  float dacc[12];  // fp32 over the item's <= 32 batches: one term per batch (the reduction below is fp64)
+#pragma unroll
+  for (int k = 0; k < 12; ++k) dacc[k] = 0.f;
+  auto dfetch = [&](int p) {
+    const int4 m = sL[min(p + yj, nl - 1)];
+    const int64_t slot = m.w + min(max(f1b + yi - m.y, 0), m.z - m.y);
+    const float4 u0 = reinterpret_cast<const float4*>(ug_slot + slot * 12)[0];
+    const float4 u1 = reinterpret_cast<const float4*>(ug_slot + slot * 12)[1];
+    du[0] = u0.x; du[1] = u0.y; du[2] = u0.z; du[3] = u0.w;
+    du[4] = u1.x; du[5] = u1.y; du[6] = u1.z; du[7] = u1.w;
+    du[8] = ug_slot[slot * 12 + 8];
+    const double* vi = a.lm_aux + (int64_t)m.x * 8;
+    dvg[0] = (float)vi[3];
+    dvg[1] = (float)vi[4];
+  };
+  auto daccum = [&](const Pre& P) {
+    if (P.ryin) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) dacc[k] += du[k];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) dacc[9 + q] += fmaf(P.ryw[2 * q], dvg[0], P.ryw[2 * q + 1] * dvg[1]);
+    }
+  };
+#else
+  constexpr bool diag = false;
+  auto dfetch = [&](int) {};
+  auto daccum = [&](const Pre&) {};
+#endif
   Pre A, B;
   if (nl > 0) {
+    if (diag) dfetch(0);
     fetch(A, 0);
     fetch(B, SNB);
     stage(A, 0);
+    if (diag) daccum(A);
   }
   __syncthreads();
+  SK_T(3);
+#ifdef SK_TIMING
+  if (skrec) {
+    sk[8] = nl;
+    sk[9] = chunk;
+  }
+#endif
   // batch p in buffer 0 from set A, batch p + SNB in buffer 1 from set B (block-uniform control flow)
   for (int p = 0; p < nl; p += 2 * SNB) {
+    SK_NOW(skt);
+    if (diag && p + SNB < nl) dfetch(p + SNB);
     fetch(A, p + 2 * SNB);
     compute(0, p + SNB >= nl);
-    if (p + SNB < nl) stage(B, 1);
+    SK_ACC(4, skt);
+    SK_NOW(skt);
+    if (p + SNB < nl) {
+      stage(B, 1);
+      if (diag) daccum(B);
+    }
+    SK_ACC(5, skt);
+    SK_NOW(skt);
     __syncthreads();
+    SK_ACC(6, skt);
     if (p + SNB >= nl) break;
+    SK_NOW(skt);
+    if (diag && p + 2 * SNB < nl) dfetch(p + 2 * SNB);
     fetch(B, p + 3 * SNB);
     compute(1, p + 2 * SNB >= nl);
-    if (p + 2 * SNB < nl) stage(A, 0);
+    SK_ACC(4, skt);
+    SK_NOW(skt);
+    if (p + 2 * SNB < nl) {
+      stage(A, 0);
+      if (diag) daccum(A);
+    }
+    SK_ACC(5, skt);
+    SK_NOW(skt);
     __syncthreads();
+    SK_ACC(6, skt);
   }
+  SK_T(7);
+#if MF_DIAG_FUSED
+  if (diag) {  // fixed-order reduction over the 16 landmark lanes of each frame (as schur_diag_terms)
+    double* red = reinterpret_cast<double*>(&sWt[0][0][0][0]);  // free after the last batch's barrier
+#pragma unroll
+    for (int k = 0; k < 12; ++k) red[(yj * SF + yi) * 12 + k] = (double)dacc[k];
+    __syncthreads();
+    if (t < SF * 12) {
+      double v = 0;
+      for (int j0 = 0; j0 < 512 / SF; ++j0) v += red[j0 * SF * 12 + t];
+      a.part_diag[(int64_t)item * SF * 12 + t] = v;
+    }
+  }
+#endif
   // partial blocks of this split: part[item][f1 local][3q + r][f2], as k_schur writes them
   float* out = (float*)a.part + (int64_t)item * (SF * 9 * WAVE);
 #pragma unroll
@@ -528,6 +642,11 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
         const int q = row / SF, i = row % SF, r = col / WAVE, f2 = col % WAVE;
         out[(i * 9 + 3 * q + r) * WAVE + f2] = (float)acc[x][y][v];
       }
+  SK_T(10);
+#ifdef SK_TIMING
+  __syncthreads();
+  if (threadIdx.x == 0 && item < 4096) g_sk_items[item][1] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // PTZBA_SCHUR=valu selects the VALU kernel for the fp32 path (A/B measurements)
