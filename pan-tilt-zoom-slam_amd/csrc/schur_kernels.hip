@@ -362,6 +362,9 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 constexpr int MKP = 40;
+#ifndef SR_UNROLL
+#define SR_UNROLL 4  // split partials in flight per thread in k_schur_reduce (4 or 8)
+#endif
 #ifndef MF_DIAG_FUSED
 #define MF_DIAG_FUSED 1  // chunk-0 diagonal terms inside the batch pipeline (0: a phase before it)
 #endif
@@ -684,6 +687,15 @@ __global__ __launch_bounds__(256) void k_schur_reduce(SchurArgs a) {
     const real* p = (const real*)a.part + e;
     double v = 0;
     int it = g.z;
+#if SR_UNROLL == 8
+    for (; it + 8 <= g.w; it += 8) {  // eight split partials in flight per thread
+      real pv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) pv[u] = p[(int64_t)(it + u) * NE];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v += (double)pv[u];
+    }
+#endif
     for (; it + 4 <= g.w; it += 4) {
       const double p0 = p[(int64_t)it * NE], p1 = p[(int64_t)(it + 1) * NE];
       const double p2 = p[(int64_t)(it + 2) * NE], p3 = p[(int64_t)(it + 3) * NE];
