@@ -5,7 +5,7 @@
 set -o pipefail
 TAG=${TAG:-r01}
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/${TAG}_gpu_tests.log 2>&1 || { echo TESTFAIL; tail -30 gpurun_out/${TAG}_gpu_tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${TAG}_gpu_tests.log 2>&1 || { echo TESTFAIL; tail -30 gpurun_out/${TAG}_gpu_tests.log; exit 1; }
 tail -2 gpurun_out/${TAG}_gpu_tests.log
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 BARGS="--steps 20 --warmup 3 --no-cpu-baseline --no-accuracy"
@@ -20,3 +20,6 @@ cat gpurun_out/${TAG}_bench.json
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/${TAG}_cal_fetch -o run --output-format csv -- ./tools/pmc_calib.bin > gpurun_out/${TAG}_cal_fetch.log 2>&1 || { echo CALFAIL; exit 1; }
 timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/${TAG}_cal_write -o run --output-format csv -- ./tools/pmc_calib.bin > gpurun_out/${TAG}_cal_write.log 2>&1 || { echo CALFAIL; exit 1; }
 python tools/pmc_calib_summary.py gpurun_out/${TAG}_cal_fetch gpurun_out/${TAG}_cal_write gpurun_out/${TAG}_pmc_calib.json
+# K2 (matrix-core Schur kernel) traffic from the same PMC passes
+python tools/pmc_traffic.py gpurun_out/${TAG}_pmc_fetch gpurun_out/${TAG}_pmc_write "k_schur_mf" config3/pair/fp32/huber/k2 gpurun_out/${TAG}_k2_traffic.json 1024 > /dev/null || { echo K2TRAFFICFAIL; exit 1; }
+cat gpurun_out/${TAG}_k2_traffic.json

@@ -3,7 +3,9 @@
 FETCH_SIZE / WRITE_SIZE are in KiB (rocprofv3 derived counters).  On gfx950 FETCH_SIZE reports half of
 the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md, HBM section), so the read bytes are
 2 x FETCH_SIZE; WRITE_SIZE is taken as is.  Writes a JSON entry keyed like bench.py's --traffic-json.
-  python tools/pmc_traffic.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR KEY OUT_JSON
+  python tools/pmc_traffic.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR KEY OUT_JSON [MIN_KIB]
+MIN_KIB drops dispatches with less traffic (the device-driven LM's speculative launches that exit at
+once: K2 after the solve's last decision).
 """
 import csv
 import glob
@@ -28,8 +30,9 @@ def per_dispatch(d, counter, kernel):
 
 def main():
     fdir, wdir, kernel, key, out = sys.argv[1:6]
-    fe = per_dispatch(fdir, "FETCH_SIZE", kernel)
-    wr = per_dispatch(wdir, "WRITE_SIZE", kernel)
+    min_kib = float(sys.argv[6]) if len(sys.argv) > 6 else 0.0
+    fe = [x for x in per_dispatch(fdir, "FETCH_SIZE", kernel) if x >= min_kib]
+    wr = [x for x in per_dispatch(wdir, "WRITE_SIZE", kernel) if x >= min_kib / 64]
     if not fe or not wr:
         raise SystemExit(f"no dispatches of {kernel}: fetch {len(fe)} write {len(wr)}")
     fkib = sum(fe) / len(fe)
