@@ -157,8 +157,9 @@ PTZBA_EXPORT int ptzba_solve(ptzba_handle h, double* ptz_inout, double* rays_ino
 PTZBA_EXPORT int ptzba_step(ptzba_handle h, double lambda);
 PTZBA_EXPORT int ptzba_read_scalars(ptzba_handle h, double* out /*PTZBA_NSCALARS*/);
 PTZBA_EXPORT int ptzba_accept(ptzba_handle h, int accept);
-/* Device pointers of the exchange regions (fp64): reduced system (n_sys*(n_sys+1) doubles: lower
- * matrix n_sys x n_sys row-major then rhs n_sys) and the additive partial scalars (PTZBA_NSCALARS). */
+/* Device pointers of the exchange regions (fp64): reduced system (ld*ld + 3*ld doubles, ld = the padded
+ * system dimension: the lower triangle of S row-major in the system order, then b, g_pose and diag U)
+ * and the additive partial scalars (PTZBA_NSCALARS). */
 PTZBA_EXPORT int ptzba_exchange(ptzba_handle h, void** sys_ptr, int64_t* sys_count, void** scal_ptr);
 /* Packed exchange for sharded solves: a contiguous device buffer (fp64, *count doubles) holding only
  * the tiles of the reduced system the Schur kernel can write, then b | g_pose | dU.  Sequence per

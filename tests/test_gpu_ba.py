@@ -422,3 +422,43 @@ def test_save_restore_state_restarts_identically(gpu_available):
     assert (a.njev, a.nfev, a.status) == (b.njev, b.nfev, b.status) and a.cost == b.cost
     assert np.array_equal(sa[0], sb[0]) and np.array_equal(sa[1], sb[1])
     h.close()
+
+
+@pytest.mark.parametrize("config,loss", [("config2", "linear"), ("config3", "huber")])
+def test_reduced_system_matrix_core_k2_matches_fp64(gpu_available, config, loss):
+    """K2 of the fp32 path runs on the matrix cores (k_schur_mf: fp16 hi/lo operand splits with power-of-
+    two landmark scaling); the fp64 path keeps the VALU kernel.  At the same linearisation
+    point the two reduced camera systems (S | b | g_pose | diag U, the exchange region) agree to the
+    fp32 record precision, element by element against each row's scale."""
+    import torch
+    import bench
+    import ptzba
+    import synthetic
+    p = synthetic.make_problem(config, seed=0)
+    lo = ptzba.LOSS_LINEAR if loss == "linear" else ptzba.LOSS_HUBER
+    out = []
+    for prec in (ptzba.FP64, ptzba.FP32):
+        h = ptzba.BAHandle(0)
+        h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=prec, loss=lo)
+        h.set_state(p.init_ptz, p.init_rays)
+        h.linearize()
+        h.build_reduced(1e-3)
+        h.sync()
+        sp, n, _ = h.exchange()
+        out.append(torch.as_tensor(bench._DevArray(sp, n), device="cuda:0").cpu().numpy().copy())
+        h.close()
+    s64, s32 = out
+    ld = int(round((-3 + np.sqrt(9 + 4 * len(s64))) / 2))  # region = S [ld x ld] | b | g_pose | diag U
+    assert ld * ld + 3 * ld == len(s64)
+    S64 = s64[:ld * ld].reshape(ld, ld)
+    S32 = s32[:ld * ld].reshape(ld, ld)
+    # entry (i, j) against sqrt(|S_ii| |S_jj|), the scale of a symmetric positive semi-definite block
+    d = np.sqrt(np.abs(np.diag(S64)) + 1e-300)
+    rel = np.abs(S32 - S64) / (np.outer(d, d) + 1e-300)
+    low = np.tril(np.ones_like(S64, dtype=bool))
+    live = low & (np.outer(d, d) > 0)
+    err = rel[live].max()
+    print(f"{config}: max |S32 - S64| / sqrt(S_ii S_jj) = {err:.3e}")
+    assert err < 1e-4, err
+    tail = np.abs(s32[ld * ld:] - s64[ld * ld:]).max() / max(np.abs(s64[ld * ld:]).max(), 1e-300)
+    assert tail < 1e-5, tail
