@@ -104,6 +104,19 @@ struct ptzba_ctx {
 
 // Cold-cache K1 timing: 16-B vector stores over a scratch buffer larger than L2 + Infinity Cache (256 MB
 // MALL, MI355X_MICROARCH.md) evict the record stream before the timed launch, so K1 reads from HBM.
+// ptzba_restore_state: state <- snapshot, Marquardt scales <- 0
+__global__ void __launch_bounds__(256) k_restore_state(double* __restrict__ ptz, const double* __restrict__ ptz_saved,
+                                                       int64_t n_ptz, double* __restrict__ rays,
+                                                       const double* __restrict__ rays_saved, int64_t n_rays,
+                                                       double* __restrict__ D_pose, int64_t n_dp,
+                                                       double* __restrict__ D_ray, int64_t n_dr) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_ptz) ptz[i] = ptz_saved[i];
+  if (i < n_rays) rays[i] = rays_saved[i];
+  if (i < n_dp) D_pose[i] = 0.0;
+  if (i < n_dr) D_ray[i] = 0.0;
+}
+
 __global__ void __launch_bounds__(256) k_flush_caches(float4* buf, int64_t n16, float v) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x)
     buf[i] = make_float4(v, v, v, v);
@@ -895,11 +908,15 @@ int ptzba_restore_state(ptzba_handle h) {
   if (!h || !h->have_problem) return fail("no problem set");
   if (!h->ptz_saved.p) return fail("no saved state (ptzba_save_state)");
   HIPCHK(hipSetDevice(h->device));
-  HIPCHK(hipMemcpyAsync(h->ptz.p, h->ptz_saved.p, 3 * (size_t)h->n_pose * 8, hipMemcpyDeviceToDevice, h->st));
-  if (h->n_lm)
-    HIPCHK(hipMemcpyAsync(h->rays.p, h->rays_saved.p, 2 * (size_t)h->n_lm * 8, hipMemcpyDeviceToDevice, h->st));
-  HIPCHK(hipMemsetAsync(h->D_pose.p, 0, h->D_pose.bytes, h->st));
-  HIPCHK(hipMemsetAsync(h->D_ray.p, 0, h->D_ray.bytes, h->st));
+  // one launch instead of two copies and two fills (four stream operations at ~4-5 us each)
+  const int64_t n_ptz = 3 * (int64_t)h->n_pose, n_rays = 2 * (int64_t)h->n_lm;
+  const int64_t n_dp = (int64_t)(h->D_pose.bytes / 8), n_dr = (int64_t)(h->D_ray.bytes / 8);
+  const int64_t n = std::max(std::max(n_ptz, n_rays), std::max(n_dp, n_dr));
+  if (n > 0)
+    hipLaunchKernelGGL(k_restore_state, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->st, h->ptz.as<double>(),
+                       h->ptz_saved.as<double>(), n_ptz, h->rays.as<double>(), h->rays_saved.as<double>(), n_rays,
+                       h->D_pose.as<double>(), n_dp, h->D_ray.as<double>(), n_dr);
+  HIPCHK(hipGetLastError());
   return 0;
 }
 
