@@ -251,6 +251,9 @@ __device__ int g_cs_level;
 // the rank-8 update to its own columns (the pivot-column values broadcast from LDS).  The trailing
 // update -- most of the FMAs -- runs on four SIMDs instead of one.
 constexpr int WB = 8;
+#ifndef CHOL_P_READLANE
+#define CHOL_P_READLANE 1  // 1: the pivot block by v_readlane instead of an LDS round trip (flag form)
+#endif
 #ifndef LA_BW
 #define LA_BW 4  // pivot block of the lookahead form
 #endif
@@ -526,17 +529,26 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
           a[j] = acc;
         }
       }
+      double P[BW][BW], y[BW], sg[BW];
+#if CHOL_P_READLANE
+      // the BW x BW diagonal block lives in lanes kb..kb+BW-1 of this wave: read it lane to lane
+      // (v_readlane, uniform lane indices) instead of a round trip through LDS
+#pragma unroll
+      for (int i = 0; i < BW; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) P[i][j] = bcast(a[j], kb + i);
+#else
       if (lane >= kb && lane < kb + BW) {
 #pragma unroll
         for (int j = 0; j < BW; ++j) Pb[lane - kb][j] = a[j];
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
       __builtin_amdgcn_wave_barrier();
-      double P[BW][BW], y[BW], sg[BW];
 #pragma unroll
       for (int i = 0; i < BW; ++i)
 #pragma unroll
         for (int j = 0; j <= i; ++j) P[i][j] = Pb[i][j];
+#endif
 #pragma unroll
       for (int j = 0; j < BW; ++j) {
         double d = P[j][j];
