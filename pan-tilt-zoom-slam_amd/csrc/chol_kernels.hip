@@ -251,6 +251,12 @@ __device__ int g_cs_level;
 // the rank-8 update to its own columns (the pivot-column values broadcast from LDS).  The trailing
 // update -- most of the FMAs -- runs on four SIMDs instead of one.
 constexpr int WB = 8;
+#ifndef CHOL_NU_RELAXED
+#define CHOL_NU_RELAXED 0  // the same for the helpers' progress counters (A/B)
+#endif
+#ifndef CHOL_NL_RELAXED
+#define CHOL_NL_RELAXED 1  // 1: publish a factor block without waiting for its LDS stores (0: wait, A/B)
+#endif
 #ifndef CHOL_P_READLANE
 #define CHOL_P_READLANE 1  // 1: the pivot block by v_readlane instead of an LDS round trip (flag form)
 #endif
@@ -593,9 +599,17 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
         }
       }
       if (s + 2 < NS) {
+#if CHOL_NL_RELAXED
+        // no wait for the Lb stores: this wave's LDS operations execute in issue order, so a helper that
+        // sees nl also sees them; the compiler barrier keeps the counter store behind them
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) __hip_atomic_store(nl, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) __hip_atomic_store(nl, s + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
       }
 #ifdef CS_TIMING
       if (wrec && s < 9) wst[1 + s] = clock64();
@@ -627,9 +641,15 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
           for (int k = 0; k < BW; ++k) acc = fma(-lr[b][k], Lb[b][m][k], acc);
         if (have) row[m] = acc;
       }
+#if CHOL_NU_RELAXED
+      asm volatile("" ::: "memory");  // as for nl: in-order LDS, no wait for the column stores
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) __hip_atomic_fetch_add(&nu[t], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
       if (lane == 0) __hip_atomic_fetch_add(&nu[t], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
     }
   }
   __syncthreads();
