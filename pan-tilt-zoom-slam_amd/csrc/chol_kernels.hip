@@ -251,6 +251,9 @@ __device__ int g_cs_level;
 // the rank-8 update to its own columns (the pivot-column values broadcast from LDS).  The trailing
 // update -- most of the FMAs -- runs on four SIMDs instead of one.
 constexpr int WB = 8;
+#ifndef CHOL_DIRECT_STORE
+#define CHOL_DIRECT_STORE 1  // store the factor tiles straight from the sweep's block buffer (0: copy back to the tiles first)
+#endif
 #ifndef CHOL_NU_RELAXED
 #define CHOL_NU_RELAXED 0  // the same for the helpers' progress counters (A/B)
 #endif
@@ -653,6 +656,7 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
     }
   }
   __syncthreads();
+#if !CHOL_DIRECT_STORE
   // wave w writes columns 8w .. 8w+7 of the factor
   if (have) {
 #pragma unroll
@@ -664,6 +668,7 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
     }
   }
   __syncthreads();
+#endif
 }
 
 #ifdef CS_TIMING
@@ -815,6 +820,26 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     CS_STAMP(4);
     g_cs_level = cs_lvl + 1;
+  }
+#endif
+#if CHOL_DIRECT_STORE && CHOL_WG == 3
+  // the factor goes to memory straight from the sweep's block buffer (rows 0..31: D, 32..63: T)
+  if (diag_only) {
+    double* C = Ldiag + (int64_t)k * NB * NB;
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+      const int r = e >> 5, m = e & 31;
+      C[e] = m <= r ? s_lb[m / LA_BW][r][m % LA_BW] : 0.0;
+    }
+    if constexpr (SG) {
+      if (threadIdx.x < NB) sgn[(int64_t)k * NB + threadIdx.x] = s_sig[threadIdx.x];
+    }
+    return;
+  }
+  {
+    double* C = A + i * NBl * ld + k * NBl;
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x)
+      C[(int64_t)(e >> 5) * ld + (e & 31)] = s_lb[(e & 31) / LA_BW][NB + (e >> 5)][(e & 31) % LA_BW];
+    return;
   }
 #endif
   if (diag_only) {
