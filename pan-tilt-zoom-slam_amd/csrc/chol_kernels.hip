@@ -251,6 +251,9 @@ __device__ int g_cs_level;
 // the rank-8 update to its own columns (the pivot-column values broadcast from LDS).  The trailing
 // update -- most of the FMAs -- runs on four SIMDs instead of one.
 constexpr int WB = 8;
+#ifndef CHOL_FEWER_BARRIERS
+#define CHOL_FEWER_BARRIERS 0  // 1: drop the sweep's entry barrier and the caller's exit barrier (A/B)
+#endif
 #ifndef CHOL_DIRECT_STORE
 #define CHOL_DIRECT_STORE 1  // store the factor tiles straight from the sweep's block buffer (0: copy back to the tiles first)
 #endif
@@ -508,8 +511,10 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
   double* row = (isT && T) ? T[r] : D[r];
   int* nl = flags;
   int* nu = flags + 1;  // [NS]
+#if !CHOL_FEWER_BARRIERS
   if (threadIdx.x <= NS) flags[threadIdx.x] = 0;
   __syncthreads();
+#endif  // else the caller zeroed the flags before its staging barrier and fenced the panel updates
 #ifdef CS_TIMING
   long long* wst = g_cs_wg[g_cs_level < 64 ? g_cs_level : 63];
   const bool wrec = threadIdx.x == 0 && blockIdx.x == 0;
@@ -712,6 +717,9 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   __shared__ double s_sgp[2][NB];  // SG: signs of the two update panels' columns
   __shared__ double s_sig[NB];     // SG: signs of this column's pivots
   const int4 tk = tasks.get(blockIdx.x);
+#if CHOL_FEWER_BARRIERS && CHOL_WG == 3
+  if (threadIdx.x <= NB / LA_BW) s_flags[threadIdx.x] = 0;  // the sweep's counters (ordered by the staging barrier)
+#endif
   const int type = tk.x, i = tk.y, j = tk.z;
   const int up0 = (tk.w & 0x3fff) - 1;
   const int up1 = ((tk.w >> 14) & 0x3fff) - 1;
@@ -814,7 +822,9 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   if (threadIdx.x < WAVE) wave_potrf_trsm32(sD, diag_only ? nullptr : sC, rdg, cb, info);
 #endif
 #endif
-  __syncthreads();
+#if !(CHOL_FEWER_BARRIERS && CHOL_DIRECT_STORE && CHOL_WG == 3)
+  __syncthreads();  // (the flag-synchronised sweep ends in a barrier of its own)
+#endif
   CS_STAMP(3);
 #ifdef CS_TIMING
   if (threadIdx.x == 0 && blockIdx.x == 0) {
