@@ -251,6 +251,9 @@ __device__ int g_cs_level;
 // the rank-8 update to its own columns (the pivot-column values broadcast from LDS).  The trailing
 // update -- most of the FMAs -- runs on four SIMDs instead of one.
 constexpr int WB = 8;
+#ifndef BS_LOADERS
+#define BS_LOADERS 1  // loader waves of the lookahead back-solve (2: ring positions alternate; measured neutral)
+#endif
 #ifndef CHOL_FEWER_BARRIERS
 #define CHOL_FEWER_BARRIERS 0  // 1: drop the sweep's entry barrier and the caller's exit barrier (A/B)
 #endif
@@ -1045,13 +1048,13 @@ __global__ __launch_bounds__(1024) void k_chol_backsolve(const double* __restric
 // A loader wave streams each position's M and lookahead L blocks into an LDS ring up to 3 positions
 // ahead, so the chain wave issues no global loads.
 // la_tasks = [lookahead tile per position (-1: none) | task offsets per (chain, helper) | tasks q<<16|j].
-__global__ __launch_bounds__(64 * (BS_HELPERS + 2)) void k_chol_backsolve_la(
+__global__ __launch_bounds__(64 * (BS_HELPERS + 1 + BS_LOADERS)) void k_chol_backsolve_la(
     const double* __restrict__ L, int64_t ld, int n, const int* __restrict__ chain_off,
     const int* __restrict__ chain_cols, const int* __restrict__ la_tasks, const double* __restrict__ Ldiag,
     const double* __restrict__ Minv, double* __restrict__ xout) {
   constexpr int NH = BS_HELPERS, RING = 3;
   extern __shared__ __attribute__((aligned(16))) double xv[];  // [ld] r / x | cols [nq] | la [nq] | tasks (int)
-  __shared__ int s_xcnt, s_prog[NH], s_toff[NH + 1], s_ready, s_cdone;
+  __shared__ int s_xcnt, s_prog[NH], s_toff[NH + 1], s_ready[RING], s_cdone;  // s_ready: per ring slot, position + 1
   __shared__ double s_ring[RING][2][NB * NB];  // M_kt | L_kt,next of the chain's coming positions
   const int nq = chain_off[gridDim.x];
   const int* toff_g = la_tasks + nq;
@@ -1080,7 +1083,7 @@ __global__ __launch_bounds__(64 * (BS_HELPERS + 2)) void k_chol_backsolve_la(
   if (t <= NH) s_toff[t] = toff_g[blockIdx.x * NH + t] - tb;
   if (t == 0) {
     s_xcnt = q0;
-    s_ready = q0;
+    for (int k = 0; k < RING; ++k) s_ready[k] = q0;
     s_cdone = q0;
   }
   if (t < NH) {  // columns before a helper's first task are trivially done
@@ -1101,7 +1104,7 @@ __global__ __launch_bounds__(64 * (BS_HELPERS + 2)) void k_chol_backsolve_la(
       BSL_STAMP(q, 0);
       // this position's M and L blocks from the ring into registers first: the reads overlap the wait
       // for the owner of the tile
-      lds_wait_ge(&s_ready, q + 1, 0);
+      lds_wait_ge(&s_ready[(q - q0) % RING], q + 1, 0);
       BSL_STAMP(q, 1);
       double mv[NB / 2], lv[NB / 2];
 #pragma unroll
@@ -1142,9 +1145,10 @@ __global__ __launch_bounds__(64 * (BS_HELPERS + 2)) void k_chol_backsolve_la(
 #ifdef BS_TIMING
     if (t == 0) g_bs_edges[blockIdx.x & 1][2] = clock64();
 #endif
-  } else if (wv == NH + 1) {
-    // loader: M_kt and L_kt,next of position q into ring slot (q - q0) % RING, up to RING positions ahead
-    for (int q = q0; q < q1; ++q) {
+  } else if (wv >= NH + 1) {
+    // loaders: M_kt and L_kt,next of position q into ring slot (q - q0) % RING, up to RING positions ahead;
+    // BS_LOADERS waves take turns by position, so one loader's memory round trip overlaps the other's
+    for (int q = q0 + (wv - NH - 1); q < q1; q += BS_LOADERS) {
       lds_wait_ge(&s_cdone, q - RING + 1, 1);
       const int kt = s_cc[q], la = max(s_la[q], 0);
       double vm[NB * NB / WAVE], vl[NB * NB / WAVE];
@@ -1161,7 +1165,7 @@ __global__ __launch_bounds__(64 * (BS_HELPERS + 2)) void k_chol_backsolve_la(
         sm[lane + WAVE * i] = vm[i];
         sl[lane + WAVE * i] = vl[i];
       }
-      lds_signal(&s_ready, q + 1);
+      lds_signal(&s_ready[(q - q0) % RING], q + 1);
     }
   } else {
     const int me = wv - 1, k0 = s_toff[me], k1 = s_toff[me + 1];
@@ -1302,7 +1306,7 @@ void launch_chol_backsolve(const double* L, int64_t ld, int n, int n_chain, int 
   }
 #if BS_LA
   const size_t lds = (size_t)ld * sizeof(double) + (size_t)(2 * n_pos + n_tasks) * sizeof(int);
-  hipLaunchKernelGGL(k_chol_backsolve_la, dim3(n_chain), dim3(64 * (BS_HELPERS + 2)), lds, st, L, ld, n, chain_off,
+  hipLaunchKernelGGL(k_chol_backsolve_la, dim3(n_chain), dim3(64 * (BS_HELPERS + 1 + BS_LOADERS)), lds, st, L, ld, n, chain_off,
                      chain_cols, la_tasks, Ldiag, Minv, xout);
 #else
   const size_t lds = (size_t)ld * sizeof(double) + (size_t)(n_pos + 1 + n_upd) * sizeof(int);
