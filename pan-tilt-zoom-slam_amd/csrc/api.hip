@@ -614,7 +614,9 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     for (size_t k = 0; k < tiles.size(); ++k)
       total_w += (int64_t)tiles[k].size() * (tile_key[2 * k + 1] == 0 ? W0 : WD);
     const int64_t n_tiles = (int64_t)tiles.size();
-    const int64_t slots = std::max<int64_t>(512 - n_tiles, 64);
+    int64_t target_items = 512;
+    if (const char* e = getenv("PTZBA_S2_ITEMS")) target_items = std::max(64, atoi(e));  // A/B knob
+    const int64_t slots = std::max<int64_t>(target_items - n_tiles, 64);
     const int64_t split_w = std::max<int64_t>(64 * WD, (total_w + slots - 1) / slots);
     for (size_t k = 0; k < tiles.size(); ++k) {
       const auto& lst = tiles[k];
