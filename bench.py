@@ -39,7 +39,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=300)  # ~0.16 s timed at config 3: host jitter averages out
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="config3")
     ap.add_argument("--form", default="pair", choices=["pair", "dedup"])
