@@ -70,6 +70,8 @@ struct ptzba_ctx {
   DBuf chol_tasks, Ldiag, Minv, dpose;  // Minv: inverses of the diagonal factor tiles (back-substitution)
   std::vector<int> chol_task_off;  // host: per elimination level, offsets into chol_tasks
   std::vector<int32_t> chol_tasks_host;  // host copy of chol_tasks (int4 records)
+  DBuf tinv_tail;                        // diagonal tiles inverted after the factorisation
+  int n_tinv_tail = 0;
   int chol_levels = 0, n_aug = 0, n_chain = 1;
   bool nested = false;
   DBuf frame_pos, row_pad, bs_chain_off, bs_chain_cols, bs_upd_off, bs_upd_tiles, bs_la_tasks;
@@ -306,6 +308,7 @@ struct CholPlan {
   std::vector<int> lo_off, lo_tiles;  // left-looking back substitution: per position the solved row tiles coupled to it
   std::vector<int32_t> xtiles;  // (ti, tj) pairs the Schur kernel can write (before fill), for the exchange
   std::vector<int32_t> ztiles;  // (ti, tj) lower tiles of the factor's pattern (incl. fill): zeroed per build
+  std::vector<int32_t> tinv_tail;  // diagonal tiles inverted after the last level (the others: type-2 tasks)
   int n_levels = 0;
 };
 
@@ -360,6 +363,12 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
   auto push = [&](int type, int i, int j, int w) {
     P.tasks.push_back(type); P.tasks.push_back(i); P.tasks.push_back(j); P.tasks.push_back(w);
   };
+  // inverses of the diagonal factor tiles (for the back-substitution): the tiles of level L-1's columns are
+  // inverted by type-2 tasks of level L, beside its panels (off the critical path); the last level's after
+  // the factorisation (tinv_tail).  Columns >= n_inv (the augmented-row tile) need none.
+  const int n_inv = (o.n_aug + CHOL_NB - 1) / CHOL_NB;
+  const bool tinv_split = !getenv("PTZBA_TINV_ALL");  // A/B knob: every inverse after the factorisation
+  P.tinv_tail.clear();
   for (int L = 0; L < nL; ++L) {
     P.level_off[L] = (int)(P.tasks.size() / 4);
     const std::vector<int> none;
@@ -394,7 +403,12 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
       push(1, i, j, chol_pack_updates(upd[x].second, y - x > 1 ? upd[x + 1].second : -1, 3));
       x = y;
     }
+    if (tinv_split)
+      for (int pp : prev)
+        if (pp < n_inv) push(2, pp, pp, 0);
   }
+  for (int k = 0; k < n_inv && k < T; ++k)
+    if (!tinv_split || level[k] == nL - 1) P.tinv_tail.push_back(k);
   P.level_off[nL] = (int)(P.tasks.size() / 4);
   P.n_levels = nL;
   // back-substitution: chains of tile columns holding unknowns and, per chain position, the chain's
@@ -684,6 +698,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   make_plan(sorder, n_pose, o.n_fixed, win, h->ld, plan);
   h->chol_task_off = plan.level_off;
   h->chol_tasks_host = plan.tasks;
+  h->n_tinv_tail = (int)plan.tinv_tail.size();
   h->chol_levels = plan.n_levels;
   h->n_chain = (int)plan.chain_off.size() - 1;
   frame_win_hi = win;  // K2 windows follow the same (possibly global) coupling
@@ -732,7 +747,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       h->s2_part.alloc((size_t)std::max(h->n_s2_items, 1) * SCHUR_F1 * 9 * WAVE * 8) ||
       h->part_diag.alloc((size_t)std::max(h->n_s2_items, 1) * SCHUR_F1 * 12 * 8))
     return -1;
-  if (upload(h->chol_tasks, plan.tasks, h->st) || upload(h->frame_pos, sorder.pos, h->st) || upload(h->row_pad, sorder.pad, h->st) ||
+  if (upload(h->chol_tasks, plan.tasks, h->st) || upload(h->tinv_tail, plan.tinv_tail, h->st) || upload(h->frame_pos, sorder.pos, h->st) || upload(h->row_pad, sorder.pad, h->st) ||
       upload(h->bs_chain_off, plan.chain_off, h->st) || upload(h->bs_chain_cols, plan.chain_cols, h->st) ||
       upload(h->bs_upd_off, plan.upd_off, h->st) || upload(h->bs_upd_tiles, plan.upd_tiles, h->st) || upload(h->xtiles, plan.xtiles, h->st) || upload(h->ztiles, plan.ztiles, h->st) ||
       upload(h->bs_la_tasks, plan.la_tasks, h->st) || upload(h->bs_lo_off, plan.lo_off, h->st) || upload(h->bs_lo_tiles, plan.lo_tiles, h->st))
@@ -1002,12 +1017,13 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
                              h->lambda, lam_dev, h->st);
   launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
                   h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr,
-                  reinterpret_cast<const int4*>(h->chol_tasks_host.data()));
+                  reinterpret_cast<const int4*>(h->chol_tasks_host.data()), h->Minv.as<double>());
   launch_chol_backsolve(h->S(), h->ld, h->n_aug, h->n_chain, h->bs_npos, h->bs_chain_off.as<int>(),
                         h->bs_chain_cols.as<int>(), h->bs_upd_off.as<int>(), h->bs_upd_tiles.as<int>(), h->bs_nupd,
                         h->bs_la_tasks.as<int>(), h->bs_ntasks,
                         h->Ldiag.as<double>(), h->Minv.as<double>(), h->dpose.as<double>(),
-                        h->bs_ll ? h->bs_lo_off.as<int>() : nullptr, h->bs_lo_tiles.as<int>(), h->st);
+                        h->bs_ll ? h->bs_lo_off.as<int>() : nullptr, h->bs_lo_tiles.as<int>(), h->st,
+                        h->tinv_tail.as<int>(), h->n_tinv_tail);
   tm_end(h, TM_CHOL);
   HIPCHK(hipGetLastError());
   tm_begin(h, TM_BACK);

@@ -689,6 +689,34 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
 // A level's tasks: by value in the kernel arguments when they fit (the workgroup's first dependent global
 // load -- tasks[blockIdx.x] before any tile address is known -- disappears from the level's critical path),
 // else a device array.
+// M = L^-1 of one 32 x 32 lower factor tile (row-major), by the whole workgroup: stage L in LDS, diagonal
+// reciprocals, then one wave: lane j computes column j by forward substitution against e_j, right-looking
+// (after m_k is known every later row's running sum takes its term at once: the dependent chain is one
+// multiply and one FMA per row).  Shared by k_tile_inv and the type-2 tasks of the level launches.
+__device__ __forceinline__ void tile_inv_wave(const double* __restrict__ src, double* __restrict__ dst,
+                                              double (*Lt)[NB + 1], double* rinv) {
+  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) Lt[e >> 5][e & 31] = src[e];
+  __syncthreads();
+  if (threadIdx.x < NB) rinv[threadIdx.x] = rcp_nr(Lt[threadIdx.x][threadIdx.x]);
+  __syncthreads();
+  if (threadIdx.x >= WAVE) return;
+  const int lane = threadIdx.x, j = lane & (NB - 1);
+  double acc[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) acc[i] = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const double mk = (k >= j) ? acc[k] * rinv[k] : 0.0;  // m_k (0 above the diagonal)
+    acc[k] = mk;
+#pragma unroll
+    for (int i = k + 1; i < NB; ++i) acc[i] = fma(-Lt[i][k], mk, acc[i]);
+  }
+  if (lane < NB) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) dst[i * NB + lane] = acc[i];
+  }
+}
+
 struct CholTaskPtr {
   const int4* p;
   __device__ int4 get(int b) const { return p[b]; }
@@ -699,7 +727,8 @@ struct CholTaskVal {
 };
 template <bool SG, typename TaskArg>
 __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64_t ld, const TaskArg tasks,
-                                                   double* __restrict__ Ldiag, int* info, double* __restrict__ sgn) {
+                                                   double* __restrict__ Ldiag, int* info, double* __restrict__ sgn,
+                                                   double* __restrict__ Minv) {
   __shared__ double sC[NB][NB + 1];     // target tile (panel T_ik / trailing A_ij)
   __shared__ double sD[NB][NB + 1];     // diagonal tile -> L_kk
   __shared__ double sA[2][NB][NB + 1];  // L_ip of the two update panels
@@ -720,6 +749,11 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   __shared__ double s_sgp[2][NB];  // SG: signs of the two update panels' columns
   __shared__ double s_sig[NB];     // SG: signs of this column's pivots
   const int4 tk = tasks.get(blockIdx.x);
+  if (tk.x == 2) {  // inverse of a diagonal factor tile of the previous level (see tile_inv_wave)
+    __shared__ double s_rinv[NB];
+    tile_inv_wave(Ldiag + (int64_t)tk.y * NB * NB, Minv + (int64_t)tk.y * NB * NB, sD, s_rinv);
+    return;
+  }
 #if CHOL_FEWER_BARRIERS && CHOL_WG == 3
   if (threadIdx.x <= NB / LA_BW) s_flags[threadIdx.x] = 0;  // the sweep's counters (ordered by the staging barrier)
 #endif
@@ -869,7 +903,7 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
 }
 
 void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_off_host, int n_launch, double* Ldiag,
-                     int* info, hipStream_t st, double* sgn, const int4* tasks_host) {
+                     int* info, hipStream_t st, double* sgn, const int4* tasks_host, double* Minv) {
   static const bool by_value = !getenv("PTZBA_CHOL_TASKS_PTR");  // A/B knob
   for (int L = 0; L < n_launch; ++L) {
     const int n = task_off_host[L + 1] - task_off_host[L];
@@ -878,16 +912,16 @@ void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_o
       CholTaskVal tv;
       std::memcpy(tv.t, tasks_host + task_off_host[L], n * sizeof(int4));
       if (sgn)
-        hipLaunchKernelGGL((k_chol_step<true, CholTaskVal>), dim3(n), dim3(256), 0, st, A, ld, tv, Ldiag, info, sgn);
+        hipLaunchKernelGGL((k_chol_step<true, CholTaskVal>), dim3(n), dim3(256), 0, st, A, ld, tv, Ldiag, info, sgn, Minv);
       else
-        hipLaunchKernelGGL((k_chol_step<false, CholTaskVal>), dim3(n), dim3(256), 0, st, A, ld, tv, Ldiag, info, sgn);
+        hipLaunchKernelGGL((k_chol_step<false, CholTaskVal>), dim3(n), dim3(256), 0, st, A, ld, tv, Ldiag, info, sgn, Minv);
       continue;
     }
     const CholTaskPtr tp{tasks + task_off_host[L]};
     if (sgn)
-      hipLaunchKernelGGL((k_chol_step<true, CholTaskPtr>), dim3(n), dim3(256), 0, st, A, ld, tp, Ldiag, info, sgn);
+      hipLaunchKernelGGL((k_chol_step<true, CholTaskPtr>), dim3(n), dim3(256), 0, st, A, ld, tp, Ldiag, info, sgn, Minv);
     else
-      hipLaunchKernelGGL((k_chol_step<false, CholTaskPtr>), dim3(n), dim3(256), 0, st, A, ld, tp, Ldiag, info, sgn);
+      hipLaunchKernelGGL((k_chol_step<false, CholTaskPtr>), dim3(n), dim3(256), 0, st, A, ld, tp, Ldiag, info, sgn, Minv);
   }
 }
 
@@ -1293,12 +1327,27 @@ extern "C" int ptzba_debug_bs_stamps(long long* out) {
 }
 #endif
 
+// the diagonal tiles listed in `tiles` (the last elimination level's; the others were inverted by type-2
+// tasks of the level launches)
+__global__ __launch_bounds__(64) void k_tile_inv_list(const double* __restrict__ Ldiag, double* __restrict__ Minv,
+                                                      const int* __restrict__ tiles) {
+  __shared__ double Lt[NB][NB + 1];
+  __shared__ double rinv[NB];
+  const int kt = tiles[blockIdx.x];
+  tile_inv_wave(Ldiag + (int64_t)kt * NB * NB, Minv + (int64_t)kt * NB * NB, Lt, rinv);
+}
+
 void launch_chol_backsolve(const double* L, int64_t ld, int n, int n_chain, int n_pos, const int* chain_off,
                            const int* chain_cols, const int* upd_off, const int* upd_tiles, int n_upd,
                            const int* la_tasks, int n_tasks, const double* Ldiag, double* Minv, double* xout,
-                           const int* lo_off, const int* lo_tiles, hipStream_t st) {
+                           const int* lo_off, const int* lo_tiles, hipStream_t st, const int* tinv_list,
+                           int n_tinv) {
   const int tx = (n + NB - 1) / NB;
-  hipLaunchKernelGGL(k_tile_inv, dim3(tx), dim3(64), 0, st, Ldiag, Minv);
+  if (tinv_list) {
+    if (n_tinv > 0) hipLaunchKernelGGL(k_tile_inv_list, dim3(n_tinv), dim3(64), 0, st, Ldiag, Minv, tinv_list);
+  } else {
+    hipLaunchKernelGGL(k_tile_inv, dim3(tx), dim3(64), 0, st, Ldiag, Minv);
+  }
   if (lo_off) {  // large systems: left-looking form (api.hip chooses it when the lookahead lists exceed LDS)
     hipLaunchKernelGGL(k_chol_backsolve_ll, dim3(n_chain), dim3(64 * BSL_WAVES), (size_t)ld * sizeof(double), st, L,
                        ld, n, chain_off, chain_cols, lo_off, lo_tiles, Ldiag, Minv, xout);

@@ -147,14 +147,16 @@ void launch_chol_prepare_damped(double* A, int64_t ld, int n, double* b, const u
 // tasks_host (optional, the host copy of `tasks`): levels of <= CHOL_KT tasks pass them by value
 constexpr int CHOL_KT = 240;  // 3.75 KB of kernel arguments
 void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_off_host, int n_launch, double* Ldiag,
-                     int* info, hipStream_t st, double* sgn = nullptr, const int4* tasks_host = nullptr);
+                     int* info, hipStream_t st, double* sgn = nullptr, const int4* tasks_host = nullptr,
+                     double* Minv = nullptr);  // Minv: target of type-2 tasks (diagonal tile inverses)
 // la_tasks: lookahead back substitution's [lookahead tile per position | task offsets per (chain, helper) |
 // tasks q << 16 | tile], built by the host plan (api.hip make_plan)
 constexpr int BS_HELPERS = 7;
 void launch_chol_backsolve(const double* L, int64_t ld, int n, int n_chain, int n_pos, const int* chain_off,
                            const int* chain_cols, const int* upd_off, const int* upd_tiles, int n_upd,
                            const int* la_tasks, int n_tasks, const double* Ldiag, double* Minv, double* xout,
-                           const int* lo_off, const int* lo_tiles, hipStream_t st);
+                           const int* lo_off, const int* lo_tiles, hipStream_t st,
+                           const int* tinv_list = nullptr, int n_tinv = 0);  // tinv_list: see k_tile_inv_list
 // largest ld the back substitution keeps in LDS (left-looking form: x [ld] doubles + 4.4 KiB)
 constexpr int64_t CHOL_MAX_LD = 18944;
 // zero the factor pattern's tiles and the b | g_pose | dU vectors before a build (replaces a memset of
