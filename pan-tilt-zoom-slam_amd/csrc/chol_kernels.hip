@@ -251,6 +251,9 @@ __device__ int g_cs_level;
 // the rank-8 update to its own columns (the pivot-column values broadcast from LDS).  The trailing
 // update -- most of the FMAs -- runs on four SIMDs instead of one.
 constexpr int WB = 8;
+#ifndef BS_NOWAIT
+#define BS_NOWAIT 0  // 1: LDS hand-offs without lgkmcnt(0) waits (in-order LDS per wave; A/B)
+#endif
 #ifndef BS_LOADERS
 #define BS_LOADERS 1  // loader waves of the lookahead back-solve (2: ring positions alternate; measured neutral)
 #endif
@@ -488,7 +491,11 @@ __device__ __forceinline__ int lds_poll(const int* p) {
 // writes (lgkmcnt) and stores the counter; the consumer polls it and its later LDS reads stay behind
 // the poll (LDS operations of a wave execute in order; compiler barrier against reordering).
 __device__ __forceinline__ void lds_signal(int* p, int v) {
+#if BS_NOWAIT
+  asm volatile("" ::: "memory");  // in-order LDS per wave: the counter store lands after the data stores
+#else
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+#endif
   __builtin_amdgcn_wave_barrier();
   if (lane_id() == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -1150,7 +1157,11 @@ __global__ __launch_bounds__(64 * (BS_HELPERS + 1 + BS_LOADERS)) void k_chol_bac
       BSL_STAMP(q, 2);
       const double r = xv[c0 + c] - la_c;
       if (h == 0) xv[c0 + c] = r;
+#if BS_NOWAIT
+      asm volatile("" ::: "memory");  // the reads below are issued after the store: in-order LDS
+#else
       __builtin_amdgcn_s_waitcnt(0xc07f);
+#endif
       __builtin_amdgcn_wave_barrier();
       double s4[4] = {0, 0, 0, 0};
 #pragma unroll
