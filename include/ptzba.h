@@ -133,9 +133,20 @@ typedef struct {
   double lambda0, min_lambda, max_lambda;     /* Marquardt damping: start, floor, give-up bound */
   int32_t max_iter, max_retries, gauss_newton; /* accepted iterations; rejections in a row; lambda0 = 0 GN */
 } ptzba_lm_opts;
+/* termination status (scipy least_squares numbering where it has one): DAMPING = the trial was rejected at
+ * every damping up to max_lambda, i.e. no cost decrease is resolvable any more (scipy's trf ends such a run
+ * through its xtol test once the trust radius collapses); FAILED = max_retries rejections in a row */
+enum {
+  PTZBA_STATUS_FAILED = -1,
+  PTZBA_STATUS_MAX_ITER = 0,
+  PTZBA_STATUS_GTOL = 1,
+  PTZBA_STATUS_FTOL = 2,
+  PTZBA_STATUS_XTOL = 3,
+  PTZBA_STATUS_DAMPING = 5
+};
 typedef struct {
   double cost, initial_cost, lambda;
-  int32_t iterations, nfev, trials, retries, status, done, accepted;  /* status: 0 max_iter, 1 gtol, 2 ftol, 3 xtol, -1 failed */
+  int32_t iterations, nfev, trials, retries, status, done, accepted;  /* status: PTZBA_STATUS_* */
 } ptzba_lm_record;
 PTZBA_EXPORT int ptzba_lm_start(ptzba_handle h);
 PTZBA_EXPORT int ptzba_lm_init(ptzba_handle h, const ptzba_lm_opts* opts);
@@ -220,7 +231,10 @@ PTZBA_EXPORT int ptz_refine_poses(int device, int32_t n_hyp, double* ptz_inout, 
                                   int32_t* status_out);
 
 /* ---------------- host bookkeeping (native) ---------------- */
-/* ---------------- feature front-end (image_process.py:178-234, 418-441) ---------------- */
+/* ---------------- feature front-end (image_process.py:178-234, 418-441) ----------------
+ * Stateless, synchronous entry points (no handle).  They keep per-device work buffers across calls and hold
+ * a per-device lock while using them: safe to call from several host threads (calls on one device run one
+ * at a time).  The ptzba_* / ptzekf_* handles are NOT thread-safe: one call at a time per handle. */
 /* Brute-force 2-nearest-neighbour matching in L2 (cv.BFMatcher().knnMatch(des1, des2, k=2)): for each of the
  * n1 query descriptors the two nearest of the n2 train descriptors, idx_out[2*i+0/1] (ties: lower index
  * first; -1 when n2 < 2) and their L2 distances dist_out[2*i+0/1].  Descriptors are fp32 rows of `dim`.

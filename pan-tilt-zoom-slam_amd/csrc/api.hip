@@ -188,27 +188,28 @@ int ptzba_use_own_stream(ptzba_handle h) { return h ? ptzba_set_stream(h, h->own
 template <typename real>
 static int upload_records(ptzba_ctx* h, const std::vector<int64_t>& order, const std::vector<int32_t>& rec_seg,
                           const std::vector<double>& base, const double* obs_xy, const double* w) {
-  // synchronous uploads: the host vectors die at return (the handle's stream does not order itself
-  // behind the legacy null stream, so every upload / memset of set_problem goes on h->st)
+  // the copies below read host vectors that die at return: every exit path (errors included) waits for the
+  // handle's stream first (the stream does not order itself behind the legacy null stream, so every upload /
+  // memset of set_problem goes on h->st)
+  SyncOnExit sync_guard{h->st};
   std::vector<real> xy(2 * h->n_rec);
   for (int64_t r = 0; r < h->n_rec; ++r) {
     const int32_t s = rec_seg[r];
     xy[2 * r] = (real)(obs_xy[2 * order[r]] - base[2 * s]);
     xy[2 * r + 1] = (real)(obs_xy[2 * order[r] + 1] - base[2 * s + 1]);
   }
-  // padded by 4 records: K1's coarsened loads read whole 4-record groups
+  std::vector<real> ww(w ? h->n_rec : 0);
+  for (int64_t r = 0; r < (int64_t)ww.size(); ++r) ww[r] = (real)w[order[r]];
+  // allocate everything before queuing any copy; padded by 4 records: K1's coarsened loads read whole groups
   if (h->rec_xy.alloc((xy.size() + 8) * sizeof(real))) return -1;
-  HIPCHK(hipMemcpyAsync(h->rec_xy.p, xy.data(), xy.size() * sizeof(real), hipMemcpyHostToDevice, h->st));
-  HIPCHK(hipMemsetAsync(reinterpret_cast<real*>(h->rec_xy.p) + xy.size(), 0, 8 * sizeof(real), h->st));
   if (w) {
-    std::vector<real> ww(h->n_rec);
-    for (int64_t r = 0; r < h->n_rec; ++r) ww[r] = (real)w[order[r]];
     if (h->rec_w.alloc(ww.size() * sizeof(real))) return -1;
-    HIPCHK(hipMemcpyAsync(h->rec_w.p, ww.data(), ww.size() * sizeof(real), hipMemcpyHostToDevice, h->st));
-    HIPCHK(hipStreamSynchronize(h->st));
   } else {
     h->rec_w.release();
   }
+  HIPCHK(hipMemcpyAsync(h->rec_xy.p, xy.data(), xy.size() * sizeof(real), hipMemcpyHostToDevice, h->st));
+  HIPCHK(hipMemsetAsync(reinterpret_cast<real*>(h->rec_xy.p) + xy.size(), 0, 8 * sizeof(real), h->st));
+  if (w) HIPCHK(hipMemcpyAsync(h->rec_w.p, ww.data(), ww.size() * sizeof(real), hipMemcpyHostToDevice, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
   return 0;
 }
@@ -882,6 +883,7 @@ int ptzba_residual(ptzba_handle h, const double* x_full, double* r_out) {
   }
   DBuf x, r;
   if (x.alloc((3 * (size_t)h->n_pose + 2 * (size_t)h->n_lm) * 8) || r.alloc(2 * (size_t)h->n_rec * 8)) return -1;
+  SyncOnExit sync_guard{h->st};  // destroyed before x and r: queued work on them ends first, also on errors
   HIPCHK(hipMemcpyAsync(x.p, x_full, x.bytes, hipMemcpyHostToDevice, h->st));
   const double* px = x.as<double>();
   tables(h, px, px + 3 * h->n_pose);
@@ -902,6 +904,7 @@ int ptzba_residual(ptzba_handle h, const double* x_full, double* r_out) {
 int ptzba_set_state(ptzba_handle h, const double* ptz, const double* rays) {
   if (!h || !h->have_problem) return fail("no problem set");
   HIPCHK(hipSetDevice(h->device));
+  SyncOnExit sync_guard{h->st};  // caller buffers: no copy outlives the call, also on errors
   HIPCHK(hipMemcpyAsync(h->ptz.p, ptz, 3 * (size_t)h->n_pose * 8, hipMemcpyHostToDevice, h->st));
   if (h->n_lm) HIPCHK(hipMemcpyAsync(h->rays.p, rays, 2 * (size_t)h->n_lm * 8, hipMemcpyHostToDevice, h->st));
   HIPCHK(hipMemsetAsync(h->D_pose.p, 0, h->D_pose.bytes, h->st));
@@ -940,6 +943,7 @@ int ptzba_restore_state(ptzba_handle h) {
 int ptzba_get_state(ptzba_handle h, double* ptz, double* rays) {
   if (!h || !h->have_problem) return fail("no problem set");
   HIPCHK(hipSetDevice(h->device));
+  SyncOnExit sync_guard{h->st};  // caller buffers: no copy outlives the call, also on errors
   if (ptz) HIPCHK(hipMemcpyAsync(ptz, h->ptz.p, 3 * (size_t)h->n_pose * 8, hipMemcpyDeviceToHost, h->st));
   if (rays && h->n_lm) HIPCHK(hipMemcpyAsync(rays, h->rays.p, 2 * (size_t)h->n_lm * 8, hipMemcpyDeviceToHost, h->st));
   HIPCHK(hipStreamSynchronize(h->st));

@@ -22,6 +22,7 @@
 // scan.  All observations of one (frame, landmark) segment share the projection and the 2x5
 // Jacobian (they depend on pose and ray only), so the Jacobian and the 3x3/3x2/2x2 normal-equation
 // blocks are formed once per segment.
+#include "../../include/ptzba.h"
 #include "ptzba_common.h"
 #include "ptzba_kernels.h"
 
@@ -914,7 +915,9 @@ __global__ void k_lm_decide(LMDev* st, const double* __restrict__ scal, const do
       s.nu *= 2.0;
       s.retries += 1;
       if (s.lam > p.max_lambda) {
-        s.status = 0;
+        // no decrease at any damping up to max_lambda: the step is below the cost's resolution (scipy's trf
+        // ends such a run through xtol once its radius collapses); its own status, not "max iterations"
+        s.status = PTZBA_STATUS_DAMPING;
         s.done = 1;
       } else if (s.retries >= p.max_retries) {
         s.status = -1;

@@ -1,7 +1,9 @@
 // Feature front-end on the GPU: the matching half of image_process.match_sift_features
 // (image_process.py:178-234) -- brute-force 2-nearest-neighbour search in L2 (cv.BFMatcher().knnMatch(k=2))
 // and the homography RANSAC behind it (homography_ransac, image_process.py:418-441, cv.findHomography with
-// RANSAC).  Detection (SIFT/ORB on pixels) and LK flow stay front-end hooks.
+// RANSAC) -- pyramidal LK (optical_flow_matching, :393-415) and cross-checked Hamming matching (:237-310).
+// SIFT detection is sift.hip.  Every entry point holds device_work_lock while it uses the per-device work
+// buffers (host_util.h): thread-safe, serialised per device.
 //
 //   ptz_match_knn2         one 64x64 tile of squared L2 distances per workgroup (fp32, 4x4 outputs per
 //                          thread, descriptors staged through LDS in k-chunks of 16), then one wave per query
@@ -24,16 +26,6 @@
 #include "ptzba_common.h"
 
 namespace ptzba {
-
-// Per-device work buffers of one entry point, kept across calls (grown by DBuf::reserve, never shrunk,
-// deliberately not freed at exit): the stream and the keyframe maps call these per frame / per pair.
-template <typename Work>
-Work& work_for(int device) {
-  static std::vector<Work*> w;
-  if ((int)w.size() <= device) w.resize(device + 1, nullptr);
-  if (!w[device]) w[device] = new Work;
-  return *w[device];
-}
 
 constexpr int KT = 64, KC = 16;  // distance tile, k-chunk
 
@@ -369,6 +361,7 @@ int ptz_match_knn2(int device, int64_t n1, int64_t n2, int32_t dim, const float*
   struct KnnWork {
     DBuf a, b, d, idx, dist;
   };
+  auto guard = device_work_lock(device);
   KnnWork& Wk = work_for<KnnWork>(device);  // kept across calls: a keyframe matches ~15 pairs
   DBuf &a = Wk.a, &b = Wk.b, &d = Wk.d, &idx = Wk.idx, &dist = Wk.dist;
   if (a.reserve((size_t)n1 * dim * 4) || b.reserve((size_t)n2 * dim * 4) || d.reserve((size_t)n1 * n2 * 4) ||
@@ -412,6 +405,7 @@ int ptz_homography_ransac(int device, int64_t n, const double* pts1, const doubl
   struct RansacWork {
     DBuf p1, p2, best, mask, H, nin;
   };
+  auto guard = device_work_lock(device);
   RansacWork& Wk = work_for<RansacWork>(device);
   DBuf &p1 = Wk.p1, &p2 = Wk.p2, &best = Wk.best, &mask = Wk.mask, &H = Wk.H, &nin = Wk.nin;
   if (p1.reserve((size_t)n * 16) || p2.reserve((size_t)n * 16) || best.reserve(8) || mask.reserve((size_t)n) ||
@@ -626,10 +620,8 @@ int ptz_lk_track(int device, int32_t width, int32_t height, const uint8_t* img0,
   struct LkWork {
     DBuf u8, bufI, bufJ, bufX, bufY, dp, dout, dst, derr;
   };
-  static std::vector<LkWork*> works;
-  if ((int)works.size() <= device) works.resize(device + 1, nullptr);
-  if (!works[device]) works[device] = new LkWork;
-  LkWork& Wk = *works[device];
+  auto guard = device_work_lock(device);
+  LkWork& Wk = work_for<LkWork>(device);
   DBuf &u8 = Wk.u8, &bufI = Wk.bufI, &bufJ = Wk.bufJ, &bufX = Wk.bufX, &bufY = Wk.bufY, &dp = Wk.dp, &dout = Wk.dout;
   DBuf &dst = Wk.dst, &derr = Wk.derr;
   if (u8.reserve((size_t)np * 2) || bufI.reserve((size_t)tot * 4) || bufJ.reserve((size_t)tot * 4) ||

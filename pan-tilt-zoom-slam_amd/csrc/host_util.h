@@ -5,7 +5,9 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <mutex>
 #include <string>
+#include <vector>
 
 namespace ptzba {
 
@@ -53,6 +55,13 @@ struct DBuf {
   T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+// waits for a stream on scope exit (host buffers read by queued async copies must outlive them, also on
+// error returns)
+struct SyncOnExit {
+  hipStream_t s;
+  ~SyncOnExit() { (void)hipStreamSynchronize(s); }
+};
+
 // Device (hipSetDevice) check shared by the handle constructors.
 inline int select_device(int device) {
   int n = 0;
@@ -60,6 +69,29 @@ inline int select_device(int device) {
   if (device < 0 || device >= n) return fail("device %d out of range (%d devices)", device, n);
   if (hipSetDevice(device) != hipSuccess) return fail("hipSetDevice(%d) failed", device);
   return 0;
+}
+
+// Per-device work buffers of a stateless entry point (front-end, SIFT), kept across calls (grown, never
+// shrunk, deliberately not freed at exit): a stream calls them per frame / per pair.  They are shared by
+// every caller on that device, so an entry point holds device_work_lock(device) for as long as it uses
+// them (ctypes releases the GIL: two host threads may call the C-ABI at once).  One lock per device
+// serialises all such entry points on it; they are synchronous on the null stream anyway.
+inline std::mutex& device_work_mutex(int device) {
+  static std::mutex mu[64];
+  return mu[(unsigned)device % 64u];
+}
+inline std::unique_lock<std::mutex> device_work_lock(int device) {
+  return std::unique_lock<std::mutex>(device_work_mutex(device));
+}
+// the caller holds device_work_lock(device)
+template <typename Work>
+Work& work_for(int device) {
+  static std::mutex vec_mu;
+  static std::vector<Work*> w;
+  std::lock_guard<std::mutex> g(vec_mu);
+  if ((int)w.size() <= device) w.resize(device + 1, nullptr);
+  if (!w[device]) w[device] = new Work;
+  return *w[device];
 }
 
 }  // namespace ptzba

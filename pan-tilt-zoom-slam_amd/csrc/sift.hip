@@ -366,12 +366,7 @@ namespace {
 struct SiftWork {
   ptzba::DBuf dimg, dg, dd, dtmp, dk, dcand, dcnt, dkp, dptr, dow, doh, dsel, ddes;
 };
-SiftWork& sift_work(int device) {
-  static std::vector<SiftWork*> w;
-  if ((int)w.size() <= device) w.resize(device + 1, nullptr);
-  if (!w[device]) w[device] = new SiftWork;
-  return *w[device];
-}
+SiftWork& sift_work(int device) { return ptzba::work_for<SiftWork>(device); }  // under device_work_lock
 
 std::vector<float> sift_kernel(double sigma) {
   int k = (int)std::nearbyint(sigma * 8 + 1) | 1;
@@ -421,6 +416,7 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
   }
   if ((int)kmax / 2 > BLUR_RMAX) return fail("blur radius %d exceeds %d", (int)kmax / 2, BLUR_RMAX);
   const int CAP = 1 << 17;
+  auto guard = device_work_lock(device);
   SiftWork& Wk = sift_work(device);
   DBuf &dimg = Wk.dimg, &dg = Wk.dg, &dd = Wk.dd, &dtmp = Wk.dtmp, &dk = Wk.dk, &dcand = Wk.dcand, &dcnt = Wk.dcnt;
   DBuf &dkp = Wk.dkp, &dptr = Wk.dptr, &dow = Wk.dow, &doh = Wk.doh, &dsel = Wk.dsel, &ddes = Wk.ddes;

@@ -1,14 +1,19 @@
 """
-Correspondence front-end hooks + matching-graph bookkeeping (reference: slam_system/image_process.py).
+Feature front-end + matching-graph bookkeeping (reference: slam_system/image_process.py).
 
-The reference detects SIFT/ORB features and matches them with OpenCV (image_process.py:14-506).
-OpenCV is not part of this build (the feature front-end is SURVEY §8f-4, out of scope for the BA
-tier), so the front-end functions here are HOOKS: a correspondence source (e.g. synthetic.py's
-SyntheticFrontEnd, or an OpenCV wrapper on a machine that has it) assigns them, exactly the way the
-reference's own tests monkeypatch them.  Calling an unassigned hook raises.
+The reference detects SIFT/ORB features and matches them with OpenCV (image_process.py:14-506).  OpenCV
+is not in this image, so the front-end the demo uses runs on the GPU through libptzba:
+  * detect_compute_sift / detect_sift / detect_compute_sift_array  -> ptz_sift (OpenCV's SIFT defaults);
+  * match_sift_features   -> ptz_match_knn2 (BF kNN-2) + the 0.7 ratio test + homography_ransac;
+  * match_orb_features / match_latch_features -> ptz_match_hamming (cross-checked) + homography_ransac;
+  * homography_ransac     -> ptz_homography_ransac;  optical_flow_matching -> ptz_lk_track (pyramidal LK).
+Their agreement with cv2's own numbers is unpinned (cv2 cannot run here): each kernel is pinned to the
+oracle's restatement of the published algorithm and to synthetic ground truth (tests/test_gpu_frontend.py).
+ORB / LATCH *detection* (detect_compute_orb / detect_compute_latch) stays a hook: a correspondence source
+(e.g. synthetic.SyntheticFrontEnd, or an OpenCV wrapper on a machine that has it) assigns it, exactly the
+way the reference's own tests monkeypatch the front-end; any of the functions above may be reassigned too.
 
-What this module does implement is the bookkeeping of `build_matching_graph`
-(image_process.py:509-667) with the reference's exact semantics:
+The bookkeeping of `build_matching_graph` (image_process.py:509-667) keeps the reference's exact semantics:
   * pairs i < j in order, skipped when image_match_mask[i][j] == 0;
   * a pair is kept if it has MORE than 20 matches (`len > min_match_num`, :590);
   * pairs with more than 200 matches are capped by `random.shuffle` of the GLOBAL `random`
@@ -159,14 +164,18 @@ def _grey_u8(img):
 def optical_flow_matching(img, next_img, points, ssd_threshold=20):
     """image_process.py:393-415 on the GPU (libptzba ptz_lk_track: pyramidal LK, 31 x 31 window, 4 levels,
     30 iterations, eps 0.01): indices of the points tracked with err < ssd_threshold and strictly inside
-    the image, and their positions in next_img ([m, 2])."""
+    the image, and their positions in next_img ([m, 2]).  The reference's filter exactly (:408-411): the LK
+    status is NOT consulted, so a point that ends in the last pixel column / row (status 0 in ptz_lk_track,
+    as in OpenCV) is kept when err and the bounds allow.  A window without texture (smaller structure-
+    tensor eigenvalue below the threshold) reports err = inf and is dropped; OpenCV leaves err unset there
+    (undefined), the one deliberate deviation."""
     import ptzba
     a, b = _grey_u8(img), _grey_u8(next_img)
     pts = np.asarray(points, np.float32).reshape(-1, 2)
     nxt, status, err = ptzba.lk_track(a, b, pts, win=31)
     h, w = a.shape[0], a.shape[1]
     x, y = nxt[:, 0], nxt[:, 1]
-    keep = (status == 1) & (err < ssd_threshold) & (x > 0) & (x < w) & (y > 0) & (y < h)
+    keep = (err < ssd_threshold) & (x > 0) & (x < w) & (y > 0) & (y < h)
     matched_index = [int(i) for i in np.flatnonzero(keep)]
     return matched_index, np.array([nxt[i] for i in matched_index])
 

@@ -17,6 +17,7 @@ linearisation (scipy `njev`); rejected trial steps are counted inside the iterat
 """
 import ctypes
 import os
+import threading
 import time
 from ctypes import POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_int64, c_void_p
 
@@ -758,7 +759,9 @@ class LMResult:
                 f"njev={self.njev}, nfev={self.nfev}, time={self.time:.4f}s)")
 
 
-STATUS_MSG = {0: "max iterations", 1: "gtol", 2: "ftol", 3: "xtol", -1: "failed"}
+STATUS_DAMPING = 5  # include/ptzba.h PTZBA_STATUS_DAMPING
+STATUS_MSG = {0: "max iterations", 1: "gtol", 2: "ftol", 3: "xtol", -1: "failed",
+              STATUS_DAMPING: "damping limit: no cost decrease resolvable up to max_lambda"}
 
 
 class LMSolver:
@@ -882,7 +885,7 @@ class LMSolver:
                     if lam > self.max_lambda:
                         break
             if not accepted:
-                status = 0 if retries < self.max_retries else -1
+                status = STATUS_DAMPING if retries < self.max_retries else -1
                 break
             it += 1
             njev += 1
@@ -908,24 +911,50 @@ class LMSolver:
 
 
 _solve_handles = {}
+_solve_lock = threading.Lock()
+
+
+def release_solve_handles(device=None):
+    """Free the BA handle(s) that solve() keeps between calls (all devices, or one): their device memory
+    (records, slot tables, reduced system) is returned at once instead of at process exit."""
+    with _solve_lock:
+        devs = list(_solve_handles) if device is None else [device]
+        for d in devs:
+            h = _solve_handles.pop(d, None)
+            if h is not None:
+                h.close()
 
 
 def solve(n_pose, n_landmark, frame, landmark, xy, u, v, init_ptz, init_rays, weight=None, precision=FP64,
-          loss=LOSS_LINEAR, f_scale=1.0, device=0, **lm_kw):
-    """Convenience one-shot solve.  Returns (ptz [N,3], rays [M,2], LMResult).  One handle per device is kept
-    between calls (a keyframe map solves on every new keyframe: creating and destroying a handle -- stream,
-    pinned records, device buffers -- cost ~6 ms per call); set_problem replaces its problem."""
-    h = _solve_handles.get(device)
-    if h is None or h.h is None:
-        h = _solve_handles[device] = BAHandle(device)
-    try:
-        h.set_problem(n_pose, n_landmark, frame, landmark, xy, u, v, weight=weight, precision=precision, loss=loss,
-                      f_scale=f_scale)
-        h.set_state(init_ptz, init_rays)
-        res = LMSolver(h, **lm_kw).run()
-        ptz, rays = h.get_state()
-        return ptz, rays, res
-    except Exception:
-        _solve_handles.pop(device, None)
-        h.close()
-        raise
+          loss=LOSS_LINEAR, f_scale=1.0, device=0, keep_handle=True, **lm_kw):
+    """Convenience one-shot solve.  Returns (ptz [N,3], rays [M,2], LMResult).  keep_handle=True (default): one
+    handle per device is kept between calls (a keyframe map solves on every new keyframe: creating and
+    destroying a handle -- stream, pinned records, device buffers -- cost ~6 ms per call); set_problem replaces
+    its problem and release_solve_handles() frees it.  keep_handle=False: a private handle, closed on return.
+    The shared handle is used under a lock: concurrent callers on one device run one at a time."""
+    if not keep_handle:
+        h = BAHandle(device)
+        try:
+            h.set_problem(n_pose, n_landmark, frame, landmark, xy, u, v, weight=weight, precision=precision, loss=loss,
+                          f_scale=f_scale)
+            h.set_state(init_ptz, init_rays)
+            res = LMSolver(h, **lm_kw).run()
+            ptz, rays = h.get_state()
+            return ptz, rays, res
+        finally:
+            h.close()
+    with _solve_lock:
+        h = _solve_handles.get(device)
+        if h is None or h.h is None:
+            h = _solve_handles[device] = BAHandle(device)
+        try:
+            h.set_problem(n_pose, n_landmark, frame, landmark, xy, u, v, weight=weight, precision=precision, loss=loss,
+                          f_scale=f_scale)
+            h.set_state(init_ptz, init_rays)
+            res = LMSolver(h, **lm_kw).run()
+            ptz, rays = h.get_state()
+            return ptz, rays, res
+        except Exception:
+            _solve_handles.pop(device, None)
+            h.close()
+            raise

@@ -24,8 +24,10 @@ def config3():
     return synthetic.make_problem("config3", seed=0)
 
 
-def _oracle_gradient(p, ptz, rays):
-    """J^T r of the pair-form linear cost at (ptz, rays): [n_pose, 3] pose part, [M, 2] ray part."""
+def _oracle_gradient(p, ptz, rays, loss="linear", f_scale=1.0):
+    """Gradient of the pair-form cost at (ptz, rays): [n_pose, 3] pose part, [M, 2] ray part.  linear: J^T r;
+    huber: scipy's convention (cost 0.5 f^2 sum rho((r_i / f)^2) over SCALAR residuals, rho' = 1 inside the
+    unit and 1/sqrt(z) beyond), i.e. J^T (rho'(z) * r) with z per residual component."""
     from oracle import ptz_oracle as orc
     fr = p.frame.astype(np.int64)
     lm = p.landmark.astype(np.int64)
@@ -37,6 +39,9 @@ def _oracle_gradient(p, ptz, rays):
         b = min(len(fr), a + chunk)
         r = orc.compute_residual_records(x_full, p.n_pose, p.u, p.v, fr[a:b], lm[a:b], p.xy[a:b]).reshape(-1, 2)
         J = orc.record_jacobian(p.u, p.v, np.asarray(ptz)[fr[a:b]], np.asarray(rays)[lm[a:b]])
+        if loss == "huber":
+            z = (r / f_scale) ** 2
+            r = r * np.where(z <= 1.0, 1.0, 1.0 / np.sqrt(np.maximum(z, 1.0)))
         g = np.einsum("rkc,rk->rc", J, r)
         np.add.at(gp, fr[a:b], g[:, :3])
         np.add.at(gr, lm[a:b], g[:, 3:])
@@ -103,6 +108,29 @@ def test_config3_fp64_optimum_is_stationary_for_oracle_cost(gpu_available, confi
         assert np.abs(gp[:, k]).max() <= 1e-6 * np.abs(gp0[:, k]).max(), (k, np.abs(gp[:, k]).max(), res)
     for k in range(2):
         assert np.abs(gr[:, k]).max() <= 1e-6 * np.abs(gr0[:, k]).max(), (3 + k, np.abs(gr[:, k]).max(), res)
+
+
+def test_config3_fp32_huber_optimum_is_stationary_for_oracle_cost(gpu_available, config3):
+    """The HEADLINE arithmetic pinned to the oracle: at the optimum of the fp32 records + Huber solve (the bench
+    configuration, matrix-core K2), the oracle's fp64 Huber gradient of the reference residual (scipy's rho'
+    weights on the per-record 2x5 Jacobian, bundle_adjustment.py:25-106 with least_squares(loss='huber')) is
+    <= 1e-5 of its value at x0, per parameter kind.  (fp32 records and the fp16-split Schur products bound how
+    far below that the fp32 solve can get; the fp64 linear-loss test above gates 1e-6.)"""
+    import ptzba
+    p = config3
+    h = ptzba.BAHandle(0)
+    h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=ptzba.FP32,
+                  loss=ptzba.LOSS_HUBER, f_scale=1.0)
+    h.set_state(p.init_ptz, p.init_rays)
+    res = ptzba.LMSolver(h, ftol=1e-12, xtol=1e-14, max_iter=60).run()
+    ptz, rays = h.get_state()
+    h.close()
+    gp0, gr0 = _oracle_gradient(p, p.init_ptz, p.init_rays, "huber")
+    gp, gr = _oracle_gradient(p, ptz, rays, "huber")
+    ratios = [np.abs(gp[:, k]).max() / np.abs(gp0[:, k]).max() for k in range(3)] + \
+             [np.abs(gr[:, k]).max() / np.abs(gr0[:, k]).max() for k in range(2)]
+    print(f"fp32-huber stationarity |g*|/|g0| per kind (pan, tilt, f, theta, phi): {ratios}, {res}")
+    assert max(ratios) <= 1e-5, (ratios, res)
 
 
 @pytest.mark.parametrize("precision", [0, 1])

@@ -139,11 +139,35 @@ def test_optical_flow_matching_gpu(gpu_available):
     p = _lk_points(6, 400, 480, 270, margin=2).astype(np.float64)
     idx, nxt = image_process.optical_flow_matching(I, J, p)
     rn, rst, rerr = orc.lk_track(I, J, p)
-    keep = (rst == 1) & (rerr < 20) & (rn[:, 0] > 0) & (rn[:, 0] < 480) & (rn[:, 1] > 0) & (rn[:, 1] < 270)
+    # the reference's filter (image_process.py:408-411): err and the bounds, the LK status is not consulted
+    keep = (rerr < 20) & (rn[:, 0] > 0) & (rn[:, 0] < 480) & (rn[:, 1] > 0) & (rn[:, 1] < 270)
     assert len(set(idx) ^ set(np.flatnonzero(keep).tolist())) <= 2
     assert nxt.shape == (len(idx), 2) and idx == sorted(idx)
     idx3, nxt3 = image_process.optical_flow_matching(np.dstack([I] * 3), np.dstack([J] * 3), p)
     assert idx3 == idx and np.array_equal(nxt3, nxt)
+
+
+def test_lk_edge_points_follow_reference_filter(gpu_available):
+    """A point that ends in the last pixel column / row: ptz_lk_track reports status 0 (outside the
+    [0, w-1] sample range, as OpenCV), but the reference keeps any point with err < 20 and 0 < x < w,
+    0 < y < h whatever the status (image_process.py:408-411) -- so optical_flow_matching keeps it; a point
+    on a textureless window (err = inf) and one that ends past the border are dropped."""
+    import image_process
+    import ptzba
+    I, _, _ = frontend_data.textured_pair(seed=7, width=320, height=240)
+    I = I.copy()
+    I[100:140, 0:60] = 90  # a flat patch: the eigenvalue test fails there
+    p = np.array([[319.5, 120.0],   # last column, inside (w-1, w): status 0, kept by the reference filter
+                  [160.0, 239.4],   # last row
+                  [318.0, 60.0],    # inside, status 1
+                  [30.0, 120.0],    # flat window: err = inf, dropped
+                  [100.0, 100.0]], np.float32)
+    nxt, st, err = ptzba.lk_track(I, I, p)
+    assert st.tolist() == [0, 0, 1, 0, 1], st
+    assert np.all(err[[0, 1, 2, 4]] < 1e-3) and np.isinf(err[3])
+    idx, pts = image_process.optical_flow_matching(I, I, p.astype(np.float64))
+    assert idx == [0, 1, 2, 4], idx
+    np.testing.assert_allclose(pts, nxt[[0, 1, 2, 4]])
 
 
 def _sift_match(kg, ko):
