@@ -16,7 +16,10 @@ N > 1 (one process per GPU): `--gpus N` without a torch.distributed environment 
 under `python -m torch.distributed.run --nproc-per-node N` (a child process, started before anything
 touches the GPU); under the launcher the records are sharded by landmark block across ranks (poses
 replicated) and the reduced camera system and the partial scalars are summed with an RCCL all-reduce
-over xGMI each iteration (`scaling: strong`, same problem at every N).  A world size that differs from
+over xGMI each iteration (`scaling: strong`, same problem at every N).  Since round 3 the landmarks follow the
+nested-dissection split of the frame chain (ptzba_partition_landmarks) and each rank factors only its part + the
+separator: the exchange is the separator block; the library issues the collectives itself over its
+own RCCL communicator (ptzba_comm, created from an RCCL unique id).  A world size that differs from
 --gpus is an error.  `--dry-run` stops after the rendezvous (launcher plumbing test, no GPU).
 """
 import argparse
@@ -237,8 +240,20 @@ def main():
     # the coupling window of the WHOLE problem: every rank passes the same one, so all ranks choose the
     # same system order and take bit-identical pose steps
     win_hi = ptzba.frame_coupling_window(prob.n_pose, frame, landmark)
+    dist_mode = "single"
+    split = None
     if world > 1:
-        sel = shard_by_landmark(landmark, prob.n_landmark, rank, world)
+        # part-owned solve: landmarks by the nested-dissection split of the frame chain, each rank
+        # factors its part + the separator; PTZBA_DIST_MODE=replicated: contiguous landmark blocks, every rank
+        # factors the whole summed system (the round-2 protocol, for A/B)
+        replicated = os.environ.get("PTZBA_DIST_MODE", "part") == "replicated"
+        if replicated:
+            sel = shard_by_landmark(landmark, prob.n_landmark, rank, world)
+            dist_mode = "replicated"
+        else:
+            owner, mode, split = ptzba.partition_landmarks(prob.n_pose, prob.n_landmark, frame, landmark, world)
+            sel = owner[landmark] == rank
+            dist_mode = "part-owned" if mode == 1 else "replicated"
         frame, landmark, xy = frame[sel], landmark[sel], xy[sel]
         w = None if w is None else w[sel]
     precision = ptzba.FP32 if a.precision == "fp32" else ptzba.FP64
@@ -247,27 +262,34 @@ def main():
     stream = torch.cuda.current_stream()
     h.set_stream(stream.cuda_stream)
     h.set_problem(prob.n_pose, prob.n_landmark, frame, landmark, xy, prob.u, prob.v, weight=w, precision=precision,
-                  loss=loss, f_scale=1.0, frame_win_hi=win_hi)
+                  loss=loss, f_scale=1.0, frame_win_hi=win_hi,
+                  dist_world=world if (world > 1 and dist_mode == "part-owned") else 0, dist_rank=rank)
     info = h.info()
     sinfo = h.solver_info()
 
     allreduce = None
-    exchange_doubles = 0
+    comm = None
+    xinfo = None
     if world > 1:
-        # packed exchange: only the tiles of the reduced system the Schur kernel writes, plus b|g|dU
-        xb_ptr, xb_n = h.exchange_packed()
-        _, _, scal_ptr = h.exchange()
-        t_sys = torch.as_tensor(_DevArray(xb_ptr, xb_n), device=f"cuda:{local}")
-        t_scal = torch.as_tensor(_DevArray(scal_ptr, ptzba.NSCALARS), device=f"cuda:{local}")
-        exchange_doubles = xb_n
+        # the library runs every exchange itself: through its own RCCL communicator (one per rank, from an RCCL
+        # unique id rank 0 makes and torch.distributed ships), or -- gloo rehearsals of several ranks on one
+        # device -- through a hook over torch.distributed
+        if backend == "gloo":
+            g0 = (world + 1) // 2
+            groups = [dist.new_group(list(range(g0))), dist.new_group(list(range(g0, world)))]
+            mine = groups[0 if rank < g0 else 1]
 
-        def allreduce(kind):
-            if kind == "sys":
-                h.pack()
-                dist.all_reduce(t_sys)
-                h.unpack()
-            else:
-                dist.all_reduce(t_scal)
+            def hook(kind, ptr, count, strm):
+                t = torch.as_tensor(_DevArray(ptr, count), device=f"cuda:{local}")
+                dist.all_reduce(t, group=mine if kind == ptzba.X_PART else None)
+
+            h.set_exchange_hook(hook)
+        else:
+            uid = [ptzba.Comm.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            comm = ptzba.Comm(uid[0], rank, world, device=local)
+            h.attach_comm(comm)
+        xinfo = h.dist_info()
 
     # x0 is uploaded once and kept on the device: each solve restarts from it without a PCIe transfer
     h.set_state(prob.init_ptz, prob.init_rays)
@@ -417,9 +439,17 @@ def main():
                                       if a.precision == "fp32" else
                                       {"records_K1": "fp64", "schur_K2": "fp64 VALU",
                                        "reduced_system_and_state": "fp64"}),
-                       "parallelism": f"landmark-sharded x{world}" if world > 1 else "single GPU",
+                       "parallelism": (f"{dist_mode} x{world} (landmark shards; "
+                                       + ("each rank factors its part of the frame chain + the separator, "
+                                          f"split A/C/B at frames {split[0]}/{split[1]}"
+                                          if dist_mode == "part-owned" else "every rank factors the whole system")
+                                       + f"; exchanges by the library over {'RCCL (ptzba_comm)' if comm else backend})")
+                                      if world > 1 else "single GPU",
                        "reduced_system": sinfo,
-                       "allreduce_bytes_per_iteration": 8 * (exchange_doubles + ptzba.NSCALARS) if world > 1 else 0,
+                       "exchange": xinfo,
+                       "allreduce_bytes_per_trial": (8 * (xinfo["sep_doubles"] + xinfo["part_doubles"] +
+                                                          xinfo["sys_doubles"] + xinfo["scal_doubles"])
+                                                     if xinfo else 0),
                        "iterations_timed": iters, "solves_timed": solves},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
@@ -462,6 +492,8 @@ def main():
                 out["cpu_baseline"] = {"value": None, "error": repr(e)}
         print(json.dumps(out))
     h.close()
+    if comm is not None:
+        comm.close()
     if dist:
         dist.destroy_process_group()
 

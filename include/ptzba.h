@@ -61,7 +61,28 @@ typedef struct {
     const int32_t* frame_win_hi;   /* optional [n_pose]: highest frame sharing a landmark with each frame,
                                       over ALL records of a sharded problem; every rank must pass the same
                                       array so all ranks pick the same system order.  NULL: local records */
+    int32_t dist_world;            /* ranks of a sharded solve (0 or 1: single process).  >= 2 with the
+                                      landmarks partitioned by ptzba_partition_landmarks: PART-OWNED solve */
+    int32_t dist_rank;             /* this process's rank in [0, dist_world) */
 } ptzba_problem_opts;
+
+/* ---------------- multi-GPU: part-owned solve of the reduced camera system ----------------
+ * The frame chain splits by one level of nested dissection into two parts A, B and the separator C that
+ * holds every frame coupled across them.  ptzba_partition_landmarks assigns each landmark to a rank:
+ * landmarks seeing a frame of A go to rank group 0 = ranks [0, (world+1)/2), those seeing B to group 1,
+ * C-only landmarks by position; inside a group, contiguous landmark blocks of equal record counts.  A
+ * rank then factors only its part's interior (A or B) plus C: the part's Schur update onto C is local,
+ * and only the separator block (C x C, its right-hand side, g and diag U over C) is summed over all ranks
+ * (exchange PTZBA_X_SEP); with more than one rank per group the part's interior is first summed inside
+ * the group (PTZBA_X_PART).  Each rank back-substitutes C and its own part.  Frames outside its part and C
+ * keep their values on a rank (ptzba_owned_frames tells which frames a rank's state holds).  With
+ * dist_world >= 2 but no valid split (every frame couples to the last one), or an odd world of 1, the
+ * solve is REPLICATED: every rank factors the whole summed system (exchange PTZBA_X_SYS).
+ * mode_out: 1 part-owned, 0 replicated; rank_of_landmark [n_landmark] (landmarks without records: -1);
+ * split_out[3] (may be NULL) = (m, c_end, n_pose): A = [n_fixed, m), C = [m, c_end), B = [c_end, n_pose). */
+PTZBA_EXPORT int ptzba_partition_landmarks(int32_t n_pose, int32_t n_landmark, int64_t n_obs, const int32_t* obs_frame,
+                                           const int32_t* obs_landmark, int32_t n_fixed, int32_t world,
+                                           int32_t* rank_of_landmark, int32_t* mode_out, int32_t* split_out);
 
 /* per-iteration scalars read back after ptzba_step (all fp64):
  * [0] cost at the current state, [1] cost at the trial state, [2] predicted reduction,
@@ -179,6 +200,44 @@ PTZBA_EXPORT int ptzba_exchange(ptzba_handle h, void** sys_ptr, int64_t* sys_cou
 PTZBA_EXPORT int ptzba_exchange_packed(ptzba_handle h, void** buf, int64_t* count);
 PTZBA_EXPORT int ptzba_pack(ptzba_handle h);
 PTZBA_EXPORT int ptzba_unpack(ptzba_handle h);
+/* ---------------- exchanges of a multi-GPU solve (done by the library) ----------------
+ * Kinds (all are in-place SUMS over ranks of fp64 device buffers, on the handle's stream):
+ *   PTZBA_X_SYS  replicated solve: the packed reduced system (all ranks);
+ *   PTZBA_X_PART part-owned solve: the part's interior region, inside the rank group (group size > 1 only);
+ *   PTZBA_X_SEP  part-owned solve: the separator region, all ranks (a group's non-leaders send zeros);
+ *   PTZBA_X_SCAL partial LM scalars, all ranks (8 doubles replicated, 16 part-owned).
+ * With an exchange set, ptzba_linearize / ptzba_build_reduced / ptzba_solve_reduced / ptzba_lm_* /
+ * ptzba_solve run them internally at the right points: the caller issues no collective.  Two ways:
+ *   ptzba_attach_comm: the library's own RCCL communicator (ptzba_comm_new from an RCCL unique id);
+ *   ptzba_set_exchange_hook: a callback (e.g. torch.distributed over gloo for single-device rehearsals).
+ * Neither set: no exchange (single GPU, or the caller's own protocol through ptzba_exchange*). */
+enum { PTZBA_X_SYS = 0, PTZBA_X_PART = 1, PTZBA_X_SEP = 2, PTZBA_X_SCAL = 3 };
+typedef int (*ptzba_exchange_fn)(void* ctx, int32_t kind, double* dev_buf, int64_t count, void* hip_stream);
+PTZBA_EXPORT int ptzba_set_exchange_hook(ptzba_handle h, ptzba_exchange_fn fn, void* ctx);
+/* library-owned RCCL communicator ("a handle per rank, created with an RCCL unique id").
+ * RCCL is loaded at run time (dlopen of librccl.so.1, or the path in PTZBA_RCCL_LIB).  Rank 0 calls
+ * ptzba_comm_unique_id and ships the PTZBA_UNIQUE_ID_BYTES bytes to the other ranks (any channel); every
+ * rank then calls ptzba_comm_new (collective).  device < 0: use the current HIP device. */
+#define PTZBA_UNIQUE_ID_BYTES 128
+typedef struct ptzba_comm_s* ptzba_comm;
+PTZBA_EXPORT int ptzba_comm_unique_id(void* id_out);
+PTZBA_EXPORT ptzba_comm ptzba_comm_new(int device, const void* unique_id, int32_t rank, int32_t world);
+PTZBA_EXPORT void ptzba_comm_delete(ptzba_comm c);
+/* collective over the parent: ranks of equal color form a new communicator, ordered by key */
+PTZBA_EXPORT ptzba_comm ptzba_comm_split(ptzba_comm parent, int32_t color, int32_t key);
+PTZBA_EXPORT int ptzba_comm_info(ptzba_comm c, int32_t* rank, int32_t* world);
+/* in-place sum of count fp64 values of a device buffer on hip_stream (NULL: default stream) */
+PTZBA_EXPORT int ptzba_comm_allreduce(ptzba_comm c, double* dev_buf, int64_t count, void* hip_stream);
+/* the handle all-reduces through comm (not owned; NULL detaches).  A part-owned handle whose group has more
+ * than one rank splits a group communicator off comm here (collective: every rank attaches). */
+PTZBA_EXPORT int ptzba_attach_comm(ptzba_handle h, ptzba_comm comm);
+/* [0] mode (1 part-owned, 0 replicated), [1] part (0 A, 1 B, -1 all), [2] group size, [3] group leader,
+ * [4] separator exchange doubles, [5] part exchange doubles (0: none), [6] system exchange doubles
+ * (replicated), [7] scalar exchange doubles */
+PTZBA_EXPORT int ptzba_dist_info(ptzba_handle h, int64_t* info8);
+/* frames whose pose this rank's solve updates (its part and C; all frames when replicated): mask [n_pose] */
+PTZBA_EXPORT int ptzba_owned_frames(ptzba_handle h, uint8_t* mask_out);
+
 /* wait for all queued work of the handle */
 PTZBA_EXPORT int ptzba_sync(ptzba_handle h);
 /* average device time (ms) per launch of the kernel groups [K1 linearisation, Schur build, Cholesky

@@ -64,7 +64,7 @@ struct ptzba_ctx {
   int cur = 0;
   DBuf lm_aux, lm_red, red_scratch;
   DBuf sys;  // [S ld*ld | b ld | g_pose ld | dU ld]
-  DBuf scal, loc, info;
+  DBuf scal, info;  // scal: [8 partial scalars | 8 pose partials ("loc")], contiguous for one exchange
   DBuf scal_pack;               // device block [scal 8 | loc 8 | info]
   double* scal_host = nullptr;   // pinned host copy of scal_pack
   DBuf chol_tasks, Ldiag, Minv, dpose;  // Minv: inverses of the diagonal factor tiles (back-substitution)
@@ -96,7 +96,24 @@ struct ptzba_ctx {
   bool tm_flush = false;  // cold-cache timing: stream a scratch buffer through the caches before each timed K1
   DBuf flush_buf;
 
+  // multi-GPU (include/ptzba.h): exchanges done by the library, part-owned solve state
+  ptzba_comm comm = nullptr;        // attached, not owned
+  ptzba_comm group_comm = nullptr;  // split off comm for a part-owned group of > 1 ranks (owned)
+  ptzba_exchange_fn hook = nullptr;
+  void* hook_ctx = nullptr;
+  int dist_world = 1, dist_rank = 0;
+  int dist_mode = 0;  // 1: part-owned solve
+  int part = -1, group_size = 1, group_leader = 1, phase2_level = 0;
+  DBuf row_phase, fmask;  // [n_aug] phase of each system row, [n_pose] bit 0 owned / bit 1 counted
+  std::vector<uint8_t> owned_host;
+  DBuf ptiles, stiles, pbuf, sbuf;  // part / separator exchange tile lists and buffers
+  int n_ptiles = 0, n_stiles = 0;
+  VecRanges pvr{}, svr{};
+  int64_t n_pbuf = 0, n_sbuf = 0;
+
   int elem() const { return precision == PTZBA_FP32 ? 4 : 8; }
+  double* locp() const { return scal.as<double>() + 8; }
+  bool has_exchange() const { return hook != nullptr || comm != nullptr; }
   double* S() const { return sys.as<double>(); }
   double* bvec() const { return sys.as<double>() + ld * ld; }
   double* gpose() const { return sys.as<double>() + ld * ld + ld; }
@@ -168,6 +185,7 @@ void ptzba_delete(ptzba_handle h) {
     for (auto e : h->ev[k]) (void)hipEventDestroy(e);
   if (h->own) (void)hipStreamDestroy(h->own);
   if (h->scal_host) (void)hipHostFree(h->scal_host);
+  if (h->group_comm) ptzba_comm_delete(h->group_comm);
   if (h->lm_host) (void)hipHostFree(h->lm_host);
   delete h;
 }
@@ -236,6 +254,7 @@ struct SysOrder {
   int n_aug = 0;
   bool nested = false;
   int tiles_a = 0, tiles_b = 0;  // nested: tile columns of parts A and B (C follows)
+  int split_m = 0, split_cend = 0;  // nested: A = [nf, m), C = [m, c_end), B = [c_end, n_pose)
 };
 
 static SysOrder natural_order(int n_pose, int nf) {
@@ -297,8 +316,19 @@ static bool nested_order(int n_pose, int nf, const std::vector<int32_t>& win, Sy
   o.nested = true;
   o.tiles_a = ap / CHOL_NB;
   o.tiles_b = bp / CHOL_NB;
+  o.split_m = m;
+  o.split_cend = cend;
   return true;
 }
+
+// The split of a part-owned (multi-GPU) solve: nested_order's choice when it shortens the critical path,
+// else its most balanced split; false when none exists (every frame couples to the last one).  A pure
+// function of the coupling window, so ptzba_partition_landmarks and every rank's set_problem agree.
+static bool dist_order(int n_pose, int nf, const std::vector<int32_t>& win, SysOrder& o) {
+  return nested_order(n_pose, nf, win, o, false) || nested_order(n_pose, nf, win, o, true);
+}
+// rank groups of a part-owned solve: part 0 = ranks [0, g0), part 1 = [g0, world)
+static int dist_g0(int world) { return (world + 1) / 2; }
 
 struct CholPlan {
   std::vector<int32_t> tasks;  // int4 records
@@ -470,6 +500,173 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
         }
       toff.push_back((int)tasks.size());
     }
+  P.n_tasks = (int)tasks.size();
+  P.la_tasks = la;
+  P.la_tasks.insert(P.la_tasks.end(), toff.begin(), toff.end());
+  P.la_tasks.insert(P.la_tasks.end(), tasks.begin(), tasks.end());
+  return true;
+}
+
+static int ensure_group_comm(ptzba_ctx* h);
+
+// Part-owned plan (multi-GPU, api: ptzba_partition_landmarks): this rank factors the tile columns of its
+// part (A = [0, tiles_a) or B = [tiles_a, tiles_a + tiles_b)) in phase 1, then one flush level applies
+// the last part level's panels to the separator tiles, so that after phase 1 every update from the part
+// into C and into the augmented row has been applied; the separator exchange sums C over the ranks;
+// phase 2 factors C (and the augmented tile), identically on every rank.  Tasks, update rules and the
+// delayed-update scheme are make_plan's; only the column set and the phase boundary differ.
+struct PartPlan {
+  std::vector<int32_t> part_tiles;  // Schur-writable tiles of this rank (part + C rows / columns): group exchange
+  std::vector<int32_t> sep_tiles;   // separator block tiles (C x C incl. fill, augmented row over C)
+  int phase2_level = 0;
+};
+static bool make_plan_part(const SysOrder& o, int part, int n_pose, int nf, const std::vector<int32_t>& win, int64_t ld,
+                           CholPlan& P, PartPlan& Q) {
+  const int T = (int)(ld / CHOL_NB);
+  const int ta = o.tiles_a, tb = o.tiles_b, c0 = ta + tb;
+  const int p_lo = part == 0 ? 0 : ta, p_hi = part == 0 ? ta : c0;
+  auto own = [&](int t) { return (t >= p_lo && t < p_hi) || t >= c0; };
+  auto phase = [&](int t) { return (t >= p_lo && t < p_hi) ? 1 : (t >= c0 ? 2 : 0); };
+  std::vector<std::vector<uint8_t>> nz(T, std::vector<uint8_t>(T, 0));
+  auto mark = [&](int r, int c) {
+    int ti = r / CHOL_NB, tj = c / CHOL_NB;
+    if (ti < tj) std::swap(ti, tj);
+    nz[ti][tj] = 1;
+  };
+  for (int f1 = nf; f1 < n_pose; ++f1)
+    for (int f2 = f1; f2 <= std::min(n_pose - 1, (int)win[f1]); ++f2) {
+      const int p1 = o.pos[f1], p2 = o.pos[f2];
+      mark(p2, p1); mark(p2 + 2, p1); mark(p2, p1 + 2); mark(p2 + 2, p1 + 2);
+    }
+  Q.part_tiles.clear();
+  for (int i = 0; i < T; ++i)
+    for (int j = 0; j <= i; ++j)
+      if ((nz[i][j] || i == j) && own(i) && own(j)) { Q.part_tiles.push_back(i); Q.part_tiles.push_back(j); }
+  const int taug = o.n_aug / CHOL_NB;
+  for (int j = 0; j <= taug; ++j) nz[taug][j] = 1;
+  for (int i = 0; i < T; ++i) nz[i][i] = 1;
+  for (int k = 0; k < T; ++k) {  // symbolic fill (global: the other part's fill lies outside this rank's tiles)
+    std::vector<int> R;
+    for (int i = k + 1; i < T; ++i)
+      if (nz[i][k]) R.push_back(i);
+    for (size_t x = 0; x < R.size(); ++x)
+      for (size_t y = 0; y <= x; ++y) nz[R[x]][R[y]] = 1;
+  }
+  for (int i = p_lo; i < p_hi; ++i)  // the part is decoupled from the other part (nested_order's separator)
+    for (int j = 0; j < T; ++j)
+      if (nz[std::max(i, j)][std::min(i, j)] && !own(j)) return false;
+  // levels: the part's columns, a flush level, then C's columns (at most two columns per launch)
+  std::vector<int> level(T, -1), count;
+  auto place = [&](int k, int L0) {
+    int L = L0;
+    for (int p = 0; p < k; ++p)
+      if (nz[k][p] && level[p] >= 0 && phase(p) == phase(k)) L = std::max(L, level[p] + 1);
+    while (L < (int)count.size() && count[L] >= 2) ++L;
+    if (L >= (int)count.size()) count.resize(L + 1, 0);
+    count[L]++;
+    level[k] = L;
+  };
+  for (int k = p_lo; k < p_hi; ++k) place(k, 0);
+  const int flush = (int)count.size();
+  count.push_back(0);
+  Q.phase2_level = flush + 1;
+  for (int k = c0; k < T; ++k) place(k, flush + 1);
+  P.ztiles.clear();
+  Q.sep_tiles.clear();
+  for (int i = 0; i < T; ++i)
+    for (int j = 0; j <= i; ++j) {
+      if (!nz[i][j] || !own(i) || !own(j)) continue;
+      P.ztiles.push_back(i); P.ztiles.push_back(j);
+      if (j >= c0 && j < taug) { Q.sep_tiles.push_back(i); Q.sep_tiles.push_back(j); }
+    }
+  P.xtiles = Q.part_tiles;
+  const int nL = (int)count.size();
+  std::vector<std::vector<int>> K(nL);
+  for (int k = 0; k < T; ++k)
+    if (level[k] >= 0) K[level[k]].push_back(k);
+  P.tasks.clear();
+  P.level_off.assign(nL + 1, 0);
+  auto push = [&](int type, int i, int j, int w) {
+    P.tasks.push_back(type); P.tasks.push_back(i); P.tasks.push_back(j); P.tasks.push_back(w);
+  };
+  const int n_inv = (o.n_aug + CHOL_NB - 1) / CHOL_NB;
+  P.tinv_tail.clear();
+  for (int L = 0; L < nL; ++L) {
+    P.level_off[L] = (int)(P.tasks.size() / 4);
+    const std::vector<int> none;
+    const std::vector<int>& prev = L > 0 ? K[L - 1] : none;
+    for (int k : K[L]) {
+      std::vector<int> pd;
+      for (int pp : prev)
+        if (pp < k && nz[k][pp]) pd.push_back(pp);
+      for (int i = k; i < T; ++i) {
+        if (!nz[i][k] || !own(i)) continue;
+        int tm = 0;
+        for (size_t u = 0; u < pd.size(); ++u)
+          if (i == k || nz[i][pd[u]]) tm |= 1 << u;
+        push(0, i, k, chol_pack_updates(pd.size() > 0 ? pd[0] : -1, pd.size() > 1 ? pd[1] : -1, tm));
+      }
+    }
+    std::vector<std::pair<int64_t, int>> upd;
+    for (int pp : prev) {
+      std::vector<int> R;
+      for (int i = pp + 1; i < T; ++i)
+        if (nz[i][pp] && own(i)) R.push_back(i);
+      for (size_t x = 0; x < R.size(); ++x)
+        for (size_t y = 0; y <= x; ++y)
+          if (level[R[y]] > L) upd.push_back({(int64_t)R[x] * T + R[y], pp});
+    }
+    std::sort(upd.begin(), upd.end());
+    for (size_t x = 0; x < upd.size();) {
+      size_t y = x + 1;
+      while (y < upd.size() && upd[y].first == upd[x].first) ++y;
+      const int i = (int)(upd[x].first / T), j = (int)(upd[x].first % T);
+      push(1, i, j, chol_pack_updates(upd[x].second, y - x > 1 ? upd[x + 1].second : -1, 3));
+      x = y;
+    }
+    for (int pp : prev)
+      if (pp < n_inv) push(2, pp, pp, 0);
+  }
+  for (int k = 0; k < n_inv && k < T; ++k)
+    if (level[k] == nL - 1) P.tinv_tail.push_back(k);
+  P.level_off[nL] = (int)(P.tasks.size() / 4);
+  P.n_levels = nL;
+  // one back-substitution chain: C, then the part (as make_plan's nested chain of this part)
+  const int Tx = n_inv;
+  P.chain_off.assign(1, 0);
+  P.chain_cols.clear();
+  for (int kt = Tx - 1; kt >= c0; --kt) P.chain_cols.push_back(kt);
+  for (int kt = p_hi - 1; kt >= p_lo; --kt) P.chain_cols.push_back(kt);
+  P.chain_off.push_back((int)P.chain_cols.size());
+  std::vector<uint8_t> in_chain(T, 0);
+  for (int kt : P.chain_cols) in_chain[kt] = 1;
+  P.upd_off.assign(1, 0);
+  P.upd_tiles.clear();
+  for (int kt : P.chain_cols) {
+    for (int j = 0; j < kt; ++j)
+      if (in_chain[j] && nz[kt][j]) P.upd_tiles.push_back(j);
+    P.upd_off.push_back((int)P.upd_tiles.size());
+  }
+  P.lo_off.assign(1, 0);
+  P.lo_tiles.clear();
+  for (int kt : P.chain_cols) {
+    for (int i = kt + 1; i < Tx; ++i)
+      if (in_chain[i] && nz[i][kt]) P.lo_tiles.push_back(i);
+    P.lo_off.push_back((int)P.lo_tiles.size());
+  }
+  const int npos = (int)P.chain_cols.size();
+  std::vector<int> la(npos, -1), toff(1, 0), tasks;
+  for (int q = 0; q + 1 < npos; ++q)
+    for (int e = P.upd_off[q]; e < P.upd_off[q + 1]; ++e)
+      if (P.upd_tiles[e] == P.chain_cols[q + 1]) la[q] = P.chain_cols[q + 1];
+  for (int hw = 0; hw < BS_HELPERS; ++hw) {
+    for (int q = 0; q < npos; ++q)
+      for (int e = P.upd_off[q]; e < P.upd_off[q + 1]; ++e) {
+        const int j = P.upd_tiles[e];
+        if (j % BS_HELPERS == hw && j != la[q]) tasks.push_back((q << 16) | j);
+      }
+    toff.push_back((int)tasks.size());
+  }
   P.n_tasks = (int)tasks.size();
   P.la_tasks = la;
   P.la_tasks.insert(P.la_tasks.end(), toff.begin(), toff.end());
@@ -686,9 +883,16 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   std::vector<int32_t> win(frame_win_hi);
   if (o.frame_win_hi)
     for (int f = 0; f < n_pose; ++f) win[f] = std::max(win[f], o.frame_win_hi[f]);
+  // multi-GPU: part-owned solve when the frame chain splits (the landmarks partitioned accordingly by
+  // ptzba_partition_landmarks), else every rank factors the whole summed system (replicated)
+  const bool dist = o.dist_world >= 2;
+  if (dist && (o.dist_rank < 0 || o.dist_rank >= o.dist_world))
+    return fail("bad rank %d of %d", o.dist_rank, o.dist_world);
+  if (dist && !o.frame_win_hi) return fail("a sharded solve needs the global coupling window (frame_win_hi)");
   SysOrder sorder;
-  if (!(o.ordering != PTZBA_ORDER_NATURAL &&
-        nested_order(n_pose, o.n_fixed, win, sorder, o.ordering == PTZBA_ORDER_NESTED_FORCE)))
+  const bool part_mode = dist && dist_order(n_pose, o.n_fixed, win, sorder);
+  if (!part_mode && !(o.ordering != PTZBA_ORDER_NATURAL &&
+                      nested_order(n_pose, o.n_fixed, win, sorder, o.ordering == PTZBA_ORDER_NESTED_FORCE)))
     sorder = natural_order(n_pose, o.n_fixed);
   h->n_aug = sorder.n_aug;
   h->nested = sorder.nested;
@@ -696,7 +900,55 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   // the back-substitution keeps x ([ld] doubles) in LDS
   if (h->ld > CHOL_MAX_LD) return fail("reduced system %d too large for the dense solver", h->n_sys);
   CholPlan plan;
-  make_plan(sorder, n_pose, o.n_fixed, win, h->ld, plan);
+  PartPlan pplan;
+  h->dist_world = dist ? o.dist_world : 1;
+  h->dist_rank = dist ? o.dist_rank : 0;
+  h->dist_mode = part_mode ? 1 : 0;
+  h->part = -1;
+  h->group_size = 1;
+  h->group_leader = 1;
+  std::vector<uint8_t> row_phase, fmask;
+  h->owned_host.assign(n_pose, 1);
+  if (part_mode) {
+    const int g0 = dist_g0(o.dist_world);
+    h->part = o.dist_rank < g0 ? 0 : 1;
+    h->group_size = h->part == 0 ? g0 : o.dist_world - g0;
+    h->group_leader = (o.dist_rank == 0 || o.dist_rank == g0) ? 1 : 0;
+    if (!make_plan_part(sorder, h->part, n_pose, o.n_fixed, win, h->ld, plan, pplan))
+      return fail("part-owned plan: the two parts are coupled (bad coupling window)");
+    h->phase2_level = pplan.phase2_level;
+    const int m = sorder.split_m, cend = sorder.split_cend;
+    auto owned = [&](int f) { return f >= o.n_fixed && (h->part == 0 ? f < cend : f >= m); };
+    for (int64_t r = 0; r < n_obs; ++r)
+      if (obs_frame[r] >= o.n_fixed && !owned(obs_frame[r]))
+        return fail("record %lld sees frame %d outside rank %d's part (partition the landmarks with "
+                    "ptzba_partition_landmarks)", (long long)r, obs_frame[r], o.dist_rank);
+    fmask.assign(n_pose, 0);
+    for (int f = 0; f < n_pose; ++f) {
+      h->owned_host[f] = owned(f) ? 1 : 0;
+      const bool in_c = f >= m && f < cend;
+      const bool counted = f < o.n_fixed ? o.dist_rank == 0 : (in_c ? o.dist_rank == 0 : (owned(f) && h->group_leader));
+      fmask[f] = (uint8_t)((owned(f) ? 1 : 0) | (counted ? 2 : 0));
+    }
+    const int ta = sorder.tiles_a, tb = sorder.tiles_b, c0 = ta + tb;
+    const int p_lo = h->part == 0 ? 0 : ta, p_hi = h->part == 0 ? ta : c0;
+    row_phase.assign(h->n_aug, 0);
+    for (int r = 0; r < h->n_aug; ++r) {
+      const int t = r / CHOL_NB;
+      row_phase[r] = (t >= p_lo && t < p_hi) ? 1 : (t >= c0 ? 2 : 0);
+    }
+    h->n_ptiles = (int)(pplan.part_tiles.size() / 2);
+    h->n_stiles = (int)(pplan.sep_tiles.size() / 2);
+    const int64_t ld = h->ld, crow = (int64_t)c0 * CHOL_NB, ccnt = h->n_aug - crow;
+    h->pvr = VecRanges{{0, 0, 0}, {3 * ld, 0, 0}, 1};
+    h->svr = VecRanges{{ld + crow, 2 * ld + crow, 0}, {ccnt, ccnt, 0}, 2};
+    h->n_pbuf = (int64_t)h->n_ptiles * CHOL_NB * CHOL_NB + 3 * ld;
+    h->n_sbuf = (int64_t)h->n_stiles * CHOL_NB * CHOL_NB + 2 * ccnt;
+  } else {
+    make_plan(sorder, n_pose, o.n_fixed, win, h->ld, plan);
+    h->n_ptiles = h->n_stiles = 0;
+    h->n_pbuf = h->n_sbuf = 0;
+  }
   h->chol_task_off = plan.level_off;
   h->chol_tasks_host = plan.tasks;
   h->n_tinv_tail = (int)plan.tinv_tail.size();
@@ -742,7 +994,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       h->w_slot[1].alloc((size_t)std::max<int64_t>(h->n_slot, 1) * 8 * e) || h->lm_out[0].alloc((size_t)n_landmark * 8 * 8) ||
       h->lm_out[1].alloc((size_t)n_landmark * 8 * 8) || h->lm_aux.alloc((size_t)n_landmark * 8 * 8) ||
       h->lm_red.alloc((size_t)n_landmark * 4 * 8) || h->sys.alloc((size_t)h->sys_count() * 8) ||
-      h->scal.alloc(PTZBA_NSCALARS * 8) || h->red_scratch.alloc(RED_SCRATCH * 8) || h->loc.alloc(PTZBA_NSCALARS * 8) || h->info.alloc(16) ||
+      h->scal.alloc(2 * PTZBA_NSCALARS * 8) || h->red_scratch.alloc(RED_SCRATCH * 8) || h->info.alloc(16) ||
       h->Ldiag.alloc((size_t)h->ld * CHOL_NB * 8) || h->Minv.alloc((size_t)h->ld * CHOL_NB * 8) ||
       h->dpose.alloc((size_t)h->ld * 8) ||
       h->s2_part.alloc((size_t)std::max(h->n_s2_items, 1) * SCHUR_F1 * 9 * WAVE * 8) ||
@@ -753,6 +1005,18 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       upload(h->bs_upd_off, plan.upd_off, h->st) || upload(h->bs_upd_tiles, plan.upd_tiles, h->st) || upload(h->xtiles, plan.xtiles, h->st) || upload(h->ztiles, plan.ztiles, h->st) ||
       upload(h->bs_la_tasks, plan.la_tasks, h->st) || upload(h->bs_lo_off, plan.lo_off, h->st) || upload(h->bs_lo_tiles, plan.lo_tiles, h->st))
     return -1;
+  if (part_mode) {
+    if (upload(h->row_phase, row_phase, h->st) || upload(h->fmask, fmask, h->st) ||
+        upload(h->ptiles, pplan.part_tiles, h->st) || upload(h->stiles, pplan.sep_tiles, h->st) ||
+        h->pbuf.alloc((size_t)h->n_pbuf * 8) || h->sbuf.alloc((size_t)h->n_sbuf * 8))
+      return -1;
+  } else {
+    h->row_phase.release();
+    h->fmask.release();
+    h->pbuf.release();
+    h->sbuf.release();
+  }
+  if (h->dpose.p) HIPCHK(hipMemsetAsync(h->dpose.p, 0, h->dpose.bytes, h->st));  // rows a part-owned rank never solves
   h->n_xtiles = (int)(plan.xtiles.size() / 2);
   h->n_ztiles = (int)(plan.ztiles.size() / 2);
   HIPCHK(hipMemsetAsync(h->sys.p, 0, h->sys.bytes, h->st));  // outside the factor's tiles it is never written
@@ -780,12 +1044,15 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   HIPCHK(hipMemsetAsync(h->red_scratch.p, 0, h->red_scratch.bytes, h->st));
   if (!h->scal_host) HIPCHK(hipHostMalloc((void**)&h->scal_host, 24 * sizeof(double), hipHostMallocDefault));
   if (!h->scal_pack.p && h->scal_pack.alloc(24 * sizeof(double))) return -1;
-  HIPCHK(hipMemsetAsync(h->loc.p, 0, h->loc.bytes, h->st));
   h->cur = 0;
   h->lambda = 0;
   HIPCHK(hipStreamSynchronize(h->st));  // every initialisation above has landed before the handle is used
   h->have_problem = true;
-  return 0;
+  if (h->group_comm) {  // the group of the previous problem; split anew (collective: every rank sets its problem)
+    ptzba_comm_delete(h->group_comm);
+    h->group_comm = nullptr;
+  }
+  return ensure_group_comm(h);
 }
 
 int ptzba_problem_info(ptzba_handle h, int64_t* info) {
@@ -803,7 +1070,7 @@ int ptzba_problem_info(ptzba_handle h, int64_t* info) {
                                     &h->frame_seg_list, &h->frame_win_hi, &h->ptz, &h->rays, &h->ptz_trial,
                                     &h->rays_trial, &h->D_pose, &h->D_ray, &h->ft, &h->rt, &h->ug_slot[0],
                                     &h->ug_slot[1], &h->w_slot[0], &h->w_slot[1], &h->lm_out[0], &h->lm_out[1], &h->lm_aux, &h->lm_red, &h->sys,
-                                    &h->scal, &h->loc});
+                                    &h->scal});
   return 0;
 }
 
@@ -950,6 +1217,34 @@ int ptzba_get_state(ptzba_handle h, double* ptz, double* rays) {
   return 0;
 }
 
+// ------------------------------------------------------------------------------------------------
+// exchanges of a multi-GPU solve (include/ptzba.h PTZBA_X_*): in-place sums on the handle's stream through
+// the attached RCCL communicator or the caller's hook
+// ------------------------------------------------------------------------------------------------
+static int exchange(ptzba_ctx* h, int kind, double* buf, int64_t n) {
+  if (h->hook) {
+    if (h->hook(h->hook_ctx, kind, buf, n, (void*)h->st)) return fail("exchange hook failed (kind %d)", kind);
+    return 0;
+  }
+  if (h->comm) {
+    ptzba_comm c = kind == PTZBA_X_PART ? h->group_comm : h->comm;
+    if (!c) return fail("part-owned group of %d ranks has no group communicator (ptzba_attach_comm)", h->group_size);
+    return ptzba_comm_allreduce(c, buf, n, (void*)h->st);
+  }
+  return 0;
+}
+static int64_t scal_count(const ptzba_ctx* h) { return h->dist_mode ? 2 * PTZBA_NSCALARS : PTZBA_NSCALARS; }
+
+// a part-owned group of more than one rank needs its own communicator (collective over comm)
+static int ensure_group_comm(ptzba_ctx* h) {
+  // ncclCommSplit is collective over ALL ranks of comm: with world >= 3 every rank splits (a rank alone in its
+  // group gets a one-rank communicator it never uses)
+  if (!h->comm || !h->have_problem || !h->dist_mode || h->dist_world < 3) return 0;
+  if (h->group_comm) return 0;
+  h->group_comm = ptzba_comm_split(h->comm, h->part, h->dist_rank);
+  return h->group_comm ? 0 : -1;
+}
+
 int ptzba_linearize(ptzba_handle h) {
   if (!h || !h->have_problem) return fail("no problem set");
   HIPCHK(hipSetDevice(h->device));
@@ -959,6 +1254,7 @@ int ptzba_linearize(ptzba_handle h) {
   launch_reduce_cols(h->lm_out[h->cur].as<double>() + 5, h->n_lm, 8, 1, 0, h->scal.as<double>(),
                      h->red_scratch.as<double>(), h->st);
   HIPCHK(hipGetLastError());
+  if (h->has_exchange()) return exchange(h, PTZBA_X_SCAL, h->scal.as<double>(), scal_count(h));
   return 0;
 }
 
@@ -999,6 +1295,22 @@ static int build_impl(ptzba_ctx* h, double lambda, const double* lam_dev, const 
     launch_schur<double>(a, h->n_s2_items, h->n_s2_groups, h->n_fixed, h->st);
   tm_end(h, TM_SCHUR);
   HIPCHK(hipGetLastError());
+  if (h->dist_mode) {
+    if (!h->has_exchange()) return fail("a part-owned handle needs an exchange (ptzba_attach_comm / ptzba_set_exchange_hook)");
+    if (h->group_size > 1) {  // the part's interior (and C's partials) summed inside the rank group
+      launch_pack_region(h->S(), h->ld, h->ptiles.as<int2>(), h->n_ptiles, h->bvec(), h->pvr, h->pbuf.as<double>(), 0, h->st);
+      if (exchange(h, PTZBA_X_PART, h->pbuf.as<double>(), h->n_pbuf)) return -1;
+      launch_pack_region(h->S(), h->ld, h->ptiles.as<int2>(), h->n_ptiles, h->bvec(), h->pvr, h->pbuf.as<double>(), 1, h->st);
+      HIPCHK(hipGetLastError());
+    }
+  } else if (h->has_exchange()) {  // replicated: the packed reduced system summed over all ranks
+    if (ptzba_exchange_packed(h, nullptr, nullptr)) return -1;
+    const int64_t n = (int64_t)h->n_xtiles * CHOL_NB * CHOL_NB + 3 * h->ld;
+    launch_pack_exchange(h->S(), h->ld, h->xtiles.as<int2>(), h->n_xtiles, h->bvec(), h->xbuf.as<double>(), 0, h->st);
+    if (exchange(h, PTZBA_X_SYS, h->xbuf.as<double>(), n)) return -1;
+    launch_pack_exchange(h->S(), h->ld, h->xtiles.as<int2>(), h->n_xtiles, h->bvec(), h->xbuf.as<double>(), 1, h->st);
+    HIPCHK(hipGetLastError());
+  }
   return 0;
 }
 
@@ -1016,12 +1328,32 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
   const int c = sel ? 0 : h->cur;
   if (sel) nx = 1;  // the trial's slot, with the other slot as the selector's alternative
   tm_begin(h, TM_CHOL);
-  launch_chol_prepare_damped(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(),
-                             h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
-                             h->lambda, lam_dev, h->st);
-  launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
-                  h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr,
-                  reinterpret_cast<const int4*>(h->chol_tasks_host.data()), h->Minv.as<double>());
+  const int4* th = reinterpret_cast<const int4*>(h->chol_tasks_host.data());
+  if (h->dist_mode) {
+    // phase 1: the part's columns (+ flush of their updates into C); separator exchange; phase 2: C
+    launch_chol_prepare_damped(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(),
+                               h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
+                               h->lambda, lam_dev, h->st, h->row_phase.as<uint8_t>(), 1);
+    launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->phase2_level,
+                    h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>(), 0);
+    launch_pack_region(h->S(), h->ld, h->stiles.as<int2>(), h->n_stiles, h->bvec(), h->svr, h->sbuf.as<double>(),
+                       h->group_leader ? 0 : 2, h->st);
+    HIPCHK(hipGetLastError());
+    if (exchange(h, PTZBA_X_SEP, h->sbuf.as<double>(), h->n_sbuf)) return -1;
+    launch_pack_region(h->S(), h->ld, h->stiles.as<int2>(), h->n_stiles, h->bvec(), h->svr, h->sbuf.as<double>(), 1, h->st);
+    launch_chol_prepare_damped(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(),
+                               h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
+                               h->lambda, lam_dev, h->st, h->row_phase.as<uint8_t>(), 2);
+    launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
+                    h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>(),
+                    h->phase2_level);
+  } else {
+    launch_chol_prepare_damped(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(),
+                               h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
+                               h->lambda, lam_dev, h->st);
+    launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
+                    h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>());
+  }
   launch_chol_backsolve(h->S(), h->ld, h->n_aug, h->n_chain, h->bs_npos, h->bs_chain_off.as<int>(),
                         h->bs_chain_cols.as<int>(), h->bs_upd_off.as<int>(), h->bs_upd_tiles.as<int>(), h->bs_nupd,
                         h->bs_la_tasks.as<int>(), h->bs_ntasks,
@@ -1052,12 +1384,14 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
   b.lm_out1 = h->lm_out[1].as<double>();
   b.sel = sel;
   // ray back-substitution, trial poses and the trial's frame / ray tables: one launch
+  const uint8_t* fm = h->dist_mode ? h->fmask.as<uint8_t>() : nullptr;
+  const int* finfo = h->dist_mode ? h->info.as<int>() : nullptr;
   if (h->precision == PTZBA_FP32)
     launch_trial<float>(b, h->ptz.as<double>(), h->gpose(), h->D_pose.as<double>(), h->ptz_trial.as<double>(),
-                        h->loc.as<double>(), h->n_pose, h->ft64.p, h->rt64.p, h->ft.p, h->rt.p, h->st);
+                        h->locp(), h->n_pose, h->ft64.p, h->rt64.p, h->ft.p, h->rt.p, h->st, fm, finfo);
   else
     launch_trial<double>(b, h->ptz.as<double>(), h->gpose(), h->D_pose.as<double>(), h->ptz_trial.as<double>(),
-                         h->loc.as<double>(), h->n_pose, h->ft64.p, h->rt64.p, h->ft64.p, h->rt64.p, h->st);
+                         h->locp(), h->n_pose, h->ft64.p, h->rt64.p, h->ft64.p, h->rt64.p, h->st, fm, finfo);
   tm_end(h, TM_BACK);
   // trial linearisation (its cost decides acceptance; kept as the next linearisation if accepted)
   linearize_into(h, nx, sel, 1);
@@ -1066,6 +1400,9 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
                      h->red_scratch.as<double>(), h->st, h->lm_red.as<double>(), 4, 3, h->scal.as<double>() + 2,
                      h->lm_out[1].as<double>() + 5, sel, 1);
   HIPCHK(hipGetLastError());
+  // partial scalars (replicated: the landmark sums; part-owned: also the pose partials, each frame counted
+  // by one rank -- the gradient max then sums the ranks' maxima, an upper bound: gtol can only stop later)
+  if (h->has_exchange()) return exchange(h, PTZBA_X_SCAL, h->scal.as<double>(), scal_count(h));
   return 0;
 }
 
@@ -1133,8 +1470,8 @@ int ptzba_lm_decide(ptzba_handle h, int trial) {
   LMDev* st = h->lmdev.as<LMDev>();
   const int k = trial % LM_RING;
   // the record is written by the decision kernel straight into pinned host memory
-  launch_lm_decide(st, h->scal.as<double>(), h->loc.as<double>(), h->info.as<int>(), h->lm_host + k, trial + 1,
-                   h->st);
+  launch_lm_decide(st, h->scal.as<double>(), h->locp(), h->info.as<int>(), h->lm_host + k, trial + 1,
+                   h->st, h->dist_mode);
   launch_lm_commit(st, h->ptz.as<double>(), h->ptz_trial.as<double>(), 3 * h->n_pose, h->rays.as<double>(),
                    h->rays_trial.as<double>(), 2 * (int64_t)h->n_lm, h->st);
   HIPCHK(hipGetLastError());
@@ -1228,7 +1565,7 @@ int ptzba_read_scalars(ptzba_handle h, double* out) {
   if (!h || !h->have_problem) return fail("no problem set");
   HIPCHK(hipSetDevice(h->device));
   // one kernel packs scal | loc | info, one copy brings the block to pinned host memory
-  launch_pack_scalars(h->scal.as<double>(), h->loc.as<double>(), h->info.as<int>(), h->scal_pack.as<double>(), h->st);
+  launch_pack_scalars(h->scal.as<double>(), h->locp(), h->info.as<int>(), h->scal_pack.as<double>(), h->st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(h->scal_host, h->scal_pack.p, 17 * sizeof(double), hipMemcpyDeviceToHost, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
@@ -1239,7 +1576,7 @@ int ptzba_read_scalars(ptzba_handle h, double* out) {
   out[2] = s[2] + l[0];
   out[3] = s[3] + l[1];
   out[4] = s[4] + l[2];
-  out[5] = h->scal_host[16];
+  out[5] = h->dist_mode ? l[4] : h->scal_host[16];  // part-owned: the status summed over ranks
   out[6] = l[3];
   out[7] = 0;
   return 0;
@@ -1284,6 +1621,44 @@ static int pack_impl(ptzba_handle h, int unpack) {
 }
 int ptzba_pack(ptzba_handle h) { return pack_impl(h, 0); }
 int ptzba_unpack(ptzba_handle h) { return pack_impl(h, 1); }
+
+int ptzba_set_exchange_hook(ptzba_handle h, ptzba_exchange_fn fn, void* ctx) {
+  if (!h) return fail("null handle");
+  h->hook = fn;
+  h->hook_ctx = ctx;
+  return 0;
+}
+
+int ptzba_attach_comm(ptzba_handle h, ptzba_comm comm) {
+  if (!h) return fail("null handle");
+  if (h->group_comm) {
+    ptzba_comm_delete(h->group_comm);
+    h->group_comm = nullptr;
+  }
+  h->comm = comm;
+  return ensure_group_comm(h);
+}
+
+int ptzba_dist_info(ptzba_handle h, int64_t* info8) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  if (!info8) return fail("null output");
+  info8[0] = h->dist_mode;
+  info8[1] = h->part;
+  info8[2] = h->group_size;
+  info8[3] = h->group_leader;
+  info8[4] = h->n_sbuf;
+  info8[5] = h->dist_mode && h->group_size > 1 ? h->n_pbuf : 0;
+  info8[6] = h->dist_mode || h->dist_world < 2 ? 0 : (int64_t)h->n_xtiles * CHOL_NB * CHOL_NB + 3 * h->ld;
+  info8[7] = scal_count(h);
+  return 0;
+}
+
+int ptzba_owned_frames(ptzba_handle h, uint8_t* mask_out) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  if (!mask_out) return fail("null output");
+  std::copy(h->owned_host.begin(), h->owned_host.end(), mask_out);
+  return 0;
+}
 
 int ptzba_sync(ptzba_handle h) {
   if (!h) return fail("null handle");
@@ -1447,6 +1822,72 @@ int ptzba_coupling_window(int32_t n_pose, int32_t n_landmark, int64_t n_obs, con
   }
   for (int f = 0; f < n_pose; ++f) win_out[f] = f;
   for (int64_t r = 0; r < n_obs; ++r) win_out[obs_frame[r]] = std::max(win_out[obs_frame[r]], hi[obs_landmark[r]]);
+  return 0;
+}
+
+// Landmark -> rank assignment of a sharded solve (include/ptzba.h): the part-owned split when the frame
+// chain has one (landmarks seeing A to rank group 0, B to group 1, C-only landmarks to the group whose part
+// their first frame is nearer; equal-record contiguous blocks inside a group), else contiguous landmark
+// blocks of equal record counts over all ranks (replicated solve).
+int ptzba_partition_landmarks(int32_t n_pose, int32_t n_landmark, int64_t n_obs, const int32_t* obs_frame,
+                              const int32_t* obs_landmark, int32_t n_fixed, int32_t world, int32_t* rank_of_landmark,
+                              int32_t* mode_out, int32_t* split_out) {
+  if (n_pose < 1 || n_landmark < 0 || n_obs < 0 || world < 1 || n_fixed < 0 || n_fixed > n_pose || !rank_of_landmark ||
+      (n_obs > 0 && (!obs_frame || !obs_landmark)))
+    return fail("bad arguments");
+  std::vector<int32_t> win(n_pose);
+  if (ptzba_coupling_window(n_pose, n_landmark, n_obs, obs_frame, obs_landmark, win.data())) return -1;
+  std::vector<int64_t> cnt(std::max(n_landmark, 1), 0);
+  std::vector<int32_t> lo(std::max(n_landmark, 1), INT32_MAX), hi(std::max(n_landmark, 1), -1);
+  for (int64_t r = 0; r < n_obs; ++r) {
+    const int l = obs_landmark[r], f = obs_frame[r];
+    cnt[l]++;
+    if (f >= n_fixed) {
+      lo[l] = std::min(lo[l], f);
+      hi[l] = std::max(hi[l], f);
+    }
+  }
+  // equal-record contiguous blocks of the landmarks in `ids` over ranks [r0, r0 + nr)
+  auto blocks = [&](const std::vector<int32_t>& ids, int r0, int nr) {
+    int64_t tot = 0;
+    for (int l : ids) tot += cnt[l];
+    int64_t acc = 0;
+    for (int l : ids) {
+      const int k = tot > 0 ? (int)std::min<int64_t>(nr - 1, (acc * nr) / std::max<int64_t>(tot, 1)) : 0;
+      rank_of_landmark[l] = r0 + k;
+      acc += cnt[l];
+    }
+  };
+  for (int l = 0; l < n_landmark; ++l) rank_of_landmark[l] = -1;
+  SysOrder o;
+  const bool part = world >= 2 && dist_order(n_pose, n_fixed, win, o);
+  if (mode_out) *mode_out = part ? 1 : 0;
+  if (split_out) {
+    split_out[0] = part ? o.split_m : 0;
+    split_out[1] = part ? o.split_cend : 0;
+    split_out[2] = n_pose;
+  }
+  std::vector<int32_t> ids[2];
+  if (!part) {
+    for (int l = 0; l < n_landmark; ++l)
+      if (cnt[l] > 0) ids[0].push_back(l);
+    blocks(ids[0], 0, world);
+    return 0;
+  }
+  const int m = o.split_m, cend = o.split_cend;
+  for (int l = 0; l < n_landmark; ++l) {
+    if (cnt[l] == 0) continue;
+    int g;
+    if (hi[l] < 0) g = 0;                                  // fixed frames only
+    else if (lo[l] < m) g = 0;                             // sees A
+    else if (hi[l] >= cend) g = 1;                         // sees B
+    else g = (lo[l] - m) < (cend - 1 - hi[l]) ? 0 : 1;     // C only: the nearer part
+    if (lo[l] < m && hi[l] >= cend) return fail("landmark %d couples both parts (bad split)", l);
+    ids[g].push_back(l);
+  }
+  const int g0 = dist_g0(world);
+  blocks(ids[0], 0, g0);
+  blocks(ids[1], g0, world - g0);
   return 0;
 }
 

@@ -611,6 +611,8 @@ struct PoseTrialArgs {
   double* ptz_trial;
   double* out4;
   int n_pose;
+  const uint8_t* fmask;  // part-owned solve: bit 0 pose updated here, bit 1 counted here (nullptr: all)
+  const int* info;       // part-owned solve: this rank's factorisation status -> out4[4] (summed over ranks)
 };
 template <typename real>
 __global__ __launch_bounds__(256) void k_trial(BacksubArgs a, PoseTrialArgs pa, FrameTab<double>* __restrict__ ft64,
@@ -623,18 +625,21 @@ __global__ __launch_bounds__(256) void k_trial(BacksubArgs a, PoseTrialArgs pa, 
     double pr = 0, dx = 0, xx = 0, gm = 0;
     for (int f = threadIdx.x; f < pa.n_pose; f += blockDim.x) {
       double x3[3];
+      const int fm = pa.fmask ? pa.fmask[f] : 3;
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         const double x = pa.ptz[3 * f + q];
-        xx += x * x;
+        if (fm & 2) xx += x * x;
         double y = x;
-        if (f >= a.n_fixed) {
+        if (f >= a.n_fixed && (fm & 1)) {
           const int k = a.frame_pos[f] + q;  // system row
           const double d = a.dpose[k];
           y = x + d;
-          pr += -0.5 * pa.g_pose[k] * d + 0.5 * lambda * pa.D_pose[3 * f + q] * d * d;
-          dx += d * d;
-          gm = fmax(gm, fabs(pa.g_pose[k]));
+          if (fm & 2) {
+            pr += -0.5 * pa.g_pose[k] * d + 0.5 * lambda * pa.D_pose[3 * f + q] * d * d;
+            dx += d * d;
+            gm = fmax(gm, fabs(pa.g_pose[k]));
+          }
         }
         pa.ptz_trial[3 * f + q] = y;
         x3[q] = y;
@@ -659,6 +664,7 @@ __global__ __launch_bounds__(256) void k_trial(BacksubArgs a, PoseTrialArgs pa, 
         s0 += red[0][k]; s1 += red[1][k]; s2 += red[2][k]; s3 = fmax(s3, red[3][k]);
       }
       pa.out4[0] = s0; pa.out4[1] = s1; pa.out4[2] = s2; pa.out4[3] = s3;
+      if (pa.info) pa.out4[4] = (double)pa.info[0];
     }
     return;
   }
@@ -719,8 +725,9 @@ __global__ __launch_bounds__(256) void k_trial(BacksubArgs a, PoseTrialArgs pa, 
 
 template <typename real>
 void launch_trial(const BacksubArgs& a, const double* ptz, const double* g_pose, const double* D_pose, double* ptz_trial,
-                  double* out4, int n_pose, void* ft64, void* rt64, void* ft, void* rt, hipStream_t st) {
-  PoseTrialArgs pa{ptz, g_pose, D_pose, ptz_trial, out4, n_pose};
+                  double* out4, int n_pose, void* ft64, void* rt64, void* ft, void* rt, hipStream_t st,
+                  const uint8_t* fmask, const int* info) {
+  PoseTrialArgs pa{ptz, g_pose, D_pose, ptz_trial, out4, n_pose, fmask, info};
   hipLaunchKernelGGL(k_trial<real>, dim3((unsigned)((a.n_lm + 3) / 4 + 1)), dim3(256), 0, st, a, pa,
                      (FrameTab<double>*)ft64, (RayTab<double>*)rt64, (FrameTab<real>*)ft, (RayTab<real>*)rt);
 }
@@ -869,7 +876,7 @@ __global__ void k_lm_init(LMDev* st, const double* __restrict__ scal, LMParams p
 }
 
 __global__ void k_lm_decide(LMDev* st, const double* __restrict__ scal, const double* __restrict__ loc,
-                            const int* __restrict__ info, LMDev* __restrict__ rec, int seq) {
+                            const int* __restrict__ info, LMDev* __restrict__ rec, int seq, int info_in_loc) {
   LMDev s = *st;
   s.accepted = 0;
   s.relin = 0;
@@ -879,7 +886,9 @@ __global__ void k_lm_decide(LMDev* st, const double* __restrict__ scal, const do
     const double gmax = loc[3];
     s.nfev += 1;
     s.trials += 1;
-    const bool ok = info[0] == 0 && isfinite(new_cost) && isfinite(pred);
+    // part-owned solve: the factorisation status summed over ranks (loc[4]), so every rank decides alike
+    const bool fact_ok = info_in_loc ? loc[4] == 0.0 : info[0] == 0;
+    const bool ok = fact_ok && isfinite(new_cost) && isfinite(pred);
     const double actual = s.cost - new_cost;
     const double rho = (ok && pred > 0) ? actual / pred : -1.0;
     const bool gn0 = p.gauss_newton && s.lam == 0.0;
@@ -947,8 +956,8 @@ void launch_lm_init(LMDev* st, const double* scal, const LMParams& p, int cur0, 
   hipLaunchKernelGGL(k_lm_init, dim3(1), dim3(1), 0, s, st, scal, p, cur0);
 }
 void launch_lm_decide(LMDev* st, const double* scal, const double* loc, const int* info, LMDev* rec, int seq,
-                      hipStream_t s) {
-  hipLaunchKernelGGL(k_lm_decide, dim3(1), dim3(1), 0, s, st, scal, loc, info, rec, seq);
+                      hipStream_t s, int info_in_loc) {
+  hipLaunchKernelGGL(k_lm_decide, dim3(1), dim3(1), 0, s, st, scal, loc, info, rec, seq, info_in_loc);
 }
 void launch_lm_commit(const LMDev* st, double* ptz, const double* ptz_trial, int n3, double* rays,
                       const double* rays_trial, int64_t n2, hipStream_t s) {
@@ -963,9 +972,9 @@ template void launch_tables<double>(const double*, const double*, int, int, void
 template void launch_linearize<float>(const LinArgs&, int, hipStream_t);
 template void launch_linearize<double>(const LinArgs&, int, hipStream_t);
 template void launch_trial<float>(const BacksubArgs&, const double*, const double*, const double*, double*, double*, int,
-                                  void*, void*, void*, void*, hipStream_t);
+                                  void*, void*, void*, void*, hipStream_t, const uint8_t*, const int*);
 template void launch_trial<double>(const BacksubArgs&, const double*, const double*, const double*, double*, double*,
-                                   int, void*, void*, void*, void*, hipStream_t);
+                                   int, void*, void*, void*, void*, hipStream_t, const uint8_t*, const int*);
 template void launch_residual<float>(const int32_t*, const int32_t*, const int32_t*, const double2*, const void*,
                                      const int64_t*, const void*, const void*, double, double, int64_t, double*,
                                      hipStream_t);

@@ -53,21 +53,31 @@ struct PoseDamp {
   int n_pose, n_fixed;
   double lambda;
   const double* lam_dev;
+  // part-owned solve (api.hip): row_phase[r] = 1 rows of this rank's part, 2 separator rows, 0 rows of the
+  // other part; phase 1 prepares the part's rows and writes the right-hand side of the part and of C (C's is
+  // this rank's partial, summed by the separator exchange), phase 2 the separator's rows and the augmented
+  // diagonal after that exchange.  phase 0: every row (replicated solve).
+  const uint8_t* row_phase;
+  int phase;
 };
 __global__ void k_chol_prepare(double* __restrict__ A, int64_t ld, int n, const double* __restrict__ b,
                                const uint8_t* __restrict__ pad, int* info, PoseDamp pd) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0) info[0] = 0;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int ph = pd.phase;
+  if (i == 0 && ph != 2) info[0] = 0;
   if (i < n) {
-    A[(int64_t)n * ld + i] = b[i];
-    if (pad && pad[i]) A[i * ld + i] = 1.0;
+    if (ph == 0 || (ph == 1 && pd.row_phase[i] != 0)) A[(int64_t)n * ld + i] = b[i];
+    if (pad && pad[i] && (ph == 0 || pd.row_phase[i] == ph)) A[i * ld + i] = 1.0;
   }
-  if (i == n) A[i * ld + i] = AUG_DIAG;
-  if (i > n && i < ld) A[i * ld + i] = 1.0;
+  if (ph != 1) {
+    if (i == n) A[i * ld + i] = AUG_DIAG;
+    if (i > n && i < ld) A[i * ld + i] = 1.0;
+  }
   if (pd.dU && i < 3 * (int64_t)(pd.n_pose - pd.n_fixed)) {
-    const double lambda = pd.lam_dev ? *pd.lam_dev : pd.lambda;
     const int f = pd.n_fixed + (int)(i / 3);
     const int64_t row = pd.frame_pos[f] + i % 3;
+    if (ph != 0 && pd.row_phase[row] != ph) return;
+    const double lambda = pd.lam_dev ? *pd.lam_dev : pd.lambda;
     double* D = pd.D_pose + 3 * pd.n_fixed + i;
     const double d = fmax(*D, fmax(pd.dU[row], 1e-12));
     *D = d;
@@ -77,14 +87,15 @@ __global__ void k_chol_prepare(double* __restrict__ A, int64_t ld, int n, const 
 
 void launch_chol_prepare(double* A, int64_t ld, int n, double* b, const uint8_t* pad, int* info, hipStream_t st) {
   hipLaunchKernelGGL(k_chol_prepare, dim3((unsigned)((ld + 255) / 256)), dim3(256), 0, st, A, ld, n, b, pad, info,
-                     PoseDamp{nullptr, nullptr, nullptr, 0, 0, 0.0, nullptr});
+                     PoseDamp{nullptr, nullptr, nullptr, 0, 0, 0.0, nullptr, nullptr, 0});
 }
 void launch_chol_prepare_damped(double* A, int64_t ld, int n, double* b, const uint8_t* pad, int* info,
                                 const double* dU, double* D_pose, const int32_t* frame_pos, int n_pose, int n_fixed,
-                                double lambda, const double* lam_dev, hipStream_t st) {
+                                double lambda, const double* lam_dev, hipStream_t st, const uint8_t* row_phase,
+                                int phase) {
   const int64_t m = std::max<int64_t>(ld, 3 * (int64_t)(n_pose - n_fixed));
   hipLaunchKernelGGL(k_chol_prepare, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, A, ld, n, b, pad, info,
-                     PoseDamp{dU, D_pose, frame_pos, n_pose, n_fixed, lambda, lam_dev});
+                     PoseDamp{dU, D_pose, frame_pos, n_pose, n_fixed, lambda, lam_dev, row_phase, phase});
 }
 
 // Batched tile staging: every thread fetches its 4 elements of each tile into registers first (all global
@@ -910,9 +921,9 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
 }
 
 void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_off_host, int n_launch, double* Ldiag,
-                     int* info, hipStream_t st, double* sgn, const int4* tasks_host, double* Minv) {
+                     int* info, hipStream_t st, double* sgn, const int4* tasks_host, double* Minv, int first_level) {
   static const bool by_value = !getenv("PTZBA_CHOL_TASKS_PTR");  // A/B knob
-  for (int L = 0; L < n_launch; ++L) {
+  for (int L = first_level; L < n_launch; ++L) {
     const int n = task_off_host[L + 1] - task_off_host[L];
     if (n <= 0) continue;
     if (tasks_host && by_value && n <= CHOL_KT) {
@@ -1418,6 +1429,39 @@ void launch_zero_tiles(double* S, int64_t ld, const int2* zt, int n_tiles, doubl
 void launch_pack_exchange(double* S, int64_t ld, const int2* xt, int n_tiles, double* vec, double* buf, int unpack,
                           hipStream_t st) {
   hipLaunchKernelGGL(k_pack_exchange, dim3(n_tiles + 1), dim3(256), 0, st, S, ld, xt, n_tiles, vec, buf, unpack);
+}
+
+// part-owned exchanges: a tile list and up to three vector ranges (offsets into vec) moved between the
+// system and a contiguous buffer.  mode 0: pack, 1: unpack, 2: pack zeros (a group's non-leader ranks take
+// part in the separator sum with nothing: their leader already contributes the group's values).
+__global__ void k_pack_region(double* __restrict__ S, int64_t ld, const int2* __restrict__ xt, int n_tiles,
+                              double* __restrict__ vec, VecRanges vr, double* __restrict__ buf, int mode) {
+  const int k = blockIdx.x;
+  if (k < n_tiles) {
+    const int2 t = xt[k];
+    double* tile = S + (int64_t)t.x * NB * ld + (int64_t)t.y * NB;
+    double* b = buf + (int64_t)k * NB * NB;
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+      double* m = tile + (int64_t)(e >> 5) * ld + (e & 31);
+      if (mode == 1) *m = b[e];
+      else b[e] = mode == 2 ? 0.0 : *m;
+    }
+    return;
+  }
+  double* b = buf + (int64_t)n_tiles * NB * NB;
+  for (int q = 0; q < vr.n; ++q) {
+    for (int64_t e = threadIdx.x; e < vr.count[q]; e += blockDim.x) {
+      double* m = vec + vr.off[q] + e;
+      if (mode == 1) *m = b[e];
+      else b[e] = mode == 2 ? 0.0 : *m;
+    }
+    b += vr.count[q];
+  }
+}
+
+void launch_pack_region(double* S, int64_t ld, const int2* xt, int n_tiles, double* vec, const VecRanges& vr,
+                        double* buf, int mode, hipStream_t st) {
+  hipLaunchKernelGGL(k_pack_region, dim3(n_tiles + 1), dim3(256), 0, st, S, ld, xt, n_tiles, vec, vr, buf, mode);
 }
 
 }  // namespace ptzba

@@ -98,7 +98,7 @@ struct LMDev {
 };
 void launch_lm_init(LMDev* st, const double* scal, const LMParams& p, int cur0, hipStream_t s);
 void launch_lm_decide(LMDev* st, const double* scal, const double* loc, const int* info, LMDev* rec, int seq,
-                      hipStream_t s);
+                      hipStream_t s, int info_in_loc = 0);
 void launch_lm_commit(const LMDev* st, double* ptz, const double* ptz_trial, int n3, double* rays,
                       const double* rays_trial, int64_t n2, hipStream_t s);
 
@@ -124,9 +124,12 @@ void launch_build_prologue(double* S, int64_t ld, const int2* zt, int n_tiles, d
                            double lambda, const double* lam_dev, const int* skip_if, hipStream_t st,
                            const double* lm_out1 = nullptr, const int* sel = nullptr);
 // trial state (ray back-substitution + pose trial + the trial's frame / ray tables) in one launch
+// fmask (part-owned solve, else nullptr): per frame bit 0 = this rank's solve updates the pose, bit 1 = the
+// frame's terms count in this rank's pose partials (each frame is counted by exactly one rank)
 template <typename real>
 void launch_trial(const BacksubArgs& a, const double* ptz, const double* g_pose, const double* D_pose, double* ptz_trial,
-                  double* out4, int n_pose, void* ft64, void* rt64, void* ft, void* rt, hipStream_t st);
+                  double* out4, int n_pose, void* ft64, void* rt64, void* ft, void* rt, hipStream_t st,
+                  const uint8_t* fmask = nullptr, const int* info = nullptr);
 template <typename real>
 void launch_residual(const int32_t* rec_seg, const int32_t* seg_frame, const int32_t* seg_lm, const double2* seg_base,
                      const void* rec_xy, const int64_t* perm, const void* ft64, const void* rt64, double u, double v,
@@ -142,13 +145,15 @@ void launch_chol_prepare(double* A, int64_t ld, int n, double* b, const uint8_t*
 // the same plus the Marquardt damping of the pose rows (k_pose_damp's work) in one launch
 void launch_chol_prepare_damped(double* A, int64_t ld, int n, double* b, const uint8_t* pad, int* info,
                                 const double* dU, double* D_pose, const int32_t* frame_pos, int n_pose, int n_fixed,
-                                double lambda, const double* lam_dev, hipStream_t st);
+                                double lambda, const double* lam_dev, hipStream_t st, const uint8_t* row_phase = nullptr,
+                                int phase = 0);  // part-owned solve: rows of one phase only (chol_kernels.hip)
 // sgn != nullptr: signed factor L Sigma L^T of an indefinite matrix (sigma per row into sgn[ld])
 // tasks_host (optional, the host copy of `tasks`): levels of <= CHOL_KT tasks pass them by value
 constexpr int CHOL_KT = 240;  // 3.75 KB of kernel arguments
 void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_off_host, int n_launch, double* Ldiag,
                      int* info, hipStream_t st, double* sgn = nullptr, const int4* tasks_host = nullptr,
-                     double* Minv = nullptr);  // Minv: target of type-2 tasks (diagonal tile inverses)
+                     double* Minv = nullptr,  // Minv: target of type-2 tasks (diagonal tile inverses)
+                     int first_level = 0);    // levels [first_level, n_launch)
 // la_tasks: lookahead back substitution's [lookahead tile per position | task offsets per (chain, helper) |
 // tasks q << 16 | tile], built by the host plan (api.hip make_plan)
 constexpr int BS_HELPERS = 7;
@@ -165,6 +170,14 @@ void launch_zero_tiles(double* S, int64_t ld, const int2* zt, int n_tiles, doubl
 // packed exchange of the Schur-written tiles + b | g_pose | dU (vec = b, contiguous 3 ld doubles)
 void launch_pack_exchange(double* S, int64_t ld, const int2* xt, int n_tiles, double* vec, double* buf, int unpack,
                           hipStream_t st);
+// part-owned exchanges: tile list + up to three ranges of the b | g_pose | dU vectors; mode 0 pack, 1 unpack,
+// 2 pack zeros
+struct VecRanges {
+  int64_t off[3], count[3];
+  int n;
+};
+void launch_pack_region(double* S, int64_t ld, const int2* xt, int n_tiles, double* vec, const VecRanges& vr,
+                        double* buf, int mode, hipStream_t st);
 // task word w: bits 0-13 update panel p1 + 1, bits 14-27 p2 + 1 (0 = none), bits 28/29: p1/p2 also update T
 inline int chol_pack_updates(int p1, int p2, int tmask) { return (p1 + 1) | ((p2 + 1) << 14) | (tmask << 28); }
 

@@ -63,7 +63,14 @@ TIME_FLUSH = 0x10000  # include/ptzba.h PTZBA_TIME_FLUSH: cold-cache K1 timing
 
 class ptzba_problem_opts(Structure):
     _fields_ = [("precision", c_int32), ("loss", c_int32), ("f_scale", c_double), ("n_fixed", c_int32),
-                ("ordering", c_int32), ("frame_win_hi", c_void_p)]
+                ("ordering", c_int32), ("frame_win_hi", c_void_p), ("dist_world", c_int32), ("dist_rank", c_int32)]
+
+
+# exchange kinds of a multi-GPU solve (include/ptzba.h PTZBA_X_*)
+X_SYS, X_PART, X_SEP, X_SCAL = 0, 1, 2, 3
+X_NAMES = {X_SYS: "sys", X_PART: "part", X_SEP: "sep", X_SCAL: "scal"}
+UNIQUE_ID_BYTES = 128
+EXCHANGE_FN = ctypes.CFUNCTYPE(c_int32, c_void_p, c_int32, c_void_p, c_int64, c_void_p)
 
 
 def _ptr(a):
@@ -132,6 +139,17 @@ def lib():
         "ptz_keyframe_features": ([I32, I64, V, V, V, V, V, V, V, V], I),
         "ptz_pack_records": ([I32, I64, V, V, V, V, V, V, V, I64, V, V, V, V], I),
         "ptz_refine_poses": ([I, I32, V, I64, V, V, D, D, V, V, POINTER(ptz_refine_opts), V, V, V], I),
+        "ptzba_partition_landmarks": ([I32, I32, I64, V, V, I32, I32, V, POINTER(c_int32), V], I),
+        "ptzba_set_exchange_hook": ([V, EXCHANGE_FN, V], I),
+        "ptzba_comm_unique_id": ([V], I),
+        "ptzba_comm_new": ([I, V, I32, I32], V),
+        "ptzba_comm_delete": ([V], None),
+        "ptzba_comm_split": ([V, I32, I32], V),
+        "ptzba_comm_info": ([V, POINTER(c_int32), POINTER(c_int32)], I),
+        "ptzba_comm_allreduce": ([V, V, I64, V], I),
+        "ptzba_attach_comm": ([V, V], I),
+        "ptzba_dist_info": ([V, V], I),
+        "ptzba_owned_frames": ([V, V], I),
         "ptzekf_new": ([I], V),
         "ptzekf_delete": ([V], None),
         "ptzekf_num_rays": ([V], I),
@@ -161,6 +179,9 @@ EXPORTED_SYMBOLS = [
     "ptz_py_shuffle_prefix", "ptz_set_order_pairs", "ptz_keyframe_features", "ptz_pack_records",
     "ptz_refine_poses", "ptzekf_new", "ptzekf_delete", "ptzekf_num_rays", "ptzekf_set_state", "ptzekf_get_state", "ptzekf_add_pose_cov",
     "ptzekf_remove_rays", "ptzekf_add_rays", "ptzekf_project_visible", "ptzekf_update",
+    "ptzba_partition_landmarks", "ptzba_set_exchange_hook", "ptzba_comm_unique_id", "ptzba_comm_new",
+    "ptzba_comm_delete", "ptzba_comm_split", "ptzba_comm_info", "ptzba_comm_allreduce", "ptzba_attach_comm",
+    "ptzba_dist_info", "ptzba_owned_frames",
 ]
 
 
@@ -482,6 +503,62 @@ def frame_coupling_window(n_pose, frame, landmark):
     return win
 
 
+def partition_landmarks(n_pose, n_landmark, frame, landmark, world, n_fixed=1):
+    """Landmark -> rank of a sharded solve (ptzba_partition_landmarks, host only): returns (rank_of_landmark
+    [n_landmark] int32 (-1: no records), mode (1 part-owned, 0 replicated), (m, c_end, n_pose) split)."""
+    frame = np.ascontiguousarray(frame, np.int32)
+    landmark = np.ascontiguousarray(landmark, np.int32)
+    out = np.empty(int(n_landmark), np.int32)
+    mode = c_int32(0)
+    split = np.zeros(3, np.int32)
+    _check(lib().ptzba_partition_landmarks(int(n_pose), int(n_landmark), len(frame), _ptr(frame), _ptr(landmark),
+                                           int(n_fixed), int(world), _ptr(out), ctypes.byref(mode), _ptr(split)),
+           "ptzba_partition_landmarks")
+    return out, int(mode.value), tuple(int(x) for x in split)
+
+
+class Comm:
+    """Library-owned RCCL communicator (ptzba_comm_*): one per rank, created from an RCCL unique id that rank 0
+    makes with unique_id() and ships to the others over any channel (include/ptzba.h)."""
+
+    def __init__(self, unique_id, rank, world, device=-1, _ptr_value=None):
+        if _ptr_value is not None:
+            self.c = _ptr_value
+        else:
+            uid = (ctypes.c_char * UNIQUE_ID_BYTES).from_buffer_copy(bytes(unique_id))
+            self.c = lib().ptzba_comm_new(int(device), uid, int(rank), int(world))
+        if not self.c:
+            raise PtzbaError(f"ptzba_comm_new: {lib().ptzba_last_error().decode()}")
+        self.rank, self.world = rank, world
+
+    @staticmethod
+    def unique_id():
+        buf = (ctypes.c_char * UNIQUE_ID_BYTES)()
+        _check(lib().ptzba_comm_unique_id(buf), "ptzba_comm_unique_id")
+        return bytes(buf)
+
+    def split(self, color, key):
+        c = lib().ptzba_comm_split(self.c, int(color), int(key))
+        if not c:
+            raise PtzbaError(f"ptzba_comm_split: {lib().ptzba_last_error().decode()}")
+        return Comm(None, -1, -1, _ptr_value=c)
+
+    def allreduce(self, dev_ptr, count, stream=0):
+        _check(lib().ptzba_comm_allreduce(self.c, c_void_p(dev_ptr), int(count), c_void_p(stream or 0)),
+               "ptzba_comm_allreduce")
+
+    def close(self):
+        if getattr(self, "c", None):
+            lib().ptzba_comm_delete(self.c)
+            self.c = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class BAHandle:
     """One device-resident BA problem (opaque C handle, rf_map_wrapper.RFMap style)."""
 
@@ -512,9 +589,13 @@ class BAHandle:
         _check(lib().ptzba_use_own_stream(self.h), "ptzba_use_own_stream")
 
     def set_problem(self, n_pose, n_landmark, frame, landmark, xy, u, v, weight=None, precision=FP64,
-                    loss=LOSS_LINEAR, f_scale=1.0, n_fixed=1, ordering=ORDER_NESTED, frame_win_hi=None):
+                    loss=LOSS_LINEAR, f_scale=1.0, n_fixed=1, ordering=ORDER_NESTED, frame_win_hi=None,
+                    dist_world=0, dist_rank=0):
         """frame_win_hi: optional global coupling window (see include/ptzba.h); pass the same array on
-        every rank of a sharded solve (frame_coupling_window() of the full record set)."""
+        every rank of a sharded solve (frame_coupling_window() of the full record set).  dist_world >= 2: this
+        rank's share of a sharded solve, its landmarks chosen by partition_landmarks (part-owned solve when the
+        frame chain splits, else replicated); the exchanges then run inside the library (attach_comm /
+        set_exchange_hook)."""
         frame = np.ascontiguousarray(frame, dtype=np.int32)
         landmark = np.ascontiguousarray(landmark, dtype=np.int32)
         xy = _f64(xy, (-1, 2))
@@ -526,11 +607,53 @@ class BAHandle:
         if self._win is not None and len(self._win) != int(n_pose):
             raise ValueError("frame_win_hi must have n_pose entries")
         opts = ptzba_problem_opts(int(precision), int(loss), float(f_scale), int(n_fixed), int(ordering),
-                                  _ptr(self._win).value if self._win is not None else None)
+                                  _ptr(self._win).value if self._win is not None else None, int(dist_world),
+                                  int(dist_rank))
         _check(lib().ptzba_set_problem(self.h, int(n_pose), int(n_landmark), n, _ptr(frame), _ptr(landmark), _ptr(xy),
                                        _ptr(w), float(u), float(v), ctypes.byref(opts)), "ptzba_set_problem")
         self.n_pose, self.n_landmark, self.n_obs = int(n_pose), int(n_landmark), n
         self.precision = precision
+
+    # multi-GPU exchanges run inside the library (include/ptzba.h PTZBA_X_*)
+    internal_exchange = False
+
+    def attach_comm(self, comm):
+        """Exchange through the library's own RCCL communicator (Comm); None detaches."""
+        _check(lib().ptzba_attach_comm(self.h, c_void_p(comm.c if comm is not None else 0)), "ptzba_attach_comm")
+        self._comm = comm
+        self.internal_exchange = comm is not None or getattr(self, "_hook", None) is not None
+
+    def set_exchange_hook(self, fn):
+        """fn(kind, dev_ptr, count, stream) -> None sums `count` fp64 values in place over the ranks of the exchange
+        `kind` (X_SYS / X_PART (the rank's group) / X_SEP / X_SCAL), e.g. torch.distributed over gloo.  None removes."""
+        if fn is None:
+            self._hook = None
+            _check(lib().ptzba_set_exchange_hook(self.h, EXCHANGE_FN(0), None), "ptzba_set_exchange_hook")
+        else:
+            def tramp(ctx, kind, ptr, count, stream):
+                try:
+                    fn(int(kind), int(ptr), int(count), int(stream or 0))
+                    return 0
+                except Exception as e:  # reported through ptzba_last_error's caller
+                    import traceback
+                    traceback.print_exc()
+                    self._hook_error = e
+                    return 1
+            self._hook = EXCHANGE_FN(tramp)  # kept alive with the handle
+            _check(lib().ptzba_set_exchange_hook(self.h, self._hook, None), "ptzba_set_exchange_hook")
+        self.internal_exchange = fn is not None or getattr(self, "_comm", None) is not None
+
+    def dist_info(self):
+        out = np.zeros(8, np.int64)
+        _check(lib().ptzba_dist_info(self.h, _ptr(out)), "ptzba_dist_info")
+        return dict(mode="part-owned" if out[0] else "replicated", part=int(out[1]), group_size=int(out[2]),
+                    group_leader=bool(out[3]), sep_doubles=int(out[4]), part_doubles=int(out[5]),
+                    sys_doubles=int(out[6]), scal_doubles=int(out[7]))
+
+    def owned_frames(self):
+        out = np.zeros(self.n_pose, np.uint8)
+        _check(lib().ptzba_owned_frames(self.h, _ptr(out)), "ptzba_owned_frames")
+        return out.astype(bool)
 
     def solver_info(self):
         out = np.zeros(8, np.int64)
@@ -788,6 +911,8 @@ class LMSolver:
         self.verbose = verbose
         self.max_retries = max_retries
         self.device_loop = device_loop and hasattr(handle, "lm_start")
+        if getattr(handle, "internal_exchange", False):
+            self.allreduce = None  # the handle's library calls run the exchanges themselves
 
     def _scalars(self):
         if self.allreduce is not None:

@@ -139,3 +139,126 @@ class NumpyBAHandle:
 
     def sync(self):
         pass
+
+
+class NumpyPartHandle(NumpyBAHandle):
+    """The PART-OWNED multi-GPU protocol of libptzba (include/ptzba.h, api.hip make_plan_part / solve_impl) in
+    numpy: this rank holds the landmarks ptzba_partition_landmarks gave it (they see its part P = A or B and
+    the separator C only); it factors P, forms P's Schur update of C locally, and sums only the separator
+    block over the ranks (X_SEP; a group's non-leaders send zeros), after summing P's interior inside its
+    rank group when the group has more than one rank (X_PART).  Pose partials are counted once over all ranks
+    (P's frames by the group leader, C's and the fixed frames by rank 0) and summed with the landmark partials
+    and the factorisation status (X_SCAL, 16 values).  `hook(kind, array)` sums in place over the kind's ranks.
+    The handle runs its exchanges itself (internal_exchange), like a GPU handle with a comm or hook."""
+    internal_exchange = True
+
+    def set_dist(self, world, rank, split, hook):
+        m, cend, _ = split
+        g0 = (world + 1) // 2
+        self.part = 0 if rank < g0 else 1
+        self.group_size = g0 if self.part == 0 else world - g0
+        self.leader = rank in (0, g0)
+        self.rank = rank
+        self.hook = hook
+        fx = self.n_fixed
+        free = np.arange(fx, self.n_pose)
+        self.P = free[(free < m) if self.part == 0 else (free >= cend)] - fx
+        self.C = free[(free >= m) & (free < cend)] - fx
+        owned = np.zeros(self.n_pose, bool)
+        owned[self.P + fx] = True
+        owned[self.C + fx] = True
+        self.owned = owned
+        cnt = np.zeros(self.n_pose, bool)
+        if self.leader:
+            cnt[self.P + fx] = True
+        if rank == 0:
+            cnt[self.C + fx] = True
+            cnt[:fx] = True
+        self.counted = cnt
+        assert np.all(owned[self.frame[self.frame >= fx]]), "a record sees a frame outside this rank's part"
+
+    def linearize(self):
+        super().linearize()
+        self.loc[:] = 0
+        red = np.concatenate([self.scal, self.loc])  # only the cost is used here
+        self.hook("scal", red)
+        self.scal[:], self.loc[:] = red[:8], red[8:]
+
+    def build_reduced(self, lam):
+        super().build_reduced(lam)
+        if self.group_size > 1:
+            self.hook("part", self.sys)
+
+    def solve_reduced(self):
+        L = self.cur
+        ns = 3 * self.nf
+        fx, fx3 = self.n_fixed, 3 * self.n_fixed
+        S = self.sys[:ns * ns].reshape(ns, ns).copy()
+        b = self.sys[ns * ns:ns * ns + ns].copy()
+        gpose = self.sys[ns * ns + ns:ns * ns + 2 * ns].copy()
+        dU = self.sys[ns * ns + 2 * ns:].copy()
+        rows = lambda fr: (3 * fr[:, None] + np.arange(3)).reshape(-1)  # noqa: E731
+        p, c = rows(self.P), rows(self.C)
+        D = self.D_pose[fx3:]
+        D[p] = np.maximum(D[p], dU[p])
+        info = 0
+        try:
+            Lpp = np.linalg.cholesky(S[np.ix_(p, p)] + np.diag(self.lam * D[p]))
+            Lcp = np.linalg.solve(Lpp, S[np.ix_(c, p)].T).T
+            yp = np.linalg.solve(Lpp, b[p])
+        except np.linalg.LinAlgError:
+            info = 1
+            Lpp = np.eye(len(p)); Lcp = np.zeros((len(c), len(p))); yp = np.zeros(len(p))
+        Scc = S[np.ix_(c, c)] - Lcp @ Lcp.T
+        bc = b[c] - Lcp @ yp
+        sep = np.concatenate([Scc.reshape(-1), bc, gpose[c], dU[c]])
+        if not self.leader:
+            sep[:] = 0.0
+        self.hook("sep", sep)
+        k = len(c)
+        Scc, bc = sep[:k * k].reshape(k, k), sep[k * k:k * k + k]
+        gpose[c], dU[c] = sep[k * k + k:k * k + 2 * k], sep[k * k + 2 * k:]
+        D[c] = np.maximum(D[c], dU[c])
+        dp = np.zeros(ns)
+        try:
+            Lcc = np.linalg.cholesky(Scc + np.diag(self.lam * D[c]))
+            dp[c] = np.linalg.solve(Lcc.T, np.linalg.solve(Lcc, bc))
+        except np.linalg.LinAlgError:
+            info = 1
+        dp[p] = np.linalg.solve(Lpp.T, yp - Lcp.T @ dp[c])
+        self.info = info
+        self.ptz_trial = self.ptz.copy()
+        self.ptz_trial[fx:] += dp.reshape(-1, 3)
+        t = L['gl'] + np.einsum('flij,fi->lj', L['W'][fx:], dp.reshape(-1, 3))
+        dl = -np.einsum('lij,lj->li', self.Vinv, t)
+        dl[~L['present']] = 0
+        self.rays_trial = self.rays + dl
+        self.trial = self._lin(self.ptz_trial, self.rays_trial)
+        pres = L['present']
+        Dr = self.D_ray.reshape(-1, 2)
+        self.scal[:] = 0
+        self.scal[0] = self.cur['cost']
+        self.scal[1] = self.trial['cost']
+        self.scal[2] = float(np.sum((-0.5 * np.sum(L['gl'] * dl, 1) + 0.5 * self.lam * np.sum(Dr * dl * dl, 1))[pres]))
+        self.scal[3] = float(np.sum((dl * dl)[pres]))
+        self.scal[4] = float(np.sum((self.rays * self.rays)[pres]))
+        cr = self.counted[fx:].repeat(3)  # counted free rows
+        self.loc[:] = 0
+        self.loc[0] = float(np.sum((-0.5 * gpose * dp + 0.5 * self.lam * D * dp * dp)[cr]))
+        self.loc[1] = float(np.sum((dp * dp)[cr]))
+        self.loc[2] = float(np.sum((self.ptz * self.ptz)[self.counted]))
+        self.loc[3] = float(np.max(np.abs(gpose[cr]))) if cr.any() else 0.0
+        self.loc[4] = float(info)
+        red = np.concatenate([self.scal, self.loc])
+        self.hook("scal", red)
+        self.scal[:], self.loc[:] = red[:8], red[8:]
+
+    def read_scalars(self):
+        s, l = self.scal, self.loc
+        return np.array([s[0], s[1], s[2] + l[0], s[3] + l[1], s[4] + l[2], l[4], l[3], 0.0])
+
+    def accept(self, ok):
+        if ok:
+            self.ptz, self.rays = self.ptz_trial, self.rays_trial
+            self.cur = self.trial
+            self.scal[0] = self.cur['cost']

@@ -137,3 +137,65 @@ def test_bench_rejects_world_size_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--dry-run"],
                        capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+
+
+def _part_worker(rank, world, port, out_dir):
+    """One rank of a PART-OWNED solve (include/ptzba.h): landmarks from ptzba_partition_landmarks, the part's
+    interior summed in its rank group ('part', only with > 1 rank per group), the separator block over all
+    ranks ('sep'), the partial scalars ('scal') -- numpy emulation of the library's protocol over gloo."""
+    sys.path[:0] = [HERE, ROOT, os.path.join(ROOT, "pan-tilt-zoom-slam_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    import ptzba
+    import synthetic
+    from numpy_handle import NumpyPartHandle
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g0 = (world + 1) // 2
+    groups = [dist.new_group(list(range(g0))), dist.new_group(list(range(g0, world)))]
+    mine = groups[0 if rank < g0 else 1]
+    prob = synthetic.make_problem("config2", seed=0)
+    owner, mode, split = ptzba.partition_landmarks(prob.n_pose, prob.n_landmark, prob.frame, prob.landmark, world)
+    assert mode == 1, "config 2 splits"
+    sel = owner[prob.landmark] == rank
+
+    def hook(kind, arr):
+        dist.all_reduce(torch.from_numpy(arr), group=mine if kind == "part" else None)
+
+    h = NumpyPartHandle()
+    h.set_problem(prob.n_pose, prob.n_landmark, prob.frame[sel], prob.landmark[sel], prob.xy[sel], prob.u, prob.v)
+    h.set_dist(world, rank, split, hook)
+    h.set_state(prob.init_ptz, prob.init_rays)
+    res = ptzba.LMSolver(h, ftol=1e-9, xtol=1e-12, max_iter=8).run()
+    ptz, rays = h.get_state()
+    own_lm = np.zeros(prob.n_landmark, bool)
+    own_lm[prob.landmark[sel]] = True
+    np.savez(os.path.join(out_dir, f"part{world}_rank{rank}.npz"), ptz=ptz, rays=rays, owned=h.owned, own_lm=own_lm,
+             cost=res.cost, njev=res.njev, n_rec=int(sel.sum()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_part_owned_solve_matches_single_rank(tmp_path, world):
+    """The part-owned multi-GPU protocol (each rank factors its part A or B plus the separator C; only C is
+    summed over all ranks, the part's interior inside its rank group when the group has > 1 rank) reproduces
+    the 1-rank solve of the whole problem (config 2: A = frames 1-9, C = 10-42, B = 43-49): same iterations
+    and cost, every owned pose and every rank's rays within 1e-8; every frame is owned by some rank."""
+    sys.path[:0] = [HERE, ROOT, os.path.join(ROOT, "pan-tilt-zoom-slam_amd")]
+    import synthetic
+    mp.start_processes(_part_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    prob = synthetic.make_problem("config2", seed=0)
+    res1, ptz1, rays1 = _solve(prob, prob.frame, prob.landmark, prob.xy, iters=8)
+    outs = [np.load(os.path.join(tmp_path, f"part{world}_rank{r}.npz")) for r in range(world)]
+    assert sum(int(o["n_rec"]) for o in outs) == len(prob.frame)
+    covered = np.zeros(prob.n_pose, bool)
+    for o in outs:
+        own = o["owned"]
+        covered |= own
+        np.testing.assert_allclose(o["ptz"][own], ptz1[own], rtol=0, atol=1e-8)
+        np.testing.assert_allclose(o["rays"][o["own_lm"]], rays1[o["own_lm"]], rtol=0, atol=1e-8)
+        assert abs(float(o["cost"]) - res1.cost) <= 1e-10 * res1.cost
+        assert int(o["njev"]) == res1.njev
+    assert covered[1:].all()

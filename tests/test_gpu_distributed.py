@@ -99,3 +99,126 @@ def test_two_rank_gpu_solve_matches_single_rank(gpu_available, tmp_path, config)
         assert abs(float(o["cost"]) - res1.cost) <= 1e-9 * res1.cost
     # the two ranks took bit-identical pose steps (same summed system, same decisions)
     assert np.array_equal(outs[0]["ptz"], outs[1]["ptz"])
+
+
+# ------------------------------------------------------------------------------------------------------
+# part-owned solve (include/ptzba.h ptzba_partition_landmarks): each rank factors its part of the frame
+# chain plus the separator; the library runs the exchanges itself through a hook (gloo here, RCCL in bench)
+# ------------------------------------------------------------------------------------------------------
+def _dev_view(ptr, n, device):
+    import torch
+    import bench
+    return torch.as_tensor(bench._DevArray(ptr, n), device=f"cuda:{device}")
+
+
+def _part_worker(rank, world, port, out_dir, config, precision, loss):
+    sys.path[:0] = [HERE, ROOT, os.path.join(ROOT, "pan-tilt-zoom-slam_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    import ptzba
+    import synthetic
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g0 = (world + 1) // 2
+    groups = [dist.new_group(list(range(g0))), dist.new_group(list(range(g0, world)))]
+    mine = groups[0 if rank < g0 else 1]
+    prob = synthetic.make_problem(config, seed=0)
+    win_hi = ptzba.frame_coupling_window(prob.n_pose, prob.frame, prob.landmark)
+    owner, mode, split = ptzba.partition_landmarks(prob.n_pose, prob.n_landmark, prob.frame, prob.landmark, world)
+    sel = owner[prob.landmark] == rank
+    h = ptzba.BAHandle(0)
+    h.set_stream(torch.cuda.current_stream().cuda_stream)
+    h.set_problem(prob.n_pose, prob.n_landmark, prob.frame[sel], prob.landmark[sel], prob.xy[sel], prob.u, prob.v,
+                  precision=precision, loss=loss, frame_win_hi=win_hi, dist_world=world, dist_rank=rank)
+    kinds = []
+
+    def hook(kind, ptr, count, stream):
+        kinds.append(kind)
+        dist.all_reduce(_dev_view(ptr, count, 0), group=mine if kind == ptzba.X_PART else None)
+
+    h.set_exchange_hook(hook)
+    h.set_state(prob.init_ptz, prob.init_rays)
+    res = ptzba.LMSolver(h, ftol=CFG["ftol"], xtol=1e-14, max_iter=CFG["max_iter"]).run()
+    ptz, rays = h.get_state()
+    own_lm = np.zeros(prob.n_landmark, bool)
+    own_lm[prob.landmark[sel]] = True
+    np.savez(os.path.join(out_dir, f"part_rank{rank}.npz"), ptz=ptz, rays=rays, owned=h.owned_frames(), own_lm=own_lm,
+             cost=res.cost, njev=res.njev, status=res.status, n_rec=int(sel.sum()), mode=mode,
+             dist=np.array(list(h.dist_info().values())[1:], np.int64), kinds=np.array(sorted(set(kinds))))
+    h.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("config,world,precision,loss", [("config2", 2, 0, 0), ("config2", 4, 0, 0),
+                                                         ("config3", 2, 0, 0), ("config3", 2, 1, 1)])
+def test_part_owned_gpu_solve_matches_single_rank(gpu_available, tmp_path, config, world, precision, loss):
+    """libptzba's part-owned solve on one device (ranks over gloo): every rank factors its part (A or B) and the
+    separator C; only C (and, with 2 ranks per part, the part's interior inside its group) is exchanged.  The
+    result equals the single-rank solve of the whole problem: same iterations and status, the cost to 1e-9
+    relative, every rank's poses (its part and C) and rays within 1e-8 (fp64; fp32 records + Huber: 1e-6 deg /
+    1e-4 px -- the per-rank Schur sums round differently).  config 3 = the headline problem (A = frames 1-199,
+    C = 200-305, B = 306-499)."""
+    import ptzba
+    import synthetic
+    mp.start_processes(_part_worker, args=(world, _free_port(), str(tmp_path), config, precision, loss), nprocs=world,
+                       join=True, start_method="spawn")
+    prob = synthetic.make_problem(config, seed=0)
+    win_hi = ptzba.frame_coupling_window(prob.n_pose, prob.frame, prob.landmark)
+    h1 = ptzba.BAHandle(0)
+    h1.set_problem(prob.n_pose, prob.n_landmark, prob.frame, prob.landmark, prob.xy, prob.u, prob.v,
+                   precision=precision, loss=loss, frame_win_hi=win_hi)
+    res1, ptz1, rays1 = _solve(h1, prob)
+    h1.close()
+    outs = [np.load(os.path.join(tmp_path, f"part_rank{r}.npz")) for r in range(world)]
+    assert all(int(o["mode"]) == 1 for o in outs)
+    assert sum(int(o["n_rec"]) for o in outs) == len(prob.frame)
+    covered = np.zeros(prob.n_pose, bool)
+    fp64 = precision == 0
+    for r, o in enumerate(outs):
+        own = o["owned"]
+        covered |= own
+        assert int(o["njev"]) == res1.njev and int(o["status"]) == res1.status, (r, int(o["njev"]), res1)
+        assert abs(float(o["cost"]) - res1.cost) <= (1e-9 if fp64 else 1e-7) * res1.cost
+        if fp64:
+            np.testing.assert_allclose(o["ptz"][own], ptz1[own], rtol=0, atol=1e-8)
+            np.testing.assert_allclose(o["rays"][o["own_lm"]], rays1[o["own_lm"]], rtol=0, atol=1e-8)
+        else:
+            rm = synthetic.pose_rmse(o["ptz"][own], ptz1[own])
+            assert rm[0] < 1e-6 and rm[1] < 1e-6 and rm[2] < 1e-4, rm
+        kinds = set(o["kinds"].tolist())
+        assert ptzba.X_SEP in kinds and ptzba.X_SCAL in kinds and ptzba.X_SYS not in kinds
+        assert (ptzba.X_PART in kinds) == (world > 2)
+    assert covered[1:].all()
+
+
+def test_library_rccl_comm_single_rank(gpu_available):
+    """The library-owned RCCL communicator on the real RCCL (one rank: every all-reduce is the identity): a
+    handle with the comm attached runs the replicated exchanges (packed system, scalars) on its stream inside
+    ptzba_lm_* and reproduces the solve without exchanges bit for bit; ptzba_comm_allreduce sums in place."""
+    import torch
+    import ptzba
+    import synthetic
+    torch.cuda.set_device(0)
+    uid = ptzba.Comm.unique_id()
+    comm = ptzba.Comm(uid, 0, 1, device=0)
+    x = torch.arange(7, dtype=torch.float64, device="cuda:0")
+    comm.allreduce(x.data_ptr(), 7, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(x.cpu(), torch.arange(7, dtype=torch.float64))
+    prob = synthetic.make_problem("config2", seed=1)
+    out = []
+    for attach in (False, True):
+        h = ptzba.BAHandle(0)
+        h.set_problem(prob.n_pose, prob.n_landmark, prob.frame, prob.landmark, prob.xy, prob.u, prob.v,
+                      precision=ptzba.FP64)
+        if attach:
+            h.attach_comm(comm)
+            assert h.internal_exchange
+        out.append(_solve(h, prob))
+        h.close()
+    (r0, p0, y0), (r1, p1, y1) = out
+    assert (r0.njev, r0.status) == (r1.njev, r1.status) and r0.cost == r1.cost
+    assert np.array_equal(p0, p1) and np.array_equal(y0, y1)
+    comm.close()
