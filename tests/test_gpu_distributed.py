@@ -111,6 +111,17 @@ def _dev_view(ptr, n, device):
     return torch.as_tensor(bench._DevArray(ptr, n), device=f"cuda:{device}")
 
 
+def _make(config):
+    import synthetic
+    if config == "grid":  # 3 tilt rows x 40 keyframes: the 2-D coupled grid of config 4 at test size
+        return synthetic.make_grid_problem(120, 6000, -20.0, 20.0, (-10.0, 0.0, 10.0), seed=3)
+    return synthetic.make_problem(config, seed=0)
+
+
+def _iters(config):
+    return 3 if config == "config4" else CFG["max_iter"]
+
+
 def _part_worker(rank, world, port, out_dir, config, precision, loss):
     sys.path[:0] = [HERE, ROOT, os.path.join(ROOT, "pan-tilt-zoom-slam_amd")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -123,7 +134,7 @@ def _part_worker(rank, world, port, out_dir, config, precision, loss):
     g0 = (world + 1) // 2
     groups = [dist.new_group(list(range(g0))), dist.new_group(list(range(g0, world)))]
     mine = groups[0 if rank < g0 else 1]
-    prob = synthetic.make_problem(config, seed=0)
+    prob = _make(config)
     win_hi = ptzba.frame_coupling_window(prob.n_pose, prob.frame, prob.landmark)
     owner, mode, split = ptzba.partition_landmarks(prob.n_pose, prob.n_landmark, prob.frame, prob.landmark, world)
     sel = owner[prob.landmark] == rank
@@ -139,7 +150,7 @@ def _part_worker(rank, world, port, out_dir, config, precision, loss):
 
     h.set_exchange_hook(hook)
     h.set_state(prob.init_ptz, prob.init_rays)
-    res = ptzba.LMSolver(h, ftol=CFG["ftol"], xtol=1e-14, max_iter=CFG["max_iter"]).run()
+    res = ptzba.LMSolver(h, ftol=CFG["ftol"], xtol=1e-14, max_iter=_iters(config)).run()
     ptz, rays = h.get_state()
     own_lm = np.zeros(prob.n_landmark, bool)
     own_lm[prob.landmark[sel]] = True
@@ -151,25 +162,31 @@ def _part_worker(rank, world, port, out_dir, config, precision, loss):
     dist.destroy_process_group()
 
 
+@pytest.mark.timeout(900)
 @pytest.mark.parametrize("config,world,precision,loss", [("config2", 2, 0, 0), ("config2", 4, 0, 0),
-                                                         ("config3", 2, 0, 0), ("config3", 2, 1, 1)])
+                                                         ("grid", 2, 0, 0), ("grid", 4, 0, 0),
+                                                         ("config3", 2, 0, 0), ("config3", 2, 1, 1),
+                                                         ("config4", 2, 1, 1)])
 def test_part_owned_gpu_solve_matches_single_rank(gpu_available, tmp_path, config, world, precision, loss):
     """libptzba's part-owned solve on one device (ranks over gloo): every rank factors its part (A or B) and the
     separator C; only C (and, with 2 ranks per part, the part's interior inside its group) is exchanged.  The
     result equals the single-rank solve of the whole problem: same iterations and status, the cost to 1e-9
     relative, every rank's poses (its part and C) and rays within 1e-8 (fp64; fp32 records + Huber: 1e-6 deg /
     1e-4 px -- the per-rank Schur sums round differently).  config 3 = the headline problem (A = frames 1-199,
-    C = 200-305, B = 306-499)."""
+    C = 200-305, B = 306-499); grid / config 4 = keyframes on tilt rows (config 4: 410M records, A = 1-2185,
+    C = 2186-2803, B = 2804-4999; 3 LM iterations)."""
     import ptzba
     import synthetic
     mp.start_processes(_part_worker, args=(world, _free_port(), str(tmp_path), config, precision, loss), nprocs=world,
                        join=True, start_method="spawn")
-    prob = synthetic.make_problem(config, seed=0)
+    prob = _make(config)
     win_hi = ptzba.frame_coupling_window(prob.n_pose, prob.frame, prob.landmark)
     h1 = ptzba.BAHandle(0)
     h1.set_problem(prob.n_pose, prob.n_landmark, prob.frame, prob.landmark, prob.xy, prob.u, prob.v,
                    precision=precision, loss=loss, frame_win_hi=win_hi)
-    res1, ptz1, rays1 = _solve(h1, prob)
+    h1.set_state(prob.init_ptz, prob.init_rays)
+    res1 = ptzba.LMSolver(h1, ftol=CFG["ftol"], xtol=1e-14, max_iter=_iters(config)).run()
+    ptz1, rays1 = h1.get_state()
     h1.close()
     outs = [np.load(os.path.join(tmp_path, f"part_rank{r}.npz")) for r in range(world)]
     assert all(int(o["mode"]) == 1 for o in outs)
