@@ -263,7 +263,8 @@ def main():
     h.set_stream(stream.cuda_stream)
     h.set_problem(prob.n_pose, prob.n_landmark, frame, landmark, xy, prob.u, prob.v, weight=w, precision=precision,
                   loss=loss, f_scale=1.0, frame_win_hi=win_hi,
-                  dist_world=world if (world > 1 and dist_mode == "part-owned") else 0, dist_rank=rank)
+                  dist_world=world if (world > 1 and not os.environ.get("PTZBA_DIST_MODE") == "replicated") else 0,
+                  dist_rank=rank)
     info = h.info()
     sinfo = h.solver_info()
 
@@ -290,6 +291,8 @@ def main():
             comm = ptzba.Comm(uid[0], rank, world, device=local)
             h.attach_comm(comm)
         xinfo = h.dist_info()
+        if xinfo["sys_doubles"] == 0 and xinfo["mode"] == "replicated":  # PTZBA_DIST_MODE=replicated (no dist opts)
+            xinfo["sys_doubles"] = h.exchange_packed()[1]
 
     # x0 is uploaded once and kept on the device: each solve restarts from it without a PCIe transfer
     h.set_state(prob.init_ptz, prob.init_rays)

@@ -76,8 +76,9 @@ typedef struct {
  * (exchange PTZBA_X_SEP); with more than one rank per group the part's interior is first summed inside
  * the group (PTZBA_X_PART).  Each rank back-substitutes C and its own part.  Frames outside its part and C
  * keep their values on a rank (ptzba_owned_frames tells which frames a rank's state holds).  With
- * dist_world >= 2 but no valid split (every frame couples to the last one), or an odd world of 1, the
- * solve is REPLICATED: every rank factors the whole summed system (exchange PTZBA_X_SYS).
+ * dist_world >= 2 but no valid split (every frame couples to the last one), the
+ * solve is REPLICATED: every rank factors the whole summed system (exchange PTZBA_X_SYS).  dist_world < 2:
+ * a single-process problem.
  * mode_out: 1 part-owned, 0 replicated; rank_of_landmark [n_landmark] (landmarks without records: -1);
  * split_out[3] (may be NULL) = (m, c_end, n_pose): A = [n_fixed, m), C = [m, c_end), B = [c_end, n_pose). */
 PTZBA_EXPORT int ptzba_partition_landmarks(int32_t n_pose, int32_t n_landmark, int64_t n_obs, const int32_t* obs_frame,
@@ -136,9 +137,11 @@ PTZBA_EXPORT int ptzba_restore_state(ptzba_handle h);
 
 /* ---------------- one Levenberg-Marquardt iteration, split at the exchange points -------------
  * Single GPU:  ptzba_linearize; loop { ptzba_step(lambda); ptzba_read_scalars; ptzba_accept(ok) }.
- * Multi-GPU (records sharded by landmark block, poses replicated): after ptzba_build_reduced the
- * caller all-reduces (sum) the exchange buffer's reduced system, then ptzba_solve_reduced, then
- * all-reduces the partial scalars, then ptzba_accept.  ptzba_step == build_reduced + solve_reduced. */
+ * Multi-GPU: with a communicator or hook attached (ptzba_attach_comm / ptzba_set_exchange_hook below) the
+ * same calls run the exchanges themselves.  Without one, a replicated sharded solve may still use the
+ * caller's own protocol: after ptzba_build_reduced the caller all-reduces (sum) the exchange buffer's
+ * reduced system, then ptzba_solve_reduced, then all-reduces the partial scalars, then ptzba_accept.
+ * ptzba_step == build_reduced + solve_reduced. */
 PTZBA_EXPORT int ptzba_linearize(ptzba_handle h);
 PTZBA_EXPORT int ptzba_build_reduced(ptzba_handle h, double lambda);
 PTZBA_EXPORT int ptzba_solve_reduced(ptzba_handle h);

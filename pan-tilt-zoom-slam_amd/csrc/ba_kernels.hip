@@ -84,6 +84,9 @@ constexpr int SEGW = K1_SEGW;  // segments per LDS window per wave
 #ifndef K1_TAIL_ATOMIC
 #define K1_TAIL_ATOMIC 0  // 1: tail-run adds of the coarsened reduction as LDS atomics (7 us slower at config 3)
 #endif
+#ifndef K1_TAIL_ORDER
+#define K1_TAIL_ORDER 1  // 1: lgkmcnt(0) before the tail read-modify-write (ordered by completion); 0: issue order
+#endif
 #ifndef K1_FTV_LATE
 #define K1_FTV_LATE 0  // 1: phase C loads its frame tables itself (frees registers; measured slower)
 #endif
@@ -362,14 +365,19 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
     seg_scan_step<DPP_ROW_BCAST15, 0xa>(kenc, t0, t1, t2, t3);
     seg_scan_step<DPP_ROW_BCAST31, 0xc>(kenc, t0, t1, t2, t3);
     const int knext = dpp_i<DPP_WAVE_SHL1, 0xf>(kenc);
-    // The next lane's head run may have added into the same slot above (ds_add).  A wave's LDS operations
-    // execute in issue order, so a plain read-modify-write issued after those adds sees them; the compiler
-    // must not hoist the read above them (per lane it can prove key[j] != kt, but the adds of OTHER lanes
-    // alias), hence the compiler barrier.  K1_TAIL_ATOMIC=1 keeps the atomic form.
+    // The next lane's head run may have added into the same slot above (ds_add).  A plain read-modify-write
+    // after those adds have completed (lgkmcnt(0)) sees them; the compiler must not hoist the read above the
+    // wait (per lane it can prove key[j] != kt, but the adds of OTHER lanes alias), hence the compiler
+    // barrier.  K1_TAIL_ATOMIC=1 keeps the atomic form, K1_TAIL_ORDER=0 the issue-order form of round 2.
     if (knext != kenc && kt >= 0 && kt < SEGW) {
 #if K1_TAIL_ATOMIC
       atomicAdd(acc0 + kt, t0); atomicAdd(acc1 + kt, t1); atomicAdd(acc2 + kt, t2); atomicAdd(acc3 + kt, t3);
 #else
+#if K1_TAIL_ORDER
+      // the read below must see the ds_adds issued above by the other lanes of this wave: wait until they have
+      // completed (lgkmcnt(0)) instead of relying on the LDS executing a wave's operations in issue order
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+#endif
       asm volatile("" ::: "memory");
       acc0[kt] += t0; acc1[kt] += t1; acc2[kt] += t2; acc3[kt] += t3;
 #endif

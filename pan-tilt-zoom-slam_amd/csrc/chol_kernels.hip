@@ -278,7 +278,9 @@ constexpr int WB = 8;
 #define CHOL_NU_RELAXED 0  // the same for the helpers' progress counters (A/B)
 #endif
 #ifndef CHOL_NL_RELAXED
-#define CHOL_NL_RELAXED 1  // 1: publish a factor block without waiting for its LDS stores (0: wait, A/B)
+#define CHOL_NL_RELAXED 0  // 0: publish a factor block after lgkmcnt(0) with a release store (ordered by
+                           // completion); 1: no wait, relying on a wave's LDS operations executing in issue
+                           // order (round 2; 5 us per trial faster at config 3, not covered by the memory model)
 #endif
 #ifndef CHOL_P_READLANE
 #define CHOL_P_READLANE 1  // 1: the pivot block by v_readlane instead of an LDS round trip (flag form)
