@@ -54,6 +54,7 @@ struct ptzba_ctx {
   DBuf frame_seg_begin, frame_seg_list, frame_win_hi;
   DBuf s2_items, s2_groups, s2_lm, lm_meta;  // K2 work items / tiles / lists, slot ranges
   DBuf s2_part, part_diag;                                    // K2 split partials (blocks, diagonal terms)
+  DBuf s2_item_group, s2_tile_cnt;                            // matrix-core K2's folded reduce
   int n_s2_items = 0, n_s2_groups = 0;
   int64_t n_slot = 0;  // dense landmark x frame slots (W table rows)
   // device: state
@@ -984,6 +985,14 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       upload(h->s2_items, s2_items, h->st) || upload(h->s2_groups, s2_groups, h->st) || upload(h->s2_lm, s2_lm, h->st) ||
       upload(h->lm_meta, lm_meta, h->st))
     return -1;
+  {  // item -> tile (group) map and the per-tile split counters of the folded reduce (zero between launches)
+    std::vector<int32_t> item_group(std::max(h->n_s2_items, 1), 0);
+    for (int g = 0; g < h->n_s2_groups; ++g)
+      for (int it = s2_groups[4 * g + 2]; it < s2_groups[4 * g + 3]; ++it) item_group[it] = g;
+    if (upload(h->s2_item_group, item_group, h->st) || h->s2_tile_cnt.alloc((size_t)std::max(h->n_s2_groups, 1) * 4))
+      return -1;
+    HIPCHK(hipMemsetAsync(h->s2_tile_cnt.p, 0, h->s2_tile_cnt.bytes, h->st));
+  }
   const size_t e = h->elem();
   if (h->ptz.alloc(3 * n_pose * 8) || h->ptz_trial.alloc(3 * n_pose * 8) || h->rays.alloc(2 * (size_t)n_landmark * 8) ||
       h->rays_trial.alloc(2 * (size_t)n_landmark * 8) || h->D_pose.alloc(3 * n_pose * 8) ||
@@ -1288,6 +1297,8 @@ static int build_impl(ptzba_ctx* h, double lambda, const double* lam_dev, const 
   a.ug_slot1 = h->ug_slot[1].p;
   a.w_slot1 = h->w_slot[1].p;
   a.sel = sel;
+  a.item_group = h->s2_item_group.as<int32_t>();
+  a.tile_cnt = h->s2_tile_cnt.as<unsigned>();  // used only by the folded-reduce A/B build (MF_FOLD_REDUCE)
   tm_begin(h, TM_SCHUR);
   if (h->precision == PTZBA_FP32)
     launch_schur<float>(a, h->n_s2_items, h->n_s2_groups, h->n_fixed, h->st);

@@ -60,6 +60,8 @@ struct SchurArgs {
   const void* ug_slot1;           // sel != nullptr: read slot *sel (1 = these buffers), see LinArgs
   const void* w_slot1;
   const int* sel;
+  const int32_t* item_group;      // [n_items] tile (group) of each item (matrix-core K2: folded reduce)
+  unsigned* tile_cnt;             // [n_groups] finished splits per tile (zero between launches)
 };
 
 struct BacksubArgs {

@@ -383,6 +383,16 @@ __device__ __forceinline__ void split_pk(float x0, float x1, hp2v& h, hp2v& l) {
   l = __builtin_amdgcn_cvt_pkrtz(x0 - (float)h[0], x1 - (float)h[1]);
 }
 
+template <typename real, bool AGENT>
+__device__ __forceinline__ void schur_reduce_elem(const SchurArgs& a, const int4 g, int e);
+template <bool AGENT>
+__device__ __forceinline__ void schur_reduce_vec(const SchurArgs& a, const int4 g, int tid);
+#ifndef MF_FOLD_REDUCE
+#define MF_FOLD_REDUCE 0  // 1: the last split of a tile reduces it (no k_schur_reduce launch); 0: separate reduce.
+                          // Measured (r03h): 258 us vs 69 us per build -- every split's agent-scope release
+                          // (needed before its counter add) writes back its XCD's L2; kept for A/B only
+#endif
+
 __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
   constexpr int SNB = 16;                // landmarks per batch
   constexpr int NSL = SNB * WAVE / 512;  // W slots staged per thread per batch
@@ -645,6 +655,30 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
         const int q = row / SF, i = row % SF, r = col / WAVE, f2 = col % WAVE;
         out[(i * 9 + 3 * q + r) * WAVE + f2] = (float)acc[x][y][v];
       }
+#if MF_FOLD_REDUCE
+  if (a.tile_cnt) {  // folded reduce: the tile's last split sums all splits in item order (schur_reduce_elem)
+    __shared__ int s_grp;
+    __syncthreads();
+    if (t == 0) {
+      const int gi = a.item_group[item];
+      const int4 gg = a.groups[gi];
+      const unsigned done = __hip_atomic_fetch_add(a.tile_cnt + gi, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      s_grp = (done == (unsigned)(gg.w - gg.z - 1)) ? gi : -1;
+    }
+    __syncthreads();
+    const int gi = s_grp;
+    if (gi >= 0) {
+      // every thread acquires (agent scope: the other splits' partials were released by their counter adds),
+      // then reads them with ordinary cached loads, several elements in flight per thread
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const int4 gg = a.groups[gi];
+#pragma unroll 4
+      for (int e = t; e < SF * 9 * WAVE; e += 512) schur_reduce_elem<float, false>(a, gg, e);
+      if (gg.y == 0 && t < SF * 3) schur_reduce_vec<false>(a, gg, t);
+      if (t == 0) __hip_atomic_store(a.tile_cnt + gi, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    }
+  }
+#endif
   SK_T(10);
 #ifdef SK_TIMING
   __syncthreads();
@@ -670,6 +704,54 @@ extern "C" int ptzba_debug_sk_items(long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sk_items), sizeof(g_sk_items)) == hipSuccess ? 0 : -1;
 }
 #endif
+
+// The matrix-core K2 reduces each tile in its LAST split (k_schur_mf, "folded reduce"): the split that
+// finishes last (agent-scope counter per tile, acq_rel) sums every split's partial in item order, exactly as
+// k_schur_reduce does (bitwise the same S), so the separate reduce launch and its boundary go away.  Partials
+// of other workgroups are read with agent-scope loads.
+template <typename real, bool AGENT>
+__device__ __forceinline__ real part_load(const real* p) {
+  if constexpr (AGENT) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+template <typename real, bool AGENT>
+__device__ __forceinline__ void schur_reduce_elem(const SchurArgs& a, const int4 g, int e) {
+  constexpr int NE = SF * 9 * WAVE;
+  const int f1b = g.x, chunk = g.y;
+  const int ln = e & 63, ik = e >> 6, i = ik / 9, k = ik - 9 * i, q = k / 3, r = k - 3 * q;
+  const int f1 = f1b + i, f2 = f1b + WAVE * chunk + ln;
+  if (!(f1 < a.n_pose && f2 >= f1 && f2 <= a.frame_win_hi[f1])) return;
+  const real* p = (const real*)a.part + e;
+  double v = 0;
+  int it = g.z;
+  for (; it + 4 <= g.w; it += 4) {
+    const double p0 = part_load<real, AGENT>(p + (int64_t)it * NE), p1 = part_load<real, AGENT>(p + (int64_t)(it + 1) * NE);
+    const double p2 = part_load<real, AGENT>(p + (int64_t)(it + 2) * NE), p3 = part_load<real, AGENT>(p + (int64_t)(it + 3) * NE);
+    v += p0; v += p1; v += p2; v += p3;
+  }
+  for (; it < g.w; ++it) v += (double)part_load<real, AGENT>(p + (int64_t)it * NE);
+  if (f2 == f1) {  // chunk 0: U of the frame, summed over the tile's splits
+    const int ui = q <= r ? (q == 0 ? r : (q == 1 ? 2 + r : 5)) : (r == 0 ? q : (r == 1 ? 2 + q : 5));
+    for (int it2 = g.z; it2 < g.w; ++it2) v += part_load<double, AGENT>(a.part_diag + ((int64_t)it2 * SF + i) * 12 + ui);
+  }
+  const int64_t ld = a.ld, col0 = a.frame_pos[f1], pf2 = a.frame_pos[f2];
+  if (pf2 >= col0) a.S[(pf2 + r) * ld + col0 + q] = v;
+  else a.S[(col0 + q) * ld + pf2 + r] = v;
+}
+template <bool AGENT>
+__device__ __forceinline__ void schur_reduce_vec(const SchurArgs& a, const int4 g, int tid) {
+  const int f1b = g.x;
+  const int i2 = tid / 3, q2 = tid - 3 * i2, f = f1b + i2;
+  if (f >= a.n_pose) return;
+  double d[12];
+  for (int k = 0; k < 12; ++k) d[k] = 0;
+  for (int it2 = g.z; it2 < g.w; ++it2)
+    for (int k = 0; k < 12; ++k) d[k] += part_load<double, AGENT>(a.part_diag + ((int64_t)it2 * SF + i2) * 12 + k);
+  const int c0 = a.frame_pos[f];
+  a.b[c0 + q2] = -d[6 + q2] + d[9 + q2];
+  a.g_pose[c0 + q2] = d[6 + q2];
+  a.dU[c0 + q2] = d[q2 == 0 ? 0 : (q2 == 1 ? 3 : 5)];
+}
 
 // tile reduction: thread = one element of a tile (grid: tile x 72 blocks of 256); fixed-order sum of the
 // splits, U on the diagonal blocks, write the lower triangle in the system order (mirror when f2
@@ -729,13 +811,17 @@ template <typename real>
 void launch_schur(const SchurArgs& a, int n_items, int n_groups, int n_fixed, hipStream_t st) {
   const int n_free = a.n_pose - n_fixed;
   if (n_free <= 0) return;
+  bool folded = false;
   if (n_items > 0) {
-    if (sizeof(real) == 4 && schur_use_mfma())
+    if (sizeof(real) == 4 && schur_use_mfma()) {
       hipLaunchKernelGGL(k_schur_mf, dim3(n_items), dim3(512), 0, st, a);
-    else
+      folded = MF_FOLD_REDUCE && a.item_group && a.tile_cnt;
+    } else {
       hipLaunchKernelGGL(k_schur<real>, dim3(n_items), dim3(512), 0, st, a);
+    }
   }
-  if (n_groups > 0) hipLaunchKernelGGL(k_schur_reduce<real>, dim3(SF * 9 * WAVE / 256, n_groups), dim3(256), 0, st, a);
+  if (n_groups > 0 && !folded)
+    hipLaunchKernelGGL(k_schur_reduce<real>, dim3(SF * 9 * WAVE / 256, n_groups), dim3(256), 0, st, a);
 }
 
 template void launch_schur<float>(const SchurArgs&, int, int, int, hipStream_t);
