@@ -336,6 +336,14 @@ PTZBA_EXPORT int ptz_match_hamming(int device, int64_t n1, int64_t n2, int32_t n
 PTZBA_EXPORT int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int32_t nfeatures, int32_t max_kp,
                           float* kp_out, float* response_out, float* des_out, int32_t* n_out);
 
+/* Shi-Tomasi corner response (cv.cornerMinEigenVal(img, blockSize=3, ksize=3): the measure of cv.goodFeaturesToTrack
+ * in detect_harris_corner_grid, image_process.py:352-390): eig_out [height][width] float32; locmax_out (may be NULL)
+ * [height][width] = 1 where eig > 0 is the maximum of its 3x3 neighbourhood and the pixel is not on the image's
+ * one-pixel border (goodFeaturesToTrack's candidates after its dilation).  The per-cell threshold, the ordering
+ * and the minimum-distance selection run on the host (image_process.detect_harris_corner_grid). */
+PTZBA_EXPORT int ptz_corner_min_eig(int device, int32_t width, int32_t height, const uint8_t* img, float* eig_out,
+                                    uint8_t* locmax_out);
+
 /* Coupling window of a record set (host only, O(n_obs)): win_out[f] = the highest frame that shares a
  * landmark with frame f (>= f).  Computed over ALL records it is the frame_win_hi every rank of a
  * landmark-sharded solve passes in ptzba_problem_opts. */

@@ -664,6 +664,59 @@ def bilinear(img, x, y):
     return (1 - ay) * ((1 - ax) * img[y0, x0] + ax * img[y0, x1]) + ay * ((1 - ax) * img[y1, x0] + ax * img[y1, x1])
 
 
+def corner_min_eig(img):
+    """cv.cornerMinEigenVal(img, blockSize=3, ksize=3) as goodFeaturesToTrack uses it (detect_harris_corner_grid,
+    image_process.py:352-390; OpenCV's published algorithm, cv2 itself is not importable here): 3x3 Sobel sums
+    scaled by 1/(4*3*255), products summed over a 3x3 block with reflect-101 borders (of the source for the
+    derivatives, of the product image for the block), smaller eigenvalue (a+c) - sqrt((a-c)^2 + b^2) with
+    a, c = half the summed squares.  float32, every operation rounded separately in the kernel's order.
+    Returns (eig [h, w] float32, 3x3 local maxima with eig > 0 off the one-pixel border [h, w] bool)."""
+    im = np.asarray(img, np.int32)
+    h, w = im.shape
+
+    def r101(i, n):
+        i = np.abs(i)
+        return np.where(i >= n, 2 * n - 2 - i, i) if n > 1 else np.zeros_like(i)
+    ys, xs = np.arange(h), np.arange(w)
+    scale = np.float32(1.0 / (4.0 * 3.0 * 255.0))
+    # derivatives at every pixel (reflected source)
+    xm, xp = r101(xs - 1, w), r101(xs + 1, w)
+    ym, yp = r101(ys - 1, h), r101(ys + 1, h)
+    gx = np.zeros((h, w), np.int64)
+    gy = np.zeros((h, w), np.int64)
+    for j, wj in ((-1, 1), (0, 2), (1, 1)):
+        yy = r101(ys + j, h)
+        xx = r101(xs + j, w)
+        gx += wj * (im[yy][:, xp] - im[yy][:, xm])
+        gy += wj * (im[yp][:, xx] - im[ym][:, xx])
+    dx = gx.astype(np.float32) * scale
+    dy = gy.astype(np.float32) * scale
+    pa, pb, pc = dx * dx, dx * dy, dy * dy
+    sa = np.zeros((h, w), np.float32)
+    sb = np.zeros((h, w), np.float32)
+    sc = np.zeros((h, w), np.float32)
+    for by in (-1, 0, 1):
+        cy = r101(ys + by, h)
+        for bx in (-1, 0, 1):
+            cx = r101(xs + bx, w)
+            sa = sa + pa[cy][:, cx]
+            sb = sb + pb[cy][:, cx]
+            sc = sc + pc[cy][:, cx]
+    a = sa * np.float32(0.5)
+    c = sc * np.float32(0.5)
+    d = (a - c) * (a - c) + sb * sb
+    eig = (a + c) - np.sqrt(d)
+    loc = np.zeros((h, w), bool)
+    if h >= 3 and w >= 3:
+        core = eig[1:-1, 1:-1]
+        mx = np.full(core.shape, -np.inf, np.float32)
+        for oy in (-1, 0, 1):
+            for ox in (-1, 0, 1):
+                mx = np.maximum(mx, eig[1 + oy:h - 1 + oy, 1 + ox:w - 1 + ox])
+        loc[1:-1, 1:-1] = (core > 0) & (core >= mx)
+    return eig.astype(np.float32), loc
+
+
 def lk_track(img0, img1, pts, win=31, levels=4, max_iter=30, eps=0.01, min_eig=1e-4):
     """Restatement of ptz_lk_track: returns (next points [n, 2], status [n] uint8, err [n])."""
     pts = np.asarray(pts, np.float64).reshape(-1, 2)

@@ -727,3 +727,80 @@ int ptz_match_hamming(int device, int64_t n1, int64_t n2, int32_t nbytes, const 
   if (n2) HIPCHK(hipMemcpy(idx21, i21.p, (size_t)n2 * 4, hipMemcpyDeviceToHost));
   return 0;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Shi-Tomasi corner response (cv.cornerMinEigenVal(img, blockSize=3, ksize=3), the measure of
+// cv.goodFeaturesToTrack as detect_harris_corner_grid calls it, image_process.py:352-390): 3x3 Sobel
+// derivatives scaled by 1 / (4 * 3 * 255) (OpenCV's scale for 8-bit input, ksize 3, blockSize 3), the
+// products dx^2, dx dy, dy^2 summed over a 3x3 block (unnormalised box filter), and the smaller eigenvalue
+// (a + c) - sqrt((a - c)^2 + b^2) with a = sum dx^2 / 2, c = sum dy^2 / 2, b = sum dx dy.  Every border is
+// reflect-101 (the source for the derivatives, the product image for the block sum).  fp32 throughout
+// (every operation rounded separately: the oracle repeats it in numpy float32).  A second pass flags the
+// 3x3 local maxima (eig == max of its neighbourhood, eig > 0, not on the one-pixel image border): the
+// candidates goodFeaturesToTrack keeps after its dilation.
+// ------------------------------------------------------------------------------------------------
+namespace ptzba {
+#pragma clang fp contract(off)
+__global__ __launch_bounds__(256) void k_min_eig(int w, int h, const uint8_t* __restrict__ img, float scale,
+                                                 float* __restrict__ eig) {
+  const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+  if (x >= w || y >= h) return;
+  float sa = 0.f, sb = 0.f, sc = 0.f;
+  for (int by = -1; by <= 1; ++by)
+    for (int bx = -1; bx <= 1; ++bx) {
+      const int cx = refl101(x + bx, w), cy = refl101(y + by, h);  // the product image is reflected here
+      int gx = 0, gy = 0;
+      for (int j = -1; j <= 1; ++j) {
+        const int wj = j == 0 ? 2 : 1;
+        const int yy = refl101(cy + j, h), xx = refl101(cx + j, w);
+        gx += wj * ((int)img[(int64_t)yy * w + refl101(cx + 1, w)] - (int)img[(int64_t)yy * w + refl101(cx - 1, w)]);
+        gy += wj * ((int)img[(int64_t)refl101(cy + 1, h) * w + xx] - (int)img[(int64_t)refl101(cy - 1, h) * w + xx]);
+      }
+      const float dx = (float)gx * scale, dy = (float)gy * scale;
+      sa = sa + dx * dx;
+      sb = sb + dx * dy;
+      sc = sc + dy * dy;
+    }
+  const float a = sa * 0.5f, b = sb, c = sc * 0.5f;
+  const float d = (a - c) * (a - c) + b * b;
+  eig[(int64_t)y * w + x] = (a + c) - sqrtf(d);
+}
+#pragma clang fp contract(on)
+__global__ __launch_bounds__(256) void k_local_max3(int w, int h, const float* __restrict__ eig, uint8_t* __restrict__ flag) {
+  const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+  if (x >= w || y >= h) return;
+  uint8_t f = 0;
+  if (x >= 1 && y >= 1 && x < w - 1 && y < h - 1) {
+    const float v = eig[(int64_t)y * w + x];
+    bool mx = v > 0.f;
+    for (int dy = -1; dy <= 1 && mx; ++dy)
+      for (int dx = -1; dx <= 1; ++dx)
+        if (eig[(int64_t)(y + dy) * w + x + dx] > v) mx = false;
+    f = mx ? 1 : 0;
+  }
+  flag[(int64_t)y * w + x] = f;
+}
+}  // namespace ptzba
+
+int ptz_corner_min_eig(int device, int32_t width, int32_t height, const uint8_t* img, float* eig_out, uint8_t* locmax_out) {
+  using namespace ptzba;
+  if (width < 1 || height < 1 || !img || !eig_out) return fail("bad image / output");
+  if (select_device(device)) return -1;
+  const size_t np = (size_t)width * height;
+  struct EigWork {
+    DBuf u8, eig, flag;
+  };
+  auto guard = device_work_lock(device);
+  EigWork& Wk = work_for<EigWork>(device);
+  if (Wk.u8.reserve(np) || Wk.eig.reserve(np * 4) || Wk.flag.reserve(np)) return -1;
+  HIPCHK(hipMemcpy(Wk.u8.p, img, np, hipMemcpyHostToDevice));
+  const dim3 grid((unsigned)((width + 15) / 16), (unsigned)((height + 15) / 16));
+  const float scale = (float)(1.0 / (4.0 * 3.0 * 255.0));
+  hipLaunchKernelGGL(k_min_eig, grid, dim3(256), 0, nullptr, width, height, Wk.u8.as<uint8_t>(), scale, Wk.eig.as<float>());
+  if (locmax_out)
+    hipLaunchKernelGGL(k_local_max3, grid, dim3(256), 0, nullptr, width, height, Wk.eig.as<float>(), Wk.flag.as<uint8_t>());
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(eig_out, Wk.eig.p, np * 4, hipMemcpyDeviceToHost));
+  if (locmax_out) HIPCHK(hipMemcpy(locmax_out, Wk.flag.p, np, hipMemcpyDeviceToHost));
+  return 0;
+}

@@ -180,6 +180,73 @@ def optical_flow_matching(img, next_img, points, ssd_threshold=20):
     return matched_index, np.array([nxt[i] for i in matched_index])
 
 
+def compute_homography(keypiont1, descriptor1, keypoint2, descriptor2):
+    """image_process.py:313-349 on the GPU: kNN-2 L2 matching (ptz_match_knn2), the 0.7 ratio test, then
+    the RANSAC homography (1 px).  Returns H [3, 3]; below 9 ratio-test survivors the reference's
+    (None, [], None, []) with its warning."""
+    import ptzba
+    d1 = np.asarray(descriptor1, dtype=np.float32)
+    d2 = np.asarray(descriptor2, dtype=np.float32)
+    idx, dist = ptzba.match_knn2(d1, d2)
+    good = np.flatnonzero(dist[:, 0] < 0.7 * dist[:, 1]) if len(d2) >= 2 else np.zeros(0, np.int64)
+    if len(good) <= 8:
+        print('warning: match sift features failed, not enough matching')
+        return None, [], None, []
+    pts1 = np.array([keypiont1[i].pt for i in good], np.float64).reshape(-1, 2)
+    pts2 = np.array([keypoint2[j].pt for j in idx[good, 0]], np.float64).reshape(-1, 2)
+    _, H = homography_ransac(pts1, pts2, 1.0, return_matrix=True)
+    return H
+
+
+def detect_harris_corner_grid(gray_img, row, column):
+    """image_process.py:352-390: per cell of a row x column grid, cv.goodFeaturesToTrack(gray, maxCorners=20,
+    qualityLevel=0.2, minDistance=10, mask=cell) -- Shi-Tomasi corners.  The response map and its 3x3 local
+    maxima come from the GPU (ptz_corner_min_eig); per cell (the last row / column take the remainder): the
+    threshold 0.2 x the cell's maximum response, candidates ordered by response (ties: later pixel first, as
+    OpenCV's pointer order), greedily kept when no kept corner lies within 10 px, at most 20.  Returns
+    float32 [n, 2] (x, y), cells in row-major order."""
+    import ptzba
+    g = _grey_u8(gray_img)
+    eig, locmax = ptzba.corner_min_eig(g)
+    return _corner_grid_select(eig, locmax, row, column)
+
+
+def _corner_grid_select(eig, locmax, row, column, max_corners=20, quality=0.2, min_distance=10.0):
+    h, w = eig.shape
+    gh, gw = h // row, w // column
+    out = []
+    for i in range(row):
+        for j in range(column):
+            y1, x1 = i * gh, j * gw
+            y2 = h if i == row - 1 else y1 + gh
+            x2 = w if j == column - 1 else x1 + gw
+            cell = eig[y1:y2, x1:x2]
+            if cell.size == 0:
+                continue
+            thr = np.float32(cell.max()) * np.float32(quality)
+            ys, xs = np.nonzero(locmax[y1:y2, x1:x2] & (cell > thr))
+            if len(ys) == 0:
+                continue
+            ys, xs = ys + y1, xs + x1
+            v = eig[ys, xs]
+            order = np.lexsort((-(ys.astype(np.int64) * w + xs), -v))  # response desc, then address desc
+            kept = []
+            for k in order:
+                x, y = float(xs[k]), float(ys[k])
+                if all((x - kx) ** 2 + (y - ky) ** 2 >= min_distance * min_distance for kx, ky in kept):
+                    kept.append((x, y))
+                    if len(kept) == max_corners:
+                        break
+            out.extend(kept)
+    return np.asarray(out, np.float32).reshape(-1, 2)
+
+
+def good_homography(h):
+    """image_process.py:445-461: the reference marks this check as not working and asserts on entry; kept
+    so callers behave identically (AssertionError)."""
+    assert False, "good_homography: disabled in the reference (image_process.py:447)"
+
+
 def keypoints_masking(kp, mask):
     """image_process.py:158-175: indices of keypoints whose (int x, int y) pixel has mask == 1."""
     if isinstance(kp, np.ndarray):

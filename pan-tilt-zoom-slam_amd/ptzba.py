@@ -139,6 +139,7 @@ def lib():
         "ptz_keyframe_features": ([I32, I64, V, V, V, V, V, V, V, V], I),
         "ptz_pack_records": ([I32, I64, V, V, V, V, V, V, V, I64, V, V, V, V], I),
         "ptz_refine_poses": ([I, I32, V, I64, V, V, D, D, V, V, POINTER(ptz_refine_opts), V, V, V], I),
+        "ptz_corner_min_eig": ([I, I32, I32, V, V, V], I),
         "ptzba_partition_landmarks": ([I32, I32, I64, V, V, I32, I32, V, POINTER(c_int32), V], I),
         "ptzba_set_exchange_hook": ([V, EXCHANGE_FN, V], I),
         "ptzba_comm_unique_id": ([V], I),
@@ -181,7 +182,7 @@ EXPORTED_SYMBOLS = [
     "ptzekf_remove_rays", "ptzekf_add_rays", "ptzekf_project_visible", "ptzekf_update",
     "ptzba_partition_landmarks", "ptzba_set_exchange_hook", "ptzba_comm_unique_id", "ptzba_comm_new",
     "ptzba_comm_delete", "ptzba_comm_split", "ptzba_comm_info", "ptzba_comm_allreduce", "ptzba_attach_comm",
-    "ptzba_dist_info", "ptzba_owned_frames",
+    "ptzba_dist_info", "ptzba_owned_frames", "ptz_corner_min_eig",
 ]
 
 
@@ -316,6 +317,19 @@ def lk_track(img0, img1, points, win=31, levels=4, max_iter=30, eps=0.01, min_ei
                                   _ptr(b), n, _ptr(pts), int(levels), int(win), int(max_iter), float(eps),
                                   float(min_eig), _ptr(out), _ptr(st), _ptr(err)), "ptz_lk_track")
     return out, st, err
+
+
+def corner_min_eig(img, device=None):
+    """cv.cornerMinEigenVal(img, blockSize=3, ksize=3) on the GPU (ptz_corner_min_eig): 8-bit grey [h, w].
+    Returns (eig [h, w] float32, local-max flags [h, w] bool: goodFeaturesToTrack's candidates)."""
+    a = np.ascontiguousarray(img, dtype=np.uint8)
+    if a.ndim != 2:
+        raise ValueError("image must be 2-D 8-bit grey")
+    eig = np.empty(a.shape, np.float32)
+    flag = np.empty(a.shape, np.uint8)
+    _check(lib().ptz_corner_min_eig(default_device() if device is None else device, a.shape[1], a.shape[0], _ptr(a),
+                                    _ptr(eig), _ptr(flag)), "ptz_corner_min_eig")
+    return eig, flag.astype(bool)
 
 
 def match_hamming_cross(des1, des2, device=None):

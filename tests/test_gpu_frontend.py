@@ -258,3 +258,47 @@ def test_match_orb_features_gpu(gpu_available):
         pts1, i1, pts2, i2 = fn(k1, d1, k2, d2)
         assert len(i1) >= 280 and all(truth.get(a) == b for a, b in zip(i1, i2))
         np.testing.assert_allclose(pts1, x1[i1])
+
+
+@pytest.mark.parametrize("seed,w,h", [(11, 320, 240), (12, 257, 131), (13, 1280, 720)])
+def test_corner_min_eig_matches_oracle(gpu_available, seed, w, h):
+    """ptz_corner_min_eig (cv.cornerMinEigenVal, blockSize 3, ksize 3 -- goodFeaturesToTrack's measure) equals the
+    oracle's float32 restatement bit for bit, and so do the 3x3 local-maximum candidates (parity vs cv2 unpinned:
+    cv2 cannot run here)."""
+    import ptzba
+    from oracle import ptz_oracle as orc
+    I, _, _ = frontend_data.textured_pair(seed=seed, width=w, height=h)
+    eig, loc = ptzba.corner_min_eig(I)
+    reig, rloc = orc.corner_min_eig(I)
+    assert eig.shape == (h, w) and eig.dtype == np.float32
+    np.testing.assert_array_equal(eig, reig)
+    np.testing.assert_array_equal(loc, rloc)
+    assert loc.sum() > 0 and not loc[0].any() and not loc[:, -1].any()
+
+
+def test_detect_harris_corner_grid(gpu_available):
+    """image_process.detect_harris_corner_grid (image_process.py:352-390): per grid cell at most 20 corners, each
+    inside its cell, pairwise >= 10 px apart within the cell, responses above 0.2 x the cell maximum and in
+    decreasing order; a flat image gives none.  compute_homography / good_homography keep the reference's
+    behaviour."""
+    import image_process
+    from oracle import ptz_oracle as orc
+    I, _, _ = frontend_data.textured_pair(seed=14, width=640, height=360)
+    pts = image_process.detect_harris_corner_grid(I, 3, 4)
+    assert pts.dtype == np.float32 and pts.ndim == 2 and pts.shape[1] == 2 and len(pts) > 12
+    eig, _ = orc.corner_min_eig(I)
+    gh, gw = 360 // 3, 640 // 4
+    cells = (pts[:, 1] // gh).astype(int) * 4 + (pts[:, 0] // gw).astype(int)
+    assert np.all(np.diff(cells) >= 0)  # row-major cells
+    for c in np.unique(cells):
+        p = pts[cells == c]
+        assert len(p) <= 20
+        i, j = divmod(int(c), 4)
+        thr = eig[i * gh:(i + 1) * gh, j * gw:(j + 1) * gw].max() * np.float32(0.2)
+        v = eig[p[:, 1].astype(int), p[:, 0].astype(int)]
+        assert np.all(v > thr) and np.all(np.diff(v) <= 0)
+        d = np.linalg.norm(p[:, None] - p[None], axis=2) + np.eye(len(p)) * 1e9
+        assert d.min() >= 10.0
+    assert len(image_process.detect_harris_corner_grid(np.full((120, 160), 77, np.uint8), 2, 2)) == 0
+    with pytest.raises(AssertionError):
+        image_process.good_homography(np.eye(3))
