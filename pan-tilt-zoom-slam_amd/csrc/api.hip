@@ -115,6 +115,13 @@ struct ptzba_ctx {
   int elem() const { return precision == PTZBA_FP32 ? 4 : 8; }
   double* locp() const { return scal.as<double>() + 8; }
   bool has_exchange() const { return hook != nullptr || comm != nullptr; }
+  bool ext_exchange = false;   // the caller ran its own exchange protocol (ptzba_exchange / _packed) once
+  bool f1_covered = false;     // every 32-frame block has a chunk-0 Schur tile (all diagonals written by K2)
+  // single-GPU builds fold k_chol_prepare into the build (FusedPrep, ptzba_kernels.h)
+  bool fused_prep() const {
+    static const bool off = getenv("PTZBA_NO_FUSED_PREP") != nullptr;  // A/B knob
+    return !off && !dist_mode && !has_exchange() && !ext_exchange && f1_covered;
+  }
   double* S() const { return sys.as<double>(); }
   double* bvec() const { return sys.as<double>() + ld * ld; }
   double* gpose() const { return sys.as<double>() + ld * ld + ld; }
@@ -854,6 +861,14 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     }
     h->n_s2_groups = (int)(s2_groups.size() / 4);
     h->n_s2_items = (int)(s2_items.size() / 4);
+    {
+      std::vector<uint8_t> cov((n_pose + SCHUR_F1) / SCHUR_F1 + 1, 0);
+      for (size_t g = 0; g < s2_groups.size(); g += 4)
+        if (s2_groups[g + 1] == 0) cov[(s2_groups[g] - o.n_fixed) / SCHUR_F1] = 1;
+      h->f1_covered = true;
+      for (int f1b = o.n_fixed; f1b < n_pose; f1b += SCHUR_F1)
+        if (!cov[(f1b - o.n_fixed) / SCHUR_F1]) h->f1_covered = false;
+    }
   }
   // ---- landmark work order: heaviest (most records) first
   std::vector<int32_t> lm_order;
@@ -1276,10 +1291,15 @@ int ptzba_linearize(ptzba_handle h) {
 static int build_impl(ptzba_ctx* h, double lambda, const double* lam_dev, const int* skip_if = nullptr,
                       const int* sel = nullptr) {
   const int c = sel ? 0 : h->cur;
+  FusedPrep fp{};
+  // fused only in the device-driven LM (sel != nullptr): the host-step API (ptzba_build_reduced) leaves the
+  // system raw for callers that sum it between build and solve (include/ptzba.h, the round-2 protocol)
+  if (sel && h->fused_prep())
+    fp = FusedPrep{h->row_pad.as<uint8_t>(), h->n_aug, h->info.as<int>(), h->D_pose.as<double>(), lambda, lam_dev};
   launch_build_prologue(h->S(), h->ld, h->ztiles.as<int2>(), h->n_ztiles, h->bvec(), 3 * h->ld,
                         h->lm_out[c].as<double>(), h->lm_seg_begin.as<int32_t>(), h->D_ray.as<double>(),
                         h->lm_aux.as<double>(), h->n_lm, lambda, lam_dev, skip_if, h->st, h->lm_out[1].as<double>(),
-                        sel);
+                        sel, fp);
   SchurArgs a;
   a.items = h->s2_items.as<int4>();
   a.groups = h->s2_groups.as<int4>();
@@ -1301,6 +1321,7 @@ static int build_impl(ptzba_ctx* h, double lambda, const double* lam_dev, const 
   a.ug_slot1 = h->ug_slot[1].p;
   a.w_slot1 = h->w_slot[1].p;
   a.sel = sel;
+  a.prep = fp;
   a.item_group = h->s2_item_group.as<int32_t>();
   a.tile_cnt = h->s2_tile_cnt.as<unsigned>();  // used only by the folded-reduce A/B build (MF_FOLD_REDUCE)
   tm_begin(h, TM_SCHUR);
@@ -1363,9 +1384,10 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
                     h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>(),
                     h->phase2_level);
   } else {
-    launch_chol_prepare_damped(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(),
-                               h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
-                               h->lambda, lam_dev, h->st);
+    if (!(sel && h->fused_prep()))  // device-driven single-GPU builds wrote the augmented row, padding, damping
+      launch_chol_prepare_damped(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(),
+                                 h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
+                                 h->lambda, lam_dev, h->st);
     launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
                     h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>());
   }
@@ -1611,6 +1633,7 @@ int ptzba_accept(ptzba_handle h, int accept) {
 
 int ptzba_exchange(ptzba_handle h, void** sys_ptr, int64_t* sys_count, void** scal_ptr) {
   if (!h || !h->have_problem) return fail("no problem set");
+  if (sys_ptr) h->ext_exchange = true;  // the caller may sum the system between build and solve: prepare after it
   if (sys_ptr) *sys_ptr = h->sys.p;
   if (sys_count) *sys_count = h->sys_count();
   if (scal_ptr) *scal_ptr = h->scal.p;
@@ -1619,6 +1642,7 @@ int ptzba_exchange(ptzba_handle h, void** sys_ptr, int64_t* sys_count, void** sc
 
 int ptzba_exchange_packed(ptzba_handle h, void** buf, int64_t* count) {
   if (!h || !h->have_problem) return fail("no problem set");
+  if (buf && !h->has_exchange()) h->ext_exchange = true;  // the caller's own protocol (see ptzba_exchange)
   const int64_t n = (int64_t)h->n_xtiles * CHOL_NB * CHOL_NB + 3 * h->ld;
   if (!h->xbuf.p && h->xbuf.alloc((size_t)n * 8)) return -1;
   if (buf) *buf = h->xbuf.p;

@@ -553,17 +553,28 @@ __global__ __launch_bounds__(256) void k_build_prologue(double* __restrict__ S, 
                                                         double* __restrict__ D_ray, double* __restrict__ lm_aux, int n_lm,
                                                         double lambda_arg, const double* __restrict__ lam_dev,
                                                         const int* __restrict__ skip_if,
-                                                        const double* __restrict__ lm_out1, const int* __restrict__ sel) {
+                                                        const double* __restrict__ lm_out1, const int* __restrict__ sel,
+                                                        FusedPrep fp) {
   const int b = blockIdx.x;
   if (b < n_tiles) {
     const int2 tij = zt[b];
     double* T = S + (int64_t)tij.x * CHOL_NB * ld + (int64_t)tij.y * CHOL_NB;
     for (int e = threadIdx.x; e < CHOL_NB * CHOL_NB / 2; e += blockDim.x)
       *reinterpret_cast<double2*>(T + (int64_t)(e >> 4) * ld + 2 * (e & 15)) = make_double2(0.0, 0.0);
+    if (fp.pad && tij.x == tij.y && threadIdx.x < CHOL_NB) {
+      // single-GPU build: the constant diagonal entries of k_chol_prepare (identity on padding rows, the
+      // augmented diagonal, identity below it), written with the zeroing (same wave, after its stores)
+      const int64_t r = (int64_t)tij.x * CHOL_NB + threadIdx.x;
+      double dv = 0.0;
+      if (r < fp.n_aug) dv = fp.pad[r] ? 1.0 : 0.0;
+      else dv = r == fp.n_aug ? 1e300 : 1.0;
+      if (dv != 0.0) S[r * ld + r] = dv;
+    }
     return;
   }
   if (b == n_tiles) {
     for (int64_t e = threadIdx.x; e < n_vec; e += blockDim.x) vec[e] = 0.0;
+    if (fp.pad && threadIdx.x == 0) fp.info[0] = 0;
     return;
   }
   if (skip_if && *skip_if) return;
@@ -596,10 +607,10 @@ __global__ __launch_bounds__(256) void k_build_prologue(double* __restrict__ S, 
 void launch_build_prologue(double* S, int64_t ld, const int2* zt, int n_tiles, double* vec, int64_t n_vec,
                            const double* lm_out, const int32_t* lm_seg_begin, double* D_ray, double* lm_aux, int n_lm,
                            double lambda, const double* lam_dev, const int* skip_if, hipStream_t st,
-                           const double* lm_out1, const int* sel) {
+                           const double* lm_out1, const int* sel, const FusedPrep& fp) {
   const unsigned nb = (unsigned)(n_tiles + 1 + (n_lm + 255) / 256);
   hipLaunchKernelGGL(k_build_prologue, dim3(nb), dim3(256), 0, st, S, ld, zt, n_tiles, vec, n_vec, lm_out, lm_seg_begin,
-                     D_ray, lm_aux, n_lm, lambda, lam_dev, skip_if, lm_out1, sel);
+                     D_ray, lm_aux, n_lm, lambda, lam_dev, skip_if, lm_out1, sel, fp);
 }
 
 // (pose damping of the exchanged reduced system: k_chol_prepare, chol_kernels.hip)

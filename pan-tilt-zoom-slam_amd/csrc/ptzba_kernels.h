@@ -39,6 +39,20 @@ struct LinArgs {
 // splits of a tile's landmark list.  Static structure built once by ptzba_set_problem.
 constexpr int SCHUR_F1 = 32;
 constexpr int SCHUR_LMAX = 512;  // landmarks per work item (split size cap)
+// Single-GPU builds fold k_chol_prepare into the build: the prologue writes the constant diagonal entries
+// (padding identity, augmented diagonal, identity below it) and resets info; k_schur_reduce writes the
+// augmented row b^T and the pose damping (D_pose = max(D_pose, diag U); S_ff += lambda D_pose), the same
+// values in the same order as the prepare launch.  pad == nullptr: not fused (multi-rank exchanges need the
+// prepare after the sum).
+struct FusedPrep {
+  const uint8_t* pad;  // [n_aug] padding rows
+  int64_t n_aug;
+  int* info;
+  double* D_pose;      // [3 n_pose]
+  double lambda;
+  const double* lam_dev;
+};
+
 struct SchurArgs {
   const int4* items;              // [n_items] {f1b, chunk, list begin, list end}
   const int4* groups;             // [n_groups] per tile {f1b, chunk, first item, end item}
@@ -62,6 +76,7 @@ struct SchurArgs {
   const int* sel;
   const int32_t* item_group;      // [n_items] tile (group) of each item (matrix-core K2: folded reduce)
   unsigned* tile_cnt;             // [n_groups] finished splits per tile (zero between launches)
+  FusedPrep prep;                 // single-GPU: the prepare's augmented row and damping (pad != nullptr)
 };
 
 struct BacksubArgs {
@@ -124,7 +139,7 @@ void launch_reduce_cols(const double* src, int64_t n, int stride, int nk, int ma
 void launch_build_prologue(double* S, int64_t ld, const int2* zt, int n_tiles, double* vec, int64_t n_vec,
                            const double* lm_out, const int32_t* lm_seg_begin, double* D_ray, double* lm_aux, int n_lm,
                            double lambda, const double* lam_dev, const int* skip_if, hipStream_t st,
-                           const double* lm_out1 = nullptr, const int* sel = nullptr);
+                           const double* lm_out1 = nullptr, const int* sel = nullptr, const FusedPrep& fp = FusedPrep{});
 // trial state (ray back-substitution + pose trial + the trial's frame / ray tables) in one launch
 // fmask (part-owned solve, else nullptr): per frame bit 0 = this rank's solve updates the pose, bit 1 = the
 // frame's terms count in this rank's pose partials (each frame is counted by exactly one rank)

@@ -732,7 +732,22 @@ __device__ __forceinline__ void schur_reduce_elem(const SchurArgs& a, const int4
   for (; it < g.w; ++it) v += (double)part_load<real, AGENT>(p + (int64_t)it * NE);
   if (f2 == f1) {  // chunk 0: U of the frame, summed over the tile's splits
     const int ui = q <= r ? (q == 0 ? r : (q == 1 ? 2 + r : 5)) : (r == 0 ? q : (r == 1 ? 2 + q : 5));
-    for (int it2 = g.z; it2 < g.w; ++it2) v += part_load<double, AGENT>(a.part_diag + ((int64_t)it2 * SF + i) * 12 + ui);
+    double du = 0;  // diag U as the chunk-0 vector block sums it (fresh, item order): the damping's scale
+    for (int it2 = g.z; it2 < g.w; ++it2) {
+      const double uu = part_load<double, AGENT>(a.part_diag + ((int64_t)it2 * SF + i) * 12 + ui);
+      v += uu;
+      du += uu;
+    }
+    if (a.prep.pad && q == r) {  // fused prepare: Marquardt damping of the pose row (k_chol_prepare's rule)
+      const double lambda = a.prep.lam_dev ? *a.prep.lam_dev : a.prep.lambda;
+      double* D = a.prep.D_pose + 3 * (int64_t)f1 + q;
+      const double d = fmax(*D, fmax(du, 1e-12));
+      *D = d;
+      const int64_t row = a.frame_pos[f1] + q;
+      a.S[row * a.ld + row] = v;
+      a.S[row * a.ld + row] += lambda * d;
+      return;
+    }
   }
   const int64_t ld = a.ld, col0 = a.frame_pos[f1], pf2 = a.frame_pos[f2];
   if (pf2 >= col0) a.S[(pf2 + r) * ld + col0 + q] = v;
@@ -748,9 +763,11 @@ __device__ __forceinline__ void schur_reduce_vec(const SchurArgs& a, const int4 
   for (int it2 = g.z; it2 < g.w; ++it2)
     for (int k = 0; k < 12; ++k) d[k] += part_load<double, AGENT>(a.part_diag + ((int64_t)it2 * SF + i2) * 12 + k);
   const int c0 = a.frame_pos[f];
-  a.b[c0 + q2] = -d[6 + q2] + d[9 + q2];
+  const double bv = -d[6 + q2] + d[9 + q2];
+  a.b[c0 + q2] = bv;
   a.g_pose[c0 + q2] = d[6 + q2];
   a.dU[c0 + q2] = d[q2 == 0 ? 0 : (q2 == 1 ? 3 : 5)];
+  if (a.prep.pad) a.S[a.prep.n_aug * a.ld + c0 + q2] = bv;  // fused prepare: the augmented row b^T
 }
 
 // tile reduction: thread = one element of a tile (grid: tile x 72 blocks of 256); fixed-order sum of the
@@ -758,53 +775,10 @@ __device__ __forceinline__ void schur_reduce_vec(const SchurArgs& a, const int4 
 // precedes f1); chunk-0 tiles also write b | g_pose | diag U of their frames.
 template <typename real>
 __global__ __launch_bounds__(256) void k_schur_reduce(SchurArgs a) {
-  constexpr int NE = SF * 9 * WAVE;
   if (a.skip_if && *a.skip_if) return;
   const int4 g = a.groups[blockIdx.y];  // {f1b, chunk, first item, end item}
-  const int f1b = g.x, chunk = g.y;
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  const int ln = e & 63, ik = e >> 6, i = ik / 9, k = ik - 9 * i, q = k / 3, r = k - 3 * q;
-  const int f1 = f1b + i, f2 = f1b + WAVE * chunk + ln;
-  if (f1 < a.n_pose && f2 >= f1 && f2 <= a.frame_win_hi[f1]) {
-    const real* p = (const real*)a.part + e;
-    double v = 0;
-    int it = g.z;
-#if SR_UNROLL == 8
-    for (; it + 8 <= g.w; it += 8) {  // eight split partials in flight per thread
-      real pv[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) pv[u] = p[(int64_t)(it + u) * NE];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v += (double)pv[u];
-    }
-#endif
-    for (; it + 4 <= g.w; it += 4) {
-      const double p0 = p[(int64_t)it * NE], p1 = p[(int64_t)(it + 1) * NE];
-      const double p2 = p[(int64_t)(it + 2) * NE], p3 = p[(int64_t)(it + 3) * NE];
-      v += p0; v += p1; v += p2; v += p3;
-    }
-    for (; it < g.w; ++it) v += (double)p[(int64_t)it * NE];
-    if (f2 == f1) {  // chunk 0: U of the frame, summed over the tile's splits
-      const int ui = q <= r ? (q == 0 ? r : (q == 1 ? 2 + r : 5)) : (r == 0 ? q : (r == 1 ? 2 + q : 5));
-      for (int it2 = g.z; it2 < g.w; ++it2) v += a.part_diag[((int64_t)it2 * SF + i) * 12 + ui];
-    }
-    const int64_t ld = a.ld, col0 = a.frame_pos[f1], pf2 = a.frame_pos[f2];
-    if (pf2 >= col0) a.S[(pf2 + r) * ld + col0 + q] = v;
-    else a.S[(col0 + q) * ld + pf2 + r] = v;
-  }
-  if (chunk == 0 && blockIdx.x == 0 && threadIdx.x < SF * 3) {
-    const int i2 = threadIdx.x / 3, q2 = threadIdx.x - 3 * i2, f = f1b + i2;
-    if (f < a.n_pose) {
-      double d[12];
-      for (int k = 0; k < 12; ++k) d[k] = 0;
-      for (int it2 = g.z; it2 < g.w; ++it2)
-        for (int k = 0; k < 12; ++k) d[k] += a.part_diag[((int64_t)it2 * SF + i2) * 12 + k];
-      const int c0 = a.frame_pos[f];
-      a.b[c0 + q2] = -d[6 + q2] + d[9 + q2];
-      a.g_pose[c0 + q2] = d[6 + q2];
-      a.dU[c0 + q2] = d[q2 == 0 ? 0 : (q2 == 1 ? 3 : 5)];
-    }
-  }
+  schur_reduce_elem<real, false>(a, g, blockIdx.x * 256 + threadIdx.x);
+  if (g.y == 0 && blockIdx.x == 0 && threadIdx.x < SF * 3) schur_reduce_vec<false>(a, g, threadIdx.x);
 }
 
 template <typename real>
