@@ -78,7 +78,9 @@ struct ptzba_ctx {
   DBuf frame_pos, row_pad, bs_chain_off, bs_chain_cols, bs_upd_off, bs_upd_tiles, bs_la_tasks;
   int bs_nupd = 0, bs_npos = 0, bs_ntasks = 0;
   DBuf bs_lo_off, bs_lo_tiles;  // left-looking back substitution lists (large systems)
-  bool bs_ll = false;
+  DBuf bsb_tasks, bsb_r;  // blocked back substitution (large systems): plan + r scratch [ld]
+  std::vector<int> bsb_step_off;
+  bool bs_ll = false, bs_blk = false;
   DBuf xtiles, xbuf;  // packed exchange: tile list, buffer
   int n_xtiles = 0;
   DBuf ztiles;  // tiles zeroed before each build (the rest of the system region stays zero)
@@ -349,7 +351,92 @@ struct CholPlan {
   std::vector<int32_t> ztiles;  // (ti, tj) lower tiles of the factor's pattern (incl. fill): zeroed per build
   std::vector<int32_t> tinv_tail;  // diagonal tiles inverted after the last level (the others: type-2 tasks)
   int n_levels = 0;
+  // blocked back substitution (large systems): tasks of 3 int4 (block columns | {p, intra-block coupling
+  // bits, first-touch bits, 0} | {target column, flags, 0, 0}) and the task offset of each step (one launch
+  // per step); empty when no valid schedule exists
+  std::vector<int32_t> bsb_tasks;
+  std::vector<int> bsb_step_off;
 };
+
+// Steps of the blocked right-looking back substitution (k_chol_backsolve_blk).  The chains' common prefix
+// (the separator C of a nested order) is cut into blocks of BSB_P consecutive positions solved one block
+// per step; the chains' remainders (A and B) then advance in lockstep, one block of each per step.  A step
+// solves its blocks (every workgroup redundantly) and applies their contribution to every later column t
+// coupled to them (one workgroup per (block, t): a plain read-modify-write of r_t, as no two tasks of a
+// step share a target and steps are stream-ordered).  First-touch flags make a column's first read take
+// the forward-substitution result y (the factor's augmented row) instead of r, so r needs no init launch.
+static void make_bs_steps(const std::vector<std::vector<uint8_t>>& nz, int Tx, CholPlan& P) {
+  P.bsb_tasks.clear();
+  P.bsb_step_off.assign(1, 0);
+  const int T = (int)nz.size(), nch = (int)P.chain_off.size() - 1;
+  if (nch < 1) return;
+  std::vector<std::vector<int>> ch(nch);
+  for (int c = 0; c < nch; ++c) ch[c].assign(P.chain_cols.begin() + P.chain_off[c], P.chain_cols.begin() + P.chain_off[c + 1]);
+  size_t pre = 0;
+  while (true) {
+    bool same = pre < ch[0].size();
+    for (int c = 1; c < nch && same; ++c) same = pre < ch[c].size() && ch[c][pre] == ch[0][pre];
+    if (!same) break;
+    ++pre;
+  }
+  std::vector<std::vector<std::vector<int>>> phases;  // phase -> sequences advancing in lockstep
+  phases.push_back({std::vector<int>(ch[0].begin(), ch[0].begin() + pre)});
+  phases.emplace_back();
+  for (int c = 0; c < nch; ++c)
+    if (ch[c].size() > pre) phases[1].emplace_back(ch[c].begin() + pre, ch[c].end());
+  std::vector<uint8_t> in_any(T, 0), solved(T, 0), touched(T, 0);
+  for (int kt : P.chain_cols) in_any[kt] = 1;
+  auto fail = [&]() {
+    P.bsb_tasks.clear();
+    P.bsb_step_off.assign(1, 0);
+  };
+  for (const auto& seqs : phases) {
+    size_t len = 0;
+    for (const auto& q : seqs) len = std::max(len, q.size());
+    for (size_t q0 = 0; q0 < len; q0 += BSB_P) {
+      std::vector<uint8_t> used(T, 0);  // block columns and targets of this step
+      std::vector<int> step_targets;
+      for (const auto& q : seqs) {
+        if (q0 >= q.size()) continue;
+        const int p = (int)std::min<size_t>(BSB_P, q.size() - q0);
+        int cols[BSB_P] = {-1, -1, -1, -1}, imask = 0, ftouch = 0;
+        for (int k = 0; k < p; ++k) {
+          cols[k] = q[q0 + k];
+          if (used[cols[k]] || solved[cols[k]]) return fail();
+          used[cols[k]] = 1;
+          if (!touched[cols[k]]) ftouch |= 1 << k;
+          for (int j = 0; j < k; ++j) {
+            if (cols[j] <= cols[k]) return fail();  // descending within a block
+            if (nz[cols[j]][cols[k]]) imask |= 1 << (j * 4 + k);
+          }
+        }
+        auto push_task = [&](int t, int flags) {
+          P.bsb_tasks.insert(P.bsb_tasks.end(), {cols[0], cols[1], cols[2], cols[3], p, imask, ftouch, 0, t, flags, 0, 0});
+        };
+        std::vector<int> tmask(T, 0);
+        for (int k = 0; k < p; ++k)
+          for (int t = 0; t < cols[k]; ++t)
+            if (in_any[t] && nz[cols[k]][t] && !(t == cols[0] || t == cols[1] || t == cols[2] || t == cols[3]))
+              tmask[t] |= 1 << k;
+        bool first = true;
+        for (int t = 0; t < T; ++t) {
+          if (!tmask[t]) continue;
+          if (used[t] || solved[t]) return fail();
+          used[t] = 1;
+          step_targets.push_back(t);
+          push_task(t, tmask[t] | (first ? 0x100 : 0) | (touched[t] ? 0 : 0x200));
+          first = false;
+        }
+        if (first) push_task(-1, 0x100);
+        for (int k = 0; k < p; ++k) solved[cols[k]] = touched[cols[k]] = 1;
+      }
+      for (int t : step_targets) touched[t] = 1;
+      P.bsb_step_off.push_back((int)(P.bsb_tasks.size() / 12));
+    }
+  }
+  for (int kt = 0; kt < Tx; ++kt)
+    if (in_any[kt] && !solved[kt]) return fail();
+}
 
 // Tile structure (coupled frame pairs + the dense augmented row + symbolic fill), elimination levels
 // (at most two tile columns per level), tasks per level and back-substitution chains.
@@ -512,6 +599,7 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
   P.la_tasks = la;
   P.la_tasks.insert(P.la_tasks.end(), toff.begin(), toff.end());
   P.la_tasks.insert(P.la_tasks.end(), tasks.begin(), tasks.end());
+  make_bs_steps(nz, Tx, P);
   return true;
 }
 
@@ -679,6 +767,7 @@ static bool make_plan_part(const SysOrder& o, int part, int n_pose, int nf, cons
   P.la_tasks = la;
   P.la_tasks.insert(P.la_tasks.end(), toff.begin(), toff.end());
   P.la_tasks.insert(P.la_tasks.end(), tasks.begin(), tasks.end());
+  make_bs_steps(nz, Tx, P);
   return true;
 }
 
@@ -1056,7 +1145,21 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   // (lookahead form: + 48 KiB ring of M / L blocks); larger systems take the left-looking form, whose lists
   // stay in global memory
   h->bs_ll = h->ld * 8 + (std::max(h->bs_npos + 1 + h->bs_nupd, 2 * h->bs_npos + h->bs_ntasks)) * 4 > 100 * 1024;
-  if (const char* e = getenv("PTZBA_BACKSOLVE")) h->bs_ll = h->bs_ll || std::string(e) == "ll";  // testing knob
+  // large systems take the blocked right-looking form (many CUs per step) when the plan has a valid schedule;
+  // testing knobs: PTZBA_BACKSOLVE=ll (left-looking, one CU per chain) / =blk (blocked form at any size)
+  const char* bse = getenv("PTZBA_BACKSOLVE");
+  const std::string bsk = bse ? bse : "";
+  h->bs_blk = (h->bs_ll || bsk == "blk") && bsk != "ll" && !plan.bsb_tasks.empty();
+  h->bs_ll = (h->bs_ll || bsk == "ll") && !h->bs_blk;
+  h->bsb_step_off = plan.bsb_step_off;
+  if (h->bs_blk) {
+    if (upload(h->bsb_tasks, plan.bsb_tasks, h->st) ||
+        h->bsb_r.alloc((size_t)h->ld * 8))
+      return -1;
+  } else {
+    h->bsb_tasks.release();
+    h->bsb_r.release();
+  }
   h->xbuf.release();  // allocated on first ptzba_exchange_packed
   HIPCHK(hipMemsetAsync(h->D_pose.p, 0, h->D_pose.bytes, h->st));
   HIPCHK(hipMemsetAsync(h->D_ray.p, 0, h->D_ray.bytes, h->st));
@@ -1162,7 +1265,7 @@ int ptzba_solver_info(ptzba_handle h, int64_t* info8) {
   info8[1] = h->ld;
   info8[2] = h->chol_levels;
   info8[3] = h->nested ? PTZBA_ORDER_NESTED : PTZBA_ORDER_NATURAL;
-  info8[4] = h->bs_ll ? 1 : 0;
+  info8[4] = h->bs_blk ? 2 : (h->bs_ll ? 1 : 0);
   info8[5] = h->n_slot;
   info8[6] = h->n_s2_items;
   info8[7] = h->n_ztiles;
@@ -1391,12 +1494,17 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
     launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
                     h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>());
   }
-  launch_chol_backsolve(h->S(), h->ld, h->n_aug, h->n_chain, h->bs_npos, h->bs_chain_off.as<int>(),
-                        h->bs_chain_cols.as<int>(), h->bs_upd_off.as<int>(), h->bs_upd_tiles.as<int>(), h->bs_nupd,
-                        h->bs_la_tasks.as<int>(), h->bs_ntasks,
-                        h->Ldiag.as<double>(), h->Minv.as<double>(), h->dpose.as<double>(),
-                        h->bs_ll ? h->bs_lo_off.as<int>() : nullptr, h->bs_lo_tiles.as<int>(), h->st,
-                        h->tinv_tail.as<int>(), h->n_tinv_tail);
+  if (h->bs_blk)
+    launch_chol_backsolve_blk(h->S(), h->ld, h->n_aug, h->bsb_tasks.as<int4>(), h->bsb_step_off.data(), (int)h->bsb_step_off.size() - 1, h->Ldiag.as<double>(),
+                              h->Minv.as<double>(), h->bsb_r.as<double>(), h->dpose.as<double>(), h->st,
+                              h->tinv_tail.as<int>(), h->n_tinv_tail);
+  else
+    launch_chol_backsolve(h->S(), h->ld, h->n_aug, h->n_chain, h->bs_npos, h->bs_chain_off.as<int>(),
+                          h->bs_chain_cols.as<int>(), h->bs_upd_off.as<int>(), h->bs_upd_tiles.as<int>(), h->bs_nupd,
+                          h->bs_la_tasks.as<int>(), h->bs_ntasks,
+                          h->Ldiag.as<double>(), h->Minv.as<double>(), h->dpose.as<double>(),
+                          h->bs_ll ? h->bs_lo_off.as<int>() : nullptr, h->bs_lo_tiles.as<int>(), h->st,
+                          h->tinv_tail.as<int>(), h->n_tinv_tail);
   tm_end(h, TM_CHOL);
   HIPCHK(hipGetLastError());
   tm_begin(h, TM_BACK);

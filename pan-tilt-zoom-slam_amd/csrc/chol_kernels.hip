@@ -1336,6 +1336,125 @@ __global__ __launch_bounds__(64 * BSL_WAVES) void k_chol_backsolve_ll(
   }
 }
 
+// Blocked right-looking back substitution for large systems (api.hip make_bs_steps).  The left-looking
+// form above streams the whole factor through ONE CU per chain (config 4: 224 MB of L tiles, 2.4 ms); here
+// every step is a launch of one workgroup per (block, target column t), so a step's L tiles are read by
+// ~60-120 CUs at once.  Workgroup = BSB_P waves, wave k owns block column c_k:
+//   * all of its tiles are requested up front: M_ck (= L_ck^-1, k_tile_inv), the intra-block tiles
+//     L_cj,ck (j < k), the target tile L_ck,t, r_ck (or y_ck on its first touch) and, wave 0, r_t;
+//   * the block solve runs down the waves: wave k waits for x_c0..x_c(k-1) (LDS counter, ordered
+//     hand-off as everywhere in this file), r'_ck = r_ck - sum_j L_cj,ck^T x_cj (fixed order j), x_ck =
+//     M_ck^T r'_ck, publishes x_ck; every workgroup of the step solves the block redundantly (~10 tiles
+//     from L2) instead of paying a second launch;
+//   * the target: r_t -= sum_k L_ck,t^T x_ck (fixed order k), a plain read-modify-write: no other task of
+//     the step touches t and steps are stream-ordered, so every r_t is summed in a fixed order
+//     (deterministic, no atomics).  The task flagged writer stores the block's x.
+// Lane = (column c, row half h) of a tile, 16 strided loads per tile as in the left-looking form.
+__global__ __launch_bounds__(64 * BSB_P) void k_chol_backsolve_blk(
+    const double* __restrict__ L, int64_t ld, int n, const int4* __restrict__ tasks,
+    const double* __restrict__ Ldiag, const double* __restrict__ Minv, double* __restrict__ r,
+    double* __restrict__ xout) {
+  __shared__ double xs[BSB_P][NB];  // x of the block columns
+  __shared__ double rs[BSB_P][NB];  // r' of a block column (before M^T)
+  __shared__ double ps[BSB_P][NB];  // the target's partial sums per block column
+  __shared__ int s_cnt;             // block columns published
+  const int lane = threadIdx.x & 63, k = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
+  if (threadIdx.x == 0) s_cnt = 0;
+  // task record (3 int4, independent loads): block columns | {p, intra-block bits, first-touch bits} |
+  // {target t (-1: none), flags: target bits per block column, 0x100 writer, 0x200 t's first touch}
+  const int4 bc = tasks[3 * blockIdx.x], bm = tasks[3 * blockIdx.x + 1], tk = tasks[3 * blockIdx.x + 2];
+  const int p = bm.x, imask = bm.y, ftouch = bm.z, t = tk.x, tmask = tk.y & 0xff;
+  const bool writer = (tk.y & 0x100) != 0, tfirst = (tk.y & 0x200) != 0;
+  const int64_t tnNB = (int64_t)(n / NB) * NB, rn = n - tnNB;
+  auto yval = [&](int64_t i) -> double {  // forward-substitution result: the factor's augmented row
+    return i < tnNB ? L[(int64_t)n * ld + i] : (i < n ? Ldiag[(tnNB + rn) * NB + (i - tnNB)] : 0.0);
+  };
+  const int ck = k == 0 ? bc.x : (k == 1 ? bc.y : (k == 2 ? bc.z : bc.w));
+  const bool act = k < p;
+  const int64_t cc = (int64_t)ck * NB;
+  double m[NB / 2], lj[BSB_P - 1][NB / 2], lt[NB / 2], rk = 0.0, rt = 0.0;
+  if (act) {
+    const double* mp = Minv + cc * NB + (int64_t)(h * (NB / 2)) * NB + c;  // M[kk][c], kk = h * 16 + i
+#pragma unroll
+    for (int i = 0; i < NB / 2; ++i) m[i] = mp[i * NB];
+#pragma unroll
+    for (int j = 0; j < BSB_P - 1; ++j) {
+      const int cj = j == 0 ? bc.x : (j == 1 ? bc.y : bc.z);
+      if (j < k && ((imask >> (j * 4 + k)) & 1)) {
+        const double* lp = L + ((int64_t)cj * NB + h * (NB / 2)) * ld + cc + c;
+#pragma unroll
+        for (int i = 0; i < NB / 2; ++i) lj[j][i] = lp[(int64_t)i * ld];
+      }
+    }
+    if ((tmask >> k) & 1) {
+      const double* lp = L + (cc + h * (NB / 2)) * ld + (int64_t)t * NB + c;
+#pragma unroll
+      for (int i = 0; i < NB / 2; ++i) lt[i] = lp[(int64_t)i * ld];
+    }
+    rk = ((ftouch >> k) & 1) ? yval(cc + c) : r[cc + c];
+    if (k == 0 && t >= 0) rt = tfirst ? yval((int64_t)t * NB + c) : r[(int64_t)t * NB + c];
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): s_cnt's init (global loads stay in flight)
+  __builtin_amdgcn_s_barrier();
+  if (act) {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < BSB_P - 1; ++j) {
+      if (j < k) {
+        lds_wait_ge(&s_cnt, j + 1, 0);
+        if ((imask >> (j * 4 + k)) & 1) {
+          double a4[4] = {0, 0, 0, 0};
+#pragma unroll
+          for (int i = 0; i < NB / 2; ++i) a4[i & 3] = fma(lj[j][i], xs[j][h * (NB / 2) + i], a4[i & 3]);
+          s += (a4[0] + a4[1]) + (a4[2] + a4[3]);
+        }
+      }
+    }
+    s += __shfl_xor(s, 32, WAVE);
+    if (h == 0) rs[k][c] = rk - s;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    double x4[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < NB / 2; ++i) x4[i & 3] = fma(m[i], rs[k][h * (NB / 2) + i], x4[i & 3]);
+    double x = (x4[0] + x4[1]) + (x4[2] + x4[3]);
+    x += __shfl_xor(x, 32, WAVE);
+    if (h == 0) xs[k][c] = x;
+    lds_signal(&s_cnt, k + 1);  // waits for this wave's LDS stores first
+    if (writer && h == 0 && cc + c < n) xout[cc + c] = x;
+    if ((tmask >> k) & 1) {
+      double a4[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int i = 0; i < NB / 2; ++i) a4[i & 3] = fma(lt[i], xs[k][h * (NB / 2) + i], a4[i & 3]);
+      double a = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+      a += __shfl_xor(a, 32, WAVE);
+      if (h == 0) ps[k][c] = a;
+    }
+  }
+  __syncthreads();
+  if (k == 0 && t >= 0 && h == 0) {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < BSB_P; ++j)
+      if ((tmask >> j) & 1) s += ps[j][c];
+    r[(int64_t)t * NB + c] = rt - s;
+  }
+}
+
+__global__ void k_tile_inv_list(const double* __restrict__ Ldiag, double* __restrict__ Minv,
+                                const int* __restrict__ tiles);
+void launch_chol_backsolve_blk(const double* L, int64_t ld, int n, const int4* tasks, const int* step_off_host,
+                               int n_steps, const double* Ldiag, double* Minv, double* r, double* xout,
+                               hipStream_t st, const int* tinv_list, int n_tinv) {
+  if (n_tinv > 0) hipLaunchKernelGGL(k_tile_inv_list, dim3(n_tinv), dim3(64), 0, st, Ldiag, Minv, tinv_list);
+  for (int s = 0; s < n_steps; ++s) {
+    const int t0 = step_off_host[s], nt = step_off_host[s + 1] - t0;
+    if (nt > 0)
+      hipLaunchKernelGGL(k_chol_backsolve_blk, dim3(nt), dim3(64 * BSB_P), 0, st, L, ld, n, tasks + 3 * t0, Ldiag,
+                         Minv, r, xout);
+  }
+}
+
 #ifdef CS_TIMING
 extern "C" int ptzba_debug_cs_stamps(long long* out) {
   const int zero = 0;

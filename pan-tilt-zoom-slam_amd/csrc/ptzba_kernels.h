@@ -179,6 +179,12 @@ void launch_chol_backsolve(const double* L, int64_t ld, int n, int n_chain, int 
                            const int* la_tasks, int n_tasks, const double* Ldiag, double* Minv, double* xout,
                            const int* lo_off, const int* lo_tiles, hipStream_t st,
                            const int* tinv_list = nullptr, int n_tinv = 0);  // tinv_list: see k_tile_inv_list
+// blocked right-looking back substitution (large systems): one launch per step of api.hip make_bs_steps'
+// schedule (step_off_host: task offsets), r: scratch [ld]; BSB_P chain columns per block
+constexpr int BSB_P = 4;
+void launch_chol_backsolve_blk(const double* L, int64_t ld, int n, const int4* tasks, const int* step_off_host,
+                               int n_steps, const double* Ldiag, double* Minv, double* r, double* xout,
+                               hipStream_t st, const int* tinv_list, int n_tinv);
 // largest ld the back substitution keeps in LDS (left-looking form: x [ld] doubles + 4.4 KiB)
 constexpr int64_t CHOL_MAX_LD = 18944;
 // zero the factor pattern's tiles and the b | g_pose | dU vectors before a build (replaces a memset of

@@ -674,7 +674,7 @@ class BAHandle:
         _check(lib().ptzba_solver_info(self.h, _ptr(out)), "ptzba_solver_info")
         return dict(n_aug=int(out[0]), ld=int(out[1]), levels=int(out[2]),
                     ordering="nested" if out[3] != ORDER_NATURAL else "natural",
-                    backsolve="left-looking" if out[4] else "lookahead", n_slot=int(out[5]), schur_items=int(out[6]),
+                    backsolve=("lookahead", "left-looking", "blocked")[int(out[4])], n_slot=int(out[5]), schur_items=int(out[6]),
                     pattern_tiles=int(out[7]))
 
     def info(self):

@@ -3,8 +3,8 @@ and of the multi-row keyframe grid it is built from.
 
 On a row-major keyframe grid a landmark seen by two tilt rows spans a whole row of frame indices, so
 the solver paths config 3 never reaches are exercised here: Schur chunk lists with per-landmark frame
-gaps, a coupling band of ~57 tiles (nested dissection on a 2-D coupled grid), and the left-looking
-back substitution (update lists larger than LDS).  Parity is the same as for the small configs: one
+gaps, a coupling band of ~57 tiles (nested dissection on a 2-D coupled grid), and the back substitutions
+for update lists larger than LDS (blocked right-looking, the default there, and left-looking).  Parity is the same as for the small configs: one
 undamped step equals the oracle's sparse normal-equation solution (bundle_adjustment.py:25-106 via
 oracle/ptz_oracle.py); at full size, the fp64 residual vector against the oracle on a sample of records,
 the cost K1 reduces against the residual vector, and a monotone LM descent (bundle_adjustment.py:200-202).
@@ -40,16 +40,16 @@ def grid():
     return synthetic.make_grid_problem(120, 6000, -20.0, 20.0, (-10.0, 0.0, 10.0), seed=3)
 
 
-@pytest.mark.parametrize("backsolve", ["lookahead", "ll"])
+@pytest.mark.parametrize("backsolve", ["lookahead", "ll", "blk"])
 @pytest.mark.parametrize("ordering", [0, 2])
 def test_grid_gauss_newton_step_is_exact(gpu_available, grid, monkeypatch, backsolve, ordering):
     import scipy.sparse.linalg as spla
     from oracle import ptz_oracle as orc
     p = grid
-    if backsolve == "ll":
-        monkeypatch.setenv("PTZBA_BACKSOLVE", "ll")
+    if backsolve != "lookahead":
+        monkeypatch.setenv("PTZBA_BACKSOLVE", backsolve)
     dx_gpu, info = _gn_step(p, 0, ordering)
-    assert info["backsolve"] == ("left-looking" if backsolve == "ll" else "lookahead")
+    assert info["backsolve"] == {"lookahead": "lookahead", "ll": "left-looking", "blk": "blocked"}[backsolve]
     assert info["ordering"] == ("nested" if ordering == 2 else "natural")
     x0 = np.concatenate([p.init_ptz[1:].reshape(-1), p.init_rays.reshape(-1)])
     fr, lm = p.frame.astype(np.int64), p.landmark.astype(np.int64)
@@ -84,7 +84,7 @@ def test_config4_residual_fp64_matches_oracle(gpu_available, config4):
     info, sinfo = h.info(), h.solver_info()
     print(f"set_problem fp64 {time.time() - t0:.1f} s; {info}; {sinfo}", flush=True)
     assert info["n_obs"] == len(p.frame) > 300_000_000
-    assert sinfo["backsolve"] == "left-looking"
+    assert sinfo["backsolve"] == "blocked"
     x_full = np.concatenate([p.init_ptz.reshape(-1), p.init_rays.reshape(-1)])
     r = h.residual(x_full)
     h.set_state(p.init_ptz, p.init_rays)
@@ -104,7 +104,7 @@ def test_config4_residual_fp64_matches_oracle(gpu_available, config4):
 def test_config4_lm_three_iterations(gpu_available, config4):
     """set_problem + 3 LM iterations at full size in the headline arithmetic (fp32 records, Huber): every
     iteration is accepted or retried by the reference's rules and the cost decreases monotonically from
-    the one fp64 K1 computes; the solve is structurally the left-looking / nested path."""
+    the one fp64 K1 computes; the solve is structurally the blocked back-substitution / nested path."""
     import ptzba
     p = config4
     t0 = time.time()

@@ -163,20 +163,23 @@ def _part_worker(rank, world, port, out_dir, config, precision, loss):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("config,world,precision,loss", [("config2", 2, 0, 0), ("config2", 4, 0, 0),
-                                                         ("grid", 2, 0, 0), ("grid", 4, 0, 0),
-                                                         ("config3", 2, 0, 0), ("config3", 2, 1, 1),
-                                                         ("config4", 2, 1, 1)])
-def test_part_owned_gpu_solve_matches_single_rank(gpu_available, tmp_path, config, world, precision, loss):
+@pytest.mark.parametrize("config,world,precision,loss,backsolve", [
+    ("config2", 2, 0, 0, ""), ("config2", 4, 0, 0, ""), ("grid", 2, 0, 0, ""), ("grid", 4, 0, 0, ""),
+    ("grid", 2, 0, 0, "blk"), ("config3", 2, 0, 0, ""), ("config3", 2, 1, 1, ""), ("config4", 2, 1, 1, "")])
+def test_part_owned_gpu_solve_matches_single_rank(gpu_available, tmp_path, monkeypatch, config, world, precision, loss,
+                                                  backsolve):
     """libptzba's part-owned solve on one device (ranks over gloo): every rank factors its part (A or B) and the
     separator C; only C (and, with 2 ranks per part, the part's interior inside its group) is exchanged.  The
     result equals the single-rank solve of the whole problem: same iterations and status, the cost to 1e-9
     relative, every rank's poses (its part and C) and rays within 1e-8 (fp64; fp32 records + Huber: 1e-6 deg /
     1e-4 px -- the per-rank Schur sums round differently).  config 3 = the headline problem (A = frames 1-199,
     C = 200-305, B = 306-499); grid / config 4 = keyframes on tilt rows (config 4: 410M records, A = 1-2185,
-    C = 2186-2803, B = 2804-4999; 3 LM iterations)."""
+    C = 2186-2803, B = 2804-4999; 3 LM iterations).  backsolve "blk": the blocked back substitution (config 4's
+    default) on the grid's one-chain part plans and on the single-rank nested plan."""
     import ptzba
     import synthetic
+    if backsolve:
+        monkeypatch.setenv("PTZBA_BACKSOLVE", backsolve)  # inherited by the spawned ranks
     mp.start_processes(_part_worker, args=(world, _free_port(), str(tmp_path), config, precision, loss), nprocs=world,
                        join=True, start_method="spawn")
     prob = _make(config)
