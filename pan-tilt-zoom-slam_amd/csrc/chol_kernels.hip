@@ -288,6 +288,9 @@ constexpr int WB = 8;
 #ifndef LA_BW
 #define LA_BW 4  // pivot block of the lookahead form
 #endif
+#ifndef CHOL_LB_ALIAS
+#define CHOL_LB_ALIAS 1  // the sweep's block buffer overlays the update panels (0: a buffer of its own, A/B)
+#endif
 #ifndef CHOL_WG
 #define CHOL_WG 3  // 3: flag-synchronised lookahead, 2: lookahead workgroup potrf+trsm, 1: workgroup (4 waves), 0: single-wave sweep
 #endif
@@ -751,7 +754,7 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
                                                    double* __restrict__ Minv) {
   __shared__ double sC[NB][NB + 1];     // target tile (panel T_ik / trailing A_ij)
   __shared__ double sD[NB][NB + 1];     // diagonal tile -> L_kk
-  __shared__ double sA[2][NB][NB + 1];  // L_ip of the two update panels
+  __shared__ __attribute__((aligned(16))) double sA[2][NB][NB + 1];  // L_ip of the two update panels
   __shared__ double sB[2][NB][NB + 1];  // L_kp or L_jp of the two update panels
 #if CHOL_WG < 2
   __shared__ double rdg[NB];
@@ -762,7 +765,15 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
 #if CHOL_WG == 1
   __shared__ double s_pan[2 * NB][WB + 1], s_mul[2 * NB][WB + 1], s_dg[NB];
 #elif CHOL_WG >= 2
+#if CHOL_LB_ALIAS
+  // the sweep's block buffer overlays the update panels' L_ip tiles, dead once the panel GEMMs are done (a
+  // barrier separates them): 51 KB of LDS per workgroup instead of 67, so three workgroups per CU instead of
+  // two -- config 4's levels carry ~1,600 trailing tasks, whose time is load latency x rounds of residency
+  static_assert((NB / LA_BW) * 2 * NB * LA_BW <= 2 * NB * (NB + 1), "block buffer must fit the panel tiles");
+  double (*s_lb)[2 * NB][LA_BW] = reinterpret_cast<double (*)[2 * NB][LA_BW]>(&sA[0][0][0]);
+#else
   __shared__ __attribute__((aligned(16))) double s_lb[NB / LA_BW][2 * NB][LA_BW];
+#endif
   __shared__ __attribute__((aligned(16))) double s_pb[LA_BW][LA_BW];
   __shared__ int s_flags[NB / LA_BW + 1];
 #endif
