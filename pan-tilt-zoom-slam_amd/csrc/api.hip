@@ -81,6 +81,7 @@ struct ptzba_ctx {
   DBuf bsb_tasks, bsb_r;  // blocked back substitution (large systems): plan + r scratch [ld]
   std::vector<int> bsb_step_off;
   bool bs_ll = false, bs_blk = false;
+  bool chol_delayed = false;  // the plan delays trailing updates (make_plan, DT = 2)
   DBuf xtiles, xbuf;  // packed exchange: tile list, buffer
   int n_xtiles = 0;
   DBuf ztiles;  // tiles zeroed before each build (the rest of the system region stays zero)
@@ -351,6 +352,7 @@ struct CholPlan {
   std::vector<int32_t> ztiles;  // (ti, tj) lower tiles of the factor's pattern (incl. fill): zeroed per build
   std::vector<int32_t> tinv_tail;  // diagonal tiles inverted after the last level (the others: type-2 tasks)
   int n_levels = 0;
+  bool delayed = false;  // tasks carry a second pair of update panels (delayed trailing updates, make_plan)
   // blocked back substitution (large systems): tasks of 3 int4 (block columns | {p, intra-block coupling
   // bits, first-touch bits, 0} | {target column, flags, 0, 0}) and the task offset of each step (one launch
   // per step); empty when no valid schedule exists
@@ -495,38 +497,65 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
   const int n_inv = (o.n_aug + CHOL_NB - 1) / CHOL_NB;
   const bool tinv_split = !getenv("PTZBA_TINV_ALL");  // A/B knob: every inverse after the factorisation
   P.tinv_tail.clear();
+  // Delayed trailing updates (period DT): trailing tasks run only at levels L = 0 mod DT and apply the
+  // panels of levels [L - DT, L - 1] at once (rank <= 2 DT x 32: half the read-modify-writes of the band's
+  // tiles at DT = 2); a panel task applies inline every update not yet applied to its tiles, the panels of
+  // levels [F, L - 1] with F the last trailing level before L.  Worth it when the levels are dominated by
+  // their trailing tasks (config 4: ~1,600 per level), not when they are chain-bound (config 3).
+  int64_t trail = 0;
+  for (int p = 0; p < T; ++p) {
+    int64_t r = 0;
+    for (int i = p + 1; i < T; ++i) r += nz[i][p];
+    trail += r * (r + 1) / 2;
+  }
+  int DT = trail > 600 * (int64_t)nL ? 2 : 1;
+  if (const char* e = getenv("PTZBA_CHOL_DELAY")) DT = std::max(1, std::min(2, atoi(e)));  // A/B knob
+  P.delayed = DT > 1;
+  auto pack2 = [](int type, const std::vector<int>& pd, int tm) {  // int4 task: x (type + panels 2, 3), w (0, 1)
+    return std::make_pair(chol_pack_type(type, pd.size() > 2 ? pd[2] : -1, pd.size() > 3 ? pd[3] : -1, (tm >> 2) & 3),
+                          chol_pack_updates(pd.size() > 0 ? pd[0] : -1, pd.size() > 1 ? pd[1] : -1, tm & 3));
+  };
   for (int L = 0; L < nL; ++L) {
     P.level_off[L] = (int)(P.tasks.size() / 4);
     const std::vector<int> none;
     const std::vector<int>& prev = L > 0 ? K[L - 1] : none;
+    std::vector<int> inl;  // panels applied inline by this level's panel tasks
+    if (L > 0)
+      for (int l = ((L - 1) / DT) * DT; l < L; ++l) inl.insert(inl.end(), K[l].begin(), K[l].end());
     for (int k : K[L]) {
       std::vector<int> pd;
-      for (int pp : prev)
+      for (int pp : inl)
         if (pp < k && nz[k][pp]) pd.push_back(pp);
       for (int i = k; i < T; ++i) {
         if (!nz[i][k]) continue;
         int tm = 0;
         for (size_t u = 0; u < pd.size(); ++u)
           if (i == k || nz[i][pd[u]]) tm |= 1 << u;
-        push(0, i, k, chol_pack_updates(pd.size() > 0 ? pd[0] : -1, pd.size() > 1 ? pd[1] : -1, tm));
+        const auto w = pack2(0, pd, tm);
+        push(w.first, i, k, w.second);
       }
     }
-    // trailing updates from the previous level's panels into tiles of columns factored later
+    // trailing updates from the panels of levels [L - DT, L - 1] into tiles of columns factored after L
     std::vector<std::pair<int64_t, int>> upd;  // (tile key, panel)
-    for (int pp : prev) {
-      std::vector<int> R;
-      for (int i = pp + 1; i < T; ++i)
-        if (nz[i][pp]) R.push_back(i);
-      for (size_t x = 0; x < R.size(); ++x)
-        for (size_t y = 0; y <= x; ++y)
-          if (level[R[y]] > L) upd.push_back({(int64_t)R[x] * T + R[y], pp});
-    }
+    if (L % DT == 0)
+      for (int l = std::max(0, L - DT); l < L; ++l)
+        for (int pp : K[l]) {
+          std::vector<int> R;
+          for (int i = pp + 1; i < T; ++i)
+            if (nz[i][pp]) R.push_back(i);
+          for (size_t x = 0; x < R.size(); ++x)
+            for (size_t y = 0; y <= x; ++y)
+              if (level[R[y]] > L) upd.push_back({(int64_t)R[x] * T + R[y], pp});
+        }
     std::sort(upd.begin(), upd.end());
     for (size_t x = 0; x < upd.size();) {
       size_t y = x + 1;
       while (y < upd.size() && upd[y].first == upd[x].first) ++y;
       const int i = (int)(upd[x].first / T), j = (int)(upd[x].first % T);
-      push(1, i, j, chol_pack_updates(upd[x].second, y - x > 1 ? upd[x + 1].second : -1, 3));
+      std::vector<int> pd;
+      for (size_t u = x; u < y; ++u) pd.push_back(upd[u].second);
+      const auto w = pack2(1, pd, 15);
+      push(w.first, i, j, w.second);
       x = y;
     }
     if (tinv_split)
@@ -1062,6 +1091,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->chol_tasks_host = plan.tasks;
   h->n_tinv_tail = (int)plan.tinv_tail.size();
   h->chol_levels = plan.n_levels;
+  h->chol_delayed = plan.delayed;
   h->n_chain = (int)plan.chain_off.size() - 1;
   frame_win_hi = win;  // K2 windows follow the same (possibly global) coupling
   h->perm_host = order;
@@ -1492,7 +1522,8 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
                                  h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
                                  h->lambda, lam_dev, h->st);
     launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
-                    h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>());
+                    h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>(), 0,
+                    h->chol_delayed);
   }
   if (h->bs_blk)
     launch_chol_backsolve_blk(h->S(), h->ld, h->n_aug, h->bsb_tasks.as<int4>(), h->bsb_step_off.data(), (int)h->bsb_step_off.size() - 1, h->Ldiag.as<double>(),

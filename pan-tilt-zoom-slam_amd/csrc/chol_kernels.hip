@@ -748,7 +748,8 @@ struct CholTaskVal {
   int4 t[CHOL_KT];
   __device__ int4 get(int b) const { return t[b]; }
 };
-template <bool SG, typename TaskArg>
+// P2: plans with delayed trailing updates (a second pair of update panels per task, api.hip make_plan)
+template <bool SG, typename TaskArg, bool P2 = false>
 __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64_t ld, const TaskArg tasks,
                                                    double* __restrict__ Ldiag, int* info, double* __restrict__ sgn,
                                                    double* __restrict__ Minv) {
@@ -780,7 +781,7 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   __shared__ double s_sgp[2][NB];  // SG: signs of the two update panels' columns
   __shared__ double s_sig[NB];     // SG: signs of this column's pivots
   const int4 tk = tasks.get(blockIdx.x);
-  if (tk.x == 2) {  // inverse of a diagonal factor tile of the previous level (see tile_inv_wave)
+  if ((tk.x & 3) == 2) {  // inverse of a diagonal factor tile of the previous level (see tile_inv_wave)
     __shared__ double s_rinv[NB];
     tile_inv_wave(Ldiag + (int64_t)tk.y * NB * NB, Minv + (int64_t)tk.y * NB * NB, sD, s_rinv);
     return;
@@ -788,10 +789,15 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
 #if CHOL_FEWER_BARRIERS && CHOL_WG == 3
   if (threadIdx.x <= NB / LA_BW) s_flags[threadIdx.x] = 0;  // the sweep's counters (ordered by the staging barrier)
 #endif
-  const int type = tk.x, i = tk.y, j = tk.z;
+  const int type = tk.x & 3, i = tk.y, j = tk.z;
   const int up0 = (tk.w & 0x3fff) - 1;
   const int up1 = ((tk.w >> 14) & 0x3fff) - 1;
   const int tmask = (tk.w >> 28) & 3;  // panel: which updates also apply to T
+  // delayed trailing updates (api.hip make_plan, period 2): a second pair of update panels rides in x
+  const int up2 = P2 ? (int)(((unsigned)tk.x >> 2) & 0x3fff) - 1 : -1;
+  const int up3 = P2 ? (int)(((unsigned)tk.x >> 16) & 0x3fff) - 1 : -1;
+  const int tmask2 = P2 ? (int)((unsigned)tk.x >> 30) : 0;
+  const bool pass2 = P2 && (up2 >= 0 || up3 >= 0);
   const int64_t NBl = NB;
 #ifdef CS_TIMING
   const int cs_lvl = g_cs_level;
@@ -804,14 +810,29 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
 #if CHOL_VARIANT == 5
   return;
 #endif
-  double v0[4], v1[4], v2[4], v3[4], v4[4], v5[4];
+  double v0[4], v1[4], v2[4], v3[4], v4[4], v5[4], w2[4], w3[4], w4[4], w5[4];
+  auto load_signs = [&](int ua, int ub) {  // SG: signs of the update panels' columns
+    if constexpr (SG) {
+      if (threadIdx.x < 2 * NB) {
+        const int q = threadIdx.x >> 5, up = q ? ub : ua;
+        s_sgp[q][threadIdx.x & 31] = up >= 0 ? sgn[(int64_t)up * NB + (threadIdx.x & 31)] : 1.0;
+      }
+    }
+  };
   if (type == 1) {
 #if CHOL_VARIANT == 3
     return;
 #endif
     // trailing: A_ij -= sum_p L_ip L_jp^T
     double* C = A + i * NBl * ld + j * NBl;
+#if CHOL_VARIANT == 7  // timing only: no C tile read / write
+    for (int r = 0; r < 4; ++r) v0[r] = 0.0;
+#else
     fetch_tile(v0, C, ld);
+#endif
+#if CHOL_VARIANT == 6  // timing only: no panel tile reads
+    for (int r = 0; r < 4; ++r) v1[r] = v2[r] = v3[r] = v4[r] = 0.0;
+#else
     if (up0 >= 0) {
       fetch_tile(v1, A + i * NBl * ld + up0 * NBl, ld);
       fetch_tile(v2, A + j * NBl * ld + up0 * NBl, ld);
@@ -819,6 +840,15 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
     if (up1 >= 0) {
       fetch_tile(v3, A + i * NBl * ld + up1 * NBl, ld);
       fetch_tile(v4, A + j * NBl * ld + up1 * NBl, ld);
+    }
+#endif
+    if (up2 >= 0) {
+      fetch_tile(w2, A + i * NBl * ld + up2 * NBl, ld);
+      fetch_tile(w3, A + j * NBl * ld + up2 * NBl, ld);
+    }
+    if (up3 >= 0) {
+      fetch_tile(w4, A + i * NBl * ld + up3 * NBl, ld);
+      fetch_tile(w5, A + j * NBl * ld + up3 * NBl, ld);
     }
     put_tile(sC, v0);
     if (up0 >= 0) {
@@ -829,42 +859,54 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
       put_tile(sA[1], v3);
       put_tile(sB[1], v4);
     }
-    if constexpr (SG) {
-      if (threadIdx.x < 2 * NB) {
-        const int q = threadIdx.x >> 5, up = q ? up1 : up0;
-        s_sgp[q][threadIdx.x & 31] = up >= 0 ? sgn[(int64_t)up * NB + (threadIdx.x & 31)] : 1.0;
-      }
-    }
+    load_signs(up0, up1);
     __syncthreads();
     // each wave owns one 16x16 block of C: consecutive updates need no barrier in between
     if (up0 >= 0) tile_gemm_nt_sub<SG>(sC, sA[0], sB[0], s_sgp[0]);
     if (up1 >= 0) tile_gemm_nt_sub<SG>(sC, sA[1], sB[1], s_sgp[1]);
+    if (pass2) {  // the second pair through the same panel buffers
+      __syncthreads();
+      if (up2 >= 0) {
+        put_tile(sA[0], w2);
+        put_tile(sB[0], w3);
+      }
+      if (up3 >= 0) {
+        put_tile(sA[1], w4);
+        put_tile(sB[1], w5);
+      }
+      load_signs(up2, up3);
+      __syncthreads();
+      if (up2 >= 0) tile_gemm_nt_sub<SG>(sC, sA[0], sB[0], s_sgp[0]);
+      if (up3 >= 0) tile_gemm_nt_sub<SG>(sC, sA[1], sB[1], s_sgp[1]);
+    }
     __syncthreads();
+#if CHOL_VARIANT != 7
     for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) C[(int64_t)(e >> 5) * ld + (e & 31)] = sC[e >> 5][e & 31];
+#endif
     return;
   }
   // panel task (i, k = j)
   const int k = j;
   const bool diag_only = (i == k);
   const bool updT0 = !diag_only && (tmask & 1), updT1 = !diag_only && (tmask & 2);
+  const bool updT2 = !diag_only && (tmask2 & 1), updT3 = !diag_only && (tmask2 & 2);
   fetch_tile(v0, A + (int64_t)k * NBl * ld + k * NBl, ld);
   if (!diag_only) fetch_tile(v1, A + i * NBl * ld + k * NBl, ld);
   if (up0 >= 0) fetch_tile(v2, A + (int64_t)k * NBl * ld + up0 * NBl, ld);
   if (updT0 && up0 >= 0) fetch_tile(v3, A + i * NBl * ld + up0 * NBl, ld);
   if (up1 >= 0) fetch_tile(v4, A + (int64_t)k * NBl * ld + up1 * NBl, ld);
   if (updT1 && up1 >= 0) fetch_tile(v5, A + i * NBl * ld + up1 * NBl, ld);
+  if (up2 >= 0) fetch_tile(w2, A + (int64_t)k * NBl * ld + up2 * NBl, ld);
+  if (updT2 && up2 >= 0) fetch_tile(w3, A + i * NBl * ld + up2 * NBl, ld);
+  if (up3 >= 0) fetch_tile(w4, A + (int64_t)k * NBl * ld + up3 * NBl, ld);
+  if (updT3 && up3 >= 0) fetch_tile(w5, A + i * NBl * ld + up3 * NBl, ld);
   put_tile(sD, v0);
   if (!diag_only) put_tile(sC, v1);
   if (up0 >= 0) put_tile(sB[0], v2);
   if (updT0 && up0 >= 0) put_tile(sA[0], v3);
   if (up1 >= 0) put_tile(sB[1], v4);
   if (updT1 && up1 >= 0) put_tile(sA[1], v5);
-  if constexpr (SG) {
-    if (threadIdx.x < 2 * NB) {
-      const int q = threadIdx.x >> 5, up = q ? up1 : up0;
-      s_sgp[q][threadIdx.x & 31] = up >= 0 ? sgn[(int64_t)up * NB + (threadIdx.x & 31)] : 1.0;
-    }
-  }
+  load_signs(up0, up1);
   __syncthreads();
   CS_STAMP(1);
 #if CHOL_VARIANT != 4
@@ -875,6 +917,23 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   if (up1 >= 0) {
     tile_gemm_nt_sub<SG>(sD, sB[1], sB[1], s_sgp[1]);
     if (updT1) tile_gemm_nt_sub<SG>(sC, sA[1], sB[1], s_sgp[1]);
+  }
+  if (pass2) {  // the delayed pair (api.hip make_plan) through the same panel buffers
+    __syncthreads();
+    if (up2 >= 0) put_tile(sB[0], w2);
+    if (updT2 && up2 >= 0) put_tile(sA[0], w3);
+    if (up3 >= 0) put_tile(sB[1], w4);
+    if (updT3 && up3 >= 0) put_tile(sA[1], w5);
+    load_signs(up2, up3);
+    __syncthreads();
+    if (up2 >= 0) {
+      tile_gemm_nt_sub<SG>(sD, sB[0], sB[0], s_sgp[0]);
+      if (updT2) tile_gemm_nt_sub<SG>(sC, sA[0], sB[0], s_sgp[0]);
+    }
+    if (up3 >= 0) {
+      tile_gemm_nt_sub<SG>(sD, sB[1], sB[1], s_sgp[1]);
+      if (updT3) tile_gemm_nt_sub<SG>(sC, sA[1], sB[1], s_sgp[1]);
+    }
   }
 #endif
   __syncthreads();
@@ -934,7 +993,8 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
 }
 
 void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_off_host, int n_launch, double* Ldiag,
-                     int* info, hipStream_t st, double* sgn, const int4* tasks_host, double* Minv, int first_level) {
+                     int* info, hipStream_t st, double* sgn, const int4* tasks_host, double* Minv, int first_level,
+                     bool delayed) {
   static const bool by_value = !getenv("PTZBA_CHOL_TASKS_PTR");  // A/B knob
   for (int L = first_level; L < n_launch; ++L) {
     const int n = task_off_host[L + 1] - task_off_host[L];
@@ -944,6 +1004,8 @@ void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_o
       std::memcpy(tv.t, tasks_host + task_off_host[L], n * sizeof(int4));
       if (sgn)
         hipLaunchKernelGGL((k_chol_step<true, CholTaskVal>), dim3(n), dim3(256), 0, st, A, ld, tv, Ldiag, info, sgn, Minv);
+      else if (delayed)
+        hipLaunchKernelGGL((k_chol_step<false, CholTaskVal, true>), dim3(n), dim3(256), 0, st, A, ld, tv, Ldiag, info, sgn, Minv);
       else
         hipLaunchKernelGGL((k_chol_step<false, CholTaskVal>), dim3(n), dim3(256), 0, st, A, ld, tv, Ldiag, info, sgn, Minv);
       continue;
@@ -951,6 +1013,8 @@ void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_o
     const CholTaskPtr tp{tasks + task_off_host[L]};
     if (sgn)
       hipLaunchKernelGGL((k_chol_step<true, CholTaskPtr>), dim3(n), dim3(256), 0, st, A, ld, tp, Ldiag, info, sgn, Minv);
+    else if (delayed)
+      hipLaunchKernelGGL((k_chol_step<false, CholTaskPtr, true>), dim3(n), dim3(256), 0, st, A, ld, tp, Ldiag, info, sgn, Minv);
     else
       hipLaunchKernelGGL((k_chol_step<false, CholTaskPtr>), dim3(n), dim3(256), 0, st, A, ld, tp, Ldiag, info, sgn, Minv);
   }

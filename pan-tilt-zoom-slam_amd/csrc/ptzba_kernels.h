@@ -170,7 +170,8 @@ constexpr int CHOL_KT = 240;  // 3.75 KB of kernel arguments
 void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_off_host, int n_launch, double* Ldiag,
                      int* info, hipStream_t st, double* sgn = nullptr, const int4* tasks_host = nullptr,
                      double* Minv = nullptr,  // Minv: target of type-2 tasks (diagonal tile inverses)
-                     int first_level = 0);    // levels [first_level, n_launch)
+                     int first_level = 0,     // levels [first_level, n_launch)
+                     bool delayed = false);   // tasks carry a second pair of update panels (api.hip make_plan)
 // la_tasks: lookahead back substitution's [lookahead tile per position | task offsets per (chain, helper) |
 // tasks q << 16 | tile], built by the host plan (api.hip make_plan)
 constexpr int BS_HELPERS = 7;
@@ -203,6 +204,10 @@ void launch_pack_region(double* S, int64_t ld, const int2* xt, int n_tiles, doub
                         double* buf, int mode, hipStream_t st);
 // task word w: bits 0-13 update panel p1 + 1, bits 14-27 p2 + 1 (0 = none), bits 28/29: p1/p2 also update T
 inline int chol_pack_updates(int p1, int p2, int tmask) { return (p1 + 1) | ((p2 + 1) << 14) | (tmask << 28); }
+// task word x: type (2 bits) + the second pair of update panels of a delayed-trailing plan (api.hip make_plan)
+inline int chol_pack_type(int type, int p3, int p4, int tmask34) {
+  return (int)((unsigned)type | ((unsigned)(p3 + 1) << 2) | ((unsigned)(p4 + 1) << 16) | ((unsigned)tmask34 << 30));
+}
 
 // camera batch kernels (camera_kernels.hip)
 void launch_ray_to_image(int64_t n, double u, double v, const double* f, const double* cp, const double* ct,

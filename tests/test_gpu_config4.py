@@ -60,6 +60,24 @@ def test_grid_gauss_newton_step_is_exact(gpu_available, grid, monkeypatch, backs
     assert err < 1e-7, err
 
 
+@pytest.mark.parametrize("ordering", [0, 2])
+def test_grid_delayed_trailing_updates_exact(gpu_available, grid, monkeypatch, ordering):
+    """The factorisation with delayed trailing updates (PTZBA_CHOL_DELAY=2: trailing tasks every other level,
+    up to four update panels per task; config 4's default) gives the same exact Gauss-Newton step."""
+    import scipy.sparse.linalg as spla
+    from oracle import ptz_oracle as orc
+    p = grid
+    monkeypatch.setenv("PTZBA_CHOL_DELAY", "2")
+    dx_gpu, info = _gn_step(p, 0, ordering)
+    x0 = np.concatenate([p.init_ptz[1:].reshape(-1), p.init_rays.reshape(-1)])
+    fr, lm = p.frame.astype(np.int64), p.landmark.astype(np.int64)
+    J = orc.ba_jacobian(x0, p.n_pose, p.n_landmark, p.u, p.v, p.init_ptz[0], fr, lm).tocsc()
+    r = orc.compute_residual_records(np.concatenate([p.init_ptz[0], x0]), p.n_pose, p.u, p.v, fr, lm, p.xy)
+    dx = spla.spsolve((J.T @ J).tocsc(), -(J.T @ r))
+    err = np.abs(dx_gpu - dx).max() / np.abs(dx).max()
+    assert err < 1e-7, err
+
+
 @pytest.fixture(scope="module")
 def config4():
     import synthetic
