@@ -288,6 +288,9 @@ constexpr int WB = 8;
 #ifndef LA_BW
 #define LA_BW 4  // pivot block of the lookahead form
 #endif
+#ifndef CHOL_TRAIL_DIRECT
+#define CHOL_TRAIL_DIRECT 0  // 1: trailing tasks from registers (A/B: config 4 5.73 vs 4.76 ms staged, r03s)
+#endif
 #ifndef CHOL_LB_ALIAS
 #define CHOL_LB_ALIAS 1  // the sweep's block buffer overlays the update panels (0: a buffer of its own, A/B)
 #endif
@@ -822,6 +825,47 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   if (type == 1) {
 #if CHOL_VARIANT == 3
     return;
+#endif
+#if CHOL_TRAIL_DIRECT && CHOL_VARIANT == 0
+    {  // trailing: A_ij -= sum_p L_ip L_jp^T straight from registers -- no LDS staging, no barriers: each wave
+       // owns one 16 x 16 block of C in the MFMA accumulator layout of tile_gemm_nt_sub, and the 32-long
+       // contraction is taken in the order k = 8 lk + s (step s, lane group lk), so a lane's A and B operands
+       // are 8 consecutive doubles of one row (two 32-B loads each) instead of 8 strided ones
+      const int w = threadIdx.x >> 6, l = threadIdx.x & 63, li = l & 15, lk = l >> 4;
+      const int bi = (w >> 1) * 16, bj = (w & 1) * 16;
+      double* C = A + (i * NBl + bi) * ld + j * NBl + bj;
+      v4f64 acc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] = C[(int64_t)(lk + 4 * r) * ld + li];
+      const int ups[4] = {up0, up1, up2, up3};
+      constexpr int NU = P2 ? 4 : 2;
+      double2 a[NU][4], b[NU][4];
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+        if (ups[u] >= 0) {
+          const double2* pa = reinterpret_cast<const double2*>(A + (i * NBl + bi + li) * ld + ups[u] * NBl + 8 * lk);
+          const double2* pb = reinterpret_cast<const double2*>(A + (j * NBl + bj + li) * ld + ups[u] * NBl + 8 * lk);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            a[u][q] = pa[q];
+            b[u][q] = pb[q];
+          }
+        }
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+        if (ups[u] >= 0) {
+#pragma unroll
+          for (int s = 0; s < 8; ++s) {
+            const double av = -((s & 1) ? a[u][s >> 1].y : a[u][s >> 1].x);
+            double bv = (s & 1) ? b[u][s >> 1].y : b[u][s >> 1].x;
+            if constexpr (SG) bv *= sgn[(int64_t)ups[u] * NB + 8 * lk + s];
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+          }
+        }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) C[(int64_t)(lk + 4 * r) * ld + li] = acc[r];
+      return;
+    }
 #endif
     // trailing: A_ij -= sum_p L_ip L_jp^T
     double* C = A + i * NBl * ld + j * NBl;
