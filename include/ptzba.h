@@ -344,6 +344,18 @@ PTZBA_EXPORT int ptz_sift(int device, int32_t width, int32_t height, const uint8
 PTZBA_EXPORT int ptz_corner_min_eig(int device, int32_t width, int32_t height, const uint8_t* img, float* eig_out,
                                     uint8_t* locmax_out);
 
+/* ORB / LATCH detection + description (image_process.py:105-155: cv.ORB_create(nfeatures).detect + compute, and
+ * LATCH_create(64).compute on those keypoints): 8-level pyramid (scale 1.2), FAST-9 (threshold 20) with 3x3
+ * non-maximum suppression and the 31-px edge, per-level retain-best by FAST score (2 n_l) then Harris response
+ * (n_l, OpenCV's geometric split), intensity-centroid angle; descriptor 0 = ORB rBRIEF (32 bytes, 7x7 sigma-2
+ * blurred level image), 1 = LATCH (64 bytes, SSD triplets on the 13x13 sigma-2 blurred image, 27-px border).
+ * The sampling tables are generated (OpenCV's learned ones are not available: descriptors are not OpenCV's bits,
+ * see csrc/orb.hip).  kp_out [max_kp][6] = x, y (level-0 pixels), size, angle (deg), response (Harris), octave;
+ * des_out [max_kp][32 or 64].  *n_out = keypoints found (all ties at the per-level cuts kept, as OpenCV): when it
+ * exceeds max_kp only max_kp are written; call again with a larger buffer.  Order: level, response desc, y, x. */
+PTZBA_EXPORT int ptz_orb(int device, int32_t width, int32_t height, const uint8_t* img, int32_t nfeatures,
+                         int32_t descriptor, int32_t max_kp, float* kp_out, uint8_t* des_out, int32_t* n_out);
+
 /* Coupling window of a record set (host only, O(n_obs)): win_out[f] = the highest frame that shares a
  * landmark with frame f (>= f).  Computed over ALL records it is the frame_win_hi every rank of a
  * landmark-sharded solve passes in ptzba_problem_opts. */

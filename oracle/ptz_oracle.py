@@ -1080,3 +1080,283 @@ def hamming_cross(des1, des2):
     i21 = np.argmin(D, axis=0)
     q = np.flatnonzero(i21[i12] == np.arange(len(a)))
     return q, i12[q], D[q, i12[q]]
+
+
+# ----------------------------------------------------------------------------------------
+# ORB / LATCH detection + description (image_process.py:105-155 -> cv.ORB_create(nfeatures), LATCH_create(64)),
+# restated step for step as csrc/orb.hip implements OpenCV's published pipeline.  OpenCV's learned sampling
+# tables are not available: both sides use the generated tables below, so descriptors are checked against
+# this restatement only (parity unpinned against cv2).  Integer stages are exact; the float stages repeat the
+# kernel's fp32 operation order.
+# ----------------------------------------------------------------------------------------
+ORB_LEVELS, ORB_EDGE, ORB_HALF, ORB_FAST_T = 8, 31, 15, 20
+LATCH_HALF_SSD = 3
+LATCH_BORDER = 48 // 2 + LATCH_HALF_SSD
+
+
+def orb_tables():
+    """(pattern [256, 4] int: x0, y0, x1, y1;  latch triplets [512, 6] int) -- csrc/orb.hip orb_tables."""
+    pat = []
+    k = 0
+    base = (0x0B5EED * 0x9E3779B97F4A7C15) & _M64
+    for _ in range(256 * 4):
+        s = 0
+        for _r in range(4):
+            s += _mix64((base + k) & _M64) % 11 - 5
+            k += 1
+        pat.append(max(-13, min(13, s)))
+    trip = []
+    c = 0
+    base = (0x1A7C4 * 0x9E3779B97F4A7C15) & _M64
+    for _ in range(512 * 3):
+        while True:
+            x = _mix64((base + c) & _M64) % 39 - 19
+            c += 1
+            y = _mix64((base + c) & _M64) % 39 - 19
+            c += 1
+            if x * x + y * y <= 19 * 19:
+                break
+        trip += [x, y]
+    return np.array(pat, np.int64).reshape(256, 4), np.array(trip, np.int64).reshape(512, 6)
+
+
+def orb_umax():
+    umax = [0] * (ORB_HALF + 2)
+    vmax = int(math.floor(ORB_HALF * float(np.sqrt(np.float32(2))) / 2 + 1))
+    vmin = int(math.ceil(ORB_HALF * float(np.sqrt(np.float32(2))) / 2))
+    for v in range(vmax + 1):
+        umax[v] = int(np.rint(math.sqrt(float(ORB_HALF * ORB_HALF - v * v))))
+    v0 = 0
+    for v in range(ORB_HALF, vmin - 1, -1):
+        while umax[v0] == umax[v0 + 1]:
+            v0 += 1
+        umax[v] = v0
+        v0 += 1
+    return umax
+
+
+def orb_scale(level):
+    return np.float32(1.2 ** level)
+
+
+def orb_level_counts(nfeatures):
+    factor = 1.0 / 1.2
+    nd = nfeatures * (1 - factor) / (1 - factor ** ORB_LEVELS)
+    n, s = [], 0
+    for _ in range(ORB_LEVELS - 1):
+        n.append(int(np.rint(nd)))
+        s += n[-1]
+        nd *= factor
+    n.append(max(nfeatures - s, 0))
+    return n
+
+
+def orb_resize(src, dw, dh):
+    """8-bit bilinear resize, pixel-centre geometry, 11-bit weights (csrc/orb.hip k_orb_resize)."""
+    sh, sw = src.shape
+
+    def axis(n_dst, n_src):
+        f = (np.arange(n_dst, dtype=np.float64) + 0.5) * (float(n_src) / float(n_dst)) - 0.5
+        i0 = np.floor(f).astype(np.int64)
+        a = np.rint((f - i0) * 2048.0).astype(np.int64)
+        a = np.where(i0 < 0, 0, a)
+        i0 = np.maximum(i0, 0)
+        a = np.where(i0 >= n_src - 1, 0, a)
+        i0 = np.minimum(i0, n_src - 1)
+        return i0, np.minimum(i0 + 1, n_src - 1), a
+
+    x0, x1, ax = axis(dw, sw)
+    y0, y1, ay = axis(dh, sh)
+    s = src.astype(np.int64)
+    t = s[y0][:, x0] * (2048 - ax) + s[y0][:, x1] * ax
+    b = s[y1][:, x0] * (2048 - ax) + s[y1][:, x1] * ax
+    return ((t * (2048 - ay)[:, None] + b * ay[:, None] + (1 << 21)) >> 22).astype(np.uint8)
+
+
+def orb_gauss_taps(n, sigma):
+    w = [math.exp(-(i - (n - 1) * 0.5) ** 2 / (2 * sigma * sigma)) for i in range(n)]
+    s = 0.0
+    for v in w:
+        s += v
+    return np.array([v / s for v in w], np.float64).astype(np.float32)
+
+
+def orb_blur(img, n, sigma):
+    """Separable Gaussian, reflect-101, fp32 mul-then-add per tap, columns rounded half to even to 8 bits."""
+    c = orb_gauss_taps(n, sigma)
+    r = n // 2
+    h, w = img.shape
+    f = img.astype(np.float32)
+    xs, ys = np.arange(w), np.arange(h)
+    acc = np.zeros_like(f)
+    for i in range(n):
+        acc = acc + c[i] * f[:, _refl101(xs + i - r, w)]
+    out = np.zeros_like(f)
+    for i in range(n):
+        out = out + c[i] * acc[_refl101(ys + i - r, h), :]
+    return np.clip(np.rint(out), 0, 255).astype(np.uint8)
+
+
+_FAST_DX = [0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1]
+_FAST_DY = [3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3]
+
+
+def fast_score(img, thr=ORB_FAST_T):
+    """FAST-9 score image (0 = no corner): max over 9-arcs of the arc minimum of p - I (darker) or I - p
+    (brighter), minus one, kept when >= thr; zero within 3 px of the border."""
+    h, w = img.shape
+    s = np.zeros((h, w), np.int64)
+    if h < 7 or w < 7:
+        return s
+    im = img.astype(np.int64)
+    p = im[3:h - 3, 3:w - 3]
+    d = np.stack([p - im[3 + dy:h - 3 + dy, 3 + dx:w - 3 + dx] for dx, dy in zip(_FAST_DX, _FAST_DY)])
+    a = np.full(p.shape, -1000, np.int64)
+    b = np.full(p.shape, -1000, np.int64)
+    for k in range(16):
+        arc = d[[(k + m) % 16 for m in range(9)]]
+        a = np.maximum(a, arc.min(0))
+        b = np.maximum(b, -arc.max(0))
+    t = np.maximum(a, b) - 1
+    s[3:h - 3, 3:w - 3] = np.where(t >= thr, t, 0)
+    return s
+
+
+def fast_nms_points(score, edge=ORB_EDGE):
+    """(x, y, score) of strict 3x3 maxima at least `edge` px inside the image."""
+    h, w = score.shape
+    if h <= 2 * edge or w <= 2 * edge:
+        return np.zeros((0, 3), np.int64)
+    c = score[edge:h - edge, edge:w - edge]
+    keep = c > 0
+    for j in (-1, 0, 1):
+        for i in (-1, 0, 1):
+            if i or j:
+                keep &= c > score[edge + j:h - edge + j, edge + i:w - edge + i]
+    ys, xs = np.nonzero(keep)
+    return np.stack([xs + edge, ys + edge, c[ys, xs]], 1).astype(np.int64)
+
+
+def orb_harris(img, xs, ys):
+    """OpenCV HarrisResponses (block 7, k 0.04) at integer points: integer Sobel sums, fp32 response."""
+    im = img.astype(np.int64)
+    a = np.zeros(len(xs), np.int64)
+    b = np.zeros(len(xs), np.int64)
+    c = np.zeros(len(xs), np.int64)
+    for v in range(-3, 4):
+        for u in range(-3, 4):
+            y, x = ys + v, xs + u
+            ix = (im[y, x + 1] - im[y, x - 1]) * 2 + (im[y - 1, x + 1] - im[y - 1, x - 1]) + (im[y + 1, x + 1] - im[y + 1, x - 1])
+            iy = (im[y + 1, x] - im[y - 1, x]) * 2 + (im[y + 1, x - 1] - im[y - 1, x - 1]) + (im[y + 1, x + 1] - im[y - 1, x + 1])
+            a += ix * ix
+            b += iy * iy
+            c += ix * iy
+    f32 = np.float32
+    sc = f32(1.0) / (f32(28) * f32(255.0))
+    s4 = sc * sc * sc * sc
+    fa, fb, fc = a.astype(f32), b.astype(f32), c.astype(f32)
+    k = f32(0.04)
+    return ((fa * fb - fc * fc - k * (fa + fb) * (fa + fb)) * s4).astype(f32)
+
+
+def _retain_best(rows, m, key):
+    """KeyPointsFilter::retainBest: order (value desc, y, x), keep m plus every point tied with the m-th."""
+    rows = sorted(rows, key=lambda r: (-key(r), r[1], r[0]))
+    if len(rows) <= m:
+        return rows
+    if m <= 0:
+        return []
+    cut = key(rows[m - 1])
+    e = m
+    while e < len(rows) and key(rows[e]) >= cut:
+        e += 1
+    return rows[:e]
+
+
+def orb_angle(img, x, y, umax):
+    m01 = m10 = 0
+    for v in range(-ORB_HALF, ORB_HALF + 1):
+        d = umax[abs(v)]
+        row = img[y + v, x - d:x + d + 1].astype(np.int64)
+        u = np.arange(-d, d + 1)
+        m10 += int((u * row).sum())
+        m01 += int(v * row.sum())
+    ang = math.atan2(float(m01), float(m10)) * (180.0 / 3.14159265358979323846)
+    if ang < 0:
+        ang += 360.0
+    return ang
+
+
+def orb_detect_compute(img, nfeatures=500, descriptor="orb"):
+    """GPU ptz_orb restated: returns (kp [n, 6] float32 = x, y, size, angle, response, octave; descriptors
+    [n, 32] (orb) or [n, 64] (latch) uint8), every tie at the per-level cuts kept, order (level, response
+    desc, y, x)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W = img.shape
+    pat, trip = orb_tables()
+    umax = orb_umax()
+    per = orb_level_counts(nfeatures)
+    levels = [img]
+    for l in range(1, ORB_LEVELS):
+        sc = orb_scale(l)
+        lw = int(np.rint(np.float32(W) / sc))
+        lh = int(np.rint(np.float32(H) / sc))
+        levels.append(orb_resize(levels[-1], lw, lh))
+    fin = []
+    for l, im in enumerate(levels):
+        pts = fast_nms_points(fast_score(im))
+        rows = [(int(x), int(y), float(s)) for x, y, s in pts]
+        rows = _retain_best(rows, 2 * per[l], key=lambda r: r[2])
+        if not rows:
+            continue
+        xs = np.array([r[0] for r in rows])
+        ys = np.array([r[1] for r in rows])
+        hr = orb_harris(im, xs, ys)
+        rows = [(r[0], r[1], float(v)) for r, v in zip(rows, hr)]
+        rows = _retain_best(rows, per[l], key=lambda r: r[2])
+        fin += [(x, y, l, r) for x, y, r in rows]
+    if descriptor == "latch":
+        keep = []
+        for x, y, l, r in fin:
+            sc = orb_scale(l)
+            X, Y = np.float32(x) * sc, np.float32(y) * sc
+            if X >= LATCH_BORDER and Y >= LATCH_BORDER and X < W - LATCH_BORDER and Y < H - LATCH_BORDER:
+                keep.append((x, y, l, r))
+        fin = keep
+        lblur = orb_blur(img, 13, 2.0).astype(np.int64)
+    else:
+        blurs = [orb_blur(im, 7, 2.0).astype(np.int64) for im in levels]
+    nb = 64 if descriptor == "latch" else 32
+    kp = np.zeros((len(fin), 6), np.float32)
+    des = np.zeros((len(fin), nb), np.uint8)
+    for i, (x, y, l, r) in enumerate(fin):
+        ang = orb_angle(levels[l], x, y, umax)
+        rad = ang * (3.14159265358979323846 / 180.0)
+        ca, sa = math.cos(rad), math.sin(rad)
+
+        def rot(p, q):
+            return int(np.rint(p * ca - q * sa)), int(np.rint(p * sa + q * ca))
+
+        bits = []
+        if descriptor == "latch":
+            sc = orb_scale(l)
+            cx, cy = int(np.rint(np.float32(x) * sc)), int(np.rint(np.float32(y) * sc))
+            for t in trip:
+                ax, ay = rot(t[0], t[1])
+                bx, by = rot(t[2], t[3])
+                ex, ey = rot(t[4], t[5])
+                A = lblur[cy + ay - 3:cy + ay + 4, cx + ax - 3:cx + ax + 4]
+                B = lblur[cy + by - 3:cy + by + 4, cx + bx - 3:cx + bx + 4]
+                E = lblur[cy + ey - 3:cy + ey + 4, cx + ex - 3:cx + ex + 4]
+                bits.append(int(((A - B) ** 2).sum()) < int(((A - E) ** 2).sum()))
+        else:
+            bl = blurs[l]
+            for p in pat:
+                x0, y0 = rot(p[0], p[1])
+                x1, y1 = rot(p[2], p[3])
+                bits.append(bl[y + y0, x + x0] < bl[y + y1, x + x1])
+        bits = np.array(bits, np.uint8).reshape(nb, 8)
+        des[i] = (bits << np.arange(8, dtype=np.uint8)).sum(1).astype(np.uint8)
+        sc = orb_scale(l)
+        kp[i] = [np.float32(x) * sc, np.float32(y) * sc, np.float32(31.0) * sc, np.float32(ang), np.float32(r), l]
+    return kp, des

@@ -6,12 +6,14 @@ is not in this image, so the front-end the demo uses runs on the GPU through lib
   * detect_compute_sift / detect_sift / detect_compute_sift_array  -> ptz_sift (OpenCV's SIFT defaults);
   * match_sift_features   -> ptz_match_knn2 (BF kNN-2) + the 0.7 ratio test + homography_ransac;
   * match_orb_features / match_latch_features -> ptz_match_hamming (cross-checked) + homography_ransac;
-  * homography_ransac     -> ptz_homography_ransac;  optical_flow_matching -> ptz_lk_track (pyramidal LK).
+  * homography_ransac     -> ptz_homography_ransac;  optical_flow_matching -> ptz_lk_track (pyramidal LK);
+  * detect_compute_orb / detect_compute_latch -> ptz_orb (OpenCV's ORB pipeline: 8-level pyramid, FAST-9,
+    Harris retain-best, intensity-centroid angle; rBRIEF 32-byte or LATCH 64-byte descriptors with generated
+    sampling tables -- OpenCV's learned tables are not available, so the bits are not cv2's).
 Their agreement with cv2's own numbers is unpinned (cv2 cannot run here): each kernel is pinned to the
 oracle's restatement of the published algorithm and to synthetic ground truth (tests/test_gpu_frontend.py).
-ORB / LATCH *detection* (detect_compute_orb / detect_compute_latch) stays a hook: a correspondence source
-(e.g. synthetic.SyntheticFrontEnd, or an OpenCV wrapper on a machine that has it) assigns it, exactly the
-way the reference's own tests monkeypatch the front-end; any of the functions above may be reassigned too.
+A correspondence source (e.g. synthetic.SyntheticFrontEnd, or an OpenCV wrapper on a machine that has it)
+may reassign any of these functions, exactly the way the reference's own tests monkeypatch the front-end.
 
 The bookkeeping of `build_matching_graph` (image_process.py:509-667) keeps the reference's exact semantics:
   * pairs i < j in order, skipped when image_match_mask[i][j] == 0;
@@ -26,14 +28,16 @@ import numpy as np
 
 
 class KeyPoint:
-    """Stand-in for cv2.KeyPoint (the reference only reads `.pt`; size / angle / response as SIFT sets them)."""
-    __slots__ = ("pt", "size", "angle", "response")
+    """Stand-in for cv2.KeyPoint (the reference only reads `.pt`; size / angle / response / octave as the
+    detectors set them)."""
+    __slots__ = ("pt", "size", "angle", "response", "octave")
 
-    def __init__(self, x, y, size=0.0, angle=-1.0, response=0.0):
+    def __init__(self, x, y, size=0.0, angle=-1.0, response=0.0, octave=0):
         self.pt = (float(x), float(y))
         self.size = float(size)
         self.angle = float(angle)
         self.response = float(response)
+        self.octave = int(octave)
 
 
 def _hook(name):
@@ -45,13 +49,43 @@ def _hook(name):
     return f
 
 
-# ---- front-end hooks (assigned by a correspondence source) ----
-detect_compute_orb = _hook("detect_compute_orb")
-detect_compute_latch = _hook("detect_compute_latch")
-# detect_compute_sift / detect_sift / match_sift_features / homography_ransac / optical_flow_matching: GPU
-# implementations below (SIFT, kNN-2 + ratio test + RANSAC, pyramidal LK); a correspondence source may
-# still assign its own
+# detect_compute_* / detect_sift / match_*_features / homography_ransac / optical_flow_matching: GPU
+# implementations below (SIFT, ORB / LATCH, kNN-2 + ratio test + RANSAC, Hamming + RANSAC, pyramidal LK); a
+# correspondence source may still assign its own
 draw_matches = None  # optional visualisation hook (bundle_adjustment.py:153-163)
+
+
+def detect_compute_orb(im, nfeatures=1000, verbose=False):
+    """image_process.py:105-126 on the GPU (libptzba ptz_orb, cv.ORB_create(nfeatures) defaults): keypoints
+    (KeyPoint with .pt, .size, .angle, .response, .octave) and descriptors [n, 32] uint8, truncated to
+    nfeatures as the reference does (the per-level cuts keep ties, so the detector may return more)."""
+    import ptzba
+    assert isinstance(im, np.ndarray)
+    assert nfeatures > 0
+    kp, des = ptzba.orb(_grey_u8(im), int(nfeatures), "orb")
+    key_point = [KeyPoint(k[0], k[1], k[2], k[3], k[4], int(k[5])) for k in kp]
+    if len(key_point) > nfeatures:
+        key_point = key_point[:nfeatures]
+        des = des[:nfeatures]
+    if verbose:
+        print('detect: %d ORB keypoints.' % len(key_point))
+    return key_point, des
+
+
+def detect_compute_latch(im, nfeatures=1500, verbose=False):
+    """image_process.py:129-155 on the GPU: ORB keypoints (cv.ORB_create(nfeatures).detect), LATCH(64)
+    descriptors [n, 64] uint8 on them (points whose 48-px patch leaves the image are dropped, as LATCH does),
+    truncated to nfeatures."""
+    import ptzba
+    assert isinstance(im, np.ndarray)
+    kp, des = ptzba.orb(_grey_u8(im), int(nfeatures) if nfeatures > 0 else 500, "latch")
+    key_point = [KeyPoint(k[0], k[1], k[2], k[3], k[4], int(k[5])) for k in kp]
+    if nfeatures > 0 and len(key_point) > nfeatures:
+        key_point = key_point[:nfeatures]
+        des = des[:nfeatures]
+    if verbose:
+        print('detect: %d LATCH keypoints.' % len(key_point))
+    return key_point, des
 
 
 def detect_compute_sift(im, nfeatures, verbose=False):

@@ -133,6 +133,7 @@ def lib():
         "ptz_homography_ransac": ([I, I64, V, V, D, I32, ctypes.c_uint64, V, V, POINTER(c_int32)], I),
         "ptz_lk_track": ([I, I32, I32, V, V, I64, V, I32, I32, I32, D, D, V, V, V], I),
         "ptz_sift": ([I, I32, I32, V, I32, I32, V, V, V, POINTER(c_int32)], I),
+        "ptz_orb": ([I, I32, I32, V, I32, I32, I32, V, V, POINTER(c_int32)], I),
         "ptz_match_hamming": ([I, I64, I64, I32, V, V, V, V, V], I),
         "ptz_py_shuffle_prefix": ([V, I64, V, I64, V], I),
         "ptz_set_order_pairs": ([I64, V, V, V, V, V], I),
@@ -182,7 +183,7 @@ EXPORTED_SYMBOLS = [
     "ptzekf_remove_rays", "ptzekf_add_rays", "ptzekf_project_visible", "ptzekf_update",
     "ptzba_partition_landmarks", "ptzba_set_exchange_hook", "ptzba_comm_unique_id", "ptzba_comm_new",
     "ptzba_comm_delete", "ptzba_comm_split", "ptzba_comm_info", "ptzba_comm_allreduce", "ptzba_attach_comm",
-    "ptzba_dist_info", "ptzba_owned_frames", "ptz_corner_min_eig",
+    "ptzba_dist_info", "ptzba_owned_frames", "ptz_corner_min_eig", "ptz_orb",
 ]
 
 
@@ -378,6 +379,31 @@ def sift(img, nfeatures=0, device=None):
         cap = n.value
     k = n.value
     return kp[:k], resp[:k], des[:k]
+
+
+def orb(img, nfeatures=500, descriptor="orb", device=None):
+    """ORB detection + ORB (32-byte) or LATCH (64-byte) description on the GPU (ptz_orb; image_process.py:105-155):
+    8-bit grey image [h, w].  Returns (keypoints [n, 6] float32 = x, y, size, angle, response, octave;
+    descriptors [n, 32 | 64] uint8), ordered by level, then response.  Every tie at the per-level cuts is kept,
+    so n may exceed nfeatures (the reference truncates; image_process.detect_compute_orb does)."""
+    a = np.ascontiguousarray(img, dtype=np.uint8)
+    if a.ndim != 2:
+        raise ValueError("orb expects a 2-D 8-bit grey image")
+    kind = {"orb": 0, "latch": 1}[descriptor]
+    nb = 64 if kind else 32
+    dev = default_device() if device is None else device
+    n = c_int32(0)
+    cap = max(2 * int(nfeatures), 64)
+    while True:
+        kp = np.zeros((cap, 6), np.float32)
+        des = np.zeros((cap, nb), np.uint8)
+        _check(lib().ptz_orb(dev, a.shape[1], a.shape[0], _ptr(a), int(nfeatures), kind, cap, _ptr(kp), _ptr(des),
+                             ctypes.byref(n)), "ptz_orb")
+        if n.value <= cap:
+            break
+        cap = n.value
+    k = n.value
+    return kp[:k], des[:k]
 
 
 def refine_poses(u, v, init_ptz, rays, points, subsets=None, ftol=1e-4, xtol=1e-8, max_iter=100, loss=LOSS_LINEAR,

@@ -92,3 +92,40 @@ def test_hamming_cross_oracle_matches_bruteforce():
     nn21 = [min(range(len(a)), key=lambda i: (D[i, j], i)) for j in range(len(b))]
     exp = [i for i in range(len(a)) if nn21[nn12[i]] == i]
     assert q.tolist() == exp and t.tolist() == [nn12[i] for i in exp] and d.tolist() == [D[i, nn12[i]] for i in exp]
+
+
+def test_orb_oracle_building_blocks():
+    """The ORB restatement's pieces against first principles: FAST scores equal a per-pixel brute force of
+    the corner definition (largest t with 9 contiguous circle pixels all > p + t or all < p - t), the
+    resize is the identity at scale 1 and exact on constant images, the per-level split sums to nfeatures,
+    the sampling tables are in range, and the umax rows are OpenCV's for a 31-px patch."""
+    from oracle import ptz_oracle as orc
+    rng = np.random.default_rng(5)
+    img = rng.integers(0, 256, (24, 26)).astype(np.uint8)
+    img[8:16, 8:16] = 250
+    s = orc.fast_score(img, 20)
+    circ = list(zip(orc._FAST_DX, orc._FAST_DY))
+    for y in range(3, 21):
+        for x in range(3, 23):
+            p = int(img[y, x])
+            best = 0
+            for t in range(20, 256):
+                ok = False
+                for k in range(16):
+                    arc = [int(img[y + circ[(k + m) % 16][1], x + circ[(k + m) % 16][0]]) for m in range(9)]
+                    if all(v > p + t for v in arc) or all(v < p - t for v in arc):
+                        ok = True
+                        break
+                if not ok:
+                    break
+                best = t
+            assert s[y, x] == best, (x, y, s[y, x], best)
+    assert (s[:3] == 0).all() and (s[:, -3:] == 0).all()
+    assert np.array_equal(orc.orb_resize(img, 26, 24), img)
+    assert (orc.orb_resize(np.full((50, 60), 77, np.uint8), 41, 33) == 77).all()
+    for nf in (500, 1000, 1500, 5000, 6000):
+        assert sum(orc.orb_level_counts(nf)) == nf
+    pat, trip = orc.orb_tables()
+    assert pat.shape == (256, 4) and np.abs(pat).max() <= 13 and 4.5 < np.abs(pat).mean() < 6.0
+    assert trip.shape == (512, 6) and ((trip[:, 0::2] ** 2 + trip[:, 1::2] ** 2) <= 361).all()
+    assert orc.orb_umax()[:16] == [15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3]

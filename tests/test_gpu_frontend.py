@@ -302,3 +302,46 @@ def test_detect_harris_corner_grid(gpu_available):
     assert len(image_process.detect_harris_corner_grid(np.full((120, 160), 77, np.uint8), 2, 2)) == 0
     with pytest.raises(AssertionError):
         image_process.good_homography(np.eye(3))
+
+
+@pytest.mark.parametrize("seed,w,h,nf,kind", [(21, 320, 240, 500, "orb"), (22, 257, 181, 300, "orb"),
+                                              (23, 320, 240, 500, "latch"), (24, 640, 360, 1500, "orb")])
+def test_orb_matches_oracle(gpu_available, seed, w, h, nf, kind):
+    """ptz_orb against the oracle restatement (OpenCV's ORB pipeline with generated sampling tables; parity
+    with cv2 unpinned): the integer stages (pyramid, FAST, suppression, Sobel sums, moments) and the fp32
+    Harris response follow the same operations, so the keypoint set, positions, sizes, octaves and responses
+    agree exactly; angles to 1e-6 deg (atan2 of two libraries); descriptors bit for bit."""
+    import ptzba
+    from oracle import ptz_oracle as orc
+    I, _, _ = frontend_data.textured_pair(seed=seed, width=w, height=h, d_pan=0.5, f=400.0)
+    kg, dg = ptzba.orb(I, nf, kind)
+    ko, do = orc.orb_detect_compute(I, nf, kind)
+    assert len(kg) == len(ko) > 50
+    assert np.array_equal(kg[:, [0, 1, 2, 4, 5]], ko[:, [0, 1, 2, 4, 5]])
+    da = np.abs(kg[:, 3].astype(np.float64) - ko[:, 3])
+    assert np.minimum(da, 360 - da).max() < 1e-3
+    assert dg.shape == (len(kg), 64 if kind == "latch" else 32)
+    assert np.array_equal(dg, do)
+    per = orc.orb_level_counts(nf)
+    for l in range(8):  # retain-best: n_l per level plus ties at the cut
+        assert (kg[:, 5] == l).sum() >= min(per[l], (ko[:, 5] == l).sum())
+
+
+def test_orb_front_end_recovers_homography(gpu_available):
+    """ORB / LATCH detection (image_process.detect_compute_orb / detect_compute_latch, GPU) -> cross-checked
+    Hamming matching + RANSAC (match_orb_features / match_latch_features) on two 640 x 360 views recovers the
+    true PTZ homography; nfeatures caps the count as the reference's truncation does."""
+    import image_process
+    I, J, H = frontend_data.textured_pair(seed=9, width=640, height=360, d_pan=1.2, d_tilt=-0.4, f=900.0, df=6.0)
+    for det, match, nb in ((image_process.detect_compute_orb, image_process.match_orb_features, 32),
+                           (image_process.detect_compute_latch, image_process.match_latch_features, 64)):
+        k1, d1 = det(I, 1500)
+        k2, d2 = det(J, 1500)
+        assert 300 < len(k1) <= 1500 and d1.shape == (len(k1), nb) and d1.dtype == np.uint8
+        assert all(hasattr(k, "pt") and hasattr(k, "octave") for k in k1)
+        pts1, i1, pts2, i2 = match(k1, d1, k2, d2)
+        assert len(i1) >= 60, (det.__name__, len(i1))
+        err = np.linalg.norm(frontend_data.apply_h(H, pts1) - pts2, axis=1)
+        assert np.median(err) < 1.0, (det.__name__, np.median(err))
+    kc, dc = image_process.detect_compute_orb(I, 100)
+    assert len(kc) == 100 and dc.shape == (100, 32)
