@@ -33,6 +33,8 @@ struct Rccl {
   int (*comm_destroy)(nccl_comm_t) = nullptr;
   int (*comm_split)(nccl_comm_t, int, int, nccl_comm_t*, void*) = nullptr;
   int (*all_reduce)(const void*, void*, size_t, int, int, nccl_comm_t, hipStream_t) = nullptr;
+  int (*user_rank)(nccl_comm_t, int*) = nullptr;
+  int (*count)(nccl_comm_t, int*) = nullptr;
   const char* (*error_string)(int) = nullptr;
   std::string err;
 };
@@ -57,6 +59,8 @@ Rccl& rccl() {
     r.comm_split = reinterpret_cast<decltype(r.comm_split)>(dlsym(r.so, "ncclCommSplit"));
     r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(dlsym(r.so, "ncclAllReduce"));
     r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(r.so, "ncclGetErrorString"));
+    r.user_rank = reinterpret_cast<decltype(r.user_rank)>(dlsym(r.so, "ncclCommUserRank"));
+    r.count = reinterpret_cast<decltype(r.count)>(dlsym(r.so, "ncclCommCount"));
     if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.all_reduce) {
       r.err = "RCCL library lacks ncclGetUniqueId / ncclCommInitRank / ncclCommDestroy / ncclAllReduce";
       r.so = nullptr;
@@ -136,14 +140,16 @@ ptzba_comm ptzba_comm_split(ptzba_comm parent, int32_t color, int32_t key) {
     rccl_fail("ncclCommSplit", e);
     return nullptr;
   }
-  // the new communicator's rank / size: ranks of this color ordered by key (the caller passes its parent
-  // rank as key, so the position is the count of smaller keys of the same color; recorded by the caller's
-  // ptzba_comm_info use only)
+  // the new communicator's rank / size (ranks of this color ordered by key), as RCCL reports them; -1 when
+  // this RCCL lacks ncclCommUserRank / ncclCommCount
   auto* pc = new ptzba_comm_s();
   pc->comm = c;
   pc->rank = -1;
   pc->world = -1;
   pc->device = parent->device;
+  int v = 0;
+  if (r.user_rank && r.user_rank(c, &v) == 0) pc->rank = v;
+  if (r.count && r.count(c, &v) == 0) pc->world = v;
   return pc;
 }
 

@@ -581,7 +581,15 @@ class Comm:
         c = lib().ptzba_comm_split(self.c, int(color), int(key))
         if not c:
             raise PtzbaError(f"ptzba_comm_split: {lib().ptzba_last_error().decode()}")
-        return Comm(None, -1, -1, _ptr_value=c)
+        g = Comm(None, -1, -1, _ptr_value=c)
+        g.rank, g.world = g.info()
+        return g
+
+    def info(self):
+        """(rank, world) of this communicator as RCCL reports them (-1 when unknown)."""
+        r, w = c_int32(-1), c_int32(-1)
+        _check(lib().ptzba_comm_info(self.c, ctypes.byref(r), ctypes.byref(w)), "ptzba_comm_info")
+        return r.value, w.value
 
     def allreduce(self, dev_ptr, count, stream=0):
         _check(lib().ptzba_comm_allreduce(self.c, c_void_p(dev_ptr), int(count), c_void_p(stream or 0)),

@@ -22,7 +22,9 @@ c = ptzba.Comm(uid, rank=1, world=3, device=-1)
 x = np.arange(5, dtype=np.float64)
 c.allreduce(x.ctypes.data, len(x))          # the stub sums 3 identical contributions
 assert np.array_equal(x, 3 * np.arange(5)), x
+assert c.info() == (1, 3), c.info()
 g = c.split(color=1, key=1)
+assert g.info() == (1, 2) and (g.rank, g.world) == (1, 2), g.info()   # reported by RCCL for the new comm
 y = np.ones(4)
 g.allreduce(y.ctypes.data, 4)
 assert np.array_equal(y, 2 * np.ones(4)), y   # the stub's split keeps (3 + 1) // 2 ranks
