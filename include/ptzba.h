@@ -81,6 +81,20 @@ typedef struct {
  * a single-process problem.
  * mode_out: 1 part-owned, 0 replicated; rank_of_landmark [n_landmark] (landmarks without records: -1);
  * split_out[3] (may be NULL) = (m, c_end, n_pose): A = [n_fixed, m), C = [m, c_end), B = [c_end, n_pose). */
+/* host only: the system order and factorisation plan ptzba_set_problem chooses for a coupling window
+ * (frame_win_hi[f] = last frame coupled to f, e.g. from ptzba_coupling_window) and ordering.  out8: [0] n_aug,
+ * [1] ld, [2] factorisation levels, [3] dissection levels (0 natural, 1, 2), [4] back-substitution chains,
+ * [5] longest chain (tile columns), [6] blocked back-solve steps (0: none), [7] most tasks in one level
+ * | (second update-panel pair in use) << 32. */
+PTZBA_EXPORT int ptzba_plan_summary(int32_t n_pose, int32_t n_fixed, const int32_t* frame_win_hi, int32_t ordering,
+                                    int64_t* out8);
+/* host only: the same choice's frame positions pos_out[n_pose] (system row of each frame's pan, -1 fixed), the
+ * factorisation tasks (int4 records {type | panels 2, 3; i; j; panels 0, 1}, tasks_cap records) and level
+ * offsets (levels_cap >= levels + 1).  counts: [0] tasks, [1] levels, [2] n_aug, [3] second panel pair in use.
+ * Call with null outputs to size them. */
+PTZBA_EXPORT int ptzba_plan_export(int32_t n_pose, int32_t n_fixed, const int32_t* frame_win_hi, int32_t ordering,
+                                   int32_t* pos_out, int32_t* tasks_out, int64_t tasks_cap, int32_t* level_off_out,
+                                   int64_t levels_cap, int64_t* counts);
 PTZBA_EXPORT int ptzba_partition_landmarks(int32_t n_pose, int32_t n_landmark, int64_t n_obs, const int32_t* obs_frame,
                                            const int32_t* obs_landmark, int32_t n_fixed, int32_t world,
                                            int32_t* rank_of_landmark, int32_t* mode_out, int32_t* split_out);
@@ -117,7 +131,7 @@ PTZBA_EXPORT int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_lan
  * [7] bytes of device memory held */
 PTZBA_EXPORT int ptzba_problem_info(ptzba_handle h, int64_t* info8);
 /* solver layout: [0] n_aug (system rows incl. padding), [1] ld, [2] factorisation launches (levels),
- * [3] ordering actually used (PTZBA_ORDER_*), [4] back-substitution form (0 lookahead, 1 left-looking:
+ * [3] ordering actually used (PTZBA_ORDER_*) | dissection levels << 8 (0 natural, 1 or 2), [4] back-substitution form (0 lookahead, 1 left-looking:
  * systems whose lists exceed LDS), [5] dense landmark x frame slots, [6] Schur work items,
  * [7] factor pattern tiles */
 PTZBA_EXPORT int ptzba_solver_info(ptzba_handle h, int64_t* info8);

@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <numeric>
 #include <string>
 #include <utility>
@@ -75,6 +76,7 @@ struct ptzba_ctx {
   int n_tinv_tail = 0;
   int chol_levels = 0, n_aug = 0, n_chain = 1;
   bool nested = false;
+  int nd_depth = 0;  // dissection levels of the system order (SysOrder::nd_depth)
   DBuf frame_pos, row_pad, bs_chain_off, bs_chain_cols, bs_upd_off, bs_upd_tiles, bs_la_tasks;
   int bs_nupd = 0, bs_npos = 0, bs_ntasks = 0;
   DBuf bs_lo_off, bs_lo_tiles;  // left-looking back substitution lists (large systems)
@@ -258,6 +260,10 @@ static int upload(DBuf& b, const std::vector<T>& v, hipStream_t st = nullptr) {
 // system order of the reduced camera system and the tile-level factorisation plan
 // ------------------------------------------------------------------------------------------------
 static int pad_tile(int x) { return (x + CHOL_NB - 1) / CHOL_NB * CHOL_NB; }
+static bool getenv_is(const char* name, const char* value) {
+  const char* e = getenv(name);
+  return e && std::string(e) == value;
+}
 
 struct SysOrder {
   std::vector<int32_t> pos;  // [n_pose] system row of the frame's pan (-1: fixed)
@@ -266,6 +272,11 @@ struct SysOrder {
   bool nested = false;
   int tiles_a = 0, tiles_b = 0;  // nested: tile columns of parts A and B (C follows)
   int split_m = 0, split_cend = 0;  // nested: A = [nf, m), C = [m, c_end), B = [c_end, n_pose)
+  // separator tree of a nested order (tile-column ranges [t0, t1); parent -1 = the root separator): the
+  // back-substitution chains are its root-to-leaf paths, the blocked back-solve's phases its depths
+  struct Node { int t0, t1, parent; };
+  std::vector<Node> nodes;
+  int nd_depth = 0;  // 0 natural, 1 = [A | B reversed | C], 2 = two dissection levels (nested_order2)
 };
 
 static SysOrder natural_order(int n_pose, int nf) {
@@ -329,6 +340,70 @@ static bool nested_order(int n_pose, int nf, const std::vector<int32_t>& win, Sy
   o.tiles_b = bp / CHOL_NB;
   o.split_m = m;
   o.split_cend = cend;
+  o.nd_depth = 1;
+  const int c0 = o.tiles_a + o.tiles_b;
+  o.nodes = {{c0, o.n_aug / CHOL_NB, -1}, {0, o.tiles_a, 0}, {o.tiles_a, c0, 0}};
+  return true;
+}
+
+// Two levels of nested dissection (round 3): the top separator C2 = [m, cend) splits the chain into halves,
+// each half is split again by its most balanced separator: A1 | C1 | A2 | C2 | A3 | C3 | A4.  System order
+// [A1 | A2 | A3 | A4 reversed | C1 | C3 | C2], each part padded to whole tiles: the four leaves factor side by
+// side, then C1 and C3, then C2 -- a critical path of max(leaf) + sub-separator + top separator tile columns
+// instead of max(A, B) + C (config 3: 26 instead of 30 levels), and four back-substitution chains C2 -> C1 ->
+// A1 / A2, C2 -> C3 -> A3 / A4.  A leaf couples only to its ancestors: A1 to C1, A2 to C1 and C2, A3 to C2
+// and C3, A4 to C3 (and, where the window reaches that far, C2).  The top split minimises the estimated chain.
+static bool nested_order2(int n_pose, int nf, const std::vector<int32_t>& win, SysOrder& o) {
+  if (n_pose - nf < 32) return false;
+  std::vector<int> pmax(n_pose + 1, -1);
+  for (int f = nf; f < n_pose; ++f) pmax[f + 1] = std::max(pmax[f], (int)win[f]);
+  auto tiles = [](int a, int b) { return pad_tile(3 * (b - a)) / CHOL_NB; };
+  // most balanced split of [lo, hi) by a separator [m1, c1) (running coupling max from lo); false if none
+  auto balanced = [&](int lo, int hi, int& m1_out, int& c1_out) {
+    int best = INT32_MAX, run = -1;
+    for (int m1 = lo + 1; m1 < hi; ++m1) {
+      run = std::max(run, (int)win[m1 - 1]);
+      const int c1 = std::max(m1, run + 1);
+      if (c1 >= hi) break;
+      const int d = std::abs((m1 - lo) - (hi - c1));
+      if (d < best) { best = d; m1_out = m1; c1_out = c1; }
+    }
+    return best != INT32_MAX;
+  };
+  int best = INT32_MAX, bm = -1, bc = -1, b1 = -1, bc1 = -1, b3 = -1, bc3 = -1;
+  for (int m = nf + 2; m < n_pose - 1; ++m) {
+    const int cend = std::max(m, pmax[m] + 1);
+    if (cend >= n_pose - 1) break;
+    int m1, c1, m3, c3;
+    if (!balanced(nf, m, m1, c1) || !balanced(cend, n_pose, m3, c3)) continue;
+    const int est = std::max(std::max(tiles(nf, m1), tiles(c1, m)) + tiles(m1, c1),
+                             std::max(tiles(cend, m3), tiles(c3, n_pose)) + tiles(m3, c3)) + tiles(m, cend) + 1;
+    if (est < best) { best = est; bm = m; bc = cend; b1 = m1; bc1 = c1; b3 = m3; bc3 = c3; }
+  }
+  if (bm < 0) return false;
+  // parts in system order: {first frame, end frame, reversed}
+  const int parts[7][3] = {{nf, b1, 0}, {bc1, bm, 0}, {bc, b3, 0}, {bc3, n_pose, 1}, {b1, bc1, 0}, {b3, bc3, 0}, {bm, bc, 0}};
+  o = SysOrder{};
+  o.pos.assign(n_pose, -1);
+  int row = 0, t[8];
+  std::vector<std::pair<int, int>> pad_ranges;
+  for (int p = 0; p < 7; ++p) {
+    const int a = parts[p][0], b = parts[p][1], nr = 3 * (b - a);
+    t[p] = row / CHOL_NB;
+    for (int f = a; f < b; ++f) o.pos[f] = row + 3 * (parts[p][2] ? (b - 1 - f) : (f - a));
+    pad_ranges.push_back({row + nr, row + pad_tile(nr)});
+    row += pad_tile(nr);
+  }
+  t[7] = row / CHOL_NB;
+  o.n_aug = row;
+  o.pad.assign(o.n_aug, 0);
+  for (auto& pr : pad_ranges)
+    for (int r = pr.first; r < pr.second; ++r) o.pad[r] = 1;
+  o.nested = true;
+  o.nd_depth = 2;
+  // nodes: 0 = C2 (root), 1 = C1, 2 = C3, 3..6 = A1..A4
+  o.nodes = {{t[6], t[7], -1}, {t[4], t[5], 0}, {t[5], t[6], 0},
+             {t[0], t[1], 1}, {t[1], t[2], 1}, {t[2], t[3], 2}, {t[3], t[4], 2}};
   return true;
 }
 
@@ -367,25 +442,14 @@ struct CholPlan {
 // coupled to them (one workgroup per (block, t): a plain read-modify-write of r_t, as no two tasks of a
 // step share a target and steps are stream-ordered).  First-touch flags make a column's first read take
 // the forward-substitution result y (the factor's augmented row) instead of r, so r needs no init launch.
-static void make_bs_steps(const std::vector<std::vector<uint8_t>>& nz, int Tx, CholPlan& P) {
+// phases: the separator tree's depths (root separator first), each a list of sequences (tile columns in
+// back-substitution order) that advance in lockstep.
+typedef std::vector<std::vector<std::vector<int>>> BsPhases;
+static void make_bs_steps(const std::vector<std::vector<uint8_t>>& nz, int Tx, CholPlan& P, const BsPhases& phases) {
   P.bsb_tasks.clear();
   P.bsb_step_off.assign(1, 0);
   const int T = (int)nz.size(), nch = (int)P.chain_off.size() - 1;
   if (nch < 1) return;
-  std::vector<std::vector<int>> ch(nch);
-  for (int c = 0; c < nch; ++c) ch[c].assign(P.chain_cols.begin() + P.chain_off[c], P.chain_cols.begin() + P.chain_off[c + 1]);
-  size_t pre = 0;
-  while (true) {
-    bool same = pre < ch[0].size();
-    for (int c = 1; c < nch && same; ++c) same = pre < ch[c].size() && ch[c][pre] == ch[0][pre];
-    if (!same) break;
-    ++pre;
-  }
-  std::vector<std::vector<std::vector<int>>> phases;  // phase -> sequences advancing in lockstep
-  phases.push_back({std::vector<int>(ch[0].begin(), ch[0].begin() + pre)});
-  phases.emplace_back();
-  for (int c = 0; c < nch; ++c)
-    if (ch[c].size() > pre) phases[1].emplace_back(ch[c].begin() + pre, ch[c].end());
   std::vector<uint8_t> in_any(T, 0), solved(T, 0), touched(T, 0);
   for (int kt : P.chain_cols) in_any[kt] = 1;
   auto fail = [&]() {
@@ -442,7 +506,8 @@ static void make_bs_steps(const std::vector<std::vector<uint8_t>>& nz, int Tx, C
 
 // Tile structure (coupled frame pairs + the dense augmented row + symbolic fill), elimination levels
 // (at most two tile columns per level), tasks per level and back-substitution chains.
-static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<int32_t>& win, int64_t ld, CholPlan& P) {
+static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<int32_t>& win, int64_t ld, CholPlan& P,
+                      int force_dt = 0) {
   const int T = (int)(ld / CHOL_NB);
   std::vector<std::vector<uint8_t>> nz(T, std::vector<uint8_t>(T, 0));
   auto mark = [&](int r, int c) {
@@ -474,7 +539,7 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
     int L = 0;
     for (int p = 0; p < k; ++p)
       if (nz[k][p]) L = std::max(L, level[p] + 1);
-    while (L < (int)count.size() && count[L] >= 2) ++L;  // at most two columns per launch
+    while (L < (int)count.size() && count[L] >= 4) ++L;  // at most four columns per launch
     if (L >= (int)count.size()) count.resize(L + 1, 0);
     count[L]++;
     level[k] = L;
@@ -510,7 +575,9 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
   }
   int DT = trail > 600 * (int64_t)nL ? 2 : 1;
   if (const char* e = getenv("PTZBA_CHOL_DELAY")) DT = std::max(1, std::min(2, atoi(e)));  // A/B knob
+  if (force_dt) DT = force_dt;
   P.delayed = DT > 1;
+  size_t max_pd = 0;  // update panels of one task: the P2 kernel takes up to four (any DT), the other two
   auto pack2 = [](int type, const std::vector<int>& pd, int tm) {  // int4 task: x (type + panels 2, 3), w (0, 1)
     return std::make_pair(chol_pack_type(type, pd.size() > 2 ? pd[2] : -1, pd.size() > 3 ? pd[3] : -1, (tm >> 2) & 3),
                           chol_pack_updates(pd.size() > 0 ? pd[0] : -1, pd.size() > 1 ? pd[1] : -1, tm & 3));
@@ -534,6 +601,7 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
         const auto w = pack2(0, pd, tm);
         push(w.first, i, k, w.second);
       }
+      max_pd = std::max(max_pd, pd.size());
     }
     // trailing updates from the panels of levels [L - DT, L - 1] into tiles of columns factored after L
     std::vector<std::pair<int64_t, int>> upd;  // (tile key, panel)
@@ -548,15 +616,53 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
               if (level[R[y]] > L) upd.push_back({(int64_t)R[x] * T + R[y], pp});
         }
     std::sort(upd.begin(), upd.end());
+    // per tile its panels (ascending); with delayed updates the tiles are grouped into 2 x 2 blocks
+    // (rows 2a, 2a + 1 x columns 2b, 2b + 1): one type-3 task per block stages each panel's four row tiles
+    // once for up to four output tiles (~6 tile loads per output tile instead of ~10).  A block's panel set
+    // is the union of its tiles' sets (at most four); a panel a tile is not coupled to has a zero L tile
+    // there, so its product adds exact zeros -- the same arithmetic, in the same panel order, as one task
+    // per tile.  PTZBA_CHOL_BLOCKS=0: one task per tile (A/B knob).
+    std::map<int64_t, std::pair<int, std::vector<int>>> blocks;  // block key -> (tile mask, panel union)
+    std::vector<std::pair<int, int>> single;                      // tiles emitted one by one (key index)
+    std::vector<std::pair<int64_t, std::vector<int>>> tiles_pd;
     for (size_t x = 0; x < upd.size();) {
       size_t y = x + 1;
       while (y < upd.size() && upd[y].first == upd[x].first) ++y;
-      const int i = (int)(upd[x].first / T), j = (int)(upd[x].first % T);
       std::vector<int> pd;
       for (size_t u = x; u < y; ++u) pd.push_back(upd[u].second);
-      const auto w = pack2(1, pd, 15);
-      push(w.first, i, j, w.second);
+      max_pd = std::max(max_pd, pd.size());
+      tiles_pd.push_back({upd[x].first, pd});
       x = y;
+    }
+    const bool blocked = DT > 1 && !getenv_is("PTZBA_CHOL_BLOCKS", "0");
+    std::vector<uint8_t> in_block(tiles_pd.size(), 0);
+    if (blocked) {
+      for (size_t q = 0; q < tiles_pd.size(); ++q) {
+        const int i = (int)(tiles_pd[q].first / T), j = (int)(tiles_pd[q].first % T);
+        auto& b = blocks[(int64_t)(i / 2) * T + j / 2];
+        b.first |= 1 << (2 * (i & 1) + (j & 1));
+        for (int pp : tiles_pd[q].second)
+          if (std::find(b.second.begin(), b.second.end(), pp) == b.second.end()) b.second.push_back(pp);
+      }
+      for (size_t q = 0; q < tiles_pd.size(); ++q) {
+        const int i = (int)(tiles_pd[q].first / T), j = (int)(tiles_pd[q].first % T);
+        const auto& b = blocks[(int64_t)(i / 2) * T + j / 2];
+        in_block[q] = b.second.size() <= 4 && __builtin_popcount(b.first) >= 2;
+      }
+      for (auto& kv : blocks) {
+        if (kv.second.second.size() > 4 || __builtin_popcount(kv.second.first) < 2) continue;
+        std::vector<int> pd = kv.second.second;
+        std::sort(pd.begin(), pd.end());
+        const int a = (int)(kv.first / T), bcol = (int)(kv.first % T), mask = kv.second.first;
+        push(chol_pack_type(3, pd.size() > 2 ? pd[2] : -1, pd.size() > 3 ? pd[3] : -1, (mask >> 2) & 3), 2 * a, 2 * bcol,
+             chol_pack_updates(pd.size() > 0 ? pd[0] : -1, pd.size() > 1 ? pd[1] : -1, mask & 3));
+      }
+    }
+    for (size_t q = 0; q < tiles_pd.size(); ++q) {
+      if (in_block[q]) continue;
+      const int i = (int)(tiles_pd[q].first / T), j = (int)(tiles_pd[q].first % T);
+      const auto w = pack2(1, tiles_pd[q].second, 15);
+      push(w.first, i, j, w.second);
     }
     if (tinv_split)
       for (int pp : prev)
@@ -566,22 +672,62 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
     if (!tinv_split || level[k] == nL - 1) P.tinv_tail.push_back(k);
   P.level_off[nL] = (int)(P.tasks.size() / 4);
   P.n_levels = nL;
+  if (getenv("PTZBA_PLAN_DEBUG")) {  // per level: columns, tasks (panel / trailing / inverse)
+    for (int L = 0; L < nL; ++L) {
+      int n[3] = {0, 0, 0};
+      for (int q = P.level_off[L]; q < P.level_off[L + 1]; ++q) n[P.tasks[4 * q] & 3]++;
+      fprintf(stderr, "level %d cols", L);
+      for (int k : K[L]) fprintf(stderr, " %d", k);
+      fprintf(stderr, " | panel %d trailing %d inv %d\n", n[0], n[1], n[2]);
+    }
+    fprintf(stderr, "max panels per task %zu\n", max_pd);
+  }
+  if (max_pd > 4) return DT > 1 ? make_plan(o, n_pose, nf, win, ld, P, 1) : false;  // too many panels: DT = 1
+  if (max_pd > 2) P.delayed = true;  // the P2 kernel (second panel pair) also at DT = 1
   // back-substitution: chains of tile columns holding unknowns and, per chain position, the chain's
-  // later columns coupled to that row tile (right-looking updates)
+  // later columns coupled to that row tile (right-looking updates).  Nested orders: one chain per leaf of
+  // the separator tree (its root-to-leaf path, each node's columns descending); natural: one chain.
   const int Tx = (o.n_aug + CHOL_NB - 1) / CHOL_NB;
   P.chain_off.assign(1, 0);
   P.chain_cols.clear();
-  if (o.nested) {
-    const int c0 = o.tiles_a + o.tiles_b;
-    for (int part = 0; part < 2; ++part) {
-      for (int kt = Tx - 1; kt >= c0; --kt) P.chain_cols.push_back(kt);
-      const int lo = part == 0 ? 0 : o.tiles_a, hi = part == 0 ? o.tiles_a : c0;
-      for (int kt = hi - 1; kt >= lo; --kt) P.chain_cols.push_back(kt);
+  BsPhases phases;
+  if (o.nested && !o.nodes.empty()) {
+    const int nn = (int)o.nodes.size();
+    std::vector<int> depth(nn, 0), nchild(nn, 0);
+    for (int v = 0; v < nn; ++v) {
+      for (int u = o.nodes[v].parent; u >= 0; u = o.nodes[u].parent) ++depth[v];
+      if (o.nodes[v].parent >= 0) ++nchild[o.nodes[v].parent];
+    }
+    auto desc = [&](int v) {
+      std::vector<int> c;
+      for (int kt = o.nodes[v].t1 - 1; kt >= o.nodes[v].t0; --kt) c.push_back(kt);
+      return c;
+    };
+    for (int v = 0; v < nn; ++v) {
+      if (nchild[v]) continue;  // leaf: the path root -> v
+      std::vector<int> path;
+      for (int u = v; u >= 0; u = o.nodes[u].parent) path.push_back(u);
+      for (auto it = path.rbegin(); it != path.rend(); ++it)
+        for (int kt : desc(*it)) P.chain_cols.push_back(kt);
       P.chain_off.push_back((int)P.chain_cols.size());
+    }
+    for (int v = 0; v < nn; ++v) {
+      if ((int)phases.size() <= depth[v]) phases.resize(depth[v] + 1);
+      phases[depth[v]].push_back(desc(v));
+    }
+    // every coupling of a chain column to a later column stays inside the chain (a leaf couples only to its
+    // ancestors); otherwise this order is unusable
+    for (size_t ch = 0; ch + 1 < P.chain_off.size(); ++ch) {
+      std::vector<uint8_t> in_chain(T, 0);
+      for (int q = P.chain_off[ch]; q < P.chain_off[ch + 1]; ++q) in_chain[P.chain_cols[q]] = 1;
+      for (int q = P.chain_off[ch]; q < P.chain_off[ch + 1]; ++q)
+        for (int i = P.chain_cols[q] + 1; i < Tx; ++i)
+          if (nz[i][P.chain_cols[q]] && !in_chain[i]) return false;
     }
   } else {
     for (int kt = Tx - 1; kt >= 0; --kt) P.chain_cols.push_back(kt);
     P.chain_off.push_back((int)P.chain_cols.size());
+    phases.push_back({P.chain_cols});
   }
   P.upd_off.assign(1, 0);
   P.upd_tiles.clear();
@@ -628,11 +774,32 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
   P.la_tasks = la;
   P.la_tasks.insert(P.la_tasks.end(), toff.begin(), toff.end());
   P.la_tasks.insert(P.la_tasks.end(), tasks.begin(), tasks.end());
-  make_bs_steps(nz, Tx, P);
+  make_bs_steps(nz, Tx, P, phases);
   return true;
 }
 
 static int ensure_group_comm(ptzba_ctx* h);
+
+// System order and plan of a single-system solve: natural, or the one-level nested order, or two dissection
+// levels when that plan has fewer levels (PTZBA_ND_DEPTH=1 / =2: A/B knob, one level only / two levels
+// whenever valid).  Returns nonzero if no plan exists.
+static int choose_order_plan(int n_pose, int nf, const std::vector<int32_t>& win, int ordering, SysOrder& so,
+                             CholPlan& plan) {
+  if (!(ordering != PTZBA_ORDER_NATURAL && nested_order(n_pose, nf, win, so, ordering == PTZBA_ORDER_NESTED_FORCE)))
+    so = natural_order(n_pose, nf);
+  if (!make_plan(so, n_pose, nf, win, pad_tile(so.n_aug + 1), plan)) return -1;
+  const char* nde = getenv("PTZBA_ND_DEPTH");
+  const int nd_env = nde ? atoi(nde) : 0;
+  SysOrder s2;
+  CholPlan p2;
+  if (ordering == PTZBA_ORDER_NESTED && nd_env != 1 && nested_order2(n_pose, nf, win, s2) &&
+      pad_tile(s2.n_aug + 1) <= CHOL_MAX_LD && make_plan(s2, n_pose, nf, win, pad_tile(s2.n_aug + 1), p2) &&
+      (p2.n_levels < plan.n_levels || nd_env == 2)) {
+    so = std::move(s2);
+    plan = std::move(p2);
+  }
+  return 0;
+}
 
 // Part-owned plan (multi-GPU, api: ptzba_partition_landmarks): this rank factors the tile columns of its
 // part (A = [0, tiles_a) or B = [tiles_a, tiles_a + tiles_b)) in phase 1, then one flush level applies
@@ -796,7 +963,7 @@ static bool make_plan_part(const SysOrder& o, int part, int n_pose, int nf, cons
   P.la_tasks = la;
   P.la_tasks.insert(P.la_tasks.end(), toff.begin(), toff.end());
   P.la_tasks.insert(P.la_tasks.end(), tasks.begin(), tasks.end());
-  make_bs_steps(nz, Tx, P);
+  make_bs_steps(nz, Tx, P, BsPhases{{P.chain_cols}});
   return true;
 }
 
@@ -1029,15 +1196,15 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   if (dist && !o.frame_win_hi) return fail("a sharded solve needs the global coupling window (frame_win_hi)");
   SysOrder sorder;
   const bool part_mode = dist && dist_order(n_pose, o.n_fixed, win, sorder);
-  if (!part_mode && !(o.ordering != PTZBA_ORDER_NATURAL &&
-                      nested_order(n_pose, o.n_fixed, win, sorder, o.ordering == PTZBA_ORDER_NESTED_FORCE)))
-    sorder = natural_order(n_pose, o.n_fixed);
+  CholPlan plan;
+  if (!part_mode && choose_order_plan(n_pose, o.n_fixed, win, o.ordering, sorder, plan))
+    return fail("factorisation plan: an update task needs more than four panels");
   h->n_aug = sorder.n_aug;
   h->nested = sorder.nested;
+  h->nd_depth = sorder.nd_depth;
   h->ld = pad_tile(h->n_aug + 1);  // + augmented rhs row
   // the back-substitution keeps x ([ld] doubles) in LDS
   if (h->ld > CHOL_MAX_LD) return fail("reduced system %d too large for the dense solver", h->n_sys);
-  CholPlan plan;
   PartPlan pplan;
   h->dist_world = dist ? o.dist_world : 1;
   h->dist_rank = dist ? o.dist_rank : 0;
@@ -1083,7 +1250,6 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     h->n_pbuf = (int64_t)h->n_ptiles * CHOL_NB * CHOL_NB + 3 * ld;
     h->n_sbuf = (int64_t)h->n_stiles * CHOL_NB * CHOL_NB + 2 * ccnt;
   } else {
-    make_plan(sorder, n_pose, o.n_fixed, win, h->ld, plan);
     h->n_ptiles = h->n_stiles = 0;
     h->n_pbuf = h->n_sbuf = 0;
   }
@@ -1294,7 +1460,7 @@ int ptzba_solver_info(ptzba_handle h, int64_t* info8) {
   info8[0] = h->n_aug;
   info8[1] = h->ld;
   info8[2] = h->chol_levels;
-  info8[3] = h->nested ? PTZBA_ORDER_NESTED : PTZBA_ORDER_NATURAL;
+  info8[3] = (h->nested ? PTZBA_ORDER_NESTED : PTZBA_ORDER_NATURAL) | ((int64_t)h->nd_depth << 8);
   info8[4] = h->bs_blk ? 2 : (h->bs_ll ? 1 : 0);
   info8[5] = h->n_slot;
   info8[6] = h->n_s2_items;
@@ -2007,6 +2173,54 @@ int ptzba_coupling_window(int32_t n_pose, int32_t n_landmark, int64_t n_obs, con
 // chain has one (landmarks seeing A to rank group 0, B to group 1, C-only landmarks to the group whose part
 // their first frame is nearer; equal-record contiguous blocks inside a group), else contiguous landmark
 // blocks of equal record counts over all ranks (replicated solve).
+// host only (no device): the order and plan set_problem would choose for a coupling window -- for tests and
+// tools (include/ptzba.h)
+int ptzba_plan_summary(int32_t n_pose, int32_t n_fixed, const int32_t* frame_win_hi, int32_t ordering, int64_t* out8) {
+  if (n_pose < 1 || n_fixed < 0 || n_fixed > n_pose || !frame_win_hi || !out8) return fail("bad arguments");
+  if (ordering < PTZBA_ORDER_NATURAL || ordering > PTZBA_ORDER_NESTED_FORCE) return fail("bad ordering %d", ordering);
+  std::vector<int32_t> win(frame_win_hi, frame_win_hi + n_pose);
+  for (int f = 0; f < n_pose; ++f)
+    if (win[f] < f || win[f] >= n_pose) return fail("frame_win_hi[%d] = %d out of range", f, win[f]);
+  SysOrder so;
+  CholPlan plan;
+  if (choose_order_plan(n_pose, n_fixed, win, ordering, so, plan)) return fail("no factorisation plan");
+  int max_tasks = 0;
+  for (int L = 0; L < plan.n_levels; ++L) max_tasks = std::max(max_tasks, plan.level_off[L + 1] - plan.level_off[L]);
+  int max_chain = 0;
+  for (size_t c = 0; c + 1 < plan.chain_off.size(); ++c) max_chain = std::max(max_chain, plan.chain_off[c + 1] - plan.chain_off[c]);
+  out8[0] = so.n_aug;
+  out8[1] = pad_tile(so.n_aug + 1);
+  out8[2] = plan.n_levels;
+  out8[3] = so.nd_depth;
+  out8[4] = (int64_t)plan.chain_off.size() - 1;
+  out8[5] = max_chain;
+  out8[6] = (int64_t)plan.bsb_step_off.size() - 1;  // blocked back-solve steps (0: no valid schedule)
+  out8[7] = max_tasks | ((int64_t)plan.delayed << 32);
+  return 0;
+}
+
+// host only: the chosen order's frame positions and the factorisation task list (int4 records, as the level
+// launches receive them) with the level offsets -- the plan a CPU executor of the tile tasks can replay
+int ptzba_plan_export(int32_t n_pose, int32_t n_fixed, const int32_t* frame_win_hi, int32_t ordering, int32_t* pos_out,
+                      int32_t* tasks_out, int64_t tasks_cap, int32_t* level_off_out, int64_t levels_cap, int64_t* counts) {
+  if (n_pose < 1 || n_fixed < 0 || n_fixed > n_pose || !frame_win_hi || !counts) return fail("bad arguments");
+  std::vector<int32_t> win(frame_win_hi, frame_win_hi + n_pose);
+  for (int f = 0; f < n_pose; ++f)
+    if (win[f] < f || win[f] >= n_pose) return fail("frame_win_hi[%d] = %d out of range", f, win[f]);
+  SysOrder so;
+  CholPlan plan;
+  if (choose_order_plan(n_pose, n_fixed, win, ordering, so, plan)) return fail("no factorisation plan");
+  const int64_t nt = (int64_t)plan.tasks.size() / 4, nl = plan.n_levels;
+  counts[0] = nt;
+  counts[1] = nl;
+  counts[2] = so.n_aug;
+  counts[3] = plan.delayed ? 1 : 0;
+  if (pos_out) std::copy(so.pos.begin(), so.pos.end(), pos_out);
+  if (tasks_out && tasks_cap >= nt) std::copy(plan.tasks.begin(), plan.tasks.end(), tasks_out);
+  if (level_off_out && levels_cap >= nl + 1) std::copy(plan.level_off.begin(), plan.level_off.end(), level_off_out);
+  return 0;
+}
+
 int ptzba_partition_landmarks(int32_t n_pose, int32_t n_landmark, int64_t n_obs, const int32_t* obs_frame,
                               const int32_t* obs_landmark, int32_t n_fixed, int32_t world, int32_t* rank_of_landmark,
                               int32_t* mode_out, int32_t* split_out) {

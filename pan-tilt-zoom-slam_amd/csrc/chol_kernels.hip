@@ -743,6 +743,82 @@ __device__ __forceinline__ void tile_inv_wave(const double* __restrict__ src, do
   }
 }
 
+// Trailing block task (type 3, plans with delayed updates): output tiles (i0 + a, j0 + b), a, b in {0, 1}, present
+// where bit 2a + b of mask is set; wave 2a + b owns tile (a, b) whole, its four 16 x 16 blocks as MFMA
+// accumulators read from and written back to memory directly.  Per update panel p (ascending, the same order as
+// the per-tile tasks) the workgroup stages the four row tiles L_{i0,p}, L_{i0+1,p} (A side) and L_{j0,p},
+// L_{j0+1,p} (B side) in LDS -- each loaded once for the (up to) two output tiles that use it -- with the next
+// panel's tiles in flight in registers.  Same MFMA sequence per output tile as tile_gemm_nt_sub: bitwise the
+// result of one task per tile.
+__device__ __forceinline__ void chol_trail_block(double* __restrict__ A, int64_t ld, int i0, int j0, int mask, int up0,
+                                                 int up1, int up2, int up3, double (*sA)[NB][NB + 1],
+                                                 double (*sB)[NB][NB + 1]) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, li = l & 15, lk = l >> 4;
+  const int64_t NBl = NB;
+  const bool mine = (mask >> w) & 1;
+  const int ta = w >> 1, tb = w & 1;
+  // which staged tiles some present output tile needs
+  const bool needA[2] = {(mask & 3) != 0, (mask & 12) != 0};
+  const bool needB[2] = {(mask & 5) != 0, (mask & 10) != 0};
+  double* C = A + (i0 + ta) * NBl * ld + (j0 + tb) * NBl;
+  v4f64 acc[2][2];
+  if (mine) {
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[x][y][r] = C[(int64_t)(16 * x + lk + 4 * r) * ld + 16 * y + li];
+  }
+  const int ups[4] = {up0, up1, up2, up3};
+  double ra[2][4], rb[2][4];  // one register set: the next panel's tiles are fetched once this one is in LDS
+  auto fetch = [&](int p) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (needA[t]) fetch_tile(ra[t], A + (i0 + t) * NBl * ld + p * NBl, ld);
+      if (needB[t]) fetch_tile(rb[t], A + (j0 + t) * NBl * ld + p * NBl, ld);
+    }
+  };
+  int u = 0;
+  while (u < 4 && ups[u] < 0) ++u;
+  if (u < 4) fetch(ups[u]);
+  while (u < 4) {
+    int un = u + 1;
+    while (un < 4 && ups[un] < 0) ++un;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (needA[t]) put_tile(sA[t], ra[t]);
+      if (needB[t]) put_tile(sB[t], rb[t]);
+    }
+    if (un < 4) fetch(ups[un]);  // in flight during this panel's MFMAs (the LDS writes above read the registers first)
+    __syncthreads();
+    if (mine) {
+      const double (*At)[NB + 1] = sA[ta];
+      const double (*Bt)[NB + 1] = sB[tb];
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+          for (int s4 = 0; s4 < NB / 4; ++s4) {
+            const double av = -At[16 * x + li][4 * s4 + lk];
+            const double bv = Bt[16 * y + li][4 * s4 + lk];
+            acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[x][y], 0, 0, 0);
+          }
+    }
+    __syncthreads();
+    u = un;
+  }
+  if (mine) {
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) C[(int64_t)(16 * x + lk + 4 * r) * ld + 16 * y + li] = acc[x][y][r];
+  }
+}
+
 struct CholTaskPtr {
   const int4* p;
   __device__ int4 get(int b) const { return p[b]; }
@@ -813,6 +889,12 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
 #if CHOL_VARIANT == 5
   return;
 #endif
+  if constexpr (P2 && !SG) {
+    if (type == 3) {  // 2 x 2 block of trailing tiles (api.hip make_plan): A_ij -= sum_p L_ip L_jp^T
+      chol_trail_block(A, ld, i, j, ((tk.w >> 28) & 3) | (((unsigned)tk.x >> 30) << 2), up0, up1, up2, up3, sA, sB);
+      return;
+    }
+  }
   double v0[4], v1[4], v2[4], v3[4], v4[4], v5[4], w2[4], w3[4], w4[4], w5[4];
   auto load_signs = [&](int ua, int ub) {  // SG: signs of the update panels' columns
     if constexpr (SG) {

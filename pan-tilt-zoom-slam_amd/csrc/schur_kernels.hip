@@ -365,6 +365,9 @@ constexpr int MKP = 40;
 #ifndef SR_UNROLL
 #define SR_UNROLL 4  // split partials in flight per thread in k_schur_reduce (4 or 8)
 #endif
+#ifndef SR_VEC
+#define SR_VEC 0  // 1: fp32 partials four elements per reduce thread with 16-B loads (r03v A/B: 77-78 vs 71 us per build, slower)
+#endif
 #ifndef MF_DIAG_FUSED
 #define MF_DIAG_FUSED 1  // chunk-0 diagonal terms inside the batch pipeline (0: a phase before it)
 #endif
@@ -770,14 +773,59 @@ __device__ __forceinline__ void schur_reduce_vec(const SchurArgs& a, const int4 
   if (a.prep.pad) a.S[a.prep.n_aug * a.ld + c0 + q2] = bv;  // fused prepare: the augmented row b^T
 }
 
-// tile reduction: thread = one element of a tile (grid: tile x 72 blocks of 256); fixed-order sum of the
-// splits, U on the diagonal blocks, write the lower triangle in the system order (mirror when f2
-// precedes f1); chunk-0 tiles also write b | g_pose | diag U of their frames.
+// Four consecutive elements (partner frames f2 .. f2 + 3 of one (f1, q, r)) per thread: the split partials
+// are read as 16-B vectors (4-B loads move a third of the bytes per request at this occupancy) and summed
+// in the same fixed item order as schur_reduce_elem, element by element -- bitwise the same S.
+__device__ __forceinline__ void schur_reduce_elem4(const SchurArgs& a, const int4 g, int e4) {
+  constexpr int NE = SF * 9 * WAVE;
+  const int e = 4 * e4;
+  const int f1b = g.x, chunk = g.y;
+  const int ln = e & 63, ik = e >> 6, i = ik / 9, k = ik - 9 * i, q = k / 3, r = k - 3 * q;
+  const int f1 = f1b + i, f20 = f1b + WAVE * chunk + ln;
+  if (f1 >= a.n_pose) return;
+  const int whi = a.frame_win_hi[f1];
+  if (f20 + 3 < f1 || f20 > whi) return;  // no element of the four is in the coupling window
+  if (f20 <= f1 && f1 <= f20 + 3) {       // the diagonal block's element is among them: the scalar path
+    for (int d = 0; d < 4; ++d) schur_reduce_elem<float, false>(a, g, e + d);
+    return;
+  }
+  const float4* p = reinterpret_cast<const float4*>((const float*)a.part + e);
+  double v[4] = {0, 0, 0, 0};
+  int it = g.z;
+  for (; it + SR_UNROLL <= g.w; it += SR_UNROLL) {
+    float4 x[SR_UNROLL];
+#pragma unroll
+    for (int u = 0; u < SR_UNROLL; ++u) x[u] = p[(int64_t)(it + u) * (NE / 4)];
+#pragma unroll
+    for (int u = 0; u < SR_UNROLL; ++u) {
+      v[0] += (double)x[u].x; v[1] += (double)x[u].y; v[2] += (double)x[u].z; v[3] += (double)x[u].w;
+    }
+  }
+  for (; it < g.w; ++it) {
+    const float4 x = p[(int64_t)it * (NE / 4)];
+    v[0] += (double)x.x; v[1] += (double)x.y; v[2] += (double)x.z; v[3] += (double)x.w;
+  }
+  const int64_t ld = a.ld, col0 = a.frame_pos[f1];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const int f2 = f20 + d;
+    if (f2 < f1 || f2 > whi) continue;  // f2 > f1 here for every element in the window
+    const int64_t pf2 = a.frame_pos[f2];
+    if (pf2 >= col0) a.S[(pf2 + r) * ld + col0 + q] = v[d];
+    else a.S[(col0 + q) * ld + pf2 + r] = v[d];
+  }
+}
+
+// tile reduction: fixed-order sum of the splits, U on the diagonal blocks, write the lower triangle in the
+// system order (mirror when f2 precedes f1); chunk-0 tiles also write b | g_pose | diag U of their frames.
+// fp32 partials: thread = four elements of a tile (grid: tile x 18 blocks of 256); fp64: one element
+// (tile x 72 blocks).
 template <typename real>
 __global__ __launch_bounds__(256) void k_schur_reduce(SchurArgs a) {
   if (a.skip_if && *a.skip_if) return;
   const int4 g = a.groups[blockIdx.y];  // {f1b, chunk, first item, end item}
-  schur_reduce_elem<real, false>(a, g, blockIdx.x * 256 + threadIdx.x);
+  if constexpr (sizeof(real) == 4 && SR_VEC) schur_reduce_elem4(a, g, blockIdx.x * 256 + threadIdx.x);
+  else schur_reduce_elem<real, false>(a, g, blockIdx.x * 256 + threadIdx.x);
   if (g.y == 0 && blockIdx.x == 0 && threadIdx.x < SF * 3) schur_reduce_vec<false>(a, g, threadIdx.x);
 }
 
@@ -795,7 +843,8 @@ void launch_schur(const SchurArgs& a, int n_items, int n_groups, int n_fixed, hi
     }
   }
   if (n_groups > 0 && !folded)
-    hipLaunchKernelGGL(k_schur_reduce<real>, dim3(SF * 9 * WAVE / 256, n_groups), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_schur_reduce<real>, dim3(SF * 9 * WAVE / (sizeof(real) == 4 && SR_VEC ? 1024 : 256), n_groups),
+                       dim3(256), 0, st, a);
 }
 
 template void launch_schur<float>(const SchurArgs&, int, int, int, hipStream_t);

@@ -129,6 +129,8 @@ def lib():
         "ptz_h_jacobian": ([I, I64, D, D, D, D, D, V, V, V], I),
         "ptzba_build_landmarks": ([I32, V, I64, V, V, V, V, V, V, V, V], I),
         "ptzba_coupling_window": ([I32, I32, I64, V, V, V], I),
+        "ptzba_plan_summary": ([I32, I32, V, I32, V], I),
+        "ptzba_plan_export": ([I32, I32, V, I32, V, V, I64, V, I64, V], I),
         "ptz_match_knn2": ([I, I64, I64, I32, V, V, V, V], I),
         "ptz_homography_ransac": ([I, I64, V, V, D, I32, ctypes.c_uint64, V, V, POINTER(c_int32)], I),
         "ptz_lk_track": ([I, I32, I32, V, V, I64, V, I32, I32, I32, D, D, V, V, V], I),
@@ -183,7 +185,8 @@ EXPORTED_SYMBOLS = [
     "ptzekf_remove_rays", "ptzekf_add_rays", "ptzekf_project_visible", "ptzekf_update",
     "ptzba_partition_landmarks", "ptzba_set_exchange_hook", "ptzba_comm_unique_id", "ptzba_comm_new",
     "ptzba_comm_delete", "ptzba_comm_split", "ptzba_comm_info", "ptzba_comm_allreduce", "ptzba_attach_comm",
-    "ptzba_dist_info", "ptzba_owned_frames", "ptz_corner_min_eig", "ptz_orb",
+    "ptzba_dist_info", "ptzba_owned_frames", "ptz_corner_min_eig", "ptz_orb", "ptzba_plan_summary",
+    "ptzba_plan_export",
 ]
 
 
@@ -543,6 +546,34 @@ def frame_coupling_window(n_pose, frame, landmark):
     return win
 
 
+def plan_summary(frame_win_hi, n_fixed=1, ordering=None):
+    """The system order and factorisation plan ptzba_set_problem would choose for a coupling window
+    (ptzba_plan_summary, host only): dict(n_aug, ld, levels, nd_depth, chains, longest_chain, bs_steps,
+    max_level_tasks, panel_pairs)."""
+    win = np.ascontiguousarray(frame_win_hi, np.int32)
+    out = np.zeros(8, np.int64)
+    _check(lib().ptzba_plan_summary(len(win), int(n_fixed), _ptr(win), ORDER_NESTED if ordering is None else int(ordering),
+                                    _ptr(out)), "ptzba_plan_summary")
+    return dict(n_aug=int(out[0]), ld=int(out[1]), levels=int(out[2]), nd_depth=int(out[3]), chains=int(out[4]),
+                longest_chain=int(out[5]), bs_steps=int(out[6]), max_level_tasks=int(out[7] & 0xFFFFFFFF),
+                panel_pairs=1 + int(out[7] >> 32))
+
+
+def plan_export(frame_win_hi, n_fixed=1, ordering=None):
+    """(pos [n_pose], tasks [n_tasks, 4] int32, level_off [levels + 1], n_aug, second_pair) of the plan
+    ptzba_set_problem would choose (ptzba_plan_export, host only) -- for replaying the tile tasks on the CPU."""
+    win = np.ascontiguousarray(frame_win_hi, np.int32)
+    o = ORDER_NESTED if ordering is None else int(ordering)
+    c = np.zeros(4, np.int64)
+    _check(lib().ptzba_plan_export(len(win), int(n_fixed), _ptr(win), o, None, None, 0, None, 0, _ptr(c)), "ptzba_plan_export")
+    pos = np.empty(len(win), np.int32)
+    tasks = np.empty((int(c[0]), 4), np.int32)
+    off = np.empty(int(c[1]) + 1, np.int32)
+    _check(lib().ptzba_plan_export(len(win), int(n_fixed), _ptr(win), o, _ptr(pos), _ptr(tasks), int(c[0]), _ptr(off),
+                                   int(c[1]) + 1, _ptr(c)), "ptzba_plan_export")
+    return pos, tasks, off, int(c[2]), bool(c[3])
+
+
 def partition_landmarks(n_pose, n_landmark, frame, landmark, world, n_fixed=1):
     """Landmark -> rank of a sharded solve (ptzba_partition_landmarks, host only): returns (rank_of_landmark
     [n_landmark] int32 (-1: no records), mode (1 part-owned, 0 replicated), (m, c_end, n_pose) split)."""
@@ -707,7 +738,7 @@ class BAHandle:
         out = np.zeros(8, np.int64)
         _check(lib().ptzba_solver_info(self.h, _ptr(out)), "ptzba_solver_info")
         return dict(n_aug=int(out[0]), ld=int(out[1]), levels=int(out[2]),
-                    ordering="nested" if out[3] != ORDER_NATURAL else "natural",
+                    ordering="nested" if (out[3] & 0xFF) != ORDER_NATURAL else "natural", nd_depth=int(out[3]) >> 8,
                     backsolve=("lookahead", "left-looking", "blocked")[int(out[4])], n_slot=int(out[5]), schur_items=int(out[6]),
                     pattern_tiles=int(out[7]))
 

@@ -192,3 +192,31 @@ def test_one_shot_solve_equals_lm_solver(gpu_available, config, precision, loss)
     assert (res.njev, res.nfev, res.status) == (ref.njev, ref.nfev, ref.status), (res, ref)
     assert res.cost == ref.cost and res.initial_cost == ref.initial_cost
     assert np.array_equal(ptz, ptz_ref) and np.array_equal(rays, rays_ref)
+
+
+def test_config3_two_level_dissection_matches_one_level(gpu_available, config3, monkeypatch):
+    """The default order at config 3 is the two-level nested dissection (26 elimination levels, four
+    back-substitution chains: api.hip nested_order2); it must give the same LM iterates as the one-level order
+    [A | B reversed | C] (PTZBA_ND_DEPTH=1): fp64 linear loss, 4 iterations, poses within 1e-9 deg / 1e-7 px,
+    rays within 1e-9 deg, same iteration count and cost to 1e-12 relative."""
+    import ptzba
+    p = config3
+    out = {}
+    for depth in ("1", "2"):
+        monkeypatch.setenv("PTZBA_ND_DEPTH", depth)
+        h = ptzba.BAHandle(0)
+        h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=ptzba.FP64)
+        info = h.solver_info()
+        assert info["nd_depth"] == int(depth), info
+        h.set_state(p.init_ptz, p.init_rays)
+        res = ptzba.LMSolver(h, ftol=1e-15, xtol=1e-15, max_iter=4).run()
+        out[depth] = (h.get_state(), res, info)
+        h.close()
+    (ptz1, rays1), r1, i1 = out["1"]
+    (ptz2, rays2), r2, i2 = out["2"]
+    assert i1["levels"] == 30 and i2["levels"] == 26, (i1, i2)
+    assert r1.njev == r2.njev and r1.nfev == r2.nfev
+    assert abs(r1.cost - r2.cost) <= 1e-12 * r1.cost
+    np.testing.assert_allclose(ptz2[:, :2], ptz1[:, :2], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(ptz2[:, 2], ptz1[:, 2], rtol=0, atol=1e-7)
+    np.testing.assert_allclose(rays2, rays1, rtol=0, atol=1e-9)

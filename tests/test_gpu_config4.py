@@ -41,7 +41,7 @@ def grid():
 
 
 @pytest.mark.parametrize("backsolve", ["lookahead", "ll", "blk"])
-@pytest.mark.parametrize("ordering", [0, 2])
+@pytest.mark.parametrize("ordering", [0, 1, 2])
 def test_grid_gauss_newton_step_is_exact(gpu_available, grid, monkeypatch, backsolve, ordering):
     import scipy.sparse.linalg as spla
     from oracle import ptz_oracle as orc
@@ -50,7 +50,29 @@ def test_grid_gauss_newton_step_is_exact(gpu_available, grid, monkeypatch, backs
         monkeypatch.setenv("PTZBA_BACKSOLVE", backsolve)
     dx_gpu, info = _gn_step(p, 0, ordering)
     assert info["backsolve"] == {"lookahead": "lookahead", "ll": "left-looking", "blk": "blocked"}[backsolve]
-    assert info["ordering"] == ("nested" if ordering == 2 else "natural")
+    if ordering != 1:  # 1: the solver's choice (natural, one or two dissection levels)
+        assert info["ordering"] == ("nested" if ordering == 2 else "natural")
+    x0 = np.concatenate([p.init_ptz[1:].reshape(-1), p.init_rays.reshape(-1)])
+    fr, lm = p.frame.astype(np.int64), p.landmark.astype(np.int64)
+    J = orc.ba_jacobian(x0, p.n_pose, p.n_landmark, p.u, p.v, p.init_ptz[0], fr, lm).tocsc()
+    r = orc.compute_residual_records(np.concatenate([p.init_ptz[0], x0]), p.n_pose, p.u, p.v, fr, lm, p.xy)
+    dx = spla.spsolve((J.T @ J).tocsc(), -(J.T @ r))
+    err = np.abs(dx_gpu - dx).max() / np.abs(dx).max()
+    assert err < 1e-7, err
+
+
+@pytest.mark.parametrize("blocks", ["1", "0"])
+@pytest.mark.parametrize("ordering", [0, 1, 2])
+def test_grid_delayed_trailing_updates_exact(gpu_available, grid, monkeypatch, ordering, blocks):
+    """The factorisation with delayed trailing updates (PTZBA_CHOL_DELAY=2: trailing tasks every other level,
+    up to four update panels per task; config 4's default), with the trailing tiles in 2 x 2 block tasks (the
+    default) or one task per tile (PTZBA_CHOL_BLOCKS=0), gives the same exact Gauss-Newton step."""
+    import scipy.sparse.linalg as spla
+    from oracle import ptz_oracle as orc
+    p = grid
+    monkeypatch.setenv("PTZBA_CHOL_DELAY", "2")
+    monkeypatch.setenv("PTZBA_CHOL_BLOCKS", blocks)
+    dx_gpu, info = _gn_step(p, 0, ordering)
     x0 = np.concatenate([p.init_ptz[1:].reshape(-1), p.init_rays.reshape(-1)])
     fr, lm = p.frame.astype(np.int64), p.landmark.astype(np.int64)
     J = orc.ba_jacobian(x0, p.n_pose, p.n_landmark, p.u, p.v, p.init_ptz[0], fr, lm).tocsc()
@@ -61,21 +83,15 @@ def test_grid_gauss_newton_step_is_exact(gpu_available, grid, monkeypatch, backs
 
 
 @pytest.mark.parametrize("ordering", [0, 2])
-def test_grid_delayed_trailing_updates_exact(gpu_available, grid, monkeypatch, ordering):
-    """The factorisation with delayed trailing updates (PTZBA_CHOL_DELAY=2: trailing tasks every other level,
-    up to four update panels per task; config 4's default) gives the same exact Gauss-Newton step."""
-    import scipy.sparse.linalg as spla
-    from oracle import ptz_oracle as orc
-    p = grid
+def test_grid_trailing_blocks_bitwise_equal_per_tile_tasks(gpu_available, grid, monkeypatch, ordering):
+    """2 x 2 trailing-block tasks apply the union of their tiles' update panels in the same order as one task per
+    tile (the extra panels multiply zero tiles): the Gauss-Newton step is bitwise the same."""
     monkeypatch.setenv("PTZBA_CHOL_DELAY", "2")
-    dx_gpu, info = _gn_step(p, 0, ordering)
-    x0 = np.concatenate([p.init_ptz[1:].reshape(-1), p.init_rays.reshape(-1)])
-    fr, lm = p.frame.astype(np.int64), p.landmark.astype(np.int64)
-    J = orc.ba_jacobian(x0, p.n_pose, p.n_landmark, p.u, p.v, p.init_ptz[0], fr, lm).tocsc()
-    r = orc.compute_residual_records(np.concatenate([p.init_ptz[0], x0]), p.n_pose, p.u, p.v, fr, lm, p.xy)
-    dx = spla.spsolve((J.T @ J).tocsc(), -(J.T @ r))
-    err = np.abs(dx_gpu - dx).max() / np.abs(dx).max()
-    assert err < 1e-7, err
+    monkeypatch.setenv("PTZBA_CHOL_BLOCKS", "1")
+    dx_blk, _ = _gn_step(grid, 1, ordering)
+    monkeypatch.setenv("PTZBA_CHOL_BLOCKS", "0")
+    dx_tile, _ = _gn_step(grid, 1, ordering)
+    assert np.array_equal(dx_blk, dx_tile)
 
 
 @pytest.fixture(scope="module")

@@ -1,0 +1,63 @@
+"""Host-side checks of the reduced-system plan (api.hip choose_order_plan, through the host-only
+ptzba_plan_summary): which system order ptzba_set_problem picks for a coupling window, its elimination
+levels and back-substitution chains.  No device is needed.  The numeric equivalence of the orders (the
+same Gauss-Newton step and optimum under every order) is checked on the GPU (test_gpu_ba.py,
+test_gpu_config3.py)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+import ptzba
+
+
+@pytest.fixture
+def nd_env():
+    old = os.environ.get("PTZBA_ND_DEPTH")
+    yield
+    if old is None:
+        os.environ.pop("PTZBA_ND_DEPTH", None)
+    else:
+        os.environ["PTZBA_ND_DEPTH"] = old
+
+
+def band_window(n, w):
+    return np.minimum(np.arange(n) + w, n - 1).astype(np.int32)
+
+
+def test_config3_two_level_dissection(nd_env):
+    """Config 3 (500 KF, coupling window ~95 frames, up to 120): two dissection levels give 26 elimination
+    levels and four back-substitution chains of at most 25 tile columns, against 30 levels and chains of 29 with one level."""
+    win = np.load(os.path.join(ROOT, "tests", "golden", "config3_window.npy"))
+    os.environ.pop("PTZBA_ND_DEPTH", None)
+    two = ptzba.plan_summary(win, 1)
+    os.environ["PTZBA_ND_DEPTH"] = "1"
+    one = ptzba.plan_summary(win, 1)
+    assert one["nd_depth"] == 1 and one["levels"] == 30 and one["chains"] == 2 and one["longest_chain"] == 29
+    assert two["nd_depth"] == 2 and two["chains"] == 4
+    assert two["levels"] == 26 and two["longest_chain"] == 25
+    assert two["n_aug"] == one["n_aug"] == 1536
+    assert two["bs_steps"] > 0  # the blocked back-solve also has a schedule over the separator tree
+
+
+def test_order_choice_follows_the_level_count(nd_env):
+    os.environ.pop("PTZBA_ND_DEPTH", None)
+    # short chain: natural order (no split shortens it)
+    s = ptzba.plan_summary(band_window(20, 5), 1)
+    assert s["nd_depth"] == 0 and s["chains"] == 1
+    # a long uniform band: the two-level order wins and stays a valid plan
+    s = ptzba.plan_summary(band_window(800, 60), 1)
+    os.environ["PTZBA_ND_DEPTH"] = "1"
+    s1 = ptzba.plan_summary(band_window(800, 60), 1)
+    assert s["nd_depth"] == 2 and s["levels"] < s1["levels"]
+    # natural ordering requested: never dissected
+    assert ptzba.plan_summary(band_window(800, 60), 1, ptzba.ORDER_NATURAL)["nd_depth"] == 0
+
+
+def test_plan_summary_rejects_bad_windows():
+    with pytest.raises(ptzba.PtzbaError):
+        ptzba.plan_summary(np.array([0, 5, 2], np.int32), 1)  # frame 1 couples past the last frame
+    with pytest.raises(ptzba.PtzbaError):
+        ptzba.plan_summary(np.array([1, 0, 2], np.int32), 1)  # frame 1's window ends before it

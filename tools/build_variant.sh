@@ -5,6 +5,7 @@ set -e
 NAME=$1; SRC=$2; DEFS=$3
 D=$(cd "$(dirname "$0")/../pan-tilt-zoom-slam_amd/csrc" && pwd)
 EXTRA=""; [ "$SRC" = schur_kernels.hip ] && EXTRA=-fno-slp-vectorize
+[ "$SRC" = chol_kernels.hip ] && EXTRA="-mllvm -amdgpu-mfma-vgpr-form=1"
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-pass-failed -Wno-unused-variable $EXTRA $DEFS \
   -c "$D/$SRC" -o /tmp/variant_$NAME.o
 OBJS=$(ls "$D"/*.o | grep -v "/${SRC%.hip}.o$")
