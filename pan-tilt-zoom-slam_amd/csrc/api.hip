@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <iterator>
 #include <map>
 #include <numeric>
 #include <string>
@@ -57,6 +58,7 @@ struct ptzba_ctx {
   DBuf s2_part, part_diag;                                    // K2 split partials (blocks, diagonal terms)
   DBuf s2_item_group, s2_tile_cnt;                            // matrix-core K2's folded reduce
   int n_s2_items = 0, n_s2_groups = 0;
+  bool s2_pair = false;  // K2 work items over chunk pairs (k_schur_mf2)
   int64_t n_slot = 0;  // dense landmark x frame slots (W table rows)
   // device: state
   DBuf ptz, rays, ptz_trial, rays_trial, D_pose, D_ray;
@@ -1127,7 +1129,63 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     if (const char* e = getenv("PTZBA_S2_ITEMS")) target_items = std::max(64, atoi(e));  // A/B knob
     const int64_t slots = std::max<int64_t>(target_items - n_tiles, 64);
     const int64_t split_w = std::max<int64_t>(64 * WD, (total_w + slots - 1) / slots);
-    for (size_t k = 0; k < tiles.size(); ++k) {
+    // matrix-core K2 over chunk PAIRS (k_schur_mf2, fp32 path): a work item covers the partner chunks 2cp and
+    // 2cp + 1 of its F1 block with the union of their landmark lists, so Y, the list and the chunk-0 diagonal
+    // terms are staged once for both chunks.  Its partial of chunk 2cp + h is partial (h * n_items + item): a
+    // tile's splits stay contiguous for k_schur_reduce (groups carry the offset).
+    h->s2_pair = h->precision == PTZBA_FP32 && schur_pair_mode();
+    if (h->s2_pair) {
+      std::vector<std::vector<int32_t>> ptl;
+      std::vector<int32_t> pkey;  // per pair tile: f1b, cp, chunk mask (bit h: chunk 2cp + h has a list)
+      for (size_t k = 0; k < tiles.size();) {
+        const int f1b = tile_key[2 * k], cp = tile_key[2 * k + 1] / 2;
+        std::vector<int32_t> u = tiles[k];
+        int mask = 1 << (tile_key[2 * k + 1] & 1);
+        size_t k2 = k + 1;
+        if (k2 < tiles.size() && tile_key[2 * k2] == f1b && tile_key[2 * k2 + 1] / 2 == cp) {
+          std::vector<int32_t> m;
+          std::set_union(u.begin(), u.end(), tiles[k2].begin(), tiles[k2].end(), std::back_inserter(m));
+          u.swap(m);
+          mask |= 1 << (tile_key[2 * k2 + 1] & 1);
+          ++k2;
+        }
+        ptl.push_back(std::move(u));
+        pkey.insert(pkey.end(), {f1b, cp, mask});
+        k = k2;
+      }
+      int64_t pw = 0;
+      for (size_t k = 0; k < ptl.size(); ++k) pw += (int64_t)ptl[k].size() * (pkey[3 * k + 1] == 0 ? W0 : WD);
+      int64_t ptarget = 256;  // one round of one workgroup per CU
+      if (const char* e = getenv("PTZBA_S2P_ITEMS")) ptarget = std::max(16, atoi(e));  // A/B knob
+      ptarget = std::min<int64_t>(ptarget, std::max<int64_t>(16, (ptarget * pw) / 240000));
+      const int64_t pslots = std::max<int64_t>(ptarget - (int64_t)ptl.size(), 16);
+      const int64_t psplit = std::max<int64_t>(32 * WD, (pw + pslots - 1) / pslots);
+      std::vector<int> first(ptl.size() + 1, 0);
+      for (size_t k = 0; k < ptl.size(); ++k) {
+        const auto& lst = ptl[k];
+        const int n = (int)lst.size();
+        const int64_t nw = (int64_t)n * (pkey[3 * k + 1] == 0 ? W0 : WD);
+        const int nparts = (int)std::max<int64_t>((nw + psplit - 1) / psplit, (n + SCHUR_PLMAX - 1) / SCHUR_PLMAX);
+        first[k] = (int)(s2_items.size() / 4);
+        for (int pp = 0; pp < nparts; ++pp) {
+          const int a0 = (int)((int64_t)n * pp / nparts), a1 = (int)((int64_t)n * (pp + 1) / nparts);
+          const int b0 = (int)(s2_lm.size() / 4);
+          for (int q = a0; q < a1; ++q) {
+            const int l = lst[q];
+            s2_lm.insert(s2_lm.end(), {l, lm_meta[4 * l], lm_meta[4 * l + 1], lm_meta[4 * l + 2]});
+          }
+          s2_items.insert(s2_items.end(), {pkey[3 * k], pkey[3 * k + 1] | (pkey[3 * k + 2] << 16), b0,
+                                           (int32_t)(s2_lm.size() / 4)});
+        }
+      }
+      first[ptl.size()] = (int)(s2_items.size() / 4);
+      const int N = first[ptl.size()];
+      for (size_t k = 0; k < ptl.size(); ++k)
+        for (int hh = 0; hh < 2; ++hh)
+          if ((pkey[3 * k + 2] >> hh) & 1)
+            s2_groups.insert(s2_groups.end(), {pkey[3 * k], 2 * pkey[3 * k + 1] + hh, hh * N + first[k], hh * N + first[k + 1]});
+    }
+    for (size_t k = 0; k < tiles.size() && !h->s2_pair; ++k) {
       const auto& lst = tiles[k];
       const int n = (int)lst.size();
       const int64_t nw = (int64_t)n * (tile_key[2 * k + 1] == 0 ? W0 : WD);
@@ -1292,7 +1350,8 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   {  // item -> tile (group) map and the per-tile split counters of the folded reduce (zero between launches)
     std::vector<int32_t> item_group(std::max(h->n_s2_items, 1), 0);
     for (int g = 0; g < h->n_s2_groups; ++g)
-      for (int it = s2_groups[4 * g + 2]; it < s2_groups[4 * g + 3]; ++it) item_group[it] = g;
+      for (int it = s2_groups[4 * g + 2]; it < s2_groups[4 * g + 3]; ++it)
+        if (it < h->n_s2_items) item_group[it] = g;  // (pair items: their first chunk's tile)
     if (upload(h->s2_item_group, item_group, h->st) || h->s2_tile_cnt.alloc((size_t)std::max(h->n_s2_groups, 1) * 4))
       return -1;
     HIPCHK(hipMemsetAsync(h->s2_tile_cnt.p, 0, h->s2_tile_cnt.bytes, h->st));
@@ -1310,7 +1369,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       h->scal.alloc(2 * PTZBA_NSCALARS * 8) || h->red_scratch.alloc(RED_SCRATCH * 8) || h->info.alloc(16) ||
       h->Ldiag.alloc((size_t)h->ld * CHOL_NB * 8) || h->Minv.alloc((size_t)h->ld * CHOL_NB * 8) ||
       h->dpose.alloc((size_t)h->ld * 8) ||
-      h->s2_part.alloc((size_t)std::max(h->n_s2_items, 1) * SCHUR_F1 * 9 * WAVE * 8) ||
+      h->s2_part.alloc((size_t)std::max(h->n_s2_items, 1) * (h->s2_pair ? 2 : 1) * SCHUR_F1 * 9 * WAVE * 8) ||
       h->part_diag.alloc((size_t)std::max(h->n_s2_items, 1) * SCHUR_F1 * 12 * 8))
     return -1;
   if (upload(h->chol_tasks, plan.tasks, h->st) || upload(h->tinv_tail, plan.tinv_tail, h->st) || upload(h->frame_pos, sorder.pos, h->st) || upload(h->row_pad, sorder.pad, h->st) ||
@@ -1624,6 +1683,7 @@ static int build_impl(ptzba_ctx* h, double lambda, const double* lam_dev, const 
   a.item_group = h->s2_item_group.as<int32_t>();
   a.tile_cnt = h->s2_tile_cnt.as<unsigned>();  // used only by the folded-reduce A/B build (MF_FOLD_REDUCE)
   tm_begin(h, TM_SCHUR);
+  a.pair = h->s2_pair;
   if (h->precision == PTZBA_FP32)
     launch_schur<float>(a, h->n_s2_items, h->n_s2_groups, h->n_fixed, h->st);
   else

@@ -756,6 +756,9 @@ void launch_trial(const BacksubArgs& a, const double* ptz, const double* g_pose,
 // ranges into scratch partials; the last workgroup to finish (agent-scope counter) combines them in
 // block order and re-arms the counter, so the result is bitwise reproducible in one launch.
 constexpr int RED_BLOCKS = 64;
+#ifndef RED_SC1
+#define RED_SC1 1  // 0: plain partial stores published by an acq_rel counter add (A/B)
+#endif
 // (src2, stride2, nk2, out2): an optional second set of columns over the same n rows, reduced in the same
 // launch into out2 (columns nk .. nk + nk2 - 1 of the internal accumulators; nk + nk2 <= 8)
 __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ src, int64_t n, int stride, int nk,
@@ -772,13 +775,19 @@ __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ 
   double acc[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) acc[k] = 0;
+  // every column of a row is requested before any is used (clamped column index, branch-free), so a row costs
+  // one memory latency instead of one per column
+  const int nkt = nk + nk2;
   for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    double x[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      if (k >= nk + nk2) break;
-      const double x = k < nk ? src[i * stride + k] : src2[i * stride2 + (k - nk)];
-      acc[k] = (maxmask & (1 << k)) ? fmax(acc[k], fabs(x)) : acc[k] + x;
+      const int kc = min(k, nkt - 1);
+      x[k] = kc < nk ? src[i * stride + kc] : src2[i * stride2 + (kc - nk)];
     }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k < nkt) acc[k] = (maxmask & (1 << k)) ? fmax(acc[k], fabs(x[k])) : acc[k] + x[k];
   }
   nk += nk2;  // from here on: all accumulated columns
 #pragma unroll
@@ -794,6 +803,28 @@ __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ 
   if (lane_id() == 0)
     for (int k = 0; k < nk; ++k) red[k][w] = acc[k];
   __syncthreads();
+#if RED_SC1
+  // the partials go out write-through (sc1 stores: L2 bypassed to memory) and the storing wave waits for them
+  // before its counter add, so the add needs no agent-scope release -- which would write back every dirty line
+  // of this XCD's L2 (K1 just stored ~90 MB of slots) -- and the last workgroup reads them with sc1 loads
+  // (MI355X_MICROARCH.md, inter-workgroup visibility, Valid forms: one lane's agent atomic add per storing
+  // workgroup, the last adder told by the returned value, stores and loads all sc1, one workgroup per CU).
+  // The partial stores and the add are issued by the same wave (wave 0: nk <= 8 lanes).
+  if (threadIdx.x < WAVE) {
+    if (threadIdx.x < nk) {
+      const int k = threadIdx.x;
+      double s = 0;
+      for (int j = 0; j < (int)(blockDim.x / WAVE); ++j) s = (maxmask & (1 << k)) ? fmax(s, red[k][j]) : s + red[k][j];
+      __hip_atomic_store(partial + blockIdx.x * 8 + k, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) {
+      const unsigned done = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = (done == gridDim.x - 1);
+    }
+  }
+  __syncthreads();
+#else
   if (threadIdx.x < nk) {
     const int k = threadIdx.x;
     double s = 0;
@@ -806,6 +837,7 @@ __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ 
     last = (done == gridDim.x - 1);
   }
   __syncthreads();
+#endif
   if (!last) return;
   // all partials in parallel (agent-scope loads: other workgroups wrote them), then a fixed-order sum
   __shared__ double fin[RED_BLOCKS][8];

@@ -39,6 +39,9 @@ struct LinArgs {
 // splits of a tile's landmark list.  Static structure built once by ptzba_set_problem.
 constexpr int SCHUR_F1 = 32;
 constexpr int SCHUR_LMAX = 512;  // landmarks per work item (split size cap)
+constexpr int SCHUR_PLMAX = 256;  // the same for chunk-pair items (k_schur_mf2: LDS holds two chunks' operands)
+// chunk-pair K2 (k_schur_mf2) for the fp32 path: PTZBA_SCHUR=mf2 / =mf (A/B); see schur_kernels.hip
+bool schur_pair_mode();
 // Single-GPU builds fold k_chol_prepare into the build: the prologue writes the constant diagonal entries
 // (padding identity, augmented diagonal, identity below it) and resets info; k_schur_reduce writes the
 // augmented row b^T and the pose damping (D_pose = max(D_pose, diag U); S_ff += lambda D_pose), the same
@@ -77,6 +80,7 @@ struct SchurArgs {
   const int32_t* item_group;      // [n_items] tile (group) of each item (matrix-core K2: folded reduce)
   unsigned* tile_cnt;             // [n_groups] finished splits per tile (zero between launches)
   FusedPrep prep;                 // single-GPU: the prepare's augmented row and damping (pad != nullptr)
+  bool pair = false;              // items over chunk pairs (k_schur_mf2; item.y = cp | chunk mask << 16)
 };
 
 struct BacksubArgs {

@@ -424,16 +424,19 @@ def test_save_restore_state_restarts_identically(gpu_available):
     h.close()
 
 
+@pytest.mark.parametrize("mode", ["mf", "mf2"])
 @pytest.mark.parametrize("config,loss", [("config2", "linear"), ("config3", "huber")])
-def test_reduced_system_matrix_core_k2_matches_fp64(gpu_available, config, loss):
+def test_reduced_system_matrix_core_k2_matches_fp64(gpu_available, config, loss, mode, monkeypatch):
     """K2 of the fp32 path runs on the matrix cores (k_schur_mf: fp16 hi/lo operand splits with power-of-
-    two landmark scaling); the fp64 path keeps the VALU kernel.  At the same linearisation
-    point the two reduced camera systems (S | b | g_pose | diag U, the exchange region) agree to the
-    fp32 record precision, element by element against each row's scale."""
+    two landmark scaling; k_schur_mf2: the same over chunk pairs, PTZBA_SCHUR=mf2); the fp64
+    path keeps the VALU kernel.  At the same linearisation point the two reduced camera systems (S | b | g_pose
+    | diag U, the exchange region) agree to the fp32 record precision, element by element against each row's
+    scale."""
     import torch
     import bench
     import ptzba
     import synthetic
+    monkeypatch.setenv("PTZBA_SCHUR", mode)
     p = synthetic.make_problem(config, seed=0)
     lo = ptzba.LOSS_LINEAR if loss == "linear" else ptzba.LOSS_HUBER
     out = []
