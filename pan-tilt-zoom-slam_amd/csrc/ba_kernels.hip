@@ -623,6 +623,21 @@ void launch_build_prologue(double* S, int64_t ld, const int2* zt, int n_tiles, d
 // Trial state in one launch (with the trial's frame / ray tables, which the trial linearisation reads):
 // blocks [0, nb) back-substitute 4 landmarks each as above, the last block forms the trial poses, their
 // tables and the pose partials (one thread per frame, fixed-order reduction: identical on every rank).
+// the 6 W values of a dense slot row (8 reals, 16-B aligned) in two vector loads
+template <typename real>
+__device__ __forceinline__ void load_w6_slot(real (&x)[6], const real* __restrict__ p) {
+  if constexpr (sizeof(real) == 4) {
+    const float4 lo = reinterpret_cast<const float4*>(p)[0];
+    const float2 hi = reinterpret_cast<const float2*>(p)[2];
+    x[0] = lo.x; x[1] = lo.y; x[2] = lo.z; x[3] = lo.w; x[4] = hi.x; x[5] = hi.y;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const double2 d = reinterpret_cast<const double2*>(p)[k];
+      x[2 * k] = d.x; x[2 * k + 1] = d.y;
+    }
+  }
+}
 struct PoseTrialArgs {
   const double* ptz;
   const double* g_pose;
@@ -694,12 +709,20 @@ __global__ __launch_bounds__(256) void k_trial(BacksubArgs a, PoseTrialArgs pa, 
   const bool alt = a.sel && *a.sel;  // device-chosen linearisation slot
   const real* __restrict__ w_slot = (const real*)(alt ? a.w_slot1 : a.w_slot);
   const int4 lmeta = a.lm_meta[l];
+  // the landmark's own operands (independent of the segment walk) requested up front: the wave's dependent
+  // chain is segment list -> frame -> W slot / system row -> dpose, then the reduction and the stores
+  const double* lo = (alt ? a.lm_out1 : a.lm_out) + (int64_t)l * 8;
+  const double* vi = a.lm_aux + (int64_t)l * 8;
+  const double g0 = lo[3], g1 = lo[4], v0 = vi[0], v1 = vi[1], v2 = vi[2];
+  const double th = a.rays[2 * l], ph = a.rays[2 * l + 1];
+  const double D0 = a.D_ray[2 * l], D1 = a.D_ray[2 * l + 1];
   double t0 = 0, t1 = 0;
   for (int s = s0 + lane; s < s1; s += WAVE) {
     const int f = a.seg_frame[s];
     if (f < a.n_fixed) continue;
     const double* dp = a.dpose + a.frame_pos[f];
-    const real* w = w_slot + ((int64_t)lmeta.z + f - lmeta.x) * 8;
+    real w[6];
+    load_w6_slot(w, w_slot + ((int64_t)lmeta.z + f - lmeta.x) * 8);
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       t0 += (double)w[2 * q] * dp[q];
@@ -710,24 +733,20 @@ __global__ __launch_bounds__(256) void k_trial(BacksubArgs a, PoseTrialArgs pa, 
   t1 = wave_total(t1);
   if (lane == WAVE - 1) {
     double* red = a.lm_red + (int64_t)l * 4;
-    const double th = a.rays[2 * l], ph = a.rays[2 * l + 1];
     double nth = th, nph = ph;
     if (s1 == s0) {
       red[0] = 0; red[1] = 0; red[2] = 0; red[3] = 0;
     } else {
-      const double* lo = (alt ? a.lm_out1 : a.lm_out) + (int64_t)l * 8;
-      const double* vi = a.lm_aux + (int64_t)l * 8;
-      const double r0 = lo[3] + t0, r1 = lo[4] + t1;
-      const double d0 = -(vi[0] * r0 + vi[1] * r1);
-      const double d1 = -(vi[1] * r0 + vi[2] * r1);
+      const double r0 = g0 + t0, r1 = g1 + t1;
+      const double d0 = -(v0 * r0 + v1 * r1);
+      const double d1 = -(v1 * r0 + v2 * r1);
       nth = th + d0;
       nph = ph + d1;
-      const double D0 = a.D_ray[2 * l], D1 = a.D_ray[2 * l + 1];
       const double lam = a.lam_dev ? *a.lam_dev : a.lambda;
-      red[0] = -0.5 * (lo[3] * d0 + lo[4] * d1) + 0.5 * lam * (D0 * d0 * d0 + D1 * d1 * d1);
+      red[0] = -0.5 * (g0 * d0 + g1 * d1) + 0.5 * lam * (D0 * d0 * d0 + D1 * d1 * d1);
       red[1] = d0 * d0 + d1 * d1;
       red[2] = th * th + ph * ph;
-      red[3] = fmax(fabs(lo[3]), fabs(lo[4]));
+      red[3] = fmax(fabs(g0), fabs(g1));
     }
     a.rays_trial[2 * l] = nth;
     a.rays_trial[2 * l + 1] = nph;
