@@ -792,11 +792,23 @@ static int choose_order_plan(int n_pose, int nf, const std::vector<int32_t>& win
   if (!make_plan(so, n_pose, nf, win, pad_tile(so.n_aug + 1), plan)) return -1;
   const char* nde = getenv("PTZBA_ND_DEPTH");
   const int nd_env = nde ? atoi(nde) : 0;
+  // estimated factorisation time of a plan: per level the longer of the pivot chain (~7 us) and its tasks in
+  // rounds of the chip (~768 resident workgroups, ~6 us a round) -- fewer levels only pay when the extra fill
+  // and the wider levels do not turn them into throughput-bound ones (config 4: the two-level order has 189
+  // levels instead of 265 but up to 18K tasks per level, 7.9 vs 4.7 ms per trial)
+  auto est_us = [](const CholPlan& P) {
+    double t = 0;
+    for (int L = 0; L < P.n_levels; ++L) {
+      const int n = P.level_off[L + 1] - P.level_off[L];
+      t += std::max(7.0, 6.0 * ((n + 767) / 768));
+    }
+    return t;
+  };
   SysOrder s2;
   CholPlan p2;
   if (ordering == PTZBA_ORDER_NESTED && nd_env != 1 && nested_order2(n_pose, nf, win, s2) &&
       pad_tile(s2.n_aug + 1) <= CHOL_MAX_LD && make_plan(s2, n_pose, nf, win, pad_tile(s2.n_aug + 1), p2) &&
-      (p2.n_levels < plan.n_levels || nd_env == 2)) {
+      ((p2.n_levels < plan.n_levels && est_us(p2) < est_us(plan)) || nd_env == 2)) {
     so = std::move(s2);
     plan = std::move(p2);
   }
@@ -1400,11 +1412,14 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   // (lookahead form: + 48 KiB ring of M / L blocks); larger systems take the left-looking form, whose lists
   // stay in global memory
   h->bs_ll = h->ld * 8 + (std::max(h->bs_npos + 1 + h->bs_nupd, 2 * h->bs_npos + h->bs_ntasks)) * 4 > 100 * 1024;
-  // large systems take the blocked right-looking form (many CUs per step) when the plan has a valid schedule;
-  // testing knobs: PTZBA_BACKSOLVE=ll (left-looking, one CU per chain) / =blk (blocked form at any size)
+  // systems of >= 512 rows take the blocked right-looking form (many CUs per step) when the plan has a valid
+  // schedule: the lookahead form reads the whole band of L through one CU per chain (config 3, same-box A/B
+  // r03ab: cholesky_solve 0.261 -> 0.248 ms per trial); smaller ones (sliding windows) keep the lookahead form.
+  // Knobs: PTZBA_BACKSOLVE=la (lookahead while its lists fit LDS) / =ll (left-looking) / =blk (blocked, any size)
   const char* bse = getenv("PTZBA_BACKSOLVE");
   const std::string bsk = bse ? bse : "";
-  h->bs_blk = (h->bs_ll || bsk == "blk") && bsk != "ll" && !plan.bsb_tasks.empty();
+  const bool want_blk = bsk == "blk" || (bsk.empty() && (h->bs_ll || h->n_aug >= 512));
+  h->bs_blk = (want_blk || (h->bs_ll && bsk != "ll")) && bsk != "ll" && !plan.bsb_tasks.empty();
   h->bs_ll = (h->bs_ll || bsk == "ll") && !h->bs_blk;
   h->bsb_step_off = plan.bsb_step_off;
   if (h->bs_blk) {

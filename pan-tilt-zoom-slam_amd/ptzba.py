@@ -166,6 +166,8 @@ def lib():
         "ptzekf_update": ([V, D, D, V, V, I64, V, V, I32, I32, D, V, POINTER(c_int32)], I),
     }
     for name, (args, res) in sigs.items():
+        if "PTZBA_LIB" in os.environ and not hasattr(L, name):
+            continue  # an older library built for an A/B run (tools/gpu_lib_ab.sh): entry points it predates stay unbound
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res

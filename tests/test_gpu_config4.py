@@ -46,8 +46,7 @@ def test_grid_gauss_newton_step_is_exact(gpu_available, grid, monkeypatch, backs
     import scipy.sparse.linalg as spla
     from oracle import ptz_oracle as orc
     p = grid
-    if backsolve != "lookahead":
-        monkeypatch.setenv("PTZBA_BACKSOLVE", backsolve)
+    monkeypatch.setenv("PTZBA_BACKSOLVE", {"lookahead": "la", "ll": "ll", "blk": "blk"}[backsolve])
     dx_gpu, info = _gn_step(p, 0, ordering)
     assert info["backsolve"] == {"lookahead": "lookahead", "ll": "left-looking", "blk": "blocked"}[backsolve]
     if ordering != 1:  # 1: the solver's choice (natural, one or two dissection levels)

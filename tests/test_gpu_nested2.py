@@ -34,8 +34,7 @@ def sparse_step(wide):
 def test_two_level_order_gauss_newton_step_is_exact(gpu_available, wide, sparse_step, monkeypatch, backsolve, delay):
     import ptzba
     p = wide
-    if backsolve != "lookahead":
-        monkeypatch.setenv("PTZBA_BACKSOLVE", backsolve)
+    monkeypatch.setenv("PTZBA_BACKSOLVE", {"lookahead": "la", "ll": "ll", "blk": "blk"}[backsolve])
     monkeypatch.setenv("PTZBA_CHOL_DELAY", delay)
     h = ptzba.BAHandle(0)
     h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=ptzba.FP64)

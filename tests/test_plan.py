@@ -61,3 +61,16 @@ def test_plan_summary_rejects_bad_windows():
         ptzba.plan_summary(np.array([0, 5, 2], np.int32), 1)  # frame 1 couples past the last frame
     with pytest.raises(ptzba.PtzbaError):
         ptzba.plan_summary(np.array([1, 0, 2], np.int32), 1)  # frame 1's window ends before it
+
+
+def test_config4_keeps_one_level_with_trailing_blocks(nd_env):
+    """Config 4 (5000 KF in 10 tilt rows, coupling window ~560 frames, up to 1114): the two-level order would
+    have fewer levels (189 vs 265) but levels of up to 18K tasks; the planner's cost estimate keeps the one-level
+    order, with delayed trailing updates in 2 x 2 blocks."""
+    os.environ.pop("PTZBA_ND_DEPTH", None)
+    win = np.load(os.path.join(ROOT, "tests", "golden", "config4_window.npy"))
+    s = ptzba.plan_summary(win, 1)
+    assert s["nd_depth"] == 1 and s["levels"] == 265 and s["panel_pairs"] == 2, s
+    _, tasks, _, _, _ = ptzba.plan_export(win, 1)
+    typ = tasks[:, 0] & 3
+    assert (typ == 3).sum() > 50 * (typ == 1).sum()  # nearly every trailing tile rides in a block
