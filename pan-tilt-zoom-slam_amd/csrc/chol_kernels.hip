@@ -823,9 +823,12 @@ struct CholTaskPtr {
   const int4* p;
   __device__ int4 get(int b) const { return p[b]; }
 };
+// the level's first CHOL_KT tasks by value in the kernel arguments (its panel tasks -- the critical path -- come
+// first in every level's list), the rest from the device array (trailing tasks of the wide levels)
 struct CholTaskVal {
   int4 t[CHOL_KT];
-  __device__ int4 get(int b) const { return t[b]; }
+  const int4* rest;
+  __device__ int4 get(int b) const { return b < CHOL_KT ? t[b] : rest[b - CHOL_KT]; }
 };
 // P2: plans with delayed trailing updates (a second pair of update panels per task, api.hip make_plan)
 template <bool SG, typename TaskArg, bool P2 = false>
@@ -1125,9 +1128,10 @@ void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_o
   for (int L = first_level; L < n_launch; ++L) {
     const int n = task_off_host[L + 1] - task_off_host[L];
     if (n <= 0) continue;
-    if (tasks_host && by_value && n <= CHOL_KT) {
+    if (tasks_host && by_value) {
       CholTaskVal tv;
-      std::memcpy(tv.t, tasks_host + task_off_host[L], n * sizeof(int4));
+      std::memcpy(tv.t, tasks_host + task_off_host[L], std::min(n, CHOL_KT) * sizeof(int4));
+      tv.rest = tasks + task_off_host[L] + CHOL_KT;
       if (sgn)
         hipLaunchKernelGGL((k_chol_step<true, CholTaskVal>), dim3(n), dim3(256), 0, st, A, ld, tv, Ldiag, info, sgn, Minv);
       else if (delayed)
