@@ -580,6 +580,7 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
   if (force_dt) DT = force_dt;
   P.delayed = DT > 1;
   size_t max_pd = 0;  // update panels of one task: the P2 kernel takes up to four (any DT), the other two
+  bool any_block = false;  // 2 x 2 trailing blocks (type 3) run in the P2 kernel only
   auto pack2 = [](int type, const std::vector<int>& pd, int tm) {  // int4 task: x (type + panels 2, 3), w (0, 1)
     return std::make_pair(chol_pack_type(type, pd.size() > 2 ? pd[2] : -1, pd.size() > 3 ? pd[3] : -1, (tm >> 2) & 3),
                           chol_pack_updates(pd.size() > 0 ? pd[0] : -1, pd.size() > 1 ? pd[1] : -1, tm & 3));
@@ -636,7 +637,7 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
       tiles_pd.push_back({upd[x].first, pd});
       x = y;
     }
-    const bool blocked = DT > 1 && !getenv_is("PTZBA_CHOL_BLOCKS", "0");
+    const bool blocked = !getenv_is("PTZBA_CHOL_BLOCKS", "0");
     std::vector<uint8_t> in_block(tiles_pd.size(), 0);
     if (blocked) {
       for (size_t q = 0; q < tiles_pd.size(); ++q) {
@@ -658,6 +659,7 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
         const int a = (int)(kv.first / T), bcol = (int)(kv.first % T), mask = kv.second.first;
         push(chol_pack_type(3, pd.size() > 2 ? pd[2] : -1, pd.size() > 3 ? pd[3] : -1, (mask >> 2) & 3), 2 * a, 2 * bcol,
              chol_pack_updates(pd.size() > 0 ? pd[0] : -1, pd.size() > 1 ? pd[1] : -1, mask & 3));
+        any_block = true;
       }
     }
     for (size_t q = 0; q < tiles_pd.size(); ++q) {
@@ -685,7 +687,7 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
     fprintf(stderr, "max panels per task %zu\n", max_pd);
   }
   if (max_pd > 4) return DT > 1 ? make_plan(o, n_pose, nf, win, ld, P, 1) : false;  // too many panels: DT = 1
-  if (max_pd > 2) P.delayed = true;  // the P2 kernel (second panel pair) also at DT = 1
+  if (max_pd > 2 || any_block) P.delayed = true;  // the P2 kernel (second panel pair, trailing blocks) also at DT = 1
   // back-substitution: chains of tile columns holding unknowns and, per chain position, the chain's
   // later columns coupled to that row tile (right-looking updates).  Nested orders: one chain per leaf of
   // the separator tree (its root-to-leaf path, each node's columns descending); natural: one chain.
