@@ -2,7 +2,7 @@
 # PMC passes, bench line with the full CPU baseline, PMC calibration, K2 traffic), then smoke() and the
 # config-4 bench line.
 set -o pipefail
-export TAG=${TAG:-r03z}
+export TAG=${TAG:-r03end}
 bash tools/gpu_measure.sh || exit 1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/${TAG}_smoke.log 2>&1 || { echo SMOKEFAIL; tail gpurun_out/${TAG}_smoke.log; exit 1; }
 tail -1 gpurun_out/${TAG}_smoke.log
