@@ -355,7 +355,7 @@ static bool nested_order(int n_pose, int nf, const std::vector<int32_t>& win, Sy
 // instead of max(A, B) + C (config 3: 26 instead of 30 levels), and four back-substitution chains C2 -> C1 ->
 // A1 / A2, C2 -> C3 -> A3 / A4.  A leaf couples only to its ancestors: A1 to C1, A2 to C1 and C2, A3 to C2
 // and C3, A4 to C3 (and, where the window reaches that far, C2).  The top split minimises the estimated chain.
-static bool nested_order2(int n_pose, int nf, const std::vector<int32_t>& win, SysOrder& o) {
+static bool nested_order2(int n_pose, int nf, const std::vector<int32_t>& win, SysOrder& o, bool halves = false) {
   if (n_pose - nf < 32) return false;
   std::vector<int> pmax(n_pose + 1, -1);
   for (int f = nf; f < n_pose; ++f) pmax[f + 1] = std::max(pmax[f], (int)win[f]);
@@ -383,8 +383,12 @@ static bool nested_order2(int n_pose, int nf, const std::vector<int32_t>& win, S
     if (est < best) { best = est; bm = m; bc = cend; b1 = m1; bc1 = c1; b3 = m3; bc3 = c3; }
   }
   if (bm < 0) return false;
-  // parts in system order: {first frame, end frame, reversed}
-  const int parts[7][3] = {{nf, b1, 0}, {bc1, bm, 0}, {bc, b3, 0}, {bc3, n_pose, 1}, {b1, bc1, 0}, {b3, bc3, 0}, {bm, bc, 0}};
+  // parts in system order: {first frame, end frame, reversed}.  halves (part-owned multi-GPU solve): each half
+  // contiguous, [A1 | A2 | C1 | A3 | A4 reversed | C3 | C2], so a rank group owns [A1 | A2 | C1] or [A3 | A4 | C3]
+  // and C2 is the separator the groups exchange (the same dependencies, so the same levels)
+  const int pa[7][3] = {{nf, b1, 0}, {bc1, bm, 0}, {bc, b3, 0}, {bc3, n_pose, 1}, {b1, bc1, 0}, {b3, bc3, 0}, {bm, bc, 0}};
+  const int ph[7][3] = {{nf, b1, 0}, {bc1, bm, 0}, {b1, bc1, 0}, {bc, b3, 0}, {bc3, n_pose, 1}, {b3, bc3, 0}, {bm, bc, 0}};
+  const int (*parts)[3] = halves ? ph : pa;
   o = SysOrder{};
   o.pos.assign(n_pose, -1);
   int row = 0, t[8];
@@ -403,6 +407,16 @@ static bool nested_order2(int n_pose, int nf, const std::vector<int32_t>& win, S
     for (int r = pr.first; r < pr.second; ++r) o.pad[r] = 1;
   o.nested = true;
   o.nd_depth = 2;
+  if (halves) {
+    // nodes: 0 = C2 (root), 1 = C1, 2 = C3, 3..6 = A1..A4 (part-owned fields: the halves and C2's frames)
+    o.nodes = {{t[6], t[7], -1}, {t[2], t[3], 0}, {t[5], t[6], 0},
+               {t[0], t[1], 1}, {t[1], t[2], 1}, {t[3], t[4], 2}, {t[4], t[5], 2}};
+    o.tiles_a = t[3];
+    o.tiles_b = t[6] - t[3];
+    o.split_m = bm;
+    o.split_cend = bc;
+    return true;
+  }
   // nodes: 0 = C2 (root), 1 = C1, 2 = C3, 3..6 = A1..A4
   o.nodes = {{t[6], t[7], -1}, {t[4], t[5], 0}, {t[5], t[6], 0},
              {t[0], t[1], 1}, {t[1], t[2], 1}, {t[2], t[3], 2}, {t[3], t[4], 2}};
@@ -412,9 +426,7 @@ static bool nested_order2(int n_pose, int nf, const std::vector<int32_t>& win, S
 // The split of a part-owned (multi-GPU) solve: nested_order's choice when it shortens the critical path,
 // else its most balanced split; false when none exists (every frame couples to the last one).  A pure
 // function of the coupling window, so ptzba_partition_landmarks and every rank's set_problem agree.
-static bool dist_order(int n_pose, int nf, const std::vector<int32_t>& win, SysOrder& o) {
-  return nested_order(n_pose, nf, win, o, false) || nested_order(n_pose, nf, win, o, true);
-}
+static bool dist_order(int n_pose, int nf, const std::vector<int32_t>& win, SysOrder& o);  // after make_plan_part
 // rank groups of a part-owned solve: part 0 = ranks [0, g0), part 1 = [g0, world)
 static int dist_g0(int world) { return (world + 1) / 2; }
 
@@ -784,6 +796,19 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
 
 static int ensure_group_comm(ptzba_ctx* h);
 
+// estimated factorisation time of a plan: per level the longer of the pivot chain (~7 us) and its tasks in
+// rounds of the chip (~768 resident workgroups, ~6 us a round) -- fewer levels only pay when the extra fill
+// and the wider levels do not turn them into throughput-bound ones (config 4: the two-level order has 189
+// levels instead of 265 but up to 18K tasks per level, 7.9 vs 4.7 ms per trial)
+static double plan_est_us(const CholPlan& P) {
+  double t = 0;
+  for (int L = 0; L < P.n_levels; ++L) {
+    const int n = P.level_off[L + 1] - P.level_off[L];
+    t += std::max(7.0, 6.0 * ((n + 767) / 768));
+  }
+  return t;
+}
+
 // System order and plan of a single-system solve: natural, or the one-level nested order, or two dissection
 // levels when that plan has fewer levels (PTZBA_ND_DEPTH=1 / =2: A/B knob, one level only / two levels
 // whenever valid).  Returns nonzero if no plan exists.
@@ -794,18 +819,7 @@ static int choose_order_plan(int n_pose, int nf, const std::vector<int32_t>& win
   if (!make_plan(so, n_pose, nf, win, pad_tile(so.n_aug + 1), plan)) return -1;
   const char* nde = getenv("PTZBA_ND_DEPTH");
   const int nd_env = nde ? atoi(nde) : 0;
-  // estimated factorisation time of a plan: per level the longer of the pivot chain (~7 us) and its tasks in
-  // rounds of the chip (~768 resident workgroups, ~6 us a round) -- fewer levels only pay when the extra fill
-  // and the wider levels do not turn them into throughput-bound ones (config 4: the two-level order has 189
-  // levels instead of 265 but up to 18K tasks per level, 7.9 vs 4.7 ms per trial)
-  auto est_us = [](const CholPlan& P) {
-    double t = 0;
-    for (int L = 0; L < P.n_levels; ++L) {
-      const int n = P.level_off[L + 1] - P.level_off[L];
-      t += std::max(7.0, 6.0 * ((n + 767) / 768));
-    }
-    return t;
-  };
+  const auto est_us = plan_est_us;
   SysOrder s2;
   CholPlan p2;
   if (ordering == PTZBA_ORDER_NESTED && nd_env != 1 && nested_order2(n_pose, nf, win, s2) &&
@@ -980,6 +994,31 @@ static bool make_plan_part(const SysOrder& o, int part, int n_pose, int nf, cons
   P.la_tasks.insert(P.la_tasks.end(), toff.begin(), toff.end());
   P.la_tasks.insert(P.la_tasks.end(), tasks.begin(), tasks.end());
   make_bs_steps(nz, Tx, P, BsPhases{{P.chain_cols}});
+  return true;
+}
+
+// The two-level order with contiguous halves replaces it when the slower rank group's estimated factorisation
+// time is shorter (config 3 at N >= 2: a rank's chain of 31 levels becomes ~27); PTZBA_ND_DEPTH=1 keeps one level.
+static bool dist_order(int n_pose, int nf, const std::vector<int32_t>& win, SysOrder& o) {
+  if (!(nested_order(n_pose, nf, win, o, false) || nested_order(n_pose, nf, win, o, true))) return false;
+  if (getenv_is("PTZBA_ND_DEPTH", "1")) return true;
+  SysOrder o2;
+  if (!nested_order2(n_pose, nf, win, o2, true) || pad_tile(o2.n_aug + 1) > CHOL_MAX_LD) return true;
+  double e[2] = {0, 0};
+  const SysOrder* os[2] = {&o, &o2};
+  for (int v = 0; v < 2; ++v)
+    for (int part = 0; part < 2; ++part) {
+      CholPlan P;
+      PartPlan Q;
+      if (!make_plan_part(*os[v], part, n_pose, nf, win, pad_tile(os[v]->n_aug + 1), P, Q)) {
+        if (getenv("PTZBA_PLAN_DEBUG")) fprintf(stderr, "dist_order: order %d part %d has no plan\n", v + 1, part);
+        return true;
+      }
+      e[v] = std::max(e[v], plan_est_us(P));
+      if (getenv("PTZBA_PLAN_DEBUG"))
+        fprintf(stderr, "dist_order: order %d part %d levels %d est %.1f us\n", v + 1, part, P.n_levels, plan_est_us(P));
+    }
+  if (e[1] < e[0]) o = std::move(o2);
   return true;
 }
 
