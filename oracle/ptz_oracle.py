@@ -419,6 +419,149 @@ def solve_scipy(x0_free, n_pose, n_landmark, u, v, ref_pose, frame, landmark, xy
     return least_squares(fun, x0_free, **kw)
 
 
+def _loss_weights(r, loss, f_scale):
+    """scipy least_squares convention (cost = 0.5 f^2 sum rho((r/f)^2) over SCALAR residuals): per residual
+    0.5 f^2 rho(z), the gradient weight rho'(z) (d cost / d r = rho' r) and the curvature weight rho' + 2 rho'' z
+    (d^2 cost / d r^2).  huber: rho = z inside the unit, 2 sqrt(z) - 1 beyond, rho' = 1 / sqrt(z) there and the
+    curvature is 0 (the cost is linear in |r|); it is floored at 0.1 rho' so every 2x2 landmark block stays
+    well conditioned -- the floor changes the convergence rate of the Newton iteration, not its fixed point (at 1.0
+    this is IRLS; at 0.1 config 2 converges in 11 instead of ~45 steps from the linear-loss optimum)."""
+    z = (r / f_scale) ** 2
+    if loss == 'huber':
+        rho = np.where(z <= 1.0, z, 2.0 * np.sqrt(z) - 1.0)
+        w1 = np.where(z <= 1.0, 1.0, 1.0 / np.sqrt(np.maximum(z, 1.0)))
+        w2 = np.where(z <= 1.0, 1.0, 0.3 * w1)
+        return 0.5 * f_scale ** 2 * rho, w1, w2
+    one = np.ones_like(r)
+    return 0.5 * r * r, one, one
+
+
+def ba_cost_chunked(ptz, rays, u, v, frame, landmark, xy, loss='linear', f_scale=1.0, chunk=2_000_000):
+    """ba_cost with bounded host memory (headline-size record arrays)."""
+    c = 0.0
+    for a in range(0, len(frame), chunk):
+        b = min(len(frame), a + chunk)
+        fr, lm = frame[a:b], landmark[a:b]
+        px, py = from_ray_to_image(u, v, ptz[fr, 2], ptz[fr, 0], ptz[fr, 1], rays[lm, 0], rays[lm, 1])
+        r = np.stack([px - xy[a:b, 0], py - xy[a:b, 1]], -1)
+        c += float(np.sum(_loss_weights(r, loss, f_scale)[0]))
+    return c
+
+
+def _normal_blocks(ptz, rays, u, v, frame, landmark, xy, seg, n_seg, loss, f_scale, chunk=2_000_000):
+    """Gauss-Newton blocks of the (robust-weighted) pair-form cost, accumulated per record without forming J:
+    U [n,3,3] (pose-pose, per frame), V [m,2,2] (ray-ray, per landmark), W [n_seg,3,2] (pose-ray, per unique
+    (frame, landmark) segment), gradients g_pose [n,3], g_ray [m,2], cost.  Per record the 2x5 analytic Jacobian
+    (record_jacobian) of the residual of bundle_adjustment.py:67-99."""
+    n, m = len(ptz), len(rays)
+    U = np.zeros((n, 9))
+    V = np.zeros((m, 4))
+    W = np.zeros((n_seg, 6))
+    gp = np.zeros((n, 3))
+    gr = np.zeros((m, 2))
+    cost = 0.0
+    for a in range(0, len(frame), chunk):
+        b = min(len(frame), a + chunk)
+        fr, lm, sg = frame[a:b], landmark[a:b], seg[a:b]
+        px, py = from_ray_to_image(u, v, ptz[fr, 2], ptz[fr, 0], ptz[fr, 1], rays[lm, 0], rays[lm, 1])
+        r = np.stack([px - xy[a:b, 0], py - xy[a:b, 1]], -1)
+        rho, w1, w2 = _loss_weights(r, loss, f_scale)
+        cost += float(np.sum(rho))
+        J = record_jacobian(u, v, ptz[fr], rays[lm])
+        Jw = J * w2[:, :, None]  # curvature-weighted rows (Hessian blocks)
+        r = r * w1  # gradient: J^T (rho' r)
+        for i in range(3):
+            for j in range(3):
+                U[:, 3 * i + j] += np.bincount(fr, np.einsum("rk,rk->r", Jw[:, :, i], J[:, :, j]), n)
+            for j in range(2):
+                W[:, 2 * i + j] += np.bincount(sg, np.einsum("rk,rk->r", Jw[:, :, i], J[:, :, 3 + j]), n_seg)
+            gp[:, i] += np.bincount(fr, np.einsum("rk,rk->r", J[:, :, i], r), n)
+        for i in range(2):
+            for j in range(2):
+                V[:, 2 * i + j] += np.bincount(lm, np.einsum("rk,rk->r", Jw[:, :, 3 + i], J[:, :, 3 + j]), m)
+            gr[:, i] += np.bincount(lm, np.einsum("rk,rk->r", J[:, :, 3 + i], r), m)
+    return U.reshape(n, 3, 3), V.reshape(m, 2, 2), W.reshape(n_seg, 3, 2), gp, gr, cost
+
+
+def schur_tight_solve(ptz0, rays0, u, v, frame, landmark, xy, loss='linear', f_scale=1.0, n_fixed=1,
+                      max_iter=100, tol=1e-11, log=None):
+    """Tight optimum of the reference BA cost (bundle_adjustment.py:25-106 residual, :200-202 least squares with
+    frame 0 as the fixed gauge, :197) at sizes where J cannot be materialised (headline: 29.2M x 41k): Levenberg-
+    Marquardt with Marquardt scaling, then undamped Gauss-Newton (for huber with the loss's own curvature weights,
+    _loss_weights) to a step of max |dx| < tol.  The landmarks are eliminated per 2x2 block (S = U - sum_l W_l V_l^-1 W_l^T as a sparse
+    product, dense Cholesky of the reduced pose system).  The stationary point is the same one scipy's trf
+    approaches; this is the parity target SURVEY §8c-4/5 prescribes (tight optimum of the reference residual).
+    Returns (ptz [n,3], rays [m,2], info dict)."""
+    import scipy.linalg as sla
+    import scipy.sparse as sp
+    ptz = np.array(ptz0, np.float64).copy()
+    rays = np.array(rays0, np.float64).copy()
+    n, m = len(ptz), len(rays)
+    frame = np.asarray(frame, np.int64)
+    landmark = np.asarray(landmark, np.int64)
+    key, seg = np.unique(landmark * n + frame, return_inverse=True)
+    seg = seg.astype(np.int64)
+    n_seg = len(key)
+    seg_lm, seg_fr = key // n, key % n
+    rows = (3 * seg_fr[:, None, None] + np.arange(3)[None, :, None]).repeat(2, 2).reshape(-1)
+    cols = (2 * seg_lm[:, None, None] + np.arange(2)[None, None, :]).repeat(3, 1).reshape(-1)
+    free = np.arange(3 * n_fixed, 3 * n)
+    lam, nu = None, 2.0
+    hist = []
+    it = 0
+    undamped = False
+    x_step = np.inf
+    while it < max_iter:
+        U, V, W, gp, gr, cost = _normal_blocks(ptz, rays, u, v, frame, landmark, xy, seg, n_seg, loss, f_scale)
+        Wm = sp.csr_matrix((W.reshape(-1), (rows, cols)), shape=(3 * n, 2 * m))
+        dU = np.einsum("nii->ni", U).reshape(-1)
+        dV = np.einsum("mii->mi", V).reshape(-1)
+        if lam is None:
+            lam = 1e-3
+        while True:
+            lv = 0.0 if undamped else lam
+            a_ = V[:, 0, 0] + lv * dV[0::2]
+            b_ = V[:, 0, 1]
+            c_ = V[:, 1, 1] + lv * dV[1::2]
+            det = a_ * c_ - b_ * b_
+            Vi = np.stack([c_ / det, -b_ / det, -b_ / det, a_ / det], -1).reshape(m, 2, 2)
+            bi = np.repeat(np.arange(m), 4) * 2 + np.tile([0, 0, 1, 1], m)
+            bj = np.repeat(np.arange(m), 4) * 2 + np.tile([0, 1, 0, 1], m)
+            Vsp = sp.csr_matrix((Vi.reshape(-1), (bi, bj)), shape=(2 * m, 2 * m))
+            Y = (Wm @ Vsp).tocsr()
+            S = sp.block_diag(list(U), format="csr").toarray() - (Y @ Wm.T).toarray()
+            S[np.diag_indices(3 * n)] += lv * dU
+            rhs = -gp.reshape(-1) + Y @ gr.reshape(-1)
+            Sf = S[np.ix_(free, free)]
+            dp = np.zeros(3 * n)
+            dp[free] = sla.cho_solve(sla.cho_factor(Sf, lower=True), rhs[free])
+            dr = -np.einsum("mij,mj->mi", Vi, gr + (Wm.T @ dp).reshape(m, 2))
+            ptz_t = ptz + dp.reshape(n, 3)
+            rays_t = rays + dr
+            cost_t = ba_cost_chunked(ptz_t, rays_t, u, v, frame, landmark, xy, loss, f_scale)
+            x_step = max(np.abs(dp).max(), np.abs(dr).max())
+            if cost_t <= cost or undamped:
+                break
+            lam *= nu
+            nu *= 2.0
+        it += 1
+        hist.append((it, cost, cost_t, 0.0 if undamped else lam, x_step))
+        if log:
+            log(f"  it {it}: cost {cost:.10f} -> {cost_t:.10f} lambda {0.0 if undamped else lam:.3g} max|dx| {x_step:.3e}")
+        ptz, rays = ptz_t, rays_t
+        if undamped:
+            if x_step < tol:
+                break
+        else:
+            lam = max(lam / 3.0, 1e-12)
+            nu = 2.0
+            if x_step < 1e-6:
+                undamped = True
+    cost = ba_cost_chunked(ptz, rays, u, v, frame, landmark, xy, loss, f_scale)
+    return ptz, rays, dict(cost=cost, iterations=it, last_step=float(x_step), history=np.array(hist),
+                           n_segments=n_seg)
+
+
 def ba_cost(x_full, n_pose, u, v, frame, landmark, xy, loss='linear', f_scale=1.0):
     """scipy cost convention: 0.5 * sum rho(r_i^2) over scalar residuals."""
     r = compute_residual_records(x_full, n_pose, u, v, frame, landmark, xy)

@@ -181,6 +181,45 @@ def test_config2_reference_residual_sample():
     assert abs(float(np.sum(r * r)) - float(d["r_ref_sumsq"])) <= 1e-10 * float(d["r_ref_sumsq"])
 
 
+def test_config3_optimum_fixture():
+    """Headline fixture (make_golden.py gen_config3): the records regenerate bit for bit, the oracle residual at x0
+    equals a sample of the REFERENCE's own _compute_residual (bundle_adjustment.py:25-106, run on all 29.2M values
+    when the fixture was made) and its sum of squares, and both stored optima are stationary points of the reference
+    cost (max |gradient| per parameter kind <= 1e-7 of its value at x0) with the stored costs."""
+    import synthetic
+    d = golden("config3_optimum.npz")
+    p = synthetic.make_problem("config3", seed=0)
+    fr, lm = p.frame.astype(np.int64), p.landmark.astype(np.int64)
+    assert len(fr) == int(d["n_records"]) and int(fr.sum()) == int(d["frame_sum"]) and int(lm.sum()) == int(d["landmark_sum"])
+    x0 = np.concatenate([p.init_ptz.reshape(-1), p.init_rays.reshape(-1)])
+    assert float(x0.sum()) == float(d["x0_sum"])
+    idx = d["r_ref_sample_idx"]
+    rec = np.unique(idx // 2)
+    r = orc.compute_residual_records(x0, p.n_pose, p.u, p.v, fr[rec], lm[rec], p.xy[rec])
+    r_all = np.full(2 * len(fr), np.nan)
+    r_all[np.repeat(2 * rec, 2) + np.tile([0, 1], len(rec))] = r
+    np.testing.assert_allclose(r_all[idx], d["r_ref_sample"], rtol=0, atol=1e-9)
+    assert np.all(d["grad_tight"] <= 1e-7 * d["grad_x0"]), (d["grad_tight"], d["grad_x0"])
+    assert np.all(d["grad_tight_huber"] <= 1e-7 * d["grad_x0_huber"]), (d["grad_tight_huber"], d["grad_x0_huber"])
+    for key, loss in (("", "linear"), ("_huber", "huber")):
+        c = orc.ba_cost_chunked(d["ptz_tight" + key], d["rays_tight" + key], p.u, p.v, fr, lm, p.xy, loss=loss)
+        assert abs(c - float(d["tight_cost" + key])) <= 1e-12 * c
+
+
+def test_schur_tight_solve_reproduces_config2_fixture():
+    """The landmark-eliminating tight solver behind the config-3 fixture (orc.schur_tight_solve) reproduces the
+    config-2 optimum that scipy trf + a sparse Gauss-Newton polish produced (config2_optimum.npz)."""
+    import synthetic
+    d = golden("config2_optimum.npz")
+    p = synthetic.make_problem("config2", seed=0)
+    ptz, rays, info = orc.schur_tight_solve(p.init_ptz, p.init_rays, p.u, p.v, p.frame, p.landmark, p.xy)
+    xt = d["x_tight"]
+    n = p.n_pose
+    np.testing.assert_allclose(ptz[1:].reshape(-1), xt[:3 * (n - 1)], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(rays.reshape(-1), xt[3 * (n - 1):], rtol=0, atol=1e-9)
+    assert abs(info["cost"] - float(d["tight_cost"])) <= 1e-10 * info["cost"]
+
+
 def test_synthetic_generator_matches_reference_rules():
     """problem_from_pairs reproduces the first-seen landmark ids and last-writer ray init."""
     import synthetic
