@@ -298,12 +298,19 @@ def main():
     h.set_state(prob.init_ptz, prob.init_rays)
     h.save_state()
 
+    # each solve restarts from the device-resident x0 and runs the C-driven LM (ptzba_solve_resident): the restart
+    # is enqueued by C the moment the final decision is on the host (PTZBA_BENCH_PYLOOP=1: the Python LMSolver loop)
+    pyloop = os.environ.get("PTZBA_BENCH_PYLOOP") == "1"
+
     def run_iters(hh, k, ar=None):
         done = 0
         solves = 0
         while done < k:
-            hh.restore_state()
-            res = ptzba.LMSolver(hh, ftol=1e-4, xtol=1e-8, max_iter=k - done, allreduce=ar).run()
+            if pyloop or ar is not None:
+                hh.restore_state()
+                res = ptzba.LMSolver(hh, ftol=1e-4, xtol=1e-8, max_iter=k - done, allreduce=ar).run()
+            else:
+                res = hh.solve_resident(restore=True, ftol=1e-4, xtol=1e-8, max_iter=k - done)
             done += max(res.njev, 1)
             solves += 1
             if res.njev == 0:
@@ -346,13 +353,29 @@ def main():
         k1_cold_ms, k1_cold_n = h.kernel_times()["linearize"]
     h.reset_kernel_times(False)
 
-    # accuracy: full fp32 LM solve vs a full fp64 solve of the same records, and vs ground truth
+    # accuracy: the benched arithmetic's solve vs the pinned oracle's tight optimum of the reference cost (the metric's
+    # "pan-tilt-focal RMSE vs reference": tests/golden/config3_optimum.npz, made by tests/golden/make_golden.py
+    # gen_config3 -- the oracle restatement of bundle_adjustment.py:25-106 minimised to a step < 1e-11, pinned to the
+    # reference's own residual on all 29.2M values), vs a full fp64 solve of the same records, and vs ground truth
     accuracy = None
     secondary = None
+    opt = None
+    opt_path = os.path.join(ROOT, "tests", "golden", f"{a.config}_optimum.npz")
+    if os.path.exists(opt_path):
+        z = np.load(opt_path)
+        if int(z["n_records"]) == len(prob.frame) and int(z["frame_sum"]) == int(prob.frame.astype(np.int64).sum()):
+            opt = {k: z[k] for k in ("ptz_tight", "rays_tight", "tight_cost", "ptz_tight_huber", "rays_tight_huber",
+                                     "tight_cost_huber")}
     if not a.no_accuracy and world == 1:
+        key = "_huber" if a.loss == "huber" else ""
+        if opt is not None:
+            # the solve exactly as benched (ftol=1e-4, the reference's termination) from x0
+            h.set_state(prob.init_ptz, prob.init_rays)
+            rb = ptzba.LMSolver(h, ftol=1e-4, xtol=1e-8, max_iter=100).run()
+            ptzb, raysb = h.get_state()
         h.set_state(prob.init_ptz, prob.init_rays)
         r32 = ptzba.LMSolver(h, ftol=1e-10, xtol=1e-12, max_iter=50).run()
-        ptz32, _ = h.get_state()
+        ptz32, rays32 = h.get_state()
         h64 = ptzba.BAHandle(0)
         h64.set_problem(prob.n_pose, prob.n_landmark, frame, landmark, xy, prob.u, prob.v, weight=w,
                         precision=ptzba.FP64, loss=loss, f_scale=1.0)
@@ -364,6 +387,18 @@ def main():
                         rmse_fp64_vs_ground_truth=[float(x) for x in synthetic.pose_rmse(ptz64, prob.gt_ptz)],
                         cost_fp32=r32.cost, cost_fp64=r64.cost, iters_fp32=r32.njev, iters_fp64=r64.njev,
                         components=["pan_deg", "tilt_deg", "f_px"])
+        if opt is not None:
+            pt, rt, ct = opt["ptz_tight" + key], opt["rays_tight" + key], float(opt["tight_cost" + key])
+            rr = lambda y: float(np.sqrt(np.mean((np.asarray(y) - rt) ** 2)))  # noqa: E731
+            accuracy["rmse_vs_oracle_optimum"] = {
+                "reference": f"tests/golden/{a.config}_optimum.npz ({a.loss} loss): tight optimum of the oracle restatement "
+                             "of the reference residual (bundle_adjustment.py:25-106), max step < 1e-11; gate 1e-4",
+                "bench_solve_ftol_1e-4": [float(x) for x in synthetic.pose_rmse(ptzb, pt)],
+                "bench_solve_rays_deg": rr(raysb), "bench_solve_iterations": rb.njev,
+                "bench_solve_cost_rel": (rb.cost - ct) / ct,
+                f"{a.precision}_tight": [float(x) for x in synthetic.pose_rmse(ptz32, pt)], f"{a.precision}_tight_rays_deg": rr(rays32),
+                "fp64_tight": [float(x) for x in synthetic.pose_rmse(ptz64, pt)],
+                "components": ["pan_deg", "tilt_deg", "f_px"]}
     if not a.no_secondary and world == 1 and not (a.precision == "fp64" and a.loss == "linear"):
         # the reference's own arithmetic and loss (fp64, linear: bundle_adjustment.py:200), same records
         hs = ptzba.BAHandle(0)
@@ -380,6 +415,13 @@ def main():
         run_iters(hs, min(5, a.steps))
         s_kt = hs.kernel_times()
         hs.reset_kernel_times(False)
+        if opt is not None and not a.no_accuracy:  # the reference's arithmetic vs the linear-loss optimum
+            hs.set_state(prob.init_ptz, prob.init_rays)
+            rs = ptzba.LMSolver(hs, ftol=1e-4, xtol=1e-8, max_iter=100).run()
+            ptzs, _ = hs.get_state()
+            s_rmse = {"ftol_1e-4": [float(x) for x in synthetic.pose_rmse(ptzs, opt["ptz_tight"])], "iterations": rs.njev}
+        else:
+            s_rmse = None
         s_alg = survey_bytes_k1(hs.info(), "fp64")
         s_alg_layout = algorithmic_bytes_k1(hs.info(), "fp64", w is not None)
         s_ach = s_alg / (s_k1 * 1e-3) / 1e9 if s_k1 > 0 else 0.0
@@ -391,7 +433,29 @@ def main():
                                   "frac_layout_bytes": s_alg_layout / (s_k1 * 1e-3) / 1e9 / HBM_PEAK_GBS if s_k1 > 0 else 0.0,
                                   "note": "fp64 K1 moves > 256 MB per launch (larger than the Infinity Cache)"},
                      "kernel_ms": {k: v[0] for k, v in s_kt.items()}}
+        if s_rmse:
+            secondary["rmse_vs_oracle_optimum"] = s_rmse
         hs.close()
+
+    # the drop-in call as a caller sees it (scene_map.py:91-115 times bundle_adjustment() as "BA time"): host
+    # preparation + upload (set_problem), x0 upload, the LM solve at the reference's ftol, the result download --
+    # NOT the metric (which excludes upload), reported beside it
+    dropin = None
+    if not a.no_secondary and world == 1:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        hd = ptzba.BAHandle(0)
+        hd.set_problem(prob.n_pose, prob.n_landmark, frame, landmark, xy, prob.u, prob.v, weight=w, precision=precision,
+                       loss=loss, f_scale=1.0)
+        t1 = time.perf_counter()
+        hd.set_state(prob.init_ptz, prob.init_rays)
+        rd = ptzba.LMSolver(hd, ftol=1e-4, xtol=1e-8, max_iter=100).run()
+        hd.get_state()
+        t2 = time.perf_counter()
+        hd.close()
+        dropin = {"set_problem_s": t1 - t0, "solve_and_io_s": t2 - t1, "total_s": t2 - t0, "iterations": rd.njev,
+                  "what": "ptzba.BAHandle: set_problem (host packing + upload) + set_state + LMSolver(ftol=1e-4) + "
+                          "get_state, one cold call (new handle)"}
 
     traffic = traffic_src = None  # PMC passes are taken on the whole problem (N = 1); a shard's launch moves less
     if world == 1 and os.path.exists(a.traffic_json):
@@ -474,6 +538,8 @@ def main():
             out["accuracy"] = accuracy
         if secondary:
             out["fp64_linear"] = secondary
+        if dropin:
+            out["dropin_call"] = dropin
         if not a.no_cpu_baseline and world == 1:
             # the full-size timing is the baseline (the scipy restatement on the 14.6M-record
             # problem itself); the keyframe-window power-law fit is kept beside it as a secondary field

@@ -165,7 +165,9 @@ PTZBA_EXPORT int ptzba_solve_reduced(ptzba_handle h);
  * lm_init; then per trial k: lm_build [all-reduce system]; lm_solve [all-reduce scalars];
  * lm_decide(k).  lm_wait(k) blocks until trial k's decision is on the host (a ring of 4 records: wait
  * for trial k before deciding trial k + 4).  Enqueueing trial k + 1's build before waiting for trial k
- * hides the host round trip; a build after the final decision is harmless. */
+ * hides the host round trip; a build after the final decision is harmless.  The state is double-buffered on
+ * the device (an accepted trial is committed by the decision itself); lm_wait of the final decision makes it the
+ * state ptzba_get_state / ptzba_save_state see, so every decided trial must be waited for. */
 typedef struct {
   double ftol, xtol, gtol;                    /* scipy's ftol/xtol/gtol tests (gtol <= 0: off) */
   double lambda0, min_lambda, max_lambda;     /* Marquardt damping: start, floor, give-up bound */
@@ -203,6 +205,10 @@ typedef struct {
 } ptzba_report;
 PTZBA_EXPORT int ptzba_solve(ptzba_handle h, double* ptz_inout, double* rays_inout, const ptzba_lm_opts* opts,
                              ptzba_report* report);
+/* The same solve on the device-resident state (no host state transfer): restore != 0 first restores the
+ * ptzba_save_state snapshot.  The state stays on the device (ptzba_get_state reads it).  Back-to-back solves
+ * from C keep the restart's host reaction out of the device's timeline (bench.py's restart loop). */
+PTZBA_EXPORT int ptzba_solve_resident(ptzba_handle h, int restore, const ptzba_lm_opts* opts, ptzba_report* report);
 PTZBA_EXPORT int ptzba_step(ptzba_handle h, double lambda);
 PTZBA_EXPORT int ptzba_read_scalars(ptzba_handle h, double* out /*PTZBA_NSCALARS*/);
 PTZBA_EXPORT int ptzba_accept(ptzba_handle h, int accept);
@@ -325,6 +331,13 @@ PTZBA_EXPORT int ptz_match_knn2(int device, int64_t n1, int64_t n2, int32_t dim,
 PTZBA_EXPORT int ptz_homography_ransac(int device, int64_t n, const double* pts1, const double* pts2, double threshold,
                                        int32_t n_hyp, uint64_t seed, uint8_t* mask_out, double* H_out,
                                        int32_t* n_inliers_out);
+/* n_sets independent RANSACs in one call (a new keyframe's pairwise matches, bundle_adjustment.py:145 ->
+ * image_process.py:178-234 once per pair): set s = correspondences [off[s], off[s + 1]) of pts1 / pts2 (off[0] =
+ * 0, each set >= 4); mask_out[off[n_sets]], H_out[9 n_sets], n_inliers_out[n_sets].  Per set the result of
+ * ptz_homography_ransac with the same seed, bit for bit. */
+PTZBA_EXPORT int ptz_homography_ransac_batch(int device, int32_t n_sets, const int64_t* off, const double* pts1,
+                                             const double* pts2, double threshold, int32_t n_hyp, uint64_t seed,
+                                             uint8_t* mask_out, double* H_out, int32_t* n_inliers_out);
 /* Pyramidal Lucas-Kanade point tracking (cv.calcOpticalFlowPyrLK(img, next_img, points, None, winSize=(31, 31))
  * as called by optical_flow_matching, image_process.py:393-415).  img0/img1: 8-bit grey, width x height,
  * row-major.  Pyramid of `levels` (cv.pyrDown: 5x5 binomial, reflect-101), Scharr gradients, window `win`

@@ -119,6 +119,7 @@ def bundle_adjustment(images, image_indices, feature_method, initial_ptzs, cente
             image_process.draw_matches(images[i], images[j], pts[i][g.k1[a:b]], pts[j][g.k2[a:b]],
                                        save_path + "/" + str(i) + "_" + str(j) + ".jpg")
     timing["graph"] = time.time() - t_start
+    timing.update(getattr(g, "timing", {}))
 
     # step 2: data (bundle_adjustment.py:167-197)
     t1 = time.time()
@@ -155,6 +156,7 @@ def bundle_adjustment(images, image_indices, feature_method, initial_ptzs, cente
         if verbose:
             print(f"GPU LM: {res}")
     timing["solve"] = time.time() - t0
+    timing.update({"solve_" + k: v for k, v in ptzba.LAST_SOLVE_TIMING.items()})
 
     # step 5: keyframes (bundle_adjustment.py:214-248), features in the reference's set() order
     t2 = time.time()

@@ -30,6 +30,8 @@ interpreter once per process (`_self_check`); if they ever disagree the interpre
 """
 import random
 
+import time
+
 import numpy as np
 
 import image_process
@@ -124,6 +126,13 @@ class CorrespondenceCache:
         self.n_match += 1
         self.matches[k] = m
         return m
+
+    def peek(self, key_i, key_j, feature_method):
+        return self.matches.get((key_i, key_j, feature_method))
+
+    def store(self, key_i, key_j, feature_method, m):
+        self.n_match += 1
+        self.matches[(key_i, key_j, feature_method)] = m
 
     def forget(self, key):
         self.detections = {k: v for k, v in self.detections.items() if k[0] != key}
@@ -225,6 +234,7 @@ def build_graph(images, image_match_mask=(), feature_method="sift", verbose=Fals
     if cache is not None:
         if keys is None or len(keys) != n or len(set(keys)) != n:
             cache = None  # keys must identify the images uniquely
+    t_det = time.perf_counter()
     dets = []
     for f, im in enumerate(images):
         if cache is not None:
@@ -232,21 +242,37 @@ def build_graph(images, image_match_mask=(), feature_method="sift", verbose=Fals
         else:
             kps, des = image_process._detect(im, feature_method)
             dets.append((kps, des, np.array([k.pt for k in kps], dtype=np.float64).reshape(-1, 2)))
+    t_match = time.perf_counter()
+    todo = [(i, j) for i in range(n) for j in range(i + 1, n)
+            if not (len(image_match_mask) != 0 and image_match_mask[i][j] == 0)]
+    # GPU SIFT matcher: every pair still to match in one batched call (kNN-2 per train image over the concatenated
+    # queries, one RANSAC launch for all pairs) -- per pair exactly match_sift_features' result
+    pre = {}
+    if feature_method == "sift" and image_process.match_sift_features is image_process.GPU_MATCH_SIFT:
+        need = [(i, j) for i, j in todo if cache is None or cache.peek(keys[i], keys[j], feature_method) is None]
+        if len(need) > 1:
+            res = image_process.match_sift_features_batch(
+                [(dets[i][0], dets[i][1], dets[j][0], dets[j][1]) for i, j in need])
+            for (i, j), (a, b) in zip(need, res):
+                m = (np.asarray(a, dtype=np.int32).reshape(-1), np.asarray(b, dtype=np.int32).reshape(-1))
+                pre[(i, j)] = m
+                if cache is not None:
+                    cache.store(keys[i], keys[j], feature_method, m)
     pi, pj, raw = [], [], []
-    for i in range(n):
-        for j in range(i + 1, n):
-            if len(image_match_mask) != 0 and image_match_mask[i][j] == 0:
-                continue
-            if cache is not None:
-                a, b = cache.match(keys[i], keys[j], dets[i], dets[j], feature_method)
-            else:
-                a, b = _match_raw(dets[i], dets[j], feature_method)
-            if len(a) > MIN_MATCH_NUM:
-                pi.append(i)
-                pj.append(j)
-                raw.append((a, b))
-            elif verbose:
-                print("no enough matches between image: %d and %d" % (i, j))
+    for i, j in todo:
+        if (i, j) in pre:
+            a, b = pre[(i, j)]
+        elif cache is not None:
+            a, b = cache.match(keys[i], keys[j], dets[i], dets[j], feature_method)
+        else:
+            a, b = _match_raw(dets[i], dets[j], feature_method)
+        if len(a) > MIN_MATCH_NUM:
+            pi.append(i)
+            pj.append(j)
+            raw.append((a, b))
+        elif verbose:
+            print("no enough matches between image: %d and %d" % (i, j))
+    t_cap = time.perf_counter()
     # 200-match cap: the reference's random.shuffle sequence, replayed in pair order
     capped = [p for p, (a, _) in enumerate(raw) if len(a) > MAX_MATCH_NUM]
     if capped:
@@ -262,6 +288,7 @@ def build_graph(images, image_match_mask=(), feature_method="sift", verbose=Fals
         for p in range(len(pi)):
             print("%d matches between image: %d and %d" % (cnt[p], pi[p], pj[p]))
     g = MatchGraph([d[0] for d in dets], [d[1] for d in dets], [d[2] for d in dets], pi, pj, off, k1, k2)
+    g.timing = {"detect_s": t_match - t_det, "match_s": t_cap - t_match, "cap_graph_s": time.perf_counter() - t_cap}
     if g.n_inconsistent and verbose:
         print("Warning: %d in-consistent matching results" % g.n_inconsistent)
     if verbose:

@@ -94,6 +94,12 @@ struct ptzba_ctx {
   // device-driven LM: state, pinned record ring, events
   DBuf lmdev;
   LMDev* lm_host = nullptr;
+  // device-driven LM: the value of LMDev::cur at which (ptz, rays) -- not (ptz_trial, rays_trial) -- hold the current
+  // state (BacksubArgs::state_xor); lm_wait swaps the pointers when the device's decisions moved it
+  int state_base = 0;
+  // single-GPU device-driven LM: the trial-cost reduction waits for ptzba_lm_decide, which fuses the decision into it
+  bool scal_deferred = false;
+  bool scal_exported = false;  // ptzba_exchange handed out the scalar buffer (a caller-run scalar exchange)
   // timing
   int timing = 0;  // bitmask of timed kernel groups (1 K1, 2 Schur, 4 Cholesky solve, 8 back-substitution)
   std::vector<hipEvent_t> ev[TM_N];
@@ -1025,6 +1031,15 @@ static bool dist_order(int n_pose, int nf, const std::vector<int32_t>& win, SysO
 int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_t n_obs, const int32_t* obs_frame,
                       const int32_t* obs_landmark, const double* obs_xy, const double* obs_weight, double u, double v,
                       const ptzba_problem_opts* opts) {
+  // PTZBA_SETUP_TIMING=1: host phase times of this call on stderr (where a config-4 set_problem spends its seconds)
+  static const bool st_on = getenv("PTZBA_SETUP_TIMING") != nullptr;
+  auto st_t0 = std::chrono::steady_clock::now();
+  auto st_mark = [&](const char* what) {
+    if (!st_on) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "set_problem %-22s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(t - st_t0).count());
+    st_t0 = t;
+  };
   if (!h) return fail("null handle");
   if (n_pose < 1 || n_landmark < 0 || n_obs < 0) return fail("bad sizes n_pose=%d n_landmark=%d n_obs=%lld", n_pose, n_landmark, (long long)n_obs);
   if (n_obs > 0 && (!obs_frame || !obs_landmark || !obs_xy)) return fail("null observation pointer");
@@ -1061,6 +1076,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->v = v;
   h->weighted = obs_weight != nullptr;
 
+  st_mark("validate");
   // ---- stable counting sorts: by frame, then by landmark -> (landmark, frame, original index)
   std::vector<int64_t> tmp(n_obs), order(n_obs);
   {
@@ -1076,6 +1092,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       order[d[obs_landmark[r]]++] = r;
     }
   }
+  st_mark("sort");
   // ---- segments (unique landmark, frame)
   std::vector<int32_t> seg_frame, seg_lm, rec_seg(n_obs);
   std::vector<int64_t> seg_rec_begin;
@@ -1112,6 +1129,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     }
     frame_win_hi[f] = hi;
   }
+  st_mark("segments+frame csr");
   // ---- register-blocked K2 structure: per landmark its frame range [first, last] and a dense W slot
   // per frame in it; K2 tiles (SCHUR_F1 frames x 64 partner frames) with the landmarks that reach them,
   std::vector<int32_t> lm_meta(4 * (size_t)std::max(n_landmark, 1), 0), s2_items, s2_groups,
@@ -1266,6 +1284,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
         if (!cov[(f1b - o.n_fixed) / SCHUR_F1]) h->f1_covered = false;
     }
   }
+  st_mark("k2 structure");
   // ---- landmark work order: heaviest (most records) first
   std::vector<int32_t> lm_order;
   int max_seg = 0;
@@ -1374,6 +1393,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->perm_host = order;
   h->perm_uploaded = false;
 
+  st_mark("work order+plan");
   // ---- upload
   std::vector<double> seg_base(2 * n_seg);
   for (int64_t s = 0; s < n_seg; ++s) {
@@ -1484,17 +1504,20 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   HIPCHK(hipMemsetAsync(h->rays.p, 0, h->rays.bytes, h->st));
   HIPCHK(hipMemsetAsync(h->scal.p, 0, h->scal.bytes, h->st));
   HIPCHK(hipMemsetAsync(h->red_scratch.p, 0, h->red_scratch.bytes, h->st));
+  st_mark("upload+alloc");
   if (!h->scal_host) HIPCHK(hipHostMalloc((void**)&h->scal_host, 24 * sizeof(double), hipHostMallocDefault));
   if (!h->scal_pack.p && h->scal_pack.alloc(24 * sizeof(double))) return -1;
   h->cur = 0;
   h->lambda = 0;
   HIPCHK(hipStreamSynchronize(h->st));  // every initialisation above has landed before the handle is used
   h->have_problem = true;
-  if (h->group_comm) {  // the group of the previous problem; split anew (collective: every rank sets its problem)
+  if (h->group_comm) {  // the group of the previous problem; split anew at the first exchange of this one
     ptzba_comm_delete(h->group_comm);
     h->group_comm = nullptr;
   }
-  return ensure_group_comm(h);
+  // no collective here: a rank whose set_problem failed validation above must not leave the others blocked in a
+  // split.  The group communicator is split by the first exchange (ensure_group_comm), which every rank reaches.
+  return 0;
 }
 
 int ptzba_problem_info(ptzba_handle h, int64_t* info) {
@@ -1562,6 +1585,7 @@ static void linearize_into(ptzba_ctx* h, int slot, const int* sel = nullptr, int
   a.ug_slot1 = h->ug_slot[1].p;
   a.w_slot1 = h->w_slot[1].p;
   a.lm_out1 = h->lm_out[1].as<double>();
+  a.n_pose = h->n_pose;
   tm_begin(h, TM_K1);
   if (h->precision == PTZBA_FP32)
     launch_linearize<float>(a, h->loss, h->st);
@@ -1669,6 +1693,9 @@ static int exchange(ptzba_ctx* h, int kind, double* buf, int64_t n) {
     return 0;
   }
   if (h->comm) {
+    // ncclCommSplit is collective over comm: done before this rank's first exchange of the problem, where every
+    // rank of a sharded solve arrives in the same order
+    if (ensure_group_comm(h)) return fail("group communicator split failed");
     ptzba_comm c = kind == PTZBA_X_PART ? h->group_comm : h->comm;
     if (!c) return fail("part-owned group of %d ranks has no group communicator (ptzba_attach_comm)", h->group_size);
     return ptzba_comm_allreduce(c, buf, n, (void*)h->st);
@@ -1841,6 +1868,7 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
   b.w_slot1 = h->w_slot[1].p;
   b.lm_out1 = h->lm_out[1].as<double>();
   b.sel = sel;
+  b.state_xor = h->state_base;
   // ray back-substitution, trial poses and the trial's frame / ray tables: one launch
   const uint8_t* fm = h->dist_mode ? h->fmask.as<uint8_t>() : nullptr;
   const int* finfo = h->dist_mode ? h->info.as<int>() : nullptr;
@@ -1854,6 +1882,11 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
   // trial linearisation (its cost decides acceptance; kept as the next linearisation if accepted)
   linearize_into(h, nx, sel, 1);
   // scal[1] (trial cost) and scal[2..4] are overwritten below, loc[0..3] by the trial kernel: no memsets
+  if (sel && !h->has_exchange() && !h->ext_exchange && !h->scal_exported && !h->dist_mode) {
+    // launched by ptzba_lm_decide with the decision fused into it (nothing runs between the two calls)
+    h->scal_deferred = true;
+    return 0;
+  }
   launch_reduce_cols(h->lm_out[sel ? 0 : nx].as<double>() + 5, h->n_lm, 8, 1, 0, h->scal.as<double>() + 1,
                      h->red_scratch.as<double>(), h->st, h->lm_red.as<double>(), 4, 3, h->scal.as<double>() + 2,
                      h->lm_out[1].as<double>() + 5, sel, 1);
@@ -1904,6 +1937,8 @@ int ptzba_lm_init(ptzba_handle h, const ptzba_lm_opts* o) {
   // no decision of an earlier run is in flight (its lm_wait returned): clear the ring's sequence tags
   for (int k = 0; k < LM_RING; ++k) __atomic_store_n(&h->lm_host[k].seq, 0, __ATOMIC_RELAXED);
   launch_lm_init(h->lmdev.as<LMDev>(), h->scal.as<double>(), p, h->cur, h->st);
+  h->state_base = h->cur;  // (ptz, rays) hold the current state now
+  h->scal_deferred = false;
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1927,11 +1962,20 @@ int ptzba_lm_decide(ptzba_handle h, int trial) {
   HIPCHK(hipSetDevice(h->device));
   LMDev* st = h->lmdev.as<LMDev>();
   const int k = trial % LM_RING;
-  // the record is written by the decision kernel straight into pinned host memory
-  launch_lm_decide(st, h->scal.as<double>(), h->locp(), h->info.as<int>(), h->lm_host + k, trial + 1,
-                   h->st, h->dist_mode);
-  launch_lm_commit(st, h->ptz.as<double>(), h->ptz_trial.as<double>(), 3 * h->n_pose, h->rays.as<double>(),
-                   h->rays_trial.as<double>(), 2 * (int64_t)h->n_lm, h->st);
+  // the record is written by the decision straight into pinned host memory.  No commit copy: an accepted trial
+  // flips LMDev::cur, which selects the state pair as it selects the linearisation slot (BacksubArgs::state_xor)
+  if (h->scal_deferred) {
+    // single GPU: the trial-cost reduction (deferred by lm_solve) with the decision in its last workgroup
+    h->scal_deferred = false;
+    const int* sel = &h->lmdev.as<LMDev>()->cur;
+    const DecideArgs dec{st, h->locp(), h->info.as<int>(), h->lm_host + k, trial + 1};
+    launch_reduce_cols(h->lm_out[0].as<double>() + 5, h->n_lm, 8, 1, 0, h->scal.as<double>() + 1,
+                       h->red_scratch.as<double>(), h->st, h->lm_red.as<double>(), 4, 3, h->scal.as<double>() + 2,
+                       h->lm_out[1].as<double>() + 5, sel, 1, &dec);
+  } else {
+    launch_lm_decide(st, h->scal.as<double>(), h->locp(), h->info.as<int>(), h->lm_host + k, trial + 1,
+                     h->st, h->dist_mode);
+  }
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1964,6 +2008,15 @@ int ptzba_lm_wait(ptzba_handle h, int trial, ptzba_lm_record* out) {
   out->done = r.done;
   out->accepted = r.accepted;
   h->cur = r.cur;  // the host's view of the current slot follows the device (ptzba_accept / linearize)
+  if ((r.cur ^ h->state_base) & 1) {
+    // the device's decisions moved the current state to the other pair: swap the pointers and the base together,
+    // so that kernels already queued (old pair, old base) and later ones (new pair, new base) select the same buffer
+    std::swap(h->ptz.p, h->ptz_trial.p);
+    std::swap(h->ptz.bytes, h->ptz_trial.bytes);
+    std::swap(h->rays.p, h->rays_trial.p);
+    std::swap(h->rays.bytes, h->rays_trial.bytes);
+    h->state_base ^= 1;
+  }
   return 0;
 }
 
@@ -1972,15 +2025,10 @@ int ptzba_lm_wait(ptzba_handle h, int trial, ptzba_lm_record* out) {
 // ftol=1e-4, method='trf') of bundle_adjustment.py:200-202 and the empty C stub bundle_adjustment_opt
 // (rf_map/python_package/backup/bundle_adjustment_python.hpp:21-24): the state goes in and the optimum
 // comes out through the caller's buffers (rf_map.cpp:77, 113-116 in/out convention).
-int ptzba_solve(ptzba_handle h, double* ptz_inout, double* rays_inout, const ptzba_lm_opts* opts,
-                ptzba_report* report) {
-  if (!h || !h->have_problem) return fail("no problem set");
-  if (!ptz_inout || (h->n_lm > 0 && !rays_inout)) return fail("null state buffer");
-  const ptzba_lm_opts def{1e-4, 1e-8, 0.0, 1e-4, 1e-12, 1e16, 100, 30, 0};
-  const ptzba_lm_opts o = opts ? *opts : def;
-  const auto t0 = std::chrono::steady_clock::now();
-  if (ptzba_set_state(h, ptz_inout, rays_inout) || ptzba_lm_start(h) || ptzba_lm_init(h, &o)) return -1;
-  ptzba_lm_record rec{};
+// the device-driven LM from the handle's current device state to termination (shared by the one-shot entries)
+static int lm_run(ptzba_ctx* h, const ptzba_lm_opts& o, ptzba_lm_record& rec) {
+  if (ptzba_lm_start(h) || ptzba_lm_init(h, &o)) return -1;
+  rec = ptzba_lm_record{};
   if (o.max_iter > 0) {
     const int64_t limit = (int64_t)o.max_iter * (o.max_retries + 1);
     if (ptzba_lm_build(h)) return -1;
@@ -1997,6 +2045,38 @@ int ptzba_solve(ptzba_handle h, double* ptz_inout, double* rays_inout, const ptz
     rec.cost = rec.initial_cost = s[0];
     rec.nfev = 1;
   }
+  return 0;
+}
+static const ptzba_lm_opts k_default_opts{1e-4, 1e-8, 0.0, 1e-4, 1e-12, 1e16, 100, 30, 0};
+
+int ptzba_solve_resident(ptzba_handle h, int restore, const ptzba_lm_opts* opts, ptzba_report* report) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  const ptzba_lm_opts o = opts ? *opts : k_default_opts;
+  const auto t0 = std::chrono::steady_clock::now();
+  if (restore && ptzba_restore_state(h)) return -1;
+  ptzba_lm_record rec{};
+  if (lm_run(h, o, rec)) return -1;
+  if (report) {
+    report->cost = rec.cost;
+    report->initial_cost = rec.initial_cost;
+    report->time_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    report->iterations = rec.iterations;
+    report->nfev = rec.nfev;
+    report->trials = rec.trials;
+    report->status = rec.status;
+  }
+  return 0;
+}
+
+int ptzba_solve(ptzba_handle h, double* ptz_inout, double* rays_inout, const ptzba_lm_opts* opts,
+                ptzba_report* report) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  if (!ptz_inout || (h->n_lm > 0 && !rays_inout)) return fail("null state buffer");
+  const ptzba_lm_opts o = opts ? *opts : k_default_opts;
+  const auto t0 = std::chrono::steady_clock::now();
+  if (ptzba_set_state(h, ptz_inout, rays_inout)) return -1;
+  ptzba_lm_record rec{};
+  if (lm_run(h, o, rec)) return -1;
   std::vector<double> ptz(3 * (size_t)h->n_pose), rays(2 * (size_t)h->n_lm);
   if (ptzba_get_state(h, ptz.data(), rays.data())) return -1;
   std::copy(ptz.begin(), ptz.end(), ptz_inout);
@@ -2057,7 +2137,10 @@ int ptzba_exchange(ptzba_handle h, void** sys_ptr, int64_t* sys_count, void** sc
   if (sys_ptr) h->ext_exchange = true;  // the caller may sum the system between build and solve: prepare after it
   if (sys_ptr) *sys_ptr = h->sys.p;
   if (sys_count) *sys_count = h->sys_count();
-  if (scal_ptr) *scal_ptr = h->scal.p;
+  if (scal_ptr) {
+    *scal_ptr = h->scal.p;
+    h->scal_exported = true;  // the caller may sum the scalars between lm_solve and lm_decide: no fused decision
+  }
   return 0;
 }
 
@@ -2096,7 +2179,7 @@ int ptzba_attach_comm(ptzba_handle h, ptzba_comm comm) {
     h->group_comm = nullptr;
   }
   h->comm = comm;
-  return ensure_group_comm(h);
+  return 0;  // the group communicator is split lazily by the first exchange (collective, every rank reaches it)
 }
 
 int ptzba_dist_info(ptzba_handle h, int64_t* info8) {
@@ -2331,9 +2414,13 @@ int ptzba_plan_export(int32_t n_pose, int32_t n_fixed, const int32_t* frame_win_
   counts[1] = nl;
   counts[2] = so.n_aug;
   counts[3] = plan.delayed ? 1 : 0;
+  // a null output buffer only queries the counts; a non-null one that is too small is an error (no partial copy)
+  if (tasks_out && tasks_cap < nt) return fail("tasks buffer holds %lld tasks, the plan has %lld", (long long)tasks_cap, (long long)nt);
+  if (level_off_out && levels_cap < nl + 1)
+    return fail("level offset buffer holds %lld entries, the plan needs %lld", (long long)levels_cap, (long long)(nl + 1));
   if (pos_out) std::copy(so.pos.begin(), so.pos.end(), pos_out);
-  if (tasks_out && tasks_cap >= nt) std::copy(plan.tasks.begin(), plan.tasks.end(), tasks_out);
-  if (level_off_out && levels_cap >= nl + 1) std::copy(plan.level_off.begin(), plan.level_off.end(), level_off_out);
+  if (tasks_out) std::copy(plan.tasks.begin(), plan.tasks.end(), tasks_out);
+  if (level_off_out) std::copy(plan.level_off.begin(), plan.level_off.end(), level_off_out);
   return 0;
 }
 

@@ -161,14 +161,19 @@ __device__ long long g_k1_items[32768][8];  // start, end, A, B, C, final, segme
 #define K1_NOW(t) do { } while (0)
 #define K1_ACC(k, t0, t1) do { } while (0)
 #endif
-template <typename real, int LOSS>
+// FTL: the frame tables are staged in LDS (n_pose <= K1_FT_LDS): phase A's chain is descriptor -> segment frame id
+// -> LDS instead of descriptor -> frame id -> global frame table (one dependent memory latency less per wave)
+template <typename real, int LOSS, bool FTL>
 __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVES64) void k_linearize(LinArgs a) {
   constexpr bool COARSE = sizeof(real) == 4 ? K1_COARSE : K1_COARSE64;
   __shared__ real s_x[4][SEGW], s_y[4][SEGW], s_acc[4][4][SEGW];
+  __shared__ double s_ft[5][FTL ? K1_FT_LDS : 1];  // ca, sa, cb, sb, f per frame (fp64)
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
   const int task = blockIdx.x * 4 + wv;
-  if (task >= a.n_work) return;  // whole wave leaves; no block-level barriers in this kernel
+  if constexpr (!FTL) {
+    if (task >= a.n_work) return;  // whole wave leaves; no block-level barriers in this variant
+  }
   long long kt0 = 0, kt1 = 0, kt2 = 0, kt3 = 0, kt4 = 0, k1acc[4] = {0, 0, 0, 0};
   (void)kt0; (void)kt1; (void)kt2; (void)kt3; (void)kt4; (void)k1acc;
   K1_NOW(kt0);
@@ -178,8 +183,27 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
   // one 32-B work descriptor {landmark, first segment, end segment, first record | first frame, last
   // frame, slot offset, end record of the first window}: no dependent lm_order -> lm_seg_begin -> seg_rec_begin -> lm_meta chain before
   // the records and the frame tables can be requested
-  const int4 wd = a.lm_work[2 * task];
-  const int4 wm = a.lm_work[2 * task + 1];
+  const int tq = FTL ? min(task, a.n_work - 1) : task;
+  const int4 wd = a.lm_work[2 * tq];
+  const int4 wm = a.lm_work[2 * tq + 1];
+  if constexpr (FTL) {
+    // the whole frame table (<= 640 frames, 20 KB at config 3), requested beside the descriptor: both latencies
+    // overlap, and the barrier below is the block's only one
+    const double4* src = reinterpret_cast<const double4*>(a.ft64);
+    for (int e = threadIdx.x; e < a.n_pose; e += blockDim.x) {
+      const double4 t0 = src[2 * e];
+      const double f = reinterpret_cast<const double*>(a.ft64)[8 * e + 4];
+      s_ft[0][e] = t0.x; s_ft[1][e] = t0.y; s_ft[2][e] = t0.z; s_ft[3][e] = t0.w; s_ft[4][e] = f;
+    }
+    __syncthreads();
+    if (task >= a.n_work) return;  // whole wave leaves after the barrier
+  }
+  auto ft_lds = [&](int fs) {
+    FrameTab<double> F;
+    F.ca = s_ft[0][fs]; F.sa = s_ft[1][fs]; F.cb = s_ft[2][fs]; F.sb = s_ft[3][fs]; F.f = s_ft[4][fs];
+    F.pad0 = F.pad1 = F.pad2 = 0.0;
+    return F;
+  };
   const int l = wd.x, s0 = wd.y, s1 = wd.z;
   const FrameTab<double>* __restrict__ ft64 = (const FrameTab<double>*)a.ft64;
   const RayTab<double> R64 = ((const RayTab<double>*)a.rt64)[l];
@@ -418,16 +442,19 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
         const int fs = a.seg_frame[s];
         fsv[i] = fs;
         double x, y;
-        ptz_project<double>(ft64[fs], R64, a.u, a.v, x, y);
+        if constexpr (FTL) ptz_project<double>(ft_lds(fs), R64, a.u, a.v, x, y);
+        else ptz_project<double>(ft64[fs], R64, a.u, a.v, x, y);
         const double2 bs = seg_base[s];
         sx[sl] = (real)(x - bs.x);
         sy[sl] = (real)(y - bs.y);
         acc0[sl] = 0; acc1[sl] = 0; acc2[sl] = 0; acc3[sl] = 0;
       }
 #if !K1_FTV_LATE
-      // the five used fields only (not the 32-B struct)
-      const FrameTab<real>* fp = ft + fsv[i];
-      ftv[i].ca = fp->ca; ftv[i].sa = fp->sa; ftv[i].cb = fp->cb; ftv[i].sb = fp->sb; ftv[i].f = fp->f;
+      if constexpr (!FTL) {  // (FTL: phase C reads its tables from LDS)
+        // the five used fields only (not the 32-B struct)
+        const FrameTab<real>* fp = ft + fsv[i];
+        ftv[i].ca = fp->ca; ftv[i].sa = fp->sa; ftv[i].cb = fp->cb; ftv[i].sb = fp->sb; ftv[i].f = fp->f;
+      }
 #endif
     }
     wave_lds_fence();
@@ -478,11 +505,20 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
       const int sl = s - w0;
       real x, y, J[2][5];
       const int fs = fsv[i];
+      if constexpr (FTL) {
+        // the record-precision table is the rounded fp64 one (k_tables): the same values as ft[fs]
+        FrameTab<real> F;
+        F.ca = (real)s_ft[0][fs]; F.sa = (real)s_ft[1][fs]; F.cb = (real)s_ft[2][fs]; F.sb = (real)s_ft[3][fs];
+        F.f = (real)s_ft[4][fs];
+        F.pad0 = F.pad1 = F.pad2 = (real)0;
+        ptz_project_jac<real>(F, R, u, v, x, y, J);
+      } else {
 #if K1_FTV_LATE
-      ptz_project_jac<real>(ft[fs], R, u, v, x, y, J);
+        ptz_project_jac<real>(ft[fs], R, u, v, x, y, J);
 #else
-      ptz_project_jac<real>(ftv[i], R, u, v, x, y, J);
+        ptz_project_jac<real>(ftv[i], R, u, v, x, y, J);
 #endif
+      }
       const real Sx = acc0[sl], Sy = acc1[sl], Srx = acc2[sl], Sry = acc3[sl];
       // W = Jp^T diag(Sx,Sy) Jr (3x2), U = Jp^T diag Jp (upper: 00 01 02 11 12 22), g_pose = Jp^T (w r)
       real W[6];
@@ -535,8 +571,15 @@ template <typename real>
 void launch_linearize(const LinArgs& a, int loss, hipStream_t st) {
   if (a.n_work <= 0) return;
   dim3 grid((a.n_work + 3) / 4);
-  if (loss == 0) hipLaunchKernelGGL((k_linearize<real, 0>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((k_linearize<real, 1>), grid, dim3(256), 0, st, a);
+  static const bool ftl_off = getenv("PTZBA_K1_FTL") && atoi(getenv("PTZBA_K1_FTL")) == 0;  // A/B knob
+  const bool ftl = a.n_pose <= K1_FT_LDS && !ftl_off;
+  if (ftl) {
+    if (loss == 0) hipLaunchKernelGGL((k_linearize<real, 0, true>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_linearize<real, 1, true>), grid, dim3(256), 0, st, a);
+  } else {
+    if (loss == 0) hipLaunchKernelGGL((k_linearize<real, 0, false>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_linearize<real, 1, false>), grid, dim3(256), 0, st, a);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -559,16 +602,21 @@ __global__ __launch_bounds__(256) void k_build_prologue(double* __restrict__ S, 
   if (b < n_tiles) {
     const int2 tij = zt[b];
     double* T = S + (int64_t)tij.x * CHOL_NB * ld + (int64_t)tij.y * CHOL_NB;
-    for (int e = threadIdx.x; e < CHOL_NB * CHOL_NB / 2; e += blockDim.x)
-      *reinterpret_cast<double2*>(T + (int64_t)(e >> 4) * ld + 2 * (e & 15)) = make_double2(0.0, 0.0);
-    if (fp.pad && tij.x == tij.y && threadIdx.x < CHOL_NB) {
-      // single-GPU build: the constant diagonal entries of k_chol_prepare (identity on padding rows, the
-      // augmented diagonal, identity below it), written with the zeroing (same wave, after its stores)
-      const int64_t r = (int64_t)tij.x * CHOL_NB + threadIdx.x;
-      double dv = 0.0;
-      if (r < fp.n_aug) dv = fp.pad[r] ? 1.0 : 0.0;
-      else dv = r == fp.n_aug ? 1e300 : 1.0;
-      if (dv != 0.0) S[r * ld + r] = dv;
+    const bool diag_tile = fp.pad && tij.x == tij.y;
+    for (int e = threadIdx.x; e < CHOL_NB * CHOL_NB / 2; e += blockDim.x) {
+      const int row = e >> 4, c0 = 2 * (e & 15);
+      double2 v = make_double2(0.0, 0.0);
+      if (diag_tile && (row == c0 || row == c0 + 1)) {
+        // single-GPU build: the constant diagonal entries of k_chol_prepare (identity on padding rows, the
+        // augmented diagonal, identity below it).  The thread that zeroes the double2 holding (row, row)
+        // stores the value itself, so no other thread's zero store can land after it.
+        const int64_t r = (int64_t)tij.x * CHOL_NB + row;
+        double dv;
+        if (r < fp.n_aug) dv = fp.pad[r] ? 1.0 : 0.0;
+        else dv = r == fp.n_aug ? 1e300 : 1.0;
+        if (row == c0) v.x = dv; else v.y = dv;
+      }
+      *reinterpret_cast<double2*>(T + (int64_t)row * ld + c0) = v;
     }
     return;
   }
@@ -648,11 +696,24 @@ struct PoseTrialArgs {
   const uint8_t* fmask;  // part-owned solve: bit 0 pose updated here, bit 1 counted here (nullptr: all)
   const int* info;       // part-owned solve: this rank's factorisation status -> out4[4] (summed over ranks)
 };
-template <typename real>
+// DPL: the pose steps by frame staged in LDS (n_pose <= K1_FT_LDS): a landmark wave walks its DENSE slot range
+// [first, last] (slots of frames that do not see it hold W = 0) instead of its segment list, so its dependent chain
+// is lm_meta -> W slots (+ LDS) instead of segment list -> frame -> system row -> dpose
+template <typename real, bool DPL>
 __global__ __launch_bounds__(256) void k_trial(BacksubArgs a, PoseTrialArgs pa, FrameTab<double>* __restrict__ ft64,
                                                RayTab<double>* __restrict__ rt64, FrameTab<real>* __restrict__ ft,
                                                RayTab<real>* __restrict__ rt) {
   const int nb = (a.n_lm + 3) / 4;
+  // device-driven LM: current state and trial output by the decision's slot (BacksubArgs::state_xor)
+  const bool sflip = a.sel && (((*a.sel) ^ a.state_xor) & 1);
+  if (sflip) {
+    const double* t = pa.ptz;
+    pa.ptz = pa.ptz_trial;
+    pa.ptz_trial = const_cast<double*>(t);
+    const double* u = a.rays;
+    a.rays = a.rays_trial;
+    a.rays_trial = const_cast<double*>(u);
+  }
   if ((int)blockIdx.x == nb) {
     const double lambda = a.lam_dev ? *a.lam_dev : a.lambda;
     __shared__ double red[4][256 / WAVE];
@@ -704,6 +765,15 @@ __global__ __launch_bounds__(256) void k_trial(BacksubArgs a, PoseTrialArgs pa, 
   }
   const int lane = lane_id();
   const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ double s_dp[DPL ? 3 * K1_FT_LDS : 1];
+  if constexpr (DPL) {
+    // dpose by frame (0 for fixed frames), requested beside the landmark's own operands below
+    for (int e = threadIdx.x; e < 3 * pa.n_pose; e += blockDim.x) {
+      const int f = e / 3;
+      s_dp[e] = f < a.n_fixed ? 0.0 : a.dpose[a.frame_pos[f] + e % 3];
+    }
+    __syncthreads();
+  }
   if (l >= a.n_lm) return;
   const int s0 = a.lm_seg_begin[l], s1 = a.lm_seg_begin[l + 1];
   const bool alt = a.sel && *a.sel;  // device-chosen linearisation slot
@@ -717,16 +787,32 @@ __global__ __launch_bounds__(256) void k_trial(BacksubArgs a, PoseTrialArgs pa, 
   const double th = a.rays[2 * l], ph = a.rays[2 * l + 1];
   const double D0 = a.D_ray[2 * l], D1 = a.D_ray[2 * l + 1];
   double t0 = 0, t1 = 0;
-  for (int s = s0 + lane; s < s1; s += WAVE) {
-    const int f = a.seg_frame[s];
-    if (f < a.n_fixed) continue;
-    const double* dp = a.dpose + a.frame_pos[f];
-    real w[6];
-    load_w6_slot(w, w_slot + ((int64_t)lmeta.z + f - lmeta.x) * 8);
+  if constexpr (DPL) {
+    if (s1 > s0) {
+      const int nsl = lmeta.y - lmeta.x + 1;  // dense slots of frames first .. last
+      for (int k = lane; k < nsl; k += WAVE) {
+        real w[6];
+        load_w6_slot(w, w_slot + ((int64_t)lmeta.z + k) * 8);
+        const double* dp = s_dp + 3 * (lmeta.x + k);
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      t0 += (double)w[2 * q] * dp[q];
-      t1 += (double)w[2 * q + 1] * dp[q];
+        for (int q = 0; q < 3; ++q) {
+          t0 += (double)w[2 * q] * dp[q];
+          t1 += (double)w[2 * q + 1] * dp[q];
+        }
+      }
+    }
+  } else {
+    for (int s = s0 + lane; s < s1; s += WAVE) {
+      const int f = a.seg_frame[s];
+      if (f < a.n_fixed) continue;
+      const double* dp = a.dpose + a.frame_pos[f];
+      real w[6];
+      load_w6_slot(w, w_slot + ((int64_t)lmeta.z + f - lmeta.x) * 8);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        t0 += (double)w[2 * q] * dp[q];
+        t1 += (double)w[2 * q + 1] * dp[q];
+      }
     }
   }
   t0 = wave_total(t0);
@@ -766,9 +852,17 @@ void launch_trial(const BacksubArgs& a, const double* ptz, const double* g_pose,
                   double* out4, int n_pose, void* ft64, void* rt64, void* ft, void* rt, hipStream_t st,
                   const uint8_t* fmask, const int* info) {
   PoseTrialArgs pa{ptz, g_pose, D_pose, ptz_trial, out4, n_pose, fmask, info};
-  hipLaunchKernelGGL(k_trial<real>, dim3((unsigned)((a.n_lm + 3) / 4 + 1)), dim3(256), 0, st, a, pa,
-                     (FrameTab<double>*)ft64, (RayTab<double>*)rt64, (FrameTab<real>*)ft, (RayTab<real>*)rt);
+  static const bool dpl_off = getenv("PTZBA_TRIAL_DPL") && atoi(getenv("PTZBA_TRIAL_DPL")) == 0;  // A/B knob
+  if (n_pose <= K1_FT_LDS && !dpl_off && !fmask)  // (part-owned solves: the other part's dpose rows are not solved here)
+    hipLaunchKernelGGL((k_trial<real, true>), dim3((unsigned)((a.n_lm + 3) / 4 + 1)), dim3(256), 0, st, a, pa,
+                       (FrameTab<double>*)ft64, (RayTab<double>*)rt64, (FrameTab<real>*)ft, (RayTab<real>*)rt);
+  else
+    hipLaunchKernelGGL((k_trial<real, false>), dim3((unsigned)((a.n_lm + 3) / 4 + 1)), dim3(256), 0, st, a, pa,
+                       (FrameTab<double>*)ft64, (RayTab<double>*)rt64, (FrameTab<real>*)ft, (RayTab<real>*)rt);
 }
+
+__device__ void lm_decide_body(LMDev* st, const double* scal, const double* __restrict__ loc,
+                               const int* __restrict__ info, LMDev* __restrict__ rec, int seq, int info_in_loc);
 
 // deterministic strided reduction: out[k] = sum_i src[i*stride + k] (fixed order), k < nk;
 // mode bit k set -> max(|.|) instead of sum for column k.  RED_BLOCKS workgroups reduce contiguous row
@@ -785,7 +879,7 @@ __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ 
                                                      double* __restrict__ partial, unsigned* __restrict__ counter,
                                                      const double* __restrict__ src2, int stride2, int nk2,
                                                      double* __restrict__ out2, const double* __restrict__ src1,
-                                                     const int* __restrict__ sel, int sel_xor) {
+                                                     const int* __restrict__ sel, int sel_xor, DecideArgs dec) {
   if (sel && ((*sel ^ sel_xor) & 1)) src = src1;
   __shared__ double red[8][256 / WAVE];
   __shared__ bool last;
@@ -858,19 +952,35 @@ __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ 
   __syncthreads();
 #endif
   if (!last) return;
+  // reader-side acquire at agent scope (invalidates this CU's vector cache; the L2 is not written back), so the
+  // partial loads below cannot be satisfied from lines older than the counter observation
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   // all partials in parallel (agent-scope loads: other workgroups wrote them), then a fixed-order sum
   __shared__ double fin[RED_BLOCKS][8];
   for (int e = threadIdx.x; e < (int)gridDim.x * 8; e += blockDim.x)
     fin[e >> 3][e & 7] = __hip_atomic_load(partial + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
+  __shared__ double tot[8];
   if (threadIdx.x < nk) {
     const int k = threadIdx.x;
     double s = 0;
     for (int b = 0; b < (int)gridDim.x; ++b) s = (maxmask & (1 << k)) ? fmax(s, fin[b][k]) : s + fin[b][k];
     if (k < nk - nk2) out[k] = s;
     else out2[k - (nk - nk2)] = s;
+    tot[k] = s;
   }
   if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (dec.st) {
+    // fused decision (trial-cost reduction of a single-GPU device-driven LM): out = scal + 1 (trial cost), out2 =
+    // scal + 2 (pred, |dx|^2, |x|^2 landmark partials); the sums come from LDS, not from the stores above
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double sc[5];
+      sc[0] = 0.0;  // (the current cost lives in LMDev)
+      sc[1] = tot[0]; sc[2] = tot[1]; sc[3] = tot[2]; sc[4] = tot[3];
+      lm_decide_body(dec.st, sc, dec.loc, dec.info, dec.rec, dec.seq, 0);
+    }
+  }
 }
 
 __global__ void k_pack_scalars(const double* __restrict__ scal, const double* __restrict__ loc,
@@ -887,10 +997,11 @@ void launch_pack_scalars(const double* scal, const double* loc, const int* info,
 
 void launch_reduce_cols(const double* src, int64_t n, int stride, int nk, int maxmask, double* out, double* scratch,
                         hipStream_t st, const double* src2, int stride2, int nk2, double* out2, const double* src1,
-                        const int* sel, int sel_xor) {
+                        const int* sel, int sel_xor, const DecideArgs* decide) {
   unsigned* counter = reinterpret_cast<unsigned*>(scratch + RED_BLOCKS * 8);
+  const DecideArgs dec = decide ? *decide : DecideArgs{nullptr, nullptr, nullptr, nullptr, 0};
   hipLaunchKernelGGL(k_reduce_cols, dim3(RED_BLOCKS), dim3(256), 0, st, src, n, stride, nk, maxmask, out, scratch,
-                     counter, src2, stride2, src2 ? nk2 : 0, out2, src1, sel, sel_xor);
+                     counter, src2, stride2, src2 ? nk2 : 0, out2, src1, sel, sel_xor, dec);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -945,8 +1056,9 @@ __global__ void k_lm_init(LMDev* st, const double* __restrict__ scal, LMParams p
   st->relin = 0;
 }
 
-__global__ void k_lm_decide(LMDev* st, const double* __restrict__ scal, const double* __restrict__ loc,
-                            const int* __restrict__ info, LMDev* __restrict__ rec, int seq, int info_in_loc) {
+// scipy trf decision rules (one thread): scal = {cost, trial cost, pred, |dx|^2, |x|^2} partial sums
+__device__ void lm_decide_body(LMDev* st, const double* scal, const double* __restrict__ loc,
+                               const int* __restrict__ info, LMDev* __restrict__ rec, int seq, int info_in_loc) {
   LMDev s = *st;
   s.accepted = 0;
   s.relin = 0;
@@ -1010,6 +1122,10 @@ __global__ void k_lm_decide(LMDev* st, const double* __restrict__ scal, const do
   // the host polls rec->seq (pinned memory): the record's fields must be visible before it
   __threadfence_system();
   __hip_atomic_store(&rec->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ void k_lm_decide(LMDev* st, const double* __restrict__ scal, const double* __restrict__ loc,
+                            const int* __restrict__ info, LMDev* __restrict__ rec, int seq, int info_in_loc) {
+  lm_decide_body(st, scal, loc, info, rec, seq, info_in_loc);
 }
 
 // accepted trial -> current state (the trial's linearisation is already in place)

@@ -190,9 +190,24 @@ __device__ __host__ inline double reproj_err2(const double (&H)[9], double x, do
 
 constexpr int RH = 64;  // hypotheses per workgroup
 
+// batched form (ptz_homography_ransac_batch): set blockIdx.y of n_sets, its points at [off[y], off[y + 1]), its own
+// normalisation and best key; the single-set call passes off = nullptr (the kernel arguments are the set)
+struct RansacSets {
+  const int64_t* off;  // [n_sets + 1] or nullptr
+  const Norm* norm;    // [n_sets]
+};
 __global__ __launch_bounds__(256) void k_ransac_score(int n, const double* __restrict__ p1, const double* __restrict__ p2,
                                                       Norm N, double thr2, int n_hyp, uint64_t seed,
-                                                      unsigned long long* __restrict__ best) {
+                                                      unsigned long long* __restrict__ best, RansacSets rs) {
+  if (rs.off) {  // batched: set blockIdx.y
+    const int y = blockIdx.y;
+    const int64_t a = rs.off[y];
+    n = (int)(rs.off[y + 1] - a);
+    p1 += 2 * a;
+    p2 += 2 * a;
+    N = rs.norm[y];
+    best += y;
+  }
   __shared__ double sH[RH][9];
   __shared__ int sOk[RH];
   __shared__ int sCnt[4][RH];
@@ -249,7 +264,19 @@ __global__ __launch_bounds__(256) void k_ransac_refine(int n, const double* __re
                                                        Norm N, double thr2, uint64_t seed,
                                                        const unsigned long long* __restrict__ best,
                                                        uint8_t* __restrict__ mask, double* __restrict__ Hout,
-                                                       int* __restrict__ nin) {
+                                                       int* __restrict__ nin, RansacSets rs) {
+  if (rs.off) {  // batched: set blockIdx.x
+    const int y = blockIdx.x;
+    const int64_t a = rs.off[y];
+    n = (int)(rs.off[y + 1] - a);
+    p1 += 2 * a;
+    p2 += 2 * a;
+    N = rs.norm[y];
+    best += y;
+    mask += a;
+    Hout += 9 * y;
+    nin += y;
+  }
   __shared__ double sH[9];
   __shared__ double red[256][45];  // 8x9 augmented normal equations (upper part of the 9x9 Gram matrix)
   __shared__ int sOk;
@@ -379,28 +406,31 @@ int ptz_match_knn2(int device, int64_t n1, int64_t n2, int32_t dim, const float*
   return 0;
 }
 
+// Hartley normalisation of each point set (centroid, mean distance sqrt(2)); host, O(n)
+static Norm hartley(int64_t n, const double* pts1, const double* pts2) {
+  Norm N{};
+  double sx1 = 0, sy1 = 0, sx2 = 0, sy2 = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    sx1 += pts1[2 * i]; sy1 += pts1[2 * i + 1]; sx2 += pts2[2 * i]; sy2 += pts2[2 * i + 1];
+  }
+  N.c1x = sx1 / n; N.c1y = sy1 / n; N.c2x = sx2 / n; N.c2y = sy2 / n;
+  double d1 = 0, d2 = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    d1 += std::sqrt((pts1[2 * i] - N.c1x) * (pts1[2 * i] - N.c1x) + (pts1[2 * i + 1] - N.c1y) * (pts1[2 * i + 1] - N.c1y));
+    d2 += std::sqrt((pts2[2 * i] - N.c2x) * (pts2[2 * i] - N.c2x) + (pts2[2 * i + 1] - N.c2y) * (pts2[2 * i + 1] - N.c2y));
+  }
+  N.s1 = d1 > 0 ? std::sqrt(2.0) * n / d1 : 1.0;
+  N.s2 = d2 > 0 ? std::sqrt(2.0) * n / d2 : 1.0;
+  return N;
+}
+
 int ptz_homography_ransac(int device, int64_t n, const double* pts1, const double* pts2, double threshold,
                           int32_t n_hyp, uint64_t seed, uint8_t* mask_out, double* H_out, int32_t* n_inliers_out) {
   if (n < 4) return fail("homography RANSAC needs at least 4 correspondences (got %lld)", (long long)n);
   if (!pts1 || !pts2 || !mask_out || !H_out || !n_inliers_out) return fail("null argument");
   if (!(threshold > 0) || n_hyp < 1) return fail("bad threshold / hypothesis count");
   if (n >= ((int64_t)1 << 31)) return fail("too many correspondences");
-  // Hartley normalisation of each point set (centroid, mean distance sqrt(2)); host, O(n)
-  Norm N{};
-  {
-    double sx1 = 0, sy1 = 0, sx2 = 0, sy2 = 0;
-    for (int64_t i = 0; i < n; ++i) {
-      sx1 += pts1[2 * i]; sy1 += pts1[2 * i + 1]; sx2 += pts2[2 * i]; sy2 += pts2[2 * i + 1];
-    }
-    N.c1x = sx1 / n; N.c1y = sy1 / n; N.c2x = sx2 / n; N.c2y = sy2 / n;
-    double d1 = 0, d2 = 0;
-    for (int64_t i = 0; i < n; ++i) {
-      d1 += std::sqrt((pts1[2 * i] - N.c1x) * (pts1[2 * i] - N.c1x) + (pts1[2 * i + 1] - N.c1y) * (pts1[2 * i + 1] - N.c1y));
-      d2 += std::sqrt((pts2[2 * i] - N.c2x) * (pts2[2 * i] - N.c2x) + (pts2[2 * i + 1] - N.c2y) * (pts2[2 * i + 1] - N.c2y));
-    }
-    N.s1 = d1 > 0 ? std::sqrt(2.0) * n / d1 : 1.0;
-    N.s2 = d2 > 0 ? std::sqrt(2.0) * n / d2 : 1.0;
-  }
+  const Norm N = hartley(n, pts1, pts2);
   if (select_device(device)) return -1;
   struct RansacWork {
     DBuf p1, p2, best, mask, H, nin;
@@ -416,13 +446,65 @@ int ptz_homography_ransac(int device, int64_t n, const double* pts1, const doubl
   HIPCHK(hipMemset(best.p, 0, 8));
   const double thr2 = threshold * threshold;
   hipLaunchKernelGGL(k_ransac_score, dim3((unsigned)((n_hyp + RH - 1) / RH)), dim3(256), 0, nullptr, (int)n,
-                     p1.as<double>(), p2.as<double>(), N, thr2, n_hyp, seed, best.as<unsigned long long>());
+                     p1.as<double>(), p2.as<double>(), N, thr2, n_hyp, seed, best.as<unsigned long long>(),
+                     RansacSets{nullptr, nullptr});
   hipLaunchKernelGGL(k_ransac_refine, dim3(1), dim3(256), 0, nullptr, (int)n, p1.as<double>(), p2.as<double>(), N, thr2,
-                     seed, best.as<unsigned long long>(), mask.as<uint8_t>(), H.as<double>(), nin.as<int>());
+                     seed, best.as<unsigned long long>(), mask.as<uint8_t>(), H.as<double>(), nin.as<int>(),
+                     RansacSets{nullptr, nullptr});
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(mask_out, mask.p, (size_t)n, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(H_out, H.p, 72, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(n_inliers_out, nin.p, 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+// n_sets independent RANSACs in two launches (a keyframe's pairwise matches): set s has the correspondences
+// [off[s], off[s + 1]) of pts1 / pts2; per set exactly the result of ptz_homography_ransac with the same seed (the
+// hypotheses are keyed by (seed, hypothesis, draw), the set's normalisation and best key are its own)
+int ptz_homography_ransac_batch(int device, int32_t n_sets, const int64_t* off, const double* pts1, const double* pts2,
+                                double threshold, int32_t n_hyp, uint64_t seed, uint8_t* mask_out, double* H_out,
+                                int32_t* n_inliers_out) {
+  if (n_sets < 0 || (n_sets > 0 && (!off || !pts1 || !pts2 || !mask_out || !H_out || !n_inliers_out)))
+    return fail("null argument");
+  if (n_sets == 0) return 0;
+  if (!(threshold > 0) || n_hyp < 1) return fail("bad threshold / hypothesis count");
+  if (n_sets > 65535) return fail("too many sets (%d)", n_sets);
+  if (off[0] != 0) return fail("off[0] must be 0");
+  std::vector<Norm> norms(n_sets);
+  for (int s = 0; s < n_sets; ++s) {
+    const int64_t n = off[s + 1] - off[s];
+    if (n < 4) return fail("set %d: homography RANSAC needs at least 4 correspondences (got %lld)", s, (long long)n);
+    if (n >= ((int64_t)1 << 31)) return fail("set %d: too many correspondences", s);
+    norms[s] = hartley(n, pts1 + 2 * off[s], pts2 + 2 * off[s]);
+  }
+  const int64_t nt = off[n_sets];
+  if (select_device(device)) return -1;
+  struct RansacBatchWork {
+    DBuf p1, p2, best, mask, H, nin, off, norm;
+  };
+  auto guard = device_work_lock(device);
+  RansacBatchWork& Wk = work_for<RansacBatchWork>(device);
+  if (Wk.p1.reserve((size_t)nt * 16) || Wk.p2.reserve((size_t)nt * 16) || Wk.best.reserve(8 * (size_t)n_sets) ||
+      Wk.mask.reserve((size_t)nt) || Wk.H.reserve(72 * (size_t)n_sets) || Wk.nin.reserve(4 * (size_t)n_sets) ||
+      Wk.off.reserve(8 * (size_t)(n_sets + 1)) || Wk.norm.reserve(sizeof(Norm) * (size_t)n_sets))
+    return -1;
+  HIPCHK(hipMemcpy(Wk.p1.p, pts1, (size_t)nt * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(Wk.p2.p, pts2, (size_t)nt * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(Wk.off.p, off, 8 * (size_t)(n_sets + 1), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(Wk.norm.p, norms.data(), sizeof(Norm) * (size_t)n_sets, hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(Wk.best.p, 0, 8 * (size_t)n_sets));
+  const double thr2 = threshold * threshold;
+  const RansacSets rs{Wk.off.as<int64_t>(), Wk.norm.as<Norm>()};
+  hipLaunchKernelGGL(k_ransac_score, dim3((unsigned)((n_hyp + RH - 1) / RH), (unsigned)n_sets), dim3(256), 0, nullptr, 0,
+                     Wk.p1.as<double>(), Wk.p2.as<double>(), Norm{}, thr2, n_hyp, seed,
+                     Wk.best.as<unsigned long long>(), rs);
+  hipLaunchKernelGGL(k_ransac_refine, dim3((unsigned)n_sets), dim3(256), 0, nullptr, 0, Wk.p1.as<double>(),
+                     Wk.p2.as<double>(), Norm{}, thr2, seed, Wk.best.as<unsigned long long>(), Wk.mask.as<uint8_t>(),
+                     Wk.H.as<double>(), Wk.nin.as<int>(), rs);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(mask_out, Wk.mask.p, (size_t)nt, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(H_out, Wk.H.p, 72 * (size_t)n_sets, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(n_inliers_out, Wk.nin.p, 4 * (size_t)n_sets, hipMemcpyDeviceToHost));
   return 0;
 }
 

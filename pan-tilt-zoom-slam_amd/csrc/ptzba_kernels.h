@@ -6,6 +6,7 @@
 namespace ptzba {
 
 constexpr int K1_SEGW = 128;  // K1 segments per LDS window per wave
+constexpr int K1_FT_LDS = 640;  // K1 stages the frame tables in LDS up to this many frames (5 x 8 B per frame)
 struct LinArgs {
   const int4* lm_work;           // [2 n_work] {landmark, s0, s1, first record}, {lm_meta}, heaviest first
   int n_work;
@@ -33,6 +34,10 @@ struct LinArgs {
   double* lm_out1;
   const int* sel;
   int sel_xor;
+  // frames of the problem: with n_pose <= K1_FT_LDS every workgroup stages the fp64 frame tables in LDS before it
+  // reads its work descriptors (off the descriptor's latency), so a segment's frame table is an LDS read instead
+  // of a global load that depends on the segment's frame id
+  int n_pose;
 };
 
 // K2 tiles: block of SCHUR_F1 consecutive free frames x chunk of 64 partner frames; work items are
@@ -103,6 +108,10 @@ struct BacksubArgs {
   const void* w_slot1;    // sel != nullptr: read slot *sel (1 = these buffers), see LinArgs
   const double* lm_out1;
   const int* sel;
+  // device-driven LM: the state is double-buffered like the linearisation slots -- with sel != nullptr the
+  // current state is (rays, ptz) when ((*sel) ^ state_xor) is even, else (rays_trial, ptz_trial), and the trial
+  // goes to the other pair, so an accepted trial needs no copy (the decision's slot flip commits it)
+  int state_xor;
 };
 
 // device-driven Levenberg-Marquardt state (ptzba_lm_*): parameters, running state, last decision
@@ -122,6 +131,15 @@ void launch_lm_decide(LMDev* st, const double* scal, const double* loc, const in
                       hipStream_t s, int info_in_loc = 0);
 void launch_lm_commit(const LMDev* st, double* ptz, const double* ptz_trial, int n3, double* rays,
                       const double* rays_trial, int64_t n2, hipStream_t s);
+// the decision fused into the trial-cost reduction (single GPU: no exchange between them): the reduction's last
+// workgroup applies k_lm_decide's rules to the sums it has just formed
+struct DecideArgs {
+  LMDev* st;
+  const double* loc;
+  const int* info;
+  LMDev* rec;
+  int seq;
+};
 
 template <typename real>
 void launch_tables(const double* ptz, const double* rays, int n_pose, int n_lm, void* ft64, void* rt64, void* ft, void* rt,
@@ -138,7 +156,7 @@ void launch_pack_scalars(const double* scal, const double* loc, const int* info,
 void launch_reduce_cols(const double* src, int64_t n, int stride, int nk, int maxmask, double* out, double* scratch,
                         hipStream_t st, const double* src2 = nullptr, int stride2 = 0, int nk2 = 0,
                         double* out2 = nullptr, const double* src1 = nullptr, const int* sel = nullptr,
-                        int sel_xor = 0);
+                        int sel_xor = 0, const DecideArgs* decide = nullptr);
 // build prologue (zero pattern tiles + b|g|dU, landmark damping) in one launch
 void launch_build_prologue(double* S, int64_t ld, const int2* zt, int n_tiles, double* vec, int64_t n_vec,
                            const double* lm_out, const int32_t* lm_seg_begin, double* D_ray, double* lm_aux, int n_lm,

@@ -52,6 +52,9 @@ def run_stream(slam, scene, n_frames, camera0, keyframe_every=None, on_frame=Non
             slam.add_keyframe(img, slam.current_camera, i, enable_rf=False)
             slam.new_keyframe = False
             added = 1
+            lr = sys.modules.get("bundle_adjustment")
+            if lr is not None and getattr(lr, "LAST_RESULT", None):
+                rec.setdefault("kf_timing", []).append(dict(lr.LAST_RESULT.get("timing", {})))
         t2 = time.perf_counter()
         cam = slam.cameras[i] if i < len(slam.cameras) else slam.current_camera
         rec["ptz"].append([cam.pan, cam.tilt, cam.focal_length])
@@ -125,6 +128,10 @@ def main():
                                "f_px": float(np.sqrt(np.mean(err[:, 2] ** 2)))},
         "device": ptzba.lib().ptzba_version().decode(),
     }
+    kt = rec.get("kf_timing", [])[1:]
+    if kt:  # where a keyframe's BA call spends its time (bundle_adjustment.LAST_RESULT["timing"], mean ms)
+        keys = sorted({k for d in kt for k in d})
+        out["keyframe_ba_breakdown_ms"] = {k: 1e3 * float(np.mean([d.get(k, 0.0) for d in kt])) for k in keys}
     print(json.dumps(out))
 
 

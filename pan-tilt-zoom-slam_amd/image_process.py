@@ -40,15 +40,6 @@ class KeyPoint:
         self.octave = int(octave)
 
 
-def _hook(name):
-    def f(*a, **k):
-        raise NotImplementedError(
-            f"image_process.{name} is a front-end hook (OpenCV SIFT/ORB/LK in the reference, image_process.py); "
-            f"assign a correspondence source, e.g. synthetic.SyntheticFrontEnd(...).install()")
-    f.__name__ = name
-    return f
-
-
 # detect_compute_* / detect_sift / match_*_features / homography_ransac / optical_flow_matching: GPU
 # implementations below (SIFT, ORB / LATCH, kNN-2 + ratio test + RANSAC, Hamming + RANSAC, pyramidal LK); a
 # correspondence source may still assign its own
@@ -151,6 +142,50 @@ def match_sift_features(keypoint1, descriptor1, keypoint2, descriptor2, pts_arra
     if verbose:
         print('%d matches passed the homography ransac' % len(inlier_index))
     return pts1[inlier_index, :], index1[inlier_index].tolist(), pts2[inlier_index, :], index2[inlier_index].tolist()
+
+
+GPU_MATCH_SIFT = match_sift_features  # (correspondence.build_graph batches pairs only while this is the matcher)
+
+
+def match_sift_features_batch(pairs):
+    """match_sift_features for several descriptor pairs in three launches instead of five per pair: `pairs` is a
+    list of (keypoints1, descriptors1, keypoints2, descriptors2); pairs sharing the same train set (descriptors2
+    object) run as ONE kNN-2 over their concatenated queries (a new keyframe against every overlapping window
+    partner), the ratio test per pair, then ONE batched homography RANSAC (ptz_homography_ransac_batch, per pair
+    the same seed and result as homography_ransac).  Returns [(index1 list, index2 list)] with exactly
+    match_sift_features' (index1, index2) per pair (empty lists where it returns none)."""
+    import ptzba
+    out = [([], []) for _ in pairs]
+    groups = {}
+    for q, (_, d1, _, d2) in enumerate(pairs):
+        groups.setdefault(id(d2), []).append(q)
+    cand = []  # (pair, index1, index2, pts1, pts2)
+    for qs in groups.values():
+        d2 = np.asarray(pairs[qs[0]][3], dtype=np.float32)
+        d1s = [np.asarray(pairs[q][1], dtype=np.float32) for q in qs]
+        lens = [len(d) for d in d1s]
+        if sum(lens) == 0:
+            continue
+        idx, dist = ptzba.match_knn2(np.concatenate(d1s), d2)
+        o = 0
+        for q, n1 in zip(qs, lens):
+            di, ii = dist[o:o + n1], idx[o:o + n1]
+            o += n1
+            good = np.flatnonzero(di[:, 0] < 0.7 * di[:, 1]) if len(d2) >= 2 else np.zeros(0, np.int64)
+            if len(good) <= 8:
+                print('warning: match sift features failed, not enough matching')
+                continue
+            index1 = good.astype(np.int32)
+            index2 = ii[good, 0].astype(np.int32)
+            kp1, kp2 = pairs[q][0], pairs[q][2]
+            pts1 = np.array([kp1[i].pt for i in index1], np.float64).reshape(-1, 2)
+            pts2 = np.array([kp2[j].pt for j in index2], np.float64).reshape(-1, 2)
+            cand.append((q, index1, index2, pts1, pts2))
+    res = ptzba.homography_ransac_batch([(c[3], c[4]) for c in cand], 1.0)
+    for (q, index1, index2, _, _), (mask, _, _) in zip(cand, res):
+        inl = np.flatnonzero(mask)
+        out[q] = (index1[inl].tolist(), index2[inl].tolist())
+    return out
 
 
 def match_orb_features(keypiont1, descriptor1, keypoint2, descriptor2, verbose=False):

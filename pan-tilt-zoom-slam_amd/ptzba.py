@@ -105,6 +105,7 @@ def lib():
         "ptzba_solve_reduced": ([V], I),
         "ptzba_step": ([V, D], I),
         "ptzba_solve": ([V, V, V, POINTER(ptzba_lm_opts), POINTER(ptzba_report)], I),
+        "ptzba_solve_resident": ([V, I32, POINTER(ptzba_lm_opts), POINTER(ptzba_report)], I),
         "ptzba_lm_start": ([V], I),
         "ptzba_lm_init": ([V, POINTER(ptzba_lm_opts)], I),
         "ptzba_lm_build": ([V], I),
@@ -133,6 +134,7 @@ def lib():
         "ptzba_plan_export": ([I32, I32, V, I32, V, V, I64, V, I64, V], I),
         "ptz_match_knn2": ([I, I64, I64, I32, V, V, V, V], I),
         "ptz_homography_ransac": ([I, I64, V, V, D, I32, ctypes.c_uint64, V, V, POINTER(c_int32)], I),
+        "ptz_homography_ransac_batch": ([I, I32, V, V, V, D, I32, ctypes.c_uint64, V, V, V], I),
         "ptz_lk_track": ([I, I32, I32, V, V, I64, V, I32, I32, I32, D, D, V, V, V], I),
         "ptz_sift": ([I, I32, I32, V, I32, I32, V, V, V, POINTER(c_int32)], I),
         "ptz_orb": ([I, I32, I32, V, I32, I32, I32, V, V, POINTER(c_int32)], I),
@@ -178,10 +180,10 @@ def lib():
 EXPORTED_SYMBOLS = [
     "ptzba_new", "ptzba_delete", "ptzba_last_error", "ptzba_version", "ptzba_set_stream", "ptzba_use_own_stream", "ptzba_set_problem",
     "ptzba_problem_info", "ptzba_solver_info", "ptzba_residual", "ptzba_set_state", "ptzba_get_state", "ptzba_linearize",
-    "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_solve", "ptzba_read_scalars", "ptzba_accept",
+    "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_solve", "ptzba_solve_resident", "ptzba_read_scalars", "ptzba_accept",
     "ptzba_lm_start", "ptzba_lm_init", "ptzba_lm_build", "ptzba_lm_solve", "ptzba_lm_decide", "ptzba_lm_wait",
     "ptzba_exchange", "ptzba_exchange_packed", "ptzba_pack", "ptzba_unpack", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptzba_save_state", "ptzba_restore_state", "ptz_ray_to_image",
-    "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks", "ptzba_coupling_window", "ptz_match_knn2", "ptz_homography_ransac", "ptz_lk_track", "ptz_sift", "ptz_match_hamming",
+    "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks", "ptzba_coupling_window", "ptz_match_knn2", "ptz_homography_ransac", "ptz_homography_ransac_batch", "ptz_lk_track", "ptz_sift", "ptz_match_hamming",
     "ptz_py_shuffle_prefix", "ptz_set_order_pairs", "ptz_keyframe_features", "ptz_pack_records",
     "ptz_refine_poses", "ptzekf_new", "ptzekf_delete", "ptzekf_num_rays", "ptzekf_set_state", "ptzekf_get_state", "ptzekf_add_pose_cov",
     "ptzekf_remove_rays", "ptzekf_add_rays", "ptzekf_project_visible", "ptzekf_update",
@@ -303,6 +305,29 @@ def homography_ransac(points1, points2, threshold, n_hyp=2000, seed=0, device=No
                                        float(threshold), int(n_hyp), int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(mask), _ptr(H),
                                        ctypes.byref(nin)), "ptz_homography_ransac")
     return mask.astype(bool), H.reshape(3, 3), int(nin.value)
+
+
+def homography_ransac_batch(sets, threshold, n_hyp=2000, seed=0, device=None):
+    """Several independent homography RANSACs in one call (ptz_homography_ransac_batch): `sets` is a list of
+    (points1 [n, 2], points2 [n, 2]) with n >= 4.  Returns a list of (mask [n] bool, H [3, 3], inlier count), each
+    equal to homography_ransac(points1, points2, threshold, n_hyp, seed)."""
+    if not sets:
+        return []
+    p1 = [_f64(a, (-1, 2)) for a, _ in sets]
+    p2 = [_f64(b, (-1, 2)) for _, b in sets]
+    if any(len(a) != len(b) for a, b in zip(p1, p2)):
+        raise ValueError("point arrays differ in length")
+    off = np.concatenate([[0], np.cumsum([len(a) for a in p1])]).astype(np.int64)
+    P1 = np.ascontiguousarray(np.concatenate(p1))
+    P2 = np.ascontiguousarray(np.concatenate(p2))
+    mask = np.zeros(int(off[-1]), np.uint8)
+    H = np.zeros((len(sets), 9))
+    nin = np.zeros(len(sets), np.int32)
+    _check(lib().ptz_homography_ransac_batch(default_device() if device is None else device, len(sets), _ptr(off),
+                                             _ptr(P1), _ptr(P2), float(threshold), int(n_hyp),
+                                             int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(mask), _ptr(H), _ptr(nin)),
+           "ptz_homography_ransac_batch")
+    return [(mask[off[k]:off[k + 1]].astype(bool), H[k].reshape(3, 3), int(nin[k])) for k in range(len(sets))]
 
 
 def lk_track(img0, img1, points, win=31, levels=4, max_iter=30, eps=0.01, min_eig=1e-4, device=None):
@@ -828,6 +853,19 @@ class BAHandle:
                        lam=float("nan"), time=rep.time_s, history=[], trials=rep.trials)
         return ptz, rays, res
 
+    def solve_resident(self, restore=False, ftol=1e-4, xtol=1e-8, gtol=0.0, max_iter=100, lambda0=1e-4,
+                       min_lambda=1e-12, max_lambda=1e16, max_retries=30, gauss_newton=False):
+        """ptzba_solve_resident: the C-driven LM on the device-resident state (restore=True: from the
+        save_state snapshot).  The state stays on the device.  Returns LMResult."""
+        opts = ptzba_lm_opts(ftol, xtol, gtol, 0.0 if gauss_newton else lambda0, min_lambda, max_lambda, int(max_iter),
+                             int(max_retries), 1 if gauss_newton else 0)
+        rep = ptzba_report()
+        _check(lib().ptzba_solve_resident(self.h, 1 if restore else 0, ctypes.byref(opts), ctypes.byref(rep)),
+               "ptzba_solve_resident")
+        return LMResult(status=rep.status, message=STATUS_MSG.get(rep.status, "?"), cost=rep.cost,
+                        initial_cost=rep.initial_cost, njev=rep.iterations, nfev=rep.nfev, iterations=rep.iterations,
+                        lam=float("nan"), time=rep.time_s, history=[], trials=rep.trials)
+
     def lm_wait(self, k):
         r = ptzba_lm_record()
         _check(lib().ptzba_lm_wait(self.h, int(k), ctypes.byref(r)), "ptzba_lm_wait")
@@ -1131,6 +1169,9 @@ def release_solve_handles(device=None):
                 h.close()
 
 
+LAST_SOLVE_TIMING = {}  # host wall times of the last shared-handle solve() (set_problem, LM incl. state I/O)
+
+
 def solve(n_pose, n_landmark, frame, landmark, xy, u, v, init_ptz, init_rays, weight=None, precision=FP64,
           loss=LOSS_LINEAR, f_scale=1.0, device=0, keep_handle=True, **lm_kw):
     """Convenience one-shot solve.  Returns (ptz [N,3], rays [M,2], LMResult).  keep_handle=True (default): one
@@ -1154,11 +1195,15 @@ def solve(n_pose, n_landmark, frame, landmark, xy, u, v, init_ptz, init_rays, we
         if h is None or h.h is None:
             h = _solve_handles[device] = BAHandle(device)
         try:
+            t0 = time.perf_counter()
             h.set_problem(n_pose, n_landmark, frame, landmark, xy, u, v, weight=weight, precision=precision, loss=loss,
                           f_scale=f_scale)
+            t1 = time.perf_counter()
             h.set_state(init_ptz, init_rays)
             res = LMSolver(h, **lm_kw).run()
             ptz, rays = h.get_state()
+            LAST_SOLVE_TIMING.clear()
+            LAST_SOLVE_TIMING.update(set_problem_s=t1 - t0, lm_s=time.perf_counter() - t1)
             return ptz, rays, res
         except Exception:
             _solve_handles.pop(device, None)

@@ -63,6 +63,45 @@ def test_match_sift_features_gpu(gpu_available):
     np.testing.assert_array_equal(pts1, x1[i1])
 
 
+def test_homography_ransac_batch_equals_single_calls(gpu_available):
+    """ptz_homography_ransac_batch: per set bit for bit the single-call result (masks, counts, H), sets of
+    different sizes and outlier fractions in one call."""
+    import ptzba
+    sets = [frontend_data.homography_points(seed=s, n=n, outlier_frac=f)[:2]
+            for s, n, f in ((3, 600, 0.25), (4, 60, 0.4), (5, 2000, 0.1), (6, 4, 0.0), (7, 333, 0.5))]
+    got = ptzba.homography_ransac_batch(sets, 1.0, n_hyp=700, seed=11)
+    for (p1, p2), (mask, H, cnt) in zip(sets, got):
+        m1, H1, c1 = ptzba.homography_ransac(p1, p2, 1.0, n_hyp=700, seed=11)
+        assert np.array_equal(mask, m1) and cnt == c1
+        assert np.array_equal(H, H1)
+
+
+def test_match_sift_features_batch_equals_per_pair(gpu_available):
+    """image_process.match_sift_features_batch (one kNN-2 per train image, one RANSAC launch): every pair's
+    (index1, index2) equals match_sift_features on that pair -- several partners against one shared train set (a
+    new keyframe) plus an independent pair and a pair below the ratio-test floor."""
+    import image_process
+    x0, d0, xn, dn, _, _ = frontend_data.two_views(seed=7)
+
+    class KP:
+        def __init__(self, p):
+            self.pt = (float(p[0]), float(p[1]))
+    kn = [KP(p) for p in xn]
+    pairs = []
+    for s in (8, 9, 10):
+        x1, d1, _, _, _, _ = frontend_data.two_views(seed=s)
+        pairs.append(([KP(p) for p in x1], d1, kn, dn))  # shared train set dn
+    pairs.append(([KP(p) for p in x0], d0, kn, dn))
+    xa, da, xb, db, _, _ = frontend_data.two_views(seed=12)
+    pairs.append(([KP(p) for p in xa], da, [KP(p) for p in xb], db))
+    pairs.append(([KP(p) for p in xa[:5]], da[:5], kn, dn))  # too few ratio-test survivors
+    got = image_process.match_sift_features_batch(pairs)
+    for (k1, d1, k2, d2), (a, b) in zip(pairs, got):
+        _, i1, _, i2 = image_process.match_sift_features(k1, d1, k2, d2)
+        assert list(a) == list(i1) and list(b) == list(i2)
+    assert len(got[3][0]) > 300 and got[5] == ([], [])
+
+
 def test_homography_ransac_hook_signature(gpu_available):
     """homography_ransac(points1, points2, threshold, return_matrix) as image_process.py:418 calls it."""
     import image_process
