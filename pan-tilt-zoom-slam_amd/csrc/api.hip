@@ -21,6 +21,7 @@
 #include "ptzba_common.h"
 #include "ptzba_kernels.h"
 #include "host_util.h"
+#include "par_util.h"
 
 using namespace ptzba;
 
@@ -84,6 +85,11 @@ struct ptzba_ctx {
   DBuf bs_lo_off, bs_lo_tiles;  // left-looking back substitution lists (large systems)
   DBuf bsb_tasks, bsb_r;  // blocked back substitution (large systems): plan + r scratch [ld]
   std::vector<int> bsb_step_off;
+  // persistent blocked back substitution (one launch, per-column update counters): expected counts, per-column
+  // totals, the counters (zeroed at set_problem, advanced by one solve's totals per launch: epoch), error flag
+  DBuf bsp_expect, bsp_tot, bsp_cnt, bsp_err;
+  bool bs_pst = false;
+  uint32_t bsp_epoch = 0;
   bool bs_ll = false, bs_blk = false;
   bool chol_delayed = false;  // the plan delays trailing updates (make_plan, DT = 2)
   DBuf xtiles, xbuf;  // packed exchange: tile list, buffer
@@ -99,7 +105,8 @@ struct ptzba_ctx {
   int state_base = 0;
   // single-GPU device-driven LM: the trial-cost reduction waits for ptzba_lm_decide, which fuses the decision into it
   bool scal_deferred = false;
-  bool scal_exported = false;  // ptzba_exchange handed out the scalar buffer (a caller-run scalar exchange)
+  bool scal_exported = false;
+  int k2_fold = 0;  // SchurArgs::fold, read from PTZBA_K2_FOLD at set_problem (A/B knob)  // ptzba_exchange handed out the scalar buffer (a caller-run scalar exchange)
   // timing
   int timing = 0;  // bitmask of timed kernel groups (1 K1, 2 Schur, 4 Cholesky solve, 8 back-substitution)
   std::vector<hipEvent_t> ev[TM_N];
@@ -232,13 +239,15 @@ static int upload_records(ptzba_ctx* h, const std::vector<int64_t>& order, const
   // memset of set_problem goes on h->st)
   SyncOnExit sync_guard{h->st};
   std::vector<real> xy(2 * h->n_rec);
-  for (int64_t r = 0; r < h->n_rec; ++r) {
-    const int32_t s = rec_seg[r];
-    xy[2 * r] = (real)(obs_xy[2 * order[r]] - base[2 * s]);
-    xy[2 * r + 1] = (real)(obs_xy[2 * order[r] + 1] - base[2 * s + 1]);
-  }
   std::vector<real> ww(w ? h->n_rec : 0);
-  for (int64_t r = 0; r < (int64_t)ww.size(); ++r) ww[r] = (real)w[order[r]];
+  parallel_chunks(h->n_rec, host_threads(h->n_rec), [&](int64_t lo, int64_t hi, int) {
+    for (int64_t r = lo; r < hi; ++r) {
+      const int32_t s = rec_seg[r];
+      xy[2 * r] = (real)(obs_xy[2 * order[r]] - base[2 * s]);
+      xy[2 * r + 1] = (real)(obs_xy[2 * order[r] + 1] - base[2 * s + 1]);
+      if (w) ww[r] = (real)w[order[r]];
+    }
+  });
   // allocate everything before queuing any copy; padded by 4 records: K1's coarsened loads read whole groups
   if (h->rec_xy.alloc((xy.size() + 8) * sizeof(real))) return -1;
   if (w) {
@@ -453,6 +462,9 @@ struct CholPlan {
   // per step); empty when no valid schedule exists
   std::vector<int32_t> bsb_tasks;
   std::vector<int> bsb_step_off;
+  // persistent form (k_chol_backsolve_pst): per task the updates its block columns / target have received before
+  // its step, {E_c0, E_c1, E_c2, E_c3, E_t, 0, 0, 0}, and per column the updates one solve applies to it
+  std::vector<int32_t> bsb_expect, bsb_tot;
 };
 
 // Steps of the blocked right-looking back substitution (k_chol_backsolve_blk).  The chains' common prefix
@@ -522,12 +534,60 @@ static void make_bs_steps(const std::vector<std::vector<uint8_t>>& nz, int Tx, C
   }
   for (int kt = 0; kt < Tx; ++kt)
     if (in_any[kt] && !solved[kt]) return fail();
+  // expected update counts for the persistent form: replay the steps in order
+  const int nt = (int)(P.bsb_tasks.size() / 12);
+  P.bsb_expect.assign(8 * (size_t)nt, 0);
+  std::vector<int32_t> done(T, 0);
+  for (size_t st = 0; st + 1 < P.bsb_step_off.size(); ++st) {
+    for (int q = P.bsb_step_off[st]; q < P.bsb_step_off[st + 1]; ++q) {
+      const int32_t* tk = &P.bsb_tasks[12 * (size_t)q];
+      for (int k = 0; k < 4; ++k) P.bsb_expect[8 * (size_t)q + k] = tk[k] >= 0 ? done[tk[k]] : 0;
+      P.bsb_expect[8 * (size_t)q + 4] = tk[8] >= 0 ? done[tk[8]] : 0;
+    }
+    for (int q = P.bsb_step_off[st]; q < P.bsb_step_off[st + 1]; ++q) {
+      const int t = P.bsb_tasks[12 * (size_t)q + 8];
+      if (t >= 0) done[t]++;
+    }
+  }
+  P.bsb_tot = done;
+}
+
+// XCD-aware order of one level's tasks (PTZBA_CHOL_XCD=1, A/B knob): workgroups are dealt round-robin over the
+// 8 XCDs (block b on XCD b % 8, MI355X_MICROARCH.md), so a task placed at a slot b = r (mod 8) for its row tile r
+// runs on the XCD whose L2 the previous level's tasks of row r wrote through.  Slots no task maps to get a no-op
+// (type 2 with i = -1).  Panel tasks keep coming first within each XCD's sequence.
+static void xcd_interleave(std::vector<int32_t>& tasks, int first_task) {
+  const int n = (int)tasks.size() / 4 - first_task;
+  if (n <= 1) return;
+  std::vector<std::vector<int>> q(8);
+  for (int t = 0; t < n; ++t) {
+    const int32_t* r = &tasks[4 * (first_task + t)];
+    q[(unsigned)r[1] % 8u].push_back(t);  // row tile i (type 3: the block's first row; type 2: the column)
+  }
+  size_t m = 0;
+  for (auto& b : q) m = std::max(m, b.size());
+  std::vector<int32_t> out;
+  out.reserve(4 * 8 * m);
+  for (size_t k = 0; k < m; ++k)
+    for (int x = 0; x < 8; ++x) {
+      if (k < q[x].size()) {
+        const int32_t* r = &tasks[4 * (first_task + q[x][k])];
+        out.insert(out.end(), r, r + 4);
+      } else {
+        out.insert(out.end(), {2, -1, -1, 0});
+      }
+    }
+  // trailing no-ops of the last round are dropped
+  while (out.size() >= 4 && out[out.size() - 4] == 2 && out[out.size() - 3] == -1) out.resize(out.size() - 4);
+  tasks.resize(4 * (size_t)first_task);
+  tasks.insert(tasks.end(), out.begin(), out.end());
 }
 
 // Tile structure (coupled frame pairs + the dense augmented row + symbolic fill), elimination levels
 // (at most two tile columns per level), tasks per level and back-substitution chains.
 static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<int32_t>& win, int64_t ld, CholPlan& P,
                       int force_dt = 0) {
+  const bool xcd_order = getenv_is("PTZBA_CHOL_XCD", "1");
   const int T = (int)(ld / CHOL_NB);
   std::vector<std::vector<uint8_t>> nz(T, std::vector<uint8_t>(T, 0));
   auto mark = [&](int r, int c) {
@@ -689,6 +749,7 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
     if (tinv_split)
       for (int pp : prev)
         if (pp < n_inv) push(2, pp, pp, 0);
+    if (xcd_order) xcd_interleave(P.tasks, P.level_off[L]);  // PTZBA_CHOL_XCD=1 (read per plan)
   }
   for (int k = 0; k < n_inv && k < T; ++k)
     if (!tinv_split || level[k] == nL - 1) P.tinv_tail.push_back(k);
@@ -1053,12 +1114,26 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   if (o.frame_win_hi)
     for (int f = 0; f < n_pose; ++f)
       if (o.frame_win_hi[f] < f || o.frame_win_hi[f] >= n_pose) return fail("frame_win_hi[%d] = %d out of range", f, o.frame_win_hi[f]);
-  for (int64_t r = 0; r < n_obs; ++r) {
-    if (obs_frame[r] < 0 || obs_frame[r] >= n_pose) return fail("record %lld: frame %d out of range", (long long)r, obs_frame[r]);
-    if (obs_landmark[r] < 0 || obs_landmark[r] >= n_landmark)
-      return fail("record %lld: landmark %d out of range", (long long)r, obs_landmark[r]);
-    if (!std::isfinite(obs_xy[2 * r]) || !std::isfinite(obs_xy[2 * r + 1])) return fail("record %lld: non-finite observation", (long long)r);
-    if (obs_weight && !(obs_weight[r] >= 0)) return fail("record %lld: negative weight", (long long)r);
+  {
+    // record validation over host threads; the error reported is the first bad record's, as a sequential scan's
+    const int T = host_threads(n_obs);
+    std::vector<int64_t> first_bad(T, n_obs);
+    parallel_chunks(n_obs, T, [&](int64_t lo, int64_t hi, int t) {
+      for (int64_t r = lo; r < hi; ++r)
+        if (obs_frame[r] < 0 || obs_frame[r] >= n_pose || obs_landmark[r] < 0 || obs_landmark[r] >= n_landmark ||
+            !std::isfinite(obs_xy[2 * r]) || !std::isfinite(obs_xy[2 * r + 1]) || (obs_weight && !(obs_weight[r] >= 0))) {
+          first_bad[t] = r;
+          return;
+        }
+    });
+    const int64_t r = *std::min_element(first_bad.begin(), first_bad.end());
+    if (r < n_obs) {
+      if (obs_frame[r] < 0 || obs_frame[r] >= n_pose) return fail("record %lld: frame %d out of range", (long long)r, obs_frame[r]);
+      if (obs_landmark[r] < 0 || obs_landmark[r] >= n_landmark)
+        return fail("record %lld: landmark %d out of range", (long long)r, obs_landmark[r]);
+      if (!std::isfinite(obs_xy[2 * r]) || !std::isfinite(obs_xy[2 * r + 1])) return fail("record %lld: non-finite observation", (long long)r);
+      return fail("record %lld: negative weight", (long long)r);
+    }
   }
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipStreamSynchronize(h->st));
@@ -1075,6 +1150,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->u = u;
   h->v = v;
   h->weighted = obs_weight != nullptr;
+  h->k2_fold = getenv("PTZBA_K2_FOLD") ? atoi(getenv("PTZBA_K2_FOLD")) : 0;
 
   st_mark("validate");
   // ---- stable counting sorts: by frame, then by landmark -> (landmark, frame, original index)
@@ -1483,6 +1559,18 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->bs_blk = (want_blk || (h->bs_ll && bsk != "ll")) && bsk != "ll" && !plan.bsb_tasks.empty();
   h->bs_ll = (h->bs_ll || bsk == "ll") && !h->bs_blk;
   h->bsb_step_off = plan.bsb_step_off;
+  // persistent form: every step's tasks in one launch (all resident at <= 512 workgroups); PTZBA_BS_PERSIST=0 keeps
+  // one launch per step (A/B knob)
+  h->bs_pst = h->bs_blk && !getenv_is("PTZBA_BS_PERSIST", "0") && getenv_is("PTZBA_BS_PERSIST", "1") &&
+              plan.bsb_tasks.size() / 12 <= 512;  // (2 workgroups per CU resident: 190 VGPRs)
+  h->bsp_epoch = 0;
+  if (h->bs_pst) {
+    if (upload(h->bsp_expect, plan.bsb_expect, h->st) || upload(h->bsp_tot, plan.bsb_tot, h->st) ||
+        h->bsp_cnt.alloc(4 * plan.bsb_tot.size()) || h->bsp_err.alloc(4))
+      return -1;
+    HIPCHK(hipMemsetAsync(h->bsp_cnt.p, 0, h->bsp_cnt.bytes, h->st));
+    HIPCHK(hipMemsetAsync(h->bsp_err.p, 0, h->bsp_err.bytes, h->st));
+  }
   if (h->bs_blk) {
     if (upload(h->bsb_tasks, plan.bsb_tasks, h->st) ||
         h->bsb_r.alloc((size_t)h->ld * 8))
@@ -1764,7 +1852,8 @@ static int build_impl(ptzba_ctx* h, double lambda, const double* lam_dev, const 
   a.sel = sel;
   a.prep = fp;
   a.item_group = h->s2_item_group.as<int32_t>();
-  a.tile_cnt = h->s2_tile_cnt.as<unsigned>();  // used only by the folded-reduce A/B build (MF_FOLD_REDUCE)
+  a.tile_cnt = h->s2_tile_cnt.as<unsigned>();  // folded reduce (SchurArgs::fold)
+  a.fold = h->k2_fold;
   tm_begin(h, TM_SCHUR);
   a.pair = h->s2_pair;
   if (h->precision == PTZBA_FP32)
@@ -1834,7 +1923,12 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
                     h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>(), 0,
                     h->chol_delayed);
   }
-  if (h->bs_blk)
+  if (h->bs_pst)
+    launch_chol_backsolve_pst(h->S(), h->ld, h->n_aug, h->bsb_tasks.as<int4>(), h->bsp_expect.as<int4>(),
+                              h->bsb_step_off.back(), h->Ldiag.as<double>(), h->Minv.as<double>(), h->bsb_r.as<double>(),
+                              h->dpose.as<double>(), h->bsp_cnt.as<unsigned>(), h->bsp_tot.as<int>(), h->bsp_epoch++,
+                              h->bsp_err.as<int>(), h->st, h->tinv_tail.as<int>(), h->n_tinv_tail);
+  else if (h->bs_blk)
     launch_chol_backsolve_blk(h->S(), h->ld, h->n_aug, h->bsb_tasks.as<int4>(), h->bsb_step_off.data(), (int)h->bsb_step_off.size() - 1, h->Ldiag.as<double>(),
                               h->Minv.as<double>(), h->bsb_r.as<double>(), h->dpose.as<double>(), h->st,
                               h->tinv_tail.as<int>(), h->n_tinv_tail);
@@ -2013,8 +2107,10 @@ int ptzba_lm_wait(ptzba_handle h, int trial, ptzba_lm_record* out) {
     // so that kernels already queued (old pair, old base) and later ones (new pair, new base) select the same buffer
     std::swap(h->ptz.p, h->ptz_trial.p);
     std::swap(h->ptz.bytes, h->ptz_trial.bytes);
+    std::swap(h->ptz.cap, h->ptz_trial.cap);
     std::swap(h->rays.p, h->rays_trial.p);
     std::swap(h->rays.bytes, h->rays_trial.bytes);
+    std::swap(h->rays.cap, h->rays_trial.cap);
     h->state_base ^= 1;
   }
   return 0;
@@ -2126,8 +2222,10 @@ int ptzba_accept(ptzba_handle h, int accept) {
     h->cur = 1 - h->cur;
     std::swap(h->ptz.p, h->ptz_trial.p);
     std::swap(h->ptz.bytes, h->ptz_trial.bytes);
+    std::swap(h->ptz.cap, h->ptz_trial.cap);
     std::swap(h->rays.p, h->rays_trial.p);
     std::swap(h->rays.bytes, h->rays_trial.bytes);
+    std::swap(h->rays.cap, h->rays_trial.cap);
   }
   return 0;
 }

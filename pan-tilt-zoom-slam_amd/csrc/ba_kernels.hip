@@ -1000,7 +1000,10 @@ void launch_reduce_cols(const double* src, int64_t n, int stride, int nk, int ma
                         const int* sel, int sel_xor, const DecideArgs* decide) {
   unsigned* counter = reinterpret_cast<unsigned*>(scratch + RED_BLOCKS * 8);
   const DecideArgs dec = decide ? *decide : DecideArgs{nullptr, nullptr, nullptr, nullptr, 0};
-  hipLaunchKernelGGL(k_reduce_cols, dim3(RED_BLOCKS), dim3(256), 0, st, src, n, stride, nk, maxmask, out, scratch,
+  // workgroups: RED_BLOCKS, or PTZBA_RED_BLOCKS (A/B knob; fewer blocks = fewer counter arrivals, more rows each)
+  static const int nb_env = getenv("PTZBA_RED_BLOCKS") ? atoi(getenv("PTZBA_RED_BLOCKS")) : 0;
+  const int nb = nb_env > 0 ? std::min(nb_env, RED_BLOCKS) : RED_BLOCKS;
+  hipLaunchKernelGGL(k_reduce_cols, dim3(nb), dim3(256), 0, st, src, n, stride, nk, maxmask, out, scratch,
                      counter, src2, stride2, src2 ? nk2 : 0, out2, src1, sel, sel_xor, dec);
 }
 

@@ -864,6 +864,7 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   __shared__ double s_sig[NB];     // SG: signs of this column's pivots
   const int4 tk = tasks.get(blockIdx.x);
   if ((tk.x & 3) == 2) {  // inverse of a diagonal factor tile of the previous level (see tile_inv_wave)
+    if (tk.y < 0) return;  // no-op slot of an XCD-ordered level (api.hip xcd_interleave)
     __shared__ double s_rinv[NB];
     tile_inv_wave(Ldiag + (int64_t)tk.y * NB * NB, Minv + (int64_t)tk.y * NB * NB, sD, s_rinv);
     return;
@@ -1646,8 +1647,142 @@ __global__ __launch_bounds__(64 * BSB_P) void k_chol_backsolve_blk(
   }
 }
 
+// Persistent form of the blocked back substitution: every step's tasks in ONE launch (blockIdx order = step order,
+// all resident: <= 512 workgroups), the launch boundaries between steps replaced by per-column update counters.
+// A task first requests every immutable operand it needs (M_ck, the intra-block L tiles, L_ck,t: written by the
+// factorisation, a previous launch), then waits -- per block column the wave that owns it, for the target wave 0 --
+// until the column's counter shows the updates of all earlier steps (counter >= epoch * tot[col] + expect), and only
+// then loads r with sc1 loads.  The target's r_t is stored sc1 by wave 0 (the only wave that stores it), drained
+// (vmcnt(0)), and lane 0 of that wave adds 1 to the target's counter (MI355X_MICROARCH.md, inter-workgroup hand-off
+// table, first row).  The arithmetic and the summation order are k_chol_backsolve_blk's: bitwise the same x.
+constexpr int BSP_SPIN = 1 << 22;  // polls before a wait gives up (err = 1): ~seconds, never a hang
+__device__ __forceinline__ bool bsp_wait(const unsigned* c, unsigned target) {
+  for (int k = 0; k < BSP_SPIN; ++k) {
+    if ((int)(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) >= 0) return true;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return false;
+}
+__global__ __launch_bounds__(64 * BSB_P) void k_chol_backsolve_pst(
+    const double* __restrict__ L, int64_t ld, int n, const int4* __restrict__ tasks, const int4* __restrict__ expect,
+    const double* __restrict__ Ldiag, const double* __restrict__ Minv, double* __restrict__ r, double* __restrict__ xout,
+    unsigned* __restrict__ cnt, const int* __restrict__ tot, uint32_t epoch, int* __restrict__ err) {
+  __shared__ double xs[BSB_P][NB];
+  __shared__ double rs[BSB_P][NB];
+  __shared__ double ps[BSB_P][NB];
+  __shared__ int s_cnt;
+  const int lane = threadIdx.x & 63, k = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
+  if (threadIdx.x == 0) s_cnt = 0;
+  const int4 bc = tasks[3 * blockIdx.x], bm = tasks[3 * blockIdx.x + 1], tk = tasks[3 * blockIdx.x + 2];
+  const int4 ex = expect[2 * blockIdx.x], ex2 = expect[2 * blockIdx.x + 1];
+  const int p = bm.x, imask = bm.y, ftouch = bm.z, t = tk.x, tmask = tk.y & 0xff;
+  const bool writer = (tk.y & 0x100) != 0, tfirst = (tk.y & 0x200) != 0;
+  const int64_t tnNB = (int64_t)(n / NB) * NB, rn = n - tnNB;
+  auto yval = [&](int64_t i) -> double {
+    return i < tnNB ? L[(int64_t)n * ld + i] : (i < n ? Ldiag[(tnNB + rn) * NB + (i - tnNB)] : 0.0);
+  };
+  const int ck = k == 0 ? bc.x : (k == 1 ? bc.y : (k == 2 ? bc.z : bc.w));
+  const int eck = k == 0 ? ex.x : (k == 1 ? ex.y : (k == 2 ? ex.z : ex.w));
+  const bool act = k < p;
+  const int64_t cc = (int64_t)ck * NB;
+  double m[NB / 2], lj[BSB_P - 1][NB / 2], lt[NB / 2], rk = 0.0, rt = 0.0;
+  bool ok = true;
+  if (act) {  // the immutable operands first: their latency overlaps the waits below
+    const double* mp = Minv + cc * NB + (int64_t)(h * (NB / 2)) * NB + c;
+#pragma unroll
+    for (int i = 0; i < NB / 2; ++i) m[i] = mp[i * NB];
+#pragma unroll
+    for (int j = 0; j < BSB_P - 1; ++j) {
+      const int cj = j == 0 ? bc.x : (j == 1 ? bc.y : bc.z);
+      if (j < k && ((imask >> (j * 4 + k)) & 1)) {
+        const double* lp = L + ((int64_t)cj * NB + h * (NB / 2)) * ld + cc + c;
+#pragma unroll
+        for (int i = 0; i < NB / 2; ++i) lj[j][i] = lp[(int64_t)i * ld];
+      }
+    }
+    if ((tmask >> k) & 1) {
+      const double* lp = L + (cc + h * (NB / 2)) * ld + (int64_t)t * NB + c;
+#pragma unroll
+      for (int i = 0; i < NB / 2; ++i) lt[i] = lp[(int64_t)i * ld];
+    }
+    if ((ftouch >> k) & 1) {
+      rk = yval(cc + c);
+    } else {
+      ok = bsp_wait(cnt + ck, epoch * (unsigned)tot[ck] + (unsigned)eck);
+      rk = __hip_atomic_load(r + cc + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (k == 0 && t >= 0) {
+      if (tfirst) {
+        rt = yval((int64_t)t * NB + c);
+      } else {
+        ok = bsp_wait(cnt + t, epoch * (unsigned)tot[t] + (unsigned)ex2.x) && ok;
+        rt = __hip_atomic_load(r + (int64_t)t * NB + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (!ok && lane == 0) atomicOr(err, 1);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): s_cnt's init
+  __builtin_amdgcn_s_barrier();
+  if (act) {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < BSB_P - 1; ++j) {
+      if (j < k) {
+        lds_wait_ge(&s_cnt, j + 1, 0);
+        if ((imask >> (j * 4 + k)) & 1) {
+          double a4[4] = {0, 0, 0, 0};
+#pragma unroll
+          for (int i = 0; i < NB / 2; ++i) a4[i & 3] = fma(lj[j][i], xs[j][h * (NB / 2) + i], a4[i & 3]);
+          s += (a4[0] + a4[1]) + (a4[2] + a4[3]);
+        }
+      }
+    }
+    s += __shfl_xor(s, 32, WAVE);
+    if (h == 0) rs[k][c] = rk - s;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    double x4[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < NB / 2; ++i) x4[i & 3] = fma(m[i], rs[k][h * (NB / 2) + i], x4[i & 3]);
+    double x = (x4[0] + x4[1]) + (x4[2] + x4[3]);
+    x += __shfl_xor(x, 32, WAVE);
+    if (h == 0) xs[k][c] = x;
+    lds_signal(&s_cnt, k + 1);
+    if (writer && h == 0 && cc + c < n) xout[cc + c] = x;
+    if ((tmask >> k) & 1) {
+      double a4[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int i = 0; i < NB / 2; ++i) a4[i & 3] = fma(lt[i], xs[k][h * (NB / 2) + i], a4[i & 3]);
+      double a = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+      a += __shfl_xor(a, 32, WAVE);
+      if (h == 0) ps[k][c] = a;
+    }
+  }
+  __syncthreads();
+  if (k == 0 && t >= 0) {
+    if (h == 0) {
+      double sum = 0.0;
+#pragma unroll
+      for (int j = 0; j < BSB_P; ++j)
+        if ((tmask >> j) & 1) sum += ps[j][c];
+      __hip_atomic_store(r + (int64_t)t * NB + c, rt - sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's r_t stores have landed (write-through)
+    if (lane == 0) __hip_atomic_fetch_add(cnt + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 __global__ void k_tile_inv_list(const double* __restrict__ Ldiag, double* __restrict__ Minv,
                                 const int* __restrict__ tiles);
+void launch_chol_backsolve_pst(const double* L, int64_t ld, int n, const int4* tasks, const int4* expect, int n_tasks,
+                               const double* Ldiag, double* Minv, double* r, double* xout, unsigned* cnt,
+                               const int* tot, uint32_t epoch, int* err, hipStream_t st, const int* tinv_list,
+                               int n_tinv) {
+  if (n_tinv > 0) hipLaunchKernelGGL(k_tile_inv_list, dim3(n_tinv), dim3(64), 0, st, Ldiag, Minv, tinv_list);
+  if (n_tasks > 0)
+    hipLaunchKernelGGL(k_chol_backsolve_pst, dim3(n_tasks), dim3(64 * BSB_P), 0, st, L, ld, n, tasks, expect, Ldiag,
+                       Minv, r, xout, cnt, tot, epoch, err);
+}
 void launch_chol_backsolve_blk(const double* L, int64_t ld, int n, const int4* tasks, const int* step_off_host,
                                int n_steps, const double* Ldiag, double* Minv, double* r, double* xout,
                                hipStream_t st, const int* tinv_list, int n_tinv) {

@@ -31,7 +31,8 @@ inline int fail(const char* fmt, ...) {
 
 struct DBuf {
   void* p = nullptr;
-  size_t bytes = 0;
+  size_t bytes = 0;  // logical size (what the last alloc asked for)
+  size_t cap = 0;    // allocated size
   DBuf() = default;
   DBuf(const DBuf&) = delete;
   DBuf& operator=(const DBuf&) = delete;
@@ -39,18 +40,24 @@ struct DBuf {
   void release() {
     if (p) (void)hipFree(p);
     p = nullptr;
-    bytes = 0;
+    bytes = cap = 0;
   }
+  // n bytes of device memory, contents undefined; an allocation of at least n bytes is kept (a sliding-window map
+  // calls set_problem per keyframe: ~40 hipFree / hipMalloc pairs per call otherwise), a smaller one replaced
   int alloc(size_t n) {
-    release();
     if (n == 0) n = 16;
+    if (p && cap >= n && cap <= 4 * n + (1u << 20)) {  // (a much larger old buffer is returned instead)
+      bytes = n;
+      return 0;
+    }
+    release();
     hipError_t e = hipMalloc(&p, n);
     if (e != hipSuccess) return fail("hipMalloc(%zu) failed: %s", n, hipGetErrorString(e));
-    bytes = n;
+    bytes = cap = n;
     return 0;
   }
   // keep the allocation when it is already large enough (contents are not preserved otherwise)
-  int reserve(size_t n) { return n <= bytes && p ? 0 : alloc(n + n / 4); }
+  int reserve(size_t n) { return n <= cap && p ? 0 : alloc(n + n / 4); }
   template <typename T>
   T* as() const { return reinterpret_cast<T*>(p); }
 };

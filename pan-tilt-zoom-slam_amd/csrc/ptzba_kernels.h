@@ -6,7 +6,10 @@
 namespace ptzba {
 
 constexpr int K1_SEGW = 128;  // K1 segments per LDS window per wave
-constexpr int K1_FT_LDS = 640;  // K1 stages the frame tables in LDS up to this many frames (5 x 8 B per frame)
+#ifndef K1_FT_LDS_N
+#define K1_FT_LDS_N 640
+#endif
+constexpr int K1_FT_LDS = K1_FT_LDS_N;  // K1 stages the frame tables in LDS up to this many frames (5 x 8 B per frame)
 struct LinArgs {
   const int4* lm_work;           // [2 n_work] {landmark, s0, s1, first record}, {lm_meta}, heaviest first
   int n_work;
@@ -86,6 +89,11 @@ struct SchurArgs {
   unsigned* tile_cnt;             // [n_groups] finished splits per tile (zero between launches)
   FusedPrep prep;                 // single-GPU: the prepare's augmented row and damping (pad != nullptr)
   bool pair = false;              // items over chunk pairs (k_schur_mf2; item.y = cp | chunk mask << 16)
+  // matrix-core K2: the tile's last split reduces it inside k_schur_mf (no k_schur_reduce launch).  1: acq_rel
+  // counter (round 3: every split's release wrote back its XCD's L2, 258 us per build); 2: write-through (sc1)
+  // partial stores, each storing wave drained (vmcnt(0)), a relaxed counter add after the workgroup barrier, sc1
+  // loads in the last split (MI355X_MICROARCH.md inter-workgroup visibility, first row of the hand-off table)
+  int fold = 0;
 };
 
 struct BacksubArgs {
@@ -208,6 +216,14 @@ constexpr int BSB_P = 4;
 void launch_chol_backsolve_blk(const double* L, int64_t ld, int n, const int4* tasks, const int* step_off_host,
                                int n_steps, const double* Ldiag, double* Minv, double* r, double* xout,
                                hipStream_t st, const int* tinv_list, int n_tinv);
+// persistent form: every step's tasks in ONE launch (task order = step order), hand-offs through per-column update
+// counters (write-through r stores, relaxed counter adds; expect: per task the counts to wait for, tot: per column
+// the updates one solve applies, epoch: the number of earlier launches on these counters); err: set to 1 when a
+// wait gives up (a bounded spin: a plan error must not hang the GPU)
+void launch_chol_backsolve_pst(const double* L, int64_t ld, int n, const int4* tasks, const int4* expect, int n_tasks,
+                               const double* Ldiag, double* Minv, double* r, double* xout, unsigned* cnt,
+                               const int* tot, uint32_t epoch, int* err, hipStream_t st, const int* tinv_list,
+                               int n_tinv);
 // largest ld the back substitution keeps in LDS (left-looking form: x [ld] doubles + 4.4 KiB)
 constexpr int64_t CHOL_MAX_LD = 18944;
 // zero the factor pattern's tiles and the b | g_pose | dU vectors before a build (replaces a memset of

@@ -642,12 +642,16 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
     if (t < SF * 12) {
       double v = 0;
       for (int j0 = 0; j0 < 512 / SF; ++j0) v += red[j0 * SF * 12 + t];
-      a.part_diag[(int64_t)item * SF * 12 + t] = v;
+      if (a.fold == 2 && a.tile_cnt)
+        __hip_atomic_store(a.part_diag + (int64_t)item * SF * 12 + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        a.part_diag[(int64_t)item * SF * 12 + t] = v;
     }
   }
 #endif
-  // partial blocks of this split: part[item][f1 local][3q + r][f2], as k_schur writes them
+  // partial blocks of this split: part[item][f1 local][3q + r][f2], as k_schur writes them (fold == 2: write-through)
   float* out = (float*)a.part + (int64_t)item * (SF * 9 * WAVE);
+  const bool wt = a.fold == 2 && a.tile_cnt;
 #pragma unroll
   for (int x = 0; x < 3; ++x)
 #pragma unroll
@@ -656,32 +660,41 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
       for (int v = 0; v < 4; ++v) {
         const int row = 16 * (3 * rg + x) + (lane >> 4) * 4 + v, col = 16 * (3 * cg + y) + fr;
         const int q = row / SF, i = row % SF, r = col / WAVE, f2 = col % WAVE;
-        out[(i * 9 + 3 * q + r) * WAVE + f2] = (float)acc[x][y][v];
+        float* dst = out + (i * 9 + 3 * q + r) * WAVE + f2;
+        if (wt) __hip_atomic_store(dst, (float)acc[x][y][v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else *dst = (float)acc[x][y][v];
       }
-#if MF_FOLD_REDUCE
-  if (a.tile_cnt) {  // folded reduce: the tile's last split sums all splits in item order (schur_reduce_elem)
+  if (a.fold && a.tile_cnt) {  // folded reduce: the tile's last split sums all splits in item order (schur_reduce_elem)
     __shared__ int s_grp;
+    if (wt) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores have landed
     __syncthreads();
     if (t == 0) {
       const int gi = a.item_group[item];
       const int4 gg = a.groups[gi];
-      const unsigned done = __hip_atomic_fetch_add(a.tile_cnt + gi, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned done = wt ? __hip_atomic_fetch_add(a.tile_cnt + gi, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : __hip_atomic_fetch_add(a.tile_cnt + gi, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
       s_grp = (done == (unsigned)(gg.w - gg.z - 1)) ? gi : -1;
     }
     __syncthreads();
     const int gi = s_grp;
     if (gi >= 0) {
-      // every thread acquires (agent scope: the other splits' partials were released by their counter adds),
-      // then reads them with ordinary cached loads, several elements in flight per thread
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       const int4 gg = a.groups[gi];
+      if (wt) {
+        // every partial of the tile was stored sc1 and drained before its split's counter add: sc1 loads see them
 #pragma unroll 4
-      for (int e = t; e < SF * 9 * WAVE; e += 512) schur_reduce_elem<float, false>(a, gg, e);
-      if (gg.y == 0 && t < SF * 3) schur_reduce_vec<false>(a, gg, t);
+        for (int e = t; e < SF * 9 * WAVE; e += 512) schur_reduce_elem<float, true>(a, gg, e);
+        if (gg.y == 0 && t < SF * 3) schur_reduce_vec<true>(a, gg, t);
+      } else {
+        // every thread acquires (agent scope: the other splits' partials were released by their counter adds),
+        // then reads them with ordinary cached loads, several elements in flight per thread
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#pragma unroll 4
+        for (int e = t; e < SF * 9 * WAVE; e += 512) schur_reduce_elem<float, false>(a, gg, e);
+        if (gg.y == 0 && t < SF * 3) schur_reduce_vec<false>(a, gg, t);
+      }
       if (t == 0) __hip_atomic_store(a.tile_cnt + gi, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
     }
   }
-#endif
   SK_T(10);
 #ifdef SK_TIMING
   __syncthreads();
@@ -1041,7 +1054,7 @@ void launch_schur(const SchurArgs& a, int n_items, int n_groups, int n_fixed, hi
       hipLaunchKernelGGL(k_schur_mf2, dim3(n_items), dim3(512), 0, st, a);
     } else if (sizeof(real) == 4 && schur_use_mfma()) {
       hipLaunchKernelGGL(k_schur_mf, dim3(n_items), dim3(512), 0, st, a);
-      folded = MF_FOLD_REDUCE && a.item_group && a.tile_cnt;
+      folded = a.fold && a.item_group && a.tile_cnt;
     } else {
       hipLaunchKernelGGL(k_schur<real>, dim3(n_items), dim3(512), 0, st, a);
     }

@@ -465,3 +465,30 @@ def test_reduced_system_matrix_core_k2_matches_fp64(gpu_available, config, loss,
     assert err < 1e-4, err
     tail = np.abs(s32[ld * ld:] - s64[ld * ld:]).max() / max(np.abs(s64[ld * ld:]).max(), 1e-300)
     assert tail < 1e-5, tail
+
+
+@pytest.mark.parametrize("config", ["config2", "config3"])
+def test_folded_schur_reduce_bitwise_equals_separate_reduce(gpu_available, config, monkeypatch):
+    """Matrix-core K2 with the tile reduction folded into the tile's last split (PTZBA_K2_FOLD=2: write-through
+    partials, a relaxed per-tile counter, sc1 loads in the last split) writes the same reduced camera system, bit
+    for bit, as the separate k_schur_reduce launch (the same partials summed in the same item order)."""
+    import torch
+    import bench
+    import ptzba
+    import synthetic
+    p = synthetic.make_problem(config, seed=0)
+    out = []
+    for fold in ("0", "2", "2"):
+        monkeypatch.setenv("PTZBA_K2_FOLD", fold)
+        h = ptzba.BAHandle(0)
+        h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=ptzba.FP32,
+                      loss=ptzba.LOSS_HUBER)
+        h.set_state(p.init_ptz, p.init_rays)
+        h.linearize()
+        for lam in (1e-3, 1e-2):  # the per-tile counters re-arm: a second build reuses them
+            h.build_reduced(lam)
+        h.sync()
+        sp, n, _ = h.exchange()
+        out.append(torch.as_tensor(bench._DevArray(sp, n), device="cuda:0").cpu().numpy().copy())
+        h.close()
+    assert np.array_equal(out[0], out[1]) and np.array_equal(out[1], out[2])

@@ -161,3 +161,58 @@ def test_config4_lm_three_iterations(gpu_available, config4):
         assert nj == 1 and c1 < c0
     assert costs[1][0] == costs[0][1] and costs[2][0] == costs[1][1]
     assert costs[2][1] < 0.5 * costs[0][0]
+
+
+def _sampled_gradient(p, ptz, rays, frames, landmarks, loss="huber"):
+    """Oracle gradient of the pair-form cost (scipy's huber rho' weights, bundle_adjustment.py:25-106 residual,
+    SURVEY Appendix A Jacobian) restricted to a sample: the pose gradient of `frames` (from all their records) and
+    the ray gradient of `landmarks` (from all theirs) -- exact for those parameters, at a fraction of the cost."""
+    from oracle import ptz_oracle as orc
+    x_full = np.concatenate([np.asarray(ptz).reshape(-1), np.asarray(rays).reshape(-1)])
+    out = []
+    for kind, sel in (("frame", np.isin(p.frame, frames)), ("landmark", np.isin(p.landmark, landmarks))):
+        fr = p.frame[sel].astype(np.int64)
+        lm = p.landmark[sel].astype(np.int64)
+        r = orc.compute_residual_records(x_full, p.n_pose, p.u, p.v, fr, lm, p.xy[sel]).reshape(-1, 2)
+        if loss == "huber":
+            r = r * np.where(r * r <= 1.0, 1.0, 1.0 / np.sqrt(np.maximum(r * r, 1.0)))
+        J = orc.record_jacobian(p.u, p.v, np.asarray(ptz)[fr], np.asarray(rays)[lm])
+        g = np.einsum("rkc,rk->rc", J, r)
+        if kind == "frame":
+            G = np.zeros((p.n_pose, 3))
+            np.add.at(G, fr, g[:, :3])
+            out.append(np.abs(G[frames]).max(0))
+        else:
+            G = np.zeros((p.n_landmark, 2))
+            np.add.at(G, lm, g[:, 3:])
+            out.append(np.abs(G[landmarks]).max(0))
+    return np.concatenate(out)
+
+
+@pytest.mark.timeout(900)
+def test_config4_optimum_is_stationary_on_samples(gpu_available, config4):
+    """Config 4's optimum in the headline arithmetic (fp32 records, matrix-core K2, Huber), pinned to the oracle
+    the way config 3's is (test_gpu_config3.py): solved to a tight tolerance, the oracle's gradient of the reference
+    cost is <= 1e-5 of its value at x0 for every parameter kind -- evaluated exactly on a sample (the poses of 12
+    keyframes from every tilt row, from all their records, and the rays of 3000 landmarks, from all theirs),
+    since the oracle's full 410M-record gradient would take minutes."""
+    import ptzba
+    p = config4
+    rng = np.random.default_rng(11)
+    frames = np.sort(rng.choice(np.arange(1, p.n_pose), 12, replace=False))
+    landmarks = np.sort(rng.choice(p.n_landmark, 3000, replace=False))
+    g0 = _sampled_gradient(p, p.init_ptz, p.init_rays, frames, landmarks)
+    h = ptzba.BAHandle(0)
+    h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=ptzba.FP32,
+                  loss=ptzba.LOSS_HUBER, f_scale=1.0)
+    h.set_state(p.init_ptz, p.init_rays)
+    res = ptzba.LMSolver(h, ftol=1e-12, xtol=1e-14, max_iter=40).run()
+    ptz, rays = h.get_state()
+    h.close()
+    g = _sampled_gradient(p, ptz, rays, frames, landmarks)
+    ratio = g / g0
+    print(f"config4 fp32-huber: {res}; sampled |g*|/|g0| (pan, tilt, f, theta, phi) {ratio}", flush=True)
+    # DAMPING (5): at this tolerance the fp32 cost stops resolving a decrease before ftol does -- at a point whose
+    # gradient is already ~1e-8 of x0's (measured), which is what this test gates
+    assert res.status in (1, 2, 3, 5) and res.cost < res.initial_cost, res
+    assert np.all(ratio <= 1e-5), ratio
