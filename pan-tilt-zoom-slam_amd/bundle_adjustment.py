@@ -165,10 +165,9 @@ def bundle_adjustment(images, image_indices, feature_method, initial_ptzs, cente
     for i in range(N):
         pan, tilt, fl = all_poses[i]
         key_frame = KeyFrame(images[i], image_indices[i], center, rotation, u, v, pan, tilt, fl)
-        local_index = loc[off[i]:off[i + 1]]
-        kps = keypoints[i]
-        key_frame.feature_pts = list(map(kps.__getitem__, local_index.tolist()))
-        key_frame.feature_des = np.asarray(descriptors[i]).take(local_index, axis=0)
+        # feature_pts = [keypoints[i][k] for k in local_index], feature_des = descriptors[i][local_index], taken on
+        # first use (KeyFrame.set_features_lazy)
+        key_frame.set_features_lazy(keypoints[i], descriptors[i], loc[off[i]:off[i + 1]])
         key_frame.landmark_index = glo[off[i]:off[i + 1]].astype(np.int32)
         keyframes.append(key_frame)
         if verbose:

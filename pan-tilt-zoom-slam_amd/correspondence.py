@@ -252,7 +252,7 @@ def build_graph(images, image_match_mask=(), feature_method="sift", verbose=Fals
         need = [(i, j) for i, j in todo if cache is None or cache.peek(keys[i], keys[j], feature_method) is None]
         if len(need) > 1:
             res = image_process.match_sift_features_batch(
-                [(dets[i][0], dets[i][1], dets[j][0], dets[j][1]) for i, j in need])
+                [(dets[i][2], dets[i][1], dets[j][2], dets[j][1]) for i, j in need])  # (xy arrays: no .pt loops)
             for (i, j), (a, b) in zip(need, res):
                 m = (np.asarray(a, dtype=np.int32).reshape(-1), np.asarray(b, dtype=np.int32).reshape(-1))
                 pre[(i, j)] = m

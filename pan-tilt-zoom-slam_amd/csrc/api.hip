@@ -87,7 +87,16 @@ struct ptzba_ctx {
   std::vector<int> bsb_step_off;
   // persistent blocked back substitution (one launch, per-column update counters): expected counts, per-column
   // totals, the counters (zeroed at set_problem, advanced by one solve's totals per launch: epoch), error flag
-  DBuf bsp_expect, bsp_tot, bsp_cnt, bsp_err;
+  DBuf bsp_expect, bsp_tot, bsp_cnt;
+  int* bsp_err = nullptr;  // pinned host flag a persistent kernel sets when a wait gave up (checked by lm_wait)
+  // pinned staging of set_problem's small uploads (bump allocated, reset once the stream has drained them)
+  uint8_t* stage = nullptr;
+  size_t stage_cap = 0, stage_used = 0;
+  // single-launch factorisation (k_chol_pst): level of each task, tasks per level, per-level completion counters
+  // [n_levels] + the ticket counter
+  DBuf chol_lvl, chol_lvl_n, chol_lvl_cnt;
+  bool chol_pst = false;
+  uint32_t chol_epoch = 0;
   bool bs_pst = false;
   uint32_t bsp_epoch = 0;
   bool bs_ll = false, bs_blk = false;
@@ -213,6 +222,8 @@ void ptzba_delete(ptzba_handle h) {
     for (auto e : h->ev[k]) (void)hipEventDestroy(e);
   if (h->own) (void)hipStreamDestroy(h->own);
   if (h->scal_host) (void)hipHostFree(h->scal_host);
+  if (h->bsp_err) (void)hipHostFree(h->bsp_err);
+  if (h->stage) (void)hipHostFree(h->stage);
   if (h->group_comm) ptzba_comm_delete(h->group_comm);
   if (h->lm_host) (void)hipHostFree(h->lm_host);
   delete h;
@@ -262,9 +273,38 @@ static int upload_records(ptzba_ctx* h, const std::vector<int64_t>& order, const
   return 0;
 }
 
+// set_problem's uploads: a small array is copied into the handle's pinned staging buffer and its H2D copy queued on
+// the handle's stream without waiting (a sliding-window map calls set_problem per keyframe: ~40 uploads, each a
+// pageable copy plus a stream synchronisation before); large ones take the blocking path below.  The staging
+// buffer is reused only after the stream has drained (set_problem synchronises before its first upload and at the
+// end; a full buffer synchronises before wrapping).
+constexpr size_t STAGE_MAX = 4u << 20, STAGE_MIN_CAP = 8u << 20;
+template <typename T>
+static int upload(DBuf& b, const std::vector<T>& v, hipStream_t st);
+template <typename T>
+static int upload_st(ptzba_ctx* h, DBuf& b, const std::vector<T>& v) {
+  const size_t n = v.size() * sizeof(T);
+  if (n > STAGE_MAX) return upload(b, v, h->st);
+  if (b.alloc(n)) return -1;
+  if (n == 0) return 0;
+  size_t off = (h->stage_used + 255) & ~(size_t)255;
+  if (!h->stage || off + n > h->stage_cap) {
+    HIPCHK(hipStreamSynchronize(h->st));  // every staged copy so far has landed
+    off = 0;
+    if (!h->stage) {
+      HIPCHK(hipHostMalloc((void**)&h->stage, STAGE_MIN_CAP, hipHostMallocDefault));
+      h->stage_cap = STAGE_MIN_CAP;
+    }
+  }
+  std::memcpy(h->stage + off, v.data(), n);
+  HIPCHK(hipMemcpyAsync(b.p, h->stage + off, n, hipMemcpyHostToDevice, h->st));
+  h->stage_used = off + n;
+  return 0;
+}
+
 // blocking upload on stream st (nullptr: the null stream); returns after the copy has landed
 template <typename T>
-static int upload(DBuf& b, const std::vector<T>& v, hipStream_t st = nullptr) {
+static int upload(DBuf& b, const std::vector<T>& v, hipStream_t st) {
   if (b.alloc(v.size() * sizeof(T))) return -1;
   if (!v.empty()) {
     HIPCHK(hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st));
@@ -1470,7 +1510,9 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->perm_uploaded = false;
 
   st_mark("work order+plan");
-  // ---- upload
+  // ---- upload (staged: the stream has drained, so the staging buffer is free)
+  HIPCHK(hipStreamSynchronize(h->st));
+  h->stage_used = 0;
   std::vector<double> seg_base(2 * n_seg);
   for (int64_t s = 0; s < n_seg; ++s) {
     const int64_t r = order[seg_rec_begin[s]];
@@ -1480,28 +1522,28 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   int rc = h->precision == PTZBA_FP32 ? upload_records<float>(h, order, rec_seg, seg_base, obs_xy, obs_weight)
                                       : upload_records<double>(h, order, rec_seg, seg_base, obs_xy, obs_weight);
   if (rc) return rc;
-  if (upload(h->seg_base, seg_base, h->st)) return -1;
+  if (upload_st(h, h->seg_base, seg_base)) return -1;
   {  // K1's 1-byte segment key: the record's segment within its landmark's window of K1_SEGW segments
     std::vector<uint8_t> key(n_obs + 4);  // + 4: K1 reads whole 4-record key groups
     for (int64_t k = 0; k < n_obs; ++k) {
       const int32_t sg = rec_seg[k];
       key[k] = (uint8_t)((sg - lm_seg_begin[seg_lm[sg]]) % K1_SEGW);
     }
-    if (upload(h->rec_key, key, h->st)) return -1;
+    if (upload_st(h, h->rec_key, key)) return -1;
   }
-  if (upload(h->rec_seg, rec_seg, h->st) || upload(h->seg_frame, seg_frame, h->st) || upload(h->seg_lm, seg_lm, h->st) ||
-      upload(h->seg_rec_begin, seg_rec_begin, h->st) || upload(h->lm_seg_begin, lm_seg_begin, h->st) ||
-      upload(h->lm_order, lm_work, h->st) || upload(h->frame_seg_begin, frame_seg_begin, h->st) ||
-      upload(h->frame_seg_list, frame_seg_list, h->st) || upload(h->frame_win_hi, frame_win_hi, h->st) ||
-      upload(h->s2_items, s2_items, h->st) || upload(h->s2_groups, s2_groups, h->st) || upload(h->s2_lm, s2_lm, h->st) ||
-      upload(h->lm_meta, lm_meta, h->st))
+  if (upload_st(h, h->rec_seg, rec_seg) || upload_st(h, h->seg_frame, seg_frame) || upload_st(h, h->seg_lm, seg_lm) ||
+      upload_st(h, h->seg_rec_begin, seg_rec_begin) || upload_st(h, h->lm_seg_begin, lm_seg_begin) ||
+      upload_st(h, h->lm_order, lm_work) || upload_st(h, h->frame_seg_begin, frame_seg_begin) ||
+      upload_st(h, h->frame_seg_list, frame_seg_list) || upload_st(h, h->frame_win_hi, frame_win_hi) ||
+      upload_st(h, h->s2_items, s2_items) || upload_st(h, h->s2_groups, s2_groups) || upload_st(h, h->s2_lm, s2_lm) ||
+      upload_st(h, h->lm_meta, lm_meta))
     return -1;
   {  // item -> tile (group) map and the per-tile split counters of the folded reduce (zero between launches)
     std::vector<int32_t> item_group(std::max(h->n_s2_items, 1), 0);
     for (int g = 0; g < h->n_s2_groups; ++g)
       for (int it = s2_groups[4 * g + 2]; it < s2_groups[4 * g + 3]; ++it)
         if (it < h->n_s2_items) item_group[it] = g;  // (pair items: their first chunk's tile)
-    if (upload(h->s2_item_group, item_group, h->st) || h->s2_tile_cnt.alloc((size_t)std::max(h->n_s2_groups, 1) * 4))
+    if (upload_st(h, h->s2_item_group, item_group) || h->s2_tile_cnt.alloc((size_t)std::max(h->n_s2_groups, 1) * 4))
       return -1;
     HIPCHK(hipMemsetAsync(h->s2_tile_cnt.p, 0, h->s2_tile_cnt.bytes, h->st));
   }
@@ -1521,14 +1563,14 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       h->s2_part.alloc((size_t)std::max(h->n_s2_items, 1) * (h->s2_pair ? 2 : 1) * SCHUR_F1 * 9 * WAVE * 8) ||
       h->part_diag.alloc((size_t)std::max(h->n_s2_items, 1) * SCHUR_F1 * 12 * 8))
     return -1;
-  if (upload(h->chol_tasks, plan.tasks, h->st) || upload(h->tinv_tail, plan.tinv_tail, h->st) || upload(h->frame_pos, sorder.pos, h->st) || upload(h->row_pad, sorder.pad, h->st) ||
-      upload(h->bs_chain_off, plan.chain_off, h->st) || upload(h->bs_chain_cols, plan.chain_cols, h->st) ||
-      upload(h->bs_upd_off, plan.upd_off, h->st) || upload(h->bs_upd_tiles, plan.upd_tiles, h->st) || upload(h->xtiles, plan.xtiles, h->st) || upload(h->ztiles, plan.ztiles, h->st) ||
-      upload(h->bs_la_tasks, plan.la_tasks, h->st) || upload(h->bs_lo_off, plan.lo_off, h->st) || upload(h->bs_lo_tiles, plan.lo_tiles, h->st))
+  if (upload_st(h, h->chol_tasks, plan.tasks) || upload_st(h, h->tinv_tail, plan.tinv_tail) || upload_st(h, h->frame_pos, sorder.pos) || upload_st(h, h->row_pad, sorder.pad) ||
+      upload_st(h, h->bs_chain_off, plan.chain_off) || upload_st(h, h->bs_chain_cols, plan.chain_cols) ||
+      upload_st(h, h->bs_upd_off, plan.upd_off) || upload_st(h, h->bs_upd_tiles, plan.upd_tiles) || upload_st(h, h->xtiles, plan.xtiles) || upload_st(h, h->ztiles, plan.ztiles) ||
+      upload_st(h, h->bs_la_tasks, plan.la_tasks) || upload_st(h, h->bs_lo_off, plan.lo_off) || upload_st(h, h->bs_lo_tiles, plan.lo_tiles))
     return -1;
   if (part_mode) {
-    if (upload(h->row_phase, row_phase, h->st) || upload(h->fmask, fmask, h->st) ||
-        upload(h->ptiles, pplan.part_tiles, h->st) || upload(h->stiles, pplan.sep_tiles, h->st) ||
+    if (upload_st(h, h->row_phase, row_phase) || upload_st(h, h->fmask, fmask) ||
+        upload_st(h, h->ptiles, pplan.part_tiles) || upload_st(h, h->stiles, pplan.sep_tiles) ||
         h->pbuf.alloc((size_t)h->n_pbuf * 8) || h->sbuf.alloc((size_t)h->n_sbuf * 8))
       return -1;
   } else {
@@ -1561,18 +1603,36 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->bsb_step_off = plan.bsb_step_off;
   // persistent form: every step's tasks in one launch (all resident at <= 512 workgroups); PTZBA_BS_PERSIST=0 keeps
   // one launch per step (A/B knob)
-  h->bs_pst = h->bs_blk && !getenv_is("PTZBA_BS_PERSIST", "0") && getenv_is("PTZBA_BS_PERSIST", "1") &&
+  // (same-box A/B r04a: cholesky_solve 245 -> 241 us per trial at config 3)
+  h->bs_pst = h->bs_blk && !getenv_is("PTZBA_BS_PERSIST", "0") &&
               plan.bsb_tasks.size() / 12 <= 512;  // (2 workgroups per CU resident: 190 VGPRs)
   h->bsp_epoch = 0;
+  // single-launch factorisation (PTZBA_CHOL_PERSIST=1, A/B knob): single-process SPD solves
+  h->chol_pst = !part_mode && !dist && getenv_is("PTZBA_CHOL_PERSIST", "1") && plan.n_levels > 0;
+  h->chol_epoch = 0;
+  if (h->chol_pst) {
+    std::vector<int32_t> lvl(std::max(plan.level_off[plan.n_levels], 1), 0), lvl_n(plan.n_levels, 0);
+    for (int L = 0; L < plan.n_levels; ++L) {
+      lvl_n[L] = plan.level_off[L + 1] - plan.level_off[L];
+      for (int t = plan.level_off[L]; t < plan.level_off[L + 1]; ++t) lvl[t] = L;
+    }
+    if (upload_st(h, h->chol_lvl, lvl) || upload_st(h, h->chol_lvl_n, lvl_n) ||
+        h->chol_lvl_cnt.alloc(4 * ((size_t)plan.n_levels + 1)))
+      return -1;
+    HIPCHK(hipMemsetAsync(h->chol_lvl_cnt.p, 0, h->chol_lvl_cnt.bytes, h->st));
+  }
+  if ((h->bs_pst || h->chol_pst) && !h->bsp_err) {
+    HIPCHK(hipHostMalloc((void**)&h->bsp_err, sizeof(int), hipHostMallocDefault));
+    *h->bsp_err = 0;
+  }
   if (h->bs_pst) {
-    if (upload(h->bsp_expect, plan.bsb_expect, h->st) || upload(h->bsp_tot, plan.bsb_tot, h->st) ||
-        h->bsp_cnt.alloc(4 * plan.bsb_tot.size()) || h->bsp_err.alloc(4))
+    if (upload_st(h, h->bsp_expect, plan.bsb_expect) || upload_st(h, h->bsp_tot, plan.bsb_tot) ||
+        h->bsp_cnt.alloc(4 * plan.bsb_tot.size()))
       return -1;
     HIPCHK(hipMemsetAsync(h->bsp_cnt.p, 0, h->bsp_cnt.bytes, h->st));
-    HIPCHK(hipMemsetAsync(h->bsp_err.p, 0, h->bsp_err.bytes, h->st));
   }
   if (h->bs_blk) {
-    if (upload(h->bsb_tasks, plan.bsb_tasks, h->st) ||
+    if (upload_st(h, h->bsb_tasks, plan.bsb_tasks) ||
         h->bsb_r.alloc((size_t)h->ld * 8))
       return -1;
   } else {
@@ -1919,15 +1979,22 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
       launch_chol_prepare_damped(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(),
                                  h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
                                  h->lambda, lam_dev, h->st);
-    launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
-                    h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>(), 0,
-                    h->chol_delayed);
+    if (h->chol_pst)
+      launch_cholesky_pst(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_lvl.as<int>(),
+                          h->chol_lvl_n.as<int>(), h->chol_lvl_cnt.as<unsigned>(),
+                          h->chol_lvl_cnt.as<unsigned>() + h->chol_levels, h->chol_epoch++, 0, h->chol_levels,
+                          h->Ldiag.as<double>(), h->info.as<int>(), h->Minv.as<double>(), h->chol_delayed, h->bsp_err,
+                          h->st);
+    else
+      launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
+                      h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>(), 0,
+                      h->chol_delayed);
   }
   if (h->bs_pst)
     launch_chol_backsolve_pst(h->S(), h->ld, h->n_aug, h->bsb_tasks.as<int4>(), h->bsp_expect.as<int4>(),
                               h->bsb_step_off.back(), h->Ldiag.as<double>(), h->Minv.as<double>(), h->bsb_r.as<double>(),
                               h->dpose.as<double>(), h->bsp_cnt.as<unsigned>(), h->bsp_tot.as<int>(), h->bsp_epoch++,
-                              h->bsp_err.as<int>(), h->st, h->tinv_tail.as<int>(), h->n_tinv_tail);
+                              h->bsp_err, h->st, h->tinv_tail.as<int>(), h->n_tinv_tail);
   else if (h->bs_blk)
     launch_chol_backsolve_blk(h->S(), h->ld, h->n_aug, h->bsb_tasks.as<int4>(), h->bsb_step_off.data(), (int)h->bsb_step_off.size() - 1, h->Ldiag.as<double>(),
                               h->Minv.as<double>(), h->bsb_r.as<double>(), h->dpose.as<double>(), h->st,
@@ -2090,6 +2157,9 @@ int ptzba_lm_wait(ptzba_handle h, int trial, ptzba_lm_record* out) {
     }
     __builtin_ia32_pause();
   }
+  if ((h->bs_pst || h->chol_pst) && __atomic_load_n(h->bsp_err, __ATOMIC_ACQUIRE))
+    return fail("lm_wait: a persistent factorisation / back-substitution kernel gave up waiting (workgroups not "
+                "co-resident?); PTZBA_CHOL_PERSIST=0 / PTZBA_BS_PERSIST=0 select the per-level forms");
   const LMDev& r = h->lm_host[k];
   out->cost = r.cost;
   out->initial_cost = r.initial_cost;
@@ -2203,6 +2273,9 @@ int ptzba_read_scalars(ptzba_handle h, double* out) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(h->scal_host, h->scal_pack.p, 17 * sizeof(double), hipMemcpyDeviceToHost, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
+  if ((h->bs_pst || h->chol_pst) && __atomic_load_n(h->bsp_err, __ATOMIC_ACQUIRE))
+    return fail("a persistent factorisation / back-substitution kernel gave up waiting (PTZBA_CHOL_PERSIST=0 / "
+                "PTZBA_BS_PERSIST=0 select the per-level forms)");
   const double* s = h->scal_host;
   const double* l = h->scal_host + 8;
   out[0] = s[0];

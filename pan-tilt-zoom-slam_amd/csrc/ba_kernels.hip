@@ -852,8 +852,10 @@ void launch_trial(const BacksubArgs& a, const double* ptz, const double* g_pose,
                   double* out4, int n_pose, void* ft64, void* rt64, void* ft, void* rt, hipStream_t st,
                   const uint8_t* fmask, const int* info) {
   PoseTrialArgs pa{ptz, g_pose, D_pose, ptz_trial, out4, n_pose, fmask, info};
-  static const bool dpl_off = getenv("PTZBA_TRIAL_DPL") && atoi(getenv("PTZBA_TRIAL_DPL")) == 0;  // A/B knob
-  if (n_pose <= K1_FT_LDS && !dpl_off && !fmask)  // (part-owned solves: the other part's dpose rows are not solved here)
+  // PTZBA_TRIAL_DPL=1: dense dpose staged in LDS (A/B knob; off: config 3 trial 35.9 -> 27.9 us without it, r04a)
+  const char* dpl_env = getenv("PTZBA_TRIAL_DPL");  // (read per launch: tests switch it between handles)
+  const bool dpl_on = dpl_env && atoi(dpl_env) == 1;
+  if (n_pose <= K1_FT_LDS && dpl_on && !fmask)  // (part-owned solves: the other part's dpose rows are not solved here)
     hipLaunchKernelGGL((k_trial<real, true>), dim3((unsigned)((a.n_lm + 3) / 4 + 1)), dim3(256), 0, st, a, pa,
                        (FrameTab<double>*)ft64, (RayTab<double>*)rt64, (FrameTab<real>*)ft, (RayTab<real>*)rt);
   else

@@ -101,11 +101,25 @@ void launch_chol_prepare_damped(double* A, int64_t ld, int n, double* b, const u
 // Batched tile staging: every thread fetches its 4 elements of each tile into registers first (all global
 // loads of a task in flight together: one memory round trip per task instead of one per update panel),
 // then writes them to LDS.  256 threads per workgroup.
+// COH (the persistent factorisation, k_chol_pst): tiles written by other workgroups of the same launch are read
+// with agent-scope loads that miss this XCD's (possibly stale) L2 and written through with agent-scope stores
+// (MI355X_MICROARCH.md, inter-workgroup hand-off table, first row); plain accesses otherwise.
+template <bool COH>
+__device__ __forceinline__ double gld(const double* p) {
+  if constexpr (COH) return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+template <bool COH>
+__device__ __forceinline__ void gst(double* p, double v) {
+  if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+template <bool COH = false>
 __device__ __forceinline__ void fetch_tile(double (&v)[4], const double* __restrict__ src, int64_t ld) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int e = threadIdx.x + 256 * q;
-    v[q] = src[(int64_t)(e >> 5) * ld + (e & 31)];
+    v[q] = gld<COH>(src + (int64_t)(e >> 5) * ld + (e & 31));
   }
 }
 __device__ __forceinline__ void put_tile(double (*dst)[NB + 1], const double (&v)[4]) {
@@ -719,9 +733,10 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
 // reciprocals, then one wave: lane j computes column j by forward substitution against e_j, right-looking
 // (after m_k is known every later row's running sum takes its term at once: the dependent chain is one
 // multiply and one FMA per row).  Shared by k_tile_inv and the type-2 tasks of the level launches.
+template <bool COH = false>
 __device__ __forceinline__ void tile_inv_wave(const double* __restrict__ src, double* __restrict__ dst,
                                               double (*Lt)[NB + 1], double* rinv) {
-  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) Lt[e >> 5][e & 31] = src[e];
+  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) Lt[e >> 5][e & 31] = gld<COH>(src + e);
   __syncthreads();
   if (threadIdx.x < NB) rinv[threadIdx.x] = rcp_nr(Lt[threadIdx.x][threadIdx.x]);
   __syncthreads();
@@ -750,6 +765,7 @@ __device__ __forceinline__ void tile_inv_wave(const double* __restrict__ src, do
 // L_{j0+1,p} (B side) in LDS -- each loaded once for the (up to) two output tiles that use it -- with the next
 // panel's tiles in flight in registers.  Same MFMA sequence per output tile as tile_gemm_nt_sub: bitwise the
 // result of one task per tile.
+template <bool COH = false>
 __device__ __forceinline__ void chol_trail_block(double* __restrict__ A, int64_t ld, int i0, int j0, int mask, int up0,
                                                  int up1, int up2, int up3, double (*sA)[NB][NB + 1],
                                                  double (*sB)[NB][NB + 1]) {
@@ -768,15 +784,15 @@ __device__ __forceinline__ void chol_trail_block(double* __restrict__ A, int64_t
 #pragma unroll
       for (int y = 0; y < 2; ++y)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[x][y][r] = C[(int64_t)(16 * x + lk + 4 * r) * ld + 16 * y + li];
+        for (int r = 0; r < 4; ++r) acc[x][y][r] = gld<COH>(C + (int64_t)(16 * x + lk + 4 * r) * ld + 16 * y + li);
   }
   const int ups[4] = {up0, up1, up2, up3};
   double ra[2][4], rb[2][4];  // one register set: the next panel's tiles are fetched once this one is in LDS
   auto fetch = [&](int p) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      if (needA[t]) fetch_tile(ra[t], A + (i0 + t) * NBl * ld + p * NBl, ld);
-      if (needB[t]) fetch_tile(rb[t], A + (j0 + t) * NBl * ld + p * NBl, ld);
+      if (needA[t]) fetch_tile<COH>(ra[t], A + (i0 + t) * NBl * ld + p * NBl, ld);
+      if (needB[t]) fetch_tile<COH>(rb[t], A + (j0 + t) * NBl * ld + p * NBl, ld);
     }
   };
   int u = 0;
@@ -815,7 +831,7 @@ __device__ __forceinline__ void chol_trail_block(double* __restrict__ A, int64_t
 #pragma unroll
       for (int y = 0; y < 2; ++y)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) C[(int64_t)(16 * x + lk + 4 * r) * ld + 16 * y + li] = acc[x][y][r];
+        for (int r = 0; r < 4; ++r) gst<COH>(C + (int64_t)(16 * x + lk + 4 * r) * ld + 16 * y + li, acc[x][y][r]);
   }
 }
 
@@ -831,10 +847,13 @@ struct CholTaskVal {
   __device__ int4 get(int b) const { return b < CHOL_KT ? t[b] : rest[b - CHOL_KT]; }
 };
 // P2: plans with delayed trailing updates (a second pair of update panels per task, api.hip make_plan)
-template <bool SG, typename TaskArg, bool P2 = false>
-__global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64_t ld, const TaskArg tasks,
-                                                   double* __restrict__ Ldiag, int* info, double* __restrict__ sgn,
-                                                   double* __restrict__ Minv) {
+// One factorisation task (api.hip make_plan: panel / trailing / inverse / trailing block) by the workgroup: the
+// body of a level launch (k_chol_step) and of the persistent form (k_chol_pst, COH = true).
+template <bool SG, bool P2, bool COH>
+__device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, const int4 tk, double* __restrict__ Ldiag,
+                                          int* info, double* __restrict__ sgn, double* __restrict__ Minv) {
+  static_assert(!(COH && SG), "the persistent form factors SPD systems only");
+  static_assert(!(COH && CHOL_TRAIL_DIRECT), "the persistent form stages trailing tiles");
   __shared__ double sC[NB][NB + 1];     // target tile (panel T_ik / trailing A_ij)
   __shared__ double sD[NB][NB + 1];     // diagonal tile -> L_kk
   __shared__ __attribute__((aligned(16))) double sA[2][NB][NB + 1];  // L_ip of the two update panels
@@ -862,11 +881,10 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
 #endif
   __shared__ double s_sgp[2][NB];  // SG: signs of the two update panels' columns
   __shared__ double s_sig[NB];     // SG: signs of this column's pivots
-  const int4 tk = tasks.get(blockIdx.x);
   if ((tk.x & 3) == 2) {  // inverse of a diagonal factor tile of the previous level (see tile_inv_wave)
     if (tk.y < 0) return;  // no-op slot of an XCD-ordered level (api.hip xcd_interleave)
     __shared__ double s_rinv[NB];
-    tile_inv_wave(Ldiag + (int64_t)tk.y * NB * NB, Minv + (int64_t)tk.y * NB * NB, sD, s_rinv);
+    tile_inv_wave<COH>(Ldiag + (int64_t)tk.y * NB * NB, Minv + (int64_t)tk.y * NB * NB, sD, s_rinv);
     return;
   }
 #if CHOL_FEWER_BARRIERS && CHOL_WG == 3
@@ -895,7 +913,7 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
 #endif
   if constexpr (P2 && !SG) {
     if (type == 3) {  // 2 x 2 block of trailing tiles (api.hip make_plan): A_ij -= sum_p L_ip L_jp^T
-      chol_trail_block(A, ld, i, j, ((tk.w >> 28) & 3) | (((unsigned)tk.x >> 30) << 2), up0, up1, up2, up3, sA, sB);
+      chol_trail_block<COH>(A, ld, i, j, ((tk.w >> 28) & 3) | (((unsigned)tk.x >> 30) << 2), up0, up1, up2, up3, sA, sB);
       return;
     }
   }
@@ -958,27 +976,27 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
 #if CHOL_VARIANT == 7  // timing only: no C tile read / write
     for (int r = 0; r < 4; ++r) v0[r] = 0.0;
 #else
-    fetch_tile(v0, C, ld);
+    fetch_tile<COH>(v0, C, ld);
 #endif
 #if CHOL_VARIANT == 6  // timing only: no panel tile reads
     for (int r = 0; r < 4; ++r) v1[r] = v2[r] = v3[r] = v4[r] = 0.0;
 #else
     if (up0 >= 0) {
-      fetch_tile(v1, A + i * NBl * ld + up0 * NBl, ld);
-      fetch_tile(v2, A + j * NBl * ld + up0 * NBl, ld);
+      fetch_tile<COH>(v1, A + i * NBl * ld + up0 * NBl, ld);
+      fetch_tile<COH>(v2, A + j * NBl * ld + up0 * NBl, ld);
     }
     if (up1 >= 0) {
-      fetch_tile(v3, A + i * NBl * ld + up1 * NBl, ld);
-      fetch_tile(v4, A + j * NBl * ld + up1 * NBl, ld);
+      fetch_tile<COH>(v3, A + i * NBl * ld + up1 * NBl, ld);
+      fetch_tile<COH>(v4, A + j * NBl * ld + up1 * NBl, ld);
     }
 #endif
     if (up2 >= 0) {
-      fetch_tile(w2, A + i * NBl * ld + up2 * NBl, ld);
-      fetch_tile(w3, A + j * NBl * ld + up2 * NBl, ld);
+      fetch_tile<COH>(w2, A + i * NBl * ld + up2 * NBl, ld);
+      fetch_tile<COH>(w3, A + j * NBl * ld + up2 * NBl, ld);
     }
     if (up3 >= 0) {
-      fetch_tile(w4, A + i * NBl * ld + up3 * NBl, ld);
-      fetch_tile(w5, A + j * NBl * ld + up3 * NBl, ld);
+      fetch_tile<COH>(w4, A + i * NBl * ld + up3 * NBl, ld);
+      fetch_tile<COH>(w5, A + j * NBl * ld + up3 * NBl, ld);
     }
     put_tile(sC, v0);
     if (up0 >= 0) {
@@ -1011,7 +1029,7 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
     }
     __syncthreads();
 #if CHOL_VARIANT != 7
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) C[(int64_t)(e >> 5) * ld + (e & 31)] = sC[e >> 5][e & 31];
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) gst<COH>(C + (int64_t)(e >> 5) * ld + (e & 31), sC[e >> 5][e & 31]);
 #endif
     return;
   }
@@ -1020,16 +1038,16 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   const bool diag_only = (i == k);
   const bool updT0 = !diag_only && (tmask & 1), updT1 = !diag_only && (tmask & 2);
   const bool updT2 = !diag_only && (tmask2 & 1), updT3 = !diag_only && (tmask2 & 2);
-  fetch_tile(v0, A + (int64_t)k * NBl * ld + k * NBl, ld);
-  if (!diag_only) fetch_tile(v1, A + i * NBl * ld + k * NBl, ld);
-  if (up0 >= 0) fetch_tile(v2, A + (int64_t)k * NBl * ld + up0 * NBl, ld);
-  if (updT0 && up0 >= 0) fetch_tile(v3, A + i * NBl * ld + up0 * NBl, ld);
-  if (up1 >= 0) fetch_tile(v4, A + (int64_t)k * NBl * ld + up1 * NBl, ld);
-  if (updT1 && up1 >= 0) fetch_tile(v5, A + i * NBl * ld + up1 * NBl, ld);
-  if (up2 >= 0) fetch_tile(w2, A + (int64_t)k * NBl * ld + up2 * NBl, ld);
-  if (updT2 && up2 >= 0) fetch_tile(w3, A + i * NBl * ld + up2 * NBl, ld);
-  if (up3 >= 0) fetch_tile(w4, A + (int64_t)k * NBl * ld + up3 * NBl, ld);
-  if (updT3 && up3 >= 0) fetch_tile(w5, A + i * NBl * ld + up3 * NBl, ld);
+  fetch_tile<COH>(v0, A + (int64_t)k * NBl * ld + k * NBl, ld);
+  if (!diag_only) fetch_tile<COH>(v1, A + i * NBl * ld + k * NBl, ld);
+  if (up0 >= 0) fetch_tile<COH>(v2, A + (int64_t)k * NBl * ld + up0 * NBl, ld);
+  if (updT0 && up0 >= 0) fetch_tile<COH>(v3, A + i * NBl * ld + up0 * NBl, ld);
+  if (up1 >= 0) fetch_tile<COH>(v4, A + (int64_t)k * NBl * ld + up1 * NBl, ld);
+  if (updT1 && up1 >= 0) fetch_tile<COH>(v5, A + i * NBl * ld + up1 * NBl, ld);
+  if (up2 >= 0) fetch_tile<COH>(w2, A + (int64_t)k * NBl * ld + up2 * NBl, ld);
+  if (updT2 && up2 >= 0) fetch_tile<COH>(w3, A + i * NBl * ld + up2 * NBl, ld);
+  if (up3 >= 0) fetch_tile<COH>(w4, A + (int64_t)k * NBl * ld + up3 * NBl, ld);
+  if (updT3 && up3 >= 0) fetch_tile<COH>(w5, A + i * NBl * ld + up3 * NBl, ld);
   put_tile(sD, v0);
   if (!diag_only) put_tile(sC, v1);
   if (up0 >= 0) put_tile(sB[0], v2);
@@ -1095,7 +1113,7 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
     double* C = Ldiag + (int64_t)k * NB * NB;
     for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
       const int r = e >> 5, m = e & 31;
-      C[e] = m <= r ? s_lb[m / LA_BW][r][m % LA_BW] : 0.0;
+      gst<COH>(C + e, m <= r ? s_lb[m / LA_BW][r][m % LA_BW] : 0.0);
     }
     if constexpr (SG) {
       if (threadIdx.x < NB) sgn[(int64_t)k * NB + threadIdx.x] = s_sig[threadIdx.x];
@@ -1105,27 +1123,108 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   {
     double* C = A + i * NBl * ld + k * NBl;
     for (int e = threadIdx.x; e < NB * NB; e += blockDim.x)
-      C[(int64_t)(e >> 5) * ld + (e & 31)] = s_lb[(e & 31) / LA_BW][NB + (e >> 5)][(e & 31) % LA_BW];
+      gst<COH>(C + (int64_t)(e >> 5) * ld + (e & 31), s_lb[(e & 31) / LA_BW][NB + (e >> 5)][(e & 31) % LA_BW]);
     return;
   }
 #endif
   if (diag_only) {
     // A_kk itself stays untouched: other panel workgroups of this launch are still reading it
     double* C = Ldiag + (int64_t)k * NB * NB;
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) C[e] = sD[e >> 5][e & 31];
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) gst<COH>(C + e, sD[e >> 5][e & 31]);
     if constexpr (SG) {
       if (threadIdx.x < NB) sgn[(int64_t)k * NB + threadIdx.x] = s_sig[threadIdx.x];
     }
     return;
   }
   double* C = A + i * NBl * ld + k * NBl;
-  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) C[(int64_t)(e >> 5) * ld + (e & 31)] = sC[e >> 5][e & 31];
+  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) gst<COH>(C + (int64_t)(e >> 5) * ld + (e & 31), sC[e >> 5][e & 31]);
+}
+
+template <bool SG, typename TaskArg, bool P2 = false, bool COH = false>
+__global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64_t ld, const TaskArg tasks,
+                                                   double* __restrict__ Ldiag, int* info, double* __restrict__ sgn,
+                                                   double* __restrict__ Minv) {
+  chol_task<SG, P2, COH>(A, ld, tasks.get(blockIdx.x), Ldiag, info, sgn, Minv);
+}
+
+// Single-launch form of the level launches (single-process SPD solves): the tasks of levels [L0, L1) in ONE launch of
+// one workgroup per task.  A workgroup takes its task by a ticket (atomic add on a counter that advances by the task
+// count per launch: ticket - epoch * n), so a task's predecessors -- all at lower indices -- belong to workgroups that
+// started earlier: forward progress needs no co-residency and no dispatch-order assumption.  A task of level L > L0
+// starts once level L - 1's counter shows all its tasks done in this epoch; tiles are read and written coherently
+// (COH), and a task's stores are drained (vmcnt(0)) before its level counter moves.  The same tasks in the same order
+// per tile as the level launches: bitwise the same factor.  The launch boundaries between levels (~26 per trial at
+// config 3) become counter hand-offs.
+constexpr int CPST_SPIN = 1 << 22;  // polls before a wait gives up (err = 1): ~seconds, never a hang
+template <bool P2>
+__global__ __launch_bounds__(256) void k_chol_pst(double* __restrict__ A, int64_t ld, const int4* __restrict__ tasks,
+                                                  const int* __restrict__ task_lvl, int t0, int n, int L0,
+                                                  const int* __restrict__ lvl_n, unsigned* __restrict__ lvl_cnt,
+                                                  unsigned* __restrict__ ticket, uint32_t epoch,
+                                                  double* __restrict__ Ldiag, int* info, double* __restrict__ Minv,
+                                                  int* err) {
+  __shared__ int s_t;
+  if (threadIdx.x == 0) {
+    const int t = t0 + (int)(__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                             epoch * (unsigned)n);
+    s_t = t;
+    const int L = task_lvl[t];
+    if (L > L0) {
+      const unsigned target = (epoch + 1u) * (unsigned)lvl_n[L - 1];
+      bool ok = false;
+      for (int k = 0; k < CPST_SPIN; ++k) {
+        if ((int)(__hip_atomic_load(lvl_cnt + L - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) >= 0) {
+          ok = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (!ok) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // pinned host flag
+    }
+  }
+  __syncthreads();
+  const int t = s_t;
+  chol_task<false, P2, true>(A, ld, tasks[t], Ldiag, info, nullptr, Minv);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's tile stores have landed (write-through)
+  __syncthreads();                                   // ... every thread's
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(lvl_cnt + task_lvl[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+int launch_cholesky_pst(double* A, int64_t ld, const int4* tasks, const int* task_off_host, const int* task_lvl,
+                        const int* lvl_n, unsigned* lvl_cnt, unsigned* ticket, uint32_t epoch, int L0, int L1,
+                        double* Ldiag, int* info, double* Minv, bool delayed, int* err, hipStream_t st) {
+  const int t0 = task_off_host[L0], n = task_off_host[L1] - t0;
+  if (n <= 0) return 0;
+  if (delayed)
+    hipLaunchKernelGGL(k_chol_pst<true>, dim3((unsigned)n), dim3(256), 0, st, A, ld, tasks, task_lvl, t0, n, L0, lvl_n,
+                       lvl_cnt, ticket, epoch, Ldiag, info, Minv, err);
+  else
+    hipLaunchKernelGGL(k_chol_pst<false>, dim3((unsigned)n), dim3(256), 0, st, A, ld, tasks, task_lvl, t0, n, L0, lvl_n,
+                       lvl_cnt, ticket, epoch, Ldiag, info, Minv, err);
+  return 0;
 }
 
 void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_off_host, int n_launch, double* Ldiag,
                      int* info, hipStream_t st, double* sgn, const int4* tasks_host, double* Minv, int first_level,
                      bool delayed) {
   static const bool by_value = !getenv("PTZBA_CHOL_TASKS_PTR");  // A/B knob
+  // diagnostic A/B knob: the level launches with the single-launch form's coherent tile traffic (what the L2 bypass
+  // costs by itself); read per call
+  const char* coh_env = getenv("PTZBA_CHOL_COH");
+  if (coh_env && atoi(coh_env) == 1 && !sgn && tasks_host && by_value) {
+    for (int L = first_level; L < n_launch; ++L) {
+      const int n = task_off_host[L + 1] - task_off_host[L];
+      if (n <= 0) continue;
+      CholTaskVal tv;
+      std::memcpy(tv.t, tasks_host + task_off_host[L], std::min(n, CHOL_KT) * sizeof(int4));
+      tv.rest = tasks + task_off_host[L] + CHOL_KT;
+      if (delayed)
+        hipLaunchKernelGGL((k_chol_step<false, CholTaskVal, true, true>), dim3(n), dim3(256), 0, st, A, ld, tv, Ldiag, info, sgn, Minv);
+      else
+        hipLaunchKernelGGL((k_chol_step<false, CholTaskVal, false, true>), dim3(n), dim3(256), 0, st, A, ld, tv, Ldiag, info, sgn, Minv);
+    }
+    return;
+  }
   for (int L = first_level; L < n_launch; ++L) {
     const int n = task_off_host[L + 1] - task_off_host[L];
     if (n <= 0) continue;
@@ -1719,7 +1818,7 @@ __global__ __launch_bounds__(64 * BSB_P) void k_chol_backsolve_pst(
         rt = __hip_atomic_load(r + (int64_t)t * NB + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    if (!ok && lane == 0) atomicOr(err, 1);
+    if (!ok && lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // pinned host flag
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): s_cnt's init
   __builtin_amdgcn_s_barrier();

@@ -147,9 +147,17 @@ def match_sift_features(keypoint1, descriptor1, keypoint2, descriptor2, pts_arra
 GPU_MATCH_SIFT = match_sift_features  # (correspondence.build_graph batches pairs only while this is the matcher)
 
 
+def _pts(kp, index):
+    """[len(index), 2] float64 positions of keypoints `index` (KeyPoint list or an [n, 2] array of .pt values)."""
+    if isinstance(kp, np.ndarray):
+        return np.asarray(kp, np.float64).reshape(-1, 2)[index]
+    return np.array([kp[i].pt for i in index], np.float64).reshape(-1, 2)
+
+
 def match_sift_features_batch(pairs):
     """match_sift_features for several descriptor pairs in three launches instead of five per pair: `pairs` is a
-    list of (keypoints1, descriptors1, keypoints2, descriptors2); pairs sharing the same train set (descriptors2
+    list of (keypoints1, descriptors1, keypoints2, descriptors2) -- keypoints as KeyPoint lists or [n, 2] arrays of
+    their .pt; pairs sharing the same train set (descriptors2
     object) run as ONE kNN-2 over their concatenated queries (a new keyframe against every overlapping window
     partner), the ratio test per pair, then ONE batched homography RANSAC (ptz_homography_ransac_batch, per pair
     the same seed and result as homography_ransac).  Returns [(index1 list, index2 list)] with exactly
@@ -177,9 +185,7 @@ def match_sift_features_batch(pairs):
                 continue
             index1 = good.astype(np.int32)
             index2 = ii[good, 0].astype(np.int32)
-            kp1, kp2 = pairs[q][0], pairs[q][2]
-            pts1 = np.array([kp1[i].pt for i in index1], np.float64).reshape(-1, 2)
-            pts2 = np.array([kp2[j].pt for j in index2], np.float64).reshape(-1, 2)
+            pts1, pts2 = _pts(pairs[q][0], index1), _pts(pairs[q][2], index2)
             cand.append((q, index1, index2, pts1, pts2))
     res = ptzba.homography_ransac_batch([(c[3], c[4]) for c in cand], 1.0)
     for (q, index1, index2, _, _), (mask, _, _) in zip(cand, res):

@@ -32,8 +32,9 @@ class KeyFrame:
     def __init__(self, img, img_index, center, rotation, u, v, pan, tilt, f):
         self.img = img
         self.img_index = img_index
-        self.feature_pts = np.ndarray(0)
-        self.feature_des = np.ndarray(0)
+        self._lazy = None
+        self._pts = np.ndarray(0)
+        self._des = np.ndarray(0)
         self.landmark_index = []
         self.pan, self.tilt, self.f = pan, tilt, f
         self.center = center
@@ -41,8 +42,47 @@ class KeyFrame:
         self.u = u
         self.v = v
 
+    # feature_pts / feature_des: plain attributes as in the reference; bundle_adjustment hands them over as (all
+    # keypoints, all descriptors, selected indices) and the subset is taken on first use -- a 30-keyframe window
+    # re-creates every keyframe per BA call, and most of them are never read before the next call replaces them
+    def set_features_lazy(self, keypoints, descriptors, index):
+        self._lazy = (keypoints, descriptors, np.asarray(index, np.int64))
+
+    def _materialise(self):
+        kps, des, idx = self._lazy
+        self._lazy = None
+        if isinstance(kps, np.ndarray):
+            self._pts = np.asarray(kps)[idx]
+        else:
+            self._pts = list(map(kps.__getitem__, idx.tolist()))
+        self._des = np.asarray(des).take(idx, axis=0)
+
+    @property
+    def feature_pts(self):
+        if self._lazy is not None:
+            self._materialise()
+        return self._pts
+
+    @feature_pts.setter
+    def feature_pts(self, value):
+        if self._lazy is not None:
+            self._materialise()
+        self._pts = value
+
+    @property
+    def feature_des(self):
+        if self._lazy is not None:
+            self._materialise()
+        return self._des
+
+    @feature_des.setter
+    def feature_des(self, value):
+        if self._lazy is not None:
+            self._materialise()
+        self._des = value
+
     def get_feature_num(self):
-        return len(self.feature_pts)
+        return len(self._lazy[2]) if self._lazy is not None else len(self._pts)
 
     def convert_keypoint_to_array(self, norm=True):
         """key_frame.py:59-73."""

@@ -492,3 +492,35 @@ def test_folded_schur_reduce_bitwise_equals_separate_reduce(gpu_available, confi
         out.append(torch.as_tensor(bench._DevArray(sp, n), device="cuda:0").cpu().numpy().copy())
         h.close()
     assert np.array_equal(out[0], out[1]) and np.array_equal(out[1], out[2])
+
+
+@pytest.mark.parametrize("config,knob", [("config2", "PTZBA_CHOL_PERSIST=1"), ("grid", "PTZBA_CHOL_PERSIST=1"),
+                                         ("grid", "PTZBA_BS_PERSIST=0")])
+def test_single_launch_schedules_bitwise_equal(gpu_available, config, knob, monkeypatch):
+    """Schedule-only forms of the factorisation / back-substitution give bit-identical LM iterates: PTZBA_CHOL_PERSIST=1
+    -- every factorisation level in ONE launch (one workgroup per task by ticket, per-level completion counters,
+    coherent tile traffic: k_chol_pst) against the per-level launches; PTZBA_BS_PERSIST=0 -- the per-step blocked
+    back-substitution against the single-launch one (the default).  config 2 (natural / one-level plan) and the
+    3-row grid (delayed trailing updates: the second panel pair and 2 x 2 trailing blocks); 3 solves of 3 LM
+    iterations per handle, so the counters run over several epochs."""
+    import ptzba
+    import synthetic
+    if config == "grid":
+        p = synthetic.make_grid_problem(120, 6000, -20.0, 20.0, (-10.0, 0.0, 10.0), seed=3)
+    else:
+        p = synthetic.make_problem(config, seed=0)
+    name, val = knob.split("=")
+    out = []
+    for v in ("0" if val == "1" else "1", val):
+        monkeypatch.setenv(name, v)
+        h = ptzba.BAHandle(0)
+        h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=ptzba.FP64)
+        h.set_state(p.init_ptz, p.init_rays)
+        h.save_state()
+        rs = [h.solve_resident(restore=True, ftol=1e-14, xtol=1e-16, max_iter=3) for _ in range(3)]
+        out.append((h.get_state(), [(r.cost, r.njev, r.nfev, r.status) for r in rs]))
+        h.close()
+    (a_ptz, a_rays), a_res = out[0]
+    (b_ptz, b_rays), b_res = out[1]
+    assert a_res == b_res
+    assert np.array_equal(a_ptz, b_ptz) and np.array_equal(a_rays, b_rays)
