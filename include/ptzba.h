@@ -66,19 +66,21 @@ typedef struct {
     int32_t dist_rank;             /* this process's rank in [0, dist_world) */
 } ptzba_problem_opts;
 
-/* ---------------- multi-GPU: part-owned solve of the reduced camera system ----------------
- * The frame chain splits by one level of nested dissection into two parts A, B and the separator C that
- * holds every frame coupled across them.  ptzba_partition_landmarks assigns each landmark to a rank:
- * landmarks seeing a frame of A go to rank group 0 = ranks [0, (world+1)/2), those seeing B to group 1,
- * C-only landmarks by position; inside a group, contiguous landmark blocks of equal record counts.  A
- * rank then factors only its part's interior (A or B) plus C: the part's Schur update onto C is local,
- * and only the separator block (C x C, its right-hand side, g and diag U over C) is summed over all ranks
- * (exchange PTZBA_X_SEP); with more than one rank per group the part's interior is first summed inside
- * the group (PTZBA_X_PART).  Each rank back-substitutes C and its own part.  Frames outside its part and C
- * keep their values on a rank (ptzba_owned_frames tells which frames a rank's state holds).  With
- * dist_world >= 2 but no valid split (every frame couples to the last one), the
- * solve is REPLICATED: every rank factors the whole summed system (exchange PTZBA_X_SYS).  dist_world < 2:
- * a single-process problem.
+/* ---------------- multi-GPU: part-owned solve of the reduced camera system (rank tree) ----------------
+ * The frame chain splits by nested dissection (one level: A | C | B, or two: A1 | C1 | A2 | C2 | A3 | C3 | A4) into
+ * a separator tree.  The ranks are dealt over it: a node with R >= 2 ranks gives ceil(R / 2) to its lower-frame
+ * child and the rest to the other; a node reached with one rank is that rank's OWN subtree, a leaf reached with
+ * R >= 2 ranks is SHARED by them.  ptzba_partition_landmarks sends each landmark down the tree to the child whose
+ * frames it sees (separator-only landmarks to the nearer child), a shared leaf's landmarks in equal-record
+ * contiguous blocks.  A rank factors its base (own subtree or shared leaf) and then each ancestor separator up to
+ * the root, in phases; before each later phase the library sums that separator's columns (its tiles, g and diag U,
+ * b via the augmented row) over the node's rank group -- PTZBA_X_SUB for an inner separator, PTZBA_X_SEP for the
+ * root -- and a shared leaf's columns before the first phase (PTZBA_X_PART).  An update from one phase into a later
+ * phase's tile is applied by one member of the phase's group only, so the separators' Schur-complement work is split
+ * over the group and every contribution is summed exactly once.  Each rank back-substitutes its phases; frames
+ * outside them keep their values on a rank (ptzba_owned_frames).  With dist_world >= 2 but no valid split (every
+ * frame couples to the last one), the solve is REPLICATED: every rank factors the whole summed system (exchange
+ * PTZBA_X_SYS).  dist_world < 2: a single-process problem.
  * mode_out: 1 part-owned, 0 replicated; rank_of_landmark [n_landmark] (landmarks without records: -1);
  * split_out[3] (may be NULL) = (m, c_end, n_pose): A = [n_fixed, m), C = [m, c_end), B = [c_end, n_pose). */
 /* host only: the system order and factorisation plan ptzba_set_problem chooses for a coupling window
@@ -95,6 +97,17 @@ PTZBA_EXPORT int ptzba_plan_summary(int32_t n_pose, int32_t n_fixed, const int32
 PTZBA_EXPORT int ptzba_plan_export(int32_t n_pose, int32_t n_fixed, const int32_t* frame_win_hi, int32_t ordering,
                                    int32_t* pos_out, int32_t* tasks_out, int64_t tasks_cap, int32_t* level_off_out,
                                    int64_t levels_cap, int64_t* counts);
+/* host only: the rank-tree plan of rank `rank` in a part-owned solve of `world` ranks for a coupling window.  out16:
+ * [0] part-owned (0: replicated / none), [1] dissection levels of the order, [2] base node, [3] phases,
+ * [4] factorisation levels, [5] estimated factorisation us, [6] tasks, [7] most tasks in one level,
+ * [8] / [9] / [10] X_PART / X_SUB / X_SEP doubles per trial, [11] / [12] / [13] their group sizes, [14] n_aug,
+ * [15] blocked back-solve steps. */
+PTZBA_EXPORT int ptzba_dist_plan_summary(int32_t n_pose, int32_t n_fixed, const int32_t* frame_win_hi, int32_t world,
+                                         int32_t rank, int64_t* out16);
+/* host only: the phases of rank `rank` of `world` (n_out of them, 0 when the solve is replicated), out[5 k ..] =
+ * {exchange kind before the phase, group first rank, group size, first frame, end frame}; out may be NULL to count */
+PTZBA_EXPORT int ptzba_dist_rank_phases(int32_t n_pose, int32_t n_fixed, const int32_t* frame_win_hi, int32_t world,
+                                        int32_t rank, int32_t* out, int32_t cap, int32_t* n_out);
 PTZBA_EXPORT int ptzba_partition_landmarks(int32_t n_pose, int32_t n_landmark, int64_t n_obs, const int32_t* obs_frame,
                                            const int32_t* obs_landmark, int32_t n_fixed, int32_t world,
                                            int32_t* rank_of_landmark, int32_t* mode_out, int32_t* split_out);
@@ -226,15 +239,17 @@ PTZBA_EXPORT int ptzba_unpack(ptzba_handle h);
 /* ---------------- exchanges of a multi-GPU solve (done by the library) ----------------
  * Kinds (all are in-place SUMS over ranks of fp64 device buffers, on the handle's stream):
  *   PTZBA_X_SYS  replicated solve: the packed reduced system (all ranks);
- *   PTZBA_X_PART part-owned solve: the part's interior region, inside the rank group (group size > 1 only);
- *   PTZBA_X_SEP  part-owned solve: the separator region, all ranks (a group's non-leaders send zeros);
+ *   PTZBA_X_PART part-owned solve: a shared leaf's columns, inside the leaf's rank group;
+ *   PTZBA_X_SUB  part-owned solve: an inner separator's columns, inside its node's rank group;
+ *   PTZBA_X_SEP  part-owned solve: the root separator's columns, all ranks;
  *   PTZBA_X_SCAL partial LM scalars, all ranks (8 doubles replicated, 16 part-owned).
+ * ptzba_exchange_group tells the group [r0, r0 + nr) of a kind on this rank (a hook sums over exactly it).
  * With an exchange set, ptzba_linearize / ptzba_build_reduced / ptzba_solve_reduced / ptzba_lm_* /
  * ptzba_solve run them internally at the right points: the caller issues no collective.  Two ways:
  *   ptzba_attach_comm: the library's own RCCL communicator (ptzba_comm_new from an RCCL unique id);
  *   ptzba_set_exchange_hook: a callback (e.g. torch.distributed over gloo for single-device rehearsals).
  * Neither set: no exchange (single GPU, or the caller's own protocol through ptzba_exchange*). */
-enum { PTZBA_X_SYS = 0, PTZBA_X_PART = 1, PTZBA_X_SEP = 2, PTZBA_X_SCAL = 3 };
+enum { PTZBA_X_SYS = 0, PTZBA_X_PART = 1, PTZBA_X_SEP = 2, PTZBA_X_SCAL = 3, PTZBA_X_SUB = 4 };
 typedef int (*ptzba_exchange_fn)(void* ctx, int32_t kind, double* dev_buf, int64_t count, void* hip_stream);
 PTZBA_EXPORT int ptzba_set_exchange_hook(ptzba_handle h, ptzba_exchange_fn fn, void* ctx);
 /* library-owned RCCL communicator ("a handle per rank, created with an RCCL unique id").
@@ -251,13 +266,21 @@ PTZBA_EXPORT ptzba_comm ptzba_comm_split(ptzba_comm parent, int32_t color, int32
 PTZBA_EXPORT int ptzba_comm_info(ptzba_comm c, int32_t* rank, int32_t* world);
 /* in-place sum of count fp64 values of a device buffer on hip_stream (NULL: default stream) */
 PTZBA_EXPORT int ptzba_comm_allreduce(ptzba_comm c, double* dev_buf, int64_t count, void* hip_stream);
-/* the handle all-reduces through comm (not owned; NULL detaches).  A part-owned handle whose group has more
- * than one rank splits a group communicator off comm here (collective: every rank attaches). */
+/* the handle all-reduces through comm (not owned; NULL detaches).  A part-owned handle splits its rank groups'
+ * communicators off comm at its first exchange (collective: every rank of the solve reaches it). */
 PTZBA_EXPORT int ptzba_attach_comm(ptzba_handle h, ptzba_comm comm);
-/* [0] mode (1 part-owned, 0 replicated), [1] part (0 A, 1 B, -1 all), [2] group size, [3] group leader,
- * [4] separator exchange doubles, [5] part exchange doubles (0: none), [6] system exchange doubles
- * (replicated), [7] scalar exchange doubles */
+/* [0] mode (1 part-owned, 0 replicated), [1] base node of the rank tree (-1 replicated), [2] ranks sharing the
+ * base, [3] first rank of the base's group, [4] root-separator exchange doubles, [5] shared-leaf exchange doubles
+ * (0: none), [6] system exchange doubles (replicated), [7] scalar exchange doubles */
 PTZBA_EXPORT int ptzba_dist_info(ptzba_handle h, int64_t* info8);
+/* this rank's exchanges per LM trial, in order: out[4 k .. 4 k + 3] = {kind, group first rank, group size, doubles}
+ * (out may be NULL to count; cap = entries out holds) */
+PTZBA_EXPORT int ptzba_dist_exchanges(ptzba_handle h, int64_t* out, int32_t cap, int32_t* n_out);
+/* every rank group of the rank tree below the whole world, {first rank, size, tree depth} each (the same list on
+ * every rank: a hook creates its groups from it) */
+PTZBA_EXPORT int ptzba_dist_groups(ptzba_handle h, int32_t* out, int32_t cap, int32_t* n_out);
+/* the group {first rank, size} exchange `kind` runs over on this rank (the whole world for X_SEP / X_SCAL / X_SYS) */
+PTZBA_EXPORT int ptzba_exchange_group(ptzba_handle h, int32_t kind, int32_t* r0_nr);
 /* frames whose pose this rank's solve updates (its part and C; all frames when replicated): mask [n_pose] */
 PTZBA_EXPORT int ptzba_owned_frames(ptzba_handle h, uint8_t* mask_out);
 

@@ -95,7 +95,7 @@ struct ptzba_ctx {
   // single-launch factorisation (k_chol_pst): level of each task, tasks per level, per-level completion counters
   // [n_levels] + the ticket counter
   DBuf chol_lvl, chol_lvl_n, chol_lvl_cnt;
-  bool chol_pst = false;
+  bool chol_pst = false, chol_pst_ticket = true;
   uint32_t chol_epoch = 0;
   bool bs_pst = false;
   uint32_t bsp_epoch = 0;
@@ -128,18 +128,35 @@ struct ptzba_ctx {
 
   // multi-GPU (include/ptzba.h): exchanges done by the library, part-owned solve state
   ptzba_comm comm = nullptr;        // attached, not owned
-  ptzba_comm group_comm = nullptr;  // split off comm for a part-owned group of > 1 ranks (owned)
+  // communicators of the rank tree's groups, one per tree depth (split off comm at the first exchange; owned)
+  ptzba_comm group_comms[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool groups_split = false;
   ptzba_exchange_fn hook = nullptr;
   void* hook_ctx = nullptr;
   int dist_world = 1, dist_rank = 0;
   int dist_mode = 0;  // 1: part-owned solve
-  int part = -1, group_size = 1, group_leader = 1, phase2_level = 0;
-  DBuf row_phase, fmask;  // [n_aug] phase of each system row, [n_pose] bit 0 owned / bit 1 counted
+  // rank-tree phases (make_plan_tree): factorisation levels, the exchange before each phase (kind, rank group,
+  // tree depth of its communicator), exchanged tiles / vector ranges and their packing buffer
+  struct DistPhase {
+    int lv0 = 0, lv1 = 0, kind = 0, r0 = 0, nr = 1, depth = 0, node = -1, n_tiles = 0;
+    VecRanges vr{};
+    int64_t n_buf = 0;
+  };
+  static constexpr int MAX_PHASES = 4;
+  DistPhase ph[MAX_PHASES];
+  DBuf ph_tiles[MAX_PHASES], ph_buf[MAX_PHASES];
+  int n_phase = 0, base_node = -1, tree_depth = 0;
+  std::vector<int32_t> tree_groups;  // (r0, nr, depth) of every tree group of >= 2 ranks below the root
+  DBuf row_phase, fmask;  // [n_aug] phase + 1 of each system row (0: not this rank's), [n_pose] bit 0 owned / bit 1 counted
   std::vector<uint8_t> owned_host;
-  DBuf ptiles, stiles, pbuf, sbuf;  // part / separator exchange tile lists and buffers
-  int n_ptiles = 0, n_stiles = 0;
-  VecRanges pvr{}, svr{};
-  int64_t n_pbuf = 0, n_sbuf = 0;
+  void drop_groups() {
+    for (auto& c : group_comms)
+      if (c) {
+        ptzba_comm_delete(c);
+        c = nullptr;
+      }
+    groups_split = false;
+  }
 
   int elem() const { return precision == PTZBA_FP32 ? 4 : 8; }
   double* locp() const { return scal.as<double>() + 8; }
@@ -224,7 +241,7 @@ void ptzba_delete(ptzba_handle h) {
   if (h->scal_host) (void)hipHostFree(h->scal_host);
   if (h->bsp_err) (void)hipHostFree(h->bsp_err);
   if (h->stage) (void)hipHostFree(h->stage);
-  if (h->group_comm) ptzba_comm_delete(h->group_comm);
+  h->drop_groups();
   if (h->lm_host) (void)hipHostFree(h->lm_host);
   delete h;
 }
@@ -331,7 +348,7 @@ struct SysOrder {
   int split_m = 0, split_cend = 0;  // nested: A = [nf, m), C = [m, c_end), B = [c_end, n_pose)
   // separator tree of a nested order (tile-column ranges [t0, t1); parent -1 = the root separator): the
   // back-substitution chains are its root-to-leaf paths, the blocked back-solve's phases its depths
-  struct Node { int t0, t1, parent; };
+  struct Node { int t0, t1, parent, f0, f1; };  // (+ the node's frames [f0, f1))
   std::vector<Node> nodes;
   int nd_depth = 0;  // 0 natural, 1 = [A | B reversed | C], 2 = two dissection levels (nested_order2)
 };
@@ -399,7 +416,7 @@ static bool nested_order(int n_pose, int nf, const std::vector<int32_t>& win, Sy
   o.split_cend = cend;
   o.nd_depth = 1;
   const int c0 = o.tiles_a + o.tiles_b;
-  o.nodes = {{c0, o.n_aug / CHOL_NB, -1}, {0, o.tiles_a, 0}, {o.tiles_a, c0, 0}};
+  o.nodes = {{c0, o.n_aug / CHOL_NB, -1, m, cend}, {0, o.tiles_a, 0, nf, m}, {o.tiles_a, c0, 0, cend, n_pose}};
   return true;
 }
 
@@ -464,8 +481,8 @@ static bool nested_order2(int n_pose, int nf, const std::vector<int32_t>& win, S
   o.nd_depth = 2;
   if (halves) {
     // nodes: 0 = C2 (root), 1 = C1, 2 = C3, 3..6 = A1..A4 (part-owned fields: the halves and C2's frames)
-    o.nodes = {{t[6], t[7], -1}, {t[2], t[3], 0}, {t[5], t[6], 0},
-               {t[0], t[1], 1}, {t[1], t[2], 1}, {t[3], t[4], 2}, {t[4], t[5], 2}};
+    o.nodes = {{t[6], t[7], -1, bm, bc}, {t[2], t[3], 0, b1, bc1}, {t[5], t[6], 0, b3, bc3},
+               {t[0], t[1], 1, nf, b1}, {t[1], t[2], 1, bc1, bm}, {t[3], t[4], 2, bc, b3}, {t[4], t[5], 2, bc3, n_pose}};
     o.tiles_a = t[3];
     o.tiles_b = t[6] - t[3];
     o.split_m = bm;
@@ -473,17 +490,98 @@ static bool nested_order2(int n_pose, int nf, const std::vector<int32_t>& win, S
     return true;
   }
   // nodes: 0 = C2 (root), 1 = C1, 2 = C3, 3..6 = A1..A4
-  o.nodes = {{t[6], t[7], -1}, {t[4], t[5], 0}, {t[5], t[6], 0},
-             {t[0], t[1], 1}, {t[1], t[2], 1}, {t[2], t[3], 2}, {t[3], t[4], 2}};
+  o.nodes = {{t[6], t[7], -1, bm, bc}, {t[4], t[5], 0, b1, bc1}, {t[5], t[6], 0, b3, bc3},
+             {t[0], t[1], 1, nf, b1}, {t[1], t[2], 1, bc1, bm}, {t[2], t[3], 2, bc, b3}, {t[3], t[4], 2, bc3, n_pose}};
   return true;
 }
 
 // The split of a part-owned (multi-GPU) solve: nested_order's choice when it shortens the critical path,
 // else its most balanced split; false when none exists (every frame couples to the last one).  A pure
 // function of the coupling window, so ptzba_partition_landmarks and every rank's set_problem agree.
-static bool dist_order(int n_pose, int nf, const std::vector<int32_t>& win, SysOrder& o);  // after make_plan_part
-// rank groups of a part-owned solve: part 0 = ranks [0, g0), part 1 = [g0, world)
-static int dist_g0(int world) { return (world + 1) / 2; }
+static bool dist_order(int n_pose, int nf, const std::vector<int32_t>& win, int world, SysOrder& o);  // after make_plan_tree
+
+// Rank tree of a part-owned (multi-GPU) solve (round 4).  The separator tree of a nested order (one or two
+// dissection levels) with the world's ranks dealt over it: a node with R >= 2 ranks gives ceil(R / 2) of them to its
+// lower-frame child and the rest to the other; a node reached with one rank is that rank's OWN subtree; a leaf
+// reached with R >= 2 ranks is SHARED by them.  A rank's phases: its base (own subtree, or shared leaf), then each
+// ancestor separator up to the root.  Every subtree's tile columns and frames are contiguous in the orders used.
+struct DistTree {
+  struct N {
+    int t0, t1, parent, f0, f1;  // separator / leaf columns and frames (SysOrder::Node)
+    int st0, st1, sf0, sf1;      // the subtree's columns and frames
+    int child[2], nch, depth;
+    int r0, nr;                  // ranks [r0, r0 + nr) below this node
+  };
+  std::vector<N> n;
+  int depth = 0;  // deepest node
+};
+static bool dist_tree(const SysOrder& o, int world, DistTree& T) {
+  const int nn = (int)o.nodes.size();
+  if (nn < 3 || world < 2) return false;
+  T.n.assign(nn, DistTree::N{});
+  for (int v = 0; v < nn; ++v) {
+    const auto& a = o.nodes[v];
+    T.n[v] = DistTree::N{a.t0, a.t1, a.parent, a.f0, a.f1, a.t0, a.t1, a.f0, a.f1, {-1, -1}, 0, 0, 0, 0};
+  }
+  for (int v = 0; v < nn; ++v) {
+    const int p = T.n[v].parent;
+    if (p < 0) continue;
+    if (T.n[p].nch >= 2) return false;
+    T.n[p].child[T.n[p].nch++] = v;
+  }
+  T.depth = 0;
+  for (int v = 0; v < nn; ++v) {
+    for (int u = T.n[v].parent; u >= 0; u = T.n[u].parent) T.n[v].depth++;
+    T.depth = std::max(T.depth, T.n[v].depth);
+    for (int u = T.n[v].parent; u >= 0; u = T.n[u].parent) {  // extend the ancestors' subtree ranges
+      T.n[u].st0 = std::min(T.n[u].st0, T.n[v].t0);
+      T.n[u].st1 = std::max(T.n[u].st1, T.n[v].t1);
+      T.n[u].sf0 = std::min(T.n[u].sf0, T.n[v].f0);
+      T.n[u].sf1 = std::max(T.n[u].sf1, T.n[v].f1);
+    }
+  }
+  for (int v = 0; v < nn; ++v) {
+    auto& x = T.n[v];
+    if (x.nch == 1) return false;
+    if (x.nch == 2 && T.n[x.child[0]].sf0 > T.n[x.child[1]].sf0) std::swap(x.child[0], x.child[1]);
+  }
+  // contiguity of every subtree (columns and frames): the sum of its nodes' sizes fills its range
+  for (int v = 0; v < nn; ++v) {
+    int64_t cols = 0, frames = 0;
+    for (int u = 0; u < nn; ++u) {
+      bool in = false;
+      for (int w = u; w >= 0; w = T.n[w].parent) in = in || w == v;
+      if (in) { cols += T.n[u].t1 - T.n[u].t0; frames += T.n[u].f1 - T.n[u].f0; }
+    }
+    if (cols != T.n[v].st1 - T.n[v].st0 || frames != T.n[v].sf1 - T.n[v].sf0) return false;
+  }
+  std::vector<std::pair<int, std::pair<int, int>>> stack{{0, {0, world}}};
+  while (!stack.empty()) {
+    const int v = stack.back().first, r0 = stack.back().second.first, nr = stack.back().second.second;
+    stack.pop_back();
+    T.n[v].r0 = r0;
+    T.n[v].nr = nr;
+    if (T.n[v].nch == 2) {
+      const int k = nr >= 2 ? (nr + 1) / 2 : 1;
+      stack.push_back({T.n[v].child[0], {r0, k}});
+      stack.push_back({T.n[v].child[1], nr >= 2 ? std::make_pair(r0 + k, nr - k) : std::make_pair(r0, 1)});
+    }
+  }
+  return true;
+}
+// a rank's base node (own subtree: nr == 1; shared leaf: nr >= 2) and its ancestors, bottom-up
+static int dist_base(const DistTree& T, int rank, std::vector<int>* anc = nullptr) {
+  int v = 0;
+  while (T.n[v].nr >= 2 && T.n[v].nch == 2) {
+    const auto& c = T.n[T.n[v].child[0]];
+    v = (rank >= c.r0 && rank < c.r0 + c.nr) ? T.n[v].child[0] : T.n[v].child[1];
+  }
+  if (anc) {
+    anc->clear();
+    for (int u = T.n[v].parent; u >= 0; u = T.n[u].parent) anc->push_back(u);
+  }
+  return v;
+}
 
 struct CholPlan {
   std::vector<int32_t> tasks;  // int4 records
@@ -901,7 +999,6 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
   return true;
 }
 
-static int ensure_group_comm(ptzba_ctx* h);
 
 // estimated factorisation time of a plan: per level the longer of the pivot chain (~7 us) and its tasks in
 // rounds of the chip (~768 resident workgroups, ~6 us a round) -- fewer levels only pay when the extra fill
@@ -938,24 +1035,67 @@ static int choose_order_plan(int n_pose, int nf, const std::vector<int32_t>& win
   return 0;
 }
 
-// Part-owned plan (multi-GPU, api: ptzba_partition_landmarks): this rank factors the tile columns of its
-// part (A = [0, tiles_a) or B = [tiles_a, tiles_a + tiles_b)) in phase 1, then one flush level applies
-// the last part level's panels to the separator tiles, so that after phase 1 every update from the part
-// into C and into the augmented row has been applied; the separator exchange sums C over the ranks;
-// phase 2 factors C (and the augmented tile), identically on every rank.  Tasks, update rules and the
-// delayed-update scheme are make_plan's; only the column set and the phase boundary differ.
-struct PartPlan {
-  std::vector<int32_t> part_tiles;  // Schur-writable tiles of this rank (part + C rows / columns): group exchange
-  std::vector<int32_t> sep_tiles;   // separator block tiles (C x C incl. fill, augmented row over C)
-  int phase2_level = 0;
+// Rank-tree plan of a part-owned (multi-GPU) solve (api: ptzba_partition_landmarks, round 4).  A rank factors the
+// tile columns of its phases in order -- its base (own subtree, or shared leaf), then each ancestor separator, the
+// root's with the augmented column -- each phase closed by a flush level that applies its last panels to the later
+// phases' tiles.  Between phases the library sums the next phase's columns over that node's rank group (X_SUB for an
+// inner separator, X_SEP for the root; a shared leaf's columns before the first phase, X_PART), so a phase always
+// starts from the complete sums of its columns.  Exactly-once rule: an update from a phase's panels into a LATER
+// phase's tile is applied by one rank of the phase's group only -- tile (i, j) by group member (i + j) mod size --
+// and the later exchange sums the members' tiles; inside the phase every member applies everything (they all factor
+// the phase).  Each member's own Schur partials enter the sum once, as they are.  So the work on the separators'
+// Schur complements is split over the group, not replicated.  Tasks, update rules and the panel packing are
+// make_plan's (at most two columns per level, no delayed updates).
+struct TreePhase {
+  int lv0 = 0, lv1 = 0;      // factorisation levels [lv0, lv1) (incl. the closing flush level)
+  int kind = PTZBA_X_PART;   // exchange BEFORE this phase (phase 0: X_PART when shared; later: X_SUB / X_SEP)
+  int node = -1, r0 = 0, nr = 1, depth = 0;
+  int c0 = 0, c1 = 0;        // tile columns
+  std::vector<int32_t> xt;   // exchanged tiles (ti, tj) (phase 0: only when shared)
+  VecRanges vr{};            // exchanged vector ranges of [b | g | dU]
 };
-static bool make_plan_part(const SysOrder& o, int part, int n_pose, int nf, const std::vector<int32_t>& win, int64_t ld,
-                           CholPlan& P, PartPlan& Q) {
-  const int T = (int)(ld / CHOL_NB);
-  const int ta = o.tiles_a, tb = o.tiles_b, c0 = ta + tb;
-  const int p_lo = part == 0 ? 0 : ta, p_hi = part == 0 ? ta : c0;
-  auto own = [&](int t) { return (t >= p_lo && t < p_hi) || t >= c0; };
-  auto phase = [&](int t) { return (t >= p_lo && t < p_hi) ? 1 : (t >= c0 ? 2 : 0); };
+struct TreePlan {
+  std::vector<TreePhase> ph;
+  std::vector<int8_t> col_phase;  // [T] phase of each tile column, -1 not this rank's
+  int base = -1;
+};
+static int tile_owner(int i, int j, int nr) { return (i + j) % nr; }
+static bool make_plan_tree(const SysOrder& o, const DistTree& DT, int rank, int n_pose, int nf,
+                           const std::vector<int32_t>& win, int64_t ld, CholPlan& P, TreePlan& Q) {
+  const int T = (int)(ld / CHOL_NB), taug = o.n_aug / CHOL_NB;
+  std::vector<int> anc;
+  Q.base = dist_base(DT, rank, &anc);
+  const auto& bn = DT.n[Q.base];
+  const bool shared = bn.nr >= 2;
+  Q.ph.clear();
+  {
+    TreePhase p0;
+    p0.kind = PTZBA_X_PART;
+    p0.node = Q.base;
+    p0.r0 = shared ? bn.r0 : rank;
+    p0.nr = shared ? bn.nr : 1;
+    p0.depth = bn.depth;
+    p0.c0 = shared ? bn.t0 : bn.st0;
+    p0.c1 = shared ? bn.t1 : bn.st1;
+    Q.ph.push_back(p0);
+  }
+  for (int u : anc) {
+    TreePhase p;
+    p.kind = DT.n[u].parent < 0 ? PTZBA_X_SEP : PTZBA_X_SUB;
+    p.node = u;
+    p.r0 = DT.n[u].r0;
+    p.nr = DT.n[u].nr;
+    p.depth = DT.n[u].depth;
+    p.c0 = DT.n[u].t0;
+    p.c1 = DT.n[u].parent < 0 ? T : DT.n[u].t1;  // the root's phase takes the augmented column too
+    Q.ph.push_back(p);
+  }
+  const int NP = (int)Q.ph.size();
+  if (Q.ph.back().c1 != T || taug != T - 1) return false;
+  Q.col_phase.assign(T, -1);
+  for (int q = 0; q < NP; ++q)
+    for (int t = Q.ph[q].c0; t < Q.ph[q].c1; ++t) Q.col_phase[t] = (int8_t)q;
+  auto own = [&](int t) { return Q.col_phase[t] >= 0; };
   std::vector<std::vector<uint8_t>> nz(T, std::vector<uint8_t>(T, 0));
   auto mark = [&](int r, int c) {
     int ti = r / CHOL_NB, tj = c / CHOL_NB;
@@ -967,48 +1107,57 @@ static bool make_plan_part(const SysOrder& o, int part, int n_pose, int nf, cons
       const int p1 = o.pos[f1], p2 = o.pos[f2];
       mark(p2, p1); mark(p2 + 2, p1); mark(p2, p1 + 2); mark(p2 + 2, p1 + 2);
     }
-  Q.part_tiles.clear();
-  for (int i = 0; i < T; ++i)
-    for (int j = 0; j <= i; ++j)
-      if ((nz[i][j] || i == j) && own(i) && own(j)) { Q.part_tiles.push_back(i); Q.part_tiles.push_back(j); }
-  const int taug = o.n_aug / CHOL_NB;
+  if (shared)  // a shared leaf's columns as the Schur kernels write them (before fill), summed before phase 0
+    for (int j = Q.ph[0].c0; j < Q.ph[0].c1; ++j)
+      for (int i = j; i < T; ++i)
+        if ((nz[i][j] || i == j) && own(i)) { Q.ph[0].xt.push_back(i); Q.ph[0].xt.push_back(j); }
   for (int j = 0; j <= taug; ++j) nz[taug][j] = 1;
   for (int i = 0; i < T; ++i) nz[i][i] = 1;
-  for (int k = 0; k < T; ++k) {  // symbolic fill (global: the other part's fill lies outside this rank's tiles)
+  for (int k = 0; k < T; ++k) {  // symbolic fill (global)
     std::vector<int> R;
     for (int i = k + 1; i < T; ++i)
       if (nz[i][k]) R.push_back(i);
     for (size_t x = 0; x < R.size(); ++x)
       for (size_t y = 0; y <= x; ++y) nz[R[x]][R[y]] = 1;
   }
-  for (int i = p_lo; i < p_hi; ++i)  // the part is decoupled from the other part (nested_order's separator)
-    for (int j = 0; j < T; ++j)
-      if (nz[std::max(i, j)][std::min(i, j)] && !own(j)) return false;
-  // levels: the part's columns, a flush level, then C's columns (at most two columns per launch)
+  for (int k = 0; k < T; ++k)  // a column this rank eliminates couples only to rows it holds
+    if (own(k))
+      for (int i = k + 1; i < T; ++i)
+        if (nz[i][k] && !own(i)) return false;
+  // levels: each phase's columns, then its flush level (at most two columns per level)
   std::vector<int> level(T, -1), count;
   auto place = [&](int k, int L0) {
     int L = L0;
     for (int p = 0; p < k; ++p)
-      if (nz[k][p] && level[p] >= 0 && phase(p) == phase(k)) L = std::max(L, level[p] + 1);
+      if (nz[k][p] && level[p] >= 0 && Q.col_phase[p] == Q.col_phase[k]) L = std::max(L, level[p] + 1);
     while (L < (int)count.size() && count[L] >= 2) ++L;
     if (L >= (int)count.size()) count.resize(L + 1, 0);
     count[L]++;
     level[k] = L;
   };
-  for (int k = p_lo; k < p_hi; ++k) place(k, 0);
-  const int flush = (int)count.size();
-  count.push_back(0);
-  Q.phase2_level = flush + 1;
-  for (int k = c0; k < T; ++k) place(k, flush + 1);
+  for (int q = 0; q < NP; ++q) {
+    Q.ph[q].lv0 = (int)count.size();
+    for (int k = Q.ph[q].c0; k < Q.ph[q].c1; ++k) place(k, Q.ph[q].lv0);
+    if (q + 1 < NP) count.push_back(0);  // flush
+    Q.ph[q].lv1 = (int)count.size();
+  }
   P.ztiles.clear();
-  Q.sep_tiles.clear();
   for (int i = 0; i < T; ++i)
-    for (int j = 0; j <= i; ++j) {
-      if (!nz[i][j] || !own(i) || !own(j)) continue;
-      P.ztiles.push_back(i); P.ztiles.push_back(j);
-      if (j >= c0 && j < taug) { Q.sep_tiles.push_back(i); Q.sep_tiles.push_back(j); }
-    }
-  P.xtiles = Q.part_tiles;
+    for (int j = 0; j <= i; ++j)
+      if (nz[i][j] && own(i) && own(j)) { P.ztiles.push_back(i); P.ztiles.push_back(j); }
+  for (int q = 1; q < NP; ++q)  // an ancestor's columns (its rows and the later phases' rows, the augmented row)
+    for (int j = Q.ph[q].c0; j < std::min(Q.ph[q].c1, taug); ++j)
+      for (int i = j; i < T; ++i)
+        if (nz[i][j] && own(i)) { Q.ph[q].xt.push_back(i); Q.ph[q].xt.push_back(j); }
+  for (int q = 0; q < NP; ++q) {
+    const int64_t r0 = (int64_t)Q.ph[q].c0 * CHOL_NB, r1 = std::min<int64_t>((int64_t)Q.ph[q].c1 * CHOL_NB, o.n_aug);
+    const int64_t cnt = std::max<int64_t>(r1 - r0, 0);
+    if (q == 0)
+      Q.ph[q].vr = VecRanges{{r0, ld + r0, 2 * ld + r0}, {cnt, cnt, cnt}, 3};  // b | g | dU of the shared leaf
+    else
+      Q.ph[q].vr = VecRanges{{ld + r0, 2 * ld + r0, 0}, {cnt, cnt, 0}, 2};  // g | dU (b rides in the augmented row)
+  }
+  P.xtiles = Q.ph[0].xt;
   const int nL = (int)count.size();
   std::vector<std::vector<int>> K(nL);
   for (int k = 0; k < T; ++k)
@@ -1038,12 +1187,18 @@ static bool make_plan_part(const SysOrder& o, int part, int n_pose, int nf, cons
     }
     std::vector<std::pair<int64_t, int>> upd;
     for (int pp : prev) {
+      const auto& ph = Q.ph[Q.col_phase[pp]];
+      const int me = rank - ph.r0;
       std::vector<int> R;
       for (int i = pp + 1; i < T; ++i)
         if (nz[i][pp] && own(i)) R.push_back(i);
       for (size_t x = 0; x < R.size(); ++x)
-        for (size_t y = 0; y <= x; ++y)
-          if (level[R[y]] > L) upd.push_back({(int64_t)R[x] * T + R[y], pp});
+        for (size_t y = 0; y <= x; ++y) {
+          if (level[R[y]] <= L) continue;
+          // into a later phase's tile: this group's member tile_owner only (the exactly-once rule)
+          if (Q.col_phase[R[y]] != Q.col_phase[pp] && tile_owner(R[x], R[y], ph.nr) != me) continue;
+          upd.push_back({(int64_t)R[x] * T + R[y], pp});
+        }
     }
     std::sort(upd.begin(), upd.end());
     for (size_t x = 0; x < upd.size();) {
@@ -1060,12 +1215,13 @@ static bool make_plan_part(const SysOrder& o, int part, int n_pose, int nf, cons
     if (level[k] == nL - 1) P.tinv_tail.push_back(k);
   P.level_off[nL] = (int)(P.tasks.size() / 4);
   P.n_levels = nL;
-  // one back-substitution chain: C, then the part (as make_plan's nested chain of this part)
+  P.delayed = false;
+  // one back-substitution chain: the phases from the root down, each phase's columns descending
   const int Tx = n_inv;
   P.chain_off.assign(1, 0);
   P.chain_cols.clear();
-  for (int kt = Tx - 1; kt >= c0; --kt) P.chain_cols.push_back(kt);
-  for (int kt = p_hi - 1; kt >= p_lo; --kt) P.chain_cols.push_back(kt);
+  for (int q = NP - 1; q >= 0; --q)
+    for (int kt = std::min(Q.ph[q].c1, Tx) - 1; kt >= Q.ph[q].c0; --kt) P.chain_cols.push_back(kt);
   P.chain_off.push_back((int)P.chain_cols.size());
   std::vector<uint8_t> in_chain(T, 0);
   for (int kt : P.chain_cols) in_chain[kt] = 1;
@@ -1104,27 +1260,39 @@ static bool make_plan_part(const SysOrder& o, int part, int n_pose, int nf, cons
   return true;
 }
 
-// The two-level order with contiguous halves replaces it when the slower rank group's estimated factorisation
-// time is shorter (config 3 at N >= 2: a rank's chain of 31 levels becomes ~27); PTZBA_ND_DEPTH=1 keeps one level.
-static bool dist_order(int n_pose, int nf, const std::vector<int32_t>& win, SysOrder& o) {
+// The order of a part-owned solve: one dissection level (nested_order's choice when it shortens the critical path,
+// else its most balanced split) or the two-level order with contiguous halves, whichever gives the slowest rank the
+// shorter estimated factorisation (PTZBA_ND_DEPTH=1 keeps one level); false when the chain has no split.  A pure
+// function of the coupling window and the world size, so ptzba_partition_landmarks and every rank's set_problem agree.
+static bool dist_order(int n_pose, int nf, const std::vector<int32_t>& win, int world, SysOrder& o) {
   if (!(nested_order(n_pose, nf, win, o, false) || nested_order(n_pose, nf, win, o, true))) return false;
   if (getenv_is("PTZBA_ND_DEPTH", "1")) return true;
   SysOrder o2;
   if (!nested_order2(n_pose, nf, win, o2, true) || pad_tile(o2.n_aug + 1) > CHOL_MAX_LD) return true;
   double e[2] = {0, 0};
   const SysOrder* os[2] = {&o, &o2};
-  for (int v = 0; v < 2; ++v)
-    for (int part = 0; part < 2; ++part) {
+  for (int v = 0; v < 2; ++v) {
+    DistTree DT;
+    if (!dist_tree(*os[v], world, DT)) {
+      if (v == 0) return false;
+      return true;
+    }
+    for (int r = 0; r < world; ++r) {
+      // ranks sharing a base have the same plan shape: one per base
+      if (r > 0 && dist_base(DT, r) == dist_base(DT, r - 1)) continue;
       CholPlan P;
-      PartPlan Q;
-      if (!make_plan_part(*os[v], part, n_pose, nf, win, pad_tile(os[v]->n_aug + 1), P, Q)) {
-        if (getenv("PTZBA_PLAN_DEBUG")) fprintf(stderr, "dist_order: order %d part %d has no plan\n", v + 1, part);
+      TreePlan Q;
+      if (!make_plan_tree(*os[v], DT, r, n_pose, nf, win, pad_tile(os[v]->n_aug + 1), P, Q)) {
+        if (getenv("PTZBA_PLAN_DEBUG")) fprintf(stderr, "dist_order: order %d rank %d has no plan\n", v + 1, r);
+        if (v == 0) return false;
         return true;
       }
       e[v] = std::max(e[v], plan_est_us(P));
       if (getenv("PTZBA_PLAN_DEBUG"))
-        fprintf(stderr, "dist_order: order %d part %d levels %d est %.1f us\n", v + 1, part, P.n_levels, plan_est_us(P));
+        fprintf(stderr, "dist_order: order %d rank %d base %d phases %zu levels %d est %.1f us\n", v + 1, r, Q.base,
+                Q.ph.size(), P.n_levels, plan_est_us(P));
     }
+  }
   if (e[1] < e[0]) o = std::move(o2);
   return true;
 }
@@ -1441,7 +1609,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     return fail("bad rank %d of %d", o.dist_rank, o.dist_world);
   if (dist && !o.frame_win_hi) return fail("a sharded solve needs the global coupling window (frame_win_hi)");
   SysOrder sorder;
-  const bool part_mode = dist && dist_order(n_pose, o.n_fixed, win, sorder);
+  const bool part_mode = dist && dist_order(n_pose, o.n_fixed, win, o.dist_world, sorder);
   CholPlan plan;
   if (!part_mode && choose_order_plan(n_pose, o.n_fixed, win, o.ordering, sorder, plan))
     return fail("factorisation plan: an update task needs more than four panels");
@@ -1451,53 +1619,62 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->ld = pad_tile(h->n_aug + 1);  // + augmented rhs row
   // the back-substitution keeps x ([ld] doubles) in LDS
   if (h->ld > CHOL_MAX_LD) return fail("reduced system %d too large for the dense solver", h->n_sys);
-  PartPlan pplan;
+  TreePlan tplan;
   h->dist_world = dist ? o.dist_world : 1;
   h->dist_rank = dist ? o.dist_rank : 0;
   h->dist_mode = part_mode ? 1 : 0;
-  h->part = -1;
-  h->group_size = 1;
-  h->group_leader = 1;
+  h->n_phase = 0;
+  h->base_node = -1;
+  h->tree_depth = 0;
+  h->tree_groups.clear();
   std::vector<uint8_t> row_phase, fmask;
   h->owned_host.assign(n_pose, 1);
   if (part_mode) {
-    const int g0 = dist_g0(o.dist_world);
-    h->part = o.dist_rank < g0 ? 0 : 1;
-    h->group_size = h->part == 0 ? g0 : o.dist_world - g0;
-    h->group_leader = (o.dist_rank == 0 || o.dist_rank == g0) ? 1 : 0;
-    if (!make_plan_part(sorder, h->part, n_pose, o.n_fixed, win, h->ld, plan, pplan))
-      return fail("part-owned plan: the two parts are coupled (bad coupling window)");
-    h->phase2_level = pplan.phase2_level;
-    const int m = sorder.split_m, cend = sorder.split_cend;
-    auto owned = [&](int f) { return f >= o.n_fixed && (h->part == 0 ? f < cend : f >= m); };
+    DistTree DT;
+    if (!dist_tree(sorder, o.dist_world, DT) ||
+        !make_plan_tree(sorder, DT, o.dist_rank, n_pose, o.n_fixed, win, h->ld, plan, tplan))
+      return fail("part-owned plan: the parts are coupled (bad coupling window)");
+    if ((int)tplan.ph.size() > ptzba_ctx::MAX_PHASES) return fail("rank tree deeper than %d phases", ptzba_ctx::MAX_PHASES);
+    h->base_node = tplan.base;
+    h->tree_depth = DT.depth;
+    for (int v = 1; v < (int)DT.n.size(); ++v)
+      if (DT.n[v].nr >= 2 && (DT.n[v].nch == 2 || true)) {
+        bool dup = false;
+        for (size_t q = 0; q < h->tree_groups.size(); q += 3)
+          dup = dup || (h->tree_groups[q] == DT.n[v].r0 && h->tree_groups[q + 1] == DT.n[v].nr);
+        if (!dup) h->tree_groups.insert(h->tree_groups.end(), {DT.n[v].r0, DT.n[v].nr, DT.n[v].depth});
+      }
+    auto fphase = [&](int f) { return sorder.pos[f] < 0 ? -1 : (int)tplan.col_phase[sorder.pos[f] / CHOL_NB]; };
     for (int64_t r = 0; r < n_obs; ++r)
-      if (obs_frame[r] >= o.n_fixed && !owned(obs_frame[r]))
+      if (obs_frame[r] >= o.n_fixed && fphase(obs_frame[r]) < 0)
         return fail("record %lld sees frame %d outside rank %d's part (partition the landmarks with "
                     "ptzba_partition_landmarks)", (long long)r, obs_frame[r], o.dist_rank);
     fmask.assign(n_pose, 0);
     for (int f = 0; f < n_pose; ++f) {
-      h->owned_host[f] = owned(f) ? 1 : 0;
-      const bool in_c = f >= m && f < cend;
-      const bool counted = f < o.n_fixed ? o.dist_rank == 0 : (in_c ? o.dist_rank == 0 : (owned(f) && h->group_leader));
-      fmask[f] = (uint8_t)((owned(f) ? 1 : 0) | (counted ? 2 : 0));
+      const int q = f < o.n_fixed ? -1 : fphase(f);
+      const bool owned = q >= 0;
+      h->owned_host[f] = owned ? 1 : 0;
+      // each frame's pose partials counted by one rank: its phase group's first rank (fixed frames: rank 0)
+      const bool counted = f < o.n_fixed ? o.dist_rank == 0 : (owned && o.dist_rank == tplan.ph[q].r0);
+      fmask[f] = (uint8_t)((owned ? 1 : 0) | (counted ? 2 : 0));
     }
-    const int ta = sorder.tiles_a, tb = sorder.tiles_b, c0 = ta + tb;
-    const int p_lo = h->part == 0 ? 0 : ta, p_hi = h->part == 0 ? ta : c0;
     row_phase.assign(h->n_aug, 0);
-    for (int r = 0; r < h->n_aug; ++r) {
-      const int t = r / CHOL_NB;
-      row_phase[r] = (t >= p_lo && t < p_hi) ? 1 : (t >= c0 ? 2 : 0);
+    for (int r = 0; r < h->n_aug; ++r) row_phase[r] = (uint8_t)(tplan.col_phase[r / CHOL_NB] + 1);
+    h->n_phase = (int)tplan.ph.size();
+    for (int q = 0; q < h->n_phase; ++q) {
+      const auto& tp = tplan.ph[q];
+      auto& d = h->ph[q];
+      d.lv0 = tp.lv0;
+      d.lv1 = tp.lv1;
+      d.kind = tp.kind;
+      d.r0 = tp.r0;
+      d.nr = tp.nr;
+      d.depth = tp.depth;
+      d.node = tp.node;
+      d.n_tiles = (int)(tp.xt.size() / 2);
+      d.vr = tp.vr;
+      d.n_buf = (q == 0 && tp.nr < 2) ? 0 : (int64_t)d.n_tiles * CHOL_NB * CHOL_NB + tp.vr.count[0] + tp.vr.count[1] + tp.vr.count[2];
     }
-    h->n_ptiles = (int)(pplan.part_tiles.size() / 2);
-    h->n_stiles = (int)(pplan.sep_tiles.size() / 2);
-    const int64_t ld = h->ld, crow = (int64_t)c0 * CHOL_NB, ccnt = h->n_aug - crow;
-    h->pvr = VecRanges{{0, 0, 0}, {3 * ld, 0, 0}, 1};
-    h->svr = VecRanges{{ld + crow, 2 * ld + crow, 0}, {ccnt, ccnt, 0}, 2};
-    h->n_pbuf = (int64_t)h->n_ptiles * CHOL_NB * CHOL_NB + 3 * ld;
-    h->n_sbuf = (int64_t)h->n_stiles * CHOL_NB * CHOL_NB + 2 * ccnt;
-  } else {
-    h->n_ptiles = h->n_stiles = 0;
-    h->n_pbuf = h->n_sbuf = 0;
   }
   h->chol_task_off = plan.level_off;
   h->chol_tasks_host = plan.tasks;
@@ -1513,6 +1690,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   // ---- upload (staged: the stream has drained, so the staging buffer is free)
   HIPCHK(hipStreamSynchronize(h->st));
   h->stage_used = 0;
+  st_mark("pre-upload sync");
   std::vector<double> seg_base(2 * n_seg);
   for (int64_t s = 0; s < n_seg; ++s) {
     const int64_t r = order[seg_rec_begin[s]];
@@ -1569,15 +1747,17 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       upload_st(h, h->bs_la_tasks, plan.la_tasks) || upload_st(h, h->bs_lo_off, plan.lo_off) || upload_st(h, h->bs_lo_tiles, plan.lo_tiles))
     return -1;
   if (part_mode) {
-    if (upload_st(h, h->row_phase, row_phase) || upload_st(h, h->fmask, fmask) ||
-        upload_st(h, h->ptiles, pplan.part_tiles) || upload_st(h, h->stiles, pplan.sep_tiles) ||
-        h->pbuf.alloc((size_t)h->n_pbuf * 8) || h->sbuf.alloc((size_t)h->n_sbuf * 8))
-      return -1;
+    if (upload_st(h, h->row_phase, row_phase) || upload_st(h, h->fmask, fmask)) return -1;
+    for (int q = 0; q < h->n_phase; ++q)
+      if (upload_st(h, h->ph_tiles[q], tplan.ph[q].xt) || h->ph_buf[q].alloc((size_t)std::max<int64_t>(h->ph[q].n_buf, 1) * 8))
+        return -1;
   } else {
     h->row_phase.release();
     h->fmask.release();
-    h->pbuf.release();
-    h->sbuf.release();
+  }
+  for (int q = h->n_phase; q < ptzba_ctx::MAX_PHASES; ++q) {
+    h->ph_tiles[q].release();
+    h->ph_buf[q].release();
   }
   if (h->dpose.p) HIPCHK(hipMemsetAsync(h->dpose.p, 0, h->dpose.bytes, h->st));  // rows a part-owned rank never solves
   h->n_xtiles = (int)(plan.xtiles.size() / 2);
@@ -1608,7 +1788,9 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
               plan.bsb_tasks.size() / 12 <= 512;  // (2 workgroups per CU resident: 190 VGPRs)
   h->bsp_epoch = 0;
   // single-launch factorisation (PTZBA_CHOL_PERSIST=1, A/B knob): single-process SPD solves
-  h->chol_pst = !part_mode && !dist && getenv_is("PTZBA_CHOL_PERSIST", "1") && plan.n_levels > 0;
+  h->chol_pst = !part_mode && !dist && (getenv_is("PTZBA_CHOL_PERSIST", "1") || getenv_is("PTZBA_CHOL_PERSIST", "2")) &&
+                plan.n_levels > 0;
+  h->chol_pst_ticket = !getenv_is("PTZBA_CHOL_PERSIST", "2");
   h->chol_epoch = 0;
   if (h->chol_pst) {
     std::vector<int32_t> lvl(std::max(plan.level_off[plan.n_levels], 1), 0), lvl_n(plan.n_levels, 0);
@@ -1658,11 +1840,9 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->cur = 0;
   h->lambda = 0;
   HIPCHK(hipStreamSynchronize(h->st));  // every initialisation above has landed before the handle is used
+  st_mark("final sync");
   h->have_problem = true;
-  if (h->group_comm) {  // the group of the previous problem; split anew at the first exchange of this one
-    ptzba_comm_delete(h->group_comm);
-    h->group_comm = nullptr;
-  }
+  h->drop_groups();  // the groups of the previous problem; split anew at the first exchange of this one
   // no collective here: a rank whose set_problem failed validation above must not leave the others blocked in a
   // split.  The group communicator is split by the first exchange (ensure_group_comm), which every rank reaches.
   return 0;
@@ -1835,6 +2015,14 @@ int ptzba_get_state(ptzba_handle h, double* ptz, double* rays) {
 // exchanges of a multi-GPU solve (include/ptzba.h PTZBA_X_*): in-place sums on the handle's stream through
 // the attached RCCL communicator or the caller's hook
 // ------------------------------------------------------------------------------------------------
+static int ensure_group_comms(ptzba_ctx* h);
+// the tree depth of the group an exchange kind runs over on this rank (0: the whole world)
+static int exchange_depth(const ptzba_ctx* h, int kind) {
+  if (!h->dist_mode || kind == PTZBA_X_SEP || kind == PTZBA_X_SCAL || kind == PTZBA_X_SYS) return 0;
+  for (int q = 0; q < h->n_phase; ++q)
+    if (h->ph[q].kind == kind) return h->ph[q].depth;
+  return -1;
+}
 static int exchange(ptzba_ctx* h, int kind, double* buf, int64_t n) {
   if (h->hook) {
     if (h->hook(h->hook_ctx, kind, buf, n, (void*)h->st)) return fail("exchange hook failed (kind %d)", kind);
@@ -1843,23 +2031,31 @@ static int exchange(ptzba_ctx* h, int kind, double* buf, int64_t n) {
   if (h->comm) {
     // ncclCommSplit is collective over comm: done before this rank's first exchange of the problem, where every
     // rank of a sharded solve arrives in the same order
-    if (ensure_group_comm(h)) return fail("group communicator split failed");
-    ptzba_comm c = kind == PTZBA_X_PART ? h->group_comm : h->comm;
-    if (!c) return fail("part-owned group of %d ranks has no group communicator (ptzba_attach_comm)", h->group_size);
+    if (ensure_group_comms(h)) return fail("group communicator split failed");
+    const int d = exchange_depth(h, kind);
+    if (d < 0 || d >= 4) return fail("no rank group for exchange kind %d", kind);
+    ptzba_comm c = d == 0 ? h->comm : h->group_comms[d];
+    if (!c) return fail("part-owned exchange kind %d has no group communicator (ptzba_attach_comm)", kind);
     return ptzba_comm_allreduce(c, buf, n, (void*)h->st);
   }
   return 0;
 }
 static int64_t scal_count(const ptzba_ctx* h) { return h->dist_mode ? 2 * PTZBA_NSCALARS : PTZBA_NSCALARS; }
 
-// a part-owned group of more than one rank needs its own communicator (collective over comm)
-static int ensure_group_comm(ptzba_ctx* h) {
-  // ncclCommSplit is collective over ALL ranks of comm: with world >= 3 every rank splits (a rank alone in its
-  // group gets a one-rank communicator it never uses)
-  if (!h->comm || !h->have_problem || !h->dist_mode || h->dist_world < 3) return 0;
-  if (h->group_comm) return 0;
-  h->group_comm = ptzba_comm_split(h->comm, h->part, h->dist_rank);
-  return h->group_comm ? 0 : -1;
+// the rank tree's group communicators, one split per tree depth 1..depth (collective over ALL ranks of comm, in the
+// same order everywhere: a rank whose path does not reach that depth, or whose node there holds it alone, joins a
+// one-rank communicator it never uses)
+static int ensure_group_comms(ptzba_ctx* h) {
+  if (!h->comm || !h->have_problem || !h->dist_mode || h->groups_split) return 0;
+  for (int d = 1; d <= h->tree_depth && d < 4; ++d) {
+    int color = 1 << 20 | h->dist_rank;
+    for (int q = 0; q < h->n_phase; ++q)
+      if (h->ph[q].depth == d && h->ph[q].nr >= 2) color = h->ph[q].node;
+    h->group_comms[d] = ptzba_comm_split(h->comm, color, h->dist_rank);
+    if (!h->group_comms[d]) return -1;
+  }
+  h->groups_split = true;
+  return 0;
 }
 
 int ptzba_linearize(ptzba_handle h) {
@@ -1924,10 +2120,11 @@ static int build_impl(ptzba_ctx* h, double lambda, const double* lam_dev, const 
   HIPCHK(hipGetLastError());
   if (h->dist_mode) {
     if (!h->has_exchange()) return fail("a part-owned handle needs an exchange (ptzba_attach_comm / ptzba_set_exchange_hook)");
-    if (h->group_size > 1) {  // the part's interior (and C's partials) summed inside the rank group
-      launch_pack_region(h->S(), h->ld, h->ptiles.as<int2>(), h->n_ptiles, h->bvec(), h->pvr, h->pbuf.as<double>(), 0, h->st);
-      if (exchange(h, PTZBA_X_PART, h->pbuf.as<double>(), h->n_pbuf)) return -1;
-      launch_pack_region(h->S(), h->ld, h->ptiles.as<int2>(), h->n_ptiles, h->bvec(), h->pvr, h->pbuf.as<double>(), 1, h->st);
+    const auto& p0 = h->ph[0];
+    if (p0.nr > 1) {  // a shared leaf: its columns (and b | g | dU over its rows) summed inside the leaf's group
+      launch_pack_region(h->S(), h->ld, h->ph_tiles[0].as<int2>(), p0.n_tiles, h->bvec(), p0.vr, h->ph_buf[0].as<double>(), 0, h->st);
+      if (exchange(h, PTZBA_X_PART, h->ph_buf[0].as<double>(), p0.n_buf)) return -1;
+      launch_pack_region(h->S(), h->ld, h->ph_tiles[0].as<int2>(), p0.n_tiles, h->bvec(), p0.vr, h->ph_buf[0].as<double>(), 1, h->st);
       HIPCHK(hipGetLastError());
     }
   } else if (h->has_exchange()) {  // replicated: the packed reduced system summed over all ranks
@@ -1957,23 +2154,22 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
   tm_begin(h, TM_CHOL);
   const int4* th = reinterpret_cast<const int4*>(h->chol_tasks_host.data());
   if (h->dist_mode) {
-    // phase 1: the part's columns (+ flush of their updates into C); separator exchange; phase 2: C
-    launch_chol_prepare_damped(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(),
-                               h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
-                               h->lambda, lam_dev, h->st, h->row_phase.as<uint8_t>(), 1);
-    launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->phase2_level,
-                    h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>(), 0);
-    launch_pack_region(h->S(), h->ld, h->stiles.as<int2>(), h->n_stiles, h->bvec(), h->svr, h->sbuf.as<double>(),
-                       h->group_leader ? 0 : 2, h->st);
-    HIPCHK(hipGetLastError());
-    if (exchange(h, PTZBA_X_SEP, h->sbuf.as<double>(), h->n_sbuf)) return -1;
-    launch_pack_region(h->S(), h->ld, h->stiles.as<int2>(), h->n_stiles, h->bvec(), h->svr, h->sbuf.as<double>(), 1, h->st);
-    launch_chol_prepare_damped(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(),
-                               h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
-                               h->lambda, lam_dev, h->st, h->row_phase.as<uint8_t>(), 2);
-    launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
-                    h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>(),
-                    h->phase2_level);
+    // the rank's phases (make_plan_tree): before each later phase its columns are summed over its node's group
+    for (int q = 0; q < h->n_phase; ++q) {
+      const auto& d = h->ph[q];
+      if (q > 0) {
+        launch_pack_region(h->S(), h->ld, h->ph_tiles[q].as<int2>(), d.n_tiles, h->bvec(), d.vr, h->ph_buf[q].as<double>(), 0, h->st);
+        HIPCHK(hipGetLastError());
+        if (exchange(h, d.kind, h->ph_buf[q].as<double>(), d.n_buf)) return -1;
+        launch_pack_region(h->S(), h->ld, h->ph_tiles[q].as<int2>(), d.n_tiles, h->bvec(), d.vr, h->ph_buf[q].as<double>(), 1, h->st);
+      }
+      launch_chol_prepare_damped(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(),
+                                 h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
+                                 h->lambda, lam_dev, h->st, h->row_phase.as<uint8_t>(), q + 1);
+      launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), d.lv1, h->Ldiag.as<double>(),
+                      h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>(), d.lv0);
+      HIPCHK(hipGetLastError());
+    }
   } else {
     if (!(sel && h->fused_prep()))  // device-driven single-GPU builds wrote the augmented row, padding, damping
       launch_chol_prepare_damped(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(),
@@ -1982,7 +2178,8 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
     if (h->chol_pst)
       launch_cholesky_pst(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_lvl.as<int>(),
                           h->chol_lvl_n.as<int>(), h->chol_lvl_cnt.as<unsigned>(),
-                          h->chol_lvl_cnt.as<unsigned>() + h->chol_levels, h->chol_epoch++, 0, h->chol_levels,
+                          h->chol_pst_ticket ? h->chol_lvl_cnt.as<unsigned>() + h->chol_levels : nullptr,
+                          h->chol_epoch++, 0, h->chol_levels,
                           h->Ldiag.as<double>(), h->info.as<int>(), h->Minv.as<double>(), h->chol_delayed, h->bsp_err,
                           h->st);
     else
@@ -2345,10 +2542,7 @@ int ptzba_set_exchange_hook(ptzba_handle h, ptzba_exchange_fn fn, void* ctx) {
 
 int ptzba_attach_comm(ptzba_handle h, ptzba_comm comm) {
   if (!h) return fail("null handle");
-  if (h->group_comm) {
-    ptzba_comm_delete(h->group_comm);
-    h->group_comm = nullptr;
-  }
+  h->drop_groups();
   h->comm = comm;
   return 0;  // the group communicator is split lazily by the first exchange (collective, every rank reaches it)
 }
@@ -2357,16 +2551,63 @@ int ptzba_dist_info(ptzba_handle h, int64_t* info8) {
   if (!h || !h->have_problem) return fail("no problem set");
   if (!info8) return fail("null output");
   info8[0] = h->dist_mode;
-  info8[1] = h->part;
-  info8[2] = h->group_size;
-  info8[3] = h->group_leader;
-  info8[4] = h->n_sbuf;
-  info8[5] = h->dist_mode && h->group_size > 1 ? h->n_pbuf : 0;
+  info8[1] = h->dist_mode ? h->base_node : -1;
+  info8[2] = h->dist_mode ? h->ph[0].nr : 1;
+  info8[3] = h->dist_mode ? (h->dist_rank == h->ph[0].r0) : 1;
+  int64_t sep = 0, sub = 0;
+  for (int q = 1; q < h->n_phase; ++q) (h->ph[q].kind == PTZBA_X_SEP ? sep : sub) += h->ph[q].n_buf;
+  info8[4] = sep;
+  info8[5] = h->dist_mode && h->ph[0].nr > 1 ? h->ph[0].n_buf : 0;
   info8[6] = h->dist_mode || h->dist_world < 2 ? 0 : (int64_t)h->n_xtiles * CHOL_NB * CHOL_NB + 3 * h->ld;
   info8[7] = scal_count(h);
   return 0;
 }
 
+int ptzba_dist_exchanges(ptzba_handle h, int64_t* out, int32_t cap, int32_t* n_out) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  if (!n_out) return fail("null output");
+  std::vector<int64_t> v;
+  if (h->dist_mode) {
+    if (h->ph[0].nr > 1) v.insert(v.end(), {PTZBA_X_PART, h->ph[0].r0, h->ph[0].nr, h->ph[0].n_buf});
+    for (int q = 1; q < h->n_phase; ++q) v.insert(v.end(), {h->ph[q].kind, h->ph[q].r0, h->ph[q].nr, h->ph[q].n_buf});
+    v.insert(v.end(), {PTZBA_X_SCAL, 0, h->dist_world, scal_count(h)});
+  } else if (h->dist_world >= 2) {
+    v.insert(v.end(), {PTZBA_X_SYS, 0, h->dist_world, (int64_t)h->n_xtiles * CHOL_NB * CHOL_NB + 3 * h->ld});
+    v.insert(v.end(), {PTZBA_X_SCAL, 0, h->dist_world, scal_count(h)});
+  }
+  *n_out = (int32_t)(v.size() / 4);
+  if (out) {
+    if (cap < *n_out) return fail("output holds %d exchanges, %d needed", cap, *n_out);
+    std::copy(v.begin(), v.end(), out);
+  }
+  return 0;
+}
+int ptzba_dist_groups(ptzba_handle h, int32_t* out, int32_t cap, int32_t* n_out) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  if (!n_out) return fail("null output");
+  *n_out = (int32_t)(h->tree_groups.size() / 3);
+  if (out) {
+    if (cap < *n_out) return fail("output holds %d groups, %d needed", cap, *n_out);
+    std::copy(h->tree_groups.begin(), h->tree_groups.end(), out);
+  }
+  return 0;
+}
+int ptzba_exchange_group(ptzba_handle h, int32_t kind, int32_t* r0_nr) {
+  if (!h || !h->have_problem) return fail("no problem set");
+  if (!r0_nr) return fail("null output");
+  r0_nr[0] = 0;
+  r0_nr[1] = h->dist_world;
+  if (h->dist_mode && kind != PTZBA_X_SEP && kind != PTZBA_X_SCAL) {
+    for (int q = 0; q < h->n_phase; ++q)
+      if (h->ph[q].kind == kind && (q > 0 || h->ph[0].nr > 1)) {
+        r0_nr[0] = h->ph[q].r0;
+        r0_nr[1] = h->ph[q].nr;
+        return 0;
+      }
+    return fail("this rank runs no exchange of kind %d", kind);
+  }
+  return 0;
+}
 int ptzba_owned_frames(ptzba_handle h, uint8_t* mask_out) {
   if (!h || !h->have_problem) return fail("no problem set");
   if (!mask_out) return fail("null output");
@@ -2595,6 +2836,73 @@ int ptzba_plan_export(int32_t n_pose, int32_t n_fixed, const int32_t* frame_win_
   return 0;
 }
 
+// host only: the rank-tree plan set_problem builds for rank `rank` of `world` (tools/dist_predict.py, tests)
+int ptzba_dist_plan_summary(int32_t n_pose, int32_t n_fixed, const int32_t* frame_win_hi, int32_t world, int32_t rank,
+                            int64_t* out16) {
+  if (n_pose < 1 || n_fixed < 0 || n_fixed > n_pose || !frame_win_hi || !out16 || world < 1 || rank < 0 || rank >= world)
+    return fail("bad arguments");
+  std::vector<int32_t> win(frame_win_hi, frame_win_hi + n_pose);
+  for (int f = 0; f < n_pose; ++f)
+    if (win[f] < f || win[f] >= n_pose) return fail("frame_win_hi[%d] = %d out of range", f, win[f]);
+  std::fill(out16, out16 + 16, 0);
+  SysOrder o;
+  DistTree DT;
+  if (world < 2 || !dist_order(n_pose, n_fixed, win, world, o) || !dist_tree(o, world, DT)) return 0;
+  CholPlan P;
+  TreePlan Q;
+  const int64_t ld = pad_tile(o.n_aug + 1);
+  if (!make_plan_tree(o, DT, rank, n_pose, n_fixed, win, ld, P, Q)) return fail("no rank-tree plan");
+  out16[0] = 1;
+  out16[1] = o.nd_depth;
+  out16[2] = Q.base;
+  out16[3] = (int64_t)Q.ph.size();
+  out16[4] = P.n_levels;
+  out16[5] = (int64_t)plan_est_us(P);
+  out16[6] = P.level_off[P.n_levels];
+  int mx = 0;
+  for (int L = 0; L < P.n_levels; ++L) mx = std::max(mx, P.level_off[L + 1] - P.level_off[L]);
+  out16[7] = mx;
+  for (size_t q = 0; q < Q.ph.size(); ++q) {
+    const auto& t = Q.ph[q];
+    if (q == 0 && t.nr < 2) continue;
+    const int64_t n = (int64_t)(t.xt.size() / 2) * CHOL_NB * CHOL_NB + t.vr.count[0] + t.vr.count[1] + t.vr.count[2];
+    out16[t.kind == PTZBA_X_PART ? 8 : (t.kind == PTZBA_X_SUB ? 9 : 10)] += n;
+    out16[t.kind == PTZBA_X_PART ? 11 : (t.kind == PTZBA_X_SUB ? 12 : 13)] = t.nr;
+  }
+  out16[14] = o.n_aug;
+  out16[15] = (int64_t)P.bsb_step_off.size() - 1;
+  return 0;
+}
+
+// host only: the phases of rank `rank` (tests/numpy_handle.py NumpyTreeHandle emulates the protocol from them):
+// per phase {exchange kind before it, group first rank, group size, first frame, end frame}
+int ptzba_dist_rank_phases(int32_t n_pose, int32_t n_fixed, const int32_t* frame_win_hi, int32_t world, int32_t rank,
+                           int32_t* out, int32_t cap, int32_t* n_out) {
+  if (n_pose < 1 || n_fixed < 0 || n_fixed > n_pose || !frame_win_hi || !n_out || world < 2 || rank < 0 || rank >= world)
+    return fail("bad arguments");
+  std::vector<int32_t> win(frame_win_hi, frame_win_hi + n_pose);
+  for (int f = 0; f < n_pose; ++f)
+    if (win[f] < f || win[f] >= n_pose) return fail("frame_win_hi[%d] = %d out of range", f, win[f]);
+  SysOrder o;
+  DistTree DT;
+  *n_out = 0;
+  if (!dist_order(n_pose, n_fixed, win, world, o) || !dist_tree(o, world, DT)) return 0;
+  std::vector<int> anc;
+  const int base = dist_base(DT, rank, &anc);
+  const auto& bn = DT.n[base];
+  std::vector<int32_t> v;
+  if (bn.nr >= 2) v.insert(v.end(), {PTZBA_X_PART, bn.r0, bn.nr, bn.f0, bn.f1});
+  else v.insert(v.end(), {PTZBA_X_PART, rank, 1, bn.sf0, bn.sf1});
+  for (int u : anc)
+    v.insert(v.end(), {DT.n[u].parent < 0 ? PTZBA_X_SEP : PTZBA_X_SUB, DT.n[u].r0, DT.n[u].nr, DT.n[u].f0, DT.n[u].f1});
+  *n_out = (int32_t)(v.size() / 5);
+  if (out) {
+    if (cap < *n_out) return fail("output holds %d phases, %d needed", cap, *n_out);
+    std::copy(v.begin(), v.end(), out);
+  }
+  return 0;
+}
+
 int ptzba_partition_landmarks(int32_t n_pose, int32_t n_landmark, int64_t n_obs, const int32_t* obs_frame,
                               const int32_t* obs_landmark, int32_t n_fixed, int32_t world, int32_t* rank_of_landmark,
                               int32_t* mode_out, int32_t* split_out) {
@@ -2626,34 +2934,64 @@ int ptzba_partition_landmarks(int32_t n_pose, int32_t n_landmark, int64_t n_obs,
   };
   for (int l = 0; l < n_landmark; ++l) rank_of_landmark[l] = -1;
   SysOrder o;
-  const bool part = world >= 2 && dist_order(n_pose, n_fixed, win, o);
+  DistTree DT;
+  const bool part = world >= 2 && dist_order(n_pose, n_fixed, win, world, o) && dist_tree(o, world, DT);
   if (mode_out) *mode_out = part ? 1 : 0;
   if (split_out) {
     split_out[0] = part ? o.split_m : 0;
     split_out[1] = part ? o.split_cend : 0;
     split_out[2] = n_pose;
   }
-  std::vector<int32_t> ids[2];
   if (!part) {
+    std::vector<int32_t> ids;
     for (int l = 0; l < n_landmark; ++l)
-      if (cnt[l] > 0) ids[0].push_back(l);
-    blocks(ids[0], 0, world);
+      if (cnt[l] > 0) ids.push_back(l);
+    blocks(ids, 0, world);
     return 0;
   }
-  const int m = o.split_m, cend = o.split_cend;
+  // rank tree (make_plan_tree): from the root, a landmark goes to the child whose subtree frames it sees (no landmark
+  // sees both: the node's separator); one that sees only separator frames goes to the child nearer to it; a node
+  // with one rank keeps it; a shared leaf deals its landmarks out in equal-record contiguous blocks
+  // the tree nodes each landmark's (non-fixed) frames lie in, as a bit mask; per node the mask of its subtree
+  const int nn = (int)DT.n.size();
+  if (nn > 32) return fail("rank tree too large");
+  std::vector<int32_t> node_of(n_pose, -1);
+  for (int v = 0; v < nn; ++v)
+    for (int f = DT.n[v].f0; f < DT.n[v].f1; ++f) node_of[f] = v;
+  std::vector<uint32_t> lmask(std::max(n_landmark, 1), 0u), smask(nn, 0u);
+  for (int64_t r = 0; r < n_obs; ++r)
+    if (obs_frame[r] >= n_fixed && node_of[obs_frame[r]] >= 0) lmask[obs_landmark[r]] |= 1u << node_of[obs_frame[r]];
+  for (int v = 0; v < nn; ++v)
+    for (int u = v; u >= 0; u = DT.n[u].parent) smask[u] |= 1u << v;
+  std::vector<std::vector<int32_t>> leaf_ids(DT.n.size());
   for (int l = 0; l < n_landmark; ++l) {
     if (cnt[l] == 0) continue;
-    int g;
-    if (hi[l] < 0) g = 0;                                  // fixed frames only
-    else if (lo[l] < m) g = 0;                             // sees A
-    else if (hi[l] >= cend) g = 1;                         // sees B
-    else g = (lo[l] - m) < (cend - 1 - hi[l]) ? 0 : 1;     // C only: the nearer part
-    if (lo[l] < m && hi[l] >= cend) return fail("landmark %d couples both parts (bad split)", l);
-    ids[g].push_back(l);
+    int v = 0;
+    for (;;) {
+      const auto& x = DT.n[v];
+      if (x.nr == 1) {
+        rank_of_landmark[l] = x.r0;
+        break;
+      }
+      if (x.nch != 2) {
+        leaf_ids[v].push_back(l);
+        break;
+      }
+      int go;
+      if (hi[l] < 0) {
+        go = 0;  // fixed frames only
+      } else {
+        const bool in0 = (lmask[l] & smask[x.child[0]]) != 0, in1 = (lmask[l] & smask[x.child[1]]) != 0;
+        if (in0 && in1) return fail("landmark %d couples both parts (bad split)", l);
+        if (in0) go = 0;
+        else if (in1) go = 1;
+        else go = (lo[l] - x.f0) < (x.f1 - 1 - hi[l]) ? 0 : 1;  // separator frames only: the nearer part
+      }
+      v = x.child[go];
+    }
   }
-  const int g0 = dist_g0(world);
-  blocks(ids[0], 0, g0);
-  blocks(ids[1], g0, world - g0);
+  for (size_t v = 0; v < DT.n.size(); ++v)
+    if (!leaf_ids[v].empty()) blocks(leaf_ids[v], DT.n[v].r0, DT.n[v].nr);
   return 0;
 }
 

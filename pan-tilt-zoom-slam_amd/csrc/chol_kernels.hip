@@ -1165,8 +1165,11 @@ __global__ __launch_bounds__(256) void k_chol_pst(double* __restrict__ A, int64_
                                                   int* err) {
   __shared__ int s_t;
   if (threadIdx.x == 0) {
-    const int t = t0 + (int)(__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
-                             epoch * (unsigned)n);
+    // ticket == nullptr: the task of blockIdx.x (relies on workgroups being dispatched in index order; A/B knob --
+    // the waits are bounded either way)
+    const int t = ticket ? t0 + (int)(__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                                      epoch * (unsigned)n)
+                         : t0 + (int)blockIdx.x;
     s_t = t;
     const int L = task_lvl[t];
     if (L > L0) {
@@ -1204,27 +1207,25 @@ int launch_cholesky_pst(double* A, int64_t ld, const int4* tasks, const int* tas
   return 0;
 }
 
+template <typename TaskArg, bool COH>
+static void launch_chol_level(const TaskArg& ta, int n, double* A, int64_t ld, double* Ldiag, int* info, double* sgn,
+                              double* Minv, bool delayed, hipStream_t st) {
+  if (sgn)
+    hipLaunchKernelGGL((k_chol_step<true, TaskArg, false, false>), dim3(n), dim3(256), 0, st, A, ld, ta, Ldiag, info, sgn, Minv);
+  else if (delayed)
+    hipLaunchKernelGGL((k_chol_step<false, TaskArg, true, COH>), dim3(n), dim3(256), 0, st, A, ld, ta, Ldiag, info, sgn, Minv);
+  else
+    hipLaunchKernelGGL((k_chol_step<false, TaskArg, false, COH>), dim3(n), dim3(256), 0, st, A, ld, ta, Ldiag, info, sgn, Minv);
+}
 void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_off_host, int n_launch, double* Ldiag,
                      int* info, hipStream_t st, double* sgn, const int4* tasks_host, double* Minv, int first_level,
                      bool delayed) {
   static const bool by_value = !getenv("PTZBA_CHOL_TASKS_PTR");  // A/B knob
-  // diagnostic A/B knob: the level launches with the single-launch form's coherent tile traffic (what the L2 bypass
-  // costs by itself); read per call
+  // SPD factorisations write their tiles through (agent-scope stores) and read them past this XCD's L2: the next
+  // level's workgroups, mostly on other XCDs, find the tiles in the Infinity Cache at once (same-box A/B r04e:
+  // cholesky_solve 240 -> 232 us per trial at config 3).  PTZBA_CHOL_COH=0: plain accesses (A/B knob, read per call)
   const char* coh_env = getenv("PTZBA_CHOL_COH");
-  if (coh_env && atoi(coh_env) == 1 && !sgn && tasks_host && by_value) {
-    for (int L = first_level; L < n_launch; ++L) {
-      const int n = task_off_host[L + 1] - task_off_host[L];
-      if (n <= 0) continue;
-      CholTaskVal tv;
-      std::memcpy(tv.t, tasks_host + task_off_host[L], std::min(n, CHOL_KT) * sizeof(int4));
-      tv.rest = tasks + task_off_host[L] + CHOL_KT;
-      if (delayed)
-        hipLaunchKernelGGL((k_chol_step<false, CholTaskVal, true, true>), dim3(n), dim3(256), 0, st, A, ld, tv, Ldiag, info, sgn, Minv);
-      else
-        hipLaunchKernelGGL((k_chol_step<false, CholTaskVal, false, true>), dim3(n), dim3(256), 0, st, A, ld, tv, Ldiag, info, sgn, Minv);
-    }
-    return;
-  }
+  const bool coh = !(coh_env && atoi(coh_env) == 0);
   for (int L = first_level; L < n_launch; ++L) {
     const int n = task_off_host[L + 1] - task_off_host[L];
     if (n <= 0) continue;
@@ -1232,21 +1233,13 @@ void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_o
       CholTaskVal tv;
       std::memcpy(tv.t, tasks_host + task_off_host[L], std::min(n, CHOL_KT) * sizeof(int4));
       tv.rest = tasks + task_off_host[L] + CHOL_KT;
-      if (sgn)
-        hipLaunchKernelGGL((k_chol_step<true, CholTaskVal>), dim3(n), dim3(256), 0, st, A, ld, tv, Ldiag, info, sgn, Minv);
-      else if (delayed)
-        hipLaunchKernelGGL((k_chol_step<false, CholTaskVal, true>), dim3(n), dim3(256), 0, st, A, ld, tv, Ldiag, info, sgn, Minv);
-      else
-        hipLaunchKernelGGL((k_chol_step<false, CholTaskVal>), dim3(n), dim3(256), 0, st, A, ld, tv, Ldiag, info, sgn, Minv);
+      if (coh) launch_chol_level<CholTaskVal, true>(tv, n, A, ld, Ldiag, info, sgn, Minv, delayed, st);
+      else launch_chol_level<CholTaskVal, false>(tv, n, A, ld, Ldiag, info, sgn, Minv, delayed, st);
       continue;
     }
     const CholTaskPtr tp{tasks + task_off_host[L]};
-    if (sgn)
-      hipLaunchKernelGGL((k_chol_step<true, CholTaskPtr>), dim3(n), dim3(256), 0, st, A, ld, tp, Ldiag, info, sgn, Minv);
-    else if (delayed)
-      hipLaunchKernelGGL((k_chol_step<false, CholTaskPtr, true>), dim3(n), dim3(256), 0, st, A, ld, tp, Ldiag, info, sgn, Minv);
-    else
-      hipLaunchKernelGGL((k_chol_step<false, CholTaskPtr>), dim3(n), dim3(256), 0, st, A, ld, tp, Ldiag, info, sgn, Minv);
+    if (coh) launch_chol_level<CholTaskPtr, true>(tp, n, A, ld, Ldiag, info, sgn, Minv, delayed, st);
+    else launch_chol_level<CholTaskPtr, false>(tp, n, A, ld, Ldiag, info, sgn, Minv, delayed, st);
   }
 }
 

@@ -67,8 +67,8 @@ class ptzba_problem_opts(Structure):
 
 
 # exchange kinds of a multi-GPU solve (include/ptzba.h PTZBA_X_*)
-X_SYS, X_PART, X_SEP, X_SCAL = 0, 1, 2, 3
-X_NAMES = {X_SYS: "sys", X_PART: "part", X_SEP: "sep", X_SCAL: "scal"}
+X_SYS, X_PART, X_SEP, X_SCAL, X_SUB = 0, 1, 2, 3, 4
+X_NAMES = {X_SYS: "sys", X_PART: "part", X_SEP: "sep", X_SCAL: "scal", X_SUB: "sub"}
 UNIQUE_ID_BYTES = 128
 EXCHANGE_FN = ctypes.CFUNCTYPE(c_int32, c_void_p, c_int32, c_void_p, c_int64, c_void_p)
 
@@ -156,6 +156,11 @@ def lib():
         "ptzba_attach_comm": ([V, V], I),
         "ptzba_dist_info": ([V, V], I),
         "ptzba_owned_frames": ([V, V], I),
+        "ptzba_dist_exchanges": ([V, V, I32, POINTER(c_int32)], I),
+        "ptzba_dist_groups": ([V, V, I32, POINTER(c_int32)], I),
+        "ptzba_exchange_group": ([V, I32, V], I),
+        "ptzba_dist_plan_summary": ([I32, I32, V, I32, I32, V], I),
+        "ptzba_dist_rank_phases": ([I32, I32, V, I32, I32, V, I32, POINTER(c_int32)], I),
         "ptzekf_new": ([I], V),
         "ptzekf_delete": ([V], None),
         "ptzekf_num_rays": ([V], I),
@@ -190,7 +195,8 @@ EXPORTED_SYMBOLS = [
     "ptzba_partition_landmarks", "ptzba_set_exchange_hook", "ptzba_comm_unique_id", "ptzba_comm_new",
     "ptzba_comm_delete", "ptzba_comm_split", "ptzba_comm_info", "ptzba_comm_allreduce", "ptzba_attach_comm",
     "ptzba_dist_info", "ptzba_owned_frames", "ptz_corner_min_eig", "ptz_orb", "ptzba_plan_summary",
-    "ptzba_plan_export",
+    "ptzba_plan_export", "ptzba_dist_exchanges", "ptzba_dist_groups", "ptzba_exchange_group", "ptzba_dist_plan_summary",
+    "ptzba_dist_rank_phases",
 ]
 
 
@@ -601,6 +607,32 @@ def plan_export(frame_win_hi, n_fixed=1, ordering=None):
     return pos, tasks, off, int(c[2]), bool(c[3])
 
 
+def dist_plan_summary(frame_win_hi, world, rank, n_fixed=1):
+    """The rank-tree plan of `rank` in a part-owned solve of `world` ranks (ptzba_dist_plan_summary, host only):
+    dict(part_owned, nd_depth, base, phases, levels, est_us, tasks, max_level_tasks, x_part, x_sub, x_sep (doubles per
+    trial), part_group, sub_group, sep_group (group sizes), n_aug, bs_steps)."""
+    win = np.ascontiguousarray(frame_win_hi, np.int32)
+    out = np.zeros(16, np.int64)
+    _check(lib().ptzba_dist_plan_summary(len(win), int(n_fixed), _ptr(win), int(world), int(rank), _ptr(out)),
+           "ptzba_dist_plan_summary")
+    keys = ("part_owned", "nd_depth", "base", "phases", "levels", "est_us", "tasks", "max_level_tasks", "x_part", "x_sub",
+            "x_sep", "part_group", "sub_group", "sep_group", "n_aug", "bs_steps")
+    return {k: int(v) for k, v in zip(keys, out)}
+
+
+def dist_rank_phases(frame_win_hi, world, rank, n_fixed=1):
+    """Phases of `rank` in a part-owned solve of `world` ranks (ptzba_dist_rank_phases, host only): [(exchange kind
+    before the phase, group first rank, group size, first frame, end frame)]; [] when the solve is replicated."""
+    win = np.ascontiguousarray(frame_win_hi, np.int32)
+    n = c_int32(0)
+    _check(lib().ptzba_dist_rank_phases(len(win), int(n_fixed), _ptr(win), int(world), int(rank), None, 0,
+                                        ctypes.byref(n)), "ptzba_dist_rank_phases")
+    out = np.zeros((max(n.value, 1), 5), np.int32)
+    _check(lib().ptzba_dist_rank_phases(len(win), int(n_fixed), _ptr(win), int(world), int(rank), _ptr(out), n.value,
+                                        ctypes.byref(n)), "ptzba_dist_rank_phases")
+    return [tuple(int(x) for x in row) for row in out[:n.value]]
+
+
 def partition_landmarks(n_pose, n_landmark, frame, landmark, world, n_fixed=1):
     """Landmark -> rank of a sharded solve (ptzba_partition_landmarks, host only): returns (rank_of_landmark
     [n_landmark] int32 (-1: no records), mode (1 part-owned, 0 replicated), (m, c_end, n_pose) split)."""
@@ -613,6 +645,31 @@ def partition_landmarks(n_pose, n_landmark, frame, landmark, world, n_fixed=1):
                                            int(n_fixed), int(world), _ptr(out), ctypes.byref(mode), _ptr(split)),
            "ptzba_partition_landmarks")
     return out, int(mode.value), tuple(int(x) for x in split)
+
+
+class DevArray:
+    """__cuda_array_interface__ view of a device pointer owned by libptzba (fp64, for torch collectives)."""
+
+    def __init__(self, ptr, n):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<f8", "data": (ptr, False), "version": 3,
+                                         "strides": None}
+
+
+def torch_exchange_hook(h, dist, device):
+    """An exchange hook over torch.distributed for handle `h` (after set_problem with dist_world / dist_rank): the
+    rank tree's groups are created on every rank from h.dist_groups() (collective: all ranks call this in the same
+    order), and each exchange sums over the group h.exchange_group(kind) names.  For gloo rehearsals of several ranks
+    on one device; a real multi-GPU run attaches the library's own RCCL communicator instead (Comm, attach_comm)."""
+    import torch
+    world = dist.get_world_size()
+    groups = {(r0, nr): dist.new_group(list(range(r0, r0 + nr))) for r0, nr, _ in h.dist_groups()}
+
+    def hook(kind, ptr, count, stream):
+        r0, nr = h.exchange_group(kind)
+        t = torch.as_tensor(DevArray(ptr, count), device=device)
+        dist.all_reduce(t, group=None if nr == world else groups[(r0, nr)])
+
+    return hook
 
 
 class Comm:
@@ -752,9 +809,31 @@ class BAHandle:
     def dist_info(self):
         out = np.zeros(8, np.int64)
         _check(lib().ptzba_dist_info(self.h, _ptr(out)), "ptzba_dist_info")
-        return dict(mode="part-owned" if out[0] else "replicated", part=int(out[1]), group_size=int(out[2]),
+        return dict(mode="part-owned" if out[0] else "replicated", base=int(out[1]), group_size=int(out[2]),
                     group_leader=bool(out[3]), sep_doubles=int(out[4]), part_doubles=int(out[5]),
                     sys_doubles=int(out[6]), scal_doubles=int(out[7]))
+
+    def dist_exchanges(self):
+        """This rank's exchanges per LM trial: [(kind, group first rank, group size, doubles)]."""
+        n = c_int32(0)
+        _check(lib().ptzba_dist_exchanges(self.h, None, 0, ctypes.byref(n)), "ptzba_dist_exchanges")
+        out = np.zeros((max(n.value, 1), 4), np.int64)
+        _check(lib().ptzba_dist_exchanges(self.h, _ptr(out), n.value, ctypes.byref(n)), "ptzba_dist_exchanges")
+        return [tuple(int(x) for x in row) for row in out[:n.value]]
+
+    def dist_groups(self):
+        """Every rank group of the rank tree below the whole world: [(first rank, size, depth)] (same on all ranks)."""
+        n = c_int32(0)
+        _check(lib().ptzba_dist_groups(self.h, None, 0, ctypes.byref(n)), "ptzba_dist_groups")
+        out = np.zeros((max(n.value, 1), 3), np.int32)
+        _check(lib().ptzba_dist_groups(self.h, _ptr(out), n.value, ctypes.byref(n)), "ptzba_dist_groups")
+        return [tuple(int(x) for x in row) for row in out[:n.value]]
+
+    def exchange_group(self, kind):
+        """(first rank, size) of the group exchange `kind` sums over on this rank."""
+        out = np.zeros(2, np.int32)
+        _check(lib().ptzba_exchange_group(self.h, int(kind), _ptr(out)), "ptzba_exchange_group")
+        return int(out[0]), int(out[1])
 
     def owned_frames(self):
         out = np.zeros(self.n_pose, np.uint8)

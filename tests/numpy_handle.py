@@ -78,7 +78,11 @@ class NumpyBAHandle:
         S = np.zeros((nf, 3, nf, 3))
         for f in range(nf):
             S[f, :, f, :] += L['U'][fx + f]
-        S -= np.einsum('flik,gljk->figj', Y, Wf)
+        # S -= sum_lk Y[f,l,i,k] W[g,l,j,k], as one BLAS product (a plain einsum loops for seconds at 160 frames)
+        nl = Y.shape[1]
+        Ym = Y.transpose(0, 2, 1, 3).reshape(nf * 3, nl * 2)
+        Wm = Wf.transpose(0, 2, 1, 3).reshape(nf * 3, nl * 2)
+        S -= (Ym @ Wm.T).reshape(nf, 3, nf, 3)
         b = -L['gp'][fx:] + np.einsum('flik,lk->fi', Y, L['gl'])
         ns = 3 * nf
         self.sys[:ns * ns] = S.reshape(ns, ns).reshape(-1)
@@ -227,6 +231,11 @@ class NumpyPartHandle(NumpyBAHandle):
             info = 1
         dp[p] = np.linalg.solve(Lpp.T, yp - Lcp.T @ dp[c])
         self.info = info
+        self._finish_trial(dp, gpose, D, info)
+
+    def _finish_trial(self, dp, gpose, D, info):
+        L = self.cur
+        fx = self.n_fixed
         self.ptz_trial = self.ptz.copy()
         self.ptz_trial[fx:] += dp.reshape(-1, 3)
         t = L['gl'] + np.einsum('flij,fi->lj', L['W'][fx:], dp.reshape(-1, 3))
@@ -262,3 +271,85 @@ class NumpyPartHandle(NumpyBAHandle):
             self.ptz, self.rays = self.ptz_trial, self.rays_trial
             self.cur = self.trial
             self.scal[0] = self.cur['cost']
+
+
+class NumpyTreeHandle(NumpyPartHandle):
+    """The RANK-TREE protocol of libptzba (round 4: include/ptzba.h, api.hip make_plan_tree / solve_impl) in numpy.
+    The rank's phases come from the library's own plan (ptzba.dist_rank_phases: its base -- own subtree or shared
+    leaf -- then each ancestor separator up to the root, with each node's rank group).  Before a phase its columns
+    (the phase block, the later phases' rows against it, b, g and diag U over its rows) are summed over the phase's
+    group -- a shared leaf's before the first phase ('part'), an inner separator's ('sub'), the root's ('sep') --
+    then the phase is damped and eliminated, and its Schur update of the later phases is applied by ONE group member
+    per entry (frame pair (f_i + f_j) mod group size; b by (f_i + n_pose) mod size): the exactly-once rule, here per
+    frame block where the library splits per 32-row tile.  Back-substitution runs the phases from the root down.
+    `hook(kind, array, (r0, nr))` sums in place over ranks [r0, r0 + nr)."""
+
+    def set_dist(self, world, rank, phases, hook):
+        fx = self.n_fixed
+        self.rank, self.world, self.hook = rank, world, hook
+        self.phases = []
+        owned = np.zeros(self.n_pose, bool)
+        cnt = np.zeros(self.n_pose, bool)
+        for kind, r0, nr, f0, f1 in phases:
+            fr = np.arange(max(f0, fx), f1)
+            owned[fr] = True
+            if rank == r0:
+                cnt[fr] = True  # a phase's frames are counted by its group's first rank
+            self.phases.append((kind, r0, nr, fr - fx))
+        if rank == 0:
+            cnt[:fx] = True
+        self.owned, self.counted = owned, cnt
+        self.group_size = 1  # (no whole-system group sum in build_reduced: the phases sum their columns)
+        assert np.all(owned[self.frame[self.frame >= fx]]), "a record sees a frame outside this rank's phases"
+
+    def linearize(self):
+        super().linearize()
+
+    def _sum(self, kind, arr, grp):
+        self.hook(kind, arr, grp)
+
+    def solve_reduced(self):
+        import ptzba
+        ns = 3 * self.nf
+        fx, fx3 = self.n_fixed, 3 * self.n_fixed
+        S = self.sys[:ns * ns].reshape(ns, ns).copy()
+        b = self.sys[ns * ns:ns * ns + ns].copy()
+        gpose = self.sys[ns * ns + ns:ns * ns + 2 * ns].copy()
+        dU = self.sys[ns * ns + 2 * ns:].copy()
+        rows = lambda fr: (3 * fr[:, None] + np.arange(3)).reshape(-1)  # noqa: E731
+        P = [rows(ph[3]) for ph in self.phases]
+        D = self.D_pose[fx3:]
+        info = 0
+        elim = []
+        for q, (kind, r0, nr, _) in enumerate(self.phases):
+            p = P[q]
+            R = np.concatenate(P[q + 1:]) if q + 1 < len(P) else np.zeros(0, np.int64)
+            if q > 0 or nr > 1:  # the phase's columns summed over its group
+                k, m = len(p), len(R)
+                buf = np.concatenate([S[np.ix_(p, p)].reshape(-1), S[np.ix_(R, p)].reshape(-1), b[p], gpose[p], dU[p]])
+                self._sum(ptzba.X_NAMES[kind], buf, (r0, nr))
+                S[np.ix_(p, p)] = buf[:k * k].reshape(k, k)
+                S[np.ix_(R, p)] = buf[k * k:k * k + m * k].reshape(m, k)
+                S[np.ix_(p, R)] = S[np.ix_(R, p)].T
+                o = k * k + m * k
+                b[p], gpose[p], dU[p] = buf[o:o + k], buf[o + k:o + 2 * k], buf[o + 2 * k:]
+            D[p] = np.maximum(D[p], dU[p])
+            try:
+                Lq = np.linalg.cholesky(S[np.ix_(p, p)] + np.diag(self.lam * D[p]))
+                X = np.linalg.solve(Lq, S[np.ix_(R, p)].T).T
+                y = np.linalg.solve(Lq, b[p])
+            except np.linalg.LinAlgError:
+                info = 1
+                Lq, X, y = np.eye(len(p)), np.zeros((len(R), len(p))), np.zeros(len(p))
+            me = self.rank - r0
+            fR = R // 3 + fx
+            own = (fR[:, None] + fR[None, :]) % nr == me
+            ownb = (fR + self.n_pose) % nr == me
+            S[np.ix_(R, R)] -= np.where(own, X @ X.T, 0.0)
+            b[R] -= np.where(ownb, X @ y, 0.0)
+            elim.append((p, R, Lq, X, y))
+        dp = np.zeros(ns)
+        for p, R, Lq, X, y in reversed(elim):
+            dp[p] = np.linalg.solve(Lq.T, y - X.T @ dp[R])
+        self.info = info
+        self._finish_trial(dp, gpose, D, info)

@@ -199,3 +199,80 @@ def test_part_owned_solve_matches_single_rank(tmp_path, world):
         assert abs(float(o["cost"]) - res1.cost) <= 1e-10 * res1.cost
         assert int(o["njev"]) == res1.njev
     assert covered[1:].all()
+
+
+def _tree_problem():
+    import synthetic
+    return synthetic.make_small_problem(160, 1000, -100.0, 100.0, seed=1)  # 160 KF: a two-level rank tree
+
+
+def _tree_worker(rank, world, port, out_dir):
+    """One rank of the RANK-TREE solve (include/ptzba.h, round 4): landmarks from ptzba_partition_landmarks, the
+    rank's phases from the library's plan (ptzba.dist_rank_phases), each phase's columns summed over its node's
+    rank group before it, the exactly-once split of the later phases' updates -- numpy emulation over gloo."""
+    sys.path[:0] = [HERE, ROOT, os.path.join(ROOT, "pan-tilt-zoom-slam_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    import ptzba
+    from numpy_handle import NumpyTreeHandle
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    prob = _tree_problem()
+    win = ptzba.frame_coupling_window(prob.n_pose, prob.frame, prob.landmark)
+    owner, mode, _ = ptzba.partition_landmarks(prob.n_pose, prob.n_landmark, prob.frame, prob.landmark, world)
+    assert mode == 1
+    # every tree group, created on every rank in the same order (the phases of all ranks name them)
+    all_groups = sorted({(r0, nr) for r in range(world) for _, r0, nr, _, _ in ptzba.dist_rank_phases(win, world, r)
+                         if 1 < nr < world})
+    groups = {g: dist.new_group(list(range(g[0], g[0] + g[1]))) for g in all_groups}
+    phases = ptzba.dist_rank_phases(win, world, rank)
+    sel = owner[prob.landmark] == rank
+    kinds = []
+
+    def hook(kind, arr, grp=None):
+        kinds.append(kind)
+        g = None if grp is None or grp[1] == world else groups[grp]
+        dist.all_reduce(torch.from_numpy(arr), group=g)
+
+    h = NumpyTreeHandle()
+    h.set_problem(prob.n_pose, prob.n_landmark, prob.frame[sel], prob.landmark[sel], prob.xy[sel], prob.u, prob.v)
+    h.set_dist(world, rank, phases, hook)
+    h.set_state(prob.init_ptz, prob.init_rays)
+    res = ptzba.LMSolver(h, ftol=1e-9, xtol=1e-12, max_iter=6).run()
+    ptz, rays = h.get_state()
+    own_lm = np.zeros(prob.n_landmark, bool)
+    own_lm[prob.landmark[sel]] = True
+    np.savez(os.path.join(out_dir, f"tree{world}_rank{rank}.npz"), ptz=ptz, rays=rays, owned=h.owned, own_lm=own_lm,
+             cost=res.cost, njev=res.njev, n_rec=int(sel.sum()), kinds=np.array(sorted(set(kinds))),
+             phases=np.array(phases, np.int64))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4, 6])
+def test_rank_tree_solve_matches_single_rank(tmp_path, world):
+    """The rank-tree protocol (round 4) on a 160-keyframe chain whose order has two dissection levels: at 2 ranks
+    each owns a half (own subtree) and only the root separator is summed; at 4 each owns a leaf and the inner
+    separators are summed over pairs ('sub'); at 6 the first leaf of each half is shared by two ranks ('part').  With
+    the later phases' updates split over the group members (exactly once), the result equals the 1-rank solve:
+    same iterations and cost, every owned pose and every rank's rays within 1e-8, every frame owned."""
+    sys.path[:0] = [HERE, ROOT, os.path.join(ROOT, "pan-tilt-zoom-slam_amd")]
+    mp.start_processes(_tree_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    prob = _tree_problem()
+    res1, ptz1, rays1 = _solve(prob, prob.frame, prob.landmark, prob.xy, iters=6)
+    outs = [np.load(os.path.join(tmp_path, f"tree{world}_rank{r}.npz")) for r in range(world)]
+    assert sum(int(o["n_rec"]) for o in outs) == len(prob.frame)
+    covered = np.zeros(prob.n_pose, bool)
+    kinds = set()
+    for o in outs:
+        own = o["owned"]
+        covered |= own
+        kinds |= set(o["kinds"].tolist())
+        np.testing.assert_allclose(o["ptz"][own], ptz1[own], rtol=0, atol=1e-8)
+        np.testing.assert_allclose(o["rays"][o["own_lm"]], rays1[o["own_lm"]], rtol=0, atol=1e-8)
+        assert abs(float(o["cost"]) - res1.cost) <= 1e-10 * res1.cost
+        assert int(o["njev"]) == res1.njev
+    assert covered[1:].all()
+    want = {"sep", "scal"} | ({"sub"} if world >= 3 else set()) | ({"part"} if world >= 6 else set())
+    assert kinds == want, kinds

@@ -131,9 +131,6 @@ def _part_worker(rank, world, port, out_dir, config, precision, loss):
     import synthetic
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    g0 = (world + 1) // 2
-    groups = [dist.new_group(list(range(g0))), dist.new_group(list(range(g0, world)))]
-    mine = groups[0 if rank < g0 else 1]
     prob = _make(config)
     win_hi = ptzba.frame_coupling_window(prob.n_pose, prob.frame, prob.landmark)
     owner, mode, split = ptzba.partition_landmarks(prob.n_pose, prob.n_landmark, prob.frame, prob.landmark, world)
@@ -143,10 +140,11 @@ def _part_worker(rank, world, port, out_dir, config, precision, loss):
     h.set_problem(prob.n_pose, prob.n_landmark, prob.frame[sel], prob.landmark[sel], prob.xy[sel], prob.u, prob.v,
                   precision=precision, loss=loss, frame_win_hi=win_hi, dist_world=world, dist_rank=rank)
     kinds = []
+    inner = ptzba.torch_exchange_hook(h, dist, "cuda:0")
 
     def hook(kind, ptr, count, stream):
         kinds.append(kind)
-        dist.all_reduce(_dev_view(ptr, count, 0), group=mine if kind == ptzba.X_PART else None)
+        inner(kind, ptr, count, stream)
 
     h.set_exchange_hook(hook)
     h.set_state(prob.init_ptz, prob.init_rays)
@@ -156,7 +154,8 @@ def _part_worker(rank, world, port, out_dir, config, precision, loss):
     own_lm[prob.landmark[sel]] = True
     np.savez(os.path.join(out_dir, f"part_rank{rank}.npz"), ptz=ptz, rays=rays, owned=h.owned_frames(), own_lm=own_lm,
              cost=res.cost, njev=res.njev, status=res.status, n_rec=int(sel.sum()), mode=mode,
-             dist=np.array(list(h.dist_info().values())[1:], np.int64), kinds=np.array(sorted(set(kinds))))
+             dist=np.array(list(h.dist_info().values())[1:], np.int64), kinds=np.array(sorted(set(kinds))),
+             exchanges=np.array(h.dist_exchanges(), np.int64).reshape(-1, 4))
     h.close()
     dist.barrier()
     dist.destroy_process_group()
@@ -165,17 +164,20 @@ def _part_worker(rank, world, port, out_dir, config, precision, loss):
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("config,world,precision,loss,backsolve", [
     ("config2", 2, 0, 0, ""), ("config2", 4, 0, 0, ""), ("grid", 2, 0, 0, ""), ("grid", 4, 0, 0, ""),
-    ("grid", 2, 0, 0, "blk"), ("config3", 2, 0, 0, ""), ("config3", 2, 1, 1, ""), ("config4", 2, 1, 1, "")])
+    ("grid", 2, 0, 0, "blk"), ("config3", 2, 0, 0, ""), ("config3", 2, 1, 1, ""), ("config3", 3, 0, 0, ""),
+    ("config3", 4, 0, 0, ""), ("config3", 8, 0, 0, ""), ("config4", 2, 1, 1, ""), ("config4", 4, 1, 1, "")])
 def test_part_owned_gpu_solve_matches_single_rank(gpu_available, tmp_path, monkeypatch, config, world, precision, loss,
                                                   backsolve):
-    """libptzba's part-owned solve on one device (ranks over gloo): every rank factors its part (A or B) and the
-    separator C; only C (and, with 2 ranks per part, the part's interior inside its group) is exchanged.  The
-    result equals the single-rank solve of the whole problem: same iterations and status, the cost to 1e-9
-    relative, every rank's poses (its part and C) and rays within 1e-8 (fp64; fp32 records + Huber: 1e-6 deg /
-    1e-4 px -- the per-rank Schur sums round differently).  config 3 = the headline problem (A = frames 1-199,
-    C = 200-305, B = 306-499); grid / config 4 = keyframes on tilt rows (config 4: 410M records, A = 1-2185,
-    C = 2186-2803, B = 2804-4999; 3 LM iterations).  backsolve "blk": the blocked back substitution (config 4's
-    default) on the grid's one-chain part plans and on the single-rank nested plan."""
+    """libptzba's part-owned (rank-tree) solve on one device (ranks over gloo): every rank factors its base (own
+    subtree or shared leaf) and its ancestor separators, the separators' columns summed over each node's rank group
+    before their phase, updates into later phases applied by one group member each.  The result equals the
+    single-rank solve of the whole problem: same iterations and status, the cost to 1e-9 relative, every rank's
+    poses (its phases' frames) and rays within 1e-8 (fp64; fp32 records + Huber: 1e-6 deg / 1e-4 px -- the per-rank
+    Schur sums round differently).  config 3 = the headline problem in the two-level order: at 3 ranks ranks 0 / 1
+    own the first half's leaves (X_SUB over them) and rank 2 the second half, at 4 each rank owns a leaf, at 8 pairs
+    share the leaves (X_PART, X_SUB and X_SEP all run);
+    grid / config 4 = keyframes on tilt rows (config 4: 410M records, 3 LM iterations; at 4 ranks two per part).
+    backsolve "blk": the blocked back substitution on the grid's one-chain plans and on the single-rank plan."""
     import ptzba
     import synthetic
     if backsolve:
@@ -209,7 +211,8 @@ def test_part_owned_gpu_solve_matches_single_rank(gpu_available, tmp_path, monke
             assert rm[0] < 1e-6 and rm[1] < 1e-6 and rm[2] < 1e-4, rm
         kinds = set(o["kinds"].tolist())
         assert ptzba.X_SEP in kinds and ptzba.X_SCAL in kinds and ptzba.X_SYS not in kinds
-        assert (ptzba.X_PART in kinds) == (world > 2)
+        # exactly the exchanges the rank's plan lists (a shared leaf: X_PART; an inner separator: X_SUB)
+        assert kinds == {int(k) for k in o["exchanges"][:, 0]}, (kinds, o["exchanges"])
     assert covered[1:].all()
 
 

@@ -43,8 +43,10 @@ def main():
             ranks, owner, mode, split = [0], None, 0, None
         else:
             owner, mode, split = ptzba.partition_landmarks(prob.n_pose, prob.n_landmark, prob.frame, prob.landmark, world)
-            g0 = (world + 1) // 2
-            ranks = [0, g0] if a.ranks == "first" else list(range(world))
+            ranks = list(range(world))
+            if a.ranks == "first":  # one rank per base of the rank tree (ranks sharing a leaf run the same plan)
+                bases = [ptzba.dist_plan_summary(win, world, r)["base"] for r in ranks]
+                ranks = [r for r in ranks if r == 0 or bases[r] != bases[r - 1]]
         for rank in ranks:
             sel = np.ones(len(prob.frame), bool) if owner is None else owner[prob.landmark] == rank
             h = ptzba.BAHandle(0)
@@ -52,6 +54,8 @@ def main():
                           prob.v, precision=ptzba.FP32, loss=ptzba.LOSS_HUBER, frame_win_hi=win,
                           dist_world=world if world > 1 else 0, dist_rank=rank)
             xi = h.dist_info() if world > 1 else None
+            if xi is not None:
+                xi["exchanges"] = h.dist_exchanges()
             if world > 1:
                 h.set_exchange_hook(lambda kind, ptr, count, stream: None)
             h.set_state(prob.init_ptz, prob.init_rays)

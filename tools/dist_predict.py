@@ -44,10 +44,13 @@ def predict(recs):
             g = x.get("group_size", 1)
             terms = {}
             for links in (1, 7):
-                t = t_allreduce_us(8 * x.get("sep_doubles", 0), world, links) + \
-                    t_allreduce_us(8 * x.get("part_doubles", 0), g, links) + \
-                    t_allreduce_us(8 * x.get("scal_doubles", 0), world, links) + \
-                    t_allreduce_us(8 * x.get("sys_doubles", 0), world, links)
+                if "exchanges" in x:  # round 4: every collective of the rank's trial, (kind, r0, group size, doubles)
+                    t = sum(t_allreduce_us(8 * n, nr, links) for _, _, nr, n in x["exchanges"])
+                else:
+                    t = t_allreduce_us(8 * x.get("sep_doubles", 0), world, links) + \
+                        t_allreduce_us(8 * x.get("part_doubles", 0), g, links) + \
+                        t_allreduce_us(8 * x.get("scal_doubles", 0), world, links) + \
+                        t_allreduce_us(8 * x.get("sys_doubles", 0), world, links)
                 terms[links] = t / 1e3
             rows.append((r["wall_ms_per_trial"], terms, r))
         dev = max(t for t, _, _ in rows)
