@@ -276,21 +276,14 @@ def main():
         # unique id rank 0 makes and torch.distributed ships), or -- gloo rehearsals of several ranks on one
         # device -- through a hook over torch.distributed
         if backend == "gloo":
-            g0 = (world + 1) // 2
-            groups = [dist.new_group(list(range(g0))), dist.new_group(list(range(g0, world)))]
-            mine = groups[0 if rank < g0 else 1]
-
-            def hook(kind, ptr, count, strm):
-                t = torch.as_tensor(_DevArray(ptr, count), device=f"cuda:{local}")
-                dist.all_reduce(t, group=mine if kind == ptzba.X_PART else None)
-
-            h.set_exchange_hook(hook)
+            h.set_exchange_hook(ptzba.torch_exchange_hook(h, dist, f"cuda:{local}"))
         else:
             uid = [ptzba.Comm.unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
             comm = ptzba.Comm(uid[0], rank, world, device=local)
             h.attach_comm(comm)
         xinfo = h.dist_info()
+        xinfo["exchanges"] = h.dist_exchanges()  # (kind, group first rank, group size, doubles) per trial
         if xinfo["sys_doubles"] == 0 and xinfo["mode"] == "replicated":  # PTZBA_DIST_MODE=replicated (no dist opts)
             xinfo["sys_doubles"] = h.exchange_packed()[1]
 
