@@ -104,6 +104,14 @@ PTZBA_EXPORT int ptzba_plan_export(int32_t n_pose, int32_t n_fixed, const int32_
  * [15] blocked back-solve steps. */
 PTZBA_EXPORT int ptzba_dist_plan_summary(int32_t n_pose, int32_t n_fixed, const int32_t* frame_win_hi, int32_t world,
                                          int32_t rank, int64_t* out16);
+/* host only: rank `rank`'s whole rank-tree plan (CPU replay in the tests): pos_out [n_pose], tasks (int4 records),
+ * level offsets, phases_out [6 per phase] = {first level, end level, exchange kind, group first rank, group size,
+ * exchanged tiles}, xt_out = every phase's exchanged tiles (ti, tj) concatenated.  counts: [0] tasks, [1] levels,
+ * [2] n_aug, [3] phases, [4] exchanged tiles; null outputs only query the counts. */
+PTZBA_EXPORT int ptzba_dist_plan_export(int32_t n_pose, int32_t n_fixed, const int32_t* frame_win_hi, int32_t world,
+                                        int32_t rank, int32_t* pos_out, int32_t* tasks_out, int64_t tasks_cap,
+                                        int32_t* level_off_out, int64_t levels_cap, int32_t* phases_out,
+                                        int32_t phases_cap, int32_t* xt_out, int64_t xt_cap, int64_t* counts);
 /* host only: the phases of rank `rank` of `world` (n_out of them, 0 when the solve is replicated), out[5 k ..] =
  * {exchange kind before the phase, group first rank, group size, first frame, end frame}; out may be NULL to count */
 PTZBA_EXPORT int ptzba_dist_rank_phases(int32_t n_pose, int32_t n_fixed, const int32_t* frame_win_hi, int32_t world,

@@ -723,8 +723,19 @@ static void xcd_interleave(std::vector<int32_t>& tasks, int first_task) {
 
 // Tile structure (coupled frame pairs + the dense augmented row + symbolic fill), elimination levels
 // (at most two tile columns per level), tasks per level and back-substitution chains.
+// Rank-tree restriction of make_plan (make_plan_tree, §7): the tile columns this rank factors, phase by phase (each
+// phase's columns depend only on the same phase's; a flush level closes every phase but the last and is always a
+// trailing level, so it applies the phase's pending panels to the later phases' tiles), and the exactly-once rule:
+// an update from phase q's panels into a later phase's tile (i, j) is kept only by group member (i + j) mod size.
+struct TreeSpec {
+  std::vector<int8_t> col_phase;  // [T] phase of each tile column, -1 not this rank's
+  std::vector<int> ph_nr, ph_me;  // per phase: group size, this rank's index in the group
+  std::vector<int> chain;         // back-substitution chain (the phases from the root down, columns descending)
+  std::vector<int> ph_lv0, ph_lv1;  // out: per phase its levels [lv0, lv1) (the closing flush level included)
+};
+static int tile_owner(int i, int j, int nr) { return (i + j) % nr; }
 static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<int32_t>& win, int64_t ld, CholPlan& P,
-                      int force_dt = 0) {
+                      int force_dt = 0, TreeSpec* ts = nullptr) {
   const bool xcd_order = getenv_is("PTZBA_CHOL_XCD", "1");
   const int T = (int)(ld / CHOL_NB);
   std::vector<std::vector<uint8_t>> nz(T, std::vector<uint8_t>(T, 0));
@@ -752,23 +763,51 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
     for (size_t x = 0; x < R.size(); ++x)
       for (size_t y = 0; y <= x; ++y) nz[R[x]][R[y]] = 1;
   }
-  std::vector<int> level(T, 0), count;
-  for (int k = 0; k < T; ++k) {
-    int L = 0;
+  auto own = [&](int t) { return !ts || ts->col_phase[t] >= 0; };
+  auto phase = [&](int t) { return ts ? (int)ts->col_phase[t] : 0; };
+  if (ts)
+    for (int k = 0; k < T; ++k)  // a column this rank eliminates couples only to rows it holds
+      if (own(k))
+        for (int i = k + 1; i < T; ++i)
+          if (nz[i][k] && !own(i)) return false;
+  std::vector<int> level(T, ts ? -1 : 0), count;
+  std::vector<uint8_t> flush_lv;
+  auto place = [&](int k, int L0) {
+    int L = L0;
     for (int p = 0; p < k; ++p)
-      if (nz[k][p]) L = std::max(L, level[p] + 1);
+      if (nz[k][p] && level[p] >= 0 && phase(p) == phase(k)) L = std::max(L, level[p] + 1);
     while (L < (int)count.size() && count[L] >= 4) ++L;  // at most four columns per launch
     if (L >= (int)count.size()) count.resize(L + 1, 0);
     count[L]++;
     level[k] = L;
+  };
+  if (!ts) {
+    for (int k = 0; k < T; ++k) place(k, 0);
+  } else {
+    const int NP = (int)ts->ph_nr.size();
+    ts->ph_lv0.assign(NP, 0);
+    ts->ph_lv1.assign(NP, 0);
+    for (int q = 0; q < NP; ++q) {
+      ts->ph_lv0[q] = (int)count.size();
+      for (int k = 0; k < T; ++k)
+        if (phase(k) == q) place(k, ts->ph_lv0[q]);
+      if (q + 1 < NP) {
+        count.push_back(0);
+        flush_lv.resize(count.size(), 0);
+        flush_lv.back() = 1;
+      }
+      ts->ph_lv1[q] = (int)count.size();
+    }
   }
+  flush_lv.resize(count.size(), 0);
   P.ztiles.clear();
   for (int i = 0; i < T; ++i)
     for (int j = 0; j <= i; ++j)
-      if (nz[i][j]) { P.ztiles.push_back(i); P.ztiles.push_back(j); }
+      if (nz[i][j] && own(i) && own(j)) { P.ztiles.push_back(i); P.ztiles.push_back(j); }
   const int nL = (int)count.size();
   std::vector<std::vector<int>> K(nL);
-  for (int k = 0; k < T; ++k) K[level[k]].push_back(k);
+  for (int k = 0; k < T; ++k)
+    if (level[k] >= 0) K[level[k]].push_back(k);
   P.tasks.clear();
   P.level_off.assign(nL + 1, 0);
   auto push = [&](int type, int i, int j, int w) {
@@ -787,8 +826,9 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
   // their trailing tasks (config 4: ~1,600 per level), not when they are chain-bound (config 3).
   int64_t trail = 0;
   for (int p = 0; p < T; ++p) {
+    if (!own(p)) continue;
     int64_t r = 0;
-    for (int i = p + 1; i < T; ++i) r += nz[i][p];
+    for (int i = p + 1; i < T; ++i) r += nz[i][p] && own(i);
     trail += r * (r + 1) / 2;
   }
   int DT = trail > 600 * (int64_t)nL ? 2 : 1;
@@ -801,19 +841,23 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
     return std::make_pair(chol_pack_type(type, pd.size() > 2 ? pd[2] : -1, pd.size() > 3 ? pd[3] : -1, (tm >> 2) & 3),
                           chol_pack_updates(pd.size() > 0 ? pd[0] : -1, pd.size() > 1 ? pd[1] : -1, tm & 3));
   };
+  // trailing levels: every DT-th, and (rank-tree plans) every phase's flush level; a trailing level applies the
+  // panels of the levels since the previous trailing level, a panel task inline those since the last one before it
+  int last_trailing = 0;
   for (int L = 0; L < nL; ++L) {
     P.level_off[L] = (int)(P.tasks.size() / 4);
     const std::vector<int> none;
     const std::vector<int>& prev = L > 0 ? K[L - 1] : none;
+    const bool trailing = L % DT == 0 || flush_lv[L];
     std::vector<int> inl;  // panels applied inline by this level's panel tasks
     if (L > 0)
-      for (int l = ((L - 1) / DT) * DT; l < L; ++l) inl.insert(inl.end(), K[l].begin(), K[l].end());
+      for (int l = last_trailing; l < L; ++l) inl.insert(inl.end(), K[l].begin(), K[l].end());
     for (int k : K[L]) {
       std::vector<int> pd;
       for (int pp : inl)
         if (pp < k && nz[k][pp]) pd.push_back(pp);
       for (int i = k; i < T; ++i) {
-        if (!nz[i][k]) continue;
+        if (!nz[i][k] || !own(i)) continue;
         int tm = 0;
         for (size_t u = 0; u < pd.size(); ++u)
           if (i == k || nz[i][pd[u]]) tm |= 1 << u;
@@ -824,16 +868,23 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
     }
     // trailing updates from the panels of levels [L - DT, L - 1] into tiles of columns factored after L
     std::vector<std::pair<int64_t, int>> upd;  // (tile key, panel)
-    if (L % DT == 0)
-      for (int l = std::max(0, L - DT); l < L; ++l)
+    if (trailing && L > 0)
+      for (int l = last_trailing; l < L; ++l)
         for (int pp : K[l]) {
           std::vector<int> R;
           for (int i = pp + 1; i < T; ++i)
-            if (nz[i][pp]) R.push_back(i);
+            if (nz[i][pp] && own(i)) R.push_back(i);
           for (size_t x = 0; x < R.size(); ++x)
-            for (size_t y = 0; y <= x; ++y)
-              if (level[R[y]] > L) upd.push_back({(int64_t)R[x] * T + R[y], pp});
+            for (size_t y = 0; y <= x; ++y) {
+              if (level[R[y]] <= L) continue;
+              // rank tree: into a later phase's tile only by its owner in this phase's group (exactly once)
+              if (ts && phase(R[y]) != phase(pp) &&
+                  tile_owner(R[x], R[y], ts->ph_nr[phase(pp)]) != ts->ph_me[phase(pp)])
+                continue;
+              upd.push_back({(int64_t)R[x] * T + R[y], pp});
+            }
         }
+    if (trailing) last_trailing = L;
     std::sort(upd.begin(), upd.end());
     // per tile its panels (ascending); with delayed updates the tiles are grouped into 2 x 2 blocks
     // (rows 2a, 2a + 1 x columns 2b, 2b + 1): one type-3 task per block stages each panel's four row tiles
@@ -890,7 +941,7 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
     if (xcd_order) xcd_interleave(P.tasks, P.level_off[L]);  // PTZBA_CHOL_XCD=1 (read per plan)
   }
   for (int k = 0; k < n_inv && k < T; ++k)
-    if (!tinv_split || level[k] == nL - 1) P.tinv_tail.push_back(k);
+    if (own(k) && (!tinv_split || level[k] == nL - 1)) P.tinv_tail.push_back(k);
   P.level_off[nL] = (int)(P.tasks.size() / 4);
   P.n_levels = nL;
   if (getenv("PTZBA_PLAN_DEBUG")) {  // per level: columns, tasks (panel / trailing / inverse)
@@ -903,7 +954,7 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
     }
     fprintf(stderr, "max panels per task %zu\n", max_pd);
   }
-  if (max_pd > 4) return DT > 1 ? make_plan(o, n_pose, nf, win, ld, P, 1) : false;  // too many panels: DT = 1
+  if (max_pd > 4) return DT > 1 ? make_plan(o, n_pose, nf, win, ld, P, 1, ts) : false;  // too many panels: DT = 1
   if (max_pd > 2 || any_block) P.delayed = true;  // the P2 kernel (second panel pair, trailing blocks) also at DT = 1
   // back-substitution: chains of tile columns holding unknowns and, per chain position, the chain's
   // later columns coupled to that row tile (right-looking updates).  Nested orders: one chain per leaf of
@@ -912,7 +963,11 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
   P.chain_off.assign(1, 0);
   P.chain_cols.clear();
   BsPhases phases;
-  if (o.nested && !o.nodes.empty()) {
+  if (ts) {  // rank tree: one chain, the phases from the root down
+    P.chain_cols = ts->chain;
+    P.chain_off.push_back((int)P.chain_cols.size());
+    phases.push_back({P.chain_cols});
+  } else if (o.nested && !o.nodes.empty()) {
     const int nn = (int)o.nodes.size();
     std::vector<int> depth(nn, 0), nchild(nn, 0);
     for (int v = 0; v < nn; ++v) {
@@ -1059,7 +1114,6 @@ struct TreePlan {
   std::vector<int8_t> col_phase;  // [T] phase of each tile column, -1 not this rank's
   int base = -1;
 };
-static int tile_owner(int i, int j, int nr) { return (i + j) % nr; }
 static bool make_plan_tree(const SysOrder& o, const DistTree& DT, int rank, int n_pose, int nf,
                            const std::vector<int32_t>& win, int64_t ld, CholPlan& P, TreePlan& Q) {
   const int T = (int)(ld / CHOL_NB), taug = o.n_aug / CHOL_NB;
@@ -1120,31 +1174,6 @@ static bool make_plan_tree(const SysOrder& o, const DistTree& DT, int rank, int 
     for (size_t x = 0; x < R.size(); ++x)
       for (size_t y = 0; y <= x; ++y) nz[R[x]][R[y]] = 1;
   }
-  for (int k = 0; k < T; ++k)  // a column this rank eliminates couples only to rows it holds
-    if (own(k))
-      for (int i = k + 1; i < T; ++i)
-        if (nz[i][k] && !own(i)) return false;
-  // levels: each phase's columns, then its flush level (at most two columns per level)
-  std::vector<int> level(T, -1), count;
-  auto place = [&](int k, int L0) {
-    int L = L0;
-    for (int p = 0; p < k; ++p)
-      if (nz[k][p] && level[p] >= 0 && Q.col_phase[p] == Q.col_phase[k]) L = std::max(L, level[p] + 1);
-    while (L < (int)count.size() && count[L] >= 2) ++L;
-    if (L >= (int)count.size()) count.resize(L + 1, 0);
-    count[L]++;
-    level[k] = L;
-  };
-  for (int q = 0; q < NP; ++q) {
-    Q.ph[q].lv0 = (int)count.size();
-    for (int k = Q.ph[q].c0; k < Q.ph[q].c1; ++k) place(k, Q.ph[q].lv0);
-    if (q + 1 < NP) count.push_back(0);  // flush
-    Q.ph[q].lv1 = (int)count.size();
-  }
-  P.ztiles.clear();
-  for (int i = 0; i < T; ++i)
-    for (int j = 0; j <= i; ++j)
-      if (nz[i][j] && own(i) && own(j)) { P.ztiles.push_back(i); P.ztiles.push_back(j); }
   for (int q = 1; q < NP; ++q)  // an ancestor's columns (its rows and the later phases' rows, the augmented row)
     for (int j = Q.ph[q].c0; j < std::min(Q.ph[q].c1, taug); ++j)
       for (int i = j; i < T; ++i)
@@ -1157,106 +1186,23 @@ static bool make_plan_tree(const SysOrder& o, const DistTree& DT, int rank, int 
     else
       Q.ph[q].vr = VecRanges{{ld + r0, 2 * ld + r0, 0}, {cnt, cnt, 0}, 2};  // g | dU (b rides in the augmented row)
   }
-  P.xtiles = Q.ph[0].xt;
-  const int nL = (int)count.size();
-  std::vector<std::vector<int>> K(nL);
-  for (int k = 0; k < T; ++k)
-    if (level[k] >= 0) K[level[k]].push_back(k);
-  P.tasks.clear();
-  P.level_off.assign(nL + 1, 0);
-  auto push = [&](int type, int i, int j, int w) {
-    P.tasks.push_back(type); P.tasks.push_back(i); P.tasks.push_back(j); P.tasks.push_back(w);
-  };
+  // the factorisation tasks: make_plan restricted to this rank's phases (delayed trailing updates and 2 x 2
+  // trailing blocks included), the exactly-once rule on the later phases' tiles
+  TreeSpec ts;
+  ts.col_phase = Q.col_phase;
+  for (const auto& ph : Q.ph) {
+    ts.ph_nr.push_back(ph.nr);
+    ts.ph_me.push_back(rank - ph.r0);
+  }
   const int n_inv = (o.n_aug + CHOL_NB - 1) / CHOL_NB;
-  P.tinv_tail.clear();
-  for (int L = 0; L < nL; ++L) {
-    P.level_off[L] = (int)(P.tasks.size() / 4);
-    const std::vector<int> none;
-    const std::vector<int>& prev = L > 0 ? K[L - 1] : none;
-    for (int k : K[L]) {
-      std::vector<int> pd;
-      for (int pp : prev)
-        if (pp < k && nz[k][pp]) pd.push_back(pp);
-      for (int i = k; i < T; ++i) {
-        if (!nz[i][k] || !own(i)) continue;
-        int tm = 0;
-        for (size_t u = 0; u < pd.size(); ++u)
-          if (i == k || nz[i][pd[u]]) tm |= 1 << u;
-        push(0, i, k, chol_pack_updates(pd.size() > 0 ? pd[0] : -1, pd.size() > 1 ? pd[1] : -1, tm));
-      }
-    }
-    std::vector<std::pair<int64_t, int>> upd;
-    for (int pp : prev) {
-      const auto& ph = Q.ph[Q.col_phase[pp]];
-      const int me = rank - ph.r0;
-      std::vector<int> R;
-      for (int i = pp + 1; i < T; ++i)
-        if (nz[i][pp] && own(i)) R.push_back(i);
-      for (size_t x = 0; x < R.size(); ++x)
-        for (size_t y = 0; y <= x; ++y) {
-          if (level[R[y]] <= L) continue;
-          // into a later phase's tile: this group's member tile_owner only (the exactly-once rule)
-          if (Q.col_phase[R[y]] != Q.col_phase[pp] && tile_owner(R[x], R[y], ph.nr) != me) continue;
-          upd.push_back({(int64_t)R[x] * T + R[y], pp});
-        }
-    }
-    std::sort(upd.begin(), upd.end());
-    for (size_t x = 0; x < upd.size();) {
-      size_t y = x + 1;
-      while (y < upd.size() && upd[y].first == upd[x].first) ++y;
-      const int i = (int)(upd[x].first / T), j = (int)(upd[x].first % T);
-      push(1, i, j, chol_pack_updates(upd[x].second, y - x > 1 ? upd[x + 1].second : -1, 3));
-      x = y;
-    }
-    for (int pp : prev)
-      if (pp < n_inv) push(2, pp, pp, 0);
-  }
-  for (int k = 0; k < n_inv && k < T; ++k)
-    if (level[k] == nL - 1) P.tinv_tail.push_back(k);
-  P.level_off[nL] = (int)(P.tasks.size() / 4);
-  P.n_levels = nL;
-  P.delayed = false;
-  // one back-substitution chain: the phases from the root down, each phase's columns descending
-  const int Tx = n_inv;
-  P.chain_off.assign(1, 0);
-  P.chain_cols.clear();
   for (int q = NP - 1; q >= 0; --q)
-    for (int kt = std::min(Q.ph[q].c1, Tx) - 1; kt >= Q.ph[q].c0; --kt) P.chain_cols.push_back(kt);
-  P.chain_off.push_back((int)P.chain_cols.size());
-  std::vector<uint8_t> in_chain(T, 0);
-  for (int kt : P.chain_cols) in_chain[kt] = 1;
-  P.upd_off.assign(1, 0);
-  P.upd_tiles.clear();
-  for (int kt : P.chain_cols) {
-    for (int j = 0; j < kt; ++j)
-      if (in_chain[j] && nz[kt][j]) P.upd_tiles.push_back(j);
-    P.upd_off.push_back((int)P.upd_tiles.size());
+    for (int kt = std::min(Q.ph[q].c1, n_inv) - 1; kt >= Q.ph[q].c0; --kt) ts.chain.push_back(kt);
+  if (!make_plan(o, n_pose, nf, win, ld, P, 0, &ts)) return false;
+  for (int q = 0; q < NP; ++q) {
+    Q.ph[q].lv0 = ts.ph_lv0[q];
+    Q.ph[q].lv1 = ts.ph_lv1[q];
   }
-  P.lo_off.assign(1, 0);
-  P.lo_tiles.clear();
-  for (int kt : P.chain_cols) {
-    for (int i = kt + 1; i < Tx; ++i)
-      if (in_chain[i] && nz[i][kt]) P.lo_tiles.push_back(i);
-    P.lo_off.push_back((int)P.lo_tiles.size());
-  }
-  const int npos = (int)P.chain_cols.size();
-  std::vector<int> la(npos, -1), toff(1, 0), tasks;
-  for (int q = 0; q + 1 < npos; ++q)
-    for (int e = P.upd_off[q]; e < P.upd_off[q + 1]; ++e)
-      if (P.upd_tiles[e] == P.chain_cols[q + 1]) la[q] = P.chain_cols[q + 1];
-  for (int hw = 0; hw < BS_HELPERS; ++hw) {
-    for (int q = 0; q < npos; ++q)
-      for (int e = P.upd_off[q]; e < P.upd_off[q + 1]; ++e) {
-        const int j = P.upd_tiles[e];
-        if (j % BS_HELPERS == hw && j != la[q]) tasks.push_back((q << 16) | j);
-      }
-    toff.push_back((int)tasks.size());
-  }
-  P.n_tasks = (int)tasks.size();
-  P.la_tasks = la;
-  P.la_tasks.insert(P.la_tasks.end(), toff.begin(), toff.end());
-  P.la_tasks.insert(P.la_tasks.end(), tasks.begin(), tasks.end());
-  make_bs_steps(nz, Tx, P, BsPhases{{P.chain_cols}});
+  P.xtiles = Q.ph[0].xt;
   return true;
 }
 
@@ -1363,7 +1309,12 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   st_mark("validate");
   // ---- stable counting sorts: by frame, then by landmark -> (landmark, frame, original index)
   std::vector<int64_t> tmp(n_obs), order(n_obs);
-  {
+  // large problems (config 4: 410M records) sort on host threads: the same stable order (par_util.h)
+  const bool par_host = host_threads(n_obs) > 1;
+  if (par_host) {
+    parallel_counting_sort(n_obs, n_pose, (const int64_t*)nullptr, tmp.data(), [&](int64_t r) { return obs_frame[r]; });
+    parallel_counting_sort(n_obs, n_landmark, tmp.data(), order.data(), [&](int64_t r) { return obs_landmark[r]; });
+  } else {
     std::vector<int64_t> c(n_pose + 1, 0);
     for (int64_t r = 0; r < n_obs; ++r) c[obs_frame[r] + 1]++;
     for (int f = 0; f < n_pose; ++f) c[f + 1] += c[f];
@@ -1381,38 +1332,83 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   std::vector<int32_t> seg_frame, seg_lm, rec_seg(n_obs);
   std::vector<int64_t> seg_rec_begin;
   std::vector<int32_t> lm_seg_begin(n_landmark + 1, 0);
-  seg_frame.reserve(n_obs / 4 + 16);
-  for (int64_t k = 0; k < n_obs; ++k) {
-    int64_t r = order[k];
-    if (k == 0 || obs_landmark[r] != obs_landmark[order[k - 1]] || obs_frame[r] != obs_frame[order[k - 1]]) {
-      if ((int64_t)seg_frame.size() >= INT32_MAX - 1) return fail("too many segments");
-      seg_frame.push_back(obs_frame[r]);
-      seg_lm.push_back(obs_landmark[r]);
-      seg_rec_begin.push_back(k);
-      lm_seg_begin[obs_landmark[r] + 1]++;
+  if (par_host) {
+    // two passes over the same record chunks: count the segment starts per chunk, then fill at the prefix offsets
+    const int T = host_threads(n_obs);
+    auto is_start = [&](int64_t k) {
+      return k == 0 || obs_landmark[order[k]] != obs_landmark[order[k - 1]] || obs_frame[order[k]] != obs_frame[order[k - 1]];
+    };
+    std::vector<int64_t> base(T + 1, 0);
+    parallel_chunks(n_obs, T, [&](int64_t lo, int64_t hi, int t) {
+      int64_t c = 0;
+      for (int64_t k = lo; k < hi; ++k) c += is_start(k);
+      base[t + 1] = c;
+    });
+    for (int t = 0; t < T; ++t) base[t + 1] += base[t];
+    if (base[T] >= INT32_MAX - 1) return fail("too many segments");
+    seg_frame.resize(base[T]);
+    seg_lm.resize(base[T]);
+    seg_rec_begin.resize(base[T]);
+    parallel_chunks(n_obs, T, [&](int64_t lo, int64_t hi, int t) {
+      int64_t sg = base[t] - 1;
+      for (int64_t k = lo; k < hi; ++k) {
+        if (is_start(k)) {
+          const int64_t r = order[k];
+          ++sg;
+          seg_frame[sg] = obs_frame[r];
+          seg_lm[sg] = obs_landmark[r];
+          seg_rec_begin[sg] = k;
+        }
+        rec_seg[k] = (int32_t)sg;
+      }
+    });
+    // segments are landmark-ordered: each landmark's first segment, landmarks without one take the next's
+    std::vector<int32_t> first(n_landmark + 1, -1);
+    first[n_landmark] = (int32_t)base[T];
+    for (int64_t sg = 0; sg < base[T]; ++sg)
+      if (sg == 0 || seg_lm[sg] != seg_lm[sg - 1]) first[seg_lm[sg]] = (int32_t)sg;
+    for (int l = n_landmark - 1; l >= 0; --l)
+      if (first[l] < 0) first[l] = first[l + 1];
+    lm_seg_begin.assign(first.begin(), first.end());
+  } else {
+    seg_frame.reserve(n_obs / 4 + 16);
+    for (int64_t k = 0; k < n_obs; ++k) {
+      int64_t r = order[k];
+      if (k == 0 || obs_landmark[r] != obs_landmark[order[k - 1]] || obs_frame[r] != obs_frame[order[k - 1]]) {
+        if ((int64_t)seg_frame.size() >= INT32_MAX - 1) return fail("too many segments");
+        seg_frame.push_back(obs_frame[r]);
+        seg_lm.push_back(obs_landmark[r]);
+        seg_rec_begin.push_back(k);
+        lm_seg_begin[obs_landmark[r] + 1]++;
+      }
+      rec_seg[k] = (int32_t)seg_frame.size() - 1;
     }
-    rec_seg[k] = (int32_t)seg_frame.size() - 1;
+    for (int l = 0; l < n_landmark; ++l) lm_seg_begin[l + 1] += lm_seg_begin[l];
   }
   const int64_t n_seg = (int64_t)seg_frame.size();
   seg_rec_begin.push_back(n_obs);
-  for (int l = 0; l < n_landmark; ++l) lm_seg_begin[l + 1] += lm_seg_begin[l];
   h->n_seg = n_seg;
   // ---- frame CSR over segments (stable: landmark ascending within a frame)
   std::vector<int32_t> frame_seg_begin(n_pose + 1, 0), frame_seg_list(n_seg), frame_win_hi(n_pose);
   for (int64_t s = 0; s < n_seg; ++s) frame_seg_begin[seg_frame[s] + 1]++;
   for (int f = 0; f < n_pose; ++f) frame_seg_begin[f + 1] += frame_seg_begin[f];
-  {
+  if (par_host && host_threads(n_seg) > 1) {
+    parallel_counting_sort(n_seg, n_pose, (const int32_t*)nullptr, frame_seg_list.data(),
+                           [&](int32_t sg) { return seg_frame[sg]; });
+  } else {
     std::vector<int32_t> c(frame_seg_begin.begin(), frame_seg_begin.end() - 1);
     for (int64_t s = 0; s < n_seg; ++s) frame_seg_list[c[seg_frame[s]]++] = (int32_t)s;
   }
-  for (int f = 0; f < n_pose; ++f) {
-    int hi = f;
-    for (int e = frame_seg_begin[f]; e < frame_seg_begin[f + 1]; ++e) {
-      int l = seg_lm[frame_seg_list[e]];
-      hi = std::max(hi, seg_frame[lm_seg_begin[l + 1] - 1]);
+  parallel_chunks(n_pose, par_host ? std::min(host_threads(n_obs), n_pose) : 1, [&](int64_t f0, int64_t f1, int) {
+    for (int64_t f = f0; f < f1; ++f) {
+      int hi = (int)f;
+      for (int e = frame_seg_begin[f]; e < frame_seg_begin[f + 1]; ++e) {
+        int l = seg_lm[frame_seg_list[e]];
+        hi = std::max(hi, seg_frame[lm_seg_begin[l + 1] - 1]);
+      }
+      frame_win_hi[f] = hi;
     }
-    frame_win_hi[f] = hi;
-  }
+  });
   st_mark("segments+frame csr");
   // ---- register-blocked K2 structure: per landmark its frame range [first, last] and a dense W slot
   // per frame in it; K2 tiles (SCHUR_F1 frames x 64 partner frames) with the landmarks that reach them,
@@ -2167,7 +2163,7 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
                                  h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
                                  h->lambda, lam_dev, h->st, h->row_phase.as<uint8_t>(), q + 1);
       launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), d.lv1, h->Ldiag.as<double>(),
-                      h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>(), d.lv0);
+                      h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>(), d.lv0, h->chol_delayed);
       HIPCHK(hipGetLastError());
     }
   } else {
@@ -2871,6 +2867,52 @@ int ptzba_dist_plan_summary(int32_t n_pose, int32_t n_fixed, const int32_t* fram
   }
   out16[14] = o.n_aug;
   out16[15] = (int64_t)P.bsb_step_off.size() - 1;
+  return 0;
+}
+
+// host only: rank `rank`'s whole rank-tree plan for a CPU replay (tests/test_plan_replay.py): frame positions, tasks,
+// level offsets, per phase {lv0, lv1, exchange kind, group first rank, group size, exchanged tiles}, and the tiles
+// (ti, tj) of every phase's exchange concatenated.  counts: [0] tasks, [1] levels, [2] n_aug, [3] phases,
+// [4] exchanged tiles.  Null outputs only query the counts.
+int ptzba_dist_plan_export(int32_t n_pose, int32_t n_fixed, const int32_t* frame_win_hi, int32_t world, int32_t rank,
+                           int32_t* pos_out, int32_t* tasks_out, int64_t tasks_cap, int32_t* level_off_out,
+                           int64_t levels_cap, int32_t* phases_out, int32_t phases_cap, int32_t* xt_out, int64_t xt_cap,
+                           int64_t* counts) {
+  if (n_pose < 1 || n_fixed < 0 || n_fixed > n_pose || !frame_win_hi || !counts || world < 2 || rank < 0 || rank >= world)
+    return fail("bad arguments");
+  std::vector<int32_t> win(frame_win_hi, frame_win_hi + n_pose);
+  for (int f = 0; f < n_pose; ++f)
+    if (win[f] < f || win[f] >= n_pose) return fail("frame_win_hi[%d] = %d out of range", f, win[f]);
+  SysOrder o;
+  DistTree DT;
+  if (!dist_order(n_pose, n_fixed, win, world, o) || !dist_tree(o, world, DT)) return fail("no rank-tree split");
+  CholPlan P;
+  TreePlan Q;
+  if (!make_plan_tree(o, DT, rank, n_pose, n_fixed, win, pad_tile(o.n_aug + 1), P, Q)) return fail("no rank-tree plan");
+  int64_t nxt = 0;
+  for (const auto& t : Q.ph) nxt += (int64_t)t.xt.size() / 2;
+  counts[0] = (int64_t)P.tasks.size() / 4;
+  counts[1] = P.n_levels;
+  counts[2] = o.n_aug;
+  counts[3] = (int64_t)Q.ph.size();
+  counts[4] = nxt;
+  if ((tasks_out && tasks_cap < counts[0]) || (level_off_out && levels_cap < counts[1] + 1) ||
+      (phases_out && phases_cap < counts[3]) || (xt_out && xt_cap < nxt))
+    return fail("an output buffer is too small");
+  if (pos_out) std::copy(o.pos.begin(), o.pos.end(), pos_out);
+  if (tasks_out) std::copy(P.tasks.begin(), P.tasks.end(), tasks_out);
+  if (level_off_out) std::copy(P.level_off.begin(), P.level_off.end(), level_off_out);
+  for (size_t q = 0; q < Q.ph.size(); ++q) {
+    const auto& t = Q.ph[q];
+    if (phases_out) {
+      int32_t* r = phases_out + 6 * q;
+      r[0] = t.lv0; r[1] = t.lv1; r[2] = t.kind; r[3] = t.r0; r[4] = t.nr; r[5] = (int32_t)(t.xt.size() / 2);
+    }
+    if (xt_out) {
+      std::copy(t.xt.begin(), t.xt.end(), xt_out);
+      xt_out += t.xt.size();
+    }
+  }
   return 0;
 }
 

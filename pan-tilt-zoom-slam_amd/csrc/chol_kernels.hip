@@ -64,7 +64,7 @@ __global__ void k_chol_prepare(double* __restrict__ A, int64_t ld, int n, const 
                                const uint8_t* __restrict__ pad, int* info, PoseDamp pd) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int ph = pd.phase;
-  if (i == 0 && ph != 2) info[0] = 0;
+  if (i == 0 && ph <= 1) info[0] = 0;  // (a part-owned solve's first phase: later phases keep the earlier verdict)
   if (i < n) {
     if (ph == 0 || (ph == 1 && pd.row_phase[i] != 0)) A[(int64_t)n * ld + i] = b[i];
     if (pad && pad[i] && (ph == 0 || pd.row_phase[i] == ph)) A[i * ld + i] = 1.0;

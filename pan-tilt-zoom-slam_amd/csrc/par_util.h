@@ -39,13 +39,13 @@ inline void parallel_chunks(int64_t n, int T, F&& fn) {
 
 // Stable counting sort of the items in[0..n) (in == nullptr: the identity 0..n-1) by key(item) in [0, K): out[0..n)
 // receives the items in (key, position in `in`) order -- exactly the sequential counting sort's result.
-template <typename Key>
-inline void parallel_counting_sort(int64_t n, int64_t K, const int64_t* in, int64_t* out, Key key) {
+template <typename Key, typename Item = int64_t>
+inline void parallel_counting_sort(int64_t n, int64_t K, const Item* in, Item* out, Key key) {
   const int T = host_threads(n);
   std::vector<std::vector<int64_t>> cnt(T, std::vector<int64_t>(K, 0));
   parallel_chunks(n, T, [&](int64_t lo, int64_t hi, int t) {
     int64_t* c = cnt[t].data();
-    for (int64_t k = lo; k < hi; ++k) c[key(in ? in[k] : k)]++;
+    for (int64_t k = lo; k < hi; ++k) c[key(in ? in[k] : (Item)k)]++;
   });
   // bucket-major, then chunk order: the start of (bucket b, chunk t)
   int64_t run = 0;
@@ -58,7 +58,7 @@ inline void parallel_counting_sort(int64_t n, int64_t K, const int64_t* in, int6
   parallel_chunks(n, T, [&](int64_t lo, int64_t hi, int t) {
     int64_t* c = cnt[t].data();
     for (int64_t k = lo; k < hi; ++k) {
-      const int64_t item = in ? in[k] : k;
+      const Item item = in ? in[k] : (Item)k;
       out[c[key(item)]++] = item;
     }
   });

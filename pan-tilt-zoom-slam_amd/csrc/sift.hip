@@ -123,6 +123,58 @@ __global__ __launch_bounds__(256) void k_sift_blur_cols(int w, int h, const floa
   }
 }
 
+// Both passes in one launch (round 4): a 64 x 64 output tile stages its input (+ halo, reflected at the borders) in
+// LDS once, blurs the 64 + 2r rows it needs along x into LDS, then along y, and -- when `prev` is given -- writes
+// the DoG level dst - prev beside it (prev = the octave's previous Gaussian level, the same pixel).  Per output
+// pixel the same products in the same order as k_sift_blur_rows + k_sift_blur_cols (+ k_sift_dog): bit-identical,
+// with the intermediate image, the second launch and the DoG pass's two reads gone.
+constexpr int BLUR2_T = 64;
+__global__ __launch_bounds__(256) void k_sift_blur2(int w, int h, const float* __restrict__ src, float* __restrict__ dst,
+                                                     const float* __restrict__ wt, int K, const float* __restrict__ prev,
+                                                     float* __restrict__ dog) {
+  extern __shared__ float smem[];
+  __shared__ float sw[2 * BLUR_RMAX + 1];
+  const int r = K / 2, n = BLUR2_T + 2 * r;  // staged rows / columns
+  float* in = smem;                          // [n][n]
+  float* rt = smem + n * n;                  // [n][BLUR2_T + 1]
+  const int x0 = blockIdx.x * BLUR2_T, y0 = blockIdx.y * BLUR2_T, t = threadIdx.x;
+  for (int e = t; e < n * n; e += 256) {
+    const int i = e / n, j = e - i * n;
+    in[e] = src[(int64_t)refl101(y0 + i - r, h) * w + refl101(x0 + j - r, w)];
+  }
+  if (t < K) sw[t] = wt[t];
+  __syncthreads();
+  const int tx = t & (BLUR2_T - 1), ty = t / BLUR2_T;  // 64 x 4
+  for (int i = ty; i < n; i += 4) {
+    float acc = 0.f;
+    for (int k = 0; k < K; ++k) acc = acc + sw[k] * in[i * n + tx + k];
+    rt[i * (BLUR2_T + 1) + tx] = acc;
+  }
+  __syncthreads();
+  const int x = x0 + tx;
+  if (x >= w) return;
+  for (int yb = ty; yb < BLUR2_T; yb += 16) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float wk = sw[k];
+      a0 = a0 + wk * rt[(yb + k) * (BLUR2_T + 1) + tx];
+      a1 = a1 + wk * rt[(yb + 4 + k) * (BLUR2_T + 1) + tx];
+      a2 = a2 + wk * rt[(yb + 8 + k) * (BLUR2_T + 1) + tx];
+      a3 = a3 + wk * rt[(yb + 12 + k) * (BLUR2_T + 1) + tx];
+    }
+    const float a[4] = {a0, a1, a2, a3};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int y = y0 + yb + 4 * q;
+      if (y < h) {
+        const int64_t p = (int64_t)y * w + x;
+        dst[p] = a[q];
+        if (prev) dog[p] = a[q] - prev[p];
+      }
+    }
+  }
+}
+
 __global__ void k_sift_down(int sw, const float* __restrict__ src, int dw, int dh, float* __restrict__ dst) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
   if (x >= dw || y >= dh) return;
@@ -439,26 +491,44 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
   for (int o = 0; o < n_oct; ++o)
     for (int i = 0; i < SIFT_S + 3; ++i) gptr[o * (SIFT_S + 3) + i] = G + goff[o] + (int64_t)i * ow[o] * oh[o];
   HIPCHK(hipMemcpy(dptr.p, gptr.data(), gptr.size() * sizeof(float*), hipMemcpyHostToDevice));
-  auto blur = [&](int w, int h, const float* src, float* dst, int ki) {
+  // PTZ_SIFT_BLUR2=0: the two-pass blur + separate DoG pass (A/B knob, read per call)
+  const char* b2e = getenv("PTZ_SIFT_BLUR2");
+  const bool blur2 = !(b2e && atoi(b2e) == 0);
+  // dog_out: the DoG level dst - src written beside dst (fused form only)
+  auto blur = [&](int w, int h, const float* src, float* dst, int ki, float* dog_out) {
+    const int K = (int)kern[ki].size(), rr = K / 2;
+    const int n2 = BLUR2_T + 2 * rr;
+    const size_t lds = ((size_t)n2 * n2 + (size_t)n2 * (BLUR2_T + 1)) * sizeof(float);
+    if (blur2 && lds <= 64 * 1024) {  // (radius <= 14: every blur of OpenCV's default SIFT)
+      hipLaunchKernelGGL(k_sift_blur2, dim3((unsigned)((w + BLUR2_T - 1) / BLUR2_T), (unsigned)((h + BLUR2_T - 1) / BLUR2_T)),
+                         dim3(256), lds, nullptr, w, h, src, dst, dk.as<float>() + ki * kmax, K,
+                         dog_out ? src : nullptr, dog_out);
+      return true;
+    }
     hipLaunchKernelGGL(k_sift_blur_rows, dim3((unsigned)((w + BLUR_TX - 1) / BLUR_TX), (unsigned)h), dim3(BLUR_TX), 0,
-                       nullptr, w, h, src, T, dk.as<float>() + ki * kmax, (int)kern[ki].size());
+                       nullptr, w, h, src, T, dk.as<float>() + ki * kmax, K);
     hipLaunchKernelGGL(k_sift_blur_cols, dim3((unsigned)((w + BLUR_CT - 1) / BLUR_CT), (unsigned)((h + BLUR_CR - 1) / BLUR_CR)),
-                       dim3(256), 0, nullptr, w, h, T, dst, dk.as<float>() + ki * kmax, (int)kern[ki].size());
+                       dim3(256), 0, nullptr, w, h, T, dst, dk.as<float>() + ki * kmax, K);
+    return false;
   };
   // base: doubled image, then the blur from the assumed input blur to sigma
   hipLaunchKernelGGL(k_sift_up, dim3((unsigned)((W0 + 127) / 128), (unsigned)H0), dim3(128), 0, nullptr, width, height,
                      dimg.as<uint8_t>(), gptr[1]);
-  blur(W0, H0, gptr[1], gptr[0], 0);
+  blur(W0, H0, gptr[1], gptr[0], 0, nullptr);
   const float thr = (float)std::floor(0.5 * SIFT_CONTR / SIFT_S * 255);
   for (int o = 0; o < n_oct; ++o) {
     const int w = ow[o], h = oh[o];
     if (o > 0)
       hipLaunchKernelGGL(k_sift_down, dim3((unsigned)((w + 127) / 128), (unsigned)h), dim3(128), 0, nullptr, ow[o - 1],
                          gptr[(o - 1) * (SIFT_S + 3) + SIFT_S], w, h, gptr[o * (SIFT_S + 3)]);
-    for (int i = 1; i < SIFT_S + 3; ++i) blur(w, h, gptr[o * (SIFT_S + 3) + i - 1], gptr[o * (SIFT_S + 3) + i], i);
     const int64_t np = (int64_t)w * h;
-    hipLaunchKernelGGL(k_sift_dog, dim3((unsigned)((np * (SIFT_S + 2) + 255) / 256)), dim3(256), 0, nullptr, np,
-                       G + goff[o], Dg + doff[o]);
+    bool fused_dog = true;
+    for (int i = 1; i < SIFT_S + 3; ++i)
+      fused_dog = blur(w, h, gptr[o * (SIFT_S + 3) + i - 1], gptr[o * (SIFT_S + 3) + i], i,
+                       blur2 ? Dg + doff[o] + (i - 1) * np : nullptr) && fused_dog;
+    if (!blur2 || !fused_dog)
+      hipLaunchKernelGGL(k_sift_dog, dim3((unsigned)((np * (SIFT_S + 2) + 255) / 256)), dim3(256), 0, nullptr, np,
+                         G + goff[o], Dg + doff[o]);
     if (w > 2 * SIFT_BORDER && h > 2 * SIFT_BORDER)
       hipLaunchKernelGGL(k_sift_extrema, dim3((unsigned)((w - 2 * SIFT_BORDER + 63) / 64), (unsigned)(h - 2 * SIFT_BORDER), SIFT_S),
                          dim3(64), 0, nullptr, o, w, h, Dg + doff[o], thr, dcand.as<SiftCand>(), dcnt.as<int>(), CAP);

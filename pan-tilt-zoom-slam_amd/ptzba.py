@@ -161,6 +161,7 @@ def lib():
         "ptzba_exchange_group": ([V, I32, V], I),
         "ptzba_dist_plan_summary": ([I32, I32, V, I32, I32, V], I),
         "ptzba_dist_rank_phases": ([I32, I32, V, I32, I32, V, I32, POINTER(c_int32)], I),
+        "ptzba_dist_plan_export": ([I32, I32, V, I32, I32, V, V, I64, V, I64, V, I32, V, I64, V], I),
         "ptzekf_new": ([I], V),
         "ptzekf_delete": ([V], None),
         "ptzekf_num_rays": ([V], I),
@@ -196,7 +197,7 @@ EXPORTED_SYMBOLS = [
     "ptzba_comm_delete", "ptzba_comm_split", "ptzba_comm_info", "ptzba_comm_allreduce", "ptzba_attach_comm",
     "ptzba_dist_info", "ptzba_owned_frames", "ptz_corner_min_eig", "ptz_orb", "ptzba_plan_summary",
     "ptzba_plan_export", "ptzba_dist_exchanges", "ptzba_dist_groups", "ptzba_exchange_group", "ptzba_dist_plan_summary",
-    "ptzba_dist_rank_phases",
+    "ptzba_dist_rank_phases", "ptzba_dist_plan_export",
 ]
 
 
@@ -618,6 +619,27 @@ def dist_plan_summary(frame_win_hi, world, rank, n_fixed=1):
     keys = ("part_owned", "nd_depth", "base", "phases", "levels", "est_us", "tasks", "max_level_tasks", "x_part", "x_sub",
             "x_sep", "part_group", "sub_group", "sep_group", "n_aug", "bs_steps")
     return {k: int(v) for k, v in zip(keys, out)}
+
+
+def dist_plan_export(frame_win_hi, world, rank, n_fixed=1):
+    """Rank `rank`'s rank-tree plan (ptzba_dist_plan_export, host only) for a CPU replay: (pos [n_pose], tasks
+    [n, 4] int32, level_off, n_aug, phases [(lv0, lv1, kind, r0, nr)], exchanged tiles per phase [[k, 2] int32])."""
+    win = np.ascontiguousarray(frame_win_hi, np.int32)
+    c = np.zeros(5, np.int64)
+    args = (len(win), int(n_fixed), _ptr(win), int(world), int(rank))
+    _check(lib().ptzba_dist_plan_export(*args, None, None, 0, None, 0, None, 0, None, 0, _ptr(c)), "ptzba_dist_plan_export")
+    pos = np.empty(len(win), np.int32)
+    tasks = np.empty((int(c[0]), 4), np.int32)
+    off = np.empty(int(c[1]) + 1, np.int32)
+    ph = np.empty((int(c[3]), 6), np.int32)
+    xt = np.empty((max(int(c[4]), 1), 2), np.int32)
+    _check(lib().ptzba_dist_plan_export(*args, _ptr(pos), _ptr(tasks), int(c[0]), _ptr(off), int(c[1]) + 1, _ptr(ph),
+                                        int(c[3]), _ptr(xt), int(c[4]), _ptr(c)), "ptzba_dist_plan_export")
+    xts, o = [], 0
+    for r in ph:
+        xts.append(xt[o:o + int(r[5])])
+        o += int(r[5])
+    return pos, tasks, off, int(c[2]), [tuple(int(x) for x in r[:5]) for r in ph], xts
 
 
 def dist_rank_phases(frame_win_hi, world, rank, n_fixed=1):

@@ -54,11 +54,28 @@ def replay(S, tasks, level_off):
     T = ld // NB
     A = np.tril(S).copy()
     Ldiag = {}
+    replay_levels(A, Ldiag, tasks, level_off, 0, len(level_off) - 1)
+    return assemble(A, Ldiag)
+
+
+def assemble(A, Ldiag):
+    T = A.shape[0] // NB
+    Lf = np.zeros_like(A)
+    for a in range(T):
+        for b in range(a):
+            Lf[a * NB:(a + 1) * NB, b * NB:(b + 1) * NB] = A[a * NB:(a + 1) * NB, b * NB:(b + 1) * NB]
+        if a in Ldiag:
+            Lf[a * NB:(a + 1) * NB, a * NB:(a + 1) * NB] = Ldiag[a]
+    return Lf, Ldiag
+
+
+def replay_levels(A, Ldiag, tasks, level_off, L0, L1):
+    """Levels [L0, L1) of a task list on A (lower tiles, in place); diagonal factor tiles go to Ldiag."""
 
     def tile(a, b):
         return A[a * NB:(a + 1) * NB, b * NB:(b + 1) * NB]
 
-    for L in range(len(level_off) - 1):
+    for L in range(L0, L1):
         for q in range(level_off[L], level_off[L + 1]):
             typ, i, j, ups, tmask = decode(tasks[q])
             if typ == 2:
@@ -85,10 +102,3 @@ def replay(S, tasks, level_off):
                 Ldiag[k] = Lkk
             else:
                 tile(i, k)[:] = np.linalg.solve(Lkk, Tt.T).T
-    Lf = np.zeros_like(A)
-    for a in range(T):
-        for b in range(a):
-            Lf[a * NB:(a + 1) * NB, b * NB:(b + 1) * NB] = tile(a, b)
-        if a in Ldiag:
-            Lf[a * NB:(a + 1) * NB, a * NB:(a + 1) * NB] = Ldiag[a]
-    return Lf, Ldiag

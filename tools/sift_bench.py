@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Wall time of one GPU SIFT detectAndCompute (ptz_sift) on a rendered 1080p frame, median of N calls; the
+fused blur (default) against PTZ_SIFT_BLUR2=0 when --ab is given (the env is read per call)."""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "pan-tilt-zoom-slam_amd")]
+
+
+def main():
+    import ptzba
+    import synthetic
+    import image_process
+    scene = synthetic.StreamScene(4, seed=0)
+    img = image_process._grey_u8(synthetic.RenderedStream(scene, seed=0).image(0))
+    out = {}
+    for tag, val in (("fused", "1"), ("two_pass", "0")):
+        os.environ["PTZ_SIFT_BLUR2"] = val
+        for _ in range(3):
+            ptzba.sift(img, 1500)
+        ts = []
+        for _ in range(20):
+            t = time.perf_counter()
+            kp, _, des = ptzba.sift(img, 1500)
+            ts.append(time.perf_counter() - t)
+        out[tag] = (1e3 * float(np.median(ts)), len(kp), float(des.sum()))
+    print({k: (round(v[0], 3), v[1], v[2]) for k, v in out.items()})
+
+
+if __name__ == "__main__":
+    main()
