@@ -2171,14 +2171,18 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
       launch_chol_prepare_damped(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(),
                                  h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
                                  h->lambda, lam_dev, h->st);
-    if (h->chol_pst)
-      launch_cholesky_pst(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_lvl.as<int>(),
-                          h->chol_lvl_n.as<int>(), h->chol_lvl_cnt.as<unsigned>(),
-                          h->chol_pst_ticket ? h->chol_lvl_cnt.as<unsigned>() + h->chol_levels : nullptr,
-                          h->chol_epoch++, 0, h->chol_levels,
-                          h->Ldiag.as<double>(), h->info.as<int>(), h->Minv.as<double>(), h->chol_delayed, h->bsp_err,
-                          h->st);
-    else
+    if (h->chol_pst) {
+      // PTZBA_CHOL_GROUP=g (block-index form only): g levels per launch instead of all (A/B knob)
+      const char* ge = getenv("PTZBA_CHOL_GROUP");
+      const int g = (ge && !h->chol_pst_ticket) ? std::max(1, atoi(ge)) : h->chol_levels;
+      for (int L0 = 0; L0 < h->chol_levels; L0 += g)
+        launch_cholesky_pst(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_lvl.as<int>(),
+                            h->chol_lvl_n.as<int>(), h->chol_lvl_cnt.as<unsigned>(),
+                            h->chol_pst_ticket ? h->chol_lvl_cnt.as<unsigned>() + h->chol_levels : nullptr,
+                            h->chol_epoch, L0, std::min(L0 + g, h->chol_levels), h->Ldiag.as<double>(),
+                            h->info.as<int>(), h->Minv.as<double>(), h->chol_delayed, h->bsp_err, h->st);
+      h->chol_epoch++;
+    } else
       launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
                       h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>(), 0,
                       h->chol_delayed);

@@ -1162,7 +1162,7 @@ __global__ __launch_bounds__(256) void k_chol_pst(double* __restrict__ A, int64_
                                                   const int* __restrict__ lvl_n, unsigned* __restrict__ lvl_cnt,
                                                   unsigned* __restrict__ ticket, uint32_t epoch,
                                                   double* __restrict__ Ldiag, int* info, double* __restrict__ Minv,
-                                                  int* err) {
+                                                  int* err, int nsleep) {
   __shared__ int s_t;
   if (threadIdx.x == 0) {
     // ticket == nullptr: the task of blockIdx.x (relies on workgroups being dispatched in index order; A/B knob --
@@ -1180,7 +1180,7 @@ __global__ __launch_bounds__(256) void k_chol_pst(double* __restrict__ A, int64_
           ok = true;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        for (int q = 0; q < nsleep; ++q) __builtin_amdgcn_s_sleep(1);  // (polling pressure on the counter, A/B)
       }
       if (!ok) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // pinned host flag
     }
@@ -1198,12 +1198,14 @@ int launch_cholesky_pst(double* A, int64_t ld, const int4* tasks, const int* tas
                         double* Ldiag, int* info, double* Minv, bool delayed, int* err, hipStream_t st) {
   const int t0 = task_off_host[L0], n = task_off_host[L1] - t0;
   if (n <= 0) return 0;
+  const char* se = getenv("PTZBA_CHOL_SPIN_SLEEP");  // A/B knob: s_sleep(1) per poll
+  const int nsleep = se ? std::max(1, atoi(se)) : 1;
   if (delayed)
     hipLaunchKernelGGL(k_chol_pst<true>, dim3((unsigned)n), dim3(256), 0, st, A, ld, tasks, task_lvl, t0, n, L0, lvl_n,
-                       lvl_cnt, ticket, epoch, Ldiag, info, Minv, err);
+                       lvl_cnt, ticket, epoch, Ldiag, info, Minv, err, nsleep);
   else
     hipLaunchKernelGGL(k_chol_pst<false>, dim3((unsigned)n), dim3(256), 0, st, A, ld, tasks, task_lvl, t0, n, L0, lvl_n,
-                       lvl_cnt, ticket, epoch, Ldiag, info, Minv, err);
+                       lvl_cnt, ticket, epoch, Ldiag, info, Minv, err, nsleep);
   return 0;
 }
 

@@ -491,9 +491,11 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
   for (int o = 0; o < n_oct; ++o)
     for (int i = 0; i < SIFT_S + 3; ++i) gptr[o * (SIFT_S + 3) + i] = G + goff[o] + (int64_t)i * ow[o] * oh[o];
   HIPCHK(hipMemcpy(dptr.p, gptr.data(), gptr.size() * sizeof(float*), hipMemcpyHostToDevice));
-  // PTZ_SIFT_BLUR2=0: the two-pass blur + separate DoG pass (A/B knob, read per call)
+  // PTZ_SIFT_BLUR2=1: both blur passes and the DoG in one launch (A/B knob, read per call; measured 2.29 vs 2.23 ms
+  // per 1080p frame against the two-pass form, tools/sift_bench.py r04i -- the LDS-staged passes were not bound by
+  // the intermediate image's traffic)
   const char* b2e = getenv("PTZ_SIFT_BLUR2");
-  const bool blur2 = !(b2e && atoi(b2e) == 0);
+  const bool blur2 = b2e && atoi(b2e) == 1;
   // dog_out: the DoG level dst - src written beside dst (fused form only)
   auto blur = [&](int w, int h, const float* src, float* dst, int ki, float* dog_out) {
     const int K = (int)kern[ki].size(), rr = K / 2;

@@ -22,5 +22,6 @@ PY
 for rep in $(seq ${REPS:-1}); do
   run A$rep || exit 1
   k=0
-  for kv in $AB_ENVS; do k=$((k+1)); run B${k}_$rep $kv || exit 1; done
+  # a variant may set several variables, comma-separated (VAR1=a,VAR2=b)
+  for kv in $AB_ENVS; do k=$((k+1)); run B${k}_$rep $(echo "$kv" | tr ',' ' ') || exit 1; done
 done

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Wall time of one GPU SIFT detectAndCompute (ptz_sift) on a rendered 1080p frame, median of N calls; the
-fused blur (default) against PTZ_SIFT_BLUR2=0 when --ab is given (the env is read per call)."""
+two-pass blur (default) and the fused one (PTZ_SIFT_BLUR2=1; the env is read per call)."""
 import os
 import sys
 import time
@@ -18,7 +18,7 @@ def main():
     scene = synthetic.StreamScene(4, seed=0)
     img = image_process._grey_u8(synthetic.RenderedStream(scene, seed=0).image(0))
     out = {}
-    for tag, val in (("fused", "1"), ("two_pass", "0")):
+    for tag, val in (("two_pass", "0"), ("fused", "1")):
         os.environ["PTZ_SIFT_BLUR2"] = val
         for _ in range(3):
             ptzba.sift(img, 1500)
