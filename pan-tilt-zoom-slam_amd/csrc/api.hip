@@ -164,10 +164,8 @@ struct ptzba_ctx {
   bool ext_exchange = false;   // the caller ran its own exchange protocol (ptzba_exchange / _packed) once
   bool f1_covered = false;     // every 32-frame block has a chunk-0 Schur tile (all diagonals written by K2)
   // single-GPU builds fold k_chol_prepare into the build (FusedPrep, ptzba_kernels.h)
-  bool fused_prep() const {
-    static const bool off = getenv("PTZBA_NO_FUSED_PREP") != nullptr;  // A/B knob
-    return !off && !dist_mode && !has_exchange() && !ext_exchange && f1_covered;
-  }
+  bool no_fused_prep = false;  // PTZBA_NO_FUSED_PREP (A/B knob, read at set_problem)
+  bool fused_prep() const { return !no_fused_prep && !dist_mode && !has_exchange() && !ext_exchange && f1_covered; }
   double* S() const { return sys.as<double>(); }
   double* bvec() const { return sys.as<double>() + ld * ld; }
   double* gpose() const { return sys.as<double>() + ld * ld + ld; }
@@ -1784,6 +1782,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
               plan.bsb_tasks.size() / 12 <= 512;  // (2 workgroups per CU resident: 190 VGPRs)
   h->bsp_epoch = 0;
   // single-launch factorisation (PTZBA_CHOL_PERSIST=1, A/B knob): single-process SPD solves
+  h->no_fused_prep = getenv("PTZBA_NO_FUSED_PREP") != nullptr;
   h->chol_pst = !part_mode && !dist && (getenv_is("PTZBA_CHOL_PERSIST", "1") || getenv_is("PTZBA_CHOL_PERSIST", "2")) &&
                 plan.n_levels > 0;
   h->chol_pst_ticket = !getenv_is("PTZBA_CHOL_PERSIST", "2");

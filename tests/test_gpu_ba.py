@@ -524,3 +524,32 @@ def test_single_launch_schedules_bitwise_equal(gpu_available, config, knob, monk
     (b_ptz, b_rays), b_res = out[1]
     assert a_res == b_res
     assert np.array_equal(a_ptz, b_ptz) and np.array_equal(a_rays, b_rays)
+
+
+def test_fused_prepare_matches_separate_prepare(gpu_available, monkeypatch):
+    """The single-GPU build writes the augmented row, the padding pivots and the pose damping itself (fused prepare,
+    k_build_prologue + the Schur kernel); PTZBA_NO_FUSED_PREP=1 runs k_chol_prepare before the factorisation instead.
+    Config 2's system has padding rows 147-159 (index mod 32 = 19-31: rows whose diagonal lies in a double2 another
+    wave zeroes -- the race ADVICE r3 found): the LM iterates agree bit for bit over 3 solves."""
+    import ptzba
+    import synthetic
+    p = synthetic.make_problem("config2", seed=0)
+    out = []
+    for v in (None, "1"):
+        if v is None:
+            monkeypatch.delenv("PTZBA_NO_FUSED_PREP", raising=False)
+        else:
+            monkeypatch.setenv("PTZBA_NO_FUSED_PREP", v)
+        h = ptzba.BAHandle(0)
+        h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=ptzba.FP32,
+                      loss=ptzba.LOSS_HUBER)
+        assert h.solver_info()["n_aug"] > 3 * (p.n_pose - 1)  # padding rows present
+        h.set_state(p.init_ptz, p.init_rays)
+        h.save_state()
+        rs = [h.solve_resident(restore=True, ftol=1e-14, xtol=1e-16, max_iter=4) for _ in range(3)]
+        out.append((h.get_state(), [(r.cost, r.njev, r.nfev, r.status) for r in rs]))
+        h.close()
+    (a_ptz, a_rays), a_res = out[0]
+    (b_ptz, b_rays), b_res = out[1]
+    assert a_res == b_res
+    assert np.array_equal(a_ptz, b_ptz) and np.array_equal(a_rays, b_rays)
