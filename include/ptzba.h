@@ -354,6 +354,15 @@ PTZBA_EXPORT int ptz_refine_poses(int device, int32_t n_hyp, double* ptz_inout, 
  * The ratio test of match_sift_features (m < 0.7 n) runs on the host. */
 PTZBA_EXPORT int ptz_match_knn2(int device, int64_t n1, int64_t n2, int32_t dim, const float* des1, const float* des2,
                                 int32_t* idx_out, float* dist_out);
+/* Device-resident descriptor sets for repeated matching (a sliding keyframe window: image_process.py:509-667 run per
+ * keyframe over the window).  ptz_desc_put uploads n fp32 rows of `dim` under a caller-chosen key (replacing what the
+ * key held); ptz_desc_drop frees the listed keys (unknown keys are ignored).  ptz_match_knn2_sets = ptz_match_knn2
+ * of the concatenation of the query sets (in the order given) against the train set, bit for bit; n_rows must equal
+ * the query sets' total row count, idx_out / dist_out hold 2 entries per row. */
+PTZBA_EXPORT int ptz_desc_put(int device, uint64_t key, int64_t n, int32_t dim, const float* des);
+PTZBA_EXPORT int ptz_desc_drop(int device, int32_t n_keys, const uint64_t* keys);
+PTZBA_EXPORT int ptz_match_knn2_sets(int device, int32_t n_sets, const uint64_t* query_keys, uint64_t train_key,
+                                     int64_t n_rows, int32_t* idx_out, float* dist_out);
 /* Homography RANSAC (cv.findHomography(..., RANSAC, threshold) as called by homography_ransac): n_hyp
  * hypotheses from 4-point samples keyed by (seed, hypothesis, draw), DLT in Hartley-normalised coordinates,
  * the hypothesis with most inliers (reprojection error < threshold px; ties: lowest index), a linear

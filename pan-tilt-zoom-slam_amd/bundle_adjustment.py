@@ -84,6 +84,23 @@ def _compute_residual(x, n_pose, n_landmark, n_residual, keypoints, src_pt_index
     return r
 
 
+class _KeyframeLists:
+    """The per-keyframe (local keypoint, global landmark) lists of one BA call in the reference's set() order
+    (bundle_adjustment.py:218-239, native: MatchGraph.keyframe_features), formed for all keyframes at the first
+    request."""
+
+    def __init__(self, graph):
+        self.graph = graph
+        self.csr = None
+
+    def lists(self, i):
+        if self.csr is None:
+            self.csr = self.graph.keyframe_features()
+            self.graph = None
+        off, loc, glo = self.csr
+        return loc[off[i]:off[i + 1]], glo[off[i]:off[i + 1]]
+
+
 def bundle_adjustment(images, image_indices, feature_method, initial_ptzs, center, rotation, u, v, save_path,
                       verbose=False, precision="fp64", loss="linear", f_scale=1.0, ftol=1e-4, xtol=1e-8,
                       max_iter=100, device=0, correspondences=None):
@@ -158,17 +175,17 @@ def bundle_adjustment(images, image_indices, feature_method, initial_ptzs, cente
     timing["solve"] = time.time() - t0
     timing.update({"solve_" + k: v for k, v in ptzba.LAST_SOLVE_TIMING.items()})
 
-    # step 5: keyframes (bundle_adjustment.py:214-248), features in the reference's set() order
+    # step 5: keyframes (bundle_adjustment.py:214-248), features in the reference's set() order -- formed for every
+    # keyframe of this call at the first access to any of their feature lists (_KeyframeLists)
     t2 = time.time()
-    off, loc, glo = g.keyframe_features()
+    lists = _KeyframeLists(g)
     keyframes = []
     for i in range(N):
         pan, tilt, fl = all_poses[i]
         key_frame = KeyFrame(images[i], image_indices[i], center, rotation, u, v, pan, tilt, fl)
-        # feature_pts = [keypoints[i][k] for k in local_index], feature_des = descriptors[i][local_index], taken on
-        # first use (KeyFrame.set_features_lazy)
-        key_frame.set_features_lazy(keypoints[i], descriptors[i], loc[off[i]:off[i + 1]])
-        key_frame.landmark_index = glo[off[i]:off[i + 1]].astype(np.int32)
+        # feature_pts = [keypoints[i][k] for k in local_index], feature_des = descriptors[i][local_index],
+        # landmark_index = global ids, on first use (KeyFrame.set_features_lazy)
+        key_frame.set_features_lazy(keypoints[i], descriptors[i], lists, i)
         keyframes.append(key_frame)
         if verbose:
             print("frame %d, landmark number %d" % (image_indices[i], len(key_frame.landmark_index)))

@@ -95,13 +95,43 @@ class CorrespondenceCache:
     Keys are the keyframes' image indices (KeyFrame.img_index); a key whose image changed is re-detected
     and its pairs re-matched."""
 
+    _next_dev_id = 1  # device descriptor-set ids, unique per process (ptzba.desc_put keys)
+
     def __init__(self):
         self.detections = {}   # key -> (image, keypoints, descriptors, xy [K, 2])
         self.matches = {}      # (key_i, key_j, method) -> (idx1 int32, idx2 int32)
+        self.dev = {}          # (key, method) -> (device descriptor-set id, rows): descriptors kept on the GPU
         self.n_detect = 0
         self.n_match = 0
         self.n_detect_hit = 0
         self.n_match_hit = 0
+
+    def dev_set(self, key, feature_method, descriptors):
+        """Id of this detection's descriptors uploaded to the device (once per detection) for the batched GPU
+        matcher (ptzba.match_knn2_sets): a sliding window re-matches its new keyframe against every older one."""
+        k = (key, feature_method)
+        hit = self.dev.get(k)
+        if hit is None:
+            d = ptzba.desc_put_new(CorrespondenceCache._next_dev_id, descriptors)
+            hit = (CorrespondenceCache._next_dev_id, d)
+            CorrespondenceCache._next_dev_id += 1
+            self.dev[k] = hit
+        return hit
+
+    def _drop_dev(self, keep):
+        gone = [k for k in self.dev if not keep(k)]
+        if gone:
+            ids = [self.dev.pop(k)[0] for k in gone]
+            try:
+                ptzba.desc_drop(ids)
+            except Exception:
+                pass
+
+    def __del__(self):
+        try:
+            self._drop_dev(lambda k: False)
+        except Exception:
+            pass
 
     def detect(self, key, image, feature_method):
         hit = self.detections.get((key, feature_method))
@@ -137,12 +167,14 @@ class CorrespondenceCache:
     def forget(self, key):
         self.detections = {k: v for k, v in self.detections.items() if k[0] != key}
         self.matches = {k: v for k, v in self.matches.items() if k[0] != key and k[1] != key}
+        self._drop_dev(lambda k: k[0] != key)
 
     def retain(self, keys):
         """Drop everything about images not in `keys` (sliding windows keep memory bounded)."""
         keep = set(keys)
         self.detections = {k: v for k, v in self.detections.items() if k[0] in keep}
         self.matches = {k: v for k, v in self.matches.items() if k[0] in keep and k[1] in keep}
+        self._drop_dev(lambda k: k[0] in keep)
 
 
 def _match_raw(det_i, det_j, feature_method):
@@ -251,8 +283,11 @@ def build_graph(images, image_match_mask=(), feature_method="sift", verbose=Fals
     if feature_method == "sift" and image_process.match_sift_features is image_process.GPU_MATCH_SIFT:
         need = [(i, j) for i, j in todo if cache is None or cache.peek(keys[i], keys[j], feature_method) is None]
         if len(need) > 1:
+            # (xy arrays: no .pt loops; with a cache the descriptors stay on the device across calls)
+            dev = None if cache is None else [(cache.dev_set(keys[i], feature_method, dets[i][1]),
+                                               cache.dev_set(keys[j], feature_method, dets[j][1])) for i, j in need]
             res = image_process.match_sift_features_batch(
-                [(dets[i][2], dets[i][1], dets[j][2], dets[j][1]) for i, j in need])  # (xy arrays: no .pt loops)
+                [(dets[i][2], dets[i][1], dets[j][2], dets[j][1]) for i, j in need], dev_sets=dev)
             for (i, j), (a, b) in zip(need, res):
                 m = (np.asarray(a, dtype=np.int32).reshape(-1), np.asarray(b, dtype=np.int32).reshape(-1))
                 pre[(i, j)] = m
@@ -273,17 +308,23 @@ def build_graph(images, image_match_mask=(), feature_method="sift", verbose=Fals
         elif verbose:
             print("no enough matches between image: %d and %d" % (i, j))
     t_cap = time.perf_counter()
-    # 200-match cap: the reference's random.shuffle sequence, replayed in pair order
-    capped = [p for p, (a, _) in enumerate(raw) if len(a) > MAX_MATCH_NUM]
-    if capped:
-        sel = _shuffle_prefixes(np.array([len(raw[p][0]) for p in capped], np.int64)).reshape(-1, MAX_MATCH_NUM)
-        for q, p in enumerate(capped):
-            a, b = raw[p]
-            raw[p] = (a[sel[q]], b[sel[q]])
-    cnt = np.array([len(a) for a, _ in raw], np.int64)
+    # 200-match cap: the reference's random.shuffle sequence, replayed in pair order; every pair's kept matches are
+    # gathered in one indexing pass over the concatenated raw lists (uncapped pairs whole, capped pairs at their
+    # shuffled prefix positions)
+    raw_len = np.array([len(a) for a, _ in raw], np.int64)
+    cnt = np.minimum(raw_len, MAX_MATCH_NUM)
     off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
-    k1 = np.concatenate([a for a, _ in raw]) if raw else np.zeros(0, np.int64)
-    k2 = np.concatenate([b for _, b in raw]) if raw else np.zeros(0, np.int64)
+    if raw:
+        raw_off = np.concatenate([[0], np.cumsum(raw_len)[:-1]]).astype(np.int64)
+        pos = np.arange(off[-1], dtype=np.int64) - np.repeat(off[:-1], cnt)  # position within the pair
+        capped = raw_len > MAX_MATCH_NUM
+        if capped.any():
+            pos[np.repeat(capped, cnt)] = _shuffle_prefixes(raw_len[capped])
+        src = np.repeat(raw_off, cnt) + pos
+        k1 = np.concatenate([a for a, _ in raw])[src]
+        k2 = np.concatenate([b for _, b in raw])[src]
+    else:
+        k1 = k2 = np.zeros(0, np.int64)
     if verbose:
         for p in range(len(pi)):
             print("%d matches between image: %d and %d" % (cnt[p], pi[p], pj[p]))

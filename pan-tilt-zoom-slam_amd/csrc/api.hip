@@ -1429,12 +1429,27 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     std::vector<std::vector<int32_t>> tiles;
     std::vector<int32_t> tile_key;
     std::vector<int32_t> un;
+    // the landmarks of an F1 block, ascending and unique: marked in a bitmap, then read out word by word between the
+    // lowest and highest marked word (no sort: a config-5 window's single block holds ~100K segments)
+    std::vector<uint64_t> lm_bits((size_t)n_landmark / 64 + 1, 0);
     for (int f1b = o.n_fixed; f1b < n_pose; f1b += SCHUR_F1) {
       un.clear();
+      size_t w_lo = lm_bits.size(), w_hi = 0;
       for (int f = f1b; f < std::min(n_pose, f1b + SCHUR_F1); ++f)
-        for (int e = frame_seg_begin[f]; e < frame_seg_begin[f + 1]; ++e) un.push_back(seg_lm[frame_seg_list[e]]);
-      std::sort(un.begin(), un.end());
-      un.erase(std::unique(un.begin(), un.end()), un.end());
+        for (int e = frame_seg_begin[f]; e < frame_seg_begin[f + 1]; ++e) {
+          const uint32_t l = (uint32_t)seg_lm[frame_seg_list[e]];
+          lm_bits[l >> 6] |= 1ull << (l & 63);
+          w_lo = std::min<size_t>(w_lo, l >> 6);
+          w_hi = std::max<size_t>(w_hi, l >> 6);
+        }
+      for (size_t wd = w_lo; wd <= w_hi && w_lo < lm_bits.size(); ++wd) {
+        uint64_t m = lm_bits[wd];
+        lm_bits[wd] = 0;
+        while (m) {
+          un.push_back((int32_t)(wd * 64 + __builtin_ctzll(m)));
+          m &= m - 1;
+        }
+      }
       int hi = f1b;
       for (int l : un) hi = std::max(hi, lm_meta[4 * l + 1]);
       const int nc = (hi - f1b) / WAVE + 1;
@@ -1571,11 +1586,21 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     if (ns > 0) lm_order.push_back(l);
     max_seg = std::max(max_seg, ns);
   }
-  std::stable_sort(lm_order.begin(), lm_order.end(), [&](int a, int b) {
-    int64_t ra = seg_rec_begin[lm_seg_begin[a + 1]] - seg_rec_begin[lm_seg_begin[a]];
-    int64_t rb = seg_rec_begin[lm_seg_begin[b + 1]] - seg_rec_begin[lm_seg_begin[b]];
-    return ra > rb;
-  });
+  {
+    // stable counting sort by record count, descending (the order std::stable_sort with `more records first` gives)
+    auto nrec = [&](int l) { return seg_rec_begin[lm_seg_begin[l + 1]] - seg_rec_begin[lm_seg_begin[l]]; };
+    int64_t mx = 0;
+    for (int l : lm_order) mx = std::max(mx, nrec(l));
+    if (mx <= 4 * (int64_t)lm_order.size() + 1024) {
+      std::vector<int32_t> c((size_t)mx + 2, 0), srt(lm_order.size());
+      for (int l : lm_order) c[mx - nrec(l) + 1]++;
+      for (int64_t q = 0; q <= mx; ++q) c[q + 1] += c[q];
+      for (int l : lm_order) srt[c[mx - nrec(l)]++] = l;
+      lm_order.swap(srt);
+    } else {
+      std::stable_sort(lm_order.begin(), lm_order.end(), [&](int a, int b) { return nrec(a) > nrec(b); });
+    }
+  }
   h->n_work = (int)lm_order.size();
   h->max_seg_per_lm = max_seg;
   if (n_obs >= ((int64_t)1 << 31)) return fail("n_obs %lld exceeds the 2^31 record limit of a handle (shard it)", (long long)n_obs);

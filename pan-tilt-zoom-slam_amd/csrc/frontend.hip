@@ -18,6 +18,8 @@
 //                          the final mask.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <vector>
 
@@ -403,6 +405,110 @@ int ptz_match_knn2(int device, int64_t n1, int64_t n2, int32_t dim, const float*
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(idx_out, idx.p, (size_t)n1 * 8, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(dist_out, dist.p, (size_t)n1 * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+// Device-resident descriptor sets (ptz_desc_put / ptz_desc_drop) and kNN-2 of several resident query sets against a
+// resident train set (ptz_match_knn2_sets): a sliding keyframe window matches its new keyframe against ~29 older
+// ones per call, whose descriptors (~22 MB of fp32 at 1500 x 128 each) would otherwise be concatenated and copied
+// host -> device again at every call.  The query sets are gathered device to device into the work buffer and run
+// through the same two kernels as ptz_match_knn2 on their concatenation: the same result bit for bit.
+struct DescSet {
+  DBuf buf;
+  int64_t n = 0;
+  int32_t dim = 0;
+};
+struct DescStore {
+  std::vector<std::pair<uint64_t, DescSet*>> sets;
+  DescSet* find(uint64_t key) {
+    for (auto& e : sets)
+      if (e.first == key) return e.second;
+    return nullptr;
+  }
+  ~DescStore() {
+    for (auto& e : sets) delete e.second;
+  }
+};
+
+int ptz_desc_put(int device, uint64_t key, int64_t n, int32_t dim, const float* des) {
+  if (n < 0 || dim <= 0 || (n > 0 && !des)) return fail("ptz_desc_put: bad arguments n=%lld dim=%d", (long long)n, dim);
+  if (select_device(device)) return -1;
+  auto guard = device_work_lock(device);
+  DescStore& S = work_for<DescStore>(device);
+  DescSet* d = S.find(key);
+  if (!d) {
+    d = new DescSet;
+    S.sets.emplace_back(key, d);
+  }
+  if (d->buf.reserve((size_t)std::max<int64_t>(n, 1) * dim * 4)) return -1;
+  d->n = n;
+  d->dim = dim;
+  if (n) HIPCHK(hipMemcpy(d->buf.p, des, (size_t)n * dim * 4, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int ptz_desc_drop(int device, int32_t n_keys, const uint64_t* keys) {
+  if (n_keys < 0 || (n_keys > 0 && !keys)) return fail("ptz_desc_drop: bad arguments");
+  if (select_device(device)) return -1;
+  auto guard = device_work_lock(device);
+  DescStore& S = work_for<DescStore>(device);
+  for (int32_t k = 0; k < n_keys; ++k)
+    for (size_t q = 0; q < S.sets.size(); ++q)
+      if (S.sets[q].first == keys[k]) {
+        delete S.sets[q].second;
+        S.sets.erase(S.sets.begin() + q);
+        break;
+      }
+  return 0;
+}
+
+int ptz_match_knn2_sets(int device, int32_t n_sets, const uint64_t* query_keys, uint64_t train_key, int64_t n_rows,
+                        int32_t* idx_out, float* dist_out) {
+  if (n_sets < 0 || (n_sets > 0 && (!query_keys || !idx_out || !dist_out))) return fail("ptz_match_knn2_sets: bad arguments");
+  if (select_device(device)) return -1;
+  auto guard = device_work_lock(device);
+  DescStore& S = work_for<DescStore>(device);
+  const DescSet* tr = S.find(train_key);
+  if (!tr) return fail("ptz_match_knn2_sets: no descriptor set under train key %llu", (unsigned long long)train_key);
+  const int32_t dim = tr->dim;
+  const int64_t n2 = tr->n;
+  int64_t n1 = 0;
+  for (int32_t q = 0; q < n_sets; ++q) {
+    const DescSet* d = S.find(query_keys[q]);
+    if (!d) return fail("ptz_match_knn2_sets: no descriptor set under query key %llu", (unsigned long long)query_keys[q]);
+    if (d->n > 0 && d->dim != dim) return fail("ptz_match_knn2_sets: query set %d has dim %d, train %d", q, d->dim, dim);
+    n1 += d->n;
+  }
+  if (n1 != n_rows) return fail("ptz_match_knn2_sets: the query sets hold %lld rows, the output %lld", (long long)n1, (long long)n_rows);
+  if (n1 == 0) return 0;
+  if (n1 * n2 > ((int64_t)1 << 31)) return fail("distance matrix %lld x %lld too large", (long long)n1, (long long)n2);
+  if (n2 == 0) {
+    for (int64_t i = 0; i < n1; ++i) {
+      idx_out[2 * i] = idx_out[2 * i + 1] = -1;
+      dist_out[2 * i] = dist_out[2 * i + 1] = INFINITY;
+    }
+    return 0;
+  }
+  struct KnnSetsWork {
+    DBuf a, d, idx, dist;
+  };
+  KnnSetsWork& Wk = work_for<KnnSetsWork>(device);
+  if (Wk.a.reserve((size_t)n1 * dim * 4) || Wk.d.reserve((size_t)n1 * n2 * 4) || Wk.idx.reserve((size_t)n1 * 8) ||
+      Wk.dist.reserve((size_t)n1 * 8))
+    return -1;
+  int64_t o = 0;
+  for (int32_t q = 0; q < n_sets; ++q) {
+    const DescSet* d = S.find(query_keys[q]);
+    if (d->n) HIPCHK(hipMemcpyAsync(Wk.a.as<char>() + o * dim * 4, d->buf.p, (size_t)d->n * dim * 4, hipMemcpyDeviceToDevice, nullptr));
+    o += d->n;
+  }
+  hipLaunchKernelGGL(k_sqdist, dim3((unsigned)((n2 + KT - 1) / KT), (unsigned)((n1 + KT - 1) / KT)), dim3(256), 0, nullptr,
+                     (int)n1, (int)n2, dim, Wk.a.as<float>(), tr->buf.as<float>(), Wk.d.as<float>());
+  hipLaunchKernelGGL(k_top2, dim3((unsigned)((n1 + 3) / 4)), dim3(256), 0, nullptr, (int)n1, (int)n2, Wk.d.as<float>(),
+                     Wk.idx.as<int>(), Wk.dist.as<float>());
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(idx_out, Wk.idx.p, (size_t)n1 * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(dist_out, Wk.dist.p, (size_t)n1 * 8, hipMemcpyDeviceToHost));
   return 0;
 }
 

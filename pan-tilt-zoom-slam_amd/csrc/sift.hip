@@ -16,6 +16,10 @@
 //               adds of one wave), normalise / clip / renormalise / round by the wave
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -442,6 +446,15 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
   if (width < 8 || height < 8 || !img || !n_out) return fail("bad image");
   if (max_kp < 0 || (max_kp > 0 && (!kp_out || !des_out))) return fail("bad output buffers");
   if (select_device(device)) return -1;
+  // PTZ_SIFT_TIMING=1: host-side phase times of this call on stderr (where a 1080p detection spends its ~2 ms)
+  static const bool st_on = getenv("PTZ_SIFT_TIMING") != nullptr;
+  auto st_t0 = std::chrono::steady_clock::now();
+  auto st_mark = [&](const char* what) {
+    if (!st_on) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "sift %-18s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - st_t0).count());
+    st_t0 = t;
+  };
   const int W0 = 2 * width, H0 = 2 * height;
   const int n_oct = (int)std::nearbyint(std::log2((double)std::min(W0, H0)) - 2);
   if (n_oct < 1) return fail("image too small");
@@ -491,6 +504,7 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
   for (int o = 0; o < n_oct; ++o)
     for (int i = 0; i < SIFT_S + 3; ++i) gptr[o * (SIFT_S + 3) + i] = G + goff[o] + (int64_t)i * ow[o] * oh[o];
   HIPCHK(hipMemcpy(dptr.p, gptr.data(), gptr.size() * sizeof(float*), hipMemcpyHostToDevice));
+  st_mark("setup+upload");
   // PTZ_SIFT_BLUR2=1: both blur passes and the DoG in one launch (A/B knob, read per call; measured 2.29 vs 2.23 ms
   // per 1080p frame against the two-pass form, tools/sift_bench.py r04i -- the LDS-staged passes were not bound by
   // the intermediate image's traffic)
@@ -536,8 +550,10 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
                          dim3(64), 0, nullptr, o, w, h, Dg + doff[o], thr, dcand.as<SiftCand>(), dcnt.as<int>(), CAP);
   }
   HIPCHK(hipGetLastError());
+  st_mark("pyramid queued");
   int cnt[2];
   HIPCHK(hipMemcpy(cnt, dcnt.p, 8, hipMemcpyDeviceToHost));
+  st_mark("pyramid+extrema");
   if (cnt[0] > CAP) return fail("%d SIFT extrema exceed the candidate list (%d)", cnt[0], CAP);
   const int nc = cnt[0];
   if (nc > 0)
@@ -550,12 +566,14 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
   const int nk = cnt[1];
   std::vector<SiftKp> kps(nk);
   if (nk) HIPCHK(hipMemcpy(kps.data(), dkp.p, (size_t)nk * sizeof(SiftKp), hipMemcpyDeviceToHost));
+  st_mark("orientation");
   std::stable_sort(kps.begin(), kps.end(), [](const SiftKp& a, const SiftKp& b) {
     if (a.response != b.response) return a.response > b.response;
     if (a.y != b.y) return a.y < b.y;
     if (a.x != b.x) return a.x < b.x;
     return a.angle < b.angle;
   });
+  st_mark("sort");
   int n = nk;
   if (nfeatures > 0) n = std::min(n, (int)nfeatures);
   *n_out = n;
@@ -567,6 +585,7 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
                      (const float* const*)dptr.p, dow.as<int>(), doh.as<int>(), ddes.as<float>());
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(des_out, ddes.p, (size_t)n * 128 * 4, hipMemcpyDeviceToHost));
+  st_mark("descriptors");
   for (int i = 0; i < n; ++i) {
     kp_out[4 * i] = kps[i].x;
     kp_out[4 * i + 1] = kps[i].y;

@@ -54,7 +54,7 @@ def detect_compute_orb(im, nfeatures=1000, verbose=False):
     assert isinstance(im, np.ndarray)
     assert nfeatures > 0
     kp, des = ptzba.orb(_grey_u8(im), int(nfeatures), "orb")
-    key_point = [KeyPoint(k[0], k[1], k[2], k[3], k[4], int(k[5])) for k in kp]
+    key_point = [KeyPoint(k[0], k[1], k[2], k[3], k[4], int(k[5])) for k in np.asarray(kp).tolist()]
     if len(key_point) > nfeatures:
         key_point = key_point[:nfeatures]
         des = des[:nfeatures]
@@ -70,7 +70,7 @@ def detect_compute_latch(im, nfeatures=1500, verbose=False):
     import ptzba
     assert isinstance(im, np.ndarray)
     kp, des = ptzba.orb(_grey_u8(im), int(nfeatures) if nfeatures > 0 else 500, "latch")
-    key_point = [KeyPoint(k[0], k[1], k[2], k[3], k[4], int(k[5])) for k in kp]
+    key_point = [KeyPoint(k[0], k[1], k[2], k[3], k[4], int(k[5])) for k in np.asarray(kp).tolist()]
     if nfeatures > 0 and len(key_point) > nfeatures:
         key_point = key_point[:nfeatures]
         des = des[:nfeatures]
@@ -84,7 +84,8 @@ def detect_compute_sift(im, nfeatures, verbose=False):
     .pt, .size, .angle, .response) strongest first, at most nfeatures (> 0), and descriptors [n, 128] float32."""
     import ptzba
     kp, resp, des = ptzba.sift(_grey_u8(im), int(nfeatures))
-    key_point = [KeyPoint(k[0], k[1], k[2], k[3], r) for k, r in zip(kp, resp)]
+    # (rows as Python floats first: per-element numpy scalar indexing costs ~1 us a keypoint)
+    key_point = [KeyPoint(x, y, sz, an, r) for (x, y, sz, an), r in zip(kp[:, :4].tolist(), np.asarray(resp).tolist())]
     if verbose:
         print('detect: %d SIFT keypoints.' % len(key_point))
     return key_point, des
@@ -154,32 +155,42 @@ def _pts(kp, index):
     return np.array([kp[i].pt for i in index], np.float64).reshape(-1, 2)
 
 
-def match_sift_features_batch(pairs):
+def match_sift_features_batch(pairs, dev_sets=None):
     """match_sift_features for several descriptor pairs in three launches instead of five per pair: `pairs` is a
     list of (keypoints1, descriptors1, keypoints2, descriptors2) -- keypoints as KeyPoint lists or [n, 2] arrays of
     their .pt; pairs sharing the same train set (descriptors2
     object) run as ONE kNN-2 over their concatenated queries (a new keyframe against every overlapping window
     partner), the ratio test per pair, then ONE batched homography RANSAC (ptz_homography_ransac_batch, per pair
     the same seed and result as homography_ransac).  Returns [(index1 list, index2 list)] with exactly
-    match_sift_features' (index1, index2) per pair (empty lists where it returns none)."""
+    match_sift_features' (index1, index2) per pair (empty lists where it returns none).
+    dev_sets: optional [((query set id, rows), (train set id, rows))] per pair -- the descriptors already on the
+    device (ptzba.desc_put, correspondence.CorrespondenceCache.dev_set): the kNN-2 then reads them there
+    (ptzba.match_knn2_sets, the same result) instead of concatenating and uploading every query set again."""
     import ptzba
     out = [([], []) for _ in pairs]
     groups = {}
     for q, (_, d1, _, d2) in enumerate(pairs):
-        groups.setdefault(id(d2), []).append(q)
+        groups.setdefault(dev_sets[q][1][0] if dev_sets is not None else id(d2), []).append(q)
     cand = []  # (pair, index1, index2, pts1, pts2)
     for qs in groups.values():
-        d2 = np.asarray(pairs[qs[0]][3], dtype=np.float32)
-        d1s = [np.asarray(pairs[q][1], dtype=np.float32) for q in qs]
-        lens = [len(d) for d in d1s]
-        if sum(lens) == 0:
-            continue
-        idx, dist = ptzba.match_knn2(np.concatenate(d1s), d2)
+        n2 = dev_sets[qs[0]][1][1] if dev_sets is not None else len(pairs[qs[0]][3])
+        if dev_sets is not None:
+            lens = [dev_sets[q][0][1] for q in qs]
+            if sum(lens) == 0:
+                continue
+            idx, dist = ptzba.match_knn2_sets([dev_sets[q][0][0] for q in qs], lens, dev_sets[qs[0]][1][0])
+        else:
+            d2 = np.asarray(pairs[qs[0]][3], dtype=np.float32)
+            d1s = [np.asarray(pairs[q][1], dtype=np.float32) for q in qs]
+            lens = [len(d) for d in d1s]
+            if sum(lens) == 0:
+                continue
+            idx, dist = ptzba.match_knn2(np.concatenate(d1s), d2)
         o = 0
         for q, n1 in zip(qs, lens):
             di, ii = dist[o:o + n1], idx[o:o + n1]
             o += n1
-            good = np.flatnonzero(di[:, 0] < 0.7 * di[:, 1]) if len(d2) >= 2 else np.zeros(0, np.int64)
+            good = np.flatnonzero(di[:, 0] < 0.7 * di[:, 1]) if n2 >= 2 else np.zeros(0, np.int64)
             if len(good) <= 8:
                 print('warning: match sift features failed, not enough matching')
                 continue

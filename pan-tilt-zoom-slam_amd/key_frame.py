@@ -35,27 +35,47 @@ class KeyFrame:
         self._lazy = None
         self._pts = np.ndarray(0)
         self._des = np.ndarray(0)
-        self.landmark_index = []
+        self._lmi = []
         self.pan, self.tilt, self.f = pan, tilt, f
         self.center = center
         self.base_rotation = rotation
         self.u = u
         self.v = v
 
-    # feature_pts / feature_des: plain attributes as in the reference; bundle_adjustment hands them over as (all
-    # keypoints, all descriptors, selected indices) and the subset is taken on first use -- a 30-keyframe window
-    # re-creates every keyframe per BA call, and most of them are never read before the next call replaces them
-    def set_features_lazy(self, keypoints, descriptors, index):
-        self._lazy = (keypoints, descriptors, np.asarray(index, np.int64))
+    # feature_pts / feature_des / landmark_index: plain attributes as in the reference; bundle_adjustment hands them
+    # over as (all keypoints, all descriptors, a provider of the call's per-keyframe (local, global) lists in the
+    # reference's set() order, this keyframe's position), and the lists are formed on first use -- a 30-keyframe
+    # window re-creates every keyframe per BA call, and in a stream most are replaced before anything reads them
+    def set_features_lazy(self, keypoints, descriptors, provider, position=None):
+        """provider: an index array (this keyframe's selected features, no landmark ids) or an object whose
+        lists(position) returns (local index array, global landmark id array)."""
+        self._lazy = (keypoints, descriptors, provider, position)
 
     def _materialise(self):
-        kps, des, idx = self._lazy
+        kps, des, prov, pos = self._lazy
         self._lazy = None
+        if pos is None:
+            idx = np.asarray(prov, np.int64)
+        else:
+            idx, glo = prov.lists(pos)
+            self._lmi = glo.astype(np.int32)
         if isinstance(kps, np.ndarray):
             self._pts = np.asarray(kps)[idx]
         else:
             self._pts = list(map(kps.__getitem__, idx.tolist()))
         self._des = np.asarray(des).take(idx, axis=0)
+
+    @property
+    def landmark_index(self):
+        if self._lazy is not None:
+            self._materialise()
+        return self._lmi
+
+    @landmark_index.setter
+    def landmark_index(self, value):
+        if self._lazy is not None:
+            self._materialise()
+        self._lmi = value
 
     @property
     def feature_pts(self):
@@ -82,7 +102,9 @@ class KeyFrame:
         self._des = value
 
     def get_feature_num(self):
-        return len(self._lazy[2]) if self._lazy is not None else len(self._pts)
+        if self._lazy is not None:
+            self._materialise()
+        return len(self._pts)
 
     def convert_keypoint_to_array(self, norm=True):
         """key_frame.py:59-73."""

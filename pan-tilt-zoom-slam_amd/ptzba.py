@@ -133,6 +133,9 @@ def lib():
         "ptzba_plan_summary": ([I32, I32, V, I32, V], I),
         "ptzba_plan_export": ([I32, I32, V, I32, V, V, I64, V, I64, V], I),
         "ptz_match_knn2": ([I, I64, I64, I32, V, V, V, V], I),
+        "ptz_desc_put": ([I, ctypes.c_uint64, I64, I32, V], I),
+        "ptz_desc_drop": ([I, I32, V], I),
+        "ptz_match_knn2_sets": ([I, I32, V, ctypes.c_uint64, I64, V, V], I),
         "ptz_homography_ransac": ([I, I64, V, V, D, I32, ctypes.c_uint64, V, V, POINTER(c_int32)], I),
         "ptz_homography_ransac_batch": ([I, I32, V, V, V, D, I32, ctypes.c_uint64, V, V, V], I),
         "ptz_lk_track": ([I, I32, I32, V, V, I64, V, I32, I32, I32, D, D, V, V, V], I),
@@ -197,7 +200,7 @@ EXPORTED_SYMBOLS = [
     "ptzba_comm_delete", "ptzba_comm_split", "ptzba_comm_info", "ptzba_comm_allreduce", "ptzba_attach_comm",
     "ptzba_dist_info", "ptzba_owned_frames", "ptz_corner_min_eig", "ptz_orb", "ptzba_plan_summary",
     "ptzba_plan_export", "ptzba_dist_exchanges", "ptzba_dist_groups", "ptzba_exchange_group", "ptzba_dist_plan_summary",
-    "ptzba_dist_rank_phases", "ptzba_dist_plan_export",
+    "ptzba_dist_rank_phases", "ptzba_dist_plan_export", "ptz_desc_put", "ptz_desc_drop", "ptz_match_knn2_sets",
 ]
 
 
@@ -295,6 +298,42 @@ def match_knn2(des1, des2, device=None):
     if n1:
         _check(lib().ptz_match_knn2(default_device() if device is None else device, n1, len(d2), d1.shape[1], _ptr(d1),
                                     _ptr(d2), _ptr(idx), _ptr(dist)), "ptz_match_knn2")
+    return idx, dist
+
+
+def desc_put(key, des, device=None):
+    """Upload descriptor rows (fp32 [n, dim]) under integer `key` on the device, kept for match_knn2_sets."""
+    d = np.ascontiguousarray(des, dtype=np.float32)
+    if d.ndim != 2:
+        raise ValueError("descriptor array must be [n, dim]")
+    _check(lib().ptz_desc_put(default_device() if device is None else device, int(key), len(d), max(d.shape[1], 1),
+                              _ptr(d)), "ptz_desc_put")
+
+
+def desc_put_new(key, des, device=None):
+    """desc_put, returning the number of rows uploaded."""
+    d = np.ascontiguousarray(des, dtype=np.float32).reshape(len(des), -1) if len(des) else np.zeros((0, 1), np.float32)
+    desc_put(key, d, device)
+    return len(d)
+
+
+def desc_drop(keys, device=None):
+    """Free the device descriptor sets under `keys` (unknown keys are ignored)."""
+    k = np.ascontiguousarray(list(keys), dtype=np.uint64)
+    if len(k):
+        _check(lib().ptz_desc_drop(default_device() if device is None else device, len(k), _ptr(k)), "ptz_desc_drop")
+
+
+def match_knn2_sets(query_keys, query_lens, train_key, device=None):
+    """match_knn2 of the concatenated device descriptor sets `query_keys` (row counts `query_lens`, as uploaded)
+    against the set `train_key`: (idx [n1, 2] int32, dist [n1, 2] float32), bit for bit match_knn2's."""
+    qk = np.ascontiguousarray(list(query_keys), dtype=np.uint64)
+    n1 = int(sum(query_lens))
+    idx = np.empty((n1, 2), np.int32)
+    dist = np.empty((n1, 2), np.float32)
+    if n1:
+        _check(lib().ptz_match_knn2_sets(default_device() if device is None else device, len(qk), _ptr(qk),
+                                         int(train_key), n1, _ptr(idx), _ptr(dist)), "ptz_match_knn2_sets")
     return idx, dist
 
 
@@ -511,7 +550,7 @@ def py_shuffle_prefix(lens, keep, rand=None):
     lens = np.ascontiguousarray(lens, dtype=np.int64)
     out = np.empty(int(np.minimum(lens, keep).sum()), np.int64)
     _check(lib().ptz_py_shuffle_prefix(_ptr(mt), len(lens), _ptr(lens), int(keep), _ptr(out)), "ptz_py_shuffle_prefix")
-    rand.setstate((version, tuple(int(x) for x in mt), gauss))
+    rand.setstate((version, tuple(mt.tolist()), gauss))
     return out
 
 

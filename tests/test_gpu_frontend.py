@@ -100,6 +100,27 @@ def test_match_sift_features_batch_equals_per_pair(gpu_available):
         _, i1, _, i2 = image_process.match_sift_features(k1, d1, k2, d2)
         assert list(a) == list(i1) and list(b) == list(i2)
     assert len(got[3][0]) > 300 and got[5] == ([], [])
+    # the same pairs with their descriptors resident on the device (ptz_desc_put / ptz_match_knn2_sets): identical
+    import ptzba
+    ids = {}
+
+    def dev(d):
+        if id(d) not in ids:
+            ids[id(d)] = (1000 + len(ids), ptzba.desc_put_new(1000 + len(ids), d))
+        return ids[id(d)]
+    try:
+        got_dev = image_process.match_sift_features_batch(pairs, dev_sets=[(dev(p[1]), dev(p[3])) for p in pairs])
+        assert got_dev == got
+        idx, dist = ptzba.match_knn2(np.concatenate([pairs[0][1], pairs[1][1]]), dn)
+        idx2, dist2 = ptzba.match_knn2_sets([ids[id(pairs[0][1])][0], ids[id(pairs[1][1])][0]],
+                                            [len(pairs[0][1]), len(pairs[1][1])], ids[id(dn)][0])
+        assert np.array_equal(idx, idx2) and np.array_equal(dist, dist2)
+        with pytest.raises(ptzba.PtzbaError):  # a row count that disagrees with the resident sets
+            ptzba.match_knn2_sets([ids[id(pairs[0][1])][0]], [len(pairs[0][1]) + 1], ids[id(dn)][0])
+    finally:
+        ptzba.desc_drop([v[0] for v in ids.values()])
+    with pytest.raises(ptzba.PtzbaError):  # dropped
+        ptzba.match_knn2_sets([1000], [len(pairs[0][1])], 1001)
 
 
 def test_homography_ransac_hook_signature(gpu_available):
