@@ -74,6 +74,8 @@ struct ptzba_ctx {
   double* scal_host = nullptr;   // pinned host copy of scal_pack
   DBuf chol_tasks, Ldiag, Minv, dpose;  // Minv: inverses of the diagonal factor tiles (back-substitution)
   std::vector<int> chol_task_off;  // host: per elimination level, offsets into chol_tasks
+  DBuf Lsub;                       // supercolumn plans: L_k+1,k of each pair until the next level copies it (chol_super)
+  bool chol_super = false;
   std::vector<int32_t> chol_tasks_host;  // host copy of chol_tasks (int4 records)
   DBuf tinv_tail;                        // diagonal tiles inverted after the factorisation
   int n_tinv_tail = 0;
@@ -593,6 +595,7 @@ struct CholPlan {
   std::vector<int32_t> tinv_tail;  // diagonal tiles inverted after the last level (the others: type-2 tasks)
   int n_levels = 0;
   bool delayed = false;  // tasks carry a second pair of update panels (delayed trailing updates, make_plan)
+  int n_super = 0;       // supercolumn pairs (chol_super tasks: the factorisation needs the Lsub buffer)
   // blocked back substitution (large systems): tasks of 3 int4 (block columns | {p, intra-block coupling
   // bits, first-touch bits, 0} | {target column, flags, 0, 0}) and the task offset of each step (one launch
   // per step); empty when no valid schedule exists
@@ -733,8 +736,12 @@ struct TreeSpec {
 };
 static int tile_owner(int i, int j, int nr) { return (i + j) % nr; }
 static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<int32_t>& win, int64_t ld, CholPlan& P,
-                      int force_dt = 0, TreeSpec* ts = nullptr) {
+                      int force_dt = 0, TreeSpec* ts = nullptr, int super_mode = -1) {
   const bool xcd_order = getenv_is("PTZBA_CHOL_XCD", "1");
+  // supercolumns (chol_super): two consecutive columns of a chain in one level -- single-rank plans at DT = 1;
+  // PTZBA_CHOL_SUPER=1 enables (A/B knob, read per plan)
+  if (super_mode < 0) super_mode = getenv_is("PTZBA_CHOL_SUPER", "1") ? 1 : 0;
+  if (ts || xcd_order) super_mode = 0;  // (continuation records must stay right behind their task)
   const int T = (int)(ld / CHOL_NB);
   std::vector<std::vector<uint8_t>> nz(T, std::vector<uint8_t>(T, 0));
   auto mark = [&](int r, int c) {
@@ -779,8 +786,23 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
     count[L]++;
     level[k] = L;
   };
+  // supercolumn pairs (k, k + 1): k + 1 joins k's level when it depends on k and every other column it depends on is
+  // factored before that level (the pair's task applies those panels' last updates inline)
+  std::vector<uint8_t> head(T, 0), tail(T, 0);
   if (!ts) {
-    for (int k = 0; k < T; ++k) place(k, 0);
+    for (int k = 0; k < T; ++k) {
+      if (super_mode && k > 0 && !head[k - 1] && !tail[k - 1] && nz[k][k - 1]) {
+        int lo = 0;
+        for (int p = 0; p < k - 1; ++p)
+          if (nz[k][p]) lo = std::max(lo, level[p] + 1);
+        if (lo <= level[k - 1]) {
+          level[k] = level[k - 1];  // (one unit of the level's four columns with its head)
+          head[k - 1] = tail[k] = 1;
+          continue;
+        }
+      }
+      place(k, 0);
+    }
   } else {
     const int NP = (int)ts->ph_nr.size();
     ts->ph_lv0.assign(NP, 0);
@@ -802,14 +824,21 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
   for (int i = 0; i < T; ++i)
     for (int j = 0; j <= i; ++j)
       if (nz[i][j] && own(i) && own(j)) { P.ztiles.push_back(i); P.ztiles.push_back(j); }
-  const int nL = (int)count.size();
+  int nL = (int)count.size();
   std::vector<std::vector<int>> K(nL);
   for (int k = 0; k < T; ++k)
     if (level[k] >= 0) K[level[k]].push_back(k);
   P.tasks.clear();
+  P.n_super = 0;
   P.level_off.assign(nL + 1, 0);
   auto push = [&](int type, int i, int j, int w) {
     P.tasks.push_back(type); P.tasks.push_back(i); P.tasks.push_back(j); P.tasks.push_back(w);
+  };
+  // continuation record of a task with more than four panels (supercolumn plans, task word w bit 31): right behind
+  // it, a type-2 no-op for its own workgroup (i = -1) whose z / w carry panels 4, 5 / 6, 7 (16 bits each, + 1)
+  auto push_cont = [&](const std::vector<int>& pd) {
+    auto pk = [&](size_t a) { return a < pd.size() ? pd[a] + 1 : 0; };
+    push(2, -1, pk(4) | (pk(5) << 16), pk(6) | (pk(7) << 16));
   };
   // inverses of the diagonal factor tiles (for the back-substitution): the tiles of level L-1's columns are
   // inverted by type-2 tasks of level L, beside its panels (off the critical path); the last level's after
@@ -834,6 +863,7 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
   if (force_dt) DT = force_dt;
   P.delayed = DT > 1;
   size_t max_pd = 0;  // update panels of one task: the P2 kernel takes up to four (any DT), the other two
+  bool super_over = false;  // a supercolumn task with more than eight panels
   bool any_block = false;  // 2 x 2 trailing blocks (type 3) run in the P2 kernel only
   auto pack2 = [](int type, const std::vector<int>& pd, int tm) {  // int4 task: x (type + panels 2, 3), w (0, 1)
     return std::make_pair(chol_pack_type(type, pd.size() > 2 ? pd[2] : -1, pd.size() > 3 ? pd[3] : -1, (tm >> 2) & 3),
@@ -851,7 +881,24 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
     if (L > 0)
       for (int l = last_trailing; l < L; ++l) inl.insert(inl.end(), K[l].begin(), K[l].end());
     for (int k : K[L]) {
+      if (tail[k]) continue;  // factored by its head's supercolumn tasks
       std::vector<int> pd;
+      if (head[k]) {  // supercolumn (k, k + 1): the diagonal task (i = k) and one task per row tile below k + 1
+        for (int pp : inl)
+          if (pp < k && (nz[k][pp] || nz[k + 1][pp])) pd.push_back(pp);
+        // panels 5..8 (a separator's first pair after four leaf pairs) ride in a continuation record right behind the
+        // task: a type-2 no-op for its own workgroup (i = -1), z / w = panels 4, 5 / 6, 7 (16 bits each)
+        if (pd.size() > 8) super_over = true;
+        const std::vector<int> pd4(pd.begin(), pd.begin() + std::min<size_t>(4, pd.size()));
+        for (int i = k; i < T; ++i) {
+          if (i == k + 1 || !(i == k || nz[i][k] || nz[i][k + 1]) || !own(i)) continue;
+          const auto w = pack2(0, pd4, 15);
+          push(w.first, i, k, (int)((unsigned)w.second | (1u << 30) | (pd.size() > 4 ? 1u << 31 : 0u)));
+          if (pd.size() > 4) push_cont(pd);
+        }
+        P.n_super++;
+        continue;
+      }
       for (int pp : inl)
         if (pp < k && nz[k][pp]) pd.push_back(pp);
       for (int i = k; i < T; ++i) {
@@ -898,7 +945,9 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
       while (y < upd.size() && upd[y].first == upd[x].first) ++y;
       std::vector<int> pd;
       for (size_t u = x; u < y; ++u) pd.push_back(upd[u].second);
-      max_pd = std::max(max_pd, pd.size());
+      // (supercolumn plans: a trailing tile takes up to eight panels, 5..8 in a continuation record)
+      if (super_mode && pd.size() > 4) super_over = super_over || pd.size() > 8;
+      else max_pd = std::max(max_pd, pd.size());
       tiles_pd.push_back({upd[x].first, pd});
       x = y;
     }
@@ -930,30 +979,50 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
     for (size_t q = 0; q < tiles_pd.size(); ++q) {
       if (in_block[q]) continue;
       const int i = (int)(tiles_pd[q].first / T), j = (int)(tiles_pd[q].first % T);
-      const auto w = pack2(1, tiles_pd[q].second, 15);
-      push(w.first, i, j, w.second);
+      const auto& pd = tiles_pd[q].second;
+      const std::vector<int> pd4(pd.begin(), pd.begin() + std::min<size_t>(4, pd.size()));
+      const auto w = pack2(1, pd4, 15);
+      push(w.first, i, j, (int)((unsigned)w.second | (pd.size() > 4 ? 1u << 31 : 0u)));
+      if (pd.size() > 4) push_cont(pd);
     }
-    if (tinv_split)
-      for (int pp : prev)
-        if (pp < n_inv) push(2, pp, pp, 0);
+    // type 2: inverses of the previous level's diagonal tiles; a supercolumn head's task also copies L_k+1,k from
+    // Lsub into the factor (w bit 0; bit 1: copy only)
+    for (int pp : prev) {
+      const bool inv = tinv_split && pp < n_inv;
+      if (head[pp]) push(2, pp, pp, inv ? 1 : 3);
+      else if (inv) push(2, pp, pp, 0);
+    }
     if (xcd_order) xcd_interleave(P.tasks, P.level_off[L]);  // PTZBA_CHOL_XCD=1 (read per plan)
   }
   for (int k = 0; k < n_inv && k < T; ++k)
     if (own(k) && (!tinv_split || level[k] == nL - 1)) P.tinv_tail.push_back(k);
   P.level_off[nL] = (int)(P.tasks.size() / 4);
+  bool last_pairs = false;
+  if (nL > 0)
+    for (int k : K[nL - 1]) last_pairs = last_pairs || head[k];
+  if (last_pairs) {  // the last level's supercolumns: one more level copies their L_k+1,k (the inverses stay in tinv_tail)
+    for (int k : K[nL - 1])
+      if (head[k]) push(2, k, k, 3);
+    ++nL;
+    P.level_off.push_back((int)(P.tasks.size() / 4));
+  }
   P.n_levels = nL;
   if (getenv("PTZBA_PLAN_DEBUG")) {  // per level: columns, tasks (panel / trailing / inverse)
     for (int L = 0; L < nL; ++L) {
       int n[3] = {0, 0, 0};
       for (int q = P.level_off[L]; q < P.level_off[L + 1]; ++q) n[P.tasks[4 * q] & 3]++;
       fprintf(stderr, "level %d cols", L);
-      for (int k : K[L]) fprintf(stderr, " %d", k);
+      if (L < (int)K.size())
+        for (int k : K[L]) fprintf(stderr, " %d%s", k, head[k] ? "+" : "");
       fprintf(stderr, " | panel %d trailing %d inv %d\n", n[0], n[1], n[2]);
     }
     fprintf(stderr, "max panels per task %zu\n", max_pd);
   }
-  if (max_pd > 4) return DT > 1 ? make_plan(o, n_pose, nf, win, ld, P, 1, ts) : false;  // too many panels: DT = 1
-  if (max_pd > 2 || any_block) P.delayed = true;  // the P2 kernel (second panel pair, trailing blocks) also at DT = 1
+  if (max_pd > 4 || super_over) {  // too many panels: DT = 1, then no supercolumns
+    if (DT > 1) return make_plan(o, n_pose, nf, win, ld, P, 1, ts, super_mode);
+    return super_mode ? make_plan(o, n_pose, nf, win, ld, P, force_dt, ts, 0) : false;
+  }
+  if (max_pd > 2 || any_block || P.n_super) P.delayed = true;  // the P2 kernel (second panel pair, trailing blocks, pairs)
   // back-substitution: chains of tile columns holding unknowns and, per chain position, the chain's
   // later columns coupled to that row tile (right-looking updates).  Nested orders: one chain per leaf of
   // the separator tree (its root-to-leaf path, each node's columns descending); natural: one chain.
@@ -1700,6 +1769,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->n_tinv_tail = (int)plan.tinv_tail.size();
   h->chol_levels = plan.n_levels;
   h->chol_delayed = plan.delayed;
+  h->chol_super = plan.n_super > 0;
   h->n_chain = (int)plan.chain_off.size() - 1;
   frame_win_hi = win;  // K2 windows follow the same (possibly global) coupling
   h->perm_host = order;
@@ -1756,6 +1826,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       h->lm_red.alloc((size_t)n_landmark * 4 * 8) || h->sys.alloc((size_t)h->sys_count() * 8) ||
       h->scal.alloc(2 * PTZBA_NSCALARS * 8) || h->red_scratch.alloc(RED_SCRATCH * 8) || h->info.alloc(16) ||
       h->Ldiag.alloc((size_t)h->ld * CHOL_NB * 8) || h->Minv.alloc((size_t)h->ld * CHOL_NB * 8) ||
+      (h->chol_super && h->Lsub.alloc((size_t)h->ld * CHOL_NB * 8)) ||
       h->dpose.alloc((size_t)h->ld * 8) ||
       h->s2_part.alloc((size_t)std::max(h->n_s2_items, 1) * (h->s2_pair ? 2 : 1) * SCHUR_F1 * 9 * WAVE * 8) ||
       h->part_diag.alloc((size_t)std::max(h->n_s2_items, 1) * SCHUR_F1 * 12 * 8))
@@ -1809,7 +1880,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   // single-launch factorisation (PTZBA_CHOL_PERSIST=1, A/B knob): single-process SPD solves
   h->no_fused_prep = getenv("PTZBA_NO_FUSED_PREP") != nullptr;
   h->chol_pst = !part_mode && !dist && (getenv_is("PTZBA_CHOL_PERSIST", "1") || getenv_is("PTZBA_CHOL_PERSIST", "2")) &&
-                plan.n_levels > 0;
+                plan.n_levels > 0 && !h->chol_super;
   h->chol_pst_ticket = !getenv_is("PTZBA_CHOL_PERSIST", "2");
   h->chol_epoch = 0;
   if (h->chol_pst) {
@@ -2209,7 +2280,7 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
     } else
       launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
                       h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>(), 0,
-                      h->chol_delayed);
+                      h->chol_delayed, h->chol_super ? h->Lsub.as<double>() : nullptr);
   }
   if (h->bs_pst)
     launch_chol_backsolve_pst(h->S(), h->ld, h->n_aug, h->bsb_tasks.as<int4>(), h->bsp_expect.as<int4>(),

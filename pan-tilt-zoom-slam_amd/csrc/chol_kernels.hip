@@ -846,12 +846,134 @@ struct CholTaskVal {
   const int4* rest;
   __device__ int4 get(int b) const { return b < CHOL_KT ? t[b] : rest[b - CHOL_KT]; }
 };
+// Supercolumn panel task (api.hip make_plan, PTZBA_CHOL_SUPER): the tile columns k and k + 1 of one chain factored in
+// ONE level -- half the launch boundaries and tile round trips of the chain.  The workgroup of row tile i stages the raw
+// tiles D00 = A_kk, D10 = A_k+1,k, D11 = A_k+1,k+1 (and T0 = A_ik, T1 = A_i,k+1 when i > k + 1), applies the update
+// panels p of the previous levels to all of them (D00 -= L_kp L_kp^T, D10 -= L_k+1,p L_kp^T, D11 -= L_k+1,p L_k+1,p^T,
+// T0 -= L_ip L_kp^T, T1 -= L_ip L_k+1,p^T; panels a tile is not coupled to meet zero tiles), then
+//   sweep 1: L00 = chol(D00) and L10 = D10 L00^-T in one pass (wg_potrf_trsm32_df);
+//   T0: L_i0 = T0 L00^-T by forward substitution (one wave, a lane per row);
+//   D11 -= L10 L10^T, T1 -= L_i0 L10^T (the intra-pair update, never a trailing task's);
+//   sweep 2: L11 = chol(D11) and L_i1 = T1 L11^-T.
+// Every task of the pair factors the 64 x 64 diagonal block itself (as every panel task factors its diagonal tile), so
+// the raw A_kk, A_k+1,k and A_k+1,k+1 stay untouched during the level: the diagonal task (i == k) writes L00 and L11 to
+// Ldiag and L10 to Lsub[k], which the type-2 task of the next level copies into A_k+1,k (no task of that level reads
+// the tile).  Tiles: D00 sD, D10 sC, D11 sE[0], T0 sE[1], T1 sB[1]; panel staging sA[0] (L_kp), sA[1] (L_k+1,p),
+// sB[0] (L_ip); the sweeps' block buffer overlays sA as in chol_task.
+template <bool COH>
+__device__ __forceinline__ void chol_super(double* __restrict__ A, int64_t ld, int i, int k, const int (&ups)[8],
+                                           double* __restrict__ Ldiag, int* info, double* __restrict__ Lsub,
+                                           double (*sD)[NB + 1], double (*sC)[NB + 1], double (*sA)[NB][NB + 1],
+                                           double (*sB)[NB][NB + 1], double (*sE)[NB][NB + 1], double (*s_lb)[2 * NB][LA_BW],
+                                           double (*s_pb)[LA_BW], int* s_flags, double* s_rinv) {
+  const bool diag = i == k;
+  const int64_t NBl = NB;
+  double r0[4], r1[4], r2[4], r3[4], r4[4], p0[4], p1[4], p2[4];
+  fetch_tile<COH>(r0, A + (int64_t)k * NBl * ld + k * NBl, ld);
+  fetch_tile<COH>(r1, A + (int64_t)(k + 1) * NBl * ld + k * NBl, ld);
+  fetch_tile<COH>(r2, A + (int64_t)(k + 1) * NBl * ld + (k + 1) * NBl, ld);
+  if (!diag) {
+    fetch_tile<COH>(r3, A + (int64_t)i * NBl * ld + k * NBl, ld);
+    fetch_tile<COH>(r4, A + (int64_t)i * NBl * ld + (k + 1) * NBl, ld);
+  }
+  auto pfetch = [&](int p) {
+    fetch_tile<COH>(p0, A + (int64_t)k * NBl * ld + p * NBl, ld);
+    fetch_tile<COH>(p1, A + (int64_t)(k + 1) * NBl * ld + p * NBl, ld);
+    if (!diag) fetch_tile<COH>(p2, A + (int64_t)i * NBl * ld + p * NBl, ld);
+  };
+  int u = 0;
+  while (u < 8 && ups[u] < 0) ++u;
+  if (u < 8) pfetch(ups[u]);
+  put_tile(sD, r0);
+  put_tile(sC, r1);
+  put_tile(sE[0], r2);
+  if (!diag) {
+    put_tile(sE[1], r3);
+    put_tile(sB[1], r4);
+  }
+  while (u < 8) {
+    int un = u + 1;
+    while (un < 8 && ups[un] < 0) ++un;
+    put_tile(sA[0], p0);
+    put_tile(sA[1], p1);
+    if (!diag) put_tile(sB[0], p2);
+    if (un < 8) pfetch(ups[un]);  // in flight during this panel's MFMAs
+    __syncthreads();
+    // each wave owns one 16 x 16 block of every output tile: no barrier between the products
+    tile_gemm_nt_sub(sD, sA[0], sA[0]);
+    tile_gemm_nt_sub(sC, sA[1], sA[0]);
+    tile_gemm_nt_sub(sE[0], sA[1], sA[1]);
+    if (!diag) {
+      tile_gemm_nt_sub(sE[1], sB[0], sA[0]);
+      tile_gemm_nt_sub(sB[1], sB[0], sA[1]);
+    }
+    __syncthreads();
+    u = un;
+  }
+  // sweep 1 (its entry barrier orders the staging above): L00 -> block rows 0..31, L10 -> rows 32..63
+  wg_potrf_trsm32_df<LA_BW, false>(sD, sC, s_lb, s_pb, s_flags, info, nullptr);
+  __syncthreads();
+  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+    const int r = e >> 5, m = e & 31;
+    sD[r][m] = m <= r ? s_lb[m / LA_BW][r][m % LA_BW] : 0.0;
+    sC[r][m] = s_lb[m / LA_BW][NB + r][m % LA_BW];
+  }
+  __syncthreads();
+  if (diag) {
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+      gst<COH>(Ldiag + (int64_t)k * NB * NB + e, sD[e >> 5][e & 31]);
+      gst<COH>(Lsub + (int64_t)k * NB * NB + e, sC[e >> 5][e & 31]);
+    }
+  } else {
+    // L_i0 = T0 L00^-T: lane r solves row r, right-looking (x_c final, then every later entry takes its term)
+    if (threadIdx.x < NB) s_rinv[threadIdx.x] = rcp_nr(sD[threadIdx.x][threadIdx.x]);
+    __syncthreads();
+    if (threadIdx.x < NB) {
+      const int r = threadIdx.x;
+      double t[NB];
+#pragma unroll
+      for (int m = 0; m < NB; ++m) t[m] = sE[1][r][m];
+#pragma unroll
+      for (int c = 0; c < NB; ++c) {
+        const double x = t[c] * s_rinv[c];
+        t[c] = x;
+#pragma unroll
+        for (int m = c + 1; m < NB; ++m) t[m] = fma(-sD[m][c], x, t[m]);
+      }
+#pragma unroll
+      for (int m = 0; m < NB; ++m) sE[1][r][m] = t[m];
+    }
+    __syncthreads();
+    tile_gemm_nt_sub(sB[1], sE[1], sC);  // T1 -= L_i0 L10^T
+  }
+  tile_gemm_nt_sub(sE[0], sC, sC);  // D11 -= L10 L10^T
+  // sweep 2 (entry barrier orders the products): L11 -> block rows 0..31, L_i1 -> rows 32..63
+  wg_potrf_trsm32_df<LA_BW, false>(sE[0], diag ? nullptr : sB[1], s_lb, s_pb, s_flags, info, nullptr);
+  __syncthreads();
+  if (diag) {
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+      const int r = e >> 5, m = e & 31;
+      gst<COH>(Ldiag + (int64_t)(k + 1) * NB * NB + e, m <= r ? s_lb[m / LA_BW][r][m % LA_BW] : 0.0);
+    }
+    return;
+  }
+  double* C0 = A + (int64_t)i * NBl * ld + k * NBl;
+  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+    const int r = e >> 5, m = e & 31;
+    gst<COH>(C0 + (int64_t)r * ld + m, sE[1][r][m]);
+    gst<COH>(C0 + (int64_t)r * ld + NB + m, s_lb[m / LA_BW][NB + r][m % LA_BW]);
+  }
+}
+
 // P2: plans with delayed trailing updates (a second pair of update panels per task, api.hip make_plan)
 // One factorisation task (api.hip make_plan: panel / trailing / inverse / trailing block) by the workgroup: the
 // body of a level launch (k_chol_step) and of the persistent form (k_chol_pst, COH = true).
-template <bool SG, bool P2, bool COH>
+template <bool SG, bool P2, bool COH, bool SUP = false>
 __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, const int4 tk, double* __restrict__ Ldiag,
-                                          int* info, double* __restrict__ sgn, double* __restrict__ Minv) {
+                                          int* info, double* __restrict__ sgn, double* __restrict__ Minv,
+                                          double* __restrict__ Lsub = nullptr, int4 tk2 = int4{0, 0, 0, 0}) {
+  static_assert(!SUP || (P2 && !SG && CHOL_WG == 3 && CHOL_LB_ALIAS && CHOL_DIRECT_STORE && !CHOL_FEWER_BARRIERS),
+                "supercolumn tasks: the P2 kernel of SPD plans with the default sweep");
   static_assert(!(COH && SG), "the persistent form factors SPD systems only");
   static_assert(!(COH && CHOL_TRAIL_DIRECT), "the persistent form stages trailing tiles");
   __shared__ double sC[NB][NB + 1];     // target tile (panel T_ik / trailing A_ij)
@@ -883,6 +1005,14 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
   __shared__ double s_sig[NB];     // SG: signs of this column's pivots
   if ((tk.x & 3) == 2) {  // inverse of a diagonal factor tile of the previous level (see tile_inv_wave)
     if (tk.y < 0) return;  // no-op slot of an XCD-ordered level (api.hip xcd_interleave)
+    if constexpr (SUP) {
+      if (tk.w & 1) {  // the previous level's supercolumn k = tk.y: its L_k+1,k from Lsub into the factor
+        double* dst = A + (int64_t)(tk.y + 1) * NB * ld + (int64_t)tk.y * NB;
+        const double* src = Lsub + (int64_t)tk.y * NB * NB;
+        for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) gst<COH>(dst + (int64_t)(e >> 5) * ld + (e & 31), gld<COH>(src + e));
+      }
+      if (tk.w & 2) return;  // copy only (a column without an inverse)
+    }
     __shared__ double s_rinv[NB];
     tile_inv_wave<COH>(Ldiag + (int64_t)tk.y * NB * NB, Minv + (int64_t)tk.y * NB * NB, sD, s_rinv);
     return;
@@ -914,6 +1044,18 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
   if constexpr (P2 && !SG) {
     if (type == 3) {  // 2 x 2 block of trailing tiles (api.hip make_plan): A_ij -= sum_p L_ip L_jp^T
       chol_trail_block<COH>(A, ld, i, j, ((tk.w >> 28) & 3) | (((unsigned)tk.x >> 30) << 2), up0, up1, up2, up3, sA, sB);
+      return;
+    }
+  }
+  if constexpr (SUP) {
+    if (type == 0 && (((unsigned)tk.w >> 30) & 1)) {  // supercolumn panel task (columns j, j + 1)
+      __shared__ double sE[2][NB][NB + 1];
+      __shared__ double s_rinv2[NB];
+      // panels 5..8 from the continuation record (w bit 31)
+      const bool cont = ((unsigned)tk.w >> 31) & 1;
+      const int ups[8] = {up0, up1, up2, up3, cont ? (tk2.z & 0xffff) - 1 : -1, cont ? ((tk2.z >> 16) & 0xffff) - 1 : -1,
+                          cont ? (tk2.w & 0xffff) - 1 : -1, cont ? ((tk2.w >> 16) & 0xffff) - 1 : -1};
+      chol_super<COH>(A, ld, i, j, ups, Ldiag, info, Lsub, sD, sC, sA, sB, sE, s_lb, s_pb, s_flags, s_rinv2);
       return;
     }
   }
@@ -1026,6 +1168,36 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
       __syncthreads();
       if (up2 >= 0) tile_gemm_nt_sub<SG>(sC, sA[0], sB[0], s_sgp[0]);
       if (up3 >= 0) tile_gemm_nt_sub<SG>(sC, sA[1], sB[1], s_sgp[1]);
+    }
+    if constexpr (SUP) {
+      if (((unsigned)tk.w >> 31) & 1) {  // panels 5..8 from the continuation record, two per pass
+        const int ux[4] = {(tk2.z & 0xffff) - 1, ((tk2.z >> 16) & 0xffff) - 1, (tk2.w & 0xffff) - 1,
+                           ((tk2.w >> 16) & 0xffff) - 1};
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const int ua = ux[2 * h2], ub = ux[2 * h2 + 1];
+          if (ua < 0 && ub < 0) continue;
+          if (ua >= 0) {
+            fetch_tile<COH>(w2, A + i * NBl * ld + ua * NBl, ld);
+            fetch_tile<COH>(w3, A + j * NBl * ld + ua * NBl, ld);
+          }
+          if (ub >= 0) {
+            fetch_tile<COH>(w4, A + i * NBl * ld + ub * NBl, ld);
+            fetch_tile<COH>(w5, A + j * NBl * ld + ub * NBl, ld);
+          }
+          __syncthreads();
+          if (ua >= 0) {
+            put_tile(sA[0], w2);
+            put_tile(sB[0], w3);
+          }
+          if (ub >= 0) {
+            put_tile(sA[1], w4);
+            put_tile(sB[1], w5);
+          }
+          __syncthreads();
+          if (ua >= 0) tile_gemm_nt_sub<SG>(sC, sA[0], sB[0], s_sgp[0]);
+          if (ub >= 0) tile_gemm_nt_sub<SG>(sC, sA[1], sB[1], s_sgp[1]);
+        }
+      }
     }
     __syncthreads();
 #if CHOL_VARIANT != 7
@@ -1140,11 +1312,16 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
   for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) gst<COH>(C + (int64_t)(e >> 5) * ld + (e & 31), sC[e >> 5][e & 31]);
 }
 
-template <bool SG, typename TaskArg, bool P2 = false, bool COH = false>
+template <bool SG, typename TaskArg, bool P2 = false, bool COH = false, bool SUP = false>
 __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64_t ld, const TaskArg tasks,
                                                    double* __restrict__ Ldiag, int* info, double* __restrict__ sgn,
-                                                   double* __restrict__ Minv) {
-  chol_task<SG, P2, COH>(A, ld, tasks.get(blockIdx.x), Ldiag, info, sgn, Minv);
+                                                   double* __restrict__ Minv, double* __restrict__ Lsub) {
+  const int4 tk = tasks.get(blockIdx.x);
+  int4 tk2{0, 0, 0, 0};
+  if constexpr (SUP) {  // a continuation record (panels 5..8 of a panel / supercolumn / trailing task) follows it
+    if ((tk.x & 3) <= 1 && ((unsigned)tk.w >> 31)) tk2 = tasks.get(blockIdx.x + 1);
+  }
+  chol_task<SG, P2, COH, SUP>(A, ld, tk, Ldiag, info, sgn, Minv, Lsub, tk2);
 }
 
 // Single-launch form of the level launches (single-process SPD solves): the tasks of levels [L0, L1) in ONE launch of
@@ -1211,17 +1388,19 @@ int launch_cholesky_pst(double* A, int64_t ld, const int4* tasks, const int* tas
 
 template <typename TaskArg, bool COH>
 static void launch_chol_level(const TaskArg& ta, int n, double* A, int64_t ld, double* Ldiag, int* info, double* sgn,
-                              double* Minv, bool delayed, hipStream_t st) {
+                              double* Minv, bool delayed, hipStream_t st, double* Lsub) {
   if (sgn)
-    hipLaunchKernelGGL((k_chol_step<true, TaskArg, false, false>), dim3(n), dim3(256), 0, st, A, ld, ta, Ldiag, info, sgn, Minv);
+    hipLaunchKernelGGL((k_chol_step<true, TaskArg, false, false>), dim3(n), dim3(256), 0, st, A, ld, ta, Ldiag, info, sgn, Minv, Lsub);
+  else if (Lsub)  // plans with supercolumn tasks (always the P2 kernel)
+    hipLaunchKernelGGL((k_chol_step<false, TaskArg, true, COH, true>), dim3(n), dim3(256), 0, st, A, ld, ta, Ldiag, info, sgn, Minv, Lsub);
   else if (delayed)
-    hipLaunchKernelGGL((k_chol_step<false, TaskArg, true, COH>), dim3(n), dim3(256), 0, st, A, ld, ta, Ldiag, info, sgn, Minv);
+    hipLaunchKernelGGL((k_chol_step<false, TaskArg, true, COH>), dim3(n), dim3(256), 0, st, A, ld, ta, Ldiag, info, sgn, Minv, Lsub);
   else
-    hipLaunchKernelGGL((k_chol_step<false, TaskArg, false, COH>), dim3(n), dim3(256), 0, st, A, ld, ta, Ldiag, info, sgn, Minv);
+    hipLaunchKernelGGL((k_chol_step<false, TaskArg, false, COH>), dim3(n), dim3(256), 0, st, A, ld, ta, Ldiag, info, sgn, Minv, Lsub);
 }
 void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_off_host, int n_launch, double* Ldiag,
                      int* info, hipStream_t st, double* sgn, const int4* tasks_host, double* Minv, int first_level,
-                     bool delayed) {
+                     bool delayed, double* Lsub) {
   static const bool by_value = !getenv("PTZBA_CHOL_TASKS_PTR");  // A/B knob
   // SPD factorisations write their tiles through (agent-scope stores) and read them past this XCD's L2: the next
   // level's workgroups, mostly on other XCDs, find the tiles in the Infinity Cache at once (same-box A/B r04e:
@@ -1235,13 +1414,13 @@ void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_o
       CholTaskVal tv;
       std::memcpy(tv.t, tasks_host + task_off_host[L], std::min(n, CHOL_KT) * sizeof(int4));
       tv.rest = tasks + task_off_host[L] + CHOL_KT;
-      if (coh) launch_chol_level<CholTaskVal, true>(tv, n, A, ld, Ldiag, info, sgn, Minv, delayed, st);
-      else launch_chol_level<CholTaskVal, false>(tv, n, A, ld, Ldiag, info, sgn, Minv, delayed, st);
+      if (coh) launch_chol_level<CholTaskVal, true>(tv, n, A, ld, Ldiag, info, sgn, Minv, delayed, st, Lsub);
+      else launch_chol_level<CholTaskVal, false>(tv, n, A, ld, Ldiag, info, sgn, Minv, delayed, st, Lsub);
       continue;
     }
     const CholTaskPtr tp{tasks + task_off_host[L]};
-    if (coh) launch_chol_level<CholTaskPtr, true>(tp, n, A, ld, Ldiag, info, sgn, Minv, delayed, st);
-    else launch_chol_level<CholTaskPtr, false>(tp, n, A, ld, Ldiag, info, sgn, Minv, delayed, st);
+    if (coh) launch_chol_level<CholTaskPtr, true>(tp, n, A, ld, Ldiag, info, sgn, Minv, delayed, st, Lsub);
+    else launch_chol_level<CholTaskPtr, false>(tp, n, A, ld, Ldiag, info, sgn, Minv, delayed, st, Lsub);
   }
 }
 

@@ -567,15 +567,28 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
   std::vector<SiftKp> kps(nk);
   if (nk) HIPCHK(hipMemcpy(kps.data(), dkp.p, (size_t)nk * sizeof(SiftKp), hipMemcpyDeviceToHost));
   st_mark("orientation");
-  std::stable_sort(kps.begin(), kps.end(), [](const SiftKp& a, const SiftKp& b) {
-    if (a.response != b.response) return a.response > b.response;
-    if (a.y != b.y) return a.y < b.y;
-    if (a.x != b.x) return a.x < b.x;
-    return a.angle < b.angle;
-  });
-  st_mark("sort");
+  // strongest first (ties: y, x, angle, then detection order -- a total order, so selecting the first n and sorting
+  // only them gives exactly the stable sort's first n)
   int n = nk;
   if (nfeatures > 0) n = std::min(n, (int)nfeatures);
+  {
+    std::vector<int> ord(nk);
+    for (int i = 0; i < nk; ++i) ord[i] = i;
+    auto before = [&](int ia, int ib) {
+      const SiftKp &a = kps[ia], &b = kps[ib];
+      if (a.response != b.response) return a.response > b.response;
+      if (a.y != b.y) return a.y < b.y;
+      if (a.x != b.x) return a.x < b.x;
+      if (a.angle != b.angle) return a.angle < b.angle;
+      return ia < ib;
+    };
+    if (n < nk) std::nth_element(ord.begin(), ord.begin() + n, ord.end(), before);
+    std::sort(ord.begin(), ord.begin() + n, before);
+    std::vector<SiftKp> top(n);
+    for (int i = 0; i < n; ++i) top[i] = kps[ord[i]];
+    kps.swap(top);
+  }
+  st_mark("sort");
   *n_out = n;
   n = std::min(n, (int)max_kp);
   if (n <= 0) return 0;
