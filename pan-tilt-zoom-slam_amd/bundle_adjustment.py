@@ -28,7 +28,7 @@ import numpy as np
 import image_process
 import ptzba
 from key_frame import KeyFrame
-from util import overlap_pan_angle
+from util import overlap_pan_angle_half_fov
 
 LAST_RESULT = {}
 
@@ -92,13 +92,24 @@ class _KeyframeLists:
     def __init__(self, graph):
         self.graph = graph
         self.csr = None
+        self.used = None
 
     def lists(self, i):
         if self.csr is None:
             self.csr = self.graph.keyframe_features()
             self.graph = None
+            self.used = None
         off, loc, glo = self.csr
         return loc[off[i]:off[i + 1]], glo[off[i]:off[i + 1]]
+
+    def nonempty(self, i):
+        """keyframe i's list is non-empty: it takes part in a match of this call."""
+        if self.csr is not None:
+            return self.csr[0][i + 1] > self.csr[0][i]
+        if self.used is None:
+            g = self.graph
+            self.used = (np.bincount(g.m_i, minlength=g.n_frames) + np.bincount(g.m_j, minlength=g.n_frames)) > 0
+        return bool(self.used[i])
 
 
 def bundle_adjustment(images, image_indices, feature_method, initial_ptzs, center, rotation, u, v, save_path,
@@ -118,13 +129,13 @@ def bundle_adjustment(images, image_indices, feature_method, initial_ptzs, cente
     timing = {}
     t_start = time.time()
 
-    # step 1: pair mask (bundle_adjustment.py:135-144)
-    image_match_mask = [[0 for _ in range(N)] for _ in range(N)]
-    for i in range(N):
-        for j in range(N):
-            if overlap_pan_angle(initial_ptzs[i][2], initial_ptzs[i][0], initial_ptzs[j][2], initial_ptzs[j][0],
-                                 1280) > 5:
-                image_match_mask[i][j] = 1
+    # step 1: pair mask (bundle_adjustment.py:135-144): overlap_pan_angle(f_i, pan_i, f_j, pan_j, 1280) > 5 for every
+    # pair, with each camera's half field of view formed once (the same float operations, so the same mask)
+    half = np.array([overlap_pan_angle_half_fov(fl, 1280) for fl in initial_ptzs[:, 2].tolist()])
+    pan = initial_ptzs[:, 0]
+    overlap = (np.minimum((pan + half)[:, None], (pan + half)[None, :]) -
+               np.maximum((pan - half)[:, None], (pan - half)[None, :]))
+    image_match_mask = (overlap > 5).astype(np.int64).tolist()
     g = correspondence.build_graph(images, image_match_mask, feature_method, verbose, cache=correspondences,
                                    keys=list(image_indices))
     keypoints, descriptors, n_landmark = g.keypoints, g.descriptors, g.n_landmark

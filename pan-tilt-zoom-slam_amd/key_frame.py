@@ -106,6 +106,13 @@ class KeyFrame:
             self._materialise()
         return len(self._pts)
 
+    def has_features(self):
+        """get_feature_num() > 0, answered without forming the lists when they are still pending (a keyframe of a BA
+        call has features iff it takes part in one of the call's matches)."""
+        if self._lazy is not None and self._lazy[3] is not None:
+            return self._lazy[2].nonempty(self._lazy[3])
+        return self.get_feature_num() > 0
+
     def convert_keypoint_to_array(self, norm=True):
         """key_frame.py:59-73."""
         n = len(self.feature_pts)

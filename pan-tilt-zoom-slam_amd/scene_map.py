@@ -71,7 +71,7 @@ class Map:
         self.global_ray = landmarks
         self.keyframe_list = list(kept)
         for i, kf in enumerate(keyframes):
-            if kf.get_feature_num() > 0:
+            if kf.has_features():  # (get_feature_num() > 0 without forming the lists: they are formed on first use)
                 self.keyframe_list.append(kf)
             else:
                 print("warning: key frame, %d, image index %d is not included in the map" % (i, image_indices[i]))

@@ -11,11 +11,15 @@ import numpy as np
 import scipy.io as sio
 
 
+def overlap_pan_angle_half_fov(fl, im_width):
+    """Half horizontal field of view (degrees) of a camera, as overlap_pan_angle forms it per camera."""
+    return math.atan((im_width / 2) / fl) * 180.0 / math.pi
+
+
 def overlap_pan_angle(fl_1, pan_1, fl_2, pan_2, im_width):
     """Overlapped pan angle (degrees) of two cameras, pan only, no wrap-around (util.py:49-72)."""
-    w = im_width / 2
-    d1 = math.atan(w / fl_1) * 180.0 / math.pi
-    d2 = math.atan(w / fl_2) * 180.0 / math.pi
+    d1 = overlap_pan_angle_half_fov(fl_1, im_width)
+    d2 = overlap_pan_angle_half_fov(fl_2, im_width)
     return max(0, min(pan_1 + d1, pan_2 + d2) - max(pan_1 - d1, pan_2 - d2))
 
 

@@ -155,3 +155,40 @@ def test_cache_redetects_changed_image():
         assert cache.n_detect == n0 + 1 and g.n_frames == 2
     finally:
         image_process.detect_compute_sift, image_process.match_sift_features = saved
+
+
+def test_lazy_keyframe_lists_equal_eager_assembly():
+    """bundle_adjustment's keyframes take their feature lists on first use (_KeyframeLists + KeyFrame.set_features_lazy):
+    every keyframe's feature_pts / feature_des / landmark_index then equal the eager assembly of
+    bundle_adjustment.py:214-248 (keyframe_features' set() order), and has_features() == get_feature_num() > 0
+    without forming the lists first.  The vectorised pair mask equals overlap_pan_angle per pair."""
+    import bundle_adjustment
+    import correspondence
+    import image_process
+    from key_frame import KeyFrame
+    sc, det, mat, calls = _scene_frontend()
+    saved = image_process.detect_compute_sift, image_process.match_sift_features
+    image_process.detect_compute_sift, image_process.match_sift_features = det, mat
+    try:
+        n = len(sc.init_ptz)
+        mask = _mask(sc.init_ptz)
+        from util import overlap_pan_angle_half_fov
+        ptz = np.asarray(sc.init_ptz, np.float64)
+        half = np.array([overlap_pan_angle_half_fov(fl, 1280) for fl in ptz[:, 2].tolist()])
+        ov = np.minimum((ptz[:, 0] + half)[:, None], (ptz[:, 0] + half)[None, :]) - \
+            np.maximum((ptz[:, 0] - half)[:, None], (ptz[:, 0] - half)[None, :])
+        assert (ov > 5).astype(np.int64).tolist() == mask
+        random.seed(5)
+        g = correspondence.build_graph(list(range(n)), mask, "sift")
+        off, loc, glo = g.keyframe_features()
+        lists = bundle_adjustment._KeyframeLists(g)
+        for i in range(n):
+            kf = KeyFrame(i, i, np.zeros(3), np.eye(3), 640, 360, 0.0, 0.0, 1000.0)
+            kf.set_features_lazy(g.keypoints[i], g.descriptors[i], lists, i)
+            assert kf.has_features() == (off[i + 1] > off[i])
+            np.testing.assert_array_equal(kf.landmark_index, glo[off[i]:off[i + 1]].astype(np.int32))
+            assert [k.pt for k in kf.feature_pts] == [g.keypoints[i][q].pt for q in loc[off[i]:off[i + 1]]]
+            np.testing.assert_array_equal(kf.feature_des, np.asarray(g.descriptors[i])[loc[off[i]:off[i + 1]]])
+            assert kf.get_feature_num() == off[i + 1] - off[i]
+    finally:
+        image_process.detect_compute_sift, image_process.match_sift_features = saved
