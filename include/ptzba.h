@@ -459,6 +459,10 @@ PTZBA_EXPORT int ptz_keyframe_features(int32_t n_frames, int64_t n_matches, cons
                                        const int32_t* m_j, const int64_t* k1, const int64_t* k2,
                                        const int64_t* lm, int64_t* out_off, int64_t* out_local,
                                        int64_t* out_global);
+/* len() of each keyframe's ptz_keyframe_features list (distinct (local keypoint, landmark) pairs), without the
+ * set() order: counts_out[n_frames]. */
+PTZBA_EXPORT int ptz_keyframe_feature_counts(int32_t n_frames, int64_t n_matches, const int32_t* m_i, const int32_t* m_j,
+                                             const int64_t* k1, const int64_t* k2, const int64_t* lm, int64_t* counts_out);
 /* Pair-form records in _compute_residual order (bundle_adjustment.py:67-99): record 2k = (m_i, k1),
  * 2k+1 = (m_j, k2), both on landmark lm[k]; xy from the keypoint table kp_xy[kp_off[f] + k][2].
  * landmark_src_rec[l] = record of the src observation of the LAST match of landmark l, the one the

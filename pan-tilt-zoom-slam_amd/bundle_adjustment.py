@@ -93,14 +93,24 @@ class _KeyframeLists:
         self.graph = graph
         self.csr = None
         self.used = None
+        self.counts = None
 
     def lists(self, i):
         if self.csr is None:
             self.csr = self.graph.keyframe_features()
             self.graph = None
-            self.used = None
+            self.used = self.counts = None
         off, loc, glo = self.csr
         return loc[off[i]:off[i + 1]], glo[off[i]:off[i + 1]]
+
+    def count(self, i):
+        """len() of keyframe i's lists, without forming them (the verbose print of bundle_adjustment.py:238)."""
+        if self.csr is not None:
+            return int(self.csr[0][i + 1] - self.csr[0][i])
+        if self.counts is None:
+            g = self.graph
+            self.counts = ptzba.keyframe_feature_counts(g.n_frames, g.m_i, g.m_j, g.k1, g.k2, g.lm)
+        return int(self.counts[i])
 
     def nonempty(self, i):
         """keyframe i's list is non-empty: it takes part in a match of this call."""
@@ -198,8 +208,8 @@ def bundle_adjustment(images, image_indices, feature_method, initial_ptzs, cente
         # landmark_index = global ids, on first use (KeyFrame.set_features_lazy)
         key_frame.set_features_lazy(keypoints[i], descriptors[i], lists, i)
         keyframes.append(key_frame)
-        if verbose:
-            print("frame %d, landmark number %d" % (image_indices[i], len(key_frame.landmark_index)))
+        if verbose:  # (the list's length without forming it)
+            print("frame %d, landmark number %d" % (image_indices[i], lists.count(i)))
     timing["keyframes"] = time.time() - t2
     LAST_RESULT.clear()
     LAST_RESULT.update(result=res, n_residual=n_residual, n_landmark=n_landmark, time=timing["solve"],

@@ -1554,11 +1554,12 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     for (size_t k = 0; k < tiles.size(); ++k)
       total_w += (int64_t)tiles[k].size() * (tile_key[2 * k + 1] == 0 ? W0 : WD);
     const int64_t n_tiles = (int64_t)tiles.size();
-    // item target: 512 (two rounds of one workgroup per CU) for a full config-3-sized build (~480K weighted
-    // landmark-tile incidences), proportionally fewer for less work -- a rank's shard of a sharded solve: each
-    // item's 74 KB split partial and the reduce over its tile's splits are fixed costs (measured at config 3,
-    // tools/dist_model.py: N = 2 shard 78 -> 55 us with 256 items, N = 8 shard 44-66 -> 37-47 us with 64-128)
-    int64_t target_items = std::min<int64_t>(512, std::max<int64_t>(64, (512 * total_w) / 480000));
+    // item target: at most 256 (ONE round of one 512-thread workgroup per CU: k_schur_mf's ~100 KB of LDS allows one
+    // per CU) -- same-box A/B at config 3 (r04j, r04p): 256 items 64.7-64.8 us per build against 73.3-74.6 with 512
+    // (two rounds), 68.0 with 192, 84.8 with 320; proportionally fewer for less work -- a rank's shard of a sharded
+    // solve: each item's 74 KB split partial and the reduce over its tile's splits are fixed costs (measured at
+    // config 3, tools/dist_model.py: N = 8 shard 44-66 -> 37-47 us with 64-128 items)
+    int64_t target_items = std::min<int64_t>(256, std::max<int64_t>(64, (512 * total_w) / 480000));
     if (const char* e = getenv("PTZBA_S2_ITEMS")) target_items = std::max(64, atoi(e));  // A/B knob
     const int64_t slots = std::max<int64_t>(target_items - n_tiles, 64);
     const int64_t split_w = std::max<int64_t>(64 * WD, (total_w + slots - 1) / slots);

@@ -306,6 +306,48 @@ int ptz_keyframe_features(int32_t n_frames, int64_t n_matches, const int32_t* m_
   return 0;
 }
 
+// Number of distinct (local keypoint, landmark) pairs per keyframe -- len() of ptz_keyframe_features' per-keyframe
+// lists without their set() order (bundle_adjustment.py:238's verbose print): per keyframe its pairs sorted and
+// counted, keyframes over host threads.
+int ptz_keyframe_feature_counts(int32_t n_frames, int64_t n_matches, const int32_t* m_i, const int32_t* m_j,
+                                const int64_t* k1, const int64_t* k2, const int64_t* lm, int64_t* counts_out) {
+  if (n_frames < 0 || n_matches < 0) return fail("ptz_keyframe_feature_counts: bad sizes");
+  for (int64_t k = 0; k < n_matches; ++k)
+    if (m_i[k] < 0 || m_i[k] >= n_frames || m_j[k] < 0 || m_j[k] >= n_frames || k1[k] < 0 || k2[k] < 0 || lm[k] < 0 ||
+        k1[k] > INT32_MAX || k2[k] > INT32_MAX || lm[k] > INT32_MAX)
+      return fail("ptz_keyframe_feature_counts: match %lld out of range", (long long)k);
+  std::vector<int64_t> off(n_frames + 1, 0);
+  for (int64_t k = 0; k < n_matches; ++k) {
+    off[m_i[k] + 1]++;
+    off[m_j[k] + 1]++;
+  }
+  for (int f = 0; f < n_frames; ++f) off[f + 1] += off[f];
+  std::vector<uint64_t> key(2 * (size_t)n_matches);
+  {
+    std::vector<int64_t> cur(off.begin(), off.end() - 1);
+    for (int64_t k = 0; k < n_matches; ++k) {
+      key[cur[m_i[k]]++] = ((uint64_t)k1[k] << 32) | (uint64_t)lm[k];
+      key[cur[m_j[k]]++] = ((uint64_t)k2[k] << 32) | (uint64_t)lm[k];
+    }
+  }
+  std::atomic<int> next{0};
+  auto work = [&] {
+    for (int f; (f = next.fetch_add(1)) < n_frames;) {
+      uint64_t* b = key.data() + off[f];
+      uint64_t* e = key.data() + off[f + 1];
+      std::sort(b, e);
+      counts_out[f] = std::unique(b, e) - b;
+    }
+  };
+  const int T = (int)std::min<int64_t>({(int64_t)n_frames, 16, 1 + n_matches / 16384,
+                                         (int64_t)std::max(1u, std::thread::hardware_concurrency())});
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; ++t) th.emplace_back(work);
+  work();
+  for (auto& x : th) x.join();
+  return 0;
+}
+
 int ptz_pack_records(int32_t n_frames, int64_t n_matches, const int32_t* m_i, const int32_t* m_j,
                      const int64_t* k1, const int64_t* k2, const int64_t* lm, const int64_t* kp_off,
                      const double* kp_xy, int64_t n_landmark, int32_t* rec_frame, int32_t* rec_landmark,

@@ -24,20 +24,44 @@ The bookkeeping of `build_matching_graph` (image_process.py:509-667) keeps the r
     (ptzba_build_landmarks), including the count of the reference's "in-consistent matching" warnings.
 The graph itself is built by correspondence.build_graph (flat arrays, native cap-shuffle replay).
 """
+import functools
+import operator
+
 import numpy as np
 
 
-class KeyPoint:
+class KeyPoint(tuple):
     """Stand-in for cv2.KeyPoint (the reference only reads `.pt`; size / angle / response / octave as the
-    detectors set them)."""
-    __slots__ = ("pt", "size", "angle", "response", "octave")
+    detectors set them).  An immutable record ((x, y), size, angle, response, octave): the detectors build their
+    1500-keypoint lists with KeyPoint.from_rows at C speed (a keyframe's detection otherwise spent ~1 ms in
+    per-keypoint constructors)."""
+    __slots__ = ()
 
-    def __init__(self, x, y, size=0.0, angle=-1.0, response=0.0, octave=0):
-        self.pt = (float(x), float(y))
-        self.size = float(size)
-        self.angle = float(angle)
-        self.response = float(response)
-        self.octave = int(octave)
+    def __new__(cls, x, y, size=0.0, angle=-1.0, response=0.0, octave=0):
+        return tuple.__new__(cls, ((float(x), float(y)), float(size), float(angle), float(response), int(octave)))
+
+    def __getnewargs__(self):
+        return (self[0][0], self[0][1], self[1], self[2], self[3], self[4])
+
+    pt = property(operator.itemgetter(0))
+    size = property(operator.itemgetter(1))
+    angle = property(operator.itemgetter(2))
+    response = property(operator.itemgetter(3))
+    octave = property(operator.itemgetter(4))
+
+    def __repr__(self):
+        return "KeyPoint(pt=%r, size=%r, angle=%r, response=%r, octave=%r)" % tuple(self)
+
+    @classmethod
+    def from_rows(cls, xy, size, angle, response, octave=None):
+        """[KeyPoint] from columns: xy [n, 2], size / angle / response [n] (Python floats after tolist: the values
+        the constructor's float() would give), octave [n] ints or None (0)."""
+        n = len(size)
+        pts = list(map(tuple, np.asarray(xy, np.float64).reshape(-1, 2).tolist()))
+        oc = [0] * n if octave is None else [int(o) for o in octave]
+        rows = zip(pts, np.asarray(size, np.float64).tolist(), np.asarray(angle, np.float64).tolist(),
+                   np.asarray(response, np.float64).tolist(), oc)
+        return list(map(functools.partial(tuple.__new__, cls), rows))
 
 
 # detect_compute_* / detect_sift / match_*_features / homography_ransac / optical_flow_matching: GPU
@@ -54,7 +78,8 @@ def detect_compute_orb(im, nfeatures=1000, verbose=False):
     assert isinstance(im, np.ndarray)
     assert nfeatures > 0
     kp, des = ptzba.orb(_grey_u8(im), int(nfeatures), "orb")
-    key_point = [KeyPoint(k[0], k[1], k[2], k[3], k[4], int(k[5])) for k in np.asarray(kp).tolist()]
+    kp = np.asarray(kp)
+    key_point = KeyPoint.from_rows(kp[:, 0:2], kp[:, 2], kp[:, 3], kp[:, 4], kp[:, 5].astype(np.int64).tolist())
     if len(key_point) > nfeatures:
         key_point = key_point[:nfeatures]
         des = des[:nfeatures]
@@ -70,7 +95,8 @@ def detect_compute_latch(im, nfeatures=1500, verbose=False):
     import ptzba
     assert isinstance(im, np.ndarray)
     kp, des = ptzba.orb(_grey_u8(im), int(nfeatures) if nfeatures > 0 else 500, "latch")
-    key_point = [KeyPoint(k[0], k[1], k[2], k[3], k[4], int(k[5])) for k in np.asarray(kp).tolist()]
+    kp = np.asarray(kp)
+    key_point = KeyPoint.from_rows(kp[:, 0:2], kp[:, 2], kp[:, 3], kp[:, 4], kp[:, 5].astype(np.int64).tolist())
     if nfeatures > 0 and len(key_point) > nfeatures:
         key_point = key_point[:nfeatures]
         des = des[:nfeatures]
@@ -84,8 +110,7 @@ def detect_compute_sift(im, nfeatures, verbose=False):
     .pt, .size, .angle, .response) strongest first, at most nfeatures (> 0), and descriptors [n, 128] float32."""
     import ptzba
     kp, resp, des = ptzba.sift(_grey_u8(im), int(nfeatures))
-    # (rows as Python floats first: per-element numpy scalar indexing costs ~1 us a keypoint)
-    key_point = [KeyPoint(x, y, sz, an, r) for (x, y, sz, an), r in zip(kp[:, :4].tolist(), np.asarray(resp).tolist())]
+    key_point = KeyPoint.from_rows(kp[:, 0:2], kp[:, 2], kp[:, 3], resp)
     if verbose:
         print('detect: %d SIFT keypoints.' % len(key_point))
     return key_point, des

@@ -145,6 +145,7 @@ def lib():
         "ptz_py_shuffle_prefix": ([V, I64, V, I64, V], I),
         "ptz_set_order_pairs": ([I64, V, V, V, V, V], I),
         "ptz_keyframe_features": ([I32, I64, V, V, V, V, V, V, V, V], I),
+        "ptz_keyframe_feature_counts": ([I32, I64, V, V, V, V, V, V], I),
         "ptz_pack_records": ([I32, I64, V, V, V, V, V, V, V, I64, V, V, V, V], I),
         "ptz_refine_poses": ([I, I32, V, I64, V, V, D, D, V, V, POINTER(ptz_refine_opts), V, V, V], I),
         "ptz_corner_min_eig": ([I, I32, I32, V, V, V], I),
@@ -201,6 +202,7 @@ EXPORTED_SYMBOLS = [
     "ptzba_dist_info", "ptzba_owned_frames", "ptz_corner_min_eig", "ptz_orb", "ptzba_plan_summary",
     "ptzba_plan_export", "ptzba_dist_exchanges", "ptzba_dist_groups", "ptzba_exchange_group", "ptzba_dist_plan_summary",
     "ptzba_dist_rank_phases", "ptzba_dist_plan_export", "ptz_desc_put", "ptz_desc_drop", "ptz_match_knn2_sets",
+    "ptz_keyframe_feature_counts",
 ]
 
 
@@ -580,6 +582,19 @@ def keyframe_features(n_frames, m_i, m_j, k1, k2, lm):
     _check(lib().ptz_keyframe_features(int(n_frames), len(m_i), _ptr(m_i), _ptr(m_j), _ptr(k1), _ptr(k2), _ptr(lm),
                                        _ptr(off), _ptr(loc), _ptr(glo)), "ptz_keyframe_features")
     return off, loc[:off[-1]], glo[:off[-1]]
+
+
+def keyframe_feature_counts(n_frames, m_i, m_j, k1, k2, lm):
+    """len() of each keyframe's keyframe_features list (distinct (local, global) pairs), without forming the lists."""
+    m_i = np.ascontiguousarray(m_i, dtype=np.int32)
+    m_j = np.ascontiguousarray(m_j, dtype=np.int32)
+    k1 = np.ascontiguousarray(k1, dtype=np.int64)
+    k2 = np.ascontiguousarray(k2, dtype=np.int64)
+    lm = np.ascontiguousarray(lm, dtype=np.int64)
+    out = np.empty(int(n_frames), np.int64)
+    _check(lib().ptz_keyframe_feature_counts(int(n_frames), len(m_i), _ptr(m_i), _ptr(m_j), _ptr(k1), _ptr(k2),
+                                             _ptr(lm), _ptr(out)), "ptz_keyframe_feature_counts")
+    return out
 
 
 def pack_records(n_frames, m_i, m_j, k1, k2, lm, kp_off, kp_xy, n_landmark):

@@ -27,6 +27,7 @@ def main():
     st = pstats.Stats(prof, stream=buf)
     st.sort_stats("cumulative").print_stats(60)
     st.sort_stats("tottime").print_stats(60)
+    st.print_callers("landmark_index|_same_image|array_equal|_materialise|hasattr")
     with open(out, "w") as f:
         f.write(buf.getvalue())
 
