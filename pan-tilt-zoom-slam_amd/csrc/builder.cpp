@@ -37,8 +37,8 @@ constexpr int MT_N = 624, MT_M = 397;
 struct MT {
   uint32_t s[MT_N];
   int idx;
-  uint32_t next() {
-    if (idx >= MT_N) {
+  __attribute__((always_inline)) inline uint32_t next() {
+    if (__builtin_expect(idx >= MT_N, 0)) {
       static const uint32_t mag01[2] = {0u, 0x9908b0dfu};
       int kk = 0;
       uint32_t y;
@@ -316,12 +316,44 @@ int ptz_keyframe_feature_counts(int32_t n_frames, int64_t n_matches, const int32
     if (m_i[k] < 0 || m_i[k] >= n_frames || m_j[k] < 0 || m_j[k] >= n_frames || k1[k] < 0 || k2[k] < 0 || lm[k] < 0 ||
         k1[k] > INT32_MAX || k2[k] > INT32_MAX || lm[k] > INT32_MAX)
       return fail("ptz_keyframe_feature_counts: match %lld out of range", (long long)k);
+  // first-seen landmark ids give every (keyframe, keypoint) ONE landmark unless the matching was inconsistent: then
+  // the distinct pairs of a keyframe are its distinct keypoints, counted with a bitmap; any keypoint seen with two
+  // landmarks sends its keyframe to the sort below
+  int64_t kmax = 0;
+  for (int64_t k = 0; k < n_matches; ++k) kmax = std::max(kmax, std::max(k1[k], k2[k]));
   std::vector<int64_t> off(n_frames + 1, 0);
   for (int64_t k = 0; k < n_matches; ++k) {
     off[m_i[k] + 1]++;
     off[m_j[k] + 1]++;
   }
   for (int f = 0; f < n_frames; ++f) off[f + 1] += off[f];
+  std::vector<uint8_t> slow(n_frames, 0);
+  if ((kmax + 1) * (int64_t)n_frames <= ((int64_t)1 << 28)) {
+    const int64_t W = kmax + 1;
+    std::vector<int32_t> lm_of((size_t)(W * n_frames), -1);
+    std::vector<int64_t> cnt(n_frames, 0);
+    auto see = [&](int f, int64_t kp, int64_t l) {
+      int32_t& e = lm_of[(size_t)(f * W + kp)];
+      if (e < 0) {
+        e = (int32_t)l;
+        cnt[f]++;
+      } else if (e != (int32_t)l) {
+        slow[f] = 1;
+      }
+    };
+    for (int64_t k = 0; k < n_matches; ++k) {
+      see(m_i[k], k1[k], lm[k]);
+      see(m_j[k], k2[k], lm[k]);
+    }
+    bool any_slow = false;
+    for (int f = 0; f < n_frames; ++f) {
+      if (!slow[f]) counts_out[f] = cnt[f];
+      any_slow = any_slow || slow[f];
+    }
+    if (!any_slow) return 0;
+  } else {
+    std::fill(slow.begin(), slow.end(), 1);
+  }
   std::vector<uint64_t> key(2 * (size_t)n_matches);
   {
     std::vector<int64_t> cur(off.begin(), off.end() - 1);
@@ -333,6 +365,7 @@ int ptz_keyframe_feature_counts(int32_t n_frames, int64_t n_matches, const int32
   std::atomic<int> next{0};
   auto work = [&] {
     for (int f; (f = next.fetch_add(1)) < n_frames;) {
+      if (!slow[f]) continue;
       uint64_t* b = key.data() + off[f];
       uint64_t* e = key.data() + off[f + 1];
       std::sort(b, e);

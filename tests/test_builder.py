@@ -192,3 +192,30 @@ def test_lazy_keyframe_lists_equal_eager_assembly():
             assert kf.get_feature_num() == off[i + 1] - off[i]
     finally:
         image_process.detect_compute_sift, image_process.match_sift_features = saved
+
+
+@pytest.mark.parametrize("consistent", [True, False])
+def test_keyframe_feature_counts_equal_list_lengths(consistent):
+    """ptz_keyframe_feature_counts (the verbose print's list lengths without the set() order: a bitmap of keypoints
+    when every keypoint has one landmark, a sort otherwise) == the lengths of ptz_keyframe_features' lists."""
+    import ptzba
+    rng = np.random.default_rng(3)
+    n, mi, mj, k1, k2, lm = 12, [], [], [], [], []
+    nxt = [0] * n
+    for l in range(3000):
+        f0 = int(rng.integers(0, n - 2))
+        fs = list(range(f0, min(n, f0 + int(rng.integers(2, 5)))))
+        ks = {f: nxt[f] for f in fs}
+        for f in fs:
+            nxt[f] += 1
+        for a in range(len(fs)):
+            for b in range(a + 1, len(fs)):
+                mi.append(fs[a]); mj.append(fs[b]); k1.append(ks[fs[a]]); k2.append(ks[fs[b]]); lm.append(l)
+    o = np.lexsort((np.arange(len(mi)), np.array(mj), np.array(mi)))
+    mi, mj = np.array(mi, np.int32)[o], np.array(mj, np.int32)[o]
+    k1, k2, lm = np.array(k1)[o], np.array(k2)[o], np.array(lm)[o]
+    if not consistent:
+        lm = lm.copy()
+        lm[::97] = rng.integers(0, 3000, len(lm[::97]))  # keypoints seen with two landmarks
+    off, _, _ = ptzba.keyframe_features(n, mi, mj, k1, k2, lm)
+    np.testing.assert_array_equal(ptzba.keyframe_feature_counts(n, mi, mj, k1, k2, lm), np.diff(off))
