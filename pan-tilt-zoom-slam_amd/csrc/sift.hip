@@ -127,6 +127,45 @@ __global__ __launch_bounds__(256) void k_sift_blur_cols(int w, int h, const floa
   }
 }
 
+// Column pass with a sliding window (round 4): thread (tx, ty) produces the 16 consecutive output rows 16 ty .. 16 ty + 15
+// of its column, keeping the 16 inputs the current tap needs in registers -- one LDS read per 16 products instead of
+// one per product.  Per output the same products in the same order (mul, then add; k ascending): bit-identical to
+// k_sift_blur_cols.  PTZ_SIFT_COLS_SW=0 restores k_sift_blur_cols (A/B).
+__global__ __launch_bounds__(256) void k_sift_blur_cols_sw(int w, int h, const float* __restrict__ src,
+                                                            float* __restrict__ dst, const float* __restrict__ wt, int K) {
+  __shared__ float tile[BLUR_CR + 2 * BLUR_RMAX][BLUR_CT + 1];
+  __shared__ float sw[2 * BLUR_RMAX + 1];
+  const int tx = threadIdx.x & (BLUR_CT - 1), ty = threadIdx.x / BLUR_CT;  // 64 x 4
+  const int x0 = blockIdx.x * BLUR_CT, y0 = blockIdx.y * BLUR_CR, r = K / 2;
+  const int x = x0 + tx;
+  const int nrow = BLUR_CR + 2 * r;
+  for (int i = ty; i < nrow; i += 256 / BLUR_CT)
+    tile[i][tx] = x < w ? src[(int64_t)refl101(y0 + i - r, h) * w + x] : 0.f;
+  if (threadIdx.x < K) sw[threadIdx.x] = wt[threadIdx.x];
+  __syncthreads();
+  if (x >= w) return;
+  constexpr int R = BLUR_CR / 4;  // 16 output rows per thread
+  const int ra = R * ty;
+  float acc[R], win[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    acc[j] = 0.f;
+    win[j] = tile[ra + j][tx];
+  }
+  for (int k = 0; k < K; ++k) {
+    const float wk = sw[k];
+#pragma unroll
+    for (int j = 0; j < R; ++j) acc[j] = acc[j] + wk * win[j];
+    if (k + 1 == K) break;
+#pragma unroll
+    for (int j = 0; j + 1 < R; ++j) win[j] = win[j + 1];
+    win[R - 1] = tile[ra + R + k][tx];  // row ra + R + k <= BLUR_CR - 1 + K - 1: inside the staged rows
+  }
+#pragma unroll
+  for (int j = 0; j < R; ++j)
+    if (y0 + ra + j < h) dst[(int64_t)(y0 + ra + j) * w + x] = acc[j];
+}
+
 // Both passes in one launch (round 4): a 64 x 64 output tile stages its input (+ halo, reflected at the borders) in
 // LDS once, blurs the 64 + 2r rows it needs along x into LDS, then along y, and -- when `prev` is given -- writes
 // the DoG level dst - prev beside it (prev = the octave's previous Gaussian level, the same pixel).  Per output
@@ -510,6 +549,8 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
   // the intermediate image's traffic)
   const char* b2e = getenv("PTZ_SIFT_BLUR2");
   const bool blur2 = b2e && atoi(b2e) == 1;
+  const char* cse = getenv("PTZ_SIFT_COLS_SW");  // sliding-window column pass (A/B knob, read per call)
+  const bool cols_sw = cse && atoi(cse) == 1;
   // dog_out: the DoG level dst - src written beside dst (fused form only)
   auto blur = [&](int w, int h, const float* src, float* dst, int ki, float* dog_out) {
     const int K = (int)kern[ki].size(), rr = K / 2;
@@ -523,8 +564,12 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
     }
     hipLaunchKernelGGL(k_sift_blur_rows, dim3((unsigned)((w + BLUR_TX - 1) / BLUR_TX), (unsigned)h), dim3(BLUR_TX), 0,
                        nullptr, w, h, src, T, dk.as<float>() + ki * kmax, K);
-    hipLaunchKernelGGL(k_sift_blur_cols, dim3((unsigned)((w + BLUR_CT - 1) / BLUR_CT), (unsigned)((h + BLUR_CR - 1) / BLUR_CR)),
-                       dim3(256), 0, nullptr, w, h, T, dst, dk.as<float>() + ki * kmax, K);
+    if (cols_sw)
+      hipLaunchKernelGGL(k_sift_blur_cols_sw, dim3((unsigned)((w + BLUR_CT - 1) / BLUR_CT), (unsigned)((h + BLUR_CR - 1) / BLUR_CR)),
+                         dim3(256), 0, nullptr, w, h, T, dst, dk.as<float>() + ki * kmax, K);
+    else
+      hipLaunchKernelGGL(k_sift_blur_cols, dim3((unsigned)((w + BLUR_CT - 1) / BLUR_CT), (unsigned)((h + BLUR_CR - 1) / BLUR_CR)),
+                         dim3(256), 0, nullptr, w, h, T, dst, dk.as<float>() + ki * kmax, K);
     return false;
   };
   // base: doubled image, then the blur from the assumed input blur to sigma

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Wall time of one GPU SIFT detectAndCompute (ptz_sift) on a rendered 1080p frame, median of N calls; the
-two-pass blur (default) and the fused one (PTZ_SIFT_BLUR2=1; the env is read per call)."""
+two-pass blur (default), the two-pass blur with the sliding-window column pass (PTZ_SIFT_COLS_SW=1) and the fused one
+(PTZ_SIFT_BLUR2=1; the env is read per call)."""
 import os
 import sys
 import time
@@ -18,8 +19,9 @@ def main():
     scene = synthetic.StreamScene(4, seed=0)
     img = image_process._grey_u8(synthetic.RenderedStream(scene, seed=0).image(0))
     out = {}
-    for tag, val in (("two_pass", "0"), ("fused", "1")):
+    for tag, val, cs in (("two_pass", "0", "0"), ("two_pass_cols_sw", "0", "1"), ("fused", "1", "0")):
         os.environ["PTZ_SIFT_BLUR2"] = val
+        os.environ["PTZ_SIFT_COLS_SW"] = cs
         for _ in range(3):
             ptzba.sift(img, 1500)
         ts = []
