@@ -1,0 +1,10 @@
+#!/bin/bash
+# round-4 pass T: the sliding-window SIFT column pass (bit-exact vs the oracle, timing), the front-end tests
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_frontend.py > gpurun_out/r04t_tests.log 2>&1 || { tail -40 gpurun_out/r04t_tests.log; exit 1; }
+tail -1 gpurun_out/r04t_tests.log
+timeout -k 10 300 python tools/sift_bench.py > gpurun_out/r04t_sift.txt 2>&1 || { tail -20 gpurun_out/r04t_sift.txt; exit 1; }
+cat gpurun_out/r04t_sift.txt
