@@ -256,54 +256,16 @@ int ptzba_set_stream(ptzba_handle h, void* stream) {
 
 int ptzba_use_own_stream(ptzba_handle h) { return h ? ptzba_set_stream(h, h->own) : fail("null handle"); }
 
-// ------------------------------------------------------------------------------------------------
-// records hold obs - base(segment) in `real`; the per-segment base observation stays fp64, so the
-// per-record arithmetic of K1 works on O(residual) magnitudes even in fp32
-template <typename real>
-static int upload_records(ptzba_ctx* h, const std::vector<int64_t>& order, const std::vector<int32_t>& rec_seg,
-                          const std::vector<double>& base, const double* obs_xy, const double* w) {
-  // the copies below read host vectors that die at return: every exit path (errors included) waits for the
-  // handle's stream first (the stream does not order itself behind the legacy null stream, so every upload /
-  // memset of set_problem goes on h->st)
-  SyncOnExit sync_guard{h->st};
-  std::vector<real> xy(2 * h->n_rec);
-  std::vector<real> ww(w ? h->n_rec : 0);
-  parallel_chunks(h->n_rec, host_threads(h->n_rec), [&](int64_t lo, int64_t hi, int) {
-    for (int64_t r = lo; r < hi; ++r) {
-      const int32_t s = rec_seg[r];
-      xy[2 * r] = (real)(obs_xy[2 * order[r]] - base[2 * s]);
-      xy[2 * r + 1] = (real)(obs_xy[2 * order[r] + 1] - base[2 * s + 1]);
-      if (w) ww[r] = (real)w[order[r]];
-    }
-  });
-  // allocate everything before queuing any copy; padded by 4 records: K1's coarsened loads read whole groups
-  if (h->rec_xy.alloc((xy.size() + 8) * sizeof(real))) return -1;
-  if (w) {
-    if (h->rec_w.alloc(ww.size() * sizeof(real))) return -1;
-  } else {
-    h->rec_w.release();
-  }
-  HIPCHK(hipMemcpyAsync(h->rec_xy.p, xy.data(), xy.size() * sizeof(real), hipMemcpyHostToDevice, h->st));
-  HIPCHK(hipMemsetAsync(reinterpret_cast<real*>(h->rec_xy.p) + xy.size(), 0, 8 * sizeof(real), h->st));
-  if (w) HIPCHK(hipMemcpyAsync(h->rec_w.p, ww.data(), ww.size() * sizeof(real), hipMemcpyHostToDevice, h->st));
-  HIPCHK(hipStreamSynchronize(h->st));
-  return 0;
-}
-
 // set_problem's uploads: a small array is copied into the handle's pinned staging buffer and its H2D copy queued on
 // the handle's stream without waiting (a sliding-window map calls set_problem per keyframe: ~40 uploads, each a
 // pageable copy plus a stream synchronisation before); large ones take the blocking path below.  The staging
 // buffer is reused only after the stream has drained (set_problem synchronises before its first upload and at the
 // end; a full buffer synchronises before wrapping).
 constexpr size_t STAGE_MAX = 4u << 20, STAGE_MIN_CAP = 8u << 20;
-template <typename T>
-static int upload(DBuf& b, const std::vector<T>& v, hipStream_t st);
-template <typename T>
-static int upload_st(ptzba_ctx* h, DBuf& b, const std::vector<T>& v) {
-  const size_t n = v.size() * sizeof(T);
-  if (n > STAGE_MAX) return upload(b, v, h->st);
-  if (b.alloc(n)) return -1;
-  if (n == 0) return 0;
+// a pinned staging slot of n bytes for one queued copy (*out = nullptr when n is too large for the staging path)
+static int stage_take(ptzba_ctx* h, size_t n, uint8_t** out) {
+  *out = nullptr;
+  if (n > STAGE_MAX) return 0;
   size_t off = (h->stage_used + 255) & ~(size_t)255;
   if (!h->stage || off + n > h->stage_cap) {
     HIPCHK(hipStreamSynchronize(h->st));  // every staged copy so far has landed
@@ -313,9 +275,69 @@ static int upload_st(ptzba_ctx* h, DBuf& b, const std::vector<T>& v) {
       h->stage_cap = STAGE_MIN_CAP;
     }
   }
-  std::memcpy(h->stage + off, v.data(), n);
-  HIPCHK(hipMemcpyAsync(b.p, h->stage + off, n, hipMemcpyHostToDevice, h->st));
+  *out = h->stage + off;
   h->stage_used = off + n;
+  return 0;
+}
+template <typename T>
+static int upload(DBuf& b, const std::vector<T>& v, hipStream_t st);
+template <typename T>
+static int upload_st(ptzba_ctx* h, DBuf& b, const std::vector<T>& v) {
+  const size_t n = v.size() * sizeof(T);
+  if (n > STAGE_MAX) return upload(b, v, h->st);
+  if (b.alloc(n)) return -1;
+  if (n == 0) return 0;
+  uint8_t* p = nullptr;
+  if (stage_take(h, n, &p)) return -1;
+  std::memcpy(p, v.data(), n);
+  HIPCHK(hipMemcpyAsync(b.p, p, n, hipMemcpyHostToDevice, h->st));
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// records hold obs - base(segment) in `real`; the per-segment base observation stays fp64, so the
+// per-record arithmetic of K1 works on O(residual) magnitudes even in fp32
+template <typename real>
+static int upload_records(ptzba_ctx* h, const std::vector<int64_t>& order, const std::vector<int32_t>& rec_seg,
+                          const std::vector<double>& base, const double* obs_xy, const double* w) {
+  // the copies below read host vectors that die at return: every exit path (errors included) waits for the
+  // handle's stream first (the stream does not order itself behind the legacy null stream, so every upload /
+  // memset of set_problem goes on h->st)
+  const size_t nxy = 2 * (size_t)h->n_rec, nw = w ? (size_t)h->n_rec : 0;
+  // allocate everything before queuing any copy; padded by 4 records: K1's coarsened loads read whole groups
+  if (h->rec_xy.alloc((nxy + 8) * sizeof(real))) return -1;
+  if (w) {
+    if (h->rec_w.alloc(nw * sizeof(real))) return -1;
+  } else {
+    h->rec_w.release();
+  }
+  // small problems (a sliding window's ~170K records) convert straight into the pinned staging buffer and queue the
+  // copies; large ones convert into host vectors and copy with a synchronisation (the vectors die at return)
+  uint8_t *pxy = nullptr, *pw = nullptr;
+  if (stage_take(h, nxy * sizeof(real), &pxy)) return -1;
+  if (pxy && w && stage_take(h, nw * sizeof(real), &pw)) return -1;
+  const bool staged = pxy && (!w || pw);
+  std::vector<real> vxy(staged ? 0 : nxy), vw(staged ? 0 : nw);
+  struct SyncIf {  // the vector path: every exit waits for the copies reading the vectors (errors included)
+    hipStream_t s;
+    bool on;
+    ~SyncIf() {
+      if (on) (void)hipStreamSynchronize(s);
+    }
+  } sync_guard{h->st, !staged};
+  real* xy = staged ? reinterpret_cast<real*>(pxy) : vxy.data();
+  real* ww = staged ? reinterpret_cast<real*>(pw) : vw.data();
+  parallel_chunks(h->n_rec, host_threads(h->n_rec), [&](int64_t lo, int64_t hi, int) {
+    for (int64_t r = lo; r < hi; ++r) {
+      const int32_t s = rec_seg[r];
+      xy[2 * r] = (real)(obs_xy[2 * order[r]] - base[2 * s]);
+      xy[2 * r + 1] = (real)(obs_xy[2 * order[r] + 1] - base[2 * s + 1]);
+      if (w) ww[r] = (real)w[order[r]];
+    }
+  });
+  HIPCHK(hipMemcpyAsync(h->rec_xy.p, xy, nxy * sizeof(real), hipMemcpyHostToDevice, h->st));
+  HIPCHK(hipMemsetAsync(reinterpret_cast<real*>(h->rec_xy.p) + nxy, 0, 8 * sizeof(real), h->st));
+  if (w) HIPCHK(hipMemcpyAsync(h->rec_w.p, ww, nw * sizeof(real), hipMemcpyHostToDevice, h->st));
   return 0;
 }
 

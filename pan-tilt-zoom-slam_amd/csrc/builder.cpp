@@ -36,30 +36,44 @@ constexpr int MT_N = 624, MT_M = 397;
 
 struct MT {
   uint32_t s[MT_N];
+  uint32_t t[MT_N];  // the tempered outputs of the current block (formed in one vectorisable pass per twist)
   int idx;
+  void twist() {
+    int kk = 0;
+    for (; kk < MT_N - MT_M; kk++) {
+      const uint32_t y = (s[kk] & 0x80000000u) | (s[kk + 1] & 0x7fffffffu);
+      s[kk] = s[kk + MT_M] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+    }
+    for (; kk < MT_N - 1; kk++) {
+      const uint32_t y = (s[kk] & 0x80000000u) | (s[kk + 1] & 0x7fffffffu);
+      s[kk] = s[kk + (MT_M - MT_N)] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+    }
+    const uint32_t y = (s[MT_N - 1] & 0x80000000u) | (s[0] & 0x7fffffffu);
+    s[MT_N - 1] = s[MT_M - 1] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+  }
+  void temper_from(int i0) {
+    for (int i = i0; i < MT_N; ++i) {
+      uint32_t y = s[i];
+      y ^= (y >> 11);
+      y ^= (y << 7) & 0x9d2c5680u;
+      y ^= (y << 15) & 0xefc60000u;
+      y ^= (y >> 18);
+      t[i] = y;
+    }
+  }
+  // state as CPython keeps it (mt[624], index); `t` is derived
+  void load(const uint32_t* st, int index) {
+    memcpy(s, st, sizeof(s));
+    idx = index;
+    if (idx < MT_N) temper_from(idx);
+  }
   __attribute__((always_inline)) inline uint32_t next() {
     if (__builtin_expect(idx >= MT_N, 0)) {
-      static const uint32_t mag01[2] = {0u, 0x9908b0dfu};
-      int kk = 0;
-      uint32_t y;
-      for (; kk < MT_N - MT_M; kk++) {
-        y = (s[kk] & 0x80000000u) | (s[kk + 1] & 0x7fffffffu);
-        s[kk] = s[kk + MT_M] ^ (y >> 1) ^ mag01[y & 1u];
-      }
-      for (; kk < MT_N - 1; kk++) {
-        y = (s[kk] & 0x80000000u) | (s[kk + 1] & 0x7fffffffu);
-        s[kk] = s[kk + (MT_M - MT_N)] ^ (y >> 1) ^ mag01[y & 1u];
-      }
-      y = (s[MT_N - 1] & 0x80000000u) | (s[0] & 0x7fffffffu);
-      s[MT_N - 1] = s[MT_M - 1] ^ (y >> 1) ^ mag01[y & 1u];
+      twist();
+      temper_from(0);
       idx = 0;
     }
-    uint32_t y = s[idx++];
-    y ^= (y >> 11);
-    y ^= (y << 7) & 0x9d2c5680u;
-    y ^= (y << 15) & 0xefc60000u;
-    y ^= (y >> 18);
-    return y;
+    return t[idx++];
   }
   // Random._randbelow_with_getrandbits(n), n < 2^31: k = n.bit_length(); r = getrandbits(k) until r < n
   uint32_t below(uint32_t n) {
@@ -188,8 +202,7 @@ int ptz_py_shuffle_prefix(uint32_t* mt_state, int64_t n_lists, const int64_t* le
   if (!mt_state || n_lists < 0 || keep < 0) return fail("ptz_py_shuffle_prefix: bad arguments");
   if (mt_state[MT_N] > (uint32_t)MT_N) return fail("ptz_py_shuffle_prefix: bad generator index");
   MT g;
-  memcpy(g.s, mt_state, sizeof(g.s));
-  g.idx = (int)mt_state[MT_N];
+  g.load(mt_state, (int)mt_state[MT_N]);
   std::vector<int64_t> perm;
   int64_t o = 0;
   for (int64_t l = 0; l < n_lists; ++l) {
