@@ -19,7 +19,7 @@ def main():
     scene = synthetic.StreamScene(4, seed=0)
     img = image_process._grey_u8(synthetic.RenderedStream(scene, seed=0).image(0))
     out = {}
-    for tag, val, cs in (("two_pass", "0", "0"), ("two_pass_cols_sw", "0", "1"), ("fused", "1", "0")):
+    for tag, val, cs in (("two_pass_cols_1out", "0", "0"), ("two_pass", "0", "1"), ("fused", "1", "0")):
         os.environ["PTZ_SIFT_BLUR2"] = val
         os.environ["PTZ_SIFT_COLS_SW"] = cs
         for _ in range(3):
