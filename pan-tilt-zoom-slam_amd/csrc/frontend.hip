@@ -117,6 +117,120 @@ __global__ __launch_bounds__(256) void k_top2(int n1, int n2, const float* __res
   }
 }
 
+// kNN-2 on the matrix cores for integer-valued 128-d descriptors (SIFT's: integers 0..255): one workgroup per 64 query
+// rows (a wave per 16), the train set streamed through LDS in tiles of 64 as f16 (exact: integers up to 2048), the
+// dot products on v_mfma_f32_16x16x32_f16 (products exact, sums exact integers below 2^24), d^2 = |q|^2 + |t|^2 - 2 q.t
+// exact -- the same integer k_sqdist's fp32 sum of (a - b)^2 gives -- and each lane keeps a running (distance, index)
+// top 2 for its four rows over its columns (ascending), merged across the 16 lanes of a row at the end with k_top2's
+// lexicographic rule: bit for bit k_sqdist + k_top2's output, without the n1 x n2 distance matrix.
+typedef _Float16 kn_h8 __attribute__((ext_vector_type(8)));
+typedef float kn_f4 __attribute__((ext_vector_type(4)));
+constexpr int KN_DIM = 128, KN_TC = 64, KN_LD = KN_DIM + 8;  // train tile columns, f16 row pitch (272 B)
+__global__ __launch_bounds__(256) void k_knn2_mf(int n1, int n2, const float* __restrict__ a, const float* __restrict__ b,
+                                                 int* __restrict__ idx, float* __restrict__ dist) {
+  __shared__ __attribute__((aligned(16))) _Float16 sb[KN_TC][KN_LD];
+  __shared__ float snb[KN_TC];
+  __shared__ float sna[4][16];
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63, fr = lane & 15, fk = (lane >> 4) * 8;
+  const int q0 = blockIdx.x * 64 + 16 * w;
+  // this wave's 16 query rows as MFMA A operands (row fr, dims 32 c + fk .. + 7) and their squared norms
+  kn_h8 qa[KN_DIM / 32];
+  {
+    const int q = min(q0 + fr, n1 - 1);
+    const float* src = a + (int64_t)q * KN_DIM;
+#pragma unroll
+    for (int c = 0; c < KN_DIM / 32; ++c) {
+      const float4 u0 = reinterpret_cast<const float4*>(src + 32 * c + fk)[0];
+      const float4 u1 = reinterpret_cast<const float4*>(src + 32 * c + fk)[1];
+      qa[c] = kn_h8{(_Float16)u0.x, (_Float16)u0.y, (_Float16)u0.z, (_Float16)u0.w,
+                    (_Float16)u1.x, (_Float16)u1.y, (_Float16)u1.z, (_Float16)u1.w};
+    }
+    if (lane < 16) {
+      float s = 0.f;
+      for (int k = 0; k < KN_DIM; ++k) s = fmaf(src[k], src[k], s);  // exact integer
+      sna[w][fr] = s;
+    }
+  }
+  float b1[4], b2[4];
+  int i1[4], i2[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    b1[v] = b2[v] = INFINITY;
+    i1[v] = i2[v] = 0x7fffffff;
+  }
+  for (int j0 = 0; j0 < n2; j0 += KN_TC) {
+    __syncthreads();  // (the previous tile's reads are done)
+    {  // stage 64 train rows as f16: thread = (row t >> 2, quarter t & 3 of the dims); their squared norms
+      const int r = t >> 2, qd = (t & 3) * (KN_DIM / 4), j = j0 + r;
+      float s = 0.f;
+      const float* src = b + (int64_t)min(j, n2 - 1) * KN_DIM + qd;
+#pragma unroll
+      for (int k = 0; k < KN_DIM / 4; k += 4) {
+        const float4 u = reinterpret_cast<const float4*>(src + k)[0];
+        sb[r][qd + k] = (_Float16)u.x;
+        sb[r][qd + k + 1] = (_Float16)u.y;
+        sb[r][qd + k + 2] = (_Float16)u.z;
+        sb[r][qd + k + 3] = (_Float16)u.w;
+        s = fmaf(u.x, u.x, s);
+        s = fmaf(u.y, u.y, s);
+        s = fmaf(u.z, u.z, s);
+        s = fmaf(u.w, u.w, s);
+      }
+      s += __shfl_xor(s, 1);
+      s += __shfl_xor(s, 2);
+      if ((t & 3) == 0) snb[r] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int y = 0; y < KN_TC / 16; ++y) {
+      kn_f4 c = kn_f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < KN_DIM / 32; ++kc) {
+        const kn_h8 bv = *reinterpret_cast<const kn_h8*>(&sb[16 * y + fr][32 * kc + fk]);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(qa[kc], bv, c, 0, 0, 0);
+      }
+      const int jl = 16 * y + fr, j = j0 + jl;
+      if (j >= n2) continue;
+      const float nb = snb[jl];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float d = (sna[w][(lane >> 4) * 4 + v] + nb) - 2.f * c[v];
+        if (lt(d, j, b1[v], i1[v])) {
+          b2[v] = b1[v]; i2[v] = i1[v]; b1[v] = d; i1[v] = j;
+        } else if (lt(d, j, b2[v], i2[v])) {
+          b2[v] = d; i2[v] = j;
+        }
+      }
+    }
+  }
+  // merge the 16 lanes of each row group (lanes with the same lane >> 4): the k_top2 merge
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) {
+      const float ob1 = __shfl_xor(b1[v], off), ob2 = __shfl_xor(b2[v], off);
+      const int oi1 = __shfl_xor(i1[v], off), oi2 = __shfl_xor(i2[v], off);
+      float n1v, n2v;
+      int n1i, n2i;
+      if (lt(b1[v], i1[v], ob1, oi1)) {
+        n1v = b1[v]; n1i = i1[v];
+        if (lt(b2[v], i2[v], ob1, oi1)) { n2v = b2[v]; n2i = i2[v]; } else { n2v = ob1; n2i = oi1; }
+      } else {
+        n1v = ob1; n1i = oi1;
+        if (lt(b1[v], i1[v], ob2, oi2)) { n2v = b1[v]; n2i = i1[v]; } else { n2v = ob2; n2i = oi2; }
+      }
+      b1[v] = n1v; i1[v] = n1i; b2[v] = n2v; i2[v] = n2i;
+    }
+    const int q = q0 + (lane >> 4) * 4 + v;
+    if (fr == 0 && q < n1) {
+      idx[2 * q] = i1[v];
+      idx[2 * q + 1] = n2 > 1 ? i2[v] : -1;
+      dist[2 * q] = sqrtf(b1[v]);
+      dist[2 * q + 1] = n2 > 1 ? sqrtf(b2[v]) : INFINITY;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // homography RANSAC
 // ---------------------------------------------------------------------------------------------
@@ -417,6 +531,7 @@ struct DescSet {
   DBuf buf;
   int64_t n = 0;
   int32_t dim = 0;
+  bool integral = false;  // every value an integer of magnitude <= 2048 (exact in f16: k_knn2_mf applies)
 };
 struct DescStore {
   std::vector<std::pair<uint64_t, DescSet*>> sets;
@@ -443,6 +558,9 @@ int ptz_desc_put(int device, uint64_t key, int64_t n, int32_t dim, const float* 
   if (d->buf.reserve((size_t)std::max<int64_t>(n, 1) * dim * 4)) return -1;
   d->n = n;
   d->dim = dim;
+  bool integral = true;
+  for (int64_t e = 0; e < n * dim && integral; ++e) integral = des[e] == std::nearbyint(des[e]) && std::fabs(des[e]) <= 2048.f;
+  d->integral = integral;
   if (n) HIPCHK(hipMemcpy(d->buf.p, des, (size_t)n * dim * 4, hipMemcpyHostToDevice));
   return 0;
 }
@@ -493,7 +611,12 @@ int ptz_match_knn2_sets(int device, int32_t n_sets, const uint64_t* query_keys, 
     DBuf a, d, idx, dist;
   };
   KnnSetsWork& Wk = work_for<KnnSetsWork>(device);
-  if (Wk.a.reserve((size_t)n1 * dim * 4) || Wk.d.reserve((size_t)n1 * n2 * 4) || Wk.idx.reserve((size_t)n1 * 8) ||
+  // integer-valued 128-d sets (SIFT's): the matrix-core kernel, no distance matrix (PTZ_KNN_MF=0: the fp32 pair, A/B)
+  bool mf = dim == KN_DIM && tr->integral;
+  for (int32_t q = 0; q < n_sets && mf; ++q) mf = S.find(query_keys[q])->integral;
+  const char* mfe = getenv("PTZ_KNN_MF");
+  if (mfe && atoi(mfe) == 0) mf = false;
+  if (Wk.a.reserve((size_t)n1 * dim * 4) || (!mf && Wk.d.reserve((size_t)n1 * n2 * 4)) || Wk.idx.reserve((size_t)n1 * 8) ||
       Wk.dist.reserve((size_t)n1 * 8))
     return -1;
   int64_t o = 0;
@@ -502,10 +625,15 @@ int ptz_match_knn2_sets(int device, int32_t n_sets, const uint64_t* query_keys, 
     if (d->n) HIPCHK(hipMemcpyAsync(Wk.a.as<char>() + o * dim * 4, d->buf.p, (size_t)d->n * dim * 4, hipMemcpyDeviceToDevice, nullptr));
     o += d->n;
   }
-  hipLaunchKernelGGL(k_sqdist, dim3((unsigned)((n2 + KT - 1) / KT), (unsigned)((n1 + KT - 1) / KT)), dim3(256), 0, nullptr,
-                     (int)n1, (int)n2, dim, Wk.a.as<float>(), tr->buf.as<float>(), Wk.d.as<float>());
-  hipLaunchKernelGGL(k_top2, dim3((unsigned)((n1 + 3) / 4)), dim3(256), 0, nullptr, (int)n1, (int)n2, Wk.d.as<float>(),
-                     Wk.idx.as<int>(), Wk.dist.as<float>());
+  if (mf) {
+    hipLaunchKernelGGL(k_knn2_mf, dim3((unsigned)((n1 + 63) / 64)), dim3(256), 0, nullptr, (int)n1, (int)n2,
+                       Wk.a.as<float>(), tr->buf.as<float>(), Wk.idx.as<int>(), Wk.dist.as<float>());
+  } else {
+    hipLaunchKernelGGL(k_sqdist, dim3((unsigned)((n2 + KT - 1) / KT), (unsigned)((n1 + KT - 1) / KT)), dim3(256), 0, nullptr,
+                       (int)n1, (int)n2, dim, Wk.a.as<float>(), tr->buf.as<float>(), Wk.d.as<float>());
+    hipLaunchKernelGGL(k_top2, dim3((unsigned)((n1 + 3) / 4)), dim3(256), 0, nullptr, (int)n1, (int)n2, Wk.d.as<float>(),
+                       Wk.idx.as<int>(), Wk.dist.as<float>());
+  }
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(idx_out, Wk.idx.p, (size_t)n1 * 8, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(dist_out, Wk.dist.p, (size_t)n1 * 8, hipMemcpyDeviceToHost));

@@ -407,3 +407,31 @@ def test_orb_front_end_recovers_homography(gpu_available):
         assert np.median(err) < 1.0, (det.__name__, np.median(err))
     kc, dc = image_process.detect_compute_orb(I, 100)
     assert len(kc) == 100 and dc.shape == (100, 32)
+
+
+@pytest.mark.parametrize("n1,n2", [(1000, 1500), (37, 70), (130, 1)])
+def test_knn2_matrix_core_sets_equal_fp32_pair(gpu_available, monkeypatch, n1, n2):
+    """ptz_match_knn2_sets on integer-valued 128-d descriptor sets (SIFT's) runs k_knn2_mf (f16 MFMA dot products,
+    exact integer distances, running top 2 per lane): the same indices and distances, bit for bit, as the fp32
+    k_sqdist + k_top2 pair (ptz_match_knn2, and the sets path with PTZ_KNN_MF=0) -- duplicated train rows included
+    (ties to the lower index), ragged sizes, a single train row."""
+    import ptzba
+    rng = np.random.default_rng(n1 + n2)
+    q = rng.integers(0, 256, (n1, 128)).astype(np.float32)
+    t = rng.integers(0, 256, (n2, 128)).astype(np.float32)
+    if n2 > 10:
+        t[5] = t[3]          # an exact tie between two train rows
+        q[:4] = t[[3, 7, 7, 9]]  # distance-0 queries
+    qa, qb = q[: n1 // 2], q[n1 // 2:]
+    ref_i, ref_d = ptzba.match_knn2(q, t)
+    keys = [501, 502, 503]
+    try:
+        ptzba.desc_put_new(keys[0], qa)
+        ptzba.desc_put_new(keys[1], qb)
+        ptzba.desc_put_new(keys[2], t)
+        for mf in ("1", "0"):
+            monkeypatch.setenv("PTZ_KNN_MF", mf)
+            i, d = ptzba.match_knn2_sets(keys[:2], [len(qa), len(qb)], keys[2])
+            assert np.array_equal(i, ref_i) and np.array_equal(d, ref_d), mf
+    finally:
+        ptzba.desc_drop(keys)
