@@ -363,6 +363,16 @@ PTZBA_EXPORT int ptz_desc_put(int device, uint64_t key, int64_t n, int32_t dim, 
 PTZBA_EXPORT int ptz_desc_drop(int device, int32_t n_keys, const uint64_t* keys);
 PTZBA_EXPORT int ptz_match_knn2_sets(int device, int32_t n_sets, const uint64_t* query_keys, uint64_t train_key,
                                      int64_t n_rows, int32_t* idx_out, float* dist_out);
+/* The batched SIFT matcher of a new keyframe against resident sets sharing one train set (image_process
+ * match_sift_features_batch): ptz_match_knn2_sets, Lowe's ratio test d1 < 0.7 d2 (float32) per query set, the
+ * survivors' points from query_xy (the query sets' keypoints concatenated, [rows, 2]) and train_xy ([train_rows, 2]),
+ * one ptz_homography_ransac_batch (threshold, n_hyp, seed) over the sets with more than 8 survivors, and the inliers
+ * as (query row, train row) pairs: out_off[n_sets + 1] into out_i1 / out_i2 (capacity: the query rows in total);
+ * status_out[s] = 1 when set s had 8 or fewer survivors (no pairs), else 0. */
+PTZBA_EXPORT int ptz_match_sets_ransac(int device, int32_t n_sets, const uint64_t* query_keys, const int64_t* query_rows,
+                                       uint64_t train_key, int64_t train_rows, const double* query_xy,
+                                       const double* train_xy, double threshold, int32_t n_hyp, uint64_t seed,
+                                       int32_t* status_out, int64_t* out_off, int32_t* out_i1, int32_t* out_i2);
 /* Homography RANSAC (cv.findHomography(..., RANSAC, threshold) as called by homography_ransac): n_hyp
  * hypotheses from 4-point samples keyed by (seed, hypothesis, draw), DLT in Hartley-normalised coordinates,
  * the hypothesis with most inliers (reprojection error < threshold px; ties: lowest index), a linear

@@ -742,6 +742,82 @@ int ptz_homography_ransac_batch(int device, int32_t n_sets, const int64_t* off, 
   return 0;
 }
 
+// The batched SIFT matcher of a new keyframe in one call (image_process.match_sift_features_batch when the pairs share
+// one resident train set): ptz_match_knn2_sets over the query sets, Lowe's ratio test d1 < 0.7 d2 in float32 per set
+// (match_sift_features, image_process.py:178-234), the survivors' points gathered from the callers' keypoint
+// arrays, one ptz_homography_ransac_batch over the sets with more than 8 survivors, and their inliers as index
+// pairs -- per set exactly match_sift_features' (index1, index2).  status_out[s] = 1: 8 or fewer survivors (the
+// caller prints the reference's warning), 0 otherwise; out_off [n_sets + 1] into out_i1 / out_i2 (capacity: the
+// query rows).
+int ptz_match_sets_ransac(int device, int32_t n_sets, const uint64_t* query_keys, const int64_t* query_rows,
+                          uint64_t train_key, int64_t train_rows, const double* query_xy, const double* train_xy,
+                          double threshold, int32_t n_hyp, uint64_t seed, int32_t* status_out, int64_t* out_off,
+                          int32_t* out_i1, int32_t* out_i2) {
+  if (n_sets < 0 || (n_sets > 0 && (!query_keys || !query_rows || !query_xy || !status_out || !out_off || !out_i1 || !out_i2)))
+    return fail("ptz_match_sets_ransac: bad arguments");
+  out_off[0] = 0;
+  if (n_sets == 0) return 0;
+  std::vector<int64_t> qoff(n_sets + 1, 0);
+  for (int32_t q = 0; q < n_sets; ++q) qoff[q + 1] = qoff[q] + query_rows[q];
+  const int64_t n1 = qoff[n_sets];
+  std::vector<int32_t> idx(2 * std::max<int64_t>(n1, 1));
+  std::vector<float> dist(2 * std::max<int64_t>(n1, 1));
+  if (ptz_match_knn2_sets(device, n_sets, query_keys, train_key, n1, idx.data(), dist.data())) return -1;
+  // ratio test and the candidate point sets
+  std::vector<int64_t> coff(1, 0);
+  std::vector<int32_t> cset, ci1, ci2;
+  std::vector<double> p1, p2;
+  for (int32_t q = 0; q < n_sets; ++q) {
+    const size_t c0 = ci1.size();
+    if (train_rows >= 2)
+      for (int64_t r = 0; r < query_rows[q]; ++r) {
+        const int64_t g = qoff[q] + r;
+        if (dist[2 * g] < 0.7f * dist[2 * g + 1]) {
+          const int32_t j = idx[2 * g];
+          if (j < 0 || j >= train_rows) return fail("ptz_match_sets_ransac: train index %d out of range", j);
+          ci1.push_back((int32_t)r);
+          ci2.push_back(j);
+          p1.push_back(query_xy[2 * g]);
+          p1.push_back(query_xy[2 * g + 1]);
+          p2.push_back(train_xy[2 * (int64_t)j]);
+          p2.push_back(train_xy[2 * (int64_t)j + 1]);
+        }
+      }
+    if (ci1.size() - c0 <= 8) {  // too few survivors: no RANSAC for this set
+      status_out[q] = 1;
+      ci1.resize(c0);
+      ci2.resize(c0);
+      p1.resize(2 * c0);
+      p2.resize(2 * c0);
+      continue;
+    }
+    status_out[q] = 0;
+    cset.push_back(q);
+    coff.push_back((int64_t)ci1.size());
+  }
+  const int32_t nc = (int32_t)cset.size();
+  std::vector<uint8_t> mask(std::max<size_t>(ci1.size(), 1));
+  std::vector<double> H(9 * std::max(nc, 1));
+  std::vector<int32_t> nin(std::max(nc, 1));
+  if (nc && ptz_homography_ransac_batch(device, nc, coff.data(), p1.data(), p2.data(), threshold, n_hyp, seed,
+                                        mask.data(), H.data(), nin.data()))
+    return -1;
+  int64_t o = 0, c = 0;
+  for (int32_t q = 0; q < n_sets; ++q) {
+    if (status_out[q] == 0) {
+      for (int64_t e = coff[c]; e < coff[c + 1]; ++e)
+        if (mask[e]) {
+          out_i1[o] = ci1[e];
+          out_i2[o] = ci2[e];
+          ++o;
+        }
+      ++c;
+    }
+    out_off[q + 1] = o;
+  }
+  return 0;
+}
+
 namespace ptzba {
 // ---------------------------------------------------------------------------------------------
 // pyramidal Lucas-Kanade point tracking (cv.calcOpticalFlowPyrLK(img, next_img, points, None,

@@ -25,6 +25,7 @@ The bookkeeping of `build_matching_graph` (image_process.py:509-667) keeps the r
 The graph itself is built by correspondence.build_graph (flat arrays, native cap-shuffle replay).
 """
 import functools
+import os
 import operator
 
 import numpy as np
@@ -196,6 +197,20 @@ def match_sift_features_batch(pairs, dev_sets=None):
     groups = {}
     for q, (_, d1, _, d2) in enumerate(pairs):
         groups.setdefault(dev_sets[q][1][0] if dev_sets is not None else id(d2), []).append(q)
+    if dev_sets is not None and len(groups) == 1 and all(isinstance(p[0], np.ndarray) for p in pairs) and \
+            isinstance(pairs[0][2], np.ndarray) and os.environ.get("PTZ_MATCH_FUSED", "1") != "0":
+        # one train set (a new keyframe against its window partners) and keypoint arrays: kNN-2, ratio tests,
+        # point gathers and RANSAC in one native call (ptz_match_sets_ransac), per pair the same result
+        res = ptzba.match_sets_ransac([dev_sets[q][0][0] for q in range(len(pairs))],
+                                      [dev_sets[q][0][1] for q in range(len(pairs))], dev_sets[0][1][0],
+                                      dev_sets[0][1][1], np.concatenate([np.asarray(p[0], np.float64).reshape(-1, 2)
+                                                                         for p in pairs]), pairs[0][2], 1.0)
+        for q, r in enumerate(res):
+            if r is None:
+                print('warning: match sift features failed, not enough matching')
+            else:
+                out[q] = (r[0].tolist(), r[1].tolist())
+        return out
     cand = []  # (pair, index1, index2, pts1, pts2)
     for qs in groups.values():
         n2 = dev_sets[qs[0]][1][1] if dev_sets is not None else len(pairs[qs[0]][3])

@@ -136,6 +136,7 @@ def lib():
         "ptz_desc_put": ([I, ctypes.c_uint64, I64, I32, V], I),
         "ptz_desc_drop": ([I, I32, V], I),
         "ptz_match_knn2_sets": ([I, I32, V, ctypes.c_uint64, I64, V, V], I),
+        "ptz_match_sets_ransac": ([I, I32, V, V, ctypes.c_uint64, I64, V, V, D, I32, ctypes.c_uint64, V, V, V, V], I),
         "ptz_homography_ransac": ([I, I64, V, V, D, I32, ctypes.c_uint64, V, V, POINTER(c_int32)], I),
         "ptz_homography_ransac_batch": ([I, I32, V, V, V, D, I32, ctypes.c_uint64, V, V, V], I),
         "ptz_lk_track": ([I, I32, I32, V, V, I64, V, I32, I32, I32, D, D, V, V, V], I),
@@ -202,7 +203,7 @@ EXPORTED_SYMBOLS = [
     "ptzba_dist_info", "ptzba_owned_frames", "ptz_corner_min_eig", "ptz_orb", "ptzba_plan_summary",
     "ptzba_plan_export", "ptzba_dist_exchanges", "ptzba_dist_groups", "ptzba_exchange_group", "ptzba_dist_plan_summary",
     "ptzba_dist_rank_phases", "ptzba_dist_plan_export", "ptz_desc_put", "ptz_desc_drop", "ptz_match_knn2_sets",
-    "ptz_keyframe_feature_counts",
+    "ptz_keyframe_feature_counts", "ptz_match_sets_ransac",
 ]
 
 
@@ -337,6 +338,27 @@ def match_knn2_sets(query_keys, query_lens, train_key, device=None):
         _check(lib().ptz_match_knn2_sets(default_device() if device is None else device, len(qk), _ptr(qk),
                                          int(train_key), n1, _ptr(idx), _ptr(dist)), "ptz_match_knn2_sets")
     return idx, dist
+
+
+def match_sets_ransac(query_keys, query_rows, train_key, train_rows, query_xy, train_xy, threshold=1.0, n_hyp=2000,
+                      seed=0, device=None):
+    """ptz_match_sets_ransac: kNN-2 of resident query sets against a resident train set, ratio test, homography RANSAC
+    per set.  Returns [(index1 int32, index2 int32) or None (8 or fewer ratio-test survivors)] per query set."""
+    qk = np.ascontiguousarray(list(query_keys), dtype=np.uint64)
+    rows = np.ascontiguousarray(list(query_rows), dtype=np.int64)
+    qxy = np.ascontiguousarray(query_xy, dtype=np.float64).reshape(-1, 2)
+    txy = np.ascontiguousarray(train_xy, dtype=np.float64).reshape(-1, 2)
+    if len(qxy) != int(rows.sum()) or len(txy) != int(train_rows):
+        raise ValueError("point arrays do not match the descriptor sets")
+    st = np.zeros(len(qk), np.int32)
+    off = np.zeros(len(qk) + 1, np.int64)
+    i1 = np.empty(max(len(qxy), 1), np.int32)
+    i2 = np.empty(max(len(qxy), 1), np.int32)
+    _check(lib().ptz_match_sets_ransac(default_device() if device is None else device, len(qk), _ptr(qk), _ptr(rows),
+                                       int(train_key), int(train_rows), _ptr(qxy), _ptr(txy), float(threshold),
+                                       int(n_hyp), int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(st), _ptr(off), _ptr(i1),
+                                       _ptr(i2)), "ptz_match_sets_ransac")
+    return [None if st[q] else (i1[off[q]:off[q + 1]], i2[off[q]:off[q + 1]]) for q in range(len(qk))]
 
 
 def homography_ransac(points1, points2, threshold, n_hyp=2000, seed=0, device=None):

@@ -123,6 +123,38 @@ def test_match_sift_features_batch_equals_per_pair(gpu_available):
         ptzba.match_knn2_sets([1000], [len(pairs[0][1])], 1001)
 
 
+def test_fused_native_matcher_equals_per_pair(gpu_available, capsys):
+    """One train set (a new keyframe) against several resident query sets with keypoint arrays: the batch matcher
+    takes ptz_match_sets_ransac (kNN-2, ratio tests, point gathers, RANSAC in one native call) -- per pair exactly
+    match_sift_features' (index1, index2), the too-few-survivors pair included (and its warning printed)."""
+    import image_process
+    import ptzba
+    x0, d0, xn, dn, _, _ = frontend_data.two_views(seed=7)
+    pairs = []
+    for s in (8, 9, 10):
+        x1, d1, _, _, _, _ = frontend_data.two_views(seed=s)
+        pairs.append((np.asarray(x1, np.float64), d1, np.asarray(xn, np.float64), dn))
+    pairs.append((np.asarray(x0, np.float64), d0, np.asarray(xn, np.float64), dn))
+    pairs.append((np.asarray(x0[:5], np.float64), d0[:5], np.asarray(xn, np.float64), dn))  # too few survivors
+    keys = {}
+
+    def dev(d, k):
+        if k not in keys:
+            keys[k] = (2000 + len(keys), ptzba.desc_put_new(2000 + len(keys), d))
+        return keys[k]
+    try:
+        dev_sets = [(dev(p[1], q), dev(dn, "train")) for q, p in enumerate(pairs)]
+        capsys.readouterr()
+        got = image_process.match_sift_features_batch(pairs, dev_sets=dev_sets)
+        assert capsys.readouterr().out.count("not enough matching") == 1
+    finally:
+        ptzba.desc_drop([v[0] for v in keys.values()])
+    for (k1, d1, k2, d2), (a, b) in zip(pairs, got):
+        _, i1, _, i2 = image_process.match_sift_features(k1, d1, k2, d2, pts_array=True)
+        assert list(a) == list(i1) and list(b) == list(i2)
+    assert len(got[3][0]) > 300 and got[4] == ([], [])
+
+
 def test_homography_ransac_hook_signature(gpu_available):
     """homography_ransac(points1, points2, threshold, return_matrix) as image_process.py:418 calls it."""
     import image_process
