@@ -166,6 +166,52 @@ __global__ __launch_bounds__(256) void k_sift_blur_cols_sw(int w, int h, const f
     if (y0 + ra + j < h) dst[(int64_t)(y0 + ra + j) * w + x] = acc[j];
 }
 
+// Row pass with a sliding window (round 4): a workgroup blurs a 64-row x 64-column block; lane = row (an odd LDS
+// pitch keeps the 64 rows of a read in distinct banks), wave w = the 16 outputs 16 w .. 16 w + 15 of every row, kept
+// with the 16 inputs the current tap needs in registers (one LDS read per 16 products); the results go back through
+// LDS so the global stores are row-contiguous.  Per output the same products in the same order (mul, then add; k
+// ascending): bit-identical to k_sift_blur_rows.  PTZ_SIFT_ROWS_SW=0 restores k_sift_blur_rows (A/B).
+constexpr int BRS_R = 64, BRS_C = 64, BRS_LD = BRS_C + 2 * BLUR_RMAX + 1;
+__global__ __launch_bounds__(256) void k_sift_blur_rows_sw(int w, int h, const float* __restrict__ src,
+                                                            float* __restrict__ dst, const float* __restrict__ wt, int K) {
+  __shared__ float tile[BRS_R][BRS_LD];
+  __shared__ float sw[2 * BLUR_RMAX + 1];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int x0 = blockIdx.x * BRS_C, y0 = blockIdx.y * BRS_R, r = K / 2;
+  const int ncol = BRS_C + 2 * r;
+  for (int e = t; e < BRS_R * ncol; e += 256) {
+    const int i = e / ncol, c = e - i * ncol, y = min(y0 + i, h - 1);
+    tile[i][c] = src[(int64_t)y * w + refl101(x0 + c - r, w)];
+  }
+  if (t < K) sw[t] = wt[t];
+  __syncthreads();
+  constexpr int R = 16;
+  const int cb = R * wv;
+  float acc[R], win[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    acc[j] = 0.f;
+    win[j] = tile[lane][cb + j];
+  }
+  for (int k = 0; k < K; ++k) {
+    const float wk = sw[k];
+#pragma unroll
+    for (int j = 0; j < R; ++j) acc[j] = acc[j] + wk * win[j];
+    if (k + 1 == K) break;
+#pragma unroll
+    for (int j = 0; j + 1 < R; ++j) win[j] = win[j + 1];
+    win[R - 1] = tile[lane][cb + R + k];  // column cb + R + k <= BRS_C - 1 + K - 1: inside the staged columns
+  }
+  __syncthreads();  // (every window read is done: the tile's first 64 columns take the results)
+#pragma unroll
+  for (int j = 0; j < R; ++j) tile[lane][cb + j] = acc[j];
+  __syncthreads();
+  for (int e = t; e < BRS_R * BRS_C; e += 256) {
+    const int i = e >> 6, c = e & 63, y = y0 + i, x = x0 + c;
+    if (y < h && x < w) dst[(int64_t)y * w + x] = tile[i][c];
+  }
+}
+
 // Both passes in one launch (round 4): a 64 x 64 output tile stages its input (+ halo, reflected at the borders) in
 // LDS once, blurs the 64 + 2r rows it needs along x into LDS, then along y, and -- when `prev` is given -- writes
 // the DoG level dst - prev beside it (prev = the octave's previous Gaussian level, the same pixel).  Per output
@@ -553,6 +599,8 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
   // 1.816 -> 1.776 ms per 1080p detection (r04t), bit-identical
   const char* cse = getenv("PTZ_SIFT_COLS_SW");
   const bool cols_sw = !(cse && atoi(cse) == 0);
+  const char* rse = getenv("PTZ_SIFT_ROWS_SW");  // sliding-window row pass (A/B knob, read per call)
+  const bool rows_sw = rse && atoi(rse) == 1;
   // dog_out: the DoG level dst - src written beside dst (fused form only)
   auto blur = [&](int w, int h, const float* src, float* dst, int ki, float* dog_out) {
     const int K = (int)kern[ki].size(), rr = K / 2;
@@ -564,8 +612,12 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
                          dog_out ? src : nullptr, dog_out);
       return true;
     }
-    hipLaunchKernelGGL(k_sift_blur_rows, dim3((unsigned)((w + BLUR_TX - 1) / BLUR_TX), (unsigned)h), dim3(BLUR_TX), 0,
-                       nullptr, w, h, src, T, dk.as<float>() + ki * kmax, K);
+    if (rows_sw)
+      hipLaunchKernelGGL(k_sift_blur_rows_sw, dim3((unsigned)((w + BRS_C - 1) / BRS_C), (unsigned)((h + BRS_R - 1) / BRS_R)),
+                         dim3(256), 0, nullptr, w, h, src, T, dk.as<float>() + ki * kmax, K);
+    else
+      hipLaunchKernelGGL(k_sift_blur_rows, dim3((unsigned)((w + BLUR_TX - 1) / BLUR_TX), (unsigned)h), dim3(BLUR_TX), 0,
+                         nullptr, w, h, src, T, dk.as<float>() + ki * kmax, K);
     if (cols_sw)
       hipLaunchKernelGGL(k_sift_blur_cols_sw, dim3((unsigned)((w + BLUR_CT - 1) / BLUR_CT), (unsigned)((h + BLUR_CR - 1) / BLUR_CR)),
                          dim3(256), 0, nullptr, w, h, T, dst, dk.as<float>() + ki * kmax, K);

@@ -19,9 +19,11 @@ def main():
     scene = synthetic.StreamScene(4, seed=0)
     img = image_process._grey_u8(synthetic.RenderedStream(scene, seed=0).image(0))
     out = {}
-    for tag, val, cs in (("two_pass_cols_1out", "0", "0"), ("two_pass", "0", "1"), ("fused", "1", "0")):
+    for tag, val, cs, rs in (("two_pass_cols_1out", "0", "0", "0"), ("two_pass", "0", "1", "0"),
+                             ("two_pass_rows_sw", "0", "1", "1"), ("fused", "1", "0", "0")):
         os.environ["PTZ_SIFT_BLUR2"] = val
         os.environ["PTZ_SIFT_COLS_SW"] = cs
+        os.environ["PTZ_SIFT_ROWS_SW"] = rs
         for _ in range(3):
             ptzba.sift(img, 1500)
         ts = []
