@@ -364,9 +364,42 @@ int ptz_keyframe_feature_counts(int32_t n_frames, int64_t n_matches, const int32
       any_slow = any_slow || slow[f];
     }
     if (!any_slow) return 0;
+    if (n_frames < (1 << 16) && kmax < (1 << 24)) {
+      // keyframes with conflicting keypoints: only those keypoints' (keypoint, landmark) pairs are sorted -- the
+      // count is the distinct keypoints plus, per conflicting keypoint, its distinct landmarks beyond the first
+      std::vector<uint8_t> conflict((size_t)(W * n_frames), 0);
+      auto mark = [&](int f, int64_t kp, int64_t l) {
+        if (lm_of[(size_t)(f * W + kp)] != (int32_t)l) conflict[(size_t)(f * W + kp)] = 1;
+      };
+      for (int64_t k = 0; k < n_matches; ++k) {
+        mark(m_i[k], k1[k], lm[k]);
+        mark(m_j[k], k2[k], lm[k]);
+      }
+      int64_t n_ex = 0;
+      for (int64_t k = 0; k < n_matches; ++k)
+        n_ex += conflict[(size_t)(m_i[k] * W + k1[k])] + conflict[(size_t)(m_j[k] * W + k2[k])];
+      if (n_ex > n_matches / 4) goto general;  // mostly conflicting (inconsistent matching): the per-keyframe sorts
+      std::vector<std::pair<uint64_t, int32_t>> ex;
+      ex.reserve((size_t)n_ex);  // ((frame << 24 | keypoint), landmark) of conflicting keypoints
+      auto take = [&](int f, int64_t kp, int64_t l) {
+        if (conflict[(size_t)(f * W + kp)]) ex.push_back({((uint64_t)f << 24) | (uint64_t)kp, (int32_t)l});
+      };
+      for (int64_t k = 0; k < n_matches; ++k) {
+        take(m_i[k], k1[k], lm[k]);
+        take(m_j[k], k2[k], lm[k]);
+      }
+      std::sort(ex.begin(), ex.end());
+      ex.erase(std::unique(ex.begin(), ex.end()), ex.end());
+      for (int f = 0; f < n_frames; ++f)
+        if (slow[f]) counts_out[f] = cnt[f];
+      for (size_t e = 0; e < ex.size(); ++e)  // every distinct pair beyond its keypoint's first adds one
+        if (e > 0 && ex[e].first == ex[e - 1].first) counts_out[ex[e].first >> 24]++;
+      return 0;
+    }
   } else {
     std::fill(slow.begin(), slow.end(), 1);
   }
+general:
   std::vector<uint64_t> key(2 * (size_t)n_matches);
   {
     std::vector<int64_t> cur(off.begin(), off.end() - 1);
