@@ -1397,23 +1397,40 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
 
   st_mark("validate");
   // ---- stable counting sorts: by frame, then by landmark -> (landmark, frame, original index)
-  std::vector<int64_t> tmp(n_obs), order(n_obs);
+  std::vector<int64_t> tmp, order(n_obs);
   // large problems (config 4: 410M records) sort on host threads: the same stable order (par_util.h)
   const bool par_host = host_threads(n_obs) > 1;
   if (par_host) {
+    tmp.resize(n_obs);
     parallel_counting_sort(n_obs, n_pose, (const int64_t*)nullptr, tmp.data(), [&](int64_t r) { return obs_frame[r]; });
     parallel_counting_sort(n_obs, n_landmark, tmp.data(), order.data(), [&](int64_t r) { return obs_landmark[r]; });
   } else {
-    std::vector<int64_t> c(n_pose + 1, 0);
-    for (int64_t r = 0; r < n_obs; ++r) c[obs_frame[r] + 1]++;
-    for (int f = 0; f < n_pose; ++f) c[f + 1] += c[f];
-    for (int64_t r = 0; r < n_obs; ++r) tmp[c[obs_frame[r]]++] = r;
+    // one counting pass by landmark (stable: record order within a landmark), then each landmark's few records
+    // stably by frame -- the same (landmark, frame, record) order as the two counting passes, one scatter less
     std::vector<int64_t> d(n_landmark + 1, 0);
     for (int64_t r = 0; r < n_obs; ++r) d[obs_landmark[r] + 1]++;
     for (int l = 0; l < n_landmark; ++l) d[l + 1] += d[l];
-    for (int64_t k = 0; k < n_obs; ++k) {
-      int64_t r = tmp[k];
-      order[d[obs_landmark[r]]++] = r;
+    {
+      std::vector<int64_t> c(d.begin(), d.end() - 1);
+      for (int64_t r = 0; r < n_obs; ++r) order[c[obs_landmark[r]]++] = r;
+    }
+    auto by_frame = [&](int64_t a, int64_t b) { return obs_frame[a] < obs_frame[b]; };
+    for (int l = 0; l < n_landmark; ++l) {
+      int64_t* b0 = order.data() + d[l];
+      int64_t* b1 = order.data() + d[l + 1];
+      if (b1 - b0 <= 32) {  // insertion sort (stable)
+        for (int64_t* p = b0 + 1; p < b1; ++p) {
+          const int64_t v = *p;
+          int64_t* q = p;
+          while (q > b0 && by_frame(v, q[-1])) {
+            *q = q[-1];
+            --q;
+          }
+          *q = v;
+        }
+      } else {
+        std::stable_sort(b0, b1, by_frame);
+      }
     }
   }
   st_mark("sort");
