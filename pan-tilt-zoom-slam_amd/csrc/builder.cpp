@@ -320,87 +320,27 @@ int ptz_keyframe_features(int32_t n_frames, int64_t n_matches, const int32_t* m_
 }
 
 // Number of distinct (local keypoint, landmark) pairs per keyframe -- len() of ptz_keyframe_features' per-keyframe
-// lists without their set() order (bundle_adjustment.py:238's verbose print): per keyframe its pairs sorted and
-// counted, keyframes over host threads.
+// lists without their set() order (bundle_adjustment.py:238's verbose print).  Keyframes over host threads; per
+// keyframe a keypoint map gives the count directly (first-seen landmark ids give a keypoint one landmark unless the
+// matching was inconsistent), and only a keyframe with a keypoint seen under two landmarks sorts its pairs.
 int ptz_keyframe_feature_counts(int32_t n_frames, int64_t n_matches, const int32_t* m_i, const int32_t* m_j,
                                 const int64_t* k1, const int64_t* k2, const int64_t* lm, int64_t* counts_out) {
   if (n_frames < 0 || n_matches < 0) return fail("ptz_keyframe_feature_counts: bad sizes");
-  for (int64_t k = 0; k < n_matches; ++k)
+  int64_t kmax = 0;
+  for (int64_t k = 0; k < n_matches; ++k) {
     if (m_i[k] < 0 || m_i[k] >= n_frames || m_j[k] < 0 || m_j[k] >= n_frames || k1[k] < 0 || k2[k] < 0 || lm[k] < 0 ||
         k1[k] > INT32_MAX || k2[k] > INT32_MAX || lm[k] > INT32_MAX)
       return fail("ptz_keyframe_feature_counts: match %lld out of range", (long long)k);
-  // first-seen landmark ids give every (keyframe, keypoint) ONE landmark unless the matching was inconsistent: then
-  // the distinct pairs of a keyframe are its distinct keypoints, counted with a bitmap; any keypoint seen with two
-  // landmarks sends its keyframe to the sort below
-  int64_t kmax = 0;
-  for (int64_t k = 0; k < n_matches; ++k) kmax = std::max(kmax, std::max(k1[k], k2[k]));
+    kmax = std::max(kmax, std::max(k1[k], k2[k]));
+  }
+  // per keyframe its (keypoint, landmark) sides: a counting sort of the 2 n_matches sides by keyframe
   std::vector<int64_t> off(n_frames + 1, 0);
   for (int64_t k = 0; k < n_matches; ++k) {
     off[m_i[k] + 1]++;
     off[m_j[k] + 1]++;
   }
   for (int f = 0; f < n_frames; ++f) off[f + 1] += off[f];
-  std::vector<uint8_t> slow(n_frames, 0);
-  if ((kmax + 1) * (int64_t)n_frames <= ((int64_t)1 << 28)) {
-    const int64_t W = kmax + 1;
-    std::vector<int32_t> lm_of((size_t)(W * n_frames), -1);
-    std::vector<int64_t> cnt(n_frames, 0);
-    auto see = [&](int f, int64_t kp, int64_t l) {
-      int32_t& e = lm_of[(size_t)(f * W + kp)];
-      if (e < 0) {
-        e = (int32_t)l;
-        cnt[f]++;
-      } else if (e != (int32_t)l) {
-        slow[f] = 1;
-      }
-    };
-    for (int64_t k = 0; k < n_matches; ++k) {
-      see(m_i[k], k1[k], lm[k]);
-      see(m_j[k], k2[k], lm[k]);
-    }
-    bool any_slow = false;
-    for (int f = 0; f < n_frames; ++f) {
-      if (!slow[f]) counts_out[f] = cnt[f];
-      any_slow = any_slow || slow[f];
-    }
-    if (!any_slow) return 0;
-    if (n_frames < (1 << 16) && kmax < (1 << 24)) {
-      // keyframes with conflicting keypoints: only those keypoints' (keypoint, landmark) pairs are sorted -- the
-      // count is the distinct keypoints plus, per conflicting keypoint, its distinct landmarks beyond the first
-      std::vector<uint8_t> conflict((size_t)(W * n_frames), 0);
-      auto mark = [&](int f, int64_t kp, int64_t l) {
-        if (lm_of[(size_t)(f * W + kp)] != (int32_t)l) conflict[(size_t)(f * W + kp)] = 1;
-      };
-      for (int64_t k = 0; k < n_matches; ++k) {
-        mark(m_i[k], k1[k], lm[k]);
-        mark(m_j[k], k2[k], lm[k]);
-      }
-      int64_t n_ex = 0;
-      for (int64_t k = 0; k < n_matches; ++k)
-        n_ex += conflict[(size_t)(m_i[k] * W + k1[k])] + conflict[(size_t)(m_j[k] * W + k2[k])];
-      if (n_ex > n_matches / 4) goto general;  // mostly conflicting (inconsistent matching): the per-keyframe sorts
-      std::vector<std::pair<uint64_t, int32_t>> ex;
-      ex.reserve((size_t)n_ex);  // ((frame << 24 | keypoint), landmark) of conflicting keypoints
-      auto take = [&](int f, int64_t kp, int64_t l) {
-        if (conflict[(size_t)(f * W + kp)]) ex.push_back({((uint64_t)f << 24) | (uint64_t)kp, (int32_t)l});
-      };
-      for (int64_t k = 0; k < n_matches; ++k) {
-        take(m_i[k], k1[k], lm[k]);
-        take(m_j[k], k2[k], lm[k]);
-      }
-      std::sort(ex.begin(), ex.end());
-      ex.erase(std::unique(ex.begin(), ex.end()), ex.end());
-      for (int f = 0; f < n_frames; ++f)
-        if (slow[f]) counts_out[f] = cnt[f];
-      for (size_t e = 0; e < ex.size(); ++e)  // every distinct pair beyond its keypoint's first adds one
-        if (e > 0 && ex[e].first == ex[e - 1].first) counts_out[ex[e].first >> 24]++;
-      return 0;
-    }
-  } else {
-    std::fill(slow.begin(), slow.end(), 1);
-  }
-general:
-  std::vector<uint64_t> key(2 * (size_t)n_matches);
+  std::vector<uint64_t> key(2 * (size_t)n_matches);  // keypoint << 32 | landmark
   {
     std::vector<int64_t> cur(off.begin(), off.end() - 1);
     for (int64_t k = 0; k < n_matches; ++k) {
@@ -408,14 +348,33 @@ general:
       key[cur[m_j[k]]++] = ((uint64_t)k2[k] << 32) | (uint64_t)lm[k];
     }
   }
+  const bool mapped = kmax < ((int64_t)1 << 26);  // keypoint map per thread: (kmax + 1) int32
   std::atomic<int> next{0};
   auto work = [&] {
+    std::vector<int32_t> lm_of(mapped ? (size_t)kmax + 1 : 0, -1);
     for (int f; (f = next.fetch_add(1)) < n_frames;) {
-      if (!slow[f]) continue;
       uint64_t* b = key.data() + off[f];
       uint64_t* e = key.data() + off[f + 1];
-      std::sort(b, e);
-      counts_out[f] = std::unique(b, e) - b;
+      bool conflict = !mapped;
+      int64_t c = 0;
+      if (mapped) {
+        for (uint64_t* p = b; p < e && !conflict; ++p) {
+          int32_t& m = lm_of[(size_t)(*p >> 32)];
+          const int32_t l = (int32_t)(*p & 0xffffffffu);
+          if (m < 0) {
+            m = l;
+            ++c;
+          } else if (m != l) {
+            conflict = true;
+          }
+        }
+        for (uint64_t* p = b; p < e; ++p) lm_of[(size_t)(*p >> 32)] = -1;  // reset for the next keyframe
+      }
+      if (conflict) {
+        std::sort(b, e);
+        c = std::unique(b, e) - b;
+      }
+      counts_out[f] = c;
     }
   };
   const int T = (int)std::min<int64_t>({(int64_t)n_frames, 16, 1 + n_matches / 16384,

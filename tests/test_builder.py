@@ -196,7 +196,7 @@ def test_lazy_keyframe_lists_equal_eager_assembly():
 
 @pytest.mark.parametrize("consistent", [True, False])
 def test_keyframe_feature_counts_equal_list_lengths(consistent):
-    """ptz_keyframe_feature_counts (the verbose print's list lengths without the set() order: a bitmap of keypoints
+    """ptz_keyframe_feature_counts (the verbose print's list lengths without the set() order: a keypoint map per keyframe
     when every keypoint has one landmark, a sort otherwise) == the lengths of ptz_keyframe_features' lists."""
     import ptzba
     rng = np.random.default_rng(3)
