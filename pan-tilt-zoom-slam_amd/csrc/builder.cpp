@@ -333,6 +333,39 @@ int ptz_keyframe_feature_counts(int32_t n_frames, int64_t n_matches, const int32
       return fail("ptz_keyframe_feature_counts: match %lld out of range", (long long)k);
     kmax = std::max(kmax, std::max(k1[k], k2[k]));
   }
+  // a window's keyframes (cells of one frame x keypoint table fit 64 MiB): one sequential pass over the matches
+  // marks each (keyframe, keypoint) with its first landmark; only a keyframe with a keypoint under two landmarks
+  // counts its distinct pairs by a sort
+  if ((int64_t)n_frames * (kmax + 1) <= ((int64_t)1 << 24)) {
+    const int64_t kw = kmax + 1;
+    std::vector<int32_t> tab((size_t)n_frames * kw, -1);
+    std::vector<uint8_t> conflict(n_frames, 0);
+    for (int f = 0; f < n_frames; ++f) counts_out[f] = 0;
+    auto put = [&](int f, int64_t kp, int32_t l) {
+      int32_t& m = tab[(size_t)f * kw + kp];
+      if (m < 0) {
+        m = l;
+        ++counts_out[f];
+      } else if (m != l) {
+        conflict[f] = 1;
+      }
+    };
+    for (int64_t k = 0; k < n_matches; ++k) {
+      put(m_i[k], k1[k], (int32_t)lm[k]);
+      put(m_j[k], k2[k], (int32_t)lm[k]);
+    }
+    for (int f = 0; f < n_frames; ++f) {
+      if (!conflict[f]) continue;
+      std::vector<uint64_t> key;
+      for (int64_t k = 0; k < n_matches; ++k) {
+        if (m_i[k] == f) key.push_back(((uint64_t)k1[k] << 32) | (uint64_t)lm[k]);
+        if (m_j[k] == f) key.push_back(((uint64_t)k2[k] << 32) | (uint64_t)lm[k]);
+      }
+      std::sort(key.begin(), key.end());
+      counts_out[f] = std::unique(key.begin(), key.end()) - key.begin();
+    }
+    return 0;
+  }
   // per keyframe its (keypoint, landmark) sides: a counting sort of the 2 n_matches sides by keyframe
   std::vector<int64_t> off(n_frames + 1, 0);
   for (int64_t k = 0; k < n_matches; ++k) {

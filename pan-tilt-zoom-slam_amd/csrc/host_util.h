@@ -51,9 +51,13 @@ struct DBuf {
       return 0;
     }
     release();
-    hipError_t e = hipMalloc(&p, n);
-    if (e != hipSuccess) return fail("hipMalloc(%zu) failed: %s", n, hipGetErrorString(e));
-    bytes = cap = n;
+    // a buffer below 256 MiB is allocated with a quarter of slack: a sliding window's problem grows by a few
+    // percent per keyframe, and an exact fit would be replaced (hipFree + hipMalloc) at nearly every call
+    const size_t c = n < ((size_t)256 << 20) ? ((n + n / 4 + 4095) & ~(size_t)4095) : n;
+    hipError_t e = hipMalloc(&p, c);
+    if (e != hipSuccess) return fail("hipMalloc(%zu) failed: %s", c, hipGetErrorString(e));
+    bytes = n;
+    cap = c;
     return 0;
   }
   // keep the allocation when it is already large enough (contents are not preserved otherwise)

@@ -195,9 +195,11 @@ def test_lazy_keyframe_lists_equal_eager_assembly():
 
 
 @pytest.mark.parametrize("consistent", [True, False])
-def test_keyframe_feature_counts_equal_list_lengths(consistent):
-    """ptz_keyframe_feature_counts (the verbose print's list lengths without the set() order: a keypoint map per keyframe
-    when every keypoint has one landmark, a sort otherwise) == the lengths of ptz_keyframe_features' lists."""
+@pytest.mark.parametrize("wide", [False, True])
+def test_keyframe_feature_counts_equal_list_lengths(consistent, wide):
+    """ptz_keyframe_feature_counts (the verbose print's list lengths without the set() order: a keyframe x keypoint
+    table, or per keyframe a keypoint map when the table is too large (`wide`: keypoint ids past 2^24 / frames), and a
+    sort where a keypoint has two landmarks) == the lengths of ptz_keyframe_features' lists."""
     import ptzba
     rng = np.random.default_rng(3)
     n, mi, mj, k1, k2, lm = 12, [], [], [], [], []
@@ -217,5 +219,7 @@ def test_keyframe_feature_counts_equal_list_lengths(consistent):
     if not consistent:
         lm = lm.copy()
         lm[::97] = rng.integers(0, 3000, len(lm[::97]))  # keypoints seen with two landmarks
+    if wide:
+        k1 = k1 + (k1 % 7 == 3) * 3_000_000  # sparse large keypoint ids
     off, _, _ = ptzba.keyframe_features(n, mi, mj, k1, k2, lm)
     np.testing.assert_array_equal(ptzba.keyframe_feature_counts(n, mi, mj, k1, k2, lm), np.diff(off))
