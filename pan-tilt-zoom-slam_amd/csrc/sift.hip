@@ -19,6 +19,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include <algorithm>
 #include <cmath>
@@ -506,6 +507,13 @@ namespace {
 // the kernels.
 struct SiftWork {
   ptzba::DBuf dimg, dg, dd, dtmp, dk, dcand, dcnt, dkp, dptr, dow, doh, dsel, ddes;
+  // the last call's image (host copy) and its oriented keypoints before the top-n cut: the pyramid in dg / dptr
+  // belongs to it, so a call on the same image (a stream detects each frame with 500 features, then the same frame
+  // again with 1500 when it becomes a keyframe) re-selects and computes descriptors only
+  std::vector<uint8_t> last_img;
+  int32_t last_w = 0, last_h = 0, last_variant = -1;  // (variant: the blur A/B knobs the pyramid was built with)
+  std::vector<ptzba::SiftKp> last_kps;
+  bool last_valid = false;
 };
 SiftWork& sift_work(int device) { return ptzba::work_for<SiftWork>(device); }  // under device_work_lock
 
@@ -575,97 +583,124 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
       dcnt.reserve(16) || dkp.reserve(CAP * sizeof(SiftKp)) || dptr.reserve(n_oct * (SIFT_S + 3) * sizeof(float*)) ||
       dow.reserve(n_oct * 4) || doh.reserve(n_oct * 4))
     return -1;
-  HIPCHK(hipMemcpy(dimg.p, img, (size_t)width * height, hipMemcpyHostToDevice));
-  std::vector<float> kflat((SIFT_S + 3) * kmax, 0.f);
-  for (int i = 0; i < SIFT_S + 3; ++i) std::copy(kern[i].begin(), kern[i].end(), kflat.begin() + i * kmax);
-  HIPCHK(hipMemcpy(dk.p, kflat.data(), kflat.size() * 4, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(dow.p, ow.data(), n_oct * 4, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(doh.p, oh.data(), n_oct * 4, hipMemcpyHostToDevice));
-  HIPCHK(hipMemset(dcnt.p, 0, 16));
-  std::vector<float*> gptr(n_oct * (SIFT_S + 3));
-  float* G = dg.as<float>();
-  float* Dg = dd.as<float>();
-  float* T = dtmp.as<float>();
-  for (int o = 0; o < n_oct; ++o)
-    for (int i = 0; i < SIFT_S + 3; ++i) gptr[o * (SIFT_S + 3) + i] = G + goff[o] + (int64_t)i * ow[o] * oh[o];
-  HIPCHK(hipMemcpy(dptr.p, gptr.data(), gptr.size() * sizeof(float*), hipMemcpyHostToDevice));
-  st_mark("setup+upload");
-  // PTZ_SIFT_BLUR2=1: both blur passes and the DoG in one launch (A/B knob, read per call; measured 2.29 vs 2.23 ms
-  // per 1080p frame against the two-pass form, tools/sift_bench.py r04i -- the LDS-staged passes were not bound by
-  // the intermediate image's traffic)
-  const char* b2e = getenv("PTZ_SIFT_BLUR2");
-  const bool blur2 = b2e && atoi(b2e) == 1;
-  // sliding-window column pass, the default (PTZ_SIFT_COLS_SW=0: one output per thread; A/B knob, read per call):
-  // 1.816 -> 1.776 ms per 1080p detection (r04t), bit-identical
-  const char* cse = getenv("PTZ_SIFT_COLS_SW");
-  const bool cols_sw = !(cse && atoi(cse) == 0);
-  const char* rse = getenv("PTZ_SIFT_ROWS_SW");  // sliding-window row pass (A/B knob, read per call)
-  const bool rows_sw = rse && atoi(rse) == 1;
-  // dog_out: the DoG level dst - src written beside dst (fused form only)
-  auto blur = [&](int w, int h, const float* src, float* dst, int ki, float* dog_out) {
-    const int K = (int)kern[ki].size(), rr = K / 2;
-    const int n2 = BLUR2_T + 2 * rr;
-    const size_t lds = ((size_t)n2 * n2 + (size_t)n2 * (BLUR2_T + 1)) * sizeof(float);
-    if (blur2 && lds <= 64 * 1024) {  // (radius <= 14: every blur of OpenCV's default SIFT)
-      hipLaunchKernelGGL(k_sift_blur2, dim3((unsigned)((w + BLUR2_T - 1) / BLUR2_T), (unsigned)((h + BLUR2_T - 1) / BLUR2_T)),
-                         dim3(256), lds, nullptr, w, h, src, dst, dk.as<float>() + ki * kmax, K,
-                         dog_out ? src : nullptr, dog_out);
-      return true;
-    }
-    if (rows_sw)
-      hipLaunchKernelGGL(k_sift_blur_rows_sw, dim3((unsigned)((w + BRS_C - 1) / BRS_C), (unsigned)((h + BRS_R - 1) / BRS_R)),
-                         dim3(256), 0, nullptr, w, h, src, T, dk.as<float>() + ki * kmax, K);
-    else
-      hipLaunchKernelGGL(k_sift_blur_rows, dim3((unsigned)((w + BLUR_TX - 1) / BLUR_TX), (unsigned)h), dim3(BLUR_TX), 0,
-                         nullptr, w, h, src, T, dk.as<float>() + ki * kmax, K);
-    if (cols_sw)
-      hipLaunchKernelGGL(k_sift_blur_cols_sw, dim3((unsigned)((w + BLUR_CT - 1) / BLUR_CT), (unsigned)((h + BLUR_CR - 1) / BLUR_CR)),
-                         dim3(256), 0, nullptr, w, h, T, dst, dk.as<float>() + ki * kmax, K);
-    else
-      hipLaunchKernelGGL(k_sift_blur_cols, dim3((unsigned)((w + BLUR_CT - 1) / BLUR_CT), (unsigned)((h + BLUR_CR - 1) / BLUR_CR)),
-                         dim3(256), 0, nullptr, w, h, T, dst, dk.as<float>() + ki * kmax, K);
-    return false;
+  // PTZ_SIFT_REUSE=0: always rebuild the pyramid (A/B knob, read per call)
+  const char* rue = getenv("PTZ_SIFT_REUSE");
+  const bool reuse = !(rue && atoi(rue) == 0);
+  const size_t img_bytes = (size_t)width * height;
+  auto knob = [](const char* name) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : -1;
   };
-  // base: doubled image, then the blur from the assumed input blur to sigma
-  hipLaunchKernelGGL(k_sift_up, dim3((unsigned)((W0 + 127) / 128), (unsigned)H0), dim3(128), 0, nullptr, width, height,
-                     dimg.as<uint8_t>(), gptr[1]);
-  blur(W0, H0, gptr[1], gptr[0], 0, nullptr);
-  const float thr = (float)std::floor(0.5 * SIFT_CONTR / SIFT_S * 255);
-  for (int o = 0; o < n_oct; ++o) {
-    const int w = ow[o], h = oh[o];
-    if (o > 0)
-      hipLaunchKernelGGL(k_sift_down, dim3((unsigned)((w + 127) / 128), (unsigned)h), dim3(128), 0, nullptr, ow[o - 1],
-                         gptr[(o - 1) * (SIFT_S + 3) + SIFT_S], w, h, gptr[o * (SIFT_S + 3)]);
-    const int64_t np = (int64_t)w * h;
-    bool fused_dog = true;
-    for (int i = 1; i < SIFT_S + 3; ++i)
-      fused_dog = blur(w, h, gptr[o * (SIFT_S + 3) + i - 1], gptr[o * (SIFT_S + 3) + i], i,
-                       blur2 ? Dg + doff[o] + (i - 1) * np : nullptr) && fused_dog;
-    if (!blur2 || !fused_dog)
-      hipLaunchKernelGGL(k_sift_dog, dim3((unsigned)((np * (SIFT_S + 2) + 255) / 256)), dim3(256), 0, nullptr, np,
-                         G + goff[o], Dg + doff[o]);
-    if (w > 2 * SIFT_BORDER && h > 2 * SIFT_BORDER)
-      hipLaunchKernelGGL(k_sift_extrema, dim3((unsigned)((w - 2 * SIFT_BORDER + 63) / 64), (unsigned)(h - 2 * SIFT_BORDER), SIFT_S),
-                         dim3(64), 0, nullptr, o, w, h, Dg + doff[o], thr, dcand.as<SiftCand>(), dcnt.as<int>(), CAP);
+  const int variant = ((knob("PTZ_SIFT_BLUR2") & 3) << 4) | ((knob("PTZ_SIFT_COLS_SW") & 3) << 2) |
+                      (knob("PTZ_SIFT_ROWS_SW") & 3);
+  std::vector<SiftKp> kps;
+  if (reuse && Wk.last_valid && Wk.last_w == width && Wk.last_h == height && Wk.last_variant == variant &&
+      std::memcmp(Wk.last_img.data(), img, img_bytes) == 0) {
+    kps = Wk.last_kps;  // the same image as the last call: its pyramid and keypoints are still on hand
+    st_mark("reuse");
+  } else {
+    Wk.last_valid = false;
+    HIPCHK(hipMemcpy(dimg.p, img, img_bytes, hipMemcpyHostToDevice));
+    std::vector<float> kflat((SIFT_S + 3) * kmax, 0.f);
+    for (int i = 0; i < SIFT_S + 3; ++i) std::copy(kern[i].begin(), kern[i].end(), kflat.begin() + i * kmax);
+    HIPCHK(hipMemcpy(dk.p, kflat.data(), kflat.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dow.p, ow.data(), n_oct * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(doh.p, oh.data(), n_oct * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(dcnt.p, 0, 16));
+    std::vector<float*> gptr(n_oct * (SIFT_S + 3));
+    float* G = dg.as<float>();
+    float* Dg = dd.as<float>();
+    float* T = dtmp.as<float>();
+    for (int o = 0; o < n_oct; ++o)
+      for (int i = 0; i < SIFT_S + 3; ++i) gptr[o * (SIFT_S + 3) + i] = G + goff[o] + (int64_t)i * ow[o] * oh[o];
+    HIPCHK(hipMemcpy(dptr.p, gptr.data(), gptr.size() * sizeof(float*), hipMemcpyHostToDevice));
+    st_mark("setup+upload");
+    // PTZ_SIFT_BLUR2=1: both blur passes and the DoG in one launch (A/B knob, read per call; measured 2.29 vs 2.23 ms
+    // per 1080p frame against the two-pass form, tools/sift_bench.py r04i -- the LDS-staged passes were not bound by
+    // the intermediate image's traffic)
+    const char* b2e = getenv("PTZ_SIFT_BLUR2");
+    const bool blur2 = b2e && atoi(b2e) == 1;
+    // sliding-window column pass, the default (PTZ_SIFT_COLS_SW=0: one output per thread; A/B knob, read per call):
+    // 1.816 -> 1.776 ms per 1080p detection (r04t), bit-identical
+    const char* cse = getenv("PTZ_SIFT_COLS_SW");
+    const bool cols_sw = !(cse && atoi(cse) == 0);
+    const char* rse = getenv("PTZ_SIFT_ROWS_SW");  // sliding-window row pass (A/B knob, read per call)
+    const bool rows_sw = rse && atoi(rse) == 1;
+    // dog_out: the DoG level dst - src written beside dst (fused form only)
+    auto blur = [&](int w, int h, const float* src, float* dst, int ki, float* dog_out) {
+      const int K = (int)kern[ki].size(), rr = K / 2;
+      const int n2 = BLUR2_T + 2 * rr;
+      const size_t lds = ((size_t)n2 * n2 + (size_t)n2 * (BLUR2_T + 1)) * sizeof(float);
+      if (blur2 && lds <= 64 * 1024) {  // (radius <= 14: every blur of OpenCV's default SIFT)
+        hipLaunchKernelGGL(k_sift_blur2, dim3((unsigned)((w + BLUR2_T - 1) / BLUR2_T), (unsigned)((h + BLUR2_T - 1) / BLUR2_T)),
+                           dim3(256), lds, nullptr, w, h, src, dst, dk.as<float>() + ki * kmax, K,
+                           dog_out ? src : nullptr, dog_out);
+        return true;
+      }
+      if (rows_sw)
+        hipLaunchKernelGGL(k_sift_blur_rows_sw, dim3((unsigned)((w + BRS_C - 1) / BRS_C), (unsigned)((h + BRS_R - 1) / BRS_R)),
+                           dim3(256), 0, nullptr, w, h, src, T, dk.as<float>() + ki * kmax, K);
+      else
+        hipLaunchKernelGGL(k_sift_blur_rows, dim3((unsigned)((w + BLUR_TX - 1) / BLUR_TX), (unsigned)h), dim3(BLUR_TX), 0,
+                           nullptr, w, h, src, T, dk.as<float>() + ki * kmax, K);
+      if (cols_sw)
+        hipLaunchKernelGGL(k_sift_blur_cols_sw, dim3((unsigned)((w + BLUR_CT - 1) / BLUR_CT), (unsigned)((h + BLUR_CR - 1) / BLUR_CR)),
+                           dim3(256), 0, nullptr, w, h, T, dst, dk.as<float>() + ki * kmax, K);
+      else
+        hipLaunchKernelGGL(k_sift_blur_cols, dim3((unsigned)((w + BLUR_CT - 1) / BLUR_CT), (unsigned)((h + BLUR_CR - 1) / BLUR_CR)),
+                           dim3(256), 0, nullptr, w, h, T, dst, dk.as<float>() + ki * kmax, K);
+      return false;
+    };
+    // base: doubled image, then the blur from the assumed input blur to sigma
+    hipLaunchKernelGGL(k_sift_up, dim3((unsigned)((W0 + 127) / 128), (unsigned)H0), dim3(128), 0, nullptr, width, height,
+                       dimg.as<uint8_t>(), gptr[1]);
+    blur(W0, H0, gptr[1], gptr[0], 0, nullptr);
+    const float thr = (float)std::floor(0.5 * SIFT_CONTR / SIFT_S * 255);
+    for (int o = 0; o < n_oct; ++o) {
+      const int w = ow[o], h = oh[o];
+      if (o > 0)
+        hipLaunchKernelGGL(k_sift_down, dim3((unsigned)((w + 127) / 128), (unsigned)h), dim3(128), 0, nullptr, ow[o - 1],
+                           gptr[(o - 1) * (SIFT_S + 3) + SIFT_S], w, h, gptr[o * (SIFT_S + 3)]);
+      const int64_t np = (int64_t)w * h;
+      bool fused_dog = true;
+      for (int i = 1; i < SIFT_S + 3; ++i)
+        fused_dog = blur(w, h, gptr[o * (SIFT_S + 3) + i - 1], gptr[o * (SIFT_S + 3) + i], i,
+                         blur2 ? Dg + doff[o] + (i - 1) * np : nullptr) && fused_dog;
+      if (!blur2 || !fused_dog)
+        hipLaunchKernelGGL(k_sift_dog, dim3((unsigned)((np * (SIFT_S + 2) + 255) / 256)), dim3(256), 0, nullptr, np,
+                           G + goff[o], Dg + doff[o]);
+      if (w > 2 * SIFT_BORDER && h > 2 * SIFT_BORDER)
+        hipLaunchKernelGGL(k_sift_extrema, dim3((unsigned)((w - 2 * SIFT_BORDER + 63) / 64), (unsigned)(h - 2 * SIFT_BORDER), SIFT_S),
+                           dim3(64), 0, nullptr, o, w, h, Dg + doff[o], thr, dcand.as<SiftCand>(), dcnt.as<int>(), CAP);
+    }
+    HIPCHK(hipGetLastError());
+    st_mark("pyramid queued");
+    int cnt[2];
+    HIPCHK(hipMemcpy(cnt, dcnt.p, 8, hipMemcpyDeviceToHost));
+    st_mark("pyramid+extrema");
+    if (cnt[0] > CAP) return fail("%d SIFT extrema exceed the candidate list (%d)", cnt[0], CAP);
+    const int nc = cnt[0];
+    if (nc > 0)
+      hipLaunchKernelGGL(k_sift_orient, dim3((unsigned)((nc + 3) / 4)), dim3(256), 0, nullptr, dcand.as<SiftCand>(),
+                         dcnt.as<int>(), (const float* const*)dptr.p, dow.as<int>(), doh.as<int>(), dkp.as<SiftKp>(),
+                         dcnt.as<int>() + 1, CAP);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(cnt, dcnt.p, 8, hipMemcpyDeviceToHost));
+    if (cnt[1] > CAP) return fail("%d SIFT keypoints exceed the keypoint list (%d)", cnt[1], CAP);
+    const int nk1 = cnt[1];
+    kps.resize(nk1);
+    if (nk1) HIPCHK(hipMemcpy(kps.data(), dkp.p, (size_t)nk1 * sizeof(SiftKp), hipMemcpyDeviceToHost));
+    if (reuse) {
+      Wk.last_img.assign(img, img + img_bytes);
+      Wk.last_w = width;
+      Wk.last_h = height;
+      Wk.last_variant = variant;
+      Wk.last_kps = kps;
+      Wk.last_valid = true;
+    }
+    st_mark("orientation");
   }
-  HIPCHK(hipGetLastError());
-  st_mark("pyramid queued");
-  int cnt[2];
-  HIPCHK(hipMemcpy(cnt, dcnt.p, 8, hipMemcpyDeviceToHost));
-  st_mark("pyramid+extrema");
-  if (cnt[0] > CAP) return fail("%d SIFT extrema exceed the candidate list (%d)", cnt[0], CAP);
-  const int nc = cnt[0];
-  if (nc > 0)
-    hipLaunchKernelGGL(k_sift_orient, dim3((unsigned)((nc + 3) / 4)), dim3(256), 0, nullptr, dcand.as<SiftCand>(),
-                       dcnt.as<int>(), (const float* const*)dptr.p, dow.as<int>(), doh.as<int>(), dkp.as<SiftKp>(),
-                       dcnt.as<int>() + 1, CAP);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpy(cnt, dcnt.p, 8, hipMemcpyDeviceToHost));
-  if (cnt[1] > CAP) return fail("%d SIFT keypoints exceed the keypoint list (%d)", cnt[1], CAP);
-  const int nk = cnt[1];
-  std::vector<SiftKp> kps(nk);
-  if (nk) HIPCHK(hipMemcpy(kps.data(), dkp.p, (size_t)nk * sizeof(SiftKp), hipMemcpyDeviceToHost));
-  st_mark("orientation");
+  const int nk = (int)kps.size();
   // strongest first (ties: y, x, angle, then detection order -- a total order, so selecting the first n and sorting
   // only them gives exactly the stable sort's first n)
   int n = nk;

@@ -300,6 +300,29 @@ def test_sift_matches_oracle(gpu_available, monkeypatch, seed, w, h, sw):
     assert np.all(np.diff(rg) <= 0)
 
 
+def test_sift_same_image_reuses_pyramid(gpu_available, monkeypatch):
+    """A call on the image of the previous call reuses its pyramid and oriented keypoints (a stream detects a frame
+    with 500 features, then again with 1500 when it becomes a keyframe): the results equal fresh detections
+    (PTZ_SIFT_REUSE=0), and a changed image of the same size is detected afresh."""
+    import ptzba
+    I, J, _ = frontend_data.textured_pair(seed=5, width=320, height=240, d_pan=0.7, f=450.0)
+    monkeypatch.setenv("PTZ_SIFT_REUSE", "0")
+    fresh = {(k, n): ptzba.sift(X, n) for k, X in (("I", I), ("J", J)) for n in (50, 0, 200)}
+    monkeypatch.setenv("PTZ_SIFT_REUSE", "1")
+    for k, X, n in (("I", I, 50), ("I", I, 0), ("I", I, 200), ("J", J, 200), ("J", J, 50), ("I", I, 0)):
+        got = ptzba.sift(X.copy(), n)  # a copy: reuse is decided by content, not by the array object
+        for a, b in zip(got, fresh[(k, n)]):
+            assert np.array_equal(a, b)
+    K = I.copy()
+    K[7, 11] ^= 1  # one pixel differs: a new detection
+    monkeypatch.setenv("PTZ_SIFT_REUSE", "0")
+    want = ptzba.sift(K, 0)
+    monkeypatch.setenv("PTZ_SIFT_REUSE", "1")
+    ptzba.sift(I, 0)
+    for a, b in zip(ptzba.sift(K, 0), want):
+        assert np.array_equal(a, b)
+
+
 def test_sift_front_end_recovers_homography(gpu_available):
     """The whole GPU front-end on two 640 x 360 textured views: SIFT (ptz_sift) -> kNN-2 + ratio test ->
     homography RANSAC (image_process.match_sift_features) recovers the true PTZ homography."""
