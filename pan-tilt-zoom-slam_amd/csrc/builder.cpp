@@ -334,35 +334,52 @@ int ptz_keyframe_feature_counts(int32_t n_frames, int64_t n_matches, const int32
     kmax = std::max(kmax, std::max(k1[k], k2[k]));
   }
   // a window's keyframes (cells of one frame x keypoint table fit 64 MiB): one sequential pass over the matches
-  // marks each (keyframe, keypoint) with its first landmark; only a keyframe with a keypoint under two landmarks
-  // counts its distinct pairs by a sort
+  // marks each (keyframe, keypoint) cell with its first landmark and counts it; a side whose keypoint already carries
+  // another landmark (inconsistent matching) is set aside as (cell, first landmark) and (cell, landmark), and those
+  // are deduplicated in one open-addressing table: every distinct (cell, landmark) beyond the cell's first is one
+  // more pair of its keyframe (no sort: the container's branchy sorts of ~15K triples cost more than the pass)
   if ((int64_t)n_frames * (kmax + 1) <= ((int64_t)1 << 24)) {
     const int64_t kw = kmax + 1;
     std::vector<int32_t> tab((size_t)n_frames * kw, -1);
-    std::vector<uint8_t> conflict(n_frames, 0);
+    std::vector<uint64_t> ex;  // cell << 32 | landmark
     for (int f = 0; f < n_frames; ++f) counts_out[f] = 0;
-    auto put = [&](int f, int64_t kp, int32_t l) {
-      int32_t& m = tab[(size_t)f * kw + kp];
-      if (m < 0) {
-        m = l;
-        ++counts_out[f];
-      } else if (m != l) {
-        conflict[f] = 1;
-      }
-    };
     for (int64_t k = 0; k < n_matches; ++k) {
-      put(m_i[k], k1[k], (int32_t)lm[k]);
-      put(m_j[k], k2[k], (int32_t)lm[k]);
-    }
-    for (int f = 0; f < n_frames; ++f) {
-      if (!conflict[f]) continue;
-      std::vector<uint64_t> key;
-      for (int64_t k = 0; k < n_matches; ++k) {
-        if (m_i[k] == f) key.push_back(((uint64_t)k1[k] << 32) | (uint64_t)lm[k]);
-        if (m_j[k] == f) key.push_back(((uint64_t)k2[k] << 32) | (uint64_t)lm[k]);
+      const int32_t l = (int32_t)lm[k];
+      const size_t c1 = (size_t)m_i[k] * kw + k1[k], c2 = (size_t)m_j[k] * kw + k2[k];
+      int32_t& a1 = tab[c1];
+      if (a1 < 0) {
+        a1 = l;
+        ++counts_out[m_i[k]];
+      } else if (a1 != l) {
+        ex.push_back(((uint64_t)c1 << 32) | (uint32_t)a1);
+        ex.push_back(((uint64_t)c1 << 32) | (uint32_t)l);
       }
-      std::sort(key.begin(), key.end());
-      counts_out[f] = std::unique(key.begin(), key.end()) - key.begin();
+      int32_t& a2 = tab[c2];
+      if (a2 < 0) {
+        a2 = l;
+        ++counts_out[m_j[k]];
+      } else if (a2 != l) {
+        ex.push_back(((uint64_t)c2 << 32) | (uint32_t)a2);
+        ex.push_back(((uint64_t)c2 << 32) | (uint32_t)l);
+      }
+    }
+    if (!ex.empty()) {
+      size_t hs = 16;
+      while (hs < 2 * ex.size()) hs <<= 1;
+      std::vector<uint64_t> h(hs, ~0ull);
+      for (const uint64_t key : ex) {
+        size_t i = (size_t)((key * 0x9E3779B97F4A7C15ull) >> 20) & (hs - 1);
+        while (h[i] != ~0ull && h[i] != key) i = (i + 1) & (hs - 1);
+        if (h[i] == key) continue;
+        h[i] = key;  // a new (cell, landmark)
+        const size_t cell = (size_t)(key >> 32);
+        const int f = (int)(cell / (size_t)kw);
+        if (tab[cell] != -2) {  // the cell's first distinct landmark is already counted
+          tab[cell] = -2;
+        } else {
+          ++counts_out[f];
+        }
+      }
     }
     return 0;
   }
