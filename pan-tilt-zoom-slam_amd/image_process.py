@@ -56,13 +56,32 @@ class KeyPoint(tuple):
     @classmethod
     def from_rows(cls, xy, size, angle, response, octave=None):
         """[KeyPoint] from columns: xy [n, 2], size / angle / response [n] (Python floats after tolist: the values
-        the constructor's float() would give), octave [n] ints or None (0)."""
+        the constructor's float() would give), octave [n] ints or None (0).  The list carries the points as an [n, 2]
+        float64 array (`.xy`, == [k.pt for k in list]) for callers that want them without a loop."""
         n = len(size)
-        pts = list(map(tuple, np.asarray(xy, np.float64).reshape(-1, 2).tolist()))
+        xy64 = np.array(xy, np.float64).reshape(-1, 2)
+        pts = list(map(tuple, xy64.tolist()))
         oc = [0] * n if octave is None else [int(o) for o in octave]
         rows = zip(pts, np.asarray(size, np.float64).tolist(), np.asarray(angle, np.float64).tolist(),
                    np.asarray(response, np.float64).tolist(), oc)
-        return list(map(functools.partial(tuple.__new__, cls), rows))
+        out = KeyPointList(map(functools.partial(tuple.__new__, cls), rows))
+        xy64.flags.writeable = False
+        out.xy = xy64
+        return out
+
+
+class KeyPointList(list):
+    """A plain list of KeyPoint plus `.xy`, the points as a read-only [n, 2] float64 array (slices and copies are
+    plain lists: only the detector's own list carries it)."""
+    xy = None
+
+
+def keypoint_xy(kps):
+    """[n, 2] float64 array of the keypoints' .pt (the detector's array when the list carries one)."""
+    xy = getattr(kps, "xy", None)
+    if xy is not None and len(xy) == len(kps):
+        return xy
+    return np.array([k.pt for k in kps], dtype=np.float64).reshape(-1, 2)
 
 
 # detect_compute_* / detect_sift / match_*_features / homography_ransac / optical_flow_matching: GPU
