@@ -94,6 +94,16 @@ struct ptzba_ctx {
   // pinned staging of set_problem's small uploads (bump allocated, reset once the stream has drained them)
   uint8_t* stage = nullptr;
   size_t stage_cap = 0, stage_used = 0;
+  // set_problem queues its staged uploads and zero fills here and lands them with ONE copy of the staging range into
+  // stage_dev plus one scatter launch (flush_stage) instead of ~50 hipMemcpyAsync / hipMemsetAsync calls
+  struct StageOp {
+    void* dst;
+    size_t off;  // offset in the staging buffer; SIZE_MAX: zero fill
+    size_t n;
+  };
+  std::vector<StageOp> stage_ops;
+  bool stage_batch = false;
+  DBuf stage_dev;
   // single-launch factorisation (k_chol_pst): level of each task, tasks per level, per-level completion counters
   // [n_levels] + the ticket counter
   DBuf chol_lvl, chol_lvl_n, chol_lvl_cnt;
@@ -262,12 +272,74 @@ int ptzba_use_own_stream(ptzba_handle h) { return h ? ptzba_set_stream(h, h->own
 // buffer is reused only after the stream has drained (set_problem synchronises before its first upload and at the
 // end; a full buffer synchronises before wrapping).
 constexpr size_t STAGE_MAX = 4u << 20, STAGE_MIN_CAP = 8u << 20;
+constexpr int STAGE_OPS_PER_LAUNCH = 48;
+struct StageScatterArgs {
+  const uint8_t* src;
+  int n_ops;
+  uint8_t* dst[STAGE_OPS_PER_LAUNCH];
+  uint64_t off[STAGE_OPS_PER_LAUNCH];  // ~0: zero fill
+  uint64_t n[STAGE_OPS_PER_LAUNCH];
+};
+// every op's bytes over the grid: 16-B vectors when both ends are 16-B aligned (staging offsets and device
+// allocations are 256-B aligned), the tail (or an unaligned op) byte by byte
+__global__ __launch_bounds__(256) void k_stage_scatter(StageScatterArgs a) {
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (size_t)gridDim.x * blockDim.x;
+  for (int q = 0; q < a.n_ops; ++q) {
+    uint8_t* d = a.dst[q];
+    const bool zero = a.off[q] == ~(uint64_t)0;
+    const uint8_t* sp = zero ? nullptr : a.src + a.off[q];
+    const bool vec = (((uintptr_t)d | (uintptr_t)sp) & 15) == 0;  // (a sub-buffer fill may start unaligned)
+    const size_t n = a.n[q], n16 = vec ? n / 16 : 0;
+    for (size_t i = tid; i < n16; i += nt)
+      reinterpret_cast<uint4*>(d)[i] = zero ? make_uint4(0, 0, 0, 0) : reinterpret_cast<const uint4*>(sp)[i];
+    for (size_t i = 16 * n16 + tid; i < n; i += nt) d[i] = zero ? 0 : sp[i];
+  }
+}
+// lands the queued staged uploads and zero fills (stream-ordered after everything queued before)
+static int flush_stage(ptzba_ctx* h) {
+  if (h->stage_ops.empty()) return 0;
+  bool any_copy = false;
+  for (const auto& o : h->stage_ops) any_copy |= o.off != SIZE_MAX;
+  if (any_copy) {
+    if (h->stage_dev.reserve(h->stage_cap)) return -1;
+    HIPCHK(hipMemcpyAsync(h->stage_dev.p, h->stage, h->stage_used, hipMemcpyHostToDevice, h->st));
+  }
+  size_t tot = 0;
+  for (const auto& o : h->stage_ops) tot += o.n;
+  const unsigned blocks = (unsigned)std::min<size_t>(1024, std::max<size_t>(1, tot / 32768));
+  for (size_t q0 = 0; q0 < h->stage_ops.size(); q0 += STAGE_OPS_PER_LAUNCH) {
+    StageScatterArgs a{};
+    a.src = h->stage_dev.as<uint8_t>();
+    a.n_ops = (int)std::min<size_t>(STAGE_OPS_PER_LAUNCH, h->stage_ops.size() - q0);
+    for (int q = 0; q < a.n_ops; ++q) {
+      const auto& o = h->stage_ops[q0 + q];
+      a.dst[q] = (uint8_t*)o.dst;
+      a.off[q] = o.off == SIZE_MAX ? ~(uint64_t)0 : (uint64_t)o.off;
+      a.n[q] = o.n;
+    }
+    hipLaunchKernelGGL(k_stage_scatter, dim3(blocks), dim3(256), 0, h->st, a);
+    HIPCHK(hipGetLastError());
+  }
+  h->stage_ops.clear();
+  return 0;
+}
+// n zero bytes at p on the handle's stream (queued with the staged uploads while set_problem batches them)
+static int zero_async(ptzba_ctx* h, void* p, size_t n) {
+  if (!p || !n) return 0;
+  if (h->stage_batch) {
+    h->stage_ops.push_back({p, SIZE_MAX, n});
+    return 0;
+  }
+  HIPCHK(hipMemsetAsync(p, 0, n, h->st));
+  return 0;
+}
 // a pinned staging slot of n bytes for one queued copy (*out = nullptr when n is too large for the staging path)
 static int stage_take(ptzba_ctx* h, size_t n, uint8_t** out) {
   *out = nullptr;
   if (n > STAGE_MAX) return 0;
   size_t off = (h->stage_used + 255) & ~(size_t)255;
   if (!h->stage || off + n > h->stage_cap) {
+    if (flush_stage(h)) return -1;         // the queued copies read the staging buffer: land them first
     HIPCHK(hipStreamSynchronize(h->st));  // every staged copy so far has landed
     off = 0;
     if (!h->stage) {
@@ -290,6 +362,10 @@ static int upload_st(ptzba_ctx* h, DBuf& b, const std::vector<T>& v) {
   uint8_t* p = nullptr;
   if (stage_take(h, n, &p)) return -1;
   std::memcpy(p, v.data(), n);
+  if (h->stage_batch) {
+    h->stage_ops.push_back({b.p, (size_t)(p - h->stage), n});
+    return 0;
+  }
   HIPCHK(hipMemcpyAsync(b.p, p, n, hipMemcpyHostToDevice, h->st));
   return 0;
 }
@@ -335,6 +411,11 @@ static int upload_records(ptzba_ctx* h, const std::vector<int64_t>& order, const
       if (w) ww[r] = (real)w[order[r]];
     }
   });
+  if (staged && h->stage_batch) {  // queued with set_problem's other staged uploads
+    h->stage_ops.push_back({h->rec_xy.p, (size_t)(pxy - h->stage), nxy * sizeof(real)});
+    if (w) h->stage_ops.push_back({h->rec_w.p, (size_t)(pw - h->stage), nw * sizeof(real)});
+    return zero_async(h, reinterpret_cast<real*>(h->rec_xy.p) + nxy, 8 * sizeof(real));
+  }
   HIPCHK(hipMemcpyAsync(h->rec_xy.p, xy, nxy * sizeof(real), hipMemcpyHostToDevice, h->st));
   HIPCHK(hipMemsetAsync(reinterpret_cast<real*>(h->rec_xy.p) + nxy, 0, 8 * sizeof(real), h->st));
   if (w) HIPCHK(hipMemcpyAsync(h->rec_w.p, ww, nw * sizeof(real), hipMemcpyHostToDevice, h->st));
@@ -1822,6 +1903,13 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   // ---- upload (staged: the stream has drained, so the staging buffer is free)
   HIPCHK(hipStreamSynchronize(h->st));
   h->stage_used = 0;
+  h->stage_ops.clear();
+  // PTZBA_STAGE_BATCH=0: one hipMemcpyAsync / hipMemsetAsync per array (A/B knob)
+  h->stage_batch = !getenv_is("PTZBA_STAGE_BATCH", "0");
+  struct BatchOff {  // every exit (errors included) leaves the batching off
+    ptzba_ctx* h;
+    ~BatchOff() { h->stage_batch = false; }
+  } batch_off{h};
   st_mark("pre-upload sync");
   std::vector<double> seg_base(2 * n_seg);
   for (int64_t s = 0; s < n_seg; ++s) {
@@ -1855,7 +1943,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
         if (it < h->n_s2_items) item_group[it] = g;  // (pair items: their first chunk's tile)
     if (upload_st(h, h->s2_item_group, item_group) || h->s2_tile_cnt.alloc((size_t)std::max(h->n_s2_groups, 1) * 4))
       return -1;
-    HIPCHK(hipMemsetAsync(h->s2_tile_cnt.p, 0, h->s2_tile_cnt.bytes, h->st));
+    if (zero_async(h, h->s2_tile_cnt.p, h->s2_tile_cnt.bytes)) return -1;
   }
   const size_t e = h->elem();
   if (h->ptz.alloc(3 * n_pose * 8) || h->ptz_trial.alloc(3 * n_pose * 8) || h->rays.alloc(2 * (size_t)n_landmark * 8) ||
@@ -1892,10 +1980,10 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     h->ph_tiles[q].release();
     h->ph_buf[q].release();
   }
-  if (h->dpose.p) HIPCHK(hipMemsetAsync(h->dpose.p, 0, h->dpose.bytes, h->st));  // rows a part-owned rank never solves
+  if (zero_async(h, h->dpose.p, h->dpose.bytes)) return -1;  // rows a part-owned rank never solves
   h->n_xtiles = (int)(plan.xtiles.size() / 2);
   h->n_ztiles = (int)(plan.ztiles.size() / 2);
-  HIPCHK(hipMemsetAsync(h->sys.p, 0, h->sys.bytes, h->st));  // outside the factor's tiles it is never written
+  if (zero_async(h, h->sys.p, h->sys.bytes)) return -1;  // outside the factor's tiles it is never written
   h->bs_nupd = (int)plan.upd_tiles.size();
   h->bs_npos = (int)plan.chain_cols.size();
   h->bs_ntasks = plan.n_tasks;
@@ -1935,7 +2023,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     if (upload_st(h, h->chol_lvl, lvl) || upload_st(h, h->chol_lvl_n, lvl_n) ||
         h->chol_lvl_cnt.alloc(4 * ((size_t)plan.n_levels + 1)))
       return -1;
-    HIPCHK(hipMemsetAsync(h->chol_lvl_cnt.p, 0, h->chol_lvl_cnt.bytes, h->st));
+    if (zero_async(h, h->chol_lvl_cnt.p, h->chol_lvl_cnt.bytes)) return -1;
   }
   if ((h->bs_pst || h->chol_pst) && !h->bsp_err) {
     HIPCHK(hipHostMalloc((void**)&h->bsp_err, sizeof(int), hipHostMallocDefault));
@@ -1945,7 +2033,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     if (upload_st(h, h->bsp_expect, plan.bsb_expect) || upload_st(h, h->bsp_tot, plan.bsb_tot) ||
         h->bsp_cnt.alloc(4 * plan.bsb_tot.size()))
       return -1;
-    HIPCHK(hipMemsetAsync(h->bsp_cnt.p, 0, h->bsp_cnt.bytes, h->st));
+    if (zero_async(h, h->bsp_cnt.p, h->bsp_cnt.bytes)) return -1;
   }
   if (h->bs_blk) {
     if (upload_st(h, h->bsb_tasks, plan.bsb_tasks) ||
@@ -1956,18 +2044,17 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     h->bsb_r.release();
   }
   h->xbuf.release();  // allocated on first ptzba_exchange_packed
-  HIPCHK(hipMemsetAsync(h->D_pose.p, 0, h->D_pose.bytes, h->st));
-  HIPCHK(hipMemsetAsync(h->D_ray.p, 0, h->D_ray.bytes, h->st));
-  HIPCHK(hipMemsetAsync(h->w_slot[0].p, 0, h->w_slot[0].bytes, h->st));  // slots of unobserved frames stay zero
-  HIPCHK(hipMemsetAsync(h->w_slot[1].p, 0, h->w_slot[1].bytes, h->st));
-  HIPCHK(hipMemsetAsync(h->lm_out[0].p, 0, h->lm_out[0].bytes, h->st));  // landmarks without records keep zero rows
-  HIPCHK(hipMemsetAsync(h->lm_out[1].p, 0, h->lm_out[1].bytes, h->st));
-  HIPCHK(hipMemsetAsync(h->ug_slot[0].p, 0, h->ug_slot[0].bytes, h->st));
-  HIPCHK(hipMemsetAsync(h->ug_slot[1].p, 0, h->ug_slot[1].bytes, h->st));
-  HIPCHK(hipMemsetAsync(h->ptz.p, 0, h->ptz.bytes, h->st));
-  HIPCHK(hipMemsetAsync(h->rays.p, 0, h->rays.bytes, h->st));
-  HIPCHK(hipMemsetAsync(h->scal.p, 0, h->scal.bytes, h->st));
-  HIPCHK(hipMemsetAsync(h->red_scratch.p, 0, h->red_scratch.bytes, h->st));
+  if (zero_async(h, h->D_pose.p, h->D_pose.bytes) || zero_async(h, h->D_ray.p, h->D_ray.bytes) ||
+      zero_async(h, h->w_slot[0].p, h->w_slot[0].bytes) ||  // slots of unobserved frames stay zero
+      zero_async(h, h->w_slot[1].p, h->w_slot[1].bytes) ||
+      zero_async(h, h->lm_out[0].p, h->lm_out[0].bytes) ||  // landmarks without records keep zero rows
+      zero_async(h, h->lm_out[1].p, h->lm_out[1].bytes) || zero_async(h, h->ug_slot[0].p, h->ug_slot[0].bytes) ||
+      zero_async(h, h->ug_slot[1].p, h->ug_slot[1].bytes) || zero_async(h, h->ptz.p, h->ptz.bytes) ||
+      zero_async(h, h->rays.p, h->rays.bytes) || zero_async(h, h->scal.p, h->scal.bytes) ||
+      zero_async(h, h->red_scratch.p, h->red_scratch.bytes))
+    return -1;
+  if (flush_stage(h)) return -1;
+  h->stage_batch = false;
   st_mark("upload+alloc");
   if (!h->scal_host) HIPCHK(hipHostMalloc((void**)&h->scal_host, 24 * sizeof(double), hipHostMallocDefault));
   if (!h->scal_pack.p && h->scal_pack.alloc(24 * sizeof(double))) return -1;
