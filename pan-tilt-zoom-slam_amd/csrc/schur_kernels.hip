@@ -938,16 +938,31 @@ __device__ __forceinline__ void schur_reduce_elem(const SchurArgs& a, const int4
   const int f1b = g.x, chunk = g.y;
   const int ln = e & 63, ik = e >> 6, i = ik / 9, k = ik - 9 * i, q = k / 3, r = k - 3 * q;
   const int f1 = f1b + i, f2 = f1b + WAVE * chunk + ln;
-  if (!(f1 < a.n_pose && f2 >= f1 && f2 <= a.frame_win_hi[f1])) return;
+  // the window bound and both frames' system positions in one round trip (clamped indices: a thread outside the
+  // window reads a valid entry and leaves)
+  const int f1c = min(f1, a.n_pose - 1), f2c = min(f2, a.n_pose - 1);
+  const int whi = a.frame_win_hi[f1c];
+  const int64_t col0 = a.frame_pos[f1c], pf2 = a.frame_pos[f2c];
+  if (!(f1 < a.n_pose && f2 >= f1 && f2 <= whi)) return;
   const real* p = (const real*)a.part + e;
   double v = 0;
   int it = g.z;
-  for (; it + 4 <= g.w; it += 4) {
-    const double p0 = part_load<real, AGENT>(p + (int64_t)it * NE), p1 = part_load<real, AGENT>(p + (int64_t)(it + 1) * NE);
-    const double p2 = part_load<real, AGENT>(p + (int64_t)(it + 2) * NE), p3 = part_load<real, AGENT>(p + (int64_t)(it + 3) * NE);
-    v += p0; v += p1; v += p2; v += p3;
+  // up to 8 splits' partials in flight (a tile has ~8 at config 3: one round trip), summed in item order
+  for (; it + 8 <= g.w; it += 8) {
+    double x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = part_load<real, AGENT>(p + (int64_t)(it + u) * NE);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v += x[u];
   }
-  for (; it < g.w; ++it) v += (double)part_load<real, AGENT>(p + (int64_t)it * NE);
+  if (it < g.w) {
+    double x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = it + u < g.w ? (double)part_load<real, AGENT>(p + (int64_t)(it + u) * NE) : 0.0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (it + u < g.w) v += x[u];
+  }
   if (f2 == f1) {  // chunk 0: U of the frame, summed over the tile's splits
     const int ui = q <= r ? (q == 0 ? r : (q == 1 ? 2 + r : 5)) : (r == 0 ? q : (r == 1 ? 2 + q : 5));
     double du = 0;  // diag U as the chunk-0 vector block sums it (fresh, item order): the damping's scale
@@ -961,13 +976,13 @@ __device__ __forceinline__ void schur_reduce_elem(const SchurArgs& a, const int4
       double* D = a.prep.D_pose + 3 * (int64_t)f1 + q;
       const double d = fmax(*D, fmax(du, 1e-12));
       *D = d;
-      const int64_t row = a.frame_pos[f1] + q;
+      const int64_t row = col0 + q;
       a.S[row * a.ld + row] = v;
       a.S[row * a.ld + row] += lambda * d;
       return;
     }
   }
-  const int64_t ld = a.ld, col0 = a.frame_pos[f1], pf2 = a.frame_pos[f2];
+  const int64_t ld = a.ld;
   if (pf2 >= col0) a.S[(pf2 + r) * ld + col0 + q] = v;
   else a.S[(col0 + q) * ld + pf2 + r] = v;
 }
