@@ -1,0 +1,6 @@
+#!/bin/bash
+# round-4 final pass, part 2: rocprofv3 kernel stats, K1 / K2 PMC traffic, the bench line with this run's traffic,
+# PMC calibration, smoke, config-4 bench (tools/r04b.sh with TAG=r04fin)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+TAG=r04fin bash tools/r04b.sh
