@@ -514,6 +514,13 @@ struct SiftWork {
   int32_t last_w = 0, last_h = 0, last_variant = -1;  // (variant: the blur A/B knobs the pyramid was built with)
   std::vector<ptzba::SiftKp> last_kps;
   bool last_valid = false;
+  // the blur kernels, octave sizes and level pointers uploaded for (width, height, pyramid buffer): constant per
+  // stream, so a frame of the same size skips their four synchronous copies
+  int32_t tab_w = 0, tab_h = 0;
+  void* tab_p[5] = {};  // dg, dk, dow, doh, dptr when the tables were uploaded
+  // pinned staging of the 8-bit image (the H2D copy is asynchronous; the call synchronises before it returns)
+  uint8_t* pin = nullptr;
+  size_t pin_cap = 0;
 };
 SiftWork& sift_work(int device) { return ptzba::work_for<SiftWork>(device); }  // under device_work_lock
 
@@ -600,20 +607,36 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
     st_mark("reuse");
   } else {
     Wk.last_valid = false;
-    HIPCHK(hipMemcpy(dimg.p, img, img_bytes, hipMemcpyHostToDevice));
-    std::vector<float> kflat((SIFT_S + 3) * kmax, 0.f);
-    for (int i = 0; i < SIFT_S + 3; ++i) std::copy(kern[i].begin(), kern[i].end(), kflat.begin() + i * kmax);
-    HIPCHK(hipMemcpy(dk.p, kflat.data(), kflat.size() * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(dow.p, ow.data(), n_oct * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(doh.p, oh.data(), n_oct * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemset(dcnt.p, 0, 16));
+    if (Wk.pin_cap < img_bytes) {
+      if (Wk.pin) (void)hipHostFree(Wk.pin);
+      Wk.pin = nullptr;
+      Wk.pin_cap = 0;
+      HIPCHK(hipHostMalloc((void**)&Wk.pin, img_bytes, hipHostMallocDefault));
+      Wk.pin_cap = img_bytes;
+    }
+    HIPCHK(hipStreamSynchronize(nullptr));  // (a previous call that failed midway may still be reading it)
+    std::memcpy(Wk.pin, img, img_bytes);
+    HIPCHK(hipMemcpyAsync(dimg.p, Wk.pin, img_bytes, hipMemcpyHostToDevice, nullptr));
     std::vector<float*> gptr(n_oct * (SIFT_S + 3));
     float* G = dg.as<float>();
     float* Dg = dd.as<float>();
     float* T = dtmp.as<float>();
     for (int o = 0; o < n_oct; ++o)
       for (int i = 0; i < SIFT_S + 3; ++i) gptr[o * (SIFT_S + 3) + i] = G + goff[o] + (int64_t)i * ow[o] * oh[o];
-    HIPCHK(hipMemcpy(dptr.p, gptr.data(), gptr.size() * sizeof(float*), hipMemcpyHostToDevice));
+    void* const tabs[5] = {dg.p, dk.p, dow.p, doh.p, dptr.p};
+    if (Wk.tab_w != width || Wk.tab_h != height || !std::equal(tabs, tabs + 5, Wk.tab_p)) {
+      Wk.tab_w = 0;  // (stays invalid if a copy below fails)
+      std::vector<float> kflat((SIFT_S + 3) * kmax, 0.f);
+      for (int i = 0; i < SIFT_S + 3; ++i) std::copy(kern[i].begin(), kern[i].end(), kflat.begin() + i * kmax);
+      HIPCHK(hipMemcpy(dk.p, kflat.data(), kflat.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(dow.p, ow.data(), n_oct * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(doh.p, oh.data(), n_oct * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(dptr.p, gptr.data(), gptr.size() * sizeof(float*), hipMemcpyHostToDevice));
+      Wk.tab_w = width;
+      Wk.tab_h = height;
+      std::copy(tabs, tabs + 5, Wk.tab_p);
+    }
+    HIPCHK(hipMemsetAsync(dcnt.p, 0, 16, nullptr));
     st_mark("setup+upload");
     // PTZ_SIFT_BLUR2=1: both blur passes and the DoG in one launch (A/B knob, read per call; measured 2.29 vs 2.23 ms
     // per 1080p frame against the two-pass form, tools/sift_bench.py r04i -- the LDS-staged passes were not bound by
