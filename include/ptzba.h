@@ -409,7 +409,10 @@ PTZBA_EXPORT int ptz_match_hamming(int device, int64_t n1, int64_t n2, int32_t n
  * it, image_process.py:56-79): img 8-bit grey width x height; OpenCV's defaults (image doubled, 3 layers per octave,
  * sigma 1.6, contrast 0.04, edge 10).  Keypoints ordered by (-response, y, x, angle) and cut to nfeatures (> 0;
  * 0 keeps all); *n_out = their number, of which the first min(n, max_kp) are written: kp_out [.][4] = (x, y, size,
- * angle in degrees), response_out [.] (may be NULL), des_out [.][128] (integer values 0..255 as float). */
+ * angle in degrees), response_out [.] (may be NULL), des_out [.][128] (integer values 0..255 as float).
+ * A call on the same image content as the previous call on this device (a frame detected with 500 features, then
+ * with 1500 as a keyframe) reuses that call's pyramid and oriented keypoints: the same result, selection and
+ * descriptors only (PTZ_SIFT_REUSE=0 disables it). */
 PTZBA_EXPORT int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int32_t nfeatures, int32_t max_kp,
                           float* kp_out, float* response_out, float* des_out, int32_t* n_out);
 
