@@ -98,6 +98,34 @@ __global__ __launch_bounds__(BLUR_TX) void k_sift_blur_rows(int w, int h, const 
   dst[(int64_t)y * w + x] = acc;
 }
 
+// Row pass over BLUR_RB rows per workgroup (round 4): the rows' segments are requested together, so a workgroup has
+// BLUR_RB times the bytes in flight of k_sift_blur_rows (whose one-row workgroups wait out one load latency each);
+// per output the same products in the same order: bit-identical (PTZ_SIFT_ROWS4=0 restores k_sift_blur_rows, A/B).
+constexpr int BLUR_RB = 4;
+__global__ __launch_bounds__(BLUR_TX) void k_sift_blur_rows4(int w, int h, const float* __restrict__ src,
+                                                              float* __restrict__ dst, const float* __restrict__ wt, int K) {
+  __shared__ float tile[BLUR_RB][BLUR_TX + 2 * BLUR_RMAX];
+  __shared__ float sw[2 * BLUR_RMAX + 1];
+  const int x0 = blockIdx.x * BLUR_TX, y0 = blockIdx.y * BLUR_RB, r = K / 2, t = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < BLUR_RB; ++q) {
+    const int y = min(y0 + q, h - 1);  // (rows past the image: a valid row, never stored)
+    const float* row = src + (int64_t)y * w;
+    for (int i = t; i < BLUR_TX + 2 * r; i += BLUR_TX) tile[q][i] = row[refl101(x0 + i - r, w)];
+  }
+  if (t < K) sw[t] = wt[t];
+  __syncthreads();
+  const int x = x0 + t;
+  if (x >= w) return;
+#pragma unroll
+  for (int q = 0; q < BLUR_RB; ++q) {
+    if (y0 + q >= h) break;
+    float acc = 0.f;
+    for (int k = 0; k < K; ++k) acc = acc + sw[k] * tile[q][t + k];
+    dst[(int64_t)(y0 + q) * w + x] = acc;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_sift_blur_cols(int w, int h, const float* __restrict__ src,
                                                          float* __restrict__ dst, const float* __restrict__ wt, int K) {
   __shared__ float tile[BLUR_CR + 2 * BLUR_RMAX][BLUR_CT + 1];
@@ -598,8 +626,8 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
     const char* e = getenv(name);
     return e ? atoi(e) : -1;
   };
-  const int variant = ((knob("PTZ_SIFT_BLUR2") & 3) << 4) | ((knob("PTZ_SIFT_COLS_SW") & 3) << 2) |
-                      (knob("PTZ_SIFT_ROWS_SW") & 3);
+  const int variant = ((knob("PTZ_SIFT_ROWS4") & 3) << 6) | ((knob("PTZ_SIFT_BLUR2") & 3) << 4) |
+                      ((knob("PTZ_SIFT_COLS_SW") & 3) << 2) | (knob("PTZ_SIFT_ROWS_SW") & 3);
   std::vector<SiftKp> kps;
   if (reuse && Wk.last_valid && Wk.last_w == width && Wk.last_h == height && Wk.last_variant == variant &&
       std::memcmp(Wk.last_img.data(), img, img_bytes) == 0) {
@@ -649,6 +677,8 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
     const bool cols_sw = !(cse && atoi(cse) == 0);
     const char* rse = getenv("PTZ_SIFT_ROWS_SW");  // sliding-window row pass (A/B knob, read per call)
     const bool rows_sw = rse && atoi(rse) == 1;
+    const char* r4e = getenv("PTZ_SIFT_ROWS4");  // row pass over 4 rows per workgroup, the default (A/B, read per call)
+    const bool rows4 = !(r4e && atoi(r4e) == 0);
     // dog_out: the DoG level dst - src written beside dst (fused form only)
     auto blur = [&](int w, int h, const float* src, float* dst, int ki, float* dog_out) {
       const int K = (int)kern[ki].size(), rr = K / 2;
@@ -660,7 +690,10 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
                            dog_out ? src : nullptr, dog_out);
         return true;
       }
-      if (rows_sw)
+      if (rows4 && !rows_sw)
+        hipLaunchKernelGGL(k_sift_blur_rows4, dim3((unsigned)((w + BLUR_TX - 1) / BLUR_TX), (unsigned)((h + BLUR_RB - 1) / BLUR_RB)),
+                           dim3(BLUR_TX), 0, nullptr, w, h, src, T, dk.as<float>() + ki * kmax, K);
+      else if (rows_sw)
         hipLaunchKernelGGL(k_sift_blur_rows_sw, dim3((unsigned)((w + BRS_C - 1) / BRS_C), (unsigned)((h + BRS_R - 1) / BRS_R)),
                            dim3(256), 0, nullptr, w, h, src, T, dk.as<float>() + ki * kmax, K);
       else
