@@ -100,7 +100,8 @@ __global__ __launch_bounds__(BLUR_TX) void k_sift_blur_rows(int w, int h, const 
 
 // Row pass over BLUR_RB rows per workgroup (round 4): the rows' segments are requested together, so a workgroup has
 // BLUR_RB times the bytes in flight of k_sift_blur_rows (whose one-row workgroups wait out one load latency each);
-// per output the same products in the same order: bit-identical (PTZ_SIFT_ROWS4=0 restores k_sift_blur_rows, A/B).
+// per output the same products in the same order: bit-identical.  Opt-in (PTZ_SIFT_ROWS4=1): 10.5 vs 9.5 us per
+// launch on average, 1.86 vs 1.81 ms per 1080p detection (r04z8) -- the one-row form was not latency-bound.
 constexpr int BLUR_RB = 4;
 __global__ __launch_bounds__(BLUR_TX) void k_sift_blur_rows4(int w, int h, const float* __restrict__ src,
                                                               float* __restrict__ dst, const float* __restrict__ wt, int K) {
@@ -677,8 +678,10 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
     const bool cols_sw = !(cse && atoi(cse) == 0);
     const char* rse = getenv("PTZ_SIFT_ROWS_SW");  // sliding-window row pass (A/B knob, read per call)
     const bool rows_sw = rse && atoi(rse) == 1;
-    const char* r4e = getenv("PTZ_SIFT_ROWS4");  // row pass over 4 rows per workgroup, the default (A/B, read per call)
-    const bool rows4 = !(r4e && atoi(r4e) == 0);
+    // row pass over 4 rows per workgroup (PTZ_SIFT_ROWS4=1, A/B knob, read per call): measured slower, 0.481 vs
+    // 0.436 ms of row passes per 1080p detection (r04z8)
+    const char* r4e = getenv("PTZ_SIFT_ROWS4");
+    const bool rows4 = r4e && atoi(r4e) == 1;
     // dog_out: the DoG level dst - src written beside dst (fused form only)
     auto blur = [&](int w, int h, const float* src, float* dst, int ki, float* dog_out) {
       const int K = (int)kern[ki].size(), rr = K / 2;
