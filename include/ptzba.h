@@ -191,8 +191,15 @@ PTZBA_EXPORT int ptzba_solve_reduced(ptzba_handle h);
  * state ptzba_get_state / ptzba_save_state see, so every decided trial must be waited for. */
 typedef struct {
   double ftol, xtol, gtol;                    /* scipy's ftol/xtol/gtol tests (gtol <= 0: off) */
-  double lambda0, min_lambda, max_lambda;     /* Marquardt damping: start, floor, give-up bound */
+  double lambda0, min_lambda, max_lambda;     /* Marquardt damping: start, floor, give-up bound.  lambda0 =
+                                                 min_lambda (1e-12, the default) starts with Gauss-Newton steps, as
+                                                 scipy's trf does while its step lies inside the trust region */
   int32_t max_iter, max_retries, gauss_newton; /* accepted iterations; rejections in a row; lambda0 = 0 GN */
+  /* huber loss only: the records' curvature weight beyond the unit is rho' (IRLS, a majoriser of the loss) until an
+   * accepted step reduces the cost by less than curvature_switch of it; from then on huber_curvature * rho' (the
+   * loss's own Newton curvature is 0 there, scipy's robust scaling; floored), the current point re-linearised at
+   * once.  curvature_switch = 0 or huber_curvature = 1: IRLS throughout.  Defaults 0.1 / 0.25. */
+  double huber_curvature, curvature_switch;
 } ptzba_lm_opts;
 /* termination status (scipy least_squares numbering where it has one): DAMPING = the trial was rejected at
  * every damping up to max_lambda, i.e. no cost decrease is resolvable any more (scipy's trf ends such a run
@@ -230,6 +237,9 @@ PTZBA_EXPORT int ptzba_solve(ptzba_handle h, double* ptz_inout, double* rays_ino
  * ptzba_save_state snapshot.  The state stays on the device (ptzba_get_state reads it).  Back-to-back solves
  * from C keep the restart's host reaction out of the device's timeline (bench.py's restart loop). */
 PTZBA_EXPORT int ptzba_solve_resident(ptzba_handle h, int restore, const ptzba_lm_opts* opts, ptzba_report* report);
+/* host-driven LM (ptzba_linearize / ptzba_step): the huber curvature weight (in (0, 1], units of rho' beyond the
+ * unit) of the following linearisations; set_problem resets it to 1 (IRLS) */
+PTZBA_EXPORT int ptzba_set_huber_curvature(ptzba_handle h, double hc);
 PTZBA_EXPORT int ptzba_step(ptzba_handle h, double lambda);
 PTZBA_EXPORT int ptzba_read_scalars(ptzba_handle h, double* out /*PTZBA_NSCALARS*/);
 PTZBA_EXPORT int ptzba_accept(ptzba_handle h, int accept);

@@ -43,6 +43,8 @@ struct ptzba_ctx {
   bool have_problem = false;
   int n_pose = 0, n_lm = 0, n_fixed = 1, precision = PTZBA_FP64, loss = PTZBA_LOSS_LINEAR;
   double fs = 1.0;
+  double hcurv = 1.0;  // huber curvature weight beyond the unit, in units of rho' (LinArgs::hcurv), host-driven LM
+  bool lm_relin = false;  // device-driven LM: queue the conditional re-linearisation in lm_build
   int64_t n_rec = 0, n_seg = 0;
   int n_work = 0, max_seg_per_lm = 0;
   int n_sys = 0;
@@ -1470,6 +1472,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->precision = o.precision;
   h->loss = o.loss;
   h->fs = o.f_scale;
+  h->hcurv = 1.0;
   h->n_fixed = o.n_fixed;
   h->u = u;
   h->v = v;
@@ -2100,7 +2103,10 @@ static void tables(ptzba_ctx* h, const double* ptz, const double* rays, const in
 }
 
 // sel != nullptr (device-driven LM): the kernel writes slot (*sel ^ sel_xor), chosen on the device
-static void linearize_into(ptzba_ctx* h, int slot, const int* sel = nullptr, int sel_xor = 0) {
+// run_if != nullptr: a conditional re-linearisation of the current point (device-driven LM, after the curvature
+// switch): the launch exits at once unless *run_if; not timed as a K1 launch (the roofline averages real ones)
+static void linearize_into(ptzba_ctx* h, int slot, const int* sel = nullptr, int sel_xor = 0,
+                           const int* run_if = nullptr) {
   LinArgs a;
   a.lm_work = h->lm_order.as<int4>();
   a.n_work = h->n_work;
@@ -2120,6 +2126,9 @@ static void linearize_into(ptzba_ctx* h, int slot, const int* sel = nullptr, int
   a.v = h->v;
   a.fs2 = h->fs * h->fs;
   a.inv_fs2 = 1.0 / (h->fs * h->fs);
+  a.hcurv = h->hcurv;
+  a.hcurv_dev = sel ? &h->lmdev.as<LMDev>()->hc : nullptr;
+  a.run_if = run_if;
   a.ug_slot = h->ug_slot[slot].p;
   a.w_slot = h->w_slot[slot].p;
   a.lm_meta = h->lm_meta.as<int4>();
@@ -2135,12 +2144,12 @@ static void linearize_into(ptzba_ctx* h, int slot, const int* sel = nullptr, int
   a.w_slot1 = h->w_slot[1].p;
   a.lm_out1 = h->lm_out[1].as<double>();
   a.n_pose = h->n_pose;
-  tm_begin(h, TM_K1);
+  if (!run_if) tm_begin(h, TM_K1);
   if (h->precision == PTZBA_FP32)
     launch_linearize<float>(a, h->loss, h->st);
   else
     launch_linearize<double>(a, h->loss, h->st);
-  tm_end(h, TM_K1);
+  if (!run_if) tm_end(h, TM_K1);
 }
 
 int ptzba_solver_info(ptzba_handle h, int64_t* info8) {
@@ -2515,8 +2524,13 @@ int ptzba_lm_init(ptzba_handle h, const ptzba_lm_opts* o) {
   if (!(o->lambda0 >= 0) || !(o->min_lambda > 0) || !(o->max_lambda > 0) || o->max_iter < 0 || o->max_retries < 1)
     return fail("bad LM options");
   HIPCHK(hipSetDevice(h->device));
-  LMParams p{o->ftol, o->xtol, o->gtol, o->lambda0, o->min_lambda, o->max_lambda, o->max_iter, o->max_retries,
+  if (!(o->huber_curvature > 0.0 && o->huber_curvature <= 1.0) || !(o->curvature_switch >= 0.0))
+    return fail("bad LM options (huber_curvature in (0, 1], curvature_switch >= 0)");
+  const bool sw = h->loss == PTZBA_LOSS_HUBER && o->curvature_switch > 0.0 && o->huber_curvature < 1.0;
+  LMParams p{o->ftol, o->xtol, o->gtol, o->lambda0, o->min_lambda, o->max_lambda,
+             sw ? o->huber_curvature : 1.0, sw ? o->curvature_switch : 0.0, o->max_iter, o->max_retries,
              o->gauss_newton ? 1 : 0, 0};
+  h->lm_relin = sw;  // re-linearisation launches are queued until the host sees the switch
   // no decision of an earlier run is in flight (its lm_wait returned): clear the ring's sequence tags
   for (int k = 0; k < LM_RING; ++k) __atomic_store_n(&h->lm_host[k].seq, 0, __ATOMIC_RELAXED);
   launch_lm_init(h->lmdev.as<LMDev>(), h->scal.as<double>(), p, h->cur, h->st);
@@ -2529,6 +2543,9 @@ int ptzba_lm_init(ptzba_handle h, const ptzba_lm_opts* o) {
 int ptzba_lm_build(ptzba_handle h) {
   if (lm_check(h)) return -1;
   HIPCHK(hipSetDevice(h->device));
+  // the curvature switch of the last decision (LMDev::relin): re-linearise the current point into its slot first.
+  // Queued only until the host has seen the switch in a decision record; the launch reads the flag on the device
+  if (h->lm_relin) linearize_into(h, 0, &h->lmdev.as<LMDev>()->cur, 0, &h->lmdev.as<LMDev>()->relin);
   // a build queued after the final decision (the host pipelines one trial ahead) exits at once
   return build_impl(h, 0.0, &h->lmdev.as<LMDev>()->lam, &h->lmdev.as<LMDev>()->done, &h->lmdev.as<LMDev>()->cur);
 }
@@ -2593,6 +2610,7 @@ int ptzba_lm_wait(ptzba_handle h, int trial, ptzba_lm_record* out) {
   out->status = r.status;
   out->done = r.done;
   out->accepted = r.accepted;
+  if (r.hc != 1.0) h->lm_relin = false;  // switched (and re-linearised in the build behind that decision)
   h->cur = r.cur;  // the host's view of the current slot follows the device (ptzba_accept / linearize)
   if ((r.cur ^ h->state_base) & 1) {
     // the device's decisions moved the current state to the other pair: swap the pointers and the base together,
@@ -2635,7 +2653,7 @@ static int lm_run(ptzba_ctx* h, const ptzba_lm_opts& o, ptzba_lm_record& rec) {
   }
   return 0;
 }
-static const ptzba_lm_opts k_default_opts{1e-4, 1e-8, 0.0, 1e-4, 1e-12, 1e16, 100, 30, 0};
+static const ptzba_lm_opts k_default_opts{1e-4, 1e-8, 0.0, 1e-12, 1e-12, 1e16, 100, 30, 0, 0.1, 0.25};
 
 int ptzba_solve_resident(ptzba_handle h, int restore, const ptzba_lm_opts* opts, ptzba_report* report) {
   if (!h || !h->have_problem) return fail("no problem set");
@@ -3313,3 +3331,12 @@ int ptzba_build_landmarks(int32_t n_frames, const int64_t* kp_count, int64_t n_p
 }
 
 
+
+// host-driven LM (ptzba.LMSolver._run_host, ptzba_linearize / ptzba_step): the huber curvature weight of the
+// following linearisations (the device-driven LM keeps its own in LMDev::hc)
+int ptzba_set_huber_curvature(ptzba_handle h, double hc) {
+  if (!h) return fail("null handle");
+  if (!(hc > 0.0 && hc <= 1.0)) return fail("huber curvature must lie in (0, 1]");
+  h->hcurv = hc;
+  return 0;
+}

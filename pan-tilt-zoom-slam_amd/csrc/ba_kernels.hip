@@ -171,6 +171,7 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
   const int task = blockIdx.x * 4 + wv;
+  if (a.run_if && !*a.run_if) return;  // conditional re-linearisation (device-driven LM): the whole grid leaves
   if constexpr (!FTL) {
     if (task >= a.n_work) return;  // whole wave leaves; no block-level barriers in this variant
   }
@@ -219,6 +220,7 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
   const int64_t slot0 = (int64_t)wm.z - wm.x;
   const real u = (real)a.u, v = (real)a.v;
   const real fs2 = (real)a.fs2, ifs2 = (real)a.inv_fs2;
+  const real hc = (real)(a.hcurv_dev ? *a.hcurv_dev : a.hcurv);
   real* sx = s_x[wv];
   real* sy = s_y[wv];
   real* acc0 = s_acc[wv][0];
@@ -263,12 +265,14 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
         ry = sy[key] - g.oy[u];
       }
       const real wt = valid ? g.wt[u] : (real)0;
-      real wx, wy, c;
+      real wx, wy, c, hx, hy;
       if constexpr (LOSS == 0) {
         wx = wt; wy = wt;
+        hx = wt; hy = wt;
         c = wt * (rx * rx + ry * ry);
       } else {
-        // scipy 'huber': rho(z) = z (z<=1), 2 sqrt(z) - 1; weight rho'(z) = 1 or 1/sqrt(z)
+        // scipy 'huber': rho(z) = z (z<=1), 2 sqrt(z) - 1; weight rho'(z) = 1 or 1/sqrt(z); curvature weight
+        // hc rho'(z) beyond the unit (hc = 1: IRLS; scipy's own rho' + 2 rho'' z is 0 there)
         real zx = rx * rx * ifs2, zy = ry * ry * ifs2;
         bool ix = zx <= (real)1, iy = zy <= (real)1;
         real sqx, sqy;
@@ -283,9 +287,11 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
           wy = iy ? wt : wt / sqy;
         }
         c = wt * fs2 * ((ix ? zx : (real)2 * sqx - (real)1) + (iy ? zy : (real)2 * sqy - (real)1));
+        hx = ix ? wx : wx * hc;
+        hy = iy ? wy : wy * hc;
       }
       cost += (double)c;
-      real v0 = wx, v1 = wy, v2 = wx * rx, v3 = wy * ry;
+      real v0 = hx, v1 = hy, v2 = wx * rx, v3 = wy * ry;
       // segmented inclusive scan over the wave, segments = runs of equal key (records are sorted):
       // shifts 1, 2, 4, 8 inside each 16-lane row, then row 15 -> rows 1, 3 and lane 31 -> rows 2, 3
       const int kenc = key + 2;  // >= 1; 0 is what a masked / out-of-row DPP source reads
@@ -344,9 +350,10 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
         ry = sy[key[j]] - g.oy[j];
       }
       const real wt = valid ? g.wt[j] : (real)0;
-      real wx, wy, c;
+      real wx, wy, c, hx, hy;
       if constexpr (LOSS == 0) {
         wx = wt; wy = wt;
+        hx = wt; hy = wt;
         c = wt * (rx * rx + ry * ry);
       } else {
         real zx = rx * rx * ifs2, zy = ry * ry * ifs2;
@@ -363,9 +370,11 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
           wy = iy ? wt : wt / sqy;
         }
         c = wt * fs2 * ((ix ? zx : (real)2 * sqx - (real)1) + (iy ? zy : (real)2 * sqy - (real)1));
+        hx = ix ? wx : wx * hc;
+        hy = iy ? wy : wy * hc;
       }
       cb += c;
-      v[j][0] = wx; v[j][1] = wy; v[j][2] = wx * rx; v[j][3] = wy * ry;
+      v[j][0] = hx; v[j][1] = hy; v[j][2] = wx * rx; v[j][3] = wy * ry;
     }
     cost += (double)cb;
     // the lane's tail run (key of its last record) joins the scan; earlier runs are the lane's alone
@@ -1051,6 +1060,7 @@ __global__ void k_lm_init(LMDev* st, const double* __restrict__ scal, LMParams p
   st->initial_cost = scal[0];
   st->lam = p.lambda0;
   st->nu = 2.0;
+  st->hc = 1.0;
   st->it = 0;
   st->nfev = 1;
   st->trials = 0;
@@ -1105,6 +1115,12 @@ __device__ void lm_decide_body(LMDev* st, const double* scal, const double* __re
       } else if (s.it >= p.max_iter) {
         s.status = 0;
         s.done = 1;
+      } else if (s.hc == 1.0 && p.curvature_switch > 0 && actual < p.curvature_switch * old) {
+        // in the final basin (the step changed the cost by < curvature_switch of it): the residuals move little
+        // against the huber scale, so the loss's own (floored Newton) curvature replaces IRLS's majoriser from the
+        // current point on, which the next build re-linearises first (LMSolver._run_host: the same rule)
+        s.hc = p.huber_curvature;
+        s.relin = 1;
       }
     } else {
       s.lam = s.lam > 0 ? fmax(s.lam * s.nu, 1e-9) : 1e-9;

@@ -26,6 +26,9 @@ struct LinArgs {
   const void* rt64;              // RayTab<double>[n_lm]
   const double2* seg_base;       // [n_seg] base observation; records hold obs - base (real)
   double u, v, fs2, inv_fs2;
+  double hcurv;                  // huber: curvature weight beyond the unit = hcurv * rho' (1: IRLS)
+  const double* hcurv_dev;       // device-driven LM: the curvature weight from LMDev::hc instead (nullptr: hcurv)
+  const int* run_if;             // nullptr, or: the launch exits at once unless *run_if != 0 (re-linearisation)
   void* ug_slot;                 // [n_slot][12] real: U (6) | g_pose (3) | 0 0 0 (dense slots)
   void* w_slot;                  // [n_slot][8] real: W (6) | 0 0 at slot toff_l + frame - first_l
   const int4* lm_meta;           // [n_lm] {first frame, last frame, slot offset, 0}
@@ -125,12 +128,15 @@ struct BacksubArgs {
 // device-driven Levenberg-Marquardt state (ptzba_lm_*): parameters, running state, last decision
 struct LMParams {
   double ftol, xtol, gtol, lambda0, min_lambda, max_lambda;
+  double huber_curvature, curvature_switch;  // see ptzba_lm_opts
   int max_iter, max_retries, gauss_newton, pad;
 };
 struct LMDev {
   LMParams p;
   double cost, initial_cost, lam, nu, last_actual, last_rho;
-  int it, nfev, trials, retries, status, done, accepted, relin;
+  double hc;  // huber curvature weight of the linearisations from now on (1 until the switch)
+  int it, nfev, trials, retries, status, done, accepted;
+  int relin;  // the decision switched the curvature: the next build re-linearises the current point first
   int seq;  // host ring record: written last (after a system-scope fence) = trial index + 1
   int cur;  // current linearisation slot (flips on an accepted trial: the trial linearised into the other)
 };

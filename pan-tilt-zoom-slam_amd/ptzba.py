@@ -44,7 +44,18 @@ class ptz_refine_opts(Structure):
 class ptzba_lm_opts(Structure):
     _fields_ = [("ftol", c_double), ("xtol", c_double), ("gtol", c_double), ("lambda0", c_double),
                 ("min_lambda", c_double), ("max_lambda", c_double), ("max_iter", c_int32), ("max_retries", c_int32),
-                ("gauss_newton", c_int32)]
+                ("gauss_newton", c_int32), ("huber_curvature", c_double), ("curvature_switch", c_double)]
+
+
+# LM defaults (include/ptzba.h ptzba_lm_opts).  lambda0 = min_lambda: Gauss-Newton steps from the start, as scipy's trf
+# takes them while the step lies inside its trust region (bundle_adjustment.py:200-202 -> trf.py); a Marquardt start
+# (1e-4, rounds 1-4) damps the frame chain's low-curvature modes and stops at ftol=1e-4 ~5e-4 deg short of the optimum
+# at config 3 (profiles/r05a_ftol_study.jsonl).  Huber: IRLS curvature until an accepted step reduces the cost by less
+# than CURVATURE_SWITCH of it, then HUBER_CURVATURE * rho' beyond the unit (profiles/r05c_switch.jsonl)
+LAMBDA0 = 1e-12
+MIN_LAMBDA = 1e-12
+HUBER_CURVATURE = 0.1
+CURVATURE_SWITCH = 0.25
 
 
 class ptzba_lm_record(Structure):
@@ -104,6 +115,7 @@ def lib():
         "ptzba_build_reduced": ([V, D], I),
         "ptzba_solve_reduced": ([V], I),
         "ptzba_step": ([V, D], I),
+        "ptzba_set_huber_curvature": ([V, D], I),
         "ptzba_solve": ([V, V, V, POINTER(ptzba_lm_opts), POINTER(ptzba_report)], I),
         "ptzba_solve_resident": ([V, I32, POINTER(ptzba_lm_opts), POINTER(ptzba_report)], I),
         "ptzba_lm_start": ([V], I),
@@ -191,7 +203,7 @@ def lib():
 EXPORTED_SYMBOLS = [
     "ptzba_new", "ptzba_delete", "ptzba_last_error", "ptzba_version", "ptzba_set_stream", "ptzba_use_own_stream", "ptzba_set_problem",
     "ptzba_problem_info", "ptzba_solver_info", "ptzba_residual", "ptzba_set_state", "ptzba_get_state", "ptzba_linearize",
-    "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_solve", "ptzba_solve_resident", "ptzba_read_scalars", "ptzba_accept",
+    "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_set_huber_curvature", "ptzba_solve", "ptzba_solve_resident", "ptzba_read_scalars", "ptzba_accept",
     "ptzba_lm_start", "ptzba_lm_init", "ptzba_lm_build", "ptzba_lm_solve", "ptzba_lm_decide", "ptzba_lm_wait",
     "ptzba_exchange", "ptzba_exchange_packed", "ptzba_pack", "ptzba_unpack", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptzba_save_state", "ptzba_restore_state", "ptz_ray_to_image",
     "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks", "ptzba_coupling_window", "ptz_match_knn2", "ptz_homography_ransac", "ptz_homography_ransac_batch", "ptz_lk_track", "ptz_sift", "ptz_match_hamming",
@@ -874,6 +886,7 @@ class BAHandle:
                                        _ptr(w), float(u), float(v), ctypes.byref(opts)), "ptzba_set_problem")
         self.n_pose, self.n_landmark, self.n_obs = int(n_pose), int(n_landmark), n
         self.precision = precision
+        self.loss = int(loss)
 
     # multi-GPU exchanges run inside the library (include/ptzba.h PTZBA_X_*)
     internal_exchange = False
@@ -983,6 +996,10 @@ class BAHandle:
     def linearize(self):
         _check(lib().ptzba_linearize(self.h), "ptzba_linearize")
 
+    def set_huber_curvature(self, hc):
+        """Host-driven LM: the huber curvature weight (units of rho' beyond the unit) of later linearisations."""
+        _check(lib().ptzba_set_huber_curvature(self.h, float(hc)), "ptzba_set_huber_curvature")
+
     def build_reduced(self, lam):
         _check(lib().ptzba_build_reduced(self.h, float(lam)), "ptzba_build_reduced")
 
@@ -1016,13 +1033,14 @@ class BAHandle:
     def lm_decide(self, k):
         _check(lib().ptzba_lm_decide(self.h, int(k)), "ptzba_lm_decide")
 
-    def solve(self, ptz, rays, ftol=1e-4, xtol=1e-8, gtol=0.0, max_iter=100, lambda0=1e-4, min_lambda=1e-12,
-              max_lambda=1e16, max_retries=30, gauss_newton=False):
+    def solve(self, ptz, rays, ftol=1e-4, xtol=1e-8, gtol=0.0, max_iter=100, lambda0=LAMBDA0, min_lambda=MIN_LAMBDA,
+              max_lambda=1e16, max_retries=30, gauss_newton=False, huber_curvature=HUBER_CURVATURE,
+              curvature_switch=CURVATURE_SWITCH):
         """One-shot ptzba_solve (C-driven LM to termination).  Returns (ptz [N,3], rays [M,2], LMResult)."""
         ptz = _f64(ptz, (self.n_pose, 3)).copy()
         rays = _f64(rays, (self.n_landmark, 2)).copy()
         opts = ptzba_lm_opts(ftol, xtol, gtol, 0.0 if gauss_newton else lambda0, min_lambda, max_lambda, int(max_iter),
-                             int(max_retries), 1 if gauss_newton else 0)
+                             int(max_retries), 1 if gauss_newton else 0, huber_curvature, curvature_switch)
         rep = ptzba_report()
         _check(lib().ptzba_solve(self.h, _ptr(ptz), _ptr(rays), ctypes.byref(opts), ctypes.byref(rep)), "ptzba_solve")
         res = LMResult(status=rep.status, message=STATUS_MSG.get(rep.status, "?"), cost=rep.cost,
@@ -1030,12 +1048,13 @@ class BAHandle:
                        lam=float("nan"), time=rep.time_s, history=[], trials=rep.trials)
         return ptz, rays, res
 
-    def solve_resident(self, restore=False, ftol=1e-4, xtol=1e-8, gtol=0.0, max_iter=100, lambda0=1e-4,
-                       min_lambda=1e-12, max_lambda=1e16, max_retries=30, gauss_newton=False):
+    def solve_resident(self, restore=False, ftol=1e-4, xtol=1e-8, gtol=0.0, max_iter=100, lambda0=LAMBDA0,
+                       min_lambda=MIN_LAMBDA, max_lambda=1e16, max_retries=30, gauss_newton=False,
+                       huber_curvature=HUBER_CURVATURE, curvature_switch=CURVATURE_SWITCH):
         """ptzba_solve_resident: the C-driven LM on the device-resident state (restore=True: from the
         save_state snapshot).  The state stays on the device.  Returns LMResult."""
         opts = ptzba_lm_opts(ftol, xtol, gtol, 0.0 if gauss_newton else lambda0, min_lambda, max_lambda, int(max_iter),
-                             int(max_retries), 1 if gauss_newton else 0)
+                             int(max_retries), 1 if gauss_newton else 0, huber_curvature, curvature_switch)
         rep = ptzba_report()
         _check(lib().ptzba_solve_resident(self.h, 1 if restore else 0, ctypes.byref(opts), ctypes.byref(rep)),
                "ptzba_solve_resident")
@@ -1195,9 +1214,11 @@ class LMSolver:
     idles on a host round trip.  device_loop=False (or verbose): the same decisions on the host after
     reading each trial's scalars (also used for handles without ptzba_lm_*, e.g. test doubles)."""
 
-    def __init__(self, handle, ftol=1e-4, xtol=1e-8, gtol=0.0, max_iter=100, lambda0=1e-4, min_lambda=1e-12,
-                 max_lambda=1e16, gauss_newton=False, allreduce=None, verbose=0, max_retries=30, device_loop=True):
+    def __init__(self, handle, ftol=1e-4, xtol=1e-8, gtol=0.0, max_iter=100, lambda0=LAMBDA0, min_lambda=MIN_LAMBDA,
+                 max_lambda=1e16, gauss_newton=False, allreduce=None, verbose=0, max_retries=30, device_loop=True,
+                 huber_curvature=HUBER_CURVATURE, curvature_switch=CURVATURE_SWITCH):
         self.h = handle
+        self.huber_curvature, self.curvature_switch = huber_curvature, curvature_switch
         self.ftol, self.xtol, self.gtol = ftol, xtol, gtol
         self.max_iter = max_iter
         self.lambda0 = 0.0 if gauss_newton else lambda0
@@ -1228,7 +1249,8 @@ class LMSolver:
         if self.allreduce is not None:
             self.allreduce("scal")
         h.lm_init(ptzba_lm_opts(self.ftol, self.xtol, self.gtol, self.lambda0, self.min_lambda, self.max_lambda,
-                                int(max_iter), int(self.max_retries), 1 if self.gauss_newton else 0))
+                                int(max_iter), int(self.max_retries), 1 if self.gauss_newton else 0,
+                                self.huber_curvature, self.curvature_switch))
 
         def build():
             h.lm_build()
@@ -1264,6 +1286,12 @@ class LMSolver:
     def _run_host(self, iterations=None, check_termination=True):
         h = self.h
         t0 = time.perf_counter()
+        # huber curvature switch (ptzba_lm_opts; the device loop's k_lm_decide rule): IRLS until an accepted step
+        # reduces the cost by less than curvature_switch of it, then huber_curvature, the current point re-linearised
+        switch = (getattr(h, "loss", LOSS_LINEAR) == LOSS_HUBER and self.curvature_switch > 0
+                  and self.huber_curvature < 1.0 and hasattr(h, "set_huber_curvature"))
+        if switch:
+            h.set_huber_curvature(1.0)
         h.linearize()
         s = self._scalars()
         cost = s[0]
@@ -1325,6 +1353,13 @@ class LMSolver:
                 if self.gtol > 0 and gmax < self.gtol:
                     status = 1
                     break
+                if it >= max_iter:
+                    break
+            if switch and actual < self.curvature_switch * old:
+                switch = False
+                h.set_huber_curvature(self.huber_curvature)
+                h.linearize()
+                self._scalars()
         h.sync()
         t1 = time.perf_counter()
         return LMResult(status=status, message=STATUS_MSG.get(status, "?"), cost=cost, initial_cost=initial_cost,

@@ -402,6 +402,35 @@ def gen_config2():
 
 
 # --------------------------------------------------------------------------------------------
+# 5a. config-2 at the reference's own termination: scipy trf, x_scale='jac', ftol=1e-4, FD Jacobian
+# --------------------------------------------------------------------------------------------
+def gen_config2_ftol():
+    """Where the reference's optimizer call (bundle_adjustment.py:200-202: least_squares(_compute_residual, x0,
+    x_scale='jac', ftol=1e-4, method='trf'), '2-point' FD Jacobian with the pair structure as jac_sparsity) stops at
+    config 2, on the pinned oracle residual (config2_optimum.npz pins it to the reference's own): x_ftol, njev,
+    nfev, cost, status -- for the reference's linear loss and for loss='huber' (f_scale 1).  The GPU's ftol=1e-4
+    solves are gated against it (tests/test_gpu_ba.py::test_config2_ftol_stop_matches_scipy_trf)."""
+    sys.path.insert(0, REPO)
+    from oracle import ptz_oracle as orc
+    p = synthetic.make_problem("config2", seed=0)
+    n, m = p.n_pose, p.n_landmark
+    frame = p.frame.astype(np.int64)
+    landmark = p.landmark.astype(np.int64)
+    x0 = np.concatenate([p.init_ptz[1:].reshape(-1), p.init_rays.reshape(-1)])
+    arrays = dict(n_pose=n, n_landmark=m, n_records=len(p.frame), frame_sum=int(p.frame.sum()), x0=x0)
+    for loss, key in (("linear", ""), ("huber", "_huber")):
+        t0 = time.time()
+        res = orc.solve_scipy(x0, n, m, p.u, p.v, p.init_ptz[0], frame, landmark, p.xy, ftol=1e-4, loss=loss,
+                              f_scale=1.0)
+        dt = time.time() - t0
+        print(f"config2 ftol=1e-4 {loss}: cost {res.cost:.8f} njev {res.njev} nfev {res.nfev} status {res.status} "
+              f"{dt:.1f}s")
+        arrays.update({"x_ftol" + key: res.x, "cost_ftol" + key: res.cost, "njev" + key: res.njev,
+                       "nfev" + key: res.nfev, "status" + key: res.status, "time" + key: dt})
+    out("config2_ftol.npz", **arrays)
+
+
+# --------------------------------------------------------------------------------------------
 # 5b. config-3 (headline, 500 KF x 20k rays) tight optimum: the parity target of the bench's RMSE
 # --------------------------------------------------------------------------------------------
 def gen_config3():
@@ -660,6 +689,8 @@ def main():
         gen_maps(21)
     if "config2" in todo:
         gen_config2()
+    if "config2_ftol" in todo or "config2" in todo:
+        gen_config2_ftol()
     if "config3" in todo:  # ~20 min; not in the default set
         gen_config3()
     if "stream" in todo:

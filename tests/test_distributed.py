@@ -17,6 +17,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 
 
+# a Marquardt start (rounds 1-4's default): the ranks' solves sum in a different order than the single-rank
+# solve, and with Gauss-Newton steps (ptzba.LAMBDA0) the tight ftol test fires at round-off, where the iteration
+# count is not reproducible across summation orders; damped steps keep the last reductions above it
+DAMPED = 1e-4
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -31,7 +36,7 @@ def _solve(prob, frame, landmark, xy, allreduce=None, iters=12):
     h = NumpyBAHandle()
     h.set_problem(prob.n_pose, prob.n_landmark, frame, landmark, xy, prob.u, prob.v)
     h.set_state(prob.init_ptz, prob.init_rays)
-    res = ptzba.LMSolver(h, ftol=1e-9, xtol=1e-12, max_iter=iters, allreduce=allreduce).run()
+    res = ptzba.LMSolver(h, ftol=1e-9, xtol=1e-12, max_iter=iters, allreduce=allreduce, lambda0=DAMPED).run()
     ptz, rays = h.get_state()
     return res, ptz, rays
 
@@ -59,7 +64,7 @@ def _worker(rank, world, port, out_dir):
     holder["h"] = h
     h.set_problem(prob.n_pose, prob.n_landmark, prob.frame[sel], prob.landmark[sel], prob.xy[sel], prob.u, prob.v)
     h.set_state(prob.init_ptz, prob.init_rays)
-    res = ptzba.LMSolver(h, ftol=1e-9, xtol=1e-12, max_iter=12, allreduce=allreduce).run()
+    res = ptzba.LMSolver(h, ftol=1e-9, xtol=1e-12, max_iter=12, allreduce=allreduce, lambda0=DAMPED).run()
     ptz, rays = h.get_state()
     owned = np.zeros(prob.n_landmark, bool)
     owned[prob.landmark[sel]] = True
@@ -166,7 +171,7 @@ def _part_worker(rank, world, port, out_dir):
     h.set_problem(prob.n_pose, prob.n_landmark, prob.frame[sel], prob.landmark[sel], prob.xy[sel], prob.u, prob.v)
     h.set_dist(world, rank, split, hook)
     h.set_state(prob.init_ptz, prob.init_rays)
-    res = ptzba.LMSolver(h, ftol=1e-9, xtol=1e-12, max_iter=8).run()
+    res = ptzba.LMSolver(h, ftol=1e-9, xtol=1e-12, max_iter=8, lambda0=DAMPED).run()
     ptz, rays = h.get_state()
     own_lm = np.zeros(prob.n_landmark, bool)
     own_lm[prob.landmark[sel]] = True
@@ -238,7 +243,7 @@ def _tree_worker(rank, world, port, out_dir):
     h.set_problem(prob.n_pose, prob.n_landmark, prob.frame[sel], prob.landmark[sel], prob.xy[sel], prob.u, prob.v)
     h.set_dist(world, rank, phases, hook)
     h.set_state(prob.init_ptz, prob.init_rays)
-    res = ptzba.LMSolver(h, ftol=1e-9, xtol=1e-12, max_iter=6).run()
+    res = ptzba.LMSolver(h, ftol=1e-9, xtol=1e-12, max_iter=6, lambda0=DAMPED).run()
     ptz, rays = h.get_state()
     own_lm = np.zeros(prob.n_landmark, bool)
     own_lm[prob.landmark[sel]] = True

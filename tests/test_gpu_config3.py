@@ -211,7 +211,9 @@ def test_config3_two_level_dissection_matches_one_level(gpu_available, config3, 
         info = h.solver_info()
         assert info["nd_depth"] == int(depth), info
         h.set_state(p.init_ptz, p.init_rays)
-        res = ptzba.LMSolver(h, ftol=1e-15, xtol=1e-15, max_iter=4).run()
+        # damped start (rounds 1-4's default): with Gauss-Newton steps the 4th trial sits at round-off, where its
+        # acceptance depends on the summation order the two orders differ in
+        res = ptzba.LMSolver(h, ftol=1e-15, xtol=1e-15, max_iter=4, lambda0=1e-4).run()
         out[depth] = (h.get_state(), res, info)
         h.close()
     (ptz1, rays1), r1, i1 = out["1"]
@@ -242,8 +244,9 @@ def test_config3_optimum_matches_oracle_fixture(gpu_available, config3, arith):
     frame 0 as the gauge), tests/golden/config3_optimum.npz.  fp32_huber is the bench's arithmetic (fp32 records,
     matrix-core K2, scipy's loss='huber') vs the fixture's Huber optimum; fp64_linear is the reference's own
     arithmetic vs its linear-loss optimum.  Gate (north star): pan / tilt / f RMSE <= 1e-4 (deg, deg, px) for the
-    converged solve; rays RMSE <= 1e-4 deg; cost within 1e-7 relative.  The solve stopped at the reference's ftol =
-    1e-4 is reported beside it (loose sanity bound only)."""
+    converged solve; rays RMSE <= 1e-4 deg; cost within 1e-7 relative.  The solve stopped by the reference's own rule
+    (ftol = 1e-4, what bench.py times) meets the same pose gate since round 5 (Gauss-Newton start, huber curvature
+    switch: ptzba.LAMBDA0 / HUBER_CURVATURE), its rays within 1e-3 deg."""
     import ptzba
     import synthetic
     p = config3
@@ -255,7 +258,7 @@ def test_config3_optimum_matches_oracle_fixture(gpu_available, config3, arith):
     h.set_state(p.init_ptz, p.init_rays)
     h.save_state()
     r_ref = ptzba.LMSolver(h, ftol=1e-4, xtol=1e-8, max_iter=100).run()  # the reference's termination
-    ptz_ref, _ = h.get_state()
+    ptz_ref, rays_ref = h.get_state()
     h.restore_state()
     res = ptzba.LMSolver(h, ftol=1e-12, xtol=1e-14, max_iter=60).run()
     ptz, rays = h.get_state()
@@ -264,12 +267,13 @@ def test_config3_optimum_matches_oracle_fixture(gpu_available, config3, arith):
     rmse = synthetic.pose_rmse(ptz, pt)
     rmse_ref = synthetic.pose_rmse(ptz_ref, pt)
     ray_rmse = float(np.sqrt(np.mean((rays - rt) ** 2)))
-    print(f"{arith}: pose RMSE vs oracle optimum {rmse} (ftol=1e-4 solve: {rmse_ref}, {r_ref.njev} its), rays "
-          f"{ray_rmse:.3e} deg, cost {res.cost:.10f} vs {ct:.10f}")
+    ray_rmse_ref = float(np.sqrt(np.mean((rays_ref - rt) ** 2)))
+    print(f"{arith}: pose RMSE vs oracle optimum {rmse} (ftol=1e-4 solve: {rmse_ref}, rays {ray_rmse_ref:.3e} deg, "
+          f"{r_ref.njev} its), rays {ray_rmse:.3e} deg, cost {res.cost:.10f} vs {ct:.10f}")
     assert np.all(rmse <= 1e-4), rmse
-    # the solve stopped by the reference's own rule (ftol = 1e-4: ~4 iterations at this size) is reported, not gated
-    # at 1e-4 -- it stops ~5e-4 deg / 0.02 px short of the optimum, as scipy's trf would at that tolerance
-    assert np.all(rmse_ref <= [1e-2, 1e-2, 0.5]), rmse_ref
+    # the solve stopped by the reference's own rule (ftol = 1e-4: ~4 iterations at this size)
+    assert np.all(rmse_ref <= 1e-4), rmse_ref
+    assert ray_rmse_ref <= 1e-3, ray_rmse_ref
     assert ray_rmse <= 1e-4
     assert abs(res.cost - ct) <= 1e-7 * ct
 

@@ -18,6 +18,11 @@ pytestmark = pytest.mark.gpu
 CFG = dict(precision="fp64", loss="linear", ftol=1e-10, max_iter=8)
 
 
+# a Marquardt start (rounds 1-4's default): the ranks' solves sum in a different order than the single-rank
+# solve, and with Gauss-Newton steps (ptzba.LAMBDA0) the tight ftol test fires at round-off, where the iteration
+# count is not reproducible across summation orders; damped steps keep the last reductions above it
+DAMPED = 1e-4
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -29,7 +34,8 @@ def _free_port():
 def _solve(h, prob, allreduce=None):
     import ptzba
     h.set_state(prob.init_ptz, prob.init_rays)
-    res = ptzba.LMSolver(h, ftol=CFG["ftol"], xtol=1e-14, max_iter=CFG["max_iter"], allreduce=allreduce).run()
+    res = ptzba.LMSolver(h, ftol=CFG["ftol"], xtol=1e-14, max_iter=CFG["max_iter"], allreduce=allreduce,
+                         lambda0=DAMPED).run()
     ptz, rays = h.get_state()
     return res, ptz, rays
 
@@ -148,7 +154,7 @@ def _part_worker(rank, world, port, out_dir, config, precision, loss):
 
     h.set_exchange_hook(hook)
     h.set_state(prob.init_ptz, prob.init_rays)
-    res = ptzba.LMSolver(h, ftol=CFG["ftol"], xtol=1e-14, max_iter=_iters(config)).run()
+    res = ptzba.LMSolver(h, ftol=CFG["ftol"], xtol=1e-14, max_iter=_iters(config), lambda0=DAMPED).run()
     ptz, rays = h.get_state()
     own_lm = np.zeros(prob.n_landmark, bool)
     own_lm[prob.landmark[sel]] = True
@@ -190,7 +196,7 @@ def test_part_owned_gpu_solve_matches_single_rank(gpu_available, tmp_path, monke
     h1.set_problem(prob.n_pose, prob.n_landmark, prob.frame, prob.landmark, prob.xy, prob.u, prob.v,
                    precision=precision, loss=loss, frame_win_hi=win_hi)
     h1.set_state(prob.init_ptz, prob.init_rays)
-    res1 = ptzba.LMSolver(h1, ftol=CFG["ftol"], xtol=1e-14, max_iter=_iters(config)).run()
+    res1 = ptzba.LMSolver(h1, ftol=CFG["ftol"], xtol=1e-14, max_iter=_iters(config), lambda0=DAMPED).run()
     ptz1, rays1 = h1.get_state()
     h1.close()
     outs = [np.load(os.path.join(tmp_path, f"part_rank{r}.npz")) for r in range(world)]
