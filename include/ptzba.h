@@ -196,7 +196,7 @@ typedef struct {
                                                  scipy's trf does while its step lies inside the trust region */
   int32_t max_iter, max_retries, gauss_newton; /* accepted iterations; rejections in a row; lambda0 = 0 GN */
   /* huber loss only: the records' curvature weight beyond the unit is rho' (IRLS, a majoriser of the loss) until an
-   * accepted step reduces the cost by less than curvature_switch of it; from then on huber_curvature * rho' (the
+   * accepted step was predicted to reduce the cost by less than curvature_switch of it; from then on huber_curvature * rho' (the
    * loss's own Newton curvature is 0 there, scipy's robust scaling; floored), the current point re-linearised at
    * once.  curvature_switch = 0 or huber_curvature = 1: IRLS throughout.  Defaults 0.1 / 0.25. */
   double huber_curvature, curvature_switch;

@@ -44,7 +44,9 @@ struct ptzba_ctx {
   int n_pose = 0, n_lm = 0, n_fixed = 1, precision = PTZBA_FP64, loss = PTZBA_LOSS_LINEAR;
   double fs = 1.0;
   double hcurv = 1.0;  // huber curvature weight beyond the unit, in units of rho' (LinArgs::hcurv), host-driven LM
-  bool lm_relin = false;  // device-driven LM: queue the conditional re-linearisation in lm_build
+  bool lm_curv_pending = false;  // device-driven LM: the huber curvature switch has not happened yet
+  bool lm_relin_mode = false;    // LMParams::relin_mode of the current run
+  DBuf curv_pred;                // [8] the curvature-mode reduction's output (the trial's landmark-part prediction)
   int64_t n_rec = 0, n_seg = 0;
   int n_work = 0, max_seg_per_lm = 0;
   int n_sys = 0;
@@ -2105,8 +2107,9 @@ static void tables(ptzba_ctx* h, const double* ptz, const double* rays, const in
 // sel != nullptr (device-driven LM): the kernel writes slot (*sel ^ sel_xor), chosen on the device
 // run_if != nullptr: a conditional re-linearisation of the current point (device-driven LM, after the curvature
 // switch): the launch exits at once unless *run_if; not timed as a K1 launch (the roofline averages real ones)
+// hc_dev: device-driven LM, the huber curvature weight from device memory (LMDev::hc / hc_trial); nullptr: h->hcurv
 static void linearize_into(ptzba_ctx* h, int slot, const int* sel = nullptr, int sel_xor = 0,
-                           const int* run_if = nullptr) {
+                           const int* run_if = nullptr, const double* hc_dev = nullptr) {
   LinArgs a;
   a.lm_work = h->lm_order.as<int4>();
   a.n_work = h->n_work;
@@ -2127,7 +2130,7 @@ static void linearize_into(ptzba_ctx* h, int slot, const int* sel = nullptr, int
   a.fs2 = h->fs * h->fs;
   a.inv_fs2 = 1.0 / (h->fs * h->fs);
   a.hcurv = h->hcurv;
-  a.hcurv_dev = sel ? &h->lmdev.as<LMDev>()->hc : nullptr;
+  a.hcurv_dev = hc_dev;
   a.run_if = run_if;
   a.ug_slot = h->ug_slot[slot].p;
   a.w_slot = h->w_slot[slot].p;
@@ -2471,8 +2474,20 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
     launch_trial<double>(b, h->ptz.as<double>(), h->gpose(), h->D_pose.as<double>(), h->ptz_trial.as<double>(),
                          h->locp(), h->n_pose, h->ft64.p, h->rt64.p, h->ft64.p, h->rt64.p, h->st, fm, finfo);
   tm_end(h, TM_BACK);
-  // trial linearisation (its cost decides acceptance; kept as the next linearisation if accepted)
-  linearize_into(h, nx, sel, 1);
+  // trial linearisation (its cost decides acceptance; kept as the next linearisation if accepted).  Device-driven LM
+  // with the huber curvature switch pending: single GPU (relin_mode 0), the trial's predicted reduction is reduced
+  // first and picks the curvature of this linearisation (LMDev::hc_trial); ranks (relin_mode 1) use LMDev::hc
+  const double* hc_dev = nullptr;
+  if (sel) {
+    LMDev* st = h->lmdev.as<LMDev>();
+    hc_dev = h->lm_relin_mode ? &st->hc : &st->hc_trial;
+    if (!h->lm_relin_mode && h->lm_curv_pending) {
+      const DecideArgs cd{st, h->locp(), nullptr, nullptr, 0, 1};
+      launch_reduce_cols(h->lm_red.as<double>(), h->n_lm, 4, 1, 0, h->curv_pred.as<double>(), h->red_scratch.as<double>(),
+                         h->st, nullptr, 0, 0, nullptr, nullptr, nullptr, 0, &cd);
+    }
+  }
+  linearize_into(h, nx, sel, 1, nullptr, hc_dev);
   // scal[1] (trial cost) and scal[2..4] are overwritten below, loc[0..3] by the trial kernel: no memsets
   if (sel && !h->has_exchange() && !h->ext_exchange && !h->scal_exported && !h->dist_mode) {
     // launched by ptzba_lm_decide with the decision fused into it (nothing runs between the two calls)
@@ -2511,6 +2526,8 @@ int ptzba_lm_start(ptzba_handle h) {
   if (!h || !h->have_problem) return fail("no problem set");
   HIPCHK(hipSetDevice(h->device));
   if (!h->lmdev.p && h->lmdev.alloc(sizeof(LMDev))) return -1;
+  if (!h->curv_pred.p && h->curv_pred.alloc(64)) return -1;
+  h->hcurv = 1.0;  // the initial linearisation: IRLS (the host-driven LM's setting does not carry over)
   if (!h->lm_host) {
     HIPCHK(hipHostMalloc((void**)&h->lm_host, LM_RING * sizeof(LMDev), hipHostMallocCoherent));
   }
@@ -2530,7 +2547,11 @@ int ptzba_lm_init(ptzba_handle h, const ptzba_lm_opts* o) {
   LMParams p{o->ftol, o->xtol, o->gtol, o->lambda0, o->min_lambda, o->max_lambda,
              sw ? o->huber_curvature : 1.0, sw ? o->curvature_switch : 0.0, o->max_iter, o->max_retries,
              o->gauss_newton ? 1 : 0, 0};
-  h->lm_relin = sw;  // re-linearisation launches are queued until the host sees the switch
+  // the switch's launches (relin_mode 1: the conditional re-linearisation in lm_build; 0: the predicted-reduction
+  // reduce in front of the trial K1) are queued until the host sees the switch in a decision record
+  h->lm_curv_pending = sw;
+  h->lm_relin_mode = h->has_exchange() || h->ext_exchange || h->scal_exported || h->dist_mode;
+  p.relin_mode = h->lm_relin_mode ? 1 : 0;
   // no decision of an earlier run is in flight (its lm_wait returned): clear the ring's sequence tags
   for (int k = 0; k < LM_RING; ++k) __atomic_store_n(&h->lm_host[k].seq, 0, __ATOMIC_RELAXED);
   launch_lm_init(h->lmdev.as<LMDev>(), h->scal.as<double>(), p, h->cur, h->st);
@@ -2545,7 +2566,8 @@ int ptzba_lm_build(ptzba_handle h) {
   HIPCHK(hipSetDevice(h->device));
   // the curvature switch of the last decision (LMDev::relin): re-linearise the current point into its slot first.
   // Queued only until the host has seen the switch in a decision record; the launch reads the flag on the device
-  if (h->lm_relin) linearize_into(h, 0, &h->lmdev.as<LMDev>()->cur, 0, &h->lmdev.as<LMDev>()->relin);
+  if (h->lm_curv_pending && h->lm_relin_mode)
+    linearize_into(h, 0, &h->lmdev.as<LMDev>()->cur, 0, &h->lmdev.as<LMDev>()->relin, &h->lmdev.as<LMDev>()->hc);
   // a build queued after the final decision (the host pipelines one trial ahead) exits at once
   return build_impl(h, 0.0, &h->lmdev.as<LMDev>()->lam, &h->lmdev.as<LMDev>()->done, &h->lmdev.as<LMDev>()->cur);
 }
@@ -2610,7 +2632,7 @@ int ptzba_lm_wait(ptzba_handle h, int trial, ptzba_lm_record* out) {
   out->status = r.status;
   out->done = r.done;
   out->accepted = r.accepted;
-  if (r.hc != 1.0) h->lm_relin = false;  // switched (and re-linearised in the build behind that decision)
+  if (r.hc != 1.0) h->lm_curv_pending = false;  // switched: the launches already queued behind it suffice
   h->cur = r.cur;  // the host's view of the current slot follows the device (ptzba_accept / linearize)
   if ((r.cur ^ h->state_base) & 1) {
     // the device's decisions moved the current state to the other pair: swap the pointers and the base together,

@@ -981,7 +981,19 @@ __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ 
     tot[k] = s;
   }
   if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (dec.st) {
+  if (dec.st && dec.curv) {
+    // curvature mode (relin_mode 0): out = the trial's landmark part of the predicted reduction; with the pose part
+    // (loc[0]) the whole predicted reduction of the trial, known before the trial point is linearised -- the trial
+    // linearisation uses the floored Newton curvature from the step that is predicted to change the cost by less
+    // than curvature_switch of it (k_lm_decide's relin_mode 1 rule, decided one launch earlier)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      LMDev* st = dec.st;
+      const double pred = tot[0] + dec.loc[0];
+      const LMParams& p = st->p;
+      st->hc_trial = (st->hc != 1.0 || pred < p.curvature_switch * st->cost) ? p.huber_curvature : 1.0;
+    }
+  } else if (dec.st) {
     // fused decision (trial-cost reduction of a single-GPU device-driven LM): out = scal + 1 (trial cost), out2 =
     // scal + 2 (pred, |dx|^2, |x|^2 landmark partials); the sums come from LDS, not from the stores above
     __syncthreads();
@@ -1010,7 +1022,7 @@ void launch_reduce_cols(const double* src, int64_t n, int stride, int nk, int ma
                         hipStream_t st, const double* src2, int stride2, int nk2, double* out2, const double* src1,
                         const int* sel, int sel_xor, const DecideArgs* decide) {
   unsigned* counter = reinterpret_cast<unsigned*>(scratch + RED_BLOCKS * 8);
-  const DecideArgs dec = decide ? *decide : DecideArgs{nullptr, nullptr, nullptr, nullptr, 0};
+  const DecideArgs dec = decide ? *decide : DecideArgs{nullptr, nullptr, nullptr, nullptr, 0, 0};
   // workgroups: RED_BLOCKS, or PTZBA_RED_BLOCKS (A/B knob; fewer blocks = fewer counter arrivals, more rows each)
   static const int nb_env = getenv("PTZBA_RED_BLOCKS") ? atoi(getenv("PTZBA_RED_BLOCKS")) : 0;
   const int nb = nb_env > 0 ? std::min(nb_env, RED_BLOCKS) : RED_BLOCKS;
@@ -1061,6 +1073,7 @@ __global__ void k_lm_init(LMDev* st, const double* __restrict__ scal, LMParams p
   st->lam = p.lambda0;
   st->nu = 2.0;
   st->hc = 1.0;
+  st->hc_trial = 1.0;
   st->it = 0;
   st->nfev = 1;
   st->trials = 0;
@@ -1115,13 +1128,15 @@ __device__ void lm_decide_body(LMDev* st, const double* scal, const double* __re
       } else if (s.it >= p.max_iter) {
         s.status = 0;
         s.done = 1;
-      } else if (s.hc == 1.0 && p.curvature_switch > 0 && actual < p.curvature_switch * old) {
-        // in the final basin (the step changed the cost by < curvature_switch of it): the residuals move little
-        // against the huber scale, so the loss's own (floored Newton) curvature replaces IRLS's majoriser from the
-        // current point on, which the next build re-linearises first (LMSolver._run_host: the same rule)
+      } else if (p.relin_mode && s.hc == 1.0 && p.curvature_switch > 0 && pred < p.curvature_switch * old) {
+        // in the final basin (the step was predicted to change the cost by < curvature_switch of it): the residuals
+        // move little against the huber scale, so the loss's own (floored Newton) curvature replaces IRLS's
+        // majoriser from the current point on, which the next build re-linearises first (LMSolver._run_host: the
+        // same rule).  relin_mode 0 reaches the same linearisations without the re-linearisation: see hc_trial
         s.hc = p.huber_curvature;
         s.relin = 1;
       }
+      if (!p.relin_mode) s.hc = s.hc_trial;  // the accepted trial's linearisation is the current one
     } else {
       s.lam = s.lam > 0 ? fmax(s.lam * s.nu, 1e-9) : 1e-9;
       s.nu *= 2.0;

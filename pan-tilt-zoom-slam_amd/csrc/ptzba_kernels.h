@@ -129,12 +129,17 @@ struct BacksubArgs {
 struct LMParams {
   double ftol, xtol, gtol, lambda0, min_lambda, max_lambda;
   double huber_curvature, curvature_switch;  // see ptzba_lm_opts
-  int max_iter, max_retries, gauss_newton, pad;
+  int max_iter, max_retries, gauss_newton;
+  // how the curvature switch reaches the linearisations: 0 (single GPU) the trial's K1 linearises with hc_trial,
+  // chosen before it from the trial's predicted reduction (k_reduce_cols curvature mode); 1 (ranks: the predicted
+  // reduction is a sum over ranks only after K1) the decision switches and the next build re-linearises (relin)
+  int relin_mode;
 };
 struct LMDev {
   LMParams p;
   double cost, initial_cost, lam, nu, last_actual, last_rho;
-  double hc;  // huber curvature weight of the linearisations from now on (1 until the switch)
+  double hc;        // huber curvature weight of the current linearisation (1 until the switch)
+  double hc_trial;  // relin_mode 0: the weight the trial's linearisation used (the current one's if accepted)
   int it, nfev, trials, retries, status, done, accepted;
   int relin;  // the decision switched the curvature: the next build re-linearises the current point first
   int seq;  // host ring record: written last (after a system-scope fence) = trial index + 1
@@ -153,6 +158,7 @@ struct DecideArgs {
   const int* info;
   LMDev* rec;
   int seq;
+  int curv;  // 1: not a decision -- the last workgroup sets st->hc_trial from the reduced predicted reduction
 };
 
 template <typename real>

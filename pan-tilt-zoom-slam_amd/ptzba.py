@@ -50,8 +50,8 @@ class ptzba_lm_opts(Structure):
 # LM defaults (include/ptzba.h ptzba_lm_opts).  lambda0 = min_lambda: Gauss-Newton steps from the start, as scipy's trf
 # takes them while the step lies inside its trust region (bundle_adjustment.py:200-202 -> trf.py); a Marquardt start
 # (1e-4, rounds 1-4) damps the frame chain's low-curvature modes and stops at ftol=1e-4 ~5e-4 deg short of the optimum
-# at config 3 (profiles/r05a_ftol_study.jsonl).  Huber: IRLS curvature until an accepted step reduces the cost by less
-# than CURVATURE_SWITCH of it, then HUBER_CURVATURE * rho' beyond the unit (profiles/r05c_switch.jsonl)
+# at config 3 (profiles/r05a_ftol_study.jsonl).  Huber: IRLS curvature until an accepted step is predicted to reduce the
+# cost by less than CURVATURE_SWITCH of it, then HUBER_CURVATURE * rho' beyond the unit (profiles/r05c_switch.jsonl)
 LAMBDA0 = 1e-12
 MIN_LAMBDA = 1e-12
 HUBER_CURVATURE = 0.1
@@ -1287,7 +1287,7 @@ class LMSolver:
         h = self.h
         t0 = time.perf_counter()
         # huber curvature switch (ptzba_lm_opts; the device loop's k_lm_decide rule): IRLS until an accepted step
-        # reduces the cost by less than curvature_switch of it, then huber_curvature, the current point re-linearised
+        # is predicted to reduce the cost by less than curvature_switch of it, then huber_curvature, the current point re-linearised
         switch = (getattr(h, "loss", LOSS_LINEAR) == LOSS_HUBER and self.curvature_switch > 0
                   and self.huber_curvature < 1.0 and hasattr(h, "set_huber_curvature"))
         if switch:
@@ -1355,7 +1355,7 @@ class LMSolver:
                     break
                 if it >= max_iter:
                     break
-            if switch and actual < self.curvature_switch * old:
+            if switch and pred < self.curvature_switch * old:
                 switch = False
                 h.set_huber_curvature(self.huber_curvature)
                 h.linearize()
