@@ -151,6 +151,9 @@ PTZBA_EXPORT int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_lan
  * [4] reduced-system size [5] landmarks with observations [6] max segments per landmark
  * [7] bytes of device memory held */
 PTZBA_EXPORT int ptzba_problem_info(ptzba_handle h, int64_t* info8);
+/* host phase times of the last ptzba_set_problem (sort, segments, K2 structure, plan, uploads ...): names[k] (static
+ * strings) and ms[k] for k < min(cap, *n_out); *n_out = the number of phases recorded */
+PTZBA_EXPORT int ptzba_setup_timing(ptzba_handle h, int32_t cap, const char** names, double* ms, int32_t* n_out);
 /* solver layout: [0] n_aug (system rows incl. padding), [1] ld, [2] factorisation launches (levels),
  * [3] ordering actually used (PTZBA_ORDER_*) | dissection levels << 8 (0 natural, 1 or 2), [4] back-substitution form (0 lookahead, 1 left-looking:
  * systems whose lists exceed LDS), [5] dense landmark x frame slots, [6] Schur work items,

@@ -44,6 +44,7 @@ struct ptzba_ctx {
   int n_pose = 0, n_lm = 0, n_fixed = 1, precision = PTZBA_FP64, loss = PTZBA_LOSS_LINEAR;
   double fs = 1.0;
   double hcurv = 1.0;  // huber curvature weight beyond the unit, in units of rho' (LinArgs::hcurv), host-driven LM
+  std::vector<std::pair<const char*, double>> setup_phases;  // the last set_problem's host phases (name, ms)
   bool lm_curv_pending = false;  // device-driven LM: the huber curvature switch has not happened yet
   bool lm_relin_mode = false;    // LMParams::relin_mode of the current run
   DBuf curv_pred;                // [8] the curvature-mode reduction's output (the trial's landmark-part prediction)
@@ -61,9 +62,7 @@ struct ptzba_ctx {
   DBuf frame_seg_begin, frame_seg_list, frame_win_hi;
   DBuf s2_items, s2_groups, s2_lm, lm_meta;  // K2 work items / tiles / lists, slot ranges
   DBuf s2_part, part_diag;                                    // K2 split partials (blocks, diagonal terms)
-  DBuf s2_item_group, s2_tile_cnt;                            // matrix-core K2's folded reduce
   int n_s2_items = 0, n_s2_groups = 0;
-  bool s2_pair = false;  // K2 work items over chunk pairs (k_schur_mf2)
   int64_t n_slot = 0;  // dense landmark x frame slots (W table rows)
   // device: state
   DBuf ptz, rays, ptz_trial, rays_trial, D_pose, D_ray;
@@ -108,11 +107,6 @@ struct ptzba_ctx {
   std::vector<StageOp> stage_ops;
   bool stage_batch = false;
   DBuf stage_dev;
-  // single-launch factorisation (k_chol_pst): level of each task, tasks per level, per-level completion counters
-  // [n_levels] + the ticket counter
-  DBuf chol_lvl, chol_lvl_n, chol_lvl_cnt;
-  bool chol_pst = false, chol_pst_ticket = true;
-  uint32_t chol_epoch = 0;
   bool bs_pst = false;
   uint32_t bsp_epoch = 0;
   bool bs_ll = false, bs_blk = false;
@@ -130,8 +124,7 @@ struct ptzba_ctx {
   int state_base = 0;
   // single-GPU device-driven LM: the trial-cost reduction waits for ptzba_lm_decide, which fuses the decision into it
   bool scal_deferred = false;
-  bool scal_exported = false;
-  int k2_fold = 0;  // SchurArgs::fold, read from PTZBA_K2_FOLD at set_problem (A/B knob)  // ptzba_exchange handed out the scalar buffer (a caller-run scalar exchange)
+  bool scal_exported = false;  // ptzba_exchange handed out the scalar buffer (a caller-run scalar exchange)
   // timing
   int timing = 0;  // bitmask of timed kernel groups (1 K1, 2 Schur, 4 Cholesky solve, 8 back-substitution)
   std::vector<hipEvent_t> ev[TM_N];
@@ -798,37 +791,6 @@ static void make_bs_steps(const std::vector<std::vector<uint8_t>>& nz, int Tx, C
   P.bsb_tot = done;
 }
 
-// XCD-aware order of one level's tasks (PTZBA_CHOL_XCD=1, A/B knob): workgroups are dealt round-robin over the
-// 8 XCDs (block b on XCD b % 8, MI355X_MICROARCH.md), so a task placed at a slot b = r (mod 8) for its row tile r
-// runs on the XCD whose L2 the previous level's tasks of row r wrote through.  Slots no task maps to get a no-op
-// (type 2 with i = -1).  Panel tasks keep coming first within each XCD's sequence.
-static void xcd_interleave(std::vector<int32_t>& tasks, int first_task) {
-  const int n = (int)tasks.size() / 4 - first_task;
-  if (n <= 1) return;
-  std::vector<std::vector<int>> q(8);
-  for (int t = 0; t < n; ++t) {
-    const int32_t* r = &tasks[4 * (first_task + t)];
-    q[(unsigned)r[1] % 8u].push_back(t);  // row tile i (type 3: the block's first row; type 2: the column)
-  }
-  size_t m = 0;
-  for (auto& b : q) m = std::max(m, b.size());
-  std::vector<int32_t> out;
-  out.reserve(4 * 8 * m);
-  for (size_t k = 0; k < m; ++k)
-    for (int x = 0; x < 8; ++x) {
-      if (k < q[x].size()) {
-        const int32_t* r = &tasks[4 * (first_task + q[x][k])];
-        out.insert(out.end(), r, r + 4);
-      } else {
-        out.insert(out.end(), {2, -1, -1, 0});
-      }
-    }
-  // trailing no-ops of the last round are dropped
-  while (out.size() >= 4 && out[out.size() - 4] == 2 && out[out.size() - 3] == -1) out.resize(out.size() - 4);
-  tasks.resize(4 * (size_t)first_task);
-  tasks.insert(tasks.end(), out.begin(), out.end());
-}
-
 // Tile structure (coupled frame pairs + the dense augmented row + symbolic fill), elimination levels
 // (at most two tile columns per level), tasks per level and back-substitution chains.
 // Rank-tree restriction of make_plan (make_plan_tree, §7): the tile columns this rank factors, phase by phase (each
@@ -844,11 +806,10 @@ struct TreeSpec {
 static int tile_owner(int i, int j, int nr) { return (i + j) % nr; }
 static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<int32_t>& win, int64_t ld, CholPlan& P,
                       int force_dt = 0, TreeSpec* ts = nullptr, int super_mode = -1) {
-  const bool xcd_order = getenv_is("PTZBA_CHOL_XCD", "1");
   // supercolumns (chol_super): two consecutive columns of a chain in one level -- single-rank plans at DT = 1;
   // PTZBA_CHOL_SUPER=1 enables (A/B knob, read per plan)
   if (super_mode < 0) super_mode = getenv_is("PTZBA_CHOL_SUPER", "1") ? 1 : 0;
-  if (ts || xcd_order) super_mode = 0;  // (continuation records must stay right behind their task)
+  if (ts) super_mode = 0;  // (continuation records must stay right behind their task)
   const int T = (int)(ld / CHOL_NB);
   std::vector<std::vector<uint8_t>> nz(T, std::vector<uint8_t>(T, 0));
   auto mark = [&](int r, int c) {
@@ -951,7 +912,7 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
   // inverted by type-2 tasks of level L, beside its panels (off the critical path); the last level's after
   // the factorisation (tinv_tail).  Columns >= n_inv (the augmented-row tile) need none.
   const int n_inv = (o.n_aug + CHOL_NB - 1) / CHOL_NB;
-  const bool tinv_split = !getenv("PTZBA_TINV_ALL");  // A/B knob: every inverse after the factorisation
+  const bool tinv_split = true;  // (round 2 A/B: every inverse after the factorisation instead: +4 us per trial)
   P.tinv_tail.clear();
   // Delayed trailing updates (period DT): trailing tasks run only at levels L = 0 mod DT and apply the
   // panels of levels [L - DT, L - 1] at once (rank <= 2 DT x 32: half the read-modify-writes of the band's
@@ -1099,7 +1060,6 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
       if (head[pp]) push(2, pp, pp, inv ? 1 : 3);
       else if (inv) push(2, pp, pp, 0);
     }
-    if (xcd_order) xcd_interleave(P.tasks, P.level_off[L]);  // PTZBA_CHOL_XCD=1 (read per plan)
   }
   for (int k = 0; k < n_inv && k < T; ++k)
     if (own(k) && (!tinv_split || level[k] == nL - 1)) P.tinv_tail.push_back(k);
@@ -1114,17 +1074,6 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
     P.level_off.push_back((int)(P.tasks.size() / 4));
   }
   P.n_levels = nL;
-  if (getenv("PTZBA_PLAN_DEBUG")) {  // per level: columns, tasks (panel / trailing / inverse)
-    for (int L = 0; L < nL; ++L) {
-      int n[3] = {0, 0, 0};
-      for (int q = P.level_off[L]; q < P.level_off[L + 1]; ++q) n[P.tasks[4 * q] & 3]++;
-      fprintf(stderr, "level %d cols", L);
-      if (L < (int)K.size())
-        for (int k : K[L]) fprintf(stderr, " %d%s", k, head[k] ? "+" : "");
-      fprintf(stderr, " | panel %d trailing %d inv %d\n", n[0], n[1], n[2]);
-    }
-    fprintf(stderr, "max panels per task %zu\n", max_pd);
-  }
   if (max_pd > 4 || super_over) {  // too many panels: DT = 1, then no supercolumns
     if (DT > 1) return make_plan(o, n_pose, nf, win, ld, P, 1, ts, super_mode);
     return super_mode ? make_plan(o, n_pose, nf, win, ld, P, force_dt, ts, 0) : false;
@@ -1403,14 +1352,10 @@ static bool dist_order(int n_pose, int nf, const std::vector<int32_t>& win, int 
       CholPlan P;
       TreePlan Q;
       if (!make_plan_tree(*os[v], DT, r, n_pose, nf, win, pad_tile(os[v]->n_aug + 1), P, Q)) {
-        if (getenv("PTZBA_PLAN_DEBUG")) fprintf(stderr, "dist_order: order %d rank %d has no plan\n", v + 1, r);
         if (v == 0) return false;
         return true;
       }
       e[v] = std::max(e[v], plan_est_us(P));
-      if (getenv("PTZBA_PLAN_DEBUG"))
-        fprintf(stderr, "dist_order: order %d rank %d base %d phases %zu levels %d est %.1f us\n", v + 1, r, Q.base,
-                Q.ph.size(), P.n_levels, plan_est_us(P));
     }
   }
   if (e[1] < e[0]) o = std::move(o2);
@@ -1420,16 +1365,15 @@ static bool dist_order(int n_pose, int nf, const std::vector<int32_t>& win, int 
 int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_t n_obs, const int32_t* obs_frame,
                       const int32_t* obs_landmark, const double* obs_xy, const double* obs_weight, double u, double v,
                       const ptzba_problem_opts* opts) {
-  // PTZBA_SETUP_TIMING=1: host phase times of this call on stderr (where a config-4 set_problem spends its seconds)
-  static const bool st_on = getenv("PTZBA_SETUP_TIMING") != nullptr;
+  if (!h) return fail("null handle");
+  // host phase times of this call (ptzba_setup_timing: where a config-4 set_problem spends its seconds)
+  h->setup_phases.clear();
   auto st_t0 = std::chrono::steady_clock::now();
   auto st_mark = [&](const char* what) {
-    if (!st_on) return;
     const auto t = std::chrono::steady_clock::now();
-    fprintf(stderr, "set_problem %-22s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(t - st_t0).count());
+    h->setup_phases.emplace_back(what, std::chrono::duration<double, std::milli>(t - st_t0).count());
     st_t0 = t;
   };
-  if (!h) return fail("null handle");
   if (n_pose < 1 || n_landmark < 0 || n_obs < 0) return fail("bad sizes n_pose=%d n_landmark=%d n_obs=%lld", n_pose, n_landmark, (long long)n_obs);
   if (n_obs > 0 && (!obs_frame || !obs_landmark || !obs_xy)) return fail("null observation pointer");
   ptzba_problem_opts o{PTZBA_FP64, PTZBA_LOSS_LINEAR, 1.0, 1, PTZBA_ORDER_NESTED, nullptr};
@@ -1479,7 +1423,6 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->u = u;
   h->v = v;
   h->weighted = obs_weight != nullptr;
-  h->k2_fold = getenv("PTZBA_K2_FOLD") ? atoi(getenv("PTZBA_K2_FOLD")) : 0;
 
   st_mark("validate");
   // ---- stable counting sorts: by frame, then by landmark -> (landmark, frame, original index)
@@ -1677,7 +1620,6 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     // are weighted so that every item takes about the same time and the two rounds pack evenly.
     int64_t W0 = 5;
     constexpr int64_t WD = 4;  // chunk-0 weight W0 / WD
-    if (const char* e = getenv("PTZBA_S2_W0")) W0 = std::max(1, atoi(e));  // A/B knob
     int64_t total_w = 0;
     for (size_t k = 0; k < tiles.size(); ++k)
       total_w += (int64_t)tiles[k].size() * (tile_key[2 * k + 1] == 0 ? W0 : WD);
@@ -1688,66 +1630,9 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     // solve: each item's 74 KB split partial and the reduce over its tile's splits are fixed costs (measured at
     // config 3, tools/dist_model.py: N = 8 shard 44-66 -> 37-47 us with 64-128 items)
     int64_t target_items = std::min<int64_t>(256, std::max<int64_t>(64, (512 * total_w) / 480000));
-    if (const char* e = getenv("PTZBA_S2_ITEMS")) target_items = std::max(64, atoi(e));  // A/B knob
     const int64_t slots = std::max<int64_t>(target_items - n_tiles, 64);
     const int64_t split_w = std::max<int64_t>(64 * WD, (total_w + slots - 1) / slots);
-    // matrix-core K2 over chunk PAIRS (k_schur_mf2, fp32 path): a work item covers the partner chunks 2cp and
-    // 2cp + 1 of its F1 block with the union of their landmark lists, so Y, the list and the chunk-0 diagonal
-    // terms are staged once for both chunks.  Its partial of chunk 2cp + h is partial (h * n_items + item): a
-    // tile's splits stay contiguous for k_schur_reduce (groups carry the offset).
-    h->s2_pair = h->precision == PTZBA_FP32 && schur_pair_mode();
-    if (h->s2_pair) {
-      std::vector<std::vector<int32_t>> ptl;
-      std::vector<int32_t> pkey;  // per pair tile: f1b, cp, chunk mask (bit h: chunk 2cp + h has a list)
-      for (size_t k = 0; k < tiles.size();) {
-        const int f1b = tile_key[2 * k], cp = tile_key[2 * k + 1] / 2;
-        std::vector<int32_t> u = tiles[k];
-        int mask = 1 << (tile_key[2 * k + 1] & 1);
-        size_t k2 = k + 1;
-        if (k2 < tiles.size() && tile_key[2 * k2] == f1b && tile_key[2 * k2 + 1] / 2 == cp) {
-          std::vector<int32_t> m;
-          std::set_union(u.begin(), u.end(), tiles[k2].begin(), tiles[k2].end(), std::back_inserter(m));
-          u.swap(m);
-          mask |= 1 << (tile_key[2 * k2 + 1] & 1);
-          ++k2;
-        }
-        ptl.push_back(std::move(u));
-        pkey.insert(pkey.end(), {f1b, cp, mask});
-        k = k2;
-      }
-      int64_t pw = 0;
-      for (size_t k = 0; k < ptl.size(); ++k) pw += (int64_t)ptl[k].size() * (pkey[3 * k + 1] == 0 ? W0 : WD);
-      int64_t ptarget = 256;  // one round of one workgroup per CU
-      if (const char* e = getenv("PTZBA_S2P_ITEMS")) ptarget = std::max(16, atoi(e));  // A/B knob
-      ptarget = std::min<int64_t>(ptarget, std::max<int64_t>(16, (ptarget * pw) / 240000));
-      const int64_t pslots = std::max<int64_t>(ptarget - (int64_t)ptl.size(), 16);
-      const int64_t psplit = std::max<int64_t>(32 * WD, (pw + pslots - 1) / pslots);
-      std::vector<int> first(ptl.size() + 1, 0);
-      for (size_t k = 0; k < ptl.size(); ++k) {
-        const auto& lst = ptl[k];
-        const int n = (int)lst.size();
-        const int64_t nw = (int64_t)n * (pkey[3 * k + 1] == 0 ? W0 : WD);
-        const int nparts = (int)std::max<int64_t>((nw + psplit - 1) / psplit, (n + SCHUR_PLMAX - 1) / SCHUR_PLMAX);
-        first[k] = (int)(s2_items.size() / 4);
-        for (int pp = 0; pp < nparts; ++pp) {
-          const int a0 = (int)((int64_t)n * pp / nparts), a1 = (int)((int64_t)n * (pp + 1) / nparts);
-          const int b0 = (int)(s2_lm.size() / 4);
-          for (int q = a0; q < a1; ++q) {
-            const int l = lst[q];
-            s2_lm.insert(s2_lm.end(), {l, lm_meta[4 * l], lm_meta[4 * l + 1], lm_meta[4 * l + 2]});
-          }
-          s2_items.insert(s2_items.end(), {pkey[3 * k], pkey[3 * k + 1] | (pkey[3 * k + 2] << 16), b0,
-                                           (int32_t)(s2_lm.size() / 4)});
-        }
-      }
-      first[ptl.size()] = (int)(s2_items.size() / 4);
-      const int N = first[ptl.size()];
-      for (size_t k = 0; k < ptl.size(); ++k)
-        for (int hh = 0; hh < 2; ++hh)
-          if ((pkey[3 * k + 2] >> hh) & 1)
-            s2_groups.insert(s2_groups.end(), {pkey[3 * k], 2 * pkey[3 * k + 1] + hh, hh * N + first[k], hh * N + first[k + 1]});
-    }
-    for (size_t k = 0; k < tiles.size() && !h->s2_pair; ++k) {
+    for (size_t k = 0; k < tiles.size(); ++k) {
       const auto& lst = tiles[k];
       const int n = (int)lst.size();
       const int64_t nw = (int64_t)n * (tile_key[2 * k + 1] == 0 ? W0 : WD);
@@ -1909,8 +1794,8 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   HIPCHK(hipStreamSynchronize(h->st));
   h->stage_used = 0;
   h->stage_ops.clear();
-  // PTZBA_STAGE_BATCH=0: one hipMemcpyAsync / hipMemsetAsync per array (A/B knob)
-  h->stage_batch = !getenv_is("PTZBA_STAGE_BATCH", "0");
+  // the staged uploads / zero fills land with one copy + one scatter launch (0.73 -> 0.66 ms per config-5 call, r04z4)
+  h->stage_batch = true;
   struct BatchOff {  // every exit (errors included) leaves the batching off
     ptzba_ctx* h;
     ~BatchOff() { h->stage_batch = false; }
@@ -1941,15 +1826,6 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       upload_st(h, h->s2_items, s2_items) || upload_st(h, h->s2_groups, s2_groups) || upload_st(h, h->s2_lm, s2_lm) ||
       upload_st(h, h->lm_meta, lm_meta))
     return -1;
-  {  // item -> tile (group) map and the per-tile split counters of the folded reduce (zero between launches)
-    std::vector<int32_t> item_group(std::max(h->n_s2_items, 1), 0);
-    for (int g = 0; g < h->n_s2_groups; ++g)
-      for (int it = s2_groups[4 * g + 2]; it < s2_groups[4 * g + 3]; ++it)
-        if (it < h->n_s2_items) item_group[it] = g;  // (pair items: their first chunk's tile)
-    if (upload_st(h, h->s2_item_group, item_group) || h->s2_tile_cnt.alloc((size_t)std::max(h->n_s2_groups, 1) * 4))
-      return -1;
-    if (zero_async(h, h->s2_tile_cnt.p, h->s2_tile_cnt.bytes)) return -1;
-  }
   const size_t e = h->elem();
   if (h->ptz.alloc(3 * n_pose * 8) || h->ptz_trial.alloc(3 * n_pose * 8) || h->rays.alloc(2 * (size_t)n_landmark * 8) ||
       h->rays_trial.alloc(2 * (size_t)n_landmark * 8) || h->D_pose.alloc(3 * n_pose * 8) ||
@@ -1964,7 +1840,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       h->Ldiag.alloc((size_t)h->ld * CHOL_NB * 8) || h->Minv.alloc((size_t)h->ld * CHOL_NB * 8) ||
       (h->chol_super && h->Lsub.alloc((size_t)h->ld * CHOL_NB * 8)) ||
       h->dpose.alloc((size_t)h->ld * 8) ||
-      h->s2_part.alloc((size_t)std::max(h->n_s2_items, 1) * (h->s2_pair ? 2 : 1) * SCHUR_F1 * 9 * WAVE * 8) ||
+      h->s2_part.alloc((size_t)std::max(h->n_s2_items, 1) * SCHUR_F1 * 9 * WAVE * 8) ||
       h->part_diag.alloc((size_t)std::max(h->n_s2_items, 1) * SCHUR_F1 * 12 * 8))
     return -1;
   if (upload_st(h, h->chol_tasks, plan.tasks) || upload_st(h, h->tinv_tail, plan.tinv_tail) || upload_st(h, h->frame_pos, sorder.pos) || upload_st(h, h->row_pad, sorder.pad) ||
@@ -2008,32 +1884,14 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->bs_ll = (h->bs_ll || bsk == "ll") && !h->bs_blk;
   h->bsb_step_off = plan.bsb_step_off;
   // persistent form: every step's tasks in one launch (all resident at <= 512 workgroups); PTZBA_BS_PERSIST=0 keeps
-  // one launch per step (A/B knob)
-  // (same-box A/B r04a: cholesky_solve 245 -> 241 us per trial at config 3)
+  // one launch per step (the bitwise schedule test compares both; same-box A/B r04a: cholesky_solve 245 -> 241 us
+  // per trial at config 3)
   h->bs_pst = h->bs_blk && !getenv_is("PTZBA_BS_PERSIST", "0") &&
               plan.bsb_tasks.size() / 12 <= 512;  // (2 workgroups per CU resident: 190 VGPRs)
   h->bsp_epoch = 0;
-  // single-launch factorisation (PTZBA_CHOL_PERSIST=1, A/B knob): single-process SPD solves
   h->no_fused_prep = getenv("PTZBA_NO_FUSED_PREP") != nullptr;
-  h->chol_pst = !part_mode && !dist && (getenv_is("PTZBA_CHOL_PERSIST", "1") || getenv_is("PTZBA_CHOL_PERSIST", "2")) &&
-                plan.n_levels > 0 && !h->chol_super;
-  h->chol_pst_ticket = !getenv_is("PTZBA_CHOL_PERSIST", "2");
-  h->chol_epoch = 0;
-  if (h->chol_pst) {
-    std::vector<int32_t> lvl(std::max(plan.level_off[plan.n_levels], 1), 0), lvl_n(plan.n_levels, 0);
-    for (int L = 0; L < plan.n_levels; ++L) {
-      lvl_n[L] = plan.level_off[L + 1] - plan.level_off[L];
-      for (int t = plan.level_off[L]; t < plan.level_off[L + 1]; ++t) lvl[t] = L;
-    }
-    if (upload_st(h, h->chol_lvl, lvl) || upload_st(h, h->chol_lvl_n, lvl_n) ||
-        h->chol_lvl_cnt.alloc(4 * ((size_t)plan.n_levels + 1)))
-      return -1;
-    if (zero_async(h, h->chol_lvl_cnt.p, h->chol_lvl_cnt.bytes)) return -1;
-  }
-  if ((h->bs_pst || h->chol_pst) && !h->bsp_err) {
-    HIPCHK(hipHostMalloc((void**)&h->bsp_err, sizeof(int), hipHostMallocDefault));
-    *h->bsp_err = 0;
-  }
+  if (h->bs_pst && !h->bsp_err) HIPCHK(hipHostMalloc((void**)&h->bsp_err, sizeof(int), hipHostMallocDefault));
+  if (h->bsp_err) *h->bsp_err = 0;  // (a wait that gave up under an earlier problem does not outlive it)
   if (h->bs_pst) {
     if (upload_st(h, h->bsp_expect, plan.bsb_expect) || upload_st(h, h->bsp_tot, plan.bsb_tot) ||
         h->bsp_cnt.alloc(4 * plan.bsb_tot.size()))
@@ -2340,11 +2198,7 @@ static int build_impl(ptzba_ctx* h, double lambda, const double* lam_dev, const 
   a.w_slot1 = h->w_slot[1].p;
   a.sel = sel;
   a.prep = fp;
-  a.item_group = h->s2_item_group.as<int32_t>();
-  a.tile_cnt = h->s2_tile_cnt.as<unsigned>();  // folded reduce (SchurArgs::fold)
-  a.fold = h->k2_fold;
   tm_begin(h, TM_SCHUR);
-  a.pair = h->s2_pair;
   if (h->precision == PTZBA_FP32)
     launch_schur<float>(a, h->n_s2_items, h->n_s2_groups, h->n_fixed, h->st);
   else
@@ -2408,19 +2262,7 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
       launch_chol_prepare_damped(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(),
                                  h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
                                  h->lambda, lam_dev, h->st);
-    if (h->chol_pst) {
-      // PTZBA_CHOL_GROUP=g (block-index form only): g levels per launch instead of all (A/B knob)
-      const char* ge = getenv("PTZBA_CHOL_GROUP");
-      const int g = (ge && !h->chol_pst_ticket) ? std::max(1, atoi(ge)) : h->chol_levels;
-      for (int L0 = 0; L0 < h->chol_levels; L0 += g)
-        launch_cholesky_pst(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_lvl.as<int>(),
-                            h->chol_lvl_n.as<int>(), h->chol_lvl_cnt.as<unsigned>(),
-                            h->chol_pst_ticket ? h->chol_lvl_cnt.as<unsigned>() + h->chol_levels : nullptr,
-                            h->chol_epoch, L0, std::min(L0 + g, h->chol_levels), h->Ldiag.as<double>(),
-                            h->info.as<int>(), h->Minv.as<double>(), h->chol_delayed, h->bsp_err, h->st);
-      h->chol_epoch++;
-    } else
-      launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
+    launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
                       h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>(), 0,
                       h->chol_delayed, h->chol_super ? h->Lsub.as<double>() : nullptr);
   }
@@ -2556,6 +2398,7 @@ int ptzba_lm_init(ptzba_handle h, const ptzba_lm_opts* o) {
   for (int k = 0; k < LM_RING; ++k) __atomic_store_n(&h->lm_host[k].seq, 0, __ATOMIC_RELAXED);
   launch_lm_init(h->lmdev.as<LMDev>(), h->scal.as<double>(), p, h->cur, h->st);
   h->state_base = h->cur;  // (ptz, rays) hold the current state now
+  if (h->bsp_err) *h->bsp_err = 0;  // a run starts without an earlier run's gave-up flag (nothing of it is in flight)
   h->scal_deferred = false;
   HIPCHK(hipGetLastError());
   return 0;
@@ -2618,9 +2461,9 @@ int ptzba_lm_wait(ptzba_handle h, int trial, ptzba_lm_record* out) {
     }
     __builtin_ia32_pause();
   }
-  if ((h->bs_pst || h->chol_pst) && __atomic_load_n(h->bsp_err, __ATOMIC_ACQUIRE))
+  if (h->bs_pst && __atomic_load_n(h->bsp_err, __ATOMIC_ACQUIRE))
     return fail("lm_wait: a persistent factorisation / back-substitution kernel gave up waiting (workgroups not "
-                "co-resident?); PTZBA_CHOL_PERSIST=0 / PTZBA_BS_PERSIST=0 select the per-level forms");
+                "co-resident?); PTZBA_BS_PERSIST=0 selects the per-step form");
   const LMDev& r = h->lm_host[k];
   out->cost = r.cost;
   out->initial_cost = r.initial_cost;
@@ -2735,9 +2578,8 @@ int ptzba_read_scalars(ptzba_handle h, double* out) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(h->scal_host, h->scal_pack.p, 17 * sizeof(double), hipMemcpyDeviceToHost, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
-  if ((h->bs_pst || h->chol_pst) && __atomic_load_n(h->bsp_err, __ATOMIC_ACQUIRE))
-    return fail("a persistent factorisation / back-substitution kernel gave up waiting (PTZBA_CHOL_PERSIST=0 / "
-                "PTZBA_BS_PERSIST=0 select the per-level forms)");
+  if (h->bs_pst && __atomic_load_n(h->bsp_err, __ATOMIC_ACQUIRE))
+    return fail("the persistent back-substitution kernel gave up waiting (PTZBA_BS_PERSIST=0 selects the per-step form)");
   const double* s = h->scal_host;
   const double* l = h->scal_host + 8;
   out[0] = s[0];
@@ -3360,5 +3202,17 @@ int ptzba_set_huber_curvature(ptzba_handle h, double hc) {
   if (!h) return fail("null handle");
   if (!(hc > 0.0 && hc <= 1.0)) return fail("huber curvature must lie in (0, 1]");
   h->hcurv = hc;
+  return 0;
+}
+
+// host phase times of the last ptzba_set_problem: names[k] (static strings) and ms[k], k < *n_out (<= cap)
+int ptzba_setup_timing(ptzba_handle h, int32_t cap, const char** names, double* ms, int32_t* n_out) {
+  if (!h || !n_out || cap < 0 || (cap > 0 && (!names || !ms))) return fail("ptzba_setup_timing: bad arguments");
+  const int32_t n = (int32_t)std::min<size_t>(h->setup_phases.size(), (size_t)cap);
+  for (int32_t k = 0; k < n; ++k) {
+    names[k] = h->setup_phases[k].first;
+    ms[k] = h->setup_phases[k].second;
+  }
+  *n_out = (int32_t)h->setup_phases.size();
   return 0;
 }

@@ -580,8 +580,7 @@ template <typename real>
 void launch_linearize(const LinArgs& a, int loss, hipStream_t st) {
   if (a.n_work <= 0) return;
   dim3 grid((a.n_work + 3) / 4);
-  static const bool ftl_off = getenv("PTZBA_K1_FTL") && atoi(getenv("PTZBA_K1_FTL")) == 0;  // A/B knob
-  const bool ftl = a.n_pose <= K1_FT_LDS && !ftl_off;
+  const bool ftl = a.n_pose <= K1_FT_LDS;  // frame tables staged in LDS (neutral vs global reads, 13 VGPRs fewer)
   if (ftl) {
     if (loss == 0) hipLaunchKernelGGL((k_linearize<real, 0, true>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((k_linearize<real, 1, true>), grid, dim3(256), 0, st, a);
@@ -705,10 +704,10 @@ struct PoseTrialArgs {
   const uint8_t* fmask;  // part-owned solve: bit 0 pose updated here, bit 1 counted here (nullptr: all)
   const int* info;       // part-owned solve: this rank's factorisation status -> out4[4] (summed over ranks)
 };
-// DPL: the pose steps by frame staged in LDS (n_pose <= K1_FT_LDS): a landmark wave walks its DENSE slot range
-// [first, last] (slots of frames that do not see it hold W = 0) instead of its segment list, so its dependent chain
-// is lm_meta -> W slots (+ LDS) instead of segment list -> frame -> system row -> dpose
-template <typename real, bool DPL>
+// (Round 4 tried staging the pose steps in LDS and walking a landmark's DENSE slot range instead of its segments:
+// 35.9 vs 27.9 us per trial, and it sums t0 / t1 in another lane order -- not bitwise the same trial.  Removed in
+// round 5.)
+template <typename real>
 __global__ __launch_bounds__(256) void k_trial(BacksubArgs a, PoseTrialArgs pa, FrameTab<double>* __restrict__ ft64,
                                                RayTab<double>* __restrict__ rt64, FrameTab<real>* __restrict__ ft,
                                                RayTab<real>* __restrict__ rt) {
@@ -774,15 +773,6 @@ __global__ __launch_bounds__(256) void k_trial(BacksubArgs a, PoseTrialArgs pa, 
   }
   const int lane = lane_id();
   const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
-  __shared__ double s_dp[DPL ? 3 * K1_FT_LDS : 1];
-  if constexpr (DPL) {
-    // dpose by frame (0 for fixed frames), requested beside the landmark's own operands below
-    for (int e = threadIdx.x; e < 3 * pa.n_pose; e += blockDim.x) {
-      const int f = e / 3;
-      s_dp[e] = f < a.n_fixed ? 0.0 : a.dpose[a.frame_pos[f] + e % 3];
-    }
-    __syncthreads();
-  }
   if (l >= a.n_lm) return;
   const int s0 = a.lm_seg_begin[l], s1 = a.lm_seg_begin[l + 1];
   const bool alt = a.sel && *a.sel;  // device-chosen linearisation slot
@@ -796,32 +786,16 @@ __global__ __launch_bounds__(256) void k_trial(BacksubArgs a, PoseTrialArgs pa, 
   const double th = a.rays[2 * l], ph = a.rays[2 * l + 1];
   const double D0 = a.D_ray[2 * l], D1 = a.D_ray[2 * l + 1];
   double t0 = 0, t1 = 0;
-  if constexpr (DPL) {
-    if (s1 > s0) {
-      const int nsl = lmeta.y - lmeta.x + 1;  // dense slots of frames first .. last
-      for (int k = lane; k < nsl; k += WAVE) {
-        real w[6];
-        load_w6_slot(w, w_slot + ((int64_t)lmeta.z + k) * 8);
-        const double* dp = s_dp + 3 * (lmeta.x + k);
+  for (int s = s0 + lane; s < s1; s += WAVE) {
+    const int f = a.seg_frame[s];
+    if (f < a.n_fixed) continue;
+    const double* dp = a.dpose + a.frame_pos[f];
+    real w[6];
+    load_w6_slot(w, w_slot + ((int64_t)lmeta.z + f - lmeta.x) * 8);
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          t0 += (double)w[2 * q] * dp[q];
-          t1 += (double)w[2 * q + 1] * dp[q];
-        }
-      }
-    }
-  } else {
-    for (int s = s0 + lane; s < s1; s += WAVE) {
-      const int f = a.seg_frame[s];
-      if (f < a.n_fixed) continue;
-      const double* dp = a.dpose + a.frame_pos[f];
-      real w[6];
-      load_w6_slot(w, w_slot + ((int64_t)lmeta.z + f - lmeta.x) * 8);
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        t0 += (double)w[2 * q] * dp[q];
-        t1 += (double)w[2 * q + 1] * dp[q];
-      }
+    for (int q = 0; q < 3; ++q) {
+      t0 += (double)w[2 * q] * dp[q];
+      t1 += (double)w[2 * q + 1] * dp[q];
     }
   }
   t0 = wave_total(t0);
@@ -861,14 +835,7 @@ void launch_trial(const BacksubArgs& a, const double* ptz, const double* g_pose,
                   double* out4, int n_pose, void* ft64, void* rt64, void* ft, void* rt, hipStream_t st,
                   const uint8_t* fmask, const int* info) {
   PoseTrialArgs pa{ptz, g_pose, D_pose, ptz_trial, out4, n_pose, fmask, info};
-  // PTZBA_TRIAL_DPL=1: dense dpose staged in LDS (A/B knob; off: config 3 trial 35.9 -> 27.9 us without it, r04a)
-  const char* dpl_env = getenv("PTZBA_TRIAL_DPL");  // (read per launch: tests switch it between handles)
-  const bool dpl_on = dpl_env && atoi(dpl_env) == 1;
-  if (n_pose <= K1_FT_LDS && dpl_on && !fmask)  // (part-owned solves: the other part's dpose rows are not solved here)
-    hipLaunchKernelGGL((k_trial<real, true>), dim3((unsigned)((a.n_lm + 3) / 4 + 1)), dim3(256), 0, st, a, pa,
-                       (FrameTab<double>*)ft64, (RayTab<double>*)rt64, (FrameTab<real>*)ft, (RayTab<real>*)rt);
-  else
-    hipLaunchKernelGGL((k_trial<real, false>), dim3((unsigned)((a.n_lm + 3) / 4 + 1)), dim3(256), 0, st, a, pa,
+  hipLaunchKernelGGL((k_trial<real>), dim3((unsigned)((a.n_lm + 3) / 4 + 1)), dim3(256), 0, st, a, pa,
                        (FrameTab<double>*)ft64, (RayTab<double>*)rt64, (FrameTab<real>*)ft, (RayTab<real>*)rt);
 }
 
@@ -1023,9 +990,7 @@ void launch_reduce_cols(const double* src, int64_t n, int stride, int nk, int ma
                         const int* sel, int sel_xor, const DecideArgs* decide) {
   unsigned* counter = reinterpret_cast<unsigned*>(scratch + RED_BLOCKS * 8);
   const DecideArgs dec = decide ? *decide : DecideArgs{nullptr, nullptr, nullptr, nullptr, 0, 0};
-  // workgroups: RED_BLOCKS, or PTZBA_RED_BLOCKS (A/B knob; fewer blocks = fewer counter arrivals, more rows each)
-  static const int nb_env = getenv("PTZBA_RED_BLOCKS") ? atoi(getenv("PTZBA_RED_BLOCKS")) : 0;
-  const int nb = nb_env > 0 ? std::min(nb_env, RED_BLOCKS) : RED_BLOCKS;
+  const int nb = RED_BLOCKS;
   hipLaunchKernelGGL(k_reduce_cols, dim3(nb), dim3(256), 0, st, src, n, stride, nk, maxmask, out, scratch,
                      counter, src2, stride2, src2 ? nk2 : 0, out2, src1, sel, sel_xor, dec);
 }

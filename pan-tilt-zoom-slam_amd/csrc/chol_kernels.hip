@@ -101,9 +101,9 @@ void launch_chol_prepare_damped(double* A, int64_t ld, int n, double* b, const u
 // Batched tile staging: every thread fetches its 4 elements of each tile into registers first (all global
 // loads of a task in flight together: one memory round trip per task instead of one per update panel),
 // then writes them to LDS.  256 threads per workgroup.
-// COH (the persistent factorisation, k_chol_pst): tiles written by other workgroups of the same launch are read
-// with agent-scope loads that miss this XCD's (possibly stale) L2 and written through with agent-scope stores
-// (MI355X_MICROARCH.md, inter-workgroup hand-off table, first row); plain accesses otherwise.
+// COH (the SPD level launches' default): tiles are read with agent-scope loads that miss this XCD's L2 and written
+// through with agent-scope stores (MI355X_MICROARCH.md, inter-workgroup hand-off table, first row), so the next
+// level's workgroups on other XCDs find them in the Infinity Cache; plain accesses otherwise.
 template <bool COH>
 __device__ __forceinline__ double gld(const double* p) {
   if constexpr (COH) return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -967,7 +967,7 @@ __device__ __forceinline__ void chol_super(double* __restrict__ A, int64_t ld, i
 
 // P2: plans with delayed trailing updates (a second pair of update panels per task, api.hip make_plan)
 // One factorisation task (api.hip make_plan: panel / trailing / inverse / trailing block) by the workgroup: the
-// body of a level launch (k_chol_step) and of the persistent form (k_chol_pst, COH = true).
+// body of a level launch (k_chol_step).
 template <bool SG, bool P2, bool COH, bool SUP = false>
 __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, const int4 tk, double* __restrict__ Ldiag,
                                           int* info, double* __restrict__ sgn, double* __restrict__ Minv,
@@ -1324,68 +1324,9 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
   chol_task<SG, P2, COH, SUP>(A, ld, tk, Ldiag, info, sgn, Minv, Lsub, tk2);
 }
 
-// Single-launch form of the level launches (single-process SPD solves): the tasks of levels [L0, L1) in ONE launch of
-// one workgroup per task.  A workgroup takes its task by a ticket (atomic add on a counter that advances by the task
-// count per launch: ticket - epoch * n), so a task's predecessors -- all at lower indices -- belong to workgroups that
-// started earlier: forward progress needs no co-residency and no dispatch-order assumption.  A task of level L > L0
-// starts once level L - 1's counter shows all its tasks done in this epoch; tiles are read and written coherently
-// (COH), and a task's stores are drained (vmcnt(0)) before its level counter moves.  The same tasks in the same order
-// per tile as the level launches: bitwise the same factor.  The launch boundaries between levels (~26 per trial at
-// config 3) become counter hand-offs.
-constexpr int CPST_SPIN = 1 << 22;  // polls before a wait gives up (err = 1): ~seconds, never a hang
-template <bool P2>
-__global__ __launch_bounds__(256) void k_chol_pst(double* __restrict__ A, int64_t ld, const int4* __restrict__ tasks,
-                                                  const int* __restrict__ task_lvl, int t0, int n, int L0,
-                                                  const int* __restrict__ lvl_n, unsigned* __restrict__ lvl_cnt,
-                                                  unsigned* __restrict__ ticket, uint32_t epoch,
-                                                  double* __restrict__ Ldiag, int* info, double* __restrict__ Minv,
-                                                  int* err, int nsleep) {
-  __shared__ int s_t;
-  if (threadIdx.x == 0) {
-    // ticket == nullptr: the task of blockIdx.x (relies on workgroups being dispatched in index order; A/B knob --
-    // the waits are bounded either way)
-    const int t = ticket ? t0 + (int)(__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
-                                      epoch * (unsigned)n)
-                         : t0 + (int)blockIdx.x;
-    s_t = t;
-    const int L = task_lvl[t];
-    if (L > L0) {
-      const unsigned target = (epoch + 1u) * (unsigned)lvl_n[L - 1];
-      bool ok = false;
-      for (int k = 0; k < CPST_SPIN; ++k) {
-        if ((int)(__hip_atomic_load(lvl_cnt + L - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) >= 0) {
-          ok = true;
-          break;
-        }
-        for (int q = 0; q < nsleep; ++q) __builtin_amdgcn_s_sleep(1);  // (polling pressure on the counter, A/B)
-      }
-      if (!ok) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // pinned host flag
-    }
-  }
-  __syncthreads();
-  const int t = s_t;
-  chol_task<false, P2, true>(A, ld, tasks[t], Ldiag, info, nullptr, Minv);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's tile stores have landed (write-through)
-  __syncthreads();                                   // ... every thread's
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(lvl_cnt + task_lvl[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-int launch_cholesky_pst(double* A, int64_t ld, const int4* tasks, const int* task_off_host, const int* task_lvl,
-                        const int* lvl_n, unsigned* lvl_cnt, unsigned* ticket, uint32_t epoch, int L0, int L1,
-                        double* Ldiag, int* info, double* Minv, bool delayed, int* err, hipStream_t st) {
-  const int t0 = task_off_host[L0], n = task_off_host[L1] - t0;
-  if (n <= 0) return 0;
-  const char* se = getenv("PTZBA_CHOL_SPIN_SLEEP");  // A/B knob: s_sleep(1) per poll
-  const int nsleep = se ? std::max(1, atoi(se)) : 1;
-  if (delayed)
-    hipLaunchKernelGGL(k_chol_pst<true>, dim3((unsigned)n), dim3(256), 0, st, A, ld, tasks, task_lvl, t0, n, L0, lvl_n,
-                       lvl_cnt, ticket, epoch, Ldiag, info, Minv, err, nsleep);
-  else
-    hipLaunchKernelGGL(k_chol_pst<false>, dim3((unsigned)n), dim3(256), 0, st, A, ld, tasks, task_lvl, t0, n, L0, lvl_n,
-                       lvl_cnt, ticket, epoch, Ldiag, info, Minv, err, nsleep);
-  return 0;
-}
-
+// (Rounds 4 tried every level of a factorisation in ONE launch -- one workgroup per task, a task of level L waiting
+// on level L - 1's completion counter: bitwise the same factor, 338-425 us per trial against ~232 with one launch per
+// level; removed in round 5.)
 template <typename TaskArg, bool COH>
 static void launch_chol_level(const TaskArg& ta, int n, double* A, int64_t ld, double* Ldiag, int* info, double* sgn,
                               double* Minv, bool delayed, hipStream_t st, double* Lsub) {
@@ -1401,7 +1342,9 @@ static void launch_chol_level(const TaskArg& ta, int n, double* A, int64_t ld, d
 void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_off_host, int n_launch, double* Ldiag,
                      int* info, hipStream_t st, double* sgn, const int4* tasks_host, double* Minv, int first_level,
                      bool delayed, double* Lsub) {
-  static const bool by_value = !getenv("PTZBA_CHOL_TASKS_PTR");  // A/B knob
+  // a level's first CHOL_KT tasks travel by value in the kernel arguments (the rest through a pointer): the
+  // workgroup's first dependent load disappears (round 2 A/B: 313 -> 308 us per trial at config 3)
+  constexpr bool by_value = true;
   // SPD factorisations write their tiles through (agent-scope stores) and read them past this XCD's L2: the next
   // level's workgroups, mostly on other XCDs, find the tiles in the Infinity Cache at once (same-box A/B r04e:
   // cholesky_solve 240 -> 232 us per trial at config 3).  PTZBA_CHOL_COH=0: plain accesses (A/B knob, read per call)
@@ -1982,6 +1925,9 @@ __global__ __launch_bounds__(64 * BSB_P) void k_chol_backsolve_pst(
       rk = yval(cc + c);
     } else {
       ok = bsp_wait(cnt + ck, epoch * (unsigned)tot[ck] + (unsigned)eck);
+      // acquire after the counter observation: the r load below cannot be reordered above the poll (by the compiler
+      // or a later toolchain) and misses this CU's vector cache; the L2 is not written back by it
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       rk = __hip_atomic_load(r + cc + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (k == 0 && t >= 0) {
@@ -1989,6 +1935,7 @@ __global__ __launch_bounds__(64 * BSB_P) void k_chol_backsolve_pst(
         rt = yval((int64_t)t * NB + c);
       } else {
         ok = bsp_wait(cnt + t, epoch * (unsigned)tot[t] + (unsigned)ex2.x) && ok;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // as above
         rt = __hip_atomic_load(r + (int64_t)t * NB + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -2040,7 +1987,9 @@ __global__ __launch_bounds__(64 * BSB_P) void k_chol_backsolve_pst(
         if ((tmask >> j) & 1) sum += ps[j][c];
       __hip_atomic_store(r + (int64_t)t * NB + c, rt - sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's r_t stores have landed (write-through)
+    // wave 0's r_t stores have landed (write-through, sc1) before the counter add; the asm's memory clobber keeps the
+    // compiler from moving the add above the stores.  No agent-scope release: it would write back this XCD's L2
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) __hip_atomic_fetch_add(cnt + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }

@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) void k_top2(int n1, int n2, const float* __res
 }
 
 // kNN-2 on the matrix cores for integer-valued 128-d descriptors (SIFT's: integers 0..255): one workgroup per 64 query
-// rows (a wave per 16), the train set streamed through LDS in tiles of 64 as f16 (exact: integers up to 2048), the
+// rows (a wave per 16), the train set streamed through LDS in tiles of 64 as f16 (exact: integers with 2 dim v^2 < 2^24, |v| <= 255 at 128-d), the
 // dot products on v_mfma_f32_16x16x32_f16 (products exact, sums exact integers below 2^24), d^2 = |q|^2 + |t|^2 - 2 q.t
 // exact -- the same integer k_sqdist's fp32 sum of (a - b)^2 gives -- and each lane keeps a running (distance, index)
 // top 2 for its four rows over its columns (ascending), merged across the 16 lanes of a row at the end with k_top2's
@@ -531,7 +531,7 @@ struct DescSet {
   DBuf buf;
   int64_t n = 0;
   int32_t dim = 0;
-  bool integral = false;  // every value an integer of magnitude <= 2048 (exact in f16: k_knn2_mf applies)
+  bool integral = false;  // every value an integer with 2 dim v^2 < 2^24 (exact in f16 sums: k_knn2_mf applies)
 };
 struct DescStore {
   std::vector<std::pair<uint64_t, DescSet*>> sets;
@@ -558,8 +558,11 @@ int ptz_desc_put(int device, uint64_t key, int64_t n, int32_t dim, const float* 
   if (d->buf.reserve((size_t)std::max<int64_t>(n, 1) * dim * 4)) return -1;
   d->n = n;
   d->dim = dim;
+  // the matrix-core kNN (k_knn2_mf) is exact while every f16 product and every distance sum stays an exact integer
+  // below 2^24: 2 * dim * v^2 < 2^24, i.e. |v| <= 255 for 128-d (SIFT) rows
+  const float vmax = std::floor(std::sqrt((float)((1 << 23) - 1) / (float)std::max(dim, 1)));
   bool integral = true;
-  for (int64_t e = 0; e < n * dim && integral; ++e) integral = des[e] == std::nearbyint(des[e]) && std::fabs(des[e]) <= 2048.f;
+  for (int64_t e = 0; e < n * dim && integral; ++e) integral = des[e] == std::nearbyint(des[e]) && std::fabs(des[e]) <= vmax;
   d->integral = integral;
   if (n) HIPCHK(hipMemcpy(d->buf.p, des, (size_t)n * dim * 4, hipMemcpyHostToDevice));
   return 0;
@@ -594,7 +597,7 @@ int ptz_match_knn2_sets(int device, int32_t n_sets, const uint64_t* query_keys, 
   for (int32_t q = 0; q < n_sets; ++q) {
     const DescSet* d = S.find(query_keys[q]);
     if (!d) return fail("ptz_match_knn2_sets: no descriptor set under query key %llu", (unsigned long long)query_keys[q]);
-    if (d->n > 0 && d->dim != dim) return fail("ptz_match_knn2_sets: query set %d has dim %d, train %d", q, d->dim, dim);
+    if (d->n > 0 && n2 > 0 && d->dim != dim) return fail("ptz_match_knn2_sets: query set %d has dim %d, train %d", q, d->dim, dim);
     n1 += d->n;
   }
   if (n1 != n_rows) return fail("ptz_match_knn2_sets: the query sets hold %lld rows, the output %lld", (long long)n1, (long long)n_rows);

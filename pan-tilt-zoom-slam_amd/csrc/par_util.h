@@ -10,13 +10,11 @@
 
 namespace ptzba {
 
-// worker threads for a pass over n items: at most PTZBA_HOST_THREADS (default 16, the GPU box's CPU share per
-// GPU), one per 256 K items (a config-5 window's ~170K records stay on one thread: 2 threads measured slower there,
+// worker threads for a pass over n items: at most 16 (the GPU box's CPU share per GPU), one per 256 K items (a config-5 window's ~170K records stay on one thread: 2 threads measured slower there,
 // sort 0.6 -> 1.1 ms, segments 1.0 -> 1.5 ms, r04t)
 inline int host_threads(int64_t n) {
   static const int cap = [] {
-    const char* e = getenv("PTZBA_HOST_THREADS");
-    int c = e ? atoi(e) : 16;
+    int c = 16;
     const int hw = (int)std::thread::hardware_concurrency();
     if (hw > 0) c = std::min(c, hw);
     return std::max(1, c);

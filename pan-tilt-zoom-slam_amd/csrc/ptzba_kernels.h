@@ -50,9 +50,6 @@ struct LinArgs {
 // splits of a tile's landmark list.  Static structure built once by ptzba_set_problem.
 constexpr int SCHUR_F1 = 32;
 constexpr int SCHUR_LMAX = 512;  // landmarks per work item (split size cap)
-constexpr int SCHUR_PLMAX = 256;  // the same for chunk-pair items (k_schur_mf2: LDS holds two chunks' operands)
-// chunk-pair K2 (k_schur_mf2) for the fp32 path: PTZBA_SCHUR=mf2 / =mf (A/B); see schur_kernels.hip
-bool schur_pair_mode();
 // Single-GPU builds fold k_chol_prepare into the build: the prologue writes the constant diagonal entries
 // (padding identity, augmented diagonal, identity below it) and resets info; k_schur_reduce writes the
 // augmented row b^T and the pose damping (D_pose = max(D_pose, diag U); S_ff += lambda D_pose), the same
@@ -88,15 +85,7 @@ struct SchurArgs {
   const void* ug_slot1;           // sel != nullptr: read slot *sel (1 = these buffers), see LinArgs
   const void* w_slot1;
   const int* sel;
-  const int32_t* item_group;      // [n_items] tile (group) of each item (matrix-core K2: folded reduce)
-  unsigned* tile_cnt;             // [n_groups] finished splits per tile (zero between launches)
   FusedPrep prep;                 // single-GPU: the prepare's augmented row and damping (pad != nullptr)
-  bool pair = false;              // items over chunk pairs (k_schur_mf2; item.y = cp | chunk mask << 16)
-  // matrix-core K2: the tile's last split reduces it inside k_schur_mf (no k_schur_reduce launch).  1: acq_rel
-  // counter (round 3: every split's release wrote back its XCD's L2, 258 us per build); 2: write-through (sc1)
-  // partial stores, each storing wave drained (vmcnt(0)), a relaxed counter add after the workgroup barrier, sc1
-  // loads in the last split (MI355X_MICROARCH.md inter-workgroup visibility, first row of the hand-off table)
-  int fold = 0;
 };
 
 struct BacksubArgs {
@@ -219,9 +208,7 @@ void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_o
 // per-level completion counters lvl_cnt and the ticket counter monotone over launches (epoch = launches so far over
 // the same level range); task_lvl[t] = level of task t, lvl_n[L] = tasks of level L; err: host-pinned flag set when
 // a wait gave up.
-int launch_cholesky_pst(double* A, int64_t ld, const int4* tasks, const int* task_off_host, const int* task_lvl,
-                        const int* lvl_n, unsigned* lvl_cnt, unsigned* ticket, uint32_t epoch, int L0, int L1,
-                        double* Ldiag, int* info, double* Minv, bool delayed, int* err, hipStream_t st);
+
 // la_tasks: lookahead back substitution's [lookahead tile per position | task offsets per (chain, helper) |
 // tasks q << 16 | tile], built by the host plan (api.hip make_plan)
 constexpr int BS_HELPERS = 7;

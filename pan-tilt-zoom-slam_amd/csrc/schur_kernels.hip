@@ -390,11 +390,6 @@ template <typename real, bool AGENT>
 __device__ __forceinline__ void schur_reduce_elem(const SchurArgs& a, const int4 g, int e);
 template <bool AGENT>
 __device__ __forceinline__ void schur_reduce_vec(const SchurArgs& a, const int4 g, int tid);
-#ifndef MF_FOLD_REDUCE
-#define MF_FOLD_REDUCE 0  // 1: the last split of a tile reduces it (no k_schur_reduce launch); 0: separate reduce.
-                          // Measured (r03h): 258 us vs 69 us per build -- every split's agent-scope release
-                          // (needed before its counter add) writes back its XCD's L2; kept for A/B only
-#endif
 
 __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
   constexpr int SNB = 16;                // landmarks per batch
@@ -642,16 +637,12 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
     if (t < SF * 12) {
       double v = 0;
       for (int j0 = 0; j0 < 512 / SF; ++j0) v += red[j0 * SF * 12 + t];
-      if (a.fold == 2 && a.tile_cnt)
-        __hip_atomic_store(a.part_diag + (int64_t)item * SF * 12 + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else
-        a.part_diag[(int64_t)item * SF * 12 + t] = v;
+      a.part_diag[(int64_t)item * SF * 12 + t] = v;
     }
   }
 #endif
-  // partial blocks of this split: part[item][f1 local][3q + r][f2], as k_schur writes them (fold == 2: write-through)
+  // partial blocks of this split: part[item][f1 local][3q + r][f2], as k_schur writes them
   float* out = (float*)a.part + (int64_t)item * (SF * 9 * WAVE);
-  const bool wt = a.fold == 2 && a.tile_cnt;
 #pragma unroll
   for (int x = 0; x < 3; ++x)
 #pragma unroll
@@ -660,41 +651,8 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
       for (int v = 0; v < 4; ++v) {
         const int row = 16 * (3 * rg + x) + (lane >> 4) * 4 + v, col = 16 * (3 * cg + y) + fr;
         const int q = row / SF, i = row % SF, r = col / WAVE, f2 = col % WAVE;
-        float* dst = out + (i * 9 + 3 * q + r) * WAVE + f2;
-        if (wt) __hip_atomic_store(dst, (float)acc[x][y][v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else *dst = (float)acc[x][y][v];
+        out[(i * 9 + 3 * q + r) * WAVE + f2] = (float)acc[x][y][v];
       }
-  if (a.fold && a.tile_cnt) {  // folded reduce: the tile's last split sums all splits in item order (schur_reduce_elem)
-    __shared__ int s_grp;
-    if (wt) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores have landed
-    __syncthreads();
-    if (t == 0) {
-      const int gi = a.item_group[item];
-      const int4 gg = a.groups[gi];
-      const unsigned done = wt ? __hip_atomic_fetch_add(a.tile_cnt + gi, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                               : __hip_atomic_fetch_add(a.tile_cnt + gi, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      s_grp = (done == (unsigned)(gg.w - gg.z - 1)) ? gi : -1;
-    }
-    __syncthreads();
-    const int gi = s_grp;
-    if (gi >= 0) {
-      const int4 gg = a.groups[gi];
-      if (wt) {
-        // every partial of the tile was stored sc1 and drained before its split's counter add: sc1 loads see them
-#pragma unroll 4
-        for (int e = t; e < SF * 9 * WAVE; e += 512) schur_reduce_elem<float, true>(a, gg, e);
-        if (gg.y == 0 && t < SF * 3) schur_reduce_vec<true>(a, gg, t);
-      } else {
-        // every thread acquires (agent scope: the other splits' partials were released by their counter adds),
-        // then reads them with ordinary cached loads, several elements in flight per thread
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#pragma unroll 4
-        for (int e = t; e < SF * 9 * WAVE; e += 512) schur_reduce_elem<float, false>(a, gg, e);
-        if (gg.y == 0 && t < SF * 3) schur_reduce_vec<false>(a, gg, t);
-      }
-      if (t == 0) __hip_atomic_store(a.tile_cnt + gi, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-    }
-  }
   SK_T(10);
 #ifdef SK_TIMING
   __syncthreads();
@@ -702,217 +660,6 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
 #endif
 }
 
-// K2 on the matrix cores over chunk PAIRS (fp32 path, PTZBA_SCHUR=mf2): a work item covers the partner chunks
-// 2cp and 2cp + 1 of its F1 block (128 partner frames, the union of the two chunks' landmark lists), so the
-// item's landmark list, Y = -W V~^-1 of its F1 frames and the chunk-0 diagonal terms are staged once for both
-// chunks, and half as many items fill the chip in one round.  Wave w owns the same 3 x 3 output blocks as in
-// k_schur_mf in each of the two chunks (18 accumulators of 16 x 16); the MFMA accumulators run in fp32 over the
-// whole item (<= SCHUR_PLMAX landmarks, 16 batches; k_schur_mf flushes to fp64 every 4 batches -- the fp64
-// registers do not fit beside the second chunk's accumulators) and are written as the item's two fp32 split
-// partials (partial h * n_items + item for chunk 2cp + h), reduced by k_schur_reduce in fixed order.
-__global__ __launch_bounds__(512) void k_schur_mf2(SchurArgs a) {
-  constexpr int SNB = 16;                    // landmarks per batch
-  constexpr int NSL = SNB * 2 * WAVE / 512;  // W slots staged per thread per batch (two chunks)
-  __shared__ __attribute__((aligned(16))) _Float16 sY[2][2][3 * SF][MKP];           // [buf][hi|lo][q*32 + f1][2j + d]
-  __shared__ __attribute__((aligned(16))) _Float16 sWt[2][2][2][3 * WAVE][MKP];     // [buf][hi|lo][chunk][r*64 + f2][2j + d]
-  __shared__ int4 sL[SCHUR_PLMAX];
-  __shared__ float sG[SCHUR_PLMAX];
-  if (a.skip_if && *a.skip_if) return;
-  const int item = xcd_swizzle(blockIdx.x, gridDim.x);
-  const int4 it = a.items[item];
-  const int f1b = it.x, cp = it.y & 0xffff, cmask = it.y >> 16, lb = it.z, nl = it.w - it.z;
-  const bool have0 = cmask & 1, have1 = (cmask >> 1) & 1;  // chunks 2cp / 2cp + 1 have a tile
-  const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
-  const int f2base = f1b + 2 * WAVE * cp;
-  const bool alt = a.sel && *a.sel;
-  const float* __restrict__ w_slot = (const float*)(alt ? a.w_slot1 : a.w_slot);
-  for (int k = t; k < nl; k += 512) {
-    const int4 m = a.item_lm[lb + k];
-    sL[k] = m;
-    const double* vi = a.lm_aux + (int64_t)m.x * 8;
-    int e = 0;
-    (void)frexp(vi[0] + vi[2], &e);
-    sG[k] = ldexpf(1.f, e / 2);
-  }
-  __syncthreads();
-  // prefetched operands of one batch (two sets in flight); the per-slot scale and in-range mask are re-derived
-  // from the LDS list when staging (registers: the second chunk's accumulators leave no room for them)
-  struct Pre {
-    float rw[NSL][6], ryw[6], ryg, rvi[3];
-    bool ryin;
-  };
-  const int yj = t / SF, yi = t & (SF - 1);
-  auto fetch = [&](Pre& P, int p) {  // landmarks [p, p + SNB) of the list (clamped, branch-free)
-#pragma unroll
-    for (int q = 0; q < NSL; ++q) {
-      const int e = t + 512 * q, j = e >> 7, ln = e & 127;
-      const int4 m = sL[min(p + j, nl - 1)];
-      const int idx = f2base + ln - m.y;
-      load_w6(P.rw[q], w_slot + (int64_t)(m.w + min(max(idx, 0), m.z - m.y)) * 8);
-    }
-    const int f = f1b + yi, jj = min(p + yj, nl - 1);
-    const int4 m = sL[jj];
-    P.ryin = (p + yj < nl) && f >= m.y && f <= m.z;
-    P.ryg = sG[jj];
-    load_w6(P.ryw, w_slot + (int64_t)(m.w + min(max(f - m.y, 0), m.z - m.y)) * 8);
-    const double* vi = a.lm_aux + (int64_t)m.x * 8;
-    P.rvi[0] = (float)vi[0]; P.rvi[1] = (float)vi[1]; P.rvi[2] = (float)vi[2];
-  };
-  auto stage = [&](const Pre& P, int buf, int p) {  // P holds landmarks [p, p + SNB)
-#pragma unroll
-    for (int q = 0; q < NSL; ++q) {
-      const int e = t + 512 * q, j = e >> 7, ln = e & 127, hc = ln >> 6, lnn = ln & 63;
-      const int jj = min(p + j, nl - 1);
-      const int4 m = sL[jj];
-      const int idx = f2base + ln - m.y;
-      const bool win = (p + j < nl) && idx >= 0 && f2base + ln <= m.z;
-      const float gq = win ? sG[jj] : 0.f;
-#pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        hp2v h, l;
-        split_pk(P.rw[q][2 * r] * gq, P.rw[q][2 * r + 1] * gq, h, l);
-        *reinterpret_cast<hp2v*>(&sWt[buf][0][hc][r * WAVE + lnn][2 * j]) = h;
-        *reinterpret_cast<hp2v*>(&sWt[buf][1][hc][r * WAVE + lnn][2 * j]) = l;
-      }
-    }
-    const float gi = P.ryin ? 1.f / P.ryg : 0.f;
-    const float v0 = P.rvi[0] * gi, v1 = P.rvi[1] * gi, v2 = P.rvi[2] * gi;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const float W0 = P.ryw[2 * q], W1 = P.ryw[2 * q + 1];
-      hp2v h, l;
-      split_pk(-fmaf(W0, v0, W1 * v1), -fmaf(W0, v1, W1 * v2), h, l);
-      *reinterpret_cast<hp2v*>(&sY[buf][0][q * SF + yi][2 * yj]) = h;
-      *reinterpret_cast<hp2v*>(&sY[buf][1][q * SF + yi][2 * yj]) = l;
-    }
-  };
-  const int rg = wv >> 2, cg = wv & 3;
-  const int fr = lane & 15, fk = (lane >> 4) * 8;
-  f4v c[2][3][3];
-#pragma unroll
-  for (int hc = 0; hc < 2; ++hc)
-#pragma unroll
-    for (int x = 0; x < 3; ++x)
-#pragma unroll
-      for (int y = 0; y < 3; ++y) c[hc][x][y] = f4v{0.f, 0.f, 0.f, 0.f};
-  auto compute_half = [&](int buf, int hc) {
-    h8v bh[3], bl[3];
-#pragma unroll
-    for (int y = 0; y < 3; ++y) {
-      const int col = 16 * (3 * cg + y) + fr;
-      bh[y] = *reinterpret_cast<const h8v*>(&sWt[buf][0][hc][col][fk]);
-      bl[y] = *reinterpret_cast<const h8v*>(&sWt[buf][1][hc][col][fk]);
-    }
-#pragma unroll
-    for (int x = 0; x < 3; ++x) {
-      const int row = 16 * (3 * rg + x) + fr;
-      const h8v ah = *reinterpret_cast<const h8v*>(&sY[buf][0][row][fk]);
-      const h8v al = *reinterpret_cast<const h8v*>(&sY[buf][1][row][fk]);
-#pragma unroll
-      for (int y = 0; y < 3; ++y) {
-        c[hc][x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[y], c[hc][x][y], 0, 0, 0);
-        c[hc][x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[y], c[hc][x][y], 0, 0, 0);
-        c[hc][x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[y], c[hc][x][y], 0, 0, 0);
-      }
-    }
-  };
-  auto compute = [&](int buf) {
-    if (have0) compute_half(buf, 0);
-    if (have1) compute_half(buf, 1);
-  };
-  // chunk-0 diagonal terms, as in k_schur_mf (pair 0 holds chunk 0)
-  const bool diag = cp == 0;
-  const float* __restrict__ ug_slot = (const float*)(alt ? a.ug_slot1 : a.ug_slot);
-  float du[9], dvg[2];
-  float dacc[12];
-#pragma unroll
-  for (int k = 0; k < 12; ++k) dacc[k] = 0.f;
-  auto dfetch = [&](int p) {
-    const int4 m = sL[min(p + yj, nl - 1)];
-    const int64_t slot = m.w + min(max(f1b + yi - m.y, 0), m.z - m.y);
-    const float4 u0 = reinterpret_cast<const float4*>(ug_slot + slot * 12)[0];
-    const float4 u1 = reinterpret_cast<const float4*>(ug_slot + slot * 12)[1];
-    du[0] = u0.x; du[1] = u0.y; du[2] = u0.z; du[3] = u0.w;
-    du[4] = u1.x; du[5] = u1.y; du[6] = u1.z; du[7] = u1.w;
-    du[8] = ug_slot[slot * 12 + 8];
-    const double* vi = a.lm_aux + (int64_t)m.x * 8;
-    dvg[0] = (float)vi[3];
-    dvg[1] = (float)vi[4];
-  };
-  auto daccum = [&](const Pre& P) {
-    if (P.ryin) {
-#pragma unroll
-      for (int k = 0; k < 9; ++k) dacc[k] += du[k];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) dacc[9 + q] += fmaf(P.ryw[2 * q], dvg[0], P.ryw[2 * q + 1] * dvg[1]);
-    }
-  };
-  Pre A, B;
-  if (nl > 0) {
-    if (diag) dfetch(0);
-    fetch(A, 0);
-    fetch(B, SNB);
-    stage(A, 0, 0);
-    if (diag) daccum(A);
-  }
-  __syncthreads();
-  for (int p = 0; p < nl; p += 2 * SNB) {
-    if (diag && p + SNB < nl) dfetch(p + SNB);
-    fetch(A, p + 2 * SNB);
-    compute(0);
-    if (p + SNB < nl) {
-      stage(B, 1, p + SNB);
-      if (diag) daccum(B);
-    }
-    __syncthreads();
-    if (p + SNB >= nl) break;
-    if (diag && p + 2 * SNB < nl) dfetch(p + 2 * SNB);
-    fetch(B, p + 3 * SNB);
-    compute(1);
-    if (p + 2 * SNB < nl) {
-      stage(A, 0, p + 2 * SNB);
-      if (diag) daccum(A);
-    }
-    __syncthreads();
-  }
-  if (diag) {  // fixed-order reduction over the 16 landmark lanes of each frame
-    double* red = reinterpret_cast<double*>(&sWt[0][0][0][0][0]);  // free after the last batch's barrier
-#pragma unroll
-    for (int k = 0; k < 12; ++k) red[(yj * SF + yi) * 12 + k] = (double)dacc[k];
-    __syncthreads();
-    if (t < SF * 12) {
-      double v = 0;
-      for (int j0 = 0; j0 < 512 / SF; ++j0) v += red[j0 * SF * 12 + t];
-      a.part_diag[(int64_t)item * SF * 12 + t] = v;
-    }
-  }
-#pragma unroll
-  for (int hc = 0; hc < 2; ++hc) {
-    if (!(hc ? have1 : have0)) continue;
-    float* out = (float*)a.part + ((int64_t)hc * gridDim.x + item) * (SF * 9 * WAVE);
-#pragma unroll
-    for (int x = 0; x < 3; ++x)
-#pragma unroll
-      for (int y = 0; y < 3; ++y)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int row = 16 * (3 * rg + x) + (lane >> 4) * 4 + v, col = 16 * (3 * cg + y) + fr;
-          const int q = row / SF, i = row % SF, r = col / WAVE, f2 = col % WAVE;
-          out[(i * 9 + 3 * q + r) * WAVE + f2] = c[hc][x][y][v];
-        }
-  }
-}
-
-// PTZBA_SCHUR selects the fp32 K2: valu (the VALU kernel), mf (matrix cores, one chunk per item), mf2 (matrix
-// cores, chunk pairs); A/B measurements.  Read at each set_problem / build (a test switches it per handle).
-static int schur_mode() {
-  const char* e = getenv("PTZBA_SCHUR");
-  if (!e) return 1;
-  const std::string v = e;
-  return v == "valu" ? 0 : (v == "mf2" ? 2 : 1);
-}
-static bool schur_use_mfma() { return schur_mode() >= 1; }
-bool schur_pair_mode() { return schur_mode() == 2; }
 
 #ifdef SK_TIMING
 extern "C" int ptzba_debug_sk(long long* out) {
@@ -923,10 +670,10 @@ extern "C" int ptzba_debug_sk_items(long long* out) {
 }
 #endif
 
-// The matrix-core K2 reduces each tile in its LAST split (k_schur_mf, "folded reduce"): the split that
-// finishes last (agent-scope counter per tile, acq_rel) sums every split's partial in item order, exactly as
-// k_schur_reduce does (bitwise the same S), so the separate reduce launch and its boundary go away.  Partials
-// of other workgroups are read with agent-scope loads.
+// split-partial loads of the tile reduction (AGENT: agent-scope loads; the reduce launch uses plain ones).  Round 3-4
+// also reduced each tile in its LAST split (k_schur_mf "folded reduce", counters per tile): 258 us per build with an
+// acq_rel counter, not faster with write-through partials; removed in round 5 with the chunk-pair k_schur_mf2 (103 vs
+// 70 us per build, r03ab).
 template <typename real, bool AGENT>
 __device__ __forceinline__ real part_load(const real* p) {
   if constexpr (AGENT) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1063,18 +810,12 @@ template <typename real>
 void launch_schur(const SchurArgs& a, int n_items, int n_groups, int n_fixed, hipStream_t st) {
   const int n_free = a.n_pose - n_fixed;
   if (n_free <= 0) return;
-  bool folded = false;
+  // fp32: the matrix cores (k_schur_mf, fp16 hi/lo splits); fp64: the VALU kernel
   if (n_items > 0) {
-    if (sizeof(real) == 4 && a.pair) {
-      hipLaunchKernelGGL(k_schur_mf2, dim3(n_items), dim3(512), 0, st, a);
-    } else if (sizeof(real) == 4 && schur_use_mfma()) {
-      hipLaunchKernelGGL(k_schur_mf, dim3(n_items), dim3(512), 0, st, a);
-      folded = a.fold && a.item_group && a.tile_cnt;
-    } else {
-      hipLaunchKernelGGL(k_schur<real>, dim3(n_items), dim3(512), 0, st, a);
-    }
+    if (sizeof(real) == 4) hipLaunchKernelGGL(k_schur_mf, dim3(n_items), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL(k_schur<real>, dim3(n_items), dim3(512), 0, st, a);
   }
-  if (n_groups > 0 && !folded)
+  if (n_groups > 0)
     hipLaunchKernelGGL(k_schur_reduce<real>, dim3(SF * 9 * WAVE / (sizeof(real) == 4 && SR_VEC ? 1024 : 256), n_groups),
                        dim3(256), 0, st, a);
 }

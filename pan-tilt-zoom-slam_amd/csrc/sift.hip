@@ -98,69 +98,12 @@ __global__ __launch_bounds__(BLUR_TX) void k_sift_blur_rows(int w, int h, const 
   dst[(int64_t)y * w + x] = acc;
 }
 
-// Row pass over BLUR_RB rows per workgroup (round 4): the rows' segments are requested together, so a workgroup has
-// BLUR_RB times the bytes in flight of k_sift_blur_rows (whose one-row workgroups wait out one load latency each);
-// per output the same products in the same order: bit-identical.  Opt-in (PTZ_SIFT_ROWS4=1): 10.5 vs 9.5 us per
-// launch on average, 1.86 vs 1.81 ms per 1080p detection (r04z8) -- the one-row form was not latency-bound.
-constexpr int BLUR_RB = 4;
-__global__ __launch_bounds__(BLUR_TX) void k_sift_blur_rows4(int w, int h, const float* __restrict__ src,
-                                                              float* __restrict__ dst, const float* __restrict__ wt, int K) {
-  __shared__ float tile[BLUR_RB][BLUR_TX + 2 * BLUR_RMAX];
-  __shared__ float sw[2 * BLUR_RMAX + 1];
-  const int x0 = blockIdx.x * BLUR_TX, y0 = blockIdx.y * BLUR_RB, r = K / 2, t = threadIdx.x;
-#pragma unroll
-  for (int q = 0; q < BLUR_RB; ++q) {
-    const int y = min(y0 + q, h - 1);  // (rows past the image: a valid row, never stored)
-    const float* row = src + (int64_t)y * w;
-    for (int i = t; i < BLUR_TX + 2 * r; i += BLUR_TX) tile[q][i] = row[refl101(x0 + i - r, w)];
-  }
-  if (t < K) sw[t] = wt[t];
-  __syncthreads();
-  const int x = x0 + t;
-  if (x >= w) return;
-#pragma unroll
-  for (int q = 0; q < BLUR_RB; ++q) {
-    if (y0 + q >= h) break;
-    float acc = 0.f;
-    for (int k = 0; k < K; ++k) acc = acc + sw[k] * tile[q][t + k];
-    dst[(int64_t)(y0 + q) * w + x] = acc;
-  }
-}
-
-__global__ __launch_bounds__(256) void k_sift_blur_cols(int w, int h, const float* __restrict__ src,
-                                                         float* __restrict__ dst, const float* __restrict__ wt, int K) {
-  __shared__ float tile[BLUR_CR + 2 * BLUR_RMAX][BLUR_CT + 1];
-  __shared__ float sw[2 * BLUR_RMAX + 1];
-  const int tx = threadIdx.x & (BLUR_CT - 1), ty = threadIdx.x / BLUR_CT;  // 64 x 4
-  const int x0 = blockIdx.x * BLUR_CT, y0 = blockIdx.y * BLUR_CR, r = K / 2;
-  const int x = x0 + tx;
-  const int nrow = BLUR_CR + 2 * r;
-  for (int i = ty; i < nrow; i += 256 / BLUR_CT)
-    tile[i][tx] = x < w ? src[(int64_t)refl101(y0 + i - r, h) * w + x] : 0.f;
-  if (threadIdx.x < K) sw[threadIdx.x] = wt[threadIdx.x];
-  __syncthreads();
-  if (x >= w) return;
-  // four independent accumulation chains per thread (rows yb, yb + 4, yb + 8, yb + 12)
-  for (int yb = ty; yb < BLUR_CR; yb += 16) {
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    for (int k = 0; k < K; ++k) {
-      const float wk = sw[k];
-      a0 = a0 + wk * tile[yb + k][tx];
-      a1 = a1 + wk * tile[yb + 4 + k][tx];
-      a2 = a2 + wk * tile[yb + 8 + k][tx];
-      a3 = a3 + wk * tile[yb + 12 + k][tx];
-    }
-    const float a[4] = {a0, a1, a2, a3};
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (y0 + yb + 4 * q < h) dst[(int64_t)(y0 + yb + 4 * q) * w + x] = a[q];
-  }
-}
-
 // Column pass with a sliding window (round 4): thread (tx, ty) produces the 16 consecutive output rows 16 ty .. 16 ty + 15
 // of its column, keeping the 16 inputs the current tap needs in registers -- one LDS read per 16 products instead of
-// one per product.  Per output the same products in the same order (mul, then add; k ascending): bit-identical to
-// k_sift_blur_cols (the default since r04t; PTZ_SIFT_COLS_SW=0 restores k_sift_blur_cols, A/B).
+// one per product (1.816 -> 1.776 ms per 1080p detection against one output per thread, r04t).  Per output the same
+// products in the same order (mul, then add; k ascending) as the oracle's sift_blur: bit-identical.
+// Measured slower and removed in round 5: a sliding-window row pass (2.00 vs 1.81 ms, r04v), a row pass over 4 rows
+// per workgroup (1.86 vs 1.81 ms, r04z8), both passes + the DoG in one launch (2.29 vs 2.23 ms, r04i).
 __global__ __launch_bounds__(256) void k_sift_blur_cols_sw(int w, int h, const float* __restrict__ src,
                                                             float* __restrict__ dst, const float* __restrict__ wt, int K) {
   __shared__ float tile[BLUR_CR + 2 * BLUR_RMAX][BLUR_CT + 1];
@@ -194,104 +137,6 @@ __global__ __launch_bounds__(256) void k_sift_blur_cols_sw(int w, int h, const f
 #pragma unroll
   for (int j = 0; j < R; ++j)
     if (y0 + ra + j < h) dst[(int64_t)(y0 + ra + j) * w + x] = acc[j];
-}
-
-// Row pass with a sliding window (round 4): a workgroup blurs a 64-row x 64-column block; lane = row (an odd LDS
-// pitch keeps the 64 rows of a read in distinct banks), wave w = the 16 outputs 16 w .. 16 w + 15 of every row, kept
-// with the 16 inputs the current tap needs in registers (one LDS read per 16 products); the results go back through
-// LDS so the global stores are row-contiguous.  Per output the same products in the same order (mul, then add; k
-// ascending): bit-identical to k_sift_blur_rows.  PTZ_SIFT_ROWS_SW=0 restores k_sift_blur_rows (A/B).
-constexpr int BRS_R = 64, BRS_C = 64, BRS_LD = BRS_C + 2 * BLUR_RMAX + 1;
-__global__ __launch_bounds__(256) void k_sift_blur_rows_sw(int w, int h, const float* __restrict__ src,
-                                                            float* __restrict__ dst, const float* __restrict__ wt, int K) {
-  __shared__ float tile[BRS_R][BRS_LD];
-  __shared__ float sw[2 * BLUR_RMAX + 1];
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int x0 = blockIdx.x * BRS_C, y0 = blockIdx.y * BRS_R, r = K / 2;
-  const int ncol = BRS_C + 2 * r;
-  for (int e = t; e < BRS_R * ncol; e += 256) {
-    const int i = e / ncol, c = e - i * ncol, y = min(y0 + i, h - 1);
-    tile[i][c] = src[(int64_t)y * w + refl101(x0 + c - r, w)];
-  }
-  if (t < K) sw[t] = wt[t];
-  __syncthreads();
-  constexpr int R = 16;
-  const int cb = R * wv;
-  float acc[R], win[R];
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    acc[j] = 0.f;
-    win[j] = tile[lane][cb + j];
-  }
-  for (int k = 0; k < K; ++k) {
-    const float wk = sw[k];
-#pragma unroll
-    for (int j = 0; j < R; ++j) acc[j] = acc[j] + wk * win[j];
-    if (k + 1 == K) break;
-#pragma unroll
-    for (int j = 0; j + 1 < R; ++j) win[j] = win[j + 1];
-    win[R - 1] = tile[lane][cb + R + k];  // column cb + R + k <= BRS_C - 1 + K - 1: inside the staged columns
-  }
-  __syncthreads();  // (every window read is done: the tile's first 64 columns take the results)
-#pragma unroll
-  for (int j = 0; j < R; ++j) tile[lane][cb + j] = acc[j];
-  __syncthreads();
-  for (int e = t; e < BRS_R * BRS_C; e += 256) {
-    const int i = e >> 6, c = e & 63, y = y0 + i, x = x0 + c;
-    if (y < h && x < w) dst[(int64_t)y * w + x] = tile[i][c];
-  }
-}
-
-// Both passes in one launch (round 4): a 64 x 64 output tile stages its input (+ halo, reflected at the borders) in
-// LDS once, blurs the 64 + 2r rows it needs along x into LDS, then along y, and -- when `prev` is given -- writes
-// the DoG level dst - prev beside it (prev = the octave's previous Gaussian level, the same pixel).  Per output
-// pixel the same products in the same order as k_sift_blur_rows + k_sift_blur_cols (+ k_sift_dog): bit-identical,
-// with the intermediate image, the second launch and the DoG pass's two reads gone.
-constexpr int BLUR2_T = 64;
-__global__ __launch_bounds__(256) void k_sift_blur2(int w, int h, const float* __restrict__ src, float* __restrict__ dst,
-                                                     const float* __restrict__ wt, int K, const float* __restrict__ prev,
-                                                     float* __restrict__ dog) {
-  extern __shared__ float smem[];
-  __shared__ float sw[2 * BLUR_RMAX + 1];
-  const int r = K / 2, n = BLUR2_T + 2 * r;  // staged rows / columns
-  float* in = smem;                          // [n][n]
-  float* rt = smem + n * n;                  // [n][BLUR2_T + 1]
-  const int x0 = blockIdx.x * BLUR2_T, y0 = blockIdx.y * BLUR2_T, t = threadIdx.x;
-  for (int e = t; e < n * n; e += 256) {
-    const int i = e / n, j = e - i * n;
-    in[e] = src[(int64_t)refl101(y0 + i - r, h) * w + refl101(x0 + j - r, w)];
-  }
-  if (t < K) sw[t] = wt[t];
-  __syncthreads();
-  const int tx = t & (BLUR2_T - 1), ty = t / BLUR2_T;  // 64 x 4
-  for (int i = ty; i < n; i += 4) {
-    float acc = 0.f;
-    for (int k = 0; k < K; ++k) acc = acc + sw[k] * in[i * n + tx + k];
-    rt[i * (BLUR2_T + 1) + tx] = acc;
-  }
-  __syncthreads();
-  const int x = x0 + tx;
-  if (x >= w) return;
-  for (int yb = ty; yb < BLUR2_T; yb += 16) {
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    for (int k = 0; k < K; ++k) {
-      const float wk = sw[k];
-      a0 = a0 + wk * rt[(yb + k) * (BLUR2_T + 1) + tx];
-      a1 = a1 + wk * rt[(yb + 4 + k) * (BLUR2_T + 1) + tx];
-      a2 = a2 + wk * rt[(yb + 8 + k) * (BLUR2_T + 1) + tx];
-      a3 = a3 + wk * rt[(yb + 12 + k) * (BLUR2_T + 1) + tx];
-    }
-    const float a[4] = {a0, a1, a2, a3};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int y = y0 + yb + 4 * q;
-      if (y < h) {
-        const int64_t p = (int64_t)y * w + x;
-        dst[p] = a[q];
-        if (prev) dog[p] = a[q] - prev[p];
-      }
-    }
-  }
 }
 
 __global__ void k_sift_down(int sw, const float* __restrict__ src, int dw, int dh, float* __restrict__ dst) {
@@ -540,7 +385,7 @@ struct SiftWork {
   // belongs to it, so a call on the same image (a stream detects each frame with 500 features, then the same frame
   // again with 1500 when it becomes a keyframe) re-selects and computes descriptors only
   std::vector<uint8_t> last_img;
-  int32_t last_w = 0, last_h = 0, last_variant = -1;  // (variant: the blur A/B knobs the pyramid was built with)
+  int32_t last_w = 0, last_h = 0;
   std::vector<ptzba::SiftKp> last_kps;
   bool last_valid = false;
   // the blur kernels, octave sizes and level pointers uploaded for (width, height, pyramid buffer): constant per
@@ -575,15 +420,6 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
   if (width < 8 || height < 8 || !img || !n_out) return fail("bad image");
   if (max_kp < 0 || (max_kp > 0 && (!kp_out || !des_out))) return fail("bad output buffers");
   if (select_device(device)) return -1;
-  // PTZ_SIFT_TIMING=1: host-side phase times of this call on stderr (where a 1080p detection spends its ~2 ms)
-  static const bool st_on = getenv("PTZ_SIFT_TIMING") != nullptr;
-  auto st_t0 = std::chrono::steady_clock::now();
-  auto st_mark = [&](const char* what) {
-    if (!st_on) return;
-    const auto t = std::chrono::steady_clock::now();
-    fprintf(stderr, "sift %-18s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - st_t0).count());
-    st_t0 = t;
-  };
   const int W0 = 2 * width, H0 = 2 * height;
   const int n_oct = (int)std::nearbyint(std::log2((double)std::min(W0, H0)) - 2);
   if (n_oct < 1) return fail("image too small");
@@ -619,21 +455,13 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
       dcnt.reserve(16) || dkp.reserve(CAP * sizeof(SiftKp)) || dptr.reserve(n_oct * (SIFT_S + 3) * sizeof(float*)) ||
       dow.reserve(n_oct * 4) || doh.reserve(n_oct * 4))
     return -1;
-  // PTZ_SIFT_REUSE=0: always rebuild the pyramid (A/B knob, read per call)
+  // PTZ_SIFT_REUSE=0: always rebuild the pyramid (read per call; the reuse test compares both)
   const char* rue = getenv("PTZ_SIFT_REUSE");
   const bool reuse = !(rue && atoi(rue) == 0);
   const size_t img_bytes = (size_t)width * height;
-  auto knob = [](const char* name) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : -1;
-  };
-  const int variant = ((knob("PTZ_SIFT_ROWS4") & 3) << 6) | ((knob("PTZ_SIFT_BLUR2") & 3) << 4) |
-                      ((knob("PTZ_SIFT_COLS_SW") & 3) << 2) | (knob("PTZ_SIFT_ROWS_SW") & 3);
   std::vector<SiftKp> kps;
-  if (reuse && Wk.last_valid && Wk.last_w == width && Wk.last_h == height && Wk.last_variant == variant &&
-      std::memcmp(Wk.last_img.data(), img, img_bytes) == 0) {
+  if (reuse && Wk.last_valid && Wk.last_w == width && Wk.last_h == height && std::memcmp(Wk.last_img.data(), img, img_bytes) == 0) {
     kps = Wk.last_kps;  // the same image as the last call: its pyramid and keypoints are still on hand
-    st_mark("reuse");
   } else {
     Wk.last_valid = false;
     if (Wk.pin_cap < img_bytes) {
@@ -666,54 +494,17 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
       std::copy(tabs, tabs + 5, Wk.tab_p);
     }
     HIPCHK(hipMemsetAsync(dcnt.p, 0, 16, nullptr));
-    st_mark("setup+upload");
-    // PTZ_SIFT_BLUR2=1: both blur passes and the DoG in one launch (A/B knob, read per call; measured 2.29 vs 2.23 ms
-    // per 1080p frame against the two-pass form, tools/sift_bench.py r04i -- the LDS-staged passes were not bound by
-    // the intermediate image's traffic)
-    const char* b2e = getenv("PTZ_SIFT_BLUR2");
-    const bool blur2 = b2e && atoi(b2e) == 1;
-    // sliding-window column pass, the default (PTZ_SIFT_COLS_SW=0: one output per thread; A/B knob, read per call):
-    // 1.816 -> 1.776 ms per 1080p detection (r04t), bit-identical
-    const char* cse = getenv("PTZ_SIFT_COLS_SW");
-    const bool cols_sw = !(cse && atoi(cse) == 0);
-    const char* rse = getenv("PTZ_SIFT_ROWS_SW");  // sliding-window row pass (A/B knob, read per call)
-    const bool rows_sw = rse && atoi(rse) == 1;
-    // row pass over 4 rows per workgroup (PTZ_SIFT_ROWS4=1, A/B knob, read per call): measured slower, 0.481 vs
-    // 0.436 ms of row passes per 1080p detection (r04z8)
-    const char* r4e = getenv("PTZ_SIFT_ROWS4");
-    const bool rows4 = r4e && atoi(r4e) == 1;
-    // dog_out: the DoG level dst - src written beside dst (fused form only)
-    auto blur = [&](int w, int h, const float* src, float* dst, int ki, float* dog_out) {
-      const int K = (int)kern[ki].size(), rr = K / 2;
-      const int n2 = BLUR2_T + 2 * rr;
-      const size_t lds = ((size_t)n2 * n2 + (size_t)n2 * (BLUR2_T + 1)) * sizeof(float);
-      if (blur2 && lds <= 64 * 1024) {  // (radius <= 14: every blur of OpenCV's default SIFT)
-        hipLaunchKernelGGL(k_sift_blur2, dim3((unsigned)((w + BLUR2_T - 1) / BLUR2_T), (unsigned)((h + BLUR2_T - 1) / BLUR2_T)),
-                           dim3(256), lds, nullptr, w, h, src, dst, dk.as<float>() + ki * kmax, K,
-                           dog_out ? src : nullptr, dog_out);
-        return true;
-      }
-      if (rows4 && !rows_sw)
-        hipLaunchKernelGGL(k_sift_blur_rows4, dim3((unsigned)((w + BLUR_TX - 1) / BLUR_TX), (unsigned)((h + BLUR_RB - 1) / BLUR_RB)),
-                           dim3(BLUR_TX), 0, nullptr, w, h, src, T, dk.as<float>() + ki * kmax, K);
-      else if (rows_sw)
-        hipLaunchKernelGGL(k_sift_blur_rows_sw, dim3((unsigned)((w + BRS_C - 1) / BRS_C), (unsigned)((h + BRS_R - 1) / BRS_R)),
-                           dim3(256), 0, nullptr, w, h, src, T, dk.as<float>() + ki * kmax, K);
-      else
-        hipLaunchKernelGGL(k_sift_blur_rows, dim3((unsigned)((w + BLUR_TX - 1) / BLUR_TX), (unsigned)h), dim3(BLUR_TX), 0,
-                           nullptr, w, h, src, T, dk.as<float>() + ki * kmax, K);
-      if (cols_sw)
-        hipLaunchKernelGGL(k_sift_blur_cols_sw, dim3((unsigned)((w + BLUR_CT - 1) / BLUR_CT), (unsigned)((h + BLUR_CR - 1) / BLUR_CR)),
-                           dim3(256), 0, nullptr, w, h, T, dst, dk.as<float>() + ki * kmax, K);
-      else
-        hipLaunchKernelGGL(k_sift_blur_cols, dim3((unsigned)((w + BLUR_CT - 1) / BLUR_CT), (unsigned)((h + BLUR_CR - 1) / BLUR_CR)),
-                           dim3(256), 0, nullptr, w, h, T, dst, dk.as<float>() + ki * kmax, K);
-      return false;
+    auto blur = [&](int w, int h, const float* src, float* dst, int ki) {
+      const int K = (int)kern[ki].size();
+      hipLaunchKernelGGL(k_sift_blur_rows, dim3((unsigned)((w + BLUR_TX - 1) / BLUR_TX), (unsigned)h), dim3(BLUR_TX), 0,
+                         nullptr, w, h, src, T, dk.as<float>() + ki * kmax, K);
+      hipLaunchKernelGGL(k_sift_blur_cols_sw, dim3((unsigned)((w + BLUR_CT - 1) / BLUR_CT), (unsigned)((h + BLUR_CR - 1) / BLUR_CR)),
+                         dim3(256), 0, nullptr, w, h, T, dst, dk.as<float>() + ki * kmax, K);
     };
     // base: doubled image, then the blur from the assumed input blur to sigma
     hipLaunchKernelGGL(k_sift_up, dim3((unsigned)((W0 + 127) / 128), (unsigned)H0), dim3(128), 0, nullptr, width, height,
                        dimg.as<uint8_t>(), gptr[1]);
-    blur(W0, H0, gptr[1], gptr[0], 0, nullptr);
+    blur(W0, H0, gptr[1], gptr[0], 0);
     const float thr = (float)std::floor(0.5 * SIFT_CONTR / SIFT_S * 255);
     for (int o = 0; o < n_oct; ++o) {
       const int w = ow[o], h = oh[o];
@@ -721,22 +512,16 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
         hipLaunchKernelGGL(k_sift_down, dim3((unsigned)((w + 127) / 128), (unsigned)h), dim3(128), 0, nullptr, ow[o - 1],
                            gptr[(o - 1) * (SIFT_S + 3) + SIFT_S], w, h, gptr[o * (SIFT_S + 3)]);
       const int64_t np = (int64_t)w * h;
-      bool fused_dog = true;
-      for (int i = 1; i < SIFT_S + 3; ++i)
-        fused_dog = blur(w, h, gptr[o * (SIFT_S + 3) + i - 1], gptr[o * (SIFT_S + 3) + i], i,
-                         blur2 ? Dg + doff[o] + (i - 1) * np : nullptr) && fused_dog;
-      if (!blur2 || !fused_dog)
-        hipLaunchKernelGGL(k_sift_dog, dim3((unsigned)((np * (SIFT_S + 2) + 255) / 256)), dim3(256), 0, nullptr, np,
-                           G + goff[o], Dg + doff[o]);
+      for (int i = 1; i < SIFT_S + 3; ++i) blur(w, h, gptr[o * (SIFT_S + 3) + i - 1], gptr[o * (SIFT_S + 3) + i], i);
+      hipLaunchKernelGGL(k_sift_dog, dim3((unsigned)((np * (SIFT_S + 2) + 255) / 256)), dim3(256), 0, nullptr, np,
+                         G + goff[o], Dg + doff[o]);
       if (w > 2 * SIFT_BORDER && h > 2 * SIFT_BORDER)
         hipLaunchKernelGGL(k_sift_extrema, dim3((unsigned)((w - 2 * SIFT_BORDER + 63) / 64), (unsigned)(h - 2 * SIFT_BORDER), SIFT_S),
                            dim3(64), 0, nullptr, o, w, h, Dg + doff[o], thr, dcand.as<SiftCand>(), dcnt.as<int>(), CAP);
     }
     HIPCHK(hipGetLastError());
-    st_mark("pyramid queued");
     int cnt[2];
     HIPCHK(hipMemcpy(cnt, dcnt.p, 8, hipMemcpyDeviceToHost));
-    st_mark("pyramid+extrema");
     if (cnt[0] > CAP) return fail("%d SIFT extrema exceed the candidate list (%d)", cnt[0], CAP);
     const int nc = cnt[0];
     if (nc > 0)
@@ -753,11 +538,9 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
       Wk.last_img.assign(img, img + img_bytes);
       Wk.last_w = width;
       Wk.last_h = height;
-      Wk.last_variant = variant;
       Wk.last_kps = kps;
       Wk.last_valid = true;
     }
-    st_mark("orientation");
   }
   const int nk = (int)kps.size();
   // strongest first (ties: y, x, angle, then detection order -- a total order, so selecting the first n and sorting
@@ -781,7 +564,6 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
     for (int i = 0; i < n; ++i) top[i] = kps[ord[i]];
     kps.swap(top);
   }
-  st_mark("sort");
   *n_out = n;
   n = std::min(n, (int)max_kp);
   if (n <= 0) return 0;
@@ -791,7 +573,6 @@ int ptz_sift(int device, int32_t width, int32_t height, const uint8_t* img, int3
                      (const float* const*)dptr.p, dow.as<int>(), doh.as<int>(), ddes.as<float>());
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(des_out, ddes.p, (size_t)n * 128 * 4, hipMemcpyDeviceToHost));
-  st_mark("descriptors");
   for (int i = 0; i < n; ++i) {
     kp_out[4 * i] = kps[i].x;
     kp_out[4 * i + 1] = kps[i].y;

@@ -116,6 +116,7 @@ def lib():
         "ptzba_solve_reduced": ([V], I),
         "ptzba_step": ([V, D], I),
         "ptzba_set_huber_curvature": ([V, D], I),
+        "ptzba_setup_timing": ([V, I32, V, V, V], I),
         "ptzba_solve": ([V, V, V, POINTER(ptzba_lm_opts), POINTER(ptzba_report)], I),
         "ptzba_solve_resident": ([V, I32, POINTER(ptzba_lm_opts), POINTER(ptzba_report)], I),
         "ptzba_lm_start": ([V], I),
@@ -203,7 +204,7 @@ def lib():
 EXPORTED_SYMBOLS = [
     "ptzba_new", "ptzba_delete", "ptzba_last_error", "ptzba_version", "ptzba_set_stream", "ptzba_use_own_stream", "ptzba_set_problem",
     "ptzba_problem_info", "ptzba_solver_info", "ptzba_residual", "ptzba_set_state", "ptzba_get_state", "ptzba_linearize",
-    "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_set_huber_curvature", "ptzba_solve", "ptzba_solve_resident", "ptzba_read_scalars", "ptzba_accept",
+    "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_set_huber_curvature", "ptzba_setup_timing", "ptzba_solve", "ptzba_solve_resident", "ptzba_read_scalars", "ptzba_accept",
     "ptzba_lm_start", "ptzba_lm_init", "ptzba_lm_build", "ptzba_lm_solve", "ptzba_lm_decide", "ptzba_lm_wait",
     "ptzba_exchange", "ptzba_exchange_packed", "ptzba_pack", "ptzba_unpack", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptzba_save_state", "ptzba_restore_state", "ptz_ray_to_image",
     "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks", "ptzba_coupling_window", "ptz_match_knn2", "ptz_homography_ransac", "ptz_homography_ransac_batch", "ptz_lk_track", "ptz_sift", "ptz_match_hamming",
@@ -327,7 +328,11 @@ def desc_put(key, des, device=None):
 
 def desc_put_new(key, des, device=None):
     """desc_put, returning the number of rows uploaded."""
-    d = np.ascontiguousarray(des, dtype=np.float32).reshape(len(des), -1) if len(des) else np.zeros((0, 1), np.float32)
+    if len(des):
+        d = np.ascontiguousarray(des, dtype=np.float32).reshape(len(des), -1)
+    else:  # an empty set keeps its column count (an empty 2-D array), else 1
+        shp = np.shape(des)
+        d = np.zeros((0, shp[1] if len(shp) == 2 and shp[1] > 0 else 1), np.float32)
     desc_put(key, d, device)
     return len(d)
 
@@ -995,6 +1000,17 @@ class BAHandle:
 
     def linearize(self):
         _check(lib().ptzba_linearize(self.h), "ptzba_linearize")
+
+    def setup_timing(self):
+        """Host phase times (ms) of the last set_problem, {phase: ms} in call order."""
+        cap = 64
+        names = (ctypes.c_char_p * cap)()
+        ms = np.zeros(cap)
+        n = ctypes.c_int32(0)
+        _check(lib().ptzba_setup_timing(self.h, cap, ctypes.cast(names, c_void_p), _ptr(ms), ctypes.byref(n)),
+               "ptzba_setup_timing")
+        k = min(cap, n.value)
+        return {names[i].decode(): float(ms[i]) for i in range(k)}
 
     def set_huber_curvature(self, hc):
         """Host-driven LM: the huber curvature weight (units of rho' beyond the unit) of later linearisations."""

@@ -522,19 +522,16 @@ def test_save_restore_state_restarts_identically(gpu_available):
     h.close()
 
 
-@pytest.mark.parametrize("mode", ["mf", "mf2"])
 @pytest.mark.parametrize("config,loss", [("config2", "linear"), ("config3", "huber")])
-def test_reduced_system_matrix_core_k2_matches_fp64(gpu_available, config, loss, mode, monkeypatch):
+def test_reduced_system_matrix_core_k2_matches_fp64(gpu_available, config, loss):
     """K2 of the fp32 path runs on the matrix cores (k_schur_mf: fp16 hi/lo operand splits with power-of-
-    two landmark scaling; k_schur_mf2: the same over chunk pairs, PTZBA_SCHUR=mf2); the fp64
-    path keeps the VALU kernel.  At the same linearisation point the two reduced camera systems (S | b | g_pose
+    two landmark scaling); the fp64 path keeps the VALU kernel.  At the same linearisation point the two reduced camera systems (S | b | g_pose
     | diag U, the exchange region) agree to the fp32 record precision, element by element against each row's
     scale."""
     import torch
     import bench
     import ptzba
     import synthetic
-    monkeypatch.setenv("PTZBA_SCHUR", mode)
     p = synthetic.make_problem(config, seed=0)
     lo = ptzba.LOSS_LINEAR if loss == "linear" else ptzba.LOSS_HUBER
     out = []
@@ -565,42 +562,12 @@ def test_reduced_system_matrix_core_k2_matches_fp64(gpu_available, config, loss,
     assert tail < 1e-5, tail
 
 
-@pytest.mark.parametrize("config", ["config2", "config3"])
-def test_folded_schur_reduce_bitwise_equals_separate_reduce(gpu_available, config, monkeypatch):
-    """Matrix-core K2 with the tile reduction folded into the tile's last split (PTZBA_K2_FOLD=2: write-through
-    partials, a relaxed per-tile counter, sc1 loads in the last split) writes the same reduced camera system, bit
-    for bit, as the separate k_schur_reduce launch (the same partials summed in the same item order)."""
-    import torch
-    import bench
-    import ptzba
-    import synthetic
-    p = synthetic.make_problem(config, seed=0)
-    out = []
-    for fold in ("0", "2", "2"):
-        monkeypatch.setenv("PTZBA_K2_FOLD", fold)
-        h = ptzba.BAHandle(0)
-        h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=ptzba.FP32,
-                      loss=ptzba.LOSS_HUBER)
-        h.set_state(p.init_ptz, p.init_rays)
-        h.linearize()
-        for lam in (1e-3, 1e-2):  # the per-tile counters re-arm: a second build reuses them
-            h.build_reduced(lam)
-        h.sync()
-        sp, n, _ = h.exchange()
-        out.append(torch.as_tensor(bench._DevArray(sp, n), device="cuda:0").cpu().numpy().copy())
-        h.close()
-    assert np.array_equal(out[0], out[1]) and np.array_equal(out[1], out[2])
-
-
-@pytest.mark.parametrize("config,knob", [("config2", "PTZBA_CHOL_PERSIST=1"), ("grid", "PTZBA_CHOL_PERSIST=1"),
-                                         ("grid", "PTZBA_BS_PERSIST=0")])
+@pytest.mark.parametrize("config,knob", [("config2", "PTZBA_BS_PERSIST=0"), ("grid", "PTZBA_BS_PERSIST=0")])
 def test_single_launch_schedules_bitwise_equal(gpu_available, config, knob, monkeypatch):
-    """Schedule-only forms of the factorisation / back-substitution give bit-identical LM iterates: PTZBA_CHOL_PERSIST=1
-    -- every factorisation level in ONE launch (one workgroup per task by ticket, per-level completion counters,
-    coherent tile traffic: k_chol_pst) against the per-level launches; PTZBA_BS_PERSIST=0 -- the per-step blocked
-    back-substitution against the single-launch one (the default).  config 2 (natural / one-level plan) and the
-    3-row grid (delayed trailing updates: the second panel pair and 2 x 2 trailing blocks); 3 solves of 3 LM
-    iterations per handle, so the counters run over several epochs."""
+    """Schedule-only forms of the back-substitution give bit-identical LM iterates: PTZBA_BS_PERSIST=0 -- the per-step
+    blocked back-substitution against the single-launch one (the default, per-column counters).  config 2 (natural /
+    one-level plan) and the 3-row grid (delayed trailing updates: the second panel pair and 2 x 2 trailing blocks); 3
+    solves of 3 LM iterations per handle, so the counters run over several epochs."""
     import ptzba
     import synthetic
     if config == "grid":
@@ -652,3 +619,16 @@ def test_fused_prepare_matches_separate_prepare(gpu_available, monkeypatch):
     (b_ptz, b_rays), b_res = out[1]
     assert a_res == b_res
     assert np.array_equal(a_ptz, b_ptz) and np.array_equal(a_rays, b_rays)
+
+
+def test_setup_timing_reports_set_problem_phases(gpu_available):
+    """ptzba_setup_timing: the host phases of the last set_problem (names and ms), replacing round 4's env knob."""
+    import ptzba
+    import synthetic
+    p = synthetic.make_problem("config2", seed=0)
+    h = ptzba.BAHandle(0)
+    h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=ptzba.FP32)
+    t = h.setup_timing()
+    h.close()
+    assert len(t) >= 4 and all(v >= 0.0 for v in t.values()), t
+    assert "upload+alloc" in t, t

@@ -274,9 +274,8 @@ def _sift_match(kg, ko):
     return np.array(pairs, np.int64).reshape(-1, 2)
 
 
-@pytest.mark.parametrize("sw", ["000", "100", "110", "101"])
 @pytest.mark.parametrize("seed,w,h", [(2, 192, 144), (3, 257, 181)])
-def test_sift_matches_oracle(gpu_available, monkeypatch, seed, w, h, sw):
+def test_sift_matches_oracle(gpu_available, seed, w, h):
     """ptz_sift against the oracle restatement: the float32 pyramid is bit-identical (no contraction, same
     operation order) and the fp64 refinement follows the same evaluation order, so the keypoint set, positions,
     sizes and responses agree exactly; angles to 1e-3 deg (atan2 / exp of different libraries); descriptors
@@ -284,9 +283,6 @@ def test_sift_matches_oracle(gpu_available, monkeypatch, seed, w, h, sw):
     of keypoints (measured: 100 %, profiles/r02_sift_check.txt)."""
     import ptzba
     from oracle import ptz_oracle as orc
-    monkeypatch.setenv("PTZ_SIFT_COLS_SW", sw[0])  # sliding-window column / row passes (bit-identical by construction)
-    monkeypatch.setenv("PTZ_SIFT_ROWS_SW", sw[1])
-    monkeypatch.setenv("PTZ_SIFT_ROWS4", sw[2])  # row pass over one row per workgroup (default) or 4 (opt-in)
     I, _, _ = frontend_data.textured_pair(seed=seed, width=w, height=h, d_pan=0.5, f=400.0)
     kg, rg, dg = ptzba.sift(I, 0)
     ko, ro, do = orc.sift_detect_compute(I, 0)

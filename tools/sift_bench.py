@@ -1,8 +1,7 @@
 #!/usr/bin/env python3
-"""Wall time of one GPU SIFT detectAndCompute (ptz_sift) on a rendered 1080p frame, median of N calls; the
-two-pass blur (default), the two-pass blur with the sliding-window column pass (PTZ_SIFT_COLS_SW=1) and the fused one
-(PTZ_SIFT_BLUR2=1; the env is read per call).  Same-image reuse is off (PTZ_SIFT_REUSE=0): every call detects.
-`--default`: the default variant only (for a rocprofv3 kernel profile)."""
+"""Wall time of one GPU SIFT detectAndCompute (ptz_sift) on a rendered 1080p frame, median of N calls.  Same-image
+reuse is off (PTZ_SIFT_REUSE=0): every call detects.  (The blur variants it compared in round 4 were removed in round 5:
+DESIGN.md §6.3.)"""
 import os
 import sys
 import time
@@ -21,14 +20,7 @@ def main():
     img = image_process._grey_u8(synthetic.RenderedStream(scene, seed=0).image(0))
     out = {}
     os.environ["PTZ_SIFT_REUSE"] = "0"
-    variants = (("two_pass_cols_1out", "0", "0", "0"), ("two_pass", "0", "1", "0"),
-                ("two_pass_rows_sw", "0", "1", "1"), ("fused", "1", "0", "0"))
-    if "--default" in sys.argv:
-        variants = variants[1:2]
-    for tag, val, cs, rs in variants:
-        os.environ["PTZ_SIFT_BLUR2"] = val
-        os.environ["PTZ_SIFT_COLS_SW"] = cs
-        os.environ["PTZ_SIFT_ROWS_SW"] = rs
+    for tag in ("default",):
         for _ in range(3):
             ptzba.sift(img, 1500)
         ts = []
