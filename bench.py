@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--no-secondary", action="store_true", help="skip the fp64 / linear-loss leg")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache K1 pass")
     ap.add_argument("--dry-run", action="store_true", help="launcher / rendezvous plumbing only (no GPU work)")
+    ap.add_argument("--stream-frames", type=int, default=100,
+                    help="config-5 leg: frames of demo_stream.py after the headline (0: skip)")
     return ap.parse_args()
 
 
@@ -180,6 +182,22 @@ def cpu_baseline(prob, windows, full=False, full_nfev=3):
                 sample=f"scipy trf (x_scale='jac', ftol=1e-4, FD jac_sparsity), 1 thread, on keyframe windows of "
                        f"{prob.meta.get('config')} [{desc}]; seconds/iteration fitted as c*R^{alpha:.3f} and evaluated at "
                        f"the full R = {R_full} records")
+
+
+def stream_leg(frames):
+    """BASELINE configs[4] beside the headline: demo_stream.py (the demo_soccer.py:31-51 loop: GPU SIFT / LK / RANSAC
+    front-end on rendered 1080p frames, EKF tracking, 30-keyframe sliding-window BA, scene_map.py:91-115's per-keyframe
+    "BA time") for `frames` frames in a child process, after the timed region.  A secondary field, not the metric."""
+    cmd = [sys.executable, os.path.join(PKG, "demo_stream.py"), "--frames", str(frames), "--window", "30"]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as e:  # report, never hide
+        return {"error": repr(e)}
+    keep = ("workload", "frontend", "frames", "fps_end_to_end", "tracking_ms", "keyframes", "keyframe_ba_ms",
+            "lost_frames", "pose_rmse_vs_truth", "keyframe_ba_breakdown_ms", "keyframe_ba_slowest_breakdown_ms",
+            "render_s_outside_loop")
+    return {k: d[k] for k in keep if k in d}
 
 
 def _git_blob(path):
@@ -552,6 +570,8 @@ def main():
                 out["vs_cpu_baseline"] = out["value"] / cbv if cbv else None
             except Exception as e:  # report, never hide
                 out["cpu_baseline"] = {"value": None, "error": repr(e)}
+        if a.stream_frames > 0 and world == 1:
+            out["config5"] = stream_leg(a.stream_frames)
         print(json.dumps(out))
     h.close()
     if comm is not None:

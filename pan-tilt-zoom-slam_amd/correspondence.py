@@ -146,6 +146,14 @@ class CorrespondenceCache:
         self.detections[(key, feature_method)] = (image, kps, des, xy)
         return kps, des, xy
 
+    def prepare(self, key, image, feature_method, device=0):
+        """A map's first keyframe (no BA yet): its detection, which the first BA call would make, and the one-time
+        costs of that call -- the interpreter self-check of the native bookkeeping and the shared BA handle
+        (ptzba.warm_up) -- so no keyframe BA call carries process warm-up."""
+        _self_check()
+        self.detect(key, image, feature_method)
+        ptzba.warm_up(device)
+
     def match(self, key_i, key_j, det_i, det_j, feature_method):
         k = (key_i, key_j, feature_method)
         hit = self.matches.get(k)

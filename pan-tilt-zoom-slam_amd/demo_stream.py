@@ -81,7 +81,25 @@ def main():
                     help="gpu: rendered 1080p frames through the GPU front-end (SIFT, LK, RANSAC); "
                          "standin: StreamFrontEnd's ground-truth correspondences")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--gc", choices=("default", "freeze"), default="freeze",
+                    help="freeze (default): gc.freeze() before the loop -- the ~10^5 objects of the imports (torch, scipy)"
+                         " leave the cyclic collector's generations, so its full collections in the loop take ~4 ms "
+                         "instead of 14-19 ms and stop landing as keyframe BA spikes (profiles/r05j_*); default: "
+                         "Python's own setting")
     a = ap.parse_args()
+    import gc
+    gc_stats = {}  # generation -> [collections, total ms, max ms] during the loop (Python's cyclic collector)
+    gc_t = [0.0]
+
+    def _gc_cb(phase, info):
+        if phase == "start":
+            gc_t[0] = time.perf_counter()
+        else:
+            dt = 1e3 * (time.perf_counter() - gc_t[0])
+            st = gc_stats.setdefault(info["generation"], [0, 0.0, 0.0])
+            st[0] += 1
+            st[1] += dt
+            st[2] = max(st[2], dt)
     import ptzba
     import synthetic
     from ptz_slam import PtzSlam
@@ -100,11 +118,16 @@ def main():
         t_render = time.perf_counter() - t0
     slam = PtzSlam()
     slam.keyframe_map = Map("sift", max_ba_frame=a.window or None)
+    if a.gc == "freeze":
+        gc.collect()
+        gc.freeze()
+    gc.callbacks.append(_gc_cb)
     quiet = contextlib.nullcontext() if a.verbose else contextlib.redirect_stdout(io.StringIO())
     t0 = time.perf_counter()
     with quiet:
         rec = run_stream(slam, source, a.frames, scene.camera(0), keyframe_every=a.keyframe_every)
     wall = time.perf_counter() - t0
+    gc.callbacks.remove(_gc_cb)
     est = np.asarray(rec["ptz"])
     err = est - scene.cams[:len(est)]
     tt = np.asarray(rec["t_track"][1:])
@@ -120,18 +143,24 @@ def main():
         "tracking_ms": {"mean": 1e3 * float(tt.mean()), "p50": 1e3 * float(np.median(tt)),
                         "p99": 1e3 * float(np.percentile(tt, 99))},
         "keyframes": int(sum(rec["keyframe"])), "keyframe_ba_ms": {"mean": 1e3 * float(tk.mean()),
-                                                                  "max": 1e3 * float(tk.max())},
+                                                                  "p50": 1e3 * float(np.median(tk)),
+                                                                  "max": 1e3 * float(tk.max()),
+                                                                  "argmax_keyframe": int(np.argmax(tk)) + 1},
         "final_keyframes_in_map": len(slam.keyframe_map.keyframe_list), "rays_final": rec["n_rays"][-1],
         "lost_frames": int(sum(rec["lost"])),
         "pose_rmse_vs_truth": {"pan_deg": float(np.sqrt(np.mean(err[:, 0] ** 2))),
                                "tilt_deg": float(np.sqrt(np.mean(err[:, 1] ** 2))),
                                "f_px": float(np.sqrt(np.mean(err[:, 2] ** 2)))},
         "device": ptzba.lib().ptzba_version().decode(),
+        "gc": a.gc, "gc_pauses_ms": {str(g): {"count": v[0], "total": v[1], "max": v[2]} for g, v in sorted(gc_stats.items())},
     }
     kt = rec.get("kf_timing", [])[1:]
     if kt:  # where a keyframe's BA call spends its time (bundle_adjustment.LAST_RESULT["timing"], mean ms)
         keys = sorted({k for d in kt for k in d})
         out["keyframe_ba_breakdown_ms"] = {k: 1e3 * float(np.mean([d.get(k, 0.0) for d in kt])) for k in keys}
+        kall = rec.get("kf_timing", [])  # one per in-loop keyframe, as tk
+        if len(kall) == len(tk):  # the slowest keyframe call's own breakdown
+            out["keyframe_ba_slowest_breakdown_ms"] = {k: 1e3 * float(kall[int(np.argmax(tk))].get(k, 0.0)) for k in keys}
     print(json.dumps(out))
 
 

@@ -1400,6 +1400,23 @@ def release_solve_handles(device=None):
 LAST_SOLVE_TIMING = {}  # host wall times of the last shared-handle solve() (set_problem, LM incl. state I/O)
 
 
+def warm_up(device=0, precision=FP64):
+    """First-use costs of solve()'s shared handle -- its creation (stream, pinned staging, device buffers) and the
+    first launch of each BA kernel (code object loading) -- paid here instead of inside the first keyframe BA call
+    (a keyframe map calls it when it receives its first keyframe, which has no BA: scene_map.Map.add_first_keyframe).
+    Solves a 3-frame problem of 12 rays (both losses) on the shared handle; nothing it computes is kept."""
+    th = np.deg2rad(np.array([[a, b] for a in (-2.0, -1.0, 0.0, 1.0, 2.0, 3.0) for b in (-3.0, 1.0)]))
+    ptz = np.array([[0.0, -2.0, 3000.0], [1.0, -2.0, 3000.0], [2.0, -2.0, 3000.0]])
+    frame = np.repeat(np.arange(3, dtype=np.int32), len(th))
+    landmark = np.tile(np.arange(len(th), dtype=np.int32), 3)
+    xy = np.stack([640.0 + 3000.0 * np.tan(th[landmark, 0] - np.deg2rad(ptz[frame, 0])),
+                   360.0 + 3000.0 * np.tan(th[landmark, 1] - np.deg2rad(ptz[frame, 1]))], 1)  # (near the model)
+    rays = np.rad2deg(th)
+    for loss in (LOSS_LINEAR, LOSS_HUBER):
+        solve(3, len(th), frame, landmark, xy, 640.0, 360.0, ptz, rays, precision=precision, loss=loss, device=device,
+              max_iter=3)
+
+
 def solve(n_pose, n_landmark, frame, landmark, xy, u, v, init_ptz, init_rays, weight=None, precision=FP64,
           loss=LOSS_LINEAR, f_scale=1.0, device=0, keep_handle=True, **lm_kw):
     """Convenience one-shot solve.  Returns (ptz [N,3], rays [M,2], LMResult).  keep_handle=True (default): one

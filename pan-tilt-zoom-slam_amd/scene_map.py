@@ -39,6 +39,8 @@ class Map:
     def add_first_keyframe(self, keyframe, verbose=False):
         assert isinstance(keyframe, KeyFrame)
         self.keyframe_list = [keyframe]
+        if self.correspondences is not None and getattr(keyframe, "img", None) is not None:
+            self.correspondences.prepare(keyframe.img_index, keyframe.img, self.feature_method)
         if verbose:
             print("first key frame is added, no bundle adjustment and landmark")
 

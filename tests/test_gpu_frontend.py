@@ -463,16 +463,17 @@ def test_orb_front_end_recovers_homography(gpu_available):
     assert len(kc) == 100 and dc.shape == (100, 32)
 
 
-@pytest.mark.parametrize("n1,n2", [(1000, 1500), (37, 70), (130, 1)])
-def test_knn2_matrix_core_sets_equal_fp32_pair(gpu_available, monkeypatch, n1, n2):
+@pytest.mark.parametrize("n1,n2,vmax", [(1000, 1500, 256), (37, 70, 256), (130, 1, 256), (300, 400, 2048)])
+def test_knn2_matrix_core_sets_equal_fp32_pair(gpu_available, monkeypatch, n1, n2, vmax):
     """ptz_match_knn2_sets on integer-valued 128-d descriptor sets (SIFT's) runs k_knn2_mf (f16 MFMA dot products,
     exact integer distances, running top 2 per lane): the same indices and distances, bit for bit, as the fp32
     k_sqdist + k_top2 pair (ptz_match_knn2, and the sets path with PTZ_KNN_MF=0) -- duplicated train rows included
-    (ties to the lower index), ragged sizes, a single train row."""
+    (ties to the lower index), ragged sizes, a single train row.  Integers beyond 255 (vmax 2048) would leave the
+    f16 sums inexact: the sets path then takes the fp32 pair by itself, still bit for bit match_knn2."""
     import ptzba
     rng = np.random.default_rng(n1 + n2)
-    q = rng.integers(0, 256, (n1, 128)).astype(np.float32)
-    t = rng.integers(0, 256, (n2, 128)).astype(np.float32)
+    q = rng.integers(0, vmax, (n1, 128)).astype(np.float32)
+    t = rng.integers(0, vmax, (n2, 128)).astype(np.float32)
     if n2 > 10:
         t[5] = t[3]          # an exact tie between two train rows
         q[:4] = t[[3, 7, 7, 9]]  # distance-0 queries
@@ -487,5 +488,31 @@ def test_knn2_matrix_core_sets_equal_fp32_pair(gpu_available, monkeypatch, n1, n
             monkeypatch.setenv("PTZ_KNN_MF", mf)
             i, d = ptzba.match_knn2_sets(keys[:2], [len(qa), len(qb)], keys[2])
             assert np.array_equal(i, ref_i) and np.array_equal(d, ref_d), mf
+    finally:
+        ptzba.desc_drop(keys)
+
+
+def test_knn2_sets_with_empty_sets(gpu_available):
+    """A keyframe without SIFT keypoints: an empty train set gives every query (-1, -1) at infinite distance, and an
+    empty query set gives no rows -- whatever column count the empty arrays carry (round 4 failed with 'query set has
+    dim 128, train 1')."""
+    import ptzba
+    rng = np.random.default_rng(7)
+    q = rng.integers(0, 256, (20, 128)).astype(np.float32)
+    t = rng.integers(0, 256, (30, 128)).astype(np.float32)
+    keys = [601, 602, 603, 604]
+    try:
+        ptzba.desc_put_new(keys[0], q)
+        ptzba.desc_put_new(keys[1], np.zeros((0, 128), np.float32))
+        ptzba.desc_put_new(keys[2], [])
+        ptzba.desc_put_new(keys[3], t)
+        for empty_train in (keys[1], keys[2]):
+            i, d = ptzba.match_knn2_sets([keys[0]], [len(q)], empty_train)
+            assert i.shape == (20, 2) and np.all(i == -1) and np.all(np.isinf(d))
+        i, d = ptzba.match_knn2_sets([keys[1], keys[0]], [0, len(q)], keys[3])
+        ri, rd = ptzba.match_knn2(q, t)
+        assert np.array_equal(i, ri) and np.array_equal(d, rd)
+        i, d = ptzba.match_knn2_sets([keys[1]], [0], keys[3])
+        assert i.shape == (0, 2) and d.shape == (0, 2)
     finally:
         ptzba.desc_drop(keys)
