@@ -169,7 +169,9 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
   __shared__ real s_x[4][SEGW], s_y[4][SEGW], s_acc[4][4][SEGW];
   __shared__ double s_ft[5][FTL ? K1_FT_LDS : 1];  // ca, sa, cb, sb, f per frame (fp64)
   const int lane = lane_id();
-  const int wv = threadIdx.x >> 6;
+  // wave-uniform by construction: with readfirstlane the compiler sees it, so the descriptor, the ray table, the
+  // window and record bounds and the slot offsets are scalar loads / SGPRs (SALU address math, fewer VGPRs)
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int task = blockIdx.x * 4 + wv;
   if (a.run_if && !*a.run_if) return;  // conditional re-linearisation (device-driven LM): the whole grid leaves
   if constexpr (!FTL) {
