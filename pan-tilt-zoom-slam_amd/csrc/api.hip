@@ -1831,9 +1831,9 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       h->rays_trial.alloc(2 * (size_t)n_landmark * 8) || h->D_pose.alloc(3 * n_pose * 8) ||
       h->D_ray.alloc(2 * (size_t)n_landmark * 8) || h->ft.alloc((size_t)n_pose * 8 * e) ||
       h->rt.alloc((size_t)n_landmark * 8 * e) || h->ft64.alloc((size_t)n_pose * 64) ||
-      h->rt64.alloc((size_t)n_landmark * 64) || h->ug_slot[0].alloc((size_t)std::max<int64_t>(h->n_slot, 1) * 12 * e) ||
-      h->ug_slot[1].alloc((size_t)std::max<int64_t>(h->n_slot, 1) * 12 * e) || h->w_slot[0].alloc((size_t)std::max<int64_t>(h->n_slot, 1) * 8 * e) ||
-      h->w_slot[1].alloc((size_t)std::max<int64_t>(h->n_slot, 1) * 8 * e) || h->lm_out[0].alloc((size_t)n_landmark * 8 * 8) ||
+      h->rt64.alloc((size_t)n_landmark * 64) || h->ug_slot[0].alloc((size_t)std::max<int64_t>(h->n_slot, 1) * UG_STRIDE * e) ||
+      h->ug_slot[1].alloc((size_t)std::max<int64_t>(h->n_slot, 1) * UG_STRIDE * e) || h->w_slot[0].alloc((size_t)std::max<int64_t>(h->n_slot, 1) * W_STRIDE * e) ||
+      h->w_slot[1].alloc((size_t)std::max<int64_t>(h->n_slot, 1) * W_STRIDE * e) || h->lm_out[0].alloc((size_t)n_landmark * 8 * 8) ||
       h->lm_out[1].alloc((size_t)n_landmark * 8 * 8) || h->lm_aux.alloc((size_t)n_landmark * 8 * 8) ||
       h->lm_red.alloc((size_t)n_landmark * 4 * 8) || h->sys.alloc((size_t)h->sys_count() * 8) ||
       h->scal.alloc(2 * PTZBA_NSCALARS * 8) || h->red_scratch.alloc(RED_SCRATCH * 8) || h->info.alloc(16) ||

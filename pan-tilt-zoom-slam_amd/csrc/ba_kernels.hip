@@ -11,9 +11,9 @@
 //   segments  one per unique (landmark, frame): seg_frame, seg_rec_begin (CSR into records);
 //             landmark CSR lm_seg_begin; frame CSR frame_seg_begin/frame_seg_list
 //   tables    FrameTab[n_pose] (cos/sin pan, cos/sin tilt, f), RayTab[n_lm] (ray direction + derivs)
-//   lin       w_slot[n_slot][8] = W(3x2) | 0 0  (real) in the dense landmark x frame slot table:
+//   lin       w_slot[n_slot][W_STRIDE] = W(3x2) (real) in the dense landmark x frame slot table:
 //                                 slot = toff_l + frame - first_l; slots of unobserved frames stay 0
-//             ug_slot[n_slot][12] = U(3x3 sym, 6) | g_pose(3) | pad (real, same slots; summed per frame by K2)
+//             ug_slot[n_slot][UG_STRIDE] = U(3x3 sym, 6) | g_pose(3) (real, same slots; summed per frame by K2)
 //             lm_out[n_lm][8]    = V(2x2 sym, 3) | g_ray(2) | cost | pad      (fp64)
 //
 // K1 `k_linearize` is the HBM-streaming kernel: one wave per landmark walks the landmark's records
@@ -540,16 +540,13 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
       }
       // W into the landmark's dense frame slot: the Schur kernel's inner-loop operand and the
       // back-substitution's W
-      real* cw = w_slot + (slot0 + fs) * 8;
-      store4(cw, W[0], W[1], W[2], W[3]);
-      store4(cw + 4, W[4], W[5], (real)0, (real)0);
-      // U (6) | g_pose (3) | 0 0 0 into the same dense slot: summed per frame by the Schur kernel
-      real* o = ug_slot + (slot0 + fs) * 12;
-      store4(o, Sx * J[0][0] * J[0][0] + Sy * J[1][0] * J[1][0], Sx * J[0][0] * J[0][1] + Sy * J[1][0] * J[1][1],
-             Sx * J[0][0] * J[0][2] + Sy * J[1][0] * J[1][2], Sx * J[0][1] * J[0][1] + Sy * J[1][1] * J[1][1]);
-      store4(o + 4, Sx * J[0][1] * J[0][2] + Sy * J[1][1] * J[1][2], Sx * J[0][2] * J[0][2] + Sy * J[1][2] * J[1][2],
-             J[0][0] * Srx + J[1][0] * Sry, J[0][1] * Srx + J[1][1] * Sry);
-      store4(o + 8, J[0][2] * Srx + J[1][2] * Sry, (real)0, (real)0, (real)0);
+      slot_store6(w_slot + (slot0 + fs) * W_STRIDE, W);
+      // U (6) | g_pose (3) into the same dense slot: summed per frame by the Schur kernel
+      const real UG[9] = {Sx * J[0][0] * J[0][0] + Sy * J[1][0] * J[1][0], Sx * J[0][0] * J[0][1] + Sy * J[1][0] * J[1][1],
+                          Sx * J[0][0] * J[0][2] + Sy * J[1][0] * J[1][2], Sx * J[0][1] * J[0][1] + Sy * J[1][1] * J[1][1],
+                          Sx * J[0][1] * J[0][2] + Sy * J[1][1] * J[1][2], Sx * J[0][2] * J[0][2] + Sy * J[1][2] * J[1][2],
+                          J[0][0] * Srx + J[1][0] * Sry, J[0][1] * Srx + J[1][1] * Sry, J[0][2] * Srx + J[1][2] * Sry};
+      slot_store9(ug_slot + (slot0 + fs) * UG_STRIDE, UG);
       V00 += (double)(Sx * J[0][3] * J[0][3] + Sy * J[1][3] * J[1][3]);
       V01 += (double)(Sx * J[0][3] * J[0][4] + Sy * J[1][3] * J[1][4]);
       V11 += (double)(Sx * J[0][4] * J[0][4] + Sy * J[1][4] * J[1][4]);
@@ -681,21 +678,6 @@ void launch_build_prologue(double* S, int64_t ld, const int2* zt, int n_tiles, d
 // Trial state in one launch (with the trial's frame / ray tables, which the trial linearisation reads):
 // blocks [0, nb) back-substitute 4 landmarks each as above, the last block forms the trial poses, their
 // tables and the pose partials (one thread per frame, fixed-order reduction: identical on every rank).
-// the 6 W values of a dense slot row (8 reals, 16-B aligned) in two vector loads
-template <typename real>
-__device__ __forceinline__ void load_w6_slot(real (&x)[6], const real* __restrict__ p) {
-  if constexpr (sizeof(real) == 4) {
-    const float4 lo = reinterpret_cast<const float4*>(p)[0];
-    const float2 hi = reinterpret_cast<const float2*>(p)[2];
-    x[0] = lo.x; x[1] = lo.y; x[2] = lo.z; x[3] = lo.w; x[4] = hi.x; x[5] = hi.y;
-  } else {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const double2 d = reinterpret_cast<const double2*>(p)[k];
-      x[2 * k] = d.x; x[2 * k + 1] = d.y;
-    }
-  }
-}
 struct PoseTrialArgs {
   const double* ptz;
   const double* g_pose;
@@ -793,7 +775,7 @@ __global__ __launch_bounds__(256) void k_trial(BacksubArgs a, PoseTrialArgs pa, 
     if (f < a.n_fixed) continue;
     const double* dp = a.dpose + a.frame_pos[f];
     real w[6];
-    load_w6_slot(w, w_slot + ((int64_t)lmeta.z + f - lmeta.x) * 8);
+    slot_load6(w, w_slot + ((int64_t)lmeta.z + f - lmeta.x) * W_STRIDE);
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       t0 += (double)w[2 * q] * dp[q];

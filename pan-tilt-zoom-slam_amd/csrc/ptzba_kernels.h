@@ -10,6 +10,62 @@ constexpr int K1_SEGW = 128;  // K1 segments per LDS window per wave
 #define K1_FT_LDS_N 640
 #endif
 constexpr int K1_FT_LDS = K1_FT_LDS_N;  // K1 stages the frame tables in LDS up to this many frames (5 x 8 B per frame)
+// dense landmark x frame slot rows, packed (no padding: K1 writes and K2 reads 60 B per fp32 slot, not 80):
+// W (3x2) in W_STRIDE reals, U (3x3 sym, 6) | g_pose (3) in UG_STRIDE reals; rows are only 4-B (fp32) / 8-B (fp64)
+// aligned, so the vector accesses go through the element-aligned vector types below (dwordx4 / x2 on gfx950)
+constexpr int W_STRIDE = 6, UG_STRIDE = 9;
+typedef float f4e __attribute__((ext_vector_type(4), aligned(4)));
+typedef float f2e __attribute__((ext_vector_type(2), aligned(4)));
+typedef double d2e __attribute__((ext_vector_type(2), aligned(8)));
+template <typename real>
+__device__ __forceinline__ void slot_load6(real (&x)[6], const real* __restrict__ p) {
+  if constexpr (sizeof(real) == 4) {
+    const f4e lo = *reinterpret_cast<const f4e*>(p);
+    const f2e hi = *reinterpret_cast<const f2e*>(p + 4);
+    x[0] = lo.x; x[1] = lo.y; x[2] = lo.z; x[3] = lo.w; x[4] = hi.x; x[5] = hi.y;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const d2e d = *reinterpret_cast<const d2e*>(p + 2 * k);
+      x[2 * k] = d.x; x[2 * k + 1] = d.y;
+    }
+  }
+}
+template <typename real>
+__device__ __forceinline__ void slot_load9(real (&x)[9], const real* __restrict__ p) {
+  if constexpr (sizeof(real) == 4) {
+    const f4e a = *reinterpret_cast<const f4e*>(p), b = *reinterpret_cast<const f4e*>(p + 4);
+    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const d2e d = *reinterpret_cast<const d2e*>(p + 2 * k);
+      x[2 * k] = d.x; x[2 * k + 1] = d.y;
+    }
+  }
+  x[8] = p[8];
+}
+template <typename real>
+__device__ __forceinline__ void slot_store6(real* p, const real (&x)[6]) {
+  if constexpr (sizeof(real) == 4) {
+    *reinterpret_cast<f4e*>(p) = f4e{x[0], x[1], x[2], x[3]};
+    *reinterpret_cast<f2e*>(p + 4) = f2e{x[4], x[5]};
+  } else {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) *reinterpret_cast<d2e*>(p + 2 * k) = d2e{x[2 * k], x[2 * k + 1]};
+  }
+}
+template <typename real>
+__device__ __forceinline__ void slot_store9(real* p, const real (&x)[9]) {
+  if constexpr (sizeof(real) == 4) {
+    *reinterpret_cast<f4e*>(p) = f4e{x[0], x[1], x[2], x[3]};
+    *reinterpret_cast<f4e*>(p + 4) = f4e{x[4], x[5], x[6], x[7]};
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) *reinterpret_cast<d2e*>(p + 2 * k) = d2e{x[2 * k], x[2 * k + 1]};
+  }
+  p[8] = x[8];
+}
 struct LinArgs {
   const int4* lm_work;           // [2 n_work] {landmark, s0, s1, first record}, {lm_meta}, heaviest first
   int n_work;
@@ -29,8 +85,8 @@ struct LinArgs {
   double hcurv;                  // huber: curvature weight beyond the unit = hcurv * rho' (1: IRLS)
   const double* hcurv_dev;       // device-driven LM: the curvature weight from LMDev::hc instead (nullptr: hcurv)
   const int* run_if;             // nullptr, or: the launch exits at once unless *run_if != 0 (re-linearisation)
-  void* ug_slot;                 // [n_slot][12] real: U (6) | g_pose (3) | 0 0 0 (dense slots)
-  void* w_slot;                  // [n_slot][8] real: W (6) | 0 0 at slot toff_l + frame - first_l
+  void* ug_slot;                 // [n_slot][UG_STRIDE] real: U (6) | g_pose (3) (dense slots)
+  void* w_slot;                  // [n_slot][W_STRIDE] real: W (6) at slot toff_l + frame - first_l
   const int4* lm_meta;           // [n_lm] {first frame, last frame, slot offset, 0}
   double* lm_out;                // [n_lm][8]
   // device-driven LM: the linearisation slot is chosen on the device -- with sel != nullptr the kernel writes
@@ -69,8 +125,8 @@ struct SchurArgs {
   const int4* groups;             // [n_groups] per tile {f1b, chunk, first item, end item}
   const int4* item_lm;            // item landmark lists: {landmark, first frame, last frame, slot offset}
   const int32_t* frame_win_hi;    // [n_pose]
-  const void* ug_slot;            // [n_slot][12] real: U (6) | g_pose (3) | 0 (dense slots)
-  const void* w_slot;             // [n_slot][8] real: W | 0 0 (dense landmark x frame slots)
+  const void* ug_slot;            // [n_slot][UG_STRIDE] real: U (6) | g_pose (3) (dense slots)
+  const void* w_slot;             // [n_slot][W_STRIDE] real: W (dense landmark x frame slots)
   const double* lm_aux;           // [n_lm][8]
   const int32_t* frame_pos;       // [n_pose] system row of the frame's pan (-1: fixed)
   void* part;                     // [n_items][SCHUR_F1][9][64] split partials (record precision)
@@ -91,7 +147,7 @@ struct SchurArgs {
 struct BacksubArgs {
   const int32_t* lm_seg_begin;
   const int32_t* seg_frame;
-  const void* w_slot;    // [n_slot][8] real: W | 0 0
+  const void* w_slot;    // [n_slot][W_STRIDE] real: W
   const int4* lm_meta;   // [n_lm] {first frame, last frame, slot offset, 0}
   const double* lm_out;
   const double* lm_aux;

@@ -49,22 +49,6 @@ __device__ __forceinline__ int xcd_swizzle(int b, int nb) {
   return start + idx;
 }
 
-// the 6 W values of a slot row (8 reals, 16-B aligned)
-template <typename real>
-__device__ __forceinline__ void load_w6(real (&x)[6], const real* __restrict__ p) {
-  if constexpr (sizeof(real) == 4) {
-    const float4 lo = reinterpret_cast<const float4*>(p)[0];
-    const float2 hi = reinterpret_cast<const float2*>(p)[2];
-    x[0] = lo.x; x[1] = lo.y; x[2] = lo.z; x[3] = lo.w; x[4] = hi.x; x[5] = hi.y;
-  } else {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const double2 d = reinterpret_cast<const double2*>(p)[k];
-      x[2 * k] = d.x; x[2 * k + 1] = d.y;
-    }
-  }
-}
-
 // chunk-0 items: diagonal terms of the F1 frames over this split's landmarks: U, g_pose and W V~^-1 g,
 // read from the dense slots (thread = (landmark j0 + 16 k, frame i): consecutive threads, consecutive
 // slots), reduced through `red` ([512][12] doubles of LDS that is free until staging) into part_diag.
@@ -81,7 +65,7 @@ __device__ __forceinline__ void schur_diag_terms(const SchurArgs& a, const int4*
   // DU landmarks per thread and step, all loads issued before any is consumed (clamped, branch-free)
   constexpr int DU = S2_DU, JS = 512 / SF;
   for (int j0 = t >> 5; j0 < nl; j0 += DU * JS) {
-    real u[DU][12], w[DU][6];
+    real u[DU][9], w[DU][6];
     double vg[DU][2];
     bool in[DU];
 #pragma unroll
@@ -90,13 +74,8 @@ __device__ __forceinline__ void schur_diag_terms(const SchurArgs& a, const int4*
       const int4 m = sL[min(j, nl - 1)];
       in[d] = j < nl && f >= m.y && f <= m.z;
       const int64_t slot = m.w + min(max(f - m.y, 0), m.z - m.y);
-      load_w6(w[d], w_slot + slot * 8);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const auto v4 = reinterpret_cast<const typename std::conditional<sizeof(real) == 4, float4, double4>::type*>(
-            ug_slot + slot * 12)[k];
-        u[d][4 * k] = v4.x; u[d][4 * k + 1] = v4.y; u[d][4 * k + 2] = v4.z; u[d][4 * k + 3] = v4.w;
-      }
+      slot_load6(w[d], w_slot + slot * W_STRIDE);
+      slot_load9(u[d], ug_slot + slot * UG_STRIDE);
       const double* vi = a.lm_aux + (int64_t)m.x * 8;
       vg[d][0] = vi[3];
       vg[d][1] = vi[4];
@@ -191,12 +170,12 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
       const int4 m = sL[min(p + j, nl - 1)];  // {landmark, first frame, last frame, slot offset}
       const int idx = f2base + ln - m.y;
       rwin[q] = (p + j < nl) && idx >= 0 && f2base + ln <= m.z;
-      load_w6(rw[q], w_slot + (int64_t)(m.w + min(max(idx, 0), m.z - m.y)) * 8);
+      slot_load6(rw[q], w_slot + (int64_t)(m.w + min(max(idx, 0), m.z - m.y)) * W_STRIDE);
     }
     const int f = f1b + yi;
     const int4 m = sL[min(p + yj, nl - 1)];
     ryin = (p + yj < nl) && f >= m.y && f <= m.z;
-    load_w6(ryw, w_slot + (int64_t)(m.w + min(max(f - m.y, 0), m.z - m.y)) * 8);
+    slot_load6(ryw, w_slot + (int64_t)(m.w + min(max(f - m.y, 0), m.z - m.y)) * W_STRIDE);
     const double* vi = a.lm_aux + (int64_t)m.x * 8;
     rvi[0] = vi[0]; rvi[1] = vi[1]; rvi[2] = vi[2];
   };
@@ -453,7 +432,7 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
       P.rwin[q] = (p + j < nl) && idx >= 0 && f2base + ln <= m.z;
       P.rgw[q] = sG[jj];
       if (MF_ABL == 2) { for (int k = 0; k < 6; ++k) P.rw[q][k] = (float)(m.w & 7); } else
-      load_w6(P.rw[q], w_slot + (int64_t)(m.w + min(max(idx, 0), m.z - m.y)) * 8);
+      slot_load6(P.rw[q], w_slot + (int64_t)(m.w + min(max(idx, 0), m.z - m.y)) * W_STRIDE);
     }
     const int f = f1b + yi, jj = min(p + yj, nl - 1);
     const int4 m = sL[jj];
@@ -464,7 +443,7 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
       P.rvi[0] = P.rvi[1] = P.rvi[2] = (float)(m.x & 1);
       return;
     }
-    load_w6(P.ryw, w_slot + (int64_t)(m.w + min(max(f - m.y, 0), m.z - m.y)) * 8);
+    slot_load6(P.ryw, w_slot + (int64_t)(m.w + min(max(f - m.y, 0), m.z - m.y)) * W_STRIDE);
     const double* vi = a.lm_aux + (int64_t)m.x * 8;
     P.rvi[0] = (float)vi[0]; P.rvi[1] = (float)vi[1]; P.rvi[2] = (float)vi[2];
   };
@@ -557,11 +536,7 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
   auto dfetch = [&](int p) {
     const int4 m = sL[min(p + yj, nl - 1)];
     const int64_t slot = m.w + min(max(f1b + yi - m.y, 0), m.z - m.y);
-    const float4 u0 = reinterpret_cast<const float4*>(ug_slot + slot * 12)[0];
-    const float4 u1 = reinterpret_cast<const float4*>(ug_slot + slot * 12)[1];
-    du[0] = u0.x; du[1] = u0.y; du[2] = u0.z; du[3] = u0.w;
-    du[4] = u1.x; du[5] = u1.y; du[6] = u1.z; du[7] = u1.w;
-    du[8] = ug_slot[slot * 12 + 8];
+    slot_load9(du, ug_slot + slot * UG_STRIDE);
     const double* vi = a.lm_aux + (int64_t)m.x * 8;
     dvg[0] = (float)vi[3];
     dvg[1] = (float)vi[4];

@@ -81,7 +81,10 @@ def test_config3_fp32_huber_equals_fp64_huber(gpu_available, config3):
         res = ptzba.LMSolver(h, ftol=tol, xtol=1e-12, max_iter=60).run()
         ptz, rays = h.get_state()
         h.close()
-        assert res.status in (1, 2, 3) and res.cost < res.initial_cost, res
+        # fp32: ftol=1e-10 is below the fp32 cost's round-off (~1e-7 relative), so the last trials may find no
+        # resolvable decrease at the optimum (damping limit, status 5); the cost and poses are gated below
+        ok = (1, 2, 3, ptzba.STATUS_DAMPING) if prec == ptzba.FP32 else (1, 2, 3)
+        assert res.status in ok and res.cost < res.initial_cost, res
         out.append((res, ptz, rays))
     (r32, p32, y32), (r64, p64, y64) = out
     rmse = synthetic.pose_rmse(p32, p64)
