@@ -1362,6 +1362,73 @@ static bool dist_order(int n_pose, int nf, const std::vector<int32_t>& win, int 
   return true;
 }
 
+// set_problem's device front for large problems (setup_kernels.hip): the records' (landmark, frame, index) order,
+// segments and device record arrays (rec_seg, seg_frame / seg_lm / seg_rec_begin, seg_base, rec_xy / rec_w, rec_key,
+// perm), bit for bit what the host path uploads; returns the per-segment arrays the host passes read (seg_rec_begin
+// with the end entry)
+constexpr int64_t GPU_SETUP_MIN_REC = (int64_t)1 << 22;  // 4M records (config 3: 14.6M; a 30-KF window: ~170K)
+static int gpu_front(ptzba_ctx* h, int64_t n, int n_pose, int n_lm, const int32_t* frame, const int32_t* lm,
+                     const double* xy, const double* w, std::vector<int32_t>& seg_frame, std::vector<int32_t>& seg_lm,
+                     std::vector<int64_t>& seg_rec_begin) {
+  DBuf order, key;
+  int64_t ns = 0;
+  {
+    DBuf d_frame, d_lm;
+    if (d_frame.alloc(4 * (size_t)n) || d_lm.alloc(4 * (size_t)n) || order.alloc(4 * (size_t)n) ||
+        key.alloc(4 * (size_t)n) || h->rec_seg.alloc(4 * (size_t)n))
+      return -1;
+    HIPCHK(hipMemcpyAsync(d_frame.p, frame, 4 * (size_t)n, hipMemcpyHostToDevice, h->st));
+    HIPCHK(hipMemcpyAsync(d_lm.p, lm, 4 * (size_t)n, hipMemcpyHostToDevice, h->st));
+    // (synchronises: the inputs die here)
+    if (setup_sort_runs(h->st, n, n_pose, n_lm, d_frame.as<int32_t>(), d_lm.as<int32_t>(), order.as<uint32_t>(),
+                        key.as<uint32_t>(), h->rec_seg.as<int32_t>(), &ns))
+      return -1;
+  }
+  if (ns >= INT32_MAX - 1) return fail("too many segments");
+  DBuf lm_first;
+  if (h->seg_frame.alloc(4 * (size_t)ns) || h->seg_lm.alloc(4 * (size_t)ns) || h->seg_rec_begin.alloc(8 * (size_t)(ns + 1)) ||
+      lm_first.alloc(4 * (size_t)std::max(n_lm, 1)))
+    return -1;
+  if (setup_fill_segments(h->st, n, n_pose, ns, key.as<uint32_t>(), h->rec_seg.as<int32_t>(), h->seg_frame.as<int32_t>(),
+                          h->seg_lm.as<int32_t>(), h->seg_rec_begin.as<int64_t>(), lm_first.as<int32_t>()))
+    return -1;
+  seg_frame.resize(ns);
+  seg_lm.resize(ns);
+  seg_rec_begin.resize(ns + 1);
+  HIPCHK(hipMemcpyAsync(seg_frame.data(), h->seg_frame.p, 4 * (size_t)ns, hipMemcpyDeviceToHost, h->st));
+  HIPCHK(hipMemcpyAsync(seg_lm.data(), h->seg_lm.p, 4 * (size_t)ns, hipMemcpyDeviceToHost, h->st));
+  HIPCHK(hipMemcpyAsync(seg_rec_begin.data(), h->seg_rec_begin.p, 8 * (size_t)(ns + 1), hipMemcpyDeviceToHost, h->st));
+  // the records: the raw observations up, the deltas from each segment's base in the record precision
+  const size_t e = h->elem();
+  DBuf d_xy, d_w;
+  if (d_xy.alloc(16 * (size_t)n) || (w && d_w.alloc(8 * (size_t)n)) || h->seg_base.alloc(16 * (size_t)ns) ||
+      h->rec_xy.alloc((2 * (size_t)n + 8) * e) || h->rec_key.alloc((size_t)n + 4) || h->perm.alloc(8 * (size_t)n))
+    return -1;
+  if (w) {
+    if (h->rec_w.alloc((size_t)n * e)) return -1;
+  } else {
+    h->rec_w.release();
+  }
+  HIPCHK(hipMemcpyAsync(d_xy.p, xy, 16 * (size_t)n, hipMemcpyHostToDevice, h->st));
+  if (w) HIPCHK(hipMemcpyAsync(d_w.p, w, 8 * (size_t)n, hipMemcpyHostToDevice, h->st));
+  const int rc = h->precision == PTZBA_FP32
+                     ? setup_records<float>(h->st, n, ns, order.as<uint32_t>(), h->rec_seg.as<int32_t>(),
+                                            h->seg_lm.as<int32_t>(), h->seg_rec_begin.as<int64_t>(), lm_first.as<int32_t>(),
+                                            d_xy.as<double>(), w ? d_w.as<double>() : nullptr, h->seg_base.as<double>(),
+                                            h->rec_xy.as<float>(), w ? h->rec_w.as<float>() : nullptr,
+                                            h->rec_key.as<uint8_t>(), h->perm.as<int64_t>())
+                     : setup_records<double>(h->st, n, ns, order.as<uint32_t>(), h->rec_seg.as<int32_t>(),
+                                             h->seg_lm.as<int32_t>(), h->seg_rec_begin.as<int64_t>(), lm_first.as<int32_t>(),
+                                             d_xy.as<double>(), w ? d_w.as<double>() : nullptr, h->seg_base.as<double>(),
+                                             h->rec_xy.as<double>(), w ? h->rec_w.as<double>() : nullptr,
+                                             h->rec_key.as<uint8_t>(), h->perm.as<int64_t>());
+  if (rc) return rc;
+  HIPCHK(hipMemsetAsync(h->rec_xy.as<uint8_t>() + 2 * (size_t)n * e, 0, 8 * e, h->st));  // K1's padded record groups
+  HIPCHK(hipMemsetAsync(h->rec_key.as<uint8_t>() + n, 0, 4, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));  // the temporaries and the host vectors' copies above complete here
+  return 0;
+}
+
 int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_t n_obs, const int32_t* obs_frame,
                       const int32_t* obs_landmark, const double* obs_xy, const double* obs_weight, double u, double v,
                       const ptzba_problem_opts* opts) {
@@ -1425,12 +1492,20 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->weighted = obs_weight != nullptr;
 
   st_mark("validate");
+  // large problems (configs 3 and 4: 14.6M / 410M records): the order, the segment runs and the record arrays are
+  // built on the device (setup_kernels.hip: one stable radix sort of the composite key landmark * n_pose + frame --
+  // the same order as the host's two stable counting sorts); the host keeps only the per-segment arrays its
+  // structure passes read.  Smaller ones (a sliding window's ~170K records) stay on the host.
+  const bool gpu_setup = n_obs >= GPU_SETUP_MIN_REC && n_obs < ((int64_t)1 << 31) &&
+                         (uint64_t)n_landmark * (uint64_t)n_pose <= ((uint64_t)1 << 32);
   // ---- stable counting sorts: by frame, then by landmark -> (landmark, frame, original index)
-  std::vector<int64_t> tmp, order(n_obs), lm_start;
+  std::vector<int64_t> tmp, order(gpu_setup ? 0 : n_obs), lm_start;
   std::vector<int32_t> sorted_frame;  // single-thread path: obs_frame in sorted order
   // large problems (config 4: 410M records) sort on host threads: the same stable order (par_util.h)
-  const bool par_host = host_threads(n_obs) > 1;
-  if (par_host) {
+  const bool par_host = !gpu_setup && host_threads(n_obs) > 1;
+  if (gpu_setup) {
+    // sorted in the segment phase below
+  } else if (par_host) {
     tmp.resize(n_obs);
     parallel_counting_sort(n_obs, n_pose, (const int64_t*)nullptr, tmp.data(), [&](int64_t r) { return obs_frame[r]; });
     parallel_counting_sort(n_obs, n_landmark, tmp.data(), order.data(), [&](int64_t r) { return obs_landmark[r]; });
@@ -1464,10 +1539,23 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   }
   st_mark("sort");
   // ---- segments (unique landmark, frame)
-  std::vector<int32_t> seg_frame, seg_lm, rec_seg(n_obs);
+  std::vector<int32_t> seg_frame, seg_lm, rec_seg(gpu_setup ? 0 : n_obs);
   std::vector<int64_t> seg_rec_begin;
   std::vector<int32_t> lm_seg_begin(n_landmark + 1, 0);
-  if (par_host) {
+  if (gpu_setup) {
+    if (gpu_front(h, n_obs, n_pose, n_landmark, obs_frame, obs_landmark, obs_xy, obs_weight, seg_frame, seg_lm,
+                  seg_rec_begin))
+      return -1;
+    // segments are landmark-ordered: each landmark's first segment, landmarks without one take the next's
+    const int64_t ns = (int64_t)seg_frame.size();
+    std::vector<int32_t> first(n_landmark + 1, -1);
+    first[n_landmark] = (int32_t)ns;
+    for (int64_t sg = 0; sg < ns; ++sg)
+      if (sg == 0 || seg_lm[sg] != seg_lm[sg - 1]) first[seg_lm[sg]] = (int32_t)sg;
+    for (int l = n_landmark - 1; l >= 0; --l)
+      if (first[l] < 0) first[l] = first[l + 1];
+    lm_seg_begin.assign(first.begin(), first.end());
+  } else if (par_host) {
     // two passes over the same record chunks: count the segment starts per chunk, then fill at the prefix offsets
     const int T = host_threads(n_obs);
     auto is_start = [&](int64_t k) {
@@ -1524,20 +1612,20 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     lm_seg_begin[n_landmark] = (int32_t)seg_frame.size();
   }
   const int64_t n_seg = (int64_t)seg_frame.size();
-  seg_rec_begin.push_back(n_obs);
+  if (!gpu_setup) seg_rec_begin.push_back(n_obs);  // (the device front returns the end entry with the segments)
   h->n_seg = n_seg;
   // ---- frame CSR over segments (stable: landmark ascending within a frame)
   std::vector<int32_t> frame_seg_begin(n_pose + 1, 0), frame_seg_list(n_seg), frame_win_hi(n_pose);
   for (int64_t s = 0; s < n_seg; ++s) frame_seg_begin[seg_frame[s] + 1]++;
   for (int f = 0; f < n_pose; ++f) frame_seg_begin[f + 1] += frame_seg_begin[f];
-  if (par_host && host_threads(n_seg) > 1) {
+  if ((par_host || gpu_setup) && host_threads(n_seg) > 1) {
     parallel_counting_sort(n_seg, n_pose, (const int32_t*)nullptr, frame_seg_list.data(),
                            [&](int32_t sg) { return seg_frame[sg]; });
   } else {
     std::vector<int32_t> c(frame_seg_begin.begin(), frame_seg_begin.end() - 1);
     for (int64_t s = 0; s < n_seg; ++s) frame_seg_list[c[seg_frame[s]]++] = (int32_t)s;
   }
-  parallel_chunks(n_pose, par_host ? std::min(host_threads(n_obs), n_pose) : 1, [&](int64_t f0, int64_t f1, int) {
+  parallel_chunks(n_pose, (par_host || gpu_setup) ? std::min(host_threads(n_obs), n_pose) : 1, [&](int64_t f0, int64_t f1, int) {
     for (int64_t f = f0; f < f1; ++f) {
       int hi = (int)f;
       for (int e = frame_seg_begin[f]; e < frame_seg_begin[f + 1]; ++e) {
@@ -1786,8 +1874,8 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->chol_super = plan.n_super > 0;
   h->n_chain = (int)plan.chain_off.size() - 1;
   frame_win_hi = win;  // K2 windows follow the same (possibly global) coupling
-  h->perm_host = order;
-  h->perm_uploaded = false;
+  h->perm_uploaded = gpu_setup;  // (the device front wrote the permutation itself)
+  if (gpu_setup) h->perm_host.clear();
 
   st_mark("work order+plan");
   // ---- upload (staged: the stream has drained, so the staging buffer is free)
@@ -1801,26 +1889,31 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     ~BatchOff() { h->stage_batch = false; }
   } batch_off{h};
   st_mark("pre-upload sync");
-  std::vector<double> seg_base(2 * n_seg);
-  for (int64_t s = 0; s < n_seg; ++s) {
-    const int64_t r = order[seg_rec_begin[s]];
-    seg_base[2 * s] = obs_xy[2 * r];
-    seg_base[2 * s + 1] = obs_xy[2 * r + 1];
-  }
-  int rc = h->precision == PTZBA_FP32 ? upload_records<float>(h, order, rec_seg, seg_base, obs_xy, obs_weight)
-                                      : upload_records<double>(h, order, rec_seg, seg_base, obs_xy, obs_weight);
-  if (rc) return rc;
-  if (upload_st(h, h->seg_base, seg_base)) return -1;
-  {  // K1's 1-byte segment key: the record's segment within its landmark's window of K1_SEGW segments
-    std::vector<uint8_t> key(n_obs + 4);  // + 4: K1 reads whole 4-record key groups
-    for (int64_t k = 0; k < n_obs; ++k) {
-      const int32_t sg = rec_seg[k];
-      key[k] = (uint8_t)((sg - lm_seg_begin[seg_lm[sg]]) % K1_SEGW);
+  if (!gpu_setup) {  // (the device front has built these on the device)
+    std::vector<double> seg_base(2 * n_seg);
+    for (int64_t s = 0; s < n_seg; ++s) {
+      const int64_t r = order[seg_rec_begin[s]];
+      seg_base[2 * s] = obs_xy[2 * r];
+      seg_base[2 * s + 1] = obs_xy[2 * r + 1];
     }
-    if (upload_st(h, h->rec_key, key)) return -1;
+    int rc = h->precision == PTZBA_FP32 ? upload_records<float>(h, order, rec_seg, seg_base, obs_xy, obs_weight)
+                                        : upload_records<double>(h, order, rec_seg, seg_base, obs_xy, obs_weight);
+    if (rc) return rc;
+    if (upload_st(h, h->seg_base, seg_base)) return -1;
+    {  // K1's 1-byte segment key: the record's segment within its landmark's window of K1_SEGW segments
+      std::vector<uint8_t> key(n_obs + 4);  // + 4: K1 reads whole 4-record key groups
+      for (int64_t k = 0; k < n_obs; ++k) {
+        const int32_t sg = rec_seg[k];
+        key[k] = (uint8_t)((sg - lm_seg_begin[seg_lm[sg]]) % K1_SEGW);
+      }
+      if (upload_st(h, h->rec_key, key)) return -1;
+    }
+    if (upload_st(h, h->rec_seg, rec_seg) || upload_st(h, h->seg_frame, seg_frame) || upload_st(h, h->seg_lm, seg_lm) ||
+        upload_st(h, h->seg_rec_begin, seg_rec_begin))
+      return -1;
+    h->perm_host = std::move(order);
   }
-  if (upload_st(h, h->rec_seg, rec_seg) || upload_st(h, h->seg_frame, seg_frame) || upload_st(h, h->seg_lm, seg_lm) ||
-      upload_st(h, h->seg_rec_begin, seg_rec_begin) || upload_st(h, h->lm_seg_begin, lm_seg_begin) ||
+  if (upload_st(h, h->lm_seg_begin, lm_seg_begin) ||
       upload_st(h, h->lm_order, lm_work) || upload_st(h, h->frame_seg_begin, frame_seg_begin) ||
       upload_st(h, h->frame_seg_list, frame_seg_list) || upload_st(h, h->frame_win_hi, frame_win_hi) ||
       upload_st(h, h->s2_items, s2_items) || upload_st(h, h->s2_groups, s2_groups) || upload_st(h, h->s2_lm, s2_lm) ||

@@ -93,6 +93,9 @@ constexpr int SEGW = K1_SEGW;  // segments per LDS window per wave
 #ifndef K1_DEPTH
 #define K1_DEPTH 2  // fp32 coarsened path: record groups in flight per wave (3: same phase B time, more registers)
 #endif
+#ifndef K1_WPB
+#define K1_WPB 4  // waves (landmarks) per workgroup: the frame tables are staged once per workgroup
+#endif
 #ifndef K1_MIN_WAVES
 #define K1_MIN_WAVES 4  // waves per SIMD the register budget must allow (occupancy)
 #endif
@@ -164,15 +167,15 @@ __device__ long long g_k1_items[32768][8];  // start, end, A, B, C, final, segme
 // FTL: the frame tables are staged in LDS (n_pose <= K1_FT_LDS): phase A's chain is descriptor -> segment frame id
 // -> LDS instead of descriptor -> frame id -> global frame table (one dependent memory latency less per wave)
 template <typename real, int LOSS, bool FTL>
-__global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVES64) void k_linearize(LinArgs a) {
+__global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVES64) void k_linearize(LinArgs a) {
   constexpr bool COARSE = sizeof(real) == 4 ? K1_COARSE : K1_COARSE64;
-  __shared__ real s_x[4][SEGW], s_y[4][SEGW], s_acc[4][4][SEGW];
+  __shared__ real s_x[K1_WPB][SEGW], s_y[K1_WPB][SEGW], s_acc[K1_WPB][4][SEGW];
   __shared__ double s_ft[5][FTL ? K1_FT_LDS : 1];  // ca, sa, cb, sb, f per frame (fp64)
   const int lane = lane_id();
   // wave-uniform by construction: with readfirstlane the compiler sees it, so the descriptor, the ray table, the
   // window and record bounds and the slot offsets are scalar loads / SGPRs (SALU address math, fewer VGPRs)
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int task = blockIdx.x * 4 + wv;
+  const int task = blockIdx.x * K1_WPB + wv;
   if (a.run_if && !*a.run_if) return;  // conditional re-linearisation (device-driven LM): the whole grid leaves
   if constexpr (!FTL) {
     if (task >= a.n_work) return;  // whole wave leaves; no block-level barriers in this variant
@@ -578,14 +581,14 @@ __global__ __launch_bounds__(256, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVE
 template <typename real>
 void launch_linearize(const LinArgs& a, int loss, hipStream_t st) {
   if (a.n_work <= 0) return;
-  dim3 grid((a.n_work + 3) / 4);
+  dim3 grid((a.n_work + K1_WPB - 1) / K1_WPB);
   const bool ftl = a.n_pose <= K1_FT_LDS;  // frame tables staged in LDS (neutral vs global reads, 13 VGPRs fewer)
   if (ftl) {
-    if (loss == 0) hipLaunchKernelGGL((k_linearize<real, 0, true>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((k_linearize<real, 1, true>), grid, dim3(256), 0, st, a);
+    if (loss == 0) hipLaunchKernelGGL((k_linearize<real, 0, true>), grid, dim3(64 * K1_WPB), 0, st, a);
+    else hipLaunchKernelGGL((k_linearize<real, 1, true>), grid, dim3(64 * K1_WPB), 0, st, a);
   } else {
-    if (loss == 0) hipLaunchKernelGGL((k_linearize<real, 0, false>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((k_linearize<real, 1, false>), grid, dim3(256), 0, st, a);
+    if (loss == 0) hipLaunchKernelGGL((k_linearize<real, 0, false>), grid, dim3(64 * K1_WPB), 0, st, a);
+    else hipLaunchKernelGGL((k_linearize<real, 1, false>), grid, dim3(64 * K1_WPB), 0, st, a);
   }
 }
 

@@ -322,4 +322,19 @@ void launch_back_project(int64_t n, double u, double v, double f, double pan, do
 void launch_h_jacobian(int64_t n, double u, double v, double f, double pan, double tilt, const double* disp6,
                        const double* rays, double* H, hipStream_t st);
 
+// setup_kernels.hip: the GPU front of set_problem (large problems; n < 2^31, n_lm * n_pose < 2^32).  Each returns 0 or
+// -1 with fail() set.  setup_sort_runs: order / key_sorted = records in (landmark, frame, index) order, rec_seg = the
+// inclusive scan of the run starts, *n_seg = the number of segments (synchronises the stream).
+int setup_sort_runs(hipStream_t st, int64_t n, int n_pose, int n_lm, const int32_t* frame, const int32_t* lm,
+                    uint32_t* order, uint32_t* key_sorted, int32_t* rec_seg, int64_t* n_seg);
+// rec_seg -> segment ids; seg_frame / seg_lm [n_seg], seg_rec_begin [n_seg + 1], lm_first [n_lm] (landmarks with
+// segments only)
+int setup_fill_segments(hipStream_t st, int64_t n, int n_pose, int64_t n_seg, const uint32_t* key_sorted, int32_t* rec_seg,
+                        int32_t* seg_frame, int32_t* seg_lm, int64_t* seg_rec_begin, int32_t* lm_first);
+// seg_base [2 n_seg] fp64, rec_xy [2 n] / rec_w [n] (w == nullptr: none) in the record precision, rec_key [n], perm [n]
+template <typename real>
+int setup_records(hipStream_t st, int64_t n, int64_t n_seg, const uint32_t* order, const int32_t* rec_seg,
+                  const int32_t* seg_lm, const int64_t* seg_rec_begin, const int32_t* lm_first, const double* xy,
+                  const double* w, double* seg_base, real* rec_xy, real* rec_w, uint8_t* rec_key, int64_t* perm);
+
 }  // namespace ptzba

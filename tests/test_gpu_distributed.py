@@ -171,7 +171,8 @@ def _part_worker(rank, world, port, out_dir, config, precision, loss):
 @pytest.mark.parametrize("config,world,precision,loss,backsolve", [
     ("config2", 2, 0, 0, ""), ("config2", 4, 0, 0, ""), ("grid", 2, 0, 0, ""), ("grid", 4, 0, 0, ""),
     ("grid", 2, 0, 0, "blk"), ("config3", 2, 0, 0, ""), ("config3", 2, 1, 1, ""), ("config3", 3, 0, 0, ""),
-    ("config3", 4, 0, 0, ""), ("config3", 8, 0, 0, ""), ("config4", 2, 1, 1, ""), ("config4", 4, 1, 1, "")])
+    ("config3", 4, 0, 0, ""), ("config3", 8, 0, 0, ""), ("config4", 2, 1, 1, ""), ("config4", 4, 1, 1, ""),
+    ("config4", 8, 1, 1, "")])
 def test_part_owned_gpu_solve_matches_single_rank(gpu_available, tmp_path, monkeypatch, config, world, precision, loss,
                                                   backsolve):
     """libptzba's part-owned (rank-tree) solve on one device (ranks over gloo): every rank factors its base (own
@@ -182,7 +183,8 @@ def test_part_owned_gpu_solve_matches_single_rank(gpu_available, tmp_path, monke
     Schur sums round differently).  config 3 = the headline problem in the two-level order: at 3 ranks ranks 0 / 1
     own the first half's leaves (X_SUB over them) and rank 2 the second half, at 4 each rank owns a leaf, at 8 pairs
     share the leaves (X_PART, X_SUB and X_SEP all run);
-    grid / config 4 = keyframes on tilt rows (config 4: 410M records, 3 LM iterations; at 4 ranks two per part).
+    grid / config 4 = keyframes on tilt rows (config 4: 410M records, 3 LM iterations; at 4 ranks two per part; at 8,
+    BASELINE's world size, pairs share the leaves: X_PART, X_SUB and X_SEP).
     backsolve "blk": the blocked back substitution on the grid's one-chain plans and on the single-rank plan."""
     import ptzba
     import synthetic
