@@ -1758,19 +1758,19 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     max_seg = std::max(max_seg, ns);
   }
   {
-    // stable counting sort by record count, descending (the order std::stable_sort with `more records first` gives)
+    // heaviest first (LPT over the workgroup slots) at 1/8-octave resolution of the record count, and inside such a
+    // size class by first frame: a K1 workgroup's landmarks then see neighbouring frames, so it stages ~a coupling
+    // window of frame tables instead of the whole table (ba_kernels.hip FTL)
     auto nrec = [&](int l) { return seg_rec_begin[lm_seg_begin[l + 1]] - seg_rec_begin[lm_seg_begin[l]]; };
-    int64_t mx = 0;
-    for (int l : lm_order) mx = std::max(mx, nrec(l));
-    if (mx <= 4 * (int64_t)lm_order.size() + 1024) {
-      std::vector<int32_t> c((size_t)mx + 2, 0), srt(lm_order.size());
-      for (int l : lm_order) c[mx - nrec(l) + 1]++;
-      for (int64_t q = 0; q <= mx; ++q) c[q + 1] += c[q];
-      for (int l : lm_order) srt[c[mx - nrec(l)]++] = l;
-      lm_order.swap(srt);
-    } else {
-      std::stable_sort(lm_order.begin(), lm_order.end(), [&](int a, int b) { return nrec(a) > nrec(b); });
-    }
+    auto size_class = [&](int l) {
+      const uint64_t c = (uint64_t)nrec(l);
+      if (c < 16) return (int)c;
+      const int msb = 63 - __builtin_clzll(c);
+      return 16 + 8 * (msb - 4) + (int)((c >> (msb - 3)) & 7);
+    };
+    std::vector<int64_t> key(n_landmark, 0);
+    for (int l : lm_order) key[l] = ((int64_t)(1 << 20) - size_class(l)) * ((int64_t)1 << 40) + ((int64_t)lm_meta[4 * l] << 20);
+    std::sort(lm_order.begin(), lm_order.end(), [&](int a, int b) { return key[a] != key[b] ? key[a] < key[b] : a < b; });
   }
   h->n_work = (int)lm_order.size();
   h->max_seg_per_lm = max_seg;

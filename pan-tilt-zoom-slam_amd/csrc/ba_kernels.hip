@@ -192,20 +192,32 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
   const int tq = FTL ? min(task, a.n_work - 1) : task;
   const int4 wd = a.lm_work[2 * tq];
   const int4 wm = a.lm_work[2 * tq + 1];
+  int fbase = 0;  // FTL: the first staged frame (s_ft[k][fs - fbase])
   if constexpr (FTL) {
-    // the whole frame table (<= 640 frames, 20 KB at config 3), requested beside the descriptor: both latencies
-    // overlap, and the barrier below is the block's only one
+    // the frames the workgroup's landmarks see, [min first frame, max last frame] over its K1_WPB descriptors (scalar
+    // loads; the work order keeps a workgroup's landmarks close in frame order, so this is ~a coupling window, not the
+    // whole table); the barrier below is the block's only one
+    int fmax = -1;
+    fbase = a.n_pose;
+#pragma unroll
+    for (int q = 0; q < K1_WPB; ++q) {
+      const int4 m = a.lm_work[2 * min((int)blockIdx.x * K1_WPB + q, a.n_work - 1) + 1];
+      fbase = min(fbase, m.x);
+      fmax = max(fmax, m.y);
+    }
     const double4* src = reinterpret_cast<const double4*>(a.ft64);
-    for (int e = threadIdx.x; e < a.n_pose; e += blockDim.x) {
+    for (int e = fbase + (int)threadIdx.x; e <= fmax; e += blockDim.x) {
       const double4 t0 = src[2 * e];
       const double f = reinterpret_cast<const double*>(a.ft64)[8 * e + 4];
-      s_ft[0][e] = t0.x; s_ft[1][e] = t0.y; s_ft[2][e] = t0.z; s_ft[3][e] = t0.w; s_ft[4][e] = f;
+      const int el = e - fbase;
+      s_ft[0][el] = t0.x; s_ft[1][el] = t0.y; s_ft[2][el] = t0.z; s_ft[3][el] = t0.w; s_ft[4][el] = f;
     }
     __syncthreads();
     if (task >= a.n_work) return;  // whole wave leaves after the barrier
   }
   auto ft_lds = [&](int fs) {
     FrameTab<double> F;
+    fs -= fbase;
     F.ca = s_ft[0][fs]; F.sa = s_ft[1][fs]; F.cb = s_ft[2][fs]; F.sb = s_ft[3][fs]; F.f = s_ft[4][fs];
     F.pad0 = F.pad1 = F.pad2 = 0.0;
     return F;
@@ -522,8 +534,9 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
       if constexpr (FTL) {
         // the record-precision table is the rounded fp64 one (k_tables): the same values as ft[fs]
         FrameTab<real> F;
-        F.ca = (real)s_ft[0][fs]; F.sa = (real)s_ft[1][fs]; F.cb = (real)s_ft[2][fs]; F.sb = (real)s_ft[3][fs];
-        F.f = (real)s_ft[4][fs];
+        const int fl = fs - fbase;
+        F.ca = (real)s_ft[0][fl]; F.sa = (real)s_ft[1][fl]; F.cb = (real)s_ft[2][fl]; F.sb = (real)s_ft[3][fl];
+        F.f = (real)s_ft[4][fl];
         F.pad0 = F.pad1 = F.pad2 = (real)0;
         ptz_project_jac<real>(F, R, u, v, x, y, J);
       } else {
