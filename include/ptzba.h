@@ -313,8 +313,12 @@ PTZBA_EXPORT int ptzba_sync(ptzba_handle h);
  * 0 off); bits 8-15 = sampling stride s (0/1: every launch): a group records its event pair around
  * every s-th launch only.  Each recorded event adds a few-microsecond gap to the stream.
  * PTZBA_TIME_FLUSH (bit 16): cold-cache K1 timing -- before each timed K1 launch a kernel writes a
- * 1 GiB scratch buffer (larger than L2 + the 256 MB Infinity Cache), outside the timed event pair. */
+ * 1 GiB scratch buffer (larger than L2 + the 256 MB Infinity Cache), outside the timed event pair; the
+ * caches are left full of dirty lines, whose write-backs then run during the timed launch.
+ * PTZBA_TIME_FLUSH_READ (bit 17, with bit 16): the scratch buffer is READ instead -- the caches hold
+ * clean unrelated lines, so the timed launch pays its own HBM traffic only. */
 #define PTZBA_TIME_FLUSH 0x10000
+#define PTZBA_TIME_FLUSH_READ 0x20000
 PTZBA_EXPORT int ptzba_kernel_times(ptzba_handle h, double* ms_out /*4*/, int64_t* count_out /*4*/);
 PTZBA_EXPORT int ptzba_reset_kernel_times(ptzba_handle h, int enable);
 

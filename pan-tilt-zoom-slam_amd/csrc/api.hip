@@ -133,6 +133,7 @@ struct ptzba_ctx {
   bool tm_sampled[TM_N] = {false, false, false, false};
   int tm_stride = 1;
   bool tm_flush = false;  // cold-cache timing: stream a scratch buffer through the caches before each timed K1
+  bool tm_flush_read = false;  // ... by reading it (clean lines) instead of writing it
   DBuf flush_buf;
 
   // multi-GPU (include/ptzba.h): exchanges done by the library, part-owned solve state
@@ -201,6 +202,17 @@ __global__ void __launch_bounds__(256) k_flush_caches(float4* buf, int64_t n16, 
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x)
     buf[i] = make_float4(v, v, v, v);
 }
+// the read flush: streams the scratch buffer (filled once by k_flush_caches) through the caches, leaving clean lines;
+// the sum is stored only if it equals an impossible value (the buffer holds small positive numbers), which keeps the
+// loads alive
+__global__ void __launch_bounds__(256) k_flush_caches_read(float4* buf, int64_t n16, float v) {
+  float s = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 x = buf[i];
+    s += x.x + x.y + x.z + x.w;
+  }
+  if (s == -v) buf[0] = make_float4(s, s, s, s);
+}
 constexpr size_t FLUSH_BYTES = (size_t)1 << 30;
 
 // a timed group records an event pair around every tm_stride-th launch (each record adds a gap to the
@@ -210,9 +222,13 @@ static void tm_begin(ptzba_ctx* h, int k) {
   if (!((h->timing >> k) & 1) || h->ev_used[k] + 2 > (int)h->ev[k].size()) return;
   if (h->tm_seen[k]++ % h->tm_stride != 0) return;
   h->tm_sampled[k] = true;
-  if (k == TM_K1 && h->tm_flush && h->flush_buf.p)
-    k_flush_caches<<<4096, 256, 0, h->st>>>(h->flush_buf.as<float4>(), (int64_t)(h->flush_buf.bytes / 16),
-                                             (float)h->tm_seen[k]);
+  if (k == TM_K1 && h->tm_flush && h->flush_buf.p) {
+    if (h->tm_flush_read)
+      k_flush_caches_read<<<4096, 256, 0, h->st>>>(h->flush_buf.as<float4>(), (int64_t)(h->flush_buf.bytes / 16), 1.0f);
+    else
+      k_flush_caches<<<4096, 256, 0, h->st>>>(h->flush_buf.as<float4>(), (int64_t)(h->flush_buf.bytes / 16),
+                                               (float)h->tm_seen[k]);
+  }
   (void)hipEventRecord(h->ev[k][h->ev_used[k]], h->st);
 }
 static void tm_end(ptzba_ctx* h, int k) {
@@ -2838,7 +2854,12 @@ int ptzba_reset_kernel_times(ptzba_handle h, int enable) {
   h->timing = enable & ((1 << TM_N) - 1);
   h->tm_stride = std::max(1, (enable >> 8) & 0xff);
   h->tm_flush = (enable & PTZBA_TIME_FLUSH) != 0;
-  if (h->tm_flush && !h->flush_buf.p && h->flush_buf.alloc(FLUSH_BYTES)) return -1;
+  h->tm_flush_read = h->tm_flush && (enable & PTZBA_TIME_FLUSH_READ) != 0;
+  if (h->tm_flush && !h->flush_buf.p) {
+    if (h->flush_buf.alloc(FLUSH_BYTES)) return -1;
+    k_flush_caches<<<4096, 256, 0, h->st>>>(h->flush_buf.as<float4>(), (int64_t)(FLUSH_BYTES / 16), 1.0f);
+    HIPCHK(hipGetLastError());
+  }
   if (!h->tm_flush) h->flush_buf.release();
   return 0;
 }

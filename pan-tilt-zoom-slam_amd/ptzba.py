@@ -70,6 +70,7 @@ class ptzba_report(Structure):
 
 
 TIME_FLUSH = 0x10000  # include/ptzba.h PTZBA_TIME_FLUSH: cold-cache K1 timing
+TIME_FLUSH_READ = 0x20000  # include/ptzba.h PTZBA_TIME_FLUSH_READ: ... by a read flush (clean caches)
 
 
 class ptzba_problem_opts(Structure):
@@ -1108,8 +1109,10 @@ class BAHandle:
     def reset_kernel_times(self, enable=True, groups=0xF, stride=1, flush=False):
         """Restart kernel timing; `groups` bitmask: 1 K1, 2 Schur, 4 Cholesky solve, 8 back-substitution;
         events around every `stride`-th launch of a group (each event record adds a gap to the stream).
-        flush: cold-cache K1 timing (a 1 GiB scratch write before each timed K1 launch, outside the events)."""
-        flags = (int(groups) | (max(1, min(255, int(stride))) << 8) | (TIME_FLUSH if flush else 0)) if enable else 0
+        flush: cold-cache K1 timing, a 1 GiB scratch buffer streamed through the caches before each timed K1 launch
+        (outside the events): True / "write" writes it (dirty lines left behind), "read" reads it (clean lines)."""
+        fl = (TIME_FLUSH | (TIME_FLUSH_READ if flush == "read" else 0)) if flush else 0
+        flags = (int(groups) | (max(1, min(255, int(stride))) << 8) | fl) if enable else 0
         _check(lib().ptzba_reset_kernel_times(self.h, flags), "ptzba_reset_kernel_times")
 
     def kernel_times(self):
