@@ -2064,11 +2064,14 @@ int ptzba_problem_info(ptzba_handle h, int64_t* info) {
 static void* ft_real(ptzba_ctx* h) { return h->precision == PTZBA_FP32 ? h->ft.p : h->ft64.p; }
 static void* rt_real(ptzba_ctx* h) { return h->precision == PTZBA_FP32 ? h->rt.p : h->rt64.p; }
 
-static void tables(ptzba_ctx* h, const double* ptz, const double* rays, const int* run_if = nullptr) {
+static void tables(ptzba_ctx* h, const double* ptz, const double* rays, const int* run_if = nullptr,
+                   double* zero = nullptr, int n_zero = 0) {
   if (h->precision == PTZBA_FP32)
-    launch_tables<float>(ptz, rays, h->n_pose, h->n_lm, h->ft64.p, h->rt64.p, h->ft.p, h->rt.p, run_if, h->st);
+    launch_tables<float>(ptz, rays, h->n_pose, h->n_lm, h->ft64.p, h->rt64.p, h->ft.p, h->rt.p, run_if, h->st, zero,
+                         n_zero);
   else
-    launch_tables<double>(ptz, rays, h->n_pose, h->n_lm, h->ft64.p, h->rt64.p, h->ft64.p, h->rt64.p, run_if, h->st);
+    launch_tables<double>(ptz, rays, h->n_pose, h->n_lm, h->ft64.p, h->rt64.p, h->ft64.p, h->rt64.p, run_if, h->st, zero,
+                          n_zero);
 }
 
 // sel != nullptr (device-driven LM): the kernel writes slot (*sel ^ sel_xor), chosen on the device
@@ -2261,9 +2264,9 @@ static int ensure_group_comms(ptzba_ctx* h) {
 int ptzba_linearize(ptzba_handle h) {
   if (!h || !h->have_problem) return fail("no problem set");
   HIPCHK(hipSetDevice(h->device));
-  tables(h, h->ptz.as<double>(), h->rays.as<double>());
+  // the scalar block is zeroed by the tables launch (one launch less than a memset)
+  tables(h, h->ptz.as<double>(), h->rays.as<double>(), nullptr, h->scal.as<double>(), (int)(h->scal.bytes / 8));
   linearize_into(h, h->cur);
-  HIPCHK(hipMemsetAsync(h->scal.p, 0, h->scal.bytes, h->st));
   launch_reduce_cols(h->lm_out[h->cur].as<double>() + 5, h->n_lm, 8, 1, 0, h->scal.as<double>(),
                      h->red_scratch.as<double>(), h->st);
   HIPCHK(hipGetLastError());

@@ -35,9 +35,10 @@ template <typename real>
 __global__ void k_tables(const double* __restrict__ ptz, const double* __restrict__ rays, int n_pose,
                          int n_lm, FrameTab<double>* __restrict__ ft64, RayTab<double>* __restrict__ rt64,
                          FrameTab<real>* __restrict__ ft, RayTab<real>* __restrict__ rt,
-                         const int* __restrict__ run_if) {
+                         const int* __restrict__ run_if, double* __restrict__ zero, int n_zero) {
   if (run_if && !*run_if) return;
   int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_zero) zero[i] = 0.0;  // (ptzba_linearize: the scalar block, instead of a memset launch)
   if (i < n_pose) {
     FrameTab<double> t = make_frame_tab<double>(ptz[3 * i], ptz[3 * i + 1], ptz[3 * i + 2]);
     ft64[i] = t;
@@ -62,10 +63,11 @@ __global__ void k_tables(const double* __restrict__ ptz, const double* __restric
 
 template <typename real>
 void launch_tables(const double* ptz, const double* rays, int n_pose, int n_lm, void* ft64, void* rt64, void* ft,
-                   void* rt, const int* run_if, hipStream_t st) {
-  int n = n_pose + n_lm;
+                   void* rt, const int* run_if, hipStream_t st, double* zero, int n_zero) {
+  int n = std::max(n_pose + n_lm, n_zero);
   hipLaunchKernelGGL(k_tables<real>, dim3((n + 255) / 256), dim3(256), 0, st, ptz, rays, n_pose, n_lm,
-                     (FrameTab<double>*)ft64, (RayTab<double>*)rt64, (FrameTab<real>*)ft, (RayTab<real>*)rt, run_if);
+                     (FrameTab<double>*)ft64, (RayTab<double>*)rt64, (FrameTab<real>*)ft, (RayTab<real>*)rt, run_if,
+                     zero, n_zero);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1153,9 +1155,9 @@ void launch_lm_commit(const LMDev* st, double* ptz, const double* ptz_trial, int
 
 // explicit instantiations
 template void launch_tables<float>(const double*, const double*, int, int, void*, void*, void*, void*, const int*,
-                                   hipStream_t);
+                                   hipStream_t, double*, int);
 template void launch_tables<double>(const double*, const double*, int, int, void*, void*, void*, void*, const int*,
-                                    hipStream_t);
+                                    hipStream_t, double*, int);
 template void launch_linearize<float>(const LinArgs&, int, hipStream_t);
 template void launch_linearize<double>(const LinArgs&, int, hipStream_t);
 template void launch_trial<float>(const BacksubArgs&, const double*, const double*, const double*, double*, double*, int,

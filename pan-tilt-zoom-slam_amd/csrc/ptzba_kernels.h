@@ -208,7 +208,7 @@ struct DecideArgs {
 
 template <typename real>
 void launch_tables(const double* ptz, const double* rays, int n_pose, int n_lm, void* ft64, void* rt64, void* ft, void* rt,
-                   const int* run_if, hipStream_t st);
+                   const int* run_if, hipStream_t st, double* zero = nullptr, int n_zero = 0);  // zero[0, n_zero) = 0
 template <typename real>
 void launch_linearize(const LinArgs& a, int loss, hipStream_t st);
 template <typename real>
