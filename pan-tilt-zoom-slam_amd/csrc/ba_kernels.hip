@@ -24,6 +24,8 @@
 // blocks are formed once per segment.
 #include "../../include/ptzba.h"
 #include "ptzba_common.h"
+#include <hip/hip_ext.h>
+
 #include "ptzba_kernels.h"
 
 namespace ptzba {
@@ -594,16 +596,20 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
 }
 
 template <typename real>
-void launch_linearize(const LinArgs& a, int loss, hipStream_t st) {
+void launch_linearize(const LinArgs& a, int loss, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
   if (a.n_work <= 0) return;
   dim3 grid((a.n_work + K1_WPB - 1) / K1_WPB);
   const bool ftl = a.n_pose <= K1_FT_LDS;  // frame tables staged in LDS (neutral vs global reads, 13 VGPRs fewer)
+  auto go = [&](auto kern) {
+    if (ev0) hipExtLaunchKernelGGL(kern, grid, dim3(64 * K1_WPB), 0, st, ev0, ev1, 0, a);
+    else hipLaunchKernelGGL(kern, grid, dim3(64 * K1_WPB), 0, st, a);
+  };
   if (ftl) {
-    if (loss == 0) hipLaunchKernelGGL((k_linearize<real, 0, true>), grid, dim3(64 * K1_WPB), 0, st, a);
-    else hipLaunchKernelGGL((k_linearize<real, 1, true>), grid, dim3(64 * K1_WPB), 0, st, a);
+    if (loss == 0) go(k_linearize<real, 0, true>);
+    else go(k_linearize<real, 1, true>);
   } else {
-    if (loss == 0) hipLaunchKernelGGL((k_linearize<real, 0, false>), grid, dim3(64 * K1_WPB), 0, st, a);
-    else hipLaunchKernelGGL((k_linearize<real, 1, false>), grid, dim3(64 * K1_WPB), 0, st, a);
+    if (loss == 0) go(k_linearize<real, 0, false>);
+    else go(k_linearize<real, 1, false>);
   }
 }
 
@@ -1158,8 +1164,8 @@ template void launch_tables<float>(const double*, const double*, int, int, void*
                                    hipStream_t, double*, int);
 template void launch_tables<double>(const double*, const double*, int, int, void*, void*, void*, void*, const int*,
                                     hipStream_t, double*, int);
-template void launch_linearize<float>(const LinArgs&, int, hipStream_t);
-template void launch_linearize<double>(const LinArgs&, int, hipStream_t);
+template void launch_linearize<float>(const LinArgs&, int, hipStream_t, hipEvent_t, hipEvent_t);
+template void launch_linearize<double>(const LinArgs&, int, hipStream_t, hipEvent_t, hipEvent_t);
 template void launch_trial<float>(const BacksubArgs&, const double*, const double*, const double*, double*, double*, int,
                                   void*, void*, void*, void*, hipStream_t, const uint8_t*, const int*);
 template void launch_trial<double>(const BacksubArgs&, const double*, const double*, const double*, double*, double*,

@@ -210,7 +210,9 @@ template <typename real>
 void launch_tables(const double* ptz, const double* rays, int n_pose, int n_lm, void* ft64, void* rt64, void* ft, void* rt,
                    const int* run_if, hipStream_t st, double* zero = nullptr, int n_zero = 0);  // zero[0, n_zero) = 0
 template <typename real>
-void launch_linearize(const LinArgs& a, int loss, hipStream_t st);
+// ev0 / ev1 != nullptr: the launch carries the event pair itself (hipExtLaunchKernelGGL: the kernel packet's own
+// start / end timestamps, no marker packets around it)
+void launch_linearize(const LinArgs& a, int loss, hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 template <typename real>
 void launch_schur(const SchurArgs& a, int n_items, int n_groups, int n_fixed, hipStream_t st);
 // scratch: RED_SCRATCH doubles (partials + counter), zero-initialised once, reused across calls
