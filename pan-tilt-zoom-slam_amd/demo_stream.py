@@ -55,6 +55,10 @@ def run_stream(slam, scene, n_frames, camera0, keyframe_every=None, on_frame=Non
             lr = sys.modules.get("bundle_adjustment")
             if lr is not None and getattr(lr, "LAST_RESULT", None):
                 rec.setdefault("kf_timing", []).append(dict(lr.LAST_RESULT.get("timing", {})))
+                res = lr.LAST_RESULT.get("result")
+                rec.setdefault("kf_lm", []).append(
+                    (int(getattr(res, "njev", 0)), int(getattr(res, "nfev", 0)), int(getattr(res, "status", 0)),
+                     int(lr.LAST_RESULT.get("n_residual", 0))))
         t2 = time.perf_counter()
         cam = slam.cameras[i] if i < len(slam.cameras) else slam.current_camera
         rec["ptz"].append([cam.pan, cam.tilt, cam.focal_length])
@@ -161,6 +165,15 @@ def main():
         kall = rec.get("kf_timing", [])  # one per in-loop keyframe, as tk
         if len(kall) == len(tk):  # the slowest keyframe call's own breakdown
             out["keyframe_ba_slowest_breakdown_ms"] = {k: 1e3 * float(kall[int(np.argmax(tk))].get(k, 0.0)) for k in keys}
+    lm = rec.get("kf_lm", [])
+    if lm and len(lm) == len(tk):  # the LM of each keyframe call: iterations (njev), evaluations (nfev), status
+        a_lm = np.asarray(lm)
+        out["keyframe_lm"] = {"njev_mean": float(a_lm[:, 0].mean()), "njev_max": int(a_lm[:, 0].max()),
+                              "nfev_mean": float(a_lm[:, 1].mean()), "nfev_max": int(a_lm[:, 1].max()),
+                              "slowest": {"njev": int(a_lm[int(np.argmax(tk)), 0]), "nfev": int(a_lm[int(np.argmax(tk)), 1]),
+                                          "status": int(a_lm[int(np.argmax(tk)), 2]),
+                                          "residuals": int(a_lm[int(np.argmax(tk)), 3])},
+                              "per_keyframe": [list(map(int, r)) for r in lm]}
     print(json.dumps(out))
 
 
