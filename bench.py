@@ -61,8 +61,9 @@ def parse():
     ap.add_argument("--no-secondary", action="store_true", help="skip the fp64 / linear-loss leg")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache K1 pass")
     ap.add_argument("--dry-run", action="store_true", help="launcher / rendezvous plumbing only (no GPU work)")
-    ap.add_argument("--stream-frames", type=int, default=100,
-                    help="config-5 leg: frames of demo_stream.py after the headline (0: skip)")
+    ap.add_argument("--stream-frames", type=int, default=300,
+                    help="config-5 leg: frames of demo_stream.py after the headline (0: skip); 300 = 60 keyframes, so the "
+                         "30-keyframe sliding window is full for the second half (100 frames never fill it)")
     return ap.parse_args()
 
 

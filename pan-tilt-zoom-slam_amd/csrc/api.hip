@@ -75,6 +75,8 @@ struct ptzba_ctx {
   DBuf scal, info;  // scal: [8 partial scalars | 8 pose partials ("loc")], contiguous for one exchange
   DBuf scal_pack;               // device block [scal 8 | loc 8 | info]
   double* scal_host = nullptr;   // pinned host copy of scal_pack
+  uint8_t* out_pin = nullptr;    // pinned landing buffer of ptzba_get_state (grown, kept)
+  size_t out_pin_cap = 0;
   DBuf chol_tasks, Ldiag, Minv, dpose;  // Minv: inverses of the diagonal factor tiles (back-substitution)
   std::vector<int> chol_task_off;  // host: per elimination level, offsets into chol_tasks
   DBuf Lsub;                       // supercolumn plans: L_k+1,k of each pair until the next level copies it (chol_super)
@@ -268,6 +270,7 @@ void ptzba_delete(ptzba_handle h) {
     for (auto e : h->ev[k]) (void)hipEventDestroy(e);
   if (h->own) (void)hipStreamDestroy(h->own);
   if (h->scal_host) (void)hipHostFree(h->scal_host);
+  if (h->out_pin) (void)hipHostFree(h->out_pin);
   if (h->bsp_err) (void)hipHostFree(h->bsp_err);
   if (h->stage) (void)hipHostFree(h->stage);
   h->drop_groups();
@@ -2214,10 +2217,27 @@ int ptzba_restore_state(ptzba_handle h) {
 int ptzba_get_state(ptzba_handle h, double* ptz, double* rays) {
   if (!h || !h->have_problem) return fail("no problem set");
   HIPCHK(hipSetDevice(h->device));
-  SyncOnExit sync_guard{h->st};  // caller buffers: no copy outlives the call, also on errors
-  if (ptz) HIPCHK(hipMemcpyAsync(ptz, h->ptz.p, 3 * (size_t)h->n_pose * 8, hipMemcpyDeviceToHost, h->st));
-  if (rays && h->n_lm) HIPCHK(hipMemcpyAsync(rays, h->rays.p, 2 * (size_t)h->n_lm * 8, hipMemcpyDeviceToHost, h->st));
+  SyncOnExit sync_guard{h->st};  // no copy outlives the call, also on errors
+  // through a pinned landing buffer kept by the handle: a pageable destination sent the copy down the runtime's
+  // pageable path, whose cost jumped at some sizes (a 30-KF stream's keyframe call: 0.4 -> 6 ms once)
+  const size_t nb_ptz = ptz ? 3 * (size_t)h->n_pose * 8 : 0, nb_rays = (rays && h->n_lm) ? 2 * (size_t)h->n_lm * 8 : 0;
+  if (nb_ptz + nb_rays == 0) return 0;
+  if (h->out_pin_cap < nb_ptz + nb_rays) {
+    if (h->out_pin) {
+      HIPCHK(hipStreamSynchronize(h->st));
+      HIPCHK(hipHostFree(h->out_pin));
+      h->out_pin = nullptr;
+      h->out_pin_cap = 0;
+    }
+    const size_t cap = (nb_ptz + nb_rays) + (nb_ptz + nb_rays) / 2 + 4096;
+    HIPCHK(hipHostMalloc((void**)&h->out_pin, cap, hipHostMallocDefault));
+    h->out_pin_cap = cap;
+  }
+  if (nb_ptz) HIPCHK(hipMemcpyAsync(h->out_pin, h->ptz.p, nb_ptz, hipMemcpyDeviceToHost, h->st));
+  if (nb_rays) HIPCHK(hipMemcpyAsync(h->out_pin + nb_ptz, h->rays.p, nb_rays, hipMemcpyDeviceToHost, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
+  if (nb_ptz) std::memcpy(ptz, h->out_pin, nb_ptz);
+  if (nb_rays) std::memcpy(rays, h->out_pin + nb_ptz, nb_rays);
   return 0;
 }
 
