@@ -76,27 +76,8 @@ void launch_tables(const double* ptz, const double* rays, int n_pose, int n_lm, 
 // K1: linearize (residual + Jacobian + per-segment / per-landmark normal-equation blocks + cost)
 // ------------------------------------------------------------------------------------------------
 constexpr int SEGW = K1_SEGW;  // segments per LDS window per wave
-#ifndef K1_UNROLL
-#define K1_UNROLL 3  // record batches per group (two groups in flight per wave)
-#endif
-#ifndef K1_COARSE
-#define K1_COARSE 1  // 0: 1 record per lane per batch; 1: 4 records per lane per batch, one scan per 256 records
-#endif
-#ifndef K1_COARSE64
-#define K1_COARSE64 K1_COARSE  // the same choice for the fp64 instantiation
-#endif
-#ifndef K1_TAIL_ATOMIC
-#define K1_TAIL_ATOMIC 0  // 1: tail-run adds of the coarsened reduction as LDS atomics (7 us slower at config 3)
-#endif
-#ifndef K1_TAIL_ORDER
-#define K1_TAIL_ORDER 1  // 1: lgkmcnt(0) before the tail read-modify-write (ordered by completion); 0: issue order
-#endif
-#ifndef K1_FTV_LATE
-#define K1_FTV_LATE 0  // 1: phase C loads its frame tables itself (frees registers; measured slower)
-#endif
-#ifndef K1_DEPTH
-#define K1_DEPTH 2  // fp32 coarsened path: record groups in flight per wave (3: same phase B time, more registers)
-#endif
+// (Round 5 removed the measured-slower build variants: one record per lane (K1_COARSE 0), three record groups in
+// flight (K1_DEPTH 3), LDS-atomic tail runs, issue-order tails and phase C's own table loads (K1_FTV_LATE))
 #ifndef K1_WPB
 #define K1_WPB 4  // waves (landmarks) per workgroup: the frame tables are staged once per workgroup
 #endif
@@ -172,7 +153,6 @@ __device__ long long g_k1_items[32768][8];  // start, end, A, B, C, final, segme
 // -> LDS instead of descriptor -> frame id -> global frame table (one dependent memory latency less per wave)
 template <typename real, int LOSS, bool FTL>
 __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVES64) void k_linearize(LinArgs a) {
-  constexpr bool COARSE = sizeof(real) == 4 ? K1_COARSE : K1_COARSE64;
   __shared__ real s_x[K1_WPB][SEGW], s_y[K1_WPB][SEGW], s_acc[K1_WPB][4][SEGW];
   __shared__ double s_ft[5][FTL ? K1_FT_LDS : 1];  // ca, sa, cb, sb, f per frame (fp64)
   const int lane = lane_id();
@@ -251,86 +231,7 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
 
   double V00 = 0, V01 = 0, V11 = 0, g0 = 0, g1 = 0, cost = 0;
 
-  // phase B record group: K1_UNROLL batches of 64 records (1-byte segment key, obs delta x, y, weight).
-  // Loads are unconditional (index clamped to the window's last record: lanes past the end re-read a
-  // line already fetched, not the next landmark's records), validity is recomputed where the group is
-  // consumed: a conditional load would merge at a join and force its wait early.
-  struct Grp {
-    int key[K1_UNROLL];
-    real ox[K1_UNROLL], oy[K1_UNROLL], wt[K1_UNROLL];
-  };
-  auto load_grp = [&](Grp& g, int64_t rb, int64_t r1) {
-#pragma unroll
-    for (int u = 0; u < K1_UNROLL; ++u) {
-      const int64_t r = min(rb + u * WAVE + lane, r1 - 1);
-      g.key[u] = a.rec_key[r];
-      if constexpr (sizeof(real) == 4) {
-        const float2 o = reinterpret_cast<const float2*>(rec_xy)[r];
-        g.ox[u] = o.x; g.oy[u] = o.y;
-      } else {
-        const double2 o = reinterpret_cast<const double2*>(rec_xy)[r];
-        g.ox[u] = o.x; g.oy[u] = o.y;
-      }
-      g.wt[u] = rec_w ? rec_w[r] : (real)1;
-    }
-  };
-  auto consume = [&](const Grp& g, int64_t rb, int64_t r1) {
-#pragma unroll
-    for (int u = 0; u < K1_UNROLL; ++u) {
-      if (rb + u * WAVE >= r1) break;  // wave-uniform
-      const bool valid = rb + u * WAVE + lane < r1;
-      const int key = valid ? g.key[u] : -1;
-      real rx = 0, ry = 0;
-      if (valid) {
-        rx = sx[key] - g.ox[u];
-        ry = sy[key] - g.oy[u];
-      }
-      const real wt = valid ? g.wt[u] : (real)0;
-      real wx, wy, c, hx, hy;
-      if constexpr (LOSS == 0) {
-        wx = wt; wy = wt;
-        hx = wt; hy = wt;
-        c = wt * (rx * rx + ry * ry);
-      } else {
-        // scipy 'huber': rho(z) = z (z<=1), 2 sqrt(z) - 1; weight rho'(z) = 1 or 1/sqrt(z); curvature weight
-        // hc rho'(z) beyond the unit (hc = 1: IRLS; scipy's own rho' + 2 rho'' z is 0 there)
-        real zx = rx * rx * ifs2, zy = ry * ry * ifs2;
-        bool ix = zx <= (real)1, iy = zy <= (real)1;
-        real sqx, sqy;
-        if constexpr (sizeof(real) == 4) {  // v_rsq_f32: 1 ulp, no IEEE divide in the record loop
-          const real rsx = __builtin_amdgcn_rsqf(ix ? (real)1 : zx), rsy = __builtin_amdgcn_rsqf(iy ? (real)1 : zy);
-          sqx = zx * rsx; sqy = zy * rsy;
-          wx = ix ? wt : wt * rsx;
-          wy = iy ? wt : wt * rsy;
-        } else {
-          sqx = sqrt(zx); sqy = sqrt(zy);
-          wx = ix ? wt : wt / sqx;
-          wy = iy ? wt : wt / sqy;
-        }
-        c = wt * fs2 * ((ix ? zx : (real)2 * sqx - (real)1) + (iy ? zy : (real)2 * sqy - (real)1));
-        hx = ix ? wx : wx * hc;
-        hy = iy ? wy : wy * hc;
-      }
-      cost += (double)c;
-      real v0 = hx, v1 = hy, v2 = wx * rx, v3 = wy * ry;
-      // segmented inclusive scan over the wave, segments = runs of equal key (records are sorted):
-      // shifts 1, 2, 4, 8 inside each 16-lane row, then row 15 -> rows 1, 3 and lane 31 -> rows 2, 3
-      const int kenc = key + 2;  // >= 1; 0 is what a masked / out-of-row DPP source reads
-      seg_scan_step<DPP_ROW_SHR1, 0xf>(kenc, v0, v1, v2, v3);
-      seg_scan_step<DPP_ROW_SHR2, 0xf>(kenc, v0, v1, v2, v3);
-      seg_scan_step<DPP_ROW_SHR4, 0xf>(kenc, v0, v1, v2, v3);
-      seg_scan_step<DPP_ROW_SHR8, 0xf>(kenc, v0, v1, v2, v3);
-      seg_scan_step<DPP_ROW_BCAST15, 0xa>(kenc, v0, v1, v2, v3);
-      seg_scan_step<DPP_ROW_BCAST31, 0xc>(kenc, v0, v1, v2, v3);
-      const int knext = dpp_i<DPP_WAVE_SHL1, 0xf>(kenc);  // lane 63 reads 0
-      const bool last = knext != kenc;
-      if (valid && last) {  // one writer per run per batch; runs crossing batches add in order
-        acc0[key] += v0; acc1[key] += v1; acc2[key] += v2; acc3[key] += v3;
-      }
-    }
-  };
-
-  // thread-coarsened variant: a lane owns 4 consecutive records of a 256-record batch (4-aligned:
+  // phase B, thread-coarsened: a lane owns 4 consecutive records of a 256-record batch (4-aligned:
   // one 4-B key load and two 16-B delta loads per lane), reduces its own runs, and only its tail run
   // enters the wave's segmented scan (one scan per 256 records); records before r0 / after r1 of the
   // aligned batch are masked (the record arrays are padded to a multiple of 4)
@@ -422,19 +323,13 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
     // The next lane's head run may have added into the same slot above (ds_add).  A plain read-modify-write
     // after those adds have completed (lgkmcnt(0)) sees them; the compiler must not hoist the read above the
     // wait (per lane it can prove key[j] != kt, but the adds of OTHER lanes alias), hence the compiler
-    // barrier.  K1_TAIL_ATOMIC=1 keeps the atomic form, K1_TAIL_ORDER=0 the issue-order form of round 2.
+    // barrier.
     if (knext != kenc && kt >= 0 && kt < SEGW) {
-#if K1_TAIL_ATOMIC
-      atomicAdd(acc0 + kt, t0); atomicAdd(acc1 + kt, t1); atomicAdd(acc2 + kt, t2); atomicAdd(acc3 + kt, t3);
-#else
-#if K1_TAIL_ORDER
       // the read below must see the ds_adds issued above by the other lanes of this wave: wait until they have
       // completed (lgkmcnt(0)) instead of relying on the LDS executing a wave's operations in issue order
       __builtin_amdgcn_s_waitcnt(0xc07f);
-#endif
       asm volatile("" ::: "memory");
       acc0[kt] += t0; acc1[kt] += t1; acc2[kt] += t2; acc3[kt] += t3;
-#endif
     }
   };
 
@@ -444,25 +339,14 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
     const int64_t r0 = (w0 == s0) ? (int64_t)(uint32_t)wd.w : a.seg_rec_begin[w0];
     const int64_t r1 = (w0 == s0) ? (int64_t)(uint32_t)wm.w : a.seg_rec_begin[w1];
     // the window's first record group is requested before phase A: its latency overlaps the projections
-    CGrp ca, cb, cc;
-    Grp ga, gb;
+    CGrp ca, cb;
     const int64_t rb0 = r0 & ~(int64_t)3;
-    constexpr bool D3 = COARSE && K1_DEPTH == 3 && sizeof(real) == 4;
-    if constexpr (D3) {
-      load_cgrp(ca, rb0, r1);
-      load_cgrp(cb, rb0 + 4 * WAVE, r1);
-    } else if constexpr (COARSE) {
-      load_cgrp(ca, rb0, r1);
-    } else {
-      load_grp(ga, r0, r1);
-    }
+    load_cgrp(ca, rb0, r1);
     // phase A: fp64 projection of every segment of the window (lanes over segments), kept as the
     // offset from the segment's base observation so phase B works on O(residual) magnitudes.  The
     // frame ids and the phase-C frame tables stay in registers.
     int fsv[SEGW / WAVE];
-#if !K1_FTV_LATE
     FrameTab<real> ftv[SEGW / WAVE];  // phase C's frame tables, loaded here (off phase C's path)
-#endif
 #pragma unroll
     for (int i = 0; i < SEGW / WAVE; ++i) {
       const int s = w0 + lane + i * WAVE;
@@ -479,13 +363,11 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
         sy[sl] = (real)(y - bs.y);
         acc0[sl] = 0; acc1[sl] = 0; acc2[sl] = 0; acc3[sl] = 0;
       }
-#if !K1_FTV_LATE
       if constexpr (!FTL) {  // (FTL: phase C reads its tables from LDS)
         // the five used fields only (not the 32-B struct)
         const FrameTab<real>* fp = ft + fsv[i];
         ftv[i].ca = fp->ca; ftv[i].sa = fp->sa; ftv[i].cb = fp->cb; ftv[i].sb = fp->sb; ftv[i].f = fp->f;
       }
-#endif
     }
     wave_lds_fence();
     K1_NOW(kt1);
@@ -494,35 +376,12 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
     // groups alternate: the next group's loads are in flight while the current one is consumed.
     // (An LDS-DMA ring of 3 batches per wave, global_load_lds, was measured slower: hipcc puts a
     // vmcnt(0) -- every pending DMA -- in front of each LDS write of the reduction)
-    if constexpr (D3) {
-      // three groups rotate: two requested before phase A, the third here; a group is refilled right
-      // after it is consumed, two batches ahead
-      for (int64_t rb = rb0; rb < r1; rb += 3 * 4 * WAVE) {
-        load_cgrp(cc, rb + 2 * 4 * WAVE, r1);
-        consume_c(ca, rb, r0, r1);
-        if (rb + 4 * WAVE >= r1) break;
-        load_cgrp(ca, rb + 3 * 4 * WAVE, r1);
-        consume_c(cb, rb + 4 * WAVE, r0, r1);
-        if (rb + 2 * 4 * WAVE >= r1) break;
-        load_cgrp(cb, rb + 4 * 4 * WAVE, r1);
-        consume_c(cc, rb + 2 * 4 * WAVE, r0, r1);
-      }
-    } else if constexpr (COARSE) {
-      for (int64_t rb = r0 & ~(int64_t)3; rb < r1; rb += 2 * 4 * WAVE) {
-        load_cgrp(cb, rb + 4 * WAVE, r1);
-        consume_c(ca, rb, r0, r1);
-        if (rb + 4 * WAVE >= r1) break;
-        load_cgrp(ca, rb + 2 * 4 * WAVE, r1);
-        consume_c(cb, rb + 4 * WAVE, r0, r1);
-      }
-    } else {
-      for (int64_t rb = r0; rb < r1; rb += 2 * K1_UNROLL * WAVE) {
-        load_grp(gb, rb + K1_UNROLL * WAVE, r1);
-        consume(ga, rb, r1);
-        if (rb + K1_UNROLL * WAVE >= r1) break;
-        load_grp(ga, rb + 2 * K1_UNROLL * WAVE, r1);
-        consume(gb, rb + K1_UNROLL * WAVE, r1);
-      }
+    for (int64_t rb = r0 & ~(int64_t)3; rb < r1; rb += 2 * 4 * WAVE) {
+      load_cgrp(cb, rb + 4 * WAVE, r1);
+      consume_c(ca, rb, r0, r1);
+      if (rb + 4 * WAVE >= r1) break;
+      load_cgrp(ca, rb + 2 * 4 * WAVE, r1);
+      consume_c(cb, rb + 4 * WAVE, r0, r1);
     }
     wave_lds_fence();
     K1_NOW(kt2);
@@ -544,11 +403,7 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
         F.pad0 = F.pad1 = F.pad2 = (real)0;
         ptz_project_jac<real>(F, R, u, v, x, y, J);
       } else {
-#if K1_FTV_LATE
-        ptz_project_jac<real>(ft[fs], R, u, v, x, y, J);
-#else
         ptz_project_jac<real>(ftv[i], R, u, v, x, y, J);
-#endif
       }
       const real Sx = acc0[sl], Sy = acc1[sl], Srx = acc2[sl], Sry = acc3[sl];
       // W = Jp^T diag(Sx,Sy) Jr (3x2), U = Jp^T diag Jp (upper: 00 01 02 11 12 22), g_pose = Jp^T (w r)
@@ -855,9 +710,6 @@ __device__ void lm_decide_body(LMDev* st, const double* scal, const double* __re
 // ranges into scratch partials; the last workgroup to finish (agent-scope counter) combines them in
 // block order and re-arms the counter, so the result is bitwise reproducible in one launch.
 constexpr int RED_BLOCKS = 64;
-#ifndef RED_SC1
-#define RED_SC1 1  // 0: plain partial stores published by an acq_rel counter add (A/B)
-#endif
 // (src2, stride2, nk2, out2): an optional second set of columns over the same n rows, reduced in the same
 // launch into out2 (columns nk .. nk + nk2 - 1 of the internal accumulators; nk + nk2 <= 8)
 __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ src, int64_t n, int stride, int nk,
@@ -902,7 +754,6 @@ __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ 
   if (lane_id() == 0)
     for (int k = 0; k < nk; ++k) red[k][w] = acc[k];
   __syncthreads();
-#if RED_SC1
   // the partials go out write-through (sc1 stores: L2 bypassed to memory) and the storing wave waits for them
   // before its counter add, so the add needs no agent-scope release -- which would write back every dirty line
   // of this XCD's L2 (K1 just stored ~90 MB of slots) -- and the last workgroup reads them with sc1 loads
@@ -923,20 +774,6 @@ __global__ __launch_bounds__(256) void k_reduce_cols(const double* __restrict__ 
     }
   }
   __syncthreads();
-#else
-  if (threadIdx.x < nk) {
-    const int k = threadIdx.x;
-    double s = 0;
-    for (int j = 0; j < (int)(blockDim.x / WAVE); ++j) s = (maxmask & (1 << k)) ? fmax(s, red[k][j]) : s + red[k][j];
-    partial[blockIdx.x * 8 + k] = s;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned done = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    last = (done == gridDim.x - 1);
-  }
-  __syncthreads();
-#endif
   if (!last) return;
   // reader-side acquire at agent scope (invalidates this CU's vector cache; the L2 is not written back), so the
   // partial loads below cannot be satisfied from lines older than the counter observation

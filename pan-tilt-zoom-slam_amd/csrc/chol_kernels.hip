@@ -12,8 +12,8 @@
 // update"; natural order = one column per level, nested dissection = the A and B chains side by side).
 // A task carries its tile (i, j) and up to two update panels p from the previous level:
 //   panel task (i, k):   D <- A_kk - sum_p L_kp L_kp^T,  T <- A_ik - sum_p L_ip L_kp^T,
-//                        then one wave factors D and solves L_ik = T L_kk^-T in the same sweep
-//                        (wave_potrf_trsm32)   [i == k: L_kk -> Ldiag]
+//                        then the workgroup factors D and solves L_ik = T L_kk^-T in the same sweep
+//                        (wg_potrf_trsm32_df)   [i == k: L_kk -> Ldiag]
 //   trailing task (i,j): A_ij <- A_ij - sum_p L_ip L_jp^T   (column j is factored at a later level)
 // Every update (i, j, p) is applied exactly once, at the level after p's: by the trailing tasks, or by
 // column j's panel tasks when j is factored at that very level.  Only structurally nonzero tiles
@@ -168,116 +168,10 @@ __device__ __forceinline__ double rsq_nr(double d) {
   return y * fma(-0.5 * d * y, y, 1.5);
 }
 
-// One wave factors the 32x32 SPD tile D and, in the same sweep, solves X = T L^-T for a 32x32 tile T.
-// Lanes 0..31 hold the rows of D, lanes 32..63 the rows of T, in registers.  Right-looking elimination
-// with the pivots in blocks of PB: step j applies  v[m] -= (v[j] / A_jj) A_mj  (m > j) to every lane's
-// row -- the Cholesky update for a row of D, the forward substitution for a row of T.
-//   * inside a block the pivot column moves by v_readlane (PB(PB-1)/2 elements per block);
-//   * after the block the D lanes publish their PB block values to LDS (cb) once, and the trailing
-//     rank-PB update reads them with uniform-address 16-byte loads (broadcast), MC rows per chunk with
-//     the next chunk's loads in flight.  A v_readlane broadcast costs ~8 cycles per 32-bit half on
-//     gfx950, an LDS-fed fp64 FMA ~6.7 cycles per element (tools/isa_probe.hip, tools/potrf_bench.hip).
-//   * every updated row value is pinned by an empty asm: otherwise the FMAs float past the chunk
-//     boundaries in the DAG and all LDS operands stay live (spills);
-//   * the 32 rsqrt run once at the end, vectorised (lane j keeps its pivot d_j).
-// At the end L_ij = v_i[j] / sqrt(A_jj) (j <= i; L_ii = sqrt(A_jj)) and X_rj = x_r[j] / sqrt(A_jj).
-// Writes the lower factor into D (zero above), X into T (when given), rdg[j] = 1/L_jj.
-constexpr int PB = 4, PMC = 4;
-__device__ __forceinline__ void wave_potrf_trsm32(double (*D)[NB + 1], double (*T)[NB + 1], double* rdg,
-                                                  double (*cb)[PB], int* info) {
-  const int lane = lane_id();
-  const bool isT = lane >= NB;
-  const int r = lane & (NB - 1);
-  double row[NB];
-#pragma unroll
-  for (int m = 0; m < NB; ++m) row[m] = (isT && T) ? T[r][m] : D[r][m];
-  bool bad = false;
-  double dm = 1.0;
-#pragma unroll
-  for (int kb = 0; kb < NB; kb += PB) {
-    double w[PB];
-#pragma unroll
-    for (int j = kb; j < kb + PB; ++j) {
-      double d = bcast(row[j], j);
-      if (!(d > 0.0)) {
-        bad = true;
-        d = 1e-300;
-      }
-      dm = (lane == j) ? d : dm;
-      const double li = row[j] * rcp_nr(d);
-      w[j - kb] = li;
-#pragma unroll
-      for (int m = j + 1; m < kb + PB; ++m) row[m] -= li * bcast(row[j], m);
-    }
-    if (kb + PB < NB) {
-      if (!isT) {
-#pragma unroll
-        for (int k = 0; k < PB; ++k) cb[r][k] = row[kb + k];
-      }
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are visible
-      __builtin_amdgcn_wave_barrier();
-      const int m0 = kb + PB;
-      double nxt[PMC][PB];
-#pragma unroll
-      for (int q = 0; q < PMC; ++q)
-#pragma unroll
-        for (int k = 0; k < PB; ++k) nxt[q][k] = (m0 + q < NB) ? cb[m0 + q][k] : 0.0;
-#pragma unroll
-      for (int mc = m0; mc < NB; mc += PMC) {
-        double cur[PMC][PB];
-#pragma unroll
-        for (int q = 0; q < PMC; ++q)
-#pragma unroll
-          for (int k = 0; k < PB; ++k) cur[q][k] = nxt[q][k];
-        if (mc + PMC < NB) {
-#pragma unroll
-          for (int q = 0; q < PMC; ++q)
-#pragma unroll
-            for (int k = 0; k < PB; ++k) nxt[q][k] = (mc + PMC + q < NB) ? cb[mc + PMC + q][k] : 0.0;
-        }
-#pragma unroll
-        for (int q = 0; q < PMC; ++q) {
-          if (mc + q < NB) {
-            double sacc = row[mc + q];
-#pragma unroll
-            for (int k = 0; k < PB; ++k) sacc -= w[k] * cur[q][k];
-            row[mc + q] = sacc;
-            asm volatile("" : "+v"(row[mc + q]));
-          }
-        }
-      }
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // all reads of cb done before the next block rewrites it
-      __builtin_amdgcn_wave_barrier();
-    }
-  }
-  if (bad && lane == 0) atomicOr(info, 1);
-  if (lane < NB) rdg[lane] = rsq_nr(dm);
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
-  if (!isT) {
-#pragma unroll
-    for (int j = 0; j < NB; ++j) D[r][j] = (j <= r) ? row[j] * rdg[j] : 0.0;
-  } else if (T) {
-#pragma unroll
-    for (int j = 0; j < NB; ++j) T[r][j] = row[j] * rdg[j];
-  }
-  wave_lds_fence();
-}
-
 #ifdef CS_TIMING
 __device__ long long g_cs_stamps[64][6];
 __device__ long long g_cs_wg[64][10];
 __device__ int g_cs_level;
-#endif
-// Workgroup form of the same factorisation (256 threads = 4 waves): rows in lanes as above (lanes 0..31
-// rows of D, 32..63 rows of T), the 32 columns split over the 4 waves (wave w keeps columns w + 4 i in
-// registers).  Pivot blocks of 8: the waves publish the block's 8 columns to LDS, wave 0 eliminates
-// inside the block (pivot values by v_readlane) and publishes the multipliers, then every wave applies
-// the rank-8 update to its own columns (the pivot-column values broadcast from LDS).  The trailing
-// update -- most of the FMAs -- runs on four SIMDs instead of one.
-constexpr int WB = 8;
-#ifndef BS_NOWAIT
-#define BS_NOWAIT 0  // 1: LDS hand-offs without lgkmcnt(0) waits (in-order LDS per wave; A/B)
 #endif
 #ifndef BS_LOADERS
 #define BS_LOADERS 1  // loader waves of the lookahead back-solve (2: ring positions alternate; measured neutral)
@@ -288,110 +182,15 @@ constexpr int WB = 8;
 #ifndef CHOL_DIRECT_STORE
 #define CHOL_DIRECT_STORE 1  // store the factor tiles straight from the sweep's block buffer (0: copy back to the tiles first)
 #endif
-#ifndef CHOL_NU_RELAXED
-#define CHOL_NU_RELAXED 0  // the same for the helpers' progress counters (A/B)
-#endif
-#ifndef CHOL_NL_RELAXED
-#define CHOL_NL_RELAXED 0  // 0: publish a factor block after lgkmcnt(0) with a release store (ordered by
-                           // completion); 1: no wait, relying on a wave's LDS operations executing in issue
-                           // order (round 2; 5 us per trial faster at config 3, not covered by the memory model)
-#endif
 #ifndef CHOL_P_READLANE
 #define CHOL_P_READLANE 1  // 1: the pivot block by v_readlane instead of an LDS round trip (flag form)
 #endif
 #ifndef LA_BW
 #define LA_BW 4  // pivot block of the lookahead form
 #endif
-#ifndef CHOL_TRAIL_DIRECT
-#define CHOL_TRAIL_DIRECT 0  // 1: trailing tasks from registers (A/B: config 4 5.73 vs 4.76 ms staged, r03s)
-#endif
 #ifndef CHOL_LB_ALIAS
 #define CHOL_LB_ALIAS 1  // the sweep's block buffer overlays the update panels (0: a buffer of its own, A/B)
 #endif
-#ifndef CHOL_WG
-#define CHOL_WG 3  // 3: flag-synchronised lookahead, 2: lookahead workgroup potrf+trsm, 1: workgroup (4 waves), 0: single-wave sweep
-#endif
-__device__ __forceinline__ void wg_potrf_trsm32(double (*D)[NB + 1], double (*T)[NB + 1], double* rdg,
-                                                double (*pan)[WB + 1], double (*mul)[WB + 1], double* dg, int* info) {
-  const int w = threadIdx.x >> 6, lane = lane_id();
-  const bool isT = lane >= NB;
-  const int r = lane & (NB - 1);
-  const bool have = !isT || T != nullptr;
-  double col[NB / 4];
-#pragma unroll
-  for (int i = 0; i < NB / 4; ++i) col[i] = have ? (isT ? T[r][w + 4 * i] : D[r][w + 4 * i]) : 0.0;
-  bool bad = false;
-#ifdef CS_TIMING
-  long long* wst = g_cs_wg[g_cs_level < 64 ? g_cs_level : 63];
-  const bool wrec = threadIdx.x == 0 && blockIdx.x == 0;
-  if (wrec) wst[0] = clock64();
-#endif
-#pragma unroll
-  for (int kb = 0; kb < NB; kb += WB) {
-    pan[lane][w] = col[kb / 4];
-    pan[lane][4 + w] = col[kb / 4 + 1];
-    __syncthreads();
-    if (w == 0) {
-      double v[WB], mu[WB];
-#pragma unroll
-      for (int k = 0; k < WB; ++k) v[k] = pan[lane][k];
-#pragma unroll
-      for (int j = 0; j < WB; ++j) {
-        double d = bcast(v[j], kb + j);
-        if (!(d > 0.0)) {
-          bad = true;
-          d = 1e-300;
-        }
-        if (lane == 0) dg[kb + j] = d;
-        mu[j] = v[j] * rcp_nr(d);
-#pragma unroll
-        for (int m = j + 1; m < WB; ++m) v[m] -= mu[j] * bcast(v[j], kb + m);
-      }
-#pragma unroll
-      for (int k = 0; k < WB; ++k) {
-        pan[lane][k] = v[k];
-        mul[lane][k] = mu[k];
-      }
-    }
-    __syncthreads();
-#ifdef CS_TIMING
-    if (wrec) wst[1 + 2 * (kb / WB)] = clock64();
-#endif
-    col[kb / 4] = pan[lane][w];
-    col[kb / 4 + 1] = pan[lane][4 + w];
-    if (kb + WB < NB) {
-      double mu[WB];
-#pragma unroll
-      for (int k = 0; k < WB; ++k) mu[k] = mul[lane][k];
-#pragma unroll
-      for (int i = kb / 4 + 2; i < NB / 4; ++i) {
-        const int m = w + 4 * i;
-        double sacc = col[i];
-#pragma unroll
-        for (int k = 0; k < WB; ++k) sacc = fma(-mu[k], pan[m][k], sacc);
-        col[i] = sacc;
-      }
-      __syncthreads();  // pan / mul are rewritten by the next block
-    }
-#ifdef CS_TIMING
-    if (wrec) wst[2 + 2 * (kb / WB)] = clock64();
-#endif
-  }
-  if (bad && lane == 0) atomicOr(info, 1);
-  if (threadIdx.x < NB) rdg[threadIdx.x] = rsq_nr(dg[threadIdx.x]);
-  __syncthreads();
-  if (have) {
-#pragma unroll
-    for (int i = 0; i < NB / 4; ++i) {
-      const int m = w + 4 * i;
-      const double val = col[i] * rdg[m];
-      if (isT) T[r][m] = val;
-      else D[r][m] = (m <= r) ? val : 0.0;
-    }
-  }
-  __syncthreads();
-}
-
 // reciprocal square root by a series step on the hardware estimate: e = 1 - d y0^2 (|e| ~ 5e-8),
 // y = y0 (1 + e/2 + 3e^2/8) -- full double precision in 4 dependent operations (rsq_nr: 6)
 __device__ __forceinline__ double rsq_fast(double d) {
@@ -400,119 +199,9 @@ __device__ __forceinline__ double rsq_fast(double d) {
   return fma(y0 * e, fma(e, 0.375, 0.5), y0);
 }
 
-// Lookahead workgroup form (CHOL_WG 2).  Rows in lanes as above; the tile stays in LDS.  Wave 0 runs
-// the critical chain, one stage per pivot block s of BW columns:
-//   * apply block s-1's update to block s (its own lanes' rows; the block-(s-1) factor rows of the D
-//     lanes come from LDS as uniform broadcast reads),
-//   * publish block s's BWxBW diagonal part P, and every lane factors P = L_P L_P^T itself (no
-//     cross-lane traffic on the pivot chain, no v_readlane),
-//   * solve its own row against L_P: l = a L_P^-T -- for a D row that is its L_ij, for a T row its
-//     X_rj -- and store l to LDS (Lb[s]).
-// Meanwhile waves 1-3 apply block s-1's update to blocks s+1.. (off the chain).  One barrier per stage.
-// fp64 VALU issue (~8 cycles per instruction for one wave) bounds the chain wave, so the block is small:
-// the redundant factorisation of P costs O(BW^3) instructions per stage.  D's upper triangle may hold
-// anything: those lanes' results are never read by another lane and are zeroed on output.
-template <int BW>
-__device__ __forceinline__ void wg_potrf_trsm32_la(double (*D)[NB + 1], double (*T)[NB + 1],
-                                                   double (*Lb)[2 * NB][BW], double (*Pb)[BW], int* info) {
-  constexpr int NS = NB / BW;
-  const int w = threadIdx.x >> 6, lane = lane_id();
-  const bool isT = lane >= NB;
-  const int r = lane & (NB - 1);
-  const bool have = !isT || T != nullptr;
-  double* row = (isT && T) ? T[r] : D[r];
-  bool bad = false;
-  double lp[BW];
-#pragma unroll
-  for (int k = 0; k < BW; ++k) lp[k] = 0.0;
-#ifdef CS_TIMING
-  long long* wst = g_cs_wg[g_cs_level < 64 ? g_cs_level : 63];
-  const bool wrec = threadIdx.x == 0 && blockIdx.x == 0;
-  if (wrec) wst[0] = clock64();
-#endif
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int kb = s * BW;
-    if (w == 0) {
-      double a[BW];
-#pragma unroll
-      for (int j = 0; j < BW; ++j) a[j] = row[kb + j];
-      if (s > 0) {
-#pragma unroll
-        for (int j = 0; j < BW; ++j) {
-          double acc = a[j];
-#pragma unroll
-          for (int k = 0; k < BW; ++k) acc = fma(-lp[k], Lb[s - 1][kb + j][k], acc);
-          a[j] = acc;
-        }
-      }
-      if (lane >= kb && lane < kb + BW) {
-#pragma unroll
-        for (int j = 0; j < BW; ++j) Pb[lane - kb][j] = a[j];
-      }
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-      __builtin_amdgcn_wave_barrier();
-      double P[BW][BW], y[BW];
-#pragma unroll
-      for (int i = 0; i < BW; ++i)
-#pragma unroll
-        for (int j = 0; j <= i; ++j) P[i][j] = Pb[i][j];
-#pragma unroll
-      for (int j = 0; j < BW; ++j) {
-        double d = P[j][j];
-        if (!(d > 0.0)) {
-          bad = true;
-          d = 1e-300;
-        }
-        y[j] = rsq_fast(d);
-#pragma unroll
-        for (int i = j + 1; i < BW; ++i) P[i][j] *= y[j];
-#pragma unroll
-        for (int i = j + 1; i < BW; ++i)
-#pragma unroll
-          for (int m = j + 1; m <= i; ++m) P[i][m] = fma(-P[i][j], P[m][j], P[i][m]);
-      }
-#pragma unroll
-      for (int j = 0; j < BW; ++j) {
-        const double x = a[j] * y[j];
-        lp[j] = x;
-#pragma unroll
-        for (int i = j + 1; i < BW; ++i) a[i] = fma(-P[i][j], x, a[i]);
-      }
-#pragma unroll
-      for (int j = 0; j < BW; ++j) Lb[s][lane][j] = lp[j];
-    } else if (s > 0 && s + 1 < NS) {
-      double l[BW];
-#pragma unroll
-      for (int k = 0; k < BW; ++k) l[k] = Lb[s - 1][lane][k];
-      for (int m = kb + BW + w - 1; m < NB; m += 3) {
-        double acc = row[m];
-#pragma unroll
-        for (int k = 0; k < BW; ++k) acc = fma(-l[k], Lb[s - 1][m][k], acc);
-        if (have) row[m] = acc;
-      }
-    }
-    __syncthreads();
-#ifdef CS_TIMING
-    if (wrec && s < 9) wst[1 + s] = clock64();
-#endif
-  }
-  if (bad && lane == 0 && w == 0) atomicOr(info, 1);
-  // wave w writes columns 8w .. 8w+7 of the factor
-  if (have) {
-#pragma unroll
-    for (int j = 0; j < NB / 4; ++j) {
-      const int m = w * (NB / 4) + j;
-      const double val = Lb[m / BW][lane][m % BW];
-      if (isT) T[r][m] = val;
-      else D[r][m] = (m <= r) ? val : 0.0;
-    }
-  }
-  __syncthreads();
-}
-
-// Flag-synchronised form of the lookahead sweep (CHOL_WG 3): the same stages, but no workgroup barrier
-// per stage.  LDS counters carry the two dependencies instead:
+// The pivot sweep (round 2-4 history: single-wave, 4-wave and barrier-per-stage lookahead forms): wave 0
+// runs the critical chain one pivot block of BW columns at a time, waves 1-3 bring the next block up to date, and
+// no workgroup barrier separates the stages.  LDS counters carry the two dependencies instead:
 //   nl = number of factor blocks wave 0 has published (waves 1-3 wait for block t-1 before stage t),
 //   nu[t] = helper waves that have brought block t+1 up to date (wave 0 waits for all 3 before it
 //           starts block t+1).
@@ -524,11 +213,7 @@ __device__ __forceinline__ int lds_poll(const int* p) {
 // writes (lgkmcnt) and stores the counter; the consumer polls it and its later LDS reads stay behind
 // the poll (LDS operations of a wave execute in order; compiler barrier against reordering).
 __device__ __forceinline__ void lds_signal(int* p, int v) {
-#if BS_NOWAIT
-  asm volatile("" ::: "memory");  // in-order LDS per wave: the counter store lands after the data stores
-#else
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-#endif
   __builtin_amdgcn_wave_barrier();
   if (lane_id() == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -650,17 +335,9 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
         }
       }
       if (s + 2 < NS) {
-#if CHOL_NL_RELAXED
-        // no wait for the Lb stores: this wave's LDS operations execute in issue order, so a helper that
-        // sees nl also sees them; the compiler barrier keeps the counter store behind them
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) __hip_atomic_store(nl, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) __hip_atomic_store(nl, s + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
       }
 #ifdef CS_TIMING
       if (wrec && s < 9) wst[1 + s] = clock64();
@@ -692,15 +369,9 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
           for (int k = 0; k < BW; ++k) acc = fma(-lr[b][k], Lb[b][m][k], acc);
         if (have) row[m] = acc;
       }
-#if CHOL_NU_RELAXED
-      asm volatile("" ::: "memory");  // as for nl: in-order LDS, no wait for the column stores
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) __hip_atomic_fetch_add(&nu[t], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
       if (lane == 0) __hip_atomic_fetch_add(&nu[t], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
     }
   }
   __syncthreads();
@@ -972,23 +643,13 @@ template <bool SG, bool P2, bool COH, bool SUP = false>
 __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, const int4 tk, double* __restrict__ Ldiag,
                                           int* info, double* __restrict__ sgn, double* __restrict__ Minv,
                                           double* __restrict__ Lsub = nullptr, int4 tk2 = int4{0, 0, 0, 0}) {
-  static_assert(!SUP || (P2 && !SG && CHOL_WG == 3 && CHOL_LB_ALIAS && CHOL_DIRECT_STORE && !CHOL_FEWER_BARRIERS),
+  static_assert(!SUP || (P2 && !SG && CHOL_LB_ALIAS && CHOL_DIRECT_STORE && !CHOL_FEWER_BARRIERS),
                 "supercolumn tasks: the P2 kernel of SPD plans with the default sweep");
   static_assert(!(COH && SG), "the persistent form factors SPD systems only");
-  static_assert(!(COH && CHOL_TRAIL_DIRECT), "the persistent form stages trailing tiles");
   __shared__ double sC[NB][NB + 1];     // target tile (panel T_ik / trailing A_ij)
   __shared__ double sD[NB][NB + 1];     // diagonal tile -> L_kk
   __shared__ __attribute__((aligned(16))) double sA[2][NB][NB + 1];  // L_ip of the two update panels
   __shared__ double sB[2][NB][NB + 1];  // L_kp or L_jp of the two update panels
-#if CHOL_WG < 2
-  __shared__ double rdg[NB];
-#endif
-#if !CHOL_WG
-  __shared__ __attribute__((aligned(16))) double cb[NB][PB];  // potrf block columns (broadcast reads)
-#endif
-#if CHOL_WG == 1
-  __shared__ double s_pan[2 * NB][WB + 1], s_mul[2 * NB][WB + 1], s_dg[NB];
-#elif CHOL_WG >= 2
 #if CHOL_LB_ALIAS
   // the sweep's block buffer overlays the update panels' L_ip tiles, dead once the panel GEMMs are done (a
   // barrier separates them): 51 KB of LDS per workgroup instead of 67, so three workgroups per CU instead of
@@ -1000,7 +661,6 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
 #endif
   __shared__ __attribute__((aligned(16))) double s_pb[LA_BW][LA_BW];
   __shared__ int s_flags[NB / LA_BW + 1];
-#endif
   __shared__ double s_sgp[2][NB];  // SG: signs of the two update panels' columns
   __shared__ double s_sig[NB];     // SG: signs of this column's pivots
   if ((tk.x & 3) == 2) {  // inverse of a diagonal factor tile of the previous level (see tile_inv_wave)
@@ -1017,7 +677,7 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
     tile_inv_wave<COH>(Ldiag + (int64_t)tk.y * NB * NB, Minv + (int64_t)tk.y * NB * NB, sD, s_rinv);
     return;
   }
-#if CHOL_FEWER_BARRIERS && CHOL_WG == 3
+#if CHOL_FEWER_BARRIERS
   if (threadIdx.x <= NB / LA_BW) s_flags[threadIdx.x] = 0;  // the sweep's counters (ordered by the staging barrier)
 #endif
   const int type = tk.x & 3, i = tk.y, j = tk.z;
@@ -1035,12 +695,6 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
   if (threadIdx.x == 0 && blockIdx.x == 0 && cs_lvl < 64) g_cs_stamps[cs_lvl][5] = type;
 #endif
   CS_STAMP(0);
-#ifndef CHOL_VARIANT
-#define CHOL_VARIANT 0
-#endif
-#if CHOL_VARIANT == 5
-  return;
-#endif
   if constexpr (P2 && !SG) {
     if (type == 3) {  // 2 x 2 block of trailing tiles (api.hip make_plan): A_ij -= sum_p L_ip L_jp^T
       chol_trail_block<COH>(A, ld, i, j, ((tk.w >> 28) & 3) | (((unsigned)tk.x >> 30) << 2), up0, up1, up2, up3, sA, sB);
@@ -1069,60 +723,9 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
     }
   };
   if (type == 1) {
-#if CHOL_VARIANT == 3
-    return;
-#endif
-#if CHOL_TRAIL_DIRECT && CHOL_VARIANT == 0
-    {  // trailing: A_ij -= sum_p L_ip L_jp^T straight from registers -- no LDS staging, no barriers: each wave
-       // owns one 16 x 16 block of C in the MFMA accumulator layout of tile_gemm_nt_sub, and the 32-long
-       // contraction is taken in the order k = 8 lk + s (step s, lane group lk), so a lane's A and B operands
-       // are 8 consecutive doubles of one row (two 32-B loads each) instead of 8 strided ones
-      const int w = threadIdx.x >> 6, l = threadIdx.x & 63, li = l & 15, lk = l >> 4;
-      const int bi = (w >> 1) * 16, bj = (w & 1) * 16;
-      double* C = A + (i * NBl + bi) * ld + j * NBl + bj;
-      v4f64 acc;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r] = C[(int64_t)(lk + 4 * r) * ld + li];
-      const int ups[4] = {up0, up1, up2, up3};
-      constexpr int NU = P2 ? 4 : 2;
-      double2 a[NU][4], b[NU][4];
-#pragma unroll
-      for (int u = 0; u < NU; ++u)
-        if (ups[u] >= 0) {
-          const double2* pa = reinterpret_cast<const double2*>(A + (i * NBl + bi + li) * ld + ups[u] * NBl + 8 * lk);
-          const double2* pb = reinterpret_cast<const double2*>(A + (j * NBl + bj + li) * ld + ups[u] * NBl + 8 * lk);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            a[u][q] = pa[q];
-            b[u][q] = pb[q];
-          }
-        }
-#pragma unroll
-      for (int u = 0; u < NU; ++u)
-        if (ups[u] >= 0) {
-#pragma unroll
-          for (int s = 0; s < 8; ++s) {
-            const double av = -((s & 1) ? a[u][s >> 1].y : a[u][s >> 1].x);
-            double bv = (s & 1) ? b[u][s >> 1].y : b[u][s >> 1].x;
-            if constexpr (SG) bv *= sgn[(int64_t)ups[u] * NB + 8 * lk + s];
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-          }
-        }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) C[(int64_t)(lk + 4 * r) * ld + li] = acc[r];
-      return;
-    }
-#endif
     // trailing: A_ij -= sum_p L_ip L_jp^T
     double* C = A + i * NBl * ld + j * NBl;
-#if CHOL_VARIANT == 7  // timing only: no C tile read / write
-    for (int r = 0; r < 4; ++r) v0[r] = 0.0;
-#else
     fetch_tile<COH>(v0, C, ld);
-#endif
-#if CHOL_VARIANT == 6  // timing only: no panel tile reads
-    for (int r = 0; r < 4; ++r) v1[r] = v2[r] = v3[r] = v4[r] = 0.0;
-#else
     if (up0 >= 0) {
       fetch_tile<COH>(v1, A + i * NBl * ld + up0 * NBl, ld);
       fetch_tile<COH>(v2, A + j * NBl * ld + up0 * NBl, ld);
@@ -1131,7 +734,6 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
       fetch_tile<COH>(v3, A + i * NBl * ld + up1 * NBl, ld);
       fetch_tile<COH>(v4, A + j * NBl * ld + up1 * NBl, ld);
     }
-#endif
     if (up2 >= 0) {
       fetch_tile<COH>(w2, A + i * NBl * ld + up2 * NBl, ld);
       fetch_tile<COH>(w3, A + j * NBl * ld + up2 * NBl, ld);
@@ -1200,9 +802,7 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
       }
     }
     __syncthreads();
-#if CHOL_VARIANT != 7
     for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) gst<COH>(C + (int64_t)(e >> 5) * ld + (e & 31), sC[e >> 5][e & 31]);
-#endif
     return;
   }
   // panel task (i, k = j)
@@ -1229,7 +829,6 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
   load_signs(up0, up1);
   __syncthreads();
   CS_STAMP(1);
-#if CHOL_VARIANT != 4
   if (up0 >= 0) {
     tile_gemm_nt_sub<SG>(sD, sB[0], sB[0], s_sgp[0]);
     if (updT0) tile_gemm_nt_sub<SG>(sC, sA[0], sB[0], s_sgp[0]);
@@ -1255,21 +854,10 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
       if (updT3) tile_gemm_nt_sub<SG>(sC, sA[1], sB[1], s_sgp[1]);
     }
   }
-#endif
   __syncthreads();
   CS_STAMP(2);
-#if CHOL_VARIANT != 1
-#if CHOL_WG == 3
   wg_potrf_trsm32_df<LA_BW, SG>(sD, diag_only ? nullptr : sC, s_lb, s_pb, s_flags, info, s_sig);
-#elif CHOL_WG == 2
-  wg_potrf_trsm32_la<LA_BW>(sD, diag_only ? nullptr : sC, s_lb, s_pb, info);
-#elif CHOL_WG == 1
-  wg_potrf_trsm32(sD, diag_only ? nullptr : sC, rdg, s_pan, s_mul, s_dg, info);
-#else
-  if (threadIdx.x < WAVE) wave_potrf_trsm32(sD, diag_only ? nullptr : sC, rdg, cb, info);
-#endif
-#endif
-#if !(CHOL_FEWER_BARRIERS && CHOL_DIRECT_STORE && CHOL_WG == 3)
+#if !(CHOL_FEWER_BARRIERS && CHOL_DIRECT_STORE)
   __syncthreads();  // (the flag-synchronised sweep ends in a barrier of its own)
 #endif
   CS_STAMP(3);
@@ -1279,7 +867,7 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
     g_cs_level = cs_lvl + 1;
   }
 #endif
-#if CHOL_DIRECT_STORE && CHOL_WG == 3
+#if CHOL_DIRECT_STORE
   // the factor goes to memory straight from the sweep's block buffer (rows 0..31: D, 32..63: T)
   if (diag_only) {
     double* C = Ldiag + (int64_t)k * NB * NB;
@@ -1592,11 +1180,7 @@ __global__ __launch_bounds__(64 * (BS_HELPERS + 1 + BS_LOADERS)) void k_chol_bac
       BSL_STAMP(q, 2);
       const double r = xv[c0 + c] - la_c;
       if (h == 0) xv[c0 + c] = r;
-#if BS_NOWAIT
-      asm volatile("" ::: "memory");  // the reads below are issued after the store: in-order LDS
-#else
       __builtin_amdgcn_s_waitcnt(0xc07f);
-#endif
       __builtin_amdgcn_wave_barrier();
       double s4[4] = {0, 0, 0, 0};
 #pragma unroll

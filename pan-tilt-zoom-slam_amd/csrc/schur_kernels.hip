@@ -35,9 +35,6 @@ namespace ptzba {
 #ifndef S2_DU
 #define S2_DU 4  // diagonal-term loads in flight per thread (chunk-0 items)
 #endif
-#ifndef S2_ABL
-#define S2_ABL 0  // ablation switch for measurements: 1 = no FMAs, 2 = no operand loads
-#endif
 constexpr int SF = SCHUR_F1;   // frames per F1 block
 constexpr int SFW = SF / 8;    // f1 frames per wave (8 waves)
 
@@ -229,7 +226,7 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
   int buf = 0;
   for (int p = 0; p < nl; p += SNB) {
     const bool more = p + SNB < nl;  // block-uniform
-    if (S2_ABL != 2) fetch(p + SNB);  // next batch's loads in flight during this batch's FMAs (unconditional: no phi
+    fetch(p + SNB);  // next batch's loads in flight during this batch's FMAs (unconditional: no phi
                      // at a join forces an early wait; past the list the lanes load clamped slots)
     real accr[SFW][9];
 #pragma unroll
@@ -341,17 +338,8 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 constexpr int MKP = 40;
-#ifndef SR_UNROLL
-#define SR_UNROLL 4  // split partials in flight per thread in k_schur_reduce (4 or 8)
-#endif
-#ifndef SR_VEC
-#define SR_VEC 0  // 1: fp32 partials four elements per reduce thread with 16-B loads (r03v A/B: 77-78 vs 71 us per build, slower)
-#endif
 #ifndef MF_DIAG_FUSED
 #define MF_DIAG_FUSED 1  // chunk-0 diagonal terms inside the batch pipeline (0: a phase before it)
-#endif
-#ifndef MF_ABL
-#define MF_ABL 0  // ablations for measurements: 1 = no MFMAs, 2 = no operand loads, 3 = no staging
 #endif
 #ifndef MF_FLUSH
 #define MF_FLUSH 4  // batches (of 16 landmarks) accumulated in fp32 between fp64 flushes
@@ -431,24 +419,17 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
       const int idx = f2base + ln - m.y;
       P.rwin[q] = (p + j < nl) && idx >= 0 && f2base + ln <= m.z;
       P.rgw[q] = sG[jj];
-      if (MF_ABL == 2) { for (int k = 0; k < 6; ++k) P.rw[q][k] = (float)(m.w & 7); } else
       slot_load6(P.rw[q], w_slot + (int64_t)(m.w + min(max(idx, 0), m.z - m.y)) * W_STRIDE);
     }
     const int f = f1b + yi, jj = min(p + yj, nl - 1);
     const int4 m = sL[jj];
     P.ryin = (p + yj < nl) && f >= m.y && f <= m.z;
     P.ryg = sG[jj];
-    if (MF_ABL == 2) {
-      for (int k = 0; k < 6; ++k) P.ryw[k] = (float)(m.w & 3);
-      P.rvi[0] = P.rvi[1] = P.rvi[2] = (float)(m.x & 1);
-      return;
-    }
     slot_load6(P.ryw, w_slot + (int64_t)(m.w + min(max(f - m.y, 0), m.z - m.y)) * W_STRIDE);
     const double* vi = a.lm_aux + (int64_t)m.x * 8;
     P.rvi[0] = (float)vi[0]; P.rvi[1] = (float)vi[1]; P.rvi[2] = (float)vi[2];
   };
   auto stage = [&](const Pre& P, int buf) {
-    if (MF_ABL == 3) return;
 #pragma unroll
     for (int q = 0; q < NSL; ++q) {
       const int e = t + 512 * q, j = e >> 6, ln = e & 63;
@@ -503,7 +484,6 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
       const h8v al = *reinterpret_cast<const h8v*>(&sY[buf][1][row][fk]);
 #pragma unroll
       for (int y = 0; y < 3; ++y) {
-        if (MF_ABL == 1) { c[x][y][0] += (float)ah[0] + (float)bl[y][1]; continue; }
         c[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[y], c[x][y], 0, 0, 0);
         c[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[y], c[x][y], 0, 0, 0);
         c[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[y], c[x][y], 0, 0, 0);
@@ -725,48 +705,8 @@ __device__ __forceinline__ void schur_reduce_vec(const SchurArgs& a, const int4 
   if (a.prep.pad) a.S[a.prep.n_aug * a.ld + c0 + q2] = bv;  // fused prepare: the augmented row b^T
 }
 
-// Four consecutive elements (partner frames f2 .. f2 + 3 of one (f1, q, r)) per thread: the split partials
-// are read as 16-B vectors (4-B loads move a third of the bytes per request at this occupancy) and summed
-// in the same fixed item order as schur_reduce_elem, element by element -- bitwise the same S.
-__device__ __forceinline__ void schur_reduce_elem4(const SchurArgs& a, const int4 g, int e4) {
-  constexpr int NE = SF * 9 * WAVE;
-  const int e = 4 * e4;
-  const int f1b = g.x, chunk = g.y;
-  const int ln = e & 63, ik = e >> 6, i = ik / 9, k = ik - 9 * i, q = k / 3, r = k - 3 * q;
-  const int f1 = f1b + i, f20 = f1b + WAVE * chunk + ln;
-  if (f1 >= a.n_pose) return;
-  const int whi = a.frame_win_hi[f1];
-  if (f20 + 3 < f1 || f20 > whi) return;  // no element of the four is in the coupling window
-  if (f20 <= f1 && f1 <= f20 + 3) {       // the diagonal block's element is among them: the scalar path
-    for (int d = 0; d < 4; ++d) schur_reduce_elem<float, false>(a, g, e + d);
-    return;
-  }
-  const float4* p = reinterpret_cast<const float4*>((const float*)a.part + e);
-  double v[4] = {0, 0, 0, 0};
-  int it = g.z;
-  for (; it + SR_UNROLL <= g.w; it += SR_UNROLL) {
-    float4 x[SR_UNROLL];
-#pragma unroll
-    for (int u = 0; u < SR_UNROLL; ++u) x[u] = p[(int64_t)(it + u) * (NE / 4)];
-#pragma unroll
-    for (int u = 0; u < SR_UNROLL; ++u) {
-      v[0] += (double)x[u].x; v[1] += (double)x[u].y; v[2] += (double)x[u].z; v[3] += (double)x[u].w;
-    }
-  }
-  for (; it < g.w; ++it) {
-    const float4 x = p[(int64_t)it * (NE / 4)];
-    v[0] += (double)x.x; v[1] += (double)x.y; v[2] += (double)x.z; v[3] += (double)x.w;
-  }
-  const int64_t ld = a.ld, col0 = a.frame_pos[f1];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const int f2 = f20 + d;
-    if (f2 < f1 || f2 > whi) continue;  // f2 > f1 here for every element in the window
-    const int64_t pf2 = a.frame_pos[f2];
-    if (pf2 >= col0) a.S[(pf2 + r) * ld + col0 + q] = v[d];
-    else a.S[(col0 + q) * ld + pf2 + r] = v[d];
-  }
-}
+// (Four elements per reduce thread with 16-B partial loads, `SR_VEC`, and four independent elements with all their
+// partials in flight, measured slower (r03v: 77-78 vs 71 us; r05ac: 93 vs 72 us per build), are gone since round 5.)
 
 // tile reduction: fixed-order sum of the splits, U on the diagonal blocks, write the lower triangle in the
 // system order (mirror when f2 precedes f1); chunk-0 tiles also write b | g_pose | diag U of their frames.
@@ -776,8 +716,7 @@ template <typename real>
 __global__ __launch_bounds__(256) void k_schur_reduce(SchurArgs a) {
   if (a.skip_if && *a.skip_if) return;
   const int4 g = a.groups[blockIdx.y];  // {f1b, chunk, first item, end item}
-  if constexpr (sizeof(real) == 4 && SR_VEC) schur_reduce_elem4(a, g, blockIdx.x * 256 + threadIdx.x);
-  else schur_reduce_elem<real, false>(a, g, blockIdx.x * 256 + threadIdx.x);
+  schur_reduce_elem<real, false>(a, g, blockIdx.x * 256 + threadIdx.x);
   if (g.y == 0 && blockIdx.x == 0 && threadIdx.x < SF * 3) schur_reduce_vec<false>(a, g, threadIdx.x);
 }
 
@@ -791,7 +730,7 @@ void launch_schur(const SchurArgs& a, int n_items, int n_groups, int n_fixed, hi
     else hipLaunchKernelGGL(k_schur<real>, dim3(n_items), dim3(512), 0, st, a);
   }
   if (n_groups > 0)
-    hipLaunchKernelGGL(k_schur_reduce<real>, dim3(SF * 9 * WAVE / (sizeof(real) == 4 && SR_VEC ? 1024 : 256), n_groups),
+    hipLaunchKernelGGL(k_schur_reduce<real>, dim3(SF * 9 * WAVE / 256, n_groups),
                        dim3(256), 0, st, a);
 }
 
