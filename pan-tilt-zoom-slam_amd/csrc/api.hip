@@ -1727,11 +1727,11 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
         tile_key.push_back(c);
       }
     }
-    // split size: at most ~512 work items (two rounds of one workgroup per CU) counting the per-tile
-    // rounding, at least 64 landmarks, at most SCHUR_LMAX (the LDS list).  Chunk-0 items also sum the
-    // diagonal terms (~25 % more time per landmark, measured with tools/schur_timing.py): their lists
-    // are weighted so that every item takes about the same time and the two rounds pack evenly.
-    int64_t W0 = 5;
+    // split size: at most 256 work items (one round of one workgroup per CU) counting the per-tile rounding, at
+    // least 64 landmarks, at most SCHUR_LMAX (the LDS list).  Chunk-0 items also sum the diagonal terms: their
+    // lists are weighted (6 / 4; per-item clock stamps, tools/schur_items.py, put a chunk-0 landmark at 1.5-1.9x
+    // the time of another's; 5 / 4 before round 5) so that the items of the round end together.
+    int64_t W0 = 6;
     constexpr int64_t WD = 4;  // chunk-0 weight W0 / WD
     int64_t total_w = 0;
     for (size_t k = 0; k < tiles.size(); ++k)
@@ -1743,8 +1743,28 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     // solve: each item's 74 KB split partial and the reduce over its tile's splits are fixed costs (measured at
     // config 3, tools/dist_model.py: N = 8 shard 44-66 -> 37-47 us with 64-128 items)
     int64_t target_items = std::min<int64_t>(256, std::max<int64_t>(64, (512 * total_w) / 480000));
-    const int64_t slots = std::max<int64_t>(target_items - n_tiles, 64);
-    const int64_t split_w = std::max<int64_t>(64 * WD, (total_w + slots - 1) / slots);
+    // the smallest split weight whose per-tile rounding still fits the target (binary search: the item count falls as
+    // the split grows), so the items are as short -- and the one round as even -- as the target allows
+    auto items_for = [&](int64_t sw) {
+      int64_t c = 0;
+      for (size_t k = 0; k < tiles.size(); ++k) {
+        const int64_t n = (int64_t)tiles[k].size(), nw = n * (tile_key[2 * k + 1] == 0 ? W0 : WD);
+        c += std::max<int64_t>((nw + sw - 1) / sw, (n + SCHUR_LMAX - 1) / SCHUR_LMAX);
+      }
+      return c;
+    };
+    int64_t sw_lo = 64 * WD, sw_hi = std::max<int64_t>(sw_lo, total_w);
+    if (items_for(sw_lo) <= target_items) {
+      sw_hi = sw_lo;
+    } else {
+      while (sw_hi - sw_lo > 1) {  // items_for(sw_lo) > target >= items_for(sw_hi)
+        const int64_t mid = (sw_lo + sw_hi) / 2;
+        if (items_for(mid) <= target_items) sw_hi = mid;
+        else sw_lo = mid;
+      }
+    }
+    (void)n_tiles;
+    const int64_t split_w = sw_hi;
     for (size_t k = 0; k < tiles.size(); ++k) {
       const auto& lst = tiles[k];
       const int n = (int)lst.size();
