@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--trials", type=int, default=40)
     ap.add_argument("--ranks", default="first", choices=["first", "all"])
+    ap.add_argument("--mode", default="part", choices=["part", "replicated"],
+                    help="replicated: contiguous landmark shards (bench.shard_by_landmark), every rank factors the whole "
+                         "summed system (one X_SYS all-reduce of the packed system per trial)")
     a = ap.parse_args()
     import torch
     import ptzba
@@ -41,6 +44,8 @@ def main():
     for world in [int(x) for x in a.worlds.split(",")]:
         if world == 1:
             ranks, owner, mode, split = [0], None, 0, None
+        elif a.mode == "replicated":
+            ranks, owner, mode, split = [0], None, 0, None  # every shard runs the same full factorisation
         else:
             owner, mode, split = ptzba.partition_landmarks(prob.n_pose, prob.n_landmark, prob.frame, prob.landmark, world)
             ranks = list(range(world))
@@ -48,13 +53,22 @@ def main():
                 bases = [ptzba.dist_plan_summary(win, world, r)["base"] for r in ranks]
                 ranks = [r for r in ranks if r == 0 or bases[r] != bases[r - 1]]
         for rank in ranks:
-            sel = np.ones(len(prob.frame), bool) if owner is None else owner[prob.landmark] == rank
+            repl = world > 1 and a.mode == "replicated"
+            if repl:
+                import bench
+                sel = bench.shard_by_landmark(prob.landmark, prob.n_landmark, rank, world)
+            else:
+                sel = np.ones(len(prob.frame), bool) if owner is None else owner[prob.landmark] == rank
             h = ptzba.BAHandle(0)
             h.set_problem(prob.n_pose, prob.n_landmark, prob.frame[sel], prob.landmark[sel], prob.xy[sel], prob.u,
                           prob.v, precision=ptzba.FP32, loss=ptzba.LOSS_HUBER, frame_win_hi=win,
-                          dist_world=world if world > 1 else 0, dist_rank=rank)
-            xi = h.dist_info() if world > 1 else None
-            if xi is not None:
+                          dist_world=world if (world > 1 and not repl) else 0, dist_rank=rank)
+            if repl:  # the packed system and the scalars, all-reduced over all ranks per trial
+                xi = {"mode": "replicated", "exchanges": [[ptzba.X_SYS, 0, world, int(h.exchange_packed()[1])],
+                                                          [ptzba.X_SCAL, 0, world, int(ptzba.NSCALARS)]]}
+            else:
+                xi = h.dist_info() if world > 1 else None
+            if xi is not None and not repl:
                 xi["exchanges"] = h.dist_exchanges()
             if world > 1:
                 h.set_exchange_hook(lambda kind, ptr, count, stream: None)
