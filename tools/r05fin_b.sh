@@ -11,7 +11,7 @@ BARGS="--steps 20 --warmup 3 --no-cpu-baseline --no-accuracy --no-cold --no-seco
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof_stats -o run --output-format csv -- python bench.py $BARGS > gpurun_out/${T}_prof_stats.log 2>&1 || { echo PROFFAIL; tail gpurun_out/${T}_prof_stats.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/${T}_pmc_fetch -o run --output-format csv -- python bench.py $BARGS > gpurun_out/${T}_pmc_fetch.log 2>&1 || { echo PMCFAIL; tail gpurun_out/${T}_pmc_fetch.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/${T}_pmc_write -o run --output-format csv -- python bench.py $BARGS > gpurun_out/${T}_pmc_write.log 2>&1 || { echo PMCFAIL; tail gpurun_out/${T}_pmc_write.log; exit 1; }
-python tools/pmc_traffic.py gpurun_out/${T}_pmc_fetch gpurun_out/${T}_pmc_write "k_linearize<float, 1>" config3/pair/fp32/huber gpurun_out/${T}_k1_traffic.json > /dev/null || { echo TRAFFICFAIL; exit 1; }
+python tools/pmc_traffic.py gpurun_out/${T}_pmc_fetch gpurun_out/${T}_pmc_write "k_linearize<float, 1, true>" config3/pair/fp32/huber gpurun_out/${T}_k1_traffic.json > /dev/null || { echo TRAFFICFAIL; exit 1; }
 python tools/pmc_traffic.py gpurun_out/${T}_pmc_fetch gpurun_out/${T}_pmc_write "k_schur_mf" config3/pair/fp32/huber/k2 gpurun_out/${T}_k2_traffic.json 1024 > /dev/null || { echo K2TRAFFICFAIL; exit 1; }
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/${T}_cal_fetch -o run --output-format csv -- ./tools/pmc_calib.bin > gpurun_out/${T}_cal_fetch.log 2>&1 || { echo CALFAIL; exit 1; }
 timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/${T}_cal_write -o run --output-format csv -- ./tools/pmc_calib.bin > gpurun_out/${T}_cal_write.log 2>&1 || { echo CALFAIL; exit 1; }
