@@ -111,12 +111,6 @@ struct ptzba_ctx {
   DBuf stage_dev;
   bool bs_pst = false;
   uint32_t bsp_epoch = 0;
-  // XCD-local tail of the factorisation (k_chol_xcd): its first level, per-task relative levels, tasks per level, the
-  // two control sets (zeroed here, then alternately by the launches), the launch parity, the grid
-  bool cx_on = false;
-  int cx_L0 = 0, cx_par = 0, cx_grid = 0;
-  uint32_t cx_epoch = 0;
-  DBuf cx_lvl, cx_lvl_off, cx_done, cx_ctl;
   bool bs_ll = false, bs_blk = false;
   bool chol_delayed = false;  // the plan delays trailing updates (make_plan, DT = 2)
   DBuf xtiles, xbuf;  // packed exchange: tile list, buffer
@@ -2034,40 +2028,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
               plan.bsb_tasks.size() / 12 <= 512;  // (2 workgroups per CU resident: 190 VGPRs)
   h->bsp_epoch = 0;
   h->no_fused_prep = getenv("PTZBA_NO_FUSED_PREP") != nullptr;
-  // XCD-local tail (k_chol_xcd, SPD plans without supercolumns, every solve but a part-owned one): the levels from the
-  // first one after which no level holds more tasks than one XCD's workgroup slots (32 CUs x 2: VGPRs) run in
-  // one launch on one XCD -- hand-offs through that XCD's L2 instead of a launch boundary and an Infinity-Cache round
-  // trip per level.  PTZBA_CHOL_XCD=0 keeps one launch per level (A/B; the bitwise test compares both), =L starts the
-  // tail at level L.
-  {
-    const int CX_SLOTS = getenv("PTZBA_CX_SLOTS") ? atoi(getenv("PTZBA_CX_SLOTS")) : 64;  // TEMP experiment
-    h->cx_on = false;
-    h->cx_par = 0;
-    const int NL = plan.n_levels;
-    const auto& off = plan.level_off;
-    int L0 = NL;
-    while (L0 > 0 && off[L0] - off[L0 - 1] <= CX_SLOTS) --L0;
-    if (const char* e = getenv("PTZBA_CHOL_XCD")) L0 = atoi(e) > 0 ? std::min(atoi(e), NL) : NL;
-    if (!part_mode && !h->chol_super && L0 < NL - 1) {
-      std::vector<int32_t> lvl(off[NL] - off[L0]), lvl_off(NL - L0 + 1);
-      int wmax = 1;
-      for (int L = L0; L < NL; ++L) {
-        lvl_off[L - L0] = off[L] - off[L0];
-        wmax = std::max(wmax, off[L + 1] - off[L]);
-        for (int t = off[L]; t < off[L + 1]; ++t) lvl[t - off[L0]] = L - L0;
-      }
-      lvl_off[NL - L0] = off[NL] - off[L0];
-      if (upload_st(h, h->cx_lvl, lvl) || upload_st(h, h->cx_lvl_off, lvl_off) ||
-          h->cx_done.alloc((size_t)4 * lvl.size()) || h->cx_ctl.alloc((size_t)2 * 2 * CHOL_XCD_WORDS * 4))
-        return -1;
-      if (zero_async(h, h->cx_ctl.p, h->cx_ctl.bytes) || zero_async(h, h->cx_done.p, h->cx_done.bytes)) return -1;
-      h->cx_epoch = 0;
-      h->cx_on = true;
-      h->cx_L0 = L0;
-      h->cx_grid = 8 * std::min(wmax, CX_SLOTS);  // (blocks are dealt round-robin over the 8 XCDs)
-    }
-  }
-  if ((h->bs_pst || h->cx_on) && !h->bsp_err) HIPCHK(hipHostMalloc((void**)&h->bsp_err, sizeof(int), hipHostMallocDefault));
+  if (h->bs_pst && !h->bsp_err) HIPCHK(hipHostMalloc((void**)&h->bsp_err, sizeof(int), hipHostMallocDefault));
   if (h->bsp_err) *h->bsp_err = 0;  // (a wait that gave up under an earlier problem does not outlive it)
   if (h->bs_pst) {
     if (upload_st(h, h->bsp_expect, plan.bsb_expect) || upload_st(h, h->bsp_tot, plan.bsb_tot) ||
@@ -2460,17 +2421,9 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
       launch_chol_prepare_damped(h->S(), h->ld, h->n_aug, h->bvec(), h->row_pad.as<uint8_t>(), h->info.as<int>(),
                                  h->dU(), h->D_pose.as<double>(), h->frame_pos.as<int32_t>(), h->n_pose, h->n_fixed,
                                  h->lambda, lam_dev, h->st);
-    launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(),
-                    h->cx_on ? h->cx_L0 : h->chol_levels, h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr, th,
-                    h->Minv.as<double>(), 0, h->chol_delayed, h->chol_super ? h->Lsub.as<double>() : nullptr);
-    if (h->cx_on) {
-      const int t0 = h->chol_task_off[h->cx_L0];
-      launch_cholesky_xcd(h->S(), h->ld, h->chol_tasks.as<int4>() + t0, h->cx_lvl.as<int>(),
-                          h->chol_task_off[h->chol_levels] - t0, h->cx_lvl_off.as<int>(), h->cx_done.as<unsigned>(),
-                          ++h->cx_epoch, h->cx_ctl.as<unsigned>(), h->cx_par, h->cx_grid, h->Ldiag.as<double>(),
-                          h->info.as<int>(), h->Minv.as<double>(), h->chol_delayed, h->bsp_err, h->st);
-      h->cx_par ^= 1;
-    }
+    launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
+                      h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>(), 0,
+                      h->chol_delayed, h->chol_super ? h->Lsub.as<double>() : nullptr);
   }
   if (h->bs_pst)
     launch_chol_backsolve_pst(h->S(), h->ld, h->n_aug, h->bsb_tasks.as<int4>(), h->bsp_expect.as<int4>(),
@@ -2610,19 +2563,6 @@ int ptzba_lm_init(ptzba_handle h, const ptzba_lm_opts* o) {
   return 0;
 }
 
-// diagnostics: the XCD-local factorisation tail's control sets (2 x 2 lines of CHOL_XCD_WORDS words: claim, ticket) and
-// done tags after the stream has drained; returns the tags copied (0: no tail), *epoch = the last launch's tag
-extern "C" int ptzba_debug_chol_xcd(ptzba_handle h, uint32_t* ctl, uint32_t* done, int n_done, uint32_t* epoch) {
-  if (!h || !h->cx_on) return 0;
-  HIPCHK(hipSetDevice(h->device));
-  HIPCHK(hipStreamSynchronize(h->st));
-  HIPCHK(hipMemcpy(ctl, h->cx_ctl.p, h->cx_ctl.bytes, hipMemcpyDeviceToHost));
-  const int nd = std::min<int>(n_done, (int)(h->cx_done.bytes / 4));
-  HIPCHK(hipMemcpy(done, h->cx_done.p, (size_t)nd * 4, hipMemcpyDeviceToHost));
-  *epoch = h->cx_epoch;
-  return nd;
-}
-
 int ptzba_lm_build(ptzba_handle h) {
   if (lm_check(h)) return -1;
   HIPCHK(hipSetDevice(h->device));
@@ -2680,9 +2620,9 @@ int ptzba_lm_wait(ptzba_handle h, int trial, ptzba_lm_record* out) {
     }
     __builtin_ia32_pause();
   }
-  if ((h->bs_pst || h->cx_on) && __atomic_load_n(h->bsp_err, __ATOMIC_ACQUIRE))
-    return fail("lm_wait: a persistent factorisation / back-substitution kernel gave up waiting; PTZBA_BS_PERSIST=0 / "
-                "PTZBA_CHOL_XCD=0 select the per-step forms");
+  if (h->bs_pst && __atomic_load_n(h->bsp_err, __ATOMIC_ACQUIRE))
+    return fail("lm_wait: a persistent factorisation / back-substitution kernel gave up waiting (workgroups not "
+                "co-resident?); PTZBA_BS_PERSIST=0 selects the per-step form");
   const LMDev& r = h->lm_host[k];
   out->cost = r.cost;
   out->initial_cost = r.initial_cost;
@@ -2797,9 +2737,8 @@ int ptzba_read_scalars(ptzba_handle h, double* out) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(h->scal_host, h->scal_pack.p, 17 * sizeof(double), hipMemcpyDeviceToHost, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
-  if ((h->bs_pst || h->cx_on) && __atomic_load_n(h->bsp_err, __ATOMIC_ACQUIRE))
-    return fail("a persistent factorisation / back-substitution kernel gave up waiting (PTZBA_BS_PERSIST=0 / "
-                "PTZBA_CHOL_XCD=0 select the per-step forms)");
+  if (h->bs_pst && __atomic_load_n(h->bsp_err, __ATOMIC_ACQUIRE))
+    return fail("the persistent back-substitution kernel gave up waiting (PTZBA_BS_PERSIST=0 selects the per-step form)");
   const double* s = h->scal_host;
   const double* l = h->scal_host + 8;
   out[0] = s[0];

@@ -103,20 +103,18 @@ void launch_chol_prepare_damped(double* A, int64_t ld, int n, double* b, const u
 // then writes them to LDS.  256 threads per workgroup.
 // COH (the SPD level launches' default): tiles are read with agent-scope loads that miss this XCD's L2 and written
 // through with agent-scope stores (MI355X_MICROARCH.md, inter-workgroup hand-off table, first row), so the next
-// level's workgroups on other XCDs find them in the Infinity Cache; plain accesses otherwise (COH = 0).
-// COH = 2 (the XCD-local tail launch, k_chol_xcd): every reader and writer of the tiles runs on ONE XCD, whose L2 is
-// their point of coherence -- plain stores (they stay in that L2), loads that bypass the CU's L1 (`sc1`, L2-served).
-template <int COH>
+// level's workgroups on other XCDs find them in the Infinity Cache; plain accesses otherwise.
+template <bool COH>
 __device__ __forceinline__ double gld(const double* p) {
-  if constexpr (COH != 0) return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if constexpr (COH) return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else return *p;
 }
-template <int COH>
+template <bool COH>
 __device__ __forceinline__ void gst(double* p, double v) {
-  if constexpr (COH == 1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else *p = v;
 }
-template <int COH = 0>
+template <bool COH = false>
 __device__ __forceinline__ void fetch_tile(double (&v)[4], const double* __restrict__ src, int64_t ld) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -406,7 +404,7 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
 // reciprocals, then one wave: lane j computes column j by forward substitution against e_j, right-looking
 // (after m_k is known every later row's running sum takes its term at once: the dependent chain is one
 // multiply and one FMA per row).  Shared by k_tile_inv and the type-2 tasks of the level launches.
-template <int COH = 0>
+template <bool COH = false>
 __device__ __forceinline__ void tile_inv_wave(const double* __restrict__ src, double* __restrict__ dst,
                                               double (*Lt)[NB + 1], double* rinv) {
   for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) Lt[e >> 5][e & 31] = gld<COH>(src + e);
@@ -438,7 +436,7 @@ __device__ __forceinline__ void tile_inv_wave(const double* __restrict__ src, do
 // L_{j0+1,p} (B side) in LDS -- each loaded once for the (up to) two output tiles that use it -- with the next
 // panel's tiles in flight in registers.  Same MFMA sequence per output tile as tile_gemm_nt_sub: bitwise the
 // result of one task per tile.
-template <int COH = 0>
+template <bool COH = false>
 __device__ __forceinline__ void chol_trail_block(double* __restrict__ A, int64_t ld, int i0, int j0, int mask, int up0,
                                                  int up1, int up2, int up3, double (*sA)[NB][NB + 1],
                                                  double (*sB)[NB][NB + 1]) {
@@ -533,7 +531,7 @@ struct CholTaskVal {
 // Ldiag and L10 to Lsub[k], which the type-2 task of the next level copies into A_k+1,k (no task of that level reads
 // the tile).  Tiles: D00 sD, D10 sC, D11 sE[0], T0 sE[1], T1 sB[1]; panel staging sA[0] (L_kp), sA[1] (L_k+1,p),
 // sB[0] (L_ip); the sweeps' block buffer overlays sA as in chol_task.
-template <int COH>
+template <bool COH>
 __device__ __forceinline__ void chol_super(double* __restrict__ A, int64_t ld, int i, int k, const int (&ups)[8],
                                            double* __restrict__ Ldiag, int* info, double* __restrict__ Lsub,
                                            double (*sD)[NB + 1], double (*sC)[NB + 1], double (*sA)[NB][NB + 1],
@@ -641,7 +639,7 @@ __device__ __forceinline__ void chol_super(double* __restrict__ A, int64_t ld, i
 // P2: plans with delayed trailing updates (a second pair of update panels per task, api.hip make_plan)
 // One factorisation task (api.hip make_plan: panel / trailing / inverse / trailing block) by the workgroup: the
 // body of a level launch (k_chol_step).
-template <bool SG, bool P2, int COH, bool SUP = false>
+template <bool SG, bool P2, bool COH, bool SUP = false>
 __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, const int4 tk, double* __restrict__ Ldiag,
                                           int* info, double* __restrict__ sgn, double* __restrict__ Minv,
                                           double* __restrict__ Lsub = nullptr, int4 tk2 = int4{0, 0, 0, 0}) {
@@ -902,7 +900,7 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
   for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) gst<COH>(C + (int64_t)(e >> 5) * ld + (e & 31), sC[e >> 5][e & 31]);
 }
 
-template <bool SG, typename TaskArg, bool P2 = false, int COH = 0, bool SUP = false>
+template <bool SG, typename TaskArg, bool P2 = false, bool COH = false, bool SUP = false>
 __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64_t ld, const TaskArg tasks,
                                                    double* __restrict__ Ldiag, int* info, double* __restrict__ sgn,
                                                    double* __restrict__ Minv, double* __restrict__ Lsub) {
@@ -917,7 +915,7 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64
 // (Rounds 4 tried every level of a factorisation in ONE launch -- one workgroup per task, a task of level L waiting
 // on level L - 1's completion counter: bitwise the same factor, 338-425 us per trial against ~232 with one launch per
 // level; removed in round 5.)
-template <typename TaskArg, int COH>
+template <typename TaskArg, bool COH>
 static void launch_chol_level(const TaskArg& ta, int n, double* A, int64_t ld, double* Ldiag, int* info, double* sgn,
                               double* Minv, bool delayed, hipStream_t st, double* Lsub) {
   if (sgn)
@@ -955,125 +953,6 @@ void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_o
     if (coh) launch_chol_level<CholTaskPtr, true>(tp, n, A, ld, Ldiag, info, sgn, Minv, delayed, st, Lsub);
     else launch_chol_level<CholTaskPtr, false>(tp, n, A, ld, Ldiag, info, sgn, Minv, delayed, st, Lsub);
   }
-}
-
-// XCD-local tail of the factorisation: the levels [L0, L1) -- the narrow ones, whose task counts fit one XCD's
-// workgroup slots -- in ONE launch whose working workgroups all sit on ONE XCD.  Every workgroup reads its XCD id
-// (HW_REG_XCC_ID); the first to arrive claims its XCD for the launch (agent-scope CAS), the others of that XCD take
-// tasks, the rest exit at once.  Correctness does not depend on where blocks land: only the workgroups that ARE on
-// the claimed XCD touch the tiles, and a single one of them would finish the list alone.
-//   * Tasks are taken in plan order from a ticket; a task of relative level l > 0 first waits until every task of
-//     level l - 1 has posted its done tag.  A workgroup takes its next ticket while it runs the current task (the
-//     atomic's round trip hides under the task).  Tickets are taken in order and a task only waits on lower tickets,
-//     all held by running workgroups that reach them: no co-residency is needed, no wait can deadlock.
-//   * Hand-off inside the XCD: the task's tile stores are plain (they land in the shared L2: the vector L1 is write-
-//     through), every thread waits for them (vmcnt(0)), the workgroup meets a barrier, one lane stores the task's done
-//     tag (plain: it stays in the L2, where the pollers' L1-bypassing loads find it -- an atomic would go to memory);
-//     wave 0 of a waiting workgroup polls the level's tags with one coalesced L1-bypassing load and, after a barrier,
-//     the workgroup reads tiles with L1-bypassing loads (COH = 2).  The launch boundary writes the L2 back.
-//   * The same tasks in the same order per tile as the level launches: bitwise the same factor.
-//   * done[n]: tag = this launch's epoch (host counter, from 1; set_problem zeroes the tags), so no clearing.  ctl: two
-//     sets (parity of the launch, alternating) of two CX_WORDS lines -- the XCD claim and the ticket; the claiming
-//     workgroup clears the OTHER set for the next launch (the one before it finished at this launch's boundary).
-//   * Control flow around the task loop is wave-uniform (readfirstlane values, wave 0 as a whole): with a per-lane
-//     condition (thread 0 only) the compiler structurises the loop so that the other lanes re-enter the task body on
-//     their own and spin on a stale ticket.
-//   * Waits are bounded (CX_SPIN polls): one that gives up raises the pinned host flag `err` (lm_wait fails loudly).
-constexpr int CX_WORDS = CHOL_XCD_WORDS;  // 128-B control lines
-constexpr int CX_SPIN = 1 << 18;    // polls before a wait gives up (~0.1-0.3 s; a level takes microseconds)
-constexpr int CX_HWREG_XCC_ID = (3 << 11) | 20;  // s_getreg_b32 hwreg(HW_REG_XCC_ID, 0, 4)
-template <bool P2>
-__global__ __launch_bounds__(256, 2) void k_chol_xcd(double* __restrict__ A, int64_t ld, const int4* __restrict__ tasks,
-                                                  const int* __restrict__ task_lvl, int n, const int* __restrict__ lvl_off,
-                                                  unsigned* __restrict__ done, unsigned epoch, unsigned* __restrict__ ctl,
-                                                  int par, double* __restrict__ Ldiag, int* info,
-                                                  double* __restrict__ Minv, int* err) {
-  __shared__ int s_t;
-  __shared__ int4 s_task;
-  unsigned* c = ctl + (int64_t)par * 2 * CX_WORDS;
-  const bool w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
-  const int lane = threadIdx.x & 63;
-  const bool l0 = lane == 0;
-  if (threadIdx.x == 0) {
-    const unsigned me = ((unsigned)__builtin_amdgcn_s_getreg(CX_HWREG_XCC_ID) & 15u) + 1u;
-    unsigned owner = 0;
-    if (__hip_atomic_compare_exchange_strong(c, &owner, me, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT)) {
-      owner = me;
-      unsigned* o = ctl + (int64_t)(par ^ 1) * 2 * CX_WORDS;
-      __hip_atomic_store(o, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      o[CX_WORDS] = 0u;
-    }
-    s_t = owner == me ? 0 : -1;
-  }
-  __syncthreads();
-  if (__builtin_amdgcn_readfirstlane(s_t) < 0) return;
-  unsigned tk = 0;  // wave 0, lane 0: the next ticket
-  if (w0 && l0) tk = __hip_atomic_fetch_add(c + CX_WORDS, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  for (;;) {
-    if (w0) {
-      const int t = __builtin_amdgcn_readfirstlane((int)tk);
-      if (t < n) {
-        const int4 rec = tasks[t];
-        const int l = task_lvl[t];
-        if (l > 0) {
-          const int lo = lvl_off[l - 1], hi = lvl_off[l];
-          for (int b = lo; b < hi; b += 64) {  // the level's done tags, 64 per coalesced load
-            const int q = b + lane;
-            for (int k = 0;; ++k) {
-              const bool ok = q >= hi || __hip_atomic_load(done + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
-              if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
-              if (k == CX_SPIN) {
-                if (l0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                break;
-              }
-              __builtin_amdgcn_s_sleep(1);
-            }
-          }
-        }
-        if (l0) {
-          s_task = rec;
-          tk = __hip_atomic_fetch_add(c + CX_WORDS, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-      }
-      if (l0) s_t = t;
-    }
-    __syncthreads();
-    const int t = __builtin_amdgcn_readfirstlane(s_t);
-    if (t >= n) return;
-    const int4 tr = s_task;
-    const int4 task{__builtin_amdgcn_readfirstlane(tr.x), __builtin_amdgcn_readfirstlane(tr.y),
-                    __builtin_amdgcn_readfirstlane(tr.z), __builtin_amdgcn_readfirstlane(tr.w)};
-    chol_task<false, P2, 2>(A, ld, task, Ldiag, info, nullptr, Minv);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's tile stores are in the XCD's L2
-    __syncthreads();                                   // ... every thread's
-    if (w0 && l0) done[t] = epoch;
-  }
-}
-
-// diagnostics: the XCD id (HW_REG_XCC_ID) each of n workgroups of 256 threads ran on
-__global__ void k_xcc_census(int* out) {
-  if (threadIdx.x == 0) out[blockIdx.x] = (int)(__builtin_amdgcn_s_getreg(CX_HWREG_XCC_ID) & 15u);
-}
-extern "C" int ptzba_debug_xcc_census(int n, int* out) {
-  int* d = nullptr;
-  if (hipMalloc(&d, sizeof(int) * n) != hipSuccess) return -1;
-  hipLaunchKernelGGL(k_xcc_census, dim3(n), dim3(256), 0, 0, d);
-  const bool ok = hipMemcpy(out, d, sizeof(int) * n, hipMemcpyDeviceToHost) == hipSuccess;
-  (void)hipFree(d);
-  return ok ? 0 : -1;
-}
-
-void launch_cholesky_xcd(double* A, int64_t ld, const int4* tasks, const int* task_lvl, int n, const int* lvl_off,
-                         unsigned* done, unsigned epoch, unsigned* ctl, int par, int grid, double* Ldiag, int* info,
-                         double* Minv, bool delayed, int* err, hipStream_t st) {
-  if (n <= 0) return;
-  if (delayed)
-    hipLaunchKernelGGL(k_chol_xcd<true>, dim3((unsigned)grid), dim3(256), 0, st, A, ld, tasks, task_lvl, n, lvl_off, done,
-                       epoch, ctl, par, Ldiag, info, Minv, err);
-  else
-    hipLaunchKernelGGL(k_chol_xcd<false>, dim3((unsigned)grid), dim3(256), 0, st, A, ld, tasks, task_lvl, n, lvl_off,
-                       done, epoch, ctl, par, Ldiag, info, Minv, err);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -262,15 +262,10 @@ void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_o
                      int first_level = 0,     // levels [first_level, n_launch)
                      bool delayed = false,    // tasks carry a second pair of update panels (api.hip make_plan)
                      double* Lsub = nullptr); // plans with supercolumn tasks: L_k+1,k of each pair (chol_super)
-// XCD-local tail of an SPD factorisation (k_chol_xcd, one launch): tasks [n] of the levels [L0, L1) in plan order,
-// task_lvl[t] = level of task t relative to L0, lvl_off[l] = first task of relative level l (n_lvl + 1 entries), done[n]
-// = per-task done tags (zeroed at set_problem; this launch posts `epoch`, a counter from 1), ctl: two control sets of
-// two 128-B lines (claim, ticket; zeroed at set_problem; par alternates per launch), grid: workgroups launched (those
-// of one XCD work), err: host-pinned flag set when a wait gave up.
-void launch_cholesky_xcd(double* A, int64_t ld, const int4* tasks, const int* task_lvl, int n, const int* lvl_off,
-                         unsigned* done, unsigned epoch, unsigned* ctl, int par, int grid, double* Ldiag, int* info,
-                         double* Minv, bool delayed, int* err, hipStream_t st);
-constexpr int CHOL_XCD_WORDS = 32;  // words per control line of launch_cholesky_xcd
+// single-launch form of levels [L0, L1) (SPD, single process): one workgroup per task taking its task by ticket,
+// per-level completion counters lvl_cnt and the ticket counter monotone over launches (epoch = launches so far over
+// the same level range); task_lvl[t] = level of task t, lvl_n[L] = tasks of level L; err: host-pinned flag set when
+// a wait gave up.
 
 // la_tasks: lookahead back substitution's [lookahead tile per position | task offsets per (chain, helper) |
 // tasks q << 16 | tile], built by the host plan (api.hip make_plan)

@@ -562,15 +562,12 @@ def test_reduced_system_matrix_core_k2_matches_fp64(gpu_available, config, loss)
     assert tail < 1e-5, tail
 
 
-@pytest.mark.parametrize("config,knob", [("config2", "PTZBA_BS_PERSIST=0"), ("grid", "PTZBA_BS_PERSIST=0"),
-                                         ("config2", "PTZBA_CHOL_XCD=0"), ("grid", "PTZBA_CHOL_XCD=0")])
+@pytest.mark.parametrize("config,knob", [("config2", "PTZBA_BS_PERSIST=0"), ("grid", "PTZBA_BS_PERSIST=0")])
 def test_single_launch_schedules_bitwise_equal(gpu_available, config, knob, monkeypatch):
-    """Schedule-only forms of the back-substitution / factorisation give bit-identical LM iterates: PTZBA_BS_PERSIST=0 --
-    the per-step blocked back-substitution against the single-launch one (the default, per-column counters);
-    PTZBA_CHOL_XCD=0 -- one launch per factorisation level against every level after the first in one XCD-local
-    launch (=1, k_chol_xcd).  config 2 (natural / one-level plan) and the 3-row grid (delayed trailing updates: the
-    second panel pair and 2 x 2 trailing blocks); 3 solves of 3 LM iterations per handle, so the counters run over
-    several epochs."""
+    """Schedule-only forms of the back-substitution give bit-identical LM iterates: PTZBA_BS_PERSIST=0 -- the per-step
+    blocked back-substitution against the single-launch one (the default, per-column counters).  config 2 (natural /
+    one-level plan) and the 3-row grid (delayed trailing updates: the second panel pair and 2 x 2 trailing blocks); 3
+    solves of 3 LM iterations per handle, so the counters run over several epochs."""
     import ptzba
     import synthetic
     if config == "grid":
