@@ -256,6 +256,15 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const int kb = s * BW;
+      // the previous block's factor rows kb..kb+BW-1 (this wave's own stores) are read before the wait for the
+      // helpers: their LDS round trip overlaps the poll's instead of following it
+      double pl[BW][BW];
+      if (s > 0) {
+#pragma unroll
+        for (int j = 0; j < BW; ++j)
+#pragma unroll
+          for (int k = 0; k < BW; ++k) pl[j][k] = Lb[s - 1][kb + j][k];
+      }
       if (s >= 2) {
         while (lds_poll(&nu[s - 1]) < 3) __builtin_amdgcn_s_sleep(0);
       }
@@ -267,7 +276,7 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
         for (int j = 0; j < BW; ++j) {
           double acc = a[j];
 #pragma unroll
-          for (int k = 0; k < BW; ++k) acc = fma(-lp[k], Lb[s - 1][kb + j][k], acc);
+          for (int k = 0; k < BW; ++k) acc = fma(-lp[k], pl[j][k], acc);
           a[j] = acc;
         }
       }
