@@ -114,19 +114,40 @@ __device__ __forceinline__ void gst(double* p, double v) {
   if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else *p = v;
 }
+// A thread stages two pairs of adjacent elements of a tile (pair p = threadIdx.x + 256 q: row p >> 4, columns
+// 2 (p & 15) and 2 (p & 15) + 1) with 16-B loads -- half the load instructions of one element per load; COH: `sc1`
+// buffer loads (aux 16), as the agent-scope loads above (tiles and ld are 16-B aligned: ld, the tile offsets and the
+// pair columns are even)
+typedef int v4i32 __attribute__((ext_vector_type(4)));
 template <bool COH = false>
 __device__ __forceinline__ void fetch_tile(double (&v)[4], const double* __restrict__ src, int64_t ld) {
+  if constexpr (COH) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(src), 0,
+                                                                       (int)((31 * ld + NB) * 8), 0x00020000);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int e = threadIdx.x + 256 * q;
-    v[q] = gld<COH>(src + (int64_t)(e >> 5) * ld + (e & 31));
+    for (int q = 0; q < 2; ++q) {
+      const int p = threadIdx.x + 256 * q;
+      const v4i32 x = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((p >> 4) * ld + 2 * (p & 15)) * 8), 0, 16);
+      const double2 d = __builtin_bit_cast(double2, x);
+      v[2 * q] = d.x;
+      v[2 * q + 1] = d.y;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int p = threadIdx.x + 256 * q;
+      const double2 d = *reinterpret_cast<const double2*>(src + (int64_t)(p >> 4) * ld + 2 * (p & 15));
+      v[2 * q] = d.x;
+      v[2 * q + 1] = d.y;
+    }
   }
 }
 __device__ __forceinline__ void put_tile(double (*dst)[NB + 1], const double (&v)[4]) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int e = threadIdx.x + 256 * q;
-    dst[e >> 5][e & 31] = v[q];
+  for (int q = 0; q < 2; ++q) {
+    const int p = threadIdx.x + 256 * q;
+    dst[p >> 4][2 * (p & 15)] = v[2 * q];
+    dst[p >> 4][2 * (p & 15) + 1] = v[2 * q + 1];
   }
 }
 
