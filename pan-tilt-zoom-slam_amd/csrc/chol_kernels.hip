@@ -142,6 +142,20 @@ __device__ __forceinline__ void fetch_tile(double (&v)[4], const double* __restr
     }
   }
 }
+// The tile stores in the same pair order: 16-B stores of get(row, col), get(row, col + 1); COH: `sc1` buffer stores
+// (write-through, as gst)
+template <bool COH, typename F>
+__device__ __forceinline__ void store_tile(double* __restrict__ dst, int64_t ld, F get) {
+  __amdgpu_buffer_rsrc_t rs;
+  if constexpr (COH) rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)((31 * ld + NB) * 8), 0x00020000);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int p = threadIdx.x + 256 * q, r = p >> 4, c = 2 * (p & 15);
+    const double2 d{get(r, c), get(r, c + 1)};
+    if constexpr (COH) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i32, d), rs, (int)((r * ld + c) * 8), 0, 16);
+    else *reinterpret_cast<double2*>(dst + (int64_t)r * ld + c) = d;
+  }
+}
 __device__ __forceinline__ void put_tile(double (*dst)[NB + 1], const double (&v)[4]) {
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
@@ -832,7 +846,7 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
       }
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) gst<COH>(C + (int64_t)(e >> 5) * ld + (e & 31), sC[e >> 5][e & 31]);
+    store_tile<COH>(C, ld, [&](int r, int m) { return sC[r][m]; });
     return;
   }
   // panel task (i, k = j)
@@ -900,20 +914,15 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
 #if CHOL_DIRECT_STORE
   // the factor goes to memory straight from the sweep's block buffer (rows 0..31: D, 32..63: T)
   if (diag_only) {
-    double* C = Ldiag + (int64_t)k * NB * NB;
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-      const int r = e >> 5, m = e & 31;
-      gst<COH>(C + e, m <= r ? s_lb[m / LA_BW][r][m % LA_BW] : 0.0);
-    }
+    store_tile<COH>(Ldiag + (int64_t)k * NB * NB, NB,
+                    [&](int r, int m) { return m <= r ? s_lb[m / LA_BW][r][m % LA_BW] : 0.0; });
     if constexpr (SG) {
       if (threadIdx.x < NB) sgn[(int64_t)k * NB + threadIdx.x] = s_sig[threadIdx.x];
     }
     return;
   }
   {
-    double* C = A + i * NBl * ld + k * NBl;
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x)
-      gst<COH>(C + (int64_t)(e >> 5) * ld + (e & 31), s_lb[(e & 31) / LA_BW][NB + (e >> 5)][(e & 31) % LA_BW]);
+    store_tile<COH>(A + i * NBl * ld + k * NBl, ld, [&](int r, int m) { return s_lb[m / LA_BW][NB + r][m % LA_BW]; });
     return;
   }
 #endif
