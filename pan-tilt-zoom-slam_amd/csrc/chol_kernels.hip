@@ -211,20 +211,8 @@ __device__ int g_cs_level;
 #ifndef BS_LOADERS
 #define BS_LOADERS 1  // loader waves of the lookahead back-solve (2: ring positions alternate; measured neutral)
 #endif
-#ifndef CHOL_FEWER_BARRIERS
-#define CHOL_FEWER_BARRIERS 0  // 1: drop the sweep's entry barrier and the caller's exit barrier (A/B)
-#endif
-#ifndef CHOL_DIRECT_STORE
-#define CHOL_DIRECT_STORE 1  // store the factor tiles straight from the sweep's block buffer (0: copy back to the tiles first)
-#endif
-#ifndef CHOL_P_READLANE
-#define CHOL_P_READLANE 1  // 1: the pivot block by v_readlane instead of an LDS round trip (flag form)
-#endif
 #ifndef LA_BW
 #define LA_BW 4  // pivot block of the lookahead form
-#endif
-#ifndef CHOL_LB_ALIAS
-#define CHOL_LB_ALIAS 1  // the sweep's block buffer overlays the update panels (0: a buffer of its own, A/B)
 #endif
 // reciprocal square root by a series step on the hardware estimate: e = 1 - d y0^2 (|e| ~ 5e-8),
 // y = y0 (1 + e/2 + 3e^2/8) -- full double precision in 4 dependent operations (rsq_nr: 6)
@@ -274,10 +262,8 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
   double* row = (isT && T) ? T[r] : D[r];
   int* nl = flags;
   int* nu = flags + 1;  // [NS]
-#if !CHOL_FEWER_BARRIERS
   if (threadIdx.x <= NS) flags[threadIdx.x] = 0;
   __syncthreads();
-#endif  // else the caller zeroed the flags before its staging barrier and fenced the panel updates
 #ifdef CS_TIMING
   long long* wst = g_cs_wg[g_cs_level < 64 ? g_cs_level : 63];
   const bool wrec = threadIdx.x == 0 && blockIdx.x == 0;
@@ -316,25 +302,12 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
         }
       }
       double P[BW][BW], y[BW], sg[BW];
-#if CHOL_P_READLANE
       // the BW x BW diagonal block lives in lanes kb..kb+BW-1 of this wave: read it lane to lane
       // (v_readlane, uniform lane indices) instead of a round trip through LDS
 #pragma unroll
       for (int i = 0; i < BW; ++i)
 #pragma unroll
         for (int j = 0; j <= i; ++j) P[i][j] = bcast(a[j], kb + i);
-#else
-      if (lane >= kb && lane < kb + BW) {
-#pragma unroll
-        for (int j = 0; j < BW; ++j) Pb[lane - kb][j] = a[j];
-      }
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int i = 0; i < BW; ++i)
-#pragma unroll
-        for (int j = 0; j <= i; ++j) P[i][j] = Pb[i][j];
-#endif
 #pragma unroll
       for (int j = 0; j < BW; ++j) {
         double d = P[j][j];
@@ -419,19 +392,6 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
     }
   }
   __syncthreads();
-#if !CHOL_DIRECT_STORE
-  // wave w writes columns 8w .. 8w+7 of the factor
-  if (have) {
-#pragma unroll
-    for (int j = 0; j < NB / 4; ++j) {
-      const int m = w * (NB / 4) + j;
-      const double val = Lb[m / BW][lane][m % BW];
-      if (isT) T[r][m] = val;
-      else D[r][m] = (m <= r) ? val : 0.0;
-    }
-  }
-  __syncthreads();
-#endif
 }
 
 #ifdef CS_TIMING
@@ -687,22 +647,18 @@ template <bool SG, bool P2, bool COH, bool SUP = false>
 __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, const int4 tk, double* __restrict__ Ldiag,
                                           int* info, double* __restrict__ sgn, double* __restrict__ Minv,
                                           double* __restrict__ Lsub = nullptr, int4 tk2 = int4{0, 0, 0, 0}) {
-  static_assert(!SUP || (P2 && !SG && CHOL_LB_ALIAS && CHOL_DIRECT_STORE && !CHOL_FEWER_BARRIERS),
+  static_assert(!SUP || (P2 && !SG),
                 "supercolumn tasks: the P2 kernel of SPD plans with the default sweep");
   static_assert(!(COH && SG), "the persistent form factors SPD systems only");
   __shared__ double sC[NB][NB + 1];     // target tile (panel T_ik / trailing A_ij)
   __shared__ double sD[NB][NB + 1];     // diagonal tile -> L_kk
   __shared__ __attribute__((aligned(16))) double sA[2][NB][NB + 1];  // L_ip of the two update panels
   __shared__ double sB[2][NB][NB + 1];  // L_kp or L_jp of the two update panels
-#if CHOL_LB_ALIAS
   // the sweep's block buffer overlays the update panels' L_ip tiles, dead once the panel GEMMs are done (a
   // barrier separates them): 51 KB of LDS per workgroup instead of 67, so three workgroups per CU instead of
   // two -- config 4's levels carry ~1,600 trailing tasks, whose time is load latency x rounds of residency
   static_assert((NB / LA_BW) * 2 * NB * LA_BW <= 2 * NB * (NB + 1), "block buffer must fit the panel tiles");
   double (*s_lb)[2 * NB][LA_BW] = reinterpret_cast<double (*)[2 * NB][LA_BW]>(&sA[0][0][0]);
-#else
-  __shared__ __attribute__((aligned(16))) double s_lb[NB / LA_BW][2 * NB][LA_BW];
-#endif
   __shared__ __attribute__((aligned(16))) double s_pb[LA_BW][LA_BW];
   __shared__ int s_flags[NB / LA_BW + 1];
   __shared__ double s_sgp[2][NB];  // SG: signs of the two update panels' columns
@@ -721,9 +677,6 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
     tile_inv_wave<COH>(Ldiag + (int64_t)tk.y * NB * NB, Minv + (int64_t)tk.y * NB * NB, sD, s_rinv);
     return;
   }
-#if CHOL_FEWER_BARRIERS
-  if (threadIdx.x <= NB / LA_BW) s_flags[threadIdx.x] = 0;  // the sweep's counters (ordered by the staging barrier)
-#endif
   const int type = tk.x & 3, i = tk.y, j = tk.z;
   const int up0 = (tk.w & 0x3fff) - 1;
   const int up1 = ((tk.w >> 14) & 0x3fff) - 1;
@@ -901,9 +854,7 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
   __syncthreads();
   CS_STAMP(2);
   wg_potrf_trsm32_df<LA_BW, SG>(sD, diag_only ? nullptr : sC, s_lb, s_pb, s_flags, info, s_sig);
-#if !(CHOL_FEWER_BARRIERS && CHOL_DIRECT_STORE)
   __syncthreads();  // (the flag-synchronised sweep ends in a barrier of its own)
-#endif
   CS_STAMP(3);
 #ifdef CS_TIMING
   if (threadIdx.x == 0 && blockIdx.x == 0) {
@@ -911,7 +862,6 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
     g_cs_level = cs_lvl + 1;
   }
 #endif
-#if CHOL_DIRECT_STORE
   // the factor goes to memory straight from the sweep's block buffer (rows 0..31: D, 32..63: T)
   if (diag_only) {
     store_tile<COH>(Ldiag + (int64_t)k * NB * NB, NB,
@@ -921,22 +871,8 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
     }
     return;
   }
-  {
-    store_tile<COH>(A + i * NBl * ld + k * NBl, ld, [&](int r, int m) { return s_lb[m / LA_BW][NB + r][m % LA_BW]; });
-    return;
-  }
-#endif
-  if (diag_only) {
-    // A_kk itself stays untouched: other panel workgroups of this launch are still reading it
-    double* C = Ldiag + (int64_t)k * NB * NB;
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) gst<COH>(C + e, sD[e >> 5][e & 31]);
-    if constexpr (SG) {
-      if (threadIdx.x < NB) sgn[(int64_t)k * NB + threadIdx.x] = s_sig[threadIdx.x];
-    }
-    return;
-  }
-  double* C = A + i * NBl * ld + k * NBl;
-  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) gst<COH>(C + (int64_t)(e >> 5) * ld + (e & 31), sC[e >> 5][e & 31]);
+  // (A_kk itself stays untouched: other panel workgroups of this launch are still reading it)
+  store_tile<COH>(A + i * NBl * ld + k * NBl, ld, [&](int r, int m) { return s_lb[m / LA_BW][NB + r][m % LA_BW]; });
 }
 
 template <bool SG, typename TaskArg, bool P2 = false, bool COH = false, bool SUP = false>
