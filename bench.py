@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--no-secondary", action="store_true", help="skip the fp64 / linear-loss leg")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold-cache K1 pass")
     ap.add_argument("--dry-run", action="store_true", help="launcher / rendezvous plumbing only (no GPU work)")
+    ap.add_argument("--config4-steps", type=int, default=3,
+                    help="secondary leg after a config3 headline: timed LM iterations of config 4 (5000 KF x 200k rays) at "
+                         "the same N (0: skip)")
     ap.add_argument("--stream-frames", type=int, default=300,
                     help="config-5 leg: frames of demo_stream.py after the headline (0: skip); 300 = 60 keyframes, so the "
                          "30-keyframe sliding window is full for the second half (100 frames never fill it)")
@@ -212,6 +215,215 @@ def _git_blob(path):
 
 K1_PASS_ITERS = 64  # LM iterations of the dedicated K1 timing pass (>= 64 event-bracketed K1 launches)
 K1_COLD_ITERS = 16  # LM iterations of the cold-cache K1 pass (a 1 GiB flush before each K1 launch)
+BASELINE_METRIC = "BA iterations/sec at 500 KF x 20k rays; pan-tilt-focal RMSE vs reference"  # BASELINE.json metric
+
+
+def metric_name(cfg):
+    """BASELINE.json's metric for the headline config; the same wording with the config's own size otherwise (a
+    --config config4 line must not carry the headline's name)."""
+    import synthetic
+    if cfg == "config3":
+        return BASELINE_METRIC
+    n_kf, n_rays = synthetic.CONFIGS[cfg][:2]
+    return f"BA iterations/sec at {n_kf} KF x {n_rays // 1000}k rays; pan-tilt-focal RMSE vs reference"
+
+
+class Ctx:
+    """Per-process run context: rank / world, torch.distributed, the stream, the library's RCCL communicator."""
+
+    def __init__(self, a, world, rank, local, dist, backend, stream, comm):
+        self.a, self.world, self.rank, self.local, self.dist, self.backend = a, world, rank, local, dist, backend
+        self.stream, self.comm = stream, comm
+
+
+def setup_leg(cx, cfg):
+    """Problem of BASELINE config `cfg` (synthetic, seed 0), sharded over the ranks in the form the planner predicts
+    faster (ptzba.choose_dist_form: rank tree or replicated; PTZBA_DIST_MODE=part|replicated forces one), on a handle
+    with x0 saved on the device.  Returns a dict of everything the legs report."""
+    import ptzba
+    import synthetic
+    a, world, rank = cx.a, cx.world, cx.rank
+    t0 = time.perf_counter()
+    prob = synthetic.make_problem(cfg, seed=0)
+    t_gen = time.perf_counter() - t0
+    frame, landmark, xy, w = prob.frame, prob.landmark, prob.xy, None
+    if a.form == "dedup":
+        frame, landmark, xy, w, _ = synthetic.dedup_records(frame, landmark, xy)
+    # the coupling window of the WHOLE problem: every rank passes the same one, so all ranks choose the same system
+    # order and take bit-identical pose steps
+    win_hi = ptzba.frame_coupling_window(prob.n_pose, frame, landmark)
+    dist_mode, split, form_est = "single", None, None
+    if world > 1:
+        form, form_est = ptzba.choose_dist_form(win_hi, world)
+        env = os.environ.get("PTZBA_DIST_MODE")
+        if env in ("part", "tree"):
+            form = "tree"
+        elif env == "replicated":
+            form = "replicated"
+        if form == "tree":
+            owner, mode, split = ptzba.partition_landmarks(prob.n_pose, prob.n_landmark, frame, landmark, world)
+            if mode != 1:
+                form = "replicated"
+        if form == "replicated":
+            owner = ptzba.replicated_shards(landmark, prob.n_landmark, world)
+        sel = owner[landmark] == rank
+        dist_mode = "part-owned" if form == "tree" else "replicated"
+        frame, landmark, xy = frame[sel], landmark[sel], xy[sel]
+        w = None if w is None else w[sel]
+    precision = ptzba.FP32 if a.precision == "fp32" else ptzba.FP64
+    loss = ptzba.LOSS_HUBER if a.loss == "huber" else ptzba.LOSS_LINEAR
+    h = ptzba.BAHandle(cx.local if world > 1 else 0)
+    h.set_stream(cx.stream.cuda_stream)
+    t1 = time.perf_counter()
+    h.set_problem(prob.n_pose, prob.n_landmark, frame, landmark, xy, prob.u, prob.v, weight=w, precision=precision,
+                  loss=loss, f_scale=1.0, frame_win_hi=win_hi, dist_world=world if dist_mode == "part-owned" else 0,
+                  dist_rank=rank)
+    t_setup = time.perf_counter() - t1
+    xinfo = None
+    if world > 1:
+        # the library runs every exchange itself: through its own RCCL communicator (one per rank, from an RCCL unique
+        # id rank 0 makes and torch.distributed ships), or -- gloo rehearsals of several ranks on one device --
+        # through a hook over torch.distributed
+        if cx.comm is None:
+            h.set_exchange_hook(ptzba.torch_exchange_hook(h, cx.dist, f"cuda:{cx.local}"))
+        else:
+            h.attach_comm(cx.comm)
+        xinfo = h.dist_info()
+        xinfo["exchanges"] = h.dist_exchanges()  # (kind, group first rank, group size, doubles) per trial
+        if xinfo["sys_doubles"] == 0 and xinfo["mode"] == "replicated":
+            xinfo["sys_doubles"] = h.exchange_packed()[1]
+        xinfo["form"] = dist_mode
+        xinfo["form_estimate"] = form_est
+    # x0 is uploaded once and kept on the device: each solve restarts from it without a PCIe transfer
+    h.set_state(prob.init_ptz, prob.init_rays)
+    h.save_state()
+    return dict(cfg=cfg, prob=prob, frame=frame, landmark=landmark, xy=xy, w=w, h=h, info=h.info(),
+                sinfo=h.solver_info(), xinfo=xinfo, dist_mode=dist_mode, split=split, precision=precision, loss=loss,
+                generate_s=t_gen, set_problem_s=t_setup)
+
+
+def run_iters(hh, k, ar=None):
+    """k LM iterations (scipy njev) of restarted ftol=1e-4 solves from the device-resident x0 (ptzba_solve_resident: the
+    restart is enqueued by C the moment the final decision is on the host; PTZBA_BENCH_PYLOOP=1: the Python loop)."""
+    import ptzba
+    pyloop = os.environ.get("PTZBA_BENCH_PYLOOP") == "1"
+    done = 0
+    solves = 0
+    while done < k:
+        if pyloop or ar is not None:
+            hh.restore_state()
+            res = ptzba.LMSolver(hh, ftol=1e-4, xtol=1e-8, max_iter=k - done, allreduce=ar).run()
+        else:
+            res = hh.solve_resident(restore=True, ftol=1e-4, xtol=1e-8, max_iter=k - done)
+        done += max(res.njev, 1)
+        solves += 1
+        if res.njev == 0:
+            break
+    return done, solves
+
+
+def timed(cx, hh, steps):
+    """Exactly `steps` iterations between a barrier + device synchronisation on both sides; the max over ranks."""
+    import torch
+    if cx.dist:
+        cx.dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    its, nsolve = run_iters(hh, steps)
+    torch.cuda.synchronize()
+    if cx.dist:
+        cx.dist.barrier()
+    el = time.perf_counter() - t0
+    if cx.dist:
+        tt = torch.tensor([el], dtype=torch.float64, device=f"cuda:{cx.local}")
+        cx.dist.all_reduce(tt, op=cx.dist.ReduceOp.MAX)
+        el = float(tt.item())
+    return its, nsolve, el
+
+
+KIND_NAMES = {0: "X_SYS", 1: "X_PART", 2: "X_SEP", 3: "X_SCAL", 4: "X_SUB"}
+
+
+def breakdown(cx, h, iters):
+    """Kernel-group times (HIP events: K1, Schur, factorisation + back-solve, trial) over `iters` iterations after the
+    timed region, and at N > 1 every collective (ptzba_comm_times: an event pair around each exchange on the handle's
+    stream) -- per rank, gathered to every rank."""
+    import ptzba
+    h.reset_kernel_times(True, groups=0xF | (ptzba.TIME_COMM if cx.world > 1 else 0))
+    its, _ = run_iters(h, iters)
+    ktn = h.kernel_times()
+    kt = {k: v[0] for k, v in ktn.items()}
+    rec = None
+    if cx.world > 1:
+        ct = h.comm_times()
+        by = {}
+        for kind, n, ms in ct:
+            d = by.setdefault(KIND_NAMES.get(kind, str(kind)), {"n": 0, "ms": 0.0, "bytes": 0})
+            d["n"] += 1
+            d["ms"] += ms
+            d["bytes"] += 8 * n
+        for d in by.values():
+            d["avg_ms"] = d["ms"] / d["n"]
+            d["avg_bytes"] = d["bytes"] / d["n"]
+        tot_ms = sum(ms for _, _, ms in ct)
+        rec = {"rank": cx.rank, "kernel_ms": kt, "iterations": its,
+               "collective_ms_per_iteration": tot_ms / max(its, 1),
+               "collective_bytes_per_iteration": sum(8 * n for _, n, _ in ct) / max(its, 1),
+               "n_collectives_per_iteration": len(ct) / max(its, 1),
+               # the factorisation group's span (one per trial) contains the tree's in-phase exchanges: net of them
+               "factorisation_ms_net": kt["cholesky_solve"] - sum(ms for kind, _, ms in ct if kind in (2, 4)) /
+               max(1, ktn["cholesky_solve"][1]),
+               "trials": ktn["cholesky_solve"][1],
+               "by_kind": by, "samples": [(int(k), int(n), round(float(ms), 5)) for k, n, ms in ct[:64]]}
+        allr = [None] * cx.world
+        cx.dist.all_gather_object(allr, rec)
+        rec = allr
+    h.reset_kernel_times(False)
+    return kt, rec
+
+
+def collective_fit(per_rank):
+    """alpha and bandwidth of the collectives as measured: least squares ms = alpha + bytes / B over every timed
+    exchange of every rank (X_SCAL's 128 B give alpha, the separator / system blocks the byte term)."""
+    pts = [(n * 8, ms) for r in per_rank or [] for (_, n, ms) in r.get("samples", [])]
+    if len(pts) < 2 or len({b for b, _ in pts}) < 2:
+        return None
+    x = np.array([b for b, _ in pts], float)
+    y = np.array([m for _, m in pts], float)
+    A = np.stack([np.ones_like(x), x], 1)
+    (c0, c1), *_ = np.linalg.lstsq(A, y, rcond=None)
+    small = y[x <= 1024]
+    return {"alpha_us": 1e3 * float(c0), "gbps": (1e-6 / float(c1)) if c1 > 0 else None,
+            "small_message_us_median": 1e3 * float(np.median(small)) if len(small) else None, "samples": len(pts),
+            "note": "each exchange's HIP-event span on its rank's stream (includes waiting for the slowest rank)"}
+
+
+def secondary_leg(cx, cfg, steps, warmup):
+    """A second BASELINE config after the headline, same N (config 4: 5000 KF x 200k rays, the workload BASELINE names
+    for 8 GPUs): a few timed iterations, the kernel breakdown and the per-rank collectives.  A secondary field."""
+    t0 = time.perf_counter()
+    leg = setup_leg(cx, cfg)
+    h = leg["h"]
+    try:
+        run_iters(h, max(warmup, 1))
+        iters, solves, el = timed(cx, h, steps)
+        kt, per_rank = breakdown(cx, h, 2)
+    finally:
+        h.close()
+    prob, info = leg["prob"], leg["info"]
+    out = {"workload": f"{cfg}: {prob.n_pose} KF x {prob.n_landmark} matched rays, {int(len(prob.frame))} pair-form "
+                       f"records, {cx.a.loss} loss, {cx.a.precision} LM",
+           "metric": metric_name(cfg), "value": iters / el, "unit": "BA it/s", "ms_per_step": 1e3 * el / iters,
+           "iterations_timed": iters, "solves_timed": solves, "warmup": max(warmup, 1), "n_gpus": cx.world,
+           "kernel_ms": kt, "records_rank0": info["n_obs"], "reduced_system": leg["sinfo"],
+           "parallelism": leg["dist_mode"] if cx.world > 1 else "single GPU",
+           "generate_s": leg["generate_s"], "set_problem_s": leg["set_problem_s"],
+           "leg_wall_s": time.perf_counter() - t0}
+    if cx.world > 1:
+        out["exchange"] = leg["xinfo"]
+        out["per_rank"] = per_rank
+        out["collective_fit"] = collective_fit(per_rank)
+    return out
 
 
 def main():
@@ -245,9 +457,8 @@ def main():
         if dist:
             dist.barrier()
         if rank == 0:
-            print(json.dumps({"metric": "BA iterations/sec at 500 KF x 20k rays; pan-tilt-focal RMSE vs reference",
-                              "value": None, "unit": "BA it/s", "n_gpus": world, "world_size": world,
-                              "backend": backend, "dry_run": True}))
+            print(json.dumps({"metric": metric_name(a.config), "value": None, "unit": "BA it/s", "n_gpus": world,
+                              "world_size": world, "backend": backend, "dry_run": True}))
         if dist:
             dist.destroy_process_group()
         return
@@ -256,125 +467,43 @@ def main():
     import ptzba
     import synthetic
 
-    prob = synthetic.make_problem(a.config, seed=0)
-    frame, landmark, xy, w = prob.frame, prob.landmark, prob.xy, None
-    if a.form == "dedup":
-        frame, landmark, xy, w, _ = synthetic.dedup_records(frame, landmark, xy)
-    # the coupling window of the WHOLE problem: every rank passes the same one, so all ranks choose the
-    # same system order and take bit-identical pose steps
-    win_hi = ptzba.frame_coupling_window(prob.n_pose, frame, landmark)
-    dist_mode = "single"
-    split = None
-    if world > 1:
-        # part-owned solve: landmarks by the nested-dissection split of the frame chain, each rank
-        # factors its part + the separator; PTZBA_DIST_MODE=replicated: contiguous landmark blocks, every rank
-        # factors the whole summed system (the round-2 protocol, for A/B)
-        replicated = os.environ.get("PTZBA_DIST_MODE", "part") == "replicated"
-        if replicated:
-            sel = shard_by_landmark(landmark, prob.n_landmark, rank, world)
-            dist_mode = "replicated"
-        else:
-            owner, mode, split = ptzba.partition_landmarks(prob.n_pose, prob.n_landmark, frame, landmark, world)
-            sel = owner[landmark] == rank
-            dist_mode = "part-owned" if mode == 1 else "replicated"
-        frame, landmark, xy = frame[sel], landmark[sel], xy[sel]
-        w = None if w is None else w[sel]
-    precision = ptzba.FP32 if a.precision == "fp32" else ptzba.FP64
-    loss = ptzba.LOSS_HUBER if a.loss == "huber" else ptzba.LOSS_LINEAR
-    h = ptzba.BAHandle(local if world > 1 else 0)
-    stream = torch.cuda.current_stream()
-    h.set_stream(stream.cuda_stream)
-    h.set_problem(prob.n_pose, prob.n_landmark, frame, landmark, xy, prob.u, prob.v, weight=w, precision=precision,
-                  loss=loss, f_scale=1.0, frame_win_hi=win_hi,
-                  dist_world=world if (world > 1 and not os.environ.get("PTZBA_DIST_MODE") == "replicated") else 0,
-                  dist_rank=rank)
-    info = h.info()
-    sinfo = h.solver_info()
-
-    allreduce = None
     comm = None
-    xinfo = None
-    if world > 1:
-        # the library runs every exchange itself: through its own RCCL communicator (one per rank, from an RCCL
-        # unique id rank 0 makes and torch.distributed ships), or -- gloo rehearsals of several ranks on one
-        # device -- through a hook over torch.distributed
-        if backend == "gloo":
-            h.set_exchange_hook(ptzba.torch_exchange_hook(h, dist, f"cuda:{local}"))
-        else:
-            uid = [ptzba.Comm.unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(uid, src=0)
-            comm = ptzba.Comm(uid[0], rank, world, device=local)
-            h.attach_comm(comm)
-        xinfo = h.dist_info()
-        xinfo["exchanges"] = h.dist_exchanges()  # (kind, group first rank, group size, doubles) per trial
-        if xinfo["sys_doubles"] == 0 and xinfo["mode"] == "replicated":  # PTZBA_DIST_MODE=replicated (no dist opts)
-            xinfo["sys_doubles"] = h.exchange_packed()[1]
-
-    # x0 is uploaded once and kept on the device: each solve restarts from it without a PCIe transfer
-    h.set_state(prob.init_ptz, prob.init_rays)
-    h.save_state()
-
-    # each solve restarts from the device-resident x0 and runs the C-driven LM (ptzba_solve_resident): the restart
-    # is enqueued by C the moment the final decision is on the host (PTZBA_BENCH_PYLOOP=1: the Python LMSolver loop)
-    pyloop = os.environ.get("PTZBA_BENCH_PYLOOP") == "1"
-
-    def run_iters(hh, k, ar=None):
-        done = 0
-        solves = 0
-        while done < k:
-            if pyloop or ar is not None:
-                hh.restore_state()
-                res = ptzba.LMSolver(hh, ftol=1e-4, xtol=1e-8, max_iter=k - done, allreduce=ar).run()
-            else:
-                res = hh.solve_resident(restore=True, ftol=1e-4, xtol=1e-8, max_iter=k - done)
-            done += max(res.njev, 1)
-            solves += 1
-            if res.njev == 0:
-                break
-        return done, solves
-
-    def timed(hh, steps, ar=None):
-        if dist:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        its, nsolve = run_iters(hh, steps, ar)
-        torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
-        el = time.perf_counter() - t0
-        if dist:
-            tt = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            el = float(tt.item())
-        return its, nsolve, el
+    if world > 1 and backend != "gloo":
+        uid = [ptzba.Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = ptzba.Comm(uid[0], rank, world, device=local)
+    stream = torch.cuda.current_stream()
+    cx = Ctx(a, world, rank, local, dist, backend, stream, comm)
+    leg = setup_leg(cx, a.config)
+    prob, frame, landmark, xy, w, h = leg["prob"], leg["frame"], leg["landmark"], leg["xy"], leg["w"], leg["h"]
+    info, sinfo, xinfo, dist_mode, split = leg["info"], leg["sinfo"], leg["xinfo"], leg["dist_mode"], leg["split"]
+    precision, loss = leg["precision"], leg["loss"]
 
     # warmup
-    run_iters(h, max(a.warmup, 1), allreduce)
+    run_iters(h, max(a.warmup, 1))
     # K1's HIP events stay on during the timed region (roofline), around every 4th K1 launch (each event
     # record adds a gap to the stream; the launches are identical work); the other groups' events are
     # timed in a separate pass afterwards
     h.reset_kernel_times(True, groups=1, stride=4)
-    iters, solves, elapsed = timed(h, a.steps, allreduce)
+    iters, solves, elapsed = timed(cx, h, a.steps)
     k1_ms_region, k1_n_region = h.kernel_times()["linearize"]
     # the roofline's K1 figure: a dedicated pass after the timed region, EVERY K1 launch of K1_PASS_ITERS LM iterations
     # event-bracketed (stride 1), so the figure does not depend on --steps (the in-region sample is kept beside it)
     h.reset_kernel_times(True, groups=1, stride=1)
-    run_iters(h, K1_PASS_ITERS, allreduce)
+    run_iters(h, K1_PASS_ITERS)
     k1_ms, k1_n = h.kernel_times()["linearize"]
-    h.reset_kernel_times(True, groups=0xF)
-    run_iters(h, min(5, a.steps), allreduce)
-    kt = h.kernel_times()
+    kt, per_rank = breakdown(cx, h, min(5, a.steps))
     # cold-cache K1: a 1 GiB scratch buffer streamed through the caches before each timed K1 launch (outside its events)
-    # evicts L2 and the 256 MB Infinity Cache, so the launch streams its records from HBM (SURVEY §8d caveat): read
-    # (clean caches, the line's cold figure) and written (dirty caches whose write-backs run during the launch)
+    # evicts L2 and the 256 MB Infinity Cache, so the launch streams its records from HBM (SURVEY §8d caveat): written
+    # (rounds 2-4's `cold_cache`: dirty caches whose write-backs run during the launch) and read (round 5 on:
+    # `cold_cache_read`, clean caches)
     k1_cold_ms = k1_cold_n = k1_dirty_ms = k1_dirty_n = None
     if not a.no_cold:
         h.reset_kernel_times(True, groups=1, flush="read")
-        run_iters(h, K1_COLD_ITERS, allreduce)
+        run_iters(h, K1_COLD_ITERS)
         k1_cold_ms, k1_cold_n = h.kernel_times()["linearize"]
         h.reset_kernel_times(True, groups=1, flush="write")
-        run_iters(h, K1_COLD_ITERS, allreduce)
+        run_iters(h, K1_COLD_ITERS)
         k1_dirty_ms, k1_dirty_n = h.kernel_times()["linearize"]
     h.reset_kernel_times(False)
 
@@ -434,7 +563,7 @@ def main():
         hs.save_state()
         run_iters(hs, max(a.warmup, 1))
         hs.reset_kernel_times(True, groups=1, stride=4)
-        s_it, s_solves, s_el = timed(hs, a.steps)
+        s_it, s_solves, s_el = timed(cx, hs, a.steps)
         s_k1, _ = hs.kernel_times()["linearize"]
         hs.reset_kernel_times(True, groups=0xF)
         run_iters(hs, min(5, a.steps))
@@ -495,6 +624,16 @@ def main():
                                                           "FETCH_SIZE / WRITE_SIZE, separate passes)")}
         except Exception:
             traffic = None
+    h.close()
+
+    # BASELINE configs[3] (5000 KF x 200k rays) at the same N after the headline: the anchor of the config the
+    # multi-GPU design is for (a secondary field, not the metric)
+    cfg4 = None
+    if a.config == "config3" and a.config4_steps > 0:
+        try:
+            cfg4 = secondary_leg(cx, "config4", a.config4_steps, 1)
+        except Exception as e:  # report, never hide
+            cfg4 = {"error": repr(e)}
 
     if rank == 0:
         # roofline bytes: SURVEY §8d's per-unit formula (234 MB at config 3 fp32 pair form) is `achieved`;
@@ -504,7 +643,7 @@ def main():
         achieved = alg / (k1_ms * 1e-3) / 1e9 if k1_ms > 0 else 0.0
         achieved_layout = alg_layout / (k1_ms * 1e-3) / 1e9 if k1_ms > 0 else 0.0
         out = {
-            "metric": "BA iterations/sec at 500 KF x 20k rays; pan-tilt-focal RMSE vs reference",
+            "metric": metric_name(a.config),
             "value": iters / elapsed,
             "unit": "BA it/s",
             "n_gpus": world,
@@ -534,8 +673,9 @@ def main():
                        "parallelism": (f"{dist_mode} x{world} (landmark shards; "
                                        + ("each rank factors its part of the frame chain + the separator, "
                                           f"split A/C/B at frames {split[0]}/{split[1]}"
-                                          if dist_mode == "part-owned" else "every rank factors the whole system")
-                                       + f"; exchanges by the library over {'RCCL (ptzba_comm)' if comm else backend})")
+                                          if dist_mode == "part-owned" else "every rank factors the whole summed system")
+                                       + f"; exchanges by the library over {'RCCL (ptzba_comm)' if comm else backend}"
+                                       + "; form chosen by ptzba.choose_dist_form)")
                                       if world > 1 else "single GPU",
                        "reduced_system": sinfo,
                        "exchange": xinfo,
@@ -555,26 +695,34 @@ def main():
                          "bytes_basis": "SURVEY §8d: N_rec*S_rec + (3 N_kf + 2 N_lm) s + N_lm 5 s + N_kf 9 s",
                          "layout_bytes_per_launch": alg_layout, "achieved_layout_bytes": achieved_layout,
                          "frac_layout_bytes": achieved_layout / HBM_PEAK_GBS},
-            "kernel_ms": {k: v[0] for k, v in kt.items()},
+            "kernel_ms": kt,
         }
+        if world > 1:
+            out["per_rank"] = per_rank
+            out["collective_fit"] = collective_fit(per_rank)
         if k1_cold_ms:
-            ach_c = alg / (k1_cold_ms * 1e-3) / 1e9
-            out["roofline"]["cold_cache"] = {"k1_avg_ms": k1_cold_ms, "launches": k1_cold_n, "achieved": ach_c,
-                                             "frac": ach_c / HBM_PEAK_GBS,
-                                             "frac_layout_bytes": alg_layout / (k1_cold_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                                             "method": "1 GiB scratch READ before each timed K1 launch (L2 and the "
-                                                       "256 MB Infinity Cache hold clean unrelated lines)"}
+            # key semantics as in rounds 2-4: `cold_cache` is the WRITE flush, the read flush (round 5 on,
+            # clean caches) is `cold_cache_read`
             ach_d = alg / (k1_dirty_ms * 1e-3) / 1e9
-            out["roofline"]["cold_cache_dirty"] = {
+            out["roofline"]["cold_cache"] = {
                 "k1_avg_ms": k1_dirty_ms, "launches": k1_dirty_n, "achieved": ach_d, "frac": ach_d / HBM_PEAK_GBS,
                 "method": "1 GiB scratch WRITE before each timed K1 launch (rounds 2-4's method: the caches are left "
                           "dirty, so ~256 MB of unrelated write-backs run during the timed launch)"}
+            ach_c = alg / (k1_cold_ms * 1e-3) / 1e9
+            out["roofline"]["cold_cache_read"] = {
+                "k1_avg_ms": k1_cold_ms, "launches": k1_cold_n, "achieved": ach_c, "frac": ach_c / HBM_PEAK_GBS,
+                "frac_layout_bytes": alg_layout / (k1_cold_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "method": "1 GiB scratch READ before each timed K1 launch (L2 and the 256 MB Infinity Cache hold clean "
+                          "unrelated lines)"}
+            out["roofline"]["cold_cache_schema"] = 2
         if accuracy:
             out["accuracy"] = accuracy
         if secondary:
             out["fp64_linear"] = secondary
         if dropin:
             out["dropin_call"] = dropin
+        if cfg4 is not None:
+            out["config4"] = cfg4
         if not a.no_cpu_baseline and world == 1:
             # the full-size timing is the baseline (the scipy restatement on the 14.6M-record
             # problem itself); the keyframe-window power-law fit is kept beside it as a secondary field
@@ -597,7 +745,6 @@ def main():
         if a.stream_frames > 0 and world == 1:
             out["config5"] = stream_leg(a.stream_frames)
         print(json.dumps(out))
-    h.close()
     if comm is not None:
         comm.close()
     if dist:

@@ -119,6 +119,14 @@ PTZBA_EXPORT int ptzba_dist_rank_phases(int32_t n_pose, int32_t n_fixed, const i
 PTZBA_EXPORT int ptzba_partition_landmarks(int32_t n_pose, int32_t n_landmark, int64_t n_obs, const int32_t* obs_frame,
                                            const int32_t* obs_landmark, int32_t n_fixed, int32_t world,
                                            int32_t* rank_of_landmark, int32_t* mode_out, int32_t* split_out);
+/* Host only (round 6): the planner's predicted cost per LM trial of the two forms of a `world`-rank solve -- the rank tree
+ * (ptzba_partition_landmarks' part-owned split) and the replicated solve (contiguous landmark blocks, one all-reduce of the
+ * packed system) -- as the slowest rank's factorisation estimate plus its collectives, each a ring all-reduce
+ * alpha_us + 2 (p - 1) / p * bytes / (link_gbs GB/s).  out8: [0] tree us (0: no tree), [1] replicated us, [2] / [3] their
+ * factorisation us, [4] / [5] the tree rank's collectives and doubles per trial, [6] replicated doubles, [7] the form
+ * with the smaller estimate (1 tree, 0 replicated).  ptzba.choose_dist_form and bench.py --gpus N use it. */
+PTZBA_EXPORT int ptzba_dist_form_estimate(int32_t n_pose, int32_t n_fixed, const int32_t* frame_win_hi, int32_t world,
+                                          double alpha_us, double link_gbs, double* out8);
 
 /* per-iteration scalars read back after ptzba_step (all fp64):
  * [0] cost at the current state, [1] cost at the trial state, [2] predicted reduction,
@@ -201,7 +209,9 @@ typedef struct {
   /* huber loss only: the records' curvature weight beyond the unit is rho' (IRLS, a majoriser of the loss) until an
    * accepted step was predicted to reduce the cost by less than curvature_switch of it; from then on huber_curvature * rho' (the
    * loss's own Newton curvature is 0 there, scipy's robust scaling; floored), the current point re-linearised at
-   * once.  curvature_switch = 0 or huber_curvature = 1: IRLS throughout.  Defaults 0.1 / 0.25. */
+   * once.  curvature_switch = 0 or huber_curvature = 1: IRLS throughout.  Defaults 0.1 / 0.25.  ABI (ptzba_version
+   * 0.2): these two fields were added after the 9-field struct of 0.1; they are read for the Huber loss only and
+   * huber_curvature = 0 selects the default 0.1, so a caller that zero-fills them keeps IRLS throughout. */
   double huber_curvature, curvature_switch;
 } ptzba_lm_opts;
 /* termination status (scipy least_squares numbering where it has one): DAMPING = the trial was rejected at
@@ -317,10 +327,17 @@ PTZBA_EXPORT int ptzba_sync(ptzba_handle h);
  * caches are left full of dirty lines, whose write-backs then run during the timed launch.
  * PTZBA_TIME_FLUSH_READ (bit 17, with bit 16): the scratch buffer is READ instead -- the caches hold
  * clean unrelated lines, so the timed launch pays its own HBM traffic only. */
+#define PTZBA_TIME_COMM 0x10  /* enable bit 4: an event pair around every exchange (ptzba_comm_times) */
 #define PTZBA_TIME_FLUSH 0x10000
 #define PTZBA_TIME_FLUSH_READ 0x20000
 PTZBA_EXPORT int ptzba_kernel_times(ptzba_handle h, double* ms_out /*4*/, int64_t* count_out /*4*/);
 PTZBA_EXPORT int ptzba_reset_kernel_times(ptzba_handle h, int enable);
+/* The exchanges timed since the last ptzba_reset_kernel_times with PTZBA_TIME_COMM (bit 4): per exchange its kind
+ * (PTZBA_X_*), its size in doubles and the elapsed ms between the events recorded on the handle's stream around it
+ * (the collective's kernel, or a hook's stream work); the first min(cap, *n_out) records (up to 2048 per reset).
+ * New in round 6 (a multi-rank run reports what its collectives cost). */
+PTZBA_EXPORT int ptzba_comm_times(ptzba_handle h, int32_t cap, int32_t* kinds, int64_t* doubles, double* ms,
+                                  int32_t* n_out);
 
 /* ---------------- camera model (batched, device-resident computation) ---------------- */
 PTZBA_EXPORT int ptz_ray_to_image(int device, int64_t n, double u, double v, const double* f,

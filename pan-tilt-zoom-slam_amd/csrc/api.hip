@@ -34,6 +34,7 @@ static size_t g_total_bytes(std::initializer_list<const DBuf*> l) {
 enum { TM_K1 = 0, TM_SCHUR = 1, TM_CHOL = 2, TM_BACK = 3, TM_N = 4 };
 constexpr int LM_RING = 4;
 constexpr int TM_POOL = 512;
+constexpr int COMM_POOL = 2048;  // timed exchanges per reset_kernel_times
 
 struct ptzba_ctx {
   int device = 0;
@@ -137,6 +138,10 @@ struct ptzba_ctx {
   bool tm_flush = false;  // cold-cache timing: stream a scratch buffer through the caches before each timed K1
   bool tm_flush_read = false;  // ... by reading it (clean lines) instead of writing it
   DBuf flush_buf;
+  // collective timing (enable bit PTZBA_TIME_COMM): an event pair around every exchange, its kind and size
+  std::vector<hipEvent_t> cev;
+  int cev_used = 0;
+  std::vector<std::pair<int, int64_t>> clog;
 
   // multi-GPU (include/ptzba.h): exchanges done by the library, part-owned solve state
   ptzba_comm comm = nullptr;        // attached, not owned
@@ -247,7 +252,9 @@ static hipEvent_t tm_k1_event(ptzba_ctx* h, int which) {
 }
 
 const char* ptzba_last_error(void) { return g_err.c_str(); }
-const char* ptzba_version(void) { return "ptzba 0.1 gfx950"; }
+// 0.2 (round 6): ptzba_lm_opts carries huber_curvature / curvature_switch (11 fields; 0.1 had 9).  They are read
+// for the Huber loss only, and huber_curvature 0 means the default 0.1, so a zero-filled tail keeps 0.1's behaviour.
+const char* ptzba_version(void) { return "ptzba 0.2 gfx950 (ptzba_lm_opts: 11 fields)"; }
 
 ptzba_handle ptzba_new(int device) {
   if (select_device(device)) return nullptr;
@@ -268,6 +275,7 @@ void ptzba_delete(ptzba_handle h) {
   if (h->st) (void)hipStreamSynchronize(h->st);
   for (int k = 0; k < TM_N; ++k)
     for (auto e : h->ev[k]) (void)hipEventDestroy(e);
+  for (auto e : h->cev) (void)hipEventDestroy(e);
   if (h->own) (void)hipStreamDestroy(h->own);
   if (h->scal_host) (void)hipHostFree(h->scal_host);
   if (h->out_pin) (void)hipHostFree(h->out_pin);
@@ -2273,7 +2281,22 @@ static int exchange_depth(const ptzba_ctx* h, int kind) {
     if (h->ph[q].kind == kind) return h->ph[q].depth;
   return -1;
 }
+static int exchange_run(ptzba_ctx* h, int kind, double* buf, int64_t n);
+// every exchange goes through here: with collective timing on (PTZBA_TIME_COMM) an event pair brackets it on the
+// handle's stream (RCCL's kernel, or a hook's stream work), so a multi-rank run reports its collectives' time and
+// bytes per kind (ptzba_comm_times) -- alpha and bandwidth measured instead of assumed
 static int exchange(ptzba_ctx* h, int kind, double* buf, int64_t n) {
+  const bool tm = (h->timing & PTZBA_TIME_COMM) && h->cev_used + 2 <= (int)h->cev.size();
+  if (tm) (void)hipEventRecord(h->cev[h->cev_used], h->st);
+  const int rc = exchange_run(h, kind, buf, n);
+  if (tm) {
+    (void)hipEventRecord(h->cev[h->cev_used + 1], h->st);
+    h->cev_used += 2;
+    h->clog.emplace_back(kind, n);
+  }
+  return rc;
+}
+static int exchange_run(ptzba_ctx* h, int kind, double* buf, int64_t n) {
   if (h->hook) {
     if (h->hook(h->hook_ctx, kind, buf, n, (void*)h->st)) return fail("exchange hook failed (kind %d)", kind);
     return 0;
@@ -2542,11 +2565,14 @@ int ptzba_lm_init(ptzba_handle h, const ptzba_lm_opts* o) {
   if (!(o->lambda0 >= 0) || !(o->min_lambda > 0) || !(o->max_lambda > 0) || o->max_iter < 0 || o->max_retries < 1)
     return fail("bad LM options");
   HIPCHK(hipSetDevice(h->device));
-  if (!(o->huber_curvature > 0.0 && o->huber_curvature <= 1.0) || !(o->curvature_switch >= 0.0))
+  // the two curvature fields (added in version 5 of the options struct) matter for the Huber loss only; a caller that
+  // zero-fills them gets the default curvature (0.1) and no switch (curvature_switch 0)
+  const double hcv = o->huber_curvature == 0.0 ? 0.1 : o->huber_curvature;
+  if (h->loss == PTZBA_LOSS_HUBER && (!(hcv > 0.0 && hcv <= 1.0) || !(o->curvature_switch >= 0.0)))
     return fail("bad LM options (huber_curvature in (0, 1], curvature_switch >= 0)");
-  const bool sw = h->loss == PTZBA_LOSS_HUBER && o->curvature_switch > 0.0 && o->huber_curvature < 1.0;
+  const bool sw = h->loss == PTZBA_LOSS_HUBER && o->curvature_switch > 0.0 && hcv < 1.0;
   LMParams p{o->ftol, o->xtol, o->gtol, o->lambda0, o->min_lambda, o->max_lambda,
-             sw ? o->huber_curvature : 1.0, sw ? o->curvature_switch : 0.0, o->max_iter, o->max_retries,
+             sw ? hcv : 1.0, sw ? o->curvature_switch : 0.0, o->max_iter, o->max_retries,
              o->gauss_newton ? 1 : 0, 0};
   // the switch's launches (relin_mode 1: the conditional re-linearisation in lm_build; 0: the predicted-reduction
   // reduce in front of the trial K1) are queued until the host sees the switch in a decision record
@@ -2901,7 +2927,13 @@ int ptzba_reset_kernel_times(ptzba_handle h, int enable) {
     h->tm_seen[k] = 0;
     h->tm_sampled[k] = false;
   }
-  h->timing = enable & ((1 << TM_N) - 1);
+  h->timing = enable & (((1 << TM_N) - 1) | PTZBA_TIME_COMM);
+  if ((enable & PTZBA_TIME_COMM) && h->cev.empty()) {
+    h->cev.resize(2 * COMM_POOL);
+    for (auto& e : h->cev) HIPCHK(hipEventCreate(&e));
+  }
+  h->cev_used = 0;
+  h->clog.clear();
   h->tm_stride = std::max(1, (enable >> 8) & 0xff);
   h->tm_flush = (enable & PTZBA_TIME_FLUSH) != 0;
   h->tm_flush_read = h->tm_flush && (enable & PTZBA_TIME_FLUSH_READ) != 0;
@@ -2929,6 +2961,22 @@ int ptzba_kernel_times(ptzba_handle h, double* ms_out, int64_t* count_out) {
     ms_out[k] = n ? tot / n : 0.0;
     count_out[k] = n;
   }
+  return 0;
+}
+
+int ptzba_comm_times(ptzba_handle h, int32_t cap, int32_t* kinds, int64_t* doubles, double* ms, int32_t* n_out) {
+  if (!h || !n_out || cap < 0 || (cap > 0 && (!kinds || !doubles || !ms))) return fail("ptzba_comm_times: bad arguments");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->st));
+  const int32_t n = (int32_t)h->clog.size();
+  for (int32_t i = 0; i < std::min(n, cap); ++i) {
+    float t = 0;
+    HIPCHK(hipEventElapsedTime(&t, h->cev[2 * i], h->cev[2 * i + 1]));
+    kinds[i] = h->clog[i].first;
+    doubles[i] = h->clog[i].second;
+    ms[i] = t;
+  }
+  *n_out = n;
   return 0;
 }
 
@@ -3104,6 +3152,69 @@ int ptzba_plan_export(int32_t n_pose, int32_t n_fixed, const int32_t* frame_win_
   if (pos_out) std::copy(so.pos.begin(), so.pos.end(), pos_out);
   if (tasks_out) std::copy(plan.tasks.begin(), plan.tasks.end(), tasks_out);
   if (level_off_out) std::copy(plan.level_off.begin(), plan.level_off.end(), level_off_out);
+  return 0;
+}
+
+// host only (round 6): which form of an N-rank solve the planner predicts faster -- the rank tree (each rank factors
+// its subtree + its ancestors' separators, separator blocks summed per group) or the replicated solve (one all-reduce
+// of the packed system, every rank factors all of it).  Both shard the landmarks over all ranks, so K1 / K2 / trial
+// cancel out; compared are the slowest rank's factorisation estimate (plan_est_us, the planner's own figure) plus its
+// collectives per trial as ring all-reduces, alpha + 2 (p - 1) / p * bytes / B.  At config 3 the tree
+// does not shorten the chain (separators ~110 frames), so its extra exchanges lose from 4 ranks on; at config 4 the
+// tree's factorisation is 1.5-2x shorter.  out8: [0] tree estimate us (0: no tree), [1] replicated us, [2] the tree's
+// slowest-rank factorisation us, [3] the full plan's factorisation us, [4] tree collectives per trial on that rank,
+// [5] tree doubles on that rank, [6] replicated doubles (packed system), [7] chosen form (1 tree, 0 replicated).
+int ptzba_dist_form_estimate(int32_t n_pose, int32_t n_fixed, const int32_t* frame_win_hi, int32_t world,
+                             double alpha_us, double link_gbs, double* out8) {
+  if (n_pose < 1 || n_fixed < 0 || n_fixed > n_pose || !frame_win_hi || !out8 || world < 1 || !(alpha_us >= 0) ||
+      !(link_gbs > 0))
+    return fail("bad arguments");
+  std::vector<int32_t> win(frame_win_hi, frame_win_hi + n_pose);
+  for (int f = 0; f < n_pose; ++f)
+    if (win[f] < f || win[f] >= n_pose) return fail("frame_win_hi[%d] = %d out of range", f, win[f]);
+  std::fill(out8, out8 + 8, 0.0);
+  auto ring_us = [&](double doubles, int p) {
+    return p < 2 ? 0.0 : alpha_us + 2.0 * (p - 1) / p * 8.0 * doubles / (link_gbs * 1e3);
+  };
+  SysOrder so;
+  CholPlan plan;
+  if (choose_order_plan(n_pose, n_fixed, win, PTZBA_ORDER_NESTED, so, plan)) return fail("no factorisation plan");
+  const double sys_doubles = (double)(plan.xtiles.size() / 2) * CHOL_NB * CHOL_NB + 3.0 * (double)pad_tile(so.n_aug + 1);
+  const double full_us = plan_est_us(plan);
+  const double scal = 2.0 * PTZBA_NSCALARS;
+  out8[1] = full_us + ring_us(sys_doubles, world) + ring_us(scal, world);
+  out8[3] = full_us;
+  out8[6] = sys_doubles;
+  SysOrder o;
+  DistTree DT;
+  if (world >= 2 && dist_order(n_pose, n_fixed, win, world, o) && dist_tree(o, world, DT)) {
+    const int64_t ld = pad_tile(o.n_aug + 1);
+    double worst = 0;
+    for (int r = 0; r < world; ++r) {
+      CholPlan P;
+      TreePlan Q;
+      if (!make_plan_tree(o, DT, r, n_pose, n_fixed, win, ld, P, Q)) return fail("no rank-tree plan for rank %d", r);
+      double comm = ring_us(scal, world), nd = 0;
+      int nx = 1;
+      for (size_t q = 0; q < Q.ph.size(); ++q) {
+        const auto& t = Q.ph[q];
+        if (q == 0 && t.nr < 2) continue;
+        const double n = (double)(t.xt.size() / 2) * CHOL_NB * CHOL_NB + t.vr.count[0] + t.vr.count[1] + t.vr.count[2];
+        comm += ring_us(n, t.nr);
+        nd += n;
+        ++nx;
+      }
+      const double est = plan_est_us(P);
+      if (est + comm > worst) {
+        worst = est + comm;
+        out8[2] = est;
+        out8[4] = nx;
+        out8[5] = nd;
+      }
+    }
+    out8[0] = worst;
+  }
+  out8[7] = (out8[0] > 0 && out8[0] <= out8[1]) ? 1.0 : 0.0;
   return 0;
 }
 

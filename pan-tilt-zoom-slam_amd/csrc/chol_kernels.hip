@@ -207,12 +207,28 @@ __device__ __forceinline__ double rsq_nr(double d) {
 __device__ long long g_cs_stamps[64][6];
 __device__ long long g_cs_wg[64][10];
 __device__ int g_cs_level;
+// sweep accounting (round 6): per level, block 0's wave 0 stamps eight points of every 4-pivot block, the helpers the
+// time they publish each block (tools/chol_timing.py --sweep)
+__device__ long long g_cs_blk[64][8][8];
+__device__ long long g_cs_hlp[64][8][3];
+// the level timeline in s_memrealtime (100 MHz, one clock for every XCD): block 0's task start, sweep end, factor
+// stores complete; and the last workgroup of the level to finish its task (atomicMax)
+__device__ long long g_cs_rt[64][4];
+#define CSB(s_, k_) do { if (wrec0 && (s_) < 8) { __builtin_amdgcn_s_waitcnt(0xc07f); cs_blk[s_][k_] = clock64(); } } while (0)
+#else
+#define CSB(s_, k_) do { } while (0)
 #endif
 #ifndef BS_LOADERS
 #define BS_LOADERS 1  // loader waves of the lookahead back-solve (2: ring positions alternate; measured neutral)
 #endif
 #ifndef LA_BW
 #define LA_BW 4  // pivot block of the lookahead form
+#endif
+#ifndef CHOL_SPEC
+#define CHOL_SPEC 0  // pivot sweep: 1 speculative row reads + deferred publication (round 6 A/B: slower, r06c), 0 round 5's
+#endif
+#ifndef CHOL_FFH
+#define CHOL_FFH 0  // SPD pivot sweep: 1 fraction-free 4 x 4 blocks with the lane's row folded in (round 6 A/B)
 #endif
 // reciprocal square root by a series step on the hardware estimate: e = 1 - d y0^2 (|e| ~ 5e-8),
 // y = y0 (1 + e/2 + 3e^2/8) -- full double precision in 4 dependent operations (rsq_nr: 6)
@@ -263,11 +279,22 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
   int* nl = flags;
   int* nu = flags + 1;  // [NS]
   if (threadIdx.x <= NS) flags[threadIdx.x] = 0;
+#if CHOL_FFH
+  __shared__ double s_g[NB];  // FFH: power-of-two column scales of the tile's entry diagonal
+  if (!SG && threadIdx.x < NB) {
+    const double d = D[threadIdx.x][threadIdx.x];
+    s_g[threadIdx.x] = d > 0.0 ? ldexp(1.0, -(ilogb(d) >> 1)) : 1.0;
+  }
+#endif
   __syncthreads();
 #ifdef CS_TIMING
   long long* wst = g_cs_wg[g_cs_level < 64 ? g_cs_level : 63];
   const bool wrec = threadIdx.x == 0 && blockIdx.x == 0;
   if (wrec) wst[0] = clock64();
+  const int cs_l = g_cs_level < 64 ? g_cs_level : 63;
+  const bool wrec0 = lane == 0 && w == 0 && blockIdx.x == 0;
+  long long (*cs_blk)[8] = g_cs_blk[cs_l];
+  if (wrec0) { cs_blk[0][1] = __builtin_amdgcn_s_memrealtime(); cs_blk[2][1] = clock64(); }
 #endif
   if (w == 0) {
     bool bad = false;
@@ -277,6 +304,7 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const int kb = s * BW;
+      CSB(s, 0);
       // the previous block's factor rows kb..kb+BW-1 (this wave's own stores) are read before the wait for the
       // helpers: their LDS round trip overlaps the poll's instead of following it
       double pl[BW][BW];
@@ -286,12 +314,38 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
 #pragma unroll
           for (int k = 0; k < BW; ++k) pl[j][k] = Lb[s - 1][kb + j][k];
       }
+      double a[BW];
+#if CHOL_SPEC
+      // the row reads go out right behind the helper counter's and are re-issued only if it was short (the helpers
+      // run ~1,000-1,500 ticks ahead, profiles/r06a_sweep.json): one LDS round trip instead of two.  A wave's LDS
+      // operations execute in order, so reads issued after the counter's see every helper store it counted.
+      {
+        int v = 3;
+        do {
+          if (s >= 2) v = __hip_atomic_load(&nu[s - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int j = 0; j < BW; ++j) a[j] = row[kb + j];
+          asm volatile("" ::: "memory");
+        } while (__builtin_expect(v < 3, 0));
+      }
+      CSB(s, 2);
+      if (s >= 1 && s + 1 < NS) {
+        // block s - 1's publication (helpers wait for nl >= t before stage t), deferred to here: the reads above were
+        // issued after that block's factor stores (and, SG, its signs) and have returned, so those stores are
+        // complete -- ordered by completion without a wait of its own
+        asm volatile("" ::"v"(a[0]) : "memory");
+        if (lane == 0) __hip_atomic_store(nl, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+#else
       if (s >= 2) {
         while (lds_poll(&nu[s - 1]) < 3) __builtin_amdgcn_s_sleep(0);
       }
-      double a[BW];
+      CSB(s, 2);
 #pragma unroll
       for (int j = 0; j < BW; ++j) a[j] = row[kb + j];
+#endif
+      CSB(s, 3);
       if (s > 0) {
 #pragma unroll
         for (int j = 0; j < BW; ++j) {
@@ -308,6 +362,56 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
       for (int i = 0; i < BW; ++i)
 #pragma unroll
         for (int j = 0; j <= i; ++j) P[i][j] = bcast(a[j], kb + i);
+#ifdef CS_TIMING
+      if (wrec0 && s < 8) {  // consume P so the stamp follows the gathers
+        double t = 0.0;
+#pragma unroll
+        for (int i = 0; i < BW; ++i) t += P[i][i];
+        if (t == 12345.678) cs_blk[s][7] = 1;
+      }
+#endif
+      CSB(s, 4);
+#if CHOL_FFH
+      if constexpr (!SG) {
+        // fraction-free 4 x 4 block (Gauss without divisions: q_im <- Q_j q_im - q_ij q_mj, Q_j = q_jj), the lane's
+        // row riding along as a fifth row, so a pivot costs one multiply + one FMA on the chain and the four
+        // reciprocal square roots come last, independent: L_rj = t_rj / sqrt(Q_0 ... Q_j).  Columns pre-scaled by
+        // exact powers of two g_j of the tile's entry diagonal (g_j^2 A_jj in [1, 4)) bound the products' growth.
+        double g[BW], t[BW], Q[BW];
+#pragma unroll
+        for (int j = 0; j < BW; ++j) g[j] = s_g[kb + j];
+#pragma unroll
+        for (int j = 0; j < BW; ++j) t[j] = a[j] * g[j];
+#pragma unroll
+        for (int i = 0; i < BW; ++i)
+#pragma unroll
+          for (int j = 0; j <= i; ++j) P[i][j] *= g[i] * g[j];
+#pragma unroll
+        for (int j = 0; j < BW; ++j) {
+          double q = P[j][j];
+          if (!(q > 0.0)) {
+            bad = true;
+            q = 1.0;
+          }
+          Q[j] = q;
+#pragma unroll
+          for (int i = j + 1; i < BW; ++i)
+#pragma unroll
+            for (int m = j + 1; m <= i; ++m) P[i][m] = fma(-P[i][j], P[m][j], q * P[i][m]);
+#pragma unroll
+          for (int m = j + 1; m < BW; ++m) t[m] = fma(-t[j], P[m][j], q * t[m]);
+        }
+        double pr = Q[0];
+#pragma unroll
+        for (int j = 0; j < BW; ++j) {
+          if (j > 0) pr *= Q[j];
+          lp[j] = t[j] * rsq_fast(pr);  // L_rj
+        }
+#pragma unroll
+        for (int j = 0; j < BW; ++j) sg[j] = 1.0;
+      } else
+#endif
+      {
 #pragma unroll
       for (int j = 0; j < BW; ++j) {
         double d = P[j][j];
@@ -333,6 +437,10 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
             else P[i][m] = fma(-P[i][j], P[m][j], P[i][m]);
           }
       }
+#ifdef CS_TIMING
+      if (wrec0 && s < 8 && y[BW - 1] == 12345.678) cs_blk[s][7] = 1;
+#endif
+      CSB(s, 5);
 #pragma unroll
       for (int j = 0; j < BW; ++j) {
         const double x = a[j] * y[j];  // sigma_j L_rj
@@ -343,6 +451,11 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
           else a[i] = fma(-P[i][j], x, a[i]);
         }
       }
+      }
+#ifdef CS_TIMING
+      if (wrec0 && s < 8 && lp[BW - 1] == 12345.678) cs_blk[s][7] = 1;
+#endif
+      CSB(s, 6);
 #pragma unroll
       for (int j = 0; j < BW; ++j) Lb[s][lane][j] = SG ? sg[j] * lp[j] : lp[j];  // L_rj
       if constexpr (SG) {
@@ -351,16 +464,20 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
           for (int j = 0; j < BW; ++j) sig[kb + j] = sg[j];
         }
       }
-      if (s + 2 < NS) {
+      if (!CHOL_SPEC && s + 2 < NS) {
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) __hip_atomic_store(nl, s + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+      CSB(s, 7);
 #ifdef CS_TIMING
       if (wrec && s < 9) wst[1 + s] = clock64();
 #endif
     }
     if (bad && lane == 0) atomicOr(info, 1);
+#ifdef CS_TIMING
+    if (wrec0) { cs_blk[1][1] = __builtin_amdgcn_s_memrealtime(); cs_blk[3][1] = clock64(); }
+#endif
   } else {
     // helpers, left-looking: during wave 0's stage t they bring block t+1 up to date with the factor
     // blocks 0..t-1 (wave 0 adds block t itself), so each block is written once and wave 0 never waits
@@ -389,6 +506,9 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
       if (lane == 0) __hip_atomic_fetch_add(&nu[t], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef CS_TIMING
+      if (lane == 0 && blockIdx.x == 0 && t < 8) g_cs_hlp[cs_l][t][u] = clock64();
+#endif
     }
   }
   __syncthreads();
@@ -396,8 +516,12 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
 
 #ifdef CS_TIMING
 #define CS_STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x == 0 && cs_lvl < 64) g_cs_stamps[cs_lvl][k] = clock64(); } while (0)
+#define CS_RT(k) do { if (threadIdx.x == 0 && blockIdx.x == 0 && cs_lvl < 64) g_cs_rt[cs_lvl][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define CS_RT_END() do { if (threadIdx.x == 0 && cs_lvl < 64) { __builtin_amdgcn_s_waitcnt(0); atomicMax((unsigned long long*)&g_cs_rt[cs_lvl][3], (unsigned long long)__builtin_amdgcn_s_memrealtime()); } } while (0)
 #else
 #define CS_STAMP(k) do { } while (0)
+#define CS_RT(k) do { } while (0)
+#define CS_RT_END() do { } while (0)
 #endif
 // SG: signed factor A = L Sigma L^T (indefinite systems: the EKF innovation block, ekf.hip); sgn[ld] holds
 // sigma per factored row, written by each column's diagonal task and applied to the update panels
@@ -692,6 +816,7 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
   if (threadIdx.x == 0 && blockIdx.x == 0 && cs_lvl < 64) g_cs_stamps[cs_lvl][5] = type;
 #endif
   CS_STAMP(0);
+  CS_RT(0);
   if constexpr (P2 && !SG) {
     if (type == 3) {  // 2 x 2 block of trailing tiles (api.hip make_plan): A_ij -= sum_p L_ip L_jp^T
       chol_trail_block<COH>(A, ld, i, j, ((tk.w >> 28) & 3) | (((unsigned)tk.x >> 30) << 2), up0, up1, up2, up3, sA, sB);
@@ -856,6 +981,7 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
   wg_potrf_trsm32_df<LA_BW, SG>(sD, diag_only ? nullptr : sC, s_lb, s_pb, s_flags, info, s_sig);
   __syncthreads();  // (the flag-synchronised sweep ends in a barrier of its own)
   CS_STAMP(3);
+  CS_RT(1);
 #ifdef CS_TIMING
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     CS_STAMP(4);
@@ -869,10 +995,24 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
     if constexpr (SG) {
       if (threadIdx.x < NB) sgn[(int64_t)k * NB + threadIdx.x] = s_sig[threadIdx.x];
     }
+#ifdef CS_TIMING
+    if (threadIdx.x == 0 && blockIdx.x == 0 && cs_lvl < 64) {
+      __builtin_amdgcn_s_waitcnt(0);
+      g_cs_rt[cs_lvl][2] = __builtin_amdgcn_s_memrealtime();
+    }
+    CS_RT_END();
+#endif
     return;
   }
   // (A_kk itself stays untouched: other panel workgroups of this launch are still reading it)
   store_tile<COH>(A + i * NBl * ld + k * NBl, ld, [&](int r, int m) { return s_lb[m / LA_BW][NB + r][m % LA_BW]; });
+#ifdef CS_TIMING
+  if (threadIdx.x == 0 && blockIdx.x == 0 && cs_lvl < 64) {
+    __builtin_amdgcn_s_waitcnt(0);
+    g_cs_rt[cs_lvl][2] = __builtin_amdgcn_s_memrealtime();
+  }
+  CS_RT_END();
+#endif
 }
 
 template <bool SG, typename TaskArg, bool P2 = false, bool COH = false, bool SUP = false>
@@ -1581,6 +1721,11 @@ extern "C" int ptzba_debug_cs_stamps(long long* out) {
   const int zero = 0;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cs_stamps), sizeof(g_cs_stamps)) != hipSuccess) return -1;
   if (hipMemcpyFromSymbol(out + 64 * 6, HIP_SYMBOL(g_cs_wg), sizeof(g_cs_wg)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out + 64 * 16, HIP_SYMBOL(g_cs_blk), sizeof(g_cs_blk)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out + 64 * 16 + 64 * 64, HIP_SYMBOL(g_cs_hlp), sizeof(g_cs_hlp)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out + 64 * 16 + 64 * 64 + 64 * 24, HIP_SYMBOL(g_cs_rt), sizeof(g_cs_rt)) != hipSuccess) return -1;
+  static long long zero_rt[64][4];
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_cs_rt), zero_rt, sizeof(zero_rt)) != hipSuccess) return -1;
   return hipMemcpyToSymbol(HIP_SYMBOL(g_cs_level), &zero, sizeof(int)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -69,6 +69,7 @@ class ptzba_report(Structure):
                 ("nfev", c_int32), ("trials", c_int32), ("status", c_int32)]
 
 
+TIME_COMM = 0x10  # include/ptzba.h PTZBA_TIME_COMM: an event pair around every exchange (comm_times)
 TIME_FLUSH = 0x10000  # include/ptzba.h PTZBA_TIME_FLUSH: cold-cache K1 timing
 TIME_FLUSH_READ = 0x20000  # include/ptzba.h PTZBA_TIME_FLUSH_READ: ... by a read flush (clean caches)
 
@@ -135,6 +136,8 @@ def lib():
         "ptzba_sync": ([V], I),
         "ptzba_kernel_times": ([V, V, V], I),
         "ptzba_reset_kernel_times": ([V, I], I),
+        "ptzba_comm_times": ([V, I32, V, V, V, V], I),
+        "ptzba_dist_form_estimate": ([I32, I32, V, I32, D, D, V], I),
         "ptzba_save_state": ([V], I),
         "ptzba_restore_state": ([V], I),
         "ptz_ray_to_image": ([I, I64, D, D, V, V, V, V, V, V, V], I),
@@ -207,7 +210,7 @@ EXPORTED_SYMBOLS = [
     "ptzba_problem_info", "ptzba_solver_info", "ptzba_residual", "ptzba_set_state", "ptzba_get_state", "ptzba_linearize",
     "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_set_huber_curvature", "ptzba_setup_timing", "ptzba_solve", "ptzba_solve_resident", "ptzba_read_scalars", "ptzba_accept",
     "ptzba_lm_start", "ptzba_lm_init", "ptzba_lm_build", "ptzba_lm_solve", "ptzba_lm_decide", "ptzba_lm_wait",
-    "ptzba_exchange", "ptzba_exchange_packed", "ptzba_pack", "ptzba_unpack", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptzba_save_state", "ptzba_restore_state", "ptz_ray_to_image",
+    "ptzba_exchange", "ptzba_exchange_packed", "ptzba_pack", "ptzba_unpack", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptzba_comm_times", "ptzba_dist_form_estimate", "ptzba_save_state", "ptzba_restore_state", "ptz_ray_to_image",
     "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks", "ptzba_coupling_window", "ptz_match_knn2", "ptz_homography_ransac", "ptz_homography_ransac_batch", "ptz_lk_track", "ptz_sift", "ptz_match_hamming",
     "ptz_py_shuffle_prefix", "ptz_set_order_pairs", "ptz_keyframe_features", "ptz_pack_records",
     "ptz_refine_poses", "ptzekf_new", "ptzekf_delete", "ptzekf_num_rays", "ptzekf_set_state", "ptzekf_get_state", "ptzekf_add_pose_cov",
@@ -749,6 +752,47 @@ def dist_rank_phases(frame_win_hi, world, rank, n_fixed=1):
     return [tuple(int(x) for x in row) for row in out[:n.value]]
 
 
+# the collective model of choose_dist_form: a ring all-reduce costs ALPHA_US + 2 (p - 1) / p * bytes / LINK_GBS.  alpha is
+# RCCL's small-message latency on an 8-GPU node, assumed (no multi-GPU node has run this build; bench.py --gpus N now
+# measures it per exchange kind, `collectives` in its line); LINK_GBS one xGMI link per direction (conservative: RCCL's
+# rings over the 7 links only shrink the byte term)
+DIST_ALPHA_US = 15.0
+DIST_LINK_GBS = 153.0
+
+
+def dist_form_estimate(frame_win_hi, world, n_fixed=1, alpha_us=DIST_ALPHA_US, link_gbs=DIST_LINK_GBS):
+    """ptzba_dist_form_estimate (host only): predicted per-trial cost of the rank-tree and the replicated form of a
+    `world`-rank solve -- the slowest rank's factorisation estimate plus its collectives (dict, microseconds)."""
+    win = np.ascontiguousarray(frame_win_hi, np.int32)
+    out = np.zeros(8)
+    _check(lib().ptzba_dist_form_estimate(len(win), int(n_fixed), _ptr(win), int(world), float(alpha_us), float(link_gbs),
+                                          _ptr(out)), "ptzba_dist_form_estimate")
+    return dict(tree_us=float(out[0]) if out[0] > 0 else None, replicated_us=float(out[1]), tree_factorisation_us=float(out[2]),
+                full_factorisation_us=float(out[3]), tree_collectives=int(out[4]), tree_doubles=int(out[5]),
+                replicated_doubles=int(out[6]), form="tree" if out[7] > 0 else "replicated",
+                model=f"slowest rank's plan_est_us + ring all-reduces (alpha {alpha_us} us, {link_gbs} GB/s per link)")
+
+
+def choose_dist_form(frame_win_hi, world, n_fixed=1, **kw):
+    """The form of a `world`-rank solve with the smaller predicted trial: 'tree' (part-owned,
+    partition_landmarks' split, set_problem(dist_world=world)) or 'replicated' (contiguous landmark blocks, one
+    all-reduce of the packed system).  Returns (form, estimate dict)."""
+    if world < 2:
+        return "single", None
+    est = dist_form_estimate(frame_win_hi, world, n_fixed, **kw)
+    return est["form"], est
+
+
+def replicated_shards(landmark, n_landmark, world):
+    """Landmark -> rank of the replicated form: contiguous landmark blocks of ~equal record counts (-1: no records)."""
+    cnt = np.bincount(np.asarray(landmark, np.int64), minlength=int(n_landmark))
+    cum = np.cumsum(cnt)
+    tot = max(int(cum[-1]) if len(cum) else 0, 1)
+    owner = np.minimum((np.concatenate([[0], cum[:-1]]) * world) // tot, world - 1).astype(np.int32)
+    owner[cnt == 0] = -1
+    return owner
+
+
 def partition_landmarks(n_pose, n_landmark, frame, landmark, world, n_fixed=1):
     """Landmark -> rank of a sharded solve (ptzba_partition_landmarks, host only): returns (rank_of_landmark
     [n_landmark] int32 (-1: no records), mode (1 part-owned, 0 replicated), (m, c_end, n_pose) split)."""
@@ -1107,13 +1151,26 @@ class BAHandle:
         _check(lib().ptzba_sync(self.h), "ptzba_sync")
 
     def reset_kernel_times(self, enable=True, groups=0xF, stride=1, flush=False):
-        """Restart kernel timing; `groups` bitmask: 1 K1, 2 Schur, 4 Cholesky solve, 8 back-substitution;
+        """Restart kernel timing; `groups` bitmask: 1 K1, 2 Schur, 4 Cholesky solve, 8 back-substitution, TIME_COMM (16)
+        every exchange (comm_times);
         events around every `stride`-th launch of a group (each event record adds a gap to the stream).
         flush: cold-cache K1 timing, a 1 GiB scratch buffer streamed through the caches before each timed K1 launch
         (outside the events): True / "write" writes it (dirty lines left behind), "read" reads it (clean lines)."""
         fl = (TIME_FLUSH | (TIME_FLUSH_READ if flush == "read" else 0)) if flush else 0
         flags = (int(groups) | (max(1, min(255, int(stride))) << 8) | fl) if enable else 0
         _check(lib().ptzba_reset_kernel_times(self.h, flags), "ptzba_reset_kernel_times")
+
+    def comm_times(self):
+        """Exchanges timed since reset_kernel_times(groups=... | TIME_COMM): a list of (kind, doubles, ms), one per
+        collective in stream order (kind: X_SYS / X_PART / X_SEP / X_SCAL / X_SUB)."""
+        n = np.zeros(1, np.int32)
+        _check(lib().ptzba_comm_times(self.h, 0, None, None, None, _ptr(n)), "ptzba_comm_times")
+        m = int(n[0])
+        kinds = np.zeros(max(m, 1), np.int32)
+        dbl = np.zeros(max(m, 1), np.int64)
+        ms = np.zeros(max(m, 1))
+        _check(lib().ptzba_comm_times(self.h, m, _ptr(kinds), _ptr(dbl), _ptr(ms), _ptr(n)), "ptzba_comm_times")
+        return [(int(k), int(d), float(t)) for k, d, t in zip(kinds[:m], dbl[:m], ms[:m])]
 
     def kernel_times(self):
         ms = np.zeros(4)
@@ -1307,9 +1364,11 @@ class LMSolver:
         t0 = time.perf_counter()
         # huber curvature switch (ptzba_lm_opts; the device loop's k_lm_decide rule): IRLS until an accepted step
         # is predicted to reduce the cost by less than curvature_switch of it, then huber_curvature, the current point re-linearised
-        switch = (getattr(h, "loss", LOSS_LINEAR) == LOSS_HUBER and self.curvature_switch > 0
-                  and self.huber_curvature < 1.0 and hasattr(h, "set_huber_curvature"))
-        if switch:
+        # every host run starts from IRLS (curvature 1), switch or not: a previous run on this handle may have left its
+        # reduced curvature behind (ptzba_set_problem / ptzba_lm_start reset it, a host run did not before round 6)
+        huber = getattr(h, "loss", LOSS_LINEAR) == LOSS_HUBER and hasattr(h, "set_huber_curvature")
+        switch = huber and self.curvature_switch > 0 and self.huber_curvature < 1.0
+        if huber:
             h.set_huber_curvature(1.0)
         h.linearize()
         s = self._scalars()
@@ -1379,6 +1438,10 @@ class LMSolver:
                 h.set_huber_curvature(self.huber_curvature)
                 h.linearize()
                 self._scalars()
+        if huber:
+            # leave the handle in the documented state (IRLS) for direct linearize() / build_reduced() callers; the
+            # state's linearisation slot is not touched (a following run re-linearises first)
+            h.set_huber_curvature(1.0)
         h.sync()
         t1 = time.perf_counter()
         return LMResult(status=status, message=STATUS_MSG.get(status, "?"), cost=cost, initial_cost=initial_cost,

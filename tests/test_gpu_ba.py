@@ -632,3 +632,71 @@ def test_setup_timing_reports_set_problem_phases(gpu_available):
     h.close()
     assert len(t) >= 4 and all(v >= 0.0 for v in t.values()), t
     assert "upload+alloc" in t, t
+
+
+def test_host_loop_curvature_does_not_carry_over(gpu_available):
+    """a host-driven Huber run that took the curvature switch must not leave its reduced curvature on the
+    handle.  Two host runs on one handle (the first switches, the second runs with curvature_switch=0, i.e. IRLS
+    throughout) equal the IRLS run on a fresh handle bit for bit, and a direct linearize() after a switched run gives
+    the IRLS cost again (the handle is back at curvature 1)."""
+    import ptzba
+    import synthetic
+    p = synthetic.make_problem("config1", seed=5)
+
+    def handle():
+        h = ptzba.BAHandle(0)
+        h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=ptzba.FP64,
+                      loss=ptzba.LOSS_HUBER, f_scale=1.0)
+        return h
+
+    kw = dict(ftol=1e-10, xtol=1e-14, max_iter=20, device_loop=False)
+    h = handle()
+    h.set_state(p.init_ptz, p.init_rays)
+    r1 = ptzba.LMSolver(h, curvature_switch=0.25, **kw).run()
+    assert r1.njev > 0
+    h.set_state(p.init_ptz, p.init_rays)
+    r2 = ptzba.LMSolver(h, curvature_switch=0.0, **kw).run()
+    s2 = h.get_state()
+    r1b = ptzba.LMSolver(h, curvature_switch=0.25, **kw).run()  # switches again, then the handle must be back at IRLS
+
+    def one_step(hh):  # a direct step: its predicted reduction depends on the curvature of the linearisation
+        hh.set_state(p.init_ptz, p.init_rays)
+        hh.linearize()
+        hh.build_reduced(1e-3)
+        hh.solve_reduced()
+        return np.asarray(hh.read_scalars()[:3], np.float64)
+
+    c_after = one_step(h)
+    h.close()
+    f = handle()
+    c_fresh = one_step(f)
+    f.set_state(p.init_ptz, p.init_rays)
+    rf = ptzba.LMSolver(f, curvature_switch=0.0, **kw).run()
+    sf = f.get_state()
+    f.close()
+    assert (r2.njev, r2.nfev, r2.status, r2.cost) == (rf.njev, rf.nfev, rf.status, rf.cost), (r2, rf)
+    assert np.array_equal(s2[0], sf[0]) and np.array_equal(s2[1], sf[1])
+    assert r1b.njev > 0 and np.array_equal(c_after, c_fresh), (c_after, c_fresh)
+
+
+def test_lm_opts_zero_filled_curvature_fields(gpu_available):
+    """ptzba_lm_init reads huber_curvature / curvature_switch for the Huber loss only, and 0 selects the
+    default curvature, so a caller that zero-fills the two fields added in ABI 0.2 is not rejected: a linear-loss solve
+    with both fields 0 equals the default-option solve, and a Huber solve with both 0 runs IRLS throughout (equal to
+    curvature_switch=0)."""
+    import ptzba
+    import synthetic
+    assert "0.2" in ptzba.lib().ptzba_version().decode()
+    p = synthetic.make_problem("config1", seed=6)
+    for loss in (ptzba.LOSS_LINEAR, ptzba.LOSS_HUBER):
+        out = []
+        for hc, cs in ((0.0, 0.0), (ptzba.HUBER_CURVATURE, 0.0 if loss == ptzba.LOSS_HUBER else ptzba.CURVATURE_SWITCH)):
+            h = ptzba.BAHandle(0)
+            h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=ptzba.FP64, loss=loss,
+                          f_scale=1.0)
+            h.set_state(p.init_ptz, p.init_rays)
+            r = ptzba.LMSolver(h, ftol=1e-10, xtol=1e-14, max_iter=20, huber_curvature=hc, curvature_switch=cs).run()
+            out.append((r.njev, r.status, r.cost, h.get_state()[0].copy()))
+            h.close()
+        assert out[0][:3] == out[1][:3], (loss, out[0][:3], out[1][:3])
+        assert np.array_equal(out[0][3], out[1][3])

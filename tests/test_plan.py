@@ -74,3 +74,46 @@ def test_config4_keeps_one_level_with_trailing_blocks(nd_env):
     _, tasks, _, _, _ = ptzba.plan_export(win, 1)
     typ = tasks[:, 0] & 3
     assert (typ == 3).sum() > 50 * (typ == 1).sum()  # nearly every trailing tile rides in a block
+
+
+def test_dist_form_choice_never_predicts_a_slowdown(nd_env):
+    """Round 6: bench.py --gpus N picks the form of the sharded solve with the smaller predicted
+    trial (ptzba.choose_dist_form, api.hip ptzba_dist_form_estimate: slowest rank's factorisation estimate + its
+    collectives as ring all-reduces).  Config 3's rank tree does not shorten the chain (its separators are dense ~110
+    frames), so from 4 ranks on its extra exchanges lose to the replicated solve; config 4's tree factorisation is
+    ~1.3x shorter than the whole system's and its exchanges are a fraction of the packed system, so it keeps the tree.
+    The chosen form's estimate is never above the other's, and at config 3 never above the single-GPU factorisation
+    plus the replicated collectives."""
+    os.environ.pop("PTZBA_ND_DEPTH", None)
+    w3 = np.load(os.path.join(ROOT, "tests", "golden", "config3_window.npy"))
+    w4 = np.load(os.path.join(ROOT, "tests", "golden", "config4_window.npy"))
+    expect3 = {2: "tree", 4: "replicated", 8: "replicated"}
+    for n, form in expect3.items():
+        f, e = ptzba.choose_dist_form(w3, n)
+        assert f == form, (n, e)
+        chosen = e["tree_us"] if f == "tree" else e["replicated_us"]
+        other = e["replicated_us"] if f == "tree" else e["tree_us"]
+        assert other is None or chosen <= other
+        assert e["replicated_doubles"] > e["tree_doubles"] > 0
+    for n in (2, 4, 8):
+        f, e = ptzba.choose_dist_form(w4, n)
+        assert f == "tree" and e["tree_factorisation_us"] < e["full_factorisation_us"], (n, e)
+    assert ptzba.choose_dist_form(w3, 1) == ("single", None)
+    # a larger alpha moves config 3 at N = 2 to the form with fewer collectives per trial
+    e2 = ptzba.dist_form_estimate(w3, 2, alpha_us=200.0)
+    assert e2["tree_collectives"] >= 2
+
+
+def test_replicated_shards_cover_every_landmark_in_contiguous_blocks():
+    """The replicated form's landmark -> rank map: contiguous blocks of ~equal record counts, -1 only for landmarks
+    without records."""
+    rng = np.random.default_rng(0)
+    n_lm = 1000
+    lm = rng.integers(0, n_lm - 10, 50000)  # the last ten landmarks have no records
+    for world in (2, 3, 8):
+        own = ptzba.replicated_shards(lm, n_lm, world)
+        assert (own[-10:] == -1).all() and (own[:n_lm - 10] >= 0).all()
+        live = own[own >= 0]
+        assert (np.diff(live) >= 0).all() and set(live.tolist()) == set(range(world))
+        counts = np.bincount(own[lm], minlength=world)
+        assert counts.max() - counts.min() <= 0.02 * len(lm) + 200, counts
