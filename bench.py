@@ -200,7 +200,7 @@ def stream_leg(frames):
         return {"error": repr(e)}
     keep = ("workload", "frontend", "frames", "fps_end_to_end", "tracking_ms", "keyframes", "keyframe_ba_ms",
             "lost_frames", "pose_rmse_vs_truth", "keyframe_ba_breakdown_ms", "keyframe_ba_slowest_breakdown_ms",
-            "render_s_outside_loop")
+            "render_s_outside_loop", "gc", "gc_pauses_ms")
     return {k: d[k] for k in keep if k in d}
 
 

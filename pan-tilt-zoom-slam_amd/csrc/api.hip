@@ -80,8 +80,6 @@ struct ptzba_ctx {
   size_t out_pin_cap = 0;
   DBuf chol_tasks, Ldiag, Minv, dpose;  // Minv: inverses of the diagonal factor tiles (back-substitution)
   std::vector<int> chol_task_off;  // host: per elimination level, offsets into chol_tasks
-  DBuf Lsub;                       // supercolumn plans: L_k+1,k of each pair until the next level copies it (chol_super)
-  bool chol_super = false;
   std::vector<int32_t> chol_tasks_host;  // host copy of chol_tasks (int4 records)
   DBuf tinv_tail;                        // diagonal tiles inverted after the factorisation
   int n_tinv_tail = 0;
@@ -138,6 +136,7 @@ struct ptzba_ctx {
   bool tm_flush = false;  // cold-cache timing: stream a scratch buffer through the caches before each timed K1
   bool tm_flush_read = false;  // ... by reading it (clean lines) instead of writing it
   DBuf flush_buf;
+  int64_t gpu_setup_min = -1;  // set_problem's device front from this many records (-1: GPU_SETUP_MIN_REC)
   // collective timing (enable bit PTZBA_TIME_COMM): an event pair around every exchange, its kind and size
   std::vector<hipEvent_t> cev;
   int cev_used = 0;
@@ -728,7 +727,6 @@ struct CholPlan {
   std::vector<int32_t> tinv_tail;  // diagonal tiles inverted after the last level (the others: type-2 tasks)
   int n_levels = 0;
   bool delayed = false;  // tasks carry a second pair of update panels (delayed trailing updates, make_plan)
-  int n_super = 0;       // supercolumn pairs (chol_super tasks: the factorisation needs the Lsub buffer)
   // blocked back substitution (large systems): tasks of 3 int4 (block columns | {p, intra-block coupling
   // bits, first-touch bits, 0} | {target column, flags, 0, 0}) and the task offset of each step (one launch
   // per step); empty when no valid schedule exists
@@ -837,12 +835,10 @@ struct TreeSpec {
   std::vector<int> ph_lv0, ph_lv1;  // out: per phase its levels [lv0, lv1) (the closing flush level included)
 };
 static int tile_owner(int i, int j, int nr) { return (i + j) % nr; }
+// (Round 4's supercolumn plans -- two chain columns per level task, measured slower: 0.31 vs 0.23 ms at config 3 --
+// were removed in round 6 with their kernel; DESIGN.md §4.3 keeps the record.)
 static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<int32_t>& win, int64_t ld, CholPlan& P,
-                      int force_dt = 0, TreeSpec* ts = nullptr, int super_mode = -1) {
-  // supercolumns (chol_super): two consecutive columns of a chain in one level -- single-rank plans at DT = 1;
-  // PTZBA_CHOL_SUPER=1 enables (A/B knob, read per plan)
-  if (super_mode < 0) super_mode = getenv_is("PTZBA_CHOL_SUPER", "1") ? 1 : 0;
-  if (ts) super_mode = 0;  // (continuation records must stay right behind their task)
+                      int force_dt = 0, TreeSpec* ts = nullptr) {
   const int T = (int)(ld / CHOL_NB);
   std::vector<std::vector<uint8_t>> nz(T, std::vector<uint8_t>(T, 0));
   auto mark = [&](int r, int c) {
@@ -887,23 +883,8 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
     count[L]++;
     level[k] = L;
   };
-  // supercolumn pairs (k, k + 1): k + 1 joins k's level when it depends on k and every other column it depends on is
-  // factored before that level (the pair's task applies those panels' last updates inline)
-  std::vector<uint8_t> head(T, 0), tail(T, 0);
   if (!ts) {
-    for (int k = 0; k < T; ++k) {
-      if (super_mode && k > 0 && !head[k - 1] && !tail[k - 1] && nz[k][k - 1]) {
-        int lo = 0;
-        for (int p = 0; p < k - 1; ++p)
-          if (nz[k][p]) lo = std::max(lo, level[p] + 1);
-        if (lo <= level[k - 1]) {
-          level[k] = level[k - 1];  // (one unit of the level's four columns with its head)
-          head[k - 1] = tail[k] = 1;
-          continue;
-        }
-      }
-      place(k, 0);
-    }
+    for (int k = 0; k < T; ++k) place(k, 0);
   } else {
     const int NP = (int)ts->ph_nr.size();
     ts->ph_lv0.assign(NP, 0);
@@ -930,16 +911,9 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
   for (int k = 0; k < T; ++k)
     if (level[k] >= 0) K[level[k]].push_back(k);
   P.tasks.clear();
-  P.n_super = 0;
   P.level_off.assign(nL + 1, 0);
   auto push = [&](int type, int i, int j, int w) {
     P.tasks.push_back(type); P.tasks.push_back(i); P.tasks.push_back(j); P.tasks.push_back(w);
-  };
-  // continuation record of a task with more than four panels (supercolumn plans, task word w bit 31): right behind
-  // it, a type-2 no-op for its own workgroup (i = -1) whose z / w carry panels 4, 5 / 6, 7 (16 bits each, + 1)
-  auto push_cont = [&](const std::vector<int>& pd) {
-    auto pk = [&](size_t a) { return a < pd.size() ? pd[a] + 1 : 0; };
-    push(2, -1, pk(4) | (pk(5) << 16), pk(6) | (pk(7) << 16));
   };
   // inverses of the diagonal factor tiles (for the back-substitution): the tiles of level L-1's columns are
   // inverted by type-2 tasks of level L, beside its panels (off the critical path); the last level's after
@@ -964,7 +938,6 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
   if (force_dt) DT = force_dt;
   P.delayed = DT > 1;
   size_t max_pd = 0;  // update panels of one task: the P2 kernel takes up to four (any DT), the other two
-  bool super_over = false;  // a supercolumn task with more than eight panels
   bool any_block = false;  // 2 x 2 trailing blocks (type 3) run in the P2 kernel only
   auto pack2 = [](int type, const std::vector<int>& pd, int tm) {  // int4 task: x (type + panels 2, 3), w (0, 1)
     return std::make_pair(chol_pack_type(type, pd.size() > 2 ? pd[2] : -1, pd.size() > 3 ? pd[3] : -1, (tm >> 2) & 3),
@@ -982,24 +955,7 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
     if (L > 0)
       for (int l = last_trailing; l < L; ++l) inl.insert(inl.end(), K[l].begin(), K[l].end());
     for (int k : K[L]) {
-      if (tail[k]) continue;  // factored by its head's supercolumn tasks
       std::vector<int> pd;
-      if (head[k]) {  // supercolumn (k, k + 1): the diagonal task (i = k) and one task per row tile below k + 1
-        for (int pp : inl)
-          if (pp < k && (nz[k][pp] || nz[k + 1][pp])) pd.push_back(pp);
-        // panels 5..8 (a separator's first pair after four leaf pairs) ride in a continuation record right behind the
-        // task: a type-2 no-op for its own workgroup (i = -1), z / w = panels 4, 5 / 6, 7 (16 bits each)
-        if (pd.size() > 8) super_over = true;
-        const std::vector<int> pd4(pd.begin(), pd.begin() + std::min<size_t>(4, pd.size()));
-        for (int i = k; i < T; ++i) {
-          if (i == k + 1 || !(i == k || nz[i][k] || nz[i][k + 1]) || !own(i)) continue;
-          const auto w = pack2(0, pd4, 15);
-          push(w.first, i, k, (int)((unsigned)w.second | (1u << 30) | (pd.size() > 4 ? 1u << 31 : 0u)));
-          if (pd.size() > 4) push_cont(pd);
-        }
-        P.n_super++;
-        continue;
-      }
       for (int pp : inl)
         if (pp < k && nz[k][pp]) pd.push_back(pp);
       for (int i = k; i < T; ++i) {
@@ -1046,9 +1002,7 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
       while (y < upd.size() && upd[y].first == upd[x].first) ++y;
       std::vector<int> pd;
       for (size_t u = x; u < y; ++u) pd.push_back(upd[u].second);
-      // (supercolumn plans: a trailing tile takes up to eight panels, 5..8 in a continuation record)
-      if (super_mode && pd.size() > 4) super_over = super_over || pd.size() > 8;
-      else max_pd = std::max(max_pd, pd.size());
+      max_pd = std::max(max_pd, pd.size());
       tiles_pd.push_back({upd[x].first, pd});
       x = y;
     }
@@ -1080,38 +1034,22 @@ static bool make_plan(const SysOrder& o, int n_pose, int nf, const std::vector<i
     for (size_t q = 0; q < tiles_pd.size(); ++q) {
       if (in_block[q]) continue;
       const int i = (int)(tiles_pd[q].first / T), j = (int)(tiles_pd[q].first % T);
-      const auto& pd = tiles_pd[q].second;
-      const std::vector<int> pd4(pd.begin(), pd.begin() + std::min<size_t>(4, pd.size()));
-      const auto w = pack2(1, pd4, 15);
-      push(w.first, i, j, (int)((unsigned)w.second | (pd.size() > 4 ? 1u << 31 : 0u)));
-      if (pd.size() > 4) push_cont(pd);
+      const auto w = pack2(1, tiles_pd[q].second, 15);
+      push(w.first, i, j, w.second);
     }
-    // type 2: inverses of the previous level's diagonal tiles; a supercolumn head's task also copies L_k+1,k from
-    // Lsub into the factor (w bit 0; bit 1: copy only)
-    for (int pp : prev) {
-      const bool inv = tinv_split && pp < n_inv;
-      if (head[pp]) push(2, pp, pp, inv ? 1 : 3);
-      else if (inv) push(2, pp, pp, 0);
-    }
+    // type 2: inverses of the previous level's diagonal tiles
+    for (int pp : prev)
+      if (tinv_split && pp < n_inv) push(2, pp, pp, 0);
   }
   for (int k = 0; k < n_inv && k < T; ++k)
     if (own(k) && (!tinv_split || level[k] == nL - 1)) P.tinv_tail.push_back(k);
   P.level_off[nL] = (int)(P.tasks.size() / 4);
-  bool last_pairs = false;
-  if (nL > 0)
-    for (int k : K[nL - 1]) last_pairs = last_pairs || head[k];
-  if (last_pairs) {  // the last level's supercolumns: one more level copies their L_k+1,k (the inverses stay in tinv_tail)
-    for (int k : K[nL - 1])
-      if (head[k]) push(2, k, k, 3);
-    ++nL;
-    P.level_off.push_back((int)(P.tasks.size() / 4));
-  }
   P.n_levels = nL;
-  if (max_pd > 4 || super_over) {  // too many panels: DT = 1, then no supercolumns
-    if (DT > 1) return make_plan(o, n_pose, nf, win, ld, P, 1, ts, super_mode);
-    return super_mode ? make_plan(o, n_pose, nf, win, ld, P, force_dt, ts, 0) : false;
+  if (max_pd > 4) {  // too many panels for one task: DT = 1
+    if (DT > 1) return make_plan(o, n_pose, nf, win, ld, P, 1, ts);
+    return false;
   }
-  if (max_pd > 2 || any_block || P.n_super) P.delayed = true;  // the P2 kernel (second panel pair, trailing blocks, pairs)
+  if (max_pd > 2 || any_block) P.delayed = true;  // the P2 kernel (second panel pair, trailing blocks)
   // back-substitution: chains of tile columns holding unknowns and, per chain position, the chain's
   // later columns coupled to that row tile (right-looking updates).  Nested orders: one chain per leaf of
   // the separator tree (its root-to-leaf path, each node's columns descending); natural: one chain.
@@ -1529,7 +1467,8 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   // built on the device (setup_kernels.hip: one stable radix sort of the composite key landmark * n_pose + frame --
   // the same order as the host's two stable counting sorts); the host keeps only the per-segment arrays its
   // structure passes read.  Smaller ones (a sliding window's ~170K records) stay on the host.
-  const bool gpu_setup = n_obs >= GPU_SETUP_MIN_REC && n_obs < ((int64_t)1 << 31) &&
+  const bool gpu_setup = n_obs >= (h->gpu_setup_min >= 0 ? h->gpu_setup_min : GPU_SETUP_MIN_REC) && n_obs > 0 &&
+                         n_obs < ((int64_t)1 << 31) &&
                          (uint64_t)n_landmark * (uint64_t)n_pose <= ((uint64_t)1 << 32);
   // ---- stable counting sorts: by frame, then by landmark -> (landmark, frame, original index)
   std::vector<int64_t> tmp, order(gpu_setup ? 0 : n_obs), lm_start;
@@ -1924,7 +1863,6 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
   h->n_tinv_tail = (int)plan.tinv_tail.size();
   h->chol_levels = plan.n_levels;
   h->chol_delayed = plan.delayed;
-  h->chol_super = plan.n_super > 0;
   h->n_chain = (int)plan.chain_off.size() - 1;
   frame_win_hi = win;  // K2 windows follow the same (possibly global) coupling
   h->perm_uploaded = gpu_setup;  // (the device front wrote the permutation itself)
@@ -1984,7 +1922,6 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
       h->lm_red.alloc((size_t)n_landmark * 4 * 8) || h->sys.alloc((size_t)h->sys_count() * 8) ||
       h->scal.alloc(2 * PTZBA_NSCALARS * 8) || h->red_scratch.alloc(RED_SCRATCH * 8) || h->info.alloc(16) ||
       h->Ldiag.alloc((size_t)h->ld * CHOL_NB * 8) || h->Minv.alloc((size_t)h->ld * CHOL_NB * 8) ||
-      (h->chol_super && h->Lsub.alloc((size_t)h->ld * CHOL_NB * 8)) ||
       h->dpose.alloc((size_t)h->ld * 8) ||
       h->s2_part.alloc((size_t)std::max(h->n_s2_items, 1) * SCHUR_F1 * 9 * WAVE * 8) ||
       h->part_diag.alloc((size_t)std::max(h->n_s2_items, 1) * SCHUR_F1 * 12 * 8))
@@ -2446,7 +2383,7 @@ static int solve_impl(ptzba_ctx* h, const double* lam_dev, int nx, const int* se
                                  h->lambda, lam_dev, h->st);
     launch_cholesky(h->S(), h->ld, h->chol_tasks.as<int4>(), h->chol_task_off.data(), h->chol_levels,
                       h->Ldiag.as<double>(), h->info.as<int>(), h->st, nullptr, th, h->Minv.as<double>(), 0,
-                      h->chol_delayed, h->chol_super ? h->Lsub.as<double>() : nullptr);
+                      h->chol_delayed);
   }
   if (h->bs_pst)
     launch_chol_backsolve_pst(h->S(), h->ld, h->n_aug, h->bsb_tasks.as<int4>(), h->bsp_expect.as<int4>(),
@@ -3477,6 +3414,15 @@ int ptzba_set_huber_curvature(ptzba_handle h, double hc) {
   if (!h) return fail("null handle");
   if (!(hc > 0.0 && hc <= 1.0)) return fail("huber curvature must lie in (0, 1]");
   h->hcurv = hc;
+  return 0;
+}
+
+// which front the following set_problem calls use (round 6): the device front from min_records records on
+// (0: always, INT64_MAX: never, -1: the default GPU_SETUP_MIN_REC = 4M).  Both fronts build the same arrays bit for bit
+// (tests/test_gpu_ba.py compares them); the knob is the test hook and a per-handle tuning point.
+int ptzba_set_setup_front(ptzba_handle h, int64_t min_records) {
+  if (!h) return fail("null handle");
+  h->gpu_setup_min = min_records < 0 ? -1 : min_records;
   return 0;
 }
 

@@ -31,9 +31,6 @@
 namespace ptzba {
 
 constexpr int NB = CHOL_NB;
-#ifndef BS_LA
-#define BS_LA 1  // 1: lookahead back substitution (k_chol_backsolve_la), 0: barrier per column
-#endif
 constexpr double AUG_DIAG = 1e300;
 
 __device__ __forceinline__ double bcast(double v, int j) {
@@ -645,135 +642,13 @@ struct CholTaskVal {
   const int4* rest;
   __device__ int4 get(int b) const { return b < CHOL_KT ? t[b] : rest[b - CHOL_KT]; }
 };
-// Supercolumn panel task (api.hip make_plan, PTZBA_CHOL_SUPER): the tile columns k and k + 1 of one chain factored in
-// ONE level -- half the launch boundaries and tile round trips of the chain.  The workgroup of row tile i stages the raw
-// tiles D00 = A_kk, D10 = A_k+1,k, D11 = A_k+1,k+1 (and T0 = A_ik, T1 = A_i,k+1 when i > k + 1), applies the update
-// panels p of the previous levels to all of them (D00 -= L_kp L_kp^T, D10 -= L_k+1,p L_kp^T, D11 -= L_k+1,p L_k+1,p^T,
-// T0 -= L_ip L_kp^T, T1 -= L_ip L_k+1,p^T; panels a tile is not coupled to meet zero tiles), then
-//   sweep 1: L00 = chol(D00) and L10 = D10 L00^-T in one pass (wg_potrf_trsm32_df);
-//   T0: L_i0 = T0 L00^-T by forward substitution (one wave, a lane per row);
-//   D11 -= L10 L10^T, T1 -= L_i0 L10^T (the intra-pair update, never a trailing task's);
-//   sweep 2: L11 = chol(D11) and L_i1 = T1 L11^-T.
-// Every task of the pair factors the 64 x 64 diagonal block itself (as every panel task factors its diagonal tile), so
-// the raw A_kk, A_k+1,k and A_k+1,k+1 stay untouched during the level: the diagonal task (i == k) writes L00 and L11 to
-// Ldiag and L10 to Lsub[k], which the type-2 task of the next level copies into A_k+1,k (no task of that level reads
-// the tile).  Tiles: D00 sD, D10 sC, D11 sE[0], T0 sE[1], T1 sB[1]; panel staging sA[0] (L_kp), sA[1] (L_k+1,p),
-// sB[0] (L_ip); the sweeps' block buffer overlays sA as in chol_task.
-template <bool COH>
-__device__ __forceinline__ void chol_super(double* __restrict__ A, int64_t ld, int i, int k, const int (&ups)[8],
-                                           double* __restrict__ Ldiag, int* info, double* __restrict__ Lsub,
-                                           double (*sD)[NB + 1], double (*sC)[NB + 1], double (*sA)[NB][NB + 1],
-                                           double (*sB)[NB][NB + 1], double (*sE)[NB][NB + 1], double (*s_lb)[2 * NB][LA_BW],
-                                           double (*s_pb)[LA_BW], int* s_flags, double* s_rinv) {
-  const bool diag = i == k;
-  const int64_t NBl = NB;
-  double r0[4], r1[4], r2[4], r3[4], r4[4], p0[4], p1[4], p2[4];
-  fetch_tile<COH>(r0, A + (int64_t)k * NBl * ld + k * NBl, ld);
-  fetch_tile<COH>(r1, A + (int64_t)(k + 1) * NBl * ld + k * NBl, ld);
-  fetch_tile<COH>(r2, A + (int64_t)(k + 1) * NBl * ld + (k + 1) * NBl, ld);
-  if (!diag) {
-    fetch_tile<COH>(r3, A + (int64_t)i * NBl * ld + k * NBl, ld);
-    fetch_tile<COH>(r4, A + (int64_t)i * NBl * ld + (k + 1) * NBl, ld);
-  }
-  auto pfetch = [&](int p) {
-    fetch_tile<COH>(p0, A + (int64_t)k * NBl * ld + p * NBl, ld);
-    fetch_tile<COH>(p1, A + (int64_t)(k + 1) * NBl * ld + p * NBl, ld);
-    if (!diag) fetch_tile<COH>(p2, A + (int64_t)i * NBl * ld + p * NBl, ld);
-  };
-  int u = 0;
-  while (u < 8 && ups[u] < 0) ++u;
-  if (u < 8) pfetch(ups[u]);
-  put_tile(sD, r0);
-  put_tile(sC, r1);
-  put_tile(sE[0], r2);
-  if (!diag) {
-    put_tile(sE[1], r3);
-    put_tile(sB[1], r4);
-  }
-  while (u < 8) {
-    int un = u + 1;
-    while (un < 8 && ups[un] < 0) ++un;
-    put_tile(sA[0], p0);
-    put_tile(sA[1], p1);
-    if (!diag) put_tile(sB[0], p2);
-    if (un < 8) pfetch(ups[un]);  // in flight during this panel's MFMAs
-    __syncthreads();
-    // each wave owns one 16 x 16 block of every output tile: no barrier between the products
-    tile_gemm_nt_sub(sD, sA[0], sA[0]);
-    tile_gemm_nt_sub(sC, sA[1], sA[0]);
-    tile_gemm_nt_sub(sE[0], sA[1], sA[1]);
-    if (!diag) {
-      tile_gemm_nt_sub(sE[1], sB[0], sA[0]);
-      tile_gemm_nt_sub(sB[1], sB[0], sA[1]);
-    }
-    __syncthreads();
-    u = un;
-  }
-  // sweep 1 (its entry barrier orders the staging above): L00 -> block rows 0..31, L10 -> rows 32..63
-  wg_potrf_trsm32_df<LA_BW, false>(sD, sC, s_lb, s_pb, s_flags, info, nullptr);
-  __syncthreads();
-  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-    const int r = e >> 5, m = e & 31;
-    sD[r][m] = m <= r ? s_lb[m / LA_BW][r][m % LA_BW] : 0.0;
-    sC[r][m] = s_lb[m / LA_BW][NB + r][m % LA_BW];
-  }
-  __syncthreads();
-  if (diag) {
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-      gst<COH>(Ldiag + (int64_t)k * NB * NB + e, sD[e >> 5][e & 31]);
-      gst<COH>(Lsub + (int64_t)k * NB * NB + e, sC[e >> 5][e & 31]);
-    }
-  } else {
-    // L_i0 = T0 L00^-T: lane r solves row r, right-looking (x_c final, then every later entry takes its term)
-    if (threadIdx.x < NB) s_rinv[threadIdx.x] = rcp_nr(sD[threadIdx.x][threadIdx.x]);
-    __syncthreads();
-    if (threadIdx.x < NB) {
-      const int r = threadIdx.x;
-      double t[NB];
-#pragma unroll
-      for (int m = 0; m < NB; ++m) t[m] = sE[1][r][m];
-#pragma unroll
-      for (int c = 0; c < NB; ++c) {
-        const double x = t[c] * s_rinv[c];
-        t[c] = x;
-#pragma unroll
-        for (int m = c + 1; m < NB; ++m) t[m] = fma(-sD[m][c], x, t[m]);
-      }
-#pragma unroll
-      for (int m = 0; m < NB; ++m) sE[1][r][m] = t[m];
-    }
-    __syncthreads();
-    tile_gemm_nt_sub(sB[1], sE[1], sC);  // T1 -= L_i0 L10^T
-  }
-  tile_gemm_nt_sub(sE[0], sC, sC);  // D11 -= L10 L10^T
-  // sweep 2 (entry barrier orders the products): L11 -> block rows 0..31, L_i1 -> rows 32..63
-  wg_potrf_trsm32_df<LA_BW, false>(sE[0], diag ? nullptr : sB[1], s_lb, s_pb, s_flags, info, nullptr);
-  __syncthreads();
-  if (diag) {
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-      const int r = e >> 5, m = e & 31;
-      gst<COH>(Ldiag + (int64_t)(k + 1) * NB * NB + e, m <= r ? s_lb[m / LA_BW][r][m % LA_BW] : 0.0);
-    }
-    return;
-  }
-  double* C0 = A + (int64_t)i * NBl * ld + k * NBl;
-  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-    const int r = e >> 5, m = e & 31;
-    gst<COH>(C0 + (int64_t)r * ld + m, sE[1][r][m]);
-    gst<COH>(C0 + (int64_t)r * ld + NB + m, s_lb[m / LA_BW][NB + r][m % LA_BW]);
-  }
-}
-
 // P2: plans with delayed trailing updates (a second pair of update panels per task, api.hip make_plan)
 // One factorisation task (api.hip make_plan: panel / trailing / inverse / trailing block) by the workgroup: the
 // body of a level launch (k_chol_step).
-template <bool SG, bool P2, bool COH, bool SUP = false>
+template <bool SG, bool P2, bool COH>
 __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, const int4 tk, double* __restrict__ Ldiag,
-                                          int* info, double* __restrict__ sgn, double* __restrict__ Minv,
-                                          double* __restrict__ Lsub = nullptr, int4 tk2 = int4{0, 0, 0, 0}) {
-  static_assert(!SUP || (P2 && !SG),
-                "supercolumn tasks: the P2 kernel of SPD plans with the default sweep");
-  static_assert(!(COH && SG), "the persistent form factors SPD systems only");
+                                          int* info, double* __restrict__ sgn, double* __restrict__ Minv) {
+  static_assert(!(COH && SG), "coherent tile accesses: SPD level launches only");
   __shared__ double sC[NB][NB + 1];     // target tile (panel T_ik / trailing A_ij)
   __shared__ double sD[NB][NB + 1];     // diagonal tile -> L_kk
   __shared__ __attribute__((aligned(16))) double sA[2][NB][NB + 1];  // L_ip of the two update panels
@@ -788,15 +663,7 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
   __shared__ double s_sgp[2][NB];  // SG: signs of the two update panels' columns
   __shared__ double s_sig[NB];     // SG: signs of this column's pivots
   if ((tk.x & 3) == 2) {  // inverse of a diagonal factor tile of the previous level (see tile_inv_wave)
-    if (tk.y < 0) return;  // no-op slot of an XCD-ordered level (api.hip xcd_interleave)
-    if constexpr (SUP) {
-      if (tk.w & 1) {  // the previous level's supercolumn k = tk.y: its L_k+1,k from Lsub into the factor
-        double* dst = A + (int64_t)(tk.y + 1) * NB * ld + (int64_t)tk.y * NB;
-        const double* src = Lsub + (int64_t)tk.y * NB * NB;
-        for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) gst<COH>(dst + (int64_t)(e >> 5) * ld + (e & 31), gld<COH>(src + e));
-      }
-      if (tk.w & 2) return;  // copy only (a column without an inverse)
-    }
+    if (tk.y < 0) return;  // (no-op slot)
     __shared__ double s_rinv[NB];
     tile_inv_wave<COH>(Ldiag + (int64_t)tk.y * NB * NB, Minv + (int64_t)tk.y * NB * NB, sD, s_rinv);
     return;
@@ -820,18 +687,6 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
   if constexpr (P2 && !SG) {
     if (type == 3) {  // 2 x 2 block of trailing tiles (api.hip make_plan): A_ij -= sum_p L_ip L_jp^T
       chol_trail_block<COH>(A, ld, i, j, ((tk.w >> 28) & 3) | (((unsigned)tk.x >> 30) << 2), up0, up1, up2, up3, sA, sB);
-      return;
-    }
-  }
-  if constexpr (SUP) {
-    if (type == 0 && (((unsigned)tk.w >> 30) & 1)) {  // supercolumn panel task (columns j, j + 1)
-      __shared__ double sE[2][NB][NB + 1];
-      __shared__ double s_rinv2[NB];
-      // panels 5..8 from the continuation record (w bit 31)
-      const bool cont = ((unsigned)tk.w >> 31) & 1;
-      const int ups[8] = {up0, up1, up2, up3, cont ? (tk2.z & 0xffff) - 1 : -1, cont ? ((tk2.z >> 16) & 0xffff) - 1 : -1,
-                          cont ? (tk2.w & 0xffff) - 1 : -1, cont ? ((tk2.w >> 16) & 0xffff) - 1 : -1};
-      chol_super<COH>(A, ld, i, j, ups, Ldiag, info, Lsub, sD, sC, sA, sB, sE, s_lb, s_pb, s_flags, s_rinv2);
       return;
     }
   }
@@ -892,36 +747,6 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
       __syncthreads();
       if (up2 >= 0) tile_gemm_nt_sub<SG>(sC, sA[0], sB[0], s_sgp[0]);
       if (up3 >= 0) tile_gemm_nt_sub<SG>(sC, sA[1], sB[1], s_sgp[1]);
-    }
-    if constexpr (SUP) {
-      if (((unsigned)tk.w >> 31) & 1) {  // panels 5..8 from the continuation record, two per pass
-        const int ux[4] = {(tk2.z & 0xffff) - 1, ((tk2.z >> 16) & 0xffff) - 1, (tk2.w & 0xffff) - 1,
-                           ((tk2.w >> 16) & 0xffff) - 1};
-        for (int h2 = 0; h2 < 2; ++h2) {
-          const int ua = ux[2 * h2], ub = ux[2 * h2 + 1];
-          if (ua < 0 && ub < 0) continue;
-          if (ua >= 0) {
-            fetch_tile<COH>(w2, A + i * NBl * ld + ua * NBl, ld);
-            fetch_tile<COH>(w3, A + j * NBl * ld + ua * NBl, ld);
-          }
-          if (ub >= 0) {
-            fetch_tile<COH>(w4, A + i * NBl * ld + ub * NBl, ld);
-            fetch_tile<COH>(w5, A + j * NBl * ld + ub * NBl, ld);
-          }
-          __syncthreads();
-          if (ua >= 0) {
-            put_tile(sA[0], w2);
-            put_tile(sB[0], w3);
-          }
-          if (ub >= 0) {
-            put_tile(sA[1], w4);
-            put_tile(sB[1], w5);
-          }
-          __syncthreads();
-          if (ua >= 0) tile_gemm_nt_sub<SG>(sC, sA[0], sB[0], s_sgp[0]);
-          if (ub >= 0) tile_gemm_nt_sub<SG>(sC, sA[1], sB[1], s_sgp[1]);
-        }
-      }
     }
     __syncthreads();
     store_tile<COH>(C, ld, [&](int r, int m) { return sC[r][m]; });
@@ -1015,58 +840,46 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
 #endif
 }
 
-template <bool SG, typename TaskArg, bool P2 = false, bool COH = false, bool SUP = false>
+template <bool SG, typename TaskArg, bool P2 = false, bool COH = false>
 __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, int64_t ld, const TaskArg tasks,
                                                    double* __restrict__ Ldiag, int* info, double* __restrict__ sgn,
-                                                   double* __restrict__ Minv, double* __restrict__ Lsub) {
-  const int4 tk = tasks.get(blockIdx.x);
-  int4 tk2{0, 0, 0, 0};
-  if constexpr (SUP) {  // a continuation record (panels 5..8 of a panel / supercolumn / trailing task) follows it
-    if ((tk.x & 3) <= 1 && ((unsigned)tk.w >> 31)) tk2 = tasks.get(blockIdx.x + 1);
-  }
-  chol_task<SG, P2, COH, SUP>(A, ld, tk, Ldiag, info, sgn, Minv, Lsub, tk2);
+                                                   double* __restrict__ Minv) {
+  chol_task<SG, P2, COH>(A, ld, tasks.get(blockIdx.x), Ldiag, info, sgn, Minv);
 }
 
 // (Rounds 4 tried every level of a factorisation in ONE launch -- one workgroup per task, a task of level L waiting
 // on level L - 1's completion counter: bitwise the same factor, 338-425 us per trial against ~232 with one launch per
 // level; removed in round 5.)
-template <typename TaskArg, bool COH>
+// SPD factorisations write their tiles through (agent-scope stores) and read them past this XCD's L2 (COH): the next
+// level's workgroups, mostly on other XCDs, find the tiles in the Infinity Cache at once (same-box A/B r04e:
+// cholesky_solve 240 -> 232 us per trial at config 3; the plain-access knob PTZBA_CHOL_COH=0 was removed in round 6).
+// The signed (EKF) factor keeps plain accesses.
+template <typename TaskArg>
 static void launch_chol_level(const TaskArg& ta, int n, double* A, int64_t ld, double* Ldiag, int* info, double* sgn,
-                              double* Minv, bool delayed, hipStream_t st, double* Lsub) {
+                              double* Minv, bool delayed, hipStream_t st) {
   if (sgn)
-    hipLaunchKernelGGL((k_chol_step<true, TaskArg, false, false>), dim3(n), dim3(256), 0, st, A, ld, ta, Ldiag, info, sgn, Minv, Lsub);
-  else if (Lsub)  // plans with supercolumn tasks (always the P2 kernel)
-    hipLaunchKernelGGL((k_chol_step<false, TaskArg, true, COH, true>), dim3(n), dim3(256), 0, st, A, ld, ta, Ldiag, info, sgn, Minv, Lsub);
+    hipLaunchKernelGGL((k_chol_step<true, TaskArg, false, false>), dim3(n), dim3(256), 0, st, A, ld, ta, Ldiag, info, sgn, Minv);
   else if (delayed)
-    hipLaunchKernelGGL((k_chol_step<false, TaskArg, true, COH>), dim3(n), dim3(256), 0, st, A, ld, ta, Ldiag, info, sgn, Minv, Lsub);
+    hipLaunchKernelGGL((k_chol_step<false, TaskArg, true, true>), dim3(n), dim3(256), 0, st, A, ld, ta, Ldiag, info, sgn, Minv);
   else
-    hipLaunchKernelGGL((k_chol_step<false, TaskArg, false, COH>), dim3(n), dim3(256), 0, st, A, ld, ta, Ldiag, info, sgn, Minv, Lsub);
+    hipLaunchKernelGGL((k_chol_step<false, TaskArg, false, true>), dim3(n), dim3(256), 0, st, A, ld, ta, Ldiag, info, sgn, Minv);
 }
 void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_off_host, int n_launch, double* Ldiag,
                      int* info, hipStream_t st, double* sgn, const int4* tasks_host, double* Minv, int first_level,
-                     bool delayed, double* Lsub) {
+                     bool delayed) {
   // a level's first CHOL_KT tasks travel by value in the kernel arguments (the rest through a pointer): the
   // workgroup's first dependent load disappears (round 2 A/B: 313 -> 308 us per trial at config 3)
-  constexpr bool by_value = true;
-  // SPD factorisations write their tiles through (agent-scope stores) and read them past this XCD's L2: the next
-  // level's workgroups, mostly on other XCDs, find the tiles in the Infinity Cache at once (same-box A/B r04e:
-  // cholesky_solve 240 -> 232 us per trial at config 3).  PTZBA_CHOL_COH=0: plain accesses (A/B knob, read per call)
-  const char* coh_env = getenv("PTZBA_CHOL_COH");
-  const bool coh = !(coh_env && atoi(coh_env) == 0);
   for (int L = first_level; L < n_launch; ++L) {
     const int n = task_off_host[L + 1] - task_off_host[L];
     if (n <= 0) continue;
-    if (tasks_host && by_value) {
+    if (tasks_host) {
       CholTaskVal tv;
       std::memcpy(tv.t, tasks_host + task_off_host[L], std::min(n, CHOL_KT) * sizeof(int4));
       tv.rest = tasks + task_off_host[L] + CHOL_KT;
-      if (coh) launch_chol_level<CholTaskVal, true>(tv, n, A, ld, Ldiag, info, sgn, Minv, delayed, st, Lsub);
-      else launch_chol_level<CholTaskVal, false>(tv, n, A, ld, Ldiag, info, sgn, Minv, delayed, st, Lsub);
+      launch_chol_level<CholTaskVal>(tv, n, A, ld, Ldiag, info, sgn, Minv, delayed, st);
       continue;
     }
-    const CholTaskPtr tp{tasks + task_off_host[L]};
-    if (coh) launch_chol_level<CholTaskPtr, true>(tp, n, A, ld, Ldiag, info, sgn, Minv, delayed, st, Lsub);
-    else launch_chol_level<CholTaskPtr, false>(tp, n, A, ld, Ldiag, info, sgn, Minv, delayed, st, Lsub);
+    launch_chol_level<CholTaskPtr>(CholTaskPtr{tasks + task_off_host[L]}, n, A, ld, Ldiag, info, sgn, Minv, delayed, st);
   }
 }
 
@@ -1101,119 +914,13 @@ __global__ __launch_bounds__(64) void k_tile_inv(const double* __restrict__ Ldia
   }
 }
 
-// back substitution L^T x = y with y = row n of the factor; x written to xout[0..n).  Workgroup c
-// walks chain c (tile columns in processing order, descending; nested dissection: C then A, C then B;
-// chains compute shared columns identically), right-looking: the running right-hand side r (init y)
-// lives in LDS; per column kt one wave forms x_kt = M_kt^T r_kt (32-term dot products, no serial
-// chain), then the waves apply x_kt to the chain's later columns coupled to row tile kt
-// (r_j -= L_kt,j^T x_kt; wave = update tile, lane = (column, row half)).  The next column's L values, update tiles
-// only, and M column do not depend on x: they are loaded into registers right after this column's
-// update, in flight during the next column's barrier and solve.  upd_off / upd_tiles (per chain
-// position) list the update tiles; more than 32 load directly.
 #ifdef BS_TIMING
 __device__ long long g_bs_stamps[2][128][6];
 __device__ long long g_bs_edges[2][4];
-#define BS_STAMP(k) do { if (threadIdx.x == 0 && q - q0 < 128) g_bs_stamps[blockIdx.x & 1][q - q0][k] = clock64(); } while (0)
-#else
-#define BS_STAMP(k) do { } while (0)
 #endif
-__global__ __launch_bounds__(1024) void k_chol_backsolve(const double* __restrict__ L, int64_t ld, int n,
-                                                         const int* __restrict__ chain_off,
-                                                         const int* __restrict__ chain_cols,
-                                                         const int* __restrict__ upd_off,
-                                                         const int* __restrict__ upd_tiles, int n_upd,
-                                                         const double* __restrict__ Ldiag,
-                                                         const double* __restrict__ Minv, double* __restrict__ xout) {
-  extern __shared__ __attribute__((aligned(16))) double xv[];  // [ld] | upd_off [nq+1] | upd_tiles [n_upd] (int)
-  __shared__ double sM[NB][NB + 1];
-#ifdef BS_TIMING
-  if (threadIdx.x == 0) g_bs_edges[blockIdx.x & 1][0] = clock64();
-#endif
-  const int nq = chain_off[gridDim.x];
-  int* s_uoff = reinterpret_cast<int*>(xv + ld);
-  int* s_ut = s_uoff + nq + 1;
-  const int t = threadIdx.x;
-  const int c = t & 31, u = t >> 5, wv = t >> 6;
-  // y = row n of the factor: off-diagonal tiles in place, the tile holding row n in Ldiag
-  const int tn = n / NB, rn = n - tn * NB;
-  for (int i = t; i < ld; i += blockDim.x)
-    xv[i] = (i >= n) ? 0.0 : (i < tn * NB ? L[(int64_t)n * ld + i] : Ldiag[((int64_t)tn * NB + rn) * NB + (i - tn * NB)]);
-  for (int i = t; i <= nq; i += blockDim.x) s_uoff[i] = upd_off[i];
-  for (int i = t; i < n_upd; i += blockDim.x) s_ut[i] = upd_tiles[i];
-  __syncthreads();
-  const int q0 = chain_off[blockIdx.x], q1 = chain_off[blockIdx.x + 1];
-  // wave w updates tiles w and w + 16 of the row's list; lane = (column c, row half h)
-  const int h = (t >> 5) & 1;
-  double pv[2][NB / 2];  // rows h*16 .. h*16+15 of the two update tiles, column c
-  double md;             // element t of M_kt (row-major), staged to LDS for the solve
-  auto prefetch = [&](int q) {
-    const int qq = min(q, q1 - 1), kt = chain_cols[qq];
-    const int e0 = s_uoff[qq], nu = s_uoff[qq + 1] - e0;
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      // waves whose tile is past the list skip the loads (wave-uniform branch); kept values are never read
-      if (__builtin_amdgcn_readfirstlane(wv + 16 * p) < nu) {
-        const int jt = s_ut[e0 + wv + 16 * p];
-        const double* src = L + ((int64_t)kt * NB + h * (NB / 2)) * ld + (int64_t)jt * NB + c;
-#pragma unroll
-        for (int i = 0; i < NB / 2; ++i) pv[p][i] = src[(int64_t)i * ld];
-      }
-    }
-    md = Minv[(int64_t)kt * NB * NB + t];
-  };
-#ifdef BS_TIMING
-  if (threadIdx.x == 0) g_bs_edges[blockIdx.x & 1][1] = clock64();
-#endif
-  prefetch(q0);
-  for (int q = q0; q < q1; ++q) {
-    const int kt = chain_cols[q];
-    const int64_t c0 = (int64_t)kt * NB;
-    BS_STAMP(0);
-    sM[t >> 5][t & 31] = md;
-    __syncthreads();  // M_kt staged; the previous column's updates of r visible
-    BS_STAMP(1);
-    if (t < WAVE) {  // x_kt = M^T r_kt: lane c sums column c of M against r (broadcast reads)
-      double s4[4] = {0, 0, 0, 0};
-#pragma unroll
-      for (int k = 0; k < NB; ++k) s4[k & 3] = fma(sM[k][c], xv[c0 + k], s4[k & 3]);
-      const double x = (s4[0] + s4[1]) + (s4[2] + s4[3]);
-      if (t < NB) {
-        xv[c0 + t] = x;
-        if (c0 + t < n) xout[c0 + t] = x;
-      }
-    }
-    BS_STAMP(2);
-    __syncthreads();  // x_kt visible
-    BS_STAMP(3);
-    const int e0 = s_uoff[q], nu = s_uoff[q + 1] - e0;
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      if (wv + 16 * p < nu) {  // wave-uniform
-        double s4[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int i = 0; i < NB / 2; ++i) s4[i & 3] = fma(pv[p][i], xv[c0 + h * (NB / 2) + i], s4[i & 3]);
-        double sacc = (s4[0] + s4[1]) + (s4[2] + s4[3]);
-        sacc += __shfl_xor(sacc, 32, WAVE);
-        if (h == 0) xv[(int64_t)s_ut[e0 + wv + 16 * p] * NB + c] -= sacc;
-      }
-    }
-    for (int uu = u + 32; uu < nu; uu += 32) {  // rare: rows with more than 32 update tiles
-      const int64_t jc = (int64_t)s_ut[e0 + uu] * NB + c;
-      double sacc = 0;
-#pragma unroll 8
-      for (int i = 0; i < NB; ++i) sacc += L[(c0 + i) * ld + jc] * xv[c0 + i];
-      xv[jc] -= sacc;
-    }
-    BS_STAMP(4);
-    prefetch(q + 1);  // next column's values in flight during its barrier and solve
-    BS_STAMP(5);
-  }
-#ifdef BS_TIMING
-  if (threadIdx.x == 0) g_bs_edges[blockIdx.x & 1][2] = clock64();
-#endif
-}
-// Back substitution with a lookahead chain wave (BS_LA, default).  Same data and result as
-// k_chol_backsolve, no workgroup barrier in the column loop:
+// Back substitution L^T x = y (y = row n of the factor, x written to xout[0..n)) with a lookahead chain wave, one
+// workgroup per chain of tile columns (nested dissection: C then A, C then B), no workgroup barrier in the column loop
+// (round 1's barrier-per-column form k_chol_backsolve was removed in round 6):
 //   * wave 0 walks the chain: x_kt = M_kt^T r_kt, publishes x (LDS counter xcnt), then at once forms the
 //     contribution of x_kt to the NEXT column's right-hand side (L_kt,next^T x_kt, in registers), so
 //     the next solve waits only for the older contributions;
@@ -1762,15 +1469,9 @@ void launch_chol_backsolve(const double* L, int64_t ld, int n, int n_chain, int 
                        ld, n, chain_off, chain_cols, lo_off, lo_tiles, Ldiag, Minv, xout);
     return;
   }
-#if BS_LA
   const size_t lds = (size_t)ld * sizeof(double) + (size_t)(2 * n_pos + n_tasks) * sizeof(int);
   hipLaunchKernelGGL(k_chol_backsolve_la, dim3(n_chain), dim3(64 * (BS_HELPERS + 1 + BS_LOADERS)), lds, st, L, ld, n, chain_off,
                      chain_cols, la_tasks, Ldiag, Minv, xout);
-#else
-  const size_t lds = (size_t)ld * sizeof(double) + (size_t)(n_pos + 1 + n_upd) * sizeof(int);
-  hipLaunchKernelGGL(k_chol_backsolve, dim3(n_chain), dim3(1024), lds, st, L, ld, n, chain_off, chain_cols, upd_off,
-                     upd_tiles, n_upd, Ldiag, Minv, xout);
-#endif
 }
 
 // packed exchange: the lower tiles the Schur kernel can write (xt[k] = (ti, tj)) and the three

@@ -260,12 +260,7 @@ void launch_cholesky(double* A, int64_t ld, const int4* tasks, const int* task_o
                      int* info, hipStream_t st, double* sgn = nullptr, const int4* tasks_host = nullptr,
                      double* Minv = nullptr,  // Minv: target of type-2 tasks (diagonal tile inverses)
                      int first_level = 0,     // levels [first_level, n_launch)
-                     bool delayed = false,    // tasks carry a second pair of update panels (api.hip make_plan)
-                     double* Lsub = nullptr); // plans with supercolumn tasks: L_k+1,k of each pair (chol_super)
-// single-launch form of levels [L0, L1) (SPD, single process): one workgroup per task taking its task by ticket,
-// per-level completion counters lvl_cnt and the ticket counter monotone over launches (epoch = launches so far over
-// the same level range); task_lvl[t] = level of task t, lvl_n[L] = tasks of level L; err: host-pinned flag set when
-// a wait gave up.
+                     bool delayed = false);   // tasks carry a second pair of update panels (api.hip make_plan)
 
 // la_tasks: lookahead back substitution's [lookahead tile per position | task offsets per (chain, helper) |
 // tasks q << 16 | tile], built by the host plan (api.hip make_plan)

@@ -85,11 +85,16 @@ def main():
                     help="gpu: rendered 1080p frames through the GPU front-end (SIFT, LK, RANSAC); "
                          "standin: StreamFrontEnd's ground-truth correspondences")
     ap.add_argument("--verbose", action="store_true")
-    ap.add_argument("--gc", choices=("default", "freeze"), default="freeze",
-                    help="freeze (default): gc.freeze() before the loop -- the ~10^5 objects of the imports (torch, scipy)"
-                         " leave the cyclic collector's generations, so its full collections in the loop take ~4 ms "
-                         "instead of 14-19 ms and stop landing as keyframe BA spikes (profiles/r05j_*); default: "
-                         "Python's own setting")
+    ap.add_argument("--gc", choices=("default", "freeze", "scheduled"), default="scheduled",
+                    help="freeze: gc.freeze() before the loop -- the ~10^5 objects of the imports (torch, scipy) leave the "
+                         "cyclic collector's generations, so its full collections in the loop take ~4 ms instead of "
+                         "14-19 ms (profiles/r05j_*); scheduled (default): freeze, and the full (generation-2) "
+                         "collections run between frames every --gc-every frames instead of wherever the allocation "
+                         "counters trip them -- with freeze alone one lands inside keyframe 51's detection in every run "
+                         "(r05j / BENCH_r05: detect 4.7-9.8 ms against ~1 ms); their time stays in the end-to-end wall; "
+                         "default: Python's own setting")
+    ap.add_argument("--gc-every", type=int, default=100,
+                    help="scheduled: frames between the full collections (freeze alone ran ~3 per 300 frames)")
     a = ap.parse_args()
     import gc
     gc_stats = {}  # generation -> [collections, total ms, max ms] during the loop (Python's cyclic collector)
@@ -122,16 +127,27 @@ def main():
         t_render = time.perf_counter() - t0
     slam = PtzSlam()
     slam.keyframe_map = Map("sift", max_ba_frame=a.window or None)
-    if a.gc == "freeze":
+    on_frame = None
+    gc_thresholds = gc.get_threshold()
+    if a.gc in ("freeze", "scheduled"):
         gc.collect()
         gc.freeze()
+    if a.gc == "scheduled":
+        # generations 0 / 1 stay automatic (sub-ms); generation 2 only where on_frame runs it: between frames, after the
+        # frame's tracking / keyframe timers, inside the end-to-end wall clock
+        gc.set_threshold(gc_thresholds[0], gc_thresholds[1], 1 << 30)
+
+        def on_frame(i, _slam):
+            if i % max(1, a.gc_every) == 0:
+                gc.collect(2)
     gc.callbacks.append(_gc_cb)
     quiet = contextlib.nullcontext() if a.verbose else contextlib.redirect_stdout(io.StringIO())
     t0 = time.perf_counter()
     with quiet:
-        rec = run_stream(slam, source, a.frames, scene.camera(0), keyframe_every=a.keyframe_every)
+        rec = run_stream(slam, source, a.frames, scene.camera(0), keyframe_every=a.keyframe_every, on_frame=on_frame)
     wall = time.perf_counter() - t0
     gc.callbacks.remove(_gc_cb)
+    gc.set_threshold(*gc_thresholds)
     est = np.asarray(rec["ptz"])
     err = est - scene.cams[:len(est)]
     tt = np.asarray(rec["t_track"][1:])
@@ -156,7 +172,8 @@ def main():
                                "tilt_deg": float(np.sqrt(np.mean(err[:, 1] ** 2))),
                                "f_px": float(np.sqrt(np.mean(err[:, 2] ** 2)))},
         "device": ptzba.lib().ptzba_version().decode(),
-        "gc": a.gc, "gc_pauses_ms": {str(g): {"count": v[0], "total": v[1], "max": v[2]} for g, v in sorted(gc_stats.items())},
+        "gc": a.gc + (f" (full collections every {a.gc_every} frames, between frames)" if a.gc == "scheduled" else ""),
+        "gc_pauses_ms": {str(g): {"count": v[0], "total": v[1], "max": v[2]} for g, v in sorted(gc_stats.items())},
     }
     kt = rec.get("kf_timing", [])[1:]
     if kt:  # where a keyframe's BA call spends its time (bundle_adjustment.LAST_RESULT["timing"], mean ms)

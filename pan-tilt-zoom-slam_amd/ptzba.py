@@ -118,6 +118,7 @@ def lib():
         "ptzba_solve_reduced": ([V], I),
         "ptzba_step": ([V, D], I),
         "ptzba_set_huber_curvature": ([V, D], I),
+        "ptzba_set_setup_front": ([V, I64], I),
         "ptzba_setup_timing": ([V, I32, V, V, V], I),
         "ptzba_solve": ([V, V, V, POINTER(ptzba_lm_opts), POINTER(ptzba_report)], I),
         "ptzba_solve_resident": ([V, I32, POINTER(ptzba_lm_opts), POINTER(ptzba_report)], I),
@@ -208,7 +209,7 @@ def lib():
 EXPORTED_SYMBOLS = [
     "ptzba_new", "ptzba_delete", "ptzba_last_error", "ptzba_version", "ptzba_set_stream", "ptzba_use_own_stream", "ptzba_set_problem",
     "ptzba_problem_info", "ptzba_solver_info", "ptzba_residual", "ptzba_set_state", "ptzba_get_state", "ptzba_linearize",
-    "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_set_huber_curvature", "ptzba_setup_timing", "ptzba_solve", "ptzba_solve_resident", "ptzba_read_scalars", "ptzba_accept",
+    "ptzba_build_reduced", "ptzba_solve_reduced", "ptzba_step", "ptzba_set_huber_curvature", "ptzba_set_setup_front", "ptzba_setup_timing", "ptzba_solve", "ptzba_solve_resident", "ptzba_read_scalars", "ptzba_accept",
     "ptzba_lm_start", "ptzba_lm_init", "ptzba_lm_build", "ptzba_lm_solve", "ptzba_lm_decide", "ptzba_lm_wait",
     "ptzba_exchange", "ptzba_exchange_packed", "ptzba_pack", "ptzba_unpack", "ptzba_sync", "ptzba_kernel_times", "ptzba_reset_kernel_times", "ptzba_comm_times", "ptzba_dist_form_estimate", "ptzba_save_state", "ptzba_restore_state", "ptz_ray_to_image",
     "ptz_image_to_ray", "ptz_project_rays", "ptz_back_project_rays", "ptz_h_jacobian", "ptzba_build_landmarks", "ptzba_coupling_window", "ptz_match_knn2", "ptz_homography_ransac", "ptz_homography_ransac_batch", "ptz_lk_track", "ptz_sift", "ptz_match_hamming",
@@ -1056,6 +1057,10 @@ class BAHandle:
                "ptzba_setup_timing")
         k = min(cap, n.value)
         return {names[i].decode(): float(ms[i]) for i in range(k)}
+
+    def set_setup_front(self, min_records):
+        """Device front of set_problem from `min_records` records on (0 always, -1 the default 4M; ptzba_set_setup_front)."""
+        _check(lib().ptzba_set_setup_front(self.h, int(min(min_records, 2 ** 62))), "ptzba_set_setup_front")
 
     def set_huber_curvature(self, hc):
         """Host-driven LM: the huber curvature weight (units of rho' beyond the unit) of later linearisations."""

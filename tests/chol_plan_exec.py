@@ -6,13 +6,9 @@ Task semantics (one int4 record, chol_kernels.hip):
   type 0  panel (i, k):  D = A_kk - sum_u L_k,p_u L_k,p_u^T;  T = A_ik - sum_{u in tmask} L_i,p_u L_k,p_u^T;
                          L_kk = chol(D) (i == k: to Ldiag, A_kk untouched), else A_ik <- T L_kk^-T
   type 1  trailing (i, j): A_ij -= sum_u L_i,p_u L_j,p_u^T
-  type 2  inverse of a diagonal factor tile (no effect on the factor); w bit 0: also copy a supercolumn's L_k+1,k
-          from Lsub into the factor (k = i)
+  type 2  inverse of a diagonal factor tile (no effect on the factor)
   type 3  2 x 2 trailing block: tiles (i + a, j + b) of the mask, each as type 1 with the block's panels
-  type 0 with w bit 30: supercolumn task (columns k = j and k + 1, chol_super): every panel to D00 = A_kk,
-          D10 = A_k+1,k, D11 = A_k+1,k+1 (and T0 = A_ik, T1 = A_i,k+1), L00 = chol(D00), L10 = D10 L00^-T,
-          L_i0 = T0 L00^-T, D11 -= L10 L10^T, T1 -= L_i0 L10^T, L11 = chol(D11), L_i1 = T1 L11^-T; the diagonal
-          task (i == k) writes L00, L11 to Ldiag and L10 to Lsub[k] (the raw tiles stay as they are for the level)
+(Round 4's supercolumn tasks and their continuation records were removed in round 6 with chol_super.)
 """
 import numpy as np
 
@@ -25,10 +21,6 @@ def decode(t):
     ups = [(w & 0x3FFF) - 1, ((w >> 14) & 0x3FFF) - 1, ((x >> 2) & 0x3FFF) - 1, ((x >> 16) & 0x3FFF) - 1]
     tmask = ((w >> 28) & 3) | ((x >> 30) << 2)
     return typ, y, z, ups, tmask
-
-
-def is_super(t):
-    return (int(t[0]) & 3) == 0 and (int(t[3]) >> 30) & 1 == 1  # (w bit 31: a continuation record follows)
 
 
 def test_matrix(pos, win, n_aug, ld, n_fixed=1, seed=0):
@@ -69,7 +61,6 @@ def replay(S, tasks, level_off):
 
 def assemble(A, Ldiag):
     T = A.shape[0] // NB
-    assert not Ldiag.get("sub"), "a supercolumn's L_k+1,k was never copied into the factor"
     Lf = np.zeros_like(A)
     for a in range(T):
         for b in range(a):
@@ -88,48 +79,12 @@ def replay_levels(A, Ldiag, tasks, level_off, L0, L1):
     def sym(a):
         return np.tril(a) + np.tril(a, -1).T
 
-    Lsub = Ldiag.setdefault("sub", {})
     for L in range(L0, L1):
         writes = []  # a level's results land after all its tasks read (the tasks of one launch run concurrently)
         for q in range(level_off[L], level_off[L + 1]):
             typ, i, j, ups, tmask = decode(tasks[q])
             if typ == 2:
-                if int(tasks[q][1]) >= 0 and int(tasks[q][3]) & 1:  # (i = -1: no-op / continuation record)
-                    writes.append(((i + 1, i), Lsub.pop(i)))
                 continue
-            if is_super(tasks[q]):
-                if (int(tasks[q][3]) >> 31) & 1:  # continuation record: panels 5..8
-                    z2, w2 = (int(v) & 0xFFFFFFFF for v in tasks[q + 1][2:4])
-                    ups = ups + [(z2 & 0xFFFF) - 1, (z2 >> 16) - 1, (w2 & 0xFFFF) - 1, (w2 >> 16) - 1]
-                k = j
-                D00, D10, D11 = sym(tile(k, k)), tile(k + 1, k).copy(), sym(tile(k + 1, k + 1))
-                T0 = tile(i, k).copy() if i != k else None
-                T1 = tile(i, k + 1).copy() if i != k else None
-                for p in ups:
-                    if p < 0:
-                        continue
-                    Bk, Bk1 = tile(k, p), tile(k + 1, p)
-                    D00 = D00 - Bk @ Bk.T
-                    D10 = D10 - Bk1 @ Bk.T
-                    D11 = D11 - Bk1 @ Bk1.T
-                    if T0 is not None:
-                        Bi = tile(i, p)
-                        T0 = T0 - Bi @ Bk.T
-                        T1 = T1 - Bi @ Bk1.T
-                L00 = np.linalg.cholesky(D00)
-                L10 = np.linalg.solve(L00, D10.T).T
-                L11 = np.linalg.cholesky(D11 - L10 @ L10.T)
-                if i == k:
-                    Ldiag[k], Ldiag[k + 1] = L00, L11
-                    Lsub[k] = L10
-                else:
-                    Li0 = np.linalg.solve(L00, T0.T).T
-                    writes.append(((i, k), Li0))
-                    writes.append(((i, k + 1), np.linalg.solve(L11, (T1 - Li0 @ L10.T).T).T))
-                continue
-            if typ == 1 and (int(tasks[q][3]) >> 31) & 1:  # continuation record: panels 5..8
-                z2, w2 = (int(v) & 0xFFFFFFFF for v in tasks[q + 1][2:4])
-                ups = ups + [(z2 & 0xFFFF) - 1, (z2 >> 16) - 1, (w2 & 0xFFFF) - 1, (w2 >> 16) - 1]
             if typ in (1, 3):
                 outs = [(i, j)] if typ == 1 else [(i + (m >> 1), j + (m & 1)) for m in range(4) if (tmask >> m) & 1]
                 for (ti, tj) in outs:

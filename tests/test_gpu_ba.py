@@ -700,3 +700,39 @@ def test_lm_opts_zero_filled_curvature_fields(gpu_available):
             h.close()
         assert out[0][:3] == out[1][:3], (loss, out[0][:3], out[1][:3])
         assert np.array_equal(out[0][3], out[1][3])
+
+
+@pytest.mark.parametrize("config,precision,weighted", [("config2", 0, False), ("config2", 1, False), ("config2", 1, True),
+                                                       ("config2", 0, True), ("config3", 1, False), ("config3", 0, True)])
+def test_device_and_host_setup_fronts_bitwise_equal(gpu_available, config, precision, weighted):
+    """set_problem's device front (rocPRIM sort, segment / record kernels; the default from 4M records) and
+    the host front (counting sorts) build the same arrays bit for bit.  ptzba_set_setup_front picks the front per
+    handle; the record-order residual (through the permutation), the LM iterates and the final state of 2 x 3 LM
+    iterations agree bitwise -- fp64 and fp32, weighted (dedup form) and unweighted records, config 2 and 3."""
+    import ptzba
+    import synthetic
+    p = synthetic.make_problem(config, seed=0)
+    frame, landmark, xy, w = p.frame, p.landmark, p.xy, None
+    if weighted:
+        frame, landmark, xy, w, _ = synthetic.dedup_records(frame, landmark, xy)
+    rng = np.random.default_rng(1)
+    x_full = np.concatenate([np.asarray(p.init_ptz).reshape(-1), np.asarray(p.init_rays).reshape(-1)])
+    x_full = x_full + rng.normal(0, 1e-3, x_full.shape)
+    out = []
+    for front in (2 ** 62, 0):  # host, device
+        h = ptzba.BAHandle(0)
+        h.set_setup_front(front)
+        h.set_problem(p.n_pose, p.n_landmark, frame, landmark, xy, p.u, p.v, weight=w, precision=precision,
+                      loss=ptzba.LOSS_HUBER, f_scale=1.0)
+        assert h.setup_timing()  # (phases recorded either way)
+        r = h.residual(x_full)
+        h.set_state(p.init_ptz, p.init_rays)
+        h.save_state()
+        rs = [h.solve_resident(restore=True, ftol=1e-12, xtol=1e-14, max_iter=3) for _ in range(2)]
+        out.append((r, h.get_state(), [(x.cost, x.njev, x.nfev, x.status) for x in rs], h.info()))
+        h.close()
+    (ra, sa, la, ia), (rb, sb, lb, ib) = out
+    assert ia == ib
+    assert np.array_equal(ra, rb)
+    assert la == lb
+    assert np.array_equal(sa[0], sb[0]) and np.array_equal(sa[1], sb[1])

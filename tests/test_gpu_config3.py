@@ -281,12 +281,12 @@ def test_config3_optimum_matches_oracle_fixture(gpu_available, config3, arith):
     assert abs(res.cost - ct) <= 1e-7 * ct
 
 
-@pytest.mark.parametrize("knob", ["PTZBA_BS_PERSIST=1", "PTZBA_CHOL_COH=1"])
+@pytest.mark.parametrize("knob", ["PTZBA_BS_PERSIST=1"])
 def test_config3_schedule_knobs_bitwise_equal(gpu_available, config3, monkeypatch, knob):
     """Schedule-only variants of the factorisation / back-substitution give bit-identical LM iterates at config 3 (the
     same arithmetic in the same order): PTZBA_BS_PERSIST=1 -- every back-substitution step in ONE launch with
-    per-column update counters (k_chol_backsolve_pst); PTZBA_CHOL_COH=1 -- the level launches with coherent
-    (L2-bypassing) tile traffic.  4 LM iterations in the headline arithmetic, twice (the persistent
+    per-column update counters (k_chol_backsolve_pst).  (Round 6 removed the PTZBA_CHOL_COH=0 plain-access knob: the
+    level launches' coherent tile traffic is the only SPD form.)  4 LM iterations in the headline arithmetic, twice (the persistent
     back-solve's counters advance by one epoch per launch)."""
     import ptzba
     p = config3

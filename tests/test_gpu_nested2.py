@@ -75,33 +75,3 @@ def test_two_level_order_lm_matches_one_level(gpu_available, wide, monkeypatch):
     assert abs(ra.cost - rb.cost) <= 1e-12 * ra.cost
     np.testing.assert_allclose(a[:, :2], b[:, :2], rtol=0, atol=1e-9)
     np.testing.assert_allclose(a[:, 2], b[:, 2], rtol=0, atol=1e-7)
-
-
-@pytest.mark.parametrize("depth", ["1", "2"])
-@pytest.mark.parametrize("backsolve", ["lookahead", "blk"])
-def test_supercolumn_gauss_newton_step_is_exact(gpu_available, wide, sparse_step, monkeypatch, depth, backsolve):
-    """Supercolumn plans (PTZBA_CHOL_SUPER=1: two consecutive chain columns per level, chol_kernels.hip chol_super,
-    incl. continuation records for more than four panels) under the one- and two-level orders: one undamped
-    Gauss-Newton step equals the oracle's sparse normal-equation solution."""
-    import ptzba
-    p = wide
-    monkeypatch.setenv("PTZBA_CHOL_SUPER", "1")
-    monkeypatch.setenv("PTZBA_ND_DEPTH", depth)
-    monkeypatch.setenv("PTZBA_BACKSOLVE", {"lookahead": "la", "blk": "blk"}[backsolve])
-    win = ptzba.frame_coupling_window(p.n_pose, p.frame, p.landmark)
-    _, tasks, _, _, _ = ptzba.plan_export(win, 1)
-    assert any((int(t[0]) & 3) == 0 and (int(t[3]) >> 30) & 1 for t in tasks)  # supercolumn tasks in the plan
-    h = ptzba.BAHandle(0)
-    h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=ptzba.FP64)
-    assert h.solver_info()["nd_depth"] == int(depth)
-    h.set_state(p.init_ptz, p.init_rays)
-    h.linearize()
-    h.build_reduced(0.0)
-    h.solve_reduced()
-    assert h.read_scalars()[5] == 0
-    h.accept(True)
-    ptz1, rays1 = h.get_state()
-    h.close()
-    dx_gpu = np.concatenate([(ptz1 - p.init_ptz)[1:].reshape(-1), (rays1 - p.init_rays).reshape(-1)])
-    err = np.abs(dx_gpu - sparse_step).max() / np.abs(sparse_step).max()
-    assert err < 1e-7, err

@@ -26,12 +26,10 @@ CASES = {
 
 @pytest.mark.parametrize("env", [{}, {"PTZBA_ND_DEPTH": "1"}, {"PTZBA_CHOL_DELAY": "2"},
                                  {"PTZBA_CHOL_DELAY": "2", "PTZBA_CHOL_BLOCKS": "0"},
-                                 {"PTZBA_CHOL_DELAY": "2", "PTZBA_ND_DEPTH": "1"},
-                                 {"PTZBA_CHOL_SUPER": "1"}, {"PTZBA_CHOL_SUPER": "1", "PTZBA_ND_DEPTH": "1"},
-                                 {"PTZBA_CHOL_SUPER": "1", "PTZBA_CHOL_DELAY": "2"}])
+                                 {"PTZBA_CHOL_DELAY": "2", "PTZBA_ND_DEPTH": "1"}])
 @pytest.mark.parametrize("case", sorted(CASES))
 def test_plan_replays_to_the_cholesky_factor(monkeypatch, case, env):
-    for k in ("PTZBA_ND_DEPTH", "PTZBA_CHOL_DELAY", "PTZBA_CHOL_BLOCKS", "PTZBA_CHOL_SUPER"):
+    for k in ("PTZBA_ND_DEPTH", "PTZBA_CHOL_DELAY", "PTZBA_CHOL_BLOCKS"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -46,8 +44,6 @@ def test_plan_replays_to_the_cholesky_factor(monkeypatch, case, env):
         assert ((tasks[:, 0] & 3) == 3).any()  # the delayed plan uses 2 x 2 trailing blocks
     if env.get("PTZBA_CHOL_BLOCKS") == "0":
         assert not ((tasks[:, 0] & 3) == 3).any()
-    if env.get("PTZBA_CHOL_SUPER") == "1":
-        assert any(cpe.is_super(t) for t in tasks)  # supercolumn tasks in use
 
 
 def _tree_problem(win0, seed=0):
