@@ -255,8 +255,9 @@ PTZBA_EXPORT int ptzba_solve_resident(ptzba_handle h, int restore, const ptzba_l
 PTZBA_EXPORT int ptzba_set_huber_curvature(ptzba_handle h, double hc);
 /* Which front builds the record arrays in the following ptzba_set_problem calls of this handle (round 6): the device
  * front (one rocPRIM radix sort + segment / record kernels) from min_records records on, the host's counting sorts
- * below.  0: always the device, INT64_MAX: never, -1: the default (4M records: configs 3 and 4 on the device, a
- * sliding window's ~170K records on the host).  Both fronts produce the same arrays bit for bit. */
+ * below.  0: always the device, INT64_MAX: never, -1: the default (64K records since round 6, 4M before: configs 3 and 4
+ * and a sliding window's ~170K records on the device, the small drop-in problems on the host).  Both fronts produce the
+ * same arrays bit for bit. */
 PTZBA_EXPORT int ptzba_set_setup_front(ptzba_handle h, int64_t min_records);
 PTZBA_EXPORT int ptzba_step(ptzba_handle h, double lambda);
 PTZBA_EXPORT int ptzba_read_scalars(ptzba_handle h, double* out /*PTZBA_NSCALARS*/);

@@ -1337,7 +1337,9 @@ static bool dist_order(int n_pose, int nf, const std::vector<int32_t>& win, int 
 // segments and device record arrays (rec_seg, seg_frame / seg_lm / seg_rec_begin, seg_base, rec_xy / rec_w, rec_key,
 // perm), bit for bit what the host path uploads; returns the per-segment arrays the host passes read (seg_rec_begin
 // with the end entry)
-constexpr int64_t GPU_SETUP_MIN_REC = (int64_t)1 << 22;  // 4M records (config 3: 14.6M; a 30-KF window: ~170K)
+// From 64K records on (round 6; 4M before): a 30-keyframe window's ~170K records take 1.3 ms on the device front against
+// 2.2 ms on the host (set_problem per keyframe, config 5: keyframe BA 8.7-9.2 -> 7.9-8.1 ms mean, profiles/r06f_*)
+constexpr int64_t GPU_SETUP_MIN_REC = (int64_t)1 << 16;
 static int gpu_front(ptzba_ctx* h, int64_t n, int n_pose, int n_lm, const int32_t* frame, const int32_t* lm,
                      const double* xy, const double* w, std::vector<int32_t>& seg_frame, std::vector<int32_t>& seg_lm,
                      std::vector<int64_t>& seg_rec_begin) {
@@ -3418,7 +3420,7 @@ int ptzba_set_huber_curvature(ptzba_handle h, double hc) {
 }
 
 // which front the following set_problem calls use (round 6): the device front from min_records records on
-// (0: always, INT64_MAX: never, -1: the default GPU_SETUP_MIN_REC = 4M).  Both fronts build the same arrays bit for bit
+// (0: always, INT64_MAX: never, -1: the default GPU_SETUP_MIN_REC = 64K).  Both fronts build the same arrays bit for bit
 // (tests/test_gpu_ba.py compares them); the knob is the test hook and a per-handle tuning point.
 int ptzba_set_setup_front(ptzba_handle h, int64_t min_records) {
   if (!h) return fail("null handle");

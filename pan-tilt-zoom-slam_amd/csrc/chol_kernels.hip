@@ -221,12 +221,6 @@ __device__ long long g_cs_rt[64][4];
 #ifndef LA_BW
 #define LA_BW 4  // pivot block of the lookahead form
 #endif
-#ifndef CHOL_SPEC
-#define CHOL_SPEC 0  // pivot sweep: 1 speculative row reads + deferred publication (round 6 A/B: slower, r06c), 0 round 5's
-#endif
-#ifndef CHOL_FFH
-#define CHOL_FFH 0  // SPD pivot sweep: 1 fraction-free 4 x 4 blocks with the lane's row folded in (round 6 A/B)
-#endif
 // reciprocal square root by a series step on the hardware estimate: e = 1 - d y0^2 (|e| ~ 5e-8),
 // y = y0 (1 + e/2 + 3e^2/8) -- full double precision in 4 dependent operations (rsq_nr: 6)
 __device__ __forceinline__ double rsq_fast(double d) {
@@ -276,13 +270,6 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
   int* nl = flags;
   int* nu = flags + 1;  // [NS]
   if (threadIdx.x <= NS) flags[threadIdx.x] = 0;
-#if CHOL_FFH
-  __shared__ double s_g[NB];  // FFH: power-of-two column scales of the tile's entry diagonal
-  if (!SG && threadIdx.x < NB) {
-    const double d = D[threadIdx.x][threadIdx.x];
-    s_g[threadIdx.x] = d > 0.0 ? ldexp(1.0, -(ilogb(d) >> 1)) : 1.0;
-  }
-#endif
   __syncthreads();
 #ifdef CS_TIMING
   long long* wst = g_cs_wg[g_cs_level < 64 ? g_cs_level : 63];
@@ -312,36 +299,12 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
           for (int k = 0; k < BW; ++k) pl[j][k] = Lb[s - 1][kb + j][k];
       }
       double a[BW];
-#if CHOL_SPEC
-      // the row reads go out right behind the helper counter's and are re-issued only if it was short (the helpers
-      // run ~1,000-1,500 ticks ahead, profiles/r06a_sweep.json): one LDS round trip instead of two.  A wave's LDS
-      // operations execute in order, so reads issued after the counter's see every helper store it counted.
-      {
-        int v = 3;
-        do {
-          if (s >= 2) v = __hip_atomic_load(&nu[s - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          asm volatile("" ::: "memory");
-#pragma unroll
-          for (int j = 0; j < BW; ++j) a[j] = row[kb + j];
-          asm volatile("" ::: "memory");
-        } while (__builtin_expect(v < 3, 0));
-      }
-      CSB(s, 2);
-      if (s >= 1 && s + 1 < NS) {
-        // block s - 1's publication (helpers wait for nl >= t before stage t), deferred to here: the reads above were
-        // issued after that block's factor stores (and, SG, its signs) and have returned, so those stores are
-        // complete -- ordered by completion without a wait of its own
-        asm volatile("" ::"v"(a[0]) : "memory");
-        if (lane == 0) __hip_atomic_store(nl, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-#else
       if (s >= 2) {
         while (lds_poll(&nu[s - 1]) < 3) __builtin_amdgcn_s_sleep(0);
       }
       CSB(s, 2);
 #pragma unroll
       for (int j = 0; j < BW; ++j) a[j] = row[kb + j];
-#endif
       CSB(s, 3);
       if (s > 0) {
 #pragma unroll
@@ -368,46 +331,6 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
       }
 #endif
       CSB(s, 4);
-#if CHOL_FFH
-      if constexpr (!SG) {
-        // fraction-free 4 x 4 block (Gauss without divisions: q_im <- Q_j q_im - q_ij q_mj, Q_j = q_jj), the lane's
-        // row riding along as a fifth row, so a pivot costs one multiply + one FMA on the chain and the four
-        // reciprocal square roots come last, independent: L_rj = t_rj / sqrt(Q_0 ... Q_j).  Columns pre-scaled by
-        // exact powers of two g_j of the tile's entry diagonal (g_j^2 A_jj in [1, 4)) bound the products' growth.
-        double g[BW], t[BW], Q[BW];
-#pragma unroll
-        for (int j = 0; j < BW; ++j) g[j] = s_g[kb + j];
-#pragma unroll
-        for (int j = 0; j < BW; ++j) t[j] = a[j] * g[j];
-#pragma unroll
-        for (int i = 0; i < BW; ++i)
-#pragma unroll
-          for (int j = 0; j <= i; ++j) P[i][j] *= g[i] * g[j];
-#pragma unroll
-        for (int j = 0; j < BW; ++j) {
-          double q = P[j][j];
-          if (!(q > 0.0)) {
-            bad = true;
-            q = 1.0;
-          }
-          Q[j] = q;
-#pragma unroll
-          for (int i = j + 1; i < BW; ++i)
-#pragma unroll
-            for (int m = j + 1; m <= i; ++m) P[i][m] = fma(-P[i][j], P[m][j], q * P[i][m]);
-#pragma unroll
-          for (int m = j + 1; m < BW; ++m) t[m] = fma(-t[j], P[m][j], q * t[m]);
-        }
-        double pr = Q[0];
-#pragma unroll
-        for (int j = 0; j < BW; ++j) {
-          if (j > 0) pr *= Q[j];
-          lp[j] = t[j] * rsq_fast(pr);  // L_rj
-        }
-#pragma unroll
-        for (int j = 0; j < BW; ++j) sg[j] = 1.0;
-      } else
-#endif
       {
 #pragma unroll
       for (int j = 0; j < BW; ++j) {
@@ -461,7 +384,7 @@ __device__ __forceinline__ void wg_potrf_trsm32_df(double (*D)[NB + 1], double (
           for (int j = 0; j < BW; ++j) sig[kb + j] = sg[j];
         }
       }
-      if (!CHOL_SPEC && s + 2 < NS) {
+      if (s + 2 < NS) {
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) __hip_atomic_store(nl, s + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);

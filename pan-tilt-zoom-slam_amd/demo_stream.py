@@ -95,6 +95,9 @@ def main():
                          "default: Python's own setting")
     ap.add_argument("--gc-every", type=int, default=100,
                     help="scheduled: frames between the full collections (freeze alone ran ~3 per 300 frames)")
+    ap.add_argument("--setup-front", type=int, default=None,
+                    help="records from which the keyframe BA's set_problem builds on the device (ptzba.SETUP_FRONT_MIN; "
+                         "default: the library's 64K, i.e. the device front for a window's ~170K records; 4194304 restores round 5)")
     a = ap.parse_args()
     import gc
     gc_stats = {}  # generation -> [collections, total ms, max ms] during the loop (Python's cyclic collector)
@@ -112,6 +115,8 @@ def main():
     import ptzba
     import synthetic
     from ptz_slam import PtzSlam
+    if a.setup_front is not None:
+        ptzba.SETUP_FRONT_MIN = a.setup_front
     from scene_map import Map
     scene = synthetic.StreamScene(a.frames, seed=a.seed, pan_lo=-a.pan_range / 2, pan_hi=a.pan_range / 2)
     t_render = 0.0

@@ -828,7 +828,8 @@ def torch_exchange_hook(h, dist, device):
     def hook(kind, ptr, count, stream):
         r0, nr = h.exchange_group(kind)
         t = torch.as_tensor(DevArray(ptr, count), device=device)
-        dist.all_reduce(t, group=None if nr == world else groups[(r0, nr)])
+        # (a replicated-form handle -- no dist_world -- reports a group of <= 1 rank: its exchanges sum over all ranks)
+        dist.all_reduce(t, group=None if (nr <= 1 or nr == world) else groups[(r0, nr)])
 
     return hook
 
@@ -1059,7 +1060,7 @@ class BAHandle:
         return {names[i].decode(): float(ms[i]) for i in range(k)}
 
     def set_setup_front(self, min_records):
-        """Device front of set_problem from `min_records` records on (0 always, -1 the default 4M; ptzba_set_setup_front)."""
+        """Device front of set_problem from `min_records` records on (0 always, -1 the library default, 64K; ptzba_set_setup_front)."""
         _check(lib().ptzba_set_setup_front(self.h, int(min(min_records, 2 ** 62))), "ptzba_set_setup_front")
 
     def set_huber_curvature(self, hc):
@@ -1354,6 +1355,11 @@ class LMSolver:
             if k + 1 < limit:
                 build()  # next trial's build queued behind this decision (harmless after the last one)
             rec = h.lm_wait(k)
+            if k == 0 and not np.isfinite(rec.initial_cost):
+                # scipy least_squares' own check (least_squares.py: "Residuals are not finite in the initial point"):
+                # a drop-in must not report a damping-limit stop for a problem it could never evaluate
+                h.sync()
+                raise ValueError("Residuals are not finite in the initial point.")
             k += 1
             if rec.done or k >= limit:
                 break
@@ -1378,6 +1384,8 @@ class LMSolver:
         h.linearize()
         s = self._scalars()
         cost = s[0]
+        if not np.isfinite(cost):
+            raise ValueError("Residuals are not finite in the initial point.")  # (scipy least_squares' check)
         initial_cost = cost
         lam = self.lambda0
         nu = 2.0
@@ -1494,6 +1502,11 @@ def warm_up(device=0, precision=FP64):
               max_iter=5)
 
 
+# solve()'s shared handles: records from which set_problem builds on the device (ptzba_set_setup_front; None: the
+# library's default, 64K records -- a sliding window's ~170K records build on the device)
+SETUP_FRONT_MIN = None
+
+
 def solve(n_pose, n_landmark, frame, landmark, xy, u, v, init_ptz, init_rays, weight=None, precision=FP64,
           loss=LOSS_LINEAR, f_scale=1.0, device=0, keep_handle=True, **lm_kw):
     """Convenience one-shot solve.  Returns (ptz [N,3], rays [M,2], LMResult).  keep_handle=True (default): one
@@ -1516,6 +1529,8 @@ def solve(n_pose, n_landmark, frame, landmark, xy, u, v, init_ptz, init_rays, we
         h = _solve_handles.get(device)
         if h is None or h.h is None:
             h = _solve_handles[device] = BAHandle(device)
+        if SETUP_FRONT_MIN is not None:
+            h.set_setup_front(SETUP_FRONT_MIN)
         try:
             t0 = time.perf_counter()
             h.set_problem(n_pose, n_landmark, frame, landmark, xy, u, v, weight=weight, precision=precision, loss=loss,
@@ -1527,6 +1542,8 @@ def solve(n_pose, n_landmark, frame, landmark, xy, u, v, init_ptz, init_rays, we
             t3 = time.perf_counter()
             ptz, rays = h.get_state()
             LAST_SOLVE_TIMING.clear()
+            for k, v in h.setup_timing().items():  # set_problem's host phases, ms -> s (keyframe BA breakdowns)
+                LAST_SOLVE_TIMING["setup_" + k.replace("+", "_").replace(" ", "_") + "_s"] = v * 1e-3
             LAST_SOLVE_TIMING.update(set_problem_s=t1 - t0, lm_s=time.perf_counter() - t1, lm_set_state_s=t2 - t1,
                                      lm_run_s=t3 - t2, lm_get_state_s=time.perf_counter() - t3)
             return ptz, rays, res

@@ -705,7 +705,7 @@ def test_lm_opts_zero_filled_curvature_fields(gpu_available):
 @pytest.mark.parametrize("config,precision,weighted", [("config2", 0, False), ("config2", 1, False), ("config2", 1, True),
                                                        ("config2", 0, True), ("config3", 1, False), ("config3", 0, True)])
 def test_device_and_host_setup_fronts_bitwise_equal(gpu_available, config, precision, weighted):
-    """set_problem's device front (rocPRIM sort, segment / record kernels; the default from 4M records) and
+    """set_problem's device front (rocPRIM sort, segment / record kernels; the default from 64K records) and
     the host front (counting sorts) build the same arrays bit for bit.  ptzba_set_setup_front picks the front per
     handle; the record-order residual (through the permutation), the LM iterates and the final state of 2 x 3 LM
     iterations agree bitwise -- fp64 and fp32, weighted (dedup form) and unweighted records, config 2 and 3."""
@@ -736,3 +736,50 @@ def test_device_and_host_setup_fronts_bitwise_equal(gpu_available, config, preci
     assert np.array_equal(ra, rb)
     assert la == lb
     assert np.array_equal(sa[0], sb[0]) and np.array_equal(sa[1], sb[1])
+
+
+@pytest.mark.parametrize("config", ["config1", "config2"])
+@pytest.mark.parametrize("precision", [0, 1])
+@pytest.mark.parametrize("loss", [0, 1])
+def test_initial_cost_is_finite_and_matches_oracle(gpu_available, config, precision, loss):
+    """a round-5 working-tree build of K1 (never committed) produced a NaN cost at x0
+    in fp32 (config 2, linear loss: initial_cost=nan, njev=0, reported as a damping-limit stop).  Every precision x loss
+    combination's x0 linearisation must give the oracle's cost (fp64 1e-10, fp32 2e-6 relative), and the LM must hand
+    back the same initial cost."""
+    import ptzba
+    import synthetic
+    from oracle import ptz_oracle as orc
+    p = synthetic.make_problem(config, seed=0)
+    x_full = np.concatenate([np.asarray(p.init_ptz).reshape(-1), np.asarray(p.init_rays).reshape(-1)])
+    want = orc.ba_cost(x_full, p.n_pose, p.u, p.v, p.frame.astype(np.int64), p.landmark.astype(np.int64), p.xy,
+                       loss="huber" if loss else "linear", f_scale=1.0)
+    h = ptzba.BAHandle(0)
+    h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=precision, loss=loss, f_scale=1.0)
+    h.set_state(p.init_ptz, p.init_rays)
+    h.linearize()
+    got = float(h.read_scalars()[0])
+    tol = 1e-10 if precision == 0 else 2e-6
+    assert np.isfinite(got) and abs(got - want) <= tol * want, (got, want)
+    h.set_state(p.init_ptz, p.init_rays)
+    res = ptzba.LMSolver(h, ftol=1e-4, xtol=1e-8, max_iter=5).run()
+    assert np.isfinite(res.initial_cost) and abs(res.initial_cost - want) <= tol * want
+    assert res.njev >= 1 and res.status in (0, 2, 3)
+    h.close()
+
+
+@pytest.mark.parametrize("device_loop", [True, False])
+def test_non_finite_initial_residual_raises_like_scipy(gpu_available, device_loop):
+    """A non-finite x0 (here one ray's theta) makes the residual non-finite: scipy's least_squares raises
+    ValueError("Residuals are not finite in the initial point."); the drop-in LM raises the same instead of reporting a
+    damping-limit stop.  (Non-finite observations are already refused by set_problem.)"""
+    import ptzba
+    import synthetic
+    p = synthetic.make_problem("config1", seed=0)
+    rays = np.array(p.init_rays, np.float64)
+    rays[int(p.landmark[7]), 0] = np.nan
+    h = ptzba.BAHandle(0)
+    h.set_problem(p.n_pose, p.n_landmark, p.frame, p.landmark, p.xy, p.u, p.v, precision=1)
+    h.set_state(p.init_ptz, rays)
+    with pytest.raises(ValueError, match="not finite in the initial point"):
+        ptzba.LMSolver(h, ftol=1e-4, device_loop=device_loop).run()
+    h.close()

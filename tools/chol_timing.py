@@ -81,13 +81,19 @@ for k, v in acc.items():
 # level timeline (ns, one clock for all XCDs): block 0's task start -> sweep end -> its stores complete; the level's
 # last panel task done; the next level's block-0 start
 r = rt[:, nz]
-tl = {"start_to_sweep_end_ns": float((r[:, :, 1] - r[:, :, 0]).mean()),
-      "sweep_end_to_stores_done_ns": float((r[:, :, 2] - r[:, :, 1]).mean()),
-      "block0_stores_done_to_last_task_done_ns": float((r[:, :, 3] - r[:, :, 2]).mean()),
-      "last_task_done_to_next_level_start_ns": float((r[:, 1:, 0] - r[:, :-1, 3]).mean()),
-      "level_start_to_next_start_ns": float((r[:, 1:, 0] - r[:, :-1, 0]).mean())}
+# (a level whose block 0 is an inverse or trailing task records no panel stamps: only levels with all three stamps, and
+# pairs of consecutive such levels for the gap)
+ok = (r[:, :, 0] > 0) & (r[:, :, 1] > 0) & (r[:, :, 2] > 0)
+okp = ok[:, :-1] & ok[:, 1:] & (r[:, :-1, 3] > 0)
+sel = lambda a, m: float(a[m].mean()) if m.any() else None  # noqa: E731
+tl = {"start_to_sweep_end_ns": sel(r[:, :, 1] - r[:, :, 0], ok),
+      "sweep_end_to_stores_done_ns": sel(r[:, :, 2] - r[:, :, 1], ok),
+      "block0_stores_done_to_last_task_done_ns": sel(r[:, :, 3] - r[:, :, 2], ok & (r[:, :, 3] > 0)),
+      "last_task_done_to_next_level_start_ns": sel(r[:, 1:, 0] - r[:, :-1, 3], okp),
+      "level_start_to_next_start_ns": sel(r[:, 1:, 0] - r[:, :-1, 0], okp),
+      "levels_with_panel_block0": int(ok[0].sum())}
 out["level_timeline"] = tl
-print("level timeline (ns):", {k: round(v) for k, v in tl.items()})
+print("level timeline (ns):", {k: (round(v) if v is not None else None) for k, v in tl.items()})
 js = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
 if js:
     json.dump(out, open(js, "w"), indent=1)

@@ -8,6 +8,7 @@
 #   ab      short bench of every libptzba_NAME.so in $AB_LIBS against the default, alternating twice
 #   dist    world-N gloo rehearsal of bench.py on one device (N in $DIST_N, default "2 8")
 #   full    the default bench.py line (what the driver runs)
+#   stream  demo_stream.py (config 5) with each argument set of $STREAM_ARGS (';'-separated), 300 frames
 set -o pipefail
 TAG=${TAG:-r06}
 CFG=${CFG:-config3}
@@ -43,6 +44,14 @@ for st in $STEPS; do
     for n in ${DIST_N:-2 8}; do
       PTZBA_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus $n --config $CFG --steps 20 --warmup 3 --no-cpu-baseline --no-accuracy --stream-frames 0 --no-cold ${DIST_ARGS} > gpurun_out/${TAG}_dist$n.json 2> gpurun_out/${TAG}_dist$n.err || { echo DISTFAIL $n; tail -20 gpurun_out/${TAG}_dist$n.err; exit 1; }
       python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('world', d['n_gpus'], 'it/s', round(d['value'],1), d['config']['parallelism'], json.dumps(d.get('collective_fit')), json.dumps([{k: r[k] for k in ('rank','kernel_ms','collective_ms_per_iteration','n_collectives_per_iteration','factorisation_ms_net')} for r in d.get('per_rank') or []])[:1500])" gpurun_out/${TAG}_dist$n.json
+    done ;;
+  stream)
+    IFS=';' read -ra SA <<< "${STREAM_ARGS:- }"
+    k=0
+    for args in "${SA[@]}"; do
+      k=$((k + 1))
+      timeout -k 10 300 python pan-tilt-zoom-slam_amd/demo_stream.py --frames 300 --window 30 $args > gpurun_out/${TAG}_stream$k.json 2> gpurun_out/${TAG}_stream$k.err || { echo STREAMFAIL; tail gpurun_out/${TAG}_stream$k.err; exit 1; }
+      python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], 'fps', round(d['fps_end_to_end'],1), 'kf', {k: round(v,2) for k,v in d['keyframe_ba_ms'].items()}, 'set_problem', round(d['keyframe_ba_breakdown_ms'].get('solve_set_problem_s',0),2), {k: round(v,3) for k,v in d['keyframe_ba_breakdown_ms'].items() if k.startswith('solve_setup_')})" gpurun_out/${TAG}_stream$k.json "[$args]"
     done ;;
   full)
     timeout -k 10 900 python bench.py ${FULL_ARGS} > gpurun_out/${TAG}_full.json 2> gpurun_out/${TAG}_full.err || { echo FULLFAIL; tail gpurun_out/${TAG}_full.err; exit 1; }
