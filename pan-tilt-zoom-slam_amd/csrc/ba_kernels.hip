@@ -76,6 +76,9 @@ void launch_tables(const double* ptz, const double* rays, int n_pose, int n_lm, 
 // K1: linearize (residual + Jacobian + per-segment / per-landmark normal-equation blocks + cost)
 // ------------------------------------------------------------------------------------------------
 constexpr int SEGW = K1_SEGW;  // segments per LDS window per wave
+#ifndef K1_BF
+#define K1_BF 1  // phase B: branch-free record validity and unconditional projection reads (round 6; 0: round 5's form)
+#endif
 // (Round 5 removed the measured-slower build variants: one record per lane (K1_COARSE 0), three record groups in
 // flight (K1_DEPTH 3), LDS-atomic tail runs, issue-order tails and phase C's own table loads (K1_FTV_LATE))
 #ifndef K1_WPB
@@ -118,6 +121,26 @@ __device__ __forceinline__ T wave_total(T v) {
   v += dpp_r<DPP_ROW_BCAST15, 0xa>(v);
   v += dpp_r<DPP_ROW_BCAST31, 0xc>(v);
   return v;
+}
+
+// Six wave totals at once, step by step across the values (round 6): each DPP step's six reads of the previous step's
+// results are independent, so the DPP read-after-write wait states of one value are covered by the others' work
+// instead of s_nop padding (six back-to-back wave_total calls serialised).  Same additions, same order per value.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void wave_total_step6(double (&v)[6]) {
+  double t[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) t[k] = dpp_r<CTRL, ROWMASK>(v[k]);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) v[k] += t[k];
+}
+__device__ __forceinline__ void wave_total6(double (&v)[6]) {
+  wave_total_step6<DPP_ROW_SHR1, 0xf>(v);
+  wave_total_step6<DPP_ROW_SHR2, 0xf>(v);
+  wave_total_step6<DPP_ROW_SHR4, 0xf>(v);
+  wave_total_step6<DPP_ROW_SHR8, 0xf>(v);
+  wave_total_step6<DPP_ROW_BCAST15, 0xa>(v);
+  wave_total_step6<DPP_ROW_BCAST31, 0xc>(v);
 }
 
 // one Kogge-Stone step of the segmented inclusive scan (keys sorted within the wave; kenc >= 1)
@@ -261,8 +284,29 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
     int key[4];
     real v[4][4];
     real cb = 0;  // the batch's cost terms, summed in the record precision, then added in fp64
+#if K1_BF
+    // branch-free (round 6): the validity test on a 32-bit offset from r0, and the four records' projection reads
+    // issued unconditionally (key clamped into the window; an invalid record's values are masked below), so one LDS
+    // wait serves the lane's four records instead of one exec-masked branch with its own wait per record
+    const int rel0 = (int)(rb - r0) + 4 * lane, nrec = (int)(r1 - r0);
+    real px[4], py[4];
+    bool vld[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
+      const int kb = (int)((g.key4 >> (8 * j)) & 0xffu);
+      vld[j] = (unsigned)(rel0 + j) < (unsigned)nrec;
+      key[j] = vld[j] ? kb : (rel0 + j < 0 ? -1 : 255);
+      px[j] = sx[kb & (SEGW - 1)];
+      py[j] = sy[kb & (SEGW - 1)];
+    }
+#endif
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#if K1_BF
+      const bool valid = vld[j];
+      const real rx = valid ? px[j] - g.ox[j] : (real)0;
+      const real ry = valid ? py[j] - g.oy[j] : (real)0;
+#else
       const int64_t idx = rb + 4 * lane + j;
       const bool valid = idx >= r0 && idx < r1;
       key[j] = valid ? (int)((g.key4 >> (8 * j)) & 0xffu) : (idx < r0 ? -1 : 255);
@@ -271,6 +315,7 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
         rx = sx[key[j]] - g.ox[j];
         ry = sy[key[j]] - g.oy[j];
       }
+#endif
       const real wt = valid ? g.wt[j] : (real)0;
       real wx, wy, c, hx, hy;
       if constexpr (LOSS == 0) {
@@ -433,8 +478,9 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
     K1_ACC(2, kt2, kt3);
     kt0 = kt3;
   }
-  V00 = wave_total(V00); V01 = wave_total(V01); V11 = wave_total(V11);
-  g0 = wave_total(g0); g1 = wave_total(g1); cost = wave_total(cost);
+  double tot[6] = {V00, V01, V11, g0, g1, cost};
+  wave_total6(tot);
+  V00 = tot[0]; V01 = tot[1]; V11 = tot[2]; g0 = tot[3]; g1 = tot[4]; cost = tot[5];
   if (lane == WAVE - 1) {
     double* o = (alt ? a.lm_out1 : a.lm_out) + (int64_t)l * 8;
     o[0] = V00; o[1] = V01; o[2] = V11; o[3] = g0; o[4] = g1; o[5] = 0.5 * cost; o[6] = 0; o[7] = 0;
