@@ -409,8 +409,8 @@ static int upload_records(ptzba_ctx* h, const std::vector<int64_t>& order, const
   // handle's stream first (the stream does not order itself behind the legacy null stream, so every upload /
   // memset of set_problem goes on h->st)
   const size_t nxy = 2 * (size_t)h->n_rec, nw = w ? (size_t)h->n_rec : 0;
-  // allocate everything before queuing any copy; padded by 4 records: K1's coarsened loads read whole groups
-  if (h->rec_xy.alloc((nxy + 8) * sizeof(real))) return -1;
+  // allocate everything before queuing any copy; padded by 8 records: K1's coarsened loads read whole groups
+  if (h->rec_xy.alloc((nxy + 16) * sizeof(real))) return -1;
   if (w) {
     if (h->rec_w.alloc(nw * sizeof(real))) return -1;
   } else {
@@ -443,10 +443,10 @@ static int upload_records(ptzba_ctx* h, const std::vector<int64_t>& order, const
   if (staged && h->stage_batch) {  // queued with set_problem's other staged uploads
     h->stage_ops.push_back({h->rec_xy.p, (size_t)(pxy - h->stage), nxy * sizeof(real)});
     if (w) h->stage_ops.push_back({h->rec_w.p, (size_t)(pw - h->stage), nw * sizeof(real)});
-    return zero_async(h, reinterpret_cast<real*>(h->rec_xy.p) + nxy, 8 * sizeof(real));
+    return zero_async(h, reinterpret_cast<real*>(h->rec_xy.p) + nxy, 16 * sizeof(real));
   }
   HIPCHK(hipMemcpyAsync(h->rec_xy.p, xy, nxy * sizeof(real), hipMemcpyHostToDevice, h->st));
-  HIPCHK(hipMemsetAsync(reinterpret_cast<real*>(h->rec_xy.p) + nxy, 0, 8 * sizeof(real), h->st));
+  HIPCHK(hipMemsetAsync(reinterpret_cast<real*>(h->rec_xy.p) + nxy, 0, 16 * sizeof(real), h->st));
   if (w) HIPCHK(hipMemcpyAsync(h->rec_w.p, ww, nw * sizeof(real), hipMemcpyHostToDevice, h->st));
   return 0;
 }
@@ -1375,7 +1375,7 @@ static int gpu_front(ptzba_ctx* h, int64_t n, int n_pose, int n_lm, const int32_
   const size_t e = h->elem();
   DBuf d_xy, d_w;
   if (d_xy.alloc(16 * (size_t)n) || (w && d_w.alloc(8 * (size_t)n)) || h->seg_base.alloc(16 * (size_t)ns) ||
-      h->rec_xy.alloc((2 * (size_t)n + 8) * e) || h->rec_key.alloc((size_t)n + 4) || h->perm.alloc(8 * (size_t)n))
+      h->rec_xy.alloc((2 * (size_t)n + 16) * e) || h->rec_key.alloc((size_t)n + 8) || h->perm.alloc(8 * (size_t)n))
     return -1;
   if (w) {
     if (h->rec_w.alloc((size_t)n * e)) return -1;
@@ -1396,8 +1396,8 @@ static int gpu_front(ptzba_ctx* h, int64_t n, int n_pose, int n_lm, const int32_
                                              h->rec_xy.as<double>(), w ? h->rec_w.as<double>() : nullptr,
                                              h->rec_key.as<uint8_t>(), h->perm.as<int64_t>());
   if (rc) return rc;
-  HIPCHK(hipMemsetAsync(h->rec_xy.as<uint8_t>() + 2 * (size_t)n * e, 0, 8 * e, h->st));  // K1's padded record groups
-  HIPCHK(hipMemsetAsync(h->rec_key.as<uint8_t>() + n, 0, 4, h->st));
+  HIPCHK(hipMemsetAsync(h->rec_xy.as<uint8_t>() + 2 * (size_t)n * e, 0, 16 * e, h->st));  // K1's padded record groups
+  HIPCHK(hipMemsetAsync(h->rec_key.as<uint8_t>() + n, 0, 8, h->st));
   HIPCHK(hipStreamSynchronize(h->st));  // the temporaries and the host vectors' copies above complete here
   return 0;
 }
@@ -1894,7 +1894,7 @@ int ptzba_set_problem(ptzba_handle h, int32_t n_pose, int32_t n_landmark, int64_
     if (rc) return rc;
     if (upload_st(h, h->seg_base, seg_base)) return -1;
     {  // K1's 1-byte segment key: the record's segment within its landmark's window of K1_SEGW segments
-      std::vector<uint8_t> key(n_obs + 4);  // + 4: K1 reads whole 4-record key groups
+      std::vector<uint8_t> key(n_obs + 8);  // + 8: K1 reads whole 8-record key groups
       for (int64_t k = 0; k < n_obs; ++k) {
         const int32_t sg = rec_seg[k];
         key[k] = (uint8_t)((sg - lm_seg_begin[seg_lm[sg]]) % K1_SEGW);

@@ -76,8 +76,8 @@ void launch_tables(const double* ptz, const double* rays, int n_pose, int n_lm, 
 // K1: linearize (residual + Jacobian + per-segment / per-landmark normal-equation blocks + cost)
 // ------------------------------------------------------------------------------------------------
 constexpr int SEGW = K1_SEGW;  // segments per LDS window per wave
-#ifndef K1_BF
-#define K1_BF 1  // phase B: branch-free record validity and unconditional projection reads (round 6; 0: round 5's form)
+#ifndef K1_RPL
+#define K1_RPL 4  // phase B: records per lane (one segmented scan per 64 K1_RPL records; 8 measured 62.0 vs 60.4 us, r06j)
 #endif
 // (Round 5 removed the measured-slower build variants: one record per lane (K1_COARSE 0), three record groups in
 // flight (K1_DEPTH 3), LDS-atomic tail runs, issue-order tails and phase C's own table loads (K1_FTV_LATE))
@@ -174,7 +174,8 @@ __device__ long long g_k1_items[32768][8];  // start, end, A, B, C, final, segme
 #endif
 // FTL: the frame tables are staged in LDS (n_pose <= K1_FT_LDS): phase A's chain is descriptor -> segment frame id
 // -> LDS instead of descriptor -> frame id -> global frame table (one dependent memory latency less per wave)
-template <typename real, int LOSS, bool FTL>
+// WT: records carry multiplicities (rec_w; the dedup form) -- unweighted problems keep no weight registers
+template <typename real, int LOSS, bool FTL, bool WT = true>
 __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_MIN_WAVES64) void k_linearize(LinArgs a) {
   __shared__ real s_x[K1_WPB][SEGW], s_y[K1_WPB][SEGW], s_acc[K1_WPB][4][SEGW];
   __shared__ double s_ft[5][FTL ? K1_FT_LDS : 1];  // ca, sa, cb, sb, f per frame (fp64)
@@ -254,69 +255,64 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
 
   double V00 = 0, V01 = 0, V11 = 0, g0 = 0, g1 = 0, cost = 0;
 
-  // phase B, thread-coarsened: a lane owns 4 consecutive records of a 256-record batch (4-aligned:
-  // one 4-B key load and two 16-B delta loads per lane), reduces its own runs, and only its tail run
-  // enters the wave's segmented scan (one scan per 256 records); records before r0 / after r1 of the
-  // aligned batch are masked (the record arrays are padded to a multiple of 4)
+  // phase B, thread-coarsened: a lane owns RPL consecutive records of a 64 RPL-record batch (RPL-aligned: RPL / 4
+  // 4-B key words and RPL / 2 16-B delta loads per lane), reduces its own runs, and only its tail run enters the wave's
+  // segmented scan (one scan per 64 RPL records); records before r0 / after r1 of the aligned batch are masked (the
+  // record arrays are padded by 8 records).  Round 6 measured RPL 8 (one scan per 512 records): slower (62.0 vs 60.4 us).
+  constexpr int RPL = sizeof(real) == 4 ? K1_RPL : 4;  // (fp64: 3 waves / SIMD already at 4)
+  static_assert(RPL == 4 || RPL == 8, "records per lane");
   struct CGrp {
-    uint32_t key4;
-    real ox[4], oy[4], wt[4];
+    uint32_t keyw[RPL / 4];
+    real ox[RPL], oy[RPL], wt[WT ? RPL : 1];
   };
   auto load_cgrp = [&](CGrp& g, int64_t rb, int64_t r1) {
-    const int64_t q = min(rb + 4 * lane, (r1 - 1) & ~(int64_t)3);
-    g.key4 = *reinterpret_cast<const uint32_t*>(a.rec_key + q);
+    const int64_t q = min(rb + RPL * lane, (r1 - 1) & ~(int64_t)(RPL - 1));
+#pragma unroll
+    for (int k = 0; k < RPL / 4; ++k) g.keyw[k] = reinterpret_cast<const uint32_t*>(a.rec_key + q)[k];
     if constexpr (sizeof(real) == 4) {
-      const float4 p0 = reinterpret_cast<const float4*>(rec_xy)[q / 2];
-      const float4 p1 = reinterpret_cast<const float4*>(rec_xy)[q / 2 + 1];
-      g.ox[0] = p0.x; g.oy[0] = p0.y; g.ox[1] = p0.z; g.oy[1] = p0.w;
-      g.ox[2] = p1.x; g.oy[2] = p1.y; g.ox[3] = p1.z; g.oy[3] = p1.w;
+#pragma unroll
+      for (int k = 0; k < RPL / 2; ++k) {
+        const float4 p = reinterpret_cast<const float4*>(rec_xy)[q / 2 + k];
+        g.ox[2 * k] = p.x; g.oy[2 * k] = p.y; g.ox[2 * k + 1] = p.z; g.oy[2 * k + 1] = p.w;
+      }
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < RPL; ++j) {
         const double2 o = reinterpret_cast<const double2*>(rec_xy)[q + j];
         g.ox[j] = o.x; g.oy[j] = o.y;
       }
     }
+    if constexpr (WT) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) g.wt[j] = rec_w ? rec_w[min(q + j, r1 - 1)] : (real)1;
+      for (int j = 0; j < RPL; ++j) g.wt[j] = rec_w[min(q + j, r1 - 1)];
+    }
   };
   auto consume_c = [&](const CGrp& g, int64_t rb, int64_t r0, int64_t r1) {
-    int key[4];
-    real v[4][4];
+    int key[RPL];
     real cb = 0;  // the batch's cost terms, summed in the record precision, then added in fp64
-#if K1_BF
-    // branch-free (round 6): the validity test on a 32-bit offset from r0, and the four records' projection reads
-    // issued unconditionally (key clamped into the window; an invalid record's values are masked below), so one LDS
-    // wait serves the lane's four records instead of one exec-masked branch with its own wait per record
-    const int rel0 = (int)(rb - r0) + 4 * lane, nrec = (int)(r1 - r0);
-    real px[4], py[4];
-    bool vld[4];
+    // branch-free (round 6): the validity test on a 32-bit offset from r0, and the records' projection reads issued
+    // unconditionally (key clamped into the window; an invalid record's values are masked below), so one LDS wait
+    // serves the lane's records instead of one exec-masked branch with its own wait per record
+    const int rel0 = (int)(rb - r0) + RPL * lane, nrec = (int)(r1 - r0);
+    real px[RPL], py[RPL];
+    bool vld[RPL];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int kb = (int)((g.key4 >> (8 * j)) & 0xffu);
+    for (int j = 0; j < RPL; ++j) {
+      const int kb = (int)((g.keyw[j >> 2] >> (8 * (j & 3))) & 0xffu);
       vld[j] = (unsigned)(rel0 + j) < (unsigned)nrec;
       key[j] = vld[j] ? kb : (rel0 + j < 0 ? -1 : 255);
       px[j] = sx[kb & (SEGW - 1)];
       py[j] = sy[kb & (SEGW - 1)];
     }
-#endif
+    real t0 = 0, t1 = 0, t2 = 0, t3 = 0;  // the open run's sums
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-#if K1_BF
+    for (int j = 0; j < RPL; ++j) {
       const bool valid = vld[j];
       const real rx = valid ? px[j] - g.ox[j] : (real)0;
       const real ry = valid ? py[j] - g.oy[j] : (real)0;
-#else
-      const int64_t idx = rb + 4 * lane + j;
-      const bool valid = idx >= r0 && idx < r1;
-      key[j] = valid ? (int)((g.key4 >> (8 * j)) & 0xffu) : (idx < r0 ? -1 : 255);
-      real rx = 0, ry = 0;
-      if (valid) {
-        rx = sx[key[j]] - g.ox[j];
-        ry = sy[key[j]] - g.oy[j];
-      }
-#endif
-      const real wt = valid ? g.wt[j] : (real)0;
+      real wt;
+      if constexpr (WT) wt = valid ? g.wt[j] : (real)0;
+      else wt = valid ? (real)1 : (real)0;
       real wx, wy, c, hx, hy;
       if constexpr (LOSS == 0) {
         wx = wt; wy = wt;
@@ -341,22 +337,24 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
         hy = iy ? wy : wy * hc;
       }
       cb += c;
-      v[j][0] = hx; v[j][1] = hy; v[j][2] = wx * rx; v[j][3] = wy * ry;
-    }
-    cost += (double)cb;
-    // the lane's tail run (key of its last record) joins the scan; earlier runs are the lane's alone
-    // unless they continue a previous lane's tail: LDS atomic adds for those
-    const int kt = key[3];
-    real t0 = v[3][0], t1 = v[3][1], t2 = v[3][2], t3 = v[3][3];
-#pragma unroll
-    for (int j = 2; j >= 0; --j) {
-      if (key[j] == kt) {
-        t0 += v[j][0]; t1 += v[j][1]; t2 += v[j][2]; t3 += v[j][3];
-      } else if (key[j] >= 0) {
-        atomicAdd(acc0 + key[j], v[j][0]); atomicAdd(acc1 + key[j], v[j][1]);
-        atomicAdd(acc2 + key[j], v[j][2]); atomicAdd(acc3 + key[j], v[j][3]);
+      // runs merged forward as the records are formed (round 6: only the open run is live, not all RPL records'
+      // terms): a run that ends inside the lane is the lane's alone unless it continues the previous lane's tail --
+      // one set of LDS atomic adds per such run; the lane's tail run (key of its last record) joins the scan
+      const real e0 = hx, e1 = hy, e2 = wx * rx, e3 = wy * ry;
+      if (j == 0) {
+        t0 = e0; t1 = e1; t2 = e2; t3 = e3;
+      } else if (key[j] == key[j - 1]) {
+        t0 += e0; t1 += e1; t2 += e2; t3 += e3;
+      } else {
+        if (key[j - 1] >= 0) {
+          atomicAdd(acc0 + key[j - 1], t0); atomicAdd(acc1 + key[j - 1], t1);
+          atomicAdd(acc2 + key[j - 1], t2); atomicAdd(acc3 + key[j - 1], t3);
+        }
+        t0 = e0; t1 = e1; t2 = e2; t3 = e3;
       }
     }
+    cost += (double)cb;
+    const int kt = key[RPL - 1];
     const int kenc = kt + 2;
     seg_scan_step<DPP_ROW_SHR1, 0xf>(kenc, t0, t1, t2, t3);
     seg_scan_step<DPP_ROW_SHR2, 0xf>(kenc, t0, t1, t2, t3);
@@ -385,7 +383,7 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
     const int64_t r1 = (w0 == s0) ? (int64_t)(uint32_t)wm.w : a.seg_rec_begin[w1];
     // the window's first record group is requested before phase A: its latency overlaps the projections
     CGrp ca, cb;
-    const int64_t rb0 = r0 & ~(int64_t)3;
+    const int64_t rb0 = r0 & ~(int64_t)(RPL - 1);
     load_cgrp(ca, rb0, r1);
     // phase A: fp64 projection of every segment of the window (lanes over segments), kept as the
     // offset from the segment's base observation so phase B works on O(residual) magnitudes.  The
@@ -421,12 +419,12 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
     // groups alternate: the next group's loads are in flight while the current one is consumed.
     // (An LDS-DMA ring of 3 batches per wave, global_load_lds, was measured slower: hipcc puts a
     // vmcnt(0) -- every pending DMA -- in front of each LDS write of the reduction)
-    for (int64_t rb = r0 & ~(int64_t)3; rb < r1; rb += 2 * 4 * WAVE) {
-      load_cgrp(cb, rb + 4 * WAVE, r1);
+    for (int64_t rb = r0 & ~(int64_t)(RPL - 1); rb < r1; rb += 2 * RPL * WAVE) {
+      load_cgrp(cb, rb + RPL * WAVE, r1);
       consume_c(ca, rb, r0, r1);
-      if (rb + 4 * WAVE >= r1) break;
-      load_cgrp(ca, rb + 2 * 4 * WAVE, r1);
-      consume_c(cb, rb + 4 * WAVE, r0, r1);
+      if (rb + RPL * WAVE >= r1) break;
+      load_cgrp(ca, rb + 2 * RPL * WAVE, r1);
+      consume_c(cb, rb + RPL * WAVE, r0, r1);
     }
     wave_lds_fence();
     K1_NOW(kt2);
@@ -505,12 +503,13 @@ void launch_linearize(const LinArgs& a, int loss, hipStream_t st, hipEvent_t ev0
     if (ev0) hipExtLaunchKernelGGL(kern, grid, dim3(64 * K1_WPB), 0, st, ev0, ev1, 0, a);
     else hipLaunchKernelGGL(kern, grid, dim3(64 * K1_WPB), 0, st, a);
   };
+  const bool wt = a.rec_w != nullptr;
   if (ftl) {
-    if (loss == 0) go(k_linearize<real, 0, true>);
-    else go(k_linearize<real, 1, true>);
+    if (loss == 0) wt ? go(k_linearize<real, 0, true, true>) : go(k_linearize<real, 0, true, false>);
+    else wt ? go(k_linearize<real, 1, true, true>) : go(k_linearize<real, 1, true, false>);
   } else {
-    if (loss == 0) go(k_linearize<real, 0, false>);
-    else go(k_linearize<real, 1, false>);
+    if (loss == 0) wt ? go(k_linearize<real, 0, false, true>) : go(k_linearize<real, 0, false, false>);
+    else wt ? go(k_linearize<real, 1, false, true>) : go(k_linearize<real, 1, false, false>);
   }
 }
 
