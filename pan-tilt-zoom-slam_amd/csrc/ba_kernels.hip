@@ -76,6 +76,9 @@ void launch_tables(const double* ptz, const double* rays, int n_pose, int n_lm, 
 // K1: linearize (residual + Jacobian + per-segment / per-landmark normal-equation blocks + cost)
 // ------------------------------------------------------------------------------------------------
 constexpr int SEGW = K1_SEGW;  // segments per LDS window per wave
+#ifndef K1_FTL_ALWAYS
+#define K1_FTL_ALWAYS 1
+#endif
 #ifndef K1_RPL
 #define K1_RPL 4  // phase B: records per lane (one segmented scan per 64 K1_RPL records; 8 measured 62.0 vs 60.4 us, r06j)
 #endif
@@ -201,6 +204,7 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
   const int4 wd = a.lm_work[2 * tq];
   const int4 wm = a.lm_work[2 * tq + 1];
   int fbase = 0;  // FTL: the first staged frame (s_ft[k][fs - fbase])
+  bool ftl_ok = FTL;  // FTL: this workgroup's frame range fits the LDS table
   if constexpr (FTL) {
     // the frames the workgroup's landmarks see, [min first frame, max last frame] over its K1_WPB descriptors (scalar
     // loads; the work order keeps a workgroup's landmarks close in frame order, so this is ~a coupling window, not the
@@ -213,7 +217,9 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
       fbase = min(fbase, m.x);
       fmax = max(fmax, m.y);
     }
+    ftl_ok = fmax - fbase < K1_FT_LDS;  // (else this workgroup reads the tables from global memory)
     const double4* src = reinterpret_cast<const double4*>(a.ft64);
+    if (ftl_ok)
     for (int e = fbase + (int)threadIdx.x; e <= fmax; e += blockDim.x) {
       const double4 t0 = src[2 * e];
       const double f = reinterpret_cast<const double*>(a.ft64)[8 * e + 4];
@@ -224,6 +230,7 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
     if (task >= a.n_work) return;  // whole wave leaves after the barrier
   }
   auto ft_lds = [&](int fs) {
+    if (!ftl_ok) return ((const FrameTab<double>*)a.ft64)[fs];
     FrameTab<double> F;
     fs -= fbase;
     F.ca = s_ft[0][fs]; F.sa = s_ft[1][fs]; F.cb = s_ft[2][fs]; F.sb = s_ft[3][fs]; F.f = s_ft[4][fs];
@@ -437,7 +444,9 @@ __global__ __launch_bounds__(64 * K1_WPB, sizeof(real) == 4 ? K1_MIN_WAVES : K1_
       const int sl = s - w0;
       real x, y, J[2][5];
       const int fs = fsv[i];
-      if constexpr (FTL) {
+      if (FTL && !ftl_ok) {
+        ptz_project_jac<real>(ft[fs], R, u, v, x, y, J);
+      } else if constexpr (FTL) {
         // the record-precision table is the rounded fp64 one (k_tables): the same values as ft[fs]
         FrameTab<real> F;
         const int fl = fs - fbase;
@@ -498,7 +507,9 @@ template <typename real>
 void launch_linearize(const LinArgs& a, int loss, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
   if (a.n_work <= 0) return;
   dim3 grid((a.n_work + K1_WPB - 1) / K1_WPB);
-  const bool ftl = a.n_pose <= K1_FT_LDS;  // frame tables staged in LDS (neutral vs global reads, 13 VGPRs fewer)
+  // frame tables staged in LDS per workgroup frame range (round 6: any n_pose; a workgroup whose range exceeds K1_FT_LDS
+  // frames reads them from global memory -- config 4's multi-row landmarks); the global-table form stays for A/B builds
+  const bool ftl = K1_FTL_ALWAYS ? true : a.n_pose <= K1_FT_LDS;
   auto go = [&](auto kern) {
     if (ev0) hipExtLaunchKernelGGL(kern, grid, dim3(64 * K1_WPB), 0, st, ev0, ev1, 0, a);
     else hipLaunchKernelGGL(kern, grid, dim3(64 * K1_WPB), 0, st, a);

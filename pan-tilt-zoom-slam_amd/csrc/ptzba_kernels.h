@@ -7,9 +7,12 @@ namespace ptzba {
 
 constexpr int K1_SEGW = 128;  // K1 segments per LDS window per wave
 #ifndef K1_FT_LDS_N
-#define K1_FT_LDS_N 640
+#define K1_FT_LDS_N 384
 #endif
-constexpr int K1_FT_LDS = K1_FT_LDS_N;  // K1 stages the frame tables in LDS up to this many frames (5 x 8 B per frame)
+// K1 stages its workgroup's frame range of the frame tables in LDS (5 x 8 B per frame) when the range holds at most this
+// many frames, else the workgroup reads them from global memory.  Round 6: 640 -> 384 frames (15 KB instead of 25 KB),
+// so five workgroups of four waves fit a CU's LDS (38 -> 27 KB per workgroup): 5 waves / SIMD instead of 4
+constexpr int K1_FT_LDS = K1_FT_LDS_N;
 // dense landmark x frame slot rows, packed (no padding: K1 writes and K2 reads 60 B per fp32 slot, not 80):
 // W (3x2) in W_STRIDE reals, U (3x3 sym, 6) | g_pose (3) in UG_STRIDE reals; rows are only 4-B (fp32) / 8-B (fp64)
 // aligned, so the vector accesses go through the element-aligned vector types below (dwordx4 / x2 on gfx950)
