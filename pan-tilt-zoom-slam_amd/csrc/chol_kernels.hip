@@ -167,15 +167,13 @@ __device__ __forceinline__ void put_tile(double (*dst)[NB + 1], const double (&v
 // maps (gfx950): A[i = l&15][k = l>>4], B[k = l>>4][j = l&15]; D[row = (l>>4) + 4 r][col = l&15].
 typedef double v4f64 __attribute__((ext_vector_type(4)));
 // SG: C -= A Sigma B^T with Sigma = diag(sg) (the signed factor of an indefinite system, see k_chol_step)
+// The level tasks keep C in registers instead (blk_acc_*): wave w's block, the 4 values of the MFMA D layout.
 template <bool SG = false>
-__device__ __forceinline__ void tile_gemm_nt_sub(double (*C)[NB + 1], double (*A)[NB + 1], double (*B)[NB + 1],
-                                                 const double* sg = nullptr) {
+__device__ __forceinline__ void blk_gemm_nt_sub(v4f64& acc, const double (*A)[NB + 1], const double (*B)[NB + 1],
+                                                const double* sg = nullptr) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int bi = (w >> 1) * 16, bj = (w & 1) * 16;
   const int li = l & 15, lk = l >> 4;
-  v4f64 acc;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) acc[r] = C[bi + lk + 4 * r][bj + li];
 #pragma unroll
   for (int s = 0; s < NB / 4; ++s) {
     const double a = -A[bi + li][4 * s + lk];
@@ -183,8 +181,27 @@ __device__ __forceinline__ void tile_gemm_nt_sub(double (*C)[NB + 1], double (*A
     if constexpr (SG) b *= sg[4 * s + lk];
     acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
   }
+}
+// wave w's 16 x 16 block of a 32 x 32 tile (rows 16 (w >> 1) + lk + 4 r, columns 16 (w & 1) + li) from / to memory
+// or LDS
+template <bool COH>
+__device__ __forceinline__ void blk_acc_load(v4f64& acc, const double* __restrict__ tile, int64_t ld) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const double* p = tile + (int64_t)((w >> 1) * 16 + (l >> 4)) * ld + (w & 1) * 16 + (l & 15);
 #pragma unroll
-  for (int r = 0; r < 4; ++r) C[bi + lk + 4 * r][bj + li] = acc[r];
+  for (int r = 0; r < 4; ++r) acc[r] = gld<COH>(p + (int64_t)(4 * r) * ld);
+}
+template <bool COH>
+__device__ __forceinline__ void blk_acc_store(double* __restrict__ tile, int64_t ld, const v4f64& acc) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  double* p = tile + (int64_t)((w >> 1) * 16 + (l >> 4)) * ld + (w & 1) * 16 + (l & 15);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) gst<COH>(p + (int64_t)(4 * r) * ld, acc[r]);
+}
+__device__ __forceinline__ void blk_acc_put(double (*C)[NB + 1], const v4f64& acc) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) C[(w >> 1) * 16 + (l >> 4) + 4 * r][(w & 1) * 16 + (l & 15)] = acc[r];
 }
 
 // fp64 reciprocal and reciprocal square root: hardware estimate + two Newton steps (full double
@@ -572,15 +589,17 @@ template <bool SG, bool P2, bool COH>
 __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, const int4 tk, double* __restrict__ Ldiag,
                                           int* info, double* __restrict__ sgn, double* __restrict__ Minv) {
   static_assert(!(COH && SG), "coherent tile accesses: SPD level launches only");
-  __shared__ double sC[NB][NB + 1];     // target tile (panel T_ik / trailing A_ij)
-  __shared__ double sD[NB][NB + 1];     // diagonal tile -> L_kk
-  __shared__ __attribute__((aligned(16))) double sA[2][NB][NB + 1];  // L_ip of the two update panels
-  __shared__ double sB[2][NB][NB + 1];  // L_kp or L_jp of the two update panels
-  // the sweep's block buffer overlays the update panels' L_ip tiles, dead once the panel GEMMs are done (a
-  // barrier separates them): 51 KB of LDS per workgroup instead of 67, so three workgroups per CU instead of
-  // two -- config 4's levels carry ~1,600 trailing tasks, whose time is load latency x rounds of residency
+  // Four tiles of LDS: the update panels' row tiles while the task's target tiles accumulate in registers (wave w
+  // owns one 16 x 16 block of each: blk_acc_*); after the last update the panel task parks D and T in sP[2] / sP[3]
+  // for the sweep, whose block buffer overlays sP[0..1].  34 KB per workgroup: four workgroups per CU (three with
+  // round 5's six LDS tiles, 51 KB) -- config 4's trailing levels carry 800-1,900 tasks each.
+  __shared__ __attribute__((aligned(16))) double sP[4][NB][NB + 1];
+  double (*const sA)[NB][NB + 1] = sP;      // L_ip (panel task: of the T side) of the two update panels in LDS
+  double (*const sB)[NB][NB + 1] = sP + 2;  // L_kp or L_jp of the two update panels
+  double (*const sD)[NB + 1] = sP[2];       // after the updates: D -> L_kk (the sweep)
+  double (*const sC)[NB + 1] = sP[3];       // after the updates: T_ik
   static_assert((NB / LA_BW) * 2 * NB * LA_BW <= 2 * NB * (NB + 1), "block buffer must fit the panel tiles");
-  double (*s_lb)[2 * NB][LA_BW] = reinterpret_cast<double (*)[2 * NB][LA_BW]>(&sA[0][0][0]);
+  double (*s_lb)[2 * NB][LA_BW] = reinterpret_cast<double (*)[2 * NB][LA_BW]>(&sP[0][0][0]);
   __shared__ __attribute__((aligned(16))) double s_pb[LA_BW][LA_BW];
   __shared__ int s_flags[NB / LA_BW + 1];
   __shared__ double s_sgp[2][NB];  // SG: signs of the two update panels' columns
@@ -613,7 +632,7 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
       return;
     }
   }
-  double v0[4], v1[4], v2[4], v3[4], v4[4], v5[4], w2[4], w3[4], w4[4], w5[4];
+  double v1[4], v2[4], v3[4], v4[4], v5[4], w2[4], w3[4], w4[4], w5[4];
   auto load_signs = [&](int ua, int ub) {  // SG: signs of the update panels' columns
     if constexpr (SG) {
       if (threadIdx.x < 2 * NB) {
@@ -622,10 +641,21 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
       }
     }
   };
+  // the update panels' row tiles through LDS, in pairs (the second pair of a delayed plan in the same buffers, a
+  // barrier between); the target blocks accumulate in registers: per output element the same MFMA sequence in the
+  // same panel order as round 5's LDS-resident targets (bitwise the same factor)
+  auto stage_pair = [&](const double (&ra0)[4], const double (&rb0)[4], const double (&ra1)[4],
+                        const double (&rb1)[4], bool a0, bool b0, bool a1, bool b1) {
+    if (a0) put_tile(sA[0], ra0);
+    if (b0) put_tile(sB[0], rb0);
+    if (a1) put_tile(sA[1], ra1);
+    if (b1) put_tile(sB[1], rb1);
+  };
   if (type == 1) {
     // trailing: A_ij -= sum_p L_ip L_jp^T
     double* C = A + i * NBl * ld + j * NBl;
-    fetch_tile<COH>(v0, C, ld);
+    v4f64 acc;
+    blk_acc_load<COH>(acc, C, ld);
     if (up0 >= 0) {
       fetch_tile<COH>(v1, A + i * NBl * ld + up0 * NBl, ld);
       fetch_tile<COH>(v2, A + j * NBl * ld + up0 * NBl, ld);
@@ -642,37 +672,20 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
       fetch_tile<COH>(w4, A + i * NBl * ld + up3 * NBl, ld);
       fetch_tile<COH>(w5, A + j * NBl * ld + up3 * NBl, ld);
     }
-    put_tile(sC, v0);
-    if (up0 >= 0) {
-      put_tile(sA[0], v1);
-      put_tile(sB[0], v2);
-    }
-    if (up1 >= 0) {
-      put_tile(sA[1], v3);
-      put_tile(sB[1], v4);
-    }
+    stage_pair(v1, v2, v3, v4, up0 >= 0, up0 >= 0, up1 >= 0, up1 >= 0);
     load_signs(up0, up1);
     __syncthreads();
-    // each wave owns one 16x16 block of C: consecutive updates need no barrier in between
-    if (up0 >= 0) tile_gemm_nt_sub<SG>(sC, sA[0], sB[0], s_sgp[0]);
-    if (up1 >= 0) tile_gemm_nt_sub<SG>(sC, sA[1], sB[1], s_sgp[1]);
+    if (up0 >= 0) blk_gemm_nt_sub<SG>(acc, sA[0], sB[0], s_sgp[0]);
+    if (up1 >= 0) blk_gemm_nt_sub<SG>(acc, sA[1], sB[1], s_sgp[1]);
     if (pass2) {  // the second pair through the same panel buffers
       __syncthreads();
-      if (up2 >= 0) {
-        put_tile(sA[0], w2);
-        put_tile(sB[0], w3);
-      }
-      if (up3 >= 0) {
-        put_tile(sA[1], w4);
-        put_tile(sB[1], w5);
-      }
+      stage_pair(w2, w3, w4, w5, up2 >= 0, up2 >= 0, up3 >= 0, up3 >= 0);
       load_signs(up2, up3);
       __syncthreads();
-      if (up2 >= 0) tile_gemm_nt_sub<SG>(sC, sA[0], sB[0], s_sgp[0]);
-      if (up3 >= 0) tile_gemm_nt_sub<SG>(sC, sA[1], sB[1], s_sgp[1]);
+      if (up2 >= 0) blk_gemm_nt_sub<SG>(acc, sA[0], sB[0], s_sgp[0]);
+      if (up3 >= 0) blk_gemm_nt_sub<SG>(acc, sA[1], sB[1], s_sgp[1]);
     }
-    __syncthreads();
-    store_tile<COH>(C, ld, [&](int r, int m) { return sC[r][m]; });
+    blk_acc_store<COH>(C, ld, acc);
     return;
   }
   // panel task (i, k = j)
@@ -680,8 +693,9 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
   const bool diag_only = (i == k);
   const bool updT0 = !diag_only && (tmask & 1), updT1 = !diag_only && (tmask & 2);
   const bool updT2 = !diag_only && (tmask2 & 1), updT3 = !diag_only && (tmask2 & 2);
-  fetch_tile<COH>(v0, A + (int64_t)k * NBl * ld + k * NBl, ld);
-  if (!diag_only) fetch_tile<COH>(v1, A + i * NBl * ld + k * NBl, ld);
+  v4f64 accD, accT;
+  blk_acc_load<COH>(accD, A + (int64_t)k * NBl * ld + k * NBl, ld);
+  if (!diag_only) blk_acc_load<COH>(accT, A + i * NBl * ld + k * NBl, ld);
   if (up0 >= 0) fetch_tile<COH>(v2, A + (int64_t)k * NBl * ld + up0 * NBl, ld);
   if (updT0 && up0 >= 0) fetch_tile<COH>(v3, A + i * NBl * ld + up0 * NBl, ld);
   if (up1 >= 0) fetch_tile<COH>(v4, A + (int64_t)k * NBl * ld + up1 * NBl, ld);
@@ -690,40 +704,38 @@ __device__ __forceinline__ void chol_task(double* __restrict__ A, int64_t ld, co
   if (updT2 && up2 >= 0) fetch_tile<COH>(w3, A + i * NBl * ld + up2 * NBl, ld);
   if (up3 >= 0) fetch_tile<COH>(w4, A + (int64_t)k * NBl * ld + up3 * NBl, ld);
   if (updT3 && up3 >= 0) fetch_tile<COH>(w5, A + i * NBl * ld + up3 * NBl, ld);
-  put_tile(sD, v0);
-  if (!diag_only) put_tile(sC, v1);
-  if (up0 >= 0) put_tile(sB[0], v2);
-  if (updT0 && up0 >= 0) put_tile(sA[0], v3);
-  if (up1 >= 0) put_tile(sB[1], v4);
-  if (updT1 && up1 >= 0) put_tile(sA[1], v5);
-  load_signs(up0, up1);
-  __syncthreads();
+  const bool any_up = up0 >= 0 || up1 >= 0;
+  if (any_up) {
+    stage_pair(v3, v2, v5, v4, updT0 && up0 >= 0, up0 >= 0, updT1 && up1 >= 0, up1 >= 0);
+    load_signs(up0, up1);
+    __syncthreads();
+  }
   CS_STAMP(1);
   if (up0 >= 0) {
-    tile_gemm_nt_sub<SG>(sD, sB[0], sB[0], s_sgp[0]);
-    if (updT0) tile_gemm_nt_sub<SG>(sC, sA[0], sB[0], s_sgp[0]);
+    blk_gemm_nt_sub<SG>(accD, sB[0], sB[0], s_sgp[0]);
+    if (updT0) blk_gemm_nt_sub<SG>(accT, sA[0], sB[0], s_sgp[0]);
   }
   if (up1 >= 0) {
-    tile_gemm_nt_sub<SG>(sD, sB[1], sB[1], s_sgp[1]);
-    if (updT1) tile_gemm_nt_sub<SG>(sC, sA[1], sB[1], s_sgp[1]);
+    blk_gemm_nt_sub<SG>(accD, sB[1], sB[1], s_sgp[1]);
+    if (updT1) blk_gemm_nt_sub<SG>(accT, sA[1], sB[1], s_sgp[1]);
   }
   if (pass2) {  // the delayed pair (api.hip make_plan) through the same panel buffers
-    __syncthreads();
-    if (up2 >= 0) put_tile(sB[0], w2);
-    if (updT2 && up2 >= 0) put_tile(sA[0], w3);
-    if (up3 >= 0) put_tile(sB[1], w4);
-    if (updT3 && up3 >= 0) put_tile(sA[1], w5);
+    if (any_up) __syncthreads();
+    stage_pair(w3, w2, w5, w4, updT2 && up2 >= 0, up2 >= 0, updT3 && up3 >= 0, up3 >= 0);
     load_signs(up2, up3);
     __syncthreads();
     if (up2 >= 0) {
-      tile_gemm_nt_sub<SG>(sD, sB[0], sB[0], s_sgp[0]);
-      if (updT2) tile_gemm_nt_sub<SG>(sC, sA[0], sB[0], s_sgp[0]);
+      blk_gemm_nt_sub<SG>(accD, sB[0], sB[0], s_sgp[0]);
+      if (updT2) blk_gemm_nt_sub<SG>(accT, sA[0], sB[0], s_sgp[0]);
     }
     if (up3 >= 0) {
-      tile_gemm_nt_sub<SG>(sD, sB[1], sB[1], s_sgp[1]);
-      if (updT3) tile_gemm_nt_sub<SG>(sC, sA[1], sB[1], s_sgp[1]);
+      blk_gemm_nt_sub<SG>(accD, sB[1], sB[1], s_sgp[1]);
+      if (updT3) blk_gemm_nt_sub<SG>(accT, sA[1], sB[1], s_sgp[1]);
     }
   }
+  if (any_up || pass2) __syncthreads();  // the panel tiles are read: D and T take their place
+  blk_acc_put(sD, accD);
+  if (!diag_only) blk_acc_put(sC, accT);
   __syncthreads();
   CS_STAMP(2);
   wg_potrf_trsm32_df<LA_BW, SG>(sD, diag_only ? nullptr : sC, s_lb, s_pb, s_flags, info, s_sig);

@@ -128,10 +128,21 @@ def _iters(config):
     return 3 if config == "config4" else CFG["max_iter"]
 
 
-def _lm(h, config, default_opts):
+def _converge(config, precision):
+    # fp32 records at config 3: solved to the optimum from the Gauss-Newton start.  Damped (lambda0 1e-4) and stopped at
+    # ftol 1e-10, the fp32 solve ends where rejected trials have grown the damping -- after round 6's K1 summation order
+    # the two-rank run stopped 1.3e-5 deg / 1.0e-3 px short of the optimum, the one-rank run 2e-6 deg / 1.7e-4 px
+    # (r06p): iterates of two summation orders part there, so the fp32 case compares optima, fp64 keeps the
+    # iterate-for-iterate comparison
+    return precision == 1 and config == "config3"
+
+
+def _lm(h, config, default_opts, precision=0):
     import ptzba
     if default_opts:  # the shipped options: Gauss-Newton start, ftol 1e-4, Huber curvature switch
         return ptzba.LMSolver(h).run()
+    if _converge(config, precision):  # Gauss-Newton start (the shipped lambda0), to the optimum
+        return ptzba.LMSolver(h, ftol=CFG["ftol"], xtol=1e-14, max_iter=60).run()
     return ptzba.LMSolver(h, ftol=CFG["ftol"], xtol=1e-14, max_iter=_iters(config), lambda0=DAMPED).run()
 
 
@@ -161,7 +172,7 @@ def _part_worker(rank, world, port, out_dir, config, precision, loss, default_op
 
     h.set_exchange_hook(hook)
     h.set_state(prob.init_ptz, prob.init_rays)
-    res = _lm(h, config, default_opts)
+    res = _lm(h, config, default_opts, precision)
     ptz, rays = h.get_state()
     own_lm = np.zeros(prob.n_landmark, bool)
     own_lm[prob.landmark[sel]] = True
@@ -187,7 +198,7 @@ def test_part_owned_gpu_solve_matches_single_rank(gpu_available, tmp_path, monke
     before their phase, updates into later phases applied by one group member each.  The result equals the
     single-rank solve of the whole problem: same iterations and status, the cost to 1e-9 relative, every rank's
     poses (its phases' frames) and rays within 1e-8 (fp64; fp32 records + Huber: 1e-5 deg / 1e-4 px -- the per-rank
-    Schur sums round differently).  config 3 = the headline problem in the two-level order: at 3 ranks ranks 0 / 1
+    Schur sums round differently, so config 3 in fp32 is solved to the optimum on both sides).  config 3 = the headline problem in the two-level order: at 3 ranks ranks 0 / 1
     own the first half's leaves (X_SUB over them) and rank 2 the second half, at 4 each rank owns a leaf, at 8 pairs
     share the leaves (X_PART, X_SUB and X_SEP all run);
     grid / config 4 = keyframes on tilt rows (config 4: 410M records, 3 LM iterations; at 4 ranks two per part; at 8,
@@ -205,10 +216,11 @@ def test_part_owned_gpu_solve_matches_single_rank(gpu_available, tmp_path, monke
     h1.set_problem(prob.n_pose, prob.n_landmark, prob.frame, prob.landmark, prob.xy, prob.u, prob.v,
                    precision=precision, loss=loss, frame_win_hi=win_hi)
     h1.set_state(prob.init_ptz, prob.init_rays)
-    res1 = ptzba.LMSolver(h1, ftol=CFG["ftol"], xtol=1e-14, max_iter=_iters(config), lambda0=DAMPED).run()
+    res1 = _lm(h1, config, False, precision)
     ptz1, rays1 = h1.get_state()
     h1.close()
     outs = [np.load(os.path.join(tmp_path, f"part_rank{r}.npz")) for r in range(world)]
+    conv = _converge(config, precision)
     assert all(int(o["mode"]) == 1 for o in outs)
     assert sum(int(o["n_rec"]) for o in outs) == len(prob.frame)
     covered = np.zeros(prob.n_pose, bool)
@@ -216,15 +228,24 @@ def test_part_owned_gpu_solve_matches_single_rank(gpu_available, tmp_path, monke
     for r, o in enumerate(outs):
         own = o["owned"]
         covered |= own
-        assert int(o["njev"]) == res1.njev and int(o["status"]) == res1.status, (r, int(o["njev"]), res1)
+        if conv:  # both at the fp32 optimum: the stop (ftol, or the damping limit below fp32's round-off) may differ
+            assert int(o["status"]) in (1, 2, 3, ptzba.STATUS_DAMPING) and res1.status in (1, 2, 3, ptzba.STATUS_DAMPING)
+        else:
+            assert int(o["njev"]) == res1.njev and int(o["status"]) == res1.status, (r, int(o["njev"]), res1)
         assert abs(float(o["cost"]) - res1.cost) <= (1e-9 if fp64 else 1e-7) * res1.cost
         if fp64:
             np.testing.assert_allclose(o["ptz"][own], ptz1[own], rtol=0, atol=1e-8)
             np.testing.assert_allclose(o["rays"][o["own_lm"]], rays1[o["own_lm"]], rtol=0, atol=1e-8)
         else:
             rm = synthetic.pose_rmse(o["ptz"][own], ptz1[own])
-            # fp32 round-off at the tight-ftol stop: the ranks' Schur sums round in another order (r05t: pan 1.6e-6 deg
-            # at 2 ranks); 10x inside the north star's 1e-4 gate
+            if conv:  # both at the pinned oracle's optimum (tests/golden/config3_optimum.npz) within the north star
+                t = np.load(os.path.join(ROOT, "tests", "golden", "config3_optimum.npz"))["ptz_tight_huber"]
+                ro, r1 = synthetic.pose_rmse(o["ptz"][own], t[own]), synthetic.pose_rmse(ptz1[own], t[own])
+                print(f"rank {r}: status {int(o['status'])} njev {int(o['njev'])}, vs one rank {rm}; vs the oracle "
+                      f"optimum: rank {ro}, one rank {r1} ({res1})")
+                assert ro.max() <= 1e-4 and r1.max() <= 1e-4, (ro, r1)
+            # fp32: config 3 compares the two optima (r06q: 6e-8 deg / 5e-6 px apart), config 4 the iterates after 3
+            # damped iterations; 10x inside the north star's 1e-4 gate
             assert rm[0] < 1e-5 and rm[1] < 1e-5 and rm[2] < 1e-4, rm
         kinds = set(o["kinds"].tolist())
         assert ptzba.X_SEP in kinds and ptzba.X_SCAL in kinds and ptzba.X_SYS not in kinds
