@@ -331,8 +331,8 @@ __global__ __launch_bounds__(512) void k_schur(SchurArgs a) {
 // 16 x 16, nine per wave (3 row blocks x 3 column blocks).  Zero products (a landmark covers ~19 % of a
 // tile) cost matrix-core cycles instead of VALU issue.
 // Precision: every operand is split x = hi + lo into two fp16 (22 significant bits) and a product is
-// hi*hi + hi*lo + lo*hi (the dropped lo*lo is ~2^-22 of it), accumulated in fp32 per batch and flushed
-// to fp64 as in k_schur.  Range: W (~1e4 px^2) and Y = -W V~^-1 (~1) would not both fit fp16, so row
+// hi*hi + hi*lo + lo*hi (the dropped lo*lo is ~2^-22 of it), accumulated in fp32 over the item's batches
+// and stored as the fp32 split partial (the reduce sums the splits in fp64).  Range: W (~1e4 px^2) and Y = -W V~^-1 (~1) would not both fit fp16, so row
 // k = (landmark, d) of W is scaled by g_l = 2^round(log2 sqrt(tr V~_l^-1)) and the same row of Y by
 // 1 / g_l: the product Y^T W is unchanged (powers of two: exact), both factors ~ sqrt(|W| |Y|).
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
@@ -341,9 +341,7 @@ constexpr int MKP = 40;
 #ifndef MF_DIAG_FUSED
 #define MF_DIAG_FUSED 1  // chunk-0 diagonal terms inside the batch pipeline (0: a phase before it)
 #endif
-#ifndef MF_FLUSH
-#define MF_FLUSH 4  // batches (of 16 landmarks) accumulated in fp32 between fp64 flushes
-#endif  // k pitch of an operand row in halves: 80-B rows keep the 16-B fragment reads aligned
+// (k pitch of an operand row in halves: 80-B rows keep the 16-B fragment reads aligned)
 
 // (x0, x1) -> hi + lo, each a packed pair of fp16 (v_cvt_pkrtz: toward zero; x - hi is exact in fp32 and
 // has at most 13 significant bits, of which lo keeps 11)
@@ -458,18 +456,16 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
 
   const int rg = wv >> 2, cg = wv & 3;             // row blocks 3rg.., column blocks 3cg..
   const int fr = lane & 15, fk = (lane >> 4) * 8;  // fragment row / column and k offset of this lane
-  double acc[3][3][4];
+  // the item's products accumulate in fp32 over all its batches (<= 32 of 16 landmarks); the split partial is
+  // stored in fp32 anyway, and round 6 measured fp64 flushes every 4 batches (72 more VGPRs: spills, and an early
+  // vmcnt(0) in the loop) as no more accurate: max |S32 - S64| / sqrt(S_ii S_jj) 2.87e-7 / 4.24e-7 at configs 2 / 3
+  // against 2.90e-7 / 3.93e-7, 3 us faster per build (profiles/r06_k2_ab.json)
   f4v c[3][3];
 #pragma unroll
   for (int x = 0; x < 3; ++x)
 #pragma unroll
-    for (int y = 0; y < 3; ++y) {
-      c[x][y] = f4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int v = 0; v < 4; ++v) acc[x][y][v] = 0;
-    }
-  int nb = 0;
-  auto compute = [&](int buf, bool last) {
+    for (int y = 0; y < 3; ++y) c[x][y] = f4v{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int buf) {
     h8v bh[3], bl[3];
 #pragma unroll
     for (int y = 0; y < 3; ++y) {
@@ -489,18 +485,6 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
         c[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[y], c[x][y], 0, 0, 0);
       }
     }
-    // fp32 partial sums over MF_FLUSH batches, then into fp64 (block-uniform condition)
-    if (++nb == MF_FLUSH || last) {
-      nb = 0;
-#pragma unroll
-      for (int x = 0; x < 3; ++x)
-#pragma unroll
-        for (int y = 0; y < 3; ++y) {
-#pragma unroll
-          for (int v = 0; v < 4; ++v) acc[x][y][v] += (double)c[x][y][v];
-          c[x][y] = f4v{0.f, 0.f, 0.f, 0.f};
-        }
-    }
   };
   SK_T(2);
 #if MF_DIAG_FUSED
@@ -509,7 +493,8 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
   // (landmark, f1) also sums that pair's terms, its U|g loads issued one batch ahead, under the MFMAs.
   const bool diag = chunk == 0;
   const float* __restrict__ ug_slot = (const float*)(alt ? a.ug_slot1 : a.ug_slot);
-  float du[9], dvg[2];
+  float du[9];
+  double dvg[2];  // converted where they are consumed (daccum): a conversion here would wait for the load at once
   float dacc[12];  // fp32 over the item's <= 32 batches: one term per batch (the reduction below is fp64)
 #pragma unroll
   for (int k = 0; k < 12; ++k) dacc[k] = 0.f;
@@ -518,15 +503,16 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
     const int64_t slot = m.w + min(max(f1b + yi - m.y, 0), m.z - m.y);
     slot_load9(du, ug_slot + slot * UG_STRIDE);
     const double* vi = a.lm_aux + (int64_t)m.x * 8;
-    dvg[0] = (float)vi[3];
-    dvg[1] = (float)vi[4];
+    dvg[0] = vi[3];
+    dvg[1] = vi[4];
   };
   auto daccum = [&](const Pre& P) {
     if (P.ryin) {
+      const float g0 = (float)dvg[0], g1 = (float)dvg[1];
 #pragma unroll
       for (int k = 0; k < 9; ++k) dacc[k] += du[k];
 #pragma unroll
-      for (int q = 0; q < 3; ++q) dacc[9 + q] += fmaf(P.ryw[2 * q], dvg[0], P.ryw[2 * q + 1] * dvg[1]);
+      for (int q = 0; q < 3; ++q) dacc[9 + q] += fmaf(P.ryw[2 * q], g0, P.ryw[2 * q + 1] * g1);
     }
   };
 #else
@@ -555,7 +541,7 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
     SK_NOW(skt);
     if (diag && p + SNB < nl) dfetch(p + SNB);
     fetch(A, p + 2 * SNB);
-    compute(0, p + SNB >= nl);
+    compute(0);
     SK_ACC(4, skt);
     SK_NOW(skt);
     if (p + SNB < nl) {
@@ -570,7 +556,7 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
     SK_NOW(skt);
     if (diag && p + 2 * SNB < nl) dfetch(p + 2 * SNB);
     fetch(B, p + 3 * SNB);
-    compute(1, p + 2 * SNB >= nl);
+    compute(1);
     SK_ACC(4, skt);
     SK_NOW(skt);
     if (p + 2 * SNB < nl) {
@@ -606,7 +592,7 @@ __global__ __launch_bounds__(512) void k_schur_mf(SchurArgs a) {
       for (int v = 0; v < 4; ++v) {
         const int row = 16 * (3 * rg + x) + (lane >> 4) * 4 + v, col = 16 * (3 * cg + y) + fr;
         const int q = row / SF, i = row % SF, r = col / WAVE, f2 = col % WAVE;
-        out[(i * 9 + 3 * q + r) * WAVE + f2] = (float)acc[x][y][v];
+        out[(i * 9 + 3 * q + r) * WAVE + f2] = c[x][y][v];
       }
   SK_T(10);
 #ifdef SK_TIMING
